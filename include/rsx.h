@@ -1,0 +1,296 @@
+/*
+ * rsx.h — flat C ABI of librsx.so, the MI355X (gfx950) graph-CF training path.
+ *
+ * The reference (EXLYSHA/Recommendar-Systems, an MMRec fork) is pure Python on
+ * PyTorch; its hot path is a handful of torch call sites inside the models'
+ * forward / calculate_loss / full_sort_predict and Trainer.evaluate.  Each entry
+ * point below replaces one of those call sites (cited per function, paths relative
+ * to the reference's root).  The Python host side in recommendar-systems_amd/rsx
+ * binds these with ctypes; INTEGRATION.md shows the binding a maintainer adds to
+ * the reference.
+ *
+ * Conventions (all entry points):
+ *   - every array argument is a DEVICE pointer unless its name ends in `_host`;
+ *   - the caller owns and allocates every buffer, including workspaces (sizes
+ *     from the matching *_ws_bytes query); no entry point allocates or syncs, so
+ *     every call is stream-ordered and can be captured into a hipGraph;
+ *   - matrices are row-major and contiguous: an [n, d] f32 matrix has row stride d;
+ *   - the return value is a hipError_t as int, or one of the RSX_ERR_* codes
+ *     below for argument errors (0 = success).  The Python wrappers raise
+ *     RuntimeError on a nonzero return (the reference raises Python exceptions).
+ */
+#ifndef RSX_H
+#define RSX_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* rsx_stream_t; /* a hipStream_t (0 = the null stream) */
+
+#define RSX_OK 0
+#define RSX_ERR_ARG 1001         /* bad size / null pointer */
+#define RSX_ERR_UNSUPPORTED 1002 /* embedding width not compiled (d in {32,64,128,256}) */
+#define RSX_ERR_WORKSPACE 1003   /* workspace too small */
+
+/* Version string of the library ("rsx <ver> gfx950"). */
+const char* rsx_version(void);
+
+/* ------------------------------------------------------------------------ */
+/* CSR adjacency with an nnz-balanced work schedule                           */
+/* ------------------------------------------------------------------------ */
+/*
+ * Replaces the torch COO sparse adjacency the models build
+ * (src/models/lightgcn.py:65-103, src/models/layergcn.py:91-117,
+ *  src/models/smore.py:176-207).  Rows are split into work items of at most
+ * `chunk` nonzeros so that power-law hub rows (10^3..10^6 neighbours) spread
+ * over many wavefronts; a row split over several items is summed in chunk order
+ * by a fixup pass, so results are deterministic.
+ */
+typedef struct rsx_csr {
+    int64_t n_rows;
+    int64_t n_cols;
+    int64_t nnz;
+    const int64_t* rowptr;    /* [n_rows + 1] */
+    const int32_t* col;       /* [nnz] */
+    const float* val;         /* [nnz] */
+    int32_t chunk;            /* max nonzeros per work item */
+    int32_t pad0;
+    int64_t n_work;           /* work items */
+    const int32_t* work;      /* [n_work][4] = {row, slot, begin, end}; slot -1: whole row */
+    int64_t n_long;           /* rows split over more than one work item */
+    const int32_t* long_rows; /* [n_long][4] = {row, slot_begin, n_slots, 0} */
+    int64_t n_slots;          /* partial-sum slab rows needed (slab = n_slots * d floats) */
+} rsx_csr;
+
+/*
+ * Host-side schedule builder.  Pass work_host/long_host = NULL to query the
+ * counts (n_work, n_long, n_slots); then call again with arrays of
+ * [n_work*4] and [n_long*4] int32.  rowptr_host is the host copy of rowptr.
+ * Returns RSX_ERR_ARG if nnz >= 2^31 (work items keep 32-bit offsets).
+ */
+int rsx_csr_schedule_host(const int64_t* rowptr_host, int64_t n_rows, int32_t chunk,
+                          int32_t* work_host, int32_t* long_host,
+                          int64_t* n_work, int64_t* n_long, int64_t* n_slots);
+
+/* ------------------------------------------------------------------------ */
+/* SpMM with fused row epilogues                                              */
+/* ------------------------------------------------------------------------ */
+/*
+ * Y = A * X for one propagation layer (src/models/lightgcn.py:122,
+ * src/models/layergcn.py:133, src/models/smore.py:282,293,297,303,307,313,317)
+ * and its autograd twin (SparseAddmmBackward; A is symmetric for the
+ * user-item Laplacian so the backward is the same product), with the
+ * per-row work that follows the product in the reference fused into the
+ * write-out:
+ *
+ *   RSX_EPI_STORE     y = alpha*acc
+ *   RSX_EPI_LAYERSUM  y = alpha*acc;  s_out = s_in + alpha*acc
+ *                     (running layer sum of lightgcn.py:124-125 / Horner backward)
+ *   RSX_EPI_FINAL     f = (s_in + alpha*acc) * beta;  zero0/zero1 rows := 0
+ *                     (last layer: mean over K+1 layers, lightgcn.py:124-125)
+ *   RSX_EPI_ADAM      g = (s_in + alpha*acc) * beta + r_add;  Adam(p, m, v, g)
+ *                     (last backward layer fused with torch.optim.Adam,
+ *                      src/common/trainer.py:133,238)
+ *   RSX_EPI_LAYERGCN  c = cos(acc, e0) (eps 1e-8, F.cosine_similarity);
+ *                     y = c*acc;  s_out = s_in + c*acc (s_in may be NULL = 0);
+ *                     saves acc (pre-scale) into `aux` and c into `aux_w`
+ *                     (src/models/layergcn.py:133-138)
+ *   RSX_EPI_AXPBY     y = alpha*acc + beta*s_in   (general accumulate)
+ *   RSX_EPI_LAYERGCN_BWD  backward of the LayerGCN row scaling: with
+ *                     dE = alpha*acc + r_add (grad reaching E^k), z = aux (saved
+ *                     pre-scale rows), c = aux_w, e = e0, nz/ne eps-clamped norms:
+ *                       y     = c*dE + <dE,z> (e/(nz ne) - c z/nz^2)      (dZ^k)
+ *                       s_out = s_in + <dE,z> (z/(nz ne) - c e/ne^2)     (d ego)
+ *   Every kind also zeroes the zero0 / zero1 rows when those are non-NULL.
+ *
+ * Each output row is written by exactly one wavefront group; s_out may alias
+ * s_in, never X.  `slab` must hold csr->n_slots * d floats (0 if n_slots == 0).
+ * d must be one of 32, 64, 128, 256.
+ */
+enum {
+    RSX_EPI_STORE = 0,
+    RSX_EPI_LAYERSUM = 1,
+    RSX_EPI_FINAL = 2,
+    RSX_EPI_ADAM = 3,
+    RSX_EPI_LAYERGCN = 4,
+    RSX_EPI_AXPBY = 5,
+    RSX_EPI_LAYERGCN_BWD = 6
+};
+
+typedef struct rsx_adam {
+    float lr, beta1, beta2, eps, weight_decay;
+    int32_t pad0;
+    const int64_t* step_dev; /* if non-NULL the (already incremented) step count is read here */
+    int64_t step;            /* otherwise this host value is used (1-based) */
+} rsx_adam;
+
+typedef struct rsx_epilogue {
+    int32_t kind;
+    int32_t pad0;
+    float alpha;
+    float beta;
+    float* y;
+    const float* s_in;
+    float* s_out;
+    float* f;
+    float* zero0;
+    float* zero1;
+    const float* r_add;
+    float* p;
+    float* m;
+    float* v;
+    float* g_out;      /* ADAM: optional copy of the gradient row (autograd path) */
+    const float* e0;   /* LAYERGCN(_BWD): ego rows */
+    float* aux;        /* LAYERGCN: pre-scale rows written; LAYERGCN_BWD: read */
+    float* aux_w;      /* LAYERGCN: cosine weight per row written; LAYERGCN_BWD: read */
+    rsx_adam adam;
+} rsx_epilogue;
+
+int rsx_spmm(const rsx_csr* a, const float* x, int32_t d, const rsx_epilogue* epi,
+             float* slab, rsx_stream_t stream);
+
+/* Row-wise epilogue with acc = 0 over rows [0, n_rows): e.g. a stand-alone Adam
+ * step (kind RSX_EPI_ADAM, s_in = grad, beta = 1) — torch.optim.Adam in
+ * src/common/trainer.py:133,238 — or the K = 0 forward. */
+int rsx_rowwise(int64_t n_rows, int32_t d, const rsx_epilogue* epi, rsx_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
+/* BPR triplet loss, forward + backward fused                                 */
+/* ------------------------------------------------------------------------ */
+/*
+ * Variants:
+ *   RSX_BPR_LIGHTGCN  mean -log(1e-10 + sigmoid(s+ - s-)) + reg * (|U0|_F+|P0|_F+|N0|_F)/B
+ *                     on ego rows (src/models/lightgcn.py:132-156, src/common/loss.py:33-51)
+ *   RSX_BPR_LAYERGCN  sum -logsigmoid(s+ - s-) + reg * 0.5*sum(ego^2)
+ *                     (src/models/layergcn.py:142-177, src/common/loss.py:58-61)
+ *   RSX_BPR_SMORE     mean -logsigmoid(s+ - s-) + reg * 0.5*(|u|^2+|p|^2+|n|^2)/batch_cfg
+ *                     on propagated rows (src/models/smore.py:366-378)
+ * Row layout: final/ego are [n_users + n_items, d] (users first, as torch.cat in
+ * the reference); triplets are int64 [3][B] = (user, pos item, neg item) with item
+ * ids local to the item block (reference TrainDataLoader, dataloader.py:226-250).
+ * Outputs: g_final (+= dL/dfinal, rows touched only), g_ego (+= dL/dego; may be
+ * NULL for SMORE), loss_out[0] = loss (f32); if loss_acc != NULL, loss is also
+ * added into loss_acc[0] (f64, per-epoch accumulator without a host sync).
+ * Workspace: rsx_bpr_ws_bytes(B).
+ */
+enum { RSX_BPR_LIGHTGCN = 0, RSX_BPR_LAYERGCN = 1, RSX_BPR_SMORE = 2 };
+
+size_t rsx_bpr_ws_bytes(int64_t batch);
+int rsx_bpr(int32_t variant, const float* final_emb, const float* ego_emb, int64_t n_users,
+            int64_t n_items, int32_t d, const int64_t* triplets, int64_t batch, float reg,
+            float batch_cfg, float* g_final, float* g_ego, float* loss_out, double* loss_acc,
+            void* ws, size_t ws_bytes, rsx_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
+/* Full-sort scoring fused with train-item masking and top-K                  */
+/* ------------------------------------------------------------------------ */
+/*
+ * Replaces  scores = u_emb[users] @ item_emb^T            (lightgcn.py:164 etc.)
+ *           scores[mask] = -1e10; topk(scores, k)          (src/common/trainer.py:521-526)
+ * without materialising the score matrix.  f32 MFMA (v_mfma_f32_32x32x2_f32,
+ * exact f32 fma chains) computes 32x32 score tiles; each row keeps a running
+ * top-K in LDS behind a threshold filter; a merge pass orders the result by
+ * (score desc, item index asc).  Masked (user, item) pairs — the user's
+ * training items, CSR mask_rowptr/mask_col over user ids with sorted columns —
+ * score exactly -1e10 as in the reference.
+ *   user_emb: [*, d] rows selected by users[b] (int64); item_emb: [n_items, d]
+ *   out_val: [n_batch, k] f32, out_idx: [n_batch, k] int64
+ * Requires k <= n_items and k <= 128. Workspace: rsx_fullsort_ws_bytes.
+ */
+size_t rsx_fullsort_ws_bytes(int64_t n_batch, int64_t n_items, int32_t k);
+int rsx_fullsort_topk(const float* user_emb, const int64_t* users, int64_t n_batch,
+                      const float* item_emb, int64_t n_items, int32_t d,
+                      const int64_t* mask_rowptr, const int32_t* mask_col, int32_t k,
+                      float* out_val, int64_t* out_idx, void* ws, size_t ws_bytes,
+                      rsx_stream_t stream);
+
+/* Dense scores (full_sort_predict) for the API path: out[b, i] = <u[users[b]], item[i]>. */
+int rsx_score_dense(const float* user_emb, const int64_t* users, int64_t n_batch,
+                    const float* item_emb, int64_t n_items, int32_t d, float* out,
+                    rsx_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
+/* Training-triplet sampler (throughput mode)                                 */
+/* ------------------------------------------------------------------------ */
+/*
+ * Device replacement of TrainDataLoader's per-epoch shuffle + rejection
+ * negative sampling (src/utils/dataloader.py:226-275,307-309,
+ * src/utils/dataset.py:98-101): batch slot t of batch `start/B` takes training
+ * interaction perm(start + t) (a keyed Feistel bijection of [0, n_inter) per
+ * (seed, epoch)) and a negative item drawn uniformly from all_items, redrawn
+ * while it is in the user's training history (CSR hist_rowptr/hist_col, columns
+ * sorted).  Writes int64 [3][count] triplets (count = min(B, n_inter - start)).
+ */
+int rsx_sample_triplets(const int32_t* inter_u, const int32_t* inter_i, int64_t n_inter,
+                        const int64_t* hist_rowptr, const int32_t* hist_col,
+                        const int32_t* all_items, int64_t n_all_items, uint64_t seed,
+                        int64_t epoch, int64_t start, int64_t batch, int64_t* out,
+                        rsx_stream_t stream);
+
+/* Gather rows: out[b] = src[idx[b] + offset]  (u_embeddings = user_all[user] etc.). */
+int rsx_gather_rows(const float* src, const int64_t* idx, int64_t n, int64_t offset, int32_t d,
+                    float* out, rsx_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
+/* Fused LightGCN training step                                               */
+/* ------------------------------------------------------------------------ */
+/*
+ * One LightGCN batch end to end (src/models/lightgcn.py:117-156 forward + loss,
+ * autograd backward, src/common/trainer.py:238 Adam step), as 2K+2 launches:
+ *   K propagation layers (last fused with the layer mean and zeroing of the
+ *   gradient buffers), BPR fwd+bwd, K backward layers (last fused with Adam).
+ * If `sample` != NULL the triplets are drawn on device first (same contract as
+ * rsx_sample_triplets; `triplets` then receives them), otherwise `triplets`
+ * holds the batch.  Buffers are [n_rows, d] f32 unless noted:
+ *   p (parameters = ego embeddings, users then items), m, v (Adam moments),
+ *   s, h0, h1 (scratch), final_emb (mean of layers), g, r (gradient scratch;
+ *   the forward's last layer zeroes them before the loss scatters into them).
+ *   s may be NULL for n_layers == 1, s/h0/h1 may be NULL for n_layers == 0.
+ */
+typedef struct rsx_sampler_args {
+    const int32_t* inter_u;
+    const int32_t* inter_i;
+    int64_t n_inter;
+    const int64_t* hist_rowptr;
+    const int32_t* hist_col;
+    const int32_t* all_items;
+    int64_t n_all_items;
+    uint64_t seed;
+    int64_t epoch;
+    int64_t start;
+} rsx_sampler_args;
+
+typedef struct rsx_lgcn_step {
+    const rsx_csr* adj;
+    int64_t n_users, n_items;
+    int32_t d, n_layers;
+    float reg;
+    int32_t pad0;
+    float* p; float* m; float* v;
+    float* s; float* h0; float* h1;
+    float* final_emb; float* g; float* r;
+    float* slab;
+    int64_t* triplets;  /* [3][batch] */
+    int64_t batch;
+    const rsx_sampler_args* sample;
+    rsx_adam adam;
+    float* loss_out;    /* [1] */
+    double* loss_acc;   /* [1] or NULL */
+    void* ws; size_t ws_bytes; /* >= rsx_bpr_ws_bytes(batch) */
+} rsx_lgcn_step;
+
+int rsx_lightgcn_step(const rsx_lgcn_step* st, rsx_stream_t stream);
+
+/* Forward only (evaluation): final_emb = mean_k A^k p, using s, h0, h1 as scratch. */
+int rsx_lightgcn_forward(const rsx_csr* adj, int32_t d, int32_t n_layers, const float* p,
+                         float* s, float* h0, float* h1, float* final_emb, float* slab,
+                         rsx_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RSX_H */

@@ -1,0 +1,263 @@
+// bpr.hip — fused BPR triplet loss forward + backward (gfx950).
+//
+// Replaces, per model variant, the gather / dot / logsigmoid / regulariser ops
+// and their autograd backward:
+//   LightGCN  src/models/lightgcn.py:132-156 + src/common/loss.py:33-51
+//   LayerGCN  src/models/layergcn.py:142-177 + src/common/loss.py:58-61
+//   SMORE     src/models/smore.py:366-378 (BPR part; InfoNCE is separate)
+//
+// Two launches: (A) one lane group per triplet computes s+, s-, the per-triplet
+// loss term and dL/d(s+ - s-), plus per-block partial sums of the regulariser's
+// squared norms (deterministic, f64); (B) every block re-reduces those partials
+// in a fixed order (the LightGCN regulariser needs the global Frobenius norms
+// before any gradient row is known) and scatters gradient rows with f32
+// atomics.  Lane li of a group owns columns {li + c*G}, so each atomic
+// wave-instruction adds G contiguous floats of a row.
+#include "rsx_common.hpp"
+
+namespace rsx {
+
+constexpr int kBprBlock = 256;
+
+struct BprArgs {
+    int variant;
+    const float* fin;
+    const float* ego;
+    int64_t n_users, n_items;
+    const int64_t* trip;
+    int64_t batch;
+    float reg, batch_cfg;
+    float* g_fin;
+    float* g_ego;
+    float* loss_out;
+    double* loss_acc;
+    float* coef;     // [batch]
+    double* part;    // [n_blocks][4]
+};
+
+__device__ __forceinline__ float softplus_neg(float x) {
+    // -logsigmoid(x) = log(1 + exp(-x)), computed stably
+    return x >= 0.f ? log1pf(expf(-x)) : -x + log1pf(expf(x));
+}
+__device__ __forceinline__ float sigmoidf(float x) { return 1.f / (1.f + expf(-x)); }
+
+template <int D>
+__global__ __launch_bounds__(kBprBlock) void bpr_fwd(BprArgs a) {
+    constexpr int G = D / 4;
+    constexpr int GPB = kBprBlock / G;
+    constexpr int NC = D / G;  // columns per lane (=4)
+    const int li = threadIdx.x % G;
+    const int64_t b = (int64_t)blockIdx.x * GPB + threadIdx.x / G;
+    double t_loss = 0.0, t_u = 0.0, t_p = 0.0, t_n = 0.0;
+    if (b < a.batch) {
+        const int64_t u = a.trip[b];
+        const int64_t p = a.trip[a.batch + b] + a.n_users;
+        const int64_t n = a.trip[2 * a.batch + b] + a.n_users;
+        float fu[NC], fp[NC], fn[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            fu[c] = a.fin[u * D + li + c * G];
+            fp[c] = a.fin[p * D + li + c * G];
+            fn[c] = a.fin[n * D + li + c * G];
+        }
+        float sp = 0.f, sn = 0.f;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            sp += fu[c] * fp[c];
+            sn += fu[c] * fn[c];
+        }
+        sp = group_sum<G>(sp);
+        sn = group_sum<G>(sn);
+        const float delta = sp - sn;
+        float term, coef;
+        if (a.variant == RSX_BPR_LIGHTGCN) {
+            // -log(1e-10 + sigmoid(delta)), mean over the batch
+            const float sg = sigmoidf(delta);
+            term = -logf(1e-10f + sg);
+            coef = -(sg * (1.f - sg)) / (1e-10f + sg) / (float)a.batch;
+        } else if (a.variant == RSX_BPR_LAYERGCN) {
+            term = softplus_neg(delta);          // sum over the batch
+            coef = -sigmoidf(-delta);
+        } else {
+            term = softplus_neg(delta);          // mean over the batch
+            coef = -sigmoidf(-delta) / (float)a.batch;
+        }
+        // squared norms for the regulariser
+        float qu = 0.f, qp = 0.f, qn = 0.f;
+        if (a.variant == RSX_BPR_SMORE) {
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                qu += fu[c] * fu[c];
+                qp += fp[c] * fp[c];
+                qn += fn[c] * fn[c];
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                const float eu = a.ego[u * D + li + c * G];
+                const float ep = a.ego[p * D + li + c * G];
+                const float en = a.ego[n * D + li + c * G];
+                qu += eu * eu;
+                qp += ep * ep;
+                qn += en * en;
+            }
+        }
+        t_u = (double)qu;  // per-lane partials; summed across the block below
+        t_p = (double)qp;
+        t_n = (double)qn;
+        if (li == 0) {
+            a.coef[b] = coef;
+            t_loss = (double)term;
+        }
+    }
+    // block reduction (fixed order: wave shuffles, then waves in order)
+    __shared__ double red[kBprBlock / kWave][4];
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) {
+        t_loss += __shfl_xor(t_loss, o, kWave);
+        t_u += __shfl_xor(t_u, o, kWave);
+        t_p += __shfl_xor(t_p, o, kWave);
+        t_n += __shfl_xor(t_n, o, kWave);
+    }
+    const int wv = threadIdx.x / kWave;
+    if ((threadIdx.x % kWave) == 0) {
+        red[wv][0] = t_loss;
+        red[wv][1] = t_u;
+        red[wv][2] = t_p;
+        red[wv][3] = t_n;
+    }
+    __syncthreads();
+    if (threadIdx.x < 4) {
+        double s = 0.0;
+        for (int w = 0; w < kBprBlock / kWave; ++w) s += red[w][threadIdx.x];
+        a.part[(int64_t)blockIdx.x * 4 + threadIdx.x] = s;
+    }
+}
+
+template <int D>
+__global__ __launch_bounds__(kBprBlock) void bpr_bwd(BprArgs a, int n_part) {
+    constexpr int G = D / 4;
+    constexpr int GPB = kBprBlock / G;
+    constexpr int NC = D / G;
+    __shared__ double tot[4];
+    if (threadIdx.x < 4) {
+        double s = 0.0;
+        for (int k = 0; k < n_part; ++k) s += a.part[(int64_t)k * 4 + threadIdx.x];
+        tot[threadIdx.x] = s;
+    }
+    __syncthreads();
+    const double B = (double)a.batch;
+    double loss;
+    float ku, kp, kn;  // regulariser gradient scale per row kind
+    if (a.variant == RSX_BPR_LIGHTGCN) {
+        const double nu = sqrt(tot[1]), np = sqrt(tot[2]), nn = sqrt(tot[3]);
+        loss = tot[0] / B + (double)a.reg * (nu + np + nn) / B;
+        ku = nu > 0 ? (float)((double)a.reg / (B * nu)) : 0.f;
+        kp = np > 0 ? (float)((double)a.reg / (B * np)) : 0.f;
+        kn = nn > 0 ? (float)((double)a.reg / (B * nn)) : 0.f;
+    } else if (a.variant == RSX_BPR_LAYERGCN) {
+        loss = tot[0] + (double)a.reg * 0.5 * (tot[1] + tot[2] + tot[3]);
+        ku = kp = kn = a.reg;
+    } else {
+        loss = tot[0] / B + (double)a.reg * 0.5 * (tot[1] + tot[2] + tot[3]) / (double)a.batch_cfg;
+        ku = kp = kn = (float)((double)a.reg / (double)a.batch_cfg);
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (a.loss_out) a.loss_out[0] = (float)loss;
+        if (a.loss_acc) a.loss_acc[0] += loss;
+    }
+    const int li = threadIdx.x % G;
+    const int64_t b = (int64_t)blockIdx.x * GPB + threadIdx.x / G;
+    if (b >= a.batch) return;
+    const int64_t u = a.trip[b];
+    const int64_t p = a.trip[a.batch + b] + a.n_users;
+    const int64_t n = a.trip[2 * a.batch + b] + a.n_users;
+    const float coef = a.coef[b];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        const int col = li + c * G;
+        const float fu = a.fin[u * D + col], fp = a.fin[p * D + col], fn = a.fin[n * D + col];
+        float gu = coef * (fp - fn), gp = coef * fu, gn = -coef * fu;
+        if (a.variant == RSX_BPR_SMORE) {
+            gu += ku * fu;
+            gp += kp * fp;
+            gn += kn * fn;
+        } else if (a.g_ego) {
+            atomicAdd(a.g_ego + u * D + col, ku * a.ego[u * D + col]);
+            atomicAdd(a.g_ego + p * D + col, kp * a.ego[p * D + col]);
+            atomicAdd(a.g_ego + n * D + col, kn * a.ego[n * D + col]);
+        }
+        atomicAdd(a.g_fin + u * D + col, gu);
+        atomicAdd(a.g_fin + p * D + col, gp);
+        atomicAdd(a.g_fin + n * D + col, gn);
+    }
+}
+
+template <int D>
+static int launch_bpr(const BprArgs& a, hipStream_t s) {
+    constexpr int GPB = kBprBlock / (D / 4);
+    const int nb = (int)((a.batch + GPB - 1) / GPB);
+    hipLaunchKernelGGL((bpr_fwd<D>), dim3(nb), dim3(kBprBlock), 0, s, a);
+    hipLaunchKernelGGL((bpr_bwd<D>), dim3(nb), dim3(kBprBlock), 0, s, a, nb);
+    return last_rc();
+}
+
+int bpr_dispatch(const BprArgs& a, int d, hipStream_t s) {
+    switch (d) {
+        case 32: return launch_bpr<32>(a, s);
+        case 64: return launch_bpr<64>(a, s);
+        case 128: return launch_bpr<128>(a, s);
+        case 256: return launch_bpr<256>(a, s);
+        default: return RSX_ERR_UNSUPPORTED;
+    }
+}
+
+size_t bpr_ws(int64_t batch) {
+    const int64_t nb = (batch + 3) / 4 + 1;  // worst case G = 64 lanes (d = 256): 4 triplets per block
+    size_t bytes = (size_t)batch * sizeof(float);
+    bytes = (bytes + 255) & ~(size_t)255;
+    return bytes + (size_t)nb * 4 * sizeof(double) + 256;
+}
+
+int bpr_call(int32_t variant, const float* fin, const float* ego, int64_t n_users, int64_t n_items, int32_t d,
+             const int64_t* trip, int64_t batch, float reg, float batch_cfg, float* g_fin, float* g_ego,
+             float* loss_out, double* loss_acc, void* ws, size_t ws_bytes, hipStream_t s) {
+    if (!fin || !trip || !g_fin || batch <= 0 || !ws) return RSX_ERR_ARG;
+    if (variant != RSX_BPR_SMORE && !ego) return RSX_ERR_ARG;
+    if (variant < 0 || variant > 2) return RSX_ERR_ARG;
+    if (ws_bytes < bpr_ws(batch)) return RSX_ERR_WORKSPACE;
+    BprArgs a;
+    a.variant = variant;
+    a.fin = fin;
+    a.ego = ego;
+    a.n_users = n_users;
+    a.n_items = n_items;
+    a.trip = trip;
+    a.batch = batch;
+    a.reg = reg;
+    a.batch_cfg = batch_cfg;
+    a.g_fin = g_fin;
+    a.g_ego = g_ego;
+    a.loss_out = loss_out;
+    a.loss_acc = loss_acc;
+    char* w = static_cast<char*>(ws);
+    a.coef = reinterpret_cast<float*>(w);
+    size_t off = ((size_t)batch * sizeof(float) + 255) & ~(size_t)255;
+    a.part = reinterpret_cast<double*>(w + off);
+    return bpr_dispatch(a, d, s);
+}
+
+}  // namespace rsx
+
+extern "C" {
+
+size_t rsx_bpr_ws_bytes(int64_t batch) { return rsx::bpr_ws(batch); }
+
+int rsx_bpr(int32_t variant, const float* final_emb, const float* ego_emb, int64_t n_users, int64_t n_items,
+            int32_t d, const int64_t* triplets, int64_t batch, float reg, float batch_cfg, float* g_final,
+            float* g_ego, float* loss_out, double* loss_acc, void* ws, size_t ws_bytes, rsx_stream_t stream) {
+    return rsx::bpr_call(variant, final_emb, ego_emb, n_users, n_items, d, triplets, batch, reg, batch_cfg,
+                         g_final, g_ego, loss_out, loss_acc, ws, ws_bytes, rsx::as_stream(stream));
+}
+
+}  // extern "C"

@@ -1,0 +1,350 @@
+// spmm.hip — nnz-balanced CSR SpMM with fused row epilogues (gfx950).
+//
+// Replaces torch.sparse.mm(norm_adj, E) of the reference's propagation loops
+// (src/models/lightgcn.py:121-125, src/models/layergcn.py:132-138,
+// src/models/smore.py:281-317) and the autograd backward of the same products.
+//
+// Layout: a row of X/Y is d f32 (d in {32,64,128,256}); a "group" of G = d/4
+// lanes owns one output row, lane li holding columns [4li, 4li+4) as a float4, so
+// every gathered neighbour row is one coalesced 16 B-per-lane read (a d=64 row is
+// 16 lanes x float4 = 256 B; d=256 is one whole wavefront).  Work items carry at
+// most `chunk` nonzeros (the schedule built by rsx_csr_schedule_host), so a hub
+// row with 10^4..10^6 neighbours is spread over many groups; its partial sums go
+// to a slab and a fixup pass adds them in chunk order and applies the epilogue:
+// results are deterministic run to run.
+#include <cmath>
+#include <cstring>
+
+#include "rsx_common.hpp"
+
+namespace rsx {
+
+// ---------------------------------------------------------------------------
+// row epilogues
+// ---------------------------------------------------------------------------
+struct AdamConst {
+    float lr, omb1, b2, omb2, eps, wd, step_size, bc2_sqrt;
+};
+
+__device__ __forceinline__ AdamConst adam_const(const rsx_adam& a) {
+    AdamConst c;
+    const int64_t step = a.step_dev ? *a.step_dev : a.step;
+    // torch.optim.Adam (_single_tensor_adam): bias corrections in double, the
+    // tensor ops in f32 with the scalars rounded to f32.
+    const double bc1 = 1.0 - pow((double)a.beta1, (double)step);
+    const double bc2 = 1.0 - pow((double)a.beta2, (double)step);
+    c.lr = a.lr;
+    c.omb1 = (float)(1.0 - (double)a.beta1);
+    c.b2 = a.beta2;
+    c.omb2 = (float)(1.0 - (double)a.beta2);
+    c.eps = a.eps;
+    c.wd = a.weight_decay;
+    c.step_size = (float)((double)a.lr / bc1);
+    c.bc2_sqrt = (float)sqrt(bc2);
+    return c;
+}
+
+__device__ __forceinline__ float adam_elem(const AdamConst& c, float& p, float& m, float& v, float g) {
+    if (c.wd != 0.f) g = g + c.wd * p;
+    m = m + c.omb1 * (g - m);                 // exp_avg.lerp_(grad, 1 - beta1)
+    v = v * c.b2 + (c.omb2 * g) * g;          // exp_avg_sq.mul_(b2).addcmul_(g, g, 1 - b2)
+    const float denom = sqrtf(v) / c.bc2_sqrt + c.eps;
+    p = p + (-c.step_size) * m / denom;       // param.addcdiv_(exp_avg, denom, -step_size)
+    return g;
+}
+
+template <int KIND, int D>
+__device__ __forceinline__ void epilogue(const rsx_epilogue& e, int64_t row, float4 acc, int li) {
+    constexpr int G = D / 4;
+    const int64_t off = row * D + li * 4;
+    acc = mul4(e.alpha, acc);
+    if constexpr (KIND == RSX_EPI_STORE) {
+        st4(e.y + off, acc);
+    } else if constexpr (KIND == RSX_EPI_LAYERSUM) {
+        if (e.y) st4(e.y + off, acc);
+        const float4 s = e.s_in ? add4(ld4(e.s_in + off), acc) : acc;
+        st4(e.s_out + off, s);
+    } else if constexpr (KIND == RSX_EPI_FINAL) {
+        const float4 s = e.s_in ? add4(ld4(e.s_in + off), acc) : acc;
+        st4(e.f + off, mul4(e.beta, s));
+    } else if constexpr (KIND == RSX_EPI_AXPBY) {
+        float4 s = acc;
+        if (e.s_in) s = fma4(e.beta, ld4(e.s_in + off), s);
+        st4(e.y + off, s);
+    } else if constexpr (KIND == RSX_EPI_ADAM) {
+        float4 g = e.s_in ? add4(ld4(e.s_in + off), acc) : acc;
+        g = mul4(e.beta, g);
+        if (e.r_add) g = add4(g, ld4(e.r_add + off));
+        const AdamConst c = adam_const(e.adam);
+        float4 p = ld4(e.p + off), m = ld4(e.m + off), v = ld4(e.v + off);
+        g.x = adam_elem(c, p.x, m.x, v.x, g.x);
+        g.y = adam_elem(c, p.y, m.y, v.y, g.y);
+        g.z = adam_elem(c, p.z, m.z, v.z, g.z);
+        g.w = adam_elem(c, p.w, m.w, v.w, g.w);
+        st4(e.p + off, p);
+        st4(e.m + off, m);
+        st4(e.v + off, v);
+        if (e.g_out) st4(e.g_out + off, g);
+    } else if constexpr (KIND == RSX_EPI_LAYERGCN) {
+        // F.cosine_similarity(z, e0, dim=-1, eps=1e-8) = <z/max(|z|,eps), e/max(|e|,eps)>
+        const float4 e0 = ld4(e.e0 + off);
+        const float zz = group_sum<G>(dot4(acc, acc));
+        const float ee = group_sum<G>(dot4(e0, e0));
+        const float ze = group_sum<G>(dot4(acc, e0));
+        const float nz = fmaxf(sqrtf(zz), 1e-8f), ne = fmaxf(sqrtf(ee), 1e-8f);
+        const float c = ze / (nz * ne);
+        const float4 out = mul4(c, acc);
+        if (e.aux) st4(e.aux + off, acc);
+        if (e.aux_w && li == 0) e.aux_w[row] = c;
+        if (e.y) st4(e.y + off, out);
+        if (e.s_out) st4(e.s_out + off, e.s_in ? add4(ld4(e.s_in + off), out) : out);
+    } else if constexpr (KIND == RSX_EPI_LAYERGCN_BWD) {
+        float4 dE = acc;
+        if (e.r_add) dE = add4(dE, ld4(e.r_add + off));
+        const float4 z = ld4(e.aux + off);
+        const float4 e0 = ld4(e.e0 + off);
+        const float c = e.aux_w[row];
+        const float zz = group_sum<G>(dot4(z, z));
+        const float ee = group_sum<G>(dot4(e0, e0));
+        const float gz = group_sum<G>(dot4(dE, z));
+        const float rz = sqrtf(zz), re = sqrtf(ee);
+        const float nz = fmaxf(rz, 1e-8f), ne = fmaxf(re, 1e-8f);
+        const float inv = 1.f / (nz * ne);
+        // d c / d z = e/(nz ne) - c z/|z|^2 ; d c / d e = z/(nz ne) - c e/|e|^2
+        // (the clamped norm is a constant when |x| < eps: no second term then)
+        const float kz = rz > 1e-8f ? c / (nz * nz) : 0.f;
+        const float ke = re > 1e-8f ? c / (ne * ne) : 0.f;
+        float4 dz = mul4(c, dE);
+        dz = fma4(gz * inv, e0, dz);
+        dz = fma4(-gz * kz, z, dz);
+        if (e.y) st4(e.y + off, dz);
+        if (e.s_out) {
+            float4 de = mul4(gz * inv, z);
+            de = fma4(-gz * ke, e0, de);
+            st4(e.s_out + off, e.s_in ? add4(ld4(e.s_in + off), de) : de);
+        }
+    }
+    if (e.zero0) st4(e.zero0 + off, f4(0.f));
+    if (e.zero1) st4(e.zero1 + off, f4(0.f));
+}
+
+// ---------------------------------------------------------------------------
+// kernels
+// ---------------------------------------------------------------------------
+constexpr int kBlock = 256;
+constexpr int kUnroll = 8;
+
+// One group of G lanes per work item {row, slot, begin, end}.
+template <int D, int KIND>
+__global__ __launch_bounds__(kBlock) void spmm_main(rsx_csr a, const float* __restrict__ x,
+                                                    rsx_epilogue e, float* __restrict__ slab) {
+    constexpr int G = D / 4;
+    constexpr int GPB = kBlock / G;
+    const int li = threadIdx.x % G;
+    const int64_t w = (int64_t)blockIdx.x * GPB + threadIdx.x / G;
+    if (w >= a.n_work) return;  // whole groups leave together
+    const int4 wk = reinterpret_cast<const int4*>(a.work)[w];
+    const int32_t* __restrict__ col = a.col;
+    const float* __restrict__ val = a.val;
+    const float* xl = x + li * 4;
+    float4 acc = f4(0.f);
+    int j = wk.z;
+    const int end = wk.w;
+    for (; j + kUnroll <= end; j += kUnroll) {
+        int c[kUnroll];
+        float v[kUnroll];
+#pragma unroll
+        for (int t = 0; t < kUnroll; ++t) {
+            c[t] = col[j + t];
+            v[t] = val[j + t];
+        }
+        float4 xv[kUnroll];
+#pragma unroll
+        for (int t = 0; t < kUnroll; ++t) xv[t] = ld4(xl + (int64_t)c[t] * D);
+#pragma unroll
+        for (int t = 0; t < kUnroll; ++t) acc = fma4(v[t], xv[t], acc);
+    }
+    if (j < end) {
+        int c[kUnroll];
+        float v[kUnroll];
+#pragma unroll
+        for (int t = 0; t < kUnroll; ++t) {
+            const bool ok = j + t < end;
+            c[t] = ok ? col[j + t] : 0;
+            v[t] = ok ? val[j + t] : 0.f;
+        }
+        float4 xv[kUnroll];
+#pragma unroll
+        for (int t = 0; t < kUnroll; ++t) xv[t] = (j + t < end) ? ld4(xl + (int64_t)c[t] * D) : f4(0.f);
+#pragma unroll
+        for (int t = 0; t < kUnroll; ++t)
+            if (j + t < end) acc = fma4(v[t], xv[t], acc);
+    }
+    if (wk.y < 0) {
+        epilogue<KIND, D>(e, wk.x, acc, li);
+    } else {
+        st4(slab + (int64_t)wk.y * D + li * 4, acc);
+    }
+}
+
+// One group per long row: add its slab partials in chunk order, then the epilogue.
+template <int D, int KIND>
+__global__ __launch_bounds__(kBlock) void spmm_fixup(rsx_csr a, rsx_epilogue e,
+                                                     const float* __restrict__ slab) {
+    constexpr int G = D / 4;
+    constexpr int GPB = kBlock / G;
+    const int li = threadIdx.x % G;
+    const int64_t w = (int64_t)blockIdx.x * GPB + threadIdx.x / G;
+    if (w >= a.n_long) return;
+    const int4 lr = reinterpret_cast<const int4*>(a.long_rows)[w];
+    float4 acc = f4(0.f);
+    for (int s = 0; s < lr.z; ++s) acc = add4(acc, ld4(slab + (int64_t)(lr.y + s) * D + li * 4));
+    epilogue<KIND, D>(e, lr.x, acc, li);
+}
+
+// acc = 0 for every row (stand-alone Adam, K = 0 forward, first LayerGCN backward step).
+template <int D, int KIND>
+__global__ __launch_bounds__(kBlock) void rowwise_kernel(int64_t n_rows, rsx_epilogue e) {
+    constexpr int G = D / 4;
+    constexpr int GPB = kBlock / G;
+    const int li = threadIdx.x % G;
+    const int64_t row = (int64_t)blockIdx.x * GPB + threadIdx.x / G;
+    if (row >= n_rows) return;
+    epilogue<KIND, D>(e, row, f4(0.f), li);
+}
+
+template <int D, int KIND>
+static int launch_spmm(const rsx_csr& a, const float* x, const rsx_epilogue& e, float* slab,
+                       hipStream_t s) {
+    constexpr int GPB = kBlock / (D / 4);
+    if (a.n_work > 0) {
+        const int64_t nb = (a.n_work + GPB - 1) / GPB;
+        hipLaunchKernelGGL((spmm_main<D, KIND>), dim3((unsigned)nb), dim3(kBlock), 0, s, a, x, e, slab);
+    }
+    if (a.n_long > 0) {
+        const int64_t nb = (a.n_long + GPB - 1) / GPB;
+        hipLaunchKernelGGL((spmm_fixup<D, KIND>), dim3((unsigned)nb), dim3(kBlock), 0, s, a, e,
+                           (const float*)slab);
+    }
+    return last_rc();
+}
+
+template <int D, int KIND>
+static int launch_rowwise(int64_t n, const rsx_epilogue& e, hipStream_t s) {
+    constexpr int GPB = kBlock / (D / 4);
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL((rowwise_kernel<D, KIND>), dim3((unsigned)((n + GPB - 1) / GPB)), dim3(kBlock), 0,
+                       s, n, e);
+    return last_rc();
+}
+
+template <int D>
+static int spmm_d(const rsx_csr& a, const float* x, const rsx_epilogue& e, float* slab, hipStream_t s) {
+    switch (e.kind) {
+        case RSX_EPI_STORE: return launch_spmm<D, RSX_EPI_STORE>(a, x, e, slab, s);
+        case RSX_EPI_LAYERSUM: return launch_spmm<D, RSX_EPI_LAYERSUM>(a, x, e, slab, s);
+        case RSX_EPI_FINAL: return launch_spmm<D, RSX_EPI_FINAL>(a, x, e, slab, s);
+        case RSX_EPI_ADAM: return launch_spmm<D, RSX_EPI_ADAM>(a, x, e, slab, s);
+        case RSX_EPI_LAYERGCN: return launch_spmm<D, RSX_EPI_LAYERGCN>(a, x, e, slab, s);
+        case RSX_EPI_AXPBY: return launch_spmm<D, RSX_EPI_AXPBY>(a, x, e, slab, s);
+        case RSX_EPI_LAYERGCN_BWD: return launch_spmm<D, RSX_EPI_LAYERGCN_BWD>(a, x, e, slab, s);
+        default: return RSX_ERR_ARG;
+    }
+}
+
+template <int D>
+static int rowwise_d(int64_t n, const rsx_epilogue& e, hipStream_t s) {
+    switch (e.kind) {
+        case RSX_EPI_STORE: return launch_rowwise<D, RSX_EPI_STORE>(n, e, s);
+        case RSX_EPI_LAYERSUM: return launch_rowwise<D, RSX_EPI_LAYERSUM>(n, e, s);
+        case RSX_EPI_FINAL: return launch_rowwise<D, RSX_EPI_FINAL>(n, e, s);
+        case RSX_EPI_ADAM: return launch_rowwise<D, RSX_EPI_ADAM>(n, e, s);
+        case RSX_EPI_LAYERGCN: return launch_rowwise<D, RSX_EPI_LAYERGCN>(n, e, s);
+        case RSX_EPI_AXPBY: return launch_rowwise<D, RSX_EPI_AXPBY>(n, e, s);
+        case RSX_EPI_LAYERGCN_BWD: return launch_rowwise<D, RSX_EPI_LAYERGCN_BWD>(n, e, s);
+        default: return RSX_ERR_ARG;
+    }
+}
+
+int spmm_dispatch(const rsx_csr& a, const float* x, int d, const rsx_epilogue& e, float* slab,
+                  hipStream_t s) {
+    if (a.n_long > 0 && !slab) return RSX_ERR_WORKSPACE;
+    switch (d) {
+        case 32: return spmm_d<32>(a, x, e, slab, s);
+        case 64: return spmm_d<64>(a, x, e, slab, s);
+        case 128: return spmm_d<128>(a, x, e, slab, s);
+        case 256: return spmm_d<256>(a, x, e, slab, s);
+        default: return RSX_ERR_UNSUPPORTED;
+    }
+}
+
+int rowwise_dispatch(int64_t n, int d, const rsx_epilogue& e, hipStream_t s) {
+    switch (d) {
+        case 32: return rowwise_d<32>(n, e, s);
+        case 64: return rowwise_d<64>(n, e, s);
+        case 128: return rowwise_d<128>(n, e, s);
+        case 256: return rowwise_d<256>(n, e, s);
+        default: return RSX_ERR_UNSUPPORTED;
+    }
+}
+
+}  // namespace rsx
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+extern "C" {
+
+const char* rsx_version(void) { return "rsx 0.1.0 gfx950"; }
+
+int rsx_csr_schedule_host(const int64_t* rowptr_host, int64_t n_rows, int32_t chunk, int32_t* work_host,
+                          int32_t* long_host, int64_t* n_work, int64_t* n_long, int64_t* n_slots) {
+    if (!rowptr_host || n_rows < 0 || chunk <= 0 || !n_work || !n_long || !n_slots) return RSX_ERR_ARG;
+    if (rowptr_host[n_rows] >= (int64_t(1) << 31)) return RSX_ERR_ARG;
+    int64_t nw = 0, nl = 0, ns = 0;
+    for (int64_t r = 0; r < n_rows; ++r) {
+        const int64_t b = rowptr_host[r], e = rowptr_host[r + 1];
+        const int64_t deg = e - b;
+        if (deg <= chunk) {
+            if (work_host) {
+                int32_t* w = work_host + 4 * nw;
+                w[0] = (int32_t)r; w[1] = -1; w[2] = (int32_t)b; w[3] = (int32_t)e;
+            }
+            ++nw;
+        } else {
+            const int64_t nc = (deg + chunk - 1) / chunk;
+            if (long_host) {
+                int32_t* l = long_host + 4 * nl;
+                l[0] = (int32_t)r; l[1] = (int32_t)ns; l[2] = (int32_t)nc; l[3] = 0;
+            }
+            for (int64_t c = 0; c < nc; ++c) {
+                if (work_host) {
+                    int32_t* w = work_host + 4 * nw;
+                    const int64_t cb = b + c * chunk;
+                    const int64_t ce = cb + chunk < e ? cb + chunk : e;
+                    w[0] = (int32_t)r; w[1] = (int32_t)(ns + c); w[2] = (int32_t)cb; w[3] = (int32_t)ce;
+                }
+                ++nw;
+            }
+            ns += nc;
+            ++nl;
+        }
+    }
+    *n_work = nw;
+    *n_long = nl;
+    *n_slots = ns;
+    return RSX_OK;
+}
+
+int rsx_spmm(const rsx_csr* a, const float* x, int32_t d, const rsx_epilogue* epi, float* slab,
+             rsx_stream_t stream) {
+    if (!a || !x || !epi) return RSX_ERR_ARG;
+    return rsx::spmm_dispatch(*a, x, d, *epi, slab, rsx::as_stream(stream));
+}
+
+int rsx_rowwise(int64_t n_rows, int32_t d, const rsx_epilogue* epi, rsx_stream_t stream) {
+    if (!epi || n_rows < 0) return RSX_ERR_ARG;
+    return rsx::rowwise_dispatch(n_rows, d, *epi, rsx::as_stream(stream));
+}
+
+}  // extern "C"

@@ -1,0 +1,233 @@
+// step.hip — device triplet sampler and the fused LightGCN step / forward (gfx950).
+//
+// Sampler: replaces TrainDataLoader's per-epoch shuffle + Python rejection
+// sampling of negatives (reference src/utils/dataloader.py:226-275,307-309,
+// src/utils/dataset.py:98-101) in throughput mode.  The epoch order is a keyed
+// Feistel bijection of [0, n_inter) (cycle walking), so a batch needs no stored
+// permutation; negatives are drawn uniformly from the training-item list and
+// redrawn while they hit the user's sorted training history.
+//
+// LightGCN step: the reference batch (src/models/lightgcn.py:117-156, autograd
+// backward, src/common/trainer.py:238 Adam) as 2K+2 launches (+1 per layer when
+// the graph has hub rows split over several work items):
+//   forward   E^k = A E^{k-1}, running sum S, last layer writes F = S/(K+1) and
+//             zeroes the gradient scratch G, R;
+//   loss      BPR fwd+bwd: G += dL/dF (batch rows), R += d reg / d E^0;
+//   backward  Horner: H_k = A H_{k-1} (H_0 = G), S = sum H; the last layer
+//             applies Adam to E^0 with g = S/(K+1) + R in its epilogue.
+#include "rsx_common.hpp"
+
+namespace rsx {
+
+int spmm_dispatch(const rsx_csr& a, const float* x, int d, const rsx_epilogue& e, float* slab, hipStream_t s);
+int rowwise_dispatch(int64_t n, int d, const rsx_epilogue& e, hipStream_t s);
+int bpr_call(int32_t variant, const float* fin, const float* ego, int64_t n_users, int64_t n_items, int32_t d,
+             const int64_t* trip, int64_t batch, float reg, float batch_cfg, float* g_fin, float* g_ego,
+             float* loss_out, double* loss_acc, void* ws, size_t ws_bytes, hipStream_t s);
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z += 0x9e3779b97f4a7c15ull;
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ uint64_t feistel(uint64_t x, int hb, uint64_t key) {
+    const uint64_t mask = (1ull << hb) - 1;
+    uint64_t L = x >> hb, R = x & mask;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const uint64_t F = mix64(R ^ (key + (uint64_t)r * 0x632be59bd9b4e019ull)) & mask;
+        const uint64_t nl = R;
+        R = L ^ F;
+        L = nl;
+    }
+    return (L << hb) | R;
+}
+
+__device__ __forceinline__ uint64_t permute(uint64_t i, uint64_t n, int hb, uint64_t key) {
+    uint64_t x = i;
+    do {
+        x = feistel(x, hb, key);
+    } while (x >= n);
+    return x;
+}
+
+__device__ __forceinline__ bool in_sorted(const int32_t* a, int64_t lo, int64_t hi, int32_t v) {
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        const int32_t x = a[mid];
+        if (x == v) return true;
+        if (x < v) lo = mid + 1; else hi = mid;
+    }
+    return false;
+}
+
+__global__ __launch_bounds__(256) void sample_kernel(rsx_sampler_args s, int hb, int64_t count, int64_t* out) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= count) return;
+    const uint64_t key = mix64(s.seed ^ mix64((uint64_t)s.epoch + 0x1234567ull));
+    const int64_t pos = s.start + t;
+    const int64_t e = (int64_t)permute((uint64_t)pos, (uint64_t)s.n_inter, hb, key);
+    const int32_t u = s.inter_u[e];
+    const int32_t p = s.inter_i[e];
+    const int64_t lo = s.hist_rowptr[u], hi = s.hist_rowptr[u + 1];
+    uint64_t st = mix64(key ^ mix64((uint64_t)pos * 0x9e3779b97f4a7c15ull + 17));
+    int32_t n = 0;
+    for (int attempt = 0; attempt < 1024; ++attempt) {
+        st = mix64(st + (uint64_t)attempt);
+        n = s.all_items[st % (uint64_t)s.n_all_items];
+        if (!in_sorted(s.hist_col, lo, hi, n)) break;
+    }
+    out[t] = u;
+    out[count + t] = p;
+    out[2 * count + t] = n;
+}
+
+int sample_call(const rsx_sampler_args& s, int64_t batch, int64_t* out, hipStream_t st) {
+    if (!s.inter_u || !s.inter_i || !s.hist_rowptr || !s.all_items || s.n_inter <= 0 || s.n_all_items <= 0 ||
+        !out || batch <= 0 || s.start < 0 || s.start >= s.n_inter)
+        return RSX_ERR_ARG;
+    const int64_t count = (s.n_inter - s.start) < batch ? (s.n_inter - s.start) : batch;
+    int bits = 2;
+    while ((1ll << bits) < s.n_inter) ++bits;
+    if (bits & 1) ++bits;
+    hipLaunchKernelGGL(sample_kernel, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, st, s, bits / 2, count,
+                       out);
+    return last_rc();
+}
+
+static rsx_epilogue epi0(int kind) {
+    rsx_epilogue e = {};
+    e.kind = kind;
+    e.alpha = 1.f;
+    e.beta = 1.f;
+    return e;
+}
+
+// forward: returns rc; writes final = mean_{k=0..K} A^k p; zeroes z0/z1 rows in the last pass.
+static int lgcn_forward(const rsx_csr& A, int d, int K, const float* p, float* s, float* h0, float* h1, float* fin,
+                        float* slab, float* z0, float* z1, hipStream_t st) {
+    const float beta = 1.f / (float)(K + 1);
+    int rc;
+    if (K == 0) {
+        rsx_epilogue e = epi0(RSX_EPI_FINAL);
+        e.s_in = p;
+        e.f = fin;
+        e.zero0 = z0;
+        e.zero1 = z1;
+        return rowwise_dispatch(A.n_rows, d, e, st);
+    }
+    const float* x = p;
+    float* bufs[2] = {h0, h1};
+    for (int k = 1; k <= K; ++k) {
+        rsx_epilogue e;
+        if (k == K) {
+            e = epi0(RSX_EPI_FINAL);
+            e.s_in = (k == 1) ? p : s;
+            e.f = fin;
+            e.beta = beta;
+            e.zero0 = z0;
+            e.zero1 = z1;
+        } else {
+            e = epi0(RSX_EPI_LAYERSUM);
+            e.y = bufs[(k - 1) & 1];
+            e.s_in = (k == 1) ? p : s;
+            e.s_out = s;
+        }
+        if ((rc = spmm_dispatch(A, x, d, e, slab, st))) return rc;
+        x = bufs[(k - 1) & 1];
+    }
+    return 0;
+}
+
+}  // namespace rsx
+
+extern "C" {
+
+int rsx_sample_triplets(const int32_t* inter_u, const int32_t* inter_i, int64_t n_inter, const int64_t* hist_rowptr,
+                        const int32_t* hist_col, const int32_t* all_items, int64_t n_all_items, uint64_t seed,
+                        int64_t epoch, int64_t start, int64_t batch, int64_t* out, rsx_stream_t stream) {
+    rsx_sampler_args s;
+    s.inter_u = inter_u;
+    s.inter_i = inter_i;
+    s.n_inter = n_inter;
+    s.hist_rowptr = hist_rowptr;
+    s.hist_col = hist_col;
+    s.all_items = all_items;
+    s.n_all_items = n_all_items;
+    s.seed = seed;
+    s.epoch = epoch;
+    s.start = start;
+    return rsx::sample_call(s, batch, out, rsx::as_stream(stream));
+}
+
+int rsx_lightgcn_forward(const rsx_csr* adj, int32_t d, int32_t n_layers, const float* p, float* s, float* h0,
+                         float* h1, float* final_emb, float* slab, rsx_stream_t stream) {
+    if (!adj || !p || !final_emb || n_layers < 0) return RSX_ERR_ARG;
+    if (n_layers >= 2 && (!s || !h0 || !h1)) return RSX_ERR_ARG;
+    return rsx::lgcn_forward(*adj, d, n_layers, p, s, h0, h1, final_emb, slab, nullptr, nullptr,
+                             rsx::as_stream(stream));
+}
+
+int rsx_lightgcn_step(const rsx_lgcn_step* st, rsx_stream_t stream) {
+    using namespace rsx;
+    if (!st || !st->adj || !st->p || !st->m || !st->v || !st->final_emb || !st->g || !st->r || !st->triplets)
+        return RSX_ERR_ARG;
+    const rsx_csr& A = *st->adj;
+    const int d = st->d, K = st->n_layers;
+    if (K < 0 || A.n_rows != st->n_users + st->n_items) return RSX_ERR_ARG;
+    if (K >= 2 && (!st->s || !st->h0 || !st->h1)) return RSX_ERR_ARG;
+    hipStream_t s = as_stream(stream);
+    int rc;
+    int64_t batch = st->batch;
+    if (st->sample) {
+        const rsx_sampler_args& sa = *st->sample;
+        if ((rc = sample_call(sa, st->batch, st->triplets, s))) return rc;
+        batch = (sa.n_inter - sa.start) < st->batch ? (sa.n_inter - sa.start) : st->batch;
+    }
+    // forward (last layer zeroes g and r)
+    if ((rc = lgcn_forward(A, d, K, st->p, st->s, st->h0, st->h1, st->final_emb, st->slab, st->g, st->r, s)))
+        return rc;
+    // BPR loss + gradients
+    if ((rc = bpr_call(RSX_BPR_LIGHTGCN, st->final_emb, st->p, st->n_users, st->n_items, d, st->triplets, batch,
+                       st->reg, (float)batch, st->g, st->r, st->loss_out, st->loss_acc, st->ws, st->ws_bytes, s)))
+        return rc;
+    // backward (Horner) with Adam fused into the last layer
+    const float beta = 1.f / (float)(K + 1);
+    if (K == 0) {
+        rsx_epilogue e = epi0(RSX_EPI_ADAM);
+        e.s_in = st->g;
+        e.r_add = st->r;
+        e.p = st->p;
+        e.m = st->m;
+        e.v = st->v;
+        e.adam = st->adam;
+        return rowwise_dispatch(A.n_rows, d, e, s);
+    }
+    const float* x = st->g;
+    float* bufs[2] = {st->h0, st->h1};
+    for (int k = 1; k <= K; ++k) {
+        rsx_epilogue e;
+        if (k == K) {
+            e = epi0(RSX_EPI_ADAM);
+            e.s_in = (k == 1) ? st->g : st->s;
+            e.beta = beta;
+            e.r_add = st->r;
+            e.p = st->p;
+            e.m = st->m;
+            e.v = st->v;
+            e.adam = st->adam;
+        } else {
+            e = epi0(RSX_EPI_LAYERSUM);
+            e.y = bufs[(k - 1) & 1];
+            e.s_in = (k == 1) ? st->g : st->s;
+            e.s_out = st->s;
+        }
+        if ((rc = spmm_dispatch(A, x, d, e, st->slab, s))) return rc;
+        x = bufs[(k - 1) & 1];
+    }
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,128 @@
+"""ctypes binding of librsx.so (include/rsx.h).
+
+The product path has no CPU fallback: `lib()` raises if the library is missing
+or cannot be loaded, and every wrapper raises RuntimeError on a nonzero return
+code, as the reference raises Python exceptions for bad inputs.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+from . import build as _build
+
+P = C.c_void_p
+I64 = C.c_int64
+I32 = C.c_int32
+F32 = C.c_float
+
+RSX_EPI_STORE = 0
+RSX_EPI_LAYERSUM = 1
+RSX_EPI_FINAL = 2
+RSX_EPI_ADAM = 3
+RSX_EPI_LAYERGCN = 4
+RSX_EPI_AXPBY = 5
+RSX_EPI_LAYERGCN_BWD = 6
+
+RSX_BPR_LIGHTGCN = 0
+RSX_BPR_LAYERGCN = 1
+RSX_BPR_SMORE = 2
+
+_ERRORS = {1001: "RSX_ERR_ARG (bad size or null pointer)",
+           1002: "RSX_ERR_UNSUPPORTED (embedding width / k not compiled)",
+           1003: "RSX_ERR_WORKSPACE (workspace too small)"}
+
+
+class Csr(C.Structure):
+    _fields_ = [("n_rows", I64), ("n_cols", I64), ("nnz", I64), ("rowptr", P), ("col", P), ("val", P),
+                ("chunk", I32), ("pad0", I32), ("n_work", I64), ("work", P), ("n_long", I64),
+                ("long_rows", P), ("n_slots", I64)]
+
+
+class Adam(C.Structure):
+    _fields_ = [("lr", F32), ("beta1", F32), ("beta2", F32), ("eps", F32), ("weight_decay", F32),
+                ("pad0", I32), ("step_dev", P), ("step", I64)]
+
+
+class Epilogue(C.Structure):
+    _fields_ = [("kind", I32), ("pad0", I32), ("alpha", F32), ("beta", F32),
+                ("y", P), ("s_in", P), ("s_out", P), ("f", P), ("zero0", P), ("zero1", P), ("r_add", P),
+                ("p", P), ("m", P), ("v", P), ("g_out", P), ("e0", P), ("aux", P), ("aux_w", P),
+                ("adam", Adam)]
+
+
+class SamplerArgs(C.Structure):
+    _fields_ = [("inter_u", P), ("inter_i", P), ("n_inter", I64), ("hist_rowptr", P), ("hist_col", P),
+                ("all_items", P), ("n_all_items", I64), ("seed", C.c_uint64), ("epoch", I64), ("start", I64)]
+
+
+class LgcnStep(C.Structure):
+    _fields_ = [("adj", C.POINTER(Csr)), ("n_users", I64), ("n_items", I64), ("d", I32), ("n_layers", I32),
+                ("reg", F32), ("pad0", I32),
+                ("p", P), ("m", P), ("v", P), ("s", P), ("h0", P), ("h1", P), ("final_emb", P), ("g", P),
+                ("r", P), ("slab", P), ("triplets", P), ("batch", I64), ("sample", C.POINTER(SamplerArgs)),
+                ("adam", Adam), ("loss_out", P), ("loss_acc", P), ("ws", P), ("ws_bytes", C.c_size_t)]
+
+
+_LIB = None
+
+
+def _declare(lib):
+    sig = {
+        "rsx_version": (C.c_char_p, []),
+        "rsx_csr_schedule_host": (C.c_int, [P, I64, I32, P, P, C.POINTER(I64), C.POINTER(I64), C.POINTER(I64)]),
+        "rsx_spmm": (C.c_int, [C.POINTER(Csr), P, I32, C.POINTER(Epilogue), P, P]),
+        "rsx_rowwise": (C.c_int, [I64, I32, C.POINTER(Epilogue), P]),
+        "rsx_bpr_ws_bytes": (C.c_size_t, [I64]),
+        "rsx_bpr": (C.c_int, [I32, P, P, I64, I64, I32, P, I64, F32, F32, P, P, P, P, P, C.c_size_t, P]),
+        "rsx_fullsort_ws_bytes": (C.c_size_t, [I64, I64, I32]),
+        "rsx_fullsort_topk": (C.c_int, [P, P, I64, P, I64, I32, P, P, I32, P, P, P, C.c_size_t, P]),
+        "rsx_score_dense": (C.c_int, [P, P, I64, P, I64, I32, P, P]),
+        "rsx_sample_triplets": (C.c_int, [P, P, I64, P, P, P, I64, C.c_uint64, I64, I64, I64, P, P]),
+        "rsx_gather_rows": (C.c_int, [P, P, I64, I64, I32, P, P]),
+        "rsx_lightgcn_step": (C.c_int, [C.POINTER(LgcnStep), P]),
+        "rsx_lightgcn_forward": (C.c_int, [C.POINTER(Csr), I32, I32, P, P, P, P, P, P, P]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    for name, (res, args) in _OPTIONAL.items():
+        if hasattr(lib, name):
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+
+
+# entry points added by later translation units (SMORE fused pass etc.)
+_OPTIONAL: dict = {}
+
+EXPORTED = ["rsx_version", "rsx_csr_schedule_host", "rsx_spmm", "rsx_rowwise", "rsx_bpr_ws_bytes", "rsx_bpr",
+            "rsx_fullsort_ws_bytes", "rsx_fullsort_topk", "rsx_score_dense", "rsx_sample_triplets",
+            "rsx_gather_rows", "rsx_lightgcn_step", "rsx_lightgcn_forward"]
+
+
+def lib_path() -> str:
+    return os.environ.get("RSX_LIB", _build.LIB)
+
+
+def lib():
+    """Load librsx.so (building it first if the sources are newer and hipcc exists)."""
+    global _LIB
+    if _LIB is None:
+        path = lib_path()
+        if not os.path.exists(path) or _build._needs_build():
+            try:
+                _build.build()
+            except Exception as e:  # noqa: BLE001
+                if not os.path.exists(path):
+                    raise RuntimeError(f"librsx.so missing at {path} and the build failed: {e}") from e
+        _LIB = C.CDLL(path)
+        _declare(_LIB)
+    return _LIB
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = _ERRORS.get(rc, f"hipError {rc}")
+        raise RuntimeError(f"{what} failed: {msg}")

@@ -1,0 +1,297 @@
+"""Torch-tensor wrappers over the librsx C ABI (device memory and streams come from torch).
+
+Every op checks that its tensors live on the GPU and raises otherwise: there is
+no CPU fallback on the product path.  Each wrapper cites the reference call
+site it replaces (paths relative to the reference root).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import torch
+
+from . import _lib as L
+
+
+def _p(t):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def _pi(t):
+    return 0 if t is None else t.data_ptr()
+
+
+def _stream():
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _gpu(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("rsx ops run on the GPU (HIP kernels); got a CPU tensor")
+        if t is not None and not t.is_contiguous():
+            raise RuntimeError("rsx ops need contiguous tensors")
+
+
+def require_device(device) -> torch.device:
+    device = torch.device(device)
+    if device.type != "cuda" or not torch.cuda.is_available():
+        raise RuntimeError("rsx: the HIP path needs a ROCm GPU (config use_gpu/device); no CPU fallback")
+    L.lib()
+    return device
+
+
+# ---------------------------------------------------------------------------
+# CSR adjacency + schedule
+# ---------------------------------------------------------------------------
+class DeviceCSR:
+    """Row-major CSR on the device plus the nnz-balanced work schedule.
+
+    Built once per graph from host arrays (rowptr int64, col int32, val f32).
+    Replaces the torch COO adjacency of reference src/models/lightgcn.py:65-103.
+    """
+
+    def __init__(self, rowptr: np.ndarray, col: np.ndarray, val: np.ndarray, n_cols: int, device,
+                 chunk: int = 32):
+        lib = L.lib()
+        rowptr = np.ascontiguousarray(rowptr, dtype=np.int64)
+        col = np.ascontiguousarray(col, dtype=np.int32)
+        val = np.ascontiguousarray(val, dtype=np.float32)
+        n_rows = rowptr.size - 1
+        nw, nl, ns = C.c_int64(), C.c_int64(), C.c_int64()
+        L.check(lib.rsx_csr_schedule_host(rowptr.ctypes.data_as(C.c_void_p), n_rows, chunk, None, None,
+                                          C.byref(nw), C.byref(nl), C.byref(ns)), "rsx_csr_schedule_host")
+        work = np.zeros((max(nw.value, 1), 4), dtype=np.int32)
+        longr = np.zeros((max(nl.value, 1), 4), dtype=np.int32)
+        L.check(lib.rsx_csr_schedule_host(rowptr.ctypes.data_as(C.c_void_p), n_rows, chunk,
+                                          work.ctypes.data_as(C.c_void_p), longr.ctypes.data_as(C.c_void_p),
+                                          C.byref(nw), C.byref(nl), C.byref(ns)), "rsx_csr_schedule_host")
+        self.device = torch.device(device)
+        self.n_rows, self.n_cols, self.nnz = int(n_rows), int(n_cols), int(col.size)
+        self.chunk = chunk
+        self.n_work, self.n_long, self.n_slots = nw.value, nl.value, ns.value
+        self.rowptr_host = rowptr
+        self.rowptr = torch.from_numpy(rowptr).to(self.device)
+        self.col = torch.from_numpy(col).to(self.device)
+        self.val = torch.from_numpy(val).to(self.device)
+        self.work = torch.from_numpy(work).to(self.device)
+        self.long_rows = torch.from_numpy(longr).to(self.device)
+        self.struct = L.Csr(self.n_rows, self.n_cols, self.nnz, self.rowptr.data_ptr(), self.col.data_ptr(),
+                            self.val.data_ptr(), chunk, 0, self.n_work, self.work.data_ptr(), self.n_long,
+                            self.long_rows.data_ptr(), self.n_slots)
+        self._slabs = {}
+
+    @classmethod
+    def from_scipy(cls, m, device, chunk: int = 32):
+        m = m.tocsr()
+        m.sort_indices()
+        return cls(m.indptr.astype(np.int64), m.indices.astype(np.int32), m.data.astype(np.float32), m.shape[1],
+                   device, chunk)
+
+    def slab(self, d: int):
+        if self.n_slots == 0:
+            return None
+        s = self._slabs.get(d)
+        if s is None:
+            s = torch.empty(self.n_slots * d, dtype=torch.float32, device=self.device)
+            self._slabs[d] = s
+        return s
+
+    def spmm_epi(self, x: torch.Tensor, epi: "L.Epilogue", d: int):
+        _gpu(x)
+        rc = L.lib().rsx_spmm(C.byref(self.struct), _p(x), d, C.byref(epi), _p(self.slab(d)), _stream())
+        L.check(rc, "rsx_spmm")
+
+    def spmm(self, x: torch.Tensor, alpha: float = 1.0, out: torch.Tensor | None = None) -> torch.Tensor:
+        """y = alpha * A @ x (torch.sparse.mm(A, x), reference lightgcn.py:122)."""
+        if x.shape[0] != self.n_cols:
+            raise RuntimeError(f"spmm: x has {x.shape[0]} rows, A has {self.n_cols} columns")
+        d = x.shape[1]
+        y = out if out is not None else torch.empty(self.n_rows, d, dtype=torch.float32, device=x.device)
+        self.spmm_epi(x, epi(L.RSX_EPI_STORE, alpha=alpha, y=y), d)
+        return y
+
+
+def epi(kind: int, alpha: float = 1.0, beta: float = 1.0, adam: "L.Adam | None" = None, **ptrs) -> "L.Epilogue":
+    e = L.Epilogue()
+    e.kind = kind
+    e.alpha = alpha
+    e.beta = beta
+    for k, t in ptrs.items():
+        setattr(e, k, _pi(t))
+    if adam is not None:
+        e.adam = adam
+    return e
+
+
+def adam_struct(lr: float, step: int, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.0, step_dev=None):
+    a = L.Adam()
+    a.lr, a.beta1, a.beta2, a.eps, a.weight_decay = lr, beta1, beta2, eps, weight_decay
+    a.step_dev = _pi(step_dev)
+    a.step = int(step)
+    return a
+
+
+def rowwise(n_rows: int, d: int, e: "L.Epilogue"):
+    L.check(L.lib().rsx_rowwise(n_rows, d, C.byref(e), _stream()), "rsx_rowwise")
+
+
+def adam_(p: torch.Tensor, g: torch.Tensor, m: torch.Tensor, v: torch.Tensor, step: int, lr: float,
+          betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0):
+    """In-place Adam on one parameter tensor (torch.optim.Adam, reference trainer.py:133,238)."""
+    _gpu(p, g, m, v)
+    d = p.shape[-1] if p.dim() > 1 else p.numel()
+    n = p.numel() // d
+    if d not in (32, 64, 128, 256):
+        # flatten into 64-wide rows plus a tail handled as another view
+        flat = [t.view(-1) for t in (p, g, m, v)]
+        tot = flat[0].numel()
+        main = (tot // 64) * 64
+        if main:
+            adam_(*(f[:main].view(-1, 64) for f in flat), step=step, lr=lr, betas=betas, eps=eps,
+                  weight_decay=weight_decay)
+        if tot - main:
+            tail = [torch.zeros(32, dtype=torch.float32, device=p.device) for _ in range(4)]
+            for tt, f in zip(tail, flat):
+                tt[: tot - main].copy_(f[main:])
+            adam_(*(t.view(1, 32) for t in tail), step=step, lr=lr, betas=betas, eps=eps,
+                  weight_decay=weight_decay)
+            for tt, f, upd in zip(tail, flat, (True, False, True, True)):
+                if upd:
+                    f[main:].copy_(tt[: tot - main])
+        return
+    e = epi(L.RSX_EPI_ADAM, s_in=g, p=p, m=m, v=v,
+            adam=adam_struct(lr, step, betas[0], betas[1], eps, weight_decay))
+    rowwise(n, d, e)
+
+
+# ---------------------------------------------------------------------------
+# BPR
+# ---------------------------------------------------------------------------
+_WS = {}
+
+
+def _ws(device, nbytes: int) -> torch.Tensor:
+    key = (str(device),)
+    t = _WS.get(key)
+    if t is None or t.numel() < nbytes:
+        t = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
+        _WS[key] = t
+    return t
+
+
+def bpr(variant: int, final: torch.Tensor, ego: torch.Tensor | None, n_users: int, n_items: int,
+        triplets: torch.Tensor, reg: float, batch_cfg: float | None = None,
+        g_final: torch.Tensor | None = None, g_ego: torch.Tensor | None = None,
+        loss_acc: torch.Tensor | None = None):
+    """Fused BPR loss forward+backward; returns (loss[1], g_final, g_ego).
+
+    LightGCN: reference lightgcn.py:132-156; LayerGCN: layergcn.py:142-177; SMORE: smore.py:366-378.
+    """
+    _gpu(final, ego, triplets)
+    if triplets.dtype != torch.int64 or triplets.dim() != 2 or triplets.shape[0] < 3:
+        raise RuntimeError("bpr: triplets must be int64 [3, B]")
+    trip = triplets[:3].contiguous()
+    B = trip.shape[1]
+    d = final.shape[1]
+    lib = L.lib()
+    if g_final is None:
+        g_final = torch.zeros_like(final)
+    if g_ego is None and ego is not None and variant != L.RSX_BPR_SMORE:
+        g_ego = torch.zeros_like(ego)
+    loss = torch.empty(1, dtype=torch.float32, device=final.device)
+    nb = lib.rsx_bpr_ws_bytes(B)
+    ws = _ws(final.device, nb)
+    rc = lib.rsx_bpr(variant, _p(final), _p(ego), n_users, n_items, d, _p(trip), B, reg,
+                     float(batch_cfg if batch_cfg is not None else B), _p(g_final), _p(g_ego), _p(loss),
+                     _p(loss_acc), _p(ws), ws.numel(), _stream())
+    L.check(rc, "rsx_bpr")
+    return loss, g_final, g_ego
+
+
+# ---------------------------------------------------------------------------
+# full sort
+# ---------------------------------------------------------------------------
+def fullsort_topk(user_emb: torch.Tensor, users: torch.Tensor | None, item_emb: torch.Tensor,
+                  mask_rowptr: torch.Tensor | None, mask_col: torch.Tensor | None, k: int):
+    """Fused scores + train-item mask (-1e10) + top-k, order (score desc, index asc).
+
+    Replaces reference trainer.py:521-526 (full_sort_predict, mask, torch.topk).
+    """
+    _gpu(user_emb, users, item_emb, mask_rowptr, mask_col)
+    nb = users.numel() if users is not None else user_emb.shape[0]
+    ni, d = item_emb.shape
+    lib = L.lib()
+    val = torch.empty(nb, k, dtype=torch.float32, device=item_emb.device)
+    idx = torch.empty(nb, k, dtype=torch.int64, device=item_emb.device)
+    if nb == 0:
+        return val, idx
+    wsb = lib.rsx_fullsort_ws_bytes(nb, ni, k)
+    ws = _ws(item_emb.device, wsb)
+    rc = lib.rsx_fullsort_topk(_p(user_emb), _p(users), nb, _p(item_emb), ni, d, _p(mask_rowptr), _p(mask_col), k,
+                               _p(val), _p(idx), _p(ws), ws.numel(), _stream())
+    L.check(rc, "rsx_fullsort_topk")
+    return val, idx
+
+
+def score_dense(user_emb: torch.Tensor, users: torch.Tensor | None, item_emb: torch.Tensor) -> torch.Tensor:
+    """scores = user_emb[users] @ item_emb.T (reference lightgcn.py:164)."""
+    _gpu(user_emb, users, item_emb)
+    nb = users.numel() if users is not None else user_emb.shape[0]
+    ni, d = item_emb.shape
+    out = torch.empty(nb, ni, dtype=torch.float32, device=item_emb.device)
+    L.check(L.lib().rsx_score_dense(_p(user_emb), _p(users), nb, _p(item_emb), ni, d, _p(out), _stream()),
+            "rsx_score_dense")
+    return out
+
+
+def gather_rows(src: torch.Tensor, idx: torch.Tensor, offset: int = 0) -> torch.Tensor:
+    _gpu(src, idx)
+    d = src.shape[1]
+    out = torch.empty(idx.numel(), d, dtype=torch.float32, device=src.device)
+    L.check(L.lib().rsx_gather_rows(_p(src), _p(idx), idx.numel(), offset, d, _p(out), _stream()),
+            "rsx_gather_rows")
+    return out
+
+
+# ---------------------------------------------------------------------------
+# sampler
+# ---------------------------------------------------------------------------
+class DeviceSampler:
+    """Per-epoch shuffle + rejection negative sampling on the device (throughput mode).
+
+    Replaces reference TrainDataLoader._get_neg_sample / _sample_neg_ids / _random
+    (src/utils/dataloader.py:226-275,307-309) and RecDataset.shuffle (dataset.py:98-101).
+    """
+
+    def __init__(self, train_u: np.ndarray, train_i: np.ndarray, n_users: int, device, seed: int = 0):
+        order = np.lexsort((train_i, train_u))
+        u_sorted = train_u[order]
+        i_sorted = train_i[order]
+        rowptr = np.zeros(n_users + 1, dtype=np.int64)
+        np.add.at(rowptr, u_sorted + 1, 1)
+        rowptr = np.cumsum(rowptr)
+        self.device = torch.device(device)
+        self.n_inter = int(train_u.size)
+        self.inter_u = torch.from_numpy(train_u.astype(np.int32)).to(self.device)
+        self.inter_i = torch.from_numpy(train_i.astype(np.int32)).to(self.device)
+        self.hist_rowptr = torch.from_numpy(rowptr).to(self.device)
+        self.hist_col = torch.from_numpy(i_sorted.astype(np.int32)).to(self.device)
+        self.all_items = torch.from_numpy(np.unique(train_i).astype(np.int32)).to(self.device)
+        self.seed = int(seed) & ((1 << 64) - 1)
+
+    def args(self, epoch: int, start: int) -> "L.SamplerArgs":
+        return L.SamplerArgs(self.inter_u.data_ptr(), self.inter_i.data_ptr(), self.n_inter,
+                             self.hist_rowptr.data_ptr(), self.hist_col.data_ptr(), self.all_items.data_ptr(),
+                             self.all_items.numel(), self.seed, epoch, start)
+
+    def sample(self, epoch: int, start: int, batch: int, out: torch.Tensor | None = None) -> torch.Tensor:
+        count = min(batch, self.n_inter - start)
+        if out is None:
+            out = torch.empty(3, count, dtype=torch.int64, device=self.device)
+        L.check(L.lib().rsx_sample_triplets(self.inter_u.data_ptr(), self.inter_i.data_ptr(), self.n_inter,
+                                            self.hist_rowptr.data_ptr(), self.hist_col.data_ptr(),
+                                            self.all_items.data_ptr(), self.all_items.numel(), self.seed,
+                                            epoch, start, batch, _pi(out), _stream()), "rsx_sample_triplets")
+        return out

@@ -1,0 +1,373 @@
+#!/usr/bin/env python3
+"""Capture golden fixtures from the reference implementation (run in the build container only).
+
+The reference (`/root/reference`, MMRec fork) is pure Python on PyTorch and imports
+on CPU here with four harness-only shims; none of them
+modifies a reference file:
+
+1. `utils.data_utils` (torchvision/PIL image helpers, unused on the hot path,
+   imported by `src/utils/dataset.py:17`) is replaced by an empty module;
+2. `str()` is called on each split so that `RecDataset.inter_num` exists
+   (`src/utils/dataset.py:115`, needed at `src/utils/dataloader.py:55`);
+3. `torch.Tensor.cuda` is the identity while SMORE is built (`src/models/smore.py:63,73`);
+4. `torch_scatter.scatter_add` is restated with `index_add_` (`src/utils/utils.py:140`).
+
+Outputs are small `.npz` files under `tests/golden/` (data only: inputs and the
+reference's outputs). The reference itself never travels to the GPU box.
+
+Usage:  python tools/capture_golden.py [--out tests/golden]
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import platform
+import shutil
+import sys
+import types
+
+sys.dont_write_bytecode = True
+REF = "/root/reference/src"
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+sys.path.insert(0, os.path.join(REPO, "recommendar-systems_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from rsx import synth  # noqa: E402
+
+DATA_ROOT = "/tmp/rsx_golden_data/"
+
+
+def _install_shims():
+    sys.path.insert(0, REF)
+    du = types.ModuleType("utils.data_utils")
+    for n in ("ImageResize", "ImagePad", "image_to_tensor", "load_decompress_img_from_lmdb_value"):
+        setattr(du, n, None)
+    sys.modules["utils.data_utils"] = du
+    ts = types.ModuleType("torch_scatter")
+
+    def scatter_add(src, index, dim=0, dim_size=None):
+        out = torch.zeros(dim_size, dtype=src.dtype)
+        return out.index_add_(0, index, src)
+
+    ts.scatter_add = scatter_add
+    sys.modules["torch_scatter"] = ts
+
+
+def _load(model: str, dataset: str, overrides: dict):
+    from utils.configurator import Config
+    from utils.dataset import RecDataset
+    from utils.dataloader import TrainDataLoader, EvalDataLoader
+
+    cwd = os.getcwd()
+    os.chdir(REF)
+    try:
+        cfg = dict(gpu_id=0, use_gpu=False, data_path=DATA_ROOT)
+        cfg.update(overrides)
+        config = Config(model, dataset, cfg)
+    finally:
+        os.chdir(cwd)
+    ds = RecDataset(config)
+    str(ds)
+    tr, va, te = ds.split()
+    for s in (tr, va, te):
+        str(s)
+    train = TrainDataLoader(config, tr, batch_size=config["train_batch_size"], shuffle=True)
+    valid = EvalDataLoader(config, va, additional_dataset=tr, batch_size=config["eval_batch_size"])
+    test = EvalDataLoader(config, te, additional_dataset=tr, batch_size=config["eval_batch_size"])
+    return config, train, valid, test
+
+
+def _select_hparams(config):
+    """Pick the first value of every list-valued hyper parameter (reference quick_start:54-62)."""
+    from itertools import product
+    hp = list(config["hyper_parameters"])
+    if "seed" not in hp:
+        hp = ["seed"] + hp
+    combo = next(iter(product(*[config[k] or [None] for k in hp])))
+    for k, v in zip(hp, combo):
+        config[k] = v
+    return dict(zip(hp, combo))
+
+
+class _Recorder:
+    """Records every batch the reference TrainDataLoader yields."""
+
+    def __init__(self, loader):
+        self.loader = loader
+        self.batches = []
+        orig = loader._next_batch_data
+
+        def wrapped():
+            b = orig()
+            self.batches.append(b.clone())
+            return b
+
+        loader._next_batch_data = wrapped
+
+
+def _topk_with_ties(scores: torch.Tensor, k: int):
+    """torch.topk as in reference trainer.py:526 plus per-row near-tie flags at the k boundary
+    and inside the list (canonical order is score desc, index asc)."""
+    vals, idx = torch.topk(scores, k, dim=-1)
+    srt, _ = torch.sort(scores, dim=-1, descending=True)
+    kth = srt[:, k - 1]
+    nxt = srt[:, k] if scores.shape[1] > k else torch.full_like(kth, -float("inf"))
+    scale = srt[:, :1].abs().clamp_min(1e-6)
+    boundary_tie = (kth - nxt).abs() <= 1e-5 * scale[:, 0]
+    d = (srt[:, : k] - srt[:, 1: k + 1]).abs() if scores.shape[1] > k else (srt[:, :k - 1] - srt[:, 1:k]).abs()
+    inner_tie = (d[:, : k - 1] <= 1e-5 * scale).any(dim=1)
+    return vals, idx, boundary_tie, inner_tie
+
+
+def _eval_dump(trainer, model, loader, tag, out, keep_scores=False):
+    """Reproduce reference Trainer.evaluate (trainer.py:509-528) while keeping scores/topk."""
+    model.eval()
+    k = max(trainer.config["topk"])
+    all_scores, all_idx, all_vals, bt, it, users = [], [], [], [], [], []
+    mats = []
+    with torch.no_grad():
+        for batch in loader:
+            scores = model.full_sort_predict(batch)
+            raw = scores.clone()
+            m = batch[1]
+            scores[m[0], m[1]] = -1e10
+            vals, idx, b_tie, i_tie = _topk_with_ties(scores, k)
+            mats.append(idx)
+            all_scores.append(raw)
+            all_idx.append(idx)
+            all_vals.append(vals)
+            bt.append(b_tie)
+            it.append(i_tie)
+            users.append(batch[0].clone())
+    metrics = trainer.evaluator.evaluate(mats, loader)
+    if keep_scores:
+        out[f"{tag}_scores"] = torch.cat(all_scores).numpy().astype(np.float32)
+    # item ids < 32768 in every fixture: int16 keeps the files small (tests widen to int64)
+    out[f"{tag}_topk_idx"] = torch.cat(all_idx).numpy().astype(np.int16)
+    if keep_scores:
+        out[f"{tag}_topk_val"] = torch.cat(all_vals).numpy().astype(np.float32)
+    out[f"{tag}_boundary_tie"] = torch.cat(bt).numpy()
+    out[f"{tag}_inner_tie"] = torch.cat(it).numpy()
+    out[f"{tag}_users"] = torch.cat(users).numpy()
+    keys = sorted(metrics)
+    out[f"{tag}_metric_keys"] = np.array(keys)
+    out[f"{tag}_metric_vals"] = np.array([metrics[x] for x in keys], dtype=np.float64)
+    return metrics
+
+
+def _param_dict(model):
+    return {n: p.detach().clone() for n, p in model.named_parameters()}
+
+
+def capture_model(model_name: str, dataset: str, overrides: dict, out_path: str, epochs: int,
+                  extra=None):
+    from utils.utils import init_seed, get_model
+    from common.trainer import Trainer
+
+    config, train, valid, test = _load(model_name, dataset, overrides)
+    hp = _select_hparams(config)
+    init_seed(config["seed"])
+    train.pretrain_setup()
+    out = {}
+    model = get_model(model_name)(config, train)
+    trainer = Trainer(config, model)
+    rec = _Recorder(train)
+
+    out["n_users"] = np.int64(model.n_users)
+    out["n_items"] = np.int64(model.n_items)
+    inter = train.inter_matrix(form="coo")
+    out["train_u"] = inter.row.astype(np.int64)
+    out["train_i"] = inter.col.astype(np.int64)
+    for n, p in _param_dict(model).items():
+        out["init." + n] = p.numpy()
+    if extra is not None:
+        extra(model, out, "pre")
+
+    losses, step_params = [], []
+    for epoch in range(epochs):
+        model.cur_epoch = epoch
+        model.pre_epoch_processing()
+        if extra is not None:
+            extra(model, out, f"epoch{epoch}")
+        n_before = len(rec.batches)
+        if epoch == 0:
+            # first batch in isolation: loss, grads, post-Adam params
+            it = iter(train)
+            batch = next(it)
+            trainer.optimizer.zero_grad()
+            model.train()
+            loss = model.calculate_loss(batch)
+            loss.backward()
+            out["step0_loss"] = np.float64(loss.item())
+            for n, p in model.named_parameters():
+                if p.grad is not None:
+                    out["step0_grad." + n] = p.grad.numpy().copy()
+            trainer.optimizer.step()
+            for n, p in _param_dict(model).items():
+                out["step0_param." + n] = p.numpy()
+            # restore the loader/model to the pre-step state and redo the epoch through the trainer
+            raise_restart = True
+        else:
+            raise_restart = False
+        if raise_restart:
+            return ("restart", out, config, hp)
+        loss_sum, _ = trainer._train_epoch(train, epoch)
+        trainer.lr_scheduler.step()
+        losses.append(loss_sum)
+    return ("done", out, config, hp)
+
+
+def capture_model_full(model_name, dataset, overrides, out_path, epochs, extra=None):
+    """Two passes with identical seeds: pass 1 captures first-step internals, pass 2 runs
+    `epochs` reference epochs through `Trainer._train_epoch` and evaluates after each."""
+    from utils.utils import init_seed, get_model
+    from common.trainer import Trainer
+
+    _, out, _, hp = capture_model(model_name, dataset, overrides, out_path, epochs, extra)
+
+    config, train, valid, test = _load(model_name, dataset, overrides)
+    _select_hparams(config)
+    init_seed(config["seed"])
+    train.pretrain_setup()
+    model = get_model(model_name)(config, train)
+    trainer = Trainer(config, model)
+    rec = _Recorder(train)
+    # identical init on both passes (seeded)
+    for n, p in _param_dict(model).items():
+        assert np.array_equal(p.numpy(), out["init." + n]), n
+    _eval_dump(trainer, model, valid, "init_valid", out, keep_scores=True)
+    ep_losses = []
+    for epoch in range(epochs):
+        model.cur_epoch = epoch
+        model.pre_epoch_processing()
+        if extra is not None:
+            extra(model, out, f"e{epoch}")
+        n0 = len(rec.batches)
+        loss_sum, _ = trainer._train_epoch(train, epoch)
+        trainer.lr_scheduler.step()
+        ep_losses.append(float(loss_sum))
+        trip = torch.cat(rec.batches[n0:], dim=1).numpy().astype(np.int32)
+        out[f"epoch{epoch}_triplets"] = trip
+        out[f"epoch{epoch}_nbatch"] = np.int64(len(rec.batches) - n0)
+        if epoch == epochs - 1:
+            for n, p in _param_dict(model).items():
+                out[f"epoch{epoch}_param." + n] = p.numpy()
+        if epoch == epochs - 1:
+            _eval_dump(trainer, model, valid, f"epoch{epoch}_valid", out)
+            _eval_dump(trainer, model, test, f"epoch{epoch}_test", out)
+    out["epoch_losses"] = np.array(ep_losses)
+    # eval split description (user ids + eval items), so tests need no pandas replay
+    for tag, ld in (("valid", valid), ("test", test)):
+        out[f"{tag}_eval_u"] = ld.get_eval_users().numpy().astype(np.int64)
+        lens = np.asarray(ld.get_eval_len_list(), dtype=np.int64)
+        out[f"{tag}_eval_len"] = lens
+        out[f"{tag}_eval_items"] = np.concatenate([np.asarray(x, dtype=np.int64) for x in ld.get_eval_items()])
+    out["hparams"] = np.array([f"{k}={v}" for k, v in hp.items()])
+    out["meta"] = np.array([f"torch={torch.__version__}", f"numpy={np.__version__}",
+                            f"python={platform.python_version()}", "ref=/root/reference@2025-10-03"])
+    np.savez_compressed(out_path, **out)
+    print(f"wrote {out_path}: {os.path.getsize(out_path) / 1e6:.2f} MB, keys={len(out)}")
+    return out
+
+
+def _adj_extra_lgcn(model, out, tag):
+    if tag == "pre":
+        A = model.norm_adj_matrix
+        out["adj_idx"] = A._indices().numpy().astype(np.int32)
+        out["adj_val"] = A._values().numpy().astype(np.float32)
+        with torch.no_grad():
+            u, i = model.forward()
+        out["fwd_user"] = u.numpy()
+        out["fwd_item"] = i.numpy()
+
+
+def _adj_extra_layergcn(model, out, tag):
+    if tag == "pre":
+        A = model.norm_adj_matrix
+        out["adj_idx"] = A._indices().numpy().astype(np.int32)
+        out["adj_val"] = A._values().numpy().astype(np.float32)
+        out["edge_idx"] = model.edge_indices.numpy().astype(np.int64)
+        out["edge_val"] = model.edge_values.numpy().astype(np.float32)
+        with torch.no_grad():
+            model.forward_adj = model.norm_adj_matrix
+            u, i = model.forward()
+        out["fwd_user"] = u.numpy()
+        out["fwd_item"] = i.numpy()
+    elif tag.startswith("e") or tag.startswith("epoch"):
+        A = model.masked_adj
+        out[f"{tag}_masked_idx"] = A._indices().numpy().astype(np.int32)
+        out[f"{tag}_masked_val"] = A._values().numpy().astype(np.float32)
+
+
+def _smore_extra(model, out, tag):
+    if tag != "pre":
+        return
+    for name in ("norm_adj", "R", "image_original_adj", "text_original_adj", "fusion_adj"):
+        A = getattr(model, name).coalesce()
+        out[f"{name}_idx"] = A.indices().numpy().astype(np.int32)
+        out[f"{name}_val"] = A.values().numpy().astype(np.float32)
+    with torch.no_grad():
+        model.eval()
+        img = model.image_trs(model.image_embedding.weight)
+        txt = model.text_trs(model.text_embedding.weight)
+        cv, ct, cf = model.spectrum_convolution(img, txt)
+        out["spec_img"] = img.numpy()
+        out["spec_txt"] = txt.numpy()
+        out["spec_conv_v"] = cv.numpy()
+        out["spec_conv_t"] = ct.numpy()
+        out["spec_conv_f"] = cf.numpy()
+        u, i = model.forward(model.norm_adj)
+        out["fwd_user"] = u.numpy()
+        out["fwd_item"] = i.numpy()
+        ua, ia, side, content = model.forward(model.norm_adj, train=True)
+        out["fwd_side"] = side.numpy()
+        out["fwd_content"] = content.numpy()
+    model.train()
+    out["v_feat"] = model.v_feat.numpy().copy()
+    out["t_feat"] = model.t_feat.numpy().copy()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=os.path.join(REPO, "tests", "golden"))
+    args = ap.parse_args()
+    os.makedirs(args.out, exist_ok=True)
+    _install_shims()
+    shutil.rmtree(DATA_ROOT, ignore_errors=True)
+
+    # small Amazon-shaped graph with hubs: 400 users, 200 items, ~4k interactions
+    df = synth.amazon_like(400, 200, 4000, seed=7)
+    synth.write_inter(df, DATA_ROOT, "baby")
+    df.to_csv(os.path.join(args.out, "gold_small.inter"), sep="\t", index=False)
+    n_items = int(df.itemID.max()) + 1
+
+    common = dict(train_batch_size=512, eval_batch_size=256, is_multimodal_model=False)
+
+    capture_model_full("LightGCN", "baby", dict(common, n_layers=[3], reg_weight=[1e-2]),
+                       os.path.join(args.out, "lightgcn_small.npz"), epochs=3, extra=_adj_extra_lgcn)
+    capture_model_full("LayerGCN", "baby", dict(common, n_layers=[2], reg_weight=[1e-2], dropout=[0.0]),
+                       os.path.join(args.out, "layergcn_small.npz"), epochs=2, extra=_adj_extra_layergcn)
+    capture_model_full("LayerGCN", "baby", dict(common, n_layers=[2], reg_weight=[1e-2], dropout=[0.1]),
+                       os.path.join(args.out, "layergcn_drop_small.npz"), epochs=2, extra=_adj_extra_layergcn)
+
+    # SMORE: synthetic features in the dataset dir (baby.yaml names *_raw.npy)
+    v = synth.features(n_items, 48, seed=11)
+    t = synth.features(n_items, 24, seed=12)
+    np.save(os.path.join(DATA_ROOT, "baby", "image_feat_raw.npy"), v)
+    np.save(os.path.join(DATA_ROOT, "baby", "text_feat_raw.npy"), t)
+    orig_cuda = torch.Tensor.cuda
+    torch.Tensor.cuda = lambda self, *a, **k: self
+    try:
+        capture_model_full("SMORE", "baby",
+                           dict(common, is_multimodal_model=True, dropout_rate=[0.0], mg_verbose=False,
+                                image_knn_k=[10], text_knn_k=[8]),
+                           os.path.join(args.out, "smore_small.npz"), epochs=1, extra=_smore_extra)
+    finally:
+        torch.Tensor.cuda = orig_cuda
+
+
+if __name__ == "__main__":
+    main()
