@@ -231,6 +231,15 @@ int rsx_sample_triplets(const int32_t* inter_u, const int32_t* inter_i, int64_t 
                         int64_t epoch, int64_t start, int64_t batch, int64_t* out,
                         rsx_stream_t stream);
 
+/* The whole epoch at once (one launch per epoch): all n_inter triplets of
+ * `epoch`, batch-major — batch j (size Bj = min(batch, n_inter - j*batch)) is
+ * [3][Bj] contiguous at out + 3*batch*j, identical to what rsx_sample_triplets
+ * returns for start = j*batch.  out holds 3*n_inter int64. */
+int rsx_sample_epoch(const int32_t* inter_u, const int32_t* inter_i, int64_t n_inter,
+                     const int64_t* hist_rowptr, const int32_t* hist_col, const int32_t* all_items,
+                     int64_t n_all_items, uint64_t seed, int64_t epoch, int64_t batch, int64_t* out,
+                     rsx_stream_t stream);
+
 /* Gather rows: out[b] = src[idx[b] + offset]  (u_embeddings = user_all[user] etc.). */
 int rsx_gather_rows(const float* src, const int64_t* idx, int64_t n, int64_t offset, int32_t d,
                     float* out, rsx_stream_t stream);

@@ -286,3 +286,42 @@ class LightGCNCPU:
         loss.backward()
         self.opt.step()
         return v
+
+
+# ---------------------------------------------------------------------------
+# training-batch feeder (cpu_baseline leg: the reference's Python sampler)
+# ---------------------------------------------------------------------------
+class ReferenceSampler:
+    """TrainDataLoader._get_neg_sample / _sample_neg_ids / _random restated
+    (src/utils/dataloader.py:226-275,307-309): sequential slices of the shuffled
+    training interactions, one negative per row drawn with random.sample from the
+    training-item list and redrawn while it is in the user's history."""
+
+    def __init__(self, train_u, train_i, seed=999):
+        import random
+
+        self.rand = random.Random(seed)
+        self.u = np.asarray(train_u)
+        self.i = np.asarray(train_i)
+        self.hist = {}
+        for a, b in zip(self.u.tolist(), self.i.tolist()):
+            self.hist.setdefault(a, set()).add(b)
+        self.all_items = sorted(set(self.i.tolist()))
+        self.rng = np.random.default_rng(seed)
+        self.order = self.rng.permutation(self.u.size)
+        self.pr = 0
+
+    def next(self, batch):
+        if self.pr >= self.u.size:
+            self.order = self.rng.permutation(self.u.size)
+            self.pr = 0
+        sel = self.order[self.pr:self.pr + batch]
+        self.pr += batch
+        us = self.u[sel]
+        neg = []
+        for a in us.tolist():
+            x = self.rand.sample(self.all_items, 1)[0]
+            while x in self.hist[a]:
+                x = self.rand.sample(self.all_items, 1)[0]
+            neg.append(x)
+        return torch.from_numpy(np.vstack([us, self.i[sel], np.asarray(neg)]).astype(np.int64))

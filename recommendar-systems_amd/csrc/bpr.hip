@@ -139,13 +139,34 @@ __global__ __launch_bounds__(kBprBlock) void bpr_bwd(BprArgs a, int n_part) {
     constexpr int G = D / 4;
     constexpr int GPB = kBprBlock / G;
     constexpr int NC = D / G;
+    // every block reduces the per-block partials in the same fixed order
+    // (thread t sums partials t, t+256, ...; then a fixed-shape tree)
+    __shared__ double red[4][kBprBlock];
     __shared__ double tot[4];
-    if (threadIdx.x < 4) {
-        double s = 0.0;
-        for (int k = 0; k < n_part; ++k) s += a.part[(int64_t)k * 4 + threadIdx.x];
-        tot[threadIdx.x] = s;
+    {
+        double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+        for (int k = threadIdx.x; k < n_part; k += kBprBlock) {
+            const double4 v = reinterpret_cast<const double4*>(a.part)[k];
+            s0 += v.x;
+            s1 += v.y;
+            s2 += v.z;
+            s3 += v.w;
+        }
+        red[0][threadIdx.x] = s0;
+        red[1][threadIdx.x] = s1;
+        red[2][threadIdx.x] = s2;
+        red[3][threadIdx.x] = s3;
+        __syncthreads();
+        for (int w = kBprBlock / 2; w > 0; w >>= 1) {
+            if (threadIdx.x < w) {
+#pragma unroll
+                for (int c = 0; c < 4; ++c) red[c][threadIdx.x] += red[c][threadIdx.x + w];
+            }
+            __syncthreads();
+        }
+        if (threadIdx.x < 4) tot[threadIdx.x] = red[threadIdx.x][0];
+        __syncthreads();
     }
-    __syncthreads();
     const double B = (double)a.batch;
     double loss;
     float ku, kp, kn;  // regulariser gradient scale per row kind

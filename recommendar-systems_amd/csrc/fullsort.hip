@@ -105,20 +105,88 @@ struct FsArgs {
     int64_t* out_idx;
 };
 
-// Sort the candidate buffer of one user slot (whole wave), keep the top k; returns the new threshold.
-__device__ __forceinline__ float compact_slot(u64* buf, int* cnt, int k, int lane) {
-    const int n = *cnt;
+constexpr int kStride = kCap + 1;  // u64 slots per user row in LDS (+1: spreads the 32 users over banks)
+
+__device__ __forceinline__ int popc64(u64 x) { return __popcll(x); }
+__device__ __forceinline__ u64 lanemask_lt(int lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
+
+// Exact k-th largest of the (unique, nonzero) keys e0/e1 held by the wave, by a
+// bitwise binary search with ballots: 32 steps on the score half, and 32 more on
+// the index half only when scores tie at the boundary.  Zero keys are padding.
+__device__ __forceinline__ u64 kth_largest(u64 e0, u64 e1, int k) {
+    const unsigned h0 = (unsigned)(e0 >> 32), h1 = (unsigned)(e1 >> 32);
+    unsigned th = 0;
+#pragma unroll 4
+    for (int bit = 31; bit >= 0; --bit) {
+        const unsigned c = th | (1u << bit);
+        const int n = popc64(__ballot(h0 >= c)) + popc64(__ballot(h1 >= c));
+        if (n >= k) th = c;
+    }
+    // th = largest score-word with at least k keys >= it
+    const int gt = popc64(__ballot(h0 > th)) + popc64(__ballot(h1 > th));
+    const int need = k - gt;  // how many of the keys with score-word == th are kept
+    const int eq = popc64(__ballot(h0 == th)) + popc64(__ballot(h1 == th));
+    if (eq == need) return ((u64)th << 32);  // every tie kept: threshold = lowest key of the tie group
+    const unsigned l0 = (unsigned)e0, l1 = (unsigned)e1;
+    unsigned tl = 0;
+    for (int bit = 31; bit >= 0; --bit) {
+        const unsigned c = tl | (1u << bit);
+        const int n = popc64(__ballot(h0 == th && l0 >= c)) + popc64(__ballot(h1 == th && l1 >= c));
+        if (n >= need) tl = c;
+    }
+    return ((u64)th << 32) | tl;
+}
+
+// Keep the k largest keys of one user's buffer (n > k entries), compacted to the
+// front; returns the new score threshold.  Whole wave, no sort.
+__device__ __forceinline__ float compact_slot(u64* buf, int n, int k, int lane) {
+    const u64 e0 = lane < n ? buf[lane] : 0ull;
+    const u64 e1 = lane + 64 < n ? buf[lane + 64] : 0ull;
+    const u64 T = kth_largest(e0, e1, k);
+    const bool k0 = e0 != 0ull && e0 >= T;
+    const bool k1 = e1 != 0ull && e1 >= T;
+    const u64 b0 = __ballot(k0), b1 = __ballot(k1);
+    const u64 lt = lanemask_lt(lane);
+    const int p0 = popc64(b0 & lt);
+    const int p1 = popc64(b0) + popc64(b1 & lt);
+    __builtin_amdgcn_wave_barrier();
+    if (k0) buf[p0] = e0;
+    if (k1) buf[p1] = e1;
+    __builtin_amdgcn_wave_barrier();
+    return key_score(T);
+}
+
+// Write the top-min(n,k) keys of one user's buffer to dst[0..k) in descending
+// order (rank by counting: every lane compares its key with all others via
+// readlane; no LDS round trips), zero-padded.  n <= kCap.
+__device__ __forceinline__ void emit_sorted(const u64* buf, int n, int k, int lane, u64* dst) {
     u64 e0 = lane < n ? buf[lane] : 0ull;
     u64 e1 = lane + 64 < n ? buf[lane + 64] : 0ull;
-    bitonic128_desc(e0, e1, lane);
-    const int keep = n < k ? n : k;
-    if (lane < keep) buf[lane] = e0;
-    if (lane + 64 < keep) buf[lane + 64] = e1;
-    const u64 kth = (k - 1) < 64 ? shfl_u64(e0, k - 1) : shfl_u64(e1, (k - 1) - 64);
-    __builtin_amdgcn_wave_barrier();
-    if (lane == 0) *cnt = keep;
-    __builtin_amdgcn_wave_barrier();
-    return keep >= k ? key_score(kth) : -INFINITY;
+    if (n > k) {
+        const u64 T = kth_largest(e0, e1, k);
+        if (e0 < T) e0 = 0ull;
+        if (e1 < T) e1 = 0ull;
+    }
+    int r0 = 0, r1 = 0;
+    const int m = n < 64 ? n : 64;
+    for (int t = 0; t < m; ++t) {
+        const unsigned lo = __builtin_amdgcn_readlane((unsigned)(e0 & 0xffffffffu), t);
+        const unsigned hi = __builtin_amdgcn_readlane((unsigned)(e0 >> 32), t);
+        const u64 x = ((u64)hi << 32) | lo;
+        r0 += x > e0;
+        r1 += x > e1;
+    }
+    for (int t = 0; t < n - 64; ++t) {
+        const unsigned lo = __builtin_amdgcn_readlane((unsigned)(e1 & 0xffffffffu), t);
+        const unsigned hi = __builtin_amdgcn_readlane((unsigned)(e1 >> 32), t);
+        const u64 x = ((u64)hi << 32) | lo;
+        r0 += x > e0;
+        r1 += x > e1;
+    }
+    if (e0 != 0ull && r0 < k) dst[r0] = e0;
+    if (e1 != 0ull && r1 < k) dst[r1] = e1;
+    const int kept = n < k ? n : k;
+    for (int e = kept + lane; e < k; e += 64) dst[e] = 0ull;
 }
 
 template <int D, int NW>
@@ -129,8 +197,7 @@ __global__ __launch_bounds__(64 * NW) void fs_tiles(FsArgs a) {
     static_assert(PER >= 1, "tile too small for block");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     float* tiles = reinterpret_cast<float*>(smem);                           // [2][32][LD]
-    u64* cbuf = reinterpret_cast<u64*>(smem + 2 * 32 * LD * sizeof(float));  // [NW*32][kCap]
-    int* ccnt = reinterpret_cast<int*>(cbuf + NW * 32 * kCap);               // [NW*32]
+    u64* cbuf = reinterpret_cast<u64*>(smem + 2 * 32 * LD * sizeof(float));  // [NW*32][kStride]
 
     const int tid = threadIdx.x;
     const int wv = tid >> 6, lane = tid & 63, j = lane & 31, h = lane >> 5;
@@ -142,6 +209,7 @@ __global__ __launch_bounds__(64 * NW) void fs_tiles(FsArgs a) {
     const int64_t i0 = (int64_t)chunk * a.chunk_items;
     const int64_t i1 = min(a.ni, i0 + a.chunk_items);
     const int ntiles = (int)((i1 - i0 + 31) / 32);
+    u64* mybuf = cbuf + slot * kStride;
 
     // user fragment: B[k][j] for k in this lane-half's contiguous half of the row
     float bu[HALF];
@@ -169,10 +237,9 @@ __global__ __launch_bounds__(64 * NW) void fs_tiles(FsArgs a) {
         mp = lo;
         next_mask = mp < me ? (int64_t)a.mcol[mp] : LLONG_MAX;
     }
-    if (h == 0) ccnt[slot] = 0;
+    int cnt = 0;  // candidates of user j (same value in lanes j and j+32)
     float tau = -INFINITY;
 
-    // stage tile 0
     float4 pre[PER];
     auto load_tile = [&](int t) {
         const int64_t base = i0 + (int64_t)t * 32;
@@ -224,40 +291,51 @@ __global__ __launch_bounds__(64 * NW) void fs_tiles(FsArgs a) {
             ++mp;
             next_mask = mp < me ? (int64_t)a.mcol[mp] : LLONG_MAX;
         }
-        if (uvalid) {
+        // which of my 16 scores pass the threshold
+        unsigned m = 0;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int ii = (r & 3) + 8 * (r >> 2) + 4 * h;
+            const float sc = ((mbits >> ii) & 1u) ? -1e10f : acc[r];
+            if (uvalid && tb + ii < i1 && sc > tau) m |= 1u << r;
+        }
+        if (__ballot(m != 0u)) {
+            const unsigned pm = (unsigned)__shfl_xor((int)m, 32, kWave);  // partner half's mask
+            int pos = cnt + (h ? __popc(pm) : 0);
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int ii = (r & 3) + 8 * (r >> 2) + 4 * h;
-                const int64_t item = tb + ii;
-                float sc = acc[r];
-                if ((mbits >> ii) & 1u) sc = -1e10f;
-                if (item < i1 && sc > tau) {
-                    const int pos = atomicAdd(&ccnt[slot], 1);
-                    cbuf[slot * kCap + pos] = make_key(sc, (int)item);
+                if ((m >> r) & 1u) {
+                    const int ii = (r & 3) + 8 * (r >> 2) + 4 * h;
+                    const float sc = ((mbits >> ii) & 1u) ? -1e10f : acc[r];
+                    mybuf[pos++] = make_key(sc, (int)(tb + ii));
+                }
+            }
+            cnt += __popc(m) + __popc(pm);
+        }
+        // keep room for the next tile (at most 32 new candidates per user)
+        u64 need = __ballot(h == 0 && cnt > kCap - 32);
+        if (need) {
+            __builtin_amdgcn_wave_barrier();
+            while (need) {
+                const int jj = __ffsll((long long)need) - 1;
+                need &= need - 1;
+                const int n = __builtin_amdgcn_readlane(cnt, jj);
+                const float nt = compact_slot(cbuf + (wv * 32 + jj) * kStride, n, a.k, lane);
+                if (j == jj) {
+                    tau = nt;
+                    cnt = a.k;
                 }
             }
         }
         __syncthreads();
-        // compact buffers that could overflow on the next tile
-        const bool need = (h == 0) && (ccnt[slot] > kCap - 32);
-        u64 bal = __ballot(need);
-        while (bal) {
-            const int jj = __ffsll((long long)bal) - 1;
-            bal &= bal - 1;
-            const int s2 = wv * 32 + jj;
-            const float nt = compact_slot(cbuf + s2 * kCap, ccnt + s2, a.k, lane);
-            if (j == jj) tau = nt;
-        }
     }
-    // final: sort every user's buffer and write its top-k keys for this chunk
+    // final: this chunk's top-k of every user, sorted, to the workspace
+    __builtin_amdgcn_wave_barrier();
     for (int jj = 0; jj < 32; ++jj) {
-        const int s2 = wv * 32 + jj;
-        const int64_t b2 = (int64_t)blockIdx.x * (32 * NW) + s2;
+        const int64_t b2 = (int64_t)blockIdx.x * (32 * NW) + wv * 32 + jj;
         if (b2 >= a.nb) break;  // wave-uniform
-        compact_slot(cbuf + s2 * kCap, ccnt + s2, a.k, lane);
-        const int n = ccnt[s2];
-        u64* dst = a.cand + ((b2 * a.n_chunks) + chunk) * a.k;
-        for (int e = lane; e < a.k; e += 64) dst[e] = e < n ? cbuf[s2 * kCap + e] : 0ull;
+        const int n = __builtin_amdgcn_readlane(cnt, jj);
+        emit_sorted(cbuf + (wv * 32 + jj) * kStride, n, a.k, lane, a.cand + ((b2 * a.n_chunks) + chunk) * a.k);
     }
 }
 
@@ -291,7 +369,7 @@ __global__ __launch_bounds__(256) void fs_merge(FsArgs a) {
 static void fs_plan(int64_t nb, int64_t ni, int d, int* nw, int* n_chunks, int64_t* chunk_items) {
     *nw = d <= 64 ? 4 : 2;
     const int64_t ublocks = (nb + 32 * (*nw) - 1) / (32 * (*nw));
-    int64_t s = (512 + ublocks - 1) / ublocks;
+    int64_t s = (256 + ublocks - 1) / ublocks;  // about one block per CU
     if (s < 1) s = 1;
     if (s > 16) s = 16;
     int64_t per = (ni + s - 1) / s;
@@ -310,7 +388,7 @@ size_t fs_ws(int64_t nb, int64_t ni, int k, int d) {
 
 template <int D, int NW>
 static int launch_fs(FsArgs& a, hipStream_t s) {
-    const size_t lds = 2 * 32 * (D + 4) * sizeof(float) + NW * 32 * kCap * sizeof(u64) + NW * 32 * sizeof(int);
+    const size_t lds = 2 * 32 * (D + 4) * sizeof(float) + NW * 32 * kStride * sizeof(u64);
     const int64_t ublocks = (a.nb + 32 * NW - 1) / (32 * NW);
     static bool attr_set = false;
     if (!attr_set) {

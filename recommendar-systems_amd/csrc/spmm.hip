@@ -187,19 +187,36 @@ __global__ __launch_bounds__(kBlock) void spmm_main(rsx_csr a, const float* __re
     }
 }
 
-// One group per long row: add its slab partials in chunk order, then the epilogue.
+// One block per long row: the block's groups each sum a strided subset of the
+// row's slab partials (4 independent accumulators, so 4+ loads stay in flight),
+// then group 0 adds the group sums in a fixed order and applies the epilogue.
 template <int D, int KIND>
 __global__ __launch_bounds__(kBlock) void spmm_fixup(rsx_csr a, rsx_epilogue e,
                                                      const float* __restrict__ slab) {
     constexpr int G = D / 4;
     constexpr int GPB = kBlock / G;
+    __shared__ float4 part[GPB][G];
     const int li = threadIdx.x % G;
-    const int64_t w = (int64_t)blockIdx.x * GPB + threadIdx.x / G;
-    if (w >= a.n_long) return;
-    const int4 lr = reinterpret_cast<const int4*>(a.long_rows)[w];
-    float4 acc = f4(0.f);
-    for (int s = 0; s < lr.z; ++s) acc = add4(acc, ld4(slab + (int64_t)(lr.y + s) * D + li * 4));
-    epilogue<KIND, D>(e, lr.x, acc, li);
+    const int gi = threadIdx.x / G;
+    const int4 lr = reinterpret_cast<const int4*>(a.long_rows)[blockIdx.x];
+    const float* base = slab + (int64_t)lr.y * D + li * 4;
+    float4 a0 = f4(0.f), a1 = f4(0.f), a2 = f4(0.f), a3 = f4(0.f);
+    int s = gi;
+    for (; s + 3 * GPB < lr.z; s += 4 * GPB) {
+        a0 = add4(a0, ld4(base + (int64_t)s * D));
+        a1 = add4(a1, ld4(base + (int64_t)(s + GPB) * D));
+        a2 = add4(a2, ld4(base + (int64_t)(s + 2 * GPB) * D));
+        a3 = add4(a3, ld4(base + (int64_t)(s + 3 * GPB) * D));
+    }
+    for (; s < lr.z; s += GPB) a0 = add4(a0, ld4(base + (int64_t)s * D));
+    part[gi][li] = add4(add4(a0, a1), add4(a2, a3));
+    __syncthreads();
+    if (gi == 0) {
+        float4 acc = part[0][li];
+#pragma unroll 4
+        for (int g = 1; g < GPB; ++g) acc = add4(acc, part[g][li]);
+        epilogue<KIND, D>(e, lr.x, acc, li);
+    }
 }
 
 // acc = 0 for every row (stand-alone Adam, K = 0 forward, first LayerGCN backward step).
@@ -222,8 +239,7 @@ static int launch_spmm(const rsx_csr& a, const float* x, const rsx_epilogue& e, 
         hipLaunchKernelGGL((spmm_main<D, KIND>), dim3((unsigned)nb), dim3(kBlock), 0, s, a, x, e, slab);
     }
     if (a.n_long > 0) {
-        const int64_t nb = (a.n_long + GPB - 1) / GPB;
-        hipLaunchKernelGGL((spmm_fixup<D, KIND>), dim3((unsigned)nb), dim3(kBlock), 0, s, a, e,
+        hipLaunchKernelGGL((spmm_fixup<D, KIND>), dim3((unsigned)a.n_long), dim3(kBlock), 0, s, a, e,
                            (const float*)slab);
     }
     return last_rc();

@@ -63,7 +63,11 @@ __device__ __forceinline__ bool in_sorted(const int32_t* a, int64_t lo, int64_t 
     return false;
 }
 
-__global__ __launch_bounds__(256) void sample_kernel(rsx_sampler_args s, int hb, int64_t count, int64_t* out) {
+// Triplet for epoch position pos = start + t.  Output layout: batch-major, batch
+// j = t / bm holding [3][Bj] contiguous at out + 3*bm*j (Bj = min(bm, count - j*bm));
+// with bm >= count this is the plain [3][count] layout.
+__global__ __launch_bounds__(256) void sample_kernel(rsx_sampler_args s, int hb, int64_t count, int64_t bm,
+                                                     int64_t* out) {
     const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (t >= count) return;
     const uint64_t key = mix64(s.seed ^ mix64((uint64_t)s.epoch + 0x1234567ull));
@@ -79,21 +83,25 @@ __global__ __launch_bounds__(256) void sample_kernel(rsx_sampler_args s, int hb,
         n = s.all_items[st % (uint64_t)s.n_all_items];
         if (!in_sorted(s.hist_col, lo, hi, n)) break;
     }
-    out[t] = u;
-    out[count + t] = p;
-    out[2 * count + t] = n;
+    const int64_t jb = t / bm, b = t - jb * bm;
+    const int64_t bj = (count - jb * bm) < bm ? (count - jb * bm) : bm;
+    int64_t* o = out + 3 * bm * jb;
+    o[b] = u;
+    o[bj + b] = p;
+    o[2 * bj + b] = n;
 }
 
-int sample_call(const rsx_sampler_args& s, int64_t batch, int64_t* out, hipStream_t st) {
+int sample_call(const rsx_sampler_args& s, int64_t batch, int64_t* out, hipStream_t st, int64_t bm = 0) {
     if (!s.inter_u || !s.inter_i || !s.hist_rowptr || !s.all_items || s.n_inter <= 0 || s.n_all_items <= 0 ||
         !out || batch <= 0 || s.start < 0 || s.start >= s.n_inter)
         return RSX_ERR_ARG;
     const int64_t count = (s.n_inter - s.start) < batch ? (s.n_inter - s.start) : batch;
+    if (bm <= 0) bm = count;
     int bits = 2;
     while ((1ll << bits) < s.n_inter) ++bits;
     if (bits & 1) ++bits;
     hipLaunchKernelGGL(sample_kernel, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, st, s, bits / 2, count,
-                       out);
+                       bm, out);
     return last_rc();
 }
 
@@ -160,6 +168,24 @@ int rsx_sample_triplets(const int32_t* inter_u, const int32_t* inter_i, int64_t 
     s.epoch = epoch;
     s.start = start;
     return rsx::sample_call(s, batch, out, rsx::as_stream(stream));
+}
+
+int rsx_sample_epoch(const int32_t* inter_u, const int32_t* inter_i, int64_t n_inter, const int64_t* hist_rowptr,
+                     const int32_t* hist_col, const int32_t* all_items, int64_t n_all_items, uint64_t seed,
+                     int64_t epoch, int64_t batch, int64_t* out, rsx_stream_t stream) {
+    rsx_sampler_args s;
+    s.inter_u = inter_u;
+    s.inter_i = inter_i;
+    s.n_inter = n_inter;
+    s.hist_rowptr = hist_rowptr;
+    s.hist_col = hist_col;
+    s.all_items = all_items;
+    s.n_all_items = n_all_items;
+    s.seed = seed;
+    s.epoch = epoch;
+    s.start = 0;
+    if (batch <= 0) return RSX_ERR_ARG;
+    return rsx::sample_call(s, n_inter, out, rsx::as_stream(stream), batch);
 }
 
 int rsx_lightgcn_forward(const rsx_csr* adj, int32_t d, int32_t n_layers, const float* p, float* s, float* h0,

@@ -80,6 +80,7 @@ def _declare(lib):
         "rsx_score_dense": (C.c_int, [P, P, I64, P, I64, I32, P, P]),
         "rsx_sample_triplets": (C.c_int, [P, P, I64, P, P, P, I64, C.c_uint64, I64, I64, I64, P, P]),
         "rsx_gather_rows": (C.c_int, [P, P, I64, I64, I32, P, P]),
+        "rsx_sample_epoch": (C.c_int, [P, P, I64, P, P, P, I64, C.c_uint64, I64, I64, P, P]),
         "rsx_lightgcn_step": (C.c_int, [C.POINTER(LgcnStep), P]),
         "rsx_lightgcn_forward": (C.c_int, [C.POINTER(Csr), I32, I32, P, P, P, P, P, P, P]),
     }
@@ -99,7 +100,7 @@ _OPTIONAL: dict = {}
 
 EXPORTED = ["rsx_version", "rsx_csr_schedule_host", "rsx_spmm", "rsx_rowwise", "rsx_bpr_ws_bytes", "rsx_bpr",
             "rsx_fullsort_ws_bytes", "rsx_fullsort_topk", "rsx_score_dense", "rsx_sample_triplets",
-            "rsx_gather_rows", "rsx_lightgcn_step", "rsx_lightgcn_forward"]
+            "rsx_gather_rows", "rsx_lightgcn_step", "rsx_lightgcn_forward", "rsx_sample_epoch"]
 
 
 def lib_path() -> str:

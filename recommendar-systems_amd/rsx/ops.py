@@ -286,6 +286,21 @@ class DeviceSampler:
                              self.hist_rowptr.data_ptr(), self.hist_col.data_ptr(), self.all_items.data_ptr(),
                              self.all_items.numel(), self.seed, epoch, start)
 
+    def sample_epoch(self, epoch: int, batch: int, out: torch.Tensor | None = None) -> torch.Tensor:
+        """All triplets of one epoch, batch-major (batch j = out[3*batch*j : ...] as [3, Bj])."""
+        if out is None:
+            out = torch.empty(3 * self.n_inter, dtype=torch.int64, device=self.device)
+        L.check(L.lib().rsx_sample_epoch(self.inter_u.data_ptr(), self.inter_i.data_ptr(), self.n_inter,
+                                         self.hist_rowptr.data_ptr(), self.hist_col.data_ptr(),
+                                         self.all_items.data_ptr(), self.all_items.numel(), self.seed, epoch,
+                                         batch, _pi(out), _stream()), "rsx_sample_epoch")
+        return out
+
+    @staticmethod
+    def batch_view(epoch_buf: torch.Tensor, n_inter: int, batch: int, j: int) -> torch.Tensor:
+        b = min(batch, n_inter - j * batch)
+        return epoch_buf[3 * batch * j: 3 * batch * j + 3 * b].view(3, b)
+
     def sample(self, epoch: int, start: int, batch: int, out: torch.Tensor | None = None) -> torch.Tensor:
         count = min(batch, self.n_inter - start)
         if out is None:

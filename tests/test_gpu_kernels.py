@@ -1,0 +1,256 @@
+"""HIP kernels (through the C ABI) against the CPU oracle and the reference's golden fixtures.
+
+Tolerances: SpMM / propagation rtol 1e-5 (f32, different summation order: fma
+chains vs torch's CPU addmm); BPR loss rtol 1e-5, gradients rtol 1e-4; Adam
+parameters atol 1e-6 (one lr=1e-3 step); top-K indices exact except among
+items whose scores tie within 1e-5 (fixture tie flags); integer work bit-exact.
+"""
+import numpy as np
+import pytest
+import torch
+
+import rsx_oracle as O
+from helpers import coo_from, eval_lists, params, topk_equal_modulo_ties, train_mask_pairs
+from rsx import _lib as L
+from rsx import graph, ops
+
+pytestmark = pytest.mark.gpu
+
+
+def _powerlaw_csr(n_rows, n_cols, seed, hub=600, empty_every=7):
+    rng = np.random.default_rng(seed)
+    deg = rng.geometric(0.15, size=n_rows)
+    deg[::empty_every] = 0
+    deg[3] = hub            # rows longer than one chunk -> fixup path
+    deg[n_rows // 2] = 33   # just over one chunk
+    deg = np.minimum(deg, n_cols)
+    rows = np.repeat(np.arange(n_rows), deg)
+    cols = np.concatenate([rng.choice(n_cols, size=k, replace=False) for k in deg]) if deg.sum() else np.zeros(0)
+    vals = rng.standard_normal(rows.size).astype(np.float32)
+    return graph.to_csr(rows.astype(np.int64), cols.astype(np.int64), vals, n_rows, n_cols)
+
+
+@pytest.mark.parametrize("d", [32, 64, 128, 256])
+def test_spmm_powerlaw_vs_torch(cuda, d):
+    rp, col, val = _powerlaw_csr(900, 700, seed=d)
+    A = ops.DeviceCSR(rp, col, val, 700, cuda)
+    assert A.n_long >= 2
+    x = torch.randn(700, d, generator=torch.Generator().manual_seed(d))
+    rows = np.repeat(np.arange(900), np.diff(rp))
+    At = torch.sparse_coo_tensor(torch.from_numpy(np.vstack([rows, col.astype(np.int64)])), torch.from_numpy(val),
+                                 (900, 700))
+    ref = torch.sparse.mm(At, x)
+    # f32 summation-order bound: |y - ref| <= 1e-5 |ref| + 2e-7 * (|A| |x|) * sqrt(deg)
+    mag = torch.sparse.mm(torch.sparse_coo_tensor(At._indices(), At._values().abs(), At.shape), x.abs()).numpy()
+    y = A.spmm(x.to(cuda)).cpu()
+    err = np.abs(y.numpy() - ref.numpy())
+    deg = np.diff(rp)[:, None]
+    assert np.all(err <= 1e-5 * np.abs(ref.numpy()) + 2e-7 * mag * np.sqrt(np.maximum(deg, 1)) + 1e-30)
+    # deterministic: same bits on a second launch
+    y2 = A.spmm(x.to(cuda)).cpu()
+    assert torch.equal(y, y2)
+
+
+def test_spmm_empty_matrix(cuda):
+    rp = np.zeros(17, dtype=np.int64)
+    A = ops.DeviceCSR(rp, np.zeros(0, np.int32), np.zeros(0, np.float32), 5, cuda)
+    y = A.spmm(torch.randn(5, 64, device=cuda))
+    assert torch.count_nonzero(y).item() == 0
+
+
+def _lgcn_csr(z, cuda):
+    nu, ni = int(z["n_users"]), int(z["n_items"])
+    rp, col, val = graph.lightgcn_norm_adj(z["train_u"], z["train_i"], nu, ni)
+    return ops.DeviceCSR(rp, col, val, nu + ni, cuda), nu, ni
+
+
+def test_lightgcn_forward_vs_fixture(cuda, golden):
+    z = golden("lightgcn_small")
+    A, nu, ni = _lgcn_csr(z, cuda)
+    U0, I0 = params(z, "init.", "LightGCN")
+    p = torch.from_numpy(np.concatenate([U0, I0])).to(cuda)
+    s, h0, h1, f = (torch.empty_like(p) for _ in range(4))
+    lib = L.lib()
+    rc = lib.rsx_lightgcn_forward(A.struct, 64, 3, ops._p(p), ops._p(s), ops._p(h0), ops._p(h1), ops._p(f),
+                                  ops._p(A.slab(64)), ops._stream())
+    L.check(rc, "forward")
+    f = f.cpu().numpy()
+    np.testing.assert_allclose(f[:nu], z["fwd_user"], rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(f[nu:], z["fwd_item"], rtol=1e-5, atol=1e-7)
+
+
+@pytest.mark.parametrize("variant", [L.RSX_BPR_LIGHTGCN, L.RSX_BPR_LAYERGCN, L.RSX_BPR_SMORE])
+def test_bpr_vs_autograd(cuda, golden, variant):
+    z = golden("lightgcn_small")
+    nu, ni = int(z["n_users"]), int(z["n_items"])
+    g = torch.Generator().manual_seed(variant)
+    fin = torch.randn(nu + ni, 64, generator=g) * 0.1
+    ego = torch.randn(nu + ni, 64, generator=g) * 0.1
+    trip = torch.from_numpy(z["epoch0_triplets"][:, :512].astype(np.int64))
+    reg = 1e-2
+    fl = fin.clone().requires_grad_(True)
+    el = ego.clone().requires_grad_(True)
+    u, p_, n_ = trip[0], trip[1] + nu, trip[2] + nu
+    ps = (fl[u] * fl[p_]).sum(1)
+    ns = (fl[u] * fl[n_]).sum(1)
+    if variant == L.RSX_BPR_LIGHTGCN:
+        mf = -torch.log(1e-10 + torch.sigmoid(ps - ns)).mean()
+        r = sum(torch.norm(x, p=2) for x in (el[u], el[p_], el[n_])) / trip.shape[1]
+        loss = mf + reg * r
+    elif variant == L.RSX_BPR_LAYERGCN:
+        loss = torch.sum(-torch.nn.functional.logsigmoid(ps - ns)) + reg * sum(
+            torch.sum(x ** 2) * 0.5 for x in (el[u], el[p_], el[n_]))
+    else:
+        reg_ = 0.5 * ((fl[u] ** 2).sum() + (fl[p_] ** 2).sum() + (fl[n_] ** 2).sum()) / 2048.0
+        loss = -torch.mean(torch.nn.functional.logsigmoid(ps - ns)) + reg * reg_
+    loss.backward()
+    lo, gf, ge = ops.bpr(variant, fin.to(cuda), ego.to(cuda), nu, ni, trip.to(cuda), reg, batch_cfg=2048.0)
+    assert abs(lo.item() - loss.item()) <= 1e-5 * abs(loss.item()) + 1e-7
+    np.testing.assert_allclose(gf.cpu().numpy(), fl.grad.numpy(), rtol=1e-4, atol=1e-7)
+    if variant != L.RSX_BPR_SMORE:
+        np.testing.assert_allclose(ge.cpu().numpy(), el.grad.numpy(), rtol=1e-4, atol=1e-7)
+
+
+def test_adam_vs_torch(cuda):
+    g = torch.Generator().manual_seed(3)
+    p = torch.randn(300, 64, generator=g)
+    ref = torch.nn.Parameter(p.clone())
+    opt = torch.optim.Adam([ref], lr=1e-3)
+    dp, dm, dv = p.clone().to(cuda), torch.zeros(300, 64, device=cuda), torch.zeros(300, 64, device=cuda)
+    for step in range(1, 4):
+        grad = torch.randn(300, 64, generator=g)
+        grad[::5] = 0.0
+        ref.grad = grad.clone()
+        opt.step()
+        ops.adam_(dp, grad.to(cuda), dm, dv, step=step, lr=1e-3)
+    np.testing.assert_allclose(dp.cpu().numpy(), ref.detach().numpy(), rtol=0, atol=1e-6)
+
+
+def test_lightgcn_fused_step_vs_fixture(cuda, golden):
+    z = golden("lightgcn_small")
+    A, nu, ni = _lgcn_csr(z, cuda)
+    U0, I0 = params(z, "init.", "LightGCN")
+    n = nu + ni
+    p = torch.from_numpy(np.concatenate([U0, I0])).to(cuda)
+    bufs = {k: torch.zeros(n, 64, device=cuda) for k in ("m", "v", "s", "h0", "h1", "f", "g", "r")}
+    trip = torch.from_numpy(z["epoch0_triplets"][:, :512].astype(np.int64)).to(cuda)
+    loss = torch.zeros(1, device=cuda)
+    lib = L.lib()
+    ws = torch.empty(lib.rsx_bpr_ws_bytes(512), dtype=torch.uint8, device=cuda)
+    st = L.LgcnStep()
+    import ctypes as C
+
+    st.adj = C.pointer(A.struct)
+    st.n_users, st.n_items, st.d, st.n_layers, st.reg = nu, ni, 64, 3, 1e-2
+    st.p, st.m, st.v = p.data_ptr(), bufs["m"].data_ptr(), bufs["v"].data_ptr()
+    st.s, st.h0, st.h1 = bufs["s"].data_ptr(), bufs["h0"].data_ptr(), bufs["h1"].data_ptr()
+    st.final_emb, st.g, st.r = bufs["f"].data_ptr(), bufs["g"].data_ptr(), bufs["r"].data_ptr()
+    slab = A.slab(64)
+    st.slab = slab.data_ptr() if slab is not None else 0
+    st.triplets = trip.data_ptr()
+    st.batch = 512
+    st.adam = ops.adam_struct(1e-3, 1)
+    st.loss_out = loss.data_ptr()
+    st.ws, st.ws_bytes = ws.data_ptr(), ws.numel()
+    L.check(lib.rsx_lightgcn_step(C.byref(st), ops._stream()), "step")
+    assert abs(loss.item() - float(z["step0_loss"])) <= 1e-5 * abs(float(z["step0_loss"]))
+    pu, pi = params(z, "step0_param.", "LightGCN")
+    out = p.cpu().numpy()
+    np.testing.assert_allclose(out[:nu], pu, rtol=0, atol=2e-6)
+    np.testing.assert_allclose(out[nu:], pi, rtol=0, atol=2e-6)
+
+
+@pytest.mark.parametrize("k", [5, 50])
+def test_fullsort_topk_vs_fixture(cuda, golden, k):
+    z = golden("lightgcn_small")
+    nu, ni = int(z["n_users"]), int(z["n_items"])
+    f = np.concatenate([z["fwd_user"], z["fwd_item"]])
+    U = torch.from_numpy(f[:nu]).to(cuda)
+    I = torch.from_numpy(f[nu:]).to(cuda)
+    users = torch.from_numpy(z["init_valid_users"].astype(np.int64)).to(cuda)
+    rp, mc = graph.history_csr(z["train_u"], z["train_i"], nu)
+    val, idx = ops.fullsort_topk(U, users, I, torch.from_numpy(rp).to(cuda), torch.from_numpy(mc).to(cuda), k)
+    scores = z["init_valid_scores"].copy()
+    r, c = train_mask_pairs(z, z["init_valid_users"])
+    scores[r, c] = -1e10
+    cv, ci = O.canonical_topk(scores, k)
+    idx = idx.cpu().numpy()
+    assert topk_equal_modulo_ties(idx, ci, scores) == 0
+    np.testing.assert_allclose(val.cpu().numpy(), cv, rtol=1e-5, atol=1e-6)
+    if k == 50:
+        ref = z["init_valid_topk_idx"].astype(np.int64)
+        ties = z["init_valid_inner_tie"] | z["init_valid_boundary_tie"]
+        assert np.all(np.all(idx == ref, axis=1) | ties)
+
+
+@pytest.mark.parametrize("d", [32, 64, 128, 256])
+def test_fullsort_random_sizes(cuda, d):
+    """Ragged batch / item counts, all-masked-but-few users, exact vs a CPU canonical top-k."""
+    g = torch.Generator().manual_seed(d)
+    nb, ni, nu = 77, 1003, 120
+    U = torch.randn(nu, d, generator=g)
+    I = torch.randn(ni, d, generator=g)
+    users = torch.randperm(nu, generator=g)[:nb]
+    rng = np.random.default_rng(d)
+    tu = np.repeat(np.arange(nu), 9)
+    ti = rng.integers(0, ni, size=tu.size)
+    # one user masks all but 20 items -> masked (-1e10) entries reach its top-50
+    heavy = int(users[0])
+    tu = np.concatenate([tu, np.full(ni - 20, heavy)])
+    ti = np.concatenate([ti, np.arange(20, ni)])
+    rp, mc = graph.history_csr(tu, ti, nu)
+    val, idx = ops.fullsort_topk(U.to(cuda), users.to(cuda), I.to(cuda), torch.from_numpy(rp).to(cuda),
+                                 torch.from_numpy(mc).to(cuda), 50)
+    scores = (U[users].double() @ I.double().T).float().numpy()
+    for b, u in enumerate(users.numpy()):
+        scores[b, mc[rp[u]:rp[u + 1]]] = -1e10
+    cv, ci = O.canonical_topk(scores, 50)
+    assert topk_equal_modulo_ties(idx.cpu().numpy(), ci, scores, rtol=1e-5) == 0
+    np.testing.assert_allclose(val.cpu().numpy(), cv, rtol=1e-4, atol=1e-4)
+
+
+def test_score_dense_and_gather(cuda):
+    g = torch.Generator().manual_seed(1)
+    U = torch.randn(50, 64, generator=g)
+    I = torch.randn(333, 64, generator=g)
+    users = torch.tensor([3, 0, 49, 7])
+    out = ops.score_dense(U.to(cuda), users.to(cuda), I.to(cuda)).cpu()
+    np.testing.assert_allclose(out.numpy(), (U[users] @ I.T).numpy(), rtol=1e-5, atol=1e-5)
+    gr = ops.gather_rows(U.to(cuda), users.to(cuda)).cpu()
+    assert torch.equal(gr, U[users])
+
+
+def test_sampler_properties(cuda, golden):
+    z = golden("lightgcn_small")
+    nu = int(z["n_users"])
+    tu, ti = z["train_u"], z["train_i"]
+    s = ops.DeviceSampler(tu, ti, nu, cuda, seed=5)
+    E = tu.size
+    hist = {(int(a), int(b)) for a, b in zip(tu, ti)}
+    all_items = set(int(x) for x in np.unique(ti))
+    seen = []
+    for start in range(0, E, 512):
+        t = s.sample(epoch=0, start=start, batch=512).cpu().numpy()
+        assert t.shape[0] == 3 and t.shape[1] == min(512, E - start)
+        for u, p, n in t.T:
+            assert (int(u), int(p)) in hist
+            assert (int(u), int(n)) not in hist
+            assert int(n) in all_items
+        seen.append(t[:2])
+    pairs = np.concatenate(seen, axis=1)
+    keys = pairs[0] * 100000 + pairs[1]
+    assert np.array_equal(np.sort(keys), np.sort(tu.astype(np.int64) * 100000 + ti))  # a permutation
+    t0 = s.sample(epoch=0, start=0, batch=512).cpu().numpy()
+    t1 = s.sample(epoch=1, start=0, batch=512).cpu().numpy()
+    assert not np.array_equal(t0, t1)
+    assert np.array_equal(t0, s.sample(epoch=0, start=0, batch=512).cpu().numpy())
+
+
+def test_sample_epoch_matches_per_batch(cuda, golden):
+    z = golden("lightgcn_small")
+    s = ops.DeviceSampler(z["train_u"], z["train_i"], int(z["n_users"]), cuda, seed=9)
+    buf = s.sample_epoch(epoch=3, batch=512)
+    for j, start in enumerate(range(0, s.n_inter, 512)):
+        a = ops.DeviceSampler.batch_view(buf, s.n_inter, 512, j).cpu()
+        b = s.sample(epoch=3, start=start, batch=512).cpu()
+        assert torch.equal(a, b)
