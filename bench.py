@@ -131,7 +131,9 @@ def main():
     else:
         eng = LightGCNEngine(tu, ti, nu, ni, 64, 3, 1e-2, 1e-3, dev, U0, I0, seed=0, batch=args.batch)
     E = eng.n_inter
-    log(f"[bench] rank {rank}/{world}: users {nu} items {ni} train {E} nnz {eng.adj.nnz}")
+    parts = [eng.adj] if hasattr(eng, "adj") else [eng.A_U, eng.A_I]
+    nnz = sum(a.nnz for a in parts)
+    log(f"[bench] rank {rank}/{world}: users {nu} items {ni} train {E} nnz {nnz}")
 
     pos = {"epoch": 0, "start": 0}
     done = {"inter": 0}
@@ -196,7 +198,14 @@ def main():
         evaluate()
     torch.cuda.synchronize()
     eval_s = (time.perf_counter() - te) / reps
-    items_per_s = vusers.size * ni / eval_s
+    n_eval = float(vusers.size)
+    if world > 1:
+        ev = torch.tensor([eval_s], dtype=torch.float64, device=dev)
+        nev = torch.tensor([n_eval], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(ev, op=torch.distributed.ReduceOp.MAX)
+        torch.distributed.all_reduce(nev, op=torch.distributed.ReduceOp.SUM)
+        eval_s, n_eval = float(ev.item()), float(nev.item())
+    items_per_s = n_eval * ni / eval_s
     # fused top-k kernel alone on one 4096-user batch (MFMA roofline)
     f = eng.forward()
     ub = vu_d[:4096]
@@ -205,9 +214,14 @@ def main():
 
     # dominant kernel: one propagation SpMM (STORE epilogue), same stream as the step
     x = eng.p
-    y = torch.empty_like(x)
-    spmm_ms = time_kernel(lambda: eng.adj.spmm(x, out=y), 50)
-    alg = spmm_bytes(eng.adj.n_rows, eng.adj.nnz, 64)
+    ys = [torch.empty(a.n_rows, 64, device=dev) for a in parts]
+
+    def run_parts():
+        for a, y in zip(parts, ys):
+            a.spmm(x, out=y)
+
+    spmm_ms = time_kernel(run_parts, 50)
+    alg = spmm_bytes(nu + ni, nnz, 64)
     achieved = alg / (spmm_ms * 1e-3) / 1e9
     traffic = None
     tfile = os.path.join(HERE, "profiles", "spmm_traffic.json")
@@ -242,7 +256,7 @@ def main():
                        "model": "LightGCN", "n_layers": 3, "embedding_size": 64, "global_batch": args.batch * world,
                        "parallelism": f"rowshard{world}" if world > 1 else "single"},
             "fullsort_items_per_s": items_per_s,
-            "fullsort": {"eval_users": int(vusers.size), "n_items": ni, "k": 50,
+            "fullsort": {"eval_users": int(n_eval), "n_items": ni, "k": 50,
                          "s_per_eval": eval_s,
                          "kernel_ms_4096_users": fs_ms,
                          "kernel_tflops": fs_flops / (fs_ms * 1e-3) / 1e12,

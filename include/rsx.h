@@ -105,6 +105,8 @@ int rsx_csr_schedule_host(const int64_t* rowptr_host, int64_t n_rows, int32_t ch
  *                     pre-scale rows), c = aux_w, e = e0, nz/ne eps-clamped norms:
  *                       y     = c*dE + <dE,z> (e/(nz ne) - c z/nz^2)      (dZ^k)
  *                       s_out = s_in + <dE,z> (z/(nz ne) - c e/ne^2)     (d ego)
+ *   RSX_EPI_ADD     y = (alpha*acc + s_in + r_add) * beta  (s_in / r_add may be NULL;
+ *                     y may alias s_in) — row-block sums of the sharded path
  *   Every kind also zeroes the zero0 / zero1 rows when those are non-NULL.
  *
  * Each output row is written by exactly one wavefront group; s_out may alias
@@ -118,7 +120,8 @@ enum {
     RSX_EPI_ADAM = 3,
     RSX_EPI_LAYERGCN = 4,
     RSX_EPI_AXPBY = 5,
-    RSX_EPI_LAYERGCN_BWD = 6
+    RSX_EPI_LAYERGCN_BWD = 6,
+    RSX_EPI_ADD = 7
 };
 
 typedef struct rsx_adam {

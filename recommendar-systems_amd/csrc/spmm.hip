@@ -71,6 +71,11 @@ __device__ __forceinline__ void epilogue(const rsx_epilogue& e, int64_t row, flo
         float4 s = acc;
         if (e.s_in) s = fma4(e.beta, ld4(e.s_in + off), s);
         st4(e.y + off, s);
+    } else if constexpr (KIND == RSX_EPI_ADD) {
+        float4 s = acc;
+        if (e.s_in) s = add4(s, ld4(e.s_in + off));
+        if (e.r_add) s = add4(s, ld4(e.r_add + off));
+        st4(e.y + off, mul4(e.beta, s));
     } else if constexpr (KIND == RSX_EPI_ADAM) {
         float4 g = e.s_in ? add4(ld4(e.s_in + off), acc) : acc;
         g = mul4(e.beta, g);
@@ -264,6 +269,7 @@ static int spmm_d(const rsx_csr& a, const float* x, const rsx_epilogue& e, float
         case RSX_EPI_LAYERGCN: return launch_spmm<D, RSX_EPI_LAYERGCN>(a, x, e, slab, s);
         case RSX_EPI_AXPBY: return launch_spmm<D, RSX_EPI_AXPBY>(a, x, e, slab, s);
         case RSX_EPI_LAYERGCN_BWD: return launch_spmm<D, RSX_EPI_LAYERGCN_BWD>(a, x, e, slab, s);
+        case RSX_EPI_ADD: return launch_spmm<D, RSX_EPI_ADD>(a, x, e, slab, s);
         default: return RSX_ERR_ARG;
     }
 }
@@ -278,6 +284,7 @@ static int rowwise_d(int64_t n, const rsx_epilogue& e, hipStream_t s) {
         case RSX_EPI_LAYERGCN: return launch_rowwise<D, RSX_EPI_LAYERGCN>(n, e, s);
         case RSX_EPI_AXPBY: return launch_rowwise<D, RSX_EPI_AXPBY>(n, e, s);
         case RSX_EPI_LAYERGCN_BWD: return launch_rowwise<D, RSX_EPI_LAYERGCN_BWD>(n, e, s);
+        case RSX_EPI_ADD: return launch_rowwise<D, RSX_EPI_ADD>(n, e, s);
         default: return RSX_ERR_ARG;
     }
 }

@@ -23,6 +23,7 @@ RSX_EPI_ADAM = 3
 RSX_EPI_LAYERGCN = 4
 RSX_EPI_AXPBY = 5
 RSX_EPI_LAYERGCN_BWD = 6
+RSX_EPI_ADD = 7
 
 RSX_BPR_LIGHTGCN = 0
 RSX_BPR_LAYERGCN = 1

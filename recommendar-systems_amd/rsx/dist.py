@@ -1,0 +1,214 @@
+"""Row-sharded LightGCN over several GPUs (one process per GPU; torch.distributed,
+backend "nccl" = RCCL over xGMI on ROCm).
+
+The reference is single-process, single-device ("Parallelism
+strategies: none"); this is the build's scaling axis for graph size.
+
+Partitioning.  A = [[0, R], [R^T, 0]] is bipartite, so with users split into
+contiguous per-rank blocks U_g and the item rows replicated:
+    users^k = R_g items^{k-1}           (local: items^{k-1} is replicated)
+    items^k = sum_g R_g^T users_g^{k-1} (each rank computes its partial, then
+                                         one all-reduce of the [n_items, d] block)
+Per propagation layer the item-row SpMM runs first and its all-reduce is
+issued asynchronously; the user-row SpMM of the same layer (which only needs
+the previous, already reduced items) runs on the compute stream meanwhile.
+The backward (Horner, as in rsx_lightgcn_step) is the same product with the
+same exchange; the item-side gradient and the last layer's partial are
+reduced together, so a K-layer step issues 2K+1 all-reduces of n_items*d
+floats.  Adam runs on every rank: user rows locally, item rows identically on
+each replica (the reduced inputs are bit-identical on all ranks).
+
+Normalisation uses GLOBAL item degrees (one all-reduce of a degree vector at
+construction), so every value equals the single-GPU graph's bit for bit
+(float64 product, cast to f32, reference src/models/lightgcn.py:93-99).
+
+Objective.  Each rank draws B triplets from its own users' interactions; the
+step minimises the sum of the per-rank reference losses (mean BPR over each
+rank's batch + its EmbLoss term), i.e. data-parallel batches of B per GPU.
+
+The compute primitives come from a backend: `HipBackend` (the product: HIP
+kernels through the C ABI) — tests substitute a CPU restatement to check the
+partitioning and the collectives with the gloo backend on CPU.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import _lib as L
+from . import graph, ops
+
+
+class HipBackend:
+    """Product backend: rsx HIP kernels on the current torch stream."""
+
+    def __init__(self, device):
+        self.device = ops.require_device(device)
+
+    def tensor(self, a):
+        return torch.as_tensor(a).to(self.device)
+
+    def csr(self, rowptr, col, val, n_cols, chunk=32):
+        return ops.DeviceCSR(rowptr, col, val, n_cols, self.device, chunk)
+
+    def spmm(self, A, x, d, kind, alpha=1.0, beta=1.0, adam=None, **t):
+        A.spmm_epi(x, ops.epi(kind, alpha, beta, adam=adam, **t), d)
+
+    def rowwise(self, n, d, kind, alpha=1.0, beta=1.0, adam=None, **t):
+        ops.rowwise(n, d, ops.epi(kind, alpha, beta, adam=adam, **t))
+
+    def adam(self, lr, step, weight_decay=0.0):
+        return ops.adam_struct(lr, step, weight_decay=weight_decay)
+
+    def bpr(self, fin, ego, nu, ni, trip, reg, g, r, loss_acc):
+        loss, _, _ = ops.bpr(L.RSX_BPR_LIGHTGCN, fin, ego, nu, ni, trip, reg, g_final=g, g_ego=r,
+                             loss_acc=loss_acc)
+        return loss
+
+    def sampler(self, train_u, train_i, n_users, seed):
+        return ops.DeviceSampler(train_u, train_i, n_users, self.device, seed=seed)
+
+
+class ShardedLightGCNEngine:
+    """LightGCN with users row-sharded over the process group, items replicated."""
+
+    def __init__(self, train_u: np.ndarray, train_i: np.ndarray, n_users: int, n_items: int, dim: int,
+                 n_layers: int, reg: float, lr: float, device, user_emb: np.ndarray, item_emb: np.ndarray,
+                 seed: int = 0, batch: int = 2048, chunk: int = 32, weight_decay: float = 0.0, group=None,
+                 backend=None):
+        if n_layers < 1:
+            raise RuntimeError("sharded LightGCN needs n_layers >= 1")
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.be = backend or HipBackend(device)
+        self.n_users, self.n_items, self.d, self.K = int(n_users), int(n_items), int(dim), int(n_layers)
+        self.reg, self.lr, self.wd = float(reg), float(lr), float(weight_decay)
+        self.batch = int(batch)
+        nu, ni, d = self.n_users, self.n_items, self.d
+        tu = np.asarray(train_u, dtype=np.int64)
+        ti = np.asarray(train_i, dtype=np.int64)
+        key = np.unique(tu * (1 << 32) + ti)
+        uu, ii = key >> 32, key & 0xFFFFFFFF
+        # global item degrees (sum of every rank's interactions)
+        deg_i = torch.from_numpy(np.bincount(ii, minlength=ni).astype(np.int64))
+        deg_i = self._allreduce_host(deg_i)
+        deg_u = np.bincount(uu, minlength=nu).astype(np.float64)
+        du = np.power(deg_u + 1e-7, -0.5)
+        di = np.power(deg_i.numpy().astype(np.float64) + 1e-7, -0.5)
+        v_u = (du[uu] * di[ii]).astype(np.float32)   # user rows: d_u * d_i
+        v_i = (di[ii] * du[uu]).astype(np.float32)   # item rows: d_i * d_u (same value)
+        n = nu + ni
+        self.A_U = self.be.csr(*graph.to_csr(uu, ii + nu, v_u, nu, n), n, chunk)
+        self.A_I = self.be.csr(*graph.to_csr(ii, uu, v_i, ni, n), n, chunk)
+        self.nnz = int(2 * key.size)
+        # replicated items: every rank starts from rank 0's item table
+        it = torch.from_numpy(np.ascontiguousarray(item_emb, dtype=np.float32))
+        it = self._broadcast_host(it)
+        p = torch.cat([torch.from_numpy(np.ascontiguousarray(user_emb, dtype=np.float32)), it])
+        self.p = self.be.tensor(p)
+        z = lambda rows=n: self.be.tensor(torch.zeros(rows, d, dtype=torch.float32))  # noqa: E731
+        self.m, self.v, self.s, self.h0, self.h1 = z(), z(), z(), z(), z()
+        self.final, self.g, self.r = z(), z(), z()
+        self.t = z(ni)
+        self.loss_acc = self.be.tensor(torch.zeros(1, dtype=torch.float64))
+        self.step_count = 0
+        self.sampler = self.be.sampler(tu, ti, nu, seed)
+        self.n_inter = self.sampler.n_inter
+        self._epoch_buf = None
+        self._epoch_sampled = None
+        self._fwd_valid = False
+
+    # ------------------------------------------------------------------ comms
+    def _allreduce_host(self, t):
+        if dist.get_backend(self.group) == "nccl":
+            x = t.to(torch.device("cuda", torch.cuda.current_device()))
+            dist.all_reduce(x, group=self.group)
+            return x.cpu()
+        dist.all_reduce(t, group=self.group)
+        return t
+
+    def _broadcast_host(self, t):
+        if dist.get_backend(self.group) == "nccl":
+            x = t.to(torch.device("cuda", torch.cuda.current_device()))
+            dist.broadcast(x, src=dist.get_global_rank(self.group, 0) if self.group else 0, group=self.group)
+            return x.cpu()
+        dist.broadcast(t, src=0, group=self.group)
+        return t
+
+    def _ar(self, x):
+        return dist.all_reduce(x, group=self.group, async_op=True)
+
+    # --------------------------------------------------------------- forward
+    def _propagate(self, zero_grads: bool):
+        be, nu, ni, d, K = self.be, self.n_users, self.n_items, self.d, self.K
+        p, s, f = self.p, self.s, self.final
+        bufs = (self.h0, self.h1)
+        beta = 1.0 / (K + 1)
+        x = p
+        for k in range(1, K + 1):
+            y = bufs[(k - 1) & 1]
+            s_in = p if k == 1 else s
+            be.spmm(self.A_I, x, d, L.RSX_EPI_STORE, y=y[nu:])          # partial items^k
+            work = self._ar(y[nu:])
+            zero = dict(zero0=self.g[:nu], zero1=self.r[:nu]) if (k == K and zero_grads) else {}
+            if k < K:
+                be.spmm(self.A_U, x, d, L.RSX_EPI_LAYERSUM, y=y[:nu], s_in=s_in[:nu], s_out=s[:nu])
+            else:
+                be.spmm(self.A_U, x, d, L.RSX_EPI_FINAL, beta=beta, f=f[:nu], s_in=s_in[:nu], **zero)
+            work.wait()
+            if k < K:
+                be.rowwise(ni, d, L.RSX_EPI_ADD, y=s[nu:], s_in=s_in[nu:], r_add=y[nu:])
+            else:
+                zi = dict(zero0=self.g[nu:], zero1=self.r[nu:]) if zero_grads else {}
+                be.rowwise(ni, d, L.RSX_EPI_ADD, beta=beta, y=f[nu:], s_in=s_in[nu:], r_add=y[nu:], **zi)
+            x = y
+
+    def forward(self):
+        if not self._fwd_valid:
+            self._propagate(zero_grads=False)
+            self._fwd_valid = True
+        return self.final
+
+    def invalidate(self):
+        self._fwd_valid = False
+
+    # ------------------------------------------------------------------ step
+    def step(self, triplets=None, epoch: int = 0, start: int = 0):
+        be, nu, ni, d, K = self.be, self.n_users, self.n_items, self.d, self.K
+        self.step_count += 1
+        if triplets is None:
+            if self._epoch_sampled != epoch:
+                self._epoch_buf = self.sampler.sample_epoch(epoch, self.batch, out=self._epoch_buf)
+                self._epoch_sampled = epoch
+            triplets = ops.DeviceSampler.batch_view(self._epoch_buf, self.n_inter, self.batch,
+                                                    start // self.batch)
+        self._propagate(zero_grads=True)
+        self.loss_out = be.bpr(self.final, self.p, nu, ni, triplets, self.reg, self.g, self.r, self.loss_acc)
+        adam = be.adam(self.lr, self.step_count, self.wd)
+        beta = 1.0 / (K + 1)
+        g, s, r, t = self.g, self.s, self.r, self.t
+        bufs = (self.h0, self.h1)
+        dist.all_reduce(g[nu:], group=self.group)  # item rows of dL/dfinal from every rank's batch
+        x = g
+        for k in range(1, K + 1):
+            y = bufs[(k - 1) & 1]
+            s_in = g if k == 1 else s
+            if k < K:
+                be.spmm(self.A_I, x, d, L.RSX_EPI_STORE, y=y[nu:])
+                work = self._ar(y[nu:])
+                be.spmm(self.A_U, x, d, L.RSX_EPI_LAYERSUM, y=y[:nu], s_in=s_in[:nu], s_out=s[:nu])
+                work.wait()
+                be.rowwise(ni, d, L.RSX_EPI_ADD, y=s[nu:], s_in=s_in[nu:], r_add=y[nu:])
+            else:
+                # t = H_I^K/(K+1) + R_I: this rank's share of the item gradient beyond s_I/(K+1)
+                be.spmm(self.A_I, x, d, L.RSX_EPI_ADD, alpha=beta, y=t, r_add=r[nu:])
+                work = self._ar(t)
+                be.spmm(self.A_U, x, d, L.RSX_EPI_ADAM, beta=beta, adam=adam, s_in=s_in[:nu], r_add=r[:nu],
+                        p=self.p[:nu], m=self.m[:nu], v=self.v[:nu])
+                work.wait()
+                be.rowwise(ni, d, L.RSX_EPI_ADAM, beta=beta, adam=adam, s_in=s_in[nu:], r_add=t,
+                           p=self.p[nu:], m=self.m[nu:], v=self.v[nu:])
+            x = y
+        self._fwd_valid = False
