@@ -1,0 +1,111 @@
+"""Top-K ranking metrics with the reference's definitions and rounding.
+
+Same results as TopKEvaluator.evaluate + utils/metrics.py
+(src/utils/topk_evaluator.py:58-102, src/utils/metrics.py:12-118): Recall,
+Recall2, NDCG, Precision, MAP at every k of `topk`, each the mean over eval
+users of the per-user cumulative value at rank k, rounded to 4 decimals.  The
+reference builds the hit matrix with a Python `i in m` loop per (user, rank)
+(its largest evaluation cost); here it is one vectorised membership
+test on (row, item) keys, producing the identical boolean matrix, after which
+the same float64 cumulative arithmetic runs.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+_KNOWN = ("recall", "recall2", "precision", "ndcg", "map")
+
+
+def hit_matrix(topk_idx: np.ndarray, eval_items: list) -> np.ndarray:
+    n, k = topk_idx.shape
+    lens = np.fromiter((len(x) for x in eval_items), dtype=np.int64, count=n)
+    rows = np.repeat(np.arange(n, dtype=np.int64), lens)
+    items = np.concatenate([np.asarray(x, dtype=np.int64) for x in eval_items]) if n else np.zeros(0, np.int64)
+    span = int(max(int(topk_idx.max(initial=0)), int(items.max(initial=0)))) + 1
+    truth = np.unique(rows * span + items)
+    keys = np.arange(n, dtype=np.int64)[:, None] * span + topk_idx.astype(np.int64)
+    return np.isin(keys, truth)
+
+
+def _ranks(k):
+    return np.arange(1, k + 1)
+
+
+def recall(hit, pos_len):
+    return (np.cumsum(hit, axis=1) / pos_len.reshape(-1, 1)).mean(axis=0)
+
+
+def recall2(hit, pos_len):
+    return np.cumsum(hit, axis=1).sum(axis=0) / pos_len.sum()
+
+
+def precision(hit, pos_len):
+    return (hit.cumsum(axis=1) / _ranks(hit.shape[1])).mean(axis=0)
+
+
+def ndcg(hit, pos_len):
+    k = hit.shape[1]
+    rank = np.zeros_like(hit, dtype=np.float64)
+    rank[:, :] = _ranks(k)
+    gain = 1.0 / np.log2(rank + 1)
+    ideal_full = np.cumsum(gain, axis=1)
+    cap = np.minimum(pos_len, k)                       # IDCG over min(|pos|, k) relevant items
+    col = np.minimum(np.arange(k)[None, :], (cap - 1)[:, None])
+    idcg = np.take_along_axis(ideal_full, col, axis=1)
+    dcg = np.cumsum(np.where(hit, gain, 0), axis=1)
+    return (dcg / idcg).mean(axis=0)
+
+
+def average_precision(hit, pos_len):
+    k = hit.shape[1]
+    prec = hit.cumsum(axis=1) / _ranks(k)
+    acc = np.cumsum(prec * hit.astype(np.float64), axis=1)
+    cap = np.minimum(pos_len, k)
+    denom = np.minimum(_ranks(k)[None, :], cap[:, None])
+    out = np.zeros_like(hit, dtype=np.float64)
+    out[:, :] = acc / denom
+    return out.mean(axis=0)
+
+
+FUNCS = {"recall": recall, "recall2": recall2, "precision": precision, "ndcg": ndcg, "map": average_precision}
+
+
+class TopKEvaluator:
+    """Evaluator with the reference's config keys: metrics, topk."""
+
+    def __init__(self, config):
+        self.config = config
+        metrics = config["metrics"]
+        if isinstance(metrics, str):
+            metrics = [metrics]
+        if not isinstance(metrics, (list, tuple)):
+            raise TypeError("metrics must be str or list")
+        for m in metrics:
+            if m.lower() not in _KNOWN:
+                raise ValueError(f"There is no user grouped topk metric named {m}!")
+        self.metrics = [m.lower() for m in metrics]
+        topk = config["topk"]
+        if isinstance(topk, int):
+            topk = [topk]
+        if not isinstance(topk, (list, tuple)):
+            raise TypeError("The topk must be a integer, list")
+        for k in topk:
+            if k <= 0:
+                raise ValueError(f"topk must be a positive integer or a list of positive integers, but get `{k}`")
+        self.topk = list(topk)
+
+    def evaluate_arrays(self, topk_idx: np.ndarray, eval_items: list, pos_len: np.ndarray) -> dict:
+        assert len(pos_len) == len(topk_idx)
+        hit = hit_matrix(topk_idx, eval_items)
+        out = {}
+        for m in self.metrics:
+            v = FUNCS[m](hit, np.asarray(pos_len))
+            for k in self.topk:
+                out[f"{m}@{k}"] = round(v[k - 1], 4)
+        return out
+
+    def evaluate(self, batch_matrix_list, eval_data, is_test=False, idx=0):
+        import torch
+
+        topk = torch.cat(batch_matrix_list, dim=0).cpu().numpy()
+        return self.evaluate_arrays(topk, eval_data.get_eval_items(), eval_data.get_eval_len_list())

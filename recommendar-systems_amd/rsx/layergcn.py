@@ -1,0 +1,187 @@
+"""LayerGCN on the rsx HIP path — drop-in for the reference's models/layergcn.py.
+
+Forward (reference src/models/layergcn.py:127-140): Z^k = A E^{k-1},
+c^k = cos(Z^k, E^0) (F.cosine_similarity, eps 1e-8), E^k = c^k Z^k,
+out = sum_{k=1..K} E^k — one SpMM per layer with the cosine scaling and the
+running sum fused into its epilogue (RSX_EPI_LAYERGCN), which also saves Z^k
+and c^k for the backward.  Training uses the per-epoch edge-dropout graph
+(`pre_epoch_processing`, layergcn.py:51-70: alternating torch.multinomial over
+the degree-normalised edge values and random.sample, float32 renormalisation —
+host-side, with the reference's own RNG calls, so the kept edges are the
+reference's); evaluation uses the full normalised graph.
+
+Backward: dE^K = G; for k = K..1 the LAYERGCN_BWD epilogue turns dE^k into
+dZ^k and accumulates the cosine's dependence on E^0; dE^{k-1} = A dZ^k + G is
+the next SpMM with the same epilogue; the last SpMM's epilogue applies Adam to
+E^0 with g = A dZ^1 + (cosine terms) + reg.  Loss: sum-BPR + reg * L2
+(layergcn.py:142-177), fused kernel RSX_BPR_LAYERGCN.
+"""
+from __future__ import annotations
+
+import random
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import _lib as L
+from . import graph, ops
+from .recommender import GeneralRecommender
+
+
+class LayerGCNEngine:
+    def __init__(self, train_u, train_i, n_users, n_items, dim, n_layers, reg, lr, device, user_emb, item_emb,
+                 chunk=32, weight_decay=0.0, batch=2048):
+        self.device = ops.require_device(device)
+        self.n_users, self.n_items, self.d, self.K = int(n_users), int(n_items), int(dim), int(n_layers)
+        if self.K < 1:
+            raise RuntimeError("LayerGCN needs n_layers >= 1")
+        self.reg, self.lr, self.wd, self.chunk = float(reg), float(lr), float(weight_decay), int(chunk)
+        n = self.n_users + self.n_items
+        rp, col, val = graph.lightgcn_norm_adj(train_u, train_i, self.n_users, self.n_items)
+        self.norm_adj = ops.DeviceCSR(rp, col, val, n, self.device, chunk)
+        self.train_adj = self.norm_adj
+        dev = self.device
+        self.p = torch.from_numpy(np.concatenate([user_emb, item_emb]).astype(np.float32)).to(dev)
+        z = lambda: torch.zeros(n, dim, dtype=torch.float32, device=dev)  # noqa: E731
+        self.m, self.v = z(), z()
+        self.out, self.g, self.r, self.acc = z(), z(), z(), z()
+        self.h = [z(), z()]
+        self.zs = [z() for _ in range(self.K)]
+        self.cs = [torch.zeros(n, dtype=torch.float32, device=dev) for _ in range(self.K)]
+        self.loss_acc = torch.zeros(1, dtype=torch.float64, device=dev)
+        self.step_count = 0
+        self._eval_out = z()
+        self._eval_valid = False
+
+    def set_train_graph(self, rowptr, col, val):
+        n = self.n_users + self.n_items
+        self.train_adj = ops.DeviceCSR(rowptr, col, val, n, self.device, self.chunk)
+
+    def use_eval_graph_for_training(self):
+        self.train_adj = self.norm_adj
+
+    def invalidate(self):
+        self._eval_valid = False
+
+    def _forward(self, A, out, zero_grads=False, save=True):
+        d, K = self.d, self.K
+        x = self.p
+        for k in range(1, K + 1):
+            y = self.h[(k - 1) & 1]
+            kw = dict(e0=self.p, y=y, s_out=out, s_in=(out if k > 1 else None))
+            if save:
+                kw.update(aux=self.zs[k - 1], aux_w=self.cs[k - 1])
+            if k == K and zero_grads:
+                kw.update(zero0=self.g, zero1=self.r)
+            A.spmm_epi(x, ops.epi(L.RSX_EPI_LAYERGCN, **kw), d)
+            x = y
+        return out
+
+    def forward(self):
+        """Evaluation forward on the full normalised graph (layergcn.py:179-188)."""
+        if not self._eval_valid:
+            self._forward(self.norm_adj, self._eval_out, save=False)
+            self._eval_valid = True
+        return self._eval_out
+
+    def step(self, triplets: torch.Tensor):
+        d, K, n = self.d, self.K, self.n_users + self.n_items
+        A = self.train_adj
+        self.step_count += 1
+        self._forward(A, self.out, zero_grads=True, save=True)
+        ops.bpr(L.RSX_BPR_LAYERGCN, self.out, self.p, self.n_users, self.n_items, triplets[:3].contiguous(),
+                self.reg, g_final=self.g, g_ego=self.r, loss_acc=self.loss_acc)
+        # dE^K = G -> dZ^K (rowwise), ego-cosine terms into acc
+        hz = self.h[0]
+        ops.rowwise(n, d, ops.epi(L.RSX_EPI_LAYERGCN_BWD, r_add=self.g, aux=self.zs[K - 1],
+                                  aux_w=self.cs[K - 1], e0=self.p, y=hz, s_out=self.acc))
+        adam = ops.adam_struct(self.lr, self.step_count, weight_decay=self.wd)
+        for k in range(K - 1, 0, -1):
+            y = self.h[(K - k) & 1]
+            A.spmm_epi(hz, ops.epi(L.RSX_EPI_LAYERGCN_BWD, r_add=self.g, aux=self.zs[k - 1], aux_w=self.cs[k - 1],
+                                   e0=self.p, y=y, s_in=self.acc, s_out=self.acc), d)
+            hz = y
+        # dE^0 = A dZ^1 + cosine terms + reg -> Adam
+        A.spmm_epi(hz, ops.epi(L.RSX_EPI_ADAM, s_in=self.acc, r_add=self.r, p=self.p, m=self.m, v=self.v,
+                               adam=adam), d)
+        self._eval_valid = False
+
+
+def reference_edge_dropout(edge_indices: torch.Tensor, edge_values: torch.Tensor, dropout: float,
+                           pruning_random: bool):
+    """Kept edge ids for one epoch with the reference's RNG calls (layergcn.py:55-62)."""
+    keep_len = int(edge_values.size(0) * (1.0 - dropout))
+    if pruning_random:
+        return torch.tensor(random.sample(range(edge_values.size(0)), keep_len))
+    return torch.multinomial(edge_values, keep_len)
+
+
+class LayerGCN(GeneralRecommender):
+    supports_fused_step = True
+
+    def __init__(self, config, dataset):
+        super().__init__(config, dataset)
+        ops.require_device(self.device)
+        self.interaction_matrix = dataset.inter_matrix(form="coo").astype(np.float32)
+        self.latent_dim = config["embedding_size"]
+        self.n_layers = config["n_layers"]
+        self.reg_weight = config["reg_weight"]
+        self.dropout = config["dropout"]
+        self.n_nodes = self.n_users + self.n_items
+        u0 = nn.init.xavier_uniform_(torch.empty(self.n_users, self.latent_dim))
+        i0 = nn.init.xavier_uniform_(torch.empty(self.n_items, self.latent_dim))
+        im = self.interaction_matrix
+        self.engine = LayerGCNEngine(im.row.astype(np.int64), im.col.astype(np.int64), self.n_users, self.n_items,
+                                     self.latent_dim, self.n_layers, self.reg_weight, config["learning_rate"] or 1e-3,
+                                     self.device, u0.numpy(), i0.numpy(), chunk=int(config["rsx_chunk"] or 32),
+                                     weight_decay=float(config["weight_decay"] or 0.0))
+        nu = self.n_users
+        self.user_embeddings = nn.Parameter(self.engine.p[:nu])
+        self.item_embeddings = nn.Parameter(self.engine.p[nu:])
+        # edge info for the per-epoch dropout (layergcn.py:83-89), CPU tensors as in the reference
+        self.edge_indices = torch.from_numpy(np.vstack([im.row, im.col]).astype(np.int64))
+        self.edge_values = torch.from_numpy(graph.layergcn_edge_values(im.row.astype(np.int64),
+                                                                       im.col.astype(np.int64), nu, self.n_items))
+        self.pruning_random = False
+
+    def train(self, mode: bool = True):
+        self.engine.invalidate()
+        return super().train(mode)
+
+    def pre_epoch_processing(self):
+        if self.dropout <= 0.0:
+            self.engine.use_eval_graph_for_training()
+            return
+        keep = reference_edge_dropout(self.edge_indices, self.edge_values, self.dropout, self.pruning_random)
+        self.pruning_random = True ^ self.pruning_random
+        kept = self.edge_indices[:, keep].numpy()
+        self.engine.set_train_graph(*graph.layergcn_masked_adj(kept[0], kept[1], self.n_users, self.n_items))
+
+    def calculate_loss(self, interaction):
+        raise NotImplementedError("LayerGCN on rsx trains through fused_step (rsx.trainer.Trainer)")
+
+    def _final(self):
+        with torch.no_grad():
+            return self.engine.forward()
+
+    def forward(self):
+        f = self._final()
+        return f[: self.n_users], f[self.n_users:]
+
+    def full_sort_predict(self, interaction):
+        f = self._final()
+        return ops.score_dense(f[: self.n_users], interaction[0].contiguous(), f[self.n_users:])
+
+    def fused_step(self, interaction, lr: float):
+        self.engine.lr = float(lr)
+        self.engine.step(interaction)
+
+    def full_sort_topk(self, interaction, k: int, eval_data):
+        f = self._final()
+        return ops.fullsort_topk(f[: self.n_users], interaction[0].contiguous(), f[self.n_users:],
+                                 eval_data.mask_rowptr, eval_data.mask_col, k)
+
+    @property
+    def device_loss_acc(self):
+        return self.engine.loss_acc

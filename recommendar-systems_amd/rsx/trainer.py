@@ -1,0 +1,298 @@
+"""Trainer with the reference's behaviour and log format (src/common/trainer.py:47-548).
+
+fit(): per epoch `pre_epoch_processing`, one pass over the training loader,
+LambdaLR step (lr * gamma^(epoch/T) from `learning_rate_scheduler`), then every
+`eval_step` epochs evaluation on valid and test, early stopping on
+`valid_metric` with patience `stopping_step`; returns (best valid score, best
+valid result, test result at the best valid epoch).
+
+Training pass, two modes:
+* fused (model.supports_fused_step and config rsx_fused_step, no classic mirror
+  gradient): `model.fused_step(batch, lr)` per batch — forward, loss, backward
+  and Adam on the device; the loss is summed on the device and read once per
+  epoch (the reference syncs `loss.item()` every batch, trainer.py:196-200; a
+  NaN loss therefore stops training at the end of the epoch, not mid-epoch);
+* autograd: calculate_loss / backward / torch optimizer exactly as the
+  reference, including classic MG (`mg=True`) and the model-level mirror
+  gradient (model.mg_enable, trainer.py:268-348).
+
+evaluate(): per eval batch `model.full_sort_topk` (fused scores + mask + top-k)
+when the model has it, else full_sort_predict + mask (-1e10) + torch.topk, then
+TopKEvaluator (vectorised hit matrix, same metric values).
+"""
+from __future__ import annotations
+
+import itertools
+from logging import getLogger
+from time import time
+
+import numpy as np
+import torch
+import torch.optim as optim
+from torch.nn.utils.clip_grad import clip_grad_norm_
+
+from .evaluator import TopKEvaluator
+from .utils import dict2str, early_stopping
+
+
+class Trainer:
+    def __init__(self, config, model, mg=False):
+        self.config = config
+        self.model = model
+        self.logger = getLogger()
+        self.learner = config["learner"]
+        self.learning_rate = config["learning_rate"]
+        self.epochs = config["epochs"]
+        self.eval_step = min(config["eval_step"], self.epochs)
+        self.stopping_step = config["stopping_step"]
+        self.clip_grad_norm = config["clip_grad_norm"]
+        self.valid_metric = config["valid_metric"].lower()
+        self.valid_metric_bigger = config["valid_metric_bigger"]
+        self.test_batch_size = config["eval_batch_size"]
+        self.device = config["device"]
+        wd = config["weight_decay"]
+        self.weight_decay = (eval(wd) if isinstance(wd, str) else wd) if wd is not None else 0.0  # noqa: S307
+        self.req_training = config["req_training"]
+        self.start_epoch = 0
+        self.cur_step = 0
+        blank = {f"{m.lower()}@{k}": 0.0 for m, k in itertools.product(config["metrics"], config["topk"])}
+        self.best_valid_score = -1
+        self.best_valid_result = blank
+        self.best_test_upon_valid = blank
+        self.train_loss_dict = {}
+        self.mg = mg
+        self.alpha1, self.alpha2, self.beta = config["alpha1"], config["alpha2"], config["beta"]
+        self.fused = bool(getattr(model, "supports_fused_step", False)) and bool(
+            config.get("rsx_fused_step", True)) and not mg and not getattr(model, "mg_enable", False)
+        sched = config["learning_rate_scheduler"] or [1.0, 50]
+        self._lr_fac = lambda epoch: sched[0] ** (epoch / sched[1])
+        self.optimizer = None if self.fused else self._build_optimizer()
+        self.lr_scheduler = (optim.lr_scheduler.LambdaLR(self.optimizer, lr_lambda=self._lr_fac)
+                             if self.optimizer is not None else None)
+        self._epoch_for_lr = 0
+        self.evaluator = TopKEvaluator(config)
+        self.mg_target_rel_step = float(config.get("mg_target_rel_step", 1e-3))
+        self.mg_alpha_max_scale = float(config.get("mg_alpha_max_scale", 20.0))
+
+    # ------------------------------------------------------------------ setup
+    def _build_optimizer(self):
+        params = self.model.parameters()
+        name = (self.learner or "adam").lower()
+        if name == "adam":
+            return optim.Adam(params, lr=self.learning_rate, weight_decay=self.weight_decay)
+        if name == "sgd":
+            return optim.SGD(params, lr=self.learning_rate, weight_decay=self.weight_decay)
+        if name == "adagrad":
+            return optim.Adagrad(params, lr=self.learning_rate, weight_decay=self.weight_decay)
+        if name == "rmsprop":
+            return optim.RMSprop(params, lr=self.learning_rate, weight_decay=self.weight_decay)
+        self.logger.warning("Received unrecognized optimizer, set default Adam optimizer")
+        return optim.Adam(params, lr=self.learning_rate)
+
+    def current_lr(self):
+        if self.optimizer is not None:
+            return self.optimizer.param_groups[0]["lr"]
+        return self.learning_rate * self._lr_fac(self._epoch_for_lr)
+
+    # ------------------------------------------------------------------ train
+    def _train_epoch(self, train_data, epoch_idx, loss_func=None):
+        if not self.req_training:
+            return 0.0, []
+        self.model.train()
+        if self.fused:
+            return self._train_epoch_fused(train_data, epoch_idx)
+        return self._train_epoch_autograd(train_data, epoch_idx, loss_func)
+
+    def _train_epoch_fused(self, train_data, epoch_idx):
+        acc = self.model.device_loss_acc
+        acc.zero_()
+        lr = self.current_lr()
+        n = 0
+        for batch in train_data:
+            self.model.fused_step(batch, lr)
+            n += 1
+        total = float(acc.item())  # one host sync per epoch
+        if np.isnan(total):
+            self.logger.info(f"Loss is nan at epoch: {epoch_idx}. Exiting.")
+            return torch.tensor(float("nan")), torch.tensor(0.0)
+        return total, n
+
+    def _check_nan(self, loss):
+        return bool(torch.isnan(loss))
+
+    def _train_epoch_autograd(self, train_data, epoch_idx, loss_func=None):
+        loss_func = loss_func or self.model.calculate_loss
+        total_loss = None
+        loss_batches = []
+        for batch_idx, interaction in enumerate(train_data):
+            self._zero_grad()
+            second = interaction.clone() if hasattr(interaction, "clone") else interaction
+            losses = loss_func(interaction)
+            if isinstance(losses, tuple):
+                loss = sum(losses)
+                part = tuple(x.item() for x in losses)
+                total_loss = part if total_loss is None else tuple(map(sum, zip(total_loss, part)))
+            else:
+                loss = losses
+                total_loss = losses.item() if total_loss is None else total_loss + losses.item()
+            if self._check_nan(loss):
+                self.logger.info(f"Loss is nan at epoch: {epoch_idx}, batch index: {batch_idx}. Exiting.")
+                return loss, torch.tensor(0.0)
+            if not getattr(self.model, "mg_enable", False):
+                if self.mg and batch_idx % self.beta == 0:
+                    (self.alpha1 * loss).backward()
+                    self.optimizer.step()
+                    self.optimizer.zero_grad()
+                    l2 = loss_func(second)
+                    loss = sum(l2) if isinstance(l2, tuple) else l2
+                    if self._check_nan(loss):
+                        self.logger.info(f"Loss is nan at epoch: {epoch_idx}, batch index: {batch_idx}. Exiting.")
+                        return loss, torch.tensor(0.0)
+                    (-1 * self.alpha2 * loss).backward()
+                else:
+                    loss.backward()
+                if self.clip_grad_norm:
+                    clip_grad_norm_(self.model.parameters(), **self.clip_grad_norm)
+                self.optimizer.step()
+                loss_batches.append(loss.detach())
+                continue
+            loss.backward()
+            if self.clip_grad_norm:
+                clip_grad_norm_(self.model.parameters(), **self.clip_grad_norm)
+            self.optimizer.step()
+            loss_batches.append(loss.detach())
+            self._mirror_gradient(loss_func, second)
+        return total_loss, loss_batches
+
+    def _zero_grad(self):
+        try:
+            self.optimizer.zero_grad(set_to_none=True)
+        except TypeError:
+            self.optimizer.zero_grad()
+
+    def _mirror_gradient(self, loss_func, inter):
+        """Model-level mirror gradient (reference trainer.py:268-348)."""
+        m = self.model
+        interval = int(getattr(m, "mg_interval", 0))
+        log_every = int(getattr(m, "mg_log_interval", 50))
+        step_id = int(getattr(m, "global_step", 0))
+        if log_every > 0 and step_id and step_id % log_every == 0 and hasattr(m, "log_mm_diagnostics"):
+            try:
+                m.log_mm_diagnostics(self.optimizer)
+            except Exception as err:  # noqa: BLE001
+                self.logger.warning(f"log_mm_diagnostics failed at step {step_id}: {err}")
+        if interval <= 0 or step_id % interval != 0:
+            return
+        lr = self.optimizer.param_groups[0].get("lr", 1.0)
+        self._zero_grad()
+        cur = loss_func(inter)
+        (sum(cur) if isinstance(cur, tuple) else cur).backward()
+        params, grads = [], []
+        for p in m.parameters():
+            if p.requires_grad and p.grad is not None:
+                params.append(p)
+                grads.append(p.grad.detach().clone())
+        with torch.no_grad():
+            base = float(getattr(m, "mg_alpha", 0.5))
+            if not grads:
+                alpha = base
+            else:
+                g_all = torch.cat([g.view(-1) for g in grads])
+                p_all = torch.cat([p.detach().view(-1) for p in params])
+                grad_rms = float(g_all.norm() / (g_all.numel() ** 0.5))
+                param_rms = float(p_all.norm() / (p_all.numel() ** 0.5) + 1e-12)
+                alpha = max(base, self.mg_target_rel_step * param_rms / (lr * grad_rms + 1e-12))
+                alpha = min(alpha, base * self.mg_alpha_max_scale)
+            m._alpha_eff = float(alpha)
+            for p, g in zip(params, grads):
+                p.add_(-alpha * lr * g)
+        self._zero_grad()
+        mir = loss_func(inter)
+        mirror = sum(mir) if isinstance(mir, tuple) else mir
+        mirror.backward()
+        with torch.no_grad():
+            beta = float(getattr(m, "mg_beta", 0.2))
+            for p in m.parameters():
+                if p.requires_grad and p.grad is not None:
+                    p.grad.mul_(-beta)
+            for p, g in zip(params, grads):
+                p.add_(alpha * lr * g)
+        self.optimizer.step()
+        self._zero_grad()
+        if getattr(m, "mg_verbose", False):
+            print(f"[MG] step={step_id} mirror_loss={float(mirror.item()):.4f} α_eff={alpha:.3g}")
+
+    # ------------------------------------------------------------------- fit
+    def _valid_epoch(self, valid_data):
+        res = self.evaluate(valid_data)
+        score = res[self.valid_metric] if self.valid_metric else res["NDCG@20"]
+        return score, res
+
+    def _generate_train_loss_output(self, epoch_idx, s_time, e_time, losses):
+        out = "epoch %d training [time: %.2fs, " % (epoch_idx, e_time - s_time)
+        if isinstance(losses, tuple):
+            out = ", ".join("train_loss%d: %.4f" % (i + 1, x) for i, x in enumerate(losses))
+        else:
+            out += "train loss: %.4f" % losses
+        return out + "]"
+
+    def fit(self, train_data, valid_data=None, test_data=None, saved=False, verbose=True):
+        for epoch_idx in range(self.start_epoch, self.epochs):
+            t0 = time()
+            self.model.cur_epoch = epoch_idx
+            self.model.pre_epoch_processing()
+            train_loss, _ = self._train_epoch(train_data, epoch_idx)
+            if torch.is_tensor(train_loss):
+                break
+            if self.lr_scheduler is not None:
+                self.lr_scheduler.step()
+            self._epoch_for_lr += 1
+            self.train_loss_dict[epoch_idx] = sum(train_loss) if isinstance(train_loss, tuple) else train_loss
+            t1 = time()
+            msg = self._generate_train_loss_output(epoch_idx, t0, t1, train_loss)
+            post = self.model.post_epoch_processing()
+            if verbose:
+                self.logger.info(msg)
+                if post is not None:
+                    self.logger.info(post)
+            if (epoch_idx + 1) % self.eval_step == 0:
+                v0 = time()
+                score, vres = self._valid_epoch(valid_data)
+                self.best_valid_score, self.cur_step, stop, update = early_stopping(
+                    score, self.best_valid_score, self.cur_step, max_step=self.stopping_step,
+                    bigger=self.valid_metric_bigger)
+                v1 = time()
+                _, tres = self._valid_epoch(test_data)
+                if verbose:
+                    self.logger.info("epoch %d evaluating [time: %.2fs, valid_score: %f]" % (epoch_idx, v1 - v0, score))
+                    self.logger.info("valid result: \n" + dict2str(vres))
+                    self.logger.info("test result: \n" + dict2str(tres))
+                if update:
+                    if verbose:
+                        self.logger.info("██ " + str(self.config["model"]) + "--Best validation results updated!!!")
+                    self.best_valid_result = vres
+                    self.best_test_upon_valid = tres
+                if stop:
+                    if verbose:
+                        self.logger.info("+++++Finished training, best eval result in epoch %d" %
+                                         (epoch_idx - self.cur_step * self.eval_step))
+                    break
+        return self.best_valid_score, self.best_valid_result, self.best_test_upon_valid
+
+    # -------------------------------------------------------------- evaluate
+    @torch.no_grad()
+    def evaluate(self, eval_data, is_test=False, idx=0):
+        self.model.eval()
+        k = max(self.config["topk"])
+        mats = []
+        fused = hasattr(self.model, "full_sort_topk") and hasattr(eval_data, "mask_rowptr")
+        for batch in eval_data:
+            if fused:
+                _, topk = self.model.full_sort_topk(batch, k, eval_data)
+            else:
+                scores = self.model.full_sort_predict(batch)
+                m = batch[1]
+                scores[m[0], m[1]] = -1e10
+                _, topk = torch.topk(scores, k, dim=-1)
+            mats.append(topk)
+        return self.evaluator.evaluate(mats, eval_data, is_test=is_test, idx=idx)

@@ -1,0 +1,142 @@
+"""End-to-end parity on the GPU: the reference's training flow (quick_start order,
+seed 999, host sampler = the reference's exact triplet stream) through the rsx
+models and Trainer, compared with what the reference itself produced on the same
+data (tests/golden, captured by tools/capture_golden.py).
+
+Tolerances: parameters after 2-3 epochs of Adam within atol 5e-5 (f32, ~20-27
+steps, summation-order differences amplified by Adam's normalisation);
+metric dicts within 1e-4 (the north-star bound); top-50 index rows equal except
+where the fixture flags a near-tie.
+"""
+import os
+import shutil
+
+import numpy as np
+import pytest
+import torch
+
+from helpers import metric_dict, params
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _setup(tmp_path, model, extra):
+    from rsx.config import Config
+    from rsx.data import EvalDataLoader, RecDataset, TrainDataLoader
+
+    d = tmp_path / "data" / "baby"
+    d.mkdir(parents=True)
+    shutil.copy(os.path.join(GOLD, "gold_small.inter"), d / "baby.inter")
+    cfg = dict(data_path=str(tmp_path / "data") + "/", train_batch_size=512, eval_batch_size=256,
+               rsx_sampler="host", is_multimodal_model=False)
+    cfg.update(extra)
+    c = Config(model, "baby", cfg)
+    for k in c["hyper_parameters"]:
+        if isinstance(c[k], list):
+            c[k] = c[k][0]
+    ds = RecDataset(c)
+    tr, va, te = ds.split()
+    for x in (ds, tr, va, te):
+        str(x)
+    train = TrainDataLoader(c, tr, batch_size=512, shuffle=True)
+    valid = EvalDataLoader(c, va, additional_dataset=tr, batch_size=256)
+    test = EvalDataLoader(c, te, additional_dataset=tr, batch_size=256)
+    return c, train, valid, test
+
+
+def _run(tmp_path, model, extra, epochs, fused=True, record=False):
+    from rsx.trainer import Trainer
+    from rsx.utils import get_model, init_seed
+
+    c, train, valid, test = _setup(tmp_path, model, dict(extra, rsx_fused_step=fused))
+    init_seed(c["seed"])
+    train.pretrain_setup()
+    m = get_model(model)(c, train)
+    t = Trainer(c, m)
+    rec = []
+    if record:
+        orig = train._next_batch_data
+
+        def wrapped():
+            b = orig()
+            rec.append(b.cpu().clone())
+            return b
+
+        train._next_batch_data = wrapped
+    graphs = []
+    for epoch in range(epochs):
+        m.cur_epoch = epoch
+        m.pre_epoch_processing()
+        if hasattr(m, "engine") and hasattr(m.engine, "train_adj"):
+            graphs.append(m.engine.train_adj)
+        loss, _ = t._train_epoch(train, epoch)
+        assert not torch.is_tensor(loss)
+        if t.lr_scheduler is not None:
+            t.lr_scheduler.step()
+        t._epoch_for_lr += 1
+    torch.cuda.synchronize()
+    vres = t.evaluate(valid)
+    tres = t.evaluate(test)
+    return m, vres, tres, rec, graphs
+
+
+def _compare_metrics(res, ref):
+    assert res.keys() == ref.keys()
+    for k in ref:
+        assert abs(res[k] - ref[k]) <= 1e-4 + 1e-12, (k, res[k], ref[k])
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_lightgcn_three_epochs_vs_reference(tmp_path, golden, fused):
+    z = golden("lightgcn_small")
+    m, vres, tres, rec, _ = _run(tmp_path, "LightGCN", dict(n_layers=[3], reg_weight=[1e-2]), 3, fused=fused,
+                                 record=True)
+    got = torch.cat(rec, dim=1).numpy()
+    want = np.concatenate([z[f"epoch{e}_triplets"] for e in range(3)], axis=1).astype(np.int64)
+    assert np.array_equal(got, want)
+    pu, pi = params(z, "epoch2_param.", "LightGCN")
+    u = m.embedding_dict["user_emb"].detach().cpu().numpy()
+    i = m.embedding_dict["item_emb"].detach().cpu().numpy()
+    np.testing.assert_allclose(u, pu, rtol=0, atol=5e-5)
+    np.testing.assert_allclose(i, pi, rtol=0, atol=5e-5)
+    _compare_metrics(vres, metric_dict(z, "epoch2_valid"))
+    _compare_metrics(tres, metric_dict(z, "epoch2_test"))
+
+
+@pytest.mark.parametrize("fx,dropout", [("layergcn_small", 0.0), ("layergcn_drop_small", 0.1)])
+def test_layergcn_two_epochs_vs_reference(tmp_path, golden, fx, dropout):
+    from helpers import coo_sorted, csr_to_sorted
+
+    z = golden(fx)
+    m, vres, tres, _, graphs = _run(tmp_path, "LayerGCN", dict(n_layers=[2], reg_weight=[1e-2], dropout=[dropout]), 2)
+    if dropout > 0:
+        for e, A in enumerate(graphs):
+            ref = coo_sorted(z[f"e{e}_masked_idx"].astype(np.int64), z[f"e{e}_masked_val"])
+            mine = csr_to_sorted(A.rowptr.cpu().numpy(), A.col.cpu().numpy(), A.val.cpu().numpy())
+            for x, y in zip(ref, mine):
+                assert np.array_equal(x, y), e
+    pu, pi = params(z, "epoch1_param.", "LayerGCN")
+    np.testing.assert_allclose(m.user_embeddings.detach().cpu().numpy(), pu, rtol=0, atol=5e-5)
+    np.testing.assert_allclose(m.item_embeddings.detach().cpu().numpy(), pi, rtol=0, atol=5e-5)
+    _compare_metrics(vres, metric_dict(z, "epoch1_valid"))
+    _compare_metrics(tres, metric_dict(z, "epoch1_test"))
+
+
+def test_quick_start_main_flow(tmp_path):
+    """`main.py -m LightGCN -d baby`-style run through quick_start (grid of one, 2 epochs)."""
+    from rsx.quick_start import quick_start
+
+    d = tmp_path / "data" / "baby"
+    d.mkdir(parents=True)
+    shutil.copy(os.path.join(GOLD, "gold_small.inter"), d / "baby.inter")
+    cwd = os.getcwd()
+    os.chdir(tmp_path)
+    try:
+        res = quick_start("LightGCN", "baby", {"data_path": str(tmp_path / "data") + "/", "epochs": 2,
+                                                "n_layers": [2], "train_batch_size": 512}, log=True)
+    finally:
+        os.chdir(cwd)
+    assert len(res) == 1 and "recall@20" in res[0][1]
+    assert os.listdir(tmp_path / "log")
