@@ -1,0 +1,351 @@
+"""SMORE on the rsx HIP path — drop-in for the reference's models/smore.py (WSDM'25).
+
+Same class name, constructor, YAML keys, module names and creation order (so
+`init_seed` gives the reference's initial weights), forward and loss
+(reference src/models/smore.py:24-449):
+
+* UI backbone: n_ui_layers propagations of the float32 sym-normalised graph,
+  mean over layers — the HIP propagation (rsx_lightgcn_forward machinery) with
+  autograd whose backward is the same operator (the graph is symmetric);
+* item-item views (image / text kNN graphs and their max-pooled fusion, built
+  once like the reference and cached next to the data) and the item -> user
+  aggregation R — HIP SpMM with autograd (backward = SpMM with the transposed
+  CSR, the kNN graphs are not symmetric);
+* projection + spectral denoise / fusion (smore.py:209-252,256-272) — the fused
+  HIP pass rsx_smore_spectral (forward and backward, see csrc/smore.hip) when the
+  library has it, else the op-for-op torch.fft form;
+* BPR part of the loss — the fused HIP BPR kernel (variant SMORE);
+* gates, query MLPs, softmax over d, InfoNCE — torch ops on the device.
+
+Diagnostics that the reference gathers with per-step `.item()` calls
+(spectrum band energies, gate statistics, CL values) are computed lazily, only
+when `log_mm_diagnostics` runs, so training issues no per-step host syncs.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _lib as L
+from . import graph, ops
+from .lightgcn import _BprLoss
+from .recommender import GeneralRecommender
+
+
+class _SpMM(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, A, AT):
+        ctx.AT = AT
+        return A.spmm(x.contiguous())
+
+    @staticmethod
+    def backward(ctx, g):
+        return ctx.AT.spmm(g.contiguous()), None, None
+
+
+def _prop_mean(A, x, K):
+    import ctypes as C
+
+    x = x.contiguous()
+    out = torch.empty_like(x)
+    s, h0, h1 = torch.empty_like(x), torch.empty_like(x), torch.empty_like(x)
+    d = x.shape[1]
+    rc = L.lib().rsx_lightgcn_forward(C.byref(A.struct), d, K, ops._p(x), ops._p(s), ops._p(h0), ops._p(h1),
+                                      ops._p(out), ops._p(A.slab(d)), ops._stream())
+    L.check(rc, "rsx_lightgcn_forward")
+    return out
+
+
+class _PropMean(torch.autograd.Function):
+    """mean_{k=0..K} A^k x for a symmetric A (backward: the same operator)."""
+
+    @staticmethod
+    def forward(ctx, x, A, K):
+        ctx.A, ctx.K = A, K
+        return _prop_mean(A, x, K)
+
+    @staticmethod
+    def backward(ctx, g):
+        return _prop_mean(ctx.A, g, ctx.K), None, None
+
+
+def knn_graph(feat: np.ndarray, k: int):
+    """build_sim + build_knn_normalized_graph(sparse, 'sym') (src/utils/utils.py:134-181) on the CPU,
+    float32 as the reference: cosine similarities, top-k per row, deg = sum of kept values,
+    w = d_r^-1/2 * s * d_c^-1/2.  Returns (rows, cols, vals)."""
+    x = torch.from_numpy(feat)
+    xn = x.div(torch.norm(x, p=2, dim=-1, keepdim=True))
+    n = xn.shape[0]
+    rows, cols, vals = [], [], []
+    step = max(1, (1 << 26) // max(n, 1))
+    for s in range(0, n, step):
+        sim = torch.mm(xn[s:s + step], xn.t())
+        v, i = torch.topk(sim, k, dim=-1)
+        rows.append(torch.arange(s, s + sim.shape[0]).repeat_interleave(k))
+        cols.append(i.reshape(-1))
+        vals.append(v.reshape(-1))
+    r, c, v = torch.cat(rows), torch.cat(cols), torch.cat(vals)
+    deg = torch.zeros(n, dtype=v.dtype).index_add_(0, r, v)
+    dis = deg.pow_(-0.5)
+    dis.masked_fill_(dis == float("inf"), 0)
+    w = dis[r] * v * dis[c]
+    return r.numpy().astype(np.int64), c.numpy().astype(np.int64), w.numpy().astype(np.float32)
+
+
+def max_pool_union(a, b, n):
+    """Elementwise max over the union of two edge sets (smore.py:153-174)."""
+    ka = a[0] * n + a[1]
+    kb = b[0] * n + b[1]
+    keys = np.concatenate([ka, kb])
+    vals = np.concatenate([a[2], b[2]])
+    # coalesce duplicates inside each graph first (values are unique per (r,c) already)
+    order = np.argsort(keys, kind="stable")
+    keys, vals = keys[order], vals[order]
+    uk, start = np.unique(keys, return_index=True)
+    mx = np.maximum.reduceat(vals, start)
+    return (uk // n).astype(np.int64), (uk % n).astype(np.int64), mx.astype(np.float32)
+
+
+class _DevGraph:
+    """A sparse operator with its transpose on the device (forward / backward SpMM)."""
+
+    def __init__(self, rows, cols, vals, n_rows, n_cols, device, chunk):
+        self.A = ops.DeviceCSR(*graph.to_csr(rows, cols, vals, n_rows, n_cols), n_cols, device, chunk)
+        self.AT = ops.DeviceCSR(*graph.to_csr(cols, rows, vals, n_cols, n_rows), n_rows, device, chunk)
+
+    def __call__(self, x):
+        return _SpMM.apply(x, self.A, self.AT)
+
+
+def spectrum_torch(img, txt, wv, wt, wf, normalize=True):
+    """Reference spectrum_convolution (smore.py:209-237) with torch.fft."""
+    d = img.shape[1]
+    fi = torch.fft.rfft(img, dim=1, norm="ortho")
+    ft = torch.fft.rfft(txt, dim=1, norm="ortho")
+    cw = [torch.view_as_complex(w) for w in (wv, wt, wf)]
+    if normalize:
+        cw = [w / (torch.abs(w) + 1e-8) for w in cw]
+    cv = torch.fft.irfft(fi * cw[0], n=d, dim=1, norm="ortho")
+    ct = torch.fft.irfft(ft * cw[1], n=d, dim=1, norm="ortho")
+    cf = torch.fft.irfft(ft * fi * cw[2], n=d, dim=1, norm="ortho")
+    return cv, ct, cf
+
+
+class SMORE(GeneralRecommender):
+    def __init__(self, config, dataset):
+        super().__init__(config, dataset)
+        ops.require_device(self.device)
+        self.sparse = True
+        self.cl_loss = config["cl_loss"]
+        self.n_ui_layers = config["n_ui_layers"]
+        self.embedding_dim = config["embedding_size"]
+        self.n_layers = config["n_layers"]
+        self.reg_weight = config["reg_weight"]
+        self.image_knn_k = config["image_knn_k"]
+        self.text_knn_k = config["text_knn_k"]
+        self.dropout_rate = config["dropout_rate"]
+        self.dropout = nn.Dropout(p=self.dropout_rate)
+        chunk = int(config["rsx_chunk"] or 32)
+        d = self.embedding_dim
+        self.interaction_matrix = dataset.inter_matrix(form="coo").astype(np.float32)
+        # parameters in the reference's creation order (identical init under init_seed)
+        self.user_embedding = nn.Embedding(self.n_users, d)
+        self.item_id_embedding = nn.Embedding(self.n_items, d)
+        nn.init.xavier_uniform_(self.user_embedding.weight)
+        nn.init.xavier_uniform_(self.item_id_embedding.weight)
+        nu, ni = self.n_users, self.n_items
+        im = self.interaction_matrix
+        rp, col, val = graph.smore_norm_adj(im.row.astype(np.int64), im.col.astype(np.int64), nu, ni)
+        self.norm_adj_csr = ops.DeviceCSR(rp, col, val, nu + ni, self.device, chunk)
+        rrp, rcol, rval = graph.csr_block(rp, col, val, 0, nu, nu, nu + ni)
+        rows = np.repeat(np.arange(nu), np.diff(rrp))
+        self.R = _DevGraph(rows, rcol.astype(np.int64), rval, nu, ni, self.device, chunk)
+        root = os.path.abspath((config["data_path"] or "") + (config["dataset"] or ""))
+        img_g = txt_g = None
+        if self.v_feat is not None:
+            self.image_embedding = nn.Embedding.from_pretrained(self.v_feat.clone(), freeze=False)
+            img_g = self._cached_knn(root, "image", self.v_feat, self.image_knn_k)
+        if self.t_feat is not None:
+            self.text_embedding = nn.Embedding.from_pretrained(self.t_feat.clone(), freeze=False)
+            txt_g = self._cached_knn(root, "text", self.t_feat, self.text_knn_k)
+        self.image_graph = _DevGraph(*img_g, ni, ni, self.device, chunk)
+        self.text_graph = _DevGraph(*txt_g, ni, ni, self.device, chunk)
+        self.fusion_graph = _DevGraph(*max_pool_union(img_g, txt_g, ni), ni, ni, self.device, chunk)
+        if self.v_feat is not None:
+            self.image_trs = nn.Linear(self.v_feat.shape[1], d)
+        if self.t_feat is not None:
+            self.text_trs = nn.Linear(self.t_feat.shape[1], d)
+        self.softmax = nn.Softmax(dim=-1)
+        self.query_v = nn.Sequential(nn.Linear(d, d), nn.Tanh(), nn.Linear(d, d, bias=False))
+        self.query_t = nn.Sequential(nn.Linear(d, d), nn.Tanh(), nn.Linear(d, d, bias=False))
+        self.gate_v = nn.Sequential(nn.Linear(d, d), nn.Sigmoid())
+        self.gate_t = nn.Sequential(nn.Linear(d, d), nn.Sigmoid())
+        self.gate_f = nn.Sequential(nn.Linear(d, d), nn.Sigmoid())
+        self.gate_image_prefer = nn.Sequential(nn.Linear(d, d), nn.Sigmoid())
+        self.gate_text_prefer = nn.Sequential(nn.Linear(d, d), nn.Sigmoid())
+        self.gate_fusion_prefer = nn.Sequential(nn.Linear(d, d), nn.Sigmoid())
+        self.image_complex_weight = nn.Parameter(torch.randn(1, d // 2 + 1, 2, dtype=torch.float32))
+        self.text_complex_weight = nn.Parameter(torch.randn(1, d // 2 + 1, 2, dtype=torch.float32))
+        self.fusion_complex_weight = nn.Parameter(torch.randn(1, d // 2 + 1, 2, dtype=torch.float32))
+        self.mg_enable = bool(config.get("mg_enable", True))
+        self.mg_interval = int(config.get("mg_interval", 3))
+        self.mg_alpha = float(config.get("mg_alpha", 0.5))
+        self.mg_beta = float(config.get("mg_beta", 0.2))
+        self.mg_verbose = bool(config.get("mg_verbose", True))
+        self.global_step = 0
+        self.inject_mode = config.get("inject_mode", "residual")
+        self.inject_scale = float(config.get("inject_scale", 0.7))
+        self.spectral_weight_norm = bool(config.get("spectral_weight_norm", True))
+        self.cl_temp = float(config.get("cl_temp", 0.2))
+        self.diag_spectrum = bool(config.get("diag_spectrum", True))
+        self.diag_gate = bool(config.get("diag_gate", True))
+        self.diag_grad = bool(config.get("diag_grad", True))
+        self.use_hip_spectral = bool(config.get("rsx_smore_spectral", True))
+        self._last = {}
+        self.to(self.device)
+
+    # ---------------------------------------------------------------- graphs
+    def _cached_knn(self, root, name, feat, k):
+        path = os.path.join(root, f"rsx_{name}_knn_{k}.npz")
+        f = feat.detach().cpu().numpy()
+        sig = np.array([f.shape[0], f.shape[1], float(np.float64(f[:4].sum())), float(np.float64(f[-4:].sum()))])
+        if os.path.exists(path):
+            z = np.load(path)
+            if np.array_equal(z["sig"], sig):
+                return z["r"], z["c"], z["v"]
+        r, c, v = knn_graph(f, k)
+        try:
+            os.makedirs(root, exist_ok=True)
+            np.savez(path, r=r, c=c, v=v, sig=sig)
+        except OSError:
+            pass
+        return r, c, v
+
+    # --------------------------------------------------------------- forward
+    def spectrum_convolution(self, image_embeds, text_embeds):
+        cv, ct, cf = spectrum_torch(image_embeds, text_embeds, self.image_complex_weight,
+                                    self.text_complex_weight, self.fusion_complex_weight, self.spectral_weight_norm)
+        self._last["spec_in"] = (image_embeds.detach(), text_embeds.detach())
+        return cv, ct, cf
+
+    def _projected_spectrum(self):
+        from .smore_spectral import spectral_available, spectral_fused
+
+        if self.use_hip_spectral and spectral_available():
+            return spectral_fused(self)
+        img = self.image_trs(self.image_embedding.weight)
+        txt = self.text_trs(self.text_embedding.weight)
+        return self.spectrum_convolution(img, txt)
+
+    def forward(self, adj=None, train=False):
+        """Reference signature: (users, items) or, with train=True, (users, items, side, content)."""
+        all_embeds, side, content = self._forward_all(train)
+        users, items = torch.split(all_embeds, [self.n_users, self.n_items], dim=0)
+        if train:
+            return users, items, side, content
+        return users, items
+
+    def _forward_all(self, train=False):
+        cv, ct, cf = self._projected_spectrum()
+        item_id = self.item_id_embedding.weight
+        if self.inject_mode == "mul":
+            img_i = item_id * self.gate_v(cv)
+            txt_i = item_id * self.gate_t(ct)
+            fus_i = item_id * self.gate_f(cf)
+        else:
+            img_i = item_id + self.inject_scale * self.gate_v(cv)
+            txt_i = item_id + self.inject_scale * self.gate_t(ct)
+            fus_i = item_id + self.inject_scale * self.gate_f(cf)
+        ego = torch.cat([self.user_embedding.weight, item_id], dim=0)
+        content = _PropMean.apply(ego, self.norm_adj_csr, self.n_ui_layers)
+        for _ in range(self.n_layers):
+            img_i = self.image_graph(img_i)
+        image_embeds = torch.cat([self.R(img_i), img_i], dim=0)
+        for _ in range(self.n_layers):
+            txt_i = self.text_graph(txt_i)
+        text_embeds = torch.cat([self.R(txt_i), txt_i], dim=0)
+        for _ in range(self.n_layers):
+            fus_i = self.fusion_graph(fus_i)
+        fusion_embeds = torch.cat([self.R(fus_i), fus_i], dim=0)
+        soft_v = self.softmax(self.query_v(fusion_embeds))
+        soft_t = self.softmax(self.query_t(fusion_embeds))
+        agg_img = soft_v * image_embeds
+        agg_txt = soft_t * text_embeds
+        ip = self.dropout(self.gate_image_prefer(content))
+        tp = self.dropout(self.gate_text_prefer(content))
+        fp = self.dropout(self.gate_fusion_prefer(content))
+        agg_img = torch.multiply(ip, agg_img)
+        agg_txt = torch.multiply(tp, agg_txt)
+        fusion_embeds = torch.multiply(fp, fusion_embeds)
+        side = torch.mean(torch.stack([agg_img, agg_txt, fusion_embeds]), dim=0)
+        all_embeds = content + side
+        if train:
+            self._last["conv"] = (cv.detach(), ct.detach(), cf.detach())
+        return all_embeds, side, content
+
+    # ------------------------------------------------------------------ loss
+    @staticmethod
+    def InfoNCE(view1, view2, temperature):
+        view1, view2 = F.normalize(view1, dim=1), F.normalize(view2, dim=1)
+        pos = torch.exp((view1 * view2).sum(dim=-1) / temperature)
+        ttl = torch.exp(torch.matmul(view1, view2.transpose(0, 1)) / temperature).sum(dim=1)
+        return torch.mean(-torch.log(pos / ttl))
+
+    def calculate_loss(self, interaction):
+        users, pos, neg = interaction[0], interaction[1], interaction[2]
+        all_embeds, side, content = self._forward_all(train=True)
+        self.global_step += 1
+        nu = self.n_users
+        bpr = _BprLoss.apply(all_embeds, None, None, interaction[:3].contiguous(), L.RSX_BPR_SMORE,
+                             float(self.reg_weight), float(self.batch_size), nu, self.n_items)
+        cl_items = self.InfoNCE(side[nu:][pos], content[nu:][pos], self.cl_temp)
+        cl_users = self.InfoNCE(side[:nu][users], content[:nu][users], self.cl_temp)
+        self._last["cl"] = (cl_items.detach(), cl_users.detach())
+        return bpr + self.cl_loss * (cl_items + cl_users)
+
+    def full_sort_predict(self, interaction):
+        with torch.no_grad():
+            u, i = self.forward(self.norm_adj_csr)
+        return ops.score_dense(u.contiguous(), interaction[0].contiguous(), i.contiguous())
+
+    def full_sort_topk(self, interaction, k, eval_data):
+        with torch.no_grad():
+            if getattr(self, "_eval_cache", None) is None:
+                u, i = self.forward(self.norm_adj_csr)
+                self._eval_cache = (u.contiguous(), i.contiguous())
+            u, i = self._eval_cache
+        return ops.fullsort_topk(u, interaction[0].contiguous(), i, eval_data.mask_rowptr, eval_data.mask_col, k)
+
+    def train(self, mode: bool = True):
+        self._eval_cache = None
+        return super().train(mode)
+
+    # ----------------------------------------------------------- diagnostics
+    @torch.no_grad()
+    def log_mm_diagnostics(self, optimizer=None):
+        if not (self.mg_verbose or self.diag_grad or self.diag_spectrum or self.diag_gate):
+            return
+        parts = []
+        if self.diag_spectrum and "spec_in" in self._last:
+            def band(x):
+                f = torch.fft.rfft(x, dim=1, norm="ortho")
+                m2 = (f.real ** 2 + f.imag ** 2).mean(dim=0)
+                n = m2.numel()
+                lo, mid, hi = m2[:max(1, n // 3)].sum(), m2[max(1, n // 3):max(2, 2 * n // 3)].sum(), m2[max(2, 2 * n // 3):].sum()
+                t = lo + mid + hi + 1e-12
+                return (lo / t).item(), (mid / t).item(), (hi / t).item()
+            a, b = self._last["spec_in"]
+            i3, t3 = band(a), band(b)
+            parts.append(f"[spec] image(lo/mid/hi)={i3[0]:.2f}/{i3[1]:.2f}/{i3[2]:.2f} "
+                         f"text={t3[0]:.2f}/{t3[1]:.2f}/{t3[2]:.2f}")
+        if "cl" in self._last:
+            ci, cu = self._last["cl"]
+            parts.append(f"[cl] cl_items={ci.item():.4f}, cl_users={cu.item():.4f}")
+        if optimizer is not None and len(optimizer.param_groups) > 0:
+            lr = optimizer.param_groups[0].get("lr", float("nan"))
+            parts.append(f"[mg] step={self.global_step} τ={self.mg_interval} α={self.mg_alpha} β={self.mg_beta} lr={lr}")
+        print(" | ".join(parts))

@@ -1,0 +1,134 @@
+"""SMORE on the GPU against the reference's own outputs (tests/golden/smore_small.npz):
+identical initial weights (same module creation order under init_seed), graphs bit
+for bit, forward within rtol 1e-5, first-batch loss / gradients / Adam step, and one
+epoch through the Trainer with the model-level mirror gradient.  Dropout 0 (the
+reference's dropout masks come from its own RNG and cannot be replayed on the GPU)."""
+import os
+import shutil
+
+import numpy as np
+import pytest
+import torch
+
+from helpers import coo_sorted, csr_to_sorted, metric_dict
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _setup(tmp_path, golden):
+    from rsx.config import Config
+    from rsx.data import EvalDataLoader, RecDataset, TrainDataLoader
+
+    z = golden("smore_small")
+    d = tmp_path / "data" / "baby"
+    d.mkdir(parents=True)
+    shutil.copy(os.path.join(GOLD, "gold_small.inter"), d / "baby.inter")
+    np.save(d / "image_feat_raw.npy", z["v_feat"])
+    np.save(d / "text_feat_raw.npy", z["t_feat"])
+    c = Config("SMORE", "baby", dict(data_path=str(tmp_path / "data") + "/", train_batch_size=512,
+                                      eval_batch_size=256, rsx_sampler="host", is_multimodal_model=True,
+                                      dropout_rate=[0.0], mg_verbose=False, image_knn_k=[10], text_knn_k=[8]))
+    for k in c["hyper_parameters"]:
+        if isinstance(c[k], list):
+            c[k] = c[k][0]
+    ds = RecDataset(c)
+    tr, va, te = ds.split()
+    for x in (ds, tr, va, te):
+        str(x)
+    train = TrainDataLoader(c, tr, batch_size=512, shuffle=True)
+    valid = EvalDataLoader(c, va, additional_dataset=tr, batch_size=256)
+    test = EvalDataLoader(c, te, additional_dataset=tr, batch_size=256)
+    return z, c, train, valid, test
+
+
+def _model(c, train):
+    from rsx.smore import SMORE
+    from rsx.utils import init_seed
+
+    init_seed(c["seed"])
+    train.pretrain_setup()
+    return SMORE(c, train)
+
+
+def test_smore_init_graphs_forward(tmp_path, golden):
+    z, c, train, valid, test = _setup(tmp_path, golden)
+    m = _model(c, train)
+    for n, p in m.named_parameters():
+        assert np.array_equal(p.detach().cpu().numpy(), z["init." + n]), n
+    nu = m.n_users
+    A = m.norm_adj_csr
+    ref = coo_sorted(z["norm_adj_idx"].astype(np.int64), z["norm_adj_val"])
+    for x, y in zip(ref, csr_to_sorted(A.rowptr.cpu().numpy(), A.col.cpu().numpy(), A.val.cpu().numpy())):
+        assert np.array_equal(x, y)
+    for name, g in (("image_original_adj", m.image_graph), ("text_original_adj", m.text_graph),
+                    ("fusion_adj", m.fusion_graph), ("R", m.R)):
+        ref = coo_sorted(z[name + "_idx"].astype(np.int64), z[name + "_val"])
+        mine = csr_to_sorted(g.A.rowptr.cpu().numpy(), g.A.col.cpu().numpy(), g.A.val.cpu().numpy())
+        assert np.array_equal(ref[0], mine[0]) and np.array_equal(ref[1], mine[1]), name
+        if name == "R":
+            assert np.array_equal(ref[2], mine[2])
+        else:
+            # kNN cosine similarities come from a CPU sgemm: 1-ulp differences across host CPUs
+            np.testing.assert_allclose(mine[2], ref[2], rtol=1e-6, atol=0, err_msg=name)
+    m.eval()
+    with torch.no_grad():
+        u, i = m.forward(None)
+        np.testing.assert_allclose(u.cpu().numpy(), z["fwd_user"], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(i.cpu().numpy(), z["fwd_item"], rtol=1e-5, atol=1e-6)
+        cv, ct, cf = m._projected_spectrum()
+        np.testing.assert_allclose(cv.cpu().numpy(), z["spec_conv_v"], rtol=1e-4, atol=1e-6)
+        np.testing.assert_allclose(ct.cpu().numpy(), z["spec_conv_t"], rtol=1e-4, atol=1e-6)
+        np.testing.assert_allclose(cf.cpu().numpy(), z["spec_conv_f"], rtol=1e-4, atol=1e-6)
+        _, _, side, content = m.forward(None, train=True)
+        np.testing.assert_allclose(side.cpu().numpy(), z["fwd_side"], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(content.cpu().numpy(), z["fwd_content"], rtol=1e-5, atol=1e-6)
+
+
+def test_smore_first_step(tmp_path, golden):
+    z, c, train, valid, test = _setup(tmp_path, golden)
+    m = _model(c, train)
+    m.train()
+    opt = torch.optim.Adam(m.parameters(), lr=c["learning_rate"])
+    trip = torch.from_numpy(z["epoch0_triplets"][:, :512].astype(np.int64)).cuda()
+    loss = m.calculate_loss(trip)
+    loss.backward()
+    assert abs(loss.item() - float(z["step0_loss"])) <= 1e-5 * abs(float(z["step0_loss"]))
+    for n, p in m.named_parameters():
+        key = "step0_grad." + n
+        if key in z:
+            g = p.grad.detach().cpu().numpy()
+            scale = max(np.abs(z[key]).max(), 1e-12)
+            np.testing.assert_allclose(g, z[key], rtol=1e-3, atol=1e-5 * scale, err_msg=n)
+    mine = {n: p.grad.detach().cpu().numpy().copy() for n, p in m.named_parameters()}
+    opt.step()
+    lr = c["learning_rate"]
+    for n, p in m.named_parameters():
+        got, want = p.detach().cpu().numpy(), z["step0_param." + n]
+        # Adam's first step is exactly -lr * g / (|g| + eps): the update differs from the
+        # reference's by at most lr * |s(g_mine) - s(g_ref)| (plus rounding), which is large
+        # only where |g| is within rounding noise of 0
+        gr = z.get("step0_grad." + n, np.zeros_like(want))
+        sgn = lambda g: g / (np.abs(g) + 1e-8)  # noqa: E731
+        bound = lr * np.abs(sgn(mine[n]) - sgn(gr)) + 2e-6
+        assert np.all(np.abs(got - want) <= bound), n
+
+
+def test_smore_one_epoch_with_mirror_gradient(tmp_path, golden):
+    from rsx.trainer import Trainer
+
+    z, c, train, valid, test = _setup(tmp_path, golden)
+    m = _model(c, train)
+    t = Trainer(c, m)
+    assert not t.fused and m.mg_enable
+    m.pre_epoch_processing()
+    loss, _ = t._train_epoch(train, 0)
+    assert abs(loss - float(z["epoch_losses"][0])) <= 1e-4 * abs(float(z["epoch_losses"][0]))
+    for n, p in m.named_parameters():
+        np.testing.assert_allclose(p.detach().cpu().numpy(), z["epoch0_param." + n], rtol=0, atol=1e-4, err_msg=n)
+    vres = t.evaluate(valid)
+    tres = t.evaluate(test)
+    for res, tag in ((vres, "epoch0_valid"), (tres, "epoch0_test")):
+        ref = metric_dict(z, tag)
+        for k in ref:
+            assert abs(res[k] - ref[k]) <= 1e-4 + 1e-12, (tag, k, res[k], ref[k])
