@@ -21,8 +21,10 @@
 // and keeps the top K, which also raises the threshold.  Items arrive in
 // ascending index order within a chunk, so the strict "> threshold" filter drops
 // nothing that the canonical order would keep.
-// Kernel 2 (fs_merge): 16 lanes per user merge the chunks' sorted top-K lists.
+// Kernel 2 (fs_select): one wavefront per user (full occupancy) takes the exact
+// top-K over every chunk's raw candidates and rank-sorts it.
 #include <climits>
+#include <cstdlib>
 
 #include "rsx_common.hpp"
 
@@ -100,9 +102,11 @@ struct FsArgs {
     int k;
     int n_chunks;
     int64_t chunk_items;
-    u64* cand;  // [nb][n_chunks][k]
+    u64* cand;    // [nb][n_chunks][kCap] raw candidate keys
+    int* ccount;  // [nb][n_chunks]
     float* out_val;
     int64_t* out_idx;
+    int mode;  // profiling ablation (RSX_FS_MODE): 0 full, 1 scores only, 2 no compaction, 3 no final emit
 };
 
 constexpr int kStride = kCap + 1;  // u64 slots per user row in LDS (+1: spreads the 32 users over banks)
@@ -110,41 +114,41 @@ constexpr int kStride = kCap + 1;  // u64 slots per user row in LDS (+1: spreads
 __device__ __forceinline__ int popc64(u64 x) { return __popcll(x); }
 __device__ __forceinline__ u64 lanemask_lt(int lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
 
-// Exact k-th largest of the (unique, nonzero) keys e0/e1 held by the wave, by a
-// bitwise binary search with ballots: 32 steps on the score half, and 32 more on
-// the index half only when scores tie at the boundary.  Zero keys are padding.
-__device__ __forceinline__ u64 kth_largest(u64 e0, u64 e1, int k) {
-    const unsigned h0 = (unsigned)(e0 >> 32), h1 = (unsigned)(e1 >> 32);
-    unsigned th = 0;
+// Shrink one user's buffer (k < n <= kCap unique nonzero keys) to exactly its top k,
+// compacted to the front, and return the k-th key's score (the new threshold).
+// Each lane ranks its two keys against every buffered key, read back as LDS
+// broadcasts (same address in all lanes): n/2 rounds of independent 64-bit compares,
+// no ballot/scalar dependency chain.  Keys are unique, so ranks are exact.
+__device__ __forceinline__ float compact_slot(u64* buf, int n, int k, int lane, int* new_cnt) {
+    const u64 e0 = lane < n ? buf[lane] : ~0ull;  // ~0: never kept, never counted
+    const u64 e1 = lane + 64 < n ? buf[lane + 64] : ~0ull;
+    int r0 = 0, r1 = 0;
+    int i = 0;
 #pragma unroll 4
-    for (int bit = 31; bit >= 0; --bit) {
-        const unsigned c = th | (1u << bit);
-        const int n = popc64(__ballot(h0 >= c)) + popc64(__ballot(h1 >= c));
-        if (n >= k) th = c;
+    for (; i + 1 < n; i += 2) {
+        const u64 x = buf[i], y = buf[i + 1];
+        r0 += (int)(x > e0) + (int)(y > e0);
+        r1 += (int)(x > e1) + (int)(y > e1);
     }
-    // th = largest score-word with at least k keys >= it
-    const int gt = popc64(__ballot(h0 > th)) + popc64(__ballot(h1 > th));
-    const int need = k - gt;  // how many of the keys with score-word == th are kept
-    const int eq = popc64(__ballot(h0 == th)) + popc64(__ballot(h1 == th));
-    if (eq == need) return ((u64)th << 32);  // every tie kept: threshold = lowest key of the tie group
-    const unsigned l0 = (unsigned)e0, l1 = (unsigned)e1;
-    unsigned tl = 0;
-    for (int bit = 31; bit >= 0; --bit) {
-        const unsigned c = tl | (1u << bit);
-        const int n = popc64(__ballot(h0 == th && l0 >= c)) + popc64(__ballot(h1 == th && l1 >= c));
-        if (n >= need) tl = c;
+    if (i < n) {
+        const u64 x = buf[i];
+        r0 += (int)(x > e0);
+        r1 += (int)(x > e1);
     }
-    return ((u64)th << 32) | tl;
-}
-
-// Keep the k largest keys of one user's buffer (n > k entries), compacted to the
-// front; returns the new score threshold.  Whole wave, no sort.
-__device__ __forceinline__ float compact_slot(u64* buf, int n, int k, int lane) {
-    const u64 e0 = lane < n ? buf[lane] : 0ull;
-    const u64 e1 = lane + 64 < n ? buf[lane + 64] : 0ull;
-    const u64 T = kth_largest(e0, e1, k);
-    const bool k0 = e0 != 0ull && e0 >= T;
-    const bool k1 = e1 != 0ull && e1 >= T;
+    const bool k0 = lane < n && r0 < k;
+    const bool k1 = lane + 64 < n && r1 < k;
+    // threshold = the key of rank k-1
+    const u64 w0 = __ballot(k0 && r0 == k - 1), w1 = __ballot(k1 && r1 == k - 1);
+    u64 T;
+    if (w0) {
+        const int src = __ffsll((long long)w0) - 1;
+        T = ((u64)__builtin_amdgcn_readlane((int)(e0 >> 32), src) << 32) |
+            (unsigned)__builtin_amdgcn_readlane((int)e0, src);
+    } else {
+        const int src = __ffsll((long long)w1) - 1;
+        T = ((u64)__builtin_amdgcn_readlane((int)(e1 >> 32), src) << 32) |
+            (unsigned)__builtin_amdgcn_readlane((int)e1, src);
+    }
     const u64 b0 = __ballot(k0), b1 = __ballot(k1);
     const u64 lt = lanemask_lt(lane);
     const int p0 = popc64(b0 & lt);
@@ -153,65 +157,52 @@ __device__ __forceinline__ float compact_slot(u64* buf, int n, int k, int lane) 
     if (k0) buf[p0] = e0;
     if (k1) buf[p1] = e1;
     __builtin_amdgcn_wave_barrier();
+    *new_cnt = popc64(b0) + popc64(b1);
     return key_score(T);
 }
 
-// Write the top-min(n,k) keys of one user's buffer to dst[0..k) in descending
-// order (rank by counting: every lane compares its key with all others via
-// readlane; no LDS round trips), zero-padded.  n <= kCap.
-__device__ __forceinline__ void emit_sorted(const u64* buf, int n, int k, int lane, u64* dst) {
-    u64 e0 = lane < n ? buf[lane] : 0ull;
-    u64 e1 = lane + 64 < n ? buf[lane + 64] : 0ull;
-    if (n > k) {
-        const u64 T = kth_largest(e0, e1, k);
-        if (e0 < T) e0 = 0ull;
-        if (e1 < T) e1 = 0ull;
+// One wavefront per block, no barriers: the wave owns 32 users and walks its item
+// chunk in 32-item tiles.  A operands (item rows) come straight from L2 into a
+// double-buffered register set (lane l: item l&31, floats [h*D/2 + 32c, +32)),
+// prefetched one 32-float chunk ahead of the MFMAs that consume the current one.
+// Waves never wait on each other, so one wave's candidate compaction overlaps the
+// other waves' MFMA streams.
+template <int D, int CW>
+__device__ __forceinline__ void load_chunk(float (&r)[CW], const float* I, int64_t item, int64_t i1, int off) {
+    if (item < i1) {
+        const float* p = I + item * D + off;
+#pragma unroll
+        for (int q = 0; q < CW / 4; ++q) {
+            const float4 v = ld4(p + 4 * q);
+            r[4 * q] = v.x;
+            r[4 * q + 1] = v.y;
+            r[4 * q + 2] = v.z;
+            r[4 * q + 3] = v.w;
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < CW; ++q) r[q] = 0.f;
     }
-    int r0 = 0, r1 = 0;
-    const int m = n < 64 ? n : 64;
-    for (int t = 0; t < m; ++t) {
-        const unsigned lo = __builtin_amdgcn_readlane((unsigned)(e0 & 0xffffffffu), t);
-        const unsigned hi = __builtin_amdgcn_readlane((unsigned)(e0 >> 32), t);
-        const u64 x = ((u64)hi << 32) | lo;
-        r0 += x > e0;
-        r1 += x > e1;
-    }
-    for (int t = 0; t < n - 64; ++t) {
-        const unsigned lo = __builtin_amdgcn_readlane((unsigned)(e1 & 0xffffffffu), t);
-        const unsigned hi = __builtin_amdgcn_readlane((unsigned)(e1 >> 32), t);
-        const u64 x = ((u64)hi << 32) | lo;
-        r0 += x > e0;
-        r1 += x > e1;
-    }
-    if (e0 != 0ull && r0 < k) dst[r0] = e0;
-    if (e1 != 0ull && r1 < k) dst[r1] = e1;
-    const int kept = n < k ? n : k;
-    for (int e = kept + lane; e < k; e += 64) dst[e] = 0ull;
 }
 
-template <int D, int NW>
-__global__ __launch_bounds__(64 * NW) void fs_tiles(FsArgs a) {
-    constexpr int LD = D + 4;
+template <int D>
+__global__ __launch_bounds__(64) void fs_tiles(FsArgs a) {
     constexpr int HALF = D / 2;
-    constexpr int PER = (32 * D / 4) / (64 * NW);  // float4 loads per thread per tile
-    static_assert(PER >= 1, "tile too small for block");
+    constexpr int CW = HALF < 32 ? HALF : 32;  // floats per operand chunk
+    constexpr int NCH = HALF / CW;             // chunks per lane-half row
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    float* tiles = reinterpret_cast<float*>(smem);                           // [2][32][LD]
-    u64* cbuf = reinterpret_cast<u64*>(smem + 2 * 32 * LD * sizeof(float));  // [NW*32][kStride]
+    u64* cbuf = reinterpret_cast<u64*>(smem);  // [32][kStride]
 
-    const int tid = threadIdx.x;
-    const int wv = tid >> 6, lane = tid & 63, j = lane & 31, h = lane >> 5;
-    const int slot = wv * 32 + j;
-    const int64_t bslot = (int64_t)blockIdx.x * (32 * NW) + slot;
+    const int lane = threadIdx.x, j = lane & 31, h = lane >> 5;
+    const int64_t bslot = (int64_t)blockIdx.x * 32 + j;
     const bool uvalid = bslot < a.nb;
     const int64_t urow = uvalid ? (a.users ? a.users[bslot] : bslot) : 0;
     const int chunk = blockIdx.y;
     const int64_t i0 = (int64_t)chunk * a.chunk_items;
     const int64_t i1 = min(a.ni, i0 + a.chunk_items);
     const int ntiles = (int)((i1 - i0 + 31) / 32);
-    u64* mybuf = cbuf + slot * kStride;
+    u64* mybuf = cbuf + j * kStride;
 
-    // user fragment: B[k][j] for k in this lane-half's contiguous half of the row
     float bu[HALF];
     {
         const float* ur = a.U + urow * D + h * HALF;
@@ -224,7 +215,6 @@ __global__ __launch_bounds__(64 * NW) void fs_tiles(FsArgs a) {
             bu[s + 3] = v.w;
         }
     }
-    // mask cursor: first training item >= i0 (columns sorted)
     int64_t mp = 0, me = 0;
     int64_t next_mask = LLONG_MAX;
     if (uvalid && a.mrp) {
@@ -237,61 +227,48 @@ __global__ __launch_bounds__(64 * NW) void fs_tiles(FsArgs a) {
         mp = lo;
         next_mask = mp < me ? (int64_t)a.mcol[mp] : LLONG_MAX;
     }
-    int cnt = 0;  // candidates of user j (same value in lanes j and j+32)
+    int cnt = 0;
     float tau = -INFINITY;
 
-    float4 pre[PER];
-    auto load_tile = [&](int t) {
-        const int64_t base = i0 + (int64_t)t * 32;
+    float ra[CW], rb[CW];
+    const int64_t nsteps = (int64_t)ntiles * NCH;
+    if (nsteps > 0) load_chunk<D, CW>(ra, a.I, i0 + j, i1, h * HALF);
+    floatx16 acc;
+    int64_t step = 0;
+    unsigned long long tm_mask = 0, tm_ins = 0, tm_cmp = 0, tm_mfma = 0;  // mode 4 cycle profile
+    // process one chunk step with operands `cur`, prefetching the next into `nxt`
+    auto do_step = [&](float (&cur)[CW], float (&nxt)[CW]) {
+        const int t = (int)(step / NCH), c = (int)(step % NCH);
+        const unsigned long long c0 = a.mode == 4 ? clock64() : 0;
+        if (c == 0) {
 #pragma unroll
-        for (int q = 0; q < PER; ++q) {
-            const int f = tid + q * 64 * NW;  // float4 index within the tile
-            const int r = f / (D / 4), c4 = f % (D / 4);
-            const int64_t item = base + r;
-            pre[q] = item < i1 ? ld4(a.I + item * D + c4 * 4) : f4(0.f);
+            for (int r = 0; r < 16; ++r) acc[r] = 0.f;
         }
-    };
-    auto store_tile = [&](int buf) {
-        float* tb = tiles + buf * 32 * LD;
-#pragma unroll
-        for (int q = 0; q < PER; ++q) {
-            const int f = tid + q * 64 * NW;
-            const int r = f / (D / 4), c4 = f % (D / 4);
-            st4(tb + r * LD + c4 * 4, pre[q]);
+        if (step + 1 < nsteps) {
+            const int64_t s1 = step + 1;
+            const int t1 = (int)(s1 / NCH), c1 = (int)(s1 % NCH);
+            load_chunk<D, CW>(nxt, a.I, i0 + (int64_t)t1 * 32 + j, i1, h * HALF + CW * c1);
         }
-    };
-    if (ntiles > 0) {
-        load_tile(0);
-        store_tile(0);
-    }
-    __syncthreads();
-
-    for (int t = 0; t < ntiles; ++t) {
-        const int buf = t & 1;
-        if (t + 1 < ntiles) load_tile(t + 1);
-        // 32x32 score tile
-        floatx16 acc;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-        const float* ar = tiles + buf * 32 * LD + j * LD + h * HALF;
-#pragma unroll
-        for (int s = 0; s < HALF; s += 4) {
-            const float4 av = ld4(ar + s);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.x, bu[s], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.y, bu[s + 1], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.z, bu[s + 2], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.w, bu[s + 3], acc, 0, 0, 0);
-        }
-        if (t + 1 < ntiles) store_tile(buf ^ 1);
-        // masked items of this tile for user j
+        for (int q = 0; q < CW; ++q) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[q], bu[CW * c + q], acc, 0, 0, 0);
+        ++step;
+        if (c != NCH - 1) return;
+        // ---- tile t complete: filter, insert, compact ----
         const int64_t tb = i0 + (int64_t)t * 32;
+        if (a.mode == 1) {
+            float sink = 0.f;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) sink += acc[r];
+            if (sink == 1234.5f) a.out_val[0] = sink;  // keep the MFMAs live
+            return;
+        }
+        const unsigned long long c1 = a.mode == 4 ? clock64() : 0;
         unsigned mbits = 0;
         while (next_mask < tb + 32) {
             mbits |= 1u << (unsigned)(next_mask - tb);
             ++mp;
             next_mask = mp < me ? (int64_t)a.mcol[mp] : LLONG_MAX;
         }
-        // which of my 16 scores pass the threshold
         unsigned m = 0;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -299,8 +276,10 @@ __global__ __launch_bounds__(64 * NW) void fs_tiles(FsArgs a) {
             const float sc = ((mbits >> ii) & 1u) ? -1e10f : acc[r];
             if (uvalid && tb + ii < i1 && sc > tau) m |= 1u << r;
         }
+        if (a.mode == 2 && cnt > kCap - 32) m = 0;
+        const unsigned long long c2 = a.mode == 4 ? clock64() : 0;
         if (__ballot(m != 0u)) {
-            const unsigned pm = (unsigned)__shfl_xor((int)m, 32, kWave);  // partner half's mask
+            const unsigned pm = (unsigned)__shfl_xor((int)m, 32, kWave);
             int pos = cnt + (h ? __popc(pm) : 0);
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
@@ -312,66 +291,155 @@ __global__ __launch_bounds__(64 * NW) void fs_tiles(FsArgs a) {
             }
             cnt += __popc(m) + __popc(pm);
         }
-        // keep room for the next tile (at most 32 new candidates per user)
-        u64 need = __ballot(h == 0 && cnt > kCap - 32);
+        const unsigned long long c3 = a.mode == 4 ? clock64() : 0;
+        u64 need = a.mode == 2 ? 0ull : __ballot(h == 0 && cnt > kCap - 32);
         if (need) {
             __builtin_amdgcn_wave_barrier();
             while (need) {
                 const int jj = __ffsll((long long)need) - 1;
                 need &= need - 1;
                 const int n = __builtin_amdgcn_readlane(cnt, jj);
-                const float nt = compact_slot(cbuf + (wv * 32 + jj) * kStride, n, a.k, lane);
+                int kept;
+                const float nt = compact_slot(cbuf + jj * kStride, n, a.k, lane, &kept);
+                if (a.mode == 4 && lane == 0) atomicAdd((unsigned long long*)a.out_idx, 1ull);
                 if (j == jj) {
                     tau = nt;
-                    cnt = a.k;
+                    cnt = kept;
                 }
             }
         }
-        __syncthreads();
+        if (a.mode == 4) {
+            const unsigned long long c4 = clock64();
+            tm_mfma += c1 - c0;
+            tm_mask += c2 - c1;
+            tm_ins += c3 - c2;
+            tm_cmp += c4 - c3;
+        }
+    };
+    while (step < nsteps) {
+        do_step(ra, rb);
+        if (step < nsteps) do_step(rb, ra);
     }
-    // final: this chunk's top-k of every user, sorted, to the workspace
+    if (a.mode == 4 && lane == 0) {
+        unsigned long long* dbg = (unsigned long long*)a.out_idx;
+        atomicAdd(dbg + 1, (unsigned long long)ntiles);
+        atomicAdd(dbg + 3, tm_mfma);
+        atomicAdd(dbg + 4, tm_mask);
+        atomicAdd(dbg + 5, tm_ins);
+        atomicAdd(dbg + 6, tm_cmp);
+    }
+    if (a.mode != 0 && a.mode != 4) return;
+    if (a.mode == 4) return;
     __builtin_amdgcn_wave_barrier();
     for (int jj = 0; jj < 32; ++jj) {
-        const int64_t b2 = (int64_t)blockIdx.x * (32 * NW) + wv * 32 + jj;
+        const int64_t b2 = (int64_t)blockIdx.x * 32 + jj;
         if (b2 >= a.nb) break;  // wave-uniform
         const int n = __builtin_amdgcn_readlane(cnt, jj);
-        emit_sorted(cbuf + (wv * 32 + jj) * kStride, n, a.k, lane, a.cand + ((b2 * a.n_chunks) + chunk) * a.k);
+        const u64* src = cbuf + jj * kStride;
+        u64* dst = a.cand + (b2 * a.n_chunks + chunk) * kCap;
+        for (int e = lane; e < n; e += 64) dst[e] = src[e];
+        if (lane == 0) a.ccount[b2 * a.n_chunks + chunk] = n;
     }
 }
 
-// 16 lanes per user: k-way merge of n_chunks sorted lists (n_chunks <= 16).
-__global__ __launch_bounds__(256) void fs_merge(FsArgs a) {
-    const int li = threadIdx.x & 15;
-    const int64_t b = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);
-    if (b >= a.nb) return;
-    const u64* src = a.cand + b * a.n_chunks * a.k + (int64_t)li * a.k;
-    const bool has = li < a.n_chunks;
-    int ptr = 0;
-    u64 head = has ? src[0] : 0ull;
-    for (int o = 0; o < a.k; ++o) {
-        u64 m = head;
+// Exact k-th largest of the nonzero keys held E per lane (radix search with ballots,
+// score word first, index word only for a tie at the boundary).
+template <int E>
+__device__ __forceinline__ u64 kth_largest_n(const u64 (&e)[E], int k) {
+    unsigned th = 0;
+    for (int bit = 31; bit >= 0; --bit) {
+        const unsigned c = th | (1u << bit);
+        int n = 0;
 #pragma unroll
-        for (int s = 8; s > 0; s >>= 1) {
-            const u64 pv = shfl_xor_u64(m, s);
-            m = m > pv ? m : pv;
-        }
-        if (has && head == m && m != 0ull) {
-            ++ptr;
-            head = ptr < a.k ? src[ptr] : 0ull;
-        }
-        if (li == 0) {
-            a.out_val[b * a.k + o] = m ? key_score(m) : -INFINITY;
-            a.out_idx[b * a.k + o] = m ? (int64_t)key_index(m) : -1;
-        }
+        for (int m = 0; m < E; ++m) n += popc64(__ballot((unsigned)(e[m] >> 32) >= c));
+        if (n >= k) th = c;
+    }
+    int gt = 0, eq = 0;
+#pragma unroll
+    for (int m = 0; m < E; ++m) {
+        const unsigned h = (unsigned)(e[m] >> 32);
+        gt += popc64(__ballot(h > th));
+        eq += popc64(__ballot(h == th && e[m] != 0ull));
+    }
+    const int need = k - gt;
+    if (eq == need) return (u64)th << 32;
+    unsigned tl = 0;
+    for (int bit = 31; bit >= 0; --bit) {
+        const unsigned c = tl | (1u << bit);
+        int n = 0;
+#pragma unroll
+        for (int m = 0; m < E; ++m)
+            n += popc64(__ballot((unsigned)(e[m] >> 32) == th && (unsigned)e[m] >= c));
+        if (n >= need) tl = c;
+    }
+    return ((u64)th << 32) | tl;
+}
+
+// One wavefront per user: the exact top-k over every chunk's raw candidates,
+// ordered by (score desc, index asc).  S = chunks per user (<= SMAX); every list
+// holds <= kCap = 128 keys, i.e. <= 2 per lane.
+template <int SMAX>
+__global__ __launch_bounds__(256) void fs_select(FsArgs a) {
+    constexpr int E = 2 * SMAX;
+    __shared__ u64 top[4][kCap];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t b = (int64_t)blockIdx.x * 4 + wv;
+    if (b >= a.nb) return;  // wave-uniform
+    u64 e[E];
+#pragma unroll
+    for (int c = 0; c < SMAX; ++c) {
+        const bool in = c < a.n_chunks;
+        const int n = in ? a.ccount[b * a.n_chunks + c] : 0;
+        const u64* src = a.cand + (b * a.n_chunks + c) * kCap;
+        e[2 * c] = lane < n ? src[lane] : 0ull;
+        e[2 * c + 1] = lane + 64 < n ? src[lane + 64] : 0ull;
+    }
+    int total = 0;
+#pragma unroll
+    for (int m = 0; m < E; ++m) total += popc64(__ballot(e[m] != 0ull));
+    const int k = a.k;
+    const u64 T = total > k ? kth_largest_n<E>(e, k) : 1ull;
+    // gather the winners (exactly min(k, total)) into LDS
+    const u64 lt = lanemask_lt(lane);
+    int base = 0;
+#pragma unroll
+    for (int m = 0; m < E; ++m) {
+        const bool kp = e[m] != 0ull && e[m] >= T;
+        const u64 bal = __ballot(kp);
+        if (kp) top[wv][base + popc64(bal & lt)] = e[m];
+        base += popc64(bal);
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    // rank-sort the winners (keys unique): position = number of larger keys
+    const int kept = base;
+    for (int q = lane; q < kept; q += 64) {
+        const u64 mine = top[wv][q];
+        int r = 0;
+        for (int t = 0; t < kept; ++t) r += top[wv][t] > mine;
+        a.out_val[b * k + r] = key_score(mine);
+        a.out_idx[b * k + r] = (int64_t)key_index(mine);
+    }
+    for (int q = kept + lane; q < k; q += 64) {
+        a.out_val[b * k + q] = -INFINITY;
+        a.out_idx[b * k + q] = -1;
     }
 }
 
 static void fs_plan(int64_t nb, int64_t ni, int d, int* nw, int* n_chunks, int64_t* chunk_items) {
-    *nw = d <= 64 ? 4 : 2;
-    const int64_t ublocks = (nb + 32 * (*nw) - 1) / (32 * (*nw));
-    int64_t s = (256 + ublocks - 1) / ublocks;  // about one block per CU
+    (void)d;
+    *nw = 1;
+    const int64_t waves = (nb + 31) / 32;
+    // item chunks per 32-user wave: just enough waves to cover the 1024 SIMDs (one
+    // wave per SIMD: the candidate buffers take the LDS).  Every extra chunk re-pays
+    // the threshold warm-up (measured: 1 chunk beats 2-4 at 1.1k waves), so no more.
+    int64_t s = (922 + waves - 1) / waves;
     if (s < 1) s = 1;
     if (s > 16) s = 16;
+    if (const char* f = getenv("RSX_FS_CHUNKS")) {  // tuning override
+        const int v = atoi(f);
+        if (v >= 1 && v <= 16) s = v;
+    }
     int64_t per = (ni + s - 1) / s;
     per = (per + 31) / 32 * 32;
     if (per < 32) per = 32;
@@ -383,21 +451,22 @@ size_t fs_ws(int64_t nb, int64_t ni, int k, int d) {
     int nw, nc;
     int64_t per;
     fs_plan(nb, ni, d, &nw, &nc, &per);
-    return (size_t)nb * nc * k * sizeof(u64) + 256;
+    return (size_t)nb * nc * kCap * sizeof(u64) + (size_t)nb * nc * sizeof(int) + 512;
 }
 
-template <int D, int NW>
+template <int D>
 static int launch_fs(FsArgs& a, hipStream_t s) {
-    const size_t lds = 2 * 32 * (D + 4) * sizeof(float) + NW * 32 * kStride * sizeof(u64);
-    const int64_t ublocks = (a.nb + 32 * NW - 1) / (32 * NW);
-    static bool attr_set = false;
-    if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)fs_tiles<D, NW>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        attr_set = true;
+    const size_t lds = 32 * kStride * sizeof(u64);
+    const int64_t waves = (a.nb + 31) / 32;
+    hipLaunchKernelGGL((fs_tiles<D>), dim3((unsigned)waves, (unsigned)a.n_chunks), dim3(64), lds, s, a);
+    const dim3 sg((unsigned)((a.nb + 3) / 4));
+    if (a.mode == 0) {
+        if (a.n_chunks <= 1) hipLaunchKernelGGL(fs_select<1>, sg, dim3(256), 0, s, a);
+        else if (a.n_chunks <= 2) hipLaunchKernelGGL(fs_select<2>, sg, dim3(256), 0, s, a);
+        else if (a.n_chunks <= 4) hipLaunchKernelGGL(fs_select<4>, sg, dim3(256), 0, s, a);
+        else if (a.n_chunks <= 8) hipLaunchKernelGGL(fs_select<8>, sg, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL(fs_select<16>, sg, dim3(256), 0, s, a);
     }
-    hipLaunchKernelGGL((fs_tiles<D, NW>), dim3((unsigned)ublocks, (unsigned)a.n_chunks), dim3(64 * NW), lds, s,
-                       a);
-    hipLaunchKernelGGL(fs_merge, dim3((unsigned)((a.nb + 15) / 16)), dim3(256), 0, s, a);
     return last_rc();
 }
 
@@ -421,13 +490,22 @@ int fs_call(const float* U, const int64_t* users, int64_t nb, const float* I, in
     a.mcol = mcol;
     a.k = k;
     a.cand = static_cast<u64*>(ws);
+    a.ccount = reinterpret_cast<int*>(static_cast<char*>(ws) + (size_t)nb * a.n_chunks * kCap * sizeof(u64));
     a.out_val = out_val;
     a.out_idx = out_idx;
+    {
+        static int mode = -1;
+        if (mode < 0) {
+            const char* e = getenv("RSX_FS_MODE");
+            mode = e ? atoi(e) : 0;
+        }
+        a.mode = mode;
+    }
     switch (d) {
-        case 32: return launch_fs<32, 4>(a, s);
-        case 64: return launch_fs<64, 4>(a, s);
-        case 128: return launch_fs<128, 2>(a, s);
-        case 256: return launch_fs<256, 2>(a, s);
+        case 32: return launch_fs<32>(a, s);
+        case 64: return launch_fs<64>(a, s);
+        case 128: return launch_fs<128>(a, s);
+        case 256: return launch_fs<256>(a, s);
         default: return RSX_ERR_UNSUPPORTED;
     }
 }

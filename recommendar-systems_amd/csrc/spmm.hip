@@ -139,6 +139,33 @@ __device__ __forceinline__ void epilogue(const rsx_epilogue& e, int64_t row, flo
 constexpr int kBlock = 256;
 constexpr int kUnroll = 8;
 
+// d = 64 helper: broadcast (col, val) entries 8H..8H+7 of the 16-lane row with
+// row_newbcast and accumulate their neighbour rows (entries >= n are skipped).
+template <int T>
+__device__ __forceinline__ int row_bcast(int x) {
+    return __builtin_amdgcn_update_dpp(0, x, 0x150 + T, 0xf, 0xf, false);
+}
+template <int H>
+__device__ __forceinline__ float4 gather8(float4 acc, int cm, float vm, int n, const float* xl) {
+    const int vi = __float_as_int(vm);
+    int c[8];
+    float v[8];
+    c[0] = row_bcast<8 * H + 0>(cm); v[0] = __int_as_float(row_bcast<8 * H + 0>(vi));
+    c[1] = row_bcast<8 * H + 1>(cm); v[1] = __int_as_float(row_bcast<8 * H + 1>(vi));
+    c[2] = row_bcast<8 * H + 2>(cm); v[2] = __int_as_float(row_bcast<8 * H + 2>(vi));
+    c[3] = row_bcast<8 * H + 3>(cm); v[3] = __int_as_float(row_bcast<8 * H + 3>(vi));
+    c[4] = row_bcast<8 * H + 4>(cm); v[4] = __int_as_float(row_bcast<8 * H + 4>(vi));
+    c[5] = row_bcast<8 * H + 5>(cm); v[5] = __int_as_float(row_bcast<8 * H + 5>(vi));
+    c[6] = row_bcast<8 * H + 6>(cm); v[6] = __int_as_float(row_bcast<8 * H + 6>(vi));
+    c[7] = row_bcast<8 * H + 7>(cm); v[7] = __int_as_float(row_bcast<8 * H + 7>(vi));
+    float4 xv[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) xv[t] = (8 * H + t < n) ? ld4(xl + (int64_t)c[t] * 64) : f4(0.f);
+#pragma unroll
+    for (int t = 0; t < 8; ++t) acc = fma4(v[t], xv[t], acc);
+    return acc;
+}
+
 // One group of G lanes per work item {row, slot, begin, end}.
 template <int D, int KIND>
 __global__ __launch_bounds__(kBlock) void spmm_main(rsx_csr a, const float* __restrict__ x,
@@ -155,6 +182,20 @@ __global__ __launch_bounds__(kBlock) void spmm_main(rsx_csr a, const float* __re
     float4 acc = f4(0.f);
     int j = wk.z;
     const int end = wk.w;
+    if constexpr (G == 16) {
+        // d = 64: a group is exactly one 16-lane DPP row.  Lane li loads the
+        // (col, val) of nonzero j+li (one coalesced load per 16 nonzeros) and
+        // row_newbcast:t hands entry t to the whole row in one VALU op, so the
+        // memory pipe only sees the neighbour-row gathers.
+        for (; j < end; j += 16) {
+            const bool mine = j + li < end;
+            const int cm = mine ? col[j + li] : 0;
+            const float vm = mine ? val[j + li] : 0.f;
+            const int n = end - j;
+            acc = gather8<0>(acc, cm, vm, n, xl);
+            if (n > 8) acc = gather8<1>(acc, cm, vm, n, xl);
+        }
+    } else {
     for (; j + kUnroll <= end; j += kUnroll) {
         int c[kUnroll];
         float v[kUnroll];
@@ -184,6 +225,7 @@ __global__ __launch_bounds__(kBlock) void spmm_main(rsx_csr a, const float* __re
 #pragma unroll
         for (int t = 0; t < kUnroll; ++t)
             if (j + t < end) acc = fma4(v[t], xv[t], acc);
+    }
     }
     if (wk.y < 0) {
         epilogue<KIND, D>(e, wk.x, acc, li);

@@ -286,13 +286,16 @@ class Trainer:
         k = max(self.config["topk"])
         mats = []
         fused = hasattr(self.model, "full_sort_topk") and hasattr(eval_data, "mask_rowptr")
-        for batch in eval_data:
-            if fused:
-                _, topk = self.model.full_sort_topk(batch, k, eval_data)
-            else:
+        if fused:
+            # one fused launch over every evaluation user: the score matrix is never
+            # materialised, so the reference's eval_batch_size memory bound does not apply
+            _, topk = self.model.full_sort_topk([eval_data.eval_u, None], k, eval_data)
+            mats.append(topk)
+        else:
+            for batch in eval_data:
                 scores = self.model.full_sort_predict(batch)
                 m = batch[1]
                 scores[m[0], m[1]] = -1e10
                 _, topk = torch.topk(scores, k, dim=-1)
-            mats.append(topk)
+                mats.append(topk)
         return self.evaluator.evaluate(mats, eval_data, is_test=is_test, idx=idx)

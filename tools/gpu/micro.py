@@ -1,0 +1,72 @@
+"""Kernel microbenchmarks on the sports-shaped graph (one process; interleaved reps).
+Usage: python tools/gpu/micro.py [spmm|fullsort|all]"""
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "..", "..", "recommendar-systems_amd"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from rsx import graph, ops, synth  # noqa: E402
+
+
+def t_ms(fn, reps=50):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps
+
+
+def main(what):
+    dev = torch.device("cuda:0")
+    nu, ni, ne = synth.SHAPES["sports"]
+    df = synth.amazon_like(nu, ni, ne, seed=0)
+    tr = df[df.x_label == 0]
+    tu, ti = tr.userID.values.astype(np.int64), tr.itemID.values.astype(np.int64)
+    rp, col, val = graph.lightgcn_norm_adj(tu, ti, nu, ni)
+    n = nu + ni
+    out = {}
+    if what in ("spmm", "all"):
+        for chunk in (16, 32, 64):
+            A = ops.DeviceCSR(rp, col, val, n, dev, chunk)
+            x = torch.randn(n, 64, device=dev)
+            y = torch.empty_like(x)
+            out[f"spmm_store_chunk{chunk}_ms"] = t_ms(lambda: A.spmm(x, out=y))
+            out[f"chunk{chunk}_nlong"] = A.n_long
+    if what in ("fullsort", "all"):
+        f = torch.randn(n, 64, device=dev) * 0.1
+        U, I = f[:nu], f[nu:]
+        hr, hc = graph.history_csr(tu, ti, nu)
+        hr, hc = torch.from_numpy(hr).to(dev), torch.from_numpy(hc).to(dev)
+        users = torch.arange(nu, device=dev)
+        if os.environ.get("RSX_FS_MODE") == "4":
+            v, idx = ops.fullsort_topk(U, users, I, hr, hc, 50)
+            idx.zero_()
+            import ctypes as C
+            from rsx import _lib as L
+            lib = L.lib()
+            ws = ops._ws(dev, lib.rsx_fullsort_ws_bytes(nu, ni, 50))
+            L.check(lib.rsx_fullsort_topk(ops._p(U), ops._p(users), nu, ops._p(I), ni, 64, ops._p(hr), ops._p(hc), 50,
+                                          ops._p(v), ops._p(idx), ops._p(ws), ws.numel(), ops._stream()), "fs")
+            torch.cuda.synchronize()
+            cts = [int(x) for x in idx.view(-1)[:7].cpu()]
+            out["compactions"], out["wave_tiles"], out["fallbacks"] = cts[:3]
+            out["compactions_per_user"] = out["compactions"] / nu
+            tot = sum(cts[3:7])
+            for name, x in zip(("cyc_mfma_issue", "cyc_mask", "cyc_insert", "cyc_compact"), cts[3:7]):
+                out[name] = round(x / tot, 3)
+            out["cycles_per_tile"] = tot / max(cts[1], 1)
+        out["fs_ms_all_users"] = t_ms(lambda: ops.fullsort_topk(U, users, I, hr, hc, 50), 10)
+        out["fs_tflops"] = 2 * 64 * ni * nu / (out["fs_ms_all_users"] * 1e-3) / 1e12
+    print(out, flush=True)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "all")
