@@ -84,24 +84,20 @@ def _declare(lib):
         "rsx_sample_epoch": (C.c_int, [P, P, I64, P, P, P, I64, C.c_uint64, I64, I64, P, P]),
         "rsx_lightgcn_step": (C.c_int, [C.POINTER(LgcnStep), P]),
         "rsx_lightgcn_forward": (C.c_int, [C.POINTER(Csr), I32, I32, P, P, P, P, P, P, P]),
+        "rsx_smore_spectral_fwd": (C.c_int, [P, I32, P, P, P, I32, P, P, P, P, P, I64, I32, P, P, P, P, P, P]),
+        "rsx_smore_spectral_bwd": (C.c_int, [P, P, P, P, P, P, P, P, I64, I32, P, P, P, P]),
+        "rsx_smore_spectral_bwd_partials": (C.c_size_t, [I64, I32]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    for name, (res, args) in _OPTIONAL.items():
-        if hasattr(lib, name):
-            fn = getattr(lib, name)
-            fn.restype = res
-            fn.argtypes = args
 
-
-# entry points added by later translation units (SMORE fused pass etc.)
-_OPTIONAL: dict = {}
 
 EXPORTED = ["rsx_version", "rsx_csr_schedule_host", "rsx_spmm", "rsx_rowwise", "rsx_bpr_ws_bytes", "rsx_bpr",
             "rsx_fullsort_ws_bytes", "rsx_fullsort_topk", "rsx_score_dense", "rsx_sample_triplets",
-            "rsx_gather_rows", "rsx_lightgcn_step", "rsx_lightgcn_forward", "rsx_sample_epoch"]
+            "rsx_gather_rows", "rsx_lightgcn_step", "rsx_lightgcn_forward", "rsx_sample_epoch",
+            "rsx_smore_spectral_fwd", "rsx_smore_spectral_bwd", "rsx_smore_spectral_bwd_partials"]
 
 
 def lib_path() -> str:

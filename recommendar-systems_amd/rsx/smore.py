@@ -233,9 +233,10 @@ class SMORE(GeneralRecommender):
         return cv, ct, cf
 
     def _projected_spectrum(self):
-        from .smore_spectral import spectral_available, spectral_fused
+        from .smore_spectral import spectral_fused, spectral_supported
 
-        if self.use_hip_spectral and spectral_available():
+        if (self.use_hip_spectral and self.v_feat is not None and self.t_feat is not None
+                and spectral_supported(self.embedding_dim, self.v_feat.shape[1], self.t_feat.shape[1])):
             return spectral_fused(self)
         img = self.image_trs(self.image_embedding.weight)
         txt = self.text_trs(self.text_embedding.weight)

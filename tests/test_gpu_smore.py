@@ -132,3 +132,32 @@ def test_smore_one_epoch_with_mirror_gradient(tmp_path, golden):
         ref = metric_dict(z, tag)
         for k in ref:
             assert abs(res[k] - ref[k]) <= 1e-4 + 1e-12, (tag, k, res[k], ref[k])
+
+
+@pytest.mark.parametrize("d,n,dv,dt", [(64, 1000, 512, 384), (128, 333, 768, 768), (64, 7, 48, 24)])
+def test_spectral_fused_vs_torch_autograd(cuda, d, n, dv, dt):
+    """rsx_smore_spectral_fwd/bwd against torch.nn.functional.linear + torch.fft (fp32, the
+    reference's ops) with autograd: outputs rtol 1e-4, every gradient within 1e-4 of its scale."""
+    from rsx.smore import spectrum_torch
+    from rsx.smore_spectral import spectral
+
+    g = torch.Generator(device="cpu").manual_seed(d + n)
+    mk = lambda *s: torch.randn(*s, generator=g).to(cuda).requires_grad_()  # noqa: E731
+    V, T = mk(n, dv), mk(n, dt)
+    Wv, Wt = (mk(d, dv) / dv ** 0.5).detach().requires_grad_(), (mk(d, dt) / dt ** 0.5).detach().requires_grad_()
+    bv, bt = mk(d), mk(d)
+    wv, wt, wf = mk(1, d // 2 + 1, 2), mk(1, d // 2 + 1, 2), mk(1, d // 2 + 1, 2)
+    leaves = [V, Wv, bv, T, Wt, bt, wv, wt, wf]
+    up = [torch.randn(n, d, generator=g).to(cuda) for _ in range(3)]
+
+    ref = spectrum_torch(torch.nn.functional.linear(V, Wv, bv), torch.nn.functional.linear(T, Wt, bt), wv, wt, wf)
+    ref_g = torch.autograd.grad(sum((r * u).sum() for r, u in zip(ref, up)), leaves)
+    got = spectral(V, Wv, bv, T, Wt, bt, wv, wt, wf)[:3]
+    got_g = torch.autograd.grad(sum((r * u).sum() for r, u in zip(got, up)), leaves)
+    for a, b in zip(got, ref):
+        np.testing.assert_allclose(a.detach().cpu().numpy(), b.detach().cpu().numpy(), rtol=1e-4,
+                                   atol=1e-5 * b.abs().max().item())
+    names = ["V", "Wv", "bv", "T", "Wt", "bt", "wv", "wt", "wf"]
+    for name, a, b in zip(names, got_g, ref_g):
+        scale = b.abs().max().item()
+        np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), rtol=1e-4, atol=1e-4 * scale, err_msg=name)
