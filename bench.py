@@ -87,8 +87,109 @@ def cpu_baseline(df_train, nu, ni, budget_s=12.0):
                       f"({el:.1f} s; Python sampler + torch.sparse.mm + autograd + Adam, oracle/rsx_oracle.py)"}
 
 
+WORKLOADS = {
+    "c1": dict(model="LayerGCN", dataset="baby", desc="C1: LayerGCN K=2 d=64, baby-shaped (19,445 users x 7,050 items), "
+                                                    "B=2048, device sampler, fused step (reference config: CPU)",
+               cfg=dict(n_layers=[2], reg_weight=[1e-2], dropout=[0.1])),
+    "c3": dict(model="SMORE", dataset="baby", desc="C3: SMORE d=64, baby-shaped, image 4096 / text 384 N(0,1) features, "
+                                                 "kNN 20/15, model-level mirror gradient, B=2048, device sampler",
+               cfg=dict(mg_verbose=False, diag_spectrum=False, diag_gate=False, diag_grad=False)),
+}
+
+
+def bench_model(args):
+    """C1 / C3 through the drop-in surface (Config -> RecDataset -> loaders -> model ->
+    Trainer): a step = one training batch exactly as Trainer runs it."""
+    import tempfile
+
+    from rsx import synth
+    from rsx.config import Config
+    from rsx.data import EvalDataLoader, RecDataset, TrainDataLoader
+    from rsx.trainer import Trainer
+    from rsx.utils import get_model, init_seed
+
+    w = WORKLOADS[args.workload]
+    root = tempfile.mkdtemp(prefix="rsx_bench_")
+    df = synth.shaped(w["dataset"], seed=0)
+    synth.write_inter(df, root, w["dataset"])
+    ni = int(df.itemID.max()) + 1
+    if w["model"] == "SMORE":
+        np.save(os.path.join(root, w["dataset"], "image_feat_raw.npy"), synth.features(ni, 4096, 1))
+        np.save(os.path.join(root, w["dataset"], "text_feat_raw.npy"), synth.features(ni, 384, 2))
+    cfg = dict(data_path=root + "/", train_batch_size=args.batch, rsx_sampler="device",
+               is_multimodal_model=w["model"] == "SMORE", **w["cfg"])
+    c = Config(w["model"], w["dataset"], cfg)
+    for k in c["hyper_parameters"]:
+        if isinstance(c[k], list):
+            c[k] = c[k][0]
+    init_seed(c["seed"])
+    ds = RecDataset(c)
+    tr, va, te = ds.split()
+    for x in (ds, tr, va, te):
+        str(x)
+    train = TrainDataLoader(c, tr, batch_size=args.batch, shuffle=True)
+    valid = EvalDataLoader(c, va, additional_dataset=tr, batch_size=c["eval_batch_size"])
+    train.pretrain_setup()
+    t_build = time.perf_counter()
+    model = get_model(w["model"])(c, train)
+    build_s = time.perf_counter() - t_build
+    t = Trainer(c, model)
+    model.train()
+
+    def batches():
+        while True:
+            model.pre_epoch_processing()
+            for b in train:
+                yield b
+
+    it = batches()
+    idx = {"i": 0}
+
+    def one_step():
+        b = next(it)
+        if t.fused:
+            model.fused_step(b, t.current_lr())
+        else:
+            t._train_batch(b, idx["i"], model.calculate_loss)
+        idx["i"] += 1
+        return b.shape[1]
+
+    for _ in range(args.warmup):
+        one_step()
+    torch.cuda.synchronize()
+    n = 0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        n += one_step()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    model.eval()
+    t.evaluate(valid)
+    torch.cuda.synchronize()
+    te0 = time.perf_counter()
+    t.evaluate(valid)
+    torch.cuda.synchronize()
+    eval_s = time.perf_counter() - te0
+    n_eval = int(len(valid.get_eval_users()))
+    out = {
+        "metric": METRIC, "value": n / wall, "unit": "interactions/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": wall * 1e3 / args.steps, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": f"synthetic Amazon-{w['dataset']}-shaped graph (rsx.synth seed 0)"
+                + ("; N(0,1) features" if w["model"] == "SMORE" else ""),
+        "config": {"workload": w["desc"], "model": w["model"], "global_batch": args.batch, "parallelism": "single",
+                   "fused_step": bool(t.fused)},
+        "fullsort_items_per_s": n_eval * ni / eval_s,
+        "fullsort": {"eval_users": n_eval, "n_items": ni, "s_per_eval_incl_forward_and_metrics": eval_s},
+        "model_build_s": build_s, "roofline": None, "cpu_baseline": None,
+    }
+    print(json.dumps(out), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="c2", choices=["c2", "c1", "c3"],
+                    help="c2 (default): the headline LightGCN sports config; c1/c3: LayerGCN / SMORE on baby")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
@@ -97,6 +198,10 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--eval-users", type=int, default=0, help="0 = all valid users")
     args = ap.parse_args()
+    if args.workload != "c2":
+        if int(os.environ.get("WORLD_SIZE", "1")) != 1:
+            raise SystemExit("--workload c1/c3 are single-GPU legs")
+        return bench_model(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -53,8 +53,46 @@ __device__ __forceinline__ float adam_elem(const AdamConst& c, float& p, float& 
     return g;
 }
 
+// Row operands of an epilogue, loaded by epi_load right after the work item is
+// known so that they are in flight during the neighbour gathers (the ADAM kind
+// reads five rows: a whole extra dependent memory trip if loaded after the loop).
+struct EpiIn {
+    float4 a, b, c, d, e;
+    float w;
+};
+
 template <int KIND, int D>
-__device__ __forceinline__ void epilogue(const rsx_epilogue& e, int64_t row, float4 acc, int li) {
+__device__ __forceinline__ EpiIn epi_load(const rsx_epilogue& e, int64_t row, int li) {
+    const int64_t off = row * D + li * 4;
+    EpiIn in;
+    in.a = in.b = in.c = in.d = in.e = f4(0.f);
+    in.w = 0.f;
+    if constexpr (KIND == RSX_EPI_LAYERSUM || KIND == RSX_EPI_FINAL || KIND == RSX_EPI_AXPBY) {
+        if (e.s_in) in.a = ld4(e.s_in + off);
+    } else if constexpr (KIND == RSX_EPI_ADD) {
+        if (e.s_in) in.a = ld4(e.s_in + off);
+        if (e.r_add) in.b = ld4(e.r_add + off);
+    } else if constexpr (KIND == RSX_EPI_ADAM) {
+        if (e.s_in) in.a = ld4(e.s_in + off);
+        if (e.r_add) in.b = ld4(e.r_add + off);
+        in.c = ld4(e.p + off);
+        in.d = ld4(e.m + off);
+        in.e = ld4(e.v + off);
+    } else if constexpr (KIND == RSX_EPI_LAYERGCN) {
+        in.a = ld4(e.e0 + off);
+        if (e.s_in) in.b = ld4(e.s_in + off);
+    } else if constexpr (KIND == RSX_EPI_LAYERGCN_BWD) {
+        if (e.r_add) in.a = ld4(e.r_add + off);
+        in.b = ld4(e.aux + off);
+        in.c = ld4(e.e0 + off);
+        if (e.s_in) in.d = ld4(e.s_in + off);
+        in.w = e.aux_w[row];
+    }
+    return in;
+}
+
+template <int KIND, int D>
+__device__ __forceinline__ void epilogue(const rsx_epilogue& e, int64_t row, float4 acc, int li, const EpiIn& in) {
     constexpr int G = D / 4;
     const int64_t off = row * D + li * 4;
     acc = mul4(e.alpha, acc);
@@ -62,26 +100,26 @@ __device__ __forceinline__ void epilogue(const rsx_epilogue& e, int64_t row, flo
         st4(e.y + off, acc);
     } else if constexpr (KIND == RSX_EPI_LAYERSUM) {
         if (e.y) st4(e.y + off, acc);
-        const float4 s = e.s_in ? add4(ld4(e.s_in + off), acc) : acc;
+        const float4 s = e.s_in ? add4(in.a, acc) : acc;
         st4(e.s_out + off, s);
     } else if constexpr (KIND == RSX_EPI_FINAL) {
-        const float4 s = e.s_in ? add4(ld4(e.s_in + off), acc) : acc;
+        const float4 s = e.s_in ? add4(in.a, acc) : acc;
         st4(e.f + off, mul4(e.beta, s));
     } else if constexpr (KIND == RSX_EPI_AXPBY) {
         float4 s = acc;
-        if (e.s_in) s = fma4(e.beta, ld4(e.s_in + off), s);
+        if (e.s_in) s = fma4(e.beta, in.a, s);
         st4(e.y + off, s);
     } else if constexpr (KIND == RSX_EPI_ADD) {
         float4 s = acc;
-        if (e.s_in) s = add4(s, ld4(e.s_in + off));
-        if (e.r_add) s = add4(s, ld4(e.r_add + off));
+        if (e.s_in) s = add4(s, in.a);
+        if (e.r_add) s = add4(s, in.b);
         st4(e.y + off, mul4(e.beta, s));
     } else if constexpr (KIND == RSX_EPI_ADAM) {
-        float4 g = e.s_in ? add4(ld4(e.s_in + off), acc) : acc;
+        float4 g = e.s_in ? add4(in.a, acc) : acc;
         g = mul4(e.beta, g);
-        if (e.r_add) g = add4(g, ld4(e.r_add + off));
+        if (e.r_add) g = add4(g, in.b);
         const AdamConst c = adam_const(e.adam);
-        float4 p = ld4(e.p + off), m = ld4(e.m + off), v = ld4(e.v + off);
+        float4 p = in.c, m = in.d, v = in.e;
         g.x = adam_elem(c, p.x, m.x, v.x, g.x);
         g.y = adam_elem(c, p.y, m.y, v.y, g.y);
         g.z = adam_elem(c, p.z, m.z, v.z, g.z);
@@ -92,7 +130,7 @@ __device__ __forceinline__ void epilogue(const rsx_epilogue& e, int64_t row, flo
         if (e.g_out) st4(e.g_out + off, g);
     } else if constexpr (KIND == RSX_EPI_LAYERGCN) {
         // F.cosine_similarity(z, e0, dim=-1, eps=1e-8) = <z/max(|z|,eps), e/max(|e|,eps)>
-        const float4 e0 = ld4(e.e0 + off);
+        const float4 e0 = in.a;
         const float zz = group_sum<G>(dot4(acc, acc));
         const float ee = group_sum<G>(dot4(e0, e0));
         const float ze = group_sum<G>(dot4(acc, e0));
@@ -102,13 +140,13 @@ __device__ __forceinline__ void epilogue(const rsx_epilogue& e, int64_t row, flo
         if (e.aux) st4(e.aux + off, acc);
         if (e.aux_w && li == 0) e.aux_w[row] = c;
         if (e.y) st4(e.y + off, out);
-        if (e.s_out) st4(e.s_out + off, e.s_in ? add4(ld4(e.s_in + off), out) : out);
+        if (e.s_out) st4(e.s_out + off, e.s_in ? add4(in.b, out) : out);
     } else if constexpr (KIND == RSX_EPI_LAYERGCN_BWD) {
         float4 dE = acc;
-        if (e.r_add) dE = add4(dE, ld4(e.r_add + off));
-        const float4 z = ld4(e.aux + off);
-        const float4 e0 = ld4(e.e0 + off);
-        const float c = e.aux_w[row];
+        if (e.r_add) dE = add4(dE, in.a);
+        const float4 z = in.b;
+        const float4 e0 = in.c;
+        const float c = in.w;
         const float zz = group_sum<G>(dot4(z, z));
         const float ee = group_sum<G>(dot4(e0, e0));
         const float gz = group_sum<G>(dot4(dE, z));
@@ -126,11 +164,16 @@ __device__ __forceinline__ void epilogue(const rsx_epilogue& e, int64_t row, flo
         if (e.s_out) {
             float4 de = mul4(gz * inv, z);
             de = fma4(-gz * ke, e0, de);
-            st4(e.s_out + off, e.s_in ? add4(ld4(e.s_in + off), de) : de);
+            st4(e.s_out + off, e.s_in ? add4(in.d, de) : de);
         }
     }
     if (e.zero0) st4(e.zero0 + off, f4(0.f));
     if (e.zero1) st4(e.zero1 + off, f4(0.f));
+}
+
+template <int KIND, int D>
+__device__ __forceinline__ void epilogue(const rsx_epilogue& e, int64_t row, float4 acc, int li) {
+    epilogue<KIND, D>(e, row, acc, li, epi_load<KIND, D>(e, row, li));
 }
 
 // ---------------------------------------------------------------------------
@@ -176,6 +219,13 @@ __global__ __launch_bounds__(kBlock) void spmm_main(rsx_csr a, const float* __re
     const int64_t w = (int64_t)blockIdx.x * GPB + threadIdx.x / G;
     if (w >= a.n_work) return;  // whole groups leave together
     const int4 wk = reinterpret_cast<const int4*>(a.work)[w];
+    EpiIn pre;
+    if (wk.y < 0) {
+        pre = epi_load<KIND, D>(e, wk.x, li);
+    } else {
+        pre.a = pre.b = pre.c = pre.d = pre.e = f4(0.f);
+        pre.w = 0.f;
+    }
     const int32_t* __restrict__ col = a.col;
     const float* __restrict__ val = a.val;
     const float* xl = x + li * 4;
@@ -228,7 +278,7 @@ __global__ __launch_bounds__(kBlock) void spmm_main(rsx_csr a, const float* __re
     }
     }
     if (wk.y < 0) {
-        epilogue<KIND, D>(e, wk.x, acc, li);
+        epilogue<KIND, D>(e, wk.x, acc, li, pre);
     } else {
         st4(slab + (int64_t)wk.y * D + li * 4, acc);
     }

@@ -121,48 +121,58 @@ class Trainer:
         return bool(torch.isnan(loss))
 
     def _train_epoch_autograd(self, train_data, epoch_idx, loss_func=None):
+        """Reference _train_epoch (trainer.py:170-260).  Per-batch losses stay on the
+        device and are summed once at the end of the epoch (the reference calls
+        .item() per batch, a host sync each); a NaN batch loss ends the epoch at the
+        next check, every `rsx_nan_check_every` batches (reference: every batch)."""
         loss_func = loss_func or self.model.calculate_loss
-        total_loss = None
+        parts = []
         loss_batches = []
+        every = max(int(self.config.get("rsx_nan_check_every", 64) or 64), 1)
         for batch_idx, interaction in enumerate(train_data):
-            self._zero_grad()
-            second = interaction.clone() if hasattr(interaction, "clone") else interaction
-            losses = loss_func(interaction)
-            if isinstance(losses, tuple):
-                loss = sum(losses)
-                part = tuple(x.item() for x in losses)
-                total_loss = part if total_loss is None else tuple(map(sum, zip(total_loss, part)))
-            else:
-                loss = losses
-                total_loss = losses.item() if total_loss is None else total_loss + losses.item()
-            if self._check_nan(loss):
+            losses, loss = self._train_batch(interaction, batch_idx, loss_func)
+            parts.append(torch.stack([x.detach() for x in losses]) if isinstance(losses, tuple) else loss.detach())
+            loss_batches.append(loss.detach())
+            if (batch_idx + 1) % every == 0 and self._check_nan(loss_batches[-1]):
                 self.logger.info(f"Loss is nan at epoch: {epoch_idx}, batch index: {batch_idx}. Exiting.")
-                return loss, torch.tensor(0.0)
-            if not getattr(self.model, "mg_enable", False):
-                if self.mg and batch_idx % self.beta == 0:
-                    (self.alpha1 * loss).backward()
-                    self.optimizer.step()
-                    self.optimizer.zero_grad()
-                    l2 = loss_func(second)
-                    loss = sum(l2) if isinstance(l2, tuple) else l2
-                    if self._check_nan(loss):
-                        self.logger.info(f"Loss is nan at epoch: {epoch_idx}, batch index: {batch_idx}. Exiting.")
-                        return loss, torch.tensor(0.0)
-                    (-1 * self.alpha2 * loss).backward()
-                else:
-                    loss.backward()
-                if self.clip_grad_norm:
-                    clip_grad_norm_(self.model.parameters(), **self.clip_grad_norm)
+                return loss_batches[-1], torch.tensor(0.0)
+        if not parts:
+            return 0.0, loss_batches
+        host = torch.stack(parts).double().cpu().numpy()  # one sync per epoch
+        if np.isnan(host).any():
+            self.logger.info(f"Loss is nan at epoch: {epoch_idx}. Exiting.")
+            return torch.tensor(float("nan")), torch.tensor(0.0)
+        total_loss = tuple(float(x) for x in host.sum(0)) if host.ndim == 2 else float(host.sum())
+        return total_loss, loss_batches
+
+    def _train_batch(self, interaction, batch_idx, loss_func):
+        """One training batch exactly as the reference's loop body: loss, backward,
+        optimizer step, and the trainer-level (alpha1/alpha2) or model-level mirror
+        gradient.  Returns (losses as returned by calculate_loss, summed loss)."""
+        self._zero_grad()
+        second = interaction.clone() if hasattr(interaction, "clone") else interaction
+        losses = loss_func(interaction)
+        loss = sum(losses) if isinstance(losses, tuple) else losses
+        if not getattr(self.model, "mg_enable", False):
+            if self.mg and batch_idx % self.beta == 0:
+                (self.alpha1 * loss).backward()
                 self.optimizer.step()
-                loss_batches.append(loss.detach())
-                continue
-            loss.backward()
+                self.optimizer.zero_grad()
+                l2 = loss_func(second)
+                loss = sum(l2) if isinstance(l2, tuple) else l2
+                (-1 * self.alpha2 * loss).backward()
+            else:
+                loss.backward()
             if self.clip_grad_norm:
                 clip_grad_norm_(self.model.parameters(), **self.clip_grad_norm)
             self.optimizer.step()
-            loss_batches.append(loss.detach())
-            self._mirror_gradient(loss_func, second)
-        return total_loss, loss_batches
+            return losses, loss
+        loss.backward()
+        if self.clip_grad_norm:
+            clip_grad_norm_(self.model.parameters(), **self.clip_grad_norm)
+        self.optimizer.step()
+        self._mirror_gradient(loss_func, second)
+        return losses, loss
 
     def _zero_grad(self):
         try:
