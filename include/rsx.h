@@ -60,10 +60,11 @@ typedef struct rsx_csr {
     int32_t chunk;            /* max nonzeros per work item */
     int32_t pad0;
     int64_t n_work;           /* work items */
-    const int32_t* work;      /* [n_work][4] = {row, slot, begin, end}; slot -1: whole row */
+    const int32_t* work;      /* [n_work][4] = {row, slot, begin, end}; slot -1: whole row, else
+                                 {long-row index, slot, begin, end}; long-row chunks come first */
     int64_t n_long;           /* rows split over more than one work item */
     const int32_t* long_rows; /* [n_long][4] = {row, slot_begin, n_slots, 0} */
-    int64_t n_slots;          /* partial-sum slab rows needed (slab = n_slots * d floats) */
+    int64_t n_slots;          /* partial-sum slab rows (slab = n_slots * d floats + n_long int32) */
 } rsx_csr;
 
 /*
@@ -110,7 +111,13 @@ int rsx_csr_schedule_host(const int64_t* rowptr_host, int64_t n_rows, int32_t ch
  *   Every kind also zeroes the zero0 / zero1 rows when those are non-NULL.
  *
  * Each output row is written by exactly one wavefront group; s_out may alias
- * s_in, never X.  `slab` must hold csr->n_slots * d floats (0 if n_slots == 0).
+ * s_in, never X.  `slab` is the workspace of the split (long) rows: n_slots * d
+ * floats of partial sums followed by n_long int32 arrival counters, which must
+ * be zero before the first call (allocate zero-filled; every call leaves them
+ * zero again).  NULL is allowed when n_long == 0.  One launch does the whole
+ * product: the long rows' chunk partials first, then one block per long row sums
+ * them in chunk order, so results are deterministic.  A slab (with its
+ * counters) must not be shared by two calls in flight at once.
  * d must be one of 32, 64, 128, 256.
  */
 enum {

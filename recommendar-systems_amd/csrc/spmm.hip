@@ -209,6 +209,64 @@ __device__ __forceinline__ float4 gather8(float4 acc, int cm, float vm, int n, c
     return acc;
 }
 
+// Fixup of long row `l` by one whole block, at the end of the same launch: thread 0
+// waits until all of the row's chunk partials are counted (their blocks come
+// earlier in dispatch order, so they are running or done and never wait
+// themselves; the poll is bounded so the wave always exits), then the block's
+// groups each sum a strided subset of the partials (4 independent accumulators),
+// group 0 adds the group sums in a fixed order and applies the epilogue: the
+// result does not depend on which chunk finished last.  Thread 0 re-arms the
+// counter for the next launch.
+template <int D, int KIND>
+__device__ __forceinline__ void fixup_block(const rsx_csr& a, const rsx_epilogue& e, float* slab, int64_t l) {
+    constexpr int G = D / 4;
+    constexpr int GPB = kBlock / G;
+    __shared__ float4 part[GPB][G];
+    __shared__ int ok;
+    const int li = threadIdx.x % G;
+    const int gi = threadIdx.x / G;
+    const int4 lr = reinterpret_cast<const int4*>(a.long_rows)[l];
+    EpiIn pre;
+    if (gi == 0) pre = epi_load<KIND, D>(e, lr.x, li);
+    int* cnt = reinterpret_cast<int*>(slab + a.n_slots * D) + l;
+    if (threadIdx.x == 0) {
+        int polls = 0;
+        while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < lr.z && polls < (1 << 24)) {
+            __builtin_amdgcn_s_sleep(2);
+            ++polls;
+        }
+        ok = polls < (1 << 24);
+    }
+    __syncthreads();
+    const float* base = slab + (int64_t)lr.y * D + li * 4;
+    auto ldp = [&](int64_t s) {
+        const float* q = base + s * D;
+        return make_float4(__hip_atomic_load(q + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                           __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                           __hip_atomic_load(q + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                           __hip_atomic_load(q + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    };
+    float4 a0 = f4(0.f), a1 = f4(0.f), a2 = f4(0.f), a3 = f4(0.f);
+    int s = gi;
+    for (; s + 3 * GPB < lr.z; s += 4 * GPB) {
+        a0 = add4(a0, ldp(s));
+        a1 = add4(a1, ldp(s + GPB));
+        a2 = add4(a2, ldp(s + 2 * GPB));
+        a3 = add4(a3, ldp(s + 3 * GPB));
+    }
+    for (; s < lr.z; s += GPB) a0 = add4(a0, ldp(s));
+    part[gi][li] = add4(add4(a0, a1), add4(a2, a3));
+    __syncthreads();
+    if (gi == 0) {
+        float4 acc = part[0][li];
+#pragma unroll 4
+        for (int g = 1; g < GPB; ++g) acc = add4(acc, part[g][li]);
+        if (!ok) acc = f4(__builtin_nanf(""));  // producers never arrived: poison the row
+        epilogue<KIND, D>(e, lr.x, acc, li, pre);
+    }
+    if (threadIdx.x == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // One group of G lanes per work item {row, slot, begin, end}.
 template <int D, int KIND>
 __global__ __launch_bounds__(kBlock) void spmm_main(rsx_csr a, const float* __restrict__ x,
@@ -216,6 +274,11 @@ __global__ __launch_bounds__(kBlock) void spmm_main(rsx_csr a, const float* __re
     constexpr int G = D / 4;
     constexpr int GPB = kBlock / G;
     const int li = threadIdx.x % G;
+    const int64_t n_main = (a.n_work + GPB - 1) / GPB;
+    if ((int64_t)blockIdx.x >= n_main) {
+        fixup_block<D, KIND>(a, e, slab, (int64_t)blockIdx.x - n_main);
+        return;
+    }
     const int64_t w = (int64_t)blockIdx.x * GPB + threadIdx.x / G;
     if (w >= a.n_work) return;  // whole groups leave together
     const int4 wk = reinterpret_cast<const int4*>(a.work)[w];
@@ -280,39 +343,20 @@ __global__ __launch_bounds__(kBlock) void spmm_main(rsx_csr a, const float* __re
     if (wk.y < 0) {
         epilogue<KIND, D>(e, wk.x, acc, li, pre);
     } else {
-        st4(slab + (int64_t)wk.y * D + li * 4, acc);
-    }
-}
-
-// One block per long row: the block's groups each sum a strided subset of the
-// row's slab partials (4 independent accumulators, so 4+ loads stay in flight),
-// then group 0 adds the group sums in a fixed order and applies the epilogue.
-template <int D, int KIND>
-__global__ __launch_bounds__(kBlock) void spmm_fixup(rsx_csr a, rsx_epilogue e,
-                                                     const float* __restrict__ slab) {
-    constexpr int G = D / 4;
-    constexpr int GPB = kBlock / G;
-    __shared__ float4 part[GPB][G];
-    const int li = threadIdx.x % G;
-    const int gi = threadIdx.x / G;
-    const int4 lr = reinterpret_cast<const int4*>(a.long_rows)[blockIdx.x];
-    const float* base = slab + (int64_t)lr.y * D + li * 4;
-    float4 a0 = f4(0.f), a1 = f4(0.f), a2 = f4(0.f), a3 = f4(0.f);
-    int s = gi;
-    for (; s + 3 * GPB < lr.z; s += 4 * GPB) {
-        a0 = add4(a0, ld4(base + (int64_t)s * D));
-        a1 = add4(a1, ld4(base + (int64_t)(s + GPB) * D));
-        a2 = add4(a2, ld4(base + (int64_t)(s + 2 * GPB) * D));
-        a3 = add4(a3, ld4(base + (int64_t)(s + 3 * GPB) * D));
-    }
-    for (; s < lr.z; s += GPB) a0 = add4(a0, ld4(base + (int64_t)s * D));
-    part[gi][li] = add4(add4(a0, a1), add4(a2, a3));
-    __syncthreads();
-    if (gi == 0) {
-        float4 acc = part[0][li];
-#pragma unroll 4
-        for (int g = 1; g < GPB; ++g) acc = add4(acc, part[g][li]);
-        epilogue<KIND, D>(e, lr.x, acc, li);
+        // partial of long row wk.x: written through the (per-XCD, non-coherent) L2
+        // with agent-scope stores, then counted once the whole group's stores are
+        // acknowledged; the fixup block of that row waits for the count
+        float* dst = slab + (int64_t)wk.y * D + li * 4;
+        __hip_atomic_store(dst + 0, acc.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(dst + 1, acc.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(dst + 2, acc.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(dst + 3, acc.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's stores are performed
+        __builtin_amdgcn_wave_barrier();
+        if (li == 0) {
+            int* cnt = reinterpret_cast<int*>(slab + a.n_slots * D) + wk.x;
+            __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
 }
 
@@ -331,14 +375,9 @@ template <int D, int KIND>
 static int launch_spmm(const rsx_csr& a, const float* x, const rsx_epilogue& e, float* slab,
                        hipStream_t s) {
     constexpr int GPB = kBlock / (D / 4);
-    if (a.n_work > 0) {
-        const int64_t nb = (a.n_work + GPB - 1) / GPB;
+    const int64_t nb = (a.n_work + GPB - 1) / GPB + a.n_long;  // work blocks, then one fixup block per long row
+    if (nb > 0)
         hipLaunchKernelGGL((spmm_main<D, KIND>), dim3((unsigned)nb), dim3(kBlock), 0, s, a, x, e, slab);
-    }
-    if (a.n_long > 0) {
-        hipLaunchKernelGGL((spmm_fixup<D, KIND>), dim3((unsigned)a.n_long), dim3(kBlock), 0, s, a, e,
-                           (const float*)slab);
-    }
     return last_rc();
 }
 
@@ -417,33 +456,38 @@ int rsx_csr_schedule_host(const int64_t* rowptr_host, int64_t n_rows, int32_t ch
     if (!rowptr_host || n_rows < 0 || chunk <= 0 || !n_work || !n_long || !n_slots) return RSX_ERR_ARG;
     if (rowptr_host[n_rows] >= (int64_t(1) << 31)) return RSX_ERR_ARG;
     int64_t nw = 0, nl = 0, ns = 0;
+    // pass 1: the chunks of long rows (slab items) come first, so that every block
+    // producing a partial is dispatched before the fixup blocks that consume it
     for (int64_t r = 0; r < n_rows; ++r) {
         const int64_t b = rowptr_host[r], e = rowptr_host[r + 1];
         const int64_t deg = e - b;
-        if (deg <= chunk) {
+        if (deg <= chunk) continue;
+        const int64_t nc = (deg + chunk - 1) / chunk;
+        if (long_host) {
+            int32_t* l = long_host + 4 * nl;
+            l[0] = (int32_t)r; l[1] = (int32_t)ns; l[2] = (int32_t)nc; l[3] = 0;
+        }
+        for (int64_t c = 0; c < nc; ++c) {
             if (work_host) {
                 int32_t* w = work_host + 4 * nw;
-                w[0] = (int32_t)r; w[1] = -1; w[2] = (int32_t)b; w[3] = (int32_t)e;
+                const int64_t cb = b + c * chunk;
+                const int64_t ce = cb + chunk < e ? cb + chunk : e;
+                w[0] = (int32_t)nl; w[1] = (int32_t)(ns + c); w[2] = (int32_t)cb; w[3] = (int32_t)ce;
             }
             ++nw;
-        } else {
-            const int64_t nc = (deg + chunk - 1) / chunk;
-            if (long_host) {
-                int32_t* l = long_host + 4 * nl;
-                l[0] = (int32_t)r; l[1] = (int32_t)ns; l[2] = (int32_t)nc; l[3] = 0;
-            }
-            for (int64_t c = 0; c < nc; ++c) {
-                if (work_host) {
-                    int32_t* w = work_host + 4 * nw;
-                    const int64_t cb = b + c * chunk;
-                    const int64_t ce = cb + chunk < e ? cb + chunk : e;
-                    w[0] = (int32_t)r; w[1] = (int32_t)(ns + c); w[2] = (int32_t)cb; w[3] = (int32_t)ce;
-                }
-                ++nw;
-            }
-            ns += nc;
-            ++nl;
         }
+        ns += nc;
+        ++nl;
+    }
+    // pass 2: whole rows
+    for (int64_t r = 0; r < n_rows; ++r) {
+        const int64_t b = rowptr_host[r], e = rowptr_host[r + 1];
+        if (e - b > chunk) continue;
+        if (work_host) {
+            int32_t* w = work_host + 4 * nw;
+            w[0] = (int32_t)r; w[1] = -1; w[2] = (int32_t)b; w[3] = (int32_t)e;
+        }
+        ++nw;
     }
     *n_work = nw;
     *n_long = nl;

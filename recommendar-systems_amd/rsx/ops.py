@@ -94,7 +94,9 @@ class DeviceCSR:
             return None
         s = self._slabs.get(d)
         if s is None:
-            s = torch.empty(self.n_slots * d, dtype=torch.float32, device=self.device)
+            # partial-sum slots, then one int32 arrival counter per long row (zero; the
+            # kernel re-arms them), see rsx_spmm in include/rsx.h
+            s = torch.zeros(self.n_slots * d + self.n_long, dtype=torch.float32, device=self.device)
             self._slabs[d] = s
         return s
 

@@ -47,13 +47,19 @@ def test_schedule_host_splits_hub_rows():
     lr = np.zeros((nl.value, 4), np.int32)
     lib.rsx_csr_schedule_host(rowptr.ctypes.data_as(C.c_void_p), deg.size, 32, work.ctypes.data_as(C.c_void_p),
                               lr.ctypes.data_as(C.c_void_p), C.byref(nw), C.byref(nl), C.byref(ns))
-    # every nonzero covered exactly once, chunks <= 32, slots contiguous per long row
+    # every nonzero covered exactly once, chunks <= 32, slots contiguous per long row;
+    # the long rows' chunks come first (x = long-row index), whole rows after them
     cover = np.zeros(rowptr[-1], np.int32)
-    for r, slot, b, e in work:
+    assert lr.tolist() == [[3, 0, 2, 0], [4, 2, 4, 0]]
+    n_chunks = int(lr[:, 2].sum())
+    for i, (x, slot, b, e) in enumerate(work):
+        r = lr[x, 0] if i < n_chunks else x
+        assert (slot >= 0) == (i < n_chunks)
+        if slot >= 0:
+            assert lr[x, 1] <= slot < lr[x, 1] + lr[x, 2]
         assert 0 <= e - b <= 32 and rowptr[r] <= b <= e <= rowptr[r + 1]
         cover[b:e] += 1
     assert np.all(cover == 1)
-    assert lr.tolist() == [[3, 0, 2, 0], [4, 2, 4, 0]]
     # nnz >= 2^31 is refused (32-bit work offsets)
     big = np.array([0, 1 << 31], dtype=np.int64)
     assert lib.rsx_csr_schedule_host(big.ctypes.data_as(C.c_void_p), 1, 32, None, None, C.byref(nw),
