@@ -11,11 +11,13 @@ contiguous per-rank blocks U_g and the item rows replicated:
                                          one all-reduce of the [n_items, d] block)
 Per propagation layer the item-row SpMM runs first and its all-reduce is
 issued asynchronously; the user-row SpMM of the same layer (which only needs
-the previous, already reduced items) runs on the compute stream meanwhile.
-The backward (Horner, as in rsx_lightgcn_step) is the same product with the
-same exchange; the item-side gradient and the last layer's partial are
-reduced together, so a K-layer step issues 2K+1 all-reduces of n_items*d
-floats.  Adam runs on every rank: user rows locally, item rows identically on
+the previous, already reduced items) runs on the compute stream meanwhile, and
+so does the NEXT layer's item partial (it needs only this layer's users), whose
+exchange is queued behind this one: the comm stream runs the exchanges back to
+back.  The backward is the same layer sums on G = dL/dfinal with the same
+exchange (G's per-rank item rows are reduced first, queued together with layer
+1's partial); the item-side gradient and the last layer's partial are reduced
+together, so a K-layer step issues 2K+1 all-reduces of n_items*d floats.  Adam runs on every rank: user rows locally, item rows identically on
 each replica (the reduced inputs are bit-identical on all ranks).
 
 Normalisation uses GLOBAL item degrees (one all-reduce of a degree vector at
@@ -142,28 +144,37 @@ class ShardedLightGCNEngine:
 
     # --------------------------------------------------------------- forward
     def _propagate(self, zero_grads: bool):
+        """Forward layers with every item all-reduce issued as soon as its partial
+        exists: layer k+1's item partial needs only users^k (local), so it is
+        computed and its exchange queued before waiting for layer k's; the comm
+        stream then runs the K exchanges back to back while the compute stream
+        does the user-row SpMMs.  Per-element arithmetic = one layer at a time."""
         be, nu, ni, d, K = self.be, self.n_users, self.n_items, self.d, self.K
         p, s, f = self.p, self.s, self.final
         bufs = (self.h0, self.h1)
         beta = 1.0 / (K + 1)
-        x = p
+        ys = [p] + [bufs[(k - 1) & 1] for k in range(1, K + 1)]  # ys[k]: users^k | items^k
+        works = {}
+
+        def item_partial(k):  # items^k partial = R_g^T users^{k-1}; exchange queued
+            be.spmm(self.A_I, ys[k - 1], d, L.RSX_EPI_STORE, y=ys[k][nu:])
+            works[k] = self._ar(ys[k][nu:])
+
+        item_partial(1)
         for k in range(1, K + 1):
-            y = bufs[(k - 1) & 1]
             s_in = p if k == 1 else s
-            be.spmm(self.A_I, x, d, L.RSX_EPI_STORE, y=y[nu:])          # partial items^k
-            work = self._ar(y[nu:])
-            zero = dict(zero0=self.g[:nu], zero1=self.r[:nu]) if (k == K and zero_grads) else {}
             if k < K:
-                be.spmm(self.A_U, x, d, L.RSX_EPI_LAYERSUM, y=y[:nu], s_in=s_in[:nu], s_out=s[:nu])
+                be.spmm(self.A_U, ys[k - 1], d, L.RSX_EPI_LAYERSUM, y=ys[k][:nu], s_in=s_in[:nu], s_out=s[:nu])
+                item_partial(k + 1)
             else:
-                be.spmm(self.A_U, x, d, L.RSX_EPI_FINAL, beta=beta, f=f[:nu], s_in=s_in[:nu], **zero)
-            work.wait()
+                zero = dict(zero0=self.g[:nu], zero1=self.r[:nu]) if zero_grads else {}
+                be.spmm(self.A_U, ys[k - 1], d, L.RSX_EPI_FINAL, beta=beta, f=f[:nu], s_in=s_in[:nu], **zero)
+            works.pop(k).wait()
             if k < K:
-                be.rowwise(ni, d, L.RSX_EPI_ADD, y=s[nu:], s_in=s_in[nu:], r_add=y[nu:])
+                be.rowwise(ni, d, L.RSX_EPI_ADD, y=s[nu:], s_in=s_in[nu:], r_add=ys[k][nu:])
             else:
                 zi = dict(zero0=self.g[nu:], zero1=self.r[nu:]) if zero_grads else {}
-                be.rowwise(ni, d, L.RSX_EPI_ADD, beta=beta, y=f[nu:], s_in=s_in[nu:], r_add=y[nu:], **zi)
-            x = y
+                be.rowwise(ni, d, L.RSX_EPI_ADD, beta=beta, y=f[nu:], s_in=s_in[nu:], r_add=ys[k][nu:], **zi)
 
     def forward(self):
         if not self._fwd_valid:
@@ -190,25 +201,33 @@ class ShardedLightGCNEngine:
         beta = 1.0 / (K + 1)
         g, s, r, t = self.g, self.s, self.r, self.t
         bufs = (self.h0, self.h1)
-        dist.all_reduce(g[nu:], group=self.group)  # item rows of dL/dfinal from every rank's batch
-        x = g
+        # backward = the same layer sums on G = dL/dfinal (A symmetric); G's item rows
+        # are per-rank partials: their exchange and layer 1's item partial (which
+        # needs only G's local user rows) are queued together, and so on per layer
+        ys = [g] + [bufs[(k - 1) & 1] for k in range(1, K + 1)]
+        works = {0: self._ar(g[nu:])}
+
+        def item_partial(k):
+            if k < K:
+                be.spmm(self.A_I, ys[k - 1], d, L.RSX_EPI_STORE, y=ys[k][nu:])
+                works[k] = self._ar(ys[k][nu:])
+            else:  # t = H_I^K/(K+1) + R_I: this rank's share of the item gradient beyond s_I/(K+1)
+                be.spmm(self.A_I, ys[k - 1], d, L.RSX_EPI_ADD, alpha=beta, y=t, r_add=r[nu:])
+                works[k] = self._ar(t)
+
+        item_partial(1)
+        works.pop(0).wait()
         for k in range(1, K + 1):
-            y = bufs[(k - 1) & 1]
             s_in = g if k == 1 else s
             if k < K:
-                be.spmm(self.A_I, x, d, L.RSX_EPI_STORE, y=y[nu:])
-                work = self._ar(y[nu:])
-                be.spmm(self.A_U, x, d, L.RSX_EPI_LAYERSUM, y=y[:nu], s_in=s_in[:nu], s_out=s[:nu])
-                work.wait()
-                be.rowwise(ni, d, L.RSX_EPI_ADD, y=s[nu:], s_in=s_in[nu:], r_add=y[nu:])
+                be.spmm(self.A_U, ys[k - 1], d, L.RSX_EPI_LAYERSUM, y=ys[k][:nu], s_in=s_in[:nu], s_out=s[:nu])
+                item_partial(k + 1)
+                works.pop(k).wait()
+                be.rowwise(ni, d, L.RSX_EPI_ADD, y=s[nu:], s_in=s_in[nu:], r_add=ys[k][nu:])
             else:
-                # t = H_I^K/(K+1) + R_I: this rank's share of the item gradient beyond s_I/(K+1)
-                be.spmm(self.A_I, x, d, L.RSX_EPI_ADD, alpha=beta, y=t, r_add=r[nu:])
-                work = self._ar(t)
-                be.spmm(self.A_U, x, d, L.RSX_EPI_ADAM, beta=beta, adam=adam, s_in=s_in[:nu], r_add=r[:nu],
+                be.spmm(self.A_U, ys[k - 1], d, L.RSX_EPI_ADAM, beta=beta, adam=adam, s_in=s_in[:nu], r_add=r[:nu],
                         p=self.p[:nu], m=self.m[:nu], v=self.v[:nu])
-                work.wait()
+                works.pop(k).wait()
                 be.rowwise(ni, d, L.RSX_EPI_ADAM, beta=beta, adam=adam, s_in=s_in[nu:], r_add=t,
                            p=self.p[nu:], m=self.m[nu:], v=self.v[nu:])
-            x = y
         self._fwd_valid = False

@@ -1,0 +1,21 @@
+"""Build a variant of librsx.so with extra -D flags into rsx/lib/variants/<name>/
+(for side-by-side timing on the GPU box via RSX_LIB=...).
+usage: python tools/build_variant.py NAME -DFOO=1 [-DBAR=2 ...]"""
+import os
+import subprocess
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "recommendar-systems_amd"))
+from rsx import build as B  # noqa: E402
+
+name, defs = sys.argv[1], sys.argv[2:]
+out = os.path.join(B.LIBDIR, "variants", name)
+os.makedirs(out, exist_ok=True)
+objs = []
+for src in B.SOURCES:
+    obj = os.path.join(out, src.replace(".hip", ".o"))
+    subprocess.run([B._hipcc(), *B._flags(), *defs, "-c", os.path.join(B.CSRC, src), "-o", obj], check=True)
+    objs.append(obj)
+subprocess.run([B._hipcc(), f"--offload-arch={B.ARCH}", "-shared", "-fPIC", "-o", os.path.join(out, "librsx.so"),
+                *objs], check=True)
+print(os.path.join(out, "librsx.so"))

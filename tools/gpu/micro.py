@@ -40,6 +40,27 @@ def main(what):
             y = torch.empty_like(x)
             out[f"spmm_store_chunk{chunk}_ms"] = t_ms(lambda: A.spmm(x, out=y))
             out[f"chunk{chunk}_nlong"] = A.n_long
+    if what == "spmmx":
+        # what bounds the SpMM: same schedule with (a) every gather on row 0 (all hits),
+        # (b) neighbours = the next rows in order (streaming), (c) no nonzeros at all
+        x = torch.randn(n, 64, device=dev)
+        y = torch.empty_like(x)
+        deg = np.diff(rp)
+        variants = {
+            "real": (rp, col),
+            "same_row": (rp, np.zeros_like(col)),
+            "sequential": (rp, ((np.repeat(np.arange(n), deg) + np.arange(col.size) % 8) % n).astype(np.int32)),
+            "empty": (np.zeros_like(rp), col[:0]),
+        }
+        for name, (r, c) in variants.items():
+            A = ops.DeviceCSR(r, c, val[: c.size].astype(np.float32), n, dev, 32)
+            out[f"spmmx_{name}_us"] = round(t_ms(lambda: A.spmm(x, out=y), 100) * 1e3, 2)
+        # the same real graph with d = 32 / 128 (bytes scale with d)
+        for d in (32, 128):
+            A = ops.DeviceCSR(rp, col, val, n, dev, 32)
+            xd = torch.randn(n, d, device=dev)
+            yd = torch.empty_like(xd)
+            out[f"spmmx_real_d{d}_us"] = round(t_ms(lambda: A.spmm(xd, out=yd), 100) * 1e3, 2)
     if what in ("fullsort", "all"):
         f = torch.randn(n, 64, device=dev) * 0.1
         U, I = f[:nu], f[nu:]
