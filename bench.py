@@ -288,11 +288,20 @@ def main():
     rp_d, mc_d = torch.from_numpy(rp).to(dev), torch.from_numpy(mc).to(dev)
     vu_d = torch.from_numpy(vusers.astype(np.int64)).to(dev)
 
+    # held-out (valid) items per evaluation user, sorted: the metric tail's CSR
+    vdf = va[va.userID.isin(vusers)].sort_values(["userID", "itemID"])
+    vlen = np.bincount(np.searchsorted(vusers, vdf.userID.values), minlength=vusers.size)
+    erp = torch.from_numpy(np.concatenate([[0], np.cumsum(vlen)]).astype(np.int64)).to(dev)
+    ecol = torch.from_numpy(vdf.itemID.values.astype(np.int32)).to(dev)
+    gain = torch.from_numpy(1.0 / np.log2(np.arange(1, 51, dtype=np.float64) + 1)).to(dev)
+
     def evaluate():
-        # forward once + one fused launch over all evaluation users (no score matrix)
+        # what Trainer.evaluate does: forward once, one fused scores+mask+top-50 launch over
+        # all evaluation users (no score matrix), the metric tail on device, metrics to host
         eng.invalidate()
         f = eng.forward()
-        ops.fullsort_topk(f[:nu], vu_d, f[nu:], rp_d, mc_d, 50)
+        _, idx = ops.fullsort_topk(f[:nu], vu_d, f[nu:], rp_d, mc_d, 50)
+        ops.topk_metrics(idx, erp, ecol, [5, 10, 20, 50], gain).cpu()
 
     evaluate()
     torch.cuda.synchronize()
@@ -361,6 +370,7 @@ def main():
             "fullsort_items_per_s": items_per_s,
             "fullsort": {"eval_users": int(n_eval), "n_items": ni, "k": 50,
                          "s_per_eval": eval_s,
+                         "s_per_eval_includes": "forward + fused top-50 + recall/ndcg/precision/map tail + D2H",
                          "kernel_ms_all_eval_users": fs_ms,
                          "kernel_tflops": fs_flops / (fs_ms * 1e-3) / 1e12,
                          "mfma_f32_peak_tflops": 157.3},

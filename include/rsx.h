@@ -345,6 +345,31 @@ int rsx_smore_spectral_bwd(const float* img, const float* txt,
                            int64_t n_items, int32_t d, float* g_img, float* g_txt,
                            float* g_w_partial, rsx_stream_t stream);
 
+/* ------------------------------------------------------------------------ */
+/* Evaluation tail: top-K ranking metrics                                     */
+/* ------------------------------------------------------------------------ */
+/*
+ * Replaces TopKEvaluator.evaluate's hit matrix (the per-(user, rank) Python
+ * `i in m` loop, src/utils/topk_evaluator.py:90-101) and utils/metrics.py
+ * (:12-118) for recall / recall2 / precision / ndcg / map.
+ *   topk_idx    [n_users][k_max] int64: ranked items per evaluation user
+ *   eval_rowptr [n_users+1] int64, eval_col int32: each user's held-out items,
+ *               SORTED within the user (binary-searched)
+ *   cutoffs     [n_cut] int32, ascending, each in [1, k_max]
+ *   gain        [k_max] float64: 1/log2(r+1), r = 1..k_max (the caller computes it
+ *               as the reference does, so results match bit for bit)
+ *   out_sums    [5][n_cut] float64: over users, summed sequentially in user order
+ *               (numpy's mean(axis=0) order) of recall, precision, ndcg, map, and
+ *               the hit count (recall2's numerator).  Divide the first four by
+ *               n_users for the reference's means; recall2 = hits / sum(|pos|).
+ *   ws          >= rsx_topk_metrics_ws_bytes(n_users, n_cut) bytes.
+ */
+size_t rsx_topk_metrics_ws_bytes(int64_t n_users, int32_t n_cut);
+int rsx_topk_metrics(const int64_t* topk_idx, int64_t n_users, int32_t k_max,
+                     const int64_t* eval_rowptr, const int32_t* eval_col,
+                     const int32_t* cutoffs, int32_t n_cut, const double* gain,
+                     double* out_sums, void* ws, size_t ws_bytes, rsx_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,102 @@
+// metrics.hip — the evaluation tail of the reference on the device:
+// TopKEvaluator.evaluate + utils/metrics.py (src/utils/topk_evaluator.py:58-102,
+// src/utils/metrics.py:12-118) for recall, recall2, precision, ndcg and map.
+//
+// Kernel 1, one thread per evaluation user: hit[r] = topk[u][r] in the user's
+// held-out items (binary search in a sorted per-user CSR, replacing the
+// reference's Python `i in m` loop), then the per-user metric values at each
+// cutoff with the reference's float64 arithmetic in its order (cumulative sums
+// over ranks 1..k; the gain table 1/log2(r+1) comes from the caller, computed by
+// numpy exactly as the reference does).  Values are written [n_users][M].
+// Kernel 2, one wavefront per column: the column summed over users SEQUENTIALLY in
+// user order — numpy's mean(axis=0) over a C-contiguous [n, k] array adds rows in
+// order — so the sums, and after the caller's division and round(., 4) the metric
+// dict, are bit-identical to the reference's.
+#include "rsx_common.hpp"
+
+namespace rsx {
+
+constexpr int kMetricCols = 5;  // recall, precision, ndcg, map, cumhit (recall2 numerator)
+
+__global__ __launch_bounds__(256) void metrics_user(const int64_t* __restrict__ topk, int64_t n, int kmax,
+                                                     const int64_t* __restrict__ erp,
+                                                     const int32_t* __restrict__ ecol,
+                                                     const int32_t* __restrict__ cut, int n_cut,
+                                                     const double* __restrict__ gain, double* __restrict__ vals) {
+    const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (u >= n) return;
+    const int64_t b = erp[u], e = erp[u + 1];
+    const int64_t pos = e - b;
+    const int cap = (int)(pos < kmax ? pos : kmax);
+    double cum = 0.0, dcg = 0.0, ap = 0.0, idcg_full = 0.0;
+    double idcg_cap = 0.0;
+    int c = 0;
+    double* out = vals + u * (int64_t)(kMetricCols * n_cut);
+    for (int r = 0; r < kmax; ++r) {
+        const int64_t it = topk[u * kmax + r];
+        int64_t lo = b, hi = e;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if ((int64_t)ecol[mid] < it) lo = mid + 1; else hi = mid;
+        }
+        const bool hit = lo < e && (int64_t)ecol[lo] == it;
+        const double rank = (double)(r + 1);
+        if (hit) cum += 1.0;
+        dcg += hit ? gain[r] : 0.0;                  // cumsum(where(hit, gain, 0))
+        ap += (cum / rank) * (hit ? 1.0 : 0.0);      // cumsum(prec * hit)
+        idcg_full += gain[r];                        // cumsum(gain)
+        if (r == cap - 1) idcg_cap = idcg_full;      // ideal_full[min(k, cap) - 1]
+        while (c < n_cut && cut[c] == r + 1) {
+            const double idcg = (r + 1 <= cap) ? idcg_full : idcg_cap;
+            const double denom = (double)((r + 1) < cap ? (r + 1) : cap);
+            out[0 * n_cut + c] = cum / (double)pos;  // recall
+            out[1 * n_cut + c] = cum / rank;         // precision
+            out[2 * n_cut + c] = dcg / idcg;         // ndcg
+            out[3 * n_cut + c] = ap / denom;         // map
+            out[4 * n_cut + c] = cum;                // recall2 numerator
+            ++c;
+        }
+    }
+}
+
+// One wavefront per column: the 64 lanes load 64 users' values at a time (the next
+// chunk is loaded before this one is added), then every lane adds them in user
+// order from registers (shuffles): the serial chain is adds only, no load latency.
+__global__ __launch_bounds__(64) void metrics_sum(const double* __restrict__ vals, int64_t n, int m,
+                                                  double* __restrict__ out) {
+    const int j = blockIdx.x, lane = threadIdx.x;
+    double s = 0.0;
+    double cur = lane < n ? vals[(int64_t)lane * m + j] : 0.0;
+    for (int64_t base = 0; base < n; base += 64) {
+        const int64_t nx = base + 64 + lane;
+        const double nxt = nx < n ? vals[nx * m + j] : 0.0;
+        const int cnt = (int)(n - base < 64 ? n - base : 64);
+        for (int t = 0; t < cnt; ++t) s += __shfl(cur, t, kWave);
+        cur = nxt;
+    }
+    if (lane == 0) out[j] = s;
+}
+
+}  // namespace rsx
+
+using namespace rsx;
+
+extern "C" size_t rsx_topk_metrics_ws_bytes(int64_t n_users, int32_t n_cut) {
+    return (size_t)(n_users > 0 ? n_users : 0) * kMetricCols * (size_t)(n_cut > 0 ? n_cut : 0) * sizeof(double);
+}
+
+extern "C" int rsx_topk_metrics(const int64_t* topk_idx, int64_t n_users, int32_t k_max, const int64_t* eval_rowptr,
+                                const int32_t* eval_col, const int32_t* cutoffs, int32_t n_cut, const double* gain,
+                                double* out_sums, void* ws, size_t ws_bytes, rsx_stream_t stream) {
+    if (n_users < 0 || k_max <= 0 || n_cut <= 0 || !cutoffs || !gain || !out_sums) return RSX_ERR_ARG;
+    if (n_users > 0 && (!topk_idx || !eval_rowptr || !eval_col)) return RSX_ERR_ARG;
+    if (ws_bytes < rsx_topk_metrics_ws_bytes(n_users, n_cut) || (n_users > 0 && !ws)) return RSX_ERR_WORKSPACE;
+    hipStream_t s = as_stream(stream);
+    const int m = kMetricCols * n_cut;
+    double* vals = static_cast<double*>(ws);
+    if (n_users > 0)
+        hipLaunchKernelGGL(metrics_user, dim3((unsigned)((n_users + 255) / 256)), dim3(256), 0, s, topk_idx, n_users,
+                           (int)k_max, eval_rowptr, eval_col, cutoffs, (int)n_cut, gain, vals);
+    hipLaunchKernelGGL(metrics_sum, dim3((unsigned)m), dim3(64), 0, s, vals, n_users, m, out_sums);
+    return last_rc();
+}

@@ -87,6 +87,8 @@ def _declare(lib):
         "rsx_smore_spectral_fwd": (C.c_int, [P, I32, P, P, P, I32, P, P, P, P, P, I64, I32, P, P, P, P, P, P]),
         "rsx_smore_spectral_bwd": (C.c_int, [P, P, P, P, P, P, P, P, I64, I32, P, P, P, P]),
         "rsx_smore_spectral_bwd_partials": (C.c_size_t, [I64, I32]),
+        "rsx_topk_metrics_ws_bytes": (C.c_size_t, [I64, I32]),
+        "rsx_topk_metrics": (C.c_int, [P, I64, I32, P, P, P, I32, P, P, P, C.c_size_t, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -97,7 +99,8 @@ def _declare(lib):
 EXPORTED = ["rsx_version", "rsx_csr_schedule_host", "rsx_spmm", "rsx_rowwise", "rsx_bpr_ws_bytes", "rsx_bpr",
             "rsx_fullsort_ws_bytes", "rsx_fullsort_topk", "rsx_score_dense", "rsx_sample_triplets",
             "rsx_gather_rows", "rsx_lightgcn_step", "rsx_lightgcn_forward", "rsx_sample_epoch",
-            "rsx_smore_spectral_fwd", "rsx_smore_spectral_bwd", "rsx_smore_spectral_bwd_partials"]
+            "rsx_smore_spectral_fwd", "rsx_smore_spectral_bwd", "rsx_smore_spectral_bwd_partials",
+            "rsx_topk_metrics_ws_bytes", "rsx_topk_metrics"]
 
 
 def lib_path() -> str:

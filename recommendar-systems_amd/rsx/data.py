@@ -285,6 +285,18 @@ class EvalDataLoader(_Loader):
         self.pr += self.step
         return [users, mask]
 
+    def eval_csr(self):
+        """Held-out items per evaluation user as a device CSR, sorted within each user
+        (rsx_topk_metrics' binary search); built on first use."""
+        if getattr(self, "_eval_csr", None) is None:
+            lens = np.asarray(self.eval_len_list, dtype=np.int64)
+            rp = np.zeros(lens.size + 1, dtype=np.int64)
+            np.cumsum(lens, out=rp[1:])
+            col = (np.concatenate([np.sort(np.asarray(x, dtype=np.int64)) for x in self.eval_items_per_u])
+                   if len(self.eval_items_per_u) else np.zeros(0, np.int64)).astype(np.int32)
+            self._eval_csr = (torch.from_numpy(rp).to(self.device), torch.from_numpy(col).to(self.device))
+        return self._eval_csr
+
     def get_eval_items(self):
         return self.eval_items_per_u
 

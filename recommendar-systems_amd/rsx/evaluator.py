@@ -107,5 +107,38 @@ class TopKEvaluator:
     def evaluate(self, batch_matrix_list, eval_data, is_test=False, idx=0):
         import torch
 
-        topk = torch.cat(batch_matrix_list, dim=0).cpu().numpy()
-        return self.evaluate_arrays(topk, eval_data.get_eval_items(), eval_data.get_eval_len_list())
+        topk = torch.cat(batch_matrix_list, dim=0)
+        if topk.is_cuda and hasattr(eval_data, "eval_csr"):
+            return self.evaluate_device(topk, eval_data)
+        return self.evaluate_arrays(topk.cpu().numpy(), eval_data.get_eval_items(), eval_data.get_eval_len_list())
+
+    def evaluate_device(self, topk, eval_data) -> dict:
+        """The same dict from device-resident top-k lists (rsx_topk_metrics): hits by
+        binary search in each user's sorted held-out items, per-user float64 values,
+        user-ordered column sums (= numpy's mean(axis=0) order), then the reference's
+        division and round(., 4) here.  One [5, n_cut] float64 copy to the host."""
+        import torch
+
+        from . import ops
+
+        k = topk.shape[1]
+        cuts = sorted(set(int(c) for c in self.topk))
+        if cuts[-1] > k:
+            raise ValueError(f"topk {cuts[-1]} > ranked list length {k}")
+        ranks = np.arange(1, k + 1, dtype=np.float64)
+        gain = torch.from_numpy(1.0 / np.log2(ranks + 1)).to(topk.device)   # as metrics.py ndcg
+        erp, ecol = eval_data.eval_csr()
+        sums = ops.topk_metrics(topk, erp, ecol, cuts, gain).cpu().numpy()
+        n = topk.shape[0]
+        pos_total = int(np.asarray(eval_data.get_eval_len_list()).sum())
+        col = {c: j for j, c in enumerate(cuts)}
+        rows = {"recall": 0, "precision": 1, "ndcg": 2, "map": 3}
+        out = {}
+        for m in self.metrics:
+            for kk in self.topk:
+                j = col[int(kk)]
+                v = sums[4, j] / np.float64(pos_total) if m == "recall2" else sums[rows[m], j] / np.float64(n)
+                # numpy's round on the float64, as the reference's round(value[k - 1], 4)
+                # (scale, round half to even): 0.05875 -> 0.0588, where float rounding gives 0.0587
+                out[f"{m}@{kk}"] = float(round(np.float64(v), 4))
+        return out

@@ -237,6 +237,26 @@ def fullsort_topk(user_emb: torch.Tensor, users: torch.Tensor | None, item_emb: 
     return val, idx
 
 
+def topk_metrics(topk_idx: torch.Tensor, eval_rowptr: torch.Tensor, eval_col: torch.Tensor, cutoffs,
+                 gain: torch.Tensor) -> torch.Tensor:
+    """Per-cutoff sums over users of recall, precision, ndcg, map and hit count
+    (rsx_topk_metrics; reference topk_evaluator.py:58-102 + metrics.py:12-118).
+    Returns a float64 device tensor [5, len(cutoffs)]."""
+    _gpu(topk_idx, eval_rowptr, eval_col, gain)
+    if topk_idx.dtype != torch.int64 or topk_idx.dim() != 2:
+        raise RuntimeError("topk_metrics: topk_idx must be int64 [n_users, k]")
+    topk_idx = topk_idx.contiguous()
+    n, k = topk_idx.shape
+    dev = topk_idx.device
+    cut = torch.tensor(list(cutoffs), dtype=torch.int32, device=dev)
+    out = torch.empty(5, cut.numel(), dtype=torch.float64, device=dev)
+    lib = L.lib()
+    ws = _ws(dev, lib.rsx_topk_metrics_ws_bytes(n, cut.numel()))
+    L.check(lib.rsx_topk_metrics(_p(topk_idx), n, k, _p(eval_rowptr), _p(eval_col), _p(cut), cut.numel(), _p(gain),
+                                 _p(out), _p(ws), ws.numel(), _stream()), "rsx_topk_metrics")
+    return out
+
+
 def score_dense(user_emb: torch.Tensor, users: torch.Tensor | None, item_emb: torch.Tensor) -> torch.Tensor:
     """scores = user_emb[users] @ item_emb.T (reference lightgcn.py:164)."""
     _gpu(user_emb, users, item_emb)

@@ -10,7 +10,7 @@ import pytest
 import torch
 
 import rsx_oracle as O
-from helpers import coo_from, eval_lists, params, topk_equal_modulo_ties, train_mask_pairs
+from helpers import coo_from, eval_lists, metric_dict, params, topk_equal_modulo_ties, train_mask_pairs
 from rsx import _lib as L
 from rsx import graph, ops
 
@@ -254,3 +254,73 @@ def test_sample_epoch_matches_per_batch(cuda, golden):
         a = ops.DeviceSampler.batch_view(buf, s.n_inter, 512, j).cpu()
         b = s.sample(epoch=3, start=start, batch=512).cpu()
         assert torch.equal(a, b)
+
+
+class _EvalStub:
+    """The two EvalDataLoader members the device metric path reads."""
+
+    def __init__(self, items, dev):
+        import torch
+
+        self.lens = np.array([len(x) for x in items], dtype=np.int64)
+        rp = np.concatenate([[0], np.cumsum(self.lens)]).astype(np.int64)
+        col = np.concatenate([np.sort(np.asarray(x, np.int64)) for x in items]).astype(np.int32)
+        self.csr = (torch.from_numpy(rp).to(dev), torch.from_numpy(col).to(dev))
+
+    def eval_csr(self):
+        return self.csr
+
+    def get_eval_len_list(self):
+        return self.lens
+
+
+@pytest.mark.parametrize("fx", ["lightgcn_small", "layergcn_small", "layergcn_drop_small", "smore_small"])
+def test_topk_metrics_device_equals_reference_dicts(cuda, golden, fx):
+    """rsx_topk_metrics + the evaluator's rounding == the reference's metric dicts (bit-exact)."""
+    import torch
+
+    from rsx.config import Config
+    from rsx.evaluator import TopKEvaluator
+
+    z = golden(fx)
+    ev = TopKEvaluator(Config("LightGCN", "baby", {"use_gpu": False}))
+    tags = [k[: -len("_metric_keys")] for k in z if k.endswith("_metric_keys")]
+    for tag in tags:
+        split = "test" if tag.endswith("test") else "valid"
+        stub = _EvalStub(eval_lists(z, split), cuda)
+        topk = torch.from_numpy(z[tag + "_topk_idx"].astype(np.int64)).to(cuda)
+        assert ev.evaluate_device(topk, stub) == metric_dict(z, tag), tag
+
+
+def test_topk_metrics_device_bitwise_vs_numpy(cuda):
+    """Large random case: the per-cutoff means before rounding equal the numpy restatement
+    (reference metrics.py formulas, mean over users in numpy's order) bit for bit."""
+    import torch
+
+    from rsx import evaluator as E
+    from rsx import ops
+
+    rng = np.random.default_rng(5)
+    n, k, ni = 6000, 50, 3000
+    items = [rng.choice(ni, size=int(rng.integers(1, 40)), replace=False) for _ in range(n)]
+    rows = []
+    for x in items:  # each ranked list: up to 10 true items, then distinct non-items, shuffled within the top 20
+        first = x[: int(rng.integers(0, min(10, x.size) + 1))]
+        rest = rng.permutation(np.setdiff1d(np.arange(ni), x))[: k - first.size]
+        r = np.concatenate([first, rest])
+        rng.shuffle(r[:20])
+        rows.append(r)
+    topk = np.stack(rows)
+    pos = np.array([len(x) for x in items])
+    hit = E.hit_matrix(topk, items)
+    cuts = [1, 5, 10, 20, 50]
+    stub = _EvalStub(items, cuda)
+    gain = torch.from_numpy(1.0 / np.log2(np.arange(1, k + 1, dtype=np.float64) + 1)).to(cuda)
+    sums = ops.topk_metrics(torch.from_numpy(topk.astype(np.int64)).to(cuda), *stub.eval_csr(), cuts, gain).cpu().numpy()
+    for row, fn in enumerate((E.recall, E.precision, E.ndcg, E.average_precision)):
+        want = fn(hit, pos)
+        for j, c in enumerate(cuts):
+            assert sums[row, j] / n == want[c - 1], (fn.__name__, c)
+    want2 = E.recall2(hit, pos)
+    for j, c in enumerate(cuts):
+        assert sums[4, j] / pos.sum() == want2[c - 1]
