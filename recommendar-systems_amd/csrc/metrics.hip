@@ -59,6 +59,24 @@ __global__ __launch_bounds__(256) void metrics_user(const int64_t* __restrict__ 
     }
 }
 
+template <int T>
+__device__ __forceinline__ double lane_d(double x) {
+    const uint64_t b = (uint64_t)__double_as_longlong(x);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, T);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), T);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+template <int T>
+__device__ __forceinline__ double add_from(double s, double x) {
+    if constexpr (T == 64) {
+        return s;
+    } else {
+        return add_from<T + 1>(s + lane_d<T>(x), x);
+    }
+}
+// s + x[lane 0] + x[lane 1] + ... + x[lane 63], in that order (constant-lane reads)
+__device__ __forceinline__ double add_lanes(double s, double x) { return add_from<0>(s, x); }
+
 // One wavefront per column: the 64 lanes load 64 users' values at a time (the next
 // chunk is loaded before this one is added), then every lane adds them in user
 // order from registers (shuffles): the serial chain is adds only, no load latency.
@@ -70,8 +88,9 @@ __global__ __launch_bounds__(64) void metrics_sum(const double* __restrict__ val
     for (int64_t base = 0; base < n; base += 64) {
         const int64_t nx = base + 64 + lane;
         const double nxt = nx < n ? vals[nx * m + j] : 0.0;
-        const int cnt = (int)(n - base < 64 ? n - base : 64);
-        for (int t = 0; t < cnt; ++t) s += __shfl(cur, t, kWave);
+        // lanes past the end hold 0.0: adding +0.0 leaves s unchanged bit for bit
+        // (s is never -0.0 here: it starts at +0.0 and the values are >= 0)
+        s = add_lanes(s, cur);
         cur = nxt;
     }
     if (lane == 0) out[j] = s;
