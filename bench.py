@@ -186,19 +186,72 @@ def bench_model(args):
     print(json.dumps(out), flush=True)
 
 
+def _c4_chunk(args):
+    from rsx import synth
+
+    c, cdf = args
+    u, i, lab = synth.chunk_graph(c, synth.C4["chunk_users"], synth.C4["n_items"], synth.C4["avg"], cdf)
+    return c, u, i, lab
+
+
+def load_graph(workload, rank, world, c4_chunks=None):
+    """(train users, train items, valid users, valid items, n_users, n_items, d, desc) of
+    this rank.  c2: every rank owns its own sports-shaped block of users (rank-seeded)
+    over the same items (weak scaling).  c4: the fixed 10M-user graph, whose 8
+    user chunks are dealt to the ranks in contiguous ranges (local user ids)."""
+    from rsx import synth
+
+    if workload == "c2":
+        nu0, ni, ne0 = synth.SHAPES["sports"]
+        df = synth.amazon_like(nu0, ni, ne0, seed=rank)
+        tr, va = df[df.x_label == 0], df[df.x_label == 1]
+        return (tr.userID.values.astype(np.int64), tr.itemID.values.astype(np.int64),
+                va.userID.values.astype(np.int64), va.itemID.values.astype(np.int64),
+                int(df.userID.max()) + 1, ni, 64,
+                "C2: LightGCN K=3 d=64, sports-shaped (35,598 users x 18,357 items per rank), B=2048 per rank, "
+                "device sampler, fused step")
+    import multiprocessing as mp
+
+    C = synth.C4
+    n_chunks = c4_chunks or C["n_users"] // C["chunk_users"]
+    c0, c1 = rank * n_chunks // world, (rank + 1) * n_chunks // world
+    cdf = synth.zipf_cdf(C["n_items"], 0)
+    with mp.get_context("fork").Pool(min(8, c1 - c0)) as pool:  # before any GPU use in this process
+        parts = sorted(pool.map(_c4_chunk, [(c, cdf) for c in range(c0, c1)]), key=lambda x: x[0])
+    tu, ti, vu, vi = [], [], [], []
+    for c, u, i, lab in parts:
+        off = (c - c0) * C["chunk_users"]
+        tr, va = lab == 0, lab == 1
+        tu.append(u[tr] + off)
+        ti.append(i[tr])
+        vu.append(u[va] + off)
+        vi.append(i[va])
+    return (np.concatenate(tu), np.concatenate(ti), np.concatenate(vu), np.concatenate(vi),
+            (c1 - c0) * C["chunk_users"], C["n_items"], 256,
+            "C4: LightGCN K=3 d=256, synthetic 10M users x 1M items (~10 interactions/user, Zipf(0.8) items; "
+            "reference split rule), users row-sharded over the ranks, items replicated, B=2048 per rank")
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", default="c2", choices=["c2", "c1", "c3"],
-                    help="c2 (default): the headline LightGCN sports config; c1/c3: LayerGCN / SMORE on baby")
+    ap.add_argument("--workload", default="c2", choices=["c2", "c1", "c3", "c4"],
+                    help="c2 (default): the headline LightGCN sports config; c1/c3: LayerGCN / SMORE on baby; "
+                         "c4: LightGCN d=256 on the 10M-user graph, row-sharded")
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=None, help="default 200 (c4: 20)")
+    ap.add_argument("--warmup", type=int, default=None, help="default 20 (c4: 3)")
     ap.add_argument("--batch", type=int, default=2048)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
-    ap.add_argument("--eval-users", type=int, default=0, help="0 = all valid users")
+    ap.add_argument("--eval-users", type=int, default=None, help="default: all valid users (c4: 32768 per rank)")
+    ap.add_argument("--c4-chunks", type=int, default=None,
+                    help="c4: build only the first N of the 8 1.25M-user chunks (1 = one rank's share at 8 GPUs)")
     args = ap.parse_args()
-    if args.workload != "c2":
+    big = args.workload == "c4"
+    args.steps = args.steps if args.steps is not None else (20 if big else 200)
+    args.warmup = args.warmup if args.warmup is not None else (3 if big else 20)
+    args.eval_users = args.eval_users if args.eval_users is not None else (32768 if big else 0)
+    if args.workload in ("c1", "c3"):
         if int(os.environ.get("WORLD_SIZE", "1")) != 1:
             raise SystemExit("--workload c1/c3 are single-GPU legs")
         return bench_model(args)
@@ -206,35 +259,41 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    tu, ti, vu_all, vi_all, nu, ni, d, desc = load_graph(args.workload, rank, world, args.c4_chunks)
+    if big and args.c4_chunks:
+        desc += f" [only {args.c4_chunks} of 8 user chunks built]"
+    sharded = world > 1 or big
+    if sharded:
         import torch.distributed as dist
 
+        if world == 1:  # a one-rank group for the sharded engine
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 1000))
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
 
-    from rsx import synth
     from rsx.engine import LightGCNEngine
     from rsx import graph, ops
 
-    nu0, ni, ne0 = synth.SHAPES["sports"]
-    df = synth.amazon_like(nu0, ni, ne0, seed=rank)
-    tr = df[df.x_label == 0]
-    tu = tr.userID.values.astype(np.int64)
-    ti = tr.itemID.values.astype(np.int64)
-    va = df[df.x_label == 1]
-    nu = int(df.userID.max()) + 1
     torch.manual_seed(999 + rank)
-    U0 = torch.nn.init.xavier_uniform_(torch.empty(nu, 64)).numpy()
-    I0 = torch.nn.init.xavier_uniform_(torch.empty(ni, 64)).numpy()
+    if big:  # xavier_uniform_ bound for [n, d]: sqrt(6 / (n + d)); drawn on the device
+        U0 = ((torch.rand(nu, d, device=dev) * 2 - 1) * (6.0 / (nu + d)) ** 0.5).cpu()
+        I0 = ((torch.rand(ni, d, device=dev) * 2 - 1) * (6.0 / (ni + d)) ** 0.5).cpu()
+    else:
+        U0 = torch.nn.init.xavier_uniform_(torch.empty(nu, d)).numpy()
+        I0 = torch.nn.init.xavier_uniform_(torch.empty(ni, d)).numpy()
 
-    if world > 1:
+    if sharded:
         from rsx.dist import ShardedLightGCNEngine
 
-        eng = ShardedLightGCNEngine(tu, ti, nu, ni, 64, 3, 1e-2, 1e-3, dev, U0, I0, seed=rank,
+        eng = ShardedLightGCNEngine(tu, ti, nu, ni, d, 3, 1e-2, 1e-3, dev, U0, I0, seed=rank,
                                     batch=args.batch)
     else:
-        eng = LightGCNEngine(tu, ti, nu, ni, 64, 3, 1e-2, 1e-3, dev, U0, I0, seed=0, batch=args.batch)
+        eng = LightGCNEngine(tu, ti, nu, ni, d, 3, 1e-2, 1e-3, dev, U0, I0, seed=0, batch=args.batch)
+    del U0, I0
     E = eng.n_inter
     parts = [eng.adj] if hasattr(eng, "adj") else [eng.A_U, eng.A_I]
     nnz = sum(a.nnz for a in parts)
@@ -281,7 +340,7 @@ def main():
     loss_mean = float(eng.loss_acc.item()) / max(eng.step_count, 1)
 
     # full-sort evaluation throughput (forward once + fused MFMA scores/mask/top-50)
-    vusers = np.unique(va.userID.values)
+    vusers = np.unique(vu_all)
     if args.eval_users:
         vusers = vusers[: args.eval_users]
     rp, mc = graph.history_csr(tu, ti, nu)
@@ -289,10 +348,12 @@ def main():
     vu_d = torch.from_numpy(vusers.astype(np.int64)).to(dev)
 
     # held-out (valid) items per evaluation user, sorted: the metric tail's CSR
-    vdf = va[va.userID.isin(vusers)].sort_values(["userID", "itemID"])
-    vlen = np.bincount(np.searchsorted(vusers, vdf.userID.values), minlength=vusers.size)
+    sel = np.isin(vu_all, vusers)
+    order = np.lexsort((vi_all[sel], vu_all[sel]))
+    v_u, v_i = vu_all[sel][order], vi_all[sel][order]
+    vlen = np.bincount(np.searchsorted(vusers, v_u), minlength=vusers.size)
     erp = torch.from_numpy(np.concatenate([[0], np.cumsum(vlen)]).astype(np.int64)).to(dev)
-    ecol = torch.from_numpy(vdf.itemID.values.astype(np.int32)).to(dev)
+    ecol = torch.from_numpy(v_i.astype(np.int32)).to(dev)
     gain = torch.from_numpy(1.0 / np.log2(np.arange(1, 51, dtype=np.float64) + 1)).to(dev)
 
     def evaluate():
@@ -322,29 +383,29 @@ def main():
     # fused scores + mask + top-50 over all evaluation users (MFMA roofline)
     f = eng.forward()
     fs_ms = time_kernel(lambda: ops.fullsort_topk(f[:nu], vu_d, f[nu:], rp_d, mc_d, 50), 10)
-    fs_flops = 2.0 * 64 * ni * vu_d.numel()
+    fs_flops = 2.0 * d * ni * vu_d.numel()
 
     # dominant kernel: one propagation SpMM (STORE epilogue), same stream as the step
     x = eng.p
-    ys = [torch.empty(a.n_rows, 64, device=dev) for a in parts]
+    ys = [torch.empty(a.n_rows, d, device=dev) for a in parts]
 
     def run_parts():
         for a, y in zip(parts, ys):
             a.spmm(x, out=y)
 
     spmm_ms = time_kernel(run_parts, 50)
-    alg = spmm_bytes(nu + ni, nnz, 64)
+    alg = spmm_bytes(nu + ni, nnz, d)
     achieved = alg / (spmm_ms * 1e-3) / 1e9
     traffic = None
     tfile = os.path.join(HERE, "profiles", "spmm_traffic.json")
-    if os.path.exists(tfile):
+    if os.path.exists(tfile) and not big:  # PMC bytes measured for the C2 launch
         try:
             traffic = json.load(open(tfile)).get("bytes_per_launch")
         except Exception:  # noqa: BLE001
             traffic = None
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not big:
         cpu = cpu_baseline((tu, ti), nu, ni, args.cpu_budget)
 
     if rank == 0:
@@ -361,12 +422,13 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic Amazon-sports-shaped graph (rsx.synth, seed=rank; Zipf(0.8) items, 5-core users, "
-                    "reference split rule); xavier-uniform init, seed 999",
-            "config": {"workload": "C2: LightGCN K=3 d=64, sports-shaped (35,598 users x 18,357 items per rank), "
-                                   "B=2048 per rank, device sampler, fused step",
-                       "model": "LightGCN", "n_layers": 3, "embedding_size": 64, "global_batch": args.batch * world,
-                       "parallelism": f"rowshard{world}" if world > 1 else "single"},
+            "data": ("synthetic Amazon-sports-shaped graph (rsx.synth, seed=rank; Zipf(0.8) items, 5-core users, "
+                     "reference split rule); xavier-uniform init, seed 999") if not big else
+                    ("synthetic C4 graph (rsx.synth.chunk_graph: 8 seeded 1.25M-user chunks, Zipf(0.8) items, "
+                     "5+Geometric degrees mean 10, reference split rule); xavier-uniform-bound init"),
+            "config": {"workload": desc, "model": "LightGCN", "n_layers": 3, "embedding_size": d,
+                       "global_batch": args.batch * world,
+                       "parallelism": f"rowshard{world}" if sharded else "single"},
             "fullsort_items_per_s": items_per_s,
             "fullsort": {"eval_users": int(n_eval), "n_items": ni, "k": 50,
                          "s_per_eval": eval_s,
@@ -374,11 +436,12 @@ def main():
                          "kernel_ms_all_eval_users": fs_ms,
                          "kernel_tflops": fs_flops / (fs_ms * 1e-3) / 1e12,
                          "mfma_f32_peak_tflops": 157.3},
-            "roofline": {"bound": "hbm", "kernel": "spmm_main<64,STORE> (+fixup) one propagation layer",
+            "roofline": {"bound": "hbm", "kernel": f"spmm_main<{d},STORE> (hub-row fixups in-launch) one propagation layer",
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "algorithmic_bytes_per_launch": alg, "avg_launch_ms": spmm_ms,
-                         "note": "sports working set (<50 MB) is Infinity-Cache resident"},
+                         "note": ("sports working set (<50 MB) is Infinity-Cache resident" if not big else
+                                  "C4 shard: tables of GBs, gathers from HBM")},
             "cpu_baseline": cpu,
             "gpu_ms_per_step_events": gpu_ms / args.steps,
             "train_loss_mean": loss_mean,

@@ -51,6 +51,9 @@ class HipBackend:
     def tensor(self, a):
         return torch.as_tensor(a).to(self.device)
 
+    def zeros(self, rows, d):
+        return torch.zeros(rows, d, dtype=torch.float32, device=self.device)
+
     def csr(self, rowptr, col, val, n_cols, chunk=32):
         return ops.DeviceCSR(rowptr, col, val, n_cols, self.device, chunk)
 
@@ -110,7 +113,10 @@ class ShardedLightGCNEngine:
         it = self._broadcast_host(it)
         p = torch.cat([torch.from_numpy(np.ascontiguousarray(user_emb, dtype=np.float32)), it])
         self.p = self.be.tensor(p)
-        z = lambda rows=n: self.be.tensor(torch.zeros(rows, d, dtype=torch.float32))  # noqa: E731
+        if hasattr(self.be, "zeros"):
+            z = lambda rows=n: self.be.zeros(rows, d)  # noqa: E731
+        else:
+            z = lambda rows=n: self.be.tensor(torch.zeros(rows, d, dtype=torch.float32))  # noqa: E731
         self.m, self.v, self.s, self.h0, self.h1 = z(), z(), z(), z(), z()
         self.final, self.g, self.r = z(), z(), z()
         self.t = z(ni)

@@ -148,3 +148,36 @@ def features(n_items: int, dim: int, seed: int, l2_normalise: bool = False) -> n
     if l2_normalise:
         x /= np.linalg.norm(x, axis=1, keepdims=True)
     return x
+
+
+# C4: 10M users x 1M items, ~10 interactions per user (1e8), Zipf(0.8)
+# items.  The global graph is a fixed sequence of user chunks, each generated from
+# its own seed, so a rank owning chunks [c0, c1) builds exactly its share of the
+# same graph whatever the world size.
+C4 = dict(n_users=10_000_000, n_items=1_000_000, avg=10.0, chunk_users=1_250_000)
+
+
+def zipf_cdf(n_items: int, seed: int, zipf: float = 0.8) -> np.ndarray:
+    """Cumulative Zipf(zipf) popularity over a seeded random permutation of item ids."""
+    rng = np.random.default_rng([seed, 0x5EED])
+    perm = rng.permutation(n_items)
+    w = np.empty(n_items, dtype=np.float64)
+    w[perm] = 1.0 / np.power(np.arange(1, n_items + 1, dtype=np.float64), zipf)
+    cdf = np.cumsum(w)
+    cdf /= cdf[-1]
+    return cdf
+
+
+def chunk_graph(chunk: int, chunk_users: int, n_items: int, avg: float, cdf: np.ndarray, seed: int = 0):
+    """Interactions of users [chunk*chunk_users, (chunk+1)*chunk_users) as
+    (user - chunk*chunk_users, item, x_label) arrays, grouped by user.  Degrees are
+    5 + Geometric (mean `avg`); duplicate draws of a user are dropped (so the mean
+    lands slightly below `avg`); labels follow the reference split rule."""
+    rng = np.random.default_rng([seed, chunk])
+    p = 1.0 / max(avg - 4.0, 1.0 + 1e-9)
+    deg = 5 + rng.geometric(p, size=chunk_users) - 1
+    u = np.repeat(np.arange(chunk_users, dtype=np.int64), deg)
+    i = np.minimum(np.searchsorted(cdf, rng.random(u.size), side="right"), n_items - 1).astype(np.int64)
+    key = np.unique(u * n_items + i)  # sorted by (user, item), duplicates dropped
+    u, i = key // n_items, key % n_items
+    return u, i, split_labels(u)
