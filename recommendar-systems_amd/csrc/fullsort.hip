@@ -7,22 +7,22 @@
 //     _, topk = torch.topk(scores, k, dim=-1)      (trainer.py:526)
 // without materialising the [B_u, n_items] score matrix.
 //
-// Kernel 1 (fs_tiles): grid = (user blocks of 32*NW users) x (item chunks).  Each
-// wavefront owns 32 users; the NW waves of a block share 32-item tiles staged in
-// LDS (double buffered, row stride D+4 floats so the 32 lanes of a half-wave hit
-// 32 distinct 4-bank slots).  A 32x32 score tile is D/2 v_mfma_f32_32x32x2_f32 —
-// exact f32 fma chains, A = item rows, B = user rows, with the reduction index k
-// permuted so that lane-half h reads the contiguous half [h*D/2, (h+1)*D/2) of its
-// row.  The C/D layout puts user j = lane&31 on the lane and 16 items in the
-// registers, so lanes j and j+32 together hold the tile's 32 scores of user j.
-// Scores above the user's running threshold go into a per-user LDS candidate
-// buffer as 64-bit keys (ordered score bits << 32 | ~item), so one u64 order is
-// (score desc, index asc); when a buffer may overflow the wave bitonic-sorts it
-// and keeps the top K, which also raises the threshold.  Items arrive in
-// ascending index order within a chunk, so the strict "> threshold" filter drops
-// nothing that the canonical order would keep.
-// Kernel 2 (fs_select): one wavefront per user (full occupancy) takes the exact
-// top-K over every chunk's raw candidates and rank-sorts it.
+// Kernel 1 (fs_tiles): grid = (blocks of 32 users) x (item chunks), one wavefront
+// per block, no LDS candidate buffers and no barriers, so two waves share every
+// SIMD (d <= 64) and the hardware overlaps one wave's selection work with the
+// other's MFMA chain.  A 32x32 score tile is D/2 v_mfma_f32_32x32x2_f32 — exact f32
+// fma chains, A = item rows (straight from L2 into double-buffered registers),
+// B = user rows (registers), reduction index permuted so lane-half h reads the
+// contiguous half of its row.  Lanes j and j+32 hold the tile's 32 scores of user
+// j.  Scores above the user's running threshold are appended, as 64-bit keys
+// (ordered score bits << 32 | ~item: one u64 order = score desc, index asc), to the
+// user's candidate row in the workspace (L2-resident); a lane walks only its set
+// bits, reading its scores back from a small LDS scratch.  When a row may overflow,
+// the wave radix-selects its k-th key with ballots, compacts the row to the top k
+// and raises the threshold.  Items arrive in ascending index order within a chunk,
+// so the strict "> threshold" filter drops nothing the canonical order would keep.
+// Kernel 2 (fs_select): one wavefront per user takes the exact top-K over every
+// chunk's list (each already cut to its top k) and rank-sorts it.
 #include <climits>
 #include <cstdlib>
 
@@ -33,8 +33,9 @@ namespace rsx {
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef unsigned long long u64;
 
-constexpr int kCap = 128;  // candidate slots per user (>= K + 32)
-constexpr int kMaxK = kCap - 32;
+constexpr int kCap = 256;   // candidate slots per (user, chunk) row; compaction when > kCap - 32
+constexpr int kNK = kCap / 64;  // candidate keys per lane while compacting
+constexpr int kMaxK = 96;     // k limit: a chunk's final list (<= k) is <= 2 keys per lane in fs_select
 
 __device__ __forceinline__ unsigned ord_f32(float f) {
     const unsigned u = __float_as_uint(f);
@@ -109,99 +110,124 @@ struct FsArgs {
     int mode;  // profiling ablation (RSX_FS_MODE): 0 full, 1 scores only, 2 no compaction, 3 no final emit
 };
 
-constexpr int kStride = kCap + 1;  // u64 slots per user row in LDS (+1: spreads the 32 users over banks)
 
 __device__ __forceinline__ int popc64(u64 x) { return __popcll(x); }
 __device__ __forceinline__ u64 lanemask_lt(int lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
 
-// Shrink one user's buffer (k < n <= kCap unique nonzero keys) to exactly its top k,
-// compacted to the front, and return the k-th key's score (the new threshold).
-// Each lane ranks its two keys against every buffered key, read back as LDS
-// broadcasts (same address in all lanes): n/2 rounds of independent 64-bit compares,
-// no ballot/scalar dependency chain.  Keys are unique, so ranks are exact.
+__device__ __forceinline__ u64 ld_u64_l2(const u64* p) {  // bypasses the CU's L1 (L2-served)
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+
+// Shrink one user's buffer (k < n <= kCap unique nonzero keys, in global memory) to
+// exactly its top k, compacted to the front, and return the k-th key's score (the
+// new threshold).  The wave loads the buffer coalesced (two keys per lane; empty
+// slots read as 0, which no valid key is) and finds the k-th largest key by a
+// bitwise radix search with ballots: 32 rounds on the ordered-score word (one VALU
+// compare per key pair and scalar counting per round), and 32 more on the index
+// word only when several keys share the boundary score.  Every round is a handful
+// of instructions, so the selection costs a fraction of an all-pairs rank count.
 __device__ __forceinline__ float compact_slot(u64* buf, int n, int k, int lane, int* new_cnt) {
-    const u64 e0 = lane < n ? buf[lane] : ~0ull;  // ~0: never kept, never counted
-    const u64 e1 = lane + 64 < n ? buf[lane + 64] : ~0ull;
-    int r0 = 0, r1 = 0;
-    int i = 0;
-#pragma unroll 4
-    for (; i + 1 < n; i += 2) {
-        const u64 x = buf[i], y = buf[i + 1];
-        r0 += (int)(x > e0) + (int)(y > e0);
-        r1 += (int)(x > e1) + (int)(y > e1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's inserts are in L2
+    u64 x[kNK];
+    unsigned hw[kNK];
+#pragma unroll
+    for (int q = 0; q < kNK; ++q) {
+        x[q] = lane + 64 * q < n ? ld_u64_l2(buf + lane + 64 * q) : 0ull;
+        hw[q] = (unsigned)(x[q] >> 32);
     }
-    if (i < n) {
-        const u64 x = buf[i];
-        r0 += (int)(x > e0);
-        r1 += (int)(x > e1);
+    unsigned th = 0;
+    for (int bit = 31; bit >= 0; --bit) {
+        const unsigned c = th | (1u << bit);
+        int m = 0;
+#pragma unroll
+        for (int q = 0; q < kNK; ++q) m += popc64(__ballot(hw[q] >= c));
+        if (m >= k) th = c;
     }
-    const bool k0 = lane < n && r0 < k;
-    const bool k1 = lane + 64 < n && r1 < k;
-    // threshold = the key of rank k-1
-    const u64 w0 = __ballot(k0 && r0 == k - 1), w1 = __ballot(k1 && r1 == k - 1);
-    u64 T;
-    if (w0) {
-        const int src = __ffsll((long long)w0) - 1;
-        T = ((u64)__builtin_amdgcn_readlane((int)(e0 >> 32), src) << 32) |
-            (unsigned)__builtin_amdgcn_readlane((int)e0, src);
-    } else {
-        const int src = __ffsll((long long)w1) - 1;
-        T = ((u64)__builtin_amdgcn_readlane((int)(e1 >> 32), src) << 32) |
-            (unsigned)__builtin_amdgcn_readlane((int)e1, src);
+    // th = the k-th largest score word
+    int gt = 0, eq = 0;
+#pragma unroll
+    for (int q = 0; q < kNK; ++q) {
+        gt += popc64(__ballot(hw[q] > th));
+        eq += popc64(__ballot(hw[q] == th));
     }
-    const u64 b0 = __ballot(k0), b1 = __ballot(k1);
+    const int need = k - gt;  // keys with score word th that are kept
+    unsigned tl = 0;          // keep (th, lo >= tl); 0 keeps the whole tie group
+    if (eq != need) {
+        for (int bit = 31; bit >= 0; --bit) {
+            const unsigned c = tl | (1u << bit);
+            int m = 0;
+#pragma unroll
+            for (int q = 0; q < kNK; ++q) m += popc64(__ballot(hw[q] == th && (unsigned)x[q] >= c));
+            if (m >= need) tl = c;
+        }
+    }
+    const u64 T = ((u64)th << 32) | tl;
     const u64 lt = lanemask_lt(lane);
-    const int p0 = popc64(b0 & lt);
-    const int p1 = popc64(b0) + popc64(b1 & lt);
-    __builtin_amdgcn_wave_barrier();
-    if (k0) buf[p0] = e0;
-    if (k1) buf[p1] = e1;
-    __builtin_amdgcn_wave_barrier();
-    *new_cnt = popc64(b0) + popc64(b1);
+    int base = 0;
+#pragma unroll
+    for (int q = 0; q < kNK; ++q) {
+        const bool kp = x[q] != 0ull && x[q] >= T;
+        const u64 bq = __ballot(kp);
+        if (kp) buf[base + popc64(bq & lt)] = x[q];
+        base += popc64(bq);
+    }
+    *new_cnt = base;
     return key_score(T);
 }
 
 // One wavefront per block, no barriers: the wave owns 32 users and walks its item
 // chunk in 32-item tiles.  A operands (item rows) come straight from L2 into a
-// double-buffered register set (lane l: item l&31, floats [h*D/2 + 32c, +32)),
-// prefetched one 32-float chunk ahead of the MFMAs that consume the current one.
-// Waves never wait on each other, so one wave's candidate compaction overlaps the
-// other waves' MFMA streams.
+// double-buffered register set (lane l: item l&31, floats [h*D/2 + CW*c, +CW)),
+// prefetched one chunk ahead of the MFMAs that consume the current one; rows past
+// the chunk are clamped to a valid row and zeroed, so the load is branch-free.
 template <int D, int CW>
-__device__ __forceinline__ void load_chunk(float (&r)[CW], const float* I, int64_t item, int64_t i1, int off) {
-    if (item < i1) {
-        const float* p = I + item * D + off;
+__device__ __forceinline__ void load_chunk(float (&r)[CW], const float* I, int64_t item, int64_t i1, int64_t ni,
+                                           int off) {
+    const bool ok = item < i1;
+    const float* p = I + (ok ? item : ni - 1) * D + off;
 #pragma unroll
-        for (int q = 0; q < CW / 4; ++q) {
-            const float4 v = ld4(p + 4 * q);
-            r[4 * q] = v.x;
-            r[4 * q + 1] = v.y;
-            r[4 * q + 2] = v.z;
-            r[4 * q + 3] = v.w;
-        }
-    } else {
-#pragma unroll
-        for (int q = 0; q < CW; ++q) r[q] = 0.f;
+    for (int q = 0; q < CW / 4; ++q) {
+        const float4 v = ld4(p + 4 * q);
+        r[4 * q] = ok ? v.x : 0.f;
+        r[4 * q + 1] = ok ? v.y : 0.f;
+        r[4 * q + 2] = ok ? v.z : 0.f;
+        r[4 * q + 3] = ok ? v.w : 0.f;
     }
 }
 
-template <int D>
-__global__ __launch_bounds__(64) void fs_tiles(FsArgs a) {
+template <int V>
+struct IntC {
+    static constexpr int value = V;
+};
+
+// No LDS and no block barrier: the candidate buffers live in the workspace (one
+// [kCap] row per (user, chunk), L2-resident), so two wavefronts fit on every SIMD
+// (VGPRs permitting) and the hardware interleaves them: one wave's filtering and
+// compaction issue while the other's MFMA chain runs.  Mask cursor and compaction
+// are per-lane / per-user branches; the MFMA chain of tile t is issued before the
+// filter of tile t-1 so the VALU work starts as soon as the previous scores exist.
+template <int D, int MODE>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D <= 64 ? 2 : 1))) void fs_tiles(FsArgs a) {
     constexpr int HALF = D / 2;
     constexpr int CW = HALF < 32 ? HALF : 32;  // floats per operand chunk
     constexpr int NCH = HALF / CW;             // chunks per lane-half row
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    u64* cbuf = reinterpret_cast<u64*>(smem);  // [32][kStride]
 
     const int lane = threadIdx.x, j = lane & 31, h = lane >> 5;
-    const int64_t bslot = (int64_t)blockIdx.x * 32 + j;
+    __shared__ __attribute__((aligned(16))) float sscr[64 * 16];
+    float* scratch = sscr + lane * 4;  // score r of this lane: scratch[256 * (r >> 2) + (r & 3)] (conflict-free float4 rows)
+    const int64_t ublock = (int64_t)blockIdx.x * 32;
+    const int64_t bslot = ublock + j;
     const bool uvalid = bslot < a.nb;
     const int64_t urow = uvalid ? (a.users ? a.users[bslot] : bslot) : 0;
     const int chunk = blockIdx.y;
     const int64_t i0 = (int64_t)chunk * a.chunk_items;
     const int64_t i1 = min(a.ni, i0 + a.chunk_items);
     const int ntiles = (int)((i1 - i0 + 31) / 32);
-    u64* mybuf = cbuf + j * kStride;
+    // candidate row of (user, chunk); the row of user jj is base + jj * rowstep
+    u64* const base = a.cand + (ublock * a.n_chunks + chunk) * (int64_t)kCap;
+    const int64_t rowstep = (int64_t)a.n_chunks * kCap;
+    u64* mybuf = base + (int64_t)j * rowstep;
 
     float bu[HALF];
     {
@@ -229,117 +255,139 @@ __global__ __launch_bounds__(64) void fs_tiles(FsArgs a) {
     }
     int cnt = 0;
     float tau = -INFINITY;
-
-    float ra[CW], rb[CW];
     const int64_t nsteps = (int64_t)ntiles * NCH;
-    if (nsteps > 0) load_chunk<D, CW>(ra, a.I, i0 + j, i1, h * HALF);
-    floatx16 acc;
-    int64_t step = 0;
-    unsigned long long tm_mask = 0, tm_ins = 0, tm_cmp = 0, tm_mfma = 0;  // mode 4 cycle profile
-    // process one chunk step with operands `cur`, prefetching the next into `nxt`
-    auto do_step = [&](float (&cur)[CW], float (&nxt)[CW]) {
-        const int t = (int)(step / NCH), c = (int)(step % NCH);
-        const unsigned long long c0 = a.mode == 4 ? clock64() : 0;
-        if (c == 0) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-        }
-        if (step + 1 < nsteps) {
-            const int64_t s1 = step + 1;
-            const int t1 = (int)(s1 / NCH), c1 = (int)(s1 % NCH);
-            load_chunk<D, CW>(nxt, a.I, i0 + (int64_t)t1 * 32 + j, i1, h * HALF + CW * c1);
-        }
-#pragma unroll
-        for (int q = 0; q < CW; ++q) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[q], bu[CW * c + q], acc, 0, 0, 0);
-        ++step;
-        if (c != NCH - 1) return;
-        // ---- tile t complete: filter, insert, compact ----
-        const int64_t tb = i0 + (int64_t)t * 32;
-        if (a.mode == 1) {
-            float sink = 0.f;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) sink += acc[r];
-            if (sink == 1234.5f) a.out_val[0] = sink;  // keep the MFMAs live
-            return;
-        }
-        const unsigned long long c1 = a.mode == 4 ? clock64() : 0;
-        unsigned mbits = 0;
+    float ra[CW], rb[CW];
+    if (ntiles > 0) load_chunk<D, CW>(ra, a.I, i0 + j, i1, a.ni, h * HALF);
+
+    auto mask_bits = [&](int64_t tb) __attribute__((always_inline)) -> unsigned {  // train items of this user in [tb, tb+32)
+        unsigned mb = 0;
         while (next_mask < tb + 32) {
-            mbits |= 1u << (unsigned)(next_mask - tb);
+            mb |= 1u << (unsigned)(next_mask - tb);
             ++mp;
             next_mask = mp < me ? (int64_t)a.mcol[mp] : LLONG_MAX;
         }
+        return mb;
+    };
+    auto mfma_tile = [&](auto par, int t, floatx16& acc) __attribute__((always_inline)) {
+        constexpr int P = decltype(par)::value;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+            float(&cur)[CW] = ((P + c) & 1) ? rb : ra;
+            float(&nxt)[CW] = ((P + c) & 1) ? ra : rb;
+            const int64_t s1 = (int64_t)t * NCH + c + 1;
+            const int t1 = (int)(s1 / NCH), c1 = (int)(s1 % NCH);
+            load_chunk<D, CW>(nxt, a.I, s1 < nsteps ? i0 + (int64_t)t1 * 32 + j : i1, i1, a.ni, h * HALF + CW * c1);
+#pragma unroll
+            for (int q = 0; q < CW; ++q)
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[q], bu[CW * c + q], acc, 0, 0, 0);
+        }
+    };
+    // FULL: all 32 items of the tile are in the chunk; MASKED: some lane has train
+    // items in it (both wave-uniform, so the common tile takes the leanest variant)
+    auto filter_v = [&](auto full_c, auto masked_c, const floatx16& sv, unsigned mb, int64_t tb) __attribute__((always_inline)) {
+        constexpr bool FULL = decltype(full_c)::value != 0, MASKED = decltype(masked_c)::value != 0;
         unsigned m = 0;
+        const int rem = (int)(i1 - tb);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int ii = (r & 3) + 8 * (r >> 2) + 4 * h;
-            const float sc = ((mbits >> ii) & 1u) ? -1e10f : acc[r];
-            if (uvalid && tb + ii < i1 && sc > tau) m |= 1u << r;
+            const float sc = (MASKED && ((mb >> ii) & 1u)) ? -1e10f : sv[r];
+            m |= ((FULL || ii < rem) && sc > tau) ? (1u << r) : 0u;
         }
-        if (a.mode == 2 && cnt > kCap - 32) m = 0;
-        const unsigned long long c2 = a.mode == 4 ? clock64() : 0;
+        if (!uvalid) m = 0;
         if (__ballot(m != 0u)) {
+            // a lane takes ~1 score per tile on average: stage the 16 scores in the
+            // lane's LDS scratch and insert only the set bits (per-lane index = address)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                *reinterpret_cast<float4*>(scratch + 256 * q) = make_float4(sv[4 * q], sv[4 * q + 1], sv[4 * q + 2], sv[4 * q + 3]);
             const unsigned pm = (unsigned)__shfl_xor((int)m, 32, kWave);
             int pos = cnt + (h ? __popc(pm) : 0);
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                if ((m >> r) & 1u) {
-                    const int ii = (r & 3) + 8 * (r >> 2) + 4 * h;
-                    const float sc = ((mbits >> ii) & 1u) ? -1e10f : acc[r];
-                    mybuf[pos++] = make_key(sc, (int)(tb + ii));
-                }
-            }
             cnt += __popc(m) + __popc(pm);
-        }
-        const unsigned long long c3 = a.mode == 4 ? clock64() : 0;
-        u64 need = a.mode == 2 ? 0ull : __ballot(h == 0 && cnt > kCap - 32);
-        if (need) {
-            __builtin_amdgcn_wave_barrier();
-            while (need) {
-                const int jj = __ffsll((long long)need) - 1;
-                need &= need - 1;
-                const int n = __builtin_amdgcn_readlane(cnt, jj);
-                int kept;
-                const float nt = compact_slot(cbuf + jj * kStride, n, a.k, lane, &kept);
-                if (a.mode == 4 && lane == 0) atomicAdd((unsigned long long*)a.out_idx, 1ull);
-                if (j == jj) {
-                    tau = nt;
-                    cnt = kept;
-                }
+            unsigned mm = m;
+            while (mm) {
+                const int r = __ffs(mm) - 1;
+                mm &= mm - 1;
+                const int ii = (r & 3) + 8 * (r >> 2) + 4 * h;
+                const float raw = scratch[256 * (r >> 2) + (r & 3)];
+                const float sc = (MASKED && ((mb >> ii) & 1u)) ? -1e10f : raw;
+                mybuf[pos++] = make_key(sc, (int)(tb + ii));
             }
-        }
-        if (a.mode == 4) {
-            const unsigned long long c4 = clock64();
-            tm_mfma += c1 - c0;
-            tm_mask += c2 - c1;
-            tm_ins += c3 - c2;
-            tm_cmp += c4 - c3;
         }
     };
-    while (step < nsteps) {
-        do_step(ra, rb);
-        if (step < nsteps) do_step(rb, ra);
+    auto filter = [&](const floatx16& sv, unsigned mb, int64_t tb) __attribute__((always_inline)) {
+        if constexpr (MODE == 1) {
+            float sink = 0.f;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) sink += sv[r];
+            if (sink == 1234.5f) a.out_val[0] = sink;  // keep the MFMAs live
+            return;
+        }
+        const bool full = tb + 32 <= i1;
+        const bool masked = __ballot(mb != 0u) != 0ull;
+        if (full) {
+            if (masked) filter_v(IntC<1>{}, IntC<1>{}, sv, mb, tb);
+            else filter_v(IntC<1>{}, IntC<0>{}, sv, mb, tb);
+        } else {
+            filter_v(IntC<0>{}, IntC<1>{}, sv, mb, tb);
+        }
+    };
+    auto compact = [&]() __attribute__((always_inline)) {
+        if constexpr (MODE == 1) return;
+        u64 need = __ballot(h == 0 && cnt > kCap - 32);
+        while (need) {
+            const int jj = __ffsll((long long)need) - 1;
+            need &= need - 1;
+            const int n = __builtin_amdgcn_readlane(cnt, jj);
+            int kept;
+            const float nt = compact_slot(base + (int64_t)jj * rowstep, n, a.k, lane, &kept);
+            if (j == jj) {
+                tau = nt;
+                cnt = kept;
+            }
+        }
+    };
+
+    if (ntiles > 0) {
+        // one tile per iteration: the chain of tile t is issued before the filter of
+        // tile t-1; the accumulator and (for NCH == 1) the operand buffers rotate
+        // by register copies, so filter and compaction have one call site each
+        floatx16 prev, cur;
+        mfma_tile(IntC<0>{}, 0, prev);
+        if constexpr ((NCH & 1) != 0) {
+#pragma unroll
+            for (int q = 0; q < CW; ++q) ra[q] = rb[q];
+        }
+        unsigned mb = mask_bits(i0);
+        for (int t = 1; t < ntiles; ++t) {
+            mfma_tile(IntC<0>{}, t, cur);
+            filter(prev, mb, i0 + (int64_t)(t - 1) * 32);
+            compact();
+            mb = mask_bits(i0 + (int64_t)t * 32);
+            prev = cur;
+            if constexpr ((NCH & 1) != 0) {
+#pragma unroll
+                for (int q = 0; q < CW; ++q) ra[q] = rb[q];
+            }
+        }
+        filter(prev, mb, i0 + (int64_t)(ntiles - 1) * 32);
+        compact();
     }
-    if (a.mode == 4 && lane == 0) {
-        unsigned long long* dbg = (unsigned long long*)a.out_idx;
-        atomicAdd(dbg + 1, (unsigned long long)ntiles);
-        atomicAdd(dbg + 3, tm_mfma);
-        atomicAdd(dbg + 4, tm_mask);
-        atomicAdd(dbg + 5, tm_ins);
-        atomicAdd(dbg + 6, tm_cmp);
+    if constexpr (MODE == 1) return;
+    {  // every list down to its top k: fs_select then reads <= k <= 96 keys per chunk
+        u64 need = __ballot(h == 0 && cnt > a.k);
+        while (need) {
+            const int jj = __ffsll((long long)need) - 1;
+            need &= need - 1;
+            const int n = __builtin_amdgcn_readlane(cnt, jj);
+            int kept;
+            compact_slot(base + (int64_t)jj * rowstep, n, a.k, lane, &kept);
+            if (j == jj) cnt = kept;
+        }
     }
-    if (a.mode != 0 && a.mode != 4) return;
-    if (a.mode == 4) return;
-    __builtin_amdgcn_wave_barrier();
-    for (int jj = 0; jj < 32; ++jj) {
-        const int64_t b2 = (int64_t)blockIdx.x * 32 + jj;
-        if (b2 >= a.nb) break;  // wave-uniform
-        const int n = __builtin_amdgcn_readlane(cnt, jj);
-        const u64* src = cbuf + jj * kStride;
-        u64* dst = a.cand + (b2 * a.n_chunks + chunk) * kCap;
-        for (int e = lane; e < n; e += 64) dst[e] = src[e];
-        if (lane == 0) a.ccount[b2 * a.n_chunks + chunk] = n;
-    }
+    if (uvalid && h == 0) a.ccount[bslot * a.n_chunks + chunk] = cnt;
 }
 
 // Exact k-th largest of the nonzero keys held E per lane (radix search with ballots,
@@ -377,7 +425,7 @@ __device__ __forceinline__ u64 kth_largest_n(const u64 (&e)[E], int k) {
 
 // One wavefront per user: the exact top-k over every chunk's raw candidates,
 // ordered by (score desc, index asc).  S = chunks per user (<= SMAX); every list
-// holds <= kCap = 128 keys, i.e. <= 2 per lane.
+// holds <= k <= 96 keys (fs_tiles compacts every list to its top k), i.e. <= 2 per lane.
 template <int SMAX>
 __global__ __launch_bounds__(256) void fs_select(FsArgs a) {
     constexpr int E = 2 * SMAX;
@@ -427,13 +475,13 @@ __global__ __launch_bounds__(256) void fs_select(FsArgs a) {
 }
 
 static void fs_plan(int64_t nb, int64_t ni, int d, int* nw, int* n_chunks, int64_t* chunk_items) {
-    (void)d;
     *nw = 1;
     const int64_t waves = (nb + 31) / 32;
-    // item chunks per 32-user wave: just enough waves to cover the 1024 SIMDs (one
-    // wave per SIMD: the candidate buffers take the LDS).  Every extra chunk re-pays
-    // the threshold warm-up (measured: 1 chunk beats 2-4 at 1.1k waves), so no more.
-    int64_t s = (922 + waves - 1) / waves;
+    // item chunks per 32-user wave: enough waves for two per SIMD (2048 on the chip:
+    // one wave's filtering/compaction overlaps the other's MFMA chain), no more
+    // (every extra chunk re-pays the threshold warm-up)
+    const int64_t target = d <= 64 ? 1900 : 950;  // fs_tiles occupancy: 2 waves/SIMD at d <= 64, else 1
+    int64_t s = (target + waves - 1) / waves;
     if (s < 1) s = 1;
     if (s > 16) s = 16;
     if (const char* f = getenv("RSX_FS_CHUNKS")) {  // tuning override
@@ -456,9 +504,11 @@ size_t fs_ws(int64_t nb, int64_t ni, int k, int d) {
 
 template <int D>
 static int launch_fs(FsArgs& a, hipStream_t s) {
-    const size_t lds = 32 * kStride * sizeof(u64);
     const int64_t waves = (a.nb + 31) / 32;
-    hipLaunchKernelGGL((fs_tiles<D>), dim3((unsigned)waves, (unsigned)a.n_chunks), dim3(64), lds, s, a);
+    if (a.mode == 1)
+        hipLaunchKernelGGL((fs_tiles<D, 1>), dim3((unsigned)waves, (unsigned)a.n_chunks), dim3(64), 0, s, a);
+    else
+        hipLaunchKernelGGL((fs_tiles<D, 0>), dim3((unsigned)waves, (unsigned)a.n_chunks), dim3(64), 0, s, a);
     const dim3 sg((unsigned)((a.nb + 3) / 4));
     if (a.mode == 0) {
         if (a.n_chunks <= 1) hipLaunchKernelGGL(fs_select<1>, sg, dim3(256), 0, s, a);
