@@ -216,11 +216,25 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D <= 64 ? 2 
     const int lane = threadIdx.x, j = lane & 31, h = lane >> 5;
     __shared__ __attribute__((aligned(16))) float sscr[64 * 16];
     float* scratch = sscr + lane * 4;  // score r of this lane: scratch[256 * (r >> 2) + (r & 3)] (conflict-free float4 rows)
-    const int64_t ublock = (int64_t)blockIdx.x * 32;
+    // block -> (user block, chunk).  Blocks are dealt round-robin to the 8 XCDs, so
+    // when the chunk count divides 8 the blocks of one XCD all work on the same
+    // chunk and its L2 holds that chunk's item rows (placement is a speed matter only)
+    const int64_t n_ub = (a.nb + 31) / 32;
+    int64_t ub;
+    int chunk;
+    if ((8 % a.n_chunks) == 0) {
+        const int64_t b = blockIdx.x, xcd = b & 7, slot = b >> 3;
+        chunk = (int)(xcd % a.n_chunks);
+        ub = slot * (8 / a.n_chunks) + xcd / a.n_chunks;
+    } else {
+        chunk = (int)(blockIdx.x % a.n_chunks);
+        ub = blockIdx.x / a.n_chunks;
+    }
+    if (ub >= n_ub) return;
+    const int64_t ublock = ub * 32;
     const int64_t bslot = ublock + j;
     const bool uvalid = bslot < a.nb;
     const int64_t urow = uvalid ? (a.users ? a.users[bslot] : bslot) : 0;
-    const int chunk = blockIdx.y;
     const int64_t i0 = (int64_t)chunk * a.chunk_items;
     const int64_t i1 = min(a.ni, i0 + a.chunk_items);
     const int ntiles = (int)((i1 - i0 + 31) / 32);
@@ -505,10 +519,12 @@ size_t fs_ws(int64_t nb, int64_t ni, int k, int d) {
 template <int D>
 static int launch_fs(FsArgs& a, hipStream_t s) {
     const int64_t waves = (a.nb + 31) / 32;
+    int64_t nblk = waves * a.n_chunks;
+    if ((8 % a.n_chunks) == 0) nblk = (nblk + 7) / 8 * 8;  // whole rounds of the XCD-aware mapping
     if (a.mode == 1)
-        hipLaunchKernelGGL((fs_tiles<D, 1>), dim3((unsigned)waves, (unsigned)a.n_chunks), dim3(64), 0, s, a);
+        hipLaunchKernelGGL((fs_tiles<D, 1>), dim3((unsigned)nblk), dim3(64), 0, s, a);
     else
-        hipLaunchKernelGGL((fs_tiles<D, 0>), dim3((unsigned)waves, (unsigned)a.n_chunks), dim3(64), 0, s, a);
+        hipLaunchKernelGGL((fs_tiles<D, 0>), dim3((unsigned)nblk), dim3(64), 0, s, a);
     const dim3 sg((unsigned)((a.nb + 3) / 4));
     if (a.mode == 0) {
         if (a.n_chunks <= 1) hipLaunchKernelGGL(fs_select<1>, sg, dim3(256), 0, s, a);

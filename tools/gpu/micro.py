@@ -66,7 +66,7 @@ def main(what):
         U, I = f[:nu], f[nu:]
         hr, hc = graph.history_csr(tu, ti, nu)
         hr, hc = torch.from_numpy(hr).to(dev), torch.from_numpy(hc).to(dev)
-        users = torch.arange(nu, device=dev)
+        users = torch.arange(int(os.environ.get("RSX_FS_NUSERS", nu)), device=dev)
         if os.environ.get("RSX_FS_MODE") == "4":
             v, idx = ops.fullsort_topk(U, users, I, hr, hc, 50)
             idx.zero_()
@@ -85,7 +85,8 @@ def main(what):
                 out[name] = round(x / tot, 3)
             out["cycles_per_tile"] = tot / max(cts[1], 1)
         out["fs_ms_all_users"] = t_ms(lambda: ops.fullsort_topk(U, users, I, hr, hc, 50), 10)
-        out["fs_tflops"] = 2 * 64 * ni * nu / (out["fs_ms_all_users"] * 1e-3) / 1e12
+        out["fs_users"] = users.numel()
+        out["fs_tflops"] = 2 * 64 * ni * users.numel() / (out["fs_ms_all_users"] * 1e-3) / 1e12
     print(out, flush=True)
 
 
