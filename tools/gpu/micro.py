@@ -61,6 +61,15 @@ def main(what):
             xd = torch.randn(n, d, device=dev)
             yd = torch.empty_like(xd)
             out[f"spmmx_real_d{d}_us"] = round(t_ms(lambda: A.spmm(xd, out=yd), 100) * 1e3, 2)
+    if what == "metrics":
+        g = np.random.default_rng(1)
+        nu_e, k = 35598, 50
+        lens = g.integers(1, 6, nu_e)
+        rp_e = torch.from_numpy(np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)).to(dev)
+        col_e = torch.from_numpy(np.sort(g.integers(0, ni, int(lens.sum()))).astype(np.int32)).to(dev)
+        topk = torch.from_numpy(g.integers(0, ni, (nu_e, k))).to(dev)
+        gain = torch.from_numpy(1.0 / np.log2(np.arange(1, k + 1, dtype=np.float64) + 1)).to(dev)
+        out["metrics_ms"] = t_ms(lambda: ops.topk_metrics(topk, rp_e, col_e, [5, 10, 20, 50], gain), 20)
     if what in ("fullsort", "all"):
         f = torch.randn(n, 64, device=dev) * 0.1
         U, I = f[:nu], f[nu:]
