@@ -127,7 +127,8 @@ __device__ __forceinline__ u64 ld_u64_l2(const u64* p) {  // bypasses the CU's L
 // compare per key pair and scalar counting per round), and 32 more on the index
 // word only when several keys share the boundary score.  Every round is a handful
 // of instructions, so the selection costs a fraction of an all-pairs rank count.
-__device__ __forceinline__ float compact_slot(u64* buf, int n, int k, int lane, int* new_cnt) {
+__device__ __forceinline__ float compact_slot(u64* buf, int n, int k, int lane, int* new_cnt, unsigned lo,
+                                              unsigned hi) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's inserts are in L2
     u64 x[kNK];
     unsigned hw[kNK];
@@ -136,8 +137,12 @@ __device__ __forceinline__ float compact_slot(u64* buf, int n, int k, int lane, 
         x[q] = lane + 64 * q < n ? ld_u64_l2(buf + lane + 64 * q) : 0ull;
         hw[q] = (unsigned)(x[q] >> 32);
     }
-    unsigned th = 0;
-    for (int bit = 31; bit >= 0; --bit) {
+    // every buffered score word lies in [lo, hi] (lo = ord(threshold): the kept k-th key sits on it; hi = the
+    // row's maximum), so the answer shares their common high bits: search below them
+    const unsigned diff = lo ^ hi;
+    const int top = diff ? 31 - __builtin_clz(diff) : -1;
+    unsigned th = top >= 31 ? 0u : (hi >> (top + 1)) << (top + 1);
+    for (int bit = top; bit >= 0; --bit) {
         const unsigned c = th | (1u << bit);
         int m = 0;
 #pragma unroll
@@ -269,6 +274,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D <= 64 ? 2 
     }
     int cnt = 0;
     float tau = -INFINITY;
+    unsigned omax = 0;  // max ordered score word this lane inserted (the row max is the pair's max)
+    u64 prof[6] = {0, 0, 0, 0, 0, 0};  // MODE 4: memtime per segment (mfma issue, -, filter, compact, mask+copy, tiles)
     const int64_t nsteps = (int64_t)ntiles * NCH;
     float ra[CW], rb[CW];
     if (ntiles > 0) load_chunk<D, CW>(ra, a.I, i0 + j, i1, a.ni, h * HALF);
@@ -286,16 +293,25 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D <= 64 ? 2 
         constexpr int P = decltype(par)::value;
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+        if constexpr (NCH == 1) {
+            // one operand buffer: once the chain has read it, it is refilled with the
+            // next tile's rows (the loads land while this tile is filtered)
 #pragma unroll
-        for (int c = 0; c < NCH; ++c) {
-            float(&cur)[CW] = ((P + c) & 1) ? rb : ra;
-            float(&nxt)[CW] = ((P + c) & 1) ? ra : rb;
-            const int64_t s1 = (int64_t)t * NCH + c + 1;
-            const int t1 = (int)(s1 / NCH), c1 = (int)(s1 % NCH);
-            load_chunk<D, CW>(nxt, a.I, s1 < nsteps ? i0 + (int64_t)t1 * 32 + j : i1, i1, a.ni, h * HALF + CW * c1);
+            for (int q = 0; q < CW; ++q) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ra[q], bu[q], acc, 0, 0, 0);
+            load_chunk<D, CW>(ra, a.I, t + 1 < ntiles ? i0 + (int64_t)(t + 1) * 32 + j : i1, i1, a.ni, h * HALF);
+        } else {
 #pragma unroll
-            for (int q = 0; q < CW; ++q)
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[q], bu[CW * c + q], acc, 0, 0, 0);
+            for (int c = 0; c < NCH; ++c) {
+                float(&cur)[CW] = ((P + c) & 1) ? rb : ra;
+                float(&nxt)[CW] = ((P + c) & 1) ? ra : rb;
+                const int64_t s1 = (int64_t)t * NCH + c + 1;
+                const int t1 = (int)(s1 / NCH), c1 = (int)(s1 % NCH);
+                load_chunk<D, CW>(nxt, a.I, s1 < nsteps ? i0 + (int64_t)t1 * 32 + j : i1, i1, a.ni,
+                                  h * HALF + CW * c1);
+#pragma unroll
+                for (int q = 0; q < CW; ++q)
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[q], bu[CW * c + q], acc, 0, 0, 0);
+            }
         }
     };
     // FULL: all 32 items of the tile are in the chunk; MASKED: some lane has train
@@ -311,6 +327,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D <= 64 ? 2 
             m |= ((FULL || ii < rem) && sc > tau) ? (1u << r) : 0u;
         }
         if (!uvalid) m = 0;
+        const u64 ci0 = MODE == 4 ? __builtin_amdgcn_s_memtime() : 0;
         if (__ballot(m != 0u)) {
             // a lane takes ~1 score per tile on average: stage the 16 scores in the
             // lane's LDS scratch and insert only the set bits (per-lane index = address)
@@ -327,9 +344,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D <= 64 ? 2 
                 const int ii = (r & 3) + 8 * (r >> 2) + 4 * h;
                 const float raw = scratch[256 * (r >> 2) + (r & 3)];
                 const float sc = (MASKED && ((mb >> ii) & 1u)) ? -1e10f : raw;
-                mybuf[pos++] = make_key(sc, (int)(tb + ii));
+                const u64 key = make_key(sc, (int)(tb + ii));
+                omax = max(omax, (unsigned)(key >> 32));
+                mybuf[pos++] = key;
             }
         }
+        if constexpr (MODE == 4) prof[1] += __builtin_amdgcn_s_memtime() - ci0;
     };
     auto filter = [&](const floatx16& sv, unsigned mb, int64_t tb) __attribute__((always_inline)) {
         if constexpr (MODE == 1) {
@@ -355,8 +375,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D <= 64 ? 2 
             const int jj = __ffsll((long long)need) - 1;
             need &= need - 1;
             const int n = __builtin_amdgcn_readlane(cnt, jj);
+            const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)ord_f32(tau), jj);
+            const unsigned hi = max((unsigned)__builtin_amdgcn_readlane((int)omax, jj),
+                                    (unsigned)__builtin_amdgcn_readlane((int)omax, jj + 32));
             int kept;
-            const float nt = compact_slot(base + (int64_t)jj * rowstep, n, a.k, lane, &kept);
+            const float nt = compact_slot(base + (int64_t)jj * rowstep, n, a.k, lane, &kept, lo, hi);
             if (j == jj) {
                 tau = nt;
                 cnt = kept;
@@ -366,38 +389,53 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D <= 64 ? 2 
 
     if (ntiles > 0) {
         // one tile per iteration: the chain of tile t is issued before the filter of
-        // tile t-1; the accumulator and (for NCH == 1) the operand buffers rotate
-        // by register copies, so filter and compaction have one call site each
+        // tile t-1; the accumulator rotates by a register copy, so filter and
+        // compaction have one call site each
         floatx16 prev, cur;
         mfma_tile(IntC<0>{}, 0, prev);
-        if constexpr ((NCH & 1) != 0) {
-#pragma unroll
-            for (int q = 0; q < CW; ++q) ra[q] = rb[q];
-        }
         unsigned mb = mask_bits(i0);
         for (int t = 1; t < ntiles; ++t) {
+            const u64 c0 = MODE == 4 ? __builtin_amdgcn_s_memtime() : 0;
             mfma_tile(IntC<0>{}, t, cur);
+            const u64 c1 = MODE == 4 ? __builtin_amdgcn_s_memtime() : 0;
             filter(prev, mb, i0 + (int64_t)(t - 1) * 32);
+            const u64 c2 = MODE == 4 ? __builtin_amdgcn_s_memtime() : 0;
             compact();
+            const u64 c3 = MODE == 4 ? __builtin_amdgcn_s_memtime() : 0;
             mb = mask_bits(i0 + (int64_t)t * 32);
             prev = cur;
-            if constexpr ((NCH & 1) != 0) {
-#pragma unroll
-                for (int q = 0; q < CW; ++q) ra[q] = rb[q];
+            if constexpr (MODE == 4) {
+                const u64 c4 = __builtin_amdgcn_s_memtime();
+                prof[0] += c1 - c0;
+                prof[2] += c2 - c1;
+                prof[3] += c3 - c2;
+                prof[4] += c4 - c3;
+                prof[5] += 1;
             }
         }
         filter(prev, mb, i0 + (int64_t)(ntiles - 1) * 32);
         compact();
     }
+    if constexpr (MODE == 4) {
+        if (lane == 0) {
+            unsigned long long* dbg = reinterpret_cast<unsigned long long*>(a.out_idx);
+#pragma unroll
+            for (int q = 0; q < 6; ++q) atomicAdd(dbg + q, (unsigned long long)prof[q]);
+        }
+        return;
+    }
     if constexpr (MODE == 1) return;
-    {  // every list down to its top k: fs_select then reads <= k <= 96 keys per chunk
+    if (a.n_chunks > 2) {  // lists cut to their top k: fs_select then reads <= k <= 96 keys per chunk
         u64 need = __ballot(h == 0 && cnt > a.k);
         while (need) {
             const int jj = __ffsll((long long)need) - 1;
             need &= need - 1;
             const int n = __builtin_amdgcn_readlane(cnt, jj);
+            const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)ord_f32(tau), jj);
+            const unsigned hi = max((unsigned)__builtin_amdgcn_readlane((int)omax, jj),
+                                    (unsigned)__builtin_amdgcn_readlane((int)omax, jj + 32));
             int kept;
-            compact_slot(base + (int64_t)jj * rowstep, n, a.k, lane, &kept);
+            compact_slot(base + (int64_t)jj * rowstep, n, a.k, lane, &kept, lo, hi);
             if (j == jj) cnt = kept;
         }
     }
@@ -440,9 +478,9 @@ __device__ __forceinline__ u64 kth_largest_n(const u64 (&e)[E], int k) {
 // One wavefront per user: the exact top-k over every chunk's raw candidates,
 // ordered by (score desc, index asc).  S = chunks per user (<= SMAX); every list
 // holds <= k <= 96 keys (fs_tiles compacts every list to its top k), i.e. <= 2 per lane.
-template <int SMAX>
+template <int SMAX, int PER>
 __global__ __launch_bounds__(256) void fs_select(FsArgs a) {
-    constexpr int E = 2 * SMAX;
+    constexpr int E = PER * SMAX;
     __shared__ u64 top[4][kCap];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int64_t b = (int64_t)blockIdx.x * 4 + wv;
@@ -453,8 +491,8 @@ __global__ __launch_bounds__(256) void fs_select(FsArgs a) {
         const bool in = c < a.n_chunks;
         const int n = in ? a.ccount[b * a.n_chunks + c] : 0;
         const u64* src = a.cand + (b * a.n_chunks + c) * kCap;
-        e[2 * c] = lane < n ? src[lane] : 0ull;
-        e[2 * c + 1] = lane + 64 < n ? src[lane + 64] : 0ull;
+#pragma unroll
+        for (int q = 0; q < PER; ++q) e[PER * c + q] = lane + 64 * q < n ? src[lane + 64 * q] : 0ull;
     }
     int total = 0;
 #pragma unroll
@@ -521,17 +559,20 @@ static int launch_fs(FsArgs& a, hipStream_t s) {
     const int64_t waves = (a.nb + 31) / 32;
     int64_t nblk = waves * a.n_chunks;
     if ((8 % a.n_chunks) == 0) nblk = (nblk + 7) / 8 * 8;  // whole rounds of the XCD-aware mapping
-    if (a.mode == 1)
+    if (a.mode == 4)
+        hipLaunchKernelGGL((fs_tiles<D, 4>), dim3((unsigned)nblk), dim3(64), 0, s, a);
+    else if (a.mode == 1)
         hipLaunchKernelGGL((fs_tiles<D, 1>), dim3((unsigned)nblk), dim3(64), 0, s, a);
     else
         hipLaunchKernelGGL((fs_tiles<D, 0>), dim3((unsigned)nblk), dim3(64), 0, s, a);
     const dim3 sg((unsigned)((a.nb + 3) / 4));
     if (a.mode == 0) {
-        if (a.n_chunks <= 1) hipLaunchKernelGGL(fs_select<1>, sg, dim3(256), 0, s, a);
-        else if (a.n_chunks <= 2) hipLaunchKernelGGL(fs_select<2>, sg, dim3(256), 0, s, a);
-        else if (a.n_chunks <= 4) hipLaunchKernelGGL(fs_select<4>, sg, dim3(256), 0, s, a);
-        else if (a.n_chunks <= 8) hipLaunchKernelGGL(fs_select<8>, sg, dim3(256), 0, s, a);
-        else hipLaunchKernelGGL(fs_select<16>, sg, dim3(256), 0, s, a);
+        // <= 2 chunks: raw lists (<= kCap keys, kNK per lane); more: lists cut to top k
+        if (a.n_chunks <= 1) hipLaunchKernelGGL((fs_select<1, kNK>), sg, dim3(256), 0, s, a);
+        else if (a.n_chunks <= 2) hipLaunchKernelGGL((fs_select<2, kNK>), sg, dim3(256), 0, s, a);
+        else if (a.n_chunks <= 4) hipLaunchKernelGGL((fs_select<4, 2>), sg, dim3(256), 0, s, a);
+        else if (a.n_chunks <= 8) hipLaunchKernelGGL((fs_select<8, 2>), sg, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((fs_select<16, 2>), sg, dim3(256), 0, s, a);
     }
     return last_rc();
 }

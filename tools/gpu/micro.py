@@ -76,23 +76,24 @@ def main(what):
         hr, hc = graph.history_csr(tu, ti, nu)
         hr, hc = torch.from_numpy(hr).to(dev), torch.from_numpy(hc).to(dev)
         users = torch.arange(int(os.environ.get("RSX_FS_NUSERS", nu)), device=dev)
-        if os.environ.get("RSX_FS_MODE") == "4":
-            v, idx = ops.fullsort_topk(U, users, I, hr, hc, 50)
-            idx.zero_()
-            import ctypes as C
+        if os.environ.get("RSX_FS_MODE") == "4":  # per-segment s_memtime sums (fs_tiles<D, 4>)
+            import ctypes as C  # noqa: F401
             from rsx import _lib as L
+            v = torch.empty(users.numel(), 50, device=dev)
+            idx = torch.zeros(users.numel(), 50, dtype=torch.int64, device=dev)
             lib = L.lib()
-            ws = ops._ws(dev, lib.rsx_fullsort_ws_bytes(nu, ni, 50))
-            L.check(lib.rsx_fullsort_topk(ops._p(U), ops._p(users), nu, ops._p(I), ni, 64, ops._p(hr), ops._p(hc), 50,
-                                          ops._p(v), ops._p(idx), ops._p(ws), ws.numel(), ops._stream()), "fs")
+            ws = ops._ws(dev, lib.rsx_fullsort_ws_bytes(users.numel(), ni, 50))
+            L.check(lib.rsx_fullsort_topk(ops._p(U), ops._p(users), users.numel(), ops._p(I), ni, 64, ops._p(hr),
+                                          ops._p(hc), 50, ops._p(v), ops._p(idx), ops._p(ws), ws.numel(),
+                                          ops._stream()), "fs")
             torch.cuda.synchronize()
-            cts = [int(x) for x in idx.view(-1)[:7].cpu()]
-            out["compactions"], out["wave_tiles"], out["fallbacks"] = cts[:3]
-            out["compactions_per_user"] = out["compactions"] / nu
-            tot = sum(cts[3:7])
-            for name, x in zip(("cyc_mfma_issue", "cyc_mask", "cyc_insert", "cyc_compact"), cts[3:7]):
-                out[name] = round(x / tot, 3)
-            out["cycles_per_tile"] = tot / max(cts[1], 1)
+            c = [int(x) for x in idx.view(-1)[:6].cpu()]
+            tot = sum(c[:5])
+            for name, x in zip(("mfma_issue", "insert", "filter_total", "compact", "mask_copy"), c[:5]):
+                out["seg_" + name] = round(x / tot, 3)
+            out["cycles_per_tile"] = round(tot / max(c[5], 1))
+            print(out, flush=True)
+            return
         out["fs_ms_all_users"] = t_ms(lambda: ops.fullsort_topk(U, users, I, hr, hc, 50), 10)
         out["fs_users"] = users.numel()
         out["fs_tflops"] = 2 * 64 * ni * users.numel() / (out["fs_ms_all_users"] * 1e-3) / 1e12
