@@ -370,6 +370,21 @@ int rsx_topk_metrics(const int64_t* topk_idx, int64_t n_users, int32_t k_max,
                      const int32_t* cutoffs, int32_t n_cut, const double* gain,
                      double* out_sums, void* ws, size_t ws_bytes, rsx_stream_t stream);
 
+/* ------------------------------------------------------------------------ */
+/* Weight gradient of a small Linear over many rows                           */
+/* ------------------------------------------------------------------------ */
+/*
+ * dW = g^T x for nn.Linear(in_dim, out_dim) applied to n rows (g [n, out_dim],
+ * x [n, in_dim], dW [out_dim, in_dim], row-major): the AddmmBackward weight
+ * gradient of SMORE's gate / query / preference layers
+ * (src/models/smore.py:106-120, applied to all users+items).  The rows are split
+ * over blocks, partials are summed in block order (deterministic).
+ * out_dim, in_dim multiples of 32.
+ */
+size_t rsx_linear_wgrad_ws_bytes(int64_t n, int32_t out_dim, int32_t in_dim);
+int rsx_linear_wgrad(const float* g, const float* x, int64_t n, int32_t out_dim, int32_t in_dim, float* dw,
+                     void* ws, size_t ws_bytes, rsx_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

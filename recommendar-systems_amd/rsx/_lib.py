@@ -89,6 +89,8 @@ def _declare(lib):
         "rsx_smore_spectral_bwd_partials": (C.c_size_t, [I64, I32]),
         "rsx_topk_metrics_ws_bytes": (C.c_size_t, [I64, I32]),
         "rsx_topk_metrics": (C.c_int, [P, I64, I32, P, P, P, I32, P, P, P, C.c_size_t, P]),
+        "rsx_linear_wgrad_ws_bytes": (C.c_size_t, [I64, I32, I32]),
+        "rsx_linear_wgrad": (C.c_int, [P, P, I64, I32, I32, P, P, C.c_size_t, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -100,7 +102,7 @@ EXPORTED = ["rsx_version", "rsx_csr_schedule_host", "rsx_spmm", "rsx_rowwise", "
             "rsx_fullsort_ws_bytes", "rsx_fullsort_topk", "rsx_score_dense", "rsx_sample_triplets",
             "rsx_gather_rows", "rsx_lightgcn_step", "rsx_lightgcn_forward", "rsx_sample_epoch",
             "rsx_smore_spectral_fwd", "rsx_smore_spectral_bwd", "rsx_smore_spectral_bwd_partials",
-            "rsx_topk_metrics_ws_bytes", "rsx_topk_metrics"]
+            "rsx_topk_metrics_ws_bytes", "rsx_topk_metrics", "rsx_linear_wgrad_ws_bytes", "rsx_linear_wgrad"]
 
 
 def lib_path() -> str:

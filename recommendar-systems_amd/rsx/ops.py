@@ -257,6 +257,21 @@ def topk_metrics(topk_idx: torch.Tensor, eval_rowptr: torch.Tensor, eval_col: to
     return out
 
 
+def linear_wgrad(g: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+    """dW = g^T x for nn.Linear over many rows (rsx_linear_wgrad): split-K over row
+    blocks with an ordered partial sum, where a library GEMM would see a 64x64
+    output and a 26k-long reduction."""
+    _gpu(g, x)
+    g, x = g.contiguous(), x.contiguous()
+    n, o = g.shape
+    i = x.shape[1]
+    dw = torch.empty(o, i, dtype=torch.float32, device=g.device)
+    lib = L.lib()
+    ws = _ws(g.device, lib.rsx_linear_wgrad_ws_bytes(n, o, i))
+    L.check(lib.rsx_linear_wgrad(_p(g), _p(x), n, o, i, _p(dw), _p(ws), ws.numel(), _stream()), "rsx_linear_wgrad")
+    return dw
+
+
 def score_dense(user_emb: torch.Tensor, users: torch.Tensor | None, item_emb: torch.Tensor) -> torch.Tensor:
     """scores = user_emb[users] @ item_emb.T (reference lightgcn.py:164)."""
     _gpu(user_emb, users, item_emb)

@@ -33,6 +33,7 @@ import torch.nn.functional as F
 from . import _lib as L
 from . import graph, ops
 from .lightgcn import _BprLoss
+from .nn import RsxLinear
 from .recommender import GeneralRecommender
 
 
@@ -180,14 +181,14 @@ class SMORE(GeneralRecommender):
         if self.t_feat is not None:
             self.text_trs = nn.Linear(self.t_feat.shape[1], d)
         self.softmax = nn.Softmax(dim=-1)
-        self.query_v = nn.Sequential(nn.Linear(d, d), nn.Tanh(), nn.Linear(d, d, bias=False))
-        self.query_t = nn.Sequential(nn.Linear(d, d), nn.Tanh(), nn.Linear(d, d, bias=False))
-        self.gate_v = nn.Sequential(nn.Linear(d, d), nn.Sigmoid())
-        self.gate_t = nn.Sequential(nn.Linear(d, d), nn.Sigmoid())
-        self.gate_f = nn.Sequential(nn.Linear(d, d), nn.Sigmoid())
-        self.gate_image_prefer = nn.Sequential(nn.Linear(d, d), nn.Sigmoid())
-        self.gate_text_prefer = nn.Sequential(nn.Linear(d, d), nn.Sigmoid())
-        self.gate_fusion_prefer = nn.Sequential(nn.Linear(d, d), nn.Sigmoid())
+        self.query_v = nn.Sequential(RsxLinear(d, d), nn.Tanh(), RsxLinear(d, d, bias=False))
+        self.query_t = nn.Sequential(RsxLinear(d, d), nn.Tanh(), RsxLinear(d, d, bias=False))
+        self.gate_v = nn.Sequential(RsxLinear(d, d), nn.Sigmoid())
+        self.gate_t = nn.Sequential(RsxLinear(d, d), nn.Sigmoid())
+        self.gate_f = nn.Sequential(RsxLinear(d, d), nn.Sigmoid())
+        self.gate_image_prefer = nn.Sequential(RsxLinear(d, d), nn.Sigmoid())
+        self.gate_text_prefer = nn.Sequential(RsxLinear(d, d), nn.Sigmoid())
+        self.gate_fusion_prefer = nn.Sequential(RsxLinear(d, d), nn.Sigmoid())
         self.image_complex_weight = nn.Parameter(torch.randn(1, d // 2 + 1, 2, dtype=torch.float32))
         self.text_complex_weight = nn.Parameter(torch.randn(1, d // 2 + 1, 2, dtype=torch.float32))
         self.fusion_complex_weight = nn.Parameter(torch.randn(1, d // 2 + 1, 2, dtype=torch.float32))

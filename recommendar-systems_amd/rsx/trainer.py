@@ -79,6 +79,11 @@ class Trainer:
         params = self.model.parameters()
         name = (self.learner or "adam").lower()
         if name == "adam":
+            params = list(params)
+            if bool(self.config.get("rsx_adam", True)) and params and all(p.is_cuda for p in params):
+                from .optim import RsxAdam
+
+                return RsxAdam(params, lr=self.learning_rate, weight_decay=self.weight_decay)
             return optim.Adam(params, lr=self.learning_rate, weight_decay=self.weight_decay)
         if name == "sgd":
             return optim.SGD(params, lr=self.learning_rate, weight_decay=self.weight_decay)

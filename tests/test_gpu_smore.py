@@ -161,3 +161,56 @@ def test_spectral_fused_vs_torch_autograd(cuda, d, n, dv, dt):
     for name, a, b in zip(names, got_g, ref_g):
         scale = b.abs().max().item()
         np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), rtol=1e-4, atol=1e-4 * scale, err_msg=name)
+
+
+@pytest.mark.parametrize("n,o,i", [(26495, 64, 64), (1000, 128, 64), (7, 32, 32), (513, 64, 128)])
+def test_linear_wgrad_vs_torch(cuda, n, o, i):
+    """rsx_linear_wgrad = g^T x (fp32; tolerance relative to the magnitude of the sums)."""
+    from rsx import ops
+
+    gen = torch.Generator(device="cpu").manual_seed(n + o)
+    g = torch.randn(n, o, generator=gen).to(cuda)
+    x = torch.randn(n, i, generator=gen).to(cuda)
+    got = ops.linear_wgrad(g, x)
+    want = (g.double().t() @ x.double()).float()
+    scale = (g.abs().double().t() @ x.abs().double()).float()
+    assert torch.all((got - want).abs() <= 2e-6 * scale + 1e-6), (got - want).abs().max()
+    assert torch.equal(got, ops.linear_wgrad(g, x))  # deterministic
+
+
+def test_rsx_linear_matches_nn_linear(cuda):
+    from rsx.nn import RsxLinear
+
+    torch.manual_seed(3)
+    a = torch.nn.Linear(64, 64).to(cuda)
+    torch.manual_seed(3)
+    b = RsxLinear(64, 64).to(cuda)
+    assert torch.equal(a.weight, b.weight) and torch.equal(a.bias, b.bias)
+    x = torch.randn(5000, 64, device=cuda, requires_grad=True)
+    up = torch.randn(5000, 64, device=cuda)
+    ga = torch.autograd.grad((a(x) * up).sum(), [x, a.weight, a.bias])
+    gb = torch.autograd.grad((b(x) * up).sum(), [x, b.weight, b.bias])
+    for p, q in zip(ga, gb):  # two fp32 summation orders over 5000 rows: relative to the magnitude
+        np.testing.assert_allclose(q.cpu().numpy(), p.cpu().numpy(), rtol=1e-4, atol=1e-5 * p.abs().max().item())
+
+
+def test_rsx_adam_matches_torch_single_tensor(cuda):
+    """RsxAdam == torch.optim.Adam(foreach=False) (the reference's CPU path) over 4 steps."""
+    from rsx.optim import RsxAdam
+
+    shapes = [(300, 64), (64,), (1, 33, 2), (70, 4096)]
+    gen = torch.Generator(device="cpu").manual_seed(1)
+    ps = [torch.randn(*s, generator=gen).to(cuda) for s in shapes]
+    a = [p.clone().requires_grad_() for p in ps]
+    b = [p.clone().requires_grad_() for p in ps]
+    oa = torch.optim.Adam(a, lr=1e-2, weight_decay=1e-4, foreach=False)
+    ob = RsxAdam(b, lr=1e-2, weight_decay=1e-4)
+    for _ in range(4):
+        gs = [torch.randn(*s, generator=gen).to(cuda) for s in shapes]
+        for x, y, gg in zip(a, b, gs):
+            x.grad = gg.clone()
+            y.grad = gg.clone()
+        oa.step()
+        ob.step()
+    for x, y in zip(a, b):
+        np.testing.assert_allclose(y.detach().cpu().numpy(), x.detach().cpu().numpy(), rtol=0, atol=1e-6)
