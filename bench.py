@@ -139,6 +139,7 @@ def bench_model(args):
     def batches():
         while True:
             model.pre_epoch_processing()
+            t.reset_graph_step()  # as Trainer._train_epoch does at each epoch start
             for b in train:
                 yield b
 
@@ -150,7 +151,7 @@ def bench_model(args):
         if t.fused:
             model.fused_step(b, t.current_lr())
         else:
-            t._train_batch(b, idx["i"], model.calculate_loss)
+            t.train_step(b, idx["i"], model.calculate_loss)
         idx["i"] += 1
         return b.shape[1]
 

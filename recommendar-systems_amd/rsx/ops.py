@@ -140,9 +140,13 @@ def rowwise(n_rows: int, d: int, e: "L.Epilogue"):
 
 
 def adam_(p: torch.Tensor, g: torch.Tensor, m: torch.Tensor, v: torch.Tensor, step: int, lr: float,
-          betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0):
-    """In-place Adam on one parameter tensor (torch.optim.Adam, reference trainer.py:133,238)."""
+          betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, step_dev=None):
+    """In-place Adam on one parameter tensor (torch.optim.Adam, reference trainer.py:133,238).
+    `step_dev`: a 0-d int64 device tensor holding the (already incremented) step,
+    read by the kernel instead of `step`."""
     _gpu(p, g, m, v)
+    if step_dev is not None and (step_dev.dtype != torch.int64 or not step_dev.is_cuda):
+        raise ValueError("step_dev must be an int64 tensor on the GPU")
     d = p.shape[-1] if p.dim() > 1 else p.numel()
     n = p.numel() // d
     if d not in (32, 64, 128, 256):
@@ -152,19 +156,19 @@ def adam_(p: torch.Tensor, g: torch.Tensor, m: torch.Tensor, v: torch.Tensor, st
         main = (tot // 64) * 64
         if main:
             adam_(*(f[:main].view(-1, 64) for f in flat), step=step, lr=lr, betas=betas, eps=eps,
-                  weight_decay=weight_decay)
+                  weight_decay=weight_decay, step_dev=step_dev)
         if tot - main:
             tail = [torch.zeros(32, dtype=torch.float32, device=p.device) for _ in range(4)]
             for tt, f in zip(tail, flat):
                 tt[: tot - main].copy_(f[main:])
             adam_(*(t.view(1, 32) for t in tail), step=step, lr=lr, betas=betas, eps=eps,
-                  weight_decay=weight_decay)
+                  weight_decay=weight_decay, step_dev=step_dev)
             for tt, f, upd in zip(tail, flat, (True, False, True, True)):
                 if upd:
                     f[main:].copy_(tt[: tot - main])
         return
     e = epi(L.RSX_EPI_ADAM, s_in=g, p=p, m=m, v=v,
-            adam=adam_struct(lr, step, betas[0], betas[1], eps, weight_decay))
+            adam=adam_struct(lr, step, betas[0], betas[1], eps, weight_decay, step_dev=step_dev))
     rowwise(n, d, e)
 
 

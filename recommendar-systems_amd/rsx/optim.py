@@ -6,6 +6,11 @@ first moment by lerp, the second by mul + addcmul, then addcdiv.  One launch per
 parameter tensor: a 28.9M-element SMORE feature table is one pass over p, g, m, v
 instead of torch's chain of foreach kernels.  Works with torch LR schedulers (it
 is a torch.optim.Optimizer and reads group["lr"] at every step).
+
+The step count lives on the device (`state["step"]`, a 0-d int64 tensor, bumped by
+one foreach launch per group; the kernel reads it through `rsx_adam.step_dev`), so
+a step holds no host-side counter and can be captured in a HIP graph and replayed
+(rsx.trainer's graph step); only a change of `lr` needs a new capture.
 """
 from __future__ import annotations
 
@@ -25,18 +30,25 @@ class RsxAdam(torch.optim.Optimizer):
             with torch.enable_grad():
                 loss = closure()
         for group in self.param_groups:
-            for p in group["params"]:
-                if p.grad is None:
-                    continue
+            live = [p for p in group["params"] if p.grad is not None]
+            for p in live:
                 if p.grad.is_sparse:
                     raise RuntimeError("RsxAdam does not support sparse gradients")
                 st = self.state[p]
                 if not st:
-                    st["step"] = 0
+                    st["step"] = torch.zeros((), dtype=torch.int64, device=p.device)
                     st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-                st["step"] += 1
+                elif not (torch.is_tensor(st["step"]) and st["step"].dtype == torch.int64
+                          and st["step"].device == p.device):
+                    # a state dict saved by torch.optim.Adam (float step) or an older RsxAdam (int)
+                    st["step"] = torch.tensor(int(st["step"]), dtype=torch.int64, device=p.device)
+            if not live:
+                continue
+            torch._foreach_add_([self.state[p]["step"] for p in live], 1)
+            for p in live:
+                st = self.state[p]
                 g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
-                ops.adam_(p.data, g, st["exp_avg"], st["exp_avg_sq"], st["step"], group["lr"],
-                          betas=group["betas"], eps=group["eps"], weight_decay=group["weight_decay"])
+                ops.adam_(p.data, g, st["exp_avg"], st["exp_avg_sq"], 0, group["lr"], betas=group["betas"],
+                          eps=group["eps"], weight_decay=group["weight_decay"], step_dev=st["step"])
         return loss

@@ -137,6 +137,10 @@ def spectrum_torch(img, txt, wv, wt, wf, normalize=True):
 
 
 class SMORE(GeneralRecommender):
+    # a training batch has no host syncs and global_step advances once per
+    # calculate_loss: the Trainer may capture it in a HIP graph (rsx.trainer._GraphStep)
+    supports_graph_step = True
+
     def __init__(self, config, dataset):
         super().__init__(config, dataset)
         ops.require_device(self.device)
@@ -327,9 +331,12 @@ class SMORE(GeneralRecommender):
         return super().train(mode)
 
     # ----------------------------------------------------------- diagnostics
+    def diagnostics_enabled(self) -> bool:
+        return bool(self.mg_verbose or self.diag_grad or self.diag_spectrum or self.diag_gate)
+
     @torch.no_grad()
     def log_mm_diagnostics(self, optimizer=None):
-        if not (self.mg_verbose or self.diag_grad or self.diag_spectrum or self.diag_gate):
+        if not self.diagnostics_enabled():
             return
         parts = []
         if self.diag_spectrum and "spec_in" in self._last:

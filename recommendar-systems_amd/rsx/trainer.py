@@ -23,6 +23,7 @@ TopKEvaluator (vectorised hit matrix, same metric values).
 from __future__ import annotations
 
 import itertools
+import os
 from logging import getLogger
 from time import time
 
@@ -33,6 +34,132 @@ from torch.nn.utils.clip_grad import clip_grad_norm_
 
 from .evaluator import TopKEvaluator
 from .utils import dict2str, early_stopping
+
+
+def _capturing() -> bool:
+    return torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+
+
+def _mg_alpha(params, grads, base, lr, rel_step, max_scale):
+    """The mirror-gradient step scale (reference trainer.py:300-318) as a 0-d float64
+    device tensor: max(base, rel * rms(p) / (lr * rms(g) + 1e-12)) capped at
+    base * max_scale.  The RMS values are f32 tensor results, as in the reference
+    (it converts them with float()); the rest is the same float64 arithmetic in the
+    same order, so the value is the reference's bit for bit, with no host sync."""
+    if not grads:
+        dev = params[0].device if params else "cpu"
+        return torch.tensor(base, dtype=torch.float64, device=dev)
+    g_all = torch.cat([g.view(-1) for g in grads])
+    p_all = torch.cat([p.detach().view(-1) for p in params])
+    grad_rms = (g_all.norm() / (g_all.numel() ** 0.5)).double()
+    param_rms = (p_all.norm() / (p_all.numel() ** 0.5) + 1e-12).double()
+    alpha = rel_step * param_rms / (lr * grad_rms + 1e-12)
+    # Python's max(base, x) keeps base when x is NaN; clamp would propagate it
+    alpha = torch.where(alpha > base, alpha, torch.full_like(alpha, base))
+    return torch.clamp(alpha, max=base * max_scale)
+
+
+def _mg_print(step_id, mirror, alpha):
+    print(f"[MG] step={step_id} mirror_loss={float(mirror.item()):.4f} α_eff={float(alpha):.3g}")
+
+
+class _GraphStep:
+    """One training batch (`Trainer._train_batch`: forward, loss, backward, Adam and
+    the model-level mirror gradient) captured as a HIP graph and replayed.
+
+    A SMORE batch is ~1000 small kernels; launched one by one from Python the host is
+    slower than the GPU, so the step is host-bound.  Replaying a captured graph
+    issues them in one submission.  What a replay must not depend on is host state,
+    so the step keeps none on the host: the Adam step count is a device counter
+    (rsx.optim.RsxAdam), the mirror-gradient scale a device scalar (_mg_alpha),
+    losses stay device tensors, and the batch is copied into a static buffer.
+
+    The control flow of a batch depends on the host counter `model.global_step`
+    (mirror gradient when the step after the first calculate_loss is a multiple of
+    mg_interval; diagnostics every mg_log_interval steps).  Each branch is its own
+    graph ("kind"), the host counter is advanced by what the capture advanced it
+    by, and batches that log diagnostics run eagerly.  A kind is captured only
+    after one eager batch of that kind at full size, so lazily allocated
+    workspaces exist outside the graph's memory pool.  A change of lr (baked into
+    the captured Adam launches) drops the graphs.  Partial batches run eagerly.
+
+    Contract for a model to opt in (`supports_graph_step = True`): calculate_loss
+    increments `global_step` by one (if it has one), and no host syncs or
+    data-dependent host branches in calculate_loss."""
+
+    def __init__(self, trainer, loss_func):
+        self.t = trainer
+        self.loss_func = loss_func
+        self.shape = None
+        self.seen = set()
+        self.graphs = {}
+        self.lr = None
+        self.replays = 0
+
+    def _kind(self):
+        """(mirror-gradient batch?) or None when the batch must run eagerly."""
+        m = self.t.model
+        g1 = int(getattr(m, "global_step", 0)) + 1  # the step id _mirror_gradient will see
+        log_every = int(getattr(m, "mg_log_interval", 50))
+        if log_every > 0 and g1 % log_every == 0 and hasattr(m, "log_mm_diagnostics"):
+            if getattr(m, "diagnostics_enabled", lambda: True)():
+                return None
+        interval = int(getattr(m, "mg_interval", 0)) if getattr(m, "mg_enable", False) else 0
+        return bool(interval > 0 and g1 % interval == 0)
+
+    def step(self, inter):
+        """The batch through a graph: (losses, loss), or None to run it eagerly."""
+        if not (torch.is_tensor(inter) and inter.is_cuda):
+            return None
+        if self.shape is None:
+            self.shape = tuple(inter.shape)
+        if tuple(inter.shape) != self.shape:
+            return None
+        kind = self._kind()
+        if kind is None:
+            return None
+        lr = self.t.optimizer.param_groups[0]["lr"]
+        if lr != self.lr:
+            self.graphs.clear()
+            self.lr = lr
+        if kind not in self.seen:
+            self.seen.add(kind)
+            return None
+        m = self.t.model
+        cap = self.graphs.get(kind)
+        if cap is None:
+            cap = self._capture(inter)
+            self.graphs[kind] = cap
+        else:
+            cap["static"].copy_(inter)
+            if hasattr(m, "global_step"):
+                m.global_step += cap["dstep"]
+        step_id = int(getattr(m, "global_step", 0)) - cap["dstep"] + 1
+        cap["graph"].replay()
+        self.replays += 1
+        losses, loss = cap["out"]
+        if cap["mg"] is not None and getattr(m, "mg_verbose", False):
+            _mg_print(step_id, cap["mg"][1], cap["mg"][2])
+        if isinstance(losses, tuple):
+            return tuple(x.clone() for x in losses), loss.clone()
+        loss = loss.clone()
+        return loss, loss
+
+    def _capture(self, inter):
+        m = self.t.model
+        static = inter.detach().clone()
+        before = int(getattr(m, "global_step", 0))
+        g = torch.cuda.CUDAGraph()
+        if os.environ.get("RSX_GRAPH_DEBUG"):
+            print(f"[graph] capture at global_step={before}", flush=True)
+        with torch.cuda.graph(g):
+            losses, loss = self.t._train_batch(static, 0, self.loss_func)
+            # detached: graph outputs that keep the captured autograd graph alive
+            # would hold its AccumulateGrad nodes into the next capture
+            out = (tuple(x.detach() for x in losses) if isinstance(losses, tuple) else losses.detach(),
+                   loss.detach())
+        return dict(graph=g, static=static, out=out, mg=getattr(self.t, "_mg_last", None),
+                    dstep=int(getattr(m, "global_step", 0)) - before)
 
 
 class Trainer:
@@ -73,6 +200,7 @@ class Trainer:
         self.evaluator = TopKEvaluator(config)
         self.mg_target_rel_step = float(config.get("mg_target_rel_step", 1e-3))
         self.mg_alpha_max_scale = float(config.get("mg_alpha_max_scale", 20.0))
+        self._graph = None
 
     # ------------------------------------------------------------------ setup
     def _build_optimizer(self):
@@ -134,10 +262,11 @@ class Trainer:
         parts = []
         loss_batches = []
         every = max(int(self.config.get("rsx_nan_check_every", 64) or 64), 1)
+        self.reset_graph_step()
         for batch_idx, interaction in enumerate(train_data):
-            losses, loss = self._train_batch(interaction, batch_idx, loss_func)
-            parts.append(torch.stack([x.detach() for x in losses]) if isinstance(losses, tuple) else loss.detach())
-            loss_batches.append(loss.detach())
+            losses, loss = self.train_step(interaction, batch_idx, loss_func)
+            parts.append(torch.stack(list(losses)) if isinstance(losses, tuple) else loss)
+            loss_batches.append(loss)
             if (batch_idx + 1) % every == 0 and self._check_nan(loss_batches[-1]):
                 self.logger.info(f"Loss is nan at epoch: {epoch_idx}, batch index: {batch_idx}. Exiting.")
                 return loss_batches[-1], torch.tensor(0.0)
@@ -149,6 +278,38 @@ class Trainer:
             return torch.tensor(float("nan")), torch.tensor(0.0)
         total_loss = tuple(float(x) for x in host.sum(0)) if host.ndim == 2 else float(host.sum())
         return total_loss, loss_batches
+
+    def graph_step_enabled(self, loss_func=None) -> bool:
+        from .optim import RsxAdam
+
+        m = self.model
+        return (bool(self.config.get("rsx_graph_step", True)) and bool(getattr(m, "supports_graph_step", False))
+                and not self.fused and not self.mg and isinstance(self.optimizer, RsxAdam)
+                and (loss_func is None or loss_func == m.calculate_loss) and torch.cuda.is_available())
+
+    def reset_graph_step(self):
+        """Drop the captured steps (at each epoch start: pre_epoch_processing may
+        have rebuilt buffers the graphs point at)."""
+        self._graph = None
+
+    def train_step(self, interaction, batch_idx, loss_func=None):
+        """One batch: replayed from a captured graph when possible (see _GraphStep),
+        else `_train_batch`.  Returns (losses, loss), detached."""
+        loss_func = loss_func or self.model.calculate_loss
+        if self.graph_step_enabled(loss_func):
+            if self._graph is None:
+                self._graph = _GraphStep(self, loss_func)
+            out = self._graph.step(interaction)
+            if out is not None:
+                return out
+        losses, loss = self._train_batch(interaction, batch_idx, loss_func)
+        # detached: a caller holding an eager batch's autograd graph keeps its
+        # AccumulateGrad nodes (bound to the eager stream) alive into the next
+        # capture, whose backward would then wait on a stream outside the graph
+        if isinstance(losses, tuple):
+            return tuple(x.detach() for x in losses), loss.detach()
+        loss = loss.detach()
+        return loss, loss
 
     def _train_batch(self, interaction, batch_idx, loss_func):
         """One training batch exactly as the reference's loop body: loss, backward,
@@ -197,6 +358,7 @@ class Trainer:
             except Exception as err:  # noqa: BLE001
                 self.logger.warning(f"log_mm_diagnostics failed at step {step_id}: {err}")
         if interval <= 0 or step_id % interval != 0:
+            self._mg_last = None
             return
         lr = self.optimizer.param_groups[0].get("lr", 1.0)
         self._zero_grad()
@@ -209,33 +371,27 @@ class Trainer:
                 grads.append(p.grad.detach().clone())
         with torch.no_grad():
             base = float(getattr(m, "mg_alpha", 0.5))
-            if not grads:
-                alpha = base
-            else:
-                g_all = torch.cat([g.view(-1) for g in grads])
-                p_all = torch.cat([p.detach().view(-1) for p in params])
-                grad_rms = float(g_all.norm() / (g_all.numel() ** 0.5))
-                param_rms = float(p_all.norm() / (p_all.numel() ** 0.5) + 1e-12)
-                alpha = max(base, self.mg_target_rel_step * param_rms / (lr * grad_rms + 1e-12))
-                alpha = min(alpha, base * self.mg_alpha_max_scale)
-            m._alpha_eff = float(alpha)
-            for p, g in zip(params, grads):
-                p.add_(-alpha * lr * g)
+            alpha = _mg_alpha(params, grads, base, lr, self.mg_target_rel_step, self.mg_alpha_max_scale)
+            m._alpha_eff = alpha
+            if params:
+                down = (alpha * -lr).float()  # -alpha * lr, rounded to f32 as the scalar of a f32 op
+                torch._foreach_add_(params, torch._foreach_mul(grads, down))
         self._zero_grad()
         mir = loss_func(inter)
         mirror = sum(mir) if isinstance(mir, tuple) else mir
         mirror.backward()
         with torch.no_grad():
             beta = float(getattr(m, "mg_beta", 0.2))
-            for p in m.parameters():
-                if p.requires_grad and p.grad is not None:
-                    p.grad.mul_(-beta)
-            for p, g in zip(params, grads):
-                p.add_(alpha * lr * g)
+            live = [p.grad for p in m.parameters() if p.requires_grad and p.grad is not None]
+            if live:
+                torch._foreach_mul_(live, -beta)
+            if params:
+                torch._foreach_add_(params, torch._foreach_mul(grads, (alpha * lr).float()))
         self.optimizer.step()
         self._zero_grad()
-        if getattr(m, "mg_verbose", False):
-            print(f"[MG] step={step_id} mirror_loss={float(mirror.item()):.4f} α_eff={alpha:.3g}")
+        self._mg_last = (step_id, mirror.detach(), alpha)
+        if getattr(m, "mg_verbose", False) and not _capturing():
+            _mg_print(step_id, mirror, alpha)
 
     # ------------------------------------------------------------------- fit
     def _valid_epoch(self, valid_data):

@@ -134,6 +134,45 @@ def test_smore_one_epoch_with_mirror_gradient(tmp_path, golden):
             assert abs(res[k] - ref[k]) <= 1e-4 + 1e-12, (tag, k, res[k], ref[k])
 
 
+def test_smore_graph_step_equals_eager(tmp_path, golden):
+    """Two epochs with the training batch replayed from captured HIP graphs
+    (rsx_graph_step) == the same epochs run eagerly: the host step counter and the
+    Adam step counts exactly; losses, parameters and Adam moments to the tolerance of
+    the golden epoch test.  (Not bit for bit: the BPR kernel scatters its row
+    gradients with float atomics, bpr.hip:14, so two eager runs already differ in
+    the last bits, and Adam turns that into up to ~lr near g = 0.)  The epoch has 6
+    full batches (plain and mirror-gradient kinds, each run eagerly once, then
+    captured and replayed) and a partial one (eager)."""
+    from rsx.trainer import Trainer
+
+    runs = []
+    for graph in (False, True):
+        z, c, train, valid, test = _setup(tmp_path / str(graph), golden)
+        c["rsx_graph_step"] = graph
+        m = _model(c, train)
+        t = Trainer(c, m)
+        losses = []
+        replays = 0
+        for ep in range(2):
+            m.pre_epoch_processing()
+            loss, _ = t._train_epoch(train, ep)
+            losses.append(loss)
+            replays += t._graph.replays if t._graph is not None else 0
+        st = [t.optimizer.state[p] for p in m.parameters()]
+        runs.append(dict(losses=losses, step=m.global_step, replays=replays,
+                         p={n: p.detach().cpu().numpy() for n, p in m.named_parameters()},
+                         m=[s["exp_avg"].cpu().numpy() for s in st], v=[s["exp_avg_sq"].cpu().numpy() for s in st],
+                         n=[int(s["step"]) for s in st]))
+    eager, graph = runs
+    assert eager["replays"] == 0 and graph["replays"] >= 4
+    assert graph["step"] == eager["step"] and graph["n"] == eager["n"]
+    np.testing.assert_allclose(graph["losses"], eager["losses"], rtol=1e-5)
+    for k in eager["p"]:
+        np.testing.assert_allclose(graph["p"][k], eager["p"][k], rtol=0, atol=1e-4, err_msg=k)
+    for a, b in zip(graph["m"] + graph["v"], eager["m"] + eager["v"]):
+        np.testing.assert_allclose(a, b, rtol=1e-3, atol=1e-7)
+
+
 @pytest.mark.parametrize("d,n,dv,dt", [(64, 1000, 512, 384), (128, 333, 768, 768), (64, 7, 48, 24)])
 def test_spectral_fused_vs_torch_autograd(cuda, d, n, dv, dt):
     """rsx_smore_spectral_fwd/bwd against torch.nn.functional.linear + torch.fft (fp32, the

@@ -2,4 +2,4 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 timeout -k 10 600 python -m pytest tests/test_gpu_smore.py -q -x -p no:cacheprovider 2>&1 | tail -15 || exit 1
-timeout -k 10 400 python bench.py --workload c3 --steps 30 --warmup 5 2>/dev/null | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('c3', d['value'], d['ms_per_step'])"
+timeout -k 10 400 python bench.py --workload c3 --steps 200 --warmup 20 2>/dev/null | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('c3', d['value'], d['ms_per_step'])"
