@@ -4,8 +4,9 @@ text_trs and :209-237 spectrum_convolution), with autograd.
 
 Forward: one launch computes img = V Wv^T + bv, txt = T Wt^T + bt (fp32 MFMA),
 their rfft's, the three filtered spectra and the three irfft's.  Backward: one
-launch for the spectral part (d img, d txt, d w), then the projection gradients as
-plain GEMMs (rocBLAS through torch): d V = d img Wv, d Wv = d img^T V, d bv = colsum.
+launch for the spectral part (d img, d txt, d w), then the projection gradients:
+d Wv = d img^T V on the split-K kernel (rsx_linear_wgrad), d V = d img Wv as a
+library GEMM, d bv = colsum.
 The unit normalisation of the complex weights (:221-229) stays a torch op on the
 (d/2+1)-sized parameters so autograd handles it exactly as the reference does.
 """
@@ -27,6 +28,14 @@ def unit_weight(w: torch.Tensor, normalize: bool) -> torch.Tensor:
     if normalize:
         cw = cw / (torch.abs(cw) + 1e-8)
     return torch.view_as_real(cw).reshape(-1, 2)
+
+
+def _wgrad(g, x):
+    """d W = g^T x (a d x dv output over the n items): the split-K kernel when the
+    widths allow it (rsx_linear_wgrad), else a library GEMM."""
+    if g.shape[1] % 32 == 0 and x.shape[1] % 32 == 0:
+        return ops.linear_wgrad(g, x)
+    return g.t() @ x
 
 
 class _Spectral(torch.autograd.Function):
@@ -66,10 +75,10 @@ class _Spectral(torch.autograd.Function):
         gw = part.view(-1, 3, d // 2 + 1, 2).sum(0)
         need = ctx.needs_input_grad
         gV = gi @ Wv if need[0] else None
-        gWv = gi.t() @ V if need[1] else None
+        gWv = _wgrad(gi, V) if need[1] else None
         gbv = gi.sum(0) if need[2] else None
         gT = gt @ Wt if need[3] else None
-        gWt = gt.t() @ T if need[4] else None
+        gWt = _wgrad(gt, T) if need[4] else None
         gbt = gt.sum(0) if need[5] else None
         return gV, gWv, gbv, gT, gWt, gbt, gw[0], gw[1], gw[2]
 

@@ -202,7 +202,8 @@ def test_spectral_fused_vs_torch_autograd(cuda, d, n, dv, dt):
         np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), rtol=1e-4, atol=1e-4 * scale, err_msg=name)
 
 
-@pytest.mark.parametrize("n,o,i", [(26495, 64, 64), (1000, 128, 64), (7, 32, 32), (513, 64, 128)])
+@pytest.mark.parametrize("n,o,i", [(26495, 64, 64), (1000, 128, 64), (7, 32, 32), (513, 64, 128), (7050, 64, 4096),
+                                   (7050, 64, 384), (0, 64, 64), (65, 32, 32), (300001, 64, 64)])
 def test_linear_wgrad_vs_torch(cuda, n, o, i):
     """rsx_linear_wgrad = g^T x (fp32; tolerance relative to the magnitude of the sums)."""
     from rsx import ops
