@@ -52,12 +52,15 @@ class DeviceCSR:
     Replaces the torch COO adjacency of reference src/models/lightgcn.py:65-103.
     """
 
-    def __init__(self, rowptr: np.ndarray, col: np.ndarray, val: np.ndarray, n_cols: int, device,
-                 chunk: int = 32):
+    def __init__(self, rowptr: np.ndarray, col, val, n_cols: int, device, chunk: int = 32):
+        """rowptr: host int64 [n_rows+1]; col / val: host arrays, or int32 / float32
+        tensors already on `device` (then used in place, see from_device)."""
         lib = L.lib()
         rowptr = np.ascontiguousarray(rowptr, dtype=np.int64)
-        col = np.ascontiguousarray(col, dtype=np.int32)
-        val = np.ascontiguousarray(val, dtype=np.float32)
+        on_dev = torch.is_tensor(col)
+        if not on_dev:
+            col = np.ascontiguousarray(col, dtype=np.int32)
+            val = np.ascontiguousarray(val, dtype=np.float32)
         n_rows = rowptr.size - 1
         nw, nl, ns = C.c_int64(), C.c_int64(), C.c_int64()
         L.check(lib.rsx_csr_schedule_host(rowptr.ctypes.data_as(C.c_void_p), n_rows, chunk, None, None,
@@ -68,19 +71,35 @@ class DeviceCSR:
                                           work.ctypes.data_as(C.c_void_p), longr.ctypes.data_as(C.c_void_p),
                                           C.byref(nw), C.byref(nl), C.byref(ns)), "rsx_csr_schedule_host")
         self.device = torch.device(device)
-        self.n_rows, self.n_cols, self.nnz = int(n_rows), int(n_cols), int(col.size)
+        self.n_rows, self.n_cols = int(n_rows), int(n_cols)
+        self.nnz = int(col.numel()) if on_dev else int(col.size)
+        if self.nnz != int(rowptr[-1]):
+            raise RuntimeError(f"DeviceCSR: rowptr ends at {int(rowptr[-1])}, {self.nnz} nonzeros given")
         self.chunk = chunk
         self.n_work, self.n_long, self.n_slots = nw.value, nl.value, ns.value
         self.rowptr_host = rowptr
         self.rowptr = torch.from_numpy(rowptr).to(self.device)
-        self.col = torch.from_numpy(col).to(self.device)
-        self.val = torch.from_numpy(val).to(self.device)
+        if on_dev:
+            if col.dtype != torch.int32 or val.dtype != torch.float32 or col.device != self.device \
+                    or val.device != self.device or not (col.is_contiguous() and val.is_contiguous()):
+                raise RuntimeError("DeviceCSR: device col/val must be contiguous int32/float32 on the CSR's device")
+            self.col, self.val = col, val
+        else:
+            self.col = torch.from_numpy(col).to(self.device)
+            self.val = torch.from_numpy(val).to(self.device)
         self.work = torch.from_numpy(work).to(self.device)
         self.long_rows = torch.from_numpy(longr).to(self.device)
         self.struct = L.Csr(self.n_rows, self.n_cols, self.nnz, self.rowptr.data_ptr(), self.col.data_ptr(),
                             self.val.data_ptr(), chunk, 0, self.n_work, self.work.data_ptr(), self.n_long,
                             self.long_rows.data_ptr(), self.n_slots)
         self._slabs = {}
+
+    @classmethod
+    def from_device(cls, rowptr: torch.Tensor, col: torch.Tensor, val: torch.Tensor, n_cols: int,
+                    chunk: int = 32):
+        """A CSR built on the device: only rowptr comes to the host (one copy, for
+        the work schedule, rsx_csr_schedule_host); col / val stay where they are."""
+        return cls(rowptr.cpu().numpy(), col, val, n_cols, col.device, chunk)
 
     @classmethod
     def from_scipy(cls, m, device, chunk: int = 32):

@@ -140,3 +140,19 @@ def test_quick_start_main_flow(tmp_path):
         os.chdir(cwd)
     assert len(res) == 1 and "recall@20" in res[0][1]
     assert os.listdir(tmp_path / "log")
+
+
+def test_layergcn_device_edge_dropout_trains(tmp_path, golden):
+    """LayerGCN dropout 0.1 with the device sampler and the device edge dropout (the
+    throughput configuration): per-epoch graphs of the right size that change
+    between epochs, and after two epochs metrics in the reference's range (its own
+    run draws other edges and triplets, so only statistically comparable)."""
+    z = golden("layergcn_drop_small")
+    m, vres, tres, _, graphs = _run(tmp_path, "LayerGCN", dict(n_layers=[2], reg_weight=[1e-2], dropout=[0.1],
+                                                               rsx_sampler="device"), 2)
+    assert m.edge_dropout_mode == "device"
+    keep_len = int(m.edge_values.numel() * 0.9)
+    assert [A.nnz for A in graphs] == [2 * keep_len] * 2
+    assert not torch.equal(graphs[0].col, graphs[1].col)
+    for k, want in metric_dict(z, "epoch1_valid").items():
+        assert np.isfinite(vres[k]) and abs(vres[k] - want) <= 0.05 + 0.5 * want, (k, vres[k], want)

@@ -324,3 +324,41 @@ def test_topk_metrics_device_bitwise_vs_numpy(cuda):
     want2 = E.recall2(hit, pos)
     for j, c in enumerate(cuts):
         assert sums[4, j] / pos.sum() == want2[c - 1]
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_device_edge_dropout_graph_equals_host_builder(cuda, seed):
+    """LayerGCN's per-epoch masked adjacency built on the device (DeviceEdgeDropout)
+    == the host builder (graph.layergcn_masked_adj, pinned against the reference's
+    tensors by the e2e parity test) on the same kept edges: rowptr, col and the
+    float32 values bit for bit.  Plus the draw: exactly keep_len distinct edges, for
+    the multinomial and the uniform epochs; an edge with weight 0 never kept by the
+    multinomial."""
+    from rsx.layergcn import DeviceEdgeDropout
+
+    rng = np.random.default_rng(seed)
+    nu, ni = 700, 300
+    pairs = np.unique(np.stack([rng.integers(0, nu, 9000), (rng.zipf(1.4, 9000) - 1) % ni], 1), axis=0)
+    e_u, e_i = pairs[:, 0].astype(np.int64), pairs[:, 1].astype(np.int64)
+    w = graph.layergcn_edge_values(e_u, e_i, nu, ni)
+    w[5] = 0.0
+    dd = DeviceEdgeDropout(e_u, e_i, nu, ni, w, cuda, chunk=32)
+    E = e_u.size
+    keep_len = int(E * 0.9)
+    for pruning_random in (False, True):
+        torch.manual_seed(seed)
+        mask = dd.keep_mask(keep_len, pruning_random)
+        m = mask.cpu().numpy()
+        assert int(m.sum()) == keep_len
+        if not pruning_random:
+            assert not m[5]
+        rp, col, val = dd.build(mask, keep_len)
+        want = graph.layergcn_masked_adj(e_u[m], e_i[m], nu, ni)
+        assert np.array_equal(rp.cpu().numpy(), want[0])
+        assert np.array_equal(col.cpu().numpy(), want[1])
+        assert np.array_equal(val.cpu().numpy().view(np.uint32), want[2].view(np.uint32))
+        A = dd.epoch_graph(0.1, pruning_random)
+        assert A.nnz == 2 * keep_len and A.n_rows == nu + ni
+        x = torch.randn(nu + ni, 64, device=cuda)
+        ref = torch.sparse_csr_tensor(A.rowptr, A.col.long(), A.val, (nu + ni, nu + ni)).to_dense() @ x
+        assert torch.allclose(A.spmm(x), ref, rtol=1e-5, atol=1e-6)
