@@ -97,6 +97,35 @@ def knn_graph(feat: np.ndarray, k: int):
     return r.numpy().astype(np.int64), c.numpy().astype(np.int64), w.numpy().astype(np.float32)
 
 
+def knn_graph_device(feat: torch.Tensor, k: int, chunk_bytes: int = 1 << 30):
+    """build_sim + build_knn_normalized_graph(sparse, 'sym') on the device: the dense
+    cosine similarity as a library GEMM (MFMA) in row chunks of <= chunk_bytes (2.1
+    GB for all of Amazon-clothing: nothing at 288 GB of HBM), torch.topk per row, and
+    the sym-norm in the reference's CPU order (deg = the row's kept values added in
+    rank order, as its index_add over row-major edges; 1/sqrt(deg), ATen's pow(-0.5);
+    (d_r * v) * d_c).  The similarities are GPU GEMM sums, so values can differ from
+    the CPU build in the last bits and neighbours at exact near-ties can swap
+    (tests/test_gpu_smore.py pins that).  Returns host (rows, cols, vals) like knn_graph."""
+    x = feat.to(torch.float32)
+    xn = x.div(torch.norm(x, p=2, dim=-1, keepdim=True))
+    n = xn.shape[0]
+    step = max(1, chunk_bytes // (4 * max(n, 1)))
+    vs, ids = [], []
+    for s in range(0, n, step):
+        v, i = torch.topk(xn[s:s + step] @ xn.t(), k, dim=-1)
+        vs.append(v)
+        ids.append(i)
+    v, i = torch.cat(vs), torch.cat(ids)
+    deg = v[:, 0].clone()
+    for j in range(1, k):
+        deg = deg + v[:, j]
+    dis = 1.0 / torch.sqrt(deg)
+    dis = torch.where(torch.isinf(dis), torch.zeros_like(dis), dis)
+    w = dis[:, None] * v * dis[i]
+    r = np.repeat(np.arange(n, dtype=np.int64), k)
+    return r, i.reshape(-1).cpu().numpy().astype(np.int64), w.reshape(-1).cpu().numpy().astype(np.float32)
+
+
 def max_pool_union(a, b, n):
     """Elementwise max over the union of two edge sets (smore.py:153-174)."""
     ka = a[0] * n + a[1]
@@ -170,6 +199,9 @@ class SMORE(GeneralRecommender):
         rows = np.repeat(np.arange(nu), np.diff(rrp))
         self.R = _DevGraph(rows, rcol.astype(np.int64), rval, nu, ni, self.device, chunk)
         root = os.path.abspath((config["data_path"] or "") + (config["dataset"] or ""))
+        self.knn_mode = config["rsx_knn"] or config["rsx_sampler"] or "device"
+        if self.knn_mode not in ("device", "host"):
+            raise ValueError(f"rsx_knn must be 'device' or 'host', got {self.knn_mode!r}")
         img_g = txt_g = None
         if self.v_feat is not None:
             self.image_embedding = nn.Embedding.from_pretrained(self.v_feat.clone(), freeze=False)
@@ -215,14 +247,18 @@ class SMORE(GeneralRecommender):
 
     # ---------------------------------------------------------------- graphs
     def _cached_knn(self, root, name, feat, k):
-        path = os.path.join(root, f"rsx_{name}_knn_{k}.npz")
+        """kNN item graph (reference smore.py:45-75, cached like its image_adj_{k}.pt):
+        built on the device (knn_graph_device) or, with rsx_knn: host (the default when
+        rsx_sampler is host), by the CPU restatement of the reference's build."""
+        device_build = self.knn_mode == "device"
+        path = os.path.join(root, f"rsx_{name}_knn_{k}{'_dev' if device_build else ''}.npz")
         f = feat.detach().cpu().numpy()
         sig = np.array([f.shape[0], f.shape[1], float(np.float64(f[:4].sum())), float(np.float64(f[-4:].sum()))])
         if os.path.exists(path):
             z = np.load(path)
             if np.array_equal(z["sig"], sig):
                 return z["r"], z["c"], z["v"]
-        r, c, v = knn_graph(f, k)
+        r, c, v = knn_graph_device(feat.detach().to(self.device), k) if device_build else knn_graph(f, k)
         try:
             os.makedirs(root, exist_ok=True)
             np.savez(path, r=r, c=c, v=v, sig=sig)

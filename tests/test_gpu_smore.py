@@ -254,3 +254,42 @@ def test_rsx_adam_matches_torch_single_tensor(cuda):
         ob.step()
     for x, y in zip(a, b):
         np.testing.assert_allclose(y.detach().cpu().numpy(), x.detach().cpu().numpy(), rtol=0, atol=1e-6)
+
+
+@pytest.mark.parametrize("src", ["golden_image", "golden_text", "random"])
+def test_knn_graph_device_vs_host(cuda, golden, src):
+    """SMORE's kNN item graph built on the device (GEMM + topk + sym-norm) against the
+    CPU restatement of the reference's build (knn_graph, pinned bit for bit to the
+    reference's graphs by test_smore_init_graphs_forward): per row the same
+    neighbours except where the host's cosine similarities of the swapped items tie
+    with the k-th within 1e-5 (the GEMMs add in another order), and the normalised
+    values of the common edges within rtol 2e-5."""
+    from rsx.smore import knn_graph, knn_graph_device
+
+    if src == "random":
+        f = np.random.default_rng(3).standard_normal((1500, 768)).astype(np.float32)
+        k = 20
+    else:
+        z = golden("smore_small")
+        f = z["v_feat" if src == "golden_image" else "t_feat"].astype(np.float32)
+        k = 10 if src == "golden_image" else 8
+    n = f.shape[0]
+    hr, hc, hv = knn_graph(f, k)
+    dr, dc, dv = knn_graph_device(torch.from_numpy(f).to(cuda), k)
+    assert np.array_equal(hr, dr)
+    fn = f.astype(np.float64) / np.linalg.norm(f.astype(np.float64), axis=1, keepdims=True)
+    hc, dc, hv, dv = hc.reshape(n, k), dc.reshape(n, k), hv.reshape(n, k), dv.reshape(n, k)
+    swapped = 0
+    for r in range(n):
+        a, b = set(hc[r].tolist()), set(dc[r].tolist())
+        if a != b:
+            sims = fn[r] @ fn.T
+            kth = np.sort(sims)[-k]
+            for c in a ^ b:
+                assert abs(sims[c] - kth) <= 1e-5, (r, c, sims[c], kth)
+            swapped += 1
+            continue
+        hm = dict(zip(hc[r].tolist(), hv[r].tolist()))
+        for c, v in zip(dc[r].tolist(), dv[r].tolist()):
+            assert abs(v - hm[c]) <= 2e-5 * abs(hm[c]) + 1e-7, (r, c, v, hm[c])
+    assert swapped <= max(2, n // 100)
