@@ -94,6 +94,11 @@ WORKLOADS = {
     "c3": dict(model="SMORE", dataset="baby", desc="C3: SMORE d=64, baby-shaped, image 4096 / text 384 N(0,1) features, "
                                                  "kNN 20/15, model-level mirror gradient, B=2048, device sampler",
                cfg=dict(mg_verbose=False, diag_spectrum=False, diag_gate=False, diag_grad=False)),
+    "c5": dict(model="SMORE", dataset="clothing", desc="C5: SMORE d=128, clothing-shaped (39,387 users x 23,033 items), "
+                                                      "CLIP-like L2-normalised 768/768 N(0,1) features, kNN 20/15, "
+                                                      "model-level mirror gradient, B=2048, device sampler, 1 GPU",
+               cfg=dict(embedding_size=128, mg_verbose=False, diag_spectrum=False, diag_gate=False, diag_grad=False),
+               feats=(768, 768, True), feat_files=("image_feat.npy", "text_feat.npy")),
 }
 
 
@@ -114,8 +119,10 @@ def bench_model(args):
     synth.write_inter(df, root, w["dataset"])
     ni = int(df.itemID.max()) + 1
     if w["model"] == "SMORE":
-        np.save(os.path.join(root, w["dataset"], "image_feat_raw.npy"), synth.features(ni, 4096, 1))
-        np.save(os.path.join(root, w["dataset"], "text_feat_raw.npy"), synth.features(ni, 384, 2))
+        dv, dt, l2 = w.get("feats", (4096, 384, False))
+        fv, ft = w.get("feat_files", ("image_feat_raw.npy", "text_feat_raw.npy"))  # configs/dataset/<name>.yaml
+        np.save(os.path.join(root, w["dataset"], fv), synth.features(ni, dv, 1, l2_normalise=l2))
+        np.save(os.path.join(root, w["dataset"], ft), synth.features(ni, dt, 2, l2_normalise=l2))
     cfg = dict(data_path=root + "/", train_batch_size=args.batch, rsx_sampler="device",
                is_multimodal_model=w["model"] == "SMORE", **w["cfg"])
     c = Config(w["model"], w["dataset"], cfg)
@@ -178,8 +185,9 @@ def bench_model(args):
         "scaling": "weak", "vs_baseline": None, "dtype": "f32",
         "data": f"synthetic Amazon-{w['dataset']}-shaped graph (rsx.synth seed 0)"
                 + ("; N(0,1) features" if w["model"] == "SMORE" else ""),
-        "config": {"workload": w["desc"], "model": w["model"], "global_batch": args.batch, "parallelism": "single",
-                   "fused_step": bool(t.fused)},
+        "config": {"workload": w["desc"], "model": w["model"], "embedding_size": int(c["embedding_size"]),
+                   "global_batch": args.batch, "parallelism": "single", "fused_step": bool(t.fused),
+                   "graph_step": t._graph is not None and t._graph.replays > 0},
         "fullsort_items_per_s": n_eval * ni / eval_s,
         "fullsort": {"eval_users": n_eval, "n_items": ni, "s_per_eval_incl_forward_and_metrics": eval_s},
         "model_build_s": build_s, "roofline": None, "cpu_baseline": None,
@@ -235,7 +243,7 @@ def load_graph(workload, rank, world, c4_chunks=None):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", default="c2", choices=["c2", "c1", "c3", "c4"],
+    ap.add_argument("--workload", default="c2", choices=["c2", "c1", "c3", "c4", "c5"],
                     help="c2 (default): the headline LightGCN sports config; c1/c3: LayerGCN / SMORE on baby; "
                          "c4: LightGCN d=256 on the 10M-user graph, row-sharded")
     ap.add_argument("--gpus", type=int, default=1)
@@ -252,9 +260,9 @@ def main():
     args.steps = args.steps if args.steps is not None else (20 if big else 200)
     args.warmup = args.warmup if args.warmup is not None else (3 if big else 20)
     args.eval_users = args.eval_users if args.eval_users is not None else (32768 if big else 0)
-    if args.workload in ("c1", "c3"):
+    if args.workload in ("c1", "c3", "c5"):
         if int(os.environ.get("WORLD_SIZE", "1")) != 1:
-            raise SystemExit("--workload c1/c3 are single-GPU legs")
+            raise SystemExit("--workload c1/c3/c5 are single-GPU legs")
         return bench_model(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
