@@ -6,103 +6,173 @@
 //   * the modality projections image_trs / text_trs (:256-259) in the spectral
 //     backward: d W_v = d img^T V, a 64 x 4096 output over the 7k items.
 // A library GEMM sees a tiny output and runs the long reduction on a few
-// workgroups.  Here the reduction is split: block (tile, s) computes one 32 x 32
-// output tile over row range s with its 4 waves taking interleaved 16-row chunks
-// (fp32 MFMA, exact f32 fma chains, next chunk prefetched), adds the 4 wave tiles
-// in LDS in wave order and writes the tile of partial s; a second pass adds the
-// partials in a fixed order.  Deterministic: the result depends only on the shapes.
+// workgroups.  Here the reduction is split (WgPlan): each wave computes a 32 x 32*IG
+// strip over its rows (fp32 MFMA, exact f32 fma chains, next chunk prefetched, one
+// g value feeding IG MFMAs) and writes it to its partial slot; a second pass adds
+// the slots in a fixed order.  Deterministic: the result depends only on the shapes.
+#include <type_traits>
+
 #include "rsx_common.hpp"
 
 namespace rsx {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
-constexpr int kWgChunk = 16;        // rows per wave step: 8 MFMAs of 2 rows
-constexpr int kWgMinRows = 64;      // rows per block at least (one chunk per wave)
-constexpr int kWgTargetBlocks = 512;
+constexpr int kWgChunk = 16;         // rows per wave step: 8 MFMA k-steps of 2 rows
+constexpr int kWgTargetWaves = 2048; // two per SIMD (LDS-staged blocks interleave)
 
+// Block geometry: a wave computes a 32 x (32*IG) strip of dW (one A value feeds IG
+// MFMAs); the block's 4 waves take OTB strips of rows o (OTB = min(4, out/32)) and
+// RW = 4/OTB row groups (16 rows each of every 16*RW-row block step).  Each row
+// group of each block writes its own partial (slot s*RW + r); the reduce adds the
+// slots in order.
 struct WgPlan {
-    int64_t rows;  // rows per block (multiple of 64)
+    int ig;        // i tiles per wave (1, 2 or 4)
+    int otb, rw;   // o strips per block, row groups per block
+    int64_t nob, nib;  // blocks along o and i
+    int64_t rows;  // rows per block (multiple of kWgChunk * rw)
     int splits;    // S
+    int slots() const { return splits * rw; }
 };
 
-// S ~ kWgTargetBlocks / tiles, at most half the input bytes in partials, at least
-// kWgMinRows rows per block.
 static WgPlan wg_plan(int64_t n, int out_dim, int in_dim) {
-    const int64_t tiles = (int64_t)(out_dim / 32) * (in_dim / 32);
-    int64_t s = (kWgTargetBlocks + tiles - 1) / tiles;
-    const int64_t cap = ((int64_t)n * (out_dim + in_dim) / 2) / ((int64_t)out_dim * in_dim);
-    if (s > cap) s = cap;
-    const int64_t smax = (n + kWgMinRows - 1) / kWgMinRows;
-    if (s > smax) s = smax;
+    WgPlan p;
+    const int it = in_dim / 32, ot = out_dim / 32;
+    p.ig = (it % 4 == 0) ? 4 : (it % 2 == 0) ? 2 : 1;
+    p.otb = ot % 4 == 0 ? 4 : ot % 2 == 0 ? 2 : 1;
+    p.rw = 4 / p.otb;
+    p.nob = ot / p.otb;
+    p.nib = it / p.ig;
+    const int64_t grid_waves = p.nob * p.nib * 4;
+    int64_t s = (kWgTargetWaves + grid_waves - 1) / grid_waves;
+    // partials: at most a quarter of the input bytes (or 4 MB)
+    const int64_t in_bytes = n * (int64_t)(out_dim + in_dim) * 4;
+    const int64_t slot_bytes = (int64_t)out_dim * in_dim * 4;
+    const int64_t cap_bytes = in_bytes / 4 > (4 << 20) ? in_bytes / 4 : (4 << 20);
+    const int64_t smax_bytes = cap_bytes / (slot_bytes * p.rw);
+    if (s > smax_bytes) s = smax_bytes;
+    const int64_t step = (int64_t)kWgChunk * p.rw;
+    const int64_t smax_rows = (n + step - 1) / step;  // at least one chunk per row group
+    if (s > smax_rows) s = smax_rows;
     if (s < 1) s = 1;
     int64_t rows = (n + s - 1) / s;
-    rows = (rows + kWgMinRows - 1) / kWgMinRows * kWgMinRows;
-    if (rows < kWgMinRows) rows = kWgMinRows;
-    s = n > 0 ? (n + rows - 1) / rows : 1;
-    return {rows, (int)s};
+    rows = (rows + step - 1) / step * step;
+    p.rows = rows;
+    p.splits = (int)(n > 0 ? (n + rows - 1) / rows : 1);
+    return p;
 }
 
-// lane l of a 16-row chunk at row c0: A = g[c0 + 2q + h][o0 + j], B = x[...][i0 + j]
-// for the q-th MFMA (k index h = l >> 5 on both sides), zero past r1
-__device__ __forceinline__ void wg_load(const float* __restrict__ g, const float* __restrict__ x, int64_t c0,
-                                        int64_t r1, int out_dim, int in_dim, int o0, int i0, int j, int h,
-                                        float (&av)[8], float (&bv)[8]) {
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        const int64_t row = c0 + 2 * q + h;
-        const bool ok = row < r1;
-        av[q] = ok ? g[row * out_dim + o0 + j] : 0.f;
-        bv[q] = ok ? x[row * in_dim + i0 + j] : 0.f;
-    }
-}
-
+// One block step = CH = 16*RW rows: the block loads the chunk's g[:, o cols] and
+// x[:, i cols] slices with float4 loads into LDS (double-buffered, the next chunk's
+// loads in flight during this chunk's MFMAs), then row group r computes its 16
+// rows from LDS: A = g[2u + h][wo + j], B_q = x[2u + h][32q + j].
+template <int IG, int OTB>
 __global__ __launch_bounds__(256) void wgrad_partial(const float* __restrict__ g, const float* __restrict__ x,
-                                                     int64_t n, int out_dim, int in_dim, int64_t rows,
-                                                     float* __restrict__ part) {
-    __shared__ float red[4][32 * 33];
+                                                     int64_t n, int out_dim, int in_dim, int64_t rows, int64_t nob,
+                                                     int64_t nib, float* __restrict__ part) {
+    constexpr int RW = 4 / OTB;
+    constexpr int OC = 32 * OTB, IC = 32 * IG;   // block's o / i columns
+    constexpr int CH = kWgChunk * RW;            // rows per block step
+    constexpr int GP = OC + 4, XP = IC + 4;      // padded LDS rows
+    constexpr int NG = CH * OC / 4, NX = CH * IC / 4;  // float4s per step
+    constexpr int PER = (NG + NX + 255) / 256;
+    __shared__ float gs[2][CH * GP];
+    __shared__ float xs[2][CH * XP];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, j = lane & 31, h = lane >> 5;
-    const int ti = in_dim / 32, tiles = (out_dim / 32) * ti;
-    const int tile = blockIdx.x % tiles;
-    const int64_t s = blockIdx.x / tiles;
-    const int o0 = (tile / ti) * 32, i0 = (tile % ti) * 32;
+    const int64_t bo = blockIdx.x % nob, bi = (blockIdx.x / nob) % nib, s = blockIdx.x / (nob * nib);
+    const int ob = (int)bo * OC, ib = (int)bi * IC;
+    const int wo = (wave % OTB) * 32;  // wave's o strip within the block
+    const int r = wave / OTB;          // row group
     const int64_t r0 = s * rows;
     const int64_t r1 = min(n, r0 + rows);
-    const int64_t nch = (r1 - r0 + kWgChunk - 1) / kWgChunk;
-    floatx16 acc;
+    const int64_t nst = (r1 - r0 + CH - 1) / CH;
+    floatx16 acc[IG];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    float av[8], bv[8];
-    int64_t c = wave;  // wave-uniform: the MFMAs need the whole wave
-    if (c < nch) wg_load(g, x, r0 + c * kWgChunk, r1, out_dim, in_dim, o0, i0, j, h, av, bv);
-    for (; c < nch; c += 4) {
-        float an[8], bn[8];
-        const bool more = c + 4 < nch;
-        if (more) wg_load(g, x, r0 + (c + 4) * kWgChunk, r1, out_dim, in_dim, o0, i0, j, h, an, bn);
+    for (int q = 0; q < IG; ++q)
 #pragma unroll
-        for (int q = 0; q < 8; ++q) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[q], bv[q], acc, 0, 0, 0);
-        if (more) {
+        for (int e = 0; e < 16; ++e) acc[q][e] = 0.f;
+    // global -> registers two steps ahead (st[k & 1]), registers -> LDS one step ahead
+    float4 st[2][PER];
+    auto gload = [&](int64_t c, float4(&v)[PER]) __attribute__((always_inline)) {
+        const int64_t c0 = r0 + c * CH;
 #pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                av[q] = an[q];
-                bv[q] = bn[q];
+        for (int k = 0; k < PER; ++k) {
+            const int e = threadIdx.x + 256 * k;
+            float4 t = f4(0.f);
+            if (e < NG) {
+                const int rr = e / (OC / 4), cc = (e % (OC / 4)) * 4;
+                const int64_t row = c0 + rr;
+                if (row < r1) t = ld4(g + row * out_dim + ob + cc);
+            } else if (e < NG + NX) {
+                const int e2 = e - NG;
+                const int rr = e2 / (IC / 4), cc = (e2 % (IC / 4)) * 4;
+                const int64_t row = c0 + rr;
+                if (row < r1) t = ld4(x + row * in_dim + ib + cc);
+            }
+            v[k] = t;
+        }
+    };
+    auto sstore = [&](int b, const float4(&v)[PER]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int e = threadIdx.x + 256 * k;
+            float* d = nullptr;
+            if (e < NG) {
+                d = &gs[b][(e / (OC / 4)) * GP + (e % (OC / 4)) * 4];
+            } else if (e < NG + NX) {
+                const int e2 = e - NG;
+                d = &xs[b][(e2 / (IC / 4)) * XP + (e2 % (IC / 4)) * 4];
+            }
+            if (d) {
+                d[0] = v[k].x;
+                d[1] = v[k].y;
+                d[2] = v[k].z;
+                d[3] = v[k].w;
             }
         }
+    };
+    if (nst > 0) {
+        gload(0, st[0]);
+        if (nst > 1) gload(1, st[1]);
+        sstore(0, st[0]);
     }
-    // C layout: lane holds column i0 + j, rows o0 + (r&3) + 8(r>>2) + 4h
-#pragma unroll
-    for (int r = 0; r < 16; ++r) red[wave][((r & 3) + 8 * (r >> 2) + 4 * h) * 33 + j] = acc[r];
     __syncthreads();
-    float* dst = part + s * (int64_t)out_dim * in_dim;
+    // one block step on buffer / register slot B (a template constant: st[] stays in
+    // registers); step c+1's data (loaded a step ago) goes to the other buffer after
+    // this step's MFMAs, step c+2's loads are issued into the slot just freed
+    auto step = [&](int64_t c, auto bc) __attribute__((always_inline)) {
+        constexpr int B = decltype(bc)::value;
+        if (c + 2 < nst) gload(c + 2, st[B]);
+        const float* gb = gs[B] + (r * kWgChunk) * GP + wo + j;
+        const float* xb = xs[B] + (r * kWgChunk) * XP + j;
+        float av[8], bv[8][IG];
 #pragma unroll
-    for (int e = threadIdx.x; e < 1024; e += 256) {
-        const int o = e >> 5, i = e & 31;
-        const float v = ((red[0][o * 33 + i] + red[1][o * 33 + i]) + red[2][o * 33 + i]) + red[3][o * 33 + i];
-        dst[(int64_t)(o0 + o) * in_dim + i0 + i] = v;
+        for (int u = 0; u < 8; ++u) {
+            av[u] = gb[(2 * u + h) * GP];
+#pragma unroll
+            for (int q = 0; q < IG; ++q) bv[u][q] = xb[(2 * u + h) * XP + 32 * q];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+#pragma unroll
+            for (int q = 0; q < IG; ++q) acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv[u][q], acc[q], 0, 0, 0);
+        if (c + 1 < nst) sstore(B ^ 1, st[B ^ 1]);
+        __syncthreads();
+    };
+    for (int64_t c = 0; c < nst; c += 2) {  // block-uniform
+        step(c, std::integral_constant<int, 0>{});
+        if (c + 1 < nst) step(c + 1, std::integral_constant<int, 1>{});
     }
+    // C layout: lane holds column ib + 32q + j, rows ob + wo + (e&3) + 8(e>>2) + 4h
+    float* dst = part + (s * RW + r) * (int64_t)out_dim * in_dim;
+#pragma unroll
+    for (int q = 0; q < IG; ++q)
+#pragma unroll
+        for (int e = 0; e < 16; ++e)
+            dst[(int64_t)(ob + wo + (e & 3) + 8 * (e >> 2) + 4 * h) * in_dim + ib + 32 * q + j] = acc[q][e];
 }
 
-// element e = blockIdx.x*64 + lane; wave w adds partials [w*S/4, (w+1)*S/4) in
+// element e = blockIdx.x*64 + lane; wave w adds slots [w*S/4, (w+1)*S/4) in
 // order, 8 loads in flight; the quarters are added in wave order
 __global__ __launch_bounds__(256) void wgrad_reduce(const float* __restrict__ part, int S, int64_t sz,
                                                     float* __restrict__ dw) {
@@ -134,7 +204,7 @@ using namespace rsx;
 extern "C" size_t rsx_linear_wgrad_ws_bytes(int64_t n, int32_t out_dim, int32_t in_dim) {
     if (n <= 0 || out_dim <= 0 || in_dim <= 0 || (out_dim % 32) || (in_dim % 32)) return 0;
     const WgPlan p = wg_plan(n, out_dim, in_dim);
-    return (size_t)p.splits * (size_t)out_dim * (size_t)in_dim * sizeof(float);
+    return (size_t)p.slots() * (size_t)out_dim * (size_t)in_dim * sizeof(float);
 }
 
 extern "C" int rsx_linear_wgrad(const float* g, const float* x, int64_t n, int32_t out_dim, int32_t in_dim, float* dw,
@@ -151,11 +221,25 @@ extern "C" int rsx_linear_wgrad(const float* g, const float* x, int64_t n, int32
     }
     if (ws_bytes < rsx_linear_wgrad_ws_bytes(n, out_dim, in_dim) || !ws) return RSX_ERR_WORKSPACE;
     const WgPlan p = wg_plan(n, out_dim, in_dim);
-    const int64_t tiles = (int64_t)(out_dim / 32) * (in_dim / 32);
     float* part = static_cast<float*>(ws);
-    hipLaunchKernelGGL(wgrad_partial, dim3((unsigned)(tiles * p.splits)), dim3(256), 0, s, g, x, n, (int)out_dim,
-                       (int)in_dim, p.rows, part);
-    hipLaunchKernelGGL(wgrad_reduce, dim3((unsigned)((sz + 63) / 64)), dim3(256), 0, s, (const float*)part, p.splits,
+    const dim3 grid((unsigned)(p.nob * p.nib * p.splits));
+#define RSX_WG(IG, OTB)                                                                                        \
+    hipLaunchKernelGGL((wgrad_partial<IG, OTB>), grid, dim3(256), 0, s, g, x, n, (int)out_dim, (int)in_dim, p.rows, \
+                       p.nob, p.nib, part)
+    const int key = p.ig * 8 + p.otb;
+    switch (key) {
+        case 4 * 8 + 4: RSX_WG(4, 4); break;
+        case 4 * 8 + 2: RSX_WG(4, 2); break;
+        case 4 * 8 + 1: RSX_WG(4, 1); break;
+        case 2 * 8 + 4: RSX_WG(2, 4); break;
+        case 2 * 8 + 2: RSX_WG(2, 2); break;
+        case 2 * 8 + 1: RSX_WG(2, 1); break;
+        case 1 * 8 + 4: RSX_WG(1, 4); break;
+        case 1 * 8 + 2: RSX_WG(1, 2); break;
+        default: RSX_WG(1, 1); break;
+    }
+#undef RSX_WG
+    hipLaunchKernelGGL(wgrad_reduce, dim3((unsigned)((sz + 63) / 64)), dim3(256), 0, s, (const float*)part, p.slots(),
                        sz, dw);
     return last_rc();
 }

@@ -1,49 +1,57 @@
 // smore.hip — SMORE's modality projection + spectral denoise / cross-modal fusion
-// as one fused pass (reference src/models/smore.py:209-237 spectrum_convolution and
-// :256-259 image_trs / text_trs), and the fused backward of the spectral part.
+// (reference src/models/smore.py:209-237 spectrum_convolution and :256-259
+// image_trs / text_trs) and the backward of the spectral part, all on fp32 MFMA
+// (exact f32 products, f32 sums: the same arithmetic as an fmaf chain).
 //
-// Forward, per block of 32 items (4 wavefronts):
-//   1. img = V W_v^T + b_v, txt = T W_t^T + b_t on fp32 MFMA (v_mfma_f32_32x32x2f32,
-//      exact f32): the K dimension (feature width, 4096 raw image / 384 text at
-//      Amazon-baby) is split over the 4 waves, partial tiles summed in LDS in wave
-//      order (deterministic), bias first.
-//   2. rfft(norm='ortho') of both rows as direct real DFTs against an LDS twiddle
-//      table (d <= 128: d*(d/2+1) MACs per row, far below the projection), the
-//      per-bin complex weights (already unit-normalised by the caller, as
-//      reference :221-229), the cross-modal product Ft*Fi*wf, and three irfft's.
-//   img / txt are written out as well (saved for the backward).
-// Backward (spectral part): dY = irfft^T(dconv); dF = dY * conj(w) (+ the product
-// rule for the fusion term); d img / d txt = rfft^T(dF); per-block partial sums of
-// dw in the parameter layout [3][d/2+1][2].  The projection gradients
-// (dW = d img^T V, dV = d img W, db) are plain GEMMs / reductions left to the
-// caller (rocBLAS via torch).
+// 1. smore_proj: img = V W_v^T + b_v, txt = T W_t^T + b_t (v_mfma_f32_32x32x2f32).
+//    A block owns 32 items of one modality; its 4 waves split the feature width K
+//    (4096 raw image / 384 text at Amazon-baby, 768 CLIP at clothing), loads one
+//    step ahead of the MFMAs, and add their tiles in LDS in wave order (bias first).
+// 2. smore_spec_fwd: a length-d real DFT is a d x (d+2) real matrix, so
+//    rfft(norm='ortho') of 16 items is a [(d+2) x d] x [d x 16] product on
+//    v_mfma_f32_16x16x4f32: the rows (Re, Im of bin b at 2b, 2b+1) come from an LDS
+//    twiddle table with 1/sqrt(d) folded in, the items are the MFMA's columns.  The
+//    accumulator of one MFMA holds (Re, Im) pairs of whole bins per lane, so the
+//    per-bin complex weights (unit-normalised by the caller, reference :221-229)
+//    and the cross-modal product Ft*Fi*wf are register ops, and those registers
+//    feed the three irfft products directly as B operands (the k index of an MFMA
+//    may be permuted freely as long as A uses the same permutation): no LDS
+//    transposes.  One wave = 16 items, no block-level synchronisation.
+// 3. smore_spec_bwd: dY = irfft^T(d conv) (the same matrices transposed), the
+//    complex product rules, d w per block (lane-group reductions, waves added in
+//    order: deterministic), d img / d txt = rfft^T(dF).  The projection gradients
+//    (dW = d img^T V on the split-K kernel, dV = d img W, db) are left to the caller.
 #include "rsx_common.hpp"
 
 namespace rsx {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
 
-struct SpecFwdArgs {
+// ---------------------------------------------------------------------------
+// projection
+// ---------------------------------------------------------------------------
+struct SpecProjArgs {
     const float* X[2];  // V [n, K0], T [n, K1]
     int32_t K[2];
     const float* W[2];  // [d, K]
     const float* b[2];  // [d]
-    const float* w[3];  // unit complex weights [(d/2+1)][2]: image, text, fusion
     int64_t n;
-    float* xo[2];       // img, txt [n, d]
-    float* conv[3];     // conv_v, conv_t, conv_f [n, d]
+    float* out[2];      // img, txt [n, d]
 };
 
-// MFMA projection of 32 rows (row0..) of X [n, K] by W [D, K] into xs[32][D+1]
-// (+ bias).  Wave w owns the k-slice [w*per, (w+1)*per) in steps of 8; lane l
-// feeds item row l&31 and, within a step of 8, k = 4*(l>>5) + q for the q-th of 4
-// MFMAs (the same permutation on the A and B side).
+// lane l feeds item row l&31 and, within a step of 8, k = 4*(l>>5) + q for the q-th
+// of 4 MFMAs (the same permutation on the A and B side)
 template <int D>
-__device__ __forceinline__ void project32(const float* __restrict__ X, int K, const float* __restrict__ W,
-                                          const float* __restrict__ bias, int64_t row0, int64_t n,
-                                          float (*xs)[D + 1]) {
+__global__ __launch_bounds__(256) void smore_proj(SpecProjArgs a) {
     constexpr int NT = D / 32;
+    __shared__ float xs[32][D + 1];
+    const int m = blockIdx.y;
+    const float* __restrict__ X = a.X[m];
+    const float* __restrict__ W = a.W[m];
+    const int K = a.K[m];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, j = lane & 31, h = lane >> 5;
+    const int64_t row0 = (int64_t)blockIdx.x * 32;
     floatx16 acc[NT];
 #pragma unroll
     for (int c = 0; c < NT; ++c)
@@ -53,21 +61,36 @@ __device__ __forceinline__ void project32(const float* __restrict__ X, int K, co
     const int per = (steps + 3) / 4;
     const int kb = wave * per * 8, ke = min(K, (wave + 1) * per * 8);
     const int64_t row = row0 + j;
-    const float* xr = X + (row < n ? row : 0) * (int64_t)K;
-    for (int k = kb; k < ke; k += 8) {
+    const bool rv = row < a.n;
+    const float* xr = X + (rv ? row : 0) * (int64_t)K;
+    auto load = [&](int k, float4& va, float4(&vb)[NT]) __attribute__((always_inline)) {
         const int kk = k + 4 * h;
         const bool ok = kk < ke;  // K % 4 == 0: the whole float4 is in range
-        const float4 a = (ok && row < n) ? ld4(xr + kk) : f4(0.f);
+        va = (ok && rv) ? ld4(xr + kk) : f4(0.f);
+#pragma unroll
+        for (int c = 0; c < NT; ++c) vb[c] = ok ? ld4(W + (int64_t)(c * 32 + j) * K + kk) : f4(0.f);
+    };
+    float4 ca, cb[NT];
+    if (kb < ke) load(kb, ca, cb);
+    for (int k = kb; k < ke; k += 8) {  // wave-uniform bounds
+        float4 na, nb[NT];
+        const bool more = k + 8 < ke;
+        if (more) load(k + 8, na, nb);
 #pragma unroll
         for (int c = 0; c < NT; ++c) {
-            const float4 bb = ok ? ld4(W + (int64_t)(c * 32 + j) * K + kk) : f4(0.f);
-            acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, bb.x, acc[c], 0, 0, 0);
-            acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, bb.y, acc[c], 0, 0, 0);
-            acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, bb.z, acc[c], 0, 0, 0);
-            acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, bb.w, acc[c], 0, 0, 0);
+            acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(ca.x, cb[c].x, acc[c], 0, 0, 0);
+            acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(ca.y, cb[c].y, acc[c], 0, 0, 0);
+            acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(ca.z, cb[c].z, acc[c], 0, 0, 0);
+            acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(ca.w, cb[c].w, acc[c], 0, 0, 0);
+        }
+        if (more) {
+            ca = na;
+#pragma unroll
+            for (int c = 0; c < NT; ++c) cb[c] = nb[c];
         }
     }
     // C layout: lane holds column (feature) c*32 + j, rows (items) (r&3) + 8(r>>2) + 4h
+    const float* bias = a.b[m];
     for (int w2 = 0; w2 < 4; ++w2) {
         if (wave == w2) {
 #pragma unroll
@@ -81,30 +104,38 @@ __device__ __forceinline__ void project32(const float* __restrict__ X, int K, co
         }
         __syncthreads();
     }
-}
-
-template <int D>
-__device__ __forceinline__ void twiddles(float* twc, float* tws) {
-    for (int t = threadIdx.x; t < D; t += blockDim.x) {
-        double s, c;
-        sincospi(2.0 * (double)t / (double)D, &s, &c);
-        twc[t] = (float)c;
-        tws[t] = (float)s;
+    float* out = a.out[m];
+    for (int e = threadIdx.x; e < 32 * D; e += 256) {
+        const int r = e / D, f = e % D;
+        if (row0 + r < a.n) out[(row0 + r) * D + f] = xs[r][f];
     }
 }
 
-// rfft bin k of a length-D real row (norm='ortho'): (re, im)
+// ---------------------------------------------------------------------------
+// spectral part on 16x16x4 MFMAs
+// ---------------------------------------------------------------------------
 template <int D>
-__device__ __forceinline__ float2 dft_bin(const float* x, int k, const float* twc, const float* tws) {
-    float re = 0.f, im = 0.f;
-#pragma unroll 8
-    for (int t = 0; t < D; ++t) {
-        const int e = (k * t) & (D - 1);
-        re = fmaf(x[t], twc[e], re);
-        im = fmaf(-x[t], tws[e], im);
-    }
-    const float s = rsqrtf((float)D);
-    return make_float2(re * s, im * s);
+struct Spec {
+    static constexpr int NB = D / 2 + 1;          // rfft bins
+    static constexpr int MR = 2 * NB;             // real rows (Re, Im per bin)
+    static constexpr int MT = (MR + 15) / 16;     // 16-row tiles of the spectrum
+    static constexpr int SI = D / 4;              // MFMA steps over the d features
+    static constexpr int OT = D / 16;             // 16-row tiles of the d features
+};
+
+// Keeps the twiddle loads of one MFMA step from being hoisted into earlier steps (or
+// merged with the same loads of another phase): a fully unrolled loop otherwise
+// loads all of them up front, hundreds of live registers and spills.  The LDS
+// tables never escape, so a memory clobber does not order their loads; an opaque
+// index does.  One step is 2-3 x MT MFMAs, ample to cover an LDS read.
+__device__ __forceinline__ void step_fence() { asm volatile("" ::: "memory"); }
+__device__ __forceinline__ int opaque(int x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
+
+__device__ __forceinline__ floatx4 mfma16(float a, float b, floatx4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
@@ -114,159 +145,298 @@ __device__ __forceinline__ float2 cmulc(float2 a, float2 b) {  // a * conj(b)
     return make_float2(a.x * b.x + a.y * b.y, a.y * b.x - a.x * b.y);
 }
 
+// tw[e] = cos(2 pi e / D) / sqrt(D), tw[D + e] = -sin(2 pi e / D) / sqrt(D)  (norm='ortho')
+template <int D>
+__device__ __forceinline__ void twiddles(float* tw) {
+    const double r = 1.0 / sqrt((double)D);
+    for (int t = threadIdx.x; t < D; t += blockDim.x) {
+        double s, c;
+        sincospi(2.0 * (double)t / (double)D, &s, &c);
+        tw[t] = (float)(c * r);
+        tw[D + t] = (float)(-s * r);
+    }
+}
+
+// rfft matrix: row j (Re of bin j/2 for even j, Im for odd j), feature f
+template <int D>
+__device__ __forceinline__ float fwd_coef(int j, int f, const float* tw) {
+    const int e = opaque((((j >> 1) * f) & (D - 1)) + (j & 1) * D);
+    const float v = tw[e];
+    return j < Spec<D>::MR ? v : 0.f;
+}
+
+// irfft matrix: output feature t, spectrum row j; bins 0 and D/2 once (their
+// imaginary parts drop out: sin 0 = sin(pi t) = 0), the others twice
+template <int D>
+__device__ __forceinline__ float inv_coef(int t, int j, const float* tw) {
+    const int b = j >> 1;
+    const int e = opaque(((b * t) & (D - 1)) + (j & 1) * D);
+    const float v = tw[e];
+    const float c = (b == 0 || b == D / 2) ? 1.f : 2.f;
+    return j < Spec<D>::MR ? c * v : 0.f;
+}
+
+// B operand of 16 item rows: lane (g = l>>4, n = l&15) holds x[item][g*SI + s] for
+// step s (contiguous: float4 loads)
+template <int D>
+__device__ __forceinline__ void load_rows(const float* __restrict__ x, int64_t item, bool ok, int g,
+                                          float (&v)[Spec<D>::SI]) {
+    constexpr int SI = Spec<D>::SI;
+    const float* p = x + (ok ? item : 0) * D + g * SI;
+#pragma unroll
+    for (int q = 0; q < SI / 4; ++q) {
+        const float4 t = (ok && x) ? ld4(p + 4 * q) : f4(0.f);
+        v[4 * q] = t.x;
+        v[4 * q + 1] = t.y;
+        v[4 * q + 2] = t.z;
+        v[4 * q + 3] = t.w;
+    }
+}
+
+// F[t] (t < MT): the spectrum of the 16 items; lane (g, n) holds rows 16t + 4g + i,
+// i.e. the (Re, Im) of bins 8t + 2g and 8t + 2g + 1 of item n
+template <int D>
+__device__ __forceinline__ void rfft16(const float (&xi)[Spec<D>::SI], const float (&xt)[Spec<D>::SI], int g, int n16,
+                                       const float* tw, floatx4 (&fi)[Spec<D>::MT],
+                                       floatx4 (&ft)[Spec<D>::MT]) {
+    constexpr int SI = Spec<D>::SI, MT = Spec<D>::MT;
+#pragma unroll
+    for (int t = 0; t < MT; ++t) fi[t] = ft[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < SI; ++s) {
+        const int f = g * SI + s;
+        step_fence();
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+            const float c = fwd_coef<D>(16 * t + n16, f, tw);
+            fi[t] = mfma16(c, xi[s], fi[t]);
+            ft[t] = mfma16(c, xt[s], ft[t]);
+        }
+    }
+}
+
+__device__ __forceinline__ float2 pair(const floatx4& v, int p) { return make_float2(v[2 * p], v[2 * p + 1]); }
+__device__ __forceinline__ void set_pair(floatx4& v, int p, float2 x) {
+    v[2 * p] = x.x;
+    v[2 * p + 1] = x.y;
+}
+
+struct SpecFwdArgs {
+    const float* x[2];  // img, txt [n, d]
+    const float* w[3];  // unit complex weights [(d/2+1)][2]: image, text, fusion
+    int64_t n;
+    float* conv[3];     // conv_v, conv_t, conv_f [n, d]
+};
+
 template <int D>
 __global__ __launch_bounds__(256) void smore_spec_fwd(SpecFwdArgs a) {
-    constexpr int NB = D / 2 + 1;
-    __shared__ float xs[2][32][D + 1];
-    __shared__ float ys[32][3][2][NB];
-    __shared__ float twc[D], tws[D];
-    const int64_t row0 = (int64_t)blockIdx.x * 32;
-    twiddles<D>(twc, tws);
-    project32<D>(a.X[0], a.K[0], a.W[0], a.b[0], row0, a.n, xs[0]);
-    project32<D>(a.X[1], a.K[1], a.W[1], a.b[1], row0, a.n, xs[1]);
-    const int r = threadIdx.x >> 3, sub = threadIdx.x & 7;
-    const int64_t row = row0 + r;
-    // spectra and filtered spectra for bins k = sub + 8i
-    for (int k = sub; k < NB; k += 8) {
-        const float2 fi = dft_bin<D>(xs[0][r], k, twc, tws);
-        const float2 ft = dft_bin<D>(xs[1][r], k, twc, tws);
-        const float2 wv = make_float2(a.w[0][2 * k], a.w[0][2 * k + 1]);
-        const float2 wt = make_float2(a.w[1][2 * k], a.w[1][2 * k + 1]);
-        const float2 wf = make_float2(a.w[2][2 * k], a.w[2][2 * k + 1]);
-        const float2 yv = cmul(fi, wv), yt = cmul(ft, wt), yf = cmul(cmul(ft, fi), wf);
-        ys[r][0][0][k] = yv.x;
-        ys[r][0][1][k] = yv.y;
-        ys[r][1][0][k] = yt.x;
-        ys[r][1][1][k] = yt.y;
-        ys[r][2][0][k] = yf.x;
-        ys[r][2][1][k] = yf.y;
-    }
+    using S = Spec<D>;
+    constexpr int SI = S::SI, MT = S::MT, NB = S::NB, OT = S::OT;
+    __shared__ float tw[2 * D];
+    __shared__ float2 ws[3][NB];
+    twiddles<D>(tw);
+    for (int e = threadIdx.x; e < 3 * NB; e += blockDim.x)
+        ws[e / NB][e % NB] = make_float2(a.w[e / NB][2 * (e % NB)], a.w[e / NB][2 * (e % NB) + 1]);
     __syncthreads();
-    if (row >= a.n) return;
-    const float s = rsqrtf((float)D);
-    for (int t = sub; t < D; t += 8) {
-        a.xo[0][row * D + t] = xs[0][r][t];
-        a.xo[1][row * D + t] = xs[1][r][t];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, n16 = lane & 15, g = lane >> 4;
+    const int64_t item = ((int64_t)blockIdx.x * 4 + wave) * 16 + n16;
+    const bool iv = item < a.n;  // a wave past the end runs on zeros (MFMAs need the whole wave)
+    floatx4 fi[MT], ft[MT], yf[MT];
+    {
+        float xi[SI], xt[SI];
+        load_rows<D>(a.x[0], item, iv, g, xi);
+        load_rows<D>(a.x[1], item, iv, g, xt);
+        rfft16<D>(xi, xt, g, n16, tw, fi, ft);
+    }
+    // filtered spectra: Yv = Fi wv, Yt = Ft wt, Yf = (Ft Fi) wf  (in place for v, t)
 #pragma unroll
-        for (int m = 0; m < 3; ++m) {
-            // irfft(norm='ortho'): bins 0 and D/2 once (their imaginary parts ignored), others twice
-            float acc = ys[r][m][0][0] + ((t & 1) ? -ys[r][m][0][D / 2] : ys[r][m][0][D / 2]);
-            float mid = 0.f;
-            for (int k = 1; k < D / 2; ++k) {
-                const int e = (k * t) & (D - 1);
-                mid = fmaf(ys[r][m][0][k], twc[e], mid);
-                mid = fmaf(-ys[r][m][1][k], tws[e], mid);
+    for (int t = 0; t < MT; ++t)
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            const int b = 8 * t + 2 * g + p;
+            const bool bv = b < NB;
+            const int bb = bv ? b : 0;
+            const float2 Fi = pair(fi[t], p), Ft = pair(ft[t], p);
+            const float2 z = make_float2(0.f, 0.f);
+            set_pair(fi[t], p, bv ? cmul(Fi, ws[0][bb]) : z);
+            set_pair(ft[t], p, bv ? cmul(Ft, ws[1][bb]) : z);
+            set_pair(yf[t], p, bv ? cmul(cmul(Ft, Fi), ws[2][bb]) : z);
+        }
+    // conv_m = irfft(Y_m): output tile tau, step (t, i) <-> spectrum row 16t + 4g + i
+#pragma unroll
+    for (int tau = 0; tau < OT; ++tau) {
+        floatx4 cv{0.f, 0.f, 0.f, 0.f}, ct = cv, cf = cv;
+        const int tq = 16 * tau + n16;
+#pragma unroll
+        for (int t = 0; t < MT; ++t)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                step_fence();
+                const float c = inv_coef<D>(tq, 16 * t + 4 * g + i, tw);
+                cv = mfma16(c, fi[t][i], cv);
+                ct = mfma16(c, ft[t][i], ct);
+                cf = mfma16(c, yf[t][i], cf);
             }
-            acc = fmaf(2.f, mid, acc);
-            a.conv[m][row * D + t] = acc * s;
+        if (iv) {  // lane (g, n) holds features 16 tau + 4g + r of item n
+            const int64_t o = item * D + 16 * tau + 4 * g;
+            st4(a.conv[0] + o, make_float4(cv[0], cv[1], cv[2], cv[3]));
+            st4(a.conv[1] + o, make_float4(ct[0], ct[1], ct[2], ct[3]));
+            st4(a.conv[2] + o, make_float4(cf[0], cf[1], cf[2], cf[3]));
         }
     }
 }
 
 struct SpecBwdArgs {
-    const float* xo[2];  // img, txt [n, d]
+    const float* x[2];  // img, txt [n, d]
     const float* w[3];
-    const float* g[3];   // d conv_v / conv_t / conv_f [n, d] (NULL = 0)
+    const float* g[3];  // d conv_v / conv_t / conv_f [n, d] (NULL = 0)
     int64_t n;
-    float* gx[2];        // d img, d txt [n, d]
-    float* gw;           // [gridDim.x][3][d/2+1][2] per-block partials
+    float* gx[2];       // d img, d txt [n, d]
+    float* gw;          // [gridDim.x][3][d/2+1][2] per-block partials
 };
 
+// the sum over the 16 items (lanes n = 0..15 of lane group g) of x, in lane n == 0
+__device__ __forceinline__ float sum16(float x) {
+    x += __shfl_xor(x, 1, kWave);
+    x += __shfl_xor(x, 2, kWave);
+    x += __shfl_xor(x, 4, kWave);
+    x += __shfl_xor(x, 8, kWave);
+    return x;
+}
+
+// dY = irfft^T(d conv) for the 16 items: dy[t] in the spectrum layout of rfft16
 template <int D>
-__global__ __launch_bounds__(256) void smore_spec_bwd(SpecBwdArgs a) {
-    constexpr int NB = D / 2 + 1;
-    __shared__ float xs[2][32][D + 1];
-    __shared__ float gs[3][32][D + 1];
-    __shared__ float df[32][2][2][NB];  // d spectrum of img / txt
-    __shared__ float dws[4][3][2][NB];  // per-wave d weight (8 rows each)
-    __shared__ float twc[D], tws[D];
-    const int64_t row0 = (int64_t)blockIdx.x * 32;
-    twiddles<D>(twc, tws);
-    for (int e = threadIdx.x; e < 32 * D; e += 256) {
-        const int r = e / D, t = e % D;
-        const int64_t row = row0 + r;
-        const bool ok = row < a.n;
+__device__ __forceinline__ void irfft_t16(const float* __restrict__ gsrc, int64_t item, bool iv, int g, int n16,
+                                          const float* tw, floatx4 (&dy)[Spec<D>::MT]) {
+    constexpr int SI = Spec<D>::SI, MT = Spec<D>::MT;
+    float gin[SI];
+    load_rows<D>(gsrc, item, iv, g, gin);
 #pragma unroll
-        for (int m = 0; m < 2; ++m) xs[m][r][t] = ok ? a.xo[m][row * D + t] : 0.f;
+    for (int t = 0; t < MT; ++t) dy[t] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int m = 0; m < 3; ++m) gs[m][r][t] = (ok && a.g[m]) ? a.g[m][row * D + t] : 0.f;
+    for (int s = 0; s < SI; ++s) {
+        const int f = g * SI + s;
+        step_fence();
+#pragma unroll
+        for (int t = 0; t < MT; ++t) dy[t] = mfma16(inv_coef<D>(f, 16 * t + n16, tw), gin[s], dy[t]);
     }
-    __syncthreads();
-    const int r = threadIdx.x >> 3, sub = threadIdx.x & 7;
-    const float s = rsqrtf((float)D);
-    // uniform trip count over the wave (the d-weight sums below shuffle across rows)
-    for (int i = 0; i < (NB + 7) / 8; ++i) {
-        const int kr = sub + 8 * i;
-        const bool kv = kr < NB;
-        const int k = kv ? kr : 0;
-        const float2 fi = dft_bin<D>(xs[0][r], k, twc, tws);
-        const float2 ft = dft_bin<D>(xs[1][r], k, twc, tws);
-        // dY = irfft^T(g): d/dRe = a_k cos/sqrt(D), d/dIm = -a_k sin/sqrt(D)
-        const float ak = (k == 0 || k == D / 2) ? 1.f : 2.f;
-        float2 dy[3];
+}
+
+// d x = rfft^T(dF) for the 16 items, stored to gx: output tiles in pairs (two
+// independent accumulators), step (t, i) <-> spectrum row 16t + 4g + i
+template <int D>
+__device__ __forceinline__ void rfft_t16_store(const floatx4 (&df)[Spec<D>::MT], float* __restrict__ gx, int64_t item,
+                                               bool iv, int g, int n16, const float* tw) {
+    constexpr int MT = Spec<D>::MT, OT = Spec<D>::OT;
+#pragma unroll 1
+    for (int tau = 0; tau < OT; tau += 2) {  // rolled: bounds the live coefficients to one pair of tiles
+        floatx4 a0{0.f, 0.f, 0.f, 0.f}, a1 = a0;
 #pragma unroll
-        for (int m = 0; m < 3; ++m) {
-            float re = 0.f, im = 0.f;
-            for (int t = 0; t < D; ++t) {
-                const int e = (k * t) & (D - 1);
-                re = fmaf(gs[m][r][t], twc[e], re);
-                im = fmaf(-gs[m][r][t], tws[e], im);
+        for (int t = 0; t < MT; ++t)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                step_fence();
+                const int j = 16 * t + 4 * g + i;
+                a0 = mfma16(fwd_coef<D>(j, 16 * tau + n16, tw), df[t][i], a0);
+                a1 = mfma16(fwd_coef<D>(j, 16 * tau + 16 + n16, tw), df[t][i], a1);
             }
-            dy[m] = make_float2(re * ak * s, im * ak * s);
-        }
-        const float2 wv = make_float2(a.w[0][2 * k], a.w[0][2 * k + 1]);
-        const float2 wt = make_float2(a.w[1][2 * k], a.w[1][2 * k + 1]);
-        const float2 wf = make_float2(a.w[2][2 * k], a.w[2][2 * k + 1]);
-        const float2 p = cmul(ft, fi);
-        const float2 dp = cmulc(dy[2], wf);
-        float2 dfi = cmulc(dy[0], wv), dft = cmulc(dy[1], wt);
-        const float2 a1 = cmulc(dp, ft), a2 = cmulc(dp, fi);
-        dfi = make_float2(dfi.x + a1.x, dfi.y + a1.y);
-        dft = make_float2(dft.x + a2.x, dft.y + a2.y);
-        const float2 dwv = cmulc(dy[0], fi), dwt = cmulc(dy[1], ft), dwf = cmulc(dy[2], p);
-        if (kv) {
-            df[r][0][0][k] = dfi.x;
-            df[r][0][1][k] = dfi.y;
-            df[r][1][0][k] = dft.x;
-            df[r][1][1][k] = dft.y;
-        }
-        // sum the 8 rows of this wave that share bin k (lanes sub, sub+8, ..., sub+56)
-        float c6[6] = {dwv.x, dwv.y, dwt.x, dwt.y, dwf.x, dwf.y};
-#pragma unroll
-        for (int q = 0; q < 6; ++q) {
-            float v = c6[q];
-            v += __shfl_xor(v, 8, kWave);
-            v += __shfl_xor(v, 16, kWave);
-            v += __shfl_xor(v, 32, kWave);
-            c6[q] = v;
-        }
-        if (kv && (threadIdx.x & 63) < 8) {
-            const int w = threadIdx.x >> 6;
-#pragma unroll
-            for (int q = 0; q < 6; ++q) dws[w][q >> 1][q & 1][k] = c6[q];
+        if (iv) {
+            const int64_t o = item * D + 16 * tau + 4 * g;
+            st4(gx + o, make_float4(a0[0], a0[1], a0[2], a0[3]));
+            st4(gx + o + 16, make_float4(a1[0], a1[1], a1[2], a1[3]));
         }
     }
+}
+
+// Order keeps the live state small: the fusion term first (only dp = dYf conj(wf)
+// is kept), then the image term (dFi formed in place of dYv and parked in LDS), the
+// text term (dFt -> d txt, after which Fi, Ft and dp are dead), and d img last.
+template <int D>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 64 ? 2 : 1))) void smore_spec_bwd(
+    SpecBwdArgs a) {
+    using S = Spec<D>;
+    constexpr int SI = S::SI, MT = S::MT, NB = S::NB;
+    __shared__ float tw[2 * D];
+    __shared__ float2 ws[3][NB];
+    __shared__ float2 dws[4][3][NB];
+    __shared__ float dfs[4][4 * MT][64];  // dFi parked per wave, lane-contiguous
+    twiddles<D>(tw);
+    for (int e = threadIdx.x; e < 3 * NB; e += blockDim.x)
+        ws[e / NB][e % NB] = make_float2(a.w[e / NB][2 * (e % NB)], a.w[e / NB][2 * (e % NB) + 1]);
     __syncthreads();
-    // per-block d weight partial, waves summed in order (deterministic)
-    for (int e = threadIdx.x; e < 3 * NB * 2; e += 256) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, n16 = lane & 15, g = lane >> 4;
+    const int64_t item = ((int64_t)blockIdx.x * 4 + wave) * 16 + n16;
+    const bool iv = item < a.n;
+    floatx4 fi[MT], ft[MT];
+    {
+        float xi[SI], xt[SI];
+        load_rows<D>(a.x[0], item, iv, g, xi);
+        load_rows<D>(a.x[1], item, iv, g, xt);
+        rfft16<D>(xi, xt, g, n16, tw, fi, ft);
+    }
+    // d w of bin b (summed over the wave's 16 items) into dws[wave][m][b]
+    auto put_dw = [&](int m, int b, bool bv, float2 dw) __attribute__((always_inline)) {
+        dw.x = sum16(dw.x);
+        dw.y = sum16(dw.y);
+        if (n16 == 0 && bv) dws[wave][m][b] = dw;
+    };
+    floatx4 dp[MT], dy[MT];
+    irfft_t16<D>(a.g[2], item, iv, g, n16, tw, dy);
+#pragma unroll
+    for (int t = 0; t < MT; ++t)
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            const int b = 8 * t + 2 * g + p;
+            const bool bv = b < NB;
+            const float2 dY = pair(dy[t], p);
+            put_dw(2, b, bv, cmulc(dY, cmul(pair(ft[t], p), pair(fi[t], p))));
+            set_pair(dp[t], p, bv ? cmulc(dY, ws[2][bv ? b : 0]) : make_float2(0.f, 0.f));
+        }
+    // image: dFi = dYv conj(wv) + dp conj(Ft)
+    irfft_t16<D>(a.g[0], item, iv, g, n16, tw, dy);
+#pragma unroll
+    for (int t = 0; t < MT; ++t)
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            const int b = 8 * t + 2 * g + p;
+            const bool bv = b < NB;
+            const float2 dY = pair(dy[t], p);
+            put_dw(0, b, bv, cmulc(dY, pair(fi[t], p)));
+            const float2 u = bv ? cmulc(dY, ws[0][bv ? b : 0]) : make_float2(0.f, 0.f);
+            const float2 v = cmulc(pair(dp[t], p), pair(ft[t], p));
+            set_pair(dy[t], p, make_float2(u.x + v.x, u.y + v.y));
+        }
+#pragma unroll
+    for (int t = 0; t < MT; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dfs[wave][4 * t + i][lane] = dy[t][i];
+    // text: dFt = dYt conj(wt) + dp conj(Fi)
+    irfft_t16<D>(a.g[1], item, iv, g, n16, tw, dy);
+#pragma unroll
+    for (int t = 0; t < MT; ++t)
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            const int b = 8 * t + 2 * g + p;
+            const bool bv = b < NB;
+            const float2 dY = pair(dy[t], p);
+            put_dw(1, b, bv, cmulc(dY, pair(ft[t], p)));
+            const float2 u = bv ? cmulc(dY, ws[1][bv ? b : 0]) : make_float2(0.f, 0.f);
+            const float2 v = cmulc(pair(dp[t], p), pair(fi[t], p));
+            set_pair(dy[t], p, make_float2(u.x + v.x, u.y + v.y));
+        }
+    rfft_t16_store<D>(dy, a.gx[1], item, iv, g, n16, tw);
+#pragma unroll
+    for (int t = 0; t < MT; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dy[t][i] = dfs[wave][4 * t + i][lane];
+    rfft_t16_store<D>(dy, a.gx[0], item, iv, g, n16, tw);
+    __syncthreads();
+    // per-block d weight partial, waves added in order (deterministic)
+    for (int e = threadIdx.x; e < 3 * NB * 2; e += blockDim.x) {
         const int m = e / (2 * NB), k = (e / 2) % NB, c = e & 1;
-        const float acc = ((dws[0][m][c][k] + dws[1][m][c][k]) + dws[2][m][c][k]) + dws[3][m][c][k];
-        a.gw[((int64_t)blockIdx.x * 3 + m) * NB * 2 + k * 2 + c] = acc;
-    }
-    const int64_t row = row0 + r;
-    if (row >= a.n) return;
-    // d x[t] = sum_k (dF_re cos - dF_im sin) / sqrt(D)
-    for (int t = sub; t < D; t += 8) {
-#pragma unroll
-        for (int m = 0; m < 2; ++m) {
-            float acc = 0.f;
-            for (int k = 0; k < NB; ++k) {
-                const int e = (k * t) & (D - 1);
-                acc = fmaf(df[r][m][0][k], twc[e], acc);
-                acc = fmaf(-df[r][m][1][k], tws[e], acc);
-            }
-            a.gx[m][row * D + t] = acc * s;
-        }
+        const float2 w0 = dws[0][m][k], w1 = dws[1][m][k], w2 = dws[2][m][k], w3 = dws[3][m][k];
+        const float v = c ? ((w0.y + w1.y) + w2.y) + w3.y : ((w0.x + w1.x) + w2.x) + w3.x;
+        a.gw[((int64_t)blockIdx.x * 3 + m) * NB * 2 + k * 2 + c] = v;
     }
 }
 
@@ -281,37 +451,45 @@ extern "C" int rsx_smore_spectral_fwd(const float* V, int32_t dv, const float* W
     if (n_items < 0 || dv <= 0 || dt <= 0 || (dv & 3) || (dt & 3)) return RSX_ERR_ARG;
     if (!V || !Wv || !bv || !T || !Wt || !bt || !wv || !wt || !wf || !img || !txt || !conv_v || !conv_t || !conv_f)
         return RSX_ERR_ARG;
+    if (d != 64 && d != 128) return RSX_ERR_UNSUPPORTED;
     if (n_items == 0) return RSX_OK;
+    SpecProjArgs p;
+    p.X[0] = V;
+    p.X[1] = T;
+    p.K[0] = dv;
+    p.K[1] = dt;
+    p.W[0] = Wv;
+    p.W[1] = Wt;
+    p.b[0] = bv;
+    p.b[1] = bt;
+    p.n = n_items;
+    p.out[0] = img;
+    p.out[1] = txt;
     SpecFwdArgs a;
-    a.X[0] = V;
-    a.X[1] = T;
-    a.K[0] = dv;
-    a.K[1] = dt;
-    a.W[0] = Wv;
-    a.W[1] = Wt;
-    a.b[0] = bv;
-    a.b[1] = bt;
+    a.x[0] = img;
+    a.x[1] = txt;
     a.w[0] = wv;
     a.w[1] = wt;
     a.w[2] = wf;
     a.n = n_items;
-    a.xo[0] = img;
-    a.xo[1] = txt;
     a.conv[0] = conv_v;
     a.conv[1] = conv_t;
     a.conv[2] = conv_f;
-    const dim3 g((unsigned)((n_items + 31) / 32));
+    const dim3 gp((unsigned)((n_items + 31) / 32), 2);
+    const dim3 gs((unsigned)((n_items + 63) / 64));
     hipStream_t s = as_stream(stream);
-    switch (d) {
-        case 64: hipLaunchKernelGGL(smore_spec_fwd<64>, g, dim3(256), 0, s, a); break;
-        case 128: hipLaunchKernelGGL(smore_spec_fwd<128>, g, dim3(256), 0, s, a); break;
-        default: return RSX_ERR_UNSUPPORTED;
+    if (d == 64) {
+        hipLaunchKernelGGL(smore_proj<64>, gp, dim3(256), 0, s, p);
+        hipLaunchKernelGGL(smore_spec_fwd<64>, gs, dim3(256), 0, s, a);
+    } else {
+        hipLaunchKernelGGL(smore_proj<128>, gp, dim3(256), 0, s, p);
+        hipLaunchKernelGGL(smore_spec_fwd<128>, gs, dim3(256), 0, s, a);
     }
     return last_rc();
 }
 
 extern "C" size_t rsx_smore_spectral_bwd_partials(int64_t n_items, int32_t d) {
-    return (size_t)((n_items + 31) / 32) * 3 * (size_t)(d / 2 + 1) * 2;
+    return (size_t)((n_items + 63) / 64) * 3 * (size_t)(d / 2 + 1) * 2;
 }
 
 extern "C" int rsx_smore_spectral_bwd(const float* img, const float* txt, const float* wv, const float* wt,
@@ -319,10 +497,11 @@ extern "C" int rsx_smore_spectral_bwd(const float* img, const float* txt, const 
                                       int64_t n_items, int32_t d, float* g_img, float* g_txt, float* g_w_partial,
                                       rsx_stream_t stream) {
     if (n_items < 0 || !img || !txt || !wv || !wt || !wf || !g_img || !g_txt || !g_w_partial) return RSX_ERR_ARG;
+    if (d != 64 && d != 128) return RSX_ERR_UNSUPPORTED;
     if (n_items == 0) return RSX_OK;
     SpecBwdArgs a;
-    a.xo[0] = img;
-    a.xo[1] = txt;
+    a.x[0] = img;
+    a.x[1] = txt;
     a.w[0] = wv;
     a.w[1] = wt;
     a.w[2] = wf;
@@ -333,12 +512,11 @@ extern "C" int rsx_smore_spectral_bwd(const float* img, const float* txt, const 
     a.gx[0] = g_img;
     a.gx[1] = g_txt;
     a.gw = g_w_partial;
-    const dim3 g((unsigned)((n_items + 31) / 32));
+    const dim3 g((unsigned)((n_items + 63) / 64));
     hipStream_t s = as_stream(stream);
-    switch (d) {
-        case 64: hipLaunchKernelGGL(smore_spec_bwd<64>, g, dim3(256), 0, s, a); break;
-        case 128: hipLaunchKernelGGL(smore_spec_bwd<128>, g, dim3(256), 0, s, a); break;
-        default: return RSX_ERR_UNSUPPORTED;
-    }
+    if (d == 64)
+        hipLaunchKernelGGL(smore_spec_bwd<64>, g, dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL(smore_spec_bwd<128>, g, dim3(256), 0, s, a);
     return last_rc();
 }
