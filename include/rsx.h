@@ -314,33 +314,36 @@ int rsx_lightgcn_forward(const rsx_csr* adj, int32_t d, int32_t n_layers, const 
 /* ------------------------------------------------------------------------ */
 /*
  * Replaces image_trs / text_trs and spectrum_convolution
- * (src/models/smore.py:256-259 and :209-237) in one launch:
+ * (src/models/smore.py:256-259 and :209-237), two launches on fp32 MFMA:
  *   img = V Wv^T + bv   (V [n_items, dv], Wv [d, dv], nn.Linear layout)
  *   txt = T Wt^T + bt   (T [n_items, dt], Wt [d, dt])
  *   Fi = rfft(img, norm='ortho'), Ft = rfft(txt)       (d/2+1 bins)
  *   conv_v = irfft(Fi * wv), conv_t = irfft(Ft * wt), conv_f = irfft(Ft * Fi * wf)
  * wv / wt / wf are the [(d/2+1)][2] complex weights AFTER the reference's unit
  * normalisation w / (|w| + 1e-8) (:221-229; the caller applies it, so autograd
- * of that step stays with the caller).  img and txt are written out for the
- * backward.  d in {64, 128}; dv, dt multiples of 4.
+ * of that step stays with the caller).  img and txt are written out; `spec`
+ * [rsx_smore_spectral_spec_floats(n, d)] receives Fi and Ft in an internal
+ * layout for the backward.  d in {64, 128}; dv, dt multiples of 4.
  */
+size_t rsx_smore_spectral_spec_floats(int64_t n_items, int32_t d);
 int rsx_smore_spectral_fwd(const float* V, int32_t dv, const float* Wv, const float* bv,
                            const float* T, int32_t dt, const float* Wt, const float* bt,
                            const float* wv, const float* wt, const float* wf,
                            int64_t n_items, int32_t d, float* img, float* txt,
-                           float* conv_v, float* conv_t, float* conv_f, rsx_stream_t stream);
+                           float* conv_v, float* conv_t, float* conv_f, float* spec,
+                           rsx_stream_t stream);
 
 /*
- * Backward of the spectral part: given d conv_v / d conv_t / d conv_f (each may
- * be NULL = zero), writes d img, d txt [n_items, d] and per-block partial sums of
- * d wv / d wt / d wf into g_w_partial [rsx_smore_spectral_bwd_partials(n, d)]
- * floats laid out [ceil(n/32)][3][d/2+1][2] (sum over the first axis for the
- * weight gradients).  The projection gradients d Wv = d img^T V, d V = d img Wv,
- * d bv = colsum(d img) (and the text twins) are plain GEMMs left to the caller.
+ * Backward of the spectral part: given the forward's `spec` and d conv_v /
+ * d conv_t / d conv_f (each may be NULL = zero), writes d img, d txt
+ * [n_items, d] and per-block partial sums of d wv / d wt / d wf into
+ * g_w_partial [rsx_smore_spectral_bwd_partials(n, d)] floats laid out
+ * [ceil(n/64)][3][d/2+1][2] (sum over the first axis for the weight gradients).
+ * The projection gradients d Wv = d img^T V (rsx_linear_wgrad), d V = d img Wv,
+ * d bv = colsum(d img) (and the text twins) are left to the caller.
  */
 size_t rsx_smore_spectral_bwd_partials(int64_t n_items, int32_t d);
-int rsx_smore_spectral_bwd(const float* img, const float* txt,
-                           const float* wv, const float* wt, const float* wf,
+int rsx_smore_spectral_bwd(const float* spec, const float* wv, const float* wt, const float* wf,
                            const float* g_v, const float* g_t, const float* g_f,
                            int64_t n_items, int32_t d, float* g_img, float* g_txt,
                            float* g_w_partial, rsx_stream_t stream);

@@ -18,8 +18,9 @@
 //    may be permuted freely as long as A uses the same permutation): no LDS
 //    transposes.  One wave = 16 items, no block-level synchronisation.
 // 3. smore_spec_bwd: dY = irfft^T(d conv) (the same matrices transposed), the
-//    complex product rules, d w per block (lane-group reductions, waves added in
-//    order: deterministic), d img / d txt = rfft^T(dF).  The projection gradients
+//    complex product rules against the spectra the forward saved, d w per block
+//    (lane-group reductions, waves added in order: deterministic), d img / d txt
+//    = rfft^T(dF).  The projection gradients
 //    (dW = d img^T V on the split-K kernel, dV = d img W, db) are left to the caller.
 #include "rsx_common.hpp"
 
@@ -133,6 +134,16 @@ __device__ __forceinline__ int opaque(int x) {
     asm volatile("" : "+v"(x));
     return x;
 }
+// Volatile asm statements keep their order, but the MFMAs around them do not: they
+// can sink below every later step's index asm, which again hoists all loads.  A
+// volatile asm that "rewrites" the coefficients of the previous step must follow
+// the MFMAs that read them, so the next step's loads cannot pass those MFMAs (and
+// still overlap their execution).
+template <int N>
+__device__ __forceinline__ void tie(float (&c)[N]) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) asm volatile("" : "+v"(c[i]));
+}
 
 __device__ __forceinline__ floatx4 mfma16(float a, float b, floatx4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -202,15 +213,19 @@ __device__ __forceinline__ void rfft16(const float (&xi)[Spec<D>::SI], const flo
     constexpr int SI = Spec<D>::SI, MT = Spec<D>::MT;
 #pragma unroll
     for (int t = 0; t < MT; ++t) fi[t] = ft[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+    float c[MT];
+#pragma unroll
+    for (int t = 0; t < MT; ++t) c[t] = 0.f;
 #pragma unroll
     for (int s = 0; s < SI; ++s) {
         const int f = g * SI + s;
-        step_fence();
+        tie(c);
+#pragma unroll
+        for (int t = 0; t < MT; ++t) c[t] = fwd_coef<D>(16 * t + n16, f, tw);
 #pragma unroll
         for (int t = 0; t < MT; ++t) {
-            const float c = fwd_coef<D>(16 * t + n16, f, tw);
-            fi[t] = mfma16(c, xi[s], fi[t]);
-            ft[t] = mfma16(c, xt[s], ft[t]);
+            fi[t] = mfma16(c[t], xi[s], fi[t]);
+            ft[t] = mfma16(c[t], xt[s], ft[t]);
         }
     }
 }
@@ -226,7 +241,14 @@ struct SpecFwdArgs {
     const float* w[3];  // unit complex weights [(d/2+1)][2]: image, text, fusion
     int64_t n;
     float* conv[3];     // conv_v, conv_t, conv_f [n, d]
+    float* spec;        // saved spectra [n][2][16 MT] (Fi, Ft) for the backward
 };
+
+// saved spectrum of item `item`, signal `sig`, rows 16t + 4g .. 16t + 4g + 3
+template <int D>
+__device__ __forceinline__ int64_t spec_off(int64_t item, int sig, int t, int g) {
+    return (item * 2 + sig) * (16 * Spec<D>::MT) + 16 * t + 4 * g;
+}
 
 template <int D>
 __global__ __launch_bounds__(256) void smore_spec_fwd(SpecFwdArgs a) {
@@ -248,6 +270,13 @@ __global__ __launch_bounds__(256) void smore_spec_fwd(SpecFwdArgs a) {
         load_rows<D>(a.x[1], item, iv, g, xt);
         rfft16<D>(xi, xt, g, n16, tw, fi, ft);
     }
+    if (iv) {
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+            st4(a.spec + spec_off<D>(item, 0, t, g), make_float4(fi[t][0], fi[t][1], fi[t][2], fi[t][3]));
+            st4(a.spec + spec_off<D>(item, 1, t, g), make_float4(ft[t][0], ft[t][1], ft[t][2], ft[t][3]));
+        }
+    }
     // filtered spectra: Yv = Fi wv, Yt = Ft wt, Yf = (Ft Fi) wf  (in place for v, t)
 #pragma unroll
     for (int t = 0; t < MT; ++t)
@@ -267,16 +296,19 @@ __global__ __launch_bounds__(256) void smore_spec_fwd(SpecFwdArgs a) {
     for (int tau = 0; tau < OT; ++tau) {
         floatx4 cv{0.f, 0.f, 0.f, 0.f}, ct = cv, cf = cv;
         const int tq = 16 * tau + n16;
+        float c[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int t = 0; t < MT; ++t)
+        for (int t = 0; t < MT; ++t) {
+            tie(c);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) c[i] = inv_coef<D>(tq, 16 * t + 4 * g + i, tw);
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                step_fence();
-                const float c = inv_coef<D>(tq, 16 * t + 4 * g + i, tw);
-                cv = mfma16(c, fi[t][i], cv);
-                ct = mfma16(c, ft[t][i], ct);
-                cf = mfma16(c, yf[t][i], cf);
+                cv = mfma16(c[i], fi[t][i], cv);
+                ct = mfma16(c[i], ft[t][i], ct);
+                cf = mfma16(c[i], yf[t][i], cf);
             }
+        }
         if (iv) {  // lane (g, n) holds features 16 tau + 4g + r of item n
             const int64_t o = item * D + 16 * tau + 4 * g;
             st4(a.conv[0] + o, make_float4(cv[0], cv[1], cv[2], cv[3]));
@@ -287,7 +319,7 @@ __global__ __launch_bounds__(256) void smore_spec_fwd(SpecFwdArgs a) {
 }
 
 struct SpecBwdArgs {
-    const float* x[2];  // img, txt [n, d]
+    const float* spec;  // the forward's saved spectra [n][2][16 MT]
     const float* w[3];
     const float* g[3];  // d conv_v / conv_t / conv_f [n, d] (NULL = 0)
     int64_t n;
@@ -313,12 +345,17 @@ __device__ __forceinline__ void irfft_t16(const float* __restrict__ gsrc, int64_
     load_rows<D>(gsrc, item, iv, g, gin);
 #pragma unroll
     for (int t = 0; t < MT; ++t) dy[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+    float c[MT];
+#pragma unroll
+    for (int t = 0; t < MT; ++t) c[t] = 0.f;
 #pragma unroll
     for (int s = 0; s < SI; ++s) {
         const int f = g * SI + s;
-        step_fence();
+        tie(c);
 #pragma unroll
-        for (int t = 0; t < MT; ++t) dy[t] = mfma16(inv_coef<D>(f, 16 * t + n16, tw), gin[s], dy[t]);
+        for (int t = 0; t < MT; ++t) c[t] = inv_coef<D>(f, 16 * t + n16, tw);
+#pragma unroll
+        for (int t = 0; t < MT; ++t) dy[t] = mfma16(c[t], gin[s], dy[t]);
     }
 }
 
@@ -331,15 +368,22 @@ __device__ __forceinline__ void rfft_t16_store(const floatx4 (&df)[Spec<D>::MT],
 #pragma unroll 1
     for (int tau = 0; tau < OT; tau += 2) {  // rolled: bounds the live coefficients to one pair of tiles
         floatx4 a0{0.f, 0.f, 0.f, 0.f}, a1 = a0;
+        float c[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int t = 0; t < MT; ++t)
+        for (int t = 0; t < MT; ++t) {
+            tie(c);
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                step_fence();
                 const int j = 16 * t + 4 * g + i;
-                a0 = mfma16(fwd_coef<D>(j, 16 * tau + n16, tw), df[t][i], a0);
-                a1 = mfma16(fwd_coef<D>(j, 16 * tau + 16 + n16, tw), df[t][i], a1);
+                c[i] = fwd_coef<D>(j, 16 * tau + n16, tw);
+                c[4 + i] = fwd_coef<D>(j, 16 * tau + 16 + n16, tw);
             }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                a0 = mfma16(c[i], df[t][i], a0);
+                a1 = mfma16(c[4 + i], df[t][i], a1);
+            }
+        }
         if (iv) {
             const int64_t o = item * D + 16 * tau + 4 * g;
             st4(gx + o, make_float4(a0[0], a0[1], a0[2], a0[3]));
@@ -348,9 +392,9 @@ __device__ __forceinline__ void rfft_t16_store(const floatx4 (&df)[Spec<D>::MT],
     }
 }
 
-// Order keeps the live state small: the fusion term first (only dp = dYf conj(wf)
-// is kept), then the image term (dFi formed in place of dYv and parked in LDS), the
-// text term (dFt -> d txt, after which Fi, Ft and dp are dead), and d img last.
+// Order keeps the live state small: the fusion term first (dp = dYf conj(wf) parked
+// in LDS), then the image term (dFi formed in place of dYv and parked in LDS), the
+// text term (dFt -> d txt, after which Fi and Ft are dead), and d img last.
 template <int D>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 64 ? 2 : 1))) void smore_spec_bwd(
     SpecBwdArgs a) {
@@ -360,6 +404,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 64 ? 2
     __shared__ float2 ws[3][NB];
     __shared__ float2 dws[4][3][NB];
     __shared__ float dfs[4][4 * MT][64];  // dFi parked per wave, lane-contiguous
+    __shared__ float dps[4][4 * MT][64];  // dp = dYf conj(wf), likewise
     twiddles<D>(tw);
     for (int e = threadIdx.x; e < 3 * NB; e += blockDim.x)
         ws[e / NB][e % NB] = make_float2(a.w[e / NB][2 * (e % NB)], a.w[e / NB][2 * (e % NB) + 1]);
@@ -367,45 +412,52 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 64 ? 2
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, n16 = lane & 15, g = lane >> 4;
     const int64_t item = ((int64_t)blockIdx.x * 4 + wave) * 16 + n16;
     const bool iv = item < a.n;
-    floatx4 fi[MT], ft[MT];
-    {
-        float xi[SI], xt[SI];
-        load_rows<D>(a.x[0], item, iv, g, xi);
-        load_rows<D>(a.x[1], item, iv, g, xt);
-        rfft16<D>(xi, xt, g, n16, tw, fi, ft);
-    }
+    // the forward's spectra of tile t (lane (g, n): bins 8t + 2g, 8t + 2g + 1 of item n)
+    auto spec4 = [&](int sig, int t) __attribute__((always_inline)) {
+        const float4 v = iv ? ld4(a.spec + spec_off<D>(item, sig, t, g)) : f4(0.f);
+        return floatx4{v.x, v.y, v.z, v.w};
+    };
     // d w of bin b (summed over the wave's 16 items) into dws[wave][m][b]
     auto put_dw = [&](int m, int b, bool bv, float2 dw) __attribute__((always_inline)) {
         dw.x = sum16(dw.x);
         dw.y = sum16(dw.y);
         if (n16 == 0 && bv) dws[wave][m][b] = dw;
     };
-    floatx4 dp[MT], dy[MT];
+    floatx4 dy[MT];
+    auto dp_at = [&](int t, int p) __attribute__((always_inline)) {
+        return make_float2(dps[wave][4 * t + 2 * p][lane], dps[wave][4 * t + 2 * p + 1][lane]);
+    };
     irfft_t16<D>(a.g[2], item, iv, g, n16, tw, dy);
 #pragma unroll
-    for (int t = 0; t < MT; ++t)
+    for (int t = 0; t < MT; ++t) {
+        const floatx4 fi4 = spec4(0, t), ft4 = spec4(1, t);
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
             const int b = 8 * t + 2 * g + p;
             const bool bv = b < NB;
             const float2 dY = pair(dy[t], p);
-            put_dw(2, b, bv, cmulc(dY, cmul(pair(ft[t], p), pair(fi[t], p))));
-            set_pair(dp[t], p, bv ? cmulc(dY, ws[2][bv ? b : 0]) : make_float2(0.f, 0.f));
+            put_dw(2, b, bv, cmulc(dY, cmul(pair(ft4, p), pair(fi4, p))));
+            const float2 v = bv ? cmulc(dY, ws[2][bv ? b : 0]) : make_float2(0.f, 0.f);
+            dps[wave][4 * t + 2 * p][lane] = v.x;
+            dps[wave][4 * t + 2 * p + 1][lane] = v.y;
         }
+    }
     // image: dFi = dYv conj(wv) + dp conj(Ft)
     irfft_t16<D>(a.g[0], item, iv, g, n16, tw, dy);
 #pragma unroll
-    for (int t = 0; t < MT; ++t)
+    for (int t = 0; t < MT; ++t) {
+        const floatx4 fi4 = spec4(0, t), ft4 = spec4(1, t);
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
             const int b = 8 * t + 2 * g + p;
             const bool bv = b < NB;
             const float2 dY = pair(dy[t], p);
-            put_dw(0, b, bv, cmulc(dY, pair(fi[t], p)));
+            put_dw(0, b, bv, cmulc(dY, pair(fi4, p)));
             const float2 u = bv ? cmulc(dY, ws[0][bv ? b : 0]) : make_float2(0.f, 0.f);
-            const float2 v = cmulc(pair(dp[t], p), pair(ft[t], p));
+            const float2 v = cmulc(dp_at(t, p), pair(ft4, p));
             set_pair(dy[t], p, make_float2(u.x + v.x, u.y + v.y));
         }
+    }
 #pragma unroll
     for (int t = 0; t < MT; ++t)
 #pragma unroll
@@ -413,17 +465,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 64 ? 2
     // text: dFt = dYt conj(wt) + dp conj(Fi)
     irfft_t16<D>(a.g[1], item, iv, g, n16, tw, dy);
 #pragma unroll
-    for (int t = 0; t < MT; ++t)
+    for (int t = 0; t < MT; ++t) {
+        const floatx4 fi4 = spec4(0, t), ft4 = spec4(1, t);
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
             const int b = 8 * t + 2 * g + p;
             const bool bv = b < NB;
             const float2 dY = pair(dy[t], p);
-            put_dw(1, b, bv, cmulc(dY, pair(ft[t], p)));
+            put_dw(1, b, bv, cmulc(dY, pair(ft4, p)));
             const float2 u = bv ? cmulc(dY, ws[1][bv ? b : 0]) : make_float2(0.f, 0.f);
-            const float2 v = cmulc(pair(dp[t], p), pair(fi[t], p));
+            const float2 v = cmulc(dp_at(t, p), pair(fi4, p));
             set_pair(dy[t], p, make_float2(u.x + v.x, u.y + v.y));
         }
+    }
     rfft_t16_store<D>(dy, a.gx[1], item, iv, g, n16, tw);
 #pragma unroll
     for (int t = 0; t < MT; ++t)
@@ -444,12 +498,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 64 ? 2
 
 using namespace rsx;
 
+extern "C" size_t rsx_smore_spectral_spec_floats(int64_t n_items, int32_t d) {
+    if (n_items <= 0) return 0;
+    const int mt = d == 64 ? Spec<64>::MT : Spec<128>::MT;
+    return (size_t)n_items * 2 * 16 * (size_t)mt;
+}
+
 extern "C" int rsx_smore_spectral_fwd(const float* V, int32_t dv, const float* Wv, const float* bv, const float* T,
                                       int32_t dt, const float* Wt, const float* bt, const float* wv, const float* wt,
                                       const float* wf, int64_t n_items, int32_t d, float* img, float* txt,
-                                      float* conv_v, float* conv_t, float* conv_f, rsx_stream_t stream) {
+                                      float* conv_v, float* conv_t, float* conv_f, float* spec, rsx_stream_t stream) {
     if (n_items < 0 || dv <= 0 || dt <= 0 || (dv & 3) || (dt & 3)) return RSX_ERR_ARG;
-    if (!V || !Wv || !bv || !T || !Wt || !bt || !wv || !wt || !wf || !img || !txt || !conv_v || !conv_t || !conv_f)
+    if (!V || !Wv || !bv || !T || !Wt || !bt || !wv || !wt || !wf || !img || !txt || !conv_v || !conv_t || !conv_f ||
+        !spec)
         return RSX_ERR_ARG;
     if (d != 64 && d != 128) return RSX_ERR_UNSUPPORTED;
     if (n_items == 0) return RSX_OK;
@@ -475,6 +536,7 @@ extern "C" int rsx_smore_spectral_fwd(const float* V, int32_t dv, const float* W
     a.conv[0] = conv_v;
     a.conv[1] = conv_t;
     a.conv[2] = conv_f;
+    a.spec = spec;
     const dim3 gp((unsigned)((n_items + 31) / 32), 2);
     const dim3 gs((unsigned)((n_items + 63) / 64));
     hipStream_t s = as_stream(stream);
@@ -492,16 +554,14 @@ extern "C" size_t rsx_smore_spectral_bwd_partials(int64_t n_items, int32_t d) {
     return (size_t)((n_items + 63) / 64) * 3 * (size_t)(d / 2 + 1) * 2;
 }
 
-extern "C" int rsx_smore_spectral_bwd(const float* img, const float* txt, const float* wv, const float* wt,
-                                      const float* wf, const float* g_v, const float* g_t, const float* g_f,
-                                      int64_t n_items, int32_t d, float* g_img, float* g_txt, float* g_w_partial,
-                                      rsx_stream_t stream) {
-    if (n_items < 0 || !img || !txt || !wv || !wt || !wf || !g_img || !g_txt || !g_w_partial) return RSX_ERR_ARG;
+extern "C" int rsx_smore_spectral_bwd(const float* spec, const float* wv, const float* wt, const float* wf,
+                                      const float* g_v, const float* g_t, const float* g_f, int64_t n_items, int32_t d,
+                                      float* g_img, float* g_txt, float* g_w_partial, rsx_stream_t stream) {
+    if (n_items < 0 || !spec || !wv || !wt || !wf || !g_img || !g_txt || !g_w_partial) return RSX_ERR_ARG;
     if (d != 64 && d != 128) return RSX_ERR_UNSUPPORTED;
     if (n_items == 0) return RSX_OK;
     SpecBwdArgs a;
-    a.x[0] = img;
-    a.x[1] = txt;
+    a.spec = spec;
     a.w[0] = wv;
     a.w[1] = wt;
     a.w[2] = wf;

@@ -2,9 +2,10 @@
 HIP pass `rsx_smore_spectral_fwd` (reference src/models/smore.py:256-259 image_trs /
 text_trs and :209-237 spectrum_convolution), with autograd.
 
-Forward: one launch computes img = V Wv^T + bv, txt = T Wt^T + bt (fp32 MFMA),
-their rfft's, the three filtered spectra and the three irfft's.  Backward: one
-launch for the spectral part (d img, d txt, d w), then the projection gradients:
+Forward: two launches (fp32 MFMA): img = V Wv^T + bv, txt = T Wt^T + bt, then
+their rfft's (saved for the backward), the three filtered spectra and the three
+irfft's.  Backward: one launch for the spectral part (d img, d txt, d w), then the
+projection gradients:
 d Wv = d img^T V on the split-K kernel (rsx_linear_wgrad), d V = d img Wv as a
 library GEMM, d bv = colsum.
 The unit normalisation of the complex weights (:221-229) stays a torch op on the
@@ -49,23 +50,29 @@ class _Spectral(torch.autograd.Function):
         img = torch.empty(n, d, device=V.device, dtype=torch.float32)
         txt = torch.empty_like(img)
         cv, ct, cf = torch.empty_like(img), torch.empty_like(img), torch.empty_like(img)
+        lib = L.lib()
+        spec = torch.empty(max(int(lib.rsx_smore_spectral_spec_floats(n, d)), 1), device=V.device,
+                           dtype=torch.float32)
         p = ops._p
-        L.check(L.lib().rsx_smore_spectral_fwd(p(V), dv, p(Wv), p(bv), p(T), dt, p(Wt), p(bt), p(wv), p(wt), p(wf),
-                                                n, d, p(img), p(txt), p(cv), p(ct), p(cf), ops._stream()),
+        L.check(lib.rsx_smore_spectral_fwd(p(V), dv, p(Wv), p(bv), p(T), dt, p(Wt), p(bt), p(wv), p(wt), p(wf),
+                                           n, d, p(img), p(txt), p(cv), p(ct), p(cf), p(spec), ops._stream()),
                 "rsx_smore_spectral_fwd")
-        ctx.save_for_backward(V, Wv, T, Wt, wv, wt, wf, img, txt)
+        ctx.save_for_backward(V, Wv, T, Wt, wv, wt, wf, spec)
+        ctx.nd = (n, d)
         return cv, ct, cf, img, txt
 
     @staticmethod
     def backward(ctx, g_cv, g_ct, g_cf, g_img_out, g_txt_out):
-        V, Wv, T, Wt, wv, wt, wf, img, txt = ctx.saved_tensors
-        n, d = img.shape
+        V, Wv, T, Wt, wv, wt, wf, spec = ctx.saved_tensors
+        n, d = ctx.nd
         p = ops._p
         lib = L.lib()
-        gi, gt = torch.empty_like(img), torch.empty_like(img)
-        part = torch.empty(int(lib.rsx_smore_spectral_bwd_partials(n, d)), device=img.device, dtype=torch.float32)
+        gi = torch.empty(n, d, device=V.device, dtype=torch.float32)
+        gt = torch.empty_like(gi)
+        part = torch.empty(max(int(lib.rsx_smore_spectral_bwd_partials(n, d)), 1), device=V.device,
+                           dtype=torch.float32)
         gs = [None if g is None else g.contiguous() for g in (g_cv, g_ct, g_cf)]
-        L.check(lib.rsx_smore_spectral_bwd(p(img), p(txt), p(wv), p(wt), p(wf),
+        L.check(lib.rsx_smore_spectral_bwd(p(spec), p(wv), p(wt), p(wf),
                                            *(None if g is None else p(g) for g in gs),
                                            n, d, p(gi), p(gt), p(part), ops._stream()), "rsx_smore_spectral_bwd")
         if g_img_out is not None:
