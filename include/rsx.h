@@ -323,15 +323,17 @@ int rsx_lightgcn_forward(const rsx_csr* adj, int32_t d, int32_t n_layers, const 
  * normalisation w / (|w| + 1e-8) (:221-229; the caller applies it, so autograd
  * of that step stays with the caller).  img and txt are written out; `spec`
  * [rsx_smore_spectral_spec_floats(n, d)] receives Fi and Ft in an internal
- * layout for the backward.  d in {64, 128}; dv, dt multiples of 4.
+ * layout for the backward; `ws` [rsx_smore_spectral_fwd_ws_bytes(...)] holds
+ * the split-K partial projections.  d in {64, 128}; dv, dt multiples of 4.
  */
 size_t rsx_smore_spectral_spec_floats(int64_t n_items, int32_t d);
+size_t rsx_smore_spectral_fwd_ws_bytes(int64_t n_items, int32_t d, int32_t dv, int32_t dt);
 int rsx_smore_spectral_fwd(const float* V, int32_t dv, const float* Wv, const float* bv,
                            const float* T, int32_t dt, const float* Wt, const float* bt,
                            const float* wv, const float* wt, const float* wf,
                            int64_t n_items, int32_t d, float* img, float* txt,
                            float* conv_v, float* conv_t, float* conv_f, float* spec,
-                           rsx_stream_t stream);
+                           void* ws, size_t ws_bytes, rsx_stream_t stream);
 
 /*
  * Backward of the spectral part: given the forward's `spec` and d conv_v /

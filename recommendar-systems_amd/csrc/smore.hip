@@ -3,10 +3,10 @@
 // image_trs / text_trs) and the backward of the spectral part, all on fp32 MFMA
 // (exact f32 products, f32 sums: the same arithmetic as an fmaf chain).
 //
-// 1. smore_proj: img = V W_v^T + b_v, txt = T W_t^T + b_t (v_mfma_f32_32x32x2f32).
-//    A block owns 32 items of one modality; its 4 waves split the feature width K
-//    (4096 raw image / 384 text at Amazon-baby, 768 CLIP at clothing), loads one
-//    step ahead of the MFMAs, and add their tiles in LDS in wave order (bias first).
+// 1. smore_proj: img = V W_v^T, txt = T W_t^T (v_mfma_f32_32x32x2f32), an LDS-staged
+//    GEMM; the feature width K (4096 raw image / 384 text at Amazon-baby, 768 CLIP at
+//    clothing) is split over blocks where it is long, the splits (and the bias) are
+//    added in order by smore_spec_fwd as it loads the rows.
 // 2. smore_spec_fwd: a length-d real DFT is a d x (d+2) real matrix, so
 //    rfft(norm='ortho') of 16 items is a [(d+2) x d] x [d x 16] product on
 //    v_mfma_f32_16x16x4f32: the rows (Re, Im of bin b at 2b, 2b+1) come from an LDS
@@ -22,6 +22,8 @@
 //    (lane-group reductions, waves added in order: deterministic), d img / d txt
 //    = rfft^T(dF).  The projection gradients
 //    (dW = d img^T V on the split-K kernel, dV = d img W, db) are left to the caller.
+#include <type_traits>
+
 #include "rsx_common.hpp"
 
 namespace rsx {
@@ -32,83 +34,121 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 // ---------------------------------------------------------------------------
 // projection
 // ---------------------------------------------------------------------------
+// out_m = X_m W_m^T (bias added by smore_spec_fwd) as an LDS-staged GEMM: a block
+// owns 64 items x all d features of one modality and one K range (split s of S_m:
+// the 4096-wide raw image features are split so that the grid fills the chip);
+// K is streamed in 32-wide chunks, float4 global loads two chunks ahead, LDS
+// double-buffered.  Waves: item tile (w & 1) x feature tiles {w >> 1, + 2, ...}.
+constexpr int kPjItems = 64, kPjK = 32, kPjPad = 36;
+
 struct SpecProjArgs {
     const float* X[2];  // V [n, K0], T [n, K1]
     int32_t K[2];
     const float* W[2];  // [d, K]
-    const float* b[2];  // [d]
     int64_t n;
-    float* out[2];      // img, txt [n, d]
+    int32_t S[2];       // K splits per modality
+    int32_t tiles;      // item tiles (ceil(n / 64))
+    float* out[2][8];   // split s of modality m: [n, d] (s = 0: img / txt themselves)
 };
 
-// lane l feeds item row l&31 and, within a step of 8, k = 4*(l>>5) + q for the q-th
-// of 4 MFMAs (the same permutation on the A and B side)
 template <int D>
 __global__ __launch_bounds__(256) void smore_proj(SpecProjArgs a) {
-    constexpr int NT = D / 32;
-    __shared__ float xs[32][D + 1];
-    const int m = blockIdx.y;
+    constexpr int FT = D / 32;            // feature tiles
+    constexpr int TPW = 2 * FT / 4;       // tiles per wave (FT/2: 1 for d=64, 2 for d=128)
+    constexpr int NX = kPjItems * kPjK / 4, NW = D * kPjK / 4;  // float4s per chunk
+    constexpr int PER = (NX + NW) / 256;
+    static_assert((NX + NW) % 256 == 0, "chunk split");
+    __shared__ float xs[2][kPjItems * kPjPad];
+    __shared__ float ws[2][D * kPjPad];
+    // blocks: modality 0 splits, then modality 1 splits, each over the item tiles
+    int bid = blockIdx.x;
+    const int nb0 = a.tiles * a.S[0];
+    const int m = bid < nb0 ? 0 : 1;
+    if (m) bid -= nb0;
+    const int S = a.S[m];
+    const int tile = bid % a.tiles, sp = bid / a.tiles;
     const float* __restrict__ X = a.X[m];
     const float* __restrict__ W = a.W[m];
     const int K = a.K[m];
+    const int nch_all = (K + kPjK - 1) / kPjK;
+    const int per = (nch_all + S - 1) / S;
+    const int c_beg = sp * per, c_end = min(nch_all, c_beg + per);
+    const int nch = max(0, c_end - c_beg);
+    const int64_t i0 = (int64_t)tile * kPjItems;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, j = lane & 31, h = lane >> 5;
-    const int64_t row0 = (int64_t)blockIdx.x * 32;
-    floatx16 acc[NT];
+    const int it = wave & 1;              // item tile of this wave
+    floatx16 acc[TPW];
 #pragma unroll
-    for (int c = 0; c < NT; ++c)
+    for (int q = 0; q < TPW; ++q)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[c][r] = 0.f;
-    const int steps = (K + 7) / 8;
-    const int per = (steps + 3) / 4;
-    const int kb = wave * per * 8, ke = min(K, (wave + 1) * per * 8);
-    const int64_t row = row0 + j;
-    const bool rv = row < a.n;
-    const float* xr = X + (rv ? row : 0) * (int64_t)K;
-    auto load = [&](int k, float4& va, float4(&vb)[NT]) __attribute__((always_inline)) {
-        const int kk = k + 4 * h;
-        const bool ok = kk < ke;  // K % 4 == 0: the whole float4 is in range
-        va = (ok && rv) ? ld4(xr + kk) : f4(0.f);
+        for (int e = 0; e < 16; ++e) acc[q][e] = 0.f;
+    float4 st[2][PER];
+    auto gload = [&](int c, float4(&v)[PER]) __attribute__((always_inline)) {
+        const int k0 = (c_beg + c) * kPjK;
 #pragma unroll
-        for (int c = 0; c < NT; ++c) vb[c] = ok ? ld4(W + (int64_t)(c * 32 + j) * K + kk) : f4(0.f);
+        for (int q = 0; q < PER; ++q) {
+            const int e = threadIdx.x + 256 * q;
+            float4 t = f4(0.f);
+            if (e < NX) {
+                const int r = e / (kPjK / 4), kk = k0 + (e % (kPjK / 4)) * 4;
+                const int64_t row = i0 + r;
+                if (row < a.n && kk < K) t = ld4(X + row * K + kk);
+            } else {
+                const int e2 = e - NX;
+                const int r = e2 / (kPjK / 4), kk = k0 + (e2 % (kPjK / 4)) * 4;
+                if (kk < K) t = ld4(W + (int64_t)r * K + kk);
+            }
+            v[q] = t;
+        }
     };
-    float4 ca, cb[NT];
-    if (kb < ke) load(kb, ca, cb);
-    for (int k = kb; k < ke; k += 8) {  // wave-uniform bounds
-        float4 na, nb[NT];
-        const bool more = k + 8 < ke;
-        if (more) load(k + 8, na, nb);
+    auto sstore = [&](int b, const float4(&v)[PER]) __attribute__((always_inline)) {
 #pragma unroll
-        for (int c = 0; c < NT; ++c) {
-            acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(ca.x, cb[c].x, acc[c], 0, 0, 0);
-            acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(ca.y, cb[c].y, acc[c], 0, 0, 0);
-            acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(ca.z, cb[c].z, acc[c], 0, 0, 0);
-            acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(ca.w, cb[c].w, acc[c], 0, 0, 0);
+        for (int q = 0; q < PER; ++q) {
+            const int e = threadIdx.x + 256 * q;
+            if (e < NX)
+                *reinterpret_cast<float4*>(&xs[b][(e / (kPjK / 4)) * kPjPad + (e % (kPjK / 4)) * 4]) = v[q];
+            else
+                *reinterpret_cast<float4*>(&ws[b][((e - NX) / (kPjK / 4)) * kPjPad + ((e - NX) % (kPjK / 4)) * 4]) =
+                    v[q];
         }
-        if (more) {
-            ca = na;
-#pragma unroll
-            for (int c = 0; c < NT; ++c) cb[c] = nb[c];
-        }
+    };
+    if (nch > 0) {
+        gload(0, st[0]);
+        if (nch > 1) gload(1, st[1]);
+        sstore(0, st[0]);
     }
-    // C layout: lane holds column (feature) c*32 + j, rows (items) (r&3) + 8(r>>2) + 4h
-    const float* bias = a.b[m];
-    for (int w2 = 0; w2 < 4; ++w2) {
-        if (wave == w2) {
+    __syncthreads();
+    auto step = [&](int c, auto bc) __attribute__((always_inline)) {
+        constexpr int B = decltype(bc)::value;
+        if (c + 2 < nch) gload(c + 2, st[B]);
+        const float* xb = xs[B] + (it * 32 + j) * kPjPad + h;
 #pragma unroll
-            for (int c = 0; c < NT; ++c)
+        for (int u = 0; u < kPjK / 2; ++u) {
+            const float av = xb[2 * u];
 #pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int i = (r & 3) + 8 * (r >> 2) + 4 * h, f = c * 32 + j;
-                    const float base = w2 == 0 ? bias[f] : xs[i][f];
-                    xs[i][f] = base + acc[c][r];
-                }
+            for (int q = 0; q < TPW; ++q) {
+                const int ft = (wave >> 1) + 2 * q;
+                acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, ws[B][(ft * 32 + j) * kPjPad + 2 * u + h], acc[q],
+                                                              0, 0, 0);
+            }
         }
+        if (c + 1 < nch) sstore(B ^ 1, st[B ^ 1]);
         __syncthreads();
+    };
+    for (int c = 0; c < nch; c += 2) {  // block-uniform
+        step(c, std::integral_constant<int, 0>{});
+        if (c + 1 < nch) step(c + 1, std::integral_constant<int, 1>{});
     }
-    float* out = a.out[m];
-    for (int e = threadIdx.x; e < 32 * D; e += 256) {
-        const int r = e / D, f = e % D;
-        if (row0 + r < a.n) out[(row0 + r) * D + f] = xs[r][f];
+    // C layout: lane holds column (feature) ft*32 + j, rows (items) it*32 + (e&3) + 8(e>>2) + 4h
+    float* out = a.out[m][sp];
+#pragma unroll
+    for (int q = 0; q < TPW; ++q) {
+        const int f = ((wave >> 1) + 2 * q) * 32 + j;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const int64_t row = i0 + it * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+            if (row < a.n) out[row * D + f] = acc[q][e];
+        }
     }
 }
 
@@ -237,7 +277,10 @@ __device__ __forceinline__ void set_pair(floatx4& v, int p, float2 x) {
 }
 
 struct SpecFwdArgs {
-    const float* x[2];  // img, txt [n, d]
+    float* x[2];        // img, txt [n, d]: projection split 0 in, the final projection out
+    const float* part[2][8];  // projection splits 1.. (S[m] - 1 of them)
+    int32_t S[2];
+    const float* b[2];  // biases [d]
     const float* w[3];  // unit complex weights [(d/2+1)][2]: image, text, fusion
     int64_t n;
     float* conv[3];     // conv_v, conv_t, conv_f [n, d]
@@ -248,6 +291,35 @@ struct SpecFwdArgs {
 template <int D>
 __device__ __forceinline__ int64_t spec_off(int64_t item, int sig, int t, int g) {
     return (item * 2 + sig) * (16 * Spec<D>::MT) + 16 * t + 4 * g;
+}
+
+// the projection rows of modality m for the 16 items (B layout, see load_rows):
+// split 0 + split 1 + ... + bias, in that order; written back as img / txt
+template <int D>
+__device__ __forceinline__ void proj_rows(const SpecFwdArgs& a, int m, int64_t item, bool iv, int g,
+                                          float (&v)[Spec<D>::SI]) {
+    constexpr int SI = Spec<D>::SI;
+    load_rows<D>(a.x[m], item, iv, g, v);
+    for (int s = 1; s < a.S[m]; ++s) {
+        float p[SI];
+        load_rows<D>(a.part[m][s], item, iv, g, p);
+#pragma unroll
+        for (int k = 0; k < SI; ++k) v[k] += p[k];
+    }
+    const float* bias = a.b[m] + g * SI;
+#pragma unroll
+    for (int q = 0; q < SI / 4; ++q) {
+        const float4 bb = ld4(bias + 4 * q);
+        v[4 * q] += bb.x;
+        v[4 * q + 1] += bb.y;
+        v[4 * q + 2] += bb.z;
+        v[4 * q + 3] += bb.w;
+    }
+    if (iv) {
+        float* o = a.x[m] + item * D + g * SI;
+#pragma unroll
+        for (int q = 0; q < SI / 4; ++q) st4(o + 4 * q, make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]));
+    }
 }
 
 template <int D>
@@ -266,8 +338,8 @@ __global__ __launch_bounds__(256) void smore_spec_fwd(SpecFwdArgs a) {
     floatx4 fi[MT], ft[MT], yf[MT];
     {
         float xi[SI], xt[SI];
-        load_rows<D>(a.x[0], item, iv, g, xi);
-        load_rows<D>(a.x[1], item, iv, g, xt);
+        proj_rows<D>(a, 0, item, iv, g, xi);
+        proj_rows<D>(a, 1, item, iv, g, xt);
         rfft16<D>(xi, xt, g, n16, tw, fi, ft);
     }
     if (iv) {
@@ -504,31 +576,64 @@ extern "C" size_t rsx_smore_spectral_spec_floats(int64_t n_items, int32_t d) {
     return (size_t)n_items * 2 * 16 * (size_t)mt;
 }
 
+// K splits of a projection: about 1024 blocks over both modalities, >= 512 of K per split
+static int proj_splits(int64_t n, int K) {
+    const int64_t tiles = (n + kPjItems - 1) / kPjItems;
+    int64_t s = (512 + 2 * tiles - 1) / (2 * tiles);  // blocks per modality ~512
+    const int64_t smax = K / 512 > 0 ? K / 512 : 1;
+    if (s > smax) s = smax;
+    if (s > 8) s = 8;
+    return (int)(s < 1 ? 1 : s);
+}
+
+extern "C" size_t rsx_smore_spectral_fwd_ws_bytes(int64_t n_items, int32_t d, int32_t dv, int32_t dt) {
+    if (n_items <= 0 || dv <= 0 || dt <= 0) return 0;
+    const int64_t extra = (proj_splits(n_items, dv) - 1) + (proj_splits(n_items, dt) - 1);
+    return (size_t)extra * (size_t)n_items * (size_t)d * sizeof(float);
+}
+
 extern "C" int rsx_smore_spectral_fwd(const float* V, int32_t dv, const float* Wv, const float* bv, const float* T,
                                       int32_t dt, const float* Wt, const float* bt, const float* wv, const float* wt,
                                       const float* wf, int64_t n_items, int32_t d, float* img, float* txt,
-                                      float* conv_v, float* conv_t, float* conv_f, float* spec, rsx_stream_t stream) {
+                                      float* conv_v, float* conv_t, float* conv_f, float* spec, void* ws,
+                                      size_t ws_bytes, rsx_stream_t stream) {
     if (n_items < 0 || dv <= 0 || dt <= 0 || (dv & 3) || (dt & 3)) return RSX_ERR_ARG;
     if (!V || !Wv || !bv || !T || !Wt || !bt || !wv || !wt || !wf || !img || !txt || !conv_v || !conv_t || !conv_f ||
         !spec)
         return RSX_ERR_ARG;
     if (d != 64 && d != 128) return RSX_ERR_UNSUPPORTED;
     if (n_items == 0) return RSX_OK;
+    if (ws_bytes < rsx_smore_spectral_fwd_ws_bytes(n_items, d, dv, dt) || (ws_bytes && !ws)) return RSX_ERR_WORKSPACE;
     SpecProjArgs p;
+    SpecFwdArgs a;
     p.X[0] = V;
     p.X[1] = T;
     p.K[0] = dv;
     p.K[1] = dt;
     p.W[0] = Wv;
     p.W[1] = Wt;
-    p.b[0] = bv;
-    p.b[1] = bt;
     p.n = n_items;
-    p.out[0] = img;
-    p.out[1] = txt;
-    SpecFwdArgs a;
+    p.tiles = (int)((n_items + kPjItems - 1) / kPjItems);
+    float* outs[2] = {img, txt};
+    float* w = static_cast<float*>(ws);
+    for (int m = 0; m < 2; ++m) {
+        p.S[m] = a.S[m] = proj_splits(n_items, p.K[m]);
+        for (int sp = 0; sp < 8; ++sp) {
+            float* o = nullptr;
+            if (sp == 0) {
+                o = outs[m];
+            } else if (sp < p.S[m]) {
+                o = w;
+                w += n_items * d;
+            }
+            p.out[m][sp] = o;
+            a.part[m][sp] = o;
+        }
+    }
     a.x[0] = img;
     a.x[1] = txt;
+    a.b[0] = bv;
+    a.b[1] = bt;
     a.w[0] = wv;
     a.w[1] = wt;
     a.w[2] = wf;
@@ -537,7 +642,7 @@ extern "C" int rsx_smore_spectral_fwd(const float* V, int32_t dv, const float* W
     a.conv[1] = conv_t;
     a.conv[2] = conv_f;
     a.spec = spec;
-    const dim3 gp((unsigned)((n_items + 31) / 32), 2);
+    const dim3 gp((unsigned)(p.tiles * (p.S[0] + p.S[1])));
     const dim3 gs((unsigned)((n_items + 63) / 64));
     hipStream_t s = as_stream(stream);
     if (d == 64) {

@@ -85,7 +85,9 @@ def _declare(lib):
         "rsx_lightgcn_step": (C.c_int, [C.POINTER(LgcnStep), P]),
         "rsx_lightgcn_forward": (C.c_int, [C.POINTER(Csr), I32, I32, P, P, P, P, P, P, P]),
         "rsx_smore_spectral_spec_floats": (C.c_size_t, [I64, I32]),
-        "rsx_smore_spectral_fwd": (C.c_int, [P, I32, P, P, P, I32, P, P, P, P, P, I64, I32, P, P, P, P, P, P, P]),
+        "rsx_smore_spectral_fwd_ws_bytes": (C.c_size_t, [I64, I32, I32, I32]),
+        "rsx_smore_spectral_fwd": (C.c_int, [P, I32, P, P, P, I32, P, P, P, P, P, I64, I32, P, P, P, P, P, P, P,
+                                             C.c_size_t, P]),
         "rsx_smore_spectral_bwd": (C.c_int, [P, P, P, P, P, P, P, I64, I32, P, P, P, P]),
         "rsx_smore_spectral_bwd_partials": (C.c_size_t, [I64, I32]),
         "rsx_topk_metrics_ws_bytes": (C.c_size_t, [I64, I32]),
@@ -102,7 +104,8 @@ def _declare(lib):
 EXPORTED = ["rsx_version", "rsx_csr_schedule_host", "rsx_spmm", "rsx_rowwise", "rsx_bpr_ws_bytes", "rsx_bpr",
             "rsx_fullsort_ws_bytes", "rsx_fullsort_topk", "rsx_score_dense", "rsx_sample_triplets",
             "rsx_gather_rows", "rsx_lightgcn_step", "rsx_lightgcn_forward", "rsx_sample_epoch",
-            "rsx_smore_spectral_spec_floats", "rsx_smore_spectral_fwd", "rsx_smore_spectral_bwd",
+            "rsx_smore_spectral_spec_floats", "rsx_smore_spectral_fwd_ws_bytes", "rsx_smore_spectral_fwd",
+            "rsx_smore_spectral_bwd",
             "rsx_smore_spectral_bwd_partials",
             "rsx_topk_metrics_ws_bytes", "rsx_topk_metrics", "rsx_linear_wgrad_ws_bytes", "rsx_linear_wgrad"]
 

@@ -54,9 +54,10 @@ class _Spectral(torch.autograd.Function):
         spec = torch.empty(max(int(lib.rsx_smore_spectral_spec_floats(n, d)), 1), device=V.device,
                            dtype=torch.float32)
         p = ops._p
+        ws = ops._ws(V.device, int(lib.rsx_smore_spectral_fwd_ws_bytes(n, d, dv, dt)))
         L.check(lib.rsx_smore_spectral_fwd(p(V), dv, p(Wv), p(bv), p(T), dt, p(Wt), p(bt), p(wv), p(wt), p(wf),
-                                           n, d, p(img), p(txt), p(cv), p(ct), p(cf), p(spec), ops._stream()),
-                "rsx_smore_spectral_fwd")
+                                           n, d, p(img), p(txt), p(cv), p(ct), p(cf), p(spec), p(ws), ws.numel(),
+                                           ops._stream()), "rsx_smore_spectral_fwd")
         ctx.save_for_backward(V, Wv, T, Wt, wv, wt, wf, spec)
         ctx.nd = (n, d)
         return cv, ct, cf, img, txt
