@@ -192,7 +192,7 @@ def bench_model(args):
         "fullsort": {"eval_users": n_eval, "n_items": ni, "s_per_eval_incl_forward_and_metrics": eval_s},
         "model_build_s": build_s, "roofline": None, "cpu_baseline": None,
     }
-    print(json.dumps(out), flush=True)
+    _json_line(out)
 
 
 def _c4_chunk(args):
@@ -241,7 +241,20 @@ def load_graph(workload, rank, world, c4_chunks=None):
             "reference split rule), users row-sharded over the ranks, items replicated, B=2048 per rank")
 
 
+def _json_line(out):
+    """The one JSON line, on the real stdout (library banners were sent to stderr)."""
+    os.write(_STDOUT_FD, (json.dumps(out) + "\n").encode())
+
+
+_STDOUT_FD = 1
+
+
 def main():
+    global _STDOUT_FD
+    # RCCL / HIP print banners on fd 1 at communicator init: keep fd 1 for the JSON line
+    sys.stdout.flush()
+    _STDOUT_FD = os.dup(1)
+    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", default="c2", choices=["c2", "c1", "c3", "c4", "c5"],
                     help="c2 (default): the headline LightGCN sports config; c1/c3: LayerGCN / SMORE on baby; "
@@ -251,6 +264,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=None, help="default 20 (c4: 3)")
     ap.add_argument("--batch", type=int, default=2048)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--sharded", action="store_true",
+                    help="use the row-sharded engine even at N=1 (measures its host/launch overhead)")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--eval-users", type=int, default=None, help="default: all valid users (c4: 32768 per rank)")
     ap.add_argument("--c4-chunks", type=int, default=None,
@@ -271,7 +286,7 @@ def main():
     tu, ti, vu_all, vi_all, nu, ni, d, desc = load_graph(args.workload, rank, world, args.c4_chunks)
     if big and args.c4_chunks:
         desc += f" [only {args.c4_chunks} of 8 user chunks built]"
-    sharded = world > 1 or big
+    sharded = world > 1 or big or args.sharded
     if sharded:
         import torch.distributed as dist
 
@@ -455,8 +470,10 @@ def main():
             "gpu_ms_per_step_events": gpu_ms / args.steps,
             "train_loss_mean": loss_mean,
         }
-        print(json.dumps(out), flush=True)
-    if world > 1:
+        _json_line(out)
+    if hasattr(eng, "close"):
+        eng.close()
+    if sharded:
         torch.distributed.destroy_process_group()
 
 

@@ -35,6 +35,7 @@ typedef void* rsx_stream_t; /* a hipStream_t (0 = the null stream) */
 #define RSX_ERR_ARG 1001         /* bad size / null pointer */
 #define RSX_ERR_UNSUPPORTED 1002 /* embedding width not compiled (d in {32,64,128,256}) */
 #define RSX_ERR_WORKSPACE 1003   /* workspace too small */
+#define RSX_ERR_COMM 1004        /* RCCL missing or a collective failed */
 
 /* Version string of the library ("rsx <ver> gfx950"). */
 const char* rsx_version(void);
@@ -389,6 +390,75 @@ int rsx_topk_metrics(const int64_t* topk_idx, int64_t n_users, int32_t k_max,
 size_t rsx_linear_wgrad_ws_bytes(int64_t n, int32_t out_dim, int32_t in_dim);
 int rsx_linear_wgrad(const float* g, const float* x, int64_t n, int32_t out_dim, int32_t in_dim, float* dw,
                      void* ws, size_t ws_bytes, rsx_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
+/* Row-sharded LightGCN over RCCL (one process per GPU)                       */
+/* ------------------------------------------------------------------------ */
+/*
+ * The reference is single-device (src/utils/configurator.py:114-118 pins one
+ * GPU); SURVEY.md 8(e) scales the propagation by sharding users in contiguous
+ * per-rank row blocks with the item rows replicated.  Per layer the item rows are
+ * a per-rank partial (R_g^T users_g) summed across ranks by an in-place RCCL
+ * all-reduce on the communicator's own stream, fenced by events against the
+ * caller's stream (fork after the partial, join before the first reader).
+ *
+ * rsx_comm_t wraps an RCCL communicator plus that stream and its events.  RCCL is
+ * resolved at run time (the copy torch loaded, else librccl.so.1); without it the
+ * rsx_comm_* calls return RSX_ERR_COMM.  Create with the usual unique-id
+ * handshake: rank 0 calls rsx_comm_get_unique_id, broadcasts the
+ * rsx_comm_unique_id_bytes() bytes, and every rank calls rsx_comm_init (a
+ * collective: all ranks must call it).  The device is the current HIP device.
+ * rsx_comm_init / rsx_comm_destroy allocate, create streams and synchronise;
+ * everything else is stream-ordered.
+ */
+typedef struct rsx_comm_s* rsx_comm_t;
+size_t rsx_comm_unique_id_bytes(void);
+int rsx_comm_get_unique_id(void* id_host);
+int rsx_comm_init(rsx_comm_t* out, const void* id_host, int32_t rank, int32_t world);
+int rsx_comm_destroy(rsx_comm_t comm);
+/* buf[0, n) := sum over ranks, in place, ordered after the work queued on `stream`
+ * and before the work queued on it afterwards. */
+int rsx_comm_allreduce_f32(rsx_comm_t comm, float* buf, int64_t n, rsx_stream_t stream);
+
+/*
+ * One LightGCN batch on this rank's shard (the sharded twin of rsx_lightgcn_step;
+ * reference src/models/lightgcn.py:117-156 + src/common/trainer.py:238):
+ *   adj_u  rows = the rank's n_users users, cols = [local users | items]
+ *          (only the item columns are populated), values d_u^-1/2 d_i^-1/2 with
+ *          GLOBAL item degrees (so every value equals the unsharded matrix's);
+ *   adj_i  rows = the n_items items, cols populated with the local users only.
+ * Every [n_users + n_items, d] table is local users first, then the replicated
+ * items; `t` is [n_items, d] scratch.  A step issues 2K+1 all-reduces of
+ * n_items*d floats: the forward's item partials of layers 1..K, G's item rows,
+ * the backward's layers 1..K-1, and the item gradient t.  Item Adam then runs
+ * identically on every rank (its inputs are bit-identical after the sums), user
+ * Adam locally.  The loss is this rank's mean BPR + its regulariser; the
+ * objective is the sum over ranks (data-parallel batches of `batch` per rank).
+ * rsx_sharded_lightgcn_forward fills final_emb only (evaluation).
+ */
+typedef struct rsx_sharded_lgcn_step {
+    const rsx_csr* adj_u;
+    const rsx_csr* adj_i;
+    int64_t n_users, n_items;   /* local users, all items */
+    int32_t d, n_layers;
+    float reg;
+    int32_t pad0;
+    float* p; float* m; float* v;
+    float* s; float* h0; float* h1;
+    float* final_emb; float* g; float* r;
+    float* t;                   /* [n_items, d] */
+    float* slab_u; float* slab_i;
+    int64_t* triplets;          /* [3][batch], item ids in [0, n_items) */
+    int64_t batch;
+    rsx_adam adam;
+    float* loss_out;            /* [1] */
+    double* loss_acc;           /* [1] or NULL */
+    void* ws; size_t ws_bytes;  /* >= rsx_bpr_ws_bytes(batch) */
+    rsx_comm_t comm;
+} rsx_sharded_lgcn_step;
+
+int rsx_sharded_lightgcn_step(const rsx_sharded_lgcn_step* st, rsx_stream_t stream);
+int rsx_sharded_lightgcn_forward(const rsx_sharded_lgcn_step* st, rsx_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,332 @@
+// dist.hip — row-sharded LightGCN step over RCCL (gfx950, one process per GPU).
+//
+// The reference is single-process; this is the build's scaling
+// axis.  A = [[0, R], [R^T, 0]] is bipartite: with users split in
+// contiguous per-rank blocks and the item rows replicated,
+//     users^k = R_g items^{k-1}             local (items^{k-1} is replicated)
+//     items^k = sum_g R_g^T users_g^{k-1}   per-rank partial + one all-reduce
+// so a K-layer step exchanges 2K+1 item blocks of n_items*d floats (K forward
+// layers, G's item rows + K-1 backward layers, the item gradient).  The
+// sequence is the one rsx/dist.py:ShardedLightGCNEngine states in Python (the
+// gloo-tested restatement of the partitioning); here the whole step is issued
+// from C++ so the host never falls behind the device: every exchange goes to the
+// communicator's own stream as soon as its partial exists (fork event from the
+// compute stream), and the compute stream waits for it (join event) only where
+// the reduced rows are read.  The user-row SpMM of a layer and the next layer's
+// item partial run on the compute stream meanwhile.
+//
+// RCCL is resolved at run time from the copy the process already loaded (torch's
+// ProcessGroupNCCL loads librccl.so.1), so librsx has no link-time dependency on
+// it and loads on machines without RCCL; rsx_comm_* return RSX_ERR_COMM then.
+#include <dlfcn.h>
+
+#include <cstring>
+
+#include <rccl/rccl.h>
+
+#include "rsx_common.hpp"
+
+namespace rsx {
+
+int spmm_dispatch(const rsx_csr& a, const float* x, int d, const rsx_epilogue& e, float* slab, hipStream_t s);
+int rowwise_dispatch(int64_t n, int d, const rsx_epilogue& e, hipStream_t s);
+int bpr_call(int32_t variant, const float* fin, const float* ego, int64_t n_users, int64_t n_items, int32_t d,
+             const int64_t* trip, int64_t batch, float reg, float batch_cfg, float* g_fin, float* g_ego,
+             float* loss_out, double* loss_acc, void* ws, size_t ws_bytes, hipStream_t s);
+
+namespace {
+
+struct Rccl {
+    decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+    decltype(&ncclCommInitRank) init_rank = nullptr;
+    decltype(&ncclCommDestroy) destroy = nullptr;
+    decltype(&ncclAllReduce) all_reduce = nullptr;
+    bool ok = false;
+};
+
+const Rccl& rccl() {
+    static Rccl r = [] {
+        Rccl x;
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);  // torch's copy, if loaded
+        if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) return x;
+        x.get_unique_id = reinterpret_cast<decltype(&ncclGetUniqueId)>(dlsym(h, "ncclGetUniqueId"));
+        x.init_rank = reinterpret_cast<decltype(&ncclCommInitRank)>(dlsym(h, "ncclCommInitRank"));
+        x.destroy = reinterpret_cast<decltype(&ncclCommDestroy)>(dlsym(h, "ncclCommDestroy"));
+        x.all_reduce = reinterpret_cast<decltype(&ncclAllReduce)>(dlsym(h, "ncclAllReduce"));
+        x.ok = x.get_unique_id && x.init_rank && x.destroy && x.all_reduce;
+        return x;
+    }();
+    return r;
+}
+
+constexpr int kJoinEvents = 64;  // > 2K+2 exchanges in flight per step for any K <= 30
+
+}  // namespace
+
+}  // namespace rsx
+
+struct rsx_comm_s {
+    ncclComm_t nccl = nullptr;
+    hipStream_t stream = nullptr;  // exchanges run here, ordered
+    hipEvent_t fork = nullptr;     // compute -> comm (waited right after it is recorded)
+    hipEvent_t join[rsx::kJoinEvents] = {};
+    int next = 0;
+    int32_t rank = 0, world = 1;
+};
+
+namespace rsx {
+namespace {
+
+// In-place sum of buf[0, n) over the communicator, after the work queued so far on
+// `s`; returns the join event the reader must wait on (nullptr on error, rc set).
+hipEvent_t exchange(rsx_comm_t c, float* buf, int64_t n, hipStream_t s, int* rc) {
+    hipError_t e;
+    if ((e = hipEventRecord(c->fork, s)) != hipSuccess || (e = hipStreamWaitEvent(c->stream, c->fork, 0)) != hipSuccess) {
+        *rc = hip_rc(e);
+        return nullptr;
+    }
+    const ncclResult_t r = rccl().all_reduce(buf, buf, (size_t)n, ncclFloat32, ncclSum, c->nccl, c->stream);
+    if (r != ncclSuccess) {
+        *rc = RSX_ERR_COMM;
+        return nullptr;
+    }
+    hipEvent_t j = c->join[c->next];
+    c->next = (c->next + 1) % kJoinEvents;
+    if ((e = hipEventRecord(j, c->stream)) != hipSuccess) {
+        *rc = hip_rc(e);
+        return nullptr;
+    }
+    return j;
+}
+
+int wait(hipStream_t s, hipEvent_t j) { return hip_rc(hipStreamWaitEvent(s, j, 0)); }
+
+rsx_epilogue epi(int kind) {
+    rsx_epilogue e = {};
+    e.kind = kind;
+    e.alpha = 1.f;
+    e.beta = 1.f;
+    return e;
+}
+
+#define RSX_TRY(x)                 \
+    do {                           \
+        const int rc_ = (x);       \
+        if (rc_) return rc_;       \
+    } while (0)
+
+// Forward layers (rsx/dist.py:_propagate).  Item rows of layer k live in
+// bufs[(k-1)&1] + nu*d; they are summed across ranks before anything reads them.
+int sharded_forward(const rsx_sharded_lgcn_step& st, bool zero_grads, hipStream_t s) {
+    const int d = st.d, K = st.n_layers;
+    const int64_t nu = st.n_users, ni = st.n_items, off = nu * (int64_t)d;
+    const float beta = 1.f / (float)(K + 1);
+    float* bufs[2] = {st.h0, st.h1};
+    auto ys = [&](int k) -> float* { return k == 0 ? st.p : bufs[(k - 1) & 1]; };
+    hipEvent_t joins[64] = {};
+    int rc = 0;
+    auto item_partial = [&](int k) -> int {  // items^k partial = R_g^T users^{k-1}; exchange queued
+        rsx_epilogue e = epi(RSX_EPI_STORE);
+        e.y = ys(k) + off;
+        RSX_TRY(spmm_dispatch(*st.adj_i, ys(k - 1), d, e, st.slab_i, s));
+        joins[k] = exchange(st.comm, ys(k) + off, ni * d, s, &rc);
+        return joins[k] ? 0 : rc;
+    };
+    RSX_TRY(item_partial(1));
+    for (int k = 1; k <= K; ++k) {
+        const float* s_in = k == 1 ? st.p : st.s;
+        if (k < K) {
+            rsx_epilogue e = epi(RSX_EPI_LAYERSUM);
+            e.y = ys(k);
+            e.s_in = s_in;
+            e.s_out = st.s;
+            RSX_TRY(spmm_dispatch(*st.adj_u, ys(k - 1), d, e, st.slab_u, s));
+            RSX_TRY(item_partial(k + 1));
+        } else {
+            rsx_epilogue e = epi(RSX_EPI_FINAL);
+            e.beta = beta;
+            e.f = st.final_emb;
+            e.s_in = s_in;
+            if (zero_grads) {
+                e.zero0 = st.g;
+                e.zero1 = st.r;
+            }
+            RSX_TRY(spmm_dispatch(*st.adj_u, ys(k - 1), d, e, st.slab_u, s));
+        }
+        RSX_TRY(wait(s, joins[k]));
+        rsx_epilogue e = epi(RSX_EPI_ADD);
+        e.s_in = s_in + off;
+        e.r_add = ys(k) + off;
+        if (k < K) {
+            e.y = st.s + off;
+        } else {
+            e.beta = beta;
+            e.y = st.final_emb + off;
+            if (zero_grads) {
+                e.zero0 = st.g + off;
+                e.zero1 = st.r + off;
+            }
+        }
+        RSX_TRY(rowwise_dispatch(ni, d, e, s));
+    }
+    return 0;
+}
+
+bool valid(const rsx_sharded_lgcn_step* st) {
+    if (!st || !st->adj_u || !st->adj_i || !st->comm || !st->p || !st->final_emb || st->n_layers < 1 ||
+        st->n_layers > 30 || st->n_users < 0 || st->n_items <= 0)
+        return false;
+    if (st->adj_u->n_rows != st->n_users || st->adj_i->n_rows != st->n_items) return false;
+    if (st->adj_u->n_cols != st->n_users + st->n_items || st->adj_i->n_cols != st->n_users + st->n_items) return false;
+    if (st->n_layers >= 2 && (!st->s || !st->h0 || !st->h1)) return false;
+    if (st->n_layers == 1 && !st->h0) return false;
+    if ((st->adj_u->n_long > 0 && !st->slab_u) || (st->adj_i->n_long > 0 && !st->slab_i)) return false;
+    return true;
+}
+
+}  // namespace
+}  // namespace rsx
+
+extern "C" {
+
+size_t rsx_comm_unique_id_bytes(void) { return sizeof(ncclUniqueId); }
+
+int rsx_comm_get_unique_id(void* id_host) {
+    if (!id_host) return RSX_ERR_ARG;
+    if (!rsx::rccl().ok) return RSX_ERR_COMM;
+    ncclUniqueId id;
+    if (rsx::rccl().get_unique_id(&id) != ncclSuccess) return RSX_ERR_COMM;
+    memcpy(id_host, &id, sizeof(id));
+    return RSX_OK;
+}
+
+int rsx_comm_init(rsx_comm_t* out, const void* id_host, int32_t rank, int32_t world) {
+    if (!out || !id_host || world < 1 || rank < 0 || rank >= world) return RSX_ERR_ARG;
+    if (!rsx::rccl().ok) return RSX_ERR_COMM;
+    rsx_comm_s* c = new rsx_comm_s();
+    c->rank = rank;
+    c->world = world;
+    ncclUniqueId id;
+    memcpy(&id, id_host, sizeof(id));
+    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork, hipEventDisableTiming);
+    for (int i = 0; e == hipSuccess && i < rsx::kJoinEvents; ++i)
+        e = hipEventCreateWithFlags(&c->join[i], hipEventDisableTiming);
+    if (e != hipSuccess) {
+        rsx_comm_destroy(c);
+        return rsx::hip_rc(e);
+    }
+    if (rsx::rccl().init_rank(&c->nccl, world, id, rank) != ncclSuccess) {
+        c->nccl = nullptr;
+        rsx_comm_destroy(c);
+        return RSX_ERR_COMM;
+    }
+    *out = c;
+    return RSX_OK;
+}
+
+int rsx_comm_destroy(rsx_comm_t c) {
+    if (!c) return RSX_OK;
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->nccl) rsx::rccl().destroy(c->nccl);
+    for (int i = 0; i < rsx::kJoinEvents; ++i)
+        if (c->join[i]) (void)hipEventDestroy(c->join[i]);
+    if (c->fork) (void)hipEventDestroy(c->fork);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return RSX_OK;
+}
+
+int rsx_comm_allreduce_f32(rsx_comm_t c, float* buf, int64_t n, rsx_stream_t stream) {
+    if (!c || (!buf && n > 0) || n < 0) return RSX_ERR_ARG;
+    int rc = 0;
+    hipStream_t s = rsx::as_stream(stream);
+    hipEvent_t j = rsx::exchange(c, buf, n, s, &rc);
+    if (!j) return rc;
+    return rsx::wait(s, j);
+}
+
+int rsx_sharded_lightgcn_forward(const rsx_sharded_lgcn_step* st, rsx_stream_t stream) {
+    if (!rsx::valid(st)) return RSX_ERR_ARG;
+    return rsx::sharded_forward(*st, false, rsx::as_stream(stream));
+}
+
+int rsx_sharded_lightgcn_step(const rsx_sharded_lgcn_step* st, rsx_stream_t stream) {
+    using namespace rsx;
+    if (!valid(st) || !st->m || !st->v || !st->g || !st->r || !st->t || !st->triplets || st->batch <= 0)
+        return RSX_ERR_ARG;
+    hipStream_t s = as_stream(stream);
+    const int d = st->d, K = st->n_layers;
+    const int64_t nu = st->n_users, ni = st->n_items, off = nu * (int64_t)d;
+    const float beta = 1.f / (float)(K + 1);
+    RSX_TRY(sharded_forward(*st, true, s));
+    RSX_TRY(bpr_call(RSX_BPR_LIGHTGCN, st->final_emb, st->p, nu, ni, d, st->triplets, st->batch, st->reg,
+                     (float)st->batch, st->g, st->r, st->loss_out, st->loss_acc, st->ws, st->ws_bytes, s));
+    // backward: the same layer sums on H^0 = G = dL/dfinal (rsx/dist.py:step)
+    float* bufs[2] = {st->h0, st->h1};
+    auto ys = [&](int k) -> float* { return k == 0 ? st->g : bufs[(k - 1) & 1]; };
+    hipEvent_t joins[64] = {};
+    int rc = 0;
+    hipEvent_t j0 = exchange(st->comm, st->g + off, ni * d, s, &rc);  // G's item rows: per-rank partials
+    if (!j0) return rc;
+    auto item_partial = [&](int k) -> int {
+        if (k < K) {
+            rsx_epilogue e = epi(RSX_EPI_STORE);
+            e.y = ys(k) + off;
+            RSX_TRY(spmm_dispatch(*st->adj_i, ys(k - 1), d, e, st->slab_i, s));
+            joins[k] = exchange(st->comm, ys(k) + off, ni * d, s, &rc);
+        } else {  // t = H_I^K/(K+1) + R_I: this rank's share of the item gradient beyond s_I/(K+1)
+            rsx_epilogue e = epi(RSX_EPI_ADD);
+            e.alpha = beta;
+            e.y = st->t;
+            e.r_add = st->r + off;
+            RSX_TRY(spmm_dispatch(*st->adj_i, ys(k - 1), d, e, st->slab_i, s));
+            joins[k] = exchange(st->comm, st->t, ni * d, s, &rc);
+        }
+        return joins[k] ? 0 : rc;
+    };
+    RSX_TRY(item_partial(1));
+    RSX_TRY(wait(s, j0));
+    for (int k = 1; k <= K; ++k) {
+        const float* s_in = k == 1 ? st->g : st->s;
+        if (k < K) {
+            rsx_epilogue e = epi(RSX_EPI_LAYERSUM);
+            e.y = ys(k);
+            e.s_in = s_in;
+            e.s_out = st->s;
+            RSX_TRY(spmm_dispatch(*st->adj_u, ys(k - 1), d, e, st->slab_u, s));
+            RSX_TRY(item_partial(k + 1));
+            RSX_TRY(wait(s, joins[k]));
+            rsx_epilogue a = epi(RSX_EPI_ADD);
+            a.y = st->s + off;
+            a.s_in = s_in + off;
+            a.r_add = ys(k) + off;
+            RSX_TRY(rowwise_dispatch(ni, d, a, s));
+        } else {
+            rsx_epilogue e = epi(RSX_EPI_ADAM);
+            e.beta = beta;
+            e.adam = st->adam;
+            e.s_in = s_in;
+            e.r_add = st->r;
+            e.p = st->p;
+            e.m = st->m;
+            e.v = st->v;
+            RSX_TRY(spmm_dispatch(*st->adj_u, ys(k - 1), d, e, st->slab_u, s));
+            RSX_TRY(wait(s, joins[k]));
+            rsx_epilogue a = epi(RSX_EPI_ADAM);
+            a.beta = beta;
+            a.adam = st->adam;
+            a.s_in = s_in + off;
+            a.r_add = st->t;
+            a.p = st->p + off;
+            a.m = st->m + off;
+            a.v = st->v + off;
+            RSX_TRY(rowwise_dispatch(ni, d, a, s));
+        }
+    }
+    return 0;
+}
+
+}  // extern "C"

@@ -31,7 +31,8 @@ RSX_BPR_SMORE = 2
 
 _ERRORS = {1001: "RSX_ERR_ARG (bad size or null pointer)",
            1002: "RSX_ERR_UNSUPPORTED (embedding width / k not compiled)",
-           1003: "RSX_ERR_WORKSPACE (workspace too small)"}
+           1003: "RSX_ERR_WORKSPACE (workspace too small)",
+           1004: "RSX_ERR_COMM (RCCL missing or a collective failed)"}
 
 
 class Csr(C.Structure):
@@ -65,6 +66,15 @@ class LgcnStep(C.Structure):
                 ("adam", Adam), ("loss_out", P), ("loss_acc", P), ("ws", P), ("ws_bytes", C.c_size_t)]
 
 
+class ShardedStep(C.Structure):
+    _fields_ = [("adj_u", C.POINTER(Csr)), ("adj_i", C.POINTER(Csr)), ("n_users", I64), ("n_items", I64),
+                ("d", I32), ("n_layers", I32), ("reg", F32), ("pad0", I32),
+                ("p", P), ("m", P), ("v", P), ("s", P), ("h0", P), ("h1", P), ("final_emb", P), ("g", P),
+                ("r", P), ("t", P), ("slab_u", P), ("slab_i", P), ("triplets", P), ("batch", I64),
+                ("adam", Adam), ("loss_out", P), ("loss_acc", P), ("ws", P), ("ws_bytes", C.c_size_t),
+                ("comm", P)]
+
+
 _LIB = None
 
 
@@ -94,6 +104,13 @@ def _declare(lib):
         "rsx_topk_metrics": (C.c_int, [P, I64, I32, P, P, P, I32, P, P, P, C.c_size_t, P]),
         "rsx_linear_wgrad_ws_bytes": (C.c_size_t, [I64, I32, I32]),
         "rsx_linear_wgrad": (C.c_int, [P, P, I64, I32, I32, P, P, C.c_size_t, P]),
+        "rsx_comm_unique_id_bytes": (C.c_size_t, []),
+        "rsx_comm_get_unique_id": (C.c_int, [P]),
+        "rsx_comm_init": (C.c_int, [C.POINTER(P), P, I32, I32]),
+        "rsx_comm_destroy": (C.c_int, [P]),
+        "rsx_comm_allreduce_f32": (C.c_int, [P, P, I64, P]),
+        "rsx_sharded_lightgcn_step": (C.c_int, [C.POINTER(ShardedStep), P]),
+        "rsx_sharded_lightgcn_forward": (C.c_int, [C.POINTER(ShardedStep), P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -107,7 +124,9 @@ EXPORTED = ["rsx_version", "rsx_csr_schedule_host", "rsx_spmm", "rsx_rowwise", "
             "rsx_smore_spectral_spec_floats", "rsx_smore_spectral_fwd_ws_bytes", "rsx_smore_spectral_fwd",
             "rsx_smore_spectral_bwd",
             "rsx_smore_spectral_bwd_partials",
-            "rsx_topk_metrics_ws_bytes", "rsx_topk_metrics", "rsx_linear_wgrad_ws_bytes", "rsx_linear_wgrad"]
+            "rsx_topk_metrics_ws_bytes", "rsx_topk_metrics", "rsx_linear_wgrad_ws_bytes", "rsx_linear_wgrad",
+            "rsx_comm_unique_id_bytes", "rsx_comm_get_unique_id", "rsx_comm_init", "rsx_comm_destroy",
+            "rsx_comm_allreduce_f32", "rsx_sharded_lightgcn_step", "rsx_sharded_lightgcn_forward"]
 
 
 def lib_path() -> str:

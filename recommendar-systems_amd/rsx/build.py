@@ -19,7 +19,7 @@ CSRC = os.path.join(ROOT, "csrc")
 INCLUDE = os.path.join(REPO, "include")
 LIBDIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIBDIR, "librsx.so")
-SOURCES = ["spmm.hip", "bpr.hip", "fullsort.hip", "step.hip", "smore.hip", "metrics.hip", "linear.hip"]
+SOURCES = ["spmm.hip", "bpr.hip", "fullsort.hip", "step.hip", "smore.hip", "metrics.hip", "linear.hip", "dist.hip"]
 ARCH = os.environ.get("RSX_OFFLOAD_ARCH", "gfx950")
 
 
@@ -63,7 +63,7 @@ def build(force: bool = False, verbose: bool = True) -> str:
     with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
         objs = list(ex.map(compile_one, srcs))
     tmp = LIB + ".tmp"
-    cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs]
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs, "-ldl"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stderr}")

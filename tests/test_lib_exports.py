@@ -32,6 +32,14 @@ def test_struct_layouts_match_header():
     assert C.sizeof(L.Csr) == 8 * 3 + 8 * 3 + 4 * 2 + 8 + 8 + 8 + 8 + 8
     assert C.sizeof(L.Adam) == 4 * 6 + 8 + 8
     assert C.sizeof(L.Epilogue) == 4 * 4 + 8 * 14 + C.sizeof(L.Adam)
+    # gcc on include/rsx.h: sizeof(rsx_lgcn_step) = 216, sizeof(rsx_sharded_lgcn_step) = 240
+    assert C.sizeof(L.LgcnStep) == 216
+    assert C.sizeof(L.ShardedStep) == 240
+
+
+def test_comm_unique_id_size():
+    # the RCCL unique id the sharded step's handshake broadcasts (ncclUniqueId = 128 bytes)
+    assert L.lib().rsx_comm_unique_id_bytes() == 128
 
 
 def test_schedule_host_splits_hub_rows():
