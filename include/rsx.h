@@ -92,8 +92,10 @@ int rsx_csr_schedule_host(const int64_t* rowptr_host, int64_t n_rows, int32_t ch
  *   RSX_EPI_STORE     y = alpha*acc
  *   RSX_EPI_LAYERSUM  y = alpha*acc;  s_out = s_in + alpha*acc
  *                     (running layer sum of lightgcn.py:124-125 / Horner backward)
- *   RSX_EPI_FINAL     f = (s_in + alpha*acc) * beta;  zero0/zero1 rows := 0
- *                     (last layer: mean over K+1 layers, lightgcn.py:124-125)
+ *   RSX_EPI_FINAL     f = (((s_in + r_add) + aux) + alpha*acc) * beta (NULL terms
+ *                     skipped);  zero0/zero1 rows := 0  (last layer: mean over K+1
+ *                     layers, lightgcn.py:124-125, from a running sum in s_in or
+ *                     from the stored layers E0 = s_in, E1 = r_add, E2 = aux)
  *   RSX_EPI_ADAM      g = (s_in + alpha*acc) * beta + r_add;  Adam(p, m, v, g)
  *                     (last backward layer fused with torch.optim.Adam,
  *                      src/common/trainer.py:133,238)
@@ -159,7 +161,25 @@ typedef struct rsx_epilogue {
     float* aux;        /* LAYERGCN: pre-scale rows written; LAYERGCN_BWD: read */
     float* aux_w;      /* LAYERGCN: cosine weight per row written; LAYERGCN_BWD: read */
     rsx_adam adam;
+    /* Batch-row tags (optional): row r is "tagged" when row_tag[r] == tag.  The
+     * tag_flags bits say which operands are known to be zero / unused off the
+     * tagged rows, so their memory traffic is skipped (results are unchanged):
+     *   RSX_TAG_ROWS      output rows not tagged are skipped entirely (no loads,
+     *                     no stores: their outputs keep their old contents);
+     *   RSX_TAG_SPARSE_X  X rows not tagged are zero: their gathers are skipped;
+     *   RSX_TAG_SPARSE_S  s_in rows not tagged are zero (not loaded);
+     *   RSX_TAG_SPARSE_R  r_add rows not tagged are zero (not loaded);
+     *   RSX_TAG_ZERO      zero0 / zero1 are cleared on tagged rows only. */
+    const int32_t* row_tag;
+    int32_t tag;
+    int32_t tag_flags;
 } rsx_epilogue;
+
+#define RSX_TAG_ROWS 1
+#define RSX_TAG_SPARSE_X 2
+#define RSX_TAG_SPARSE_S 4
+#define RSX_TAG_SPARSE_R 8
+#define RSX_TAG_ZERO 16
 
 int rsx_spmm(const rsx_csr* a, const float* x, int32_t d, const rsx_epilogue* epi,
              float* slab, rsx_stream_t stream);
@@ -301,6 +321,17 @@ typedef struct rsx_lgcn_step {
     float* loss_out;    /* [1] */
     double* loss_acc;   /* [1] or NULL */
     void* ws; size_t ws_bytes; /* >= rsx_bpr_ws_bytes(batch) */
+    /* Optional [n_users + n_items] int32 scratch, zero-filled before the first step
+     * (K >= 2 only; NULL = dense path).  Each step tags its batch rows with a fresh
+     * value (`tag`, > 0 and different from every earlier step's, e.g. the step
+     * count) and uses the tags to skip the work a batch does not need: the last
+     * forward layer computes the batch rows only (only they reach the loss), the
+     * first backward layer skips gathers of the all-zero rows of G = dL/dfinal, and
+     * the gradient scratch G, R is cleared on the batch rows after Adam instead of
+     * densely before the loss.  With tags, G and R must be zero between steps
+     * (true from zero-filled buffers and after every tagged step). */
+    int32_t* row_tag;
+    int64_t tag;
 } rsx_lgcn_step;
 
 int rsx_lightgcn_step(const rsx_lgcn_step* st, rsx_stream_t stream);

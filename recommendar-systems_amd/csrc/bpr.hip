@@ -27,6 +27,7 @@ struct BprArgs {
     const int64_t* trip;
     int64_t batch;
     float reg, batch_cfg;
+    float g_div;     // LightGCN: dL/dfinal is divided by this (K+1: the mean's backward), 1 = none
     float* g_fin;
     float* g_ego;
     float* loss_out;
@@ -199,6 +200,11 @@ __global__ __launch_bounds__(kBprBlock) void bpr_bwd(BprArgs a, int n_part) {
         const int col = li + c * G;
         const float fu = a.fin[u * D + col], fp = a.fin[p * D + col], fn = a.fin[n * D + col];
         float gu = coef * (fp - fn), gp = coef * fu, gn = -coef * fu;
+        if (a.g_div != 1.f) {  // gradient of each layer's share of the mean (MeanBackward: grad / n)
+            gu /= a.g_div;
+            gp /= a.g_div;
+            gn /= a.g_div;
+        }
         if (a.variant == RSX_BPR_SMORE) {
             gu += ku * fu;
             gp += kp * fp;
@@ -242,7 +248,7 @@ size_t bpr_ws(int64_t batch) {
 
 int bpr_call(int32_t variant, const float* fin, const float* ego, int64_t n_users, int64_t n_items, int32_t d,
              const int64_t* trip, int64_t batch, float reg, float batch_cfg, float* g_fin, float* g_ego,
-             float* loss_out, double* loss_acc, void* ws, size_t ws_bytes, hipStream_t s) {
+             float* loss_out, double* loss_acc, void* ws, size_t ws_bytes, hipStream_t s, float g_div) {
     if (!fin || !trip || !g_fin || batch <= 0 || !ws) return RSX_ERR_ARG;
     if (variant != RSX_BPR_SMORE && !ego) return RSX_ERR_ARG;
     if (variant < 0 || variant > 2) return RSX_ERR_ARG;
@@ -257,6 +263,7 @@ int bpr_call(int32_t variant, const float* fin, const float* ego, int64_t n_user
     a.batch = batch;
     a.reg = reg;
     a.batch_cfg = batch_cfg;
+    a.g_div = variant == RSX_BPR_LIGHTGCN ? g_div : 1.f;
     a.g_fin = g_fin;
     a.g_ego = g_ego;
     a.loss_out = loss_out;
@@ -278,7 +285,7 @@ int rsx_bpr(int32_t variant, const float* final_emb, const float* ego_emb, int64
             int32_t d, const int64_t* triplets, int64_t batch, float reg, float batch_cfg, float* g_final,
             float* g_ego, float* loss_out, double* loss_acc, void* ws, size_t ws_bytes, rsx_stream_t stream) {
     return rsx::bpr_call(variant, final_emb, ego_emb, n_users, n_items, d, triplets, batch, reg, batch_cfg,
-                         g_final, g_ego, loss_out, loss_acc, ws, ws_bytes, rsx::as_stream(stream));
+                         g_final, g_ego, loss_out, loss_acc, ws, ws_bytes, rsx::as_stream(stream), 1.f);
 }
 
 }  // extern "C"

@@ -32,7 +32,7 @@ int spmm_dispatch(const rsx_csr& a, const float* x, int d, const rsx_epilogue& e
 int rowwise_dispatch(int64_t n, int d, const rsx_epilogue& e, hipStream_t s);
 int bpr_call(int32_t variant, const float* fin, const float* ego, int64_t n_users, int64_t n_items, int32_t d,
              const int64_t* trip, int64_t batch, float reg, float batch_cfg, float* g_fin, float* g_ego,
-             float* loss_out, double* loss_acc, void* ws, size_t ws_bytes, hipStream_t s);
+             float* loss_out, double* loss_acc, void* ws, size_t ws_bytes, hipStream_t s, float g_div = 1.f);
 
 namespace {
 

@@ -60,7 +60,11 @@ __device__ __forceinline__ float adam_elem(const AdamConst& c, float& p, float& 
 struct EpiIn {
     float4 a, b, c, d, e;
     float w;
+    bool tagged;  // row_tag[row] == tag (true when no tag flag needs it)
 };
+
+// tag flags in effect (none without a tag array)
+__device__ __forceinline__ int tag_flags(const rsx_epilogue& e) { return e.row_tag ? e.tag_flags : 0; }
 
 template <int KIND, int D>
 __device__ __forceinline__ EpiIn epi_load(const rsx_epilogue& e, int64_t row, int li) {
@@ -68,14 +72,23 @@ __device__ __forceinline__ EpiIn epi_load(const rsx_epilogue& e, int64_t row, in
     EpiIn in;
     in.a = in.b = in.c = in.d = in.e = f4(0.f);
     in.w = 0.f;
-    if constexpr (KIND == RSX_EPI_LAYERSUM || KIND == RSX_EPI_FINAL || KIND == RSX_EPI_AXPBY) {
-        if (e.s_in) in.a = ld4(e.s_in + off);
+    const int tf = tag_flags(e);
+    in.tagged = (tf & (RSX_TAG_SPARSE_S | RSX_TAG_SPARSE_R | RSX_TAG_ZERO)) ? e.row_tag[row] == e.tag : true;
+    // rows of s_in / r_add known to be zero off the tagged rows are not loaded
+    const float* s_in = (!(tf & RSX_TAG_SPARSE_S) || in.tagged) ? e.s_in : nullptr;
+    const float* r_add = (!(tf & RSX_TAG_SPARSE_R) || in.tagged) ? e.r_add : nullptr;
+    if constexpr (KIND == RSX_EPI_LAYERSUM || KIND == RSX_EPI_AXPBY) {
+        if (s_in) in.a = ld4(s_in + off);
+    } else if constexpr (KIND == RSX_EPI_FINAL) {
+        if (s_in) in.a = ld4(s_in + off);
+        if (r_add) in.b = ld4(r_add + off);
+        if (e.aux) in.c = ld4(e.aux + off);
     } else if constexpr (KIND == RSX_EPI_ADD) {
-        if (e.s_in) in.a = ld4(e.s_in + off);
-        if (e.r_add) in.b = ld4(e.r_add + off);
+        if (s_in) in.a = ld4(s_in + off);
+        if (r_add) in.b = ld4(r_add + off);
     } else if constexpr (KIND == RSX_EPI_ADAM) {
-        if (e.s_in) in.a = ld4(e.s_in + off);
-        if (e.r_add) in.b = ld4(e.r_add + off);
+        if (s_in) in.a = ld4(s_in + off);
+        if (r_add) in.b = ld4(r_add + off);
         in.c = ld4(e.p + off);
         in.d = ld4(e.m + off);
         in.e = ld4(e.v + off);
@@ -104,7 +117,11 @@ __device__ __forceinline__ void epilogue(const rsx_epilogue& e, int64_t row, flo
         const float4 s = e.s_in ? add4(in.a, acc) : acc;
         st4(e.s_out + off, s);
     } else if constexpr (KIND == RSX_EPI_FINAL) {
-        const float4 s = e.s_in ? add4(in.a, acc) : acc;
+        // ((s_in + r_add) + aux) + acc: the stored layers summed in layer order
+        float4 t = in.a;
+        if (e.r_add) t = add4(t, in.b);
+        if (e.aux) t = add4(t, in.c);
+        const float4 s = (e.s_in || e.r_add || e.aux) ? add4(t, acc) : acc;
         st4(e.f + off, mul4(e.beta, s));
     } else if constexpr (KIND == RSX_EPI_AXPBY) {
         float4 s = acc;
@@ -168,8 +185,10 @@ __device__ __forceinline__ void epilogue(const rsx_epilogue& e, int64_t row, flo
             st4(e.s_out + off, e.s_in ? add4(in.d, de) : de);
         }
     }
-    if (e.zero0) st4(e.zero0 + off, f4(0.f));
-    if (e.zero1) st4(e.zero1 + off, f4(0.f));
+    if (!(tag_flags(e) & RSX_TAG_ZERO) || in.tagged) {
+        if (e.zero0) st4(e.zero0 + off, f4(0.f));
+        if (e.zero1) st4(e.zero1 + off, f4(0.f));
+    }
 }
 
 template <int KIND, int D>
@@ -204,7 +223,7 @@ __device__ __forceinline__ float4 gather8(float4 acc, int cm, float vm, int n, c
     c[7] = row_bcast<8 * H + 7>(cm); v[7] = __int_as_float(row_bcast<8 * H + 7>(vi));
     float4 xv[8];
 #pragma unroll
-    for (int t = 0; t < 8; ++t) xv[t] = (8 * H + t < n) ? ld4(xl + (int64_t)c[t] * 64) : f4(0.f);
+    for (int t = 0; t < 8; ++t) xv[t] = (8 * H + t < n && c[t] >= 0) ? ld4(xl + (int64_t)c[t] * 64) : f4(0.f);
 #pragma unroll
     for (int t = 0; t < 8; ++t) acc = fma4(v[t], xv[t], acc);
     return acc;
@@ -227,6 +246,8 @@ __device__ __forceinline__ void fixup_block(const rsx_csr& a, const rsx_epilogue
     const int li = threadIdx.x % G;
     const int gi = threadIdx.x / G;
     const int4 lr = reinterpret_cast<const int4*>(a.long_rows)[l];
+    // an untagged row's chunks skipped too (nothing arrives; the counter stays 0)
+    if ((tag_flags(e) & RSX_TAG_ROWS) && e.row_tag[lr.x] != e.tag) return;
     EpiIn pre;
     if (gi == 0) pre = epi_load<KIND, D>(e, lr.x, li);
     int* cnt = reinterpret_cast<int*>(slab + a.n_slots * D) + l;
@@ -289,7 +310,7 @@ __device__ __forceinline__ float4 gather16(float4 acc, int cm, float vm, int n, 
     bcast8<1>(cm, vi, c + 8, v + 8);
     float4 xv[16];
 #pragma unroll
-    for (int t = 0; t < 16; ++t) xv[t] = t < n ? ld4(xl + (int64_t)c[t] * 64) : f4(0.f);
+    for (int t = 0; t < 16; ++t) xv[t] = (t < n && c[t] >= 0) ? ld4(xl + (int64_t)c[t] * 64) : f4(0.f);
 #pragma unroll
     for (int t = 0; t < 16; ++t) acc = fma4(v[t], xv[t], acc);
     return acc;
@@ -321,12 +342,19 @@ __device__ __forceinline__ void st4_sc1(float* p, float4 v) {
 template <int D, int KIND>
 __device__ __forceinline__ void spmm_item(const rsx_csr& a, const float* __restrict__ x, const rsx_epilogue& e,
                                           float* __restrict__ slab, int4 wk, int li) {
+    const int tf = tag_flags(e);
+    if (tf & RSX_TAG_ROWS) {  // whole group leaves together (one row per group)
+        const int64_t r = wk.y < 0 ? wk.x : reinterpret_cast<const int4*>(a.long_rows)[wk.x].x;
+        if (e.row_tag[r] != e.tag) return;
+    }
+    const bool sparse_x = tf & RSX_TAG_SPARSE_X;
     EpiIn pre;
     if (wk.y < 0) {
         pre = epi_load<KIND, D>(e, wk.x, li);
     } else {
         pre.a = pre.b = pre.c = pre.d = pre.e = f4(0.f);
         pre.w = 0.f;
+        pre.tagged = true;
     }
     const int32_t* __restrict__ col = a.col;
     const float* __restrict__ val = a.val;
@@ -341,8 +369,9 @@ __device__ __forceinline__ void spmm_item(const rsx_csr& a, const float* __restr
         // memory pipe only sees the neighbour-row gathers.
         for (; j < end; j += 16) {
             const bool mine = j + li < end;
-            const int cm = mine ? col[j + li] : 0;
+            int cm = mine ? col[j + li] : 0;
             const float vm = mine ? val[j + li] : 0.f;
+            if (sparse_x && mine && e.row_tag[cm] != e.tag) cm = -1;  // zero X row: no gather
             const int n = end - j;
 #if RSX_SPMM_G16
             acc = gather16(acc, cm, vm, n, xl);
@@ -360,9 +389,14 @@ __device__ __forceinline__ void spmm_item(const rsx_csr& a, const float* __restr
                 c[t] = col[j + t];
                 v[t] = val[j + t];
             }
+            if (sparse_x) {
+#pragma unroll
+                for (int t = 0; t < kUnroll; ++t)
+                    if (e.row_tag[c[t]] != e.tag) c[t] = -1;
+            }
             float4 xv[kUnroll];
 #pragma unroll
-            for (int t = 0; t < kUnroll; ++t) xv[t] = ld4(xl + (int64_t)c[t] * D);
+            for (int t = 0; t < kUnroll; ++t) xv[t] = c[t] >= 0 ? ld4(xl + (int64_t)c[t] * D) : f4(0.f);
 #pragma unroll
             for (int t = 0; t < kUnroll; ++t) acc = fma4(v[t], xv[t], acc);
         }
@@ -374,10 +408,11 @@ __device__ __forceinline__ void spmm_item(const rsx_csr& a, const float* __restr
                 const bool ok = j + t < end;
                 c[t] = ok ? col[j + t] : 0;
                 v[t] = ok ? val[j + t] : 0.f;
+                if (sparse_x && ok && e.row_tag[c[t]] != e.tag) c[t] = -1;
             }
             float4 xv[kUnroll];
 #pragma unroll
-            for (int t = 0; t < kUnroll; ++t) xv[t] = (j + t < end) ? ld4(xl + (int64_t)c[t] * D) : f4(0.f);
+            for (int t = 0; t < kUnroll; ++t) xv[t] = (j + t < end && c[t] >= 0) ? ld4(xl + (int64_t)c[t] * D) : f4(0.f);
 #pragma unroll
             for (int t = 0; t < kUnroll; ++t)
                 if (j + t < end) acc = fma4(v[t], xv[t], acc);
@@ -440,6 +475,7 @@ __global__ __launch_bounds__(kBlock) void rowwise_kernel(int64_t n_rows, rsx_epi
     const int li = threadIdx.x % G;
     const int64_t row = (int64_t)blockIdx.x * GPB + threadIdx.x / G;
     if (row >= n_rows) return;
+    if ((tag_flags(e) & RSX_TAG_ROWS) && e.row_tag[row] != e.tag) return;
     epilogue<KIND, D>(e, row, f4(0.f), li);
 }
 

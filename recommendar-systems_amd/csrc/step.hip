@@ -13,8 +13,13 @@
 //   forward   E^k = A E^{k-1}, running sum S, last layer writes F = S/(K+1) and
 //             zeroes the gradient scratch G, R;
 //   loss      BPR fwd+bwd: G += dL/dF (batch rows), R += d reg / d E^0;
-//   backward  Horner: H_k = A H_{k-1} (H_0 = G), S = sum H; the last layer
+//   backward  H_k = A H_{k-1} (H_0 = G), S = sum H; the last layer
 //             applies Adam to E^0 with g = S/(K+1) + R in its epilogue.
+// With batch-row tags (rsx_lgcn_step.row_tag, K = 2, 3) the step stores the
+// layers instead of a running sum, computes the last forward layer on the batch
+// rows only and runs the backward as the reference autograd's recursion on
+// G' = G/(K+1) (lgcn_step_stored_layers below): about 110 MB less traffic per
+// sports-shaped step.
 #include "rsx_common.hpp"
 
 namespace rsx {
@@ -23,7 +28,7 @@ int spmm_dispatch(const rsx_csr& a, const float* x, int d, const rsx_epilogue& e
 int rowwise_dispatch(int64_t n, int d, const rsx_epilogue& e, hipStream_t s);
 int bpr_call(int32_t variant, const float* fin, const float* ego, int64_t n_users, int64_t n_items, int32_t d,
              const int64_t* trip, int64_t batch, float reg, float batch_cfg, float* g_fin, float* g_ego,
-             float* loss_out, double* loss_acc, void* ws, size_t ws_bytes, hipStream_t s);
+             float* loss_out, double* loss_acc, void* ws, size_t ws_bytes, hipStream_t s, float g_div = 1.f);
 
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     z += 0x9e3779b97f4a7c15ull;
@@ -105,6 +110,15 @@ int sample_call(const rsx_sampler_args& s, int64_t batch, int64_t* out, hipStrea
     return last_rc();
 }
 
+// row_tag[u] = row_tag[n_users + i] = row_tag[n_users + j] = tag for every triplet
+__global__ __launch_bounds__(256) void tag_rows_kernel(const int64_t* __restrict__ trip, int64_t batch,
+                                                       int64_t n_users, int32_t* __restrict__ row_tag, int32_t tag) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= 3 * batch) return;
+    const int64_t id = trip[t];
+    row_tag[t < batch ? id : n_users + id] = tag;
+}
+
 static rsx_epilogue epi0(int kind) {
     rsx_epilogue e = {};
     e.kind = kind;
@@ -115,7 +129,8 @@ static rsx_epilogue epi0(int kind) {
 
 // forward: returns rc; writes final = mean_{k=0..K} A^k p; zeroes z0/z1 rows in the last pass.
 static int lgcn_forward(const rsx_csr& A, int d, int K, const float* p, float* s, float* h0, float* h1, float* fin,
-                        float* slab, float* z0, float* z1, hipStream_t st) {
+                        float* slab, float* z0, float* z1, hipStream_t st, const int32_t* row_tag = nullptr,
+                        int32_t tag = 0) {
     const float beta = 1.f / (float)(K + 1);
     int rc;
     if (K == 0) {
@@ -137,6 +152,11 @@ static int lgcn_forward(const rsx_csr& A, int d, int K, const float* p, float* s
             e.beta = beta;
             e.zero0 = z0;
             e.zero1 = z1;
+            if (row_tag) {  // only the tagged (batch) rows of the final table are needed
+                e.row_tag = row_tag;
+                e.tag = tag;
+                e.tag_flags = RSX_TAG_ROWS;
+            }
         } else {
             e = epi0(RSX_EPI_LAYERSUM);
             e.y = bufs[(k - 1) & 1];
@@ -147,6 +167,69 @@ static int lgcn_forward(const rsx_csr& A, int d, int K, const float* p, float* s
         x = bufs[(k - 1) & 1];
     }
     return 0;
+}
+
+// The batch-tagged LightGCN step for K = 2, 3: the forward keeps E^1..E^{K-1} in
+// h0 / h1 (no running sum) and computes the last layer and the mean on the batch
+// rows only; BPR writes G' = dL/dfinal / (K+1) (each layer's share of the mean,
+// MeanBackward); the backward is Horner on G', the reference autograd's own
+// recursion  dE^{k-1} = G' + A dE^k  (A symmetric), so no layer sum is stored
+// either: layer 1 gathers only the batch rows of G' (the rest are zero) and every
+// layer adds G' on the batch rows only.  The last layer applies Adam with
+// g = (G' + A dE^1) + R and clears G', R on the batch rows for the next step.
+static int lgcn_step_stored_layers(const rsx_lgcn_step& st, int64_t batch, int32_t tag, hipStream_t s) {
+    const rsx_csr& A = *st.adj;
+    const int d = st.d, K = st.n_layers;
+    int rc;
+    float* bufs[2] = {st.h0, st.h1};
+    // forward: E^k = A E^{k-1} stored (k < K), then F = mean on the tagged rows
+    const float* x = st.p;
+    for (int k = 1; k < K; ++k) {
+        rsx_epilogue e = epi0(RSX_EPI_STORE);
+        e.y = bufs[k - 1];
+        if ((rc = spmm_dispatch(A, x, d, e, st.slab, s))) return rc;
+        x = bufs[k - 1];
+    }
+    {
+        rsx_epilogue e = epi0(RSX_EPI_FINAL);
+        e.beta = 1.f / (float)(K + 1);
+        e.f = st.final_emb;
+        e.s_in = st.p;                        // E^0
+        e.r_add = st.h0;                      // E^1
+        e.aux = K == 3 ? st.h1 : nullptr;     // E^2
+        e.row_tag = st.row_tag;
+        e.tag = tag;
+        e.tag_flags = RSX_TAG_ROWS;
+        if ((rc = spmm_dispatch(A, x, d, e, st.slab, s))) return rc;
+    }
+    if ((rc = bpr_call(RSX_BPR_LIGHTGCN, st.final_emb, st.p, st.n_users, st.n_items, d, st.triplets, batch, st.reg,
+                       (float)batch, st.g, st.r, st.loss_out, st.loss_acc, st.ws, st.ws_bytes, s, (float)(K + 1))))
+        return rc;
+    // backward: H = G' + A H, H_0 = G'
+    x = st.g;
+    for (int k = 1; k < K; ++k) {
+        rsx_epilogue e = epi0(RSX_EPI_ADD);
+        e.y = bufs[k - 1];
+        e.s_in = st.g;
+        e.row_tag = st.row_tag;
+        e.tag = tag;
+        e.tag_flags = RSX_TAG_SPARSE_S | (k == 1 ? RSX_TAG_SPARSE_X : 0);
+        if ((rc = spmm_dispatch(A, x, d, e, st.slab, s))) return rc;
+        x = bufs[k - 1];
+    }
+    rsx_epilogue e = epi0(RSX_EPI_ADAM);
+    e.s_in = st.g;
+    e.r_add = st.r;
+    e.p = st.p;
+    e.m = st.m;
+    e.v = st.v;
+    e.adam = st.adam;
+    e.zero0 = st.g;  // nothing reads G' or R after this layer (K >= 2)
+    e.zero1 = st.r;
+    e.row_tag = st.row_tag;
+    e.tag = tag;
+    e.tag_flags = RSX_TAG_SPARSE_S | RSX_TAG_SPARSE_R | RSX_TAG_ZERO;
+    return spmm_dispatch(A, x, d, e, st.slab, s);
 }
 
 }  // namespace rsx
@@ -212,8 +295,20 @@ int rsx_lightgcn_step(const rsx_lgcn_step* st, rsx_stream_t stream) {
         if ((rc = sample_call(sa, st->batch, st->triplets, s))) return rc;
         batch = (sa.n_inter - sa.start) < st->batch ? (sa.n_inter - sa.start) : st->batch;
     }
-    // forward (last layer zeroes g and r)
-    if ((rc = lgcn_forward(A, d, K, st->p, st->s, st->h0, st->h1, st->final_emb, st->slab, st->g, st->r, s)))
+    // batch-row tags (K >= 2): last forward layer on the batch rows only, sparse G in
+    // the first backward layer, G / R cleared on the batch rows by the Adam layer
+    const bool tags = st->row_tag && K >= 2;
+    const int32_t tag = (int32_t)st->tag;
+    if (tags) {
+        if (st->tag <= 0 || st->tag > INT32_MAX) return RSX_ERR_ARG;
+        hipLaunchKernelGGL(tag_rows_kernel, dim3((unsigned)((3 * batch + 255) / 256)), dim3(256), 0, s, st->triplets,
+                           batch, st->n_users, st->row_tag, tag);
+        if ((rc = last_rc())) return rc;
+    }
+    if (tags && K <= 3) return lgcn_step_stored_layers(*st, batch, tag, s);
+    // forward (dense path: the last layer zeroes g and r)
+    if ((rc = lgcn_forward(A, d, K, st->p, st->s, st->h0, st->h1, st->final_emb, st->slab, tags ? nullptr : st->g,
+                           tags ? nullptr : st->r, s, tags ? st->row_tag : nullptr, tag)))
         return rc;
     // BPR loss + gradients
     if ((rc = bpr_call(RSX_BPR_LIGHTGCN, st->final_emb, st->p, st->n_users, st->n_items, d, st->triplets, batch,
@@ -244,11 +339,23 @@ int rsx_lightgcn_step(const rsx_lgcn_step* st, rsx_stream_t stream) {
             e.m = st->m;
             e.v = st->v;
             e.adam = st->adam;
+            if (tags) {  // K >= 2: nothing reads G or R after this layer
+                e.row_tag = st->row_tag;
+                e.tag = tag;
+                e.tag_flags = RSX_TAG_SPARSE_R | RSX_TAG_ZERO;
+                e.zero0 = st->g;
+                e.zero1 = st->r;
+            }
         } else {
             e = epi0(RSX_EPI_LAYERSUM);
             e.y = bufs[(k - 1) & 1];
             e.s_in = (k == 1) ? st->g : st->s;
             e.s_out = st->s;
+            if (tags && k == 1) {  // X = G and s_in = G: zero off the batch rows
+                e.row_tag = st->row_tag;
+                e.tag = tag;
+                e.tag_flags = RSX_TAG_SPARSE_X | RSX_TAG_SPARSE_S;
+            }
         }
         if ((rc = spmm_dispatch(A, x, d, e, st->slab, s))) return rc;
         x = bufs[(k - 1) & 1];

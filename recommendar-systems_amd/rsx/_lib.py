@@ -50,7 +50,14 @@ class Epilogue(C.Structure):
     _fields_ = [("kind", I32), ("pad0", I32), ("alpha", F32), ("beta", F32),
                 ("y", P), ("s_in", P), ("s_out", P), ("f", P), ("zero0", P), ("zero1", P), ("r_add", P),
                 ("p", P), ("m", P), ("v", P), ("g_out", P), ("e0", P), ("aux", P), ("aux_w", P),
-                ("adam", Adam)]
+                ("adam", Adam), ("row_tag", P), ("tag", I32), ("tag_flags", I32)]
+
+
+RSX_TAG_ROWS = 1
+RSX_TAG_SPARSE_X = 2
+RSX_TAG_SPARSE_S = 4
+RSX_TAG_SPARSE_R = 8
+RSX_TAG_ZERO = 16
 
 
 class SamplerArgs(C.Structure):
@@ -63,7 +70,8 @@ class LgcnStep(C.Structure):
                 ("reg", F32), ("pad0", I32),
                 ("p", P), ("m", P), ("v", P), ("s", P), ("h0", P), ("h1", P), ("final_emb", P), ("g", P),
                 ("r", P), ("slab", P), ("triplets", P), ("batch", I64), ("sample", C.POINTER(SamplerArgs)),
-                ("adam", Adam), ("loss_out", P), ("loss_acc", P), ("ws", P), ("ws_bytes", C.c_size_t)]
+                ("adam", Adam), ("loss_out", P), ("loss_acc", P), ("ws", P), ("ws_bytes", C.c_size_t),
+                ("row_tag", P), ("tag", I64)]
 
 
 class ShardedStep(C.Structure):

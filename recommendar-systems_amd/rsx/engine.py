@@ -12,6 +12,7 @@ src/common/trainer.py:196-200).
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import numpy as np
 import torch
@@ -54,6 +55,10 @@ class LightGCNEngine:
         self.trip = torch.zeros(3, self.batch, dtype=torch.int64, device=dev)
         self.epoch_trip = torch.zeros(3 * self.n_inter, dtype=torch.int64, device=dev)
         self._epoch_sampled = None
+        # batch-row tags (rsx_lgcn_step.row_tag): last forward layer on the batch rows,
+        # sparse G in the first backward layer; RSX_BATCH_TAGS=0 selects the dense path
+        self.row_tag = torch.zeros(n, dtype=torch.int32, device=dev)
+        self.use_tags = self.K >= 2 and os.environ.get("RSX_BATCH_TAGS", "1") != "0"
         self._st = L.LgcnStep()
         self._sa = L.SamplerArgs()
         self._fill_static()
@@ -80,6 +85,7 @@ class LightGCNEngine:
         st.loss_out = self.loss_out.data_ptr()
         st.loss_acc = self.loss_acc.data_ptr()
         st.ws, st.ws_bytes = self.ws.data_ptr(), self.ws.numel()
+        st.row_tag = self.row_tag.data_ptr() if self.use_tags else None
 
     def set_lr(self, lr: float):
         self.lr = float(lr)
@@ -90,6 +96,7 @@ class LightGCNEngine:
         st = self._st
         self.step_count += 1
         st.adam = ops.adam_struct(self.lr, self.step_count, weight_decay=self.wd)
+        st.tag = self.step_count  # fresh per step, > 0
         if triplets is not None:
             t = triplets[:3].contiguous()
             if t.shape[1] > self.batch:

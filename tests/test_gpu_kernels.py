@@ -362,3 +362,41 @@ def test_device_edge_dropout_graph_equals_host_builder(cuda, seed):
         x = torch.randn(nu + ni, 64, device=cuda)
         ref = torch.sparse_csr_tensor(A.rowptr, A.col.long(), A.val, (nu + ni, nu + ni)).to_dense() @ x
         assert torch.allclose(A.spmm(x), ref, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("K", [2, 3])
+def test_batch_row_tags_equal_dense_step(cuda, K):
+    """rsx_lgcn_step.row_tag (last forward layer on the batch rows, sparse G, G/R
+    cleared on the batch rows) gives the dense path's parameters and losses on a
+    power-law graph with hub rows; G and R are all-zero between tagged steps."""
+    from rsx import synth
+    from rsx.engine import LightGCNEngine
+
+    df = synth.amazon_like(3000, 800, 30000, seed=3)
+    tr = df[df.x_label == 0]
+    tu, ti = tr.userID.values.astype(np.int64), tr.itemID.values.astype(np.int64)
+    nu, ni = int(df.userID.max()) + 1, 800
+    torch.manual_seed(5)
+    U0 = torch.nn.init.xavier_uniform_(torch.empty(nu, 64)).numpy()
+    I0 = torch.nn.init.xavier_uniform_(torch.empty(ni, 64)).numpy()
+    engs = []
+    for tags in (True, False):
+        e = LightGCNEngine(tu, ti, nu, ni, 64, K, 1e-2, 1e-3, cuda, U0, I0, seed=0, batch=512)
+        e.use_tags = tags
+        e._fill_static()
+        engs.append(e)
+    assert engs[0].adj.n_long > 0  # hub rows split over several work items
+    for s in range(0, 3 * 512, 512):
+        for e in engs:
+            e.step(epoch=0, start=s)
+    torch.cuda.synchronize()
+    a, b = engs
+    assert torch.count_nonzero(a.g).item() == 0 and torch.count_nonzero(a.r).item() == 0
+    np.testing.assert_allclose(a.loss_acc.item(), b.loss_acc.item(), rtol=1e-9)
+    for name in ("p", "m", "v"):
+        np.testing.assert_allclose(getattr(a, name).cpu().numpy(), getattr(b, name).cpu().numpy(), rtol=0,
+                                   atol=1e-6, err_msg=name)
+    # the forward for evaluation (dense) is unaffected
+    a.invalidate()
+    b.invalidate()
+    np.testing.assert_allclose(a.forward().cpu().numpy(), b.forward().cpu().numpy(), rtol=0, atol=1e-6)

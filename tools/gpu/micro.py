@@ -61,6 +61,31 @@ def main(what):
             xd = torch.randn(n, d, device=dev)
             yd = torch.empty_like(xd)
             out[f"spmmx_real_d{d}_us"] = round(t_ms(lambda: A.spmm(xd, out=yd), 100) * 1e3, 2)
+    if what == "floor":
+        # what one SpMM layer costs beyond the work: launch, a plain 13.8 MB write, the
+        # epilogues alone (rowwise), empty-graph and real launches per epilogue kind
+        from rsx import _lib as L
+        x = torch.randn(n, 64, device=dev)
+        y = torch.empty_like(x)
+        tabs = {k: torch.randn(n, 64, device=dev).abs() * 0.01 for k in ("p", "m", "v", "g", "r")}
+        tiny = torch.empty(1, device=dev)
+        out["launch_only_us"] = round(t_ms(lambda: tiny.zero_(), 200) * 1e3, 2)
+        out["write_13.8MB_us"] = round(t_ms(lambda: y.zero_(), 200) * 1e3, 2)
+        out["copy_13.8MB_us"] = round(t_ms(lambda: y.copy_(x), 200) * 1e3, 2)
+        A = ops.DeviceCSR(rp, col, val, n, dev, 32)
+        E = ops.DeviceCSR(np.zeros_like(rp), col[:0], val[:0], n, dev, 32)
+        adam = ops.adam_struct(1e-3, 5)
+        kinds = {
+            "store": lambda: ops.epi(L.RSX_EPI_STORE, y=y),
+            "add_sparse": lambda: ops.epi(L.RSX_EPI_ADD, y=y, s_in=tabs["g"]),
+            "adam": lambda: ops.epi(L.RSX_EPI_ADAM, adam=adam, s_in=tabs["g"], r_add=tabs["r"], p=tabs["p"],
+                                    m=tabs["m"], v=tabs["v"]),
+        }
+        for name, mk in kinds.items():
+            e = mk()
+            out[f"{name}_rowwise_us"] = round(t_ms(lambda: ops.rowwise(n, 64, e), 100) * 1e3, 2)
+            out[f"{name}_empty_us"] = round(t_ms(lambda: E.spmm_epi(x, e, 64), 100) * 1e3, 2)
+            out[f"{name}_real_us"] = round(t_ms(lambda: A.spmm_epi(x, e, 64), 100) * 1e3, 2)
     if what == "metrics":
         g = np.random.default_rng(1)
         nu_e, k = 35598, 50
