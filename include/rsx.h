@@ -447,6 +447,12 @@ size_t rsx_comm_unique_id_bytes(void);
 int rsx_comm_get_unique_id(void* id_host);
 int rsx_comm_init(rsx_comm_t* out, const void* id_host, int32_t rank, int32_t world);
 int rsx_comm_destroy(rsx_comm_t comm);
+/* Test hook: a communicator whose exchanges call `fn(buf, n, ctx)` on the host
+ * (after synchronising the caller's stream) instead of RCCL — lets a host-side
+ * collective (e.g. torch gloo) drive the sharded step with several ranks on one
+ * GPU.  `fn` returns 0 on success. */
+typedef int (*rsx_host_allreduce_fn)(float* buf, int64_t n, void* ctx);
+int rsx_comm_init_host(rsx_comm_t* out, int32_t rank, int32_t world, rsx_host_allreduce_fn fn, void* ctx);
 /* buf[0, n) := sum over ranks, in place, ordered after the work queued on `stream`
  * and before the work queued on it afterwards. */
 int rsx_comm_allreduce_f32(rsx_comm_t comm, float* buf, int64_t n, rsx_stream_t stream);
@@ -463,7 +469,12 @@ int rsx_comm_allreduce_f32(rsx_comm_t comm, float* buf, int64_t n, rsx_stream_t 
  * n_items*d floats: the forward's item partials of layers 1..K, G's item rows,
  * the backward's layers 1..K-1, and the item gradient t.  Item Adam then runs
  * identically on every rank (its inputs are bit-identical after the sums), user
- * Adam locally.  The loss is this rank's mean BPR + its regulariser; the
+ * Adam locally.  With `row_tag` ([n_users + n_items] int32, zero-filled before
+ * the first step, `tag` fresh per step as in rsx_lgcn_step) and K = 2 or 3 the
+ * step keeps the layers instead of running sums, computes the last user layer on
+ * the batch rows only and runs the backward as Horner on G/(K+1) (2K SpMM
+ * launches and one item-Adam launch per step, no layer-sum passes); G and R must
+ * then be zero between steps.  The loss is this rank's mean BPR + its regulariser; the
  * objective is the sum over ranks (data-parallel batches of `batch` per rank).
  * rsx_sharded_lightgcn_forward fills final_emb only (evaluation).
  */
@@ -486,6 +497,8 @@ typedef struct rsx_sharded_lgcn_step {
     double* loss_acc;           /* [1] or NULL */
     void* ws; size_t ws_bytes;  /* >= rsx_bpr_ws_bytes(batch) */
     rsx_comm_t comm;
+    int32_t* row_tag;           /* optional, see above */
+    int64_t tag;
 } rsx_sharded_lgcn_step;
 
 int rsx_sharded_lightgcn_step(const rsx_sharded_lgcn_step* st, rsx_stream_t stream);

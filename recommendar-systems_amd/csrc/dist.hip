@@ -33,6 +33,7 @@ int rowwise_dispatch(int64_t n, int d, const rsx_epilogue& e, hipStream_t s);
 int bpr_call(int32_t variant, const float* fin, const float* ego, int64_t n_users, int64_t n_items, int32_t d,
              const int64_t* trip, int64_t batch, float reg, float batch_cfg, float* g_fin, float* g_ego,
              float* loss_out, double* loss_acc, void* ws, size_t ws_bytes, hipStream_t s, float g_div = 1.f);
+int tag_rows(const int64_t* trip, int64_t batch, int64_t n_users, int32_t* row_tag, int32_t tag, hipStream_t s);
 
 namespace {
 
@@ -41,6 +42,8 @@ struct Rccl {
     decltype(&ncclCommInitRank) init_rank = nullptr;
     decltype(&ncclCommDestroy) destroy = nullptr;
     decltype(&ncclAllReduce) all_reduce = nullptr;
+    decltype(&ncclGroupStart) group_start = nullptr;
+    decltype(&ncclGroupEnd) group_end = nullptr;
     bool ok = false;
 };
 
@@ -55,7 +58,9 @@ const Rccl& rccl() {
         x.init_rank = reinterpret_cast<decltype(&ncclCommInitRank)>(dlsym(h, "ncclCommInitRank"));
         x.destroy = reinterpret_cast<decltype(&ncclCommDestroy)>(dlsym(h, "ncclCommDestroy"));
         x.all_reduce = reinterpret_cast<decltype(&ncclAllReduce)>(dlsym(h, "ncclAllReduce"));
-        x.ok = x.get_unique_id && x.init_rank && x.destroy && x.all_reduce;
+        x.group_start = reinterpret_cast<decltype(&ncclGroupStart)>(dlsym(h, "ncclGroupStart"));
+        x.group_end = reinterpret_cast<decltype(&ncclGroupEnd)>(dlsym(h, "ncclGroupEnd"));
+        x.ok = x.get_unique_id && x.init_rank && x.destroy && x.all_reduce && x.group_start && x.group_end;
         return x;
     }();
     return r;
@@ -74,32 +79,62 @@ struct rsx_comm_s {
     hipEvent_t join[rsx::kJoinEvents] = {};
     int next = 0;
     int32_t rank = 0, world = 1;
+    rsx_host_allreduce_fn host_fn = nullptr;  // test hook: host-side collective instead of RCCL
+    void* host_ctx = nullptr;
 };
 
 namespace rsx {
 namespace {
 
-// In-place sum of buf[0, n) over the communicator, after the work queued so far on
-// `s`; returns the join event the reader must wait on (nullptr on error, rc set).
-hipEvent_t exchange(rsx_comm_t c, float* buf, int64_t n, hipStream_t s, int* rc) {
+// In-place sums of a[0, n) (and b[0, n) when b != nullptr, one RCCL group) over the
+// communicator, after the work queued so far on `s`; returns the join event the
+// reader must wait on (nullptr on error, rc set).  A host-hook communicator
+// synchronises `s`, calls the hook per buffer and returns an event on `s`.
+hipEvent_t exchange(rsx_comm_t c, float* a, float* b, int64_t n, hipStream_t s, int* rc) {
     hipError_t e;
+    hipEvent_t j = c->join[c->next];
+    c->next = (c->next + 1) % kJoinEvents;
+    if (c->host_fn) {
+        if ((e = hipStreamSynchronize(s)) != hipSuccess) {
+            *rc = hip_rc(e);
+            return nullptr;
+        }
+        if (c->host_fn(a, n, c->host_ctx) || (b && c->host_fn(b, n, c->host_ctx))) {
+            *rc = RSX_ERR_COMM;
+            return nullptr;
+        }
+        if ((e = hipEventRecord(j, s)) != hipSuccess) {
+            *rc = hip_rc(e);
+            return nullptr;
+        }
+        return j;
+    }
     if ((e = hipEventRecord(c->fork, s)) != hipSuccess || (e = hipStreamWaitEvent(c->stream, c->fork, 0)) != hipSuccess) {
         *rc = hip_rc(e);
         return nullptr;
     }
-    const ncclResult_t r = rccl().all_reduce(buf, buf, (size_t)n, ncclFloat32, ncclSum, c->nccl, c->stream);
-    if (r != ncclSuccess) {
+    const Rccl& r = rccl();
+    ncclResult_t nr = ncclSuccess;
+    if (b) {
+        nr = r.group_start();
+        if (nr == ncclSuccess) nr = r.all_reduce(a, a, (size_t)n, ncclFloat32, ncclSum, c->nccl, c->stream);
+        if (nr == ncclSuccess) nr = r.all_reduce(b, b, (size_t)n, ncclFloat32, ncclSum, c->nccl, c->stream);
+        const ncclResult_t ge = r.group_end();
+        if (nr == ncclSuccess) nr = ge;
+    } else {
+        nr = r.all_reduce(a, a, (size_t)n, ncclFloat32, ncclSum, c->nccl, c->stream);
+    }
+    if (nr != ncclSuccess) {
         *rc = RSX_ERR_COMM;
         return nullptr;
     }
-    hipEvent_t j = c->join[c->next];
-    c->next = (c->next + 1) % kJoinEvents;
     if ((e = hipEventRecord(j, c->stream)) != hipSuccess) {
         *rc = hip_rc(e);
         return nullptr;
     }
     return j;
 }
+hipEvent_t exchange(rsx_comm_t c, float* a, int64_t n, hipStream_t s, int* rc) { return exchange(c, a, nullptr, n, s, rc); }
 
 int wait(hipStream_t s, hipEvent_t j) { return hip_rc(hipStreamWaitEvent(s, j, 0)); }
 
@@ -174,6 +209,133 @@ int sharded_forward(const rsx_sharded_lgcn_step& st, bool zero_grads, hipStream_
     return 0;
 }
 
+// Stored-layer step for K = 2, 3 (the sharded twin of step.hip's
+// lgcn_step_stored_layers).  Forward: E^k user rows local, item rows = the sum of
+// the ranks' partials (one exchange per layer); the last layer writes the mean
+// directly: on rank 0 the item partial's epilogue adds the (already summed)
+// E^0..E^{K-1} item rows, so one exchange of the final item rows gives the mean
+// (scaled by 1/(K+1) before the sum), and the user rows' mean is computed on the
+// batch rows only.  Backward: Horner on G' = dL/dfinal / (K+1) (BPR's g_div),
+//   H^k = G' + A H^{k-1},  H^0 = G',  Adam on g = H^K + R,
+// with G', R's item rows summed once (one grouped exchange) and added to the item
+// partials by rank 0 only; the last item partial carries G' + R so one exchange
+// gives the whole item gradient.  2K+1 exchanges of n_items*d floats per step
+// (the first a group of two), 2K SpMM launches + 1 item Adam launch, no layer-sum
+// passes.  `train` false: forward only, every final row (evaluation).
+int sharded_stored_layers(const rsx_sharded_lgcn_step& st, bool train, hipStream_t s) {
+    const int d = st.d, K = st.n_layers;
+    const int64_t nu = st.n_users, ni = st.n_items, off = nu * (int64_t)d;
+    const bool root = st.comm->rank == 0;
+    const float beta = 1.f / (float)(K + 1);
+    const int32_t tag = (int32_t)st.tag;
+    float* bufs[2] = {st.h0, st.h1};
+    hipEvent_t joins[4] = {};
+    int rc = 0;
+    if (train) RSX_TRY(tag_rows(st.triplets, st.batch, nu, st.row_tag, tag, s));
+    // ---- forward
+    const float* x = st.p;
+    for (int k = 1; k < K; ++k) {
+        rsx_epilogue e = epi(RSX_EPI_STORE);
+        e.y = bufs[k - 1] + off;
+        RSX_TRY(spmm_dispatch(*st.adj_i, x, d, e, st.slab_i, s));   // item partial of E^k
+        if (!(joins[k] = exchange(st.comm, bufs[k - 1] + off, ni * d, s, &rc))) return rc;
+        if (k >= 2) RSX_TRY(wait(s, joins[k - 1]));                  // E^{k-1} items summed
+        e.y = bufs[k - 1];
+        RSX_TRY(spmm_dispatch(*st.adj_u, x, d, e, st.slab_u, s));   // E^k user rows
+        x = bufs[k - 1];
+    }
+    RSX_TRY(wait(s, joins[K - 1]));
+    {
+        rsx_epilogue e = epi(RSX_EPI_FINAL);
+        e.beta = beta;
+        e.f = st.final_emb + off;
+        if (root) {
+            e.s_in = st.p + off;
+            e.r_add = st.h0 + off;
+            e.aux = K == 3 ? st.h1 + off : nullptr;
+        }
+        RSX_TRY(spmm_dispatch(*st.adj_i, x, d, e, st.slab_i, s));
+        if (!(joins[K] = exchange(st.comm, st.final_emb + off, ni * d, s, &rc))) return rc;
+        e.f = st.final_emb;
+        e.s_in = st.p;
+        e.r_add = st.h0;
+        e.aux = K == 3 ? st.h1 : nullptr;
+        if (train) {
+            e.row_tag = st.row_tag;
+            e.tag = tag;
+            e.tag_flags = RSX_TAG_ROWS;
+        }
+        RSX_TRY(spmm_dispatch(*st.adj_u, x, d, e, st.slab_u, s));
+        RSX_TRY(wait(s, joins[K]));
+    }
+    if (!train) return 0;
+    // ---- loss: G' = dL/dfinal / (K+1), R = d reg / d ego on this rank's batch rows
+    RSX_TRY(bpr_call(RSX_BPR_LIGHTGCN, st.final_emb, st.p, nu, ni, d, st.triplets, st.batch, st.reg,
+                     (float)st.batch, st.g, st.r, st.loss_out, st.loss_acc, st.ws, st.ws_bytes, s, (float)(K + 1)));
+    hipEvent_t j0 = exchange(st.comm, st.g + off, st.r + off, ni * d, s, &rc);  // G'_I, R_I summed
+    if (!j0) return rc;
+    RSX_TRY(wait(s, j0));
+    // ---- backward
+    x = st.g;
+    for (int k = 1; k < K; ++k) {
+        rsx_epilogue e = epi(RSX_EPI_ADD);
+        e.y = bufs[k - 1] + off;
+        if (root) e.s_in = st.g + off;  // + G'_I once
+        if (k == 1) {                   // X = G': only this rank's batch users are nonzero
+            e.row_tag = st.row_tag;
+            e.tag = tag;
+            e.tag_flags = RSX_TAG_SPARSE_X;
+        }
+        RSX_TRY(spmm_dispatch(*st.adj_i, x, d, e, st.slab_i, s));
+        if (!(joins[k] = exchange(st.comm, bufs[k - 1] + off, ni * d, s, &rc))) return rc;
+        if (k >= 2) RSX_TRY(wait(s, joins[k - 1]));
+        rsx_epilogue u = epi(RSX_EPI_ADD);  // H^k users = G'_U + A_U H^{k-1}_I (G'_U on batch users only)
+        u.y = bufs[k - 1];
+        u.s_in = st.g;
+        u.row_tag = st.row_tag;
+        u.tag = tag;
+        u.tag_flags = RSX_TAG_SPARSE_S;
+        RSX_TRY(spmm_dispatch(*st.adj_u, x, d, u, st.slab_u, s));
+        x = bufs[k - 1];
+    }
+    {
+        rsx_epilogue e = epi(RSX_EPI_ADD);  // item gradient partial: A_I H^{K-1}_U (+ G'_I + R_I on rank 0)
+        e.y = st.t;
+        if (root) {
+            e.s_in = st.g + off;
+            e.r_add = st.r + off;
+        }
+        RSX_TRY(spmm_dispatch(*st.adj_i, x, d, e, st.slab_i, s));
+        hipEvent_t jt = exchange(st.comm, st.t, ni * d, s, &rc);
+        if (!jt) return rc;
+        if (K >= 2) RSX_TRY(wait(s, joins[K - 1]));
+        rsx_epilogue u = epi(RSX_EPI_ADAM);  // user rows: g = (G'_U + A_U H^{K-1}_I) + R_U
+        u.s_in = st.g;
+        u.r_add = st.r;
+        u.p = st.p;
+        u.m = st.m;
+        u.v = st.v;
+        u.adam = st.adam;
+        u.zero0 = st.g;  // G'_U, R_U cleared on the batch users (nothing reads them later)
+        u.zero1 = st.r;
+        u.row_tag = st.row_tag;
+        u.tag = tag;
+        u.tag_flags = RSX_TAG_SPARSE_S | RSX_TAG_SPARSE_R | RSX_TAG_ZERO;
+        RSX_TRY(spmm_dispatch(*st.adj_u, x, d, u, st.slab_u, s));
+        RSX_TRY(wait(s, jt));
+        rsx_epilogue a = epi(RSX_EPI_ADAM);  // item rows, identical on every rank
+        a.s_in = st.t;
+        a.p = st.p + off;
+        a.m = st.m + off;
+        a.v = st.v + off;
+        a.adam = st.adam;
+        a.zero0 = st.g + off;  // the summed G'_I, R_I: cleared densely
+        a.zero1 = st.r + off;
+        RSX_TRY(rowwise_dispatch(ni, d, a, s));
+    }
+    return 0;
+}
+
 bool valid(const rsx_sharded_lgcn_step* st) {
     if (!st || !st->adj_u || !st->adj_i || !st->comm || !st->p || !st->final_emb || st->n_layers < 1 ||
         st->n_layers > 30 || st->n_users < 0 || st->n_items <= 0)
@@ -227,6 +389,24 @@ int rsx_comm_init(rsx_comm_t* out, const void* id_host, int32_t rank, int32_t wo
     return RSX_OK;
 }
 
+int rsx_comm_init_host(rsx_comm_t* out, int32_t rank, int32_t world, rsx_host_allreduce_fn fn, void* ctx) {
+    if (!out || !fn || world < 1 || rank < 0 || rank >= world) return RSX_ERR_ARG;
+    rsx_comm_s* c = new rsx_comm_s();
+    c->rank = rank;
+    c->world = world;
+    c->host_fn = fn;
+    c->host_ctx = ctx;
+    hipError_t e = hipSuccess;
+    for (int i = 0; e == hipSuccess && i < rsx::kJoinEvents; ++i)
+        e = hipEventCreateWithFlags(&c->join[i], hipEventDisableTiming);
+    if (e != hipSuccess) {
+        rsx_comm_destroy(c);
+        return rsx::hip_rc(e);
+    }
+    *out = c;
+    return RSX_OK;
+}
+
 int rsx_comm_destroy(rsx_comm_t c) {
     if (!c) return RSX_OK;
     if (c->stream) (void)hipStreamSynchronize(c->stream);
@@ -250,6 +430,8 @@ int rsx_comm_allreduce_f32(rsx_comm_t c, float* buf, int64_t n, rsx_stream_t str
 
 int rsx_sharded_lightgcn_forward(const rsx_sharded_lgcn_step* st, rsx_stream_t stream) {
     if (!rsx::valid(st)) return RSX_ERR_ARG;
+    if (st->row_tag && (st->n_layers == 2 || st->n_layers == 3))
+        return rsx::sharded_stored_layers(*st, false, rsx::as_stream(stream));
     return rsx::sharded_forward(*st, false, rsx::as_stream(stream));
 }
 
@@ -259,6 +441,10 @@ int rsx_sharded_lightgcn_step(const rsx_sharded_lgcn_step* st, rsx_stream_t stre
         return RSX_ERR_ARG;
     hipStream_t s = as_stream(stream);
     const int d = st->d, K = st->n_layers;
+    if (st->row_tag && (K == 2 || K == 3)) {
+        if (st->tag <= 0 || st->tag > INT32_MAX) return RSX_ERR_ARG;
+        return sharded_stored_layers(*st, true, s);
+    }
     const int64_t nu = st->n_users, ni = st->n_items, off = nu * (int64_t)d;
     const float beta = 1.f / (float)(K + 1);
     RSX_TRY(sharded_forward(*st, true, s));

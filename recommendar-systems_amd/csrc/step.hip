@@ -119,6 +119,13 @@ __global__ __launch_bounds__(256) void tag_rows_kernel(const int64_t* __restrict
     row_tag[t < batch ? id : n_users + id] = tag;
 }
 
+int tag_rows(const int64_t* trip, int64_t batch, int64_t n_users, int32_t* row_tag, int32_t tag, hipStream_t s) {
+    if (batch <= 0) return 0;
+    hipLaunchKernelGGL(tag_rows_kernel, dim3((unsigned)((3 * batch + 255) / 256)), dim3(256), 0, s, trip, batch,
+                       n_users, row_tag, tag);
+    return last_rc();
+}
+
 static rsx_epilogue epi0(int kind) {
     rsx_epilogue e = {};
     e.kind = kind;
@@ -301,9 +308,7 @@ int rsx_lightgcn_step(const rsx_lgcn_step* st, rsx_stream_t stream) {
     const int32_t tag = (int32_t)st->tag;
     if (tags) {
         if (st->tag <= 0 || st->tag > INT32_MAX) return RSX_ERR_ARG;
-        hipLaunchKernelGGL(tag_rows_kernel, dim3((unsigned)((3 * batch + 255) / 256)), dim3(256), 0, s, st->triplets,
-                           batch, st->n_users, st->row_tag, tag);
-        if ((rc = last_rc())) return rc;
+        if ((rc = tag_rows(st->triplets, batch, st->n_users, st->row_tag, tag, s))) return rc;
     }
     if (tags && K <= 3) return lgcn_step_stored_layers(*st, batch, tag, s);
     // forward (dense path: the last layer zeroes g and r)

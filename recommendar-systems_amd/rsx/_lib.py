@@ -80,7 +80,10 @@ class ShardedStep(C.Structure):
                 ("p", P), ("m", P), ("v", P), ("s", P), ("h0", P), ("h1", P), ("final_emb", P), ("g", P),
                 ("r", P), ("t", P), ("slab_u", P), ("slab_i", P), ("triplets", P), ("batch", I64),
                 ("adam", Adam), ("loss_out", P), ("loss_acc", P), ("ws", P), ("ws_bytes", C.c_size_t),
-                ("comm", P)]
+                ("comm", P), ("row_tag", P), ("tag", I64)]
+
+
+HOST_ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, P, I64, P)
 
 
 _LIB = None
@@ -116,6 +119,7 @@ def _declare(lib):
         "rsx_comm_get_unique_id": (C.c_int, [P]),
         "rsx_comm_init": (C.c_int, [C.POINTER(P), P, I32, I32]),
         "rsx_comm_destroy": (C.c_int, [P]),
+        "rsx_comm_init_host": (C.c_int, [C.POINTER(P), I32, I32, HOST_ALLREDUCE_FN, P]),
         "rsx_comm_allreduce_f32": (C.c_int, [P, P, I64, P]),
         "rsx_sharded_lightgcn_step": (C.c_int, [C.POINTER(ShardedStep), P]),
         "rsx_sharded_lightgcn_forward": (C.c_int, [C.POINTER(ShardedStep), P]),
@@ -134,6 +138,7 @@ EXPORTED = ["rsx_version", "rsx_csr_schedule_host", "rsx_spmm", "rsx_rowwise", "
             "rsx_smore_spectral_bwd_partials",
             "rsx_topk_metrics_ws_bytes", "rsx_topk_metrics", "rsx_linear_wgrad_ws_bytes", "rsx_linear_wgrad",
             "rsx_comm_unique_id_bytes", "rsx_comm_get_unique_id", "rsx_comm_init", "rsx_comm_destroy",
+            "rsx_comm_init_host",
             "rsx_comm_allreduce_f32", "rsx_sharded_lightgcn_step", "rsx_sharded_lightgcn_forward"]
 
 

@@ -40,7 +40,13 @@ created by the unique-id handshake over this process group).  Issued from
 Python, the ~20 launches + 7 collectives of a step cost more host time than the
 device needs for them (0.46 ms/step vs 0.16 ms at N=1, bench --sharded); the
 Python sequence remains the statement the gloo tests check and the fallback
-when `native=False`.
+when `native=False`.  For K = 2, 3 the native step is the stored-layer form
+(csrc/dist.hip:sharded_stored_layers): no layer-sum passes, the last user layer
+on the batch rows only, the backward as Horner on G/(K+1) with rank 0 adding the
+summed G'_I (+ R_I) into its item partials — 2K SpMM launches + one item Adam
+per step instead of 2K SpMMs + 2K row-block sums.  With a non-RCCL group
+(gloo, tests) the native step's exchanges go through a host hook
+(`rsx_comm_init_host`) so several ranks can share one GPU.
 """
 from __future__ import annotations
 
@@ -139,6 +145,10 @@ class ShardedLightGCNEngine:
         self._epoch_buf = None
         self._epoch_sampled = None
         self._fwd_valid = False
+        # batch-row tags (rsx_sharded_lgcn_step.row_tag): the stored-layer step for K = 2, 3
+        self.row_tag = None
+        if isinstance(self.be, HipBackend) and self.K in (2, 3):
+            self.row_tag = torch.zeros(n, dtype=torch.int32, device=self.be.device)
         if native is None:
             native = isinstance(self.be, HipBackend) and dist.get_backend(self.group) == "nccl"
         self.native = bool(native)
@@ -147,20 +157,43 @@ class ShardedLightGCNEngine:
             if not isinstance(self.be, HipBackend):
                 raise RuntimeError("the native sharded step needs the HIP backend")
             self._init_native()
+        elif self.row_tag is not None and self.K in (2, 3):
+            self.row_tag = None  # the Python-issued sequence keeps the running sums
 
     # ------------------------------------------------------------ native step
     def _init_native(self):
-        """RCCL communicator of this process group for csrc/dist.hip (unique-id handshake)."""
+        """Communicator for csrc/dist.hip: RCCL over this process group ("nccl": unique-id
+        handshake), or — any other backend, tests — the host hook driving this group's
+        all_reduce on host copies of the exchanged rows."""
         lib = L.lib()
-        nb = int(lib.rsx_comm_unique_id_bytes())
-        buf = (C.c_uint8 * nb)()
-        if self.rank == 0:
-            L.check(lib.rsx_comm_get_unique_id(buf), "rsx_comm_get_unique_id")
-        uid = self._broadcast_host(torch.tensor(bytearray(bytes(buf)), dtype=torch.uint8))
-        C.memmove(buf, bytes(uid.numpy().tobytes()), nb)
         comm = C.c_void_p()
-        with torch.cuda.device(self.be.device):
-            L.check(lib.rsx_comm_init(C.byref(comm), buf, self.rank, self.world), "rsx_comm_init")
+        if dist.get_backend(self.group) == "nccl":
+            nb = int(lib.rsx_comm_unique_id_bytes())
+            buf = (C.c_uint8 * nb)()
+            if self.rank == 0:
+                L.check(lib.rsx_comm_get_unique_id(buf), "rsx_comm_get_unique_id")
+            uid = self._broadcast_host(torch.tensor(bytearray(bytes(buf)), dtype=torch.uint8))
+            C.memmove(buf, bytes(uid.numpy().tobytes()), nb)
+            with torch.cuda.device(self.be.device):
+                L.check(lib.rsx_comm_init(C.byref(comm), buf, self.rank, self.world), "rsx_comm_init")
+        else:
+            nu = self.n_users
+            views = [self.t] + [getattr(self, k)[nu:] for k in ("h0", "h1", "final", "g", "r")]
+            self._views = {(v.data_ptr(), v.numel()): v for v in views}
+
+            def host_allreduce(ptr, n, _ctx):
+                try:
+                    v = self._views[(ptr, n)]
+                    x = v.cpu()
+                    dist.all_reduce(x, group=self.group)
+                    v.copy_(x)
+                    return 0
+                except Exception:  # noqa: BLE001
+                    return 1
+
+            self._host_cb = L.HOST_ALLREDUCE_FN(host_allreduce)  # kept alive with the engine
+            L.check(lib.rsx_comm_init_host(C.byref(comm), self.rank, self.world, self._host_cb, None),
+                    "rsx_comm_init_host")
         self._comm = comm
         st = self._st = L.ShardedStep()
         st.adj_u = C.pointer(self.A_U.struct)
@@ -178,6 +211,7 @@ class ShardedLightGCNEngine:
         self.ws = torch.empty(lib.rsx_bpr_ws_bytes(max(self.batch, 1)), dtype=torch.uint8, device=self.be.device)
         st.ws, st.ws_bytes = self.ws.data_ptr(), self.ws.numel()
         st.comm = comm.value
+        st.row_tag = self.row_tag.data_ptr() if self.row_tag is not None else None
 
     def close(self):
         """Release the rsx communicator (before destroy_process_group)."""
@@ -278,6 +312,7 @@ class ShardedLightGCNEngine:
                 st.ws, st.ws_bytes = self.ws.data_ptr(), self.ws.numel()
             st.triplets, st.batch = t.data_ptr(), t.shape[1]
             st.adam = ops.adam_struct(self.lr, self.step_count, weight_decay=self.wd)
+            st.tag = self.step_count  # fresh per step, > 0
             L.check(L.lib().rsx_sharded_lightgcn_step(C.byref(st), ops._stream()), "rsx_sharded_lightgcn_step")
             self._fwd_valid = False
             return

@@ -17,7 +17,7 @@ from test_dist_gloo import D, K, LR, NI, NU, REG, _local_graph
 pytestmark = pytest.mark.gpu
 
 
-def _worker(rank, world, port, out_dir):
+def _worker(rank, world, port, out_dir, native):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -27,7 +27,9 @@ def _worker(rank, world, port, out_dir):
     I0 = torch.nn.init.xavier_uniform_(torch.empty(NI, D)).numpy() if rank == 0 else np.zeros((NI, D), np.float32)
     U0 = torch.nn.init.xavier_uniform_(torch.empty(NU, D), generator=torch.Generator().manual_seed(rank)).numpy()
     tu, ti, trip = _local_graph(rank)
-    eng = ShardedLightGCNEngine(tu, ti, NU, NI, D, K, REG, LR, "cuda:0", U0, I0, batch=16)
+    # native: csrc/dist.hip's one-call step, its exchanges through the host hook (gloo)
+    eng = ShardedLightGCNEngine(tu, ti, NU, NI, D, K, REG, LR, "cuda:0", U0, I0, batch=16, native=native)
+    assert eng.native == native
     f0 = eng.forward().cpu().clone()
     eng.step(triplets=torch.from_numpy(trip).cuda())
     p1 = eng.p.cpu().numpy()
@@ -48,10 +50,11 @@ def _free_port():
     return p
 
 
-def test_sharded_hip_step_matches_global_objective():
+@pytest.mark.parametrize("native", [False, True])
+def test_sharded_hip_step_matches_global_objective(native):
     world = 2
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(world, _free_port(), d), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, _free_port(), d, native), nprocs=world, join=True)
         res = [dict(np.load(os.path.join(d, f"r{r}.npz"))) for r in range(world)]
     gu, gi, trips = [], [], []
     for r in range(world):
@@ -127,7 +130,8 @@ def _native_worker(rank, world, port, out_dir):
 
 def test_native_sharded_step_equals_python_sequence():
     """csrc/dist.hip's one-call step over an RCCL communicator (one rank here: the box
-    has one GPU) is bit-identical to the Python-issued sequence it restates."""
+    has one GPU) equals the Python-issued sequence it restates: the forward bit for
+    bit, training within 1e-5."""
     with tempfile.TemporaryDirectory() as d:
         mp.spawn(_native_worker, args=(1, _free_port(), d), nprocs=1, join=True)
         z = dict(np.load(os.path.join(d, "native.npz")))
@@ -135,6 +139,8 @@ def test_native_sharded_step_equals_python_sequence():
     # steps the BPR gradient scatter's float atomics (duplicate rows in a batch, as the
     # reference's index_put_) may order differently run to run: 1e-6 absolute
     assert np.array_equal(z["True_0"], z["False_0"])
+    # (the native step keeps the layers and runs Horner on G/(K+1); the Python sequence
+    # keeps running sums: same objective, different rounding order)
     for i in range(1, 5):
-        np.testing.assert_allclose(z[f"True_{i}"], z[f"False_{i}"], rtol=1e-6, atol=1e-6, err_msg=str(i))
+        np.testing.assert_allclose(z[f"True_{i}"], z[f"False_{i}"], rtol=1e-5, atol=1e-5, err_msg=str(i))
     assert np.isfinite(z["True_1"]).all()
