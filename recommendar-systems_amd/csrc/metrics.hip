@@ -8,10 +8,11 @@
 // cutoff with the reference's float64 arithmetic in its order (cumulative sums
 // over ranks 1..k; the gain table 1/log2(r+1) comes from the caller, computed by
 // numpy exactly as the reference does).  Values are written [n_users][M].
-// Kernel 2, one wavefront per column: the column summed over users SEQUENTIALLY in
-// user order — numpy's mean(axis=0) over a C-contiguous [n, k] array adds rows in
-// order — so the sums, and after the caller's division and round(., 4) the metric
-// dict, are bit-identical to the reference's.
+// Kernel 2: every column summed over users SEQUENTIALLY in user order — numpy's
+// mean(axis=0) over a C-contiguous [n, k] array adds rows in order — so the sums,
+// and after the caller's division and round(., 4) the metric dict, are
+// bit-identical to the reference's (metrics_sum_lds: one lane per column, all
+// chains in one wave from LDS tiles; metrics_sum: one wave per column, m > 64).
 #include "rsx_common.hpp"
 
 namespace rsx {
@@ -96,6 +97,62 @@ __global__ __launch_bounds__(64) void metrics_sum(const double* __restrict__ val
     if (lane == 0) out[j] = s;
 }
 
+// All columns at once, one lane per column (m <= 64): every add of a column's
+// serial chain is one v_add_f64 of wave 0 on operands already in LDS, so the m
+// chains advance together and the cost is one dependent add per user, not m.
+// Waves 1-3 stream the next tile of [users][m] values (contiguous in `vals`) into
+// the other LDS buffer meanwhile.  Same order, same bits as metrics_sum.
+constexpr int kSumTileD = 8192;  // doubles per LDS tile (64 KB; two tiles)
+constexpr int kSumThreads = 1024;
+constexpr int kSumLoaders = kSumThreads - kWave;                    // waves 1..15
+constexpr int kSumPer = (kSumTileD + kSumLoaders - 1) / kSumLoaders;  // loads per loader thread, all in flight
+__global__ __launch_bounds__(kSumThreads) void metrics_sum_lds(const double* __restrict__ vals, int64_t n, int m,
+                                                               double* __restrict__ out) {
+    __shared__ double buf[2][kSumTileD];
+    const int upt = kSumTileD / m;  // users per tile
+    const int64_t nt = (n + upt - 1) / upt;
+    const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
+    auto load = [&](int64_t t, double* dst) {  // loader waves: every load issued before any LDS write
+        const int64_t u0 = t * upt;
+        const int64_t cnt = ((n - u0) < upt ? (n - u0) : upt) * (int64_t)m;
+        const double* src = vals + u0 * m;
+        const int i0 = tid - kWave;
+        double r[kSumPer];
+#pragma unroll
+        for (int q = 0; q < kSumPer; ++q) {
+            const int64_t i = i0 + (int64_t)q * kSumLoaders;
+            r[q] = i < cnt ? src[i] : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < kSumPer; ++q) {
+            const int64_t i = i0 + (int64_t)q * kSumLoaders;
+            if (i < cnt) dst[i] = r[q];
+        }
+    };
+    if (nt > 0 && wave > 0) load(0, buf[0]);
+    __syncthreads();
+    double s = 0.0;
+    for (int64_t t = 0; t < nt; ++t) {
+        if (wave > 0 && t + 1 < nt) load(t + 1, buf[(t + 1) & 1]);
+        if (wave == 0 && lane < m) {
+            const double* b = buf[t & 1] + lane;
+            const int64_t u0 = t * upt;
+            const int cnt = (int)((n - u0) < upt ? (n - u0) : upt);
+            int u = 0;
+            for (; u + 8 <= cnt; u += 8) {
+                double x[8];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) x[q] = b[(u + q) * m];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) s += x[q];
+            }
+            for (; u < cnt; ++u) s += b[u * m];
+        }
+        __syncthreads();
+    }
+    if (wave == 0 && lane < m) out[lane] = s;
+}
+
 }  // namespace rsx
 
 using namespace rsx;
@@ -116,6 +173,9 @@ extern "C" int rsx_topk_metrics(const int64_t* topk_idx, int64_t n_users, int32_
     if (n_users > 0)
         hipLaunchKernelGGL(metrics_user, dim3((unsigned)((n_users + 255) / 256)), dim3(256), 0, s, topk_idx, n_users,
                            (int)k_max, eval_rowptr, eval_col, cutoffs, (int)n_cut, gain, vals);
-    hipLaunchKernelGGL(metrics_sum, dim3((unsigned)m), dim3(64), 0, s, vals, n_users, m, out_sums);
+    if (m <= kWave)
+        hipLaunchKernelGGL(metrics_sum_lds, dim3(1), dim3(kSumThreads), 0, s, vals, n_users, m, out_sums);
+    else
+        hipLaunchKernelGGL(metrics_sum, dim3((unsigned)m), dim3(64), 0, s, vals, n_users, m, out_sums);
     return last_rc();
 }
