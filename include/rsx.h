@@ -173,6 +173,12 @@ typedef struct rsx_epilogue {
     const int32_t* row_tag;
     int32_t tag;
     int32_t tag_flags;
+    /* ADAM only (optional): the regulariser gradient as occurrence counts,
+     * r = (cnt[3r] k[0] + cnt[3r+1] k[1] + cnt[3r+2] k[2]) * p_old (what the fused
+     * LightGCN BPR leaves instead of a dense R); with RSX_TAG_ZERO the counts of the
+     * tagged rows are cleared too.  Used instead of r_add when non-NULL. */
+    int32_t* reg_cnt;
+    const float* reg_k;
 } rsx_epilogue;
 
 #define RSX_TAG_ROWS 1
@@ -332,6 +338,11 @@ typedef struct rsx_lgcn_step {
      * (true from zero-filled buffers and after every tagged step). */
     int32_t* row_tag;
     int64_t tag;
+    /* Optional with row_tag: [3 (n_users + n_items) + 4] int32, zero-filled before the
+     * first step.  BPR then runs as ONE launch and leaves the regulariser gradient as
+     * per-row occurrence counts (+ a done counter and three scales in the tail) that
+     * the Adam layer applies and clears; R is not used. */
+    int32_t* reg_cnt;
 } rsx_lgcn_step;
 
 int rsx_lightgcn_step(const rsx_lgcn_step* st, rsx_stream_t stream);

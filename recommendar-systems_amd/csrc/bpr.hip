@@ -34,6 +34,8 @@ struct BprArgs {
     double* loss_acc;
     float* coef;     // [batch]
     double* part;    // [n_blocks][4]
+    int32_t* reg_cnt;  // bpr_fused: [n_rows][3] occurrence counts + [4] tail (done counter, ku, kp, kn)
+    int64_t n_rows;
 };
 
 __device__ __forceinline__ float softplus_neg(float x) {
@@ -220,6 +222,152 @@ __global__ __launch_bounds__(kBprBlock) void bpr_bwd(BprArgs a, int n_part) {
     }
 }
 
+// LightGCN BPR in ONE launch (the batch-tagged step): per triplet the loss term and
+// dL/dfinal rows are scattered at once (divided by g_div); the regulariser's
+// gradient, which needs the batch's global Frobenius norms, is left to the
+// consumer as occurrence counts per row (as user, positive, negative) and three
+// scales ku, kp, kn: R[row] = (c_u ku + c_p kp + c_n kn) ego[row] (the reference
+// sums c equal terms per row).  Every block stores its f64 partials; the last
+// block to arrive (agent-scope release/acquire around one counter) reduces them in
+// bpr_bwd's fixed order, writes the loss and the scales and re-arms the counter.
+template <int D>
+__global__ __launch_bounds__(kBprBlock) void bpr_fused(BprArgs a) {
+    constexpr int G = D / 4;
+    constexpr int GPB = kBprBlock / G;
+    constexpr int NC = D / G;
+    const int li = threadIdx.x % G;
+    const int64_t b = (int64_t)blockIdx.x * GPB + threadIdx.x / G;
+    double t_loss = 0.0, t_u = 0.0, t_p = 0.0, t_n = 0.0;
+    if (b < a.batch) {
+        const int64_t u = a.trip[b];
+        const int64_t p = a.trip[a.batch + b] + a.n_users;
+        const int64_t n = a.trip[2 * a.batch + b] + a.n_users;
+        float fu[NC], fp[NC], fn[NC], eu[NC], ep[NC], en[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            fu[c] = a.fin[u * D + li + c * G];
+            fp[c] = a.fin[p * D + li + c * G];
+            fn[c] = a.fin[n * D + li + c * G];
+            eu[c] = a.ego[u * D + li + c * G];
+            ep[c] = a.ego[p * D + li + c * G];
+            en[c] = a.ego[n * D + li + c * G];
+        }
+        float sp = 0.f, sn = 0.f, qu = 0.f, qp = 0.f, qn = 0.f;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            sp += fu[c] * fp[c];
+            sn += fu[c] * fn[c];
+        }
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            qu += eu[c] * eu[c];
+            qp += ep[c] * ep[c];
+            qn += en[c] * en[c];
+        }
+        sp = group_sum<G>(sp);
+        sn = group_sum<G>(sn);
+        const float delta = sp - sn;
+        const float sg = 1.f / (1.f + expf(-delta));
+        const float term = -logf(1e-10f + sg);
+        const float coef = -(sg * (1.f - sg)) / (1e-10f + sg) / (float)a.batch;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            const int col = li + c * G;
+            float gu = coef * (fp[c] - fn[c]), gp = coef * fu[c], gn = -coef * fu[c];
+            if (a.g_div != 1.f) {
+                gu /= a.g_div;
+                gp /= a.g_div;
+                gn /= a.g_div;
+            }
+            atomicAdd(a.g_fin + u * D + col, gu);
+            atomicAdd(a.g_fin + p * D + col, gp);
+            atomicAdd(a.g_fin + n * D + col, gn);
+        }
+        if (li == 0) {
+            atomicAdd(a.reg_cnt + 3 * u + 0, 1);
+            atomicAdd(a.reg_cnt + 3 * p + 1, 1);
+            atomicAdd(a.reg_cnt + 3 * n + 2, 1);
+            t_loss = (double)term;
+        }
+        t_u = (double)qu;
+        t_p = (double)qp;
+        t_n = (double)qn;
+    }
+    __shared__ double red[kBprBlock / kWave][4];
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) {
+        t_loss += __shfl_xor(t_loss, o, kWave);
+        t_u += __shfl_xor(t_u, o, kWave);
+        t_p += __shfl_xor(t_p, o, kWave);
+        t_n += __shfl_xor(t_n, o, kWave);
+    }
+    const int wv = threadIdx.x / kWave;
+    if ((threadIdx.x % kWave) == 0) {
+        red[wv][0] = t_loss;
+        red[wv][1] = t_u;
+        red[wv][2] = t_p;
+        red[wv][3] = t_n;
+    }
+    __syncthreads();
+    __shared__ int last;
+    if (threadIdx.x < 4) {
+        double v = 0.0;
+        for (int w = 0; w < kBprBlock / kWave; ++w) v += red[w][threadIdx.x];
+        __hip_atomic_store(a.part + (int64_t)blockIdx.x * 4 + threadIdx.x, v, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    int* done = a.reg_cnt + 3 * a.n_rows;
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        const int prev = __hip_atomic_fetch_add(done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = prev == (int)gridDim.x - 1;
+        if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    __syncthreads();
+    if (!last) return;
+    // the last block: bpr_bwd's fixed-order reduction of the per-block partials
+    __shared__ double tr[4][kBprBlock];
+    {
+        double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+        for (int k = threadIdx.x; k < (int)gridDim.x; k += kBprBlock) {
+            const double* q = a.part + (int64_t)k * 4;
+            s0 += __hip_atomic_load(q + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s1 += __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s2 += __hip_atomic_load(q + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s3 += __hip_atomic_load(q + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        tr[0][threadIdx.x] = s0;
+        tr[1][threadIdx.x] = s1;
+        tr[2][threadIdx.x] = s2;
+        tr[3][threadIdx.x] = s3;
+        __syncthreads();
+        for (int w = kBprBlock / 2; w > 0; w >>= 1) {
+            if (threadIdx.x < w) {
+#pragma unroll
+                for (int c = 0; c < 4; ++c) tr[c][threadIdx.x] += tr[c][threadIdx.x + w];
+            }
+            __syncthreads();
+        }
+    }
+    if (threadIdx.x == 0) {
+        const double B = (double)a.batch;
+        const double nu = sqrt(tr[1][0]), np = sqrt(tr[2][0]), nn = sqrt(tr[3][0]);
+        const double loss = tr[0][0] / B + (double)a.reg * (nu + np + nn) / B;
+        float* k = reinterpret_cast<float*>(done + 1);
+        k[0] = nu > 0 ? (float)((double)a.reg / (B * nu)) : 0.f;
+        k[1] = np > 0 ? (float)((double)a.reg / (B * np)) : 0.f;
+        k[2] = nn > 0 ? (float)((double)a.reg / (B * nn)) : 0.f;
+        if (a.loss_out) a.loss_out[0] = (float)loss;
+        if (a.loss_acc) a.loss_acc[0] += loss;
+        *done = 0;  // re-armed for the next launch (stream order)
+    }
+}
+
+int bpr_fused_call(const float* fin, const float* ego, int64_t n_users, int64_t n_items, int32_t d,
+                   const int64_t* trip, int64_t batch, float reg, float g_div, float* g_fin, int32_t* reg_cnt,
+                   float* loss_out, double* loss_acc, void* ws, size_t ws_bytes, hipStream_t s);
+
 template <int D>
 static int launch_bpr(const BprArgs& a, hipStream_t s) {
     constexpr int GPB = kBprBlock / (D / 4);
@@ -273,6 +421,40 @@ int bpr_call(int32_t variant, const float* fin, const float* ego, int64_t n_user
     size_t off = ((size_t)batch * sizeof(float) + 255) & ~(size_t)255;
     a.part = reinterpret_cast<double*>(w + off);
     return bpr_dispatch(a, d, s);
+}
+
+int bpr_fused_call(const float* fin, const float* ego, int64_t n_users, int64_t n_items, int32_t d,
+                   const int64_t* trip, int64_t batch, float reg, float g_div, float* g_fin, int32_t* reg_cnt,
+                   float* loss_out, double* loss_acc, void* ws, size_t ws_bytes, hipStream_t s) {
+    if (!fin || !ego || !trip || !g_fin || !reg_cnt || batch <= 0 || !ws) return RSX_ERR_ARG;
+    if (ws_bytes < bpr_ws(batch)) return RSX_ERR_WORKSPACE;
+    BprArgs a = {};
+    a.variant = RSX_BPR_LIGHTGCN;
+    a.fin = fin;
+    a.ego = ego;
+    a.n_users = n_users;
+    a.n_items = n_items;
+    a.trip = trip;
+    a.batch = batch;
+    a.reg = reg;
+    a.batch_cfg = (float)batch;
+    a.g_div = g_div;
+    a.g_fin = g_fin;
+    a.loss_out = loss_out;
+    a.loss_acc = loss_acc;
+    char* w = static_cast<char*>(ws);
+    a.coef = reinterpret_cast<float*>(w);
+    a.part = reinterpret_cast<double*>(w + (((size_t)batch * sizeof(float) + 255) & ~(size_t)255));
+    a.reg_cnt = reg_cnt;
+    a.n_rows = n_users + n_items;
+    switch (d) {
+        case 32: hipLaunchKernelGGL((bpr_fused<32>), dim3((unsigned)((batch + 31) / 32)), dim3(kBprBlock), 0, s, a); break;
+        case 64: hipLaunchKernelGGL((bpr_fused<64>), dim3((unsigned)((batch + 15) / 16)), dim3(kBprBlock), 0, s, a); break;
+        case 128: hipLaunchKernelGGL((bpr_fused<128>), dim3((unsigned)((batch + 7) / 8)), dim3(kBprBlock), 0, s, a); break;
+        case 256: hipLaunchKernelGGL((bpr_fused<256>), dim3((unsigned)((batch + 3) / 4)), dim3(kBprBlock), 0, s, a); break;
+        default: return RSX_ERR_UNSUPPORTED;
+    }
+    return last_rc();
 }
 
 }  // namespace rsx

@@ -60,6 +60,7 @@ __device__ __forceinline__ float adam_elem(const AdamConst& c, float& p, float& 
 struct EpiIn {
     float4 a, b, c, d, e;
     float w;
+    float regc;   // ADAM with reg_cnt: the row's regulariser scale (0 off the tagged rows)
     bool tagged;  // row_tag[row] == tag (true when no tag flag needs it)
 };
 
@@ -72,6 +73,7 @@ __device__ __forceinline__ EpiIn epi_load(const rsx_epilogue& e, int64_t row, in
     EpiIn in;
     in.a = in.b = in.c = in.d = in.e = f4(0.f);
     in.w = 0.f;
+    in.regc = 0.f;
     const int tf = tag_flags(e);
     in.tagged = (tf & (RSX_TAG_SPARSE_S | RSX_TAG_SPARSE_R | RSX_TAG_ZERO)) ? e.row_tag[row] == e.tag : true;
     // rows of s_in / r_add known to be zero off the tagged rows are not loaded
@@ -92,6 +94,10 @@ __device__ __forceinline__ EpiIn epi_load(const rsx_epilogue& e, int64_t row, in
         in.c = ld4(e.p + off);
         in.d = ld4(e.m + off);
         in.e = ld4(e.v + off);
+        if (e.reg_cnt && (!(tf & RSX_TAG_SPARSE_R) || in.tagged)) {
+            const int32_t* c = e.reg_cnt + 3 * row;
+            in.regc = (float)c[0] * e.reg_k[0] + (float)c[1] * e.reg_k[1] + (float)c[2] * e.reg_k[2];
+        }
     } else if constexpr (KIND == RSX_EPI_LAYERGCN) {
         in.a = ld4(e.e0 + off);
         if (e.s_in) in.b = ld4(e.s_in + off);
@@ -135,7 +141,8 @@ __device__ __forceinline__ void epilogue(const rsx_epilogue& e, int64_t row, flo
     } else if constexpr (KIND == RSX_EPI_ADAM) {
         float4 g = e.s_in ? add4(in.a, acc) : acc;
         g = mul4(e.beta, g);
-        if (e.r_add) g = add4(g, in.b);
+        if (e.reg_cnt) g = add4(g, mul4(in.regc, in.c));  // sum over occurrences of k * ego row
+        else if (e.r_add) g = add4(g, in.b);
         const AdamConst c = adam_const(e.adam);
         float4 p = in.c, m = in.d, v = in.e;
         g.x = adam_elem(c, p.x, m.x, v.x, g.x);
@@ -188,6 +195,14 @@ __device__ __forceinline__ void epilogue(const rsx_epilogue& e, int64_t row, flo
     if (!(tag_flags(e) & RSX_TAG_ZERO) || in.tagged) {
         if (e.zero0) st4(e.zero0 + off, f4(0.f));
         if (e.zero1) st4(e.zero1 + off, f4(0.f));
+        if constexpr (KIND == RSX_EPI_ADAM) {
+            if (e.reg_cnt && (tag_flags(e) & RSX_TAG_ZERO) && li == 0) {
+                int32_t* c = e.reg_cnt + 3 * row;
+                c[0] = 0;
+                c[1] = 0;
+                c[2] = 0;
+            }
+        }
     }
 }
 
@@ -354,6 +369,7 @@ __device__ __forceinline__ void spmm_item(const rsx_csr& a, const float* __restr
     } else {
         pre.a = pre.b = pre.c = pre.d = pre.e = f4(0.f);
         pre.w = 0.f;
+        pre.regc = 0.f;
         pre.tagged = true;
     }
     const int32_t* __restrict__ col = a.col;

@@ -119,6 +119,10 @@ __global__ __launch_bounds__(256) void tag_rows_kernel(const int64_t* __restrict
     row_tag[t < batch ? id : n_users + id] = tag;
 }
 
+int bpr_fused_call(const float* fin, const float* ego, int64_t n_users, int64_t n_items, int32_t d,
+                   const int64_t* trip, int64_t batch, float reg, float g_div, float* g_fin, int32_t* reg_cnt,
+                   float* loss_out, double* loss_acc, void* ws, size_t ws_bytes, hipStream_t s);
+
 int tag_rows(const int64_t* trip, int64_t batch, int64_t n_users, int32_t* row_tag, int32_t tag, hipStream_t s) {
     if (batch <= 0) return 0;
     hipLaunchKernelGGL(tag_rows_kernel, dim3((unsigned)((3 * batch + 255) / 256)), dim3(256), 0, s, trip, batch,
@@ -209,9 +213,15 @@ static int lgcn_step_stored_layers(const rsx_lgcn_step& st, int64_t batch, int32
         e.tag_flags = RSX_TAG_ROWS;
         if ((rc = spmm_dispatch(A, x, d, e, st.slab, s))) return rc;
     }
-    if ((rc = bpr_call(RSX_BPR_LIGHTGCN, st.final_emb, st.p, st.n_users, st.n_items, d, st.triplets, batch, st.reg,
-                       (float)batch, st.g, st.r, st.loss_out, st.loss_acc, st.ws, st.ws_bytes, s, (float)(K + 1))))
+    if (st.reg_cnt) {  // one launch; the regulariser gradient as occurrence counts for the Adam layer
+        if ((rc = bpr_fused_call(st.final_emb, st.p, st.n_users, st.n_items, d, st.triplets, batch, st.reg,
+                                 (float)(K + 1), st.g, st.reg_cnt, st.loss_out, st.loss_acc, st.ws, st.ws_bytes, s)))
+            return rc;
+    } else if ((rc = bpr_call(RSX_BPR_LIGHTGCN, st.final_emb, st.p, st.n_users, st.n_items, d, st.triplets, batch,
+                              st.reg, (float)batch, st.g, st.r, st.loss_out, st.loss_acc, st.ws, st.ws_bytes, s,
+                              (float)(K + 1)))) {
         return rc;
+    }
     // backward: H = G' + A H, H_0 = G'
     x = st.g;
     for (int k = 1; k < K; ++k) {
@@ -233,6 +243,12 @@ static int lgcn_step_stored_layers(const rsx_lgcn_step& st, int64_t batch, int32
     e.adam = st.adam;
     e.zero0 = st.g;  // nothing reads G' or R after this layer (K >= 2)
     e.zero1 = st.r;
+    if (st.reg_cnt) {
+        e.r_add = nullptr;
+        e.zero1 = nullptr;
+        e.reg_cnt = st.reg_cnt;
+        e.reg_k = reinterpret_cast<const float*>(st.reg_cnt + 3 * (st.n_users + st.n_items) + 1);
+    }
     e.row_tag = st.row_tag;
     e.tag = tag;
     e.tag_flags = RSX_TAG_SPARSE_S | RSX_TAG_SPARSE_R | RSX_TAG_ZERO;

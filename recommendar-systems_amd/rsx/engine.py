@@ -59,6 +59,9 @@ class LightGCNEngine:
         # sparse G in the first backward layer; RSX_BATCH_TAGS=0 selects the dense path
         self.row_tag = torch.zeros(n, dtype=torch.int32, device=dev)
         self.use_tags = self.K >= 2 and os.environ.get("RSX_BATCH_TAGS", "1") != "0"
+        # one-launch BPR with the regulariser gradient as per-row counts (tagged step only)
+        self.reg_cnt = torch.zeros(3 * n + 4, dtype=torch.int32, device=dev)
+        self.use_reg_cnt = os.environ.get("RSX_BPR_FUSED", "1") != "0"
         self._st = L.LgcnStep()
         self._sa = L.SamplerArgs()
         self._fill_static()
@@ -86,6 +89,7 @@ class LightGCNEngine:
         st.loss_acc = self.loss_acc.data_ptr()
         st.ws, st.ws_bytes = self.ws.data_ptr(), self.ws.numel()
         st.row_tag = self.row_tag.data_ptr() if self.use_tags else None
+        st.reg_cnt = self.reg_cnt.data_ptr() if (self.use_tags and self.use_reg_cnt) else None
 
     def set_lr(self, lr: float):
         self.lr = float(lr)

@@ -392,6 +392,9 @@ def test_batch_row_tags_equal_dense_step(cuda, K):
     torch.cuda.synchronize()
     a, b = engs
     assert torch.count_nonzero(a.g).item() == 0 and torch.count_nonzero(a.r).item() == 0
+    # the one-launch BPR's occurrence counts are cleared by the Adam layer, its done counter re-armed
+    n = nu + ni
+    assert a.use_reg_cnt and torch.count_nonzero(a.reg_cnt[: 3 * n + 1]).item() == 0
     np.testing.assert_allclose(a.loss_acc.item(), b.loss_acc.item(), rtol=1e-9)
     for name in ("p", "m", "v"):
         np.testing.assert_allclose(getattr(a, name).cpu().numpy(), getattr(b, name).cpu().numpy(), rtol=0,
