@@ -103,13 +103,14 @@ __global__ __launch_bounds__(64) void metrics_sum(const double* __restrict__ val
 // Waves 1-3 stream the next tile of [users][m] values (contiguous in `vals`) into
 // the other LDS buffer meanwhile.  Same order, same bits as metrics_sum.
 constexpr int kSumTileD = 8192;  // doubles per LDS tile (64 KB; two tiles)
-constexpr int kSumThreads = 1024;
-constexpr int kSumLoaders = kSumThreads - kWave;                    // waves 1..15
+constexpr int kSumThreads = 256;
+constexpr int kSumLoaders = kSumThreads - kWave;                    // waves 1..3
 constexpr int kSumPer = (kSumTileD + kSumLoaders - 1) / kSumLoaders;  // loads per loader thread, all in flight
+constexpr int kSumB = 32;                                            // users per register batch of the chain
 __global__ __launch_bounds__(kSumThreads) void metrics_sum_lds(const double* __restrict__ vals, int64_t n, int m,
                                                                double* __restrict__ out) {
     __shared__ double buf[2][kSumTileD];
-    const int upt = kSumTileD / m;  // users per tile
+    const int upt = (kSumTileD / m) & ~(kSumB - 1);  // users per tile, a multiple of the batch
     const int64_t nt = (n + upt - 1) / upt;
     const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
     auto load = [&](int64_t t, double* dst) {  // loader waves: every load issued before any LDS write
@@ -135,16 +136,19 @@ __global__ __launch_bounds__(kSumThreads) void metrics_sum_lds(const double* __r
     for (int64_t t = 0; t < nt; ++t) {
         if (wave > 0 && t + 1 < nt) load(t + 1, buf[(t + 1) & 1]);
         if (wave == 0 && lane < m) {
+            // the column's serial chain: batches of 32 values read from LDS into
+            // registers at once, then 32 dependent adds (one per user, in order)
             const double* b = buf[t & 1] + lane;
             const int64_t u0 = t * upt;
             const int cnt = (int)((n - u0) < upt ? (n - u0) : upt);
             int u = 0;
-            for (; u + 8 <= cnt; u += 8) {
-                double x[8];
+            for (; u + kSumB <= cnt; u += kSumB) {
+                double x[kSumB];
 #pragma unroll
-                for (int q = 0; q < 8; ++q) x[q] = b[(u + q) * m];
+                for (int q = 0; q < kSumB; ++q) x[q] = b[(u + q) * m];
+                __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-                for (int q = 0; q < 8; ++q) s += x[q];
+                for (int q = 0; q < kSumB; ++q) s += x[q];
             }
             for (; u < cnt; ++u) s += b[u * m];
         }
