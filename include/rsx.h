@@ -179,6 +179,8 @@ typedef struct rsx_epilogue {
      * tagged rows are cleared too.  Used instead of r_add when non-NULL. */
     int32_t* reg_cnt;
     const float* reg_k;
+    /* optional: the tag is read from device memory (graph-captured steps) */
+    const int32_t* tag_dev;
 } rsx_epilogue;
 
 #define RSX_TAG_ROWS 1
@@ -510,6 +512,11 @@ typedef struct rsx_sharded_lgcn_step {
     rsx_comm_t comm;
     int32_t* row_tag;           /* optional, see above */
     int64_t tag;
+    /* optional: read the tag from here instead (device int32, e.g. the low word of
+     * the adam.step_dev counter), so that the step can be captured once in a hipGraph
+     * and replayed: with adam.step_dev and tag_dev every per-step value lives on
+     * the device and the step's launches and collectives are fixed. */
+    const int32_t* tag_dev;
 } rsx_sharded_lgcn_step;
 
 int rsx_sharded_lightgcn_step(const rsx_sharded_lgcn_step* st, rsx_stream_t stream);

@@ -33,7 +33,8 @@ int rowwise_dispatch(int64_t n, int d, const rsx_epilogue& e, hipStream_t s);
 int bpr_call(int32_t variant, const float* fin, const float* ego, int64_t n_users, int64_t n_items, int32_t d,
              const int64_t* trip, int64_t batch, float reg, float batch_cfg, float* g_fin, float* g_ego,
              float* loss_out, double* loss_acc, void* ws, size_t ws_bytes, hipStream_t s, float g_div = 1.f);
-int tag_rows(const int64_t* trip, int64_t batch, int64_t n_users, int32_t* row_tag, int32_t tag, hipStream_t s);
+int tag_rows(const int64_t* trip, int64_t batch, int64_t n_users, int32_t* row_tag, int32_t tag, hipStream_t s,
+             const int32_t* tag_dev);
 
 namespace {
 
@@ -231,7 +232,7 @@ int sharded_stored_layers(const rsx_sharded_lgcn_step& st, bool train, hipStream
     float* bufs[2] = {st.h0, st.h1};
     hipEvent_t joins[4] = {};
     int rc = 0;
-    if (train) RSX_TRY(tag_rows(st.triplets, st.batch, nu, st.row_tag, tag, s));
+    if (train) RSX_TRY(tag_rows(st.triplets, st.batch, nu, st.row_tag, tag, s, st.tag_dev));
     // ---- forward
     const float* x = st.p;
     for (int k = 1; k < K; ++k) {
@@ -263,6 +264,7 @@ int sharded_stored_layers(const rsx_sharded_lgcn_step& st, bool train, hipStream
         if (train) {
             e.row_tag = st.row_tag;
             e.tag = tag;
+            e.tag_dev = st.tag_dev;
             e.tag_flags = RSX_TAG_ROWS;
         }
         RSX_TRY(spmm_dispatch(*st.adj_u, x, d, e, st.slab_u, s));
@@ -284,6 +286,7 @@ int sharded_stored_layers(const rsx_sharded_lgcn_step& st, bool train, hipStream
         if (k == 1) {                   // X = G': only this rank's batch users are nonzero
             e.row_tag = st.row_tag;
             e.tag = tag;
+            e.tag_dev = st.tag_dev;
             e.tag_flags = RSX_TAG_SPARSE_X;
         }
         RSX_TRY(spmm_dispatch(*st.adj_i, x, d, e, st.slab_i, s));
@@ -294,6 +297,7 @@ int sharded_stored_layers(const rsx_sharded_lgcn_step& st, bool train, hipStream
         u.s_in = st.g;
         u.row_tag = st.row_tag;
         u.tag = tag;
+        u.tag_dev = st.tag_dev;
         u.tag_flags = RSX_TAG_SPARSE_S;
         RSX_TRY(spmm_dispatch(*st.adj_u, x, d, u, st.slab_u, s));
         x = bufs[k - 1];
@@ -320,6 +324,7 @@ int sharded_stored_layers(const rsx_sharded_lgcn_step& st, bool train, hipStream
         u.zero1 = st.r;
         u.row_tag = st.row_tag;
         u.tag = tag;
+        u.tag_dev = st.tag_dev;
         u.tag_flags = RSX_TAG_SPARSE_S | RSX_TAG_SPARSE_R | RSX_TAG_ZERO;
         RSX_TRY(spmm_dispatch(*st.adj_u, x, d, u, st.slab_u, s));
         RSX_TRY(wait(s, jt));
@@ -442,7 +447,7 @@ int rsx_sharded_lightgcn_step(const rsx_sharded_lgcn_step* st, rsx_stream_t stre
     hipStream_t s = as_stream(stream);
     const int d = st->d, K = st->n_layers;
     if (st->row_tag && (K == 2 || K == 3)) {
-        if (st->tag <= 0 || st->tag > INT32_MAX) return RSX_ERR_ARG;
+        if (!st->tag_dev && (st->tag <= 0 || st->tag > INT32_MAX)) return RSX_ERR_ARG;
         return sharded_stored_layers(*st, true, s);
     }
     const int64_t nu = st->n_users, ni = st->n_items, off = nu * (int64_t)d;

@@ -66,6 +66,7 @@ struct EpiIn {
 
 // tag flags in effect (none without a tag array)
 __device__ __forceinline__ int tag_flags(const rsx_epilogue& e) { return e.row_tag ? e.tag_flags : 0; }
+__device__ __forceinline__ int32_t tag_of(const rsx_epilogue& e) { return e.tag_dev ? *e.tag_dev : e.tag; }
 
 template <int KIND, int D>
 __device__ __forceinline__ EpiIn epi_load(const rsx_epilogue& e, int64_t row, int li) {
@@ -75,7 +76,7 @@ __device__ __forceinline__ EpiIn epi_load(const rsx_epilogue& e, int64_t row, in
     in.w = 0.f;
     in.regc = 0.f;
     const int tf = tag_flags(e);
-    in.tagged = (tf & (RSX_TAG_SPARSE_S | RSX_TAG_SPARSE_R | RSX_TAG_ZERO)) ? e.row_tag[row] == e.tag : true;
+    in.tagged = (tf & (RSX_TAG_SPARSE_S | RSX_TAG_SPARSE_R | RSX_TAG_ZERO)) ? e.row_tag[row] == tag_of(e) : true;
     // rows of s_in / r_add known to be zero off the tagged rows are not loaded
     const float* s_in = (!(tf & RSX_TAG_SPARSE_S) || in.tagged) ? e.s_in : nullptr;
     const float* r_add = (!(tf & RSX_TAG_SPARSE_R) || in.tagged) ? e.r_add : nullptr;
@@ -262,7 +263,7 @@ __device__ __forceinline__ void fixup_block(const rsx_csr& a, const rsx_epilogue
     const int gi = threadIdx.x / G;
     const int4 lr = reinterpret_cast<const int4*>(a.long_rows)[l];
     // an untagged row's chunks skipped too (nothing arrives; the counter stays 0)
-    if ((tag_flags(e) & RSX_TAG_ROWS) && e.row_tag[lr.x] != e.tag) return;
+    if ((tag_flags(e) & RSX_TAG_ROWS) && e.row_tag[lr.x] != tag_of(e)) return;
     EpiIn pre;
     if (gi == 0) pre = epi_load<KIND, D>(e, lr.x, li);
     int* cnt = reinterpret_cast<int*>(slab + a.n_slots * D) + l;
@@ -360,7 +361,7 @@ __device__ __forceinline__ void spmm_item(const rsx_csr& a, const float* __restr
     const int tf = tag_flags(e);
     if (tf & RSX_TAG_ROWS) {  // whole group leaves together (one row per group)
         const int64_t r = wk.y < 0 ? wk.x : reinterpret_cast<const int4*>(a.long_rows)[wk.x].x;
-        if (e.row_tag[r] != e.tag) return;
+        if (e.row_tag[r] != tag_of(e)) return;
     }
     const bool sparse_x = tf & RSX_TAG_SPARSE_X;
     EpiIn pre;
@@ -387,7 +388,7 @@ __device__ __forceinline__ void spmm_item(const rsx_csr& a, const float* __restr
             const bool mine = j + li < end;
             int cm = mine ? col[j + li] : 0;
             const float vm = mine ? val[j + li] : 0.f;
-            if (sparse_x && mine && e.row_tag[cm] != e.tag) cm = -1;  // zero X row: no gather
+            if (sparse_x && mine && e.row_tag[cm] != tag_of(e)) cm = -1;  // zero X row: no gather
             const int n = end - j;
 #if RSX_SPMM_G16
             acc = gather16(acc, cm, vm, n, xl);
@@ -408,7 +409,7 @@ __device__ __forceinline__ void spmm_item(const rsx_csr& a, const float* __restr
             if (sparse_x) {
 #pragma unroll
                 for (int t = 0; t < kUnroll; ++t)
-                    if (e.row_tag[c[t]] != e.tag) c[t] = -1;
+                    if (e.row_tag[c[t]] != tag_of(e)) c[t] = -1;
             }
             float4 xv[kUnroll];
 #pragma unroll
@@ -424,7 +425,7 @@ __device__ __forceinline__ void spmm_item(const rsx_csr& a, const float* __restr
                 const bool ok = j + t < end;
                 c[t] = ok ? col[j + t] : 0;
                 v[t] = ok ? val[j + t] : 0.f;
-                if (sparse_x && ok && e.row_tag[c[t]] != e.tag) c[t] = -1;
+                if (sparse_x && ok && e.row_tag[c[t]] != tag_of(e)) c[t] = -1;
             }
             float4 xv[kUnroll];
 #pragma unroll
@@ -491,7 +492,7 @@ __global__ __launch_bounds__(kBlock) void rowwise_kernel(int64_t n_rows, rsx_epi
     const int li = threadIdx.x % G;
     const int64_t row = (int64_t)blockIdx.x * GPB + threadIdx.x / G;
     if (row >= n_rows) return;
-    if ((tag_flags(e) & RSX_TAG_ROWS) && e.row_tag[row] != e.tag) return;
+    if ((tag_flags(e) & RSX_TAG_ROWS) && e.row_tag[row] != tag_of(e)) return;
     epilogue<KIND, D>(e, row, f4(0.f), li);
 }
 

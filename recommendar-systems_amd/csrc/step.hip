@@ -112,21 +112,23 @@ int sample_call(const rsx_sampler_args& s, int64_t batch, int64_t* out, hipStrea
 
 // row_tag[u] = row_tag[n_users + i] = row_tag[n_users + j] = tag for every triplet
 __global__ __launch_bounds__(256) void tag_rows_kernel(const int64_t* __restrict__ trip, int64_t batch,
-                                                       int64_t n_users, int32_t* __restrict__ row_tag, int32_t tag) {
+                                                       int64_t n_users, int32_t* __restrict__ row_tag, int32_t tag,
+                                                       const int32_t* __restrict__ tag_dev) {
     const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (t >= 3 * batch) return;
     const int64_t id = trip[t];
-    row_tag[t < batch ? id : n_users + id] = tag;
+    row_tag[t < batch ? id : n_users + id] = tag_dev ? *tag_dev : tag;
 }
 
 int bpr_fused_call(const float* fin, const float* ego, int64_t n_users, int64_t n_items, int32_t d,
                    const int64_t* trip, int64_t batch, float reg, float g_div, float* g_fin, int32_t* reg_cnt,
                    float* loss_out, double* loss_acc, void* ws, size_t ws_bytes, hipStream_t s);
 
-int tag_rows(const int64_t* trip, int64_t batch, int64_t n_users, int32_t* row_tag, int32_t tag, hipStream_t s) {
+int tag_rows(const int64_t* trip, int64_t batch, int64_t n_users, int32_t* row_tag, int32_t tag, hipStream_t s,
+             const int32_t* tag_dev) {
     if (batch <= 0) return 0;
     hipLaunchKernelGGL(tag_rows_kernel, dim3((unsigned)((3 * batch + 255) / 256)), dim3(256), 0, s, trip, batch,
-                       n_users, row_tag, tag);
+                       n_users, row_tag, tag, tag_dev);
     return last_rc();
 }
 
@@ -324,7 +326,7 @@ int rsx_lightgcn_step(const rsx_lgcn_step* st, rsx_stream_t stream) {
     const int32_t tag = (int32_t)st->tag;
     if (tags) {
         if (st->tag <= 0 || st->tag > INT32_MAX) return RSX_ERR_ARG;
-        if ((rc = tag_rows(st->triplets, batch, st->n_users, st->row_tag, tag, s))) return rc;
+        if ((rc = tag_rows(st->triplets, batch, st->n_users, st->row_tag, tag, s, nullptr))) return rc;
     }
     if (tags && K <= 3) return lgcn_step_stored_layers(*st, batch, tag, s);
     // forward (dense path: the last layer zeroes g and r)

@@ -50,7 +50,8 @@ class Epilogue(C.Structure):
     _fields_ = [("kind", I32), ("pad0", I32), ("alpha", F32), ("beta", F32),
                 ("y", P), ("s_in", P), ("s_out", P), ("f", P), ("zero0", P), ("zero1", P), ("r_add", P),
                 ("p", P), ("m", P), ("v", P), ("g_out", P), ("e0", P), ("aux", P), ("aux_w", P),
-                ("adam", Adam), ("row_tag", P), ("tag", I32), ("tag_flags", I32), ("reg_cnt", P), ("reg_k", P)]
+                ("adam", Adam), ("row_tag", P), ("tag", I32), ("tag_flags", I32), ("reg_cnt", P), ("reg_k", P),
+                ("tag_dev", P)]
 
 
 RSX_TAG_ROWS = 1
@@ -80,7 +81,7 @@ class ShardedStep(C.Structure):
                 ("p", P), ("m", P), ("v", P), ("s", P), ("h0", P), ("h1", P), ("final_emb", P), ("g", P),
                 ("r", P), ("t", P), ("slab_u", P), ("slab_i", P), ("triplets", P), ("batch", I64),
                 ("adam", Adam), ("loss_out", P), ("loss_acc", P), ("ws", P), ("ws_bytes", C.c_size_t),
-                ("comm", P), ("row_tag", P), ("tag", I64)]
+                ("comm", P), ("row_tag", P), ("tag", I64), ("tag_dev", P)]
 
 
 HOST_ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, P, I64, P)

@@ -100,9 +100,12 @@ def _native_worker(rank, world, port, out_dir):
     U0 = torch.nn.init.xavier_uniform_(torch.empty(NU, D)).numpy()
     tu, ti, trip = _local_graph(rank)
     res = {}
-    for native in (True, False):
-        eng = ShardedLightGCNEngine(tu, ti, NU, NI, D, K, REG, LR, "cuda:0", U0, I0, batch=16, native=native)
-        assert eng.native == native
+    for native in ("graph", True, False):
+        eng = ShardedLightGCNEngine(tu, ti, NU, NI, D, K, REG, LR, "cuda:0", U0, I0, batch=16,
+                                    native=bool(native))
+        assert eng.native == bool(native)
+        if native is True:
+            eng.use_graph = False  # the eagerly issued native step
         f0 = eng.forward().cpu().clone()
         eng.step(triplets=torch.from_numpy(trip).cuda())
         losses = [float(eng.loss_acc.item())]
@@ -112,8 +115,10 @@ def _native_worker(rank, world, port, out_dir):
         losses.append(float(eng.loss_acc.item()))
         eng.invalidate()
         f1 = eng.forward().cpu().clone()
+        if native == "graph":  # full batches after the first were replayed from one capture
+            assert eng._graph is not None
         res[native] = (f0.numpy(), eng.p.cpu().numpy(), eng.m.cpu().numpy(), np.array(losses), f1.numpy())
-        if native:  # the bare collective: one rank = identity, stream-ordered
+        if native is True:  # the bare collective: one rank = identity, stream-ordered
             from rsx import _lib as L
             from rsx import ops
             import ctypes as C
@@ -123,7 +128,7 @@ def _native_worker(rank, world, port, out_dir):
                     "allreduce")
             assert torch.equal(x.cpu(), torch.arange(1000, dtype=torch.float32))
         eng.close()
-    np.savez(os.path.join(out_dir, "native.npz"), **{f"{k}_{i}": v for k in (True, False)
+    np.savez(os.path.join(out_dir, "native.npz"), **{f"{k}_{i}": v for k in ("graph", True, False)
                                                      for i, v in enumerate(res[k])})
     dist.destroy_process_group()
 
@@ -138,9 +143,11 @@ def test_native_sharded_step_equals_python_sequence():
     # forward before any step: same kernels, same order -> bit-identical; after the
     # steps the BPR gradient scatter's float atomics (duplicate rows in a batch, as the
     # reference's index_put_) may order differently run to run: 1e-6 absolute
-    assert np.array_equal(z["True_0"], z["False_0"])
+    assert np.array_equal(z["True_0"], z["False_0"]) and np.array_equal(z["graph_0"], z["False_0"])
     # (the native step keeps the layers and runs Horner on G/(K+1); the Python sequence
     # keeps running sums: same objective, different rounding order)
     for i in range(1, 5):
         np.testing.assert_allclose(z[f"True_{i}"], z[f"False_{i}"], rtol=1e-5, atol=1e-5, err_msg=str(i))
+        # the graph-replayed native step = the eagerly issued one (up to the BPR atomics' order)
+        np.testing.assert_allclose(z[f"graph_{i}"], z[f"True_{i}"], rtol=1e-6, atol=1e-6, err_msg=str(i))
     assert np.isfinite(z["True_1"]).all()

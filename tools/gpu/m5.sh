@@ -1,0 +1,4 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+for c in 2 3 4 6 8; do for m in 0 1; do RSX_FS_CHUNKS=$c RSX_FS_MODE=$m timeout -k 10 100 python tools/gpu/micro.py fullsort 2>/dev/null | tr -d '\n' || exit 1; echo " chunks $c mode $m"; done; done
