@@ -33,7 +33,10 @@ namespace rsx {
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef unsigned long long u64;
 
-constexpr int kCap = 256;   // candidate slots per (user, chunk) row; compaction when > kCap - 32
+#ifndef RSX_FS_CAP
+#define RSX_FS_CAP 256
+#endif
+constexpr int kCap = RSX_FS_CAP;  // candidate slots per (user, chunk) row; compaction when > kCap - 32
 constexpr int kNK = kCap / 64;  // candidate keys per lane while compacting
 constexpr int kMaxK = 96;     // k limit: a chunk's final list (<= k) is <= 2 keys per lane in fs_select
 

@@ -16,6 +16,6 @@ for src in B.SOURCES:
     obj = os.path.join(out, src.replace(".hip", ".o"))
     subprocess.run([B._hipcc(), *B._flags(), *defs, "-c", os.path.join(B.CSRC, src), "-o", obj], check=True)
     objs.append(obj)
-subprocess.run([B._hipcc(), f"--offload-arch={B.ARCH}", "-shared", "-fPIC", "-o", os.path.join(out, "librsx.so"),
+subprocess.run([B._hipcc(), f"--offload-arch={B.ARCH}", "-shared", "-fPIC", "-o", os.path.join(out, "librsx.so"), "-ldl",
                 *objs], check=True)
 print(os.path.join(out, "librsx.so"))
