@@ -354,11 +354,27 @@ __device__ __forceinline__ void st4_sc1(float* p, float4 v) {
     asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(t) : "memory");
 }
 
+#ifndef RSX_SPMM_PF
+#define RSX_SPMM_PF 1
+#endif
+
+// (col, val) of the next work item's first 16 nonzeros, loaded while the current
+// item's first gathers are in flight (d = 64): the next item starts with its
+// gathers instead of a dependent (col, val) trip.
+struct NextCV {
+    int cm;
+    float vm;
+    bool ok;
+};
+
 // One work item {row, slot, begin, end} by a group of G lanes.
 template <int D, int KIND>
 __device__ __forceinline__ void spmm_item(const rsx_csr& a, const float* __restrict__ x, const rsx_epilogue& e,
-                                          float* __restrict__ slab, int4 wk, int li) {
+                                          float* __restrict__ slab, int4 wk, int li, NextCV& pf, int4 nxt,
+                                          bool has_nxt) {
     const int tf = tag_flags(e);
+    const bool have_pf = pf.ok;
+    pf.ok = false;
     if (tf & RSX_TAG_ROWS) {  // whole group leaves together (one row per group)
         const int64_t r = wk.y < 0 ? wk.x : reinterpret_cast<const int4*>(a.long_rows)[wk.x].x;
         if (e.row_tag[r] != tag_of(e)) return;
@@ -386,14 +402,42 @@ __device__ __forceinline__ void spmm_item(const rsx_csr& a, const float* __restr
         // memory pipe only sees the neighbour-row gathers.
         for (; j < end; j += 16) {
             const bool mine = j + li < end;
-            int cm = mine ? col[j + li] : 0;
-            const float vm = mine ? val[j + li] : 0.f;
+            int cm;
+            float vm;
+            if (RSX_SPMM_PF && j == wk.z && have_pf) {
+                cm = mine ? pf.cm : 0;
+                vm = mine ? pf.vm : 0.f;
+            } else {
+                cm = mine ? col[j + li] : 0;
+                vm = mine ? val[j + li] : 0.f;
+            }
             if (sparse_x && mine && e.row_tag[cm] != tag_of(e)) cm = -1;  // zero X row: no gather
             const int n = end - j;
 #if RSX_SPMM_G16
             acc = gather16(acc, cm, vm, n, xl);
 #else
+#if RSX_SPMM_PF
+            if (j == wk.z && has_nxt) {
+                // issue this chunk's first 8 gathers, then the next item's (col, val), then add
+                const int vi = __float_as_int(vm);
+                int c[8];
+                float v[8];
+                bcast8<0>(cm, vi, c, v);
+                float4 xv[8];
+#pragma unroll
+                for (int t = 0; t < 8; ++t) xv[t] = (t < n && c[t] >= 0) ? ld4(xl + (int64_t)c[t] * 64) : f4(0.f);
+                const bool nm = nxt.z + li < nxt.w;
+                pf.cm = nm ? col[nxt.z + li] : 0;
+                pf.vm = nm ? val[nxt.z + li] : 0.f;
+                pf.ok = true;
+#pragma unroll
+                for (int t = 0; t < 8; ++t) acc = fma4(v[t], xv[t], acc);
+            } else {
+                acc = gather8<0>(acc, cm, vm, n, xl);
+            }
+#else
             acc = gather8<0>(acc, cm, vm, n, xl);
+#endif
             if (n > 8) acc = gather8<1>(acc, cm, vm, n, xl);
 #endif
         }
@@ -474,10 +518,11 @@ __global__ RSX_SPMM_ATTR __launch_bounds__(kBlock) void spmm_main(rsx_csr a, con
     if (w >= a.n_work) return;  // whole groups leave together
     const int4* work = reinterpret_cast<const int4*>(a.work);
     int4 wk = work[w];
+    NextCV pf = {0, 0.f, false};
     for (;;) {
         const int64_t wn = w + stride;
         const int4 nxt = wn < a.n_work ? work[wn] : make_int4(0, 0, 0, 0);
-        spmm_item<D, KIND>(a, x, e, slab, wk, li);
+        spmm_item<D, KIND>(a, x, e, slab, wk, li, pf, nxt, wn < a.n_work);
         if (wn >= a.n_work) break;
         w = wn;
         wk = nxt;
