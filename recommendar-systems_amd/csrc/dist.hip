@@ -43,8 +43,6 @@ struct Rccl {
     decltype(&ncclCommInitRank) init_rank = nullptr;
     decltype(&ncclCommDestroy) destroy = nullptr;
     decltype(&ncclAllReduce) all_reduce = nullptr;
-    decltype(&ncclGroupStart) group_start = nullptr;
-    decltype(&ncclGroupEnd) group_end = nullptr;
     bool ok = false;
 };
 
@@ -59,9 +57,7 @@ const Rccl& rccl() {
         x.init_rank = reinterpret_cast<decltype(&ncclCommInitRank)>(dlsym(h, "ncclCommInitRank"));
         x.destroy = reinterpret_cast<decltype(&ncclCommDestroy)>(dlsym(h, "ncclCommDestroy"));
         x.all_reduce = reinterpret_cast<decltype(&ncclAllReduce)>(dlsym(h, "ncclAllReduce"));
-        x.group_start = reinterpret_cast<decltype(&ncclGroupStart)>(dlsym(h, "ncclGroupStart"));
-        x.group_end = reinterpret_cast<decltype(&ncclGroupEnd)>(dlsym(h, "ncclGroupEnd"));
-        x.ok = x.get_unique_id && x.init_rank && x.destroy && x.all_reduce && x.group_start && x.group_end;
+        x.ok = x.get_unique_id && x.init_rank && x.destroy && x.all_reduce;
         return x;
     }();
     return r;
@@ -87,11 +83,11 @@ struct rsx_comm_s {
 namespace rsx {
 namespace {
 
-// In-place sums of a[0, n) (and b[0, n) when b != nullptr, one RCCL group) over the
-// communicator, after the work queued so far on `s`; returns the join event the
-// reader must wait on (nullptr on error, rc set).  A host-hook communicator
-// synchronises `s`, calls the hook per buffer and returns an event on `s`.
-hipEvent_t exchange(rsx_comm_t c, float* a, float* b, int64_t n, hipStream_t s, int* rc) {
+// In-place sum of a[0, n) over the communicator, after the work queued so far on
+// `s`; returns the join event the reader must wait on (nullptr on error, rc set).
+// A host-hook communicator synchronises `s`, calls the hook and returns an event
+// recorded on `s`.
+hipEvent_t exchange(rsx_comm_t c, float* a, int64_t n, hipStream_t s, int* rc) {
     hipError_t e;
     hipEvent_t j = c->join[c->next];
     c->next = (c->next + 1) % kJoinEvents;
@@ -100,7 +96,7 @@ hipEvent_t exchange(rsx_comm_t c, float* a, float* b, int64_t n, hipStream_t s, 
             *rc = hip_rc(e);
             return nullptr;
         }
-        if (c->host_fn(a, n, c->host_ctx) || (b && c->host_fn(b, n, c->host_ctx))) {
+        if (c->host_fn(a, n, c->host_ctx)) {
             *rc = RSX_ERR_COMM;
             return nullptr;
         }
@@ -114,18 +110,7 @@ hipEvent_t exchange(rsx_comm_t c, float* a, float* b, int64_t n, hipStream_t s, 
         *rc = hip_rc(e);
         return nullptr;
     }
-    const Rccl& r = rccl();
-    ncclResult_t nr = ncclSuccess;
-    if (b) {
-        nr = r.group_start();
-        if (nr == ncclSuccess) nr = r.all_reduce(a, a, (size_t)n, ncclFloat32, ncclSum, c->nccl, c->stream);
-        if (nr == ncclSuccess) nr = r.all_reduce(b, b, (size_t)n, ncclFloat32, ncclSum, c->nccl, c->stream);
-        const ncclResult_t ge = r.group_end();
-        if (nr == ncclSuccess) nr = ge;
-    } else {
-        nr = r.all_reduce(a, a, (size_t)n, ncclFloat32, ncclSum, c->nccl, c->stream);
-    }
-    if (nr != ncclSuccess) {
+    if (rccl().all_reduce(a, a, (size_t)n, ncclFloat32, ncclSum, c->nccl, c->stream) != ncclSuccess) {
         *rc = RSX_ERR_COMM;
         return nullptr;
     }
@@ -135,7 +120,6 @@ hipEvent_t exchange(rsx_comm_t c, float* a, float* b, int64_t n, hipStream_t s, 
     }
     return j;
 }
-hipEvent_t exchange(rsx_comm_t c, float* a, int64_t n, hipStream_t s, int* rc) { return exchange(c, a, nullptr, n, s, rc); }
 
 int wait(hipStream_t s, hipEvent_t j) { return hip_rc(hipStreamWaitEvent(s, j, 0)); }
 
@@ -218,11 +202,10 @@ int sharded_forward(const rsx_sharded_lgcn_step& st, bool zero_grads, hipStream_
 // (scaled by 1/(K+1) before the sum), and the user rows' mean is computed on the
 // batch rows only.  Backward: Horner on G' = dL/dfinal / (K+1) (BPR's g_div),
 //   H^k = G' + A H^{k-1},  H^0 = G',  Adam on g = H^K + R,
-// with G', R's item rows summed once (one grouped exchange) and added to the item
-// partials by rank 0 only; the last item partial carries G' + R so one exchange
-// gives the whole item gradient.  2K+1 exchanges of n_items*d floats per step
-// (the first a group of two), 2K SpMM launches + 1 item Adam launch, no layer-sum
-// passes.  `train` false: forward only, every final row (evaluation).
+// with G''s item rows summed once and added to the item partials by rank 0 only;
+// the last item partial carries (rank 0) G'_I and (every rank) its own R_I, so one
+// exchange gives the whole item gradient.  2K+1 exchanges of n_items*d floats per
+// step, 2K SpMM launches + 1 item Adam launch, no layer-sum passes.  `train` false: forward only, every final row (evaluation).
 int sharded_stored_layers(const rsx_sharded_lgcn_step& st, bool train, hipStream_t s) {
     const int d = st.d, K = st.n_layers;
     const int64_t nu = st.n_users, ni = st.n_items, off = nu * (int64_t)d;
@@ -274,7 +257,9 @@ int sharded_stored_layers(const rsx_sharded_lgcn_step& st, bool train, hipStream
     // ---- loss: G' = dL/dfinal / (K+1), R = d reg / d ego on this rank's batch rows
     RSX_TRY(bpr_call(RSX_BPR_LIGHTGCN, st.final_emb, st.p, nu, ni, d, st.triplets, st.batch, st.reg,
                      (float)st.batch, st.g, st.r, st.loss_out, st.loss_acc, st.ws, st.ws_bytes, s, (float)(K + 1)));
-    hipEvent_t j0 = exchange(st.comm, st.g + off, st.r + off, ni * d, s, &rc);  // G'_I, R_I summed
+    // G'_I summed (R_I is not: every rank adds its own R_I to its last item partial,
+    // whose exchange then sums them; one n_items*d exchange less per step)
+    hipEvent_t j0 = exchange(st.comm, st.g + off, ni * d, s, &rc);
     if (!j0) return rc;
     RSX_TRY(wait(s, j0));
     // ---- backward
@@ -303,12 +288,10 @@ int sharded_stored_layers(const rsx_sharded_lgcn_step& st, bool train, hipStream
         x = bufs[k - 1];
     }
     {
-        rsx_epilogue e = epi(RSX_EPI_ADD);  // item gradient partial: A_I H^{K-1}_U (+ G'_I + R_I on rank 0)
+        rsx_epilogue e = epi(RSX_EPI_ADD);  // item gradient partial: A_I H^{K-1}_U + own R_I (+ G'_I on rank 0)
         e.y = st.t;
-        if (root) {
-            e.s_in = st.g + off;
-            e.r_add = st.r + off;
-        }
+        if (root) e.s_in = st.g + off;
+        e.r_add = st.r + off;
         RSX_TRY(spmm_dispatch(*st.adj_i, x, d, e, st.slab_i, s));
         hipEvent_t jt = exchange(st.comm, st.t, ni * d, s, &rc);
         if (!jt) return rc;
@@ -334,7 +317,7 @@ int sharded_stored_layers(const rsx_sharded_lgcn_step& st, bool train, hipStream
         a.m = st.m + off;
         a.v = st.v + off;
         a.adam = st.adam;
-        a.zero0 = st.g + off;  // the summed G'_I, R_I: cleared densely
+        a.zero0 = st.g + off;  // the summed G'_I and this rank's R_I: cleared densely
         a.zero1 = st.r + off;
         RSX_TRY(rowwise_dispatch(ni, d, a, s));
     }
