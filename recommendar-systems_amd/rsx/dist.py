@@ -43,8 +43,10 @@ Python sequence remains the statement the gloo tests check and the fallback
 when `native=False`.  For K = 2, 3 the native step is the stored-layer form
 (csrc/dist.hip:sharded_stored_layers): no layer-sum passes, the last user layer
 on the batch rows only, the backward as Horner on G/(K+1) with rank 0 adding the
-summed G'_I (+ R_I) into its item partials — 2K SpMM launches + one item Adam
-per step instead of 2K SpMMs + 2K row-block sums.  With a non-RCCL group
+summed G'_I into its item partials and every rank its own regulariser rows into
+the last one — 2K SpMM launches + one item Adam per step instead of 2K SpMMs +
+2K row-block sums.  Over RCCL it is captured once as a HIP graph and replayed
+(`_native_step`).  With a non-RCCL group
 (gloo, tests) the native step's exchanges go through a host hook
 (`rsx_comm_init_host`) so several ranks can share one GPU.
 """
