@@ -403,3 +403,23 @@ def test_batch_row_tags_equal_dense_step(cuda, K):
     a.invalidate()
     b.invalidate()
     np.testing.assert_allclose(a.forward().cpu().numpy(), b.forward().cpu().numpy(), rtol=0, atol=1e-6)
+
+
+def test_tagged_step_vs_fixture(cuda, golden):
+    """The engine's default step (batch-row tags, stored layers, one-launch BPR with the
+    regulariser as counts) against the reference's first LightGCN step (fixture)."""
+    from rsx.engine import LightGCNEngine
+
+    z = golden("lightgcn_small")
+    nu, ni = int(z["n_users"]), int(z["n_items"])
+    U0, I0 = params(z, "init.", "LightGCN")
+    eng = LightGCNEngine(z["train_u"], z["train_i"], nu, ni, 64, 3, 1e-2, 1e-3, cuda, U0, I0, batch=512)
+    assert eng.use_tags and eng.use_reg_cnt
+    trip = torch.from_numpy(z["epoch0_triplets"][:, :512].astype(np.int64)).to(cuda)
+    eng.step(triplets=trip)
+    ref = float(z["step0_loss"])
+    assert abs(eng.loss_out.item() - ref) <= 1e-5 * abs(ref)
+    pu, pi = params(z, "step0_param.", "LightGCN")
+    out = eng.p.cpu().numpy()
+    np.testing.assert_allclose(out[:nu], pu, rtol=0, atol=2e-6)
+    np.testing.assert_allclose(out[nu:], pi, rtol=0, atol=2e-6)
