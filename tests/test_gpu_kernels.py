@@ -364,8 +364,8 @@ def test_device_edge_dropout_graph_equals_host_builder(cuda, seed):
         assert torch.allclose(A.spmm(x), ref, rtol=1e-5, atol=1e-6)
 
 
-@pytest.mark.parametrize("K", [2, 3])
-def test_batch_row_tags_equal_dense_step(cuda, K):
+@pytest.mark.parametrize("K,d", [(2, 64), (3, 64), (3, 128), (2, 256), (3, 32)])
+def test_batch_row_tags_equal_dense_step(cuda, K, d):
     """rsx_lgcn_step.row_tag (last forward layer on the batch rows, sparse G, G/R
     cleared on the batch rows) gives the dense path's parameters and losses on a
     power-law graph with hub rows; G and R are all-zero between tagged steps."""
@@ -377,11 +377,11 @@ def test_batch_row_tags_equal_dense_step(cuda, K):
     tu, ti = tr.userID.values.astype(np.int64), tr.itemID.values.astype(np.int64)
     nu, ni = int(df.userID.max()) + 1, 800
     torch.manual_seed(5)
-    U0 = torch.nn.init.xavier_uniform_(torch.empty(nu, 64)).numpy()
-    I0 = torch.nn.init.xavier_uniform_(torch.empty(ni, 64)).numpy()
+    U0 = torch.nn.init.xavier_uniform_(torch.empty(nu, d)).numpy()
+    I0 = torch.nn.init.xavier_uniform_(torch.empty(ni, d)).numpy()
     engs = []
     for tags in (True, False):
-        e = LightGCNEngine(tu, ti, nu, ni, 64, K, 1e-2, 1e-3, cuda, U0, I0, seed=0, batch=512)
+        e = LightGCNEngine(tu, ti, nu, ni, d, K, 1e-2, 1e-3, cuda, U0, I0, seed=0, batch=512)
         e.use_tags = tags
         e._fill_static()
         engs.append(e)
