@@ -189,9 +189,27 @@ __device__ __forceinline__ float compact_slot(u64* buf, int n, int k, int lane, 
 // double-buffered register set (lane l: item l&31, floats [h*D/2 + CW*c, +CW)),
 // prefetched one chunk ahead of the MFMAs that consume the current one; rows past
 // the chunk are clamped to a valid row and zeroed, so the load is branch-free.
+#ifndef RSX_FS_FULLLOAD
+#define RSX_FS_FULLLOAD 1
+#endif
+#ifndef RSX_FS_GUARD
+#define RSX_FS_GUARD 1
+#endif
 template <int D, int CW>
 __device__ __forceinline__ void load_chunk(float (&r)[CW], const float* I, int64_t item, int64_t i1, int64_t ni,
-                                           int off) {
+                                           int off, bool full = false) {
+    if (RSX_FS_FULLLOAD && full) {  // the whole 32-item tile is inside the chunk (wave-uniform): no clamps, no selects
+        const float* p = I + item * D + off;
+#pragma unroll
+        for (int q = 0; q < CW / 4; ++q) {
+            const float4 v = ld4(p + 4 * q);
+            r[4 * q] = v.x;
+            r[4 * q + 1] = v.y;
+            r[4 * q + 2] = v.z;
+            r[4 * q + 3] = v.w;
+        }
+        return;
+    }
     const bool ok = item < i1;
     const float* p = I + (ok ? item : ni - 1) * D + off;
 #pragma unroll
@@ -281,7 +299,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D <= 64 ? 2 
     u64 prof[6] = {0, 0, 0, 0, 0, 0};  // MODE 4: memtime per segment (mfma issue, -, filter, compact, mask+copy, tiles)
     const int64_t nsteps = (int64_t)ntiles * NCH;
     float ra[CW], rb[CW];
-    if (ntiles > 0) load_chunk<D, CW>(ra, a.I, i0 + j, i1, a.ni, h * HALF);
+    if (ntiles > 0) load_chunk<D, CW>(ra, a.I, i0 + j, i1, a.ni, h * HALF, i0 + 32 <= i1);
 
     auto mask_bits = [&](int64_t tb) __attribute__((always_inline)) -> unsigned {  // train items of this user in [tb, tb+32)
         unsigned mb = 0;
@@ -301,7 +319,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D <= 64 ? 2 
             // next tile's rows (the loads land while this tile is filtered)
 #pragma unroll
             for (int q = 0; q < CW; ++q) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ra[q], bu[q], acc, 0, 0, 0);
-            load_chunk<D, CW>(ra, a.I, t + 1 < ntiles ? i0 + (int64_t)(t + 1) * 32 + j : i1, i1, a.ni, h * HALF);
+            if (!RSX_FS_GUARD || t + 1 < ntiles)  // the chain has read ra: refill it with the next tile (none after the last)
+                load_chunk<D, CW>(ra, a.I, i0 + (int64_t)(t + 1) * 32 + j, i1, a.ni, h * HALF,
+                                  i0 + (int64_t)(t + 2) * 32 <= i1);
         } else {
 #pragma unroll
             for (int c = 0; c < NCH; ++c) {
@@ -310,7 +330,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D <= 64 ? 2 
                 const int64_t s1 = (int64_t)t * NCH + c + 1;
                 const int t1 = (int)(s1 / NCH), c1 = (int)(s1 % NCH);
                 load_chunk<D, CW>(nxt, a.I, s1 < nsteps ? i0 + (int64_t)t1 * 32 + j : i1, i1, a.ni,
-                                  h * HALF + CW * c1);
+                                  h * HALF + CW * c1, s1 < nsteps && i0 + (int64_t)(t1 + 1) * 32 <= i1);
 #pragma unroll
                 for (int q = 0; q < CW; ++q)
                     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[q], bu[CW * c + q], acc, 0, 0, 0);
@@ -321,6 +341,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D <= 64 ? 2 
     // items in it (both wave-uniform, so the common tile takes the leanest variant)
     auto filter_v = [&](auto full_c, auto masked_c, const floatx16& sv, unsigned mb, int64_t tb) __attribute__((always_inline)) {
         constexpr bool FULL = decltype(full_c)::value != 0, MASKED = decltype(masked_c)::value != 0;
+        if constexpr (FULL && !MASKED) {
+            // the common tile once the threshold has settled: one max over the 16
+            // scores decides whether this lane (and, by ballot, the wave) has anything
+            float mx = sv[0];
+#pragma unroll
+            for (int r = 1; r < 16; ++r) mx = fmaxf(mx, sv[r]);
+            if (__ballot(uvalid && mx > tau) == 0ull) return;
+        }
         unsigned m = 0;
         const int rem = (int)(i1 - tb);
 #pragma unroll

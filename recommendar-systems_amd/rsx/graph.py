@@ -35,8 +35,7 @@ def to_csr(rows: np.ndarray, cols: np.ndarray, vals: np.ndarray, n_rows: int, n_
     order = np.lexsort((cols, rows))
     r = rows[order]
     rowptr = np.zeros(n_rows + 1, dtype=np.int64)
-    np.add.at(rowptr, r + 1, 1)
-    rowptr = np.cumsum(rowptr)
+    rowptr[1:] = np.cumsum(np.bincount(r, minlength=n_rows)[:n_rows])
     return rowptr, cols[order].astype(np.int32), vals[order].astype(np.float32)
 
 
@@ -98,5 +97,5 @@ def history_csr(train_u: np.ndarray, train_i: np.ndarray, n_users: int):
     u = (key >> 32).astype(np.int64)
     i = (key & 0xFFFFFFFF).astype(np.int32)
     rowptr = np.zeros(n_users + 1, dtype=np.int64)
-    np.add.at(rowptr, u + 1, 1)
-    return np.cumsum(rowptr), i
+    rowptr[1:] = np.cumsum(np.bincount(u, minlength=n_users)[:n_users])
+    return rowptr, i

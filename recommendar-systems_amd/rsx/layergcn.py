@@ -142,8 +142,8 @@ class DeviceEdgeDropout:
         eid = np.concatenate([np.arange(E), np.arange(E)])
         order = np.lexsort((cols, rows))
         rowptr = np.zeros(n + 1, dtype=np.int64)
-        np.add.at(rowptr, rows + 1, 1)
-        self.t_rowptr = torch.from_numpy(np.cumsum(rowptr)).to(self.device)
+        rowptr[1:] = np.cumsum(np.bincount(rows, minlength=n)[:n])
+        self.t_rowptr = torch.from_numpy(rowptr).to(self.device)
         self.t_col = torch.from_numpy(cols[order].astype(np.int32)).to(self.device)
         self.t_eid = torch.from_numpy(eid[order].astype(np.int64)).to(self.device)
 

@@ -330,8 +330,7 @@ class DeviceSampler:
         u_sorted = train_u[order]
         i_sorted = train_i[order]
         rowptr = np.zeros(n_users + 1, dtype=np.int64)
-        np.add.at(rowptr, u_sorted + 1, 1)
-        rowptr = np.cumsum(rowptr)
+        rowptr[1:] = np.cumsum(np.bincount(u_sorted, minlength=n_users)[:n_users])
         self.device = torch.device(device)
         self.n_inter = int(train_u.size)
         self.inter_u = torch.from_numpy(train_u.astype(np.int32)).to(self.device)
