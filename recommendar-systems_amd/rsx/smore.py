@@ -126,6 +126,32 @@ def knn_graph_device(feat: torch.Tensor, k: int, chunk_bytes: int = 1 << 30):
     return r, i.reshape(-1).cpu().numpy().astype(np.int64), w.reshape(-1).cpu().numpy().astype(np.float32)
 
 
+def load_reference_knn(path: str, n: int):
+    """The reference's own kNN cache (smore.py:46-47,56-62: `torch.save` of the
+    sparse [n, n] graph as `{image,text}_adj_{k}_{sparse}.pt` in the dataset
+    directory), read with the loader that executes nothing from the file
+    (`weights_only=True`).  Returns (rows, cols, vals) in coalesced order, or None
+    when the file is absent, refused by the safe loader or not an [n, n] graph."""
+    if not os.path.exists(path):
+        return None
+    try:
+        t = torch.load(path, map_location="cpu", weights_only=True)
+    except Exception:  # noqa: BLE001 - a file the safe loader refuses is rebuilt, not trusted
+        return None
+    if not isinstance(t, torch.Tensor) or t.dim() != 2 or tuple(t.shape) != (n, n):
+        return None
+    if t.layout == torch.sparse_coo:
+        t = t.coalesce()
+        idx, val = t.indices(), t.values()
+    elif t.layout == torch.strided:  # is_sparse False: build_knn_normalized_graph's dense matrix
+        idx = t.nonzero().t()
+        val = t[idx[0], idx[1]]
+    else:
+        return None
+    return (idx[0].numpy().astype(np.int64), idx[1].numpy().astype(np.int64),
+            val.to(torch.float32).numpy().astype(np.float32))
+
+
 def max_pool_union(a, b, n):
     """Elementwise max over the union of two edge sets (smore.py:153-174)."""
     ka = a[0] * n + a[1]
@@ -247,9 +273,14 @@ class SMORE(GeneralRecommender):
 
     # ---------------------------------------------------------------- graphs
     def _cached_knn(self, root, name, feat, k):
-        """kNN item graph (reference smore.py:45-75, cached like its image_adj_{k}.pt):
+        """kNN item graph (reference smore.py:45-75): the reference's own
+        {name}_adj_{k}_{sparse}.pt cache when the dataset directory holds one, else
         built on the device (knn_graph_device) or, with rsx_knn: host (the default when
         rsx_sampler is host), by the CPU restatement of the reference's build."""
+        # a cache the reference wrote for this dataset is the graph its runs trained on: use it
+        ref = load_reference_knn(os.path.join(root, f"{name}_adj_{k}_{self.sparse}.pt"), feat.shape[0])
+        if ref is not None:
+            return ref
         device_build = self.knn_mode == "device"
         path = os.path.join(root, f"rsx_{name}_knn_{k}{'_dev' if device_build else ''}.npz")
         f = feat.detach().cpu().numpy()

@@ -154,3 +154,36 @@ def test_canonical_topk_matches_reference_modulo_ties(golden):
     ties = z["init_valid_inner_tie"] | z["init_valid_boundary_tie"]
     same = np.all(idx == ref, axis=1)
     assert np.all(same | ties)
+
+
+def test_reference_knn_cache_is_read(golden, tmp_path):
+    """SMORE reads the kNN cache the reference writes (smore.py:46-47,56-62: torch.save of
+    the sparse [n_items, n_items] graph) through the safe loader; the graph it returns is
+    the reference's own, and the product's host build (knn_graph) equals it too."""
+    from rsx.smore import knn_graph, load_reference_knn
+
+    z = golden("smore_small")
+    ni = int(z["n_items"])
+    for name, feat, k in (("image_original_adj", "v_feat", 10), ("text_original_adj", "t_feat", 8)):
+        ref = coo_sorted(z[name + "_idx"], z[name + "_val"])
+        t = torch.sparse_coo_tensor(torch.from_numpy(z[name + "_idx"]), torch.from_numpy(z[name + "_val"]),
+                                    (ni, ni))
+        path = tmp_path / f"{name}_{k}_True.pt"
+        torch.save(t, path)
+        r, c, v = load_reference_knn(str(path), ni)
+        for x, y in zip(ref, coo_sorted(np.stack([r, c]), v)):
+            assert np.array_equal(x, y)
+        dense = tmp_path / f"{name}_{k}_False.pt"  # is_sparse False: the dense matrix
+        torch.save(t.to_dense(), dense)
+        r, c, v = load_reference_knn(str(dense), ni)
+        for x, y in zip(ref, coo_sorted(np.stack([r, c]), v)):
+            assert np.array_equal(x, y)
+        hr, hc, hv = knn_graph(z[feat], k)
+        for x, y in zip(ref, coo_sorted(np.stack([hr, hc]), hv)):
+            assert np.array_equal(x, y)
+    # absent, wrong shape, or not a tensor file: rebuilt instead
+    assert load_reference_knn(str(tmp_path / "missing.pt"), ni) is None
+    torch.save(torch.zeros(3, 3), tmp_path / "small.pt")
+    assert load_reference_knn(str(tmp_path / "small.pt"), ni) is None
+    (tmp_path / "junk.pt").write_bytes(b"not a torch file")
+    assert load_reference_knn(str(tmp_path / "junk.pt"), ni) is None
