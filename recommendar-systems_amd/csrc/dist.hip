@@ -29,12 +29,12 @@
 namespace rsx {
 
 int spmm_dispatch(const rsx_csr& a, const float* x, int d, const rsx_epilogue& e, float* slab, hipStream_t s);
+int spmm_dispatch_tagging(const rsx_csr& a, const float* x, int d, const rsx_epilogue& e, float* slab,
+                          hipStream_t s, const TagJob& tj);
 int rowwise_dispatch(int64_t n, int d, const rsx_epilogue& e, hipStream_t s);
 int bpr_call(int32_t variant, const float* fin, const float* ego, int64_t n_users, int64_t n_items, int32_t d,
              const int64_t* trip, int64_t batch, float reg, float batch_cfg, float* g_fin, float* g_ego,
              float* loss_out, double* loss_acc, void* ws, size_t ws_bytes, hipStream_t s, float g_div = 1.f);
-int tag_rows(const int64_t* trip, int64_t batch, int64_t n_users, int32_t* row_tag, int32_t tag, hipStream_t s,
-             const int32_t* tag_dev);
 
 namespace {
 
@@ -215,13 +215,21 @@ int sharded_stored_layers(const rsx_sharded_lgcn_step& st, bool train, hipStream
     float* bufs[2] = {st.h0, st.h1};
     hipEvent_t joins[4] = {};
     int rc = 0;
-    if (train) RSX_TRY(tag_rows(st.triplets, st.batch, nu, st.row_tag, tag, s, st.tag_dev));
-    // ---- forward
+    // ---- forward (the first item partial's launch also tags the batch rows when training)
     const float* x = st.p;
     for (int k = 1; k < K; ++k) {
         rsx_epilogue e = epi(RSX_EPI_STORE);
         e.y = bufs[k - 1] + off;
-        RSX_TRY(spmm_dispatch(*st.adj_i, x, d, e, st.slab_i, s));   // item partial of E^k
+        TagJob tj;
+        if (train && k == 1) {
+            tj.trip = st.triplets;
+            tj.batch = st.batch;
+            tj.n_users = nu;
+            tj.row_tag = st.row_tag;
+            tj.tag = tag;
+            tj.tag_dev = st.tag_dev;
+        }
+        RSX_TRY(spmm_dispatch_tagging(*st.adj_i, x, d, e, st.slab_i, s, tj));   // item partial of E^k
         if (!(joins[k] = exchange(st.comm, bufs[k - 1] + off, ni * d, s, &rc))) return rc;
         if (k >= 2) RSX_TRY(wait(s, joins[k - 1]));                  // E^{k-1} items summed
         e.y = bufs[k - 1];

@@ -43,4 +43,15 @@ inline int hip_rc(hipError_t e) { return static_cast<int>(e); }
 inline int last_rc() { return static_cast<int>(hipGetLastError()); }
 inline hipStream_t as_stream(rsx_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
 
+// Batch-row tagging carried by an SpMM launch (extra blocks after the work and
+// fixup blocks): row_tag[u] = row_tag[n_users + i] = tag for every triplet.
+struct TagJob {
+    const int64_t* trip = nullptr;  // [3, batch]
+    int64_t batch = 0;
+    int64_t n_users = 0;
+    int32_t* row_tag = nullptr;
+    int32_t tag = 0;
+    const int32_t* tag_dev = nullptr;  // device tag word (graph replays), else `tag`
+};
+
 }  // namespace rsx

@@ -501,10 +501,22 @@ __device__ __forceinline__ void spmm_item(const rsx_csr& a, const float* __restr
 template <int D, int KIND>
 __global__ RSX_SPMM_ATTR __launch_bounds__(kBlock) void spmm_main(rsx_csr a, const float* __restrict__ x,
                                                                   rsx_epilogue e, float* __restrict__ slab,
-                                                                  int64_t n_main, int fix_only) {
+                                                                  int64_t n_main, int fix_only, TagJob tj) {
     constexpr int G = D / 4;
     constexpr int GPB = kBlock / G;
     const int li = threadIdx.x % G;
+    if (tj.batch > 0) {  // the last blocks tag the batch rows (nothing in this launch reads row_tag)
+        const int64_t n_tag = (3 * tj.batch + kBlock - 1) / kBlock;
+        const int64_t tb = (int64_t)blockIdx.x - ((int64_t)gridDim.x - n_tag);
+        if (tb >= 0) {
+            const int64_t t = tb * kBlock + threadIdx.x;
+            if (t < 3 * tj.batch) {
+                const int64_t id = tj.trip[t];
+                tj.row_tag[t < tj.batch ? id : tj.n_users + id] = tj.tag_dev ? *tj.tag_dev : tj.tag;
+            }
+            return;
+        }
+    }
     if (fix_only) {
         fixup_block<D, KIND>(a, e, slab, (int64_t)blockIdx.x);
         return;
@@ -559,17 +571,19 @@ constexpr int64_t kInlineFixups = 1024;
 
 template <int D, int KIND>
 static int launch_spmm(const rsx_csr& a, const float* x, const rsx_epilogue& e, float* slab,
-                       hipStream_t s) {
+                       hipStream_t s, const TagJob& tj) {
     constexpr int GPB = kBlock / (D / 4);
     int64_t n_main = (a.n_work + GPB - 1) / GPB;
     if (n_main > spmm_max_blocks()) n_main = spmm_max_blocks();
     const bool inl = a.n_long <= kInlineFixups;
-    const int64_t nb = n_main + (inl ? a.n_long : 0);
+    const int64_t n_tag = tj.batch > 0 ? (3 * tj.batch + kBlock - 1) / kBlock : 0;
+    const int64_t nb = n_main + (inl ? a.n_long : 0) + n_tag;
     if (nb > 0)
-        hipLaunchKernelGGL((spmm_main<D, KIND>), dim3((unsigned)nb), dim3(kBlock), 0, s, a, x, e, slab, n_main, 0);
+        hipLaunchKernelGGL((spmm_main<D, KIND>), dim3((unsigned)nb), dim3(kBlock), 0, s, a, x, e, slab, n_main, 0,
+                           tj);
     if (!inl)
         hipLaunchKernelGGL((spmm_main<D, KIND>), dim3((unsigned)a.n_long), dim3(kBlock), 0, s, a, x, e, slab,
-                           n_main, 1);
+                           n_main, 1, TagJob{});
     return last_rc();
 }
 
@@ -583,16 +597,17 @@ static int launch_rowwise(int64_t n, const rsx_epilogue& e, hipStream_t s) {
 }
 
 template <int D>
-static int spmm_d(const rsx_csr& a, const float* x, const rsx_epilogue& e, float* slab, hipStream_t s) {
+static int spmm_d(const rsx_csr& a, const float* x, const rsx_epilogue& e, float* slab, hipStream_t s,
+                  const TagJob& tj) {
     switch (e.kind) {
-        case RSX_EPI_STORE: return launch_spmm<D, RSX_EPI_STORE>(a, x, e, slab, s);
-        case RSX_EPI_LAYERSUM: return launch_spmm<D, RSX_EPI_LAYERSUM>(a, x, e, slab, s);
-        case RSX_EPI_FINAL: return launch_spmm<D, RSX_EPI_FINAL>(a, x, e, slab, s);
-        case RSX_EPI_ADAM: return launch_spmm<D, RSX_EPI_ADAM>(a, x, e, slab, s);
-        case RSX_EPI_LAYERGCN: return launch_spmm<D, RSX_EPI_LAYERGCN>(a, x, e, slab, s);
-        case RSX_EPI_AXPBY: return launch_spmm<D, RSX_EPI_AXPBY>(a, x, e, slab, s);
-        case RSX_EPI_LAYERGCN_BWD: return launch_spmm<D, RSX_EPI_LAYERGCN_BWD>(a, x, e, slab, s);
-        case RSX_EPI_ADD: return launch_spmm<D, RSX_EPI_ADD>(a, x, e, slab, s);
+        case RSX_EPI_STORE: return launch_spmm<D, RSX_EPI_STORE>(a, x, e, slab, s, tj);
+        case RSX_EPI_LAYERSUM: return launch_spmm<D, RSX_EPI_LAYERSUM>(a, x, e, slab, s, tj);
+        case RSX_EPI_FINAL: return launch_spmm<D, RSX_EPI_FINAL>(a, x, e, slab, s, tj);
+        case RSX_EPI_ADAM: return launch_spmm<D, RSX_EPI_ADAM>(a, x, e, slab, s, tj);
+        case RSX_EPI_LAYERGCN: return launch_spmm<D, RSX_EPI_LAYERGCN>(a, x, e, slab, s, tj);
+        case RSX_EPI_AXPBY: return launch_spmm<D, RSX_EPI_AXPBY>(a, x, e, slab, s, tj);
+        case RSX_EPI_LAYERGCN_BWD: return launch_spmm<D, RSX_EPI_LAYERGCN_BWD>(a, x, e, slab, s, tj);
+        case RSX_EPI_ADD: return launch_spmm<D, RSX_EPI_ADD>(a, x, e, slab, s, tj);
         default: return RSX_ERR_ARG;
     }
 }
@@ -612,16 +627,23 @@ static int rowwise_d(int64_t n, const rsx_epilogue& e, hipStream_t s) {
     }
 }
 
-int spmm_dispatch(const rsx_csr& a, const float* x, int d, const rsx_epilogue& e, float* slab,
-                  hipStream_t s) {
+// `tj`: the launch also tags the batch rows (internal: the step's first forward layer)
+int spmm_dispatch_tagging(const rsx_csr& a, const float* x, int d, const rsx_epilogue& e, float* slab,
+                          hipStream_t s, const TagJob& tj) {
     if (a.n_long > 0 && !slab) return RSX_ERR_WORKSPACE;
+    if (tj.batch > 0 && (!tj.trip || !tj.row_tag)) return RSX_ERR_ARG;
     switch (d) {
-        case 32: return spmm_d<32>(a, x, e, slab, s);
-        case 64: return spmm_d<64>(a, x, e, slab, s);
-        case 128: return spmm_d<128>(a, x, e, slab, s);
-        case 256: return spmm_d<256>(a, x, e, slab, s);
+        case 32: return spmm_d<32>(a, x, e, slab, s, tj);
+        case 64: return spmm_d<64>(a, x, e, slab, s, tj);
+        case 128: return spmm_d<128>(a, x, e, slab, s, tj);
+        case 256: return spmm_d<256>(a, x, e, slab, s, tj);
         default: return RSX_ERR_UNSUPPORTED;
     }
+}
+
+int spmm_dispatch(const rsx_csr& a, const float* x, int d, const rsx_epilogue& e, float* slab,
+                  hipStream_t s) {
+    return spmm_dispatch_tagging(a, x, d, e, slab, s, TagJob{});
 }
 
 int rowwise_dispatch(int64_t n, int d, const rsx_epilogue& e, hipStream_t s) {

@@ -25,6 +25,8 @@
 namespace rsx {
 
 int spmm_dispatch(const rsx_csr& a, const float* x, int d, const rsx_epilogue& e, float* slab, hipStream_t s);
+int spmm_dispatch_tagging(const rsx_csr& a, const float* x, int d, const rsx_epilogue& e, float* slab,
+                          hipStream_t s, const TagJob& tj);
 int rowwise_dispatch(int64_t n, int d, const rsx_epilogue& e, hipStream_t s);
 int bpr_call(int32_t variant, const float* fin, const float* ego, int64_t n_users, int64_t n_items, int32_t d,
              const int64_t* trip, int64_t batch, float reg, float batch_cfg, float* g_fin, float* g_ego,
@@ -200,7 +202,15 @@ static int lgcn_step_stored_layers(const rsx_lgcn_step& st, int64_t batch, int32
     for (int k = 1; k < K; ++k) {
         rsx_epilogue e = epi0(RSX_EPI_STORE);
         e.y = bufs[k - 1];
-        if ((rc = spmm_dispatch(A, x, d, e, st.slab, s))) return rc;
+        TagJob tj;  // layer 1 also tags the batch rows (nothing reads the tags before the last layer)
+        if (k == 1) {
+            tj.trip = st.triplets;
+            tj.batch = batch;
+            tj.n_users = st.n_users;
+            tj.row_tag = st.row_tag;
+            tj.tag = tag;
+        }
+        if ((rc = spmm_dispatch_tagging(A, x, d, e, st.slab, s, tj))) return rc;
         x = bufs[k - 1];
     }
     {
@@ -326,9 +336,9 @@ int rsx_lightgcn_step(const rsx_lgcn_step* st, rsx_stream_t stream) {
     const int32_t tag = (int32_t)st->tag;
     if (tags) {
         if (st->tag <= 0 || st->tag > INT32_MAX) return RSX_ERR_ARG;
+        if (K <= 3) return lgcn_step_stored_layers(*st, batch, tag, s);  // tags written by its layer 1
         if ((rc = tag_rows(st->triplets, batch, st->n_users, st->row_tag, tag, s, nullptr))) return rc;
     }
-    if (tags && K <= 3) return lgcn_step_stored_layers(*st, batch, tag, s);
     // forward (dense path: the last layer zeroes g and r)
     if ((rc = lgcn_forward(A, d, K, st->p, st->s, st->h0, st->h1, st->final_emb, st->slab, tags ? nullptr : st->g,
                            tags ? nullptr : st->r, s, tags ? st->row_tag : nullptr, tag)))
