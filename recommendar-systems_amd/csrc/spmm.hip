@@ -112,8 +112,17 @@ __device__ __forceinline__ EpiIn epi_load(const rsx_epilogue& e, int64_t row, in
     return in;
 }
 
+// Adam's per-launch constants (two f64 pows of the step count): evaluated once per
+// thread, not once per row
+template <int KIND>
+__device__ __forceinline__ AdamConst adam_for(const rsx_epilogue& e) {
+    if constexpr (KIND == RSX_EPI_ADAM) return adam_const(e.adam);
+    else return AdamConst{};
+}
+
 template <int KIND, int D>
-__device__ __forceinline__ void epilogue(const rsx_epilogue& e, int64_t row, float4 acc, int li, const EpiIn& in) {
+__device__ __forceinline__ void epilogue(const rsx_epilogue& e, int64_t row, float4 acc, int li, const EpiIn& in,
+                                         const AdamConst& c) {
     constexpr int G = D / 4;
     const int64_t off = row * D + li * 4;
     acc = mul4(e.alpha, acc);
@@ -144,7 +153,6 @@ __device__ __forceinline__ void epilogue(const rsx_epilogue& e, int64_t row, flo
         g = mul4(e.beta, g);
         if (e.reg_cnt) g = add4(g, mul4(in.regc, in.c));  // sum over occurrences of k * ego row
         else if (e.r_add) g = add4(g, in.b);
-        const AdamConst c = adam_const(e.adam);
         float4 p = in.c, m = in.d, v = in.e;
         g.x = adam_elem(c, p.x, m.x, v.x, g.x);
         g.y = adam_elem(c, p.y, m.y, v.y, g.y);
@@ -209,7 +217,7 @@ __device__ __forceinline__ void epilogue(const rsx_epilogue& e, int64_t row, flo
 
 template <int KIND, int D>
 __device__ __forceinline__ void epilogue(const rsx_epilogue& e, int64_t row, float4 acc, int li) {
-    epilogue<KIND, D>(e, row, acc, li, epi_load<KIND, D>(e, row, li));
+    epilogue<KIND, D>(e, row, acc, li, epi_load<KIND, D>(e, row, li), adam_for<KIND>(e));
 }
 
 // ---------------------------------------------------------------------------
@@ -300,7 +308,7 @@ __device__ __forceinline__ void fixup_block(const rsx_csr& a, const rsx_epilogue
 #pragma unroll 4
         for (int g = 1; g < GPB; ++g) acc = add4(acc, part[g][li]);
         if (!ok) acc = f4(__builtin_nanf(""));  // producers never arrived: poison the row
-        epilogue<KIND, D>(e, lr.x, acc, li, pre);
+        epilogue<KIND, D>(e, lr.x, acc, li, pre, adam_for<KIND>(e));
     }
     if (threadIdx.x == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -371,7 +379,7 @@ struct NextCV {
 template <int D, int KIND>
 __device__ __forceinline__ void spmm_item(const rsx_csr& a, const float* __restrict__ x, const rsx_epilogue& e,
                                           float* __restrict__ slab, int4 wk, int li, NextCV& pf, int4 nxt,
-                                          bool has_nxt) {
+                                          bool has_nxt, const AdamConst& ac) {
     const int tf = tag_flags(e);
     const bool have_pf = pf.ok;
     pf.ok = false;
@@ -480,7 +488,7 @@ __device__ __forceinline__ void spmm_item(const rsx_csr& a, const float* __restr
         }
     }
     if (wk.y < 0) {
-        epilogue<KIND, D>(e, wk.x, acc, li, pre);
+        epilogue<KIND, D>(e, wk.x, acc, li, pre, ac);
     } else {
         // partial of long row wk.x: written through the (per-XCD, non-coherent) L2,
         // drained (vmcnt(0)), then counted by one lane of the group; the row's fixup
@@ -531,10 +539,11 @@ __global__ RSX_SPMM_ATTR __launch_bounds__(kBlock) void spmm_main(rsx_csr a, con
     const int4* work = reinterpret_cast<const int4*>(a.work);
     int4 wk = work[w];
     NextCV pf = {0, 0.f, false};
+    const AdamConst ac = adam_for<KIND>(e);
     for (;;) {
         const int64_t wn = w + stride;
         const int4 nxt = wn < a.n_work ? work[wn] : make_int4(0, 0, 0, 0);
-        spmm_item<D, KIND>(a, x, e, slab, wk, li, pf, nxt, wn < a.n_work);
+        spmm_item<D, KIND>(a, x, e, slab, wk, li, pf, nxt, wn < a.n_work, ac);
         if (wn >= a.n_work) break;
         w = wn;
         wk = nxt;
