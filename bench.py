@@ -422,7 +422,7 @@ def main():
     achieved = alg / (spmm_ms * 1e-3) / 1e9
     traffic = None
     tfile = os.path.join(HERE, "profiles", "spmm_traffic.json")
-    if os.path.exists(tfile) and not big:  # PMC bytes measured for the C2 launch
+    if os.path.exists(tfile) and not big and not sharded:  # PMC bytes measured for the single C2 launch
         try:
             traffic = json.load(open(tfile)).get("bytes_per_launch")
         except Exception:  # noqa: BLE001
