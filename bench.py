@@ -378,7 +378,8 @@ def main():
     vlen = np.bincount(np.searchsorted(vusers, v_u), minlength=vusers.size)
     erp = torch.from_numpy(np.concatenate([[0], np.cumsum(vlen)]).astype(np.int64)).to(dev)
     ecol = torch.from_numpy(v_i.astype(np.int32)).to(dev)
-    gain = torch.from_numpy(1.0 / np.log2(np.arange(1, 51, dtype=np.float64) + 1)).to(dev)
+    n_pos = int(v_i.size)
+    from rsx.evaluator import device_metric_dict
 
     def evaluate():
         # what Trainer.evaluate does: forward once, one fused scores+mask+top-50 launch over
@@ -386,7 +387,7 @@ def main():
         eng.invalidate()
         f = eng.forward()
         _, idx = ops.fullsort_topk(f[:nu], vu_d, f[nu:], rp_d, mc_d, 50)
-        ops.topk_metrics(idx, erp, ecol, [5, 10, 20, 50], gain).cpu()
+        device_metric_dict(idx, erp, ecol, ["recall", "ndcg", "precision", "map"], [5, 10, 20, 50], n_pos)
 
     evaluate()
     torch.cuda.synchronize()

@@ -157,6 +157,49 @@ __global__ __launch_bounds__(kSumThreads) void metrics_sum_lds(const double* __r
     if (wave == 0 && lane < m) out[lane] = s;
 }
 
+// Fast form: the same column sums in a fixed PARALLEL order (per-thread strided
+// partials, a wave butterfly, the block's 16 wave sums in order): deterministic,
+// not numpy's order.  Summation-tree depth h = ceil(n/1024) + 6 + 16, so
+// |fast - sequential| <= (gamma_h + gamma_{n-1}) * sum|x| (all values are >= 0):
+// the caller rounds to 4 decimals and re-runs the sequential kernels only when a
+// mean lies within that bound of a rounding boundary (rsx/evaluator.py).
+constexpr int kParCols = 8;
+constexpr int kParThreads = 1024;
+__global__ __launch_bounds__(kParThreads) void metrics_sum_par(const double* __restrict__ vals, int64_t n, int m,
+                                                              double* __restrict__ out) {
+    const int c0 = blockIdx.x * kParCols;
+    const int nc = (m - c0) < kParCols ? (m - c0) : kParCols;
+    double s[kParCols];
+#pragma unroll
+    for (int j = 0; j < kParCols; ++j) s[j] = 0.0;
+    for (int64_t u = threadIdx.x; u < n; u += kParThreads) {
+        const double* r = vals + u * m + c0;
+#pragma unroll
+        for (int j = 0; j < kParCols; ++j)
+            if (j < nc) s[j] += r[j];
+    }
+    // butterfly: every lane ends with the same bits (a + b == b + a in IEEE)
+#pragma unroll
+    for (int j = 0; j < kParCols; ++j)
+#pragma unroll
+        for (int o = kWave / 2; o > 0; o >>= 1) s[j] += __shfl_xor(s[j], o, kWave);
+    __shared__ double part[kParThreads / kWave][kParCols];
+    const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+    if (lane == 0)
+#pragma unroll
+        for (int j = 0; j < kParCols; ++j) part[wave][j] = s[j];
+    __syncthreads();
+    if ((int)threadIdx.x < nc) {
+        double t = 0.0;
+        for (int w = 0; w < kParThreads / kWave; ++w) t += part[w][threadIdx.x];
+        out[c0 + threadIdx.x] = t;
+    }
+}
+
+static int topk_metrics_impl(const int64_t* topk_idx, int64_t n_users, int32_t k_max, const int64_t* eval_rowptr,
+                             const int32_t* eval_col, const int32_t* cutoffs, int32_t n_cut, const double* gain,
+                             double* out_sums, void* ws, size_t ws_bytes, hipStream_t s, bool fast);
+
 }  // namespace rsx
 
 using namespace rsx;
@@ -165,21 +208,39 @@ extern "C" size_t rsx_topk_metrics_ws_bytes(int64_t n_users, int32_t n_cut) {
     return (size_t)(n_users > 0 ? n_users : 0) * kMetricCols * (size_t)(n_cut > 0 ? n_cut : 0) * sizeof(double);
 }
 
-extern "C" int rsx_topk_metrics(const int64_t* topk_idx, int64_t n_users, int32_t k_max, const int64_t* eval_rowptr,
-                                const int32_t* eval_col, const int32_t* cutoffs, int32_t n_cut, const double* gain,
-                                double* out_sums, void* ws, size_t ws_bytes, rsx_stream_t stream) {
+static int rsx::topk_metrics_impl(const int64_t* topk_idx, int64_t n_users, int32_t k_max,
+                                  const int64_t* eval_rowptr, const int32_t* eval_col, const int32_t* cutoffs,
+                                  int32_t n_cut, const double* gain, double* out_sums, void* ws, size_t ws_bytes,
+                                  hipStream_t s, bool fast) {
     if (n_users < 0 || k_max <= 0 || n_cut <= 0 || !cutoffs || !gain || !out_sums) return RSX_ERR_ARG;
     if (n_users > 0 && (!topk_idx || !eval_rowptr || !eval_col)) return RSX_ERR_ARG;
     if (ws_bytes < rsx_topk_metrics_ws_bytes(n_users, n_cut) || (n_users > 0 && !ws)) return RSX_ERR_WORKSPACE;
-    hipStream_t s = as_stream(stream);
     const int m = kMetricCols * n_cut;
     double* vals = static_cast<double*>(ws);
     if (n_users > 0)
         hipLaunchKernelGGL(metrics_user, dim3((unsigned)((n_users + 255) / 256)), dim3(256), 0, s, topk_idx, n_users,
                            (int)k_max, eval_rowptr, eval_col, cutoffs, (int)n_cut, gain, vals);
-    if (m <= kWave)
+    if (fast)
+        hipLaunchKernelGGL(metrics_sum_par, dim3((unsigned)((m + kParCols - 1) / kParCols)), dim3(kParThreads), 0, s,
+                           vals, n_users, m, out_sums);
+    else if (m <= kWave)
         hipLaunchKernelGGL(metrics_sum_lds, dim3(1), dim3(kSumThreads), 0, s, vals, n_users, m, out_sums);
     else
         hipLaunchKernelGGL(metrics_sum, dim3((unsigned)m), dim3(64), 0, s, vals, n_users, m, out_sums);
     return last_rc();
+}
+
+extern "C" int rsx_topk_metrics(const int64_t* topk_idx, int64_t n_users, int32_t k_max, const int64_t* eval_rowptr,
+                                const int32_t* eval_col, const int32_t* cutoffs, int32_t n_cut, const double* gain,
+                                double* out_sums, void* ws, size_t ws_bytes, rsx_stream_t stream) {
+    return topk_metrics_impl(topk_idx, n_users, k_max, eval_rowptr, eval_col, cutoffs, n_cut, gain, out_sums, ws,
+                             ws_bytes, as_stream(stream), false);
+}
+
+extern "C" int rsx_topk_metrics_fast(const int64_t* topk_idx, int64_t n_users, int32_t k_max,
+                                     const int64_t* eval_rowptr, const int32_t* eval_col, const int32_t* cutoffs,
+                                     int32_t n_cut, const double* gain, double* out_sums, void* ws, size_t ws_bytes,
+                                     rsx_stream_t stream) {
+    return topk_metrics_impl(topk_idx, n_users, k_max, eval_rowptr, eval_col, cutoffs, n_cut, gain, out_sums, ws,
+                             ws_bytes, as_stream(stream), true);
 }

@@ -53,6 +53,7 @@ the last one — 2K SpMM launches + one item Adam per step instead of 2K SpMMs +
 from __future__ import annotations
 
 import ctypes as C
+import gc
 import os
 
 import numpy as np
@@ -246,6 +247,8 @@ class ShardedLightGCNEngine:
             self._trip_buf.copy_(trip)
             st.triplets, st.batch = self._trip_buf.data_ptr(), B
             g = torch.cuda.CUDAGraph()
+            gc_on = gc.isenabled()
+            gc.disable()  # no finalizers inside the capture (see rsx/trainer.py:_capture)
             try:
                 with torch.cuda.graph(g):
                     self._step_dev.add_(1)
@@ -255,6 +258,10 @@ class ShardedLightGCNEngine:
                 torch.cuda.synchronize()
             else:
                 self._graph, self._graph_lr = g, self.lr
+            finally:
+                if gc_on:
+                    gc.enable()
+            if self._graph is g:
                 g.replay()
                 return
         t = trip.contiguous()

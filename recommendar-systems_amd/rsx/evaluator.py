@@ -113,32 +113,75 @@ class TopKEvaluator:
         return self.evaluate_arrays(topk.cpu().numpy(), eval_data.get_eval_items(), eval_data.get_eval_len_list())
 
     def evaluate_device(self, topk, eval_data) -> dict:
-        """The same dict from device-resident top-k lists (rsx_topk_metrics): hits by
-        binary search in each user's sorted held-out items, per-user float64 values,
-        user-ordered column sums (= numpy's mean(axis=0) order), then the reference's
-        division and round(., 4) here.  One [5, n_cut] float64 copy to the host."""
-        import torch
-
-        from . import ops
-
-        k = topk.shape[1]
-        cuts = sorted(set(int(c) for c in self.topk))
-        if cuts[-1] > k:
-            raise ValueError(f"topk {cuts[-1]} > ranked list length {k}")
-        ranks = np.arange(1, k + 1, dtype=np.float64)
-        gain = torch.from_numpy(1.0 / np.log2(ranks + 1)).to(topk.device)   # as metrics.py ndcg
+        """The same dict from device-resident top-k lists (device_metric_dict)."""
         erp, ecol = eval_data.eval_csr()
-        sums = ops.topk_metrics(topk, erp, ecol, cuts, gain).cpu().numpy()
-        n = topk.shape[0]
         pos_total = int(np.asarray(eval_data.get_eval_len_list()).sum())
-        col = {c: j for j, c in enumerate(cuts)}
-        rows = {"recall": 0, "precision": 1, "ndcg": 2, "map": 3}
-        out = {}
-        for m in self.metrics:
-            for kk in self.topk:
-                j = col[int(kk)]
-                v = sums[4, j] / np.float64(pos_total) if m == "recall2" else sums[rows[m], j] / np.float64(n)
-                # numpy's round on the float64, as the reference's round(value[k - 1], 4)
-                # (scale, round half to even): 0.05875 -> 0.0588, where float rounding gives 0.0587
-                out[f"{m}@{kk}"] = float(round(np.float64(v), 4))
-        return out
+        return device_metric_dict(topk, erp, ecol, self.metrics, self.topk, pos_total)
+
+
+_U = 2.0 ** -53
+
+
+def sum_order_bound(n: int, total: float) -> float:
+    """Bound on |parallel-order sum - user-order sum| of n values >= 0 summing to
+    about `total` (rsx_topk_metrics_fast, include/rsx.h): (gamma_h + gamma_{n-1}) *
+    sum, h = ceil(n/1024) + 22 the parallel tree's depth, gamma_j = j u / (1 - j u)."""
+    j = (n - 1) + (-(-n // 1024) + 22)
+    return j * _U / (1.0 - j * _U) * np.abs(total) * 1.0001
+
+
+def device_metric_dict(topk, erp, ecol, metrics, topk_list, pos_total: int) -> dict:
+    """The reference's metric dict from device-resident top-k lists: hits by binary
+    search in each user's sorted held-out items, per-user float64 values and their
+    column sums on the device (rsx_topk_metrics_fast: a fixed parallel order), then
+    the reference's division and round(., 4) here.  Every mean whose rounding could
+    differ between that order and numpy's user order (mean(axis=0)) -- one within
+    sum_order_bound of a 4-decimal rounding step, for any realistic n a 1e-9-level
+    event -- sends the dict through the user-ordered sums (rsx_topk_metrics), so the
+    dict always equals the one from the sequential sums.  One [5, n_cut] float64
+    copy to the host per pass."""
+    import torch
+
+    from . import ops
+
+    k = topk.shape[1]
+    cuts = sorted(set(int(c) for c in topk_list))
+    if cuts[-1] > k:
+        raise ValueError(f"topk {cuts[-1]} > ranked list length {k}")
+    gain = _gain(k, topk.device)
+    n = topk.shape[0]
+    col = {c: j for j, c in enumerate(cuts)}
+    rows = {"recall": 0, "precision": 1, "ndcg": 2, "map": 3, "recall2": 4}
+    keys = [(m, kk) for m in metrics for kk in topk_list]
+    ri = np.array([rows[m] for m, _ in keys], dtype=np.int64)
+    ci = np.array([col[int(kk)] for _, kk in keys], dtype=np.int64)
+    den = np.array([pos_total if m == "recall2" else n for m, _ in keys], dtype=np.float64)
+    for exact in (False, True):
+        sums = ops.topk_metrics(topk, erp, ecol, cuts, gain, exact=exact).cpu().numpy()
+        s = sums[ri, ci]
+        v = s / den
+        # numpy's round on the float64s, as the reference's round(value[k - 1], 4)
+        # (scale, round half to even): 0.05875 -> 0.0588, where float rounding gives 0.0587
+        r = np.round(v, 4)
+        if not exact:
+            # the division rounds once more: relative u on either side
+            b = sum_order_bound(n, s) / den + 4 * _U * np.abs(v)
+            if not np.array_equal(np.round(v - b, 4), np.round(v + b, 4)):
+                continue  # a mean within the order bound of a rounding step: user-order sums
+        return {f"{m}@{kk}": float(x) for (m, kk), x in zip(keys, r)}
+    raise AssertionError("unreachable")
+
+
+_GAIN = {}
+
+
+def _gain(k: int, device):
+    """1/log2(r+1), r = 1..k, as metrics.py's ndcg computes it (cached per device)."""
+    import torch
+
+    key = (k, str(device))
+    g = _GAIN.get(key)
+    if g is None:
+        ranks = np.arange(1, k + 1, dtype=np.float64)
+        g = _GAIN[key] = torch.from_numpy(1.0 / np.log2(ranks + 1)).to(device)
+    return g

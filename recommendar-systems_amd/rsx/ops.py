@@ -261,10 +261,12 @@ def fullsort_topk(user_emb: torch.Tensor, users: torch.Tensor | None, item_emb: 
 
 
 def topk_metrics(topk_idx: torch.Tensor, eval_rowptr: torch.Tensor, eval_col: torch.Tensor, cutoffs,
-                 gain: torch.Tensor) -> torch.Tensor:
+                 gain: torch.Tensor, exact: bool = True) -> torch.Tensor:
     """Per-cutoff sums over users of recall, precision, ndcg, map and hit count
     (rsx_topk_metrics; reference topk_evaluator.py:58-102 + metrics.py:12-118).
-    Returns a float64 device tensor [5, len(cutoffs)]."""
+    Returns a float64 device tensor [5, len(cutoffs)].  exact: summed in user
+    order (numpy's mean(axis=0) order, bit for bit); else in a fixed parallel order
+    (rsx_topk_metrics_fast, within evaluator.sum_order_bound of it)."""
     _gpu(topk_idx, eval_rowptr, eval_col, gain)
     if topk_idx.dtype != torch.int64 or topk_idx.dim() != 2:
         raise RuntimeError("topk_metrics: topk_idx must be int64 [n_users, k]")
@@ -275,8 +277,9 @@ def topk_metrics(topk_idx: torch.Tensor, eval_rowptr: torch.Tensor, eval_col: to
     out = torch.empty(5, cut.numel(), dtype=torch.float64, device=dev)
     lib = L.lib()
     ws = _ws(dev, lib.rsx_topk_metrics_ws_bytes(n, cut.numel()))
-    L.check(lib.rsx_topk_metrics(_p(topk_idx), n, k, _p(eval_rowptr), _p(eval_col), _p(cut), cut.numel(), _p(gain),
-                                 _p(out), _p(ws), ws.numel(), _stream()), "rsx_topk_metrics")
+    fn = lib.rsx_topk_metrics if exact else lib.rsx_topk_metrics_fast
+    L.check(fn(_p(topk_idx), n, k, _p(eval_rowptr), _p(eval_col), _p(cut), cut.numel(), _p(gain),
+               _p(out), _p(ws), ws.numel(), _stream()), "rsx_topk_metrics")
     return out
 
 

@@ -22,6 +22,7 @@ TopKEvaluator (vectorised hit matrix, same metric values).
 """
 from __future__ import annotations
 
+import gc
 import itertools
 import os
 from logging import getLogger
@@ -152,12 +153,22 @@ class _GraphStep:
         g = torch.cuda.CUDAGraph()
         if os.environ.get("RSX_GRAPH_DEBUG"):
             print(f"[graph] capture at global_step={before}", flush=True)
-        with torch.cuda.graph(g):
-            losses, loss = self.t._train_batch(static, 0, self.loss_func)
-            # detached: graph outputs that keep the captured autograd graph alive
-            # would hold its AccumulateGrad nodes into the next capture
-            out = (tuple(x.detach() for x in losses) if isinstance(losses, tuple) else losses.detach(),
-                   loss.detach())
+        # no cyclic GC inside the capture: a finalizer of some unrelated object (a
+        # CUDA graph or stream-ordered buffer of an earlier run) that issues a HIP call
+        # forbidden while a stream captures would abort the process
+        # (torch.cuda.graph collects once on entry)
+        gc_on = gc.isenabled()
+        gc.disable()
+        try:
+            with torch.cuda.graph(g):
+                losses, loss = self.t._train_batch(static, 0, self.loss_func)
+                # detached: graph outputs that keep the captured autograd graph alive
+                # would hold its AccumulateGrad nodes into the next capture
+                out = (tuple(x.detach() for x in losses) if isinstance(losses, tuple) else losses.detach(),
+                       loss.detach())
+        finally:
+            if gc_on:
+                gc.enable()
         return dict(graph=g, static=static, out=out, mg=getattr(self.t, "_mg_last", None),
                     dstep=int(getattr(m, "global_step", 0)) - before)
 

@@ -97,3 +97,35 @@ def test_evaluator_matches_reference_metrics(golden, fx):
         items = eval_lists(z, split)
         out = ev.evaluate_arrays(z[tag + "_topk_idx"].astype(np.int64), items, z[split + "_eval_len"])
         assert out == metric_dict(z, tag), tag
+
+
+def test_device_metric_dict_falls_back_to_user_order_sums(monkeypatch):
+    """device_metric_dict rounds the parallel-order sums and re-runs the user-ordered
+    ones only when a mean lies within sum_order_bound of a 4-decimal rounding step."""
+    import torch
+
+    from rsx import evaluator as E
+    from rsx import ops
+
+    n = 1000
+    calls = []
+
+    def fake(topk, erp, ecol, cuts, gain, exact=True):
+        calls.append(exact)
+        s = np.zeros((5, len(cuts)))
+        s[0, 0] = state["fast"] if not exact else state["exact"]
+        return torch.from_numpy(s)
+
+    monkeypatch.setattr(ops, "topk_metrics", fake)
+    topk = torch.zeros(n, 5, dtype=torch.int64)
+    # far from a rounding step: one pass
+    state = {"fast": 0.123456 * n, "exact": 0.0}
+    assert E.device_metric_dict(topk, None, None, ["recall"], [5], 10)["recall@5"] == 0.1235
+    assert calls == [False]
+    # mean 0.12345 (+1e-15): both sides of the step are within the bound -> user-order sums decide
+    calls.clear()
+    state = {"fast": 0.12345 * n + 1e-12, "exact": 0.12345 * n - 1e-12}
+    got = E.device_metric_dict(topk, None, None, ["recall"], [5], 10)["recall@5"]
+    assert calls == [False, True]
+    assert got == float(round(np.float64(state["exact"] / n), 4))
+    assert E.sum_order_bound(n, 1.0) < 1e-12

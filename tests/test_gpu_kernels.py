@@ -324,6 +324,21 @@ def test_topk_metrics_device_bitwise_vs_numpy(cuda):
     want2 = E.recall2(hit, pos)
     for j, c in enumerate(cuts):
         assert sums[4, j] / pos.sum() == want2[c - 1]
+    # the parallel-order sums (rsx_topk_metrics_fast): deterministic, within the
+    # stated bound of the user-order sums, the same rounded dict
+    args = (torch.from_numpy(topk.astype(np.int64)).to(cuda), *stub.eval_csr(), cuts, gain)
+    fast = ops.topk_metrics(*args, exact=False).cpu().numpy()
+    assert np.array_equal(fast, ops.topk_metrics(*args, exact=False).cpu().numpy())
+    assert np.array_equal(fast[4], sums[4])  # integer hit counts: exact in any order
+    for row in range(4):
+        for j in range(len(cuts)):
+            assert abs(fast[row, j] - sums[row, j]) <= E.sum_order_bound(n, sums[row, j])
+    metrics = ["recall", "recall2", "precision", "ndcg", "map"]
+    got = E.device_metric_dict(args[0], *stub.eval_csr(), metrics, cuts, int(pos.sum()))
+    for m, fn in zip(metrics, (E.recall, E.recall2, E.precision, E.ndcg, E.average_precision)):
+        want = fn(hit, pos)
+        for c in cuts:
+            assert got[f"{m}@{c}"] == float(round(np.float64(want[c - 1]), 4)), (m, c)
 
 
 @pytest.mark.parametrize("seed", [0, 1])
