@@ -421,9 +421,11 @@ int rsx_topk_metrics(const int64_t* topk_idx, int64_t n_users, int32_t k_max,
                      double* out_sums, void* ws, size_t ws_bytes, rsx_stream_t stream);
 /*
  * Same arguments and outputs, but each column summed in a fixed parallel order
- * (per-thread strided partials over 1024 threads, a 64-lane butterfly, 16 wave
- * sums in order): deterministic, and within (gamma_h + gamma_{n_users-1}) * sum
- * of the sequential sums, h = ceil(n_users/1024) + 22, gamma_j = j*2^-53/(1-j*2^-53)
+ * (nblk = min(1024, max(1, ceil(n_users/256))) blocks of 256 threads with
+ * grid-strided users, a 64-lane butterfly and 4 wave sums per block; then per
+ * column one wave over the nblk block sums and a butterfly): deterministic, and
+ * within (gamma_h + gamma_{n_users-1}) * sum of the sequential sums, h =
+ * ceil(n_users/(256*nblk)) + 16 + ceil(nblk/64), gamma_j = j*2^-53/(1-j*2^-53)
  * (every value is >= 0).  The evaluator rounds the means to 4 decimals from these
  * and falls back to rsx_topk_metrics only when a mean lies within that bound of a
  * rounding boundary, so the metric dict is the same as from the sequential sums.

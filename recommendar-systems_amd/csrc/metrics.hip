@@ -157,32 +157,46 @@ __global__ __launch_bounds__(kSumThreads) void metrics_sum_lds(const double* __r
     if (wave == 0 && lane < m) out[lane] = s;
 }
 
-// Fast form: the same column sums in a fixed PARALLEL order (per-thread strided
-// partials, a wave butterfly, the block's 16 wave sums in order): deterministic,
-// not numpy's order.  Summation-tree depth h = ceil(n/1024) + 6 + 16, so
+// Fast form: the same column sums in a fixed PARALLEL order, deterministic but not
+// numpy's: pass 1, block b of kParBlocks(n) and thread t add users b*256+t,
+// b*256+t + 256*nblk, ... (ppt = ceil(n / (256*nblk)) of them), then a 64-lane
+// butterfly and the block's 4 wave sums in order -> partial[b][col]; pass 2, one
+// wave per column adds partial[lane], partial[lane+64], ... then a butterfly.
+// Summation-tree depth h = ppt + 6 + 4 + ceil(nblk/64) + 6 (sum_par_depth), so
 // |fast - sequential| <= (gamma_h + gamma_{n-1}) * sum|x| (all values are >= 0):
 // the caller rounds to 4 decimals and re-runs the sequential kernels only when a
 // mean lies within that bound of a rounding boundary (rsx/evaluator.py).
 constexpr int kParCols = 8;
-constexpr int kParThreads = 1024;
-__global__ __launch_bounds__(kParThreads) void metrics_sum_par(const double* __restrict__ vals, int64_t n, int m,
-                                                              double* __restrict__ out) {
-    const int c0 = blockIdx.x * kParCols;
+constexpr int kParThreads = 256;
+constexpr int kParMaxBlocks = 1024;
+
+__host__ __device__ inline int64_t par_blocks(int64_t n) {
+    const int64_t b = (n + kParThreads - 1) / kParThreads;
+    return b < 1 ? 1 : (b > kParMaxBlocks ? kParMaxBlocks : b);
+}
+
+__device__ __forceinline__ double wave_sum(double x) {  // butterfly: every lane ends with the same bits
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) x += __shfl_xor(x, o, kWave);
+    return x;
+}
+
+__global__ __launch_bounds__(kParThreads) void metrics_sum_par1(const double* __restrict__ vals, int64_t n, int m,
+                                                                double* __restrict__ partial) {
+    const int64_t nblk = gridDim.x;
+    const int c0 = blockIdx.y * kParCols;
     const int nc = (m - c0) < kParCols ? (m - c0) : kParCols;
     double s[kParCols];
 #pragma unroll
     for (int j = 0; j < kParCols; ++j) s[j] = 0.0;
-    for (int64_t u = threadIdx.x; u < n; u += kParThreads) {
+    for (int64_t u = (int64_t)blockIdx.x * kParThreads + threadIdx.x; u < n; u += nblk * kParThreads) {
         const double* r = vals + u * m + c0;
 #pragma unroll
         for (int j = 0; j < kParCols; ++j)
             if (j < nc) s[j] += r[j];
     }
-    // butterfly: every lane ends with the same bits (a + b == b + a in IEEE)
 #pragma unroll
-    for (int j = 0; j < kParCols; ++j)
-#pragma unroll
-        for (int o = kWave / 2; o > 0; o >>= 1) s[j] += __shfl_xor(s[j], o, kWave);
+    for (int j = 0; j < kParCols; ++j) s[j] = wave_sum(s[j]);
     __shared__ double part[kParThreads / kWave][kParCols];
     const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
     if (lane == 0)
@@ -191,9 +205,19 @@ __global__ __launch_bounds__(kParThreads) void metrics_sum_par(const double* __r
     __syncthreads();
     if ((int)threadIdx.x < nc) {
         double t = 0.0;
+#pragma unroll
         for (int w = 0; w < kParThreads / kWave; ++w) t += part[w][threadIdx.x];
-        out[c0 + threadIdx.x] = t;
+        partial[(int64_t)blockIdx.x * m + c0 + threadIdx.x] = t;
     }
+}
+
+__global__ __launch_bounds__(kWave) void metrics_sum_par2(const double* __restrict__ partial, int64_t nblk, int m,
+                                                          double* __restrict__ out) {
+    const int c = blockIdx.x, lane = threadIdx.x;
+    double t = 0.0;
+    for (int64_t b = lane; b < nblk; b += kWave) t += partial[b * m + c];
+    t = wave_sum(t);
+    if (lane == 0) out[c] = t;
 }
 
 static int topk_metrics_impl(const int64_t* topk_idx, int64_t n_users, int32_t k_max, const int64_t* eval_rowptr,
@@ -205,7 +229,9 @@ static int topk_metrics_impl(const int64_t* topk_idx, int64_t n_users, int32_t k
 using namespace rsx;
 
 extern "C" size_t rsx_topk_metrics_ws_bytes(int64_t n_users, int32_t n_cut) {
-    return (size_t)(n_users > 0 ? n_users : 0) * kMetricCols * (size_t)(n_cut > 0 ? n_cut : 0) * sizeof(double);
+    // per-user values, then the fast form's per-block partials
+    const size_t m = kMetricCols * (size_t)(n_cut > 0 ? n_cut : 0);
+    return ((size_t)(n_users > 0 ? n_users : 0) + (size_t)par_blocks(n_users)) * m * sizeof(double);
 }
 
 static int rsx::topk_metrics_impl(const int64_t* topk_idx, int64_t n_users, int32_t k_max,
@@ -216,14 +242,18 @@ static int rsx::topk_metrics_impl(const int64_t* topk_idx, int64_t n_users, int3
     if (n_users > 0 && (!topk_idx || !eval_rowptr || !eval_col)) return RSX_ERR_ARG;
     if (ws_bytes < rsx_topk_metrics_ws_bytes(n_users, n_cut) || (n_users > 0 && !ws)) return RSX_ERR_WORKSPACE;
     const int m = kMetricCols * n_cut;
+    if (n_users == 0) return hip_rc(hipMemsetAsync(out_sums, 0, (size_t)m * sizeof(double), s));
     double* vals = static_cast<double*>(ws);
     if (n_users > 0)
         hipLaunchKernelGGL(metrics_user, dim3((unsigned)((n_users + 255) / 256)), dim3(256), 0, s, topk_idx, n_users,
                            (int)k_max, eval_rowptr, eval_col, cutoffs, (int)n_cut, gain, vals);
-    if (fast)
-        hipLaunchKernelGGL(metrics_sum_par, dim3((unsigned)((m + kParCols - 1) / kParCols)), dim3(kParThreads), 0, s,
-                           vals, n_users, m, out_sums);
-    else if (m <= kWave)
+    if (fast) {
+        const int64_t nblk = par_blocks(n_users);
+        double* partial = vals + (size_t)(n_users > 0 ? n_users : 0) * m;
+        hipLaunchKernelGGL(metrics_sum_par1, dim3((unsigned)nblk, (unsigned)((m + kParCols - 1) / kParCols)),
+                           dim3(kParThreads), 0, s, vals, n_users, m, partial);
+        hipLaunchKernelGGL(metrics_sum_par2, dim3((unsigned)m), dim3(kWave), 0, s, partial, nblk, m, out_sums);
+    } else if (m <= kWave)
         hipLaunchKernelGGL(metrics_sum_lds, dim3(1), dim3(kSumThreads), 0, s, vals, n_users, m, out_sums);
     else
         hipLaunchKernelGGL(metrics_sum, dim3((unsigned)m), dim3(64), 0, s, vals, n_users, m, out_sums);

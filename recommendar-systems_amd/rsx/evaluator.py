@@ -125,8 +125,10 @@ _U = 2.0 ** -53
 def sum_order_bound(n: int, total: float) -> float:
     """Bound on |parallel-order sum - user-order sum| of n values >= 0 summing to
     about `total` (rsx_topk_metrics_fast, include/rsx.h): (gamma_h + gamma_{n-1}) *
-    sum, h = ceil(n/1024) + 22 the parallel tree's depth, gamma_j = j u / (1 - j u)."""
-    j = (n - 1) + (-(-n // 1024) + 22)
+    sum, h the parallel tree's depth, gamma_j = j u / (1 - j u)."""
+    nblk = min(1024, max(1, -(-n // 256)))
+    h = -(-n // (256 * nblk)) + 16 + -(-nblk // 64)
+    j = (n - 1) + h
     return j * _U / (1.0 - j * _U) * np.abs(total) * 1.0001
 
 

@@ -260,6 +260,9 @@ def fullsort_topk(user_emb: torch.Tensor, users: torch.Tensor | None, item_emb: 
     return val, idx
 
 
+_CUTS = {}
+
+
 def topk_metrics(topk_idx: torch.Tensor, eval_rowptr: torch.Tensor, eval_col: torch.Tensor, cutoffs,
                  gain: torch.Tensor, exact: bool = True) -> torch.Tensor:
     """Per-cutoff sums over users of recall, precision, ndcg, map and hit count
@@ -273,7 +276,10 @@ def topk_metrics(topk_idx: torch.Tensor, eval_rowptr: torch.Tensor, eval_col: to
     topk_idx = topk_idx.contiguous()
     n, k = topk_idx.shape
     dev = topk_idx.device
-    cut = torch.tensor(list(cutoffs), dtype=torch.int32, device=dev)
+    key = (tuple(int(c) for c in cutoffs), str(dev))
+    cut = _CUTS.get(key)
+    if cut is None:  # a host->device copy once, not per evaluation (a pageable copy waits for the stream)
+        cut = _CUTS[key] = torch.tensor(list(key[0]), dtype=torch.int32, device=dev)
     out = torch.empty(5, cut.numel(), dtype=torch.float64, device=dev)
     lib = L.lib()
     ws = _ws(dev, lib.rsx_topk_metrics_ws_bytes(n, cut.numel()))
