@@ -195,6 +195,9 @@ __device__ __forceinline__ float compact_slot(u64* buf, int n, int k, int lane, 
 #ifndef RSX_FS_GUARD
 #define RSX_FS_GUARD 1
 #endif
+#ifndef RSX_FS_WARM
+#define RSX_FS_WARM 8  // tiles scored up front for the warm-up threshold (0: off)
+#endif
 template <int D, int CW>
 __device__ __forceinline__ void load_chunk(float (&r)[CW], const float* I, int64_t item, int64_t i1, int64_t ni,
                                            int off, bool full = false) {
@@ -417,6 +420,51 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D <= 64 ? 2 
             }
         }
     };
+
+    // Warm-up threshold (d <= 64): score the chunk's first RSX_FS_WARM tiles once
+    // without inserting anything, keeping per lane the two largest (masked) scores of
+    // each of its 16 accumulator slots -- 64 distinct items per user, so for k <= 64
+    // the k-th largest of those scores bounds the chunk's k-th best score from below
+    // -- then restart at tile 0 keeping only scores >= that bound.  This replaces the
+    // warm-up's unfiltered inserts and every user's first compaction with
+    // RSX_FS_WARM extra tiles of MFMA.
+    if constexpr (NCH == 1 && MODE != 1) {
+        if (RSX_FS_WARM > 0 && ntiles > RSX_FS_WARM && a.k <= 64) {
+            const int64_t mp0 = mp, nm0 = next_mask;
+            float t1[16], t2[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) t1[r] = t2[r] = -INFINITY;
+            for (int t = 0; t < RSX_FS_WARM; ++t) {
+                floatx16 acc;
+                mfma_tile(IntC<0>{}, t, acc);
+                const unsigned mb = mask_bits(i0 + (int64_t)t * 32);
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int ii = (r & 3) + 8 * (r >> 2) + 4 * h;
+                    const float sc = ((mb >> ii) & 1u) ? -1e10f : acc[r];
+                    const float lo = fminf(t1[r], sc);
+                    t1[r] = fmaxf(t1[r], sc);
+                    t2[r] = fmaxf(t2[r], lo);
+                }
+            }
+            // the k-th largest of the lane pair's 64 scores (radix search on ordered words)
+            unsigned th = 0;
+            for (int bit = 31; bit >= 0; --bit) {
+                const unsigned c = th | (1u << bit);
+                int n = 0;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) n += (int)(ord_f32(t1[r]) >= c) + (int)(ord_f32(t2[r]) >= c);
+                n += __shfl_xor(n, 32, kWave);
+                if (n >= a.k) th = c;
+            }
+            // keep ord(score) >= th, i.e. score > unord(th - 1): ties with the bound stay
+            // (items before the bound's own item rank above it in (score, index) order)
+            if (uvalid && th > 0) tau = unord_f32(th - 1);
+            mp = mp0;
+            next_mask = nm0;
+            load_chunk<D, CW>(ra, a.I, i0 + j, i1, a.ni, h * HALF, i0 + 32 <= i1);
+        }
+    }
 
     if (ntiles > 0) {
         // one tile per iteration: the chain of tile t is issued before the filter of
