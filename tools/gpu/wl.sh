@@ -1,8 +1,8 @@
+# the other configs' bench lines (C1 LayerGCN baby, C3 SMORE baby, C5 SMORE clothing d=128)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-mkdir -p gpurun_out/wl
-timeout -k 10 300 python bench.py --workload c1 --steps 100 --warmup 10 > gpurun_out/wl/c1.json 2> gpurun_out/wl/c1.err && cat gpurun_out/wl/c1.json && \
-timeout -k 10 400 python bench.py --workload c3 --steps 30 --warmup 5 > gpurun_out/wl/c3.json 2> gpurun_out/wl/c3.err && cat gpurun_out/wl/c3.json && \
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/wl/prof_c3 -o c3 -- python bench.py --workload c3 --steps 30 --warmup 5 > gpurun_out/wl/c3p.json 2> gpurun_out/wl/c3p.err
-echo "rc=$?"
+for w in c1 c3 c5; do
+  timeout -k 10 400 python bench.py --workload $w --no-cpu-baseline > gpurun_out/wl_$w.json 2> gpurun_out/wl_$w.err || exit 1
+  python -c "import json; d=json.load(open('gpurun_out/wl_$w.json')); print('$w', round(d['value']), d['ms_per_step'], d.get('fullsort_items_per_s'))"
+done
