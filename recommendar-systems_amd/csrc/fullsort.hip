@@ -459,7 +459,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D <= 64 ? 2 
             }
             // keep ord(score) >= th, i.e. score > unord(th - 1): ties with the bound stay
             // (items before the bound's own item rank above it in (score, index) order)
-            if (uvalid && th > 0) tau = unord_f32(th - 1);
+            // (-0.0 == +0.0 as floats: a bound at +0.0 filters with a negative denormal)
+            if (uvalid && th > 0) {
+                const float tb = unord_f32(th - 1);
+                tau = tb == 0.f ? -__FLT_DENORM_MIN__ : tb;
+            }
             mp = mp0;
             next_mask = nm0;
             load_chunk<D, CW>(ra, a.I, i0 + j, i1, a.ni, h * HALF, i0 + 32 <= i1);
