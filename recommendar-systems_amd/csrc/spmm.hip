@@ -23,6 +23,10 @@ namespace rsx {
 // ---------------------------------------------------------------------------
 // row epilogues
 // ---------------------------------------------------------------------------
+#ifndef RSX_ADAM_LATE
+#define RSX_ADAM_LATE 0
+#endif
+
 struct AdamConst {
     float lr, omb1, b2, omb2, eps, wd, step_size, bc2_sqrt;
 };
@@ -92,9 +96,11 @@ __device__ __forceinline__ EpiIn epi_load(const rsx_epilogue& e, int64_t row, in
     } else if constexpr (KIND == RSX_EPI_ADAM) {
         if (s_in) in.a = ld4(s_in + off);
         if (r_add) in.b = ld4(r_add + off);
-        in.c = ld4(e.p + off);
-        in.d = ld4(e.m + off);
-        in.e = ld4(e.v + off);
+        if (!RSX_ADAM_LATE) {
+            in.c = ld4(e.p + off);
+            in.d = ld4(e.m + off);
+            in.e = ld4(e.v + off);
+        }
         if (e.reg_cnt && (!(tf & RSX_TAG_SPARSE_R) || in.tagged)) {
             const int32_t* c = e.reg_cnt + 3 * row;
             in.regc = (float)c[0] * e.reg_k[0] + (float)c[1] * e.reg_k[1] + (float)c[2] * e.reg_k[2];
@@ -114,10 +120,26 @@ __device__ __forceinline__ EpiIn epi_load(const rsx_epilogue& e, int64_t row, in
 
 // Adam's per-launch constants (two f64 pows of the step count): evaluated once per
 // thread, not once per row
+__device__ __forceinline__ float uniform_f(float x) {  // wave-uniform: lives in an SGPR
+    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x)));
+}
+
 template <int KIND>
 __device__ __forceinline__ AdamConst adam_for(const rsx_epilogue& e) {
-    if constexpr (KIND == RSX_EPI_ADAM) return adam_const(e.adam);
-    else return AdamConst{};
+    if constexpr (KIND == RSX_EPI_ADAM) {
+        AdamConst c = adam_const(e.adam);
+        c.lr = uniform_f(c.lr);
+        c.omb1 = uniform_f(c.omb1);
+        c.b2 = uniform_f(c.b2);
+        c.omb2 = uniform_f(c.omb2);
+        c.eps = uniform_f(c.eps);
+        c.wd = uniform_f(c.wd);
+        c.step_size = uniform_f(c.step_size);
+        c.bc2_sqrt = uniform_f(c.bc2_sqrt);
+        return c;
+    } else {
+        return AdamConst{};
+    }
 }
 
 template <int KIND, int D>
@@ -149,11 +171,16 @@ __device__ __forceinline__ void epilogue(const rsx_epilogue& e, int64_t row, flo
         if (e.r_add) s = add4(s, in.b);
         st4(e.y + off, mul4(e.beta, s));
     } else if constexpr (KIND == RSX_EPI_ADAM) {
+        float4 p = in.c, m = in.d, v = in.e;
+        if (RSX_ADAM_LATE) {  // moments loaded after the gathers (fewer registers live across them)
+            p = ld4(e.p + off);
+            m = ld4(e.m + off);
+            v = ld4(e.v + off);
+        }
         float4 g = e.s_in ? add4(in.a, acc) : acc;
         g = mul4(e.beta, g);
-        if (e.reg_cnt) g = add4(g, mul4(in.regc, in.c));  // sum over occurrences of k * ego row
+        if (e.reg_cnt) g = add4(g, mul4(in.regc, p));  // sum over occurrences of k * ego row
         else if (e.r_add) g = add4(g, in.b);
-        float4 p = in.c, m = in.d, v = in.e;
         g.x = adam_elem(c, p.x, m.x, v.x, g.x);
         g.y = adam_elem(c, p.y, m.y, v.y, g.y);
         g.z = adam_elem(c, p.z, m.z, v.z, g.z);
