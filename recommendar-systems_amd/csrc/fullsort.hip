@@ -130,8 +130,13 @@ __device__ __forceinline__ u64 ld_u64_l2(const u64* p) {  // bypasses the CU's L
 // compare per key pair and scalar counting per round), and 32 more on the index
 // word only when several keys share the boundary score.  Every round is a handful
 // of instructions, so the selection costs a fraction of an all-pairs rank count.
+// slack >= 0 (running compactions): stop the search as soon as the keys at or above
+// the current score-word bound number k..k+slack and keep them all (no tie pass):
+// the returned bound's score is then a valid strict filter for later (higher-index)
+// items, since at least k kept keys outrank any later key of that score or less.
+// slack < 0: exactly the top k (the final per-chunk cut fs_select relies on).
 __device__ __forceinline__ float compact_slot(u64* buf, int n, int k, int lane, int* new_cnt, unsigned lo,
-                                              unsigned hi) {
+                                              unsigned hi, int slack = -1) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's inserts are in L2
     u64 x[kNK];
     unsigned hw[kNK];
@@ -150,7 +155,22 @@ __device__ __forceinline__ float compact_slot(u64* buf, int n, int k, int lane, 
         int m = 0;
 #pragma unroll
         for (int q = 0; q < kNK; ++q) m += popc64(__ballot(hw[q] >= c));
-        if (m >= k) th = c;
+        if (m >= k) {
+            th = c;
+            if (m <= k + slack) {  // early stop: keep every key whose score word is >= th
+                const u64 lt = lanemask_lt(lane);
+                int base = 0;
+#pragma unroll
+                for (int q = 0; q < kNK; ++q) {
+                    const bool kp = x[q] != 0ull && hw[q] >= th;
+                    const u64 bq = __ballot(kp);
+                    if (kp) buf[base + popc64(bq & lt)] = x[q];
+                    base += popc64(bq);
+                }
+                *new_cnt = base;
+                return unord_f32(th);
+            }
+        }
     }
     // th = the k-th largest score word
     int gt = 0, eq = 0;
@@ -194,6 +214,9 @@ __device__ __forceinline__ float compact_slot(u64* buf, int n, int k, int lane, 
 #endif
 #ifndef RSX_FS_GUARD
 #define RSX_FS_GUARD 1
+#endif
+#ifndef RSX_FS_SLACK
+#define RSX_FS_SLACK 16  // running compactions keep up to k + this many keys (-1: exact top k)
 #endif
 #ifndef RSX_FS_WARM
 #define RSX_FS_WARM 8  // tiles scored up front for the warm-up threshold (0: off)
@@ -413,7 +436,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D <= 64 ? 2 
             const unsigned hi = max((unsigned)__builtin_amdgcn_readlane((int)omax, jj),
                                     (unsigned)__builtin_amdgcn_readlane((int)omax, jj + 32));
             int kept;
-            const float nt = compact_slot(base + (int64_t)jj * rowstep, n, a.k, lane, &kept, lo, hi);
+            const float nt = compact_slot(base + (int64_t)jj * rowstep, n, a.k, lane, &kept, lo, hi, RSX_FS_SLACK);
             if (j == jj) {
                 tau = nt;
                 cnt = kept;
