@@ -173,10 +173,12 @@ typedef struct rsx_epilogue {
     const int32_t* row_tag;
     int32_t tag;
     int32_t tag_flags;
-    /* ADAM only (optional): the regulariser gradient as occurrence counts,
+    /* ADAM and ADD (optional): the regulariser gradient as occurrence counts,
      * r = (cnt[3r] k[0] + cnt[3r+1] k[1] + cnt[3r+2] k[2]) * p_old (what the fused
-     * LightGCN BPR leaves instead of a dense R); with RSX_TAG_ZERO the counts of the
-     * tagged rows are cleared too.  Used instead of r_add when non-NULL. */
+     * LightGCN BPR leaves instead of a dense R; p_old = the row of `p`).  Used
+     * instead of r_add when non-NULL.  ADAM: with RSX_TAG_ZERO the counts of the
+     * tagged rows are cleared too.  ADD: s = ((acc + s_in) + r) * beta, and every
+     * row's counts are cleared (rows here are relative to reg_cnt and p). */
     int32_t* reg_cnt;
     const float* reg_k;
     /* optional: the tag is read from device memory (graph-captured steps) */
@@ -532,6 +534,11 @@ typedef struct rsx_sharded_lgcn_step {
      * and replayed: with adam.step_dev and tag_dev every per-step value lives on
      * the device and the step's launches and collectives are fixed. */
     const int32_t* tag_dev;
+    /* optional with row_tag: [3 (n_users + n_items) + 4] int32, zero-filled before
+     * the first step (as rsx_lgcn_step.reg_cnt): BPR runs as ONE launch and leaves
+     * the regulariser gradient as per-row occurrence counts; the user rows' Adam and
+     * the last item partial apply and clear them; r is not used. */
+    int32_t* reg_cnt;
 } rsx_sharded_lgcn_step;
 
 int rsx_sharded_lightgcn_step(const rsx_sharded_lgcn_step* st, rsx_stream_t stream);

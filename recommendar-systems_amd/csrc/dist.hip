@@ -35,6 +35,9 @@ int rowwise_dispatch(int64_t n, int d, const rsx_epilogue& e, hipStream_t s);
 int bpr_call(int32_t variant, const float* fin, const float* ego, int64_t n_users, int64_t n_items, int32_t d,
              const int64_t* trip, int64_t batch, float reg, float batch_cfg, float* g_fin, float* g_ego,
              float* loss_out, double* loss_acc, void* ws, size_t ws_bytes, hipStream_t s, float g_div = 1.f);
+int bpr_fused_call(const float* fin, const float* ego, int64_t n_users, int64_t n_items, int32_t d,
+                   const int64_t* trip, int64_t batch, float reg, float g_div, float* g_fin, int32_t* reg_cnt,
+                   float* loss_out, double* loss_acc, void* ws, size_t ws_bytes, hipStream_t s);
 
 namespace {
 
@@ -263,8 +266,15 @@ int sharded_stored_layers(const rsx_sharded_lgcn_step& st, bool train, hipStream
     }
     if (!train) return 0;
     // ---- loss: G' = dL/dfinal / (K+1), R = d reg / d ego on this rank's batch rows
-    RSX_TRY(bpr_call(RSX_BPR_LIGHTGCN, st.final_emb, st.p, nu, ni, d, st.triplets, st.batch, st.reg,
-                     (float)st.batch, st.g, st.r, st.loss_out, st.loss_acc, st.ws, st.ws_bytes, s, (float)(K + 1)));
+    // (with reg_cnt: one launch, the regulariser left as per-row occurrence counts)
+    const float* reg_k = st.reg_cnt ? reinterpret_cast<const float*>(st.reg_cnt + 3 * (nu + ni) + 1) : nullptr;
+    if (st.reg_cnt)
+        RSX_TRY(bpr_fused_call(st.final_emb, st.p, nu, ni, d, st.triplets, st.batch, st.reg, (float)(K + 1), st.g,
+                               st.reg_cnt, st.loss_out, st.loss_acc, st.ws, st.ws_bytes, s));
+    else
+        RSX_TRY(bpr_call(RSX_BPR_LIGHTGCN, st.final_emb, st.p, nu, ni, d, st.triplets, st.batch, st.reg,
+                         (float)st.batch, st.g, st.r, st.loss_out, st.loss_acc, st.ws, st.ws_bytes, s,
+                         (float)(K + 1)));
     // G'_I summed (R_I is not: every rank adds its own R_I to its last item partial,
     // whose exchange then sums them; one n_items*d exchange less per step)
     hipEvent_t j0 = exchange(st.comm, st.g + off, ni * d, s, &rc);
@@ -299,7 +309,13 @@ int sharded_stored_layers(const rsx_sharded_lgcn_step& st, bool train, hipStream
         rsx_epilogue e = epi(RSX_EPI_ADD);  // item gradient partial: A_I H^{K-1}_U + own R_I (+ G'_I on rank 0)
         e.y = st.t;
         if (root) e.s_in = st.g + off;
-        e.r_add = st.r + off;
+        if (st.reg_cnt) {  // own R_I from the counts (cleared here), as the single-GPU Adam layer does
+            e.reg_cnt = st.reg_cnt + 3 * nu;
+            e.reg_k = reg_k;
+            e.p = st.p + off;
+        } else {
+            e.r_add = st.r + off;
+        }
         RSX_TRY(spmm_dispatch(*st.adj_i, x, d, e, st.slab_i, s));
         hipEvent_t jt = exchange(st.comm, st.t, ni * d, s, &rc);
         if (!jt) return rc;
@@ -313,6 +329,12 @@ int sharded_stored_layers(const rsx_sharded_lgcn_step& st, bool train, hipStream
         u.adam = st.adam;
         u.zero0 = st.g;  // G'_U, R_U cleared on the batch users (nothing reads them later)
         u.zero1 = st.r;
+        if (st.reg_cnt) {  // R_U from the counts (cleared on the batch users)
+            u.r_add = nullptr;
+            u.zero1 = nullptr;
+            u.reg_cnt = st.reg_cnt;
+            u.reg_k = reg_k;
+        }
         u.row_tag = st.row_tag;
         u.tag = tag;
         u.tag_dev = st.tag_dev;
@@ -326,7 +348,7 @@ int sharded_stored_layers(const rsx_sharded_lgcn_step& st, bool train, hipStream
         a.v = st.v + off;
         a.adam = st.adam;
         a.zero0 = st.g + off;  // the summed G'_I and this rank's R_I: cleared densely
-        a.zero1 = st.r + off;
+        a.zero1 = st.reg_cnt ? nullptr : st.r + off;
         RSX_TRY(rowwise_dispatch(ni, d, a, s));
     }
     return 0;

@@ -168,7 +168,19 @@ __device__ __forceinline__ void epilogue(const rsx_epilogue& e, int64_t row, flo
     } else if constexpr (KIND == RSX_EPI_ADD) {
         float4 s = acc;
         if (e.s_in) s = add4(s, in.a);
-        if (e.r_add) s = add4(s, in.b);
+        if (e.reg_cnt) {  // sum over occurrences of k * ego row; loaded here, after the gathers
+            // (only the sharded step's last item partial has counts: no registers held across the loop)
+            int32_t* c = e.reg_cnt + 3 * row;
+            const float regc = (float)c[0] * e.reg_k[0] + (float)c[1] * e.reg_k[1] + (float)c[2] * e.reg_k[2];
+            s = add4(s, mul4(regc, ld4(e.p + off)));
+            if (li == 0) {
+                c[0] = 0;
+                c[1] = 0;
+                c[2] = 0;
+            }
+        } else if (e.r_add) {
+            s = add4(s, in.b);
+        }
         st4(e.y + off, mul4(e.beta, s));
     } else if constexpr (KIND == RSX_EPI_ADAM) {
         float4 p = in.c, m = in.d, v = in.e;

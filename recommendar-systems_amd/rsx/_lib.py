@@ -81,7 +81,7 @@ class ShardedStep(C.Structure):
                 ("p", P), ("m", P), ("v", P), ("s", P), ("h0", P), ("h1", P), ("final_emb", P), ("g", P),
                 ("r", P), ("t", P), ("slab_u", P), ("slab_i", P), ("triplets", P), ("batch", I64),
                 ("adam", Adam), ("loss_out", P), ("loss_acc", P), ("ws", P), ("ws_bytes", C.c_size_t),
-                ("comm", P), ("row_tag", P), ("tag", I64), ("tag_dev", P)]
+                ("comm", P), ("row_tag", P), ("tag", I64), ("tag_dev", P), ("reg_cnt", P)]
 
 
 HOST_ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, P, I64, P)

@@ -216,6 +216,13 @@ class ShardedLightGCNEngine:
         st.ws, st.ws_bytes = self.ws.data_ptr(), self.ws.numel()
         st.comm = comm.value
         st.row_tag = self.row_tag.data_ptr() if self.row_tag is not None else None
+        # the one-launch BPR (regulariser as per-row occurrence counts, applied and
+        # cleared by the user Adam layer and the last item partial), as the single engine
+        self.reg_cnt = None
+        if self.row_tag is not None and os.environ.get("RSX_BPR_FUSED", "1") != "0":
+            self.reg_cnt = torch.zeros(3 * (self.n_users + self.n_items) + 4, dtype=torch.int32,
+                                       device=self.be.device)
+        st.reg_cnt = self.reg_cnt.data_ptr() if self.reg_cnt is not None else None
         # Adam's step count and (its low word) the batch-row tag live on the device, so
         # the step's launches and collectives are the same every batch: over RCCL the
         # step is captured once as a HIP graph and replayed (host cost per batch: one
