@@ -552,8 +552,26 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D <= 64 ? 2 
 // score word first, index word only for a tie at the boundary).
 template <int E>
 __device__ __forceinline__ u64 kth_largest_n(const u64 (&e)[E], int k) {
-    unsigned th = 0;
-    for (int bit = 31; bit >= 0; --bit) {
+    // the nonzero keys' score words lie in [lo, hi] (wave min / max), so the answer
+    // shares their common high bits: search only below them (as compact_slot)
+    unsigned hi = 0u, lo = 0xffffffffu;
+#pragma unroll
+    for (int m = 0; m < E; ++m) {
+        const unsigned w = (unsigned)(e[m] >> 32);
+        if (e[m] != 0ull) {
+            hi = max(hi, w);
+            lo = min(lo, w);
+        }
+    }
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) {
+        hi = max(hi, (unsigned)__shfl_xor((int)hi, o, kWave));
+        lo = min(lo, (unsigned)__shfl_xor((int)lo, o, kWave));
+    }
+    const unsigned diff = lo ^ hi;
+    const int top = diff ? 31 - __builtin_clz(diff) : -1;
+    unsigned th = top >= 31 ? 0u : (hi >> (top + 1)) << (top + 1);
+    for (int bit = top; bit >= 0; --bit) {
         const unsigned c = th | (1u << bit);
         int n = 0;
 #pragma unroll
