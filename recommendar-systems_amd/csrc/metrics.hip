@@ -19,7 +19,8 @@ namespace rsx {
 
 constexpr int kMetricCols = 5;  // recall, precision, ndcg, map, cumhit (recall2 numerator)
 
-__global__ __launch_bounds__(256) void metrics_user(const int64_t* __restrict__ topk, int64_t n, int kmax,
+constexpr int kUserBlock = 64;  // one wave per block: 35,598 users spread over all CUs (557 blocks, not 139)
+__global__ __launch_bounds__(kUserBlock) void metrics_user(const int64_t* __restrict__ topk, int64_t n, int kmax,
                                                      const int64_t* __restrict__ erp,
                                                      const int32_t* __restrict__ ecol,
                                                      const int32_t* __restrict__ cut, int n_cut,
@@ -33,14 +34,46 @@ __global__ __launch_bounds__(256) void metrics_user(const int64_t* __restrict__ 
     double idcg_cap = 0.0;
     int c = 0;
     double* out = vals + u * (int64_t)(kMetricCols * n_cut);
-    for (int r = 0; r < kmax; ++r) {
-        const int64_t it = topk[u * kmax + r];
-        int64_t lo = b, hi = e;
-        while (lo < hi) {
-            const int64_t mid = (lo + hi) >> 1;
-            if ((int64_t)ecol[mid] < it) lo = mid + 1; else hi = mid;
+    // hits first (k <= 64): 8 binary searches in lockstep, so a thread has 8
+    // independent loads in flight per probe instead of one dependent chain per rank
+    uint64_t hits = 0;
+    if (kmax <= 64) {
+        const int rounds = pos > 0 ? 64 - __builtin_clzll((unsigned long long)pos) : 0;
+        for (int r0 = 0; r0 < kmax; r0 += 8) {
+            int64_t it[8], lo[8], hi[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                it[j] = r0 + j < kmax ? topk[u * kmax + r0 + j] : -1;
+                lo[j] = b;
+                hi[j] = e;
+            }
+            for (int q = 0; q < rounds; ++q) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    if (lo[j] < hi[j]) {
+                        const int64_t mid = (lo[j] + hi[j]) >> 1;
+                        if ((int64_t)ecol[mid] < it[j]) lo[j] = mid + 1; else hi[j] = mid;
+                    }
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (r0 + j < kmax && lo[j] < e && (int64_t)ecol[lo[j]] == it[j]) hits |= 1ull << (r0 + j);
         }
-        const bool hit = lo < e && (int64_t)ecol[lo] == it;
+    }
+    for (int r = 0; r < kmax; ++r) {
+        bool hit;
+        if (kmax <= 64) {
+            hit = (hits >> r) & 1ull;
+        } else {
+            const int64_t it = topk[u * kmax + r];
+            int64_t lo = b, hi = e;
+            while (lo < hi) {
+                const int64_t mid = (lo + hi) >> 1;
+                if ((int64_t)ecol[mid] < it) lo = mid + 1; else hi = mid;
+            }
+            hit = lo < e && (int64_t)ecol[lo] == it;
+        }
         const double rank = (double)(r + 1);
         if (hit) cum += 1.0;
         dcg += hit ? gain[r] : 0.0;                  // cumsum(where(hit, gain, 0))
@@ -245,7 +278,8 @@ static int rsx::topk_metrics_impl(const int64_t* topk_idx, int64_t n_users, int3
     if (n_users == 0) return hip_rc(hipMemsetAsync(out_sums, 0, (size_t)m * sizeof(double), s));
     double* vals = static_cast<double*>(ws);
     if (n_users > 0)
-        hipLaunchKernelGGL(metrics_user, dim3((unsigned)((n_users + 255) / 256)), dim3(256), 0, s, topk_idx, n_users,
+        hipLaunchKernelGGL(metrics_user, dim3((unsigned)((n_users + kUserBlock - 1) / kUserBlock)), dim3(kUserBlock), 0, s,
+                           topk_idx, n_users,
                            (int)k_max, eval_rowptr, eval_col, cutoffs, (int)n_cut, gain, vals);
     if (fast) {
         const int64_t nblk = par_blocks(n_users);
