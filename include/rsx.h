@@ -240,9 +240,12 @@ int rsx_bpr(int32_t variant, const float* final_emb, const float* ego_emb, int64
  * score exactly -1e10 as in the reference.
  *   user_emb: [*, d] rows selected by users[b] (int64); item_emb: [n_items, d]
  *   out_val: [n_batch, k] f32, out_idx: [n_batch, k] int64
- * Requires k <= n_items and k <= 128. Workspace: rsx_fullsort_ws_bytes.
+ * Requires k <= n_items and k <= 96. Workspace: rsx_fullsort_ws_bytes.
  */
 size_t rsx_fullsort_ws_bytes(int64_t n_batch, int64_t n_items, int32_t k);
+/* The item-chunk plan rsx_fullsort_topk uses for (n_batch, n_items, d): chunks per
+ * 32-user wave and items per chunk (tests assert which selection path they cover). */
+int rsx_fullsort_plan(int64_t n_batch, int64_t n_items, int32_t d, int32_t* n_chunks, int64_t* chunk_items);
 int rsx_fullsort_topk(const float* user_emb, const int64_t* users, int64_t n_batch,
                       const float* item_emb, int64_t n_items, int32_t d,
                       const int64_t* mask_rowptr, const int32_t* mask_col, int32_t k,

@@ -787,6 +787,16 @@ size_t rsx_fullsort_ws_bytes(int64_t n_batch, int64_t n_items, int32_t k) {
     return a > b ? a : b;
 }
 
+int rsx_fullsort_plan(int64_t n_batch, int64_t n_items, int32_t d, int32_t* n_chunks, int64_t* chunk_items) {
+    if (!n_chunks || !chunk_items || n_batch < 0 || n_items <= 0) return RSX_ERR_ARG;
+    int nw, nc;
+    int64_t per;
+    rsx::fs_plan(n_batch, n_items, d, &nw, &nc, &per);
+    *n_chunks = nc;
+    *chunk_items = per;
+    return RSX_OK;
+}
+
 int rsx_fullsort_topk(const float* user_emb, const int64_t* users, int64_t n_batch, const float* item_emb,
                       int64_t n_items, int32_t d, const int64_t* mask_rowptr, const int32_t* mask_col, int32_t k,
                       float* out_val, int64_t* out_idx, void* ws, size_t ws_bytes, rsx_stream_t stream) {

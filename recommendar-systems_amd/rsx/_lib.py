@@ -99,6 +99,7 @@ def _declare(lib):
         "rsx_bpr_ws_bytes": (C.c_size_t, [I64]),
         "rsx_bpr": (C.c_int, [I32, P, P, I64, I64, I32, P, I64, F32, F32, P, P, P, P, P, C.c_size_t, P]),
         "rsx_fullsort_ws_bytes": (C.c_size_t, [I64, I64, I32]),
+        "rsx_fullsort_plan": (C.c_int, [I64, I64, I32, C.POINTER(I32), C.POINTER(I64)]),
         "rsx_fullsort_topk": (C.c_int, [P, P, I64, P, I64, I32, P, P, I32, P, P, P, C.c_size_t, P]),
         "rsx_score_dense": (C.c_int, [P, P, I64, P, I64, I32, P, P]),
         "rsx_sample_triplets": (C.c_int, [P, P, I64, P, P, P, I64, C.c_uint64, I64, I64, I64, P, P]),
@@ -133,7 +134,7 @@ def _declare(lib):
 
 
 EXPORTED = ["rsx_version", "rsx_csr_schedule_host", "rsx_spmm", "rsx_rowwise", "rsx_bpr_ws_bytes", "rsx_bpr",
-            "rsx_fullsort_ws_bytes", "rsx_fullsort_topk", "rsx_score_dense", "rsx_sample_triplets",
+            "rsx_fullsort_ws_bytes", "rsx_fullsort_plan", "rsx_fullsort_topk", "rsx_score_dense", "rsx_sample_triplets",
             "rsx_gather_rows", "rsx_lightgcn_step", "rsx_lightgcn_forward", "rsx_sample_epoch",
             "rsx_smore_spectral_spec_floats", "rsx_smore_spectral_fwd_ws_bytes", "rsx_smore_spectral_fwd",
             "rsx_smore_spectral_bwd",

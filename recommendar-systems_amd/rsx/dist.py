@@ -275,6 +275,12 @@ class ShardedLightGCNEngine:
         self._keep = t
         nb = lib.rsx_bpr_ws_bytes(B)
         if nb > self.ws.numel():  # a given batch larger than the engine's
+            # a captured graph holds the old workspace pointer: drop it (and re-warm)
+            # before that memory returns to the caching allocator
+            if self._graph is not None:
+                torch.cuda.synchronize(self.be.device)
+                self._graph = None
+            self._graph_warm = False
             self.ws = torch.empty(nb, dtype=torch.uint8, device=self.be.device)
             st.ws, st.ws_bytes = self.ws.data_ptr(), self.ws.numel()
         st.triplets, st.batch = t.data_ptr(), B

@@ -113,6 +113,8 @@ def _native_worker(rank, world, port, out_dir):
             eng.step(epoch=0, start=s)
         torch.cuda.synchronize()
         losses.append(float(eng.loss_acc.item()))
+        if getattr(eng, "reg_cnt", None) is not None:  # the one-launch BPR's occurrence counts are all cleared
+            assert torch.count_nonzero(eng.reg_cnt[:-4]).item() == 0
         eng.invalidate()
         f1 = eng.forward().cpu().clone()
         if native == "graph":  # full batches after the first were replayed from one capture
@@ -127,6 +129,18 @@ def _native_worker(rank, world, port, out_dir):
             L.check(L.lib().rsx_comm_allreduce_f32(eng._comm, C.c_void_p(x.data_ptr()), 1000, ops._stream()),
                     "allreduce")
             assert torch.equal(x.cpu(), torch.arange(1000, dtype=torch.float32))
+        if native == "graph":
+            # a batch larger than the engine's reallocates the workspace: the captured graph
+            # (which holds the old pointer) is dropped, and the next full batches re-capture
+            p_before = eng.p.clone()
+            big = torch.from_numpy(np.concatenate([trip, trip], axis=1)).cuda()
+            eng.step(triplets=big)
+            assert eng._graph is None
+            for s in range(0, 3 * 16, 16):
+                eng.step(epoch=1, start=s)
+            torch.cuda.synchronize()
+            assert eng._graph is not None and torch.isfinite(eng.p).all()
+            assert not torch.equal(p_before, eng.p)
         eng.close()
     np.savez(os.path.join(out_dir, "native.npz"), **{f"{k}_{i}": v for k in ("graph", True, False)
                                                      for i, v in enumerate(res[k])})

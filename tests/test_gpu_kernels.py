@@ -292,16 +292,18 @@ def test_topk_metrics_device_equals_reference_dicts(cuda, golden, fx):
         assert ev.evaluate_device(topk, stub) == metric_dict(z, tag), tag
 
 
-def test_topk_metrics_device_bitwise_vs_numpy(cuda):
+@pytest.mark.parametrize("k", [50, 64, 100])
+def test_topk_metrics_device_bitwise_vs_numpy(cuda, k):
     """Large random case: the per-cutoff means before rounding equal the numpy restatement
-    (reference metrics.py formulas, mean over users in numpy's order) bit for bit."""
+    (reference metrics.py formulas, mean over users in numpy's order) bit for bit.  k = 64
+    is the lockstep search's 64-bit hit-mask edge, k = 100 its serial fallback."""
     import torch
 
     from rsx import evaluator as E
     from rsx import ops
 
     rng = np.random.default_rng(5)
-    n, k, ni = 6000, 50, 3000
+    n, ni = 6000, 3000
     items = [rng.choice(ni, size=int(rng.integers(1, 40)), replace=False) for _ in range(n)]
     rows = []
     for x in items:  # each ranked list: up to 10 true items, then distinct non-items, shuffled within the top 20
@@ -313,7 +315,7 @@ def test_topk_metrics_device_bitwise_vs_numpy(cuda):
     topk = np.stack(rows)
     pos = np.array([len(x) for x in items])
     hit = E.hit_matrix(topk, items)
-    cuts = [1, 5, 10, 20, 50]
+    cuts = [1, 5, 10, 20, k]
     stub = _EvalStub(items, cuda)
     gain = torch.from_numpy(1.0 / np.log2(np.arange(1, k + 1, dtype=np.float64) + 1)).to(cuda)
     sums = ops.topk_metrics(torch.from_numpy(topk.astype(np.int64)).to(cuda), *stub.eval_csr(), cuts, gain).cpu().numpy()

@@ -16,19 +16,30 @@ pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
-def _setup(tmp_path, golden):
+# (fixture, dataset name, .inter file, feature file names, config overrides)
+FIXTURES = {
+    "smore_small": ("baby", "gold_small.inter", ("image_feat_raw.npy", "text_feat_raw.npy"), {}),
+    # C5-shaped: embedding_size 128, CLIP-like L2-normalised 768/768 features (clothing.yaml file names)
+    "smore_d128_small": ("clothing", "gold_clothing.inter", ("image_feat.npy", "text_feat.npy"),
+                         dict(embedding_size=128)),
+}
+
+
+def _setup(tmp_path, golden, fx="smore_small"):
     from rsx.config import Config
     from rsx.data import EvalDataLoader, RecDataset, TrainDataLoader
 
-    z = golden("smore_small")
-    d = tmp_path / "data" / "baby"
+    dataset, inter, (vf, tf), extra = FIXTURES[fx]
+    z = golden(fx)
+    d = tmp_path / "data" / dataset
     d.mkdir(parents=True)
-    shutil.copy(os.path.join(GOLD, "gold_small.inter"), d / "baby.inter")
-    np.save(d / "image_feat_raw.npy", z["v_feat"])
-    np.save(d / "text_feat_raw.npy", z["t_feat"])
-    c = Config("SMORE", "baby", dict(data_path=str(tmp_path / "data") + "/", train_batch_size=512,
+    shutil.copy(os.path.join(GOLD, inter), d / f"{dataset}.inter")
+    np.save(d / vf, z["v_feat"])
+    np.save(d / tf, z["t_feat"])
+    c = Config("SMORE", dataset, dict(data_path=str(tmp_path / "data") + "/", train_batch_size=512,
                                       eval_batch_size=256, rsx_sampler="host", is_multimodal_model=True,
-                                      dropout_rate=[0.0], mg_verbose=False, image_knn_k=[10], text_knn_k=[8]))
+                                      dropout_rate=[0.0], mg_verbose=False, image_knn_k=[10], text_knn_k=[8],
+                                      **extra))
     for k in c["hyper_parameters"]:
         if isinstance(c[k], list):
             c[k] = c[k][0]
@@ -51,8 +62,9 @@ def _model(c, train):
     return SMORE(c, train)
 
 
-def test_smore_init_graphs_forward(tmp_path, golden):
-    z, c, train, valid, test = _setup(tmp_path, golden)
+@pytest.mark.parametrize("fx", list(FIXTURES))
+def test_smore_init_graphs_forward(tmp_path, golden, fx):
+    z, c, train, valid, test = _setup(tmp_path, golden, fx)
     m = _model(c, train)
     for n, p in m.named_parameters():
         assert np.array_equal(p.detach().cpu().numpy(), z["init." + n]), n
@@ -69,8 +81,8 @@ def test_smore_init_graphs_forward(tmp_path, golden):
         if name == "R":
             assert np.array_equal(ref[2], mine[2])
         else:
-            # kNN cosine similarities come from a CPU sgemm: 1-ulp differences across host CPUs
-            np.testing.assert_allclose(mine[2], ref[2], rtol=1e-6, atol=0, err_msg=name)
+            # kNN cosine similarities come from a CPU sgemm: a few ulp apart across host CPUs (768-long dots)
+            np.testing.assert_allclose(mine[2], ref[2], rtol=3e-6, atol=0, err_msg=name)
     m.eval()
     with torch.no_grad():
         u, i = m.forward(None)
@@ -85,8 +97,9 @@ def test_smore_init_graphs_forward(tmp_path, golden):
         np.testing.assert_allclose(content.cpu().numpy(), z["fwd_content"], rtol=1e-5, atol=1e-6)
 
 
-def test_smore_first_step(tmp_path, golden):
-    z, c, train, valid, test = _setup(tmp_path, golden)
+@pytest.mark.parametrize("fx", list(FIXTURES))
+def test_smore_first_step(tmp_path, golden, fx):
+    z, c, train, valid, test = _setup(tmp_path, golden, fx)
     m = _model(c, train)
     m.train()
     opt = torch.optim.Adam(m.parameters(), lr=c["learning_rate"])
@@ -114,10 +127,11 @@ def test_smore_first_step(tmp_path, golden):
         assert np.all(np.abs(got - want) <= bound), n
 
 
-def test_smore_one_epoch_with_mirror_gradient(tmp_path, golden):
+@pytest.mark.parametrize("fx", list(FIXTURES))
+def test_smore_one_epoch_with_mirror_gradient(tmp_path, golden, fx):
     from rsx.trainer import Trainer
 
-    z, c, train, valid, test = _setup(tmp_path, golden)
+    z, c, train, valid, test = _setup(tmp_path, golden, fx)
     m = _model(c, train)
     t = Trainer(c, m)
     assert not t.fused and m.mg_enable

@@ -330,13 +330,40 @@ def _smore_extra(model, out, tag):
     out["t_feat"] = model.t_feat.numpy().copy()
 
 
+def capture_smore_d128(out_dir):
+    """C5-shaped SMORE fixture: embedding_size 128, CLIP-like L2-normalised 768/768
+    image/text features (clothing.yaml names image_feat.npy / text_feat.npy), a small
+    clothing-shaped graph; first step + one epoch with the mirror gradient + eval."""
+    df = synth.amazon_like(360, 180, 3000, seed=9)
+    synth.write_inter(df, DATA_ROOT, "clothing")
+    df.to_csv(os.path.join(out_dir, "gold_clothing.inter"), sep="\t", index=False)
+    n_items = int(df.itemID.max()) + 1
+    np.save(os.path.join(DATA_ROOT, "clothing", "image_feat.npy"), synth.features(n_items, 768, 21, l2_normalise=True))
+    np.save(os.path.join(DATA_ROOT, "clothing", "text_feat.npy"), synth.features(n_items, 768, 22, l2_normalise=True))
+    orig_cuda = torch.Tensor.cuda
+    torch.Tensor.cuda = lambda self, *a, **k: self
+    try:
+        capture_model_full("SMORE", "clothing",
+                           dict(train_batch_size=512, eval_batch_size=256, is_multimodal_model=True,
+                                embedding_size=128, dropout_rate=[0.0], mg_verbose=False,
+                                image_knn_k=[10], text_knn_k=[8]),
+                           os.path.join(out_dir, "smore_d128_small.npz"), epochs=1, extra=_smore_extra)
+    finally:
+        torch.Tensor.cuda = orig_cuda
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(REPO, "tests", "golden"))
+    ap.add_argument("--only", default=None, help="capture one fixture set: small | smore_d128")
     args = ap.parse_args()
     os.makedirs(args.out, exist_ok=True)
     _install_shims()
     shutil.rmtree(DATA_ROOT, ignore_errors=True)
+    if args.only in (None, "smore_d128"):
+        capture_smore_d128(args.out)
+    if args.only == "smore_d128":
+        return
 
     # small Amazon-shaped graph with hubs: 400 users, 200 items, ~4k interactions
     df = synth.amazon_like(400, 200, 4000, seed=7)
