@@ -59,32 +59,84 @@ def time_kernel(fn, reps):
     return s.elapsed_time(e) / reps  # ms
 
 
-def cpu_baseline(df_train, nu, ni, budget_s=12.0):
-    """Reference-identical CPU LightGCN (oracle restatement) on this host's cores:
-    Python negative sampler + torch.sparse.mm propagation + autograd + Adam."""
+def _oracle():
     sys.path.insert(0, os.path.join(HERE, "oracle"))
     import rsx_oracle as O
 
-    tu, ti = df_train
-    A = O.lightgcn_norm_adj_vec(tu, ti, nu, ni)
-    torch.manual_seed(999)
-    U0 = torch.nn.init.xavier_uniform_(torch.empty(nu, 64)).numpy()
-    I0 = torch.nn.init.xavier_uniform_(torch.empty(ni, 64)).numpy()
-    cpu = O.LightGCNCPU(A, U0, I0, 3, 1e-2)
-    smp = O.ReferenceSampler(tu, ti)
-    cpu.step(smp.next(2048))  # warm
+    return O
+
+
+def _timed_loop(step, budget_s, min_steps=3, max_steps=200):
+    """Run step() until budget_s has elapsed (at least min_steps); returns (steps, seconds)."""
     t0 = time.perf_counter()
     steps = 0
     while True:
-        cpu.step(smp.next(2048))
+        step()
         steps += 1
         el = time.perf_counter() - t0
-        if (el > budget_s and steps >= 3) or steps >= 200:
-            break
-    return {"value": steps * 2048 / el, "unit": "interactions/s", "cores": torch.get_num_threads(),
+        if (el > budget_s and steps >= min_steps) or steps >= max_steps:
+            return steps, el
+
+
+def cpu_baseline(df_train, nu, ni, budget_s=12.0, d=64, shape="sports", scale=1):
+    """Reference-identical CPU LightGCN (oracle restatement) on this host's cores:
+    Python negative sampler + torch.sparse.mm propagation + autograd + Adam.  With
+    scale > 1 the graph is a 1/scale slice and the rate is divided by scale."""
+    O = _oracle()
+    tu, ti = df_train
+    A = O.lightgcn_norm_adj_vec(tu, ti, nu, ni)
+    torch.manual_seed(999)
+    U0 = torch.nn.init.xavier_uniform_(torch.empty(nu, d)).numpy()
+    I0 = torch.nn.init.xavier_uniform_(torch.empty(ni, d)).numpy()
+    cpu = O.LightGCNCPU(A, U0, I0, 3, 1e-2)
+    smp = O.ReferenceSampler(tu, ti)
+    if scale == 1:
+        cpu.step(smp.next(2048))  # warm
+    steps, el = _timed_loop(lambda: cpu.step(smp.next(2048)), budget_s, min_steps=1 if scale > 1 else 3)
+    what = (f"{steps} LightGCN K=3 d={d} B=2048 steps on the same {shape}-shaped graph" if scale == 1 else
+            f"{steps} LightGCN K=3 d={d} B=2048 step(s) on a 1/{scale} user slice ({nu:,} users x {ni:,} items, "
+            f"{len(tu):,} train interactions), rate divided by {scale}")
+    return {"value": steps * 2048 / el / scale, "unit": "interactions/s", "cores": torch.get_num_threads(),
             "kind": "port",
-            "sample": f"{steps} LightGCN K=3 d=64 B=2048 steps on the same sports-shaped graph "
-                      f"({el:.1f} s; Python sampler + torch.sparse.mm + autograd + Adam, oracle/rsx_oracle.py)"}
+            "sample": f"{what} ({el:.1f} s; Python sampler + torch.sparse.mm + autograd + Adam, oracle/rsx_oracle.py)"}
+
+
+def cpu_baseline_layergcn(tu, ti, nu, ni, K, reg, dropout, budget_s, batches_per_epoch):
+    """oracle.LayerGCNCPU: per-epoch edge dropout (amortised over the epoch's batches) +
+    cosine-gated propagation + BPR/L2 + autograd + Adam."""
+    O = _oracle()
+    torch.manual_seed(999)
+    U0 = torch.nn.init.xavier_uniform_(torch.empty(nu, 64)).numpy()
+    I0 = torch.nn.init.xavier_uniform_(torch.empty(ni, 64)).numpy()
+    cpu = O.LayerGCNCPU(tu, ti, nu, ni, U0, I0, K, reg, dropout)
+    smp = O.ReferenceSampler(tu, ti)
+    t0 = time.perf_counter()
+    cpu.pre_epoch()
+    t_pre = time.perf_counter() - t0
+    cpu.step(smp.next(2048))
+    steps, el = _timed_loop(lambda: cpu.step(smp.next(2048)), budget_s)
+    per = el / steps + t_pre / batches_per_epoch
+    return {"value": 2048 / per, "unit": "interactions/s", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"{steps} LayerGCN K={K} d=64 B=2048 steps ({el:.1f} s) + one edge-dropout rebuild "
+                      f"({t_pre:.2f} s, amortised over {batches_per_epoch} batches) on the same graph "
+                      f"(oracle.LayerGCNCPU: torch.sparse.mm + autograd + Adam)"}
+
+
+def cpu_baseline_smore(tu, ti, nu, ni, v, t, d, image_k, text_k, dropout, budget_s):
+    """oracle.SMORECPU + smore_train_batch: the reference's SMORE batch with the
+    model-level mirror gradient (3 forward/backward passes, 2 Adam steps per batch
+    once it triggers) on this host's cores; the first two (MG-free) batches untimed."""
+    O = _oracle()
+    torch.manual_seed(999)
+    m = O.SMORECPU(tu, ti, nu, ni, v, t, d=d, image_k=image_k, text_k=text_k, dropout=dropout, batch_size=2048)
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+    smp = O.ReferenceSampler(tu, ti)
+    for _ in range(2):
+        O.smore_train_batch(m, opt, smp.next(2048), 1e-3)
+    steps, el = _timed_loop(lambda: O.smore_train_batch(m, opt, smp.next(2048), 1e-3), budget_s, min_steps=2)
+    return {"value": steps * 2048 / el, "unit": "interactions/s", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"{steps} SMORE d={d} B=2048 batches with the mirror gradient ({el:.1f} s) on the same graph "
+                      f"and features (oracle.SMORECPU: torch CPU forward/autograd/Adam)"}
 
 
 WORKLOADS = {
@@ -118,11 +170,13 @@ def bench_model(args):
     df = synth.shaped(w["dataset"], seed=0)
     synth.write_inter(df, root, w["dataset"])
     ni = int(df.itemID.max()) + 1
+    feats = None
     if w["model"] == "SMORE":
         dv, dt, l2 = w.get("feats", (4096, 384, False))
         fv, ft = w.get("feat_files", ("image_feat_raw.npy", "text_feat_raw.npy"))  # configs/dataset/<name>.yaml
-        np.save(os.path.join(root, w["dataset"], fv), synth.features(ni, dv, 1, l2_normalise=l2))
-        np.save(os.path.join(root, w["dataset"], ft), synth.features(ni, dt, 2, l2_normalise=l2))
+        feats = (synth.features(ni, dv, 1, l2_normalise=l2), synth.features(ni, dt, 2, l2_normalise=l2))
+        np.save(os.path.join(root, w["dataset"], fv), feats[0])
+        np.save(os.path.join(root, w["dataset"], ft), feats[1])
     cfg = dict(data_path=root + "/", train_batch_size=args.batch, rsx_sampler="device",
                is_multimodal_model=w["model"] == "SMORE", **w["cfg"])
     c = Config(w["model"], w["dataset"], cfg)
@@ -179,6 +233,35 @@ def bench_model(args):
     torch.cuda.synchronize()
     eval_s = time.perf_counter() - te0
     n_eval = int(len(valid.get_eval_users()))
+
+    # roofline: one propagation SpMM (STORE) over the model's training graph, d columns
+    d = int(c["embedding_size"])
+    if w["model"] == "SMORE":
+        A = model.norm_adj_csr
+        x = torch.cat([model.user_embedding.weight, model.item_id_embedding.weight]).detach().contiguous()
+        kname = f"spmm_main<{d},STORE> UI-graph propagation layer"
+    else:
+        A = model.engine.train_adj
+        x = model.engine.p
+        kname = f"spmm_main<{d},STORE> propagation layer (the epoch's edge-dropout graph)"
+    y = torch.empty(A.n_rows, d, device=x.device)
+    spmm_ms = time_kernel(lambda: A.spmm(x, out=y), 50)
+    alg = spmm_bytes(A.n_rows, A.nnz, d)
+    roof = {"bound": "hbm", "kernel": kname, "achieved": alg / (spmm_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": alg / (spmm_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
+            "algorithmic_bytes_per_launch": alg, "avg_launch_ms": spmm_ms,
+            "note": "baby/clothing working sets are Infinity-Cache resident"}
+    cpu = None
+    if not args.no_cpu_baseline:
+        tr_df = df[df.x_label == 0]
+        tu_, ti_ = tr_df.userID.values.astype(np.int64), tr_df.itemID.values.astype(np.int64)
+        nu_ = int(df.userID.max()) + 1
+        if w["model"] == "SMORE":
+            cpu = cpu_baseline_smore(tu_, ti_, nu_, ni, feats[0], feats[1], d, int(c["image_knn_k"]),
+                                     int(c["text_knn_k"]), float(c["dropout_rate"]), args.cpu_budget)
+        else:
+            cpu = cpu_baseline_layergcn(tu_, ti_, nu_, ni, int(c["n_layers"]), float(c["reg_weight"]),
+                                        float(c["dropout"]), args.cpu_budget, -(-tu_.size // args.batch))
     out = {
         "metric": METRIC, "value": n / wall, "unit": "interactions/s", "n_gpus": 1, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": wall * 1e3 / args.steps, "higher_is_better": True,
@@ -190,7 +273,7 @@ def bench_model(args):
                    "graph_step": t._graph is not None and t._graph.replays > 0},
         "fullsort_items_per_s": n_eval * ni / eval_s,
         "fullsort": {"eval_users": n_eval, "n_items": ni, "s_per_eval_incl_forward_and_metrics": eval_s},
-        "model_build_s": build_s, "roofline": None, "cpu_baseline": None,
+        "model_build_s": build_s, "roofline": roof, "cpu_baseline": cpu,
     }
     _json_line(out)
 
@@ -210,15 +293,18 @@ def load_graph(workload, rank, world, c4_chunks=None):
     user chunks are dealt to the ranks in contiguous ranges (local user ids)."""
     from rsx import synth
 
-    if workload == "c2":
-        nu0, ni, ne0 = synth.SHAPES["sports"]
+    if workload in ("c2", "baby"):
+        shape = "sports" if workload == "c2" else "baby"
+        nu0, ni, ne0 = synth.SHAPES[shape]
         df = synth.amazon_like(nu0, ni, ne0, seed=rank)
         tr, va = df[df.x_label == 0], df[df.x_label == 1]
+        desc = (f"C2: LightGCN K=3 d=64, sports-shaped (35,598 users x 18,357 items per rank), B=2048 per rank, "
+                f"device sampler, fused step" if workload == "c2" else
+                "north_star baby leg: LightGCN K=3 d=64, baby-shaped (19,445 users x 7,050 items per rank), "
+                "B=2048 per rank, device sampler, fused step")
         return (tr.userID.values.astype(np.int64), tr.itemID.values.astype(np.int64),
                 va.userID.values.astype(np.int64), va.itemID.values.astype(np.int64),
-                int(df.userID.max()) + 1, ni, 64,
-                "C2: LightGCN K=3 d=64, sports-shaped (35,598 users x 18,357 items per rank), B=2048 per rank, "
-                "device sampler, fused step")
+                int(df.userID.max()) + 1, ni, 64, desc)
     import multiprocessing as mp
 
     C = synth.C4
@@ -256,8 +342,9 @@ def main():
     _STDOUT_FD = os.dup(1)
     os.dup2(2, 1)
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", default="c2", choices=["c2", "c1", "c3", "c4", "c5"],
-                    help="c2 (default): the headline LightGCN sports config; c1/c3: LayerGCN / SMORE on baby; "
+    ap.add_argument("--workload", default="c2", choices=["c2", "baby", "c1", "c3", "c4", "c5"],
+                    help="c2 (default): the headline LightGCN sports config; baby: LightGCN on baby (north_star's "
+                         "10x leg); c1/c3: LayerGCN / SMORE on baby; c5: SMORE d=128 CLIP on clothing; "
                          "c4: LightGCN d=256 on the 10M-user graph, row-sharded")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=None, help="default 200 (c4: 20)")
@@ -363,6 +450,31 @@ def main():
         total_inter = float(done["inter"])
     loss_mean = float(eng.loss_acc.item()) / max(eng.step_count, 1)
 
+    # epoch-inclusive rate: one whole fresh epoch, its sampling launch included
+    epoch_rate = None
+    if not big:
+        pos["epoch"] += 1
+        pos["start"] = 0
+        ep0 = pos["epoch"]
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+        done["inter"] = 0
+        t_ep = time.perf_counter()
+        while pos["epoch"] == ep0:
+            one_step()
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+        ep_s = time.perf_counter() - t_ep
+        er = torch.tensor([ep_s, float(done["inter"])], dtype=torch.float64, device=dev)
+        if world > 1:
+            torch.distributed.all_reduce(er[:1], op=torch.distributed.ReduceOp.MAX)
+            torch.distributed.all_reduce(er[1:], op=torch.distributed.ReduceOp.SUM)
+        epoch_rate = {"interactions_per_s": float(er[1] / er[0]), "s_per_epoch": float(er[0]),
+                      "batches_per_rank": -(-E // args.batch),
+                      "includes": "the epoch's device sampling launch (shuffle + negatives), every batch's step"}
+
     # full-sort evaluation throughput (forward once + fused MFMA scores/mask/top-50)
     vusers = np.unique(vu_all)
     if args.eval_users:
@@ -423,15 +535,19 @@ def main():
     achieved = alg / (spmm_ms * 1e-3) / 1e9
     traffic = None
     tfile = os.path.join(HERE, "profiles", "spmm_traffic.json")
-    if os.path.exists(tfile) and not big and not sharded:  # PMC bytes measured for the single C2 launch
+    if os.path.exists(tfile) and args.workload == "c2" and not sharded:  # PMC bytes measured for the C2 launch
         try:
             traffic = json.load(open(tfile)).get("bytes_per_launch")
         except Exception:  # noqa: BLE001
             traffic = None
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not big:
-        cpu = cpu_baseline((tu, ti), nu, ni, args.cpu_budget)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        if not big:
+            cpu = cpu_baseline((tu, ti), nu, ni, args.cpu_budget, shape="sports" if args.workload == "c2" else "baby")
+        else:  # C4: a 1/10 user slice (the first 1M users of the graph) over all 1M items, per step
+            m = tu < 1_000_000
+            cpu = cpu_baseline((tu[m], ti[m]), 1_000_000, ni, args.cpu_budget, d=d, shape="C4", scale=10)
 
     if rank == 0:
         ms = wall * 1e3 / args.steps
@@ -444,11 +560,13 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": ms,
             "higher_is_better": True,
-            "scaling": "weak",
+            # c4: the graph is fixed whatever N (strong), each rank's batch is its own users' 2048
+            "scaling": "strong" if big else "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": ("synthetic Amazon-sports-shaped graph (rsx.synth, seed=rank; Zipf(0.8) items, 5-core users, "
-                     "reference split rule); xavier-uniform init, seed 999") if not big else
+            "data": (f"synthetic Amazon-{'sports' if args.workload == 'c2' else 'baby'}-shaped graph (rsx.synth, "
+                     "seed=rank; Zipf(0.8) items, 5-core users, reference split rule); xavier-uniform init, seed 999")
+                    if not big else
                     ("synthetic C4 graph (rsx.synth.chunk_graph: 8 seeded 1.25M-user chunks, Zipf(0.8) items, "
                      "5+Geometric degrees mean 10, reference split rule); xavier-uniform-bound init"),
             "config": {"workload": desc, "model": "LightGCN", "n_layers": 3, "embedding_size": d,
@@ -465,9 +583,10 @@ def main():
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "algorithmic_bytes_per_launch": alg, "avg_launch_ms": spmm_ms,
-                         "note": ("sports working set (<50 MB) is Infinity-Cache resident" if not big else
+                         "note": ("the sports/baby working set (<50 MB) is Infinity-Cache resident" if not big else
                                   "C4 shard: tables of GBs, gathers from HBM")},
             "cpu_baseline": cpu,
+            "epoch": epoch_rate,
             "gpu_ms_per_step_events": gpu_ms / args.steps,
             "train_loss_mean": loss_mean,
         }

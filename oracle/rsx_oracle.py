@@ -325,3 +325,209 @@ class ReferenceSampler:
                 x = self.rand.sample(self.all_items, 1)[0]
             neg.append(x)
         return torch.from_numpy(np.vstack([us, self.i[sel], np.asarray(neg)]).astype(np.int64))
+
+
+# ---------------------------------------------------------------------------
+# SMORE on CPU (parity oracle for the SMORE path + the C3/C5 cpu_baseline leg)
+# ---------------------------------------------------------------------------
+class SMORECPU(torch.nn.Module):
+    """SMORE (src/models/smore.py:24-411) restated in torch on the CPU: parameters in
+    the reference's creation order (:38-138), graphs from the restatements above
+    (:45-75, 176-207), forward (:256-349), bpr_loss / InfoNCE / calculate_loss
+    (:352-411).  inject_mode 'residual', spectral_weight_norm True (the YAML
+    defaults); the diagnostics (.item() statistics) are omitted, they change no state."""
+
+    def __init__(self, train_u, train_i, n_users, n_items, v_feat, t_feat, d=64, n_ui_layers=4, n_layers=1,
+                 reg_weight=1e-5, image_k=20, text_k=15, dropout=0.0, cl_loss=0.01, cl_temp=0.2, batch_size=2048,
+                 init: dict | None = None):
+        super().__init__()
+        nn = torch.nn
+        self.n_users, self.n_items, self.d = n_users, n_items, d
+        self.n_ui_layers, self.n_layers = n_ui_layers, n_layers
+        self.reg_weight, self.cl_loss, self.cl_temp, self.batch_size = reg_weight, cl_loss, cl_temp, batch_size
+        self.inject_scale = 0.7
+        self.dropout = nn.Dropout(p=dropout)
+        self.user_embedding = nn.Embedding(n_users, d)
+        self.item_id_embedding = nn.Embedding(n_items, d)
+        nn.init.xavier_uniform_(self.user_embedding.weight)
+        nn.init.xavier_uniform_(self.item_id_embedding.weight)
+        self.norm_adj, self.R = smore_norm_adj(np.asarray(train_u), np.asarray(train_i), n_users, n_items)
+        v = torch.as_tensor(np.asarray(v_feat, dtype=np.float32))
+        t = torch.as_tensor(np.asarray(t_feat, dtype=np.float32))
+        self.image_embedding = nn.Embedding.from_pretrained(v.clone(), freeze=False)
+        self.image_original_adj = knn_normalized_graph(v, image_k)
+        self.text_embedding = nn.Embedding.from_pretrained(t.clone(), freeze=False)
+        self.text_original_adj = knn_normalized_graph(t, text_k)
+        self.fusion_adj = max_pool_fusion(self.image_original_adj, self.text_original_adj)
+        self.image_trs = nn.Linear(v.shape[1], d)
+        self.text_trs = nn.Linear(t.shape[1], d)
+        self.query_v = nn.Sequential(nn.Linear(d, d), nn.Tanh(), nn.Linear(d, d, bias=False))
+        self.query_t = nn.Sequential(nn.Linear(d, d), nn.Tanh(), nn.Linear(d, d, bias=False))
+        self.gate_v = nn.Sequential(nn.Linear(d, d), nn.Sigmoid())
+        self.gate_t = nn.Sequential(nn.Linear(d, d), nn.Sigmoid())
+        self.gate_f = nn.Sequential(nn.Linear(d, d), nn.Sigmoid())
+        self.gate_image_prefer = nn.Sequential(nn.Linear(d, d), nn.Sigmoid())
+        self.gate_text_prefer = nn.Sequential(nn.Linear(d, d), nn.Sigmoid())
+        self.gate_fusion_prefer = nn.Sequential(nn.Linear(d, d), nn.Sigmoid())
+        self.image_complex_weight = nn.Parameter(torch.randn(1, d // 2 + 1, 2, dtype=torch.float32))
+        self.text_complex_weight = nn.Parameter(torch.randn(1, d // 2 + 1, 2, dtype=torch.float32))
+        self.fusion_complex_weight = nn.Parameter(torch.randn(1, d // 2 + 1, 2, dtype=torch.float32))
+        self.mg_interval, self.mg_alpha, self.mg_beta = 3, 0.5, 0.2
+        self.global_step = 0
+        if init is not None:
+            with torch.no_grad():
+                for n, p in self.named_parameters():
+                    p.copy_(torch.as_tensor(init[n]))
+
+    def spectrum_convolution(self, img, txt):
+        """smore.py:209-252 (band-energy diagnostics omitted)."""
+        fi = torch.fft.rfft(img, dim=1, norm="ortho")
+        ft = torch.fft.rfft(txt, dim=1, norm="ortho")
+
+        def unit(w):
+            wc = torch.view_as_complex(w)
+            return wc / (torch.abs(wc) + 1e-8)
+
+        n = img.shape[1]
+        cv = torch.fft.irfft(fi * unit(self.image_complex_weight), n=n, dim=1, norm="ortho")
+        ct = torch.fft.irfft(ft * unit(self.text_complex_weight), n=n, dim=1, norm="ortho")
+        cf = torch.fft.irfft(ft * fi * unit(self.fusion_complex_weight), n=n, dim=1, norm="ortho")
+        return cv, ct, cf
+
+    def forward(self, train=False):
+        """smore.py:256-349 (sparse=True, inject_mode='residual')."""
+        cv, ct, cf = self.spectrum_convolution(self.image_trs(self.image_embedding.weight),
+                                               self.text_trs(self.text_embedding.weight))
+        item_id = self.item_id_embedding.weight
+        img_i = item_id + self.inject_scale * self.gate_v(cv)
+        txt_i = item_id + self.inject_scale * self.gate_t(ct)
+        fus_i = item_id + self.inject_scale * self.gate_f(cf)
+        ego = torch.cat([self.user_embedding.weight, item_id], dim=0)
+        layers = [ego]
+        for _ in range(self.n_ui_layers):
+            ego = torch.sparse.mm(self.norm_adj, ego)
+            layers.append(ego)
+        content = torch.stack(layers, dim=1).mean(dim=1)
+        for _ in range(self.n_layers):
+            img_i = torch.sparse.mm(self.image_original_adj, img_i)
+        image_embeds = torch.cat([torch.sparse.mm(self.R, img_i), img_i], dim=0)
+        for _ in range(self.n_layers):
+            txt_i = torch.sparse.mm(self.text_original_adj, txt_i)
+        text_embeds = torch.cat([torch.sparse.mm(self.R, txt_i), txt_i], dim=0)
+        for _ in range(self.n_layers):
+            fus_i = torch.sparse.mm(self.fusion_adj, fus_i)
+        fusion_embeds = torch.cat([torch.sparse.mm(self.R, fus_i), fus_i], dim=0)
+        agg_img = torch.softmax(self.query_v(fusion_embeds), dim=-1) * image_embeds
+        agg_txt = torch.softmax(self.query_t(fusion_embeds), dim=-1) * text_embeds
+        ip = self.dropout(self.gate_image_prefer(content))
+        tp = self.dropout(self.gate_text_prefer(content))
+        fp = self.dropout(self.gate_fusion_prefer(content))
+        side = torch.mean(torch.stack([ip * agg_img, tp * agg_txt, fp * fusion_embeds]), dim=0)
+        all_e = content + side
+        u, i = torch.split(all_e, [self.n_users, self.n_items], dim=0)
+        if train:
+            return u, i, side, content
+        return u, i
+
+    @staticmethod
+    def info_nce(v1, v2, temp):
+        """smore.py:366-373."""
+        v1, v2 = F.normalize(v1, dim=1), F.normalize(v2, dim=1)
+        pos = torch.exp((v1 * v2).sum(dim=-1) / temp)
+        ttl = torch.exp(torch.matmul(v1, v2.transpose(0, 1)) / temp).sum(dim=1)
+        return torch.mean(-torch.log(pos / ttl))
+
+    def calculate_loss(self, inter):
+        """smore.py:352-364 (bpr_loss) + 375-391."""
+        users, pos, neg = inter[0], inter[1], inter[2]
+        ua, ia, side, content = self.forward(train=True)
+        self.global_step += 1
+        u, p, n = ua[users], ia[pos], ia[neg]
+        ps, ns = (u * p).sum(dim=1), (u * n).sum(dim=1)
+        reg = (0.5 * (u ** 2).sum() + 0.5 * (p ** 2).sum() + 0.5 * (n ** 2).sum()) / self.batch_size
+        mf = -torch.mean(F.logsigmoid(ps - ns))
+        su, si = torch.split(side, [self.n_users, self.n_items], dim=0)
+        cu, ci = torch.split(content, [self.n_users, self.n_items], dim=0)
+        cl = self.info_nce(si[pos], ci[pos], self.cl_temp) + self.info_nce(su[users], cu[users], self.cl_temp)
+        return mf + self.reg_weight * reg + 0.0 + self.cl_loss * cl
+
+
+def smore_train_batch(model: SMORECPU, opt, inter, lr, target_rel=1e-3, max_scale=20.0):
+    """One batch of Trainer._train_epoch on a model with mg_enable (src/common/trainer.py:
+    186-201, 244-336): loss, backward, Adam step, then the model-level mirror gradient
+    when global_step % mg_interval == 0.  Returns the batch loss (a float)."""
+    opt.zero_grad(set_to_none=True)
+    loss = model.calculate_loss(inter)
+    value = loss.item()
+    loss.backward()
+    opt.step()
+    if model.global_step % model.mg_interval == 0:
+        opt.zero_grad(set_to_none=True)
+        model.calculate_loss(inter).backward()
+        params, grads = [], []
+        for p in model.parameters():
+            if p.requires_grad and p.grad is not None:
+                params.append(p)
+                grads.append(p.grad.detach().clone())
+        with torch.no_grad():
+            g_all = torch.cat([g.view(-1) for g in grads])
+            grad_rms = float(g_all.norm() / (g_all.numel() ** 0.5))
+            p_all = torch.cat([p.detach().view(-1) for p in params])
+            param_rms = float(p_all.norm() / (p_all.numel() ** 0.5) + 1e-12)
+            alpha = max(model.mg_alpha, target_rel * param_rms / (lr * grad_rms + 1e-12))
+            alpha = min(alpha, model.mg_alpha * max_scale)
+            for p, g in zip(params, grads):
+                p.add_(-alpha * lr * g)
+        opt.zero_grad(set_to_none=True)
+        model.calculate_loss(inter).backward()
+        with torch.no_grad():
+            for p in model.parameters():
+                if p.requires_grad and p.grad is not None:
+                    p.grad.mul_(-model.mg_beta)
+            for p, g in zip(params, grads):
+                p.add_(+alpha * lr * g)
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+    return value
+
+
+class LayerGCNCPU:
+    """Reference-identical CPU LayerGCN training (src/models/layergcn.py:31-177):
+    per-epoch edge dropout (`pre_epoch_processing`, :51-70: torch.multinomial on the
+    normalised edge values, alternating with random.sample), the cosine-gated
+    propagation on the masked graph, BPR-sum + L2 loss, autograd, torch.optim.Adam."""
+
+    def __init__(self, train_u, train_i, n_users, n_items, user_emb, item_emb, K, reg, dropout, lr=1e-3, seed=999):
+        import random
+
+        self.rand = random.Random(seed)
+        self.n_users, self.n_items, self.K, self.reg, self.dropout = n_users, n_items, K, reg, dropout
+        self.norm_adj = lightgcn_norm_adj_vec(np.asarray(train_u), np.asarray(train_i), n_users, n_items)
+        self.edge_indices = torch.from_numpy(np.vstack([np.asarray(train_u), np.asarray(train_i)]).astype(np.int64))
+        self.edge_values = layergcn_normalize(self.edge_indices, n_users, n_items)
+        self.pruning_random = False
+        self.masked_adj = self.norm_adj
+        self.u = torch.nn.Parameter(torch.from_numpy(np.array(user_emb, dtype=np.float32)))
+        self.i = torch.nn.Parameter(torch.from_numpy(np.array(item_emb, dtype=np.float32)))
+        self.opt = torch.optim.Adam([self.u, self.i], lr=lr)
+
+    def pre_epoch(self):
+        if self.dropout <= 0.0:
+            self.masked_adj = self.norm_adj
+            return
+        n = self.edge_values.size(0)
+        keep_len = int(n * (1.0 - self.dropout))
+        if self.pruning_random:
+            keep = torch.tensor(self.rand.sample(range(n), keep_len))
+        else:
+            keep = torch.multinomial(self.edge_values, keep_len)
+        self.pruning_random = not self.pruning_random
+        self.masked_adj = layergcn_masked_adj(self.edge_indices, keep, self.n_users, self.n_items)
+
+    def step(self, trip: torch.Tensor) -> float:
+        self.opt.zero_grad()
+        loss = layergcn_loss(self.u, self.i, self.masked_adj, self.K, trip, self.reg)
+        v = loss.item()
+        loss.backward()
+        self.opt.step()
+        return v

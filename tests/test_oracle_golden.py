@@ -192,3 +192,17 @@ def test_reference_knn_cache_is_read(golden, tmp_path):
     assert load_reference_knn(str(tmp_path / "small.pt"), ni) is None
     (tmp_path / "junk.pt").write_bytes(b"not a torch file")
     assert load_reference_knn(str(tmp_path / "junk.pt"), ni) is None
+
+
+def test_layergcn_cpu_class_step0(golden):
+    """oracle.LayerGCNCPU (the C1 cpu_baseline): its first Adam step equals the reference's."""
+    z = golden("layergcn_small")
+    nu, ni = _nm(z)
+    U0, I0 = params(z, "init.", "LayerGCN")
+    m = O.LayerGCNCPU(z["train_u"], z["train_i"], nu, ni, U0, I0, 2, 1e-2, dropout=0.0)
+    m.pre_epoch()
+    loss = m.step(torch.from_numpy(z["epoch0_triplets"][:, :512].astype(np.int64)))
+    assert abs(loss - float(z["step0_loss"])) <= 1e-5 * abs(float(z["step0_loss"]))
+    pu, pi = params(z, "step0_param.", "LayerGCN")
+    np.testing.assert_allclose(m.u.detach().numpy(), pu, rtol=0, atol=2e-6)
+    np.testing.assert_allclose(m.i.detach().numpy(), pi, rtol=0, atol=2e-6)
