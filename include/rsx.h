@@ -456,6 +456,72 @@ int rsx_linear_wgrad(const float* g, const float* x, int64_t n, int32_t out_dim,
                      void* ws, size_t ws_bytes, rsx_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
+/* SMORE per-row blocks, InfoNCE and the multi-tensor Adam (smore_fuse.hip)   */
+/* ------------------------------------------------------------------------ */
+/*
+ * Modality gates (reference src/models/smore.py:262-272):
+ *   forward  (backward = 0): out[m] = item + scale * sigmoid(conv[m] W[m]^T + b[m])
+ *            (mul = 1: item * sigmoid(..)), m = v, t, f; rows [n, d], W [d, d].
+ *   backward (backward = 1): given gout[m] (NULL = zero) writes g_item, g_conv[m]
+ *            and dz[m] = d pre-activation (rows of the gate Linear's weight gradient,
+ *            dW = dz^T conv: rsx_smore_wgrad).
+ * d in {64, 128}.  Replaces gate_v/gate_t/gate_f + the inject step, forward and
+ * autograd backward.
+ */
+int rsx_smore_gates(int32_t backward, const float* const* conv, const float* item, const float* const* W,
+                    const float* const* b, int64_t n, int32_t d, float scale, int32_t mul, float* const* out,
+                    const float* const* gout, float* g_item, float* const* g_conv, float* const* dz,
+                    rsx_stream_t stream);
+/*
+ * Preference block (reference src/models/smore.py:320-341), over every user+item row:
+ *   W[7] / b[7]: query_v.0, query_v.2 (no bias), query_t.0, query_t.2 (no bias),
+ *   gate_image_prefer.0, gate_text_prefer.0, gate_fusion_prefer.0.
+ *   forward: side = mean(ip * softmax(qv(F)) * I, tp * softmax(qt(F)) * T, fp * F),
+ *            all = content + side; ip/tp/fp = dropout(sigmoid(Linear(content)), p_drop)
+ *            with the mask a hash of (*seed_dev, gate, row, feature) (p_drop = 0: off).
+ *   backward: from g_all (and g_side, may be NULL) writes g_content, g_image,
+ *            g_text, g_fusion, the recomputed tanh rows hv / ht and dz[7] (each
+ *            Linear's pre-activation gradient; wgrad inputs: F, hv, F, ht, content x3).
+ */
+int rsx_smore_pref(int32_t backward, const float* const* W, const float* const* b, const float* content,
+                   const float* image_emb, const float* text_emb, const float* fusion_emb, int64_t n, int32_t d,
+                   float p_drop, const int64_t* seed_dev, float* all_out, float* side_out, const float* g_all,
+                   const float* g_side, float* g_content, float* g_image, float* g_text, float* g_fusion,
+                   float* hv, float* ht, float* const* dz, rsx_stream_t stream);
+/*
+ * dW[p] = dz[p]^T x[p] ([d, d]) and db[p] = colsum(dz[p]) (db[p] may be NULL) for up to
+ * 8 pairs of [n, d] row sets: row-split partials + one ordered reduction.
+ */
+size_t rsx_smore_wgrad_ws_bytes(int64_t n, int32_t d, int32_t n_pairs);
+int rsx_smore_wgrad(int32_t n_pairs, const float* const* dz, const float* const* x, float* const* dw,
+                    float* const* db, int64_t n, int32_t d, void* ws, size_t ws_bytes, rsx_stream_t stream);
+/*
+ * SMORE's two InfoNCE terms (reference src/models/smore.py:380-387, called at :398-404):
+ *   loss_out[0] = InfoNCE(side[n_users + pos], content[n_users + pos], tau)   (cl_items)
+ *   loss_out[1] = InfoNCE(side[users], content[users], tau)                   (cl_users)
+ * InfoNCE(a, b) = mean_i -log(exp(<a_i, b_i>/tau) / sum_j exp(<a_i, b_j>/tau)) on
+ * F.normalize'd rows.  The workspace [rsx_smore_infonce_ws_bytes] written by the
+ * forward (normalised rows, norms, row sums) is read by the backward, which ADDS
+ * g_loss[0] * d cl_items + g_loss[1] * d cl_users into g_side / g_content [N, d].
+ */
+size_t rsx_smore_infonce_ws_bytes(int64_t batch, int32_t d);
+int rsx_smore_infonce_fwd(const float* side, const float* content, const int64_t* users, const int64_t* pos_items,
+                          int64_t n_users, int64_t batch, int32_t d, float tau, float* loss_out, void* ws,
+                          size_t ws_bytes, rsx_stream_t stream);
+int rsx_smore_infonce_bwd(const float* side, const float* content, const int64_t* users, const int64_t* pos_items,
+                          int64_t n_users, int64_t batch, int32_t d, float tau, const float* g_loss, float* g_side,
+                          float* g_content, void* ws, size_t ws_bytes, rsx_stream_t stream);
+/*
+ * torch.optim.Adam (single-tensor arithmetic, as rsx_rowwise's ADAM epilogue) over
+ * `count` flat tensors in one launch per 32 tensors; step_dev[i]: tensor i's
+ * (already incremented) int64 step count on the device.  Replaces the per-parameter
+ * optimizer loop of reference src/common/trainer.py:238 (optimizer.step()).
+ */
+int rsx_adam_multi(int32_t count, float* const* p, const float* const* g, float* const* m, float* const* v,
+                   const int64_t* const* step_dev, const int64_t* n, float lr, float beta1, float beta2, float eps,
+                   float weight_decay, rsx_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
 /* Row-sharded LightGCN over RCCL (one process per GPU)                       */
 /* ------------------------------------------------------------------------ */
 /*

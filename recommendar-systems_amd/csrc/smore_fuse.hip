@@ -1,0 +1,951 @@
+// smore_fuse.hip — SMORE's per-row MLP blocks, its InfoNCE terms and a
+// multi-tensor Adam, each one launch (gfx950, f32 MFMA: exact f32 products, f32 sums).
+//
+// Replaces, per SMORE forward/backward (reference src/models/smore.py):
+//  * the modality gates  g = sigmoid(Linear(conv)); item + 0.7 g     (:262-272)
+//  * the preference block: softmax(query MLP(fusion)) * view, the dropout'd
+//    sigmoid preference gates on the content rows, their mean, content + side
+//                                                                     (:320-341)
+//  * InfoNCE(side[pos], content[pos]) and InfoNCE(side[u], content[u]) (:380-387,
+//    :398-404): L2-normalise, B x B similarity GEMM, exp, row sums, -log ratio
+//  * torch.optim.Adam over every SMORE parameter tensor (trainer.py:133,238)
+// which torch ran as ~30 elementwise / GEMM / reduction kernels each (per SMORE
+// step under the mirror gradient, ~1000 launches of 5-20 us: C3 was launch-bound).
+//
+// Row fields.  A 16-row tile of [rows x D] lives in a wave as the accumulator
+// layout of v_mfma_f32_16x16x4f32 transposed: lane l = n + 16 g holds row n0 + n,
+// features 16 t + 4 g + r (t < D/16, r < 4) in register 4 t + r.  A row's D
+// features are 4 lanes' registers (row reductions: registers, then xor 16, 32);
+// loads and stores are float4s.  A matrix product z = W x of every row
+// (nn.Linear) is Z^T = W X^T on the MFMA with A = W (lane (o, g) reads W[o][k] for
+// the K slot k = 16 t + 4 g + r that its own B register x[n][k] holds: the K index
+// of an MFMA may be permuted freely when A and B agree), so Z lands in the same
+// field layout: a chain of Linears / activations never leaves registers.  W^T x
+// (the backward) reads W by columns the same way.  Weights stay in global memory
+// (a 16-64 KB matrix is L1/L2 resident; a float4 per lane feeds 4 MFMAs).
+//
+// Weight gradients: the backward kernels write each Linear's pre-activation
+// gradient rows dZ (and the recomputed hidden rows the second Linear of a query
+// MLP reads); rsx_smore_wgrad then forms dW = dZ^T X and db = colsum(dZ) for up
+// to 8 (dZ, X) pairs in one launch of row-split partials plus one ordered
+// reduction (deterministic).
+#include <cmath>
+
+#include "rsx_adam.hpp"
+#include "rsx_common.hpp"
+
+namespace rsx {
+namespace sf {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+template <int D>
+struct Fld {
+    floatx4 f[D / 16];
+};
+
+template <int D>
+__device__ __forceinline__ Fld<D> fzero() {
+    Fld<D> x;
+#pragma unroll
+    for (int t = 0; t < D / 16; ++t) x.f[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+    return x;
+}
+
+// row `row` of X [.., D] (row < 0: zeros); this lane's features 16t + 4g .. +3
+template <int D>
+__device__ __forceinline__ Fld<D> fload(const float* X, int64_t row, int g) {
+    Fld<D> x;
+#pragma unroll
+    for (int t = 0; t < D / 16; ++t) {
+        if (row >= 0) {
+            const float4 v = ld4(X + row * D + 16 * t + 4 * g);
+            x.f[t] = floatx4{v.x, v.y, v.z, v.w};
+        } else {
+            x.f[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+        }
+    }
+    return x;
+}
+
+template <int D>
+__device__ __forceinline__ void fstore(float* Y, int64_t row, int g, const Fld<D>& x) {
+    if (row < 0 || !Y) return;
+#pragma unroll
+    for (int t = 0; t < D / 16; ++t) st4(Y + row * D + 16 * t + 4 * g, make_float4(x.f[t][0], x.f[t][1], x.f[t][2], x.f[t][3]));
+}
+
+// a per-feature vector (bias) in the field layout
+template <int D>
+__device__ __forceinline__ Fld<D> fvec(const float* b, int g) {
+    return b ? fload<D>(b, 0, g) : fzero<D>();
+}
+
+template <int D, class F>
+__device__ __forceinline__ Fld<D> fmap(const Fld<D>& a, F fn) {
+    Fld<D> z;
+#pragma unroll
+    for (int t = 0; t < D / 16; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) z.f[t][r] = fn(a.f[t][r]);
+    return z;
+}
+template <int D, class F>
+__device__ __forceinline__ Fld<D> fmap2(const Fld<D>& a, const Fld<D>& b, F fn) {
+    Fld<D> z;
+#pragma unroll
+    for (int t = 0; t < D / 16; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) z.f[t][r] = fn(a.f[t][r], b.f[t][r]);
+    return z;
+}
+template <int D, class F>
+__device__ __forceinline__ Fld<D> fmap3(const Fld<D>& a, const Fld<D>& b, const Fld<D>& c, F fn) {
+    Fld<D> z;
+#pragma unroll
+    for (int t = 0; t < D / 16; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) z.f[t][r] = fn(a.f[t][r], b.f[t][r], c.f[t][r]);
+    return z;
+}
+
+// sum / max over a row's D features (every lane of the row gets it)
+template <int D>
+__device__ __forceinline__ float rsum(const Fld<D>& x) {
+    float s = 0.f;
+#pragma unroll
+    for (int t = 0; t < D / 16; ++t) s += (x.f[t][0] + x.f[t][1]) + (x.f[t][2] + x.f[t][3]);
+    s += __shfl_xor(s, 16, kWave);
+    s += __shfl_xor(s, 32, kWave);
+    return s;
+}
+template <int D>
+__device__ __forceinline__ float rmax(const Fld<D>& x) {
+    float s = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < D / 16; ++t) s = fmaxf(fmaxf(s, fmaxf(x.f[t][0], x.f[t][1])), fmaxf(x.f[t][2], x.f[t][3]));
+    s = fmaxf(s, __shfl_xor(s, 16, kWave));
+    s = fmaxf(s, __shfl_xor(s, 32, kWave));
+    return s;
+}
+
+__device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// z[n][o] = sum_k W[o][k] x[n][k]  (+ b[o]),  W [D][D] row-major (nn.Linear weight).
+// K outer, output tiles inner: consecutive MFMAs go to different accumulators (the
+// 16x16x4 form's dependent latency is 40 cycles against a 32-cycle issue).
+template <int D>
+__device__ __forceinline__ Fld<D> mv(const float* __restrict__ W, const float* b, const Fld<D>& x, int lane) {
+    constexpr int T = D / 16;
+    const int c = lane & 15, g = lane >> 4;
+    Fld<D> z = fvec<D>(b, g);
+    const float* wr = W + (int64_t)c * D + 4 * g;
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        float4 w[T];
+#pragma unroll
+        for (int to = 0; to < T; ++to) w[to] = ld4(wr + (int64_t)16 * to * D + 16 * t);
+#pragma unroll
+        for (int to = 0; to < T; ++to) z.f[to] = mfma4(w[to].x, x.f[t][0], z.f[to]);
+#pragma unroll
+        for (int to = 0; to < T; ++to) z.f[to] = mfma4(w[to].y, x.f[t][1], z.f[to]);
+#pragma unroll
+        for (int to = 0; to < T; ++to) z.f[to] = mfma4(w[to].z, x.f[t][2], z.f[to]);
+#pragma unroll
+        for (int to = 0; to < T; ++to) z.f[to] = mfma4(w[to].w, x.f[t][3], z.f[to]);
+    }
+    return z;
+}
+
+// z[n][k] = sum_o W[o][k] x[n][o]  (the input gradient of a Linear)
+template <int D>
+__device__ __forceinline__ Fld<D> mvt(const float* __restrict__ W, const Fld<D>& x, int lane) {
+    constexpr int T = D / 16;
+    const int c = lane & 15, g = lane >> 4;
+    Fld<D> z = fzero<D>();
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float* wr = W + (int64_t)(16 * t + 4 * g + r) * D + c;
+#pragma unroll
+            for (int tk = 0; tk < T; ++tk) z.f[tk] = mfma4(wr[16 * tk], x.f[t][r], z.f[tk]);
+        }
+    }
+    return z;
+}
+
+// S^T tile: s[r] = <Y row (4g + r), X row c> over D (two accumulators, summed at the end)
+template <int D>
+__device__ __forceinline__ floatx4 tile_dot(const Fld<D>& Y, const Fld<D>& X) {
+    constexpr int T = D / 16;
+    floatx4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < T; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; r += 2) {
+            s0 = mfma4(Y.f[t][r], X.f[t][r], s0);
+            s1 = mfma4(Y.f[t][r + 1], X.f[t][r + 1], s1);
+        }
+    return s0 + s1;
+}
+
+struct Sigm {
+    __device__ float operator()(float x) const { return 1.f / (1.f + expf(-x)); }
+};
+struct Tanh {
+    __device__ float operator()(float x) const { return tanhf(x); }
+};
+constexpr Sigm sigm{};
+constexpr Tanh tanh_{};
+
+template <int D>
+__device__ __forceinline__ Fld<D> softmax_row(const Fld<D>& q) {
+    const float mx = rmax<D>(q);
+    const Fld<D> e = fmap<D>(q, [&](float v) { return expf(v - mx); });
+    const float s = rsum<D>(e);
+    return fmap<D>(e, [&](float v) { return v / s; });
+}
+
+// dropout keep-scale of element (row, feature) of preference gate `gate`: 0 or 1/(1-p)
+__device__ __forceinline__ uint32_t mix32(uint64_t x) {
+    x ^= x >> 33;
+    x *= 0xff51afd7ed558ccdULL;
+    x ^= x >> 33;
+    x *= 0xc4ceb9fe1a85ec53ULL;
+    x ^= x >> 33;
+    return (uint32_t)x;
+}
+template <int D>
+__device__ __forceinline__ Fld<D> drop_scale(uint64_t seed, int gate, int64_t row, int g, float p, float scale) {
+    Fld<D> m;
+    const uint32_t thr = (uint32_t)fminf(p * 4294967296.f, 4294967295.f);
+#pragma unroll
+    for (int t = 0; t < D / 16; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const uint64_t key = seed * 0x9E3779B97F4A7C15ULL + ((uint64_t)gate << 58) + (uint64_t)row * D +
+                                 (uint64_t)(16 * t + 4 * g + r);
+            m.f[t][r] = mix32(key) >= thr ? scale : 0.f;
+        }
+    return m;
+}
+
+// ---------------------------------------------------------------------------
+// modality gates (smore.py:262-272)
+// ---------------------------------------------------------------------------
+struct GateArgs {
+    const float* conv[3];   // conv_v, conv_t, conv_f [n, D]
+    const float* item;      // item_id embedding [n, D]
+    const float* W[3];      // gate_v/t/f Linear weights [D, D]
+    const float* b[3];
+    int64_t n;
+    float scale;            // inject_scale (residual mode)
+    int32_t mul;            // inject_mode == "mul"
+    int32_t pad0;
+    float* out[3];          // forward: img_i, txt_i, fus_i
+    const float* gout[3];   // backward: their gradients (NULL = zero)
+    float* g_item;          // backward outputs
+    float* g_conv[3];
+    float* dz[3];           // pre-activation gradients (wgrad rows)
+};
+
+template <int D>
+__global__ __launch_bounds__(256) void gates_fwd(GateArgs a) {
+    const int lane = threadIdx.x & 63, g = lane >> 4;
+    const int64_t n0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 16;
+    if (n0 >= a.n) return;
+    const int64_t row = n0 + (lane & 15) < a.n ? n0 + (lane & 15) : -1;
+    const Fld<D> it = fload<D>(a.item, row, g);
+#pragma unroll 1
+    for (int m = 0; m < 3; ++m) {
+        const Fld<D> cv = fload<D>(a.conv[m], row, g);
+        const Fld<D> s = fmap<D>(mv<D>(a.W[m], a.b[m], cv, lane), sigm);
+        const Fld<D> o = a.mul ? fmap2<D>(it, s, [](float x, float y) { return x * y; })
+                               : fmap2<D>(it, s, [&](float x, float y) { return x + a.scale * y; });
+        fstore<D>(a.out[m], row, g, o);
+    }
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void gates_bwd(GateArgs a) {
+    const int lane = threadIdx.x & 63, g = lane >> 4;
+    const int64_t n0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 16;
+    if (n0 >= a.n) return;
+    const int64_t row = n0 + (lane & 15) < a.n ? n0 + (lane & 15) : -1;
+    const Fld<D> it = fload<D>(a.item, row, g);
+    Fld<D> gi = fzero<D>();
+#pragma unroll 1
+    for (int m = 0; m < 3; ++m) {
+        const Fld<D> go = a.gout[m] ? fload<D>(a.gout[m], row, g) : fzero<D>();
+        const Fld<D> cv = fload<D>(a.conv[m], row, g);
+        const Fld<D> s = fmap<D>(mv<D>(a.W[m], a.b[m], cv, lane), sigm);
+        Fld<D> ds;
+        if (a.mul) {
+            gi = fmap3<D>(gi, go, s, [](float acc, float x, float y) { return acc + x * y; });
+            ds = fmap2<D>(go, it, [](float x, float y) { return x * y; });
+        } else {
+            gi = fmap2<D>(gi, go, [](float acc, float x) { return acc + x; });
+            ds = fmap<D>(go, [&](float x) { return a.scale * x; });
+        }
+        const Fld<D> dz = fmap2<D>(ds, s, [](float x, float y) { return x * ((1.f - y) * y); });
+        fstore<D>(a.dz[m], row, g, dz);
+        fstore<D>(a.g_conv[m], row, g, mvt<D>(a.W[m], dz, lane));
+    }
+    fstore<D>(a.g_item, row, g, gi);
+}
+
+// ---------------------------------------------------------------------------
+// preference block (smore.py:320-341)
+// ---------------------------------------------------------------------------
+enum { kW1v = 0, kW2v, kW1t, kW2t, kWip, kWtp, kWfp, kNW };
+
+struct PrefArgs {
+    const float* W[kNW];     // query_v.0, query_v.2, query_t.0, query_t.2, gate_{image,text,fusion}_prefer.0
+    const float* b[kNW];     // biases (query_*.2 have none: NULL)
+    const float* C;          // content rows [n, D]
+    const float* IE;         // image_embeds
+    const float* TE;         // text_embeds
+    const float* FE;         // fusion_embeds
+    int64_t n;
+    float p_drop;            // dropout probability of the three preference gates (0 = eval / off)
+    float drop_scale;        // 1 / (1 - p)
+    const int64_t* seed;     // device word: the call's dropout seed
+    float* all;              // forward outputs: content + side, side
+    float* side;
+    const float* g_all;      // backward inputs (g_side may be NULL)
+    const float* g_side;
+    float* gC;               // backward outputs
+    float* gIE;
+    float* gTE;
+    float* gFE;
+    float* hv;               // recomputed tanh rows of the query MLPs (wgrad inputs)
+    float* ht;
+    float* dz[kNW];          // pre-activation gradients (wgrad rows)
+};
+
+template <int D>
+__global__ __launch_bounds__(256) void pref_fwd(PrefArgs a) {
+    const int lane = threadIdx.x & 63, g = lane >> 4;
+    const int64_t n0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 16;
+    if (n0 >= a.n) return;
+    const int64_t row = n0 + (lane & 15) < a.n ? n0 + (lane & 15) : -1;
+    const uint64_t seed = a.p_drop > 0.f ? (uint64_t)*a.seed : 0;
+    const auto mul = [](float x, float y) { return x * y; };
+    const Fld<D> FE = fload<D>(a.FE, row, g);
+    const Fld<D> C = fload<D>(a.C, row, g);
+    // agg_img = ip * (softmax(query_v(FE)) * IE)
+    Fld<D> h = fmap<D>(mv<D>(a.W[kW1v], a.b[kW1v], FE, lane), tanh_);
+    Fld<D> s = softmax_row<D>(mv<D>(a.W[kW2v], nullptr, h, lane));
+    Fld<D> ip = fmap<D>(mv<D>(a.W[kWip], a.b[kWip], C, lane), sigm);
+    if (a.p_drop > 0.f) ip = fmap2<D>(ip, drop_scale<D>(seed, 0, row, g, a.p_drop, a.drop_scale), mul);
+    const Fld<D> x1 = fmap3<D>(ip, s, fload<D>(a.IE, row, g), [](float p, float q, float e) { return p * (q * e); });
+    h = fmap<D>(mv<D>(a.W[kW1t], a.b[kW1t], FE, lane), tanh_);
+    s = softmax_row<D>(mv<D>(a.W[kW2t], nullptr, h, lane));
+    Fld<D> tp = fmap<D>(mv<D>(a.W[kWtp], a.b[kWtp], C, lane), sigm);
+    if (a.p_drop > 0.f) tp = fmap2<D>(tp, drop_scale<D>(seed, 1, row, g, a.p_drop, a.drop_scale), mul);
+    const Fld<D> x2 = fmap3<D>(tp, s, fload<D>(a.TE, row, g), [](float p, float q, float e) { return p * (q * e); });
+    Fld<D> fp = fmap<D>(mv<D>(a.W[kWfp], a.b[kWfp], C, lane), sigm);
+    if (a.p_drop > 0.f) fp = fmap2<D>(fp, drop_scale<D>(seed, 2, row, g, a.p_drop, a.drop_scale), mul);
+    // side = mean(stack([x1, x2, fp * FE]))  (sum, then * 1/3 as torch's mean)
+    const Fld<D> sd = fmap3<D>(x1, x2, fmap2<D>(fp, FE, mul),
+                               [](float u, float v, float w) { return ((u + v) + w) * (1.f / 3.f); });
+    fstore<D>(a.side, row, g, sd);
+    fstore<D>(a.all, row, g, fmap2<D>(C, sd, [](float u, float v) { return u + v; }));
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void pref_bwd(PrefArgs a) {
+    const int lane = threadIdx.x & 63, g = lane >> 4;
+    const int64_t n0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 16;
+    if (n0 >= a.n) return;
+    const int64_t row = n0 + (lane & 15) < a.n ? n0 + (lane & 15) : -1;
+    const uint64_t seed = a.p_drop > 0.f ? (uint64_t)*a.seed : 0;
+    const auto mul = [](float x, float y) { return x * y; };
+    const auto add = [](float x, float y) { return x + y; };
+    const auto sig_bwd = [](float gy, float y) { return gy * ((1.f - y) * y); };
+    const Fld<D> gA = fload<D>(a.g_all, row, g);
+    // d side = g_all + g_side;  each of the three stacked views gets d side / 3
+    const Fld<D> g1 = a.g_side ? fmap2<D>(gA, fload<D>(a.g_side, row, g), [](float u, float v) { return (u + v) * (1.f / 3.f); })
+                               : fmap<D>(gA, [](float u) { return u * (1.f / 3.f); });
+    const Fld<D> FE = fload<D>(a.FE, row, g);
+    const Fld<D> C = fload<D>(a.C, row, g);
+    Fld<D> gC = gA;
+    Fld<D> gFE;
+    {   // fusion view: x3 = fp * FE
+        const Fld<D> sf = fmap<D>(mv<D>(a.W[kWfp], a.b[kWfp], C, lane), sigm);
+        const Fld<D> mf = a.p_drop > 0.f ? drop_scale<D>(seed, 2, row, g, a.p_drop, a.drop_scale) : Fld<D>{};
+        const Fld<D> fp = a.p_drop > 0.f ? fmap2<D>(sf, mf, mul) : sf;
+        Fld<D> dp = fmap2<D>(g1, FE, mul);
+        if (a.p_drop > 0.f) dp = fmap2<D>(dp, mf, mul);
+        const Fld<D> dz = fmap2<D>(dp, sf, sig_bwd);
+        fstore<D>(a.dz[kWfp], row, g, dz);
+        gC = fmap2<D>(gC, mvt<D>(a.W[kWfp], dz, lane), add);
+        gFE = fmap2<D>(g1, fp, mul);
+    }
+#pragma unroll 1
+    for (int v = 0; v < 2; ++v) {  // v = 0: image view, 1: text view
+        const int w1 = v ? kW1t : kW1v, w2 = v ? kW2t : kW2v, wp = v ? kWtp : kWip;
+        const Fld<D> h = fmap<D>(mv<D>(a.W[w1], a.b[w1], FE, lane), tanh_);
+        fstore<D>(v ? a.ht : a.hv, row, g, h);
+        const Fld<D> s = softmax_row<D>(mv<D>(a.W[w2], nullptr, h, lane));
+        const Fld<D> sp = fmap<D>(mv<D>(a.W[wp], a.b[wp], C, lane), sigm);
+        const Fld<D> mp = a.p_drop > 0.f ? drop_scale<D>(seed, v, row, g, a.p_drop, a.drop_scale) : Fld<D>{};
+        const Fld<D> pp = a.p_drop > 0.f ? fmap2<D>(sp, mp, mul) : sp;
+        const Fld<D> E = fload<D>(v ? a.TE : a.IE, row, g);
+        // x = pp * (s * E)
+        Fld<D> dpp = fmap3<D>(g1, s, E, [](float u, float q, float e) { return u * (q * e); });
+        if (a.p_drop > 0.f) dpp = fmap2<D>(dpp, mp, mul);
+        const Fld<D> dzp = fmap2<D>(dpp, sp, sig_bwd);
+        fstore<D>(a.dz[wp], row, g, dzp);
+        gC = fmap2<D>(gC, mvt<D>(a.W[wp], dzp, lane), add);
+        const Fld<D> da = fmap2<D>(g1, pp, mul);          // d (s * E)
+        fstore<D>(v ? a.gTE : a.gIE, row, g, fmap2<D>(da, s, mul));
+        const Fld<D> dsm = fmap2<D>(da, E, mul);          // d softmax output
+        const float dot = rsum<D>(fmap2<D>(dsm, s, mul));
+        const Fld<D> dq = fmap2<D>(s, dsm, [&](float y, float gy) { return y * (gy - dot); });
+        fstore<D>(a.dz[w2], row, g, dq);
+        const Fld<D> dh = mvt<D>(a.W[w2], dq, lane);
+        const Fld<D> dz1 = fmap2<D>(dh, h, [](float gy, float y) { return gy * (1.f - y * y); });
+        fstore<D>(a.dz[w1], row, g, dz1);
+        gFE = fmap2<D>(gFE, mvt<D>(a.W[w1], dz1, lane), add);
+    }
+    fstore<D>(a.gC, row, g, gC);
+    fstore<D>(a.gFE, row, g, gFE);
+}
+
+// ---------------------------------------------------------------------------
+// batched weight gradients: dW_p = dZ_p^T X_p, db_p = colsum(dZ_p)
+// ---------------------------------------------------------------------------
+constexpr int kWgPairs = 8, kWgRows = 512;
+
+struct WgArgs {
+    const float* dz[kWgPairs];  // [n, D]
+    const float* x[kWgPairs];   // [n, D]
+    float* dw[kWgPairs];        // [D, D]
+    float* db[kWgPairs];        // [D] or NULL
+    int32_t n_pairs;
+    int32_t n_splits;
+    int64_t n;
+    float* part;                // [n_pairs][n_splits][D*D + D]
+};
+
+// block (split, pair); wave w owns output row tiles to = w, w+4, ..; lane (k, g)
+template <int D>
+__global__ __launch_bounds__(256) void wgrad_part(WgArgs a) {
+    constexpr int T = D / 16, TPW = (T + 3) / 4;
+    const int split = blockIdx.x, pr = blockIdx.y;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
+    const float* __restrict__ dz = a.dz[pr];
+    const float* __restrict__ x = a.x[pr];
+    const int64_t r0 = (int64_t)split * kWgRows, r1 = min(a.n, r0 + kWgRows);
+    float* out = a.part + ((int64_t)pr * a.n_splits + split) * (D * D + D);
+#pragma unroll 1
+    for (int q = 0; q < TPW; ++q) {
+        const int to = w + 4 * q;
+        if (to >= T) break;
+        floatx4 acc[T];
+#pragma unroll
+        for (int tk = 0; tk < T; ++tk) acc[tk] = floatx4{0.f, 0.f, 0.f, 0.f};
+        float bs = 0.f;
+        for (int64_t r = r0; r < r1; r += 4) {
+            const int64_t rr = r + g;
+            const bool ok = rr < r1;
+            const float av = ok ? dz[rr * D + 16 * to + c] : 0.f;  // A[o = 16to + c][K = rr]
+            bs += av;
+#pragma unroll
+            for (int tk = 0; tk < T; ++tk) {
+                const float bv = ok ? x[rr * D + 16 * tk + c] : 0.f;  // B[K = rr][k = 16tk + c]
+                acc[tk] = mfma4(av, bv, acc[tk]);
+            }
+        }
+        // D[o][k]: lane (k, g) reg r holds o = 16to + 4g + r, k = 16tk + c
+#pragma unroll
+        for (int tk = 0; tk < T; ++tk)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) out[(16 * to + 4 * g + r) * D + 16 * tk + c] = acc[tk][r];
+        bs += __shfl_xor(bs, 16, kWave);
+        bs += __shfl_xor(bs, 32, kWave);
+        if (g == 0) out[D * D + 16 * to + c] = bs;
+    }
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void wgrad_reduce(WgArgs a) {
+    const int pr = blockIdx.y;
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= D * D + D) return;
+    const float* p = a.part + (int64_t)pr * a.n_splits * (D * D + D) + e;
+    float s = 0.f;
+    for (int i = 0; i < a.n_splits; ++i) s += p[(int64_t)i * (D * D + D)];
+    if (e < D * D) a.dw[pr][e] = s;
+    else if (a.db[pr]) a.db[pr][e - D * D] = s;
+}
+
+// ---------------------------------------------------------------------------
+// InfoNCE (smore.py:380-387) over two (view1, view2) row sets
+// ---------------------------------------------------------------------------
+// term t: view1 rows src1[idx_t[b] + off_t], view2 rows src2[idx_t[b] + off_t], b < B.
+// Forward block (own tile of 16 rows, term): waves split the other tiles; each
+// normalises what it loads (F.normalize: x / max(|x|, 1e-12)); S = n1 n2^T / tau on the
+// MFMA (A = other rows, B = own rows: S^T lands with the own row per lane), row sums of
+// exp(S) combined over waves in order; l_b = -log(pos_b / ttl_b).  The normalised rows,
+// norms and ttl go to the workspace for the backward; the last block adds each term's
+// l_b in order (mean).
+// Backward block (own tile, mode, term): P = exp(S)/ttl_i; mode 0 (own = view1 rows i):
+// O_i = sum_j P_ij n2_j; mode 1 (own = view2 rows j): O_j = sum_i P_ij n1_i (ttl by the
+// other row).  d n = g/(B tau) (O - n_other_own); through F.normalize; atomically added
+// into the row's gradient (pos items / users repeat within a batch).
+constexpr int kNceWaves = 8;
+
+struct NceArgs {
+    const float* src1;       // side   [N, D]
+    const float* src2;       // content [N, D]
+    const int64_t* idx[2];   // [B] each
+    int64_t off[2];
+    int64_t B;
+    float tau;
+    int32_t pad0;
+    float* nrm;              // ws: [2 terms][2 views][B][D] normalised rows
+    float* norms;            // ws: [2][2][B] |x|
+    float* ttl;              // ws: [2][B]
+    float* lrow;             // ws: [2][B]
+    float* loss;             // [2]: cl_items, cl_users
+    const float* gloss;      // backward: [2] upstream gradients of the two losses
+    float* g1;               // d src1 [N, D] (accumulated)
+    float* g2;               // d src2
+};
+
+template <int D>
+__device__ __forceinline__ Fld<D> nce_load_norm(const NceArgs& a, int term, int view, int64_t b, int g, float* nrm_out) {
+    const int64_t row = b >= 0 ? a.idx[term][b] + a.off[term] : -1;
+    Fld<D> x = fload<D>(view ? a.src2 : a.src1, row, g);
+    const float n = sqrtf(rsum<D>(fmap<D>(x, [](float v) { return v * v; })));
+    const float den = fmaxf(n, 1e-12f);
+    if (nrm_out) *nrm_out = n;
+    return fmap<D>(x, [&](float v) { return v / den; });
+}
+
+template <int D>
+__global__ __launch_bounds__(64 * kNceWaves) void nce_fwd(NceArgs a) {
+    __shared__ float part[kNceWaves][16];
+    const int term = blockIdx.y;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
+    const int64_t B = a.B;
+    const int64_t n0 = (int64_t)blockIdx.x * 16;
+    const int64_t bo = n0 + c < B ? n0 + c : -1;
+    float nn1 = 0.f;
+    const Fld<D> X = nce_load_norm<D>(a, term, 0, bo, g, &nn1);  // own view1 rows (B operand)
+    const int64_t ntile = (B + 15) / 16;
+    float es = 0.f;  // exp sum of own row c over the other rows 4g + r of this wave's tiles
+    for (int64_t mt = w; mt < ntile; mt += kNceWaves) {
+        const int64_t m0 = mt * 16;
+        const int64_t bm = m0 + c < B ? m0 + c : -1;
+        const Fld<D> Y = nce_load_norm<D>(a, term, 1, bm, g, nullptr);  // other view2 rows (A operand)
+        const floatx4 s = tile_dot<D>(Y, X);  // s[r] = S[own c][other m0 + 4g + r] * tau
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            if (m0 + 4 * g + r < B) es += expf(s[r] / a.tau);
+    }
+    es += __shfl_xor(es, 16, kWave);
+    es += __shfl_xor(es, 32, kWave);
+    if (lane < 16) part[w][lane] = es;
+    float dot = 0.f;
+    if (w == 0) {  // own rows' normalised views and norms, kept for the backward
+        fstore<D>(a.nrm + ((int64_t)(term * 2 + 0) * B) * D, bo, g, X);
+        if (g == 0 && bo >= 0) a.norms[(term * 2 + 0) * B + bo] = nn1;
+        float nn2 = 0.f;
+        const Fld<D> X2 = nce_load_norm<D>(a, term, 1, bo, g, &nn2);
+        fstore<D>(a.nrm + ((int64_t)(term * 2 + 1) * B) * D, bo, g, X2);
+        if (g == 0 && bo >= 0) a.norms[(term * 2 + 1) * B + bo] = nn2;
+        dot = rsum<D>(fmap2<D>(X, X2, [](float u, float v) { return u * v; }));  // (n1 * n2).sum(-1)
+    }
+    __syncthreads();
+    if (w == 0 && lane < 16 && bo >= 0) {
+        float ttl = 0.f;
+#pragma unroll
+        for (int i = 0; i < kNceWaves; ++i) ttl += part[i][lane];
+        const float pos = expf(dot / a.tau);
+        a.ttl[term * B + bo] = ttl;
+        a.lrow[term * B + bo] = -logf(pos / ttl);
+    }
+}
+
+// the two means (cl_items, cl_users): one wave per term, rows summed in a fixed order
+__global__ __launch_bounds__(64) void nce_mean(NceArgs a) {
+    const int term = blockIdx.x, lane = threadIdx.x;
+    const float* l = a.lrow + (int64_t)term * a.B;
+    double acc = 0.0;
+    for (int64_t i = lane; i < a.B; i += 64) acc += (double)l[i];
+    acc = group_sum_d<64>(acc);
+    if (lane == 0) a.loss[term] = (float)(acc / (double)a.B);
+}
+
+template <int D>
+__global__ __launch_bounds__(64 * kNceWaves) void nce_bwd(NceArgs a) {
+    constexpr int T = D / 16;
+    __shared__ floatx4 red[kNceWaves][64][T];
+    const int term = blockIdx.z, mode = blockIdx.y;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
+    const int64_t B = a.B;
+    const int64_t n0 = (int64_t)blockIdx.x * 16;
+    const int64_t bo = n0 + c < B ? n0 + c : -1;
+    const float* own_n = a.nrm + ((int64_t)(term * 2 + mode) * B) * D;
+    const float* oth_n = a.nrm + ((int64_t)(term * 2 + (mode ^ 1)) * B) * D;
+    const float* ttl = a.ttl + term * B;
+    const Fld<D> X = fload<D>(own_n, bo, g);
+    const float inv_tau = 1.f / a.tau;
+    const float ttl_own = (mode == 0 && bo >= 0) ? ttl[bo] : 1.f;
+    Fld<D> O = fzero<D>();
+    const int64_t ntile = (B + 15) / 16;
+    for (int64_t mt = w; mt < ntile; mt += kNceWaves) {
+        const int64_t m0 = mt * 16;
+        const int64_t bm = m0 + c < B ? m0 + c : -1;
+        const Fld<D> Y = fload<D>(oth_n, bm, g);
+        const floatx4 s = tile_dot<D>(Y, X);
+        // P for own row c and other rows m0 + 4g + r
+        floatx4 p;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int64_t m = m0 + 4 * g + r;
+            const float den = mode == 0 ? ttl_own : (m < B ? ttl[m] : 1.f);
+            p[r] = m < B ? expf(s[r] / a.tau) / den : 0.f;
+        }
+        // O^T[k][own] += sum_m Y^T[k][m] P^T[m][own]: K slot (r, g) = other row m0 + 4g + r
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int64_t m = m0 + 4 * g + r;
+            const float* yr = oth_n + (m < B ? m : 0) * D + c;
+#pragma unroll
+            for (int tk = 0; tk < T; ++tk) O.f[tk] = mfma4(m < B ? yr[16 * tk] : 0.f, p[r], O.f[tk]);
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < T; ++t) red[w][lane][t] = O.f[t];
+    __syncthreads();
+    if (w != 0) return;
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        floatx4 s = red[0][lane][t];
+#pragma unroll
+        for (int i = 1; i < kNceWaves; ++i) s += red[i][lane][t];
+        O.f[t] = s;
+    }
+    if (bo < 0) return;
+    const float coef = a.gloss[term] * inv_tau / (float)B;
+    const Fld<D> Z = fload<D>(oth_n, bo, g);  // the own row's other view
+    const Fld<D> dn = fmap2<D>(O, Z, [&](float o, float z) { return coef * (o - z); });
+    // F.normalize backward: (dn - y <y, dn>) / |x|, or dn / eps when |x| <= eps
+    const float nx = a.norms[(term * 2 + mode) * B + bo];
+    Fld<D> dv;
+    if (nx > 1e-12f) {
+        const float yd = rsum<D>(fmap2<D>(X, dn, [](float u, float v) { return u * v; }));
+        dv = fmap2<D>(dn, X, [&](float u, float y) { return (u - y * yd) / nx; });
+    } else {
+        dv = fmap<D>(dn, [](float u) { return u / 1e-12f; });
+    }
+    float* dst = (mode == 0 ? a.g1 : a.g2) + (a.idx[term][bo] + a.off[term]) * D;
+#pragma unroll
+    for (int t = 0; t < T; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) atomicAdd(dst + 16 * t + 4 * g + r, dv.f[t][r]);
+}
+
+// ---------------------------------------------------------------------------
+// multi-tensor Adam
+// ---------------------------------------------------------------------------
+constexpr int kAdamMax = 32, kAdamPerBlock = 2048;
+
+struct AdamList {
+    float* p[kAdamMax];
+    const float* g[kAdamMax];
+    float* m[kAdamMax];
+    float* v[kAdamMax];
+    const int64_t* step[kAdamMax];
+    int64_t n[kAdamMax];
+    int64_t blk[kAdamMax + 1];
+    int32_t count;
+    float lr, beta1, beta2, eps, wd;
+};
+
+__global__ __launch_bounds__(256) void adam_multi(AdamList L) {
+    int t = 0;
+    while (t + 1 < L.count && (int64_t)blockIdx.x >= L.blk[t + 1]) ++t;
+    rsx_adam cfg;
+    cfg.lr = L.lr;
+    cfg.beta1 = L.beta1;
+    cfg.beta2 = L.beta2;
+    cfg.eps = L.eps;
+    cfg.weight_decay = L.wd;
+    cfg.step_dev = L.step[t];
+    cfg.step = 1;
+    const AdamConst c = adam_const(cfg);
+    float* __restrict__ p = L.p[t];
+    const float* __restrict__ gr = L.g[t];
+    float* __restrict__ m = L.m[t];
+    float* __restrict__ v = L.v[t];
+    const int64_t base = ((int64_t)blockIdx.x - L.blk[t]) * kAdamPerBlock;
+    const int64_t n = L.n[t];
+#pragma unroll
+    for (int k = 0; k < kAdamPerBlock / 256; ++k) {
+        const int64_t i = base + k * 256 + threadIdx.x;
+        if (i < n) {
+            float pp = p[i], mm = m[i], vv = v[i];
+            adam_elem(c, pp, mm, vv, gr[i]);
+            p[i] = pp;
+            m[i] = mm;
+            v[i] = vv;
+        }
+    }
+}
+
+}  // namespace sf
+}  // namespace rsx
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+using namespace rsx;
+
+extern "C" {
+
+int rsx_smore_gates(int32_t backward, const float* const* conv, const float* item, const float* const* W,
+                    const float* const* b, int64_t n, int32_t d, float scale, int32_t mul, float* const* out,
+                    const float* const* gout, float* g_item, float* const* g_conv, float* const* dz,
+                    rsx_stream_t stream) {
+    if (n < 0 || !conv || !item || !W || !b) return RSX_ERR_ARG;
+    if (n == 0) return RSX_OK;
+    sf::GateArgs a{};
+    for (int m = 0; m < 3; ++m) {
+        a.conv[m] = conv[m];
+        a.W[m] = W[m];
+        a.b[m] = b[m];
+        if (!conv[m] || !W[m]) return RSX_ERR_ARG;
+        if (backward) {
+            if (!g_conv || !dz || !g_conv[m] || !dz[m]) return RSX_ERR_ARG;
+            a.gout[m] = gout ? gout[m] : nullptr;
+            a.g_conv[m] = g_conv[m];
+            a.dz[m] = dz[m];
+        } else {
+            if (!out || !out[m]) return RSX_ERR_ARG;
+            a.out[m] = out[m];
+        }
+    }
+    if (backward && !g_item) return RSX_ERR_ARG;
+    a.item = item;
+    a.n = n;
+    a.scale = scale;
+    a.mul = mul;
+    a.g_item = g_item;
+    const dim3 grid((unsigned)(((n + 15) / 16 + 3) / 4));
+    hipStream_t s = as_stream(stream);
+    switch (d) {
+        case 64:
+            if (backward) hipLaunchKernelGGL(sf::gates_bwd<64>, grid, dim3(256), 0, s, a);
+            else hipLaunchKernelGGL(sf::gates_fwd<64>, grid, dim3(256), 0, s, a);
+            break;
+        case 128:
+            if (backward) hipLaunchKernelGGL(sf::gates_bwd<128>, grid, dim3(256), 0, s, a);
+            else hipLaunchKernelGGL(sf::gates_fwd<128>, grid, dim3(256), 0, s, a);
+            break;
+        default: return RSX_ERR_UNSUPPORTED;
+    }
+    return last_rc();
+}
+
+int rsx_smore_pref(int32_t backward, const float* const* W, const float* const* b, const float* content,
+                   const float* image_emb, const float* text_emb, const float* fusion_emb, int64_t n, int32_t d,
+                   float p_drop, const int64_t* seed_dev, float* all_out, float* side_out, const float* g_all,
+                   const float* g_side, float* g_content, float* g_image, float* g_text, float* g_fusion,
+                   float* hv, float* ht, float* const* dz, rsx_stream_t stream) {
+    if (n < 0 || !W || !b || !content || !image_emb || !text_emb || !fusion_emb) return RSX_ERR_ARG;
+    if (p_drop < 0.f || p_drop >= 1.f || (p_drop > 0.f && !seed_dev)) return RSX_ERR_ARG;
+    if (n == 0) return RSX_OK;
+    sf::PrefArgs a{};
+    for (int i = 0; i < sf::kNW; ++i) {
+        if (!W[i]) return RSX_ERR_ARG;
+        a.W[i] = W[i];
+        a.b[i] = b[i];
+        if (backward) {
+            if (!dz || !dz[i]) return RSX_ERR_ARG;
+            a.dz[i] = dz[i];
+        }
+    }
+    if (backward ? (!g_all || !g_content || !g_image || !g_text || !g_fusion || !hv || !ht) : (!all_out || !side_out))
+        return RSX_ERR_ARG;
+    a.C = content;
+    a.IE = image_emb;
+    a.TE = text_emb;
+    a.FE = fusion_emb;
+    a.n = n;
+    a.p_drop = p_drop;
+    a.drop_scale = p_drop > 0.f ? (float)(1.0 / (1.0 - (double)p_drop)) : 1.f;
+    a.seed = seed_dev;
+    a.all = all_out;
+    a.side = side_out;
+    a.g_all = g_all;
+    a.g_side = g_side;
+    a.gC = g_content;
+    a.gIE = g_image;
+    a.gTE = g_text;
+    a.gFE = g_fusion;
+    a.hv = hv;
+    a.ht = ht;
+    const dim3 grid((unsigned)(((n + 15) / 16 + 3) / 4));
+    hipStream_t s = as_stream(stream);
+    switch (d) {
+        case 64:
+            if (backward) hipLaunchKernelGGL(sf::pref_bwd<64>, grid, dim3(256), 0, s, a);
+            else hipLaunchKernelGGL(sf::pref_fwd<64>, grid, dim3(256), 0, s, a);
+            break;
+        case 128:
+            if (backward) hipLaunchKernelGGL(sf::pref_bwd<128>, grid, dim3(256), 0, s, a);
+            else hipLaunchKernelGGL(sf::pref_fwd<128>, grid, dim3(256), 0, s, a);
+            break;
+        default: return RSX_ERR_UNSUPPORTED;
+    }
+    return last_rc();
+}
+
+size_t rsx_smore_wgrad_ws_bytes(int64_t n, int32_t d, int32_t n_pairs) {
+    const int64_t splits = (n + sf::kWgRows - 1) / sf::kWgRows;
+    return (size_t)(n_pairs > 0 ? n_pairs : 0) * (size_t)(splits > 0 ? splits : 1) * (size_t)(d * d + d) * 4;
+}
+
+int rsx_smore_wgrad(int32_t n_pairs, const float* const* dz, const float* const* x, float* const* dw,
+                    float* const* db, int64_t n, int32_t d, void* ws, size_t ws_bytes, rsx_stream_t stream) {
+    if (n_pairs <= 0 || n_pairs > sf::kWgPairs || n < 0 || !dz || !x || !dw) return RSX_ERR_ARG;
+    if (d != 64 && d != 128) return RSX_ERR_UNSUPPORTED;
+    hipStream_t s = as_stream(stream);
+    if (n == 0) {
+        for (int i = 0; i < n_pairs; ++i) {
+            if (hipMemsetAsync(dw[i], 0, (size_t)d * d * 4, s) != hipSuccess) return last_rc();
+            if (db && db[i] && hipMemsetAsync(db[i], 0, (size_t)d * 4, s) != hipSuccess) return last_rc();
+        }
+        return RSX_OK;
+    }
+    if (ws_bytes < rsx_smore_wgrad_ws_bytes(n, d, n_pairs) || !ws) return RSX_ERR_WORKSPACE;
+    sf::WgArgs a{};
+    for (int i = 0; i < n_pairs; ++i) {
+        if (!dz[i] || !x[i] || !dw[i]) return RSX_ERR_ARG;
+        a.dz[i] = dz[i];
+        a.x[i] = x[i];
+        a.dw[i] = dw[i];
+        a.db[i] = db ? db[i] : nullptr;
+    }
+    a.n_pairs = n_pairs;
+    a.n = n;
+    a.n_splits = (int32_t)((n + sf::kWgRows - 1) / sf::kWgRows);
+    a.part = static_cast<float*>(ws);
+    const dim3 g1((unsigned)a.n_splits, (unsigned)n_pairs);
+    const dim3 g2((unsigned)((d * d + d + 255) / 256), (unsigned)n_pairs);
+    if (d == 64) {
+        hipLaunchKernelGGL(sf::wgrad_part<64>, g1, dim3(256), 0, s, a);
+        hipLaunchKernelGGL(sf::wgrad_reduce<64>, g2, dim3(256), 0, s, a);
+    } else {
+        hipLaunchKernelGGL(sf::wgrad_part<128>, g1, dim3(256), 0, s, a);
+        hipLaunchKernelGGL(sf::wgrad_reduce<128>, g2, dim3(256), 0, s, a);
+    }
+    return last_rc();
+}
+
+size_t rsx_smore_infonce_ws_bytes(int64_t batch, int32_t d) {
+    return (size_t)(4 * batch * d + 4 * batch + 2 * batch + 2 * batch) * 4;
+}
+
+static int nce_setup(sf::NceArgs& a, const float* side, const float* content, const int64_t* users,
+                     const int64_t* pos_items, int64_t n_users, int64_t batch, int32_t d, float tau, void* ws,
+                     size_t ws_bytes) {
+    if (!side || !content || !users || !pos_items || batch < 0 || n_users < 0 || !(tau > 0.f)) return RSX_ERR_ARG;
+    if (d != 64 && d != 128) return RSX_ERR_UNSUPPORTED;
+    if (!ws || ws_bytes < rsx_smore_infonce_ws_bytes(batch, d)) return RSX_ERR_WORKSPACE;
+    a.src1 = side;
+    a.src2 = content;
+    a.idx[0] = pos_items;  // term 0: cl_items = InfoNCE(side_i[pos], content_i[pos])
+    a.off[0] = n_users;
+    a.idx[1] = users;      // term 1: cl_users = InfoNCE(side_u[u], content_u[u])
+    a.off[1] = 0;
+    a.B = batch;
+    a.tau = tau;
+    float* f = static_cast<float*>(ws);
+    a.nrm = f;
+    a.norms = a.nrm + 4 * batch * d;
+    a.ttl = a.norms + 4 * batch;
+    a.lrow = a.ttl + 2 * batch;
+    return RSX_OK;
+}
+
+int rsx_smore_infonce_fwd(const float* side, const float* content, const int64_t* users, const int64_t* pos_items,
+                          int64_t n_users, int64_t batch, int32_t d, float tau, float* loss_out, void* ws,
+                          size_t ws_bytes, rsx_stream_t stream) {
+    sf::NceArgs a{};
+    int rc = nce_setup(a, side, content, users, pos_items, n_users, batch, d, tau, ws, ws_bytes);
+    if (rc) return rc;
+    if (!loss_out) return RSX_ERR_ARG;
+    a.loss = loss_out;
+    hipStream_t s = as_stream(stream);
+    if (batch == 0) return hip_rc(hipMemsetAsync(loss_out, 0xff, 8, s));  // mean of nothing: NaN
+    const dim3 grid((unsigned)((batch + 15) / 16), 2);
+    if (d == 64) hipLaunchKernelGGL(sf::nce_fwd<64>, grid, dim3(64 * sf::kNceWaves), 0, s, a);
+    else hipLaunchKernelGGL(sf::nce_fwd<128>, grid, dim3(64 * sf::kNceWaves), 0, s, a);
+    hipLaunchKernelGGL(sf::nce_mean, dim3(2), dim3(64), 0, s, a);
+    return last_rc();
+}
+
+int rsx_smore_infonce_bwd(const float* side, const float* content, const int64_t* users, const int64_t* pos_items,
+                          int64_t n_users, int64_t batch, int32_t d, float tau, const float* g_loss, float* g_side,
+                          float* g_content, void* ws, size_t ws_bytes, rsx_stream_t stream) {
+    sf::NceArgs a{};
+    int rc = nce_setup(a, side, content, users, pos_items, n_users, batch, d, tau, ws, ws_bytes);
+    if (rc) return rc;
+    if (!g_loss || !g_side || !g_content) return RSX_ERR_ARG;
+    if (batch == 0) return RSX_OK;
+    a.gloss = g_loss;
+    a.g1 = g_side;
+    a.g2 = g_content;
+    hipStream_t s = as_stream(stream);
+    const dim3 grid((unsigned)((batch + 15) / 16), 2, 2);
+    if (d == 64) hipLaunchKernelGGL(sf::nce_bwd<64>, grid, dim3(64 * sf::kNceWaves), 0, s, a);
+    else hipLaunchKernelGGL(sf::nce_bwd<128>, grid, dim3(64 * sf::kNceWaves), 0, s, a);
+    return last_rc();
+}
+
+int rsx_adam_multi(int32_t count, float* const* p, const float* const* g, float* const* m, float* const* v,
+                   const int64_t* const* step_dev, const int64_t* n, float lr, float beta1, float beta2, float eps,
+                   float weight_decay, rsx_stream_t stream) {
+    if (count < 0 || (count > 0 && (!p || !g || !m || !v || !step_dev || !n))) return RSX_ERR_ARG;
+    hipStream_t s = as_stream(stream);
+    for (int32_t c0 = 0; c0 < count; c0 += sf::kAdamMax) {
+        sf::AdamList L{};
+        L.lr = lr;
+        L.beta1 = beta1;
+        L.beta2 = beta2;
+        L.eps = eps;
+        L.wd = weight_decay;
+        int64_t blocks = 0;
+        int k = 0;
+        for (int32_t i = c0; i < count && k < sf::kAdamMax; ++i) {
+            if (n[i] < 0 || (n[i] > 0 && (!p[i] || !g[i] || !m[i] || !v[i] || !step_dev[i]))) return RSX_ERR_ARG;
+            if (n[i] == 0) continue;
+            L.p[k] = p[i];
+            L.g[k] = g[i];
+            L.m[k] = m[i];
+            L.v[k] = v[i];
+            L.step[k] = step_dev[i];
+            L.n[k] = n[i];
+            L.blk[k] = blocks;
+            blocks += (n[i] + sf::kAdamPerBlock - 1) / sf::kAdamPerBlock;
+            ++k;
+        }
+        L.blk[k] = blocks;
+        L.count = k;
+        if (blocks > 0) hipLaunchKernelGGL(sf::adam_multi, dim3((unsigned)blocks), dim3(256), 0, s, L);
+        const int rc = last_rc();
+        if (rc) return rc;
+    }
+    return RSX_OK;
+}
+
+}  // extern "C"

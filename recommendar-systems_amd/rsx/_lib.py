@@ -126,6 +126,14 @@ def _declare(lib):
         "rsx_comm_allreduce_f32": (C.c_int, [P, P, I64, P]),
         "rsx_sharded_lightgcn_step": (C.c_int, [C.POINTER(ShardedStep), P]),
         "rsx_sharded_lightgcn_forward": (C.c_int, [C.POINTER(ShardedStep), P]),
+        "rsx_smore_gates": (C.c_int, [I32, P, P, P, P, I64, I32, F32, I32, P, P, P, P, P, P]),
+        "rsx_smore_pref": (C.c_int, [I32, P, P, P, P, P, P, I64, I32, F32, P, P, P, P, P, P, P, P, P, P, P, P, P]),
+        "rsx_smore_wgrad_ws_bytes": (C.c_size_t, [I64, I32, I32]),
+        "rsx_smore_wgrad": (C.c_int, [I32, P, P, P, P, I64, I32, P, C.c_size_t, P]),
+        "rsx_smore_infonce_ws_bytes": (C.c_size_t, [I64, I32]),
+        "rsx_smore_infonce_fwd": (C.c_int, [P, P, P, P, I64, I64, I32, F32, P, P, C.c_size_t, P]),
+        "rsx_smore_infonce_bwd": (C.c_int, [P, P, P, P, I64, I64, I32, F32, P, P, P, P, C.c_size_t, P]),
+        "rsx_adam_multi": (C.c_int, [I32, P, P, P, P, P, P, F32, F32, F32, F32, F32, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -142,7 +150,9 @@ EXPORTED = ["rsx_version", "rsx_csr_schedule_host", "rsx_spmm", "rsx_rowwise", "
             "rsx_topk_metrics_ws_bytes", "rsx_topk_metrics", "rsx_topk_metrics_fast", "rsx_linear_wgrad_ws_bytes", "rsx_linear_wgrad",
             "rsx_comm_unique_id_bytes", "rsx_comm_get_unique_id", "rsx_comm_init", "rsx_comm_destroy",
             "rsx_comm_init_host",
-            "rsx_comm_allreduce_f32", "rsx_sharded_lightgcn_step", "rsx_sharded_lightgcn_forward"]
+            "rsx_comm_allreduce_f32", "rsx_sharded_lightgcn_step", "rsx_sharded_lightgcn_forward",
+            "rsx_smore_gates", "rsx_smore_pref", "rsx_smore_wgrad_ws_bytes", "rsx_smore_wgrad",
+            "rsx_smore_infonce_ws_bytes", "rsx_smore_infonce_fwd", "rsx_smore_infonce_bwd", "rsx_adam_multi"]
 
 
 def lib_path() -> str:

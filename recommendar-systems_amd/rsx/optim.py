@@ -2,9 +2,10 @@
 
 Same update as torch.optim.Adam's single-tensor path, which is what the reference
 runs on CPU (src/common/trainer.py:133,238): bias corrections in float64, the
-first moment by lerp, the second by mul + addcmul, then addcdiv.  One launch per
-parameter tensor: a 28.9M-element SMORE feature table is one pass over p, g, m, v
-instead of torch's chain of foreach kernels.  Works with torch LR schedulers (it
+first moment by lerp, the second by mul + addcmul, then addcdiv.  One launch for
+all of a group's parameter tensors (rsx_adam_multi, up to 32 tensors per launch):
+a 28.9M-element SMORE feature table and its 28 small Linear / spectral tensors
+are one pass over p, g, m, v instead of torch's chain of foreach kernels.  Works with torch LR schedulers (it
 is a torch.optim.Optimizer and reads group["lr"] at every step).
 
 The step count lives on the device (`state["step"]`, a 0-d int64 tensor, bumped by
@@ -17,6 +18,7 @@ from __future__ import annotations
 import torch
 
 from . import ops
+from .smore_fuse import adam_multi
 
 
 class RsxAdam(torch.optim.Optimizer):
@@ -45,7 +47,15 @@ class RsxAdam(torch.optim.Optimizer):
                     st["step"] = torch.tensor(int(st["step"]), dtype=torch.int64, device=p.device)
             if not live:
                 continue
-            torch._foreach_add_([self.state[p]["step"] for p in live], 1)
+            steps = [self.state[p]["step"] for p in live]
+            torch._foreach_add_(steps, 1)
+            if all(p.is_contiguous() for p in live):
+                adam_multi([p.data for p in live], [p.grad if p.grad.is_contiguous() else p.grad.contiguous()
+                                                    for p in live],
+                           [self.state[p]["exp_avg"] for p in live], [self.state[p]["exp_avg_sq"] for p in live],
+                           steps, group["lr"], betas=group["betas"], eps=group["eps"],
+                           weight_decay=group["weight_decay"])
+                continue
             for p in live:
                 st = self.state[p]
                 g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()

@@ -15,7 +15,11 @@ Same class name, constructor, YAML keys, module names and creation order (so
   HIP pass rsx_smore_spectral (forward and backward, see csrc/smore.hip) when the
   library has it, else the op-for-op torch.fft form;
 * BPR part of the loss — the fused HIP BPR kernel (variant SMORE);
-* gates, query MLPs, softmax over d, InfoNCE — torch ops on the device.
+* gates + inject, the item views' propagation into [R x; x], the preference
+  block (query MLPs, softmax over d, dropout'd preference gates, mean, content +
+  side) and both InfoNCE terms — fused HIP kernels with autograd (rsx.smore_fuse,
+  csrc/smore_fuse.hip) for d in {64, 128}; the op-for-op torch form otherwise or
+  with rsx_smore_fused: False.
 
 Diagnostics that the reference gathers with per-step `.item()` calls
 (spectrum band energies, gate statistics, CL values) are computed lazily, only
@@ -33,6 +37,7 @@ import torch.nn.functional as F
 from . import _lib as L
 from . import graph, ops
 from .lightgcn import _BprLoss
+from . import smore_fuse as SF
 from .nn import RsxLinear
 from .recommender import GeneralRecommender
 
@@ -268,6 +273,13 @@ class SMORE(GeneralRecommender):
         self.diag_gate = bool(config.get("diag_gate", True))
         self.diag_grad = bool(config.get("diag_grad", True))
         self.use_hip_spectral = bool(config.get("rsx_smore_spectral", True))
+        self.use_fused = bool(config.get("rsx_smore_fused", True)) and SF.supported(d)
+        # dropout masks of the fused preference block: a hash of (seed, call, row,
+        # feature); the seed word lives on the device and advances once per training
+        # forward (graph-capture safe).  Derived from the config seed, not torch's RNG,
+        # so the parameter initialisation stream matches the reference.
+        self._drop_seed = torch.tensor([int(config["seed"] or 999) * 1000003 + 17], dtype=torch.int64,
+                                       device=self.device)
         self._last = {}
         self.to(self.device)
 
@@ -323,6 +335,32 @@ class SMORE(GeneralRecommender):
         return users, items
 
     def _forward_all(self, train=False):
+        if self.use_fused:
+            return self._forward_all_fused(train)
+        return self._forward_all_torch(train)
+
+    def _forward_all_fused(self, train=False):
+        cv, ct, cf = self._projected_spectrum()
+        item_id = self.item_id_embedding.weight
+        img_i, txt_i, fus_i = SF.gates(cv, ct, cf, item_id, self.gate_v, self.gate_t, self.gate_f,
+                                       self.inject_scale, self.inject_mode == "mul")
+        ego = torch.cat([self.user_embedding.weight, item_id], dim=0)
+        content = _PropMean.apply(ego, self.norm_adj_csr, self.n_ui_layers)
+        nu, L_ = self.n_users, self.n_layers
+        image_embeds = SF.view_prop(img_i, self.image_graph, self.R, L_, nu)
+        text_embeds = SF.view_prop(txt_i, self.text_graph, self.R, L_, nu)
+        fusion_embeds = SF.view_prop(fus_i, self.fusion_graph, self.R, L_, nu)
+        if self.training and self.dropout.p > 0:
+            seed = self._drop_seed.clone()
+            self._drop_seed.add_(1)
+        else:
+            seed = self._drop_seed
+        all_embeds, side = SF.preference(self, content, image_embeds, text_embeds, fusion_embeds, seed)
+        if train:
+            self._last["conv"] = (cv.detach(), ct.detach(), cf.detach())
+        return all_embeds, side, content
+
+    def _forward_all_torch(self, train=False):
         cv, ct, cf = self._projected_spectrum()
         item_id = self.item_id_embedding.weight
         if self.inject_mode == "mul":
@@ -375,8 +413,11 @@ class SMORE(GeneralRecommender):
         nu = self.n_users
         bpr = _BprLoss.apply(all_embeds, None, None, interaction[:3].contiguous(), L.RSX_BPR_SMORE,
                              float(self.reg_weight), float(self.batch_size), nu, self.n_items)
-        cl_items = self.InfoNCE(side[nu:][pos], content[nu:][pos], self.cl_temp)
-        cl_users = self.InfoNCE(side[:nu][users], content[:nu][users], self.cl_temp)
+        if self.use_fused:
+            cl_items, cl_users = SF.infonce2(side, content, users, pos, nu, self.cl_temp)
+        else:
+            cl_items = self.InfoNCE(side[nu:][pos], content[nu:][pos], self.cl_temp)
+            cl_users = self.InfoNCE(side[:nu][users], content[:nu][users], self.cl_temp)
         self._last["cl"] = (cl_items.detach(), cl_users.detach())
         return bpr + self.cl_loss * (cl_items + cl_users)
 

@@ -1,0 +1,250 @@
+"""SMORE's per-row blocks on the fused HIP kernels (csrc/smore_fuse.hip), with autograd.
+
+Each torch.autograd.Function below replaces a chain of ~10-40 torch kernels of the
+reference forward (src/models/smore.py) and its autograd backward by one forward
+launch and one backward launch (+ one batched weight-gradient launch pair):
+
+* `gates`       — gate_v/t/f + inject (smore.py:262-272)
+* `preference`  — query MLPs, softmax over d, view products, dropout'd preference
+                  gates, mean of the three views, content + side (smore.py:320-341)
+* `view_prop`   — an item view through n_layers item-item SpMMs, then the item ->
+                  user aggregation R, written as one [n_users + n_items, d] table (the
+                  reference's torch.cat([R x, x]), smore.py:299-317)
+* `infonce2`    — InfoNCE(side[pos], content[pos]) and InfoNCE(side[u], content[u])
+                  (smore.py:380-387, 398-404) from the full side/content tables and the
+                  batch indices (no gathered copies, no index_put backward)
+
+The weight gradients of every Linear (dW = dZ^T X, db = colsum dZ) come from
+rsx_smore_wgrad in one launch pair per block.  Arithmetic is f32 throughout (MFMA
+f32 products are exact, sums in f32); results equal the torch ops within float
+rounding, which tests/test_gpu_smore_fuse.py checks against torch autograd.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from . import _lib as L
+from . import ops
+
+_p = ops._p
+
+
+def _arr(ts):
+    return (C.c_void_p * len(ts))(*[(t.data_ptr() if t is not None else None) for t in ts])
+
+
+def supported(d: int) -> bool:
+    return d in (64, 128)
+
+
+def _c(t):
+    return t if t.is_contiguous() else t.contiguous()
+
+
+def _wgrad(pairs, d, device):
+    """[(dz, x, has_bias)] -> [(dW, db | None)] through rsx_smore_wgrad (<= 8 pairs)."""
+    lib = L.lib()
+    n = pairs[0][0].shape[0]
+    dws = [torch.empty(d, d, dtype=torch.float32, device=device) for _ in pairs]
+    dbs = [torch.empty(d, dtype=torch.float32, device=device) if hb else None for _, _, hb in pairs]
+    ws = torch.empty(max(int(lib.rsx_smore_wgrad_ws_bytes(n, d, len(pairs))), 4), dtype=torch.uint8,
+                     device=device)
+    L.check(lib.rsx_smore_wgrad(len(pairs), _arr([p[0] for p in pairs]), _arr([p[1] for p in pairs]), _arr(dws),
+                                _arr(dbs), n, d, _p(ws), ws.numel(), ops._stream()), "rsx_smore_wgrad")
+    return list(zip(dws, dbs))
+
+
+# ---------------------------------------------------------------------------
+# modality gates
+# ---------------------------------------------------------------------------
+class _Gates(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, cv, ct, cf, item, Wv, bv, Wt, bt, Wf, bf, scale, mul):
+        conv = [_c(x) for x in (cv, ct, cf)]
+        W = [_c(x) for x in (Wv, Wt, Wf)]
+        b = [_c(x) for x in (bv, bt, bf)]
+        item = _c(item)
+        n, d = item.shape
+        outs = [torch.empty_like(item) for _ in range(3)]
+        L.check(L.lib().rsx_smore_gates(0, _arr(conv), _p(item), _arr(W), _arr(b), n, d, float(scale), int(mul),
+                                        _arr(outs), None, None, None, None, ops._stream()), "rsx_smore_gates")
+        ctx.save_for_backward(*conv, item, *W, *b)
+        ctx.cfg = (float(scale), int(mul))
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, gv, gt, gf):
+        cv, ct, cf, item, Wv, Wt, Wf, bv, bt, bf = ctx.saved_tensors
+        scale, mul = ctx.cfg
+        n, d = item.shape
+        gi = torch.empty_like(item)
+        gc = [torch.empty_like(item) for _ in range(3)]
+        dz = [torch.empty_like(item) for _ in range(3)]
+        gouts = [None if g is None else _c(g) for g in (gv, gt, gf)]
+        L.check(L.lib().rsx_smore_gates(1, _arr([cv, ct, cf]), _p(item), _arr([Wv, Wt, Wf]), _arr([bv, bt, bf]), n,
+                                        d, scale, mul, None, _arr(gouts), _p(gi), _arr(gc), _arr(dz),
+                                        ops._stream()), "rsx_smore_gates")
+        (gWv, gbv), (gWt, gbt), (gWf, gbf) = _wgrad([(dz[0], cv, True), (dz[1], ct, True), (dz[2], cf, True)], d,
+                                                    item.device)
+        return gc[0], gc[1], gc[2], gi, gWv, gbv, gWt, gbt, gWf, gbf, None, None
+
+
+def gates(cv, ct, cf, item, gate_v, gate_t, gate_f, scale: float, mul: bool):
+    """(img_i, txt_i, fus_i) = item + scale * sigmoid(gate_x(conv_x)) (or item * sigmoid(..));
+    gate_x are the reference's nn.Sequential(Linear, Sigmoid) modules."""
+    lv, lt, lf = gate_v[0], gate_t[0], gate_f[0]
+    return _Gates.apply(cv, ct, cf, item, lv.weight, lv.bias, lt.weight, lt.bias, lf.weight, lf.bias, scale, mul)
+
+
+# ---------------------------------------------------------------------------
+# preference block
+# ---------------------------------------------------------------------------
+class _Pref(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, C_, IE, TE, FE, p_drop, seed, *wb):
+        W = [_c(x) for x in wb[:7]]
+        b = [None if x is None else _c(x) for x in wb[7:]]
+        C_, IE, TE, FE = _c(C_), _c(IE), _c(TE), _c(FE)
+        n, d = C_.shape
+        all_ = torch.empty_like(C_)
+        side = torch.empty_like(C_)
+        L.check(L.lib().rsx_smore_pref(0, _arr(W), _arr(b), _p(C_), _p(IE), _p(TE), _p(FE), n, d, float(p_drop),
+                                       _p(seed), _p(all_), _p(side), None, None, None, None, None, None, None,
+                                       None, None, ops._stream()), "rsx_smore_pref")
+        ctx.save_for_backward(C_, IE, TE, FE, seed, *W, *[x if x is not None else torch.empty(0) for x in b])
+        ctx.has_b = [x is not None for x in b]
+        ctx.p_drop = float(p_drop)
+        return all_, side
+
+    @staticmethod
+    def backward(ctx, g_all, g_side):
+        sv = ctx.saved_tensors
+        C_, IE, TE, FE, seed = sv[:5]
+        W = list(sv[5:12])
+        b = [x if h else None for x, h in zip(sv[12:19], ctx.has_b)]
+        n, d = C_.shape
+        if g_all is None:
+            g_all = torch.zeros_like(C_)
+        g_all = _c(g_all)
+        g_side = None if g_side is None else _c(g_side)
+        gC, gIE, gTE, gFE = (torch.empty_like(C_) for _ in range(4))
+        hv, ht = torch.empty_like(C_), torch.empty_like(C_)
+        dz = [torch.empty_like(C_) for _ in range(7)]
+        L.check(L.lib().rsx_smore_pref(1, _arr(W), _arr(b), _p(C_), _p(IE), _p(TE), _p(FE), n, d, ctx.p_drop,
+                                       _p(seed), None, None, _p(g_all), _p(g_side), _p(gC), _p(gIE), _p(gTE),
+                                       _p(gFE), _p(hv), _p(ht), _arr(dz), ops._stream()), "rsx_smore_pref")
+        # Linear inputs: query_v.0 <- F, query_v.2 <- hv, query_t.0 <- F, query_t.2 <- ht, prefer gates <- content
+        xs = [FE, hv, FE, ht, C_, C_, C_]
+        grads = _wgrad([(dz[i], xs[i], ctx.has_b[i]) for i in range(7)], d, C_.device)
+        gW = [g[0] for g in grads]
+        gb = [g[1] for g in grads]
+        return (gC, gIE, gTE, gFE, None, None, *gW, *gb)
+
+
+def preference(model, content, image_embeds, text_embeds, fusion_embeds, seed):
+    """(all_embeds, side) of the reference's preference block; `seed`: a 1-element
+    int64 device tensor (this call's dropout seed; unused when dropout is off)."""
+    m = model
+    lin = [m.query_v[0], m.query_v[2], m.query_t[0], m.query_t[2], m.gate_image_prefer[0], m.gate_text_prefer[0],
+           m.gate_fusion_prefer[0]]
+    p = float(m.dropout.p) if m.training else 0.0
+    return _Pref.apply(content, image_embeds, text_embeds, fusion_embeds, p, seed, *[x.weight for x in lin],
+                       *[x.bias for x in lin])
+
+
+# ---------------------------------------------------------------------------
+# item view -> [users; items] table
+# ---------------------------------------------------------------------------
+class _ViewProp(torch.autograd.Function):
+    """out = [R G^L x ; G^L x] for one item-item graph G (L = n_layers) and the
+    user-item block R (smore.py:299-317: the loop, then torch.cat([R x, x]))."""
+
+    @staticmethod
+    def forward(ctx, x, G, R, n_layers, n_users):
+        x = _c(x)
+        ni, d = x.shape
+        out = torch.empty(n_users + ni, d, dtype=torch.float32, device=x.device)
+        cur = x
+        for k in range(n_layers):
+            dst = out[n_users:] if k == n_layers - 1 else torch.empty_like(x)
+            G.A.spmm(cur, out=dst)
+            cur = dst
+        if n_layers == 0:
+            out[n_users:].copy_(x)
+        R.A.spmm(out[n_users:], out=out[:n_users])
+        ctx.G, ctx.R, ctx.L, ctx.nu = G, R, n_layers, n_users
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        g = _c(g)
+        nu = ctx.nu
+        d = g.shape[1]
+        gi = torch.empty_like(g[nu:])
+        # d items = g_items + R^T g_users, in one launch (ADD epilogue)
+        ctx.R.AT.spmm_epi(g[:nu], ops.epi(L.RSX_EPI_ADD, y=gi, r_add=g[nu:]), d)
+        for _ in range(ctx.L):
+            gi = ctx.G.AT.spmm(gi)
+        return gi, None, None, None, None
+
+
+def view_prop(x, G, R, n_layers, n_users):
+    return _ViewProp.apply(x, G, R, int(n_layers), int(n_users))
+
+
+# ---------------------------------------------------------------------------
+# InfoNCE x 2
+# ---------------------------------------------------------------------------
+class _InfoNCE2(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, side, content, users, pos, n_users, tau):
+        side, content = _c(side), _c(content)
+        users, pos = _c(users), _c(pos)
+        B = users.numel()
+        d = side.shape[1]
+        lib = L.lib()
+        ws = torch.empty(max(int(lib.rsx_smore_infonce_ws_bytes(B, d)), 4), dtype=torch.uint8, device=side.device)
+        loss = torch.empty(2, dtype=torch.float32, device=side.device)
+        L.check(lib.rsx_smore_infonce_fwd(_p(side), _p(content), _p(users), _p(pos), int(n_users), B, d, float(tau),
+                                          _p(loss), _p(ws), ws.numel(), ops._stream()), "rsx_smore_infonce_fwd")
+        ctx.save_for_backward(side, content, users, pos, ws)
+        ctx.cfg = (int(n_users), float(tau), side.shape)
+        return loss[0], loss[1]
+
+    @staticmethod
+    def backward(ctx, g_items, g_users):
+        side, content, users, pos, ws = ctx.saved_tensors
+        nu, tau, shape = ctx.cfg
+        dev = side.device
+        gl = torch.stack([g_items if g_items is not None else torch.zeros((), device=dev),
+                          g_users if g_users is not None else torch.zeros((), device=dev)]).float().contiguous()
+        gs = torch.zeros(shape, dtype=torch.float32, device=dev)
+        gc = torch.zeros(shape, dtype=torch.float32, device=dev)
+        L.check(L.lib().rsx_smore_infonce_bwd(_p(side), _p(content), _p(users), _p(pos), nu, users.numel(),
+                                              shape[1], tau, _p(gl), _p(gs), _p(gc), _p(ws), ws.numel(),
+                                              ops._stream()), "rsx_smore_infonce_bwd")
+        return gs, gc, None, None, None, None
+
+
+def infonce2(side, content, users, pos, n_users, tau):
+    """(cl_items, cl_users) = (InfoNCE(side_i[pos], content_i[pos]), InfoNCE(side_u[u], content_u[u]))."""
+    return _InfoNCE2.apply(side, content, users, pos, n_users, tau)
+
+
+# ---------------------------------------------------------------------------
+# multi-tensor Adam
+# ---------------------------------------------------------------------------
+def adam_multi(params, grads, exp_avgs, exp_avg_sqs, steps, lr, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
+    """torch.optim.Adam's update over many tensors in one launch (per 32 tensors)."""
+    n = len(params)
+    if n == 0:
+        return
+    for t in (*params, *grads, *exp_avgs, *exp_avg_sqs):
+        if not (t.is_cuda and t.is_contiguous() and t.dtype == torch.float32):
+            raise RuntimeError("adam_multi: contiguous f32 GPU tensors only")
+    sizes = (C.c_int64 * n)(*[p.numel() for p in params])
+    L.check(L.lib().rsx_adam_multi(n, _arr(params), _arr(grads), _arr(exp_avgs), _arr(exp_avg_sqs), _arr(steps),
+                                   sizes, float(lr), float(betas[0]), float(betas[1]), float(eps),
+                                   float(weight_decay), ops._stream()), "rsx_adam_multi")

@@ -1,0 +1,222 @@
+"""The fused SMORE kernels (csrc/smore_fuse.hip through rsx.smore_fuse) against the
+reference's torch ops (src/models/smore.py:262-272 gates, :299-317 item views,
+:320-341 preference block, :380-387 InfoNCE) evaluated in fp32 with autograd, on
+the same inputs: outputs and every input / weight gradient within 1e-4 of the
+tensor's scale (f32 sums in another order).  Dropout > 0 checks the kernel's mask
+against a numpy restatement of its hash, then the same torch ops with that mask."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _close(got, want, name, tol=1e-4):
+    g = got.detach().double().cpu().numpy()
+    w = want.detach().double().cpu().numpy()
+    scale = max(np.abs(w).max(), 1e-30)
+    err = np.abs(g - w).max() if g.size else 0.0
+    assert err <= tol * scale, f"{name}: max err {err:.3g} vs scale {scale:.3g}"
+
+
+def _lin(d, gen, dev, bias=True):
+    m = torch.nn.Linear(d, d, bias=bias)
+    with torch.no_grad():
+        m.weight.copy_(torch.randn(d, d, generator=gen) / d ** 0.5)
+        if bias:
+            m.bias.copy_(torch.randn(d, generator=gen) * 0.1)
+    return m.to(dev)
+
+
+def _drop_mask_np(seed, gate, n, d, p):
+    """The kernel's dropout scale per element (mix32 of seed * phi + gate << 58 + row * d + f)."""
+    M = np.uint64(0xFFFFFFFFFFFFFFFF)
+    rows = np.arange(n, dtype=np.uint64)[:, None]
+    feats = np.arange(d, dtype=np.uint64)[None, :]
+    with np.errstate(over="ignore"):
+        x = (np.uint64(seed) * np.uint64(0x9E3779B97F4A7C15) + (np.uint64(gate) << np.uint64(58))
+             + rows * np.uint64(d) + feats) & M
+        x ^= x >> np.uint64(33)
+        x = (x * np.uint64(0xFF51AFD7ED558CCD)) & M
+        x ^= x >> np.uint64(33)
+        x = (x * np.uint64(0xC4CEB9FE1A85EC53)) & M
+        x ^= x >> np.uint64(33)
+    u = (x & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+    thr = np.uint32(min(np.float32(p) * np.float32(4294967296.0), np.float32(4294967295.0)))
+    scale = np.float32(1.0 / (1.0 - p))
+    return np.where(u >= thr, scale, np.float32(0)).astype(np.float32)
+
+
+@pytest.mark.parametrize("d,n,mul", [(64, 7050, False), (128, 1001, False), (64, 37, True), (128, 5, True)])
+def test_gates_vs_torch(cuda, d, n, mul):
+    from rsx import smore_fuse as SF
+
+    gen = torch.Generator().manual_seed(d + n)
+    mk = lambda: torch.randn(n, d, generator=gen).to(cuda).requires_grad_()  # noqa: E731
+    cv, ct, cf, item = mk(), mk(), mk(), mk()
+    gates = [torch.nn.Sequential(_lin(d, gen, cuda), torch.nn.Sigmoid()) for _ in range(3)]
+    up = [torch.randn(n, d, generator=gen).to(cuda) for _ in range(3)]
+    params = [cv, ct, cf, item] + [p for gm in gates for p in gm.parameters()]
+
+    def ref():
+        outs = []
+        for c, gm in zip((cv, ct, cf), gates):
+            outs.append(item * gm(c) if mul else item + 0.7 * gm(c))
+        return outs
+
+    want = ref()
+    wg = torch.autograd.grad(sum((o * u).sum() for o, u in zip(want, up)), params)
+    got = SF.gates(cv, ct, cf, item, *gates, 0.7, mul)
+    gg = torch.autograd.grad(sum((o * u).sum() for o, u in zip(got, up)), params)
+    for i, (a, b) in enumerate(zip(got, want)):
+        _close(a, b, f"out{i}")
+    for i, (a, b) in enumerate(zip(gg, wg)):
+        _close(a, b, f"grad{i}")
+
+
+class _PrefModel(torch.nn.Module):
+    """The reference's preference-module submodules (smore.py:104-120)."""
+
+    def __init__(self, d, gen, dev, p):
+        super().__init__()
+        self.query_v = torch.nn.Sequential(_lin(d, gen, dev), torch.nn.Tanh(), _lin(d, gen, dev, bias=False))
+        self.query_t = torch.nn.Sequential(_lin(d, gen, dev), torch.nn.Tanh(), _lin(d, gen, dev, bias=False))
+        self.gate_image_prefer = torch.nn.Sequential(_lin(d, gen, dev), torch.nn.Sigmoid())
+        self.gate_text_prefer = torch.nn.Sequential(_lin(d, gen, dev), torch.nn.Sigmoid())
+        self.gate_fusion_prefer = torch.nn.Sequential(_lin(d, gen, dev), torch.nn.Sigmoid())
+        self.dropout = torch.nn.Dropout(p)
+
+    def ref(self, C, IE, TE, FE, masks):
+        sv = torch.softmax(self.query_v(FE), dim=-1)
+        st = torch.softmax(self.query_t(FE), dim=-1)
+        a1, a2 = sv * IE, st * TE
+        ip, tp, fp = self.gate_image_prefer(C), self.gate_text_prefer(C), self.gate_fusion_prefer(C)
+        if masks is not None:
+            ip, tp, fp = ip * masks[0], tp * masks[1], fp * masks[2]
+        side = torch.mean(torch.stack([ip * a1, tp * a2, fp * FE]), dim=0)
+        return C + side, side
+
+
+@pytest.mark.parametrize("d,n,p", [(64, 26495, 0.0), (128, 1000, 0.0), (64, 333, 0.1), (128, 45, 0.3)])
+def test_preference_vs_torch(cuda, d, n, p):
+    from rsx import smore_fuse as SF
+
+    gen = torch.Generator().manual_seed(d * 7 + n)
+    mk = lambda: torch.randn(n, d, generator=gen).to(cuda).requires_grad_()  # noqa: E731
+    C_, IE, TE, FE = mk(), mk(), mk(), mk()
+    m = _PrefModel(d, gen, cuda, p).train()
+    seed = torch.tensor([12345], dtype=torch.int64, device=cuda)
+    masks = None
+    if p > 0:
+        masks = [torch.from_numpy(_drop_mask_np(12345, k, n, d, p)).to(cuda) for k in range(3)]
+        keep = float(np.mean([(mm > 0).float().mean().item() for mm in masks]))
+        assert abs(keep - (1 - p)) < 0.02, keep
+    up_a, up_s = torch.randn(n, d, generator=gen).to(cuda), torch.randn(n, d, generator=gen).to(cuda)
+    params = [C_, IE, TE, FE] + list(m.parameters())
+    wa, ws = m.ref(C_, IE, TE, FE, masks)
+    wg = torch.autograd.grad((wa * up_a).sum() + (ws * up_s).sum(), params)
+    ga, gs = SF.preference(m, C_, IE, TE, FE, seed)
+    gg = torch.autograd.grad((ga * up_a).sum() + (gs * up_s).sum(), params)
+    _close(ga, wa, "all")
+    _close(gs, ws, "side")
+    names = ["content", "image", "text", "fusion"] + [k for k, _ in m.named_parameters()]
+    for name, a, b in zip(names, gg, wg):
+        _close(a, b, name)
+    # eval mode: no dropout whatever p
+    m.eval()
+    ea, _ = SF.preference(m, C_, IE, TE, FE, seed)
+    _close(ea, m.ref(C_, IE, TE, FE, None)[0], "eval all")
+
+
+def test_view_prop_vs_torch(cuda):
+    from rsx import smore_fuse as SF
+    from rsx.smore import _DevGraph
+
+    rng = np.random.default_rng(3)
+    nu, ni, d = 300, 200, 64
+    g_r = rng.integers(0, ni, 3000), rng.integers(0, ni, 3000)
+    gv = rng.random(3000).astype(np.float32)
+    key = np.unique(g_r[0] * ni + g_r[1], return_index=True)[1]
+    G = _DevGraph(g_r[0][key], g_r[1][key], gv[key], ni, ni, cuda, 32)
+    r_r = rng.integers(0, nu, 4000), rng.integers(0, ni, 4000)
+    key = np.unique(r_r[0] * ni + r_r[1], return_index=True)[1]
+    rv = rng.random(key.size).astype(np.float32)
+    R = _DevGraph(r_r[0][key], r_r[1][key], rv, nu, ni, cuda, 32)
+    # dense references of the two operators from their CSR arrays
+    def dense(A):
+        rp = A.rowptr.cpu().numpy()
+        M = torch.zeros(A.n_rows, A.n_cols, dtype=torch.float64)
+        rows = np.repeat(np.arange(A.n_rows), np.diff(rp))
+        M[torch.from_numpy(rows), A.col.cpu().long()] = A.val.cpu().double()
+        return M.to(cuda)
+
+    Gm, Rm = dense(G.A), dense(R.A)
+    for L_ in (1, 2):
+        x = torch.randn(ni, d, device=cuda, requires_grad=True)
+        up = torch.randn(nu + ni, d, device=cuda)
+        out = SF.view_prop(x, G, R, L_, nu)
+        (gx,) = torch.autograd.grad((out * up).sum(), [x])
+        xi = x.detach().double()
+        for _ in range(L_):
+            xi = Gm @ xi
+        want = torch.cat([Rm @ xi, xi])
+        _close(out, want, f"out L={L_}", 1e-5)
+        gi = up[nu:].double() + Rm.t() @ up[:nu].double()
+        for _ in range(L_):
+            gi = Gm.t() @ gi
+        _close(gx, gi, f"grad L={L_}", 1e-5)
+
+
+def _infonce_ref(v1, v2, tau):
+    """The reference's InfoNCE (smore.py:380-387)."""
+    v1, v2 = F.normalize(v1, dim=1), F.normalize(v2, dim=1)
+    pos = torch.exp((v1 * v2).sum(dim=-1) / tau)
+    ttl = torch.exp(torch.matmul(v1, v2.transpose(0, 1)) / tau).sum(dim=1)
+    return torch.mean(-torch.log(pos / ttl))
+
+
+@pytest.mark.parametrize("d,B,nu,ni", [(64, 2048, 19445, 7050), (128, 2048, 3000, 2000), (64, 1000, 500, 300),
+                                       (64, 17, 40, 30)])
+def test_infonce2_vs_torch(cuda, d, B, nu, ni):
+    from rsx import smore_fuse as SF
+
+    gen = torch.Generator().manual_seed(B + d)
+    side = torch.randn(nu + ni, d, generator=gen).to(cuda).requires_grad_()
+    content = torch.randn(nu + ni, d, generator=gen).to(cuda).requires_grad_()
+    users = torch.randint(0, nu, (B,), generator=gen).to(cuda)
+    pos = torch.randint(0, min(ni, 50), (B,), generator=gen).to(cuda)  # heavy repeats: the atomics' case
+    ci, cu = SF.infonce2(side, content, users, pos, nu, 0.2)
+    gg = torch.autograd.grad(0.7 * ci + 1.3 * cu, [side, content])
+    wi = _infonce_ref(side[nu:][pos], content[nu:][pos], 0.2)
+    wu = _infonce_ref(side[:nu][users], content[:nu][users], 0.2)
+    wg = torch.autograd.grad(0.7 * wi + 1.3 * wu, [side, content])
+    _close(ci, wi, "cl_items", 2e-5)
+    _close(cu, wu, "cl_users", 2e-5)
+    _close(gg[0], wg[0], "d side")
+    _close(gg[1], wg[1], "d content")
+
+
+def test_adam_multi_vs_torch(cuda):
+    """One launch over many tensors of odd sizes == torch.optim.Adam(foreach=False)."""
+    from rsx.optim import RsxAdam
+
+    shapes = [(300, 64), (64,), (1, 33, 2), (70, 4096), (5,), (7050, 384), (1,)] + [(3, 3)] * 30
+    gen = torch.Generator(device="cpu").manual_seed(2)
+    ps = [torch.randn(*s, generator=gen).to(cuda) for s in shapes]
+    a = [p.clone().requires_grad_() for p in ps]
+    b = [p.clone().requires_grad_() for p in ps]
+    oa = torch.optim.Adam(a, lr=1e-2, foreach=False)
+    ob = RsxAdam(b, lr=1e-2)
+    for it in range(3):
+        gs = [torch.randn(*s, generator=gen).to(cuda) for s in shapes]
+        for k, (x, y, g) in enumerate(zip(a, b, gs)):
+            if it == 1 and k % 5 == 0:  # a parameter without a gradient this step keeps its own step count
+                x.grad = y.grad = None
+                continue
+            x.grad = g.clone()
+            y.grad = g.clone()
+        oa.step()
+        ob.step()
+    for x, y in zip(a, b):
+        np.testing.assert_allclose(y.detach().cpu().numpy(), x.detach().cpu().numpy(), rtol=0, atol=1e-6)
