@@ -512,6 +512,34 @@ int rsx_smore_infonce_bwd(const float* side, const float* content, const int64_t
                           int64_t n_users, int64_t batch, int32_t d, float tau, const float* g_loss, float* g_side,
                           float* g_content, void* ws, size_t ws_bytes, rsx_stream_t stream);
 /*
+ * Model-level mirror gradient (reference src/common/trainer.py:285-336) over `count`
+ * (param, grad) pairs of n[i] floats:
+ *   rsx_mg_alpha: alpha_out (device f64) = min(max(base, rel_step * rms(p) /
+ *     (lr * rms(g) + 1e-12)), base * max_scale), rms over all pairs together (sums of
+ *     squares in f64, per-block partials reduced in order: deterministic);
+ *   rsx_axpy_multi: y[i] += float(*alpha_dev * mult) * x[i] (the mirror step with
+ *     mult = -lr, its restore with mult = +lr), one launch per 32 tensors.
+ */
+size_t rsx_mg_alpha_ws_bytes(int32_t count, const int64_t* n);
+int rsx_mg_alpha(int32_t count, const float* const* params, const float* const* grads, const int64_t* n,
+                 double base, double lr, double rel_step, double max_scale, double* alpha_out, void* ws,
+                 size_t ws_bytes, rsx_stream_t stream);
+int rsx_axpy_multi(int32_t count, float* const* y, const float* const* x, const int64_t* n,
+                   const double* alpha_dev, double mult, rsx_stream_t stream);
+/*
+ * SMORE's spectral filter weights (reference src/models/smore.py:221-229): three
+ * [d/2+1][2] (re, im) parameters -> out [3][d/2+1][2], each w / (|w| + 1e-8) when
+ * normalize (else copied): the unit weights rsx_smore_spectral_fwd/bwd take.  The
+ * backward sums rsx_smore_spectral_bwd's per-block partials [n_blocks][3][d/2+1][2]
+ * in block order and applies the normalisation's Jacobian: gradients of the raw
+ * parameters.
+ */
+int rsx_smore_unit_weights(const float* wv, const float* wt, const float* wf, int32_t d, int32_t normalize,
+                           float* out, rsx_stream_t stream);
+int rsx_smore_unit_weights_bwd(const float* partials, int64_t n_blocks, const float* wv, const float* wt,
+                               const float* wf, int32_t d, int32_t normalize, float* gv, float* gt, float* gf,
+                               rsx_stream_t stream);
+/*
  * torch.optim.Adam (single-tensor arithmetic, as rsx_rowwise's ADAM epilogue) over
  * `count` flat tensors in one launch per 32 tensors; step_dev[i]: tensor i's
  * (already incremented) int64 step count on the device.  Replaces the per-parameter

@@ -133,20 +133,21 @@ __device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-// z[n][o] = sum_k W[o][k] x[n][k]  (+ b[o]),  W [D][D] row-major (nn.Linear weight).
+// z[n][o] = sum_k W[o][k] x[n][k]  (+ b[o]),  W [D][D] row-major (nn.Linear weight)
+// with row stride LD (the padded LDS copy: LD = D + 4, conflict-free float4 reads).
 // K outer, output tiles inner: consecutive MFMAs go to different accumulators (the
 // 16x16x4 form's dependent latency is 40 cycles against a 32-cycle issue).
-template <int D>
+template <int D, int LD>
 __device__ __forceinline__ Fld<D> mv(const float* __restrict__ W, const float* b, const Fld<D>& x, int lane) {
     constexpr int T = D / 16;
     const int c = lane & 15, g = lane >> 4;
     Fld<D> z = fvec<D>(b, g);
-    const float* wr = W + (int64_t)c * D + 4 * g;
+    const float* wr = W + c * LD + 4 * g;
 #pragma unroll
     for (int t = 0; t < T; ++t) {
         float4 w[T];
 #pragma unroll
-        for (int to = 0; to < T; ++to) w[to] = ld4(wr + (int64_t)16 * to * D + 16 * t);
+        for (int to = 0; to < T; ++to) w[to] = ld4(wr + 16 * to * LD + 16 * t);
 #pragma unroll
         for (int to = 0; to < T; ++to) z.f[to] = mfma4(w[to].x, x.f[t][0], z.f[to]);
 #pragma unroll
@@ -160,7 +161,7 @@ __device__ __forceinline__ Fld<D> mv(const float* __restrict__ W, const float* b
 }
 
 // z[n][k] = sum_o W[o][k] x[n][o]  (the input gradient of a Linear)
-template <int D>
+template <int D, int LD>
 __device__ __forceinline__ Fld<D> mvt(const float* __restrict__ W, const Fld<D>& x, int lane) {
     constexpr int T = D / 16;
     const int c = lane & 15, g = lane >> 4;
@@ -169,12 +170,30 @@ __device__ __forceinline__ Fld<D> mvt(const float* __restrict__ W, const Fld<D>&
     for (int t = 0; t < T; ++t) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const float* wr = W + (int64_t)(16 * t + 4 * g + r) * D + c;
+            const float* wr = W + (16 * t + 4 * g + r) * LD + c;
 #pragma unroll
             for (int tk = 0; tk < T; ++tk) z.f[tk] = mfma4(wr[16 * tk], x.f[t][r], z.f[tk]);
         }
     }
     return z;
+}
+
+// A block's copy of one [D][D] weight in LDS, rows padded to D + 4 floats: every
+// wave of the block reads it (a 16-row tile each) instead of streaming it from L2
+// per MFMA step.  All threads of the block call it, in the same order.
+template <int D>
+constexpr int kLd = D + 4;
+
+template <int D>
+__device__ __forceinline__ const float* stage_w(float* __restrict__ lds, const float* __restrict__ W) {
+    __syncthreads();  // the previous weight's readers are done
+    constexpr int Q = D / 4;
+    for (int i = threadIdx.x; i < D * Q; i += blockDim.x) {
+        const int row = i / Q, c4 = i - row * Q;
+        *reinterpret_cast<float4*>(lds + row * kLd<D> + 4 * c4) = ld4(W + (int64_t)row * D + 4 * c4);
+    }
+    __syncthreads();
+    return lds;
 }
 
 // S^T tile: s[r] = <Y row (4g + r), X row c> over D (two accumulators, summed at the end)
@@ -254,15 +273,15 @@ struct GateArgs {
 
 template <int D>
 __global__ __launch_bounds__(256) void gates_fwd(GateArgs a) {
+    __shared__ __attribute__((aligned(16))) float wl[D * kLd<D>];
     const int lane = threadIdx.x & 63, g = lane >> 4;
     const int64_t n0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 16;
-    if (n0 >= a.n) return;
     const int64_t row = n0 + (lane & 15) < a.n ? n0 + (lane & 15) : -1;
     const Fld<D> it = fload<D>(a.item, row, g);
 #pragma unroll 1
     for (int m = 0; m < 3; ++m) {
         const Fld<D> cv = fload<D>(a.conv[m], row, g);
-        const Fld<D> s = fmap<D>(mv<D>(a.W[m], a.b[m], cv, lane), sigm);
+        const Fld<D> s = fmap<D>(mv<D, kLd<D>>(stage_w<D>(wl, a.W[m]), a.b[m], cv, lane), sigm);
         const Fld<D> o = a.mul ? fmap2<D>(it, s, [](float x, float y) { return x * y; })
                                : fmap2<D>(it, s, [&](float x, float y) { return x + a.scale * y; });
         fstore<D>(a.out[m], row, g, o);
@@ -271,9 +290,9 @@ __global__ __launch_bounds__(256) void gates_fwd(GateArgs a) {
 
 template <int D>
 __global__ __launch_bounds__(256) void gates_bwd(GateArgs a) {
+    __shared__ __attribute__((aligned(16))) float wl[D * kLd<D>];
     const int lane = threadIdx.x & 63, g = lane >> 4;
     const int64_t n0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 16;
-    if (n0 >= a.n) return;
     const int64_t row = n0 + (lane & 15) < a.n ? n0 + (lane & 15) : -1;
     const Fld<D> it = fload<D>(a.item, row, g);
     Fld<D> gi = fzero<D>();
@@ -281,7 +300,8 @@ __global__ __launch_bounds__(256) void gates_bwd(GateArgs a) {
     for (int m = 0; m < 3; ++m) {
         const Fld<D> go = a.gout[m] ? fload<D>(a.gout[m], row, g) : fzero<D>();
         const Fld<D> cv = fload<D>(a.conv[m], row, g);
-        const Fld<D> s = fmap<D>(mv<D>(a.W[m], a.b[m], cv, lane), sigm);
+        const float* W = stage_w<D>(wl, a.W[m]);
+        const Fld<D> s = fmap<D>(mv<D, kLd<D>>(W, a.b[m], cv, lane), sigm);
         Fld<D> ds;
         if (a.mul) {
             gi = fmap3<D>(gi, go, s, [](float acc, float x, float y) { return acc + x * y; });
@@ -292,7 +312,7 @@ __global__ __launch_bounds__(256) void gates_bwd(GateArgs a) {
         }
         const Fld<D> dz = fmap2<D>(ds, s, [](float x, float y) { return x * ((1.f - y) * y); });
         fstore<D>(a.dz[m], row, g, dz);
-        fstore<D>(a.g_conv[m], row, g, mvt<D>(a.W[m], dz, lane));
+        fstore<D>(a.g_conv[m], row, g, mvt<D, kLd<D>>(W, dz, lane));
     }
     fstore<D>(a.g_item, row, g, gi);
 }
@@ -328,26 +348,27 @@ struct PrefArgs {
 
 template <int D>
 __global__ __launch_bounds__(256) void pref_fwd(PrefArgs a) {
+    __shared__ __attribute__((aligned(16))) float wl[D * kLd<D>];
     const int lane = threadIdx.x & 63, g = lane >> 4;
     const int64_t n0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 16;
-    if (n0 >= a.n) return;
     const int64_t row = n0 + (lane & 15) < a.n ? n0 + (lane & 15) : -1;
     const uint64_t seed = a.p_drop > 0.f ? (uint64_t)*a.seed : 0;
     const auto mul = [](float x, float y) { return x * y; };
+    const auto lin = [&](int k, const Fld<D>& x) { return mv<D, kLd<D>>(stage_w<D>(wl, a.W[k]), a.b[k], x, lane); };
     const Fld<D> FE = fload<D>(a.FE, row, g);
     const Fld<D> C = fload<D>(a.C, row, g);
     // agg_img = ip * (softmax(query_v(FE)) * IE)
-    Fld<D> h = fmap<D>(mv<D>(a.W[kW1v], a.b[kW1v], FE, lane), tanh_);
-    Fld<D> s = softmax_row<D>(mv<D>(a.W[kW2v], nullptr, h, lane));
-    Fld<D> ip = fmap<D>(mv<D>(a.W[kWip], a.b[kWip], C, lane), sigm);
+    Fld<D> h = fmap<D>(lin(kW1v, FE), tanh_);
+    Fld<D> s = softmax_row<D>(lin(kW2v, h));
+    Fld<D> ip = fmap<D>(lin(kWip, C), sigm);
     if (a.p_drop > 0.f) ip = fmap2<D>(ip, drop_scale<D>(seed, 0, row, g, a.p_drop, a.drop_scale), mul);
     const Fld<D> x1 = fmap3<D>(ip, s, fload<D>(a.IE, row, g), [](float p, float q, float e) { return p * (q * e); });
-    h = fmap<D>(mv<D>(a.W[kW1t], a.b[kW1t], FE, lane), tanh_);
-    s = softmax_row<D>(mv<D>(a.W[kW2t], nullptr, h, lane));
-    Fld<D> tp = fmap<D>(mv<D>(a.W[kWtp], a.b[kWtp], C, lane), sigm);
+    h = fmap<D>(lin(kW1t, FE), tanh_);
+    s = softmax_row<D>(lin(kW2t, h));
+    Fld<D> tp = fmap<D>(lin(kWtp, C), sigm);
     if (a.p_drop > 0.f) tp = fmap2<D>(tp, drop_scale<D>(seed, 1, row, g, a.p_drop, a.drop_scale), mul);
     const Fld<D> x2 = fmap3<D>(tp, s, fload<D>(a.TE, row, g), [](float p, float q, float e) { return p * (q * e); });
-    Fld<D> fp = fmap<D>(mv<D>(a.W[kWfp], a.b[kWfp], C, lane), sigm);
+    Fld<D> fp = fmap<D>(lin(kWfp, C), sigm);
     if (a.p_drop > 0.f) fp = fmap2<D>(fp, drop_scale<D>(seed, 2, row, g, a.p_drop, a.drop_scale), mul);
     // side = mean(stack([x1, x2, fp * FE]))  (sum, then * 1/3 as torch's mean)
     const Fld<D> sd = fmap3<D>(x1, x2, fmap2<D>(fp, FE, mul),
@@ -358,9 +379,9 @@ __global__ __launch_bounds__(256) void pref_fwd(PrefArgs a) {
 
 template <int D>
 __global__ __launch_bounds__(256) void pref_bwd(PrefArgs a) {
+    __shared__ __attribute__((aligned(16))) float wl[D * kLd<D>];
     const int lane = threadIdx.x & 63, g = lane >> 4;
     const int64_t n0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 16;
-    if (n0 >= a.n) return;
     const int64_t row = n0 + (lane & 15) < a.n ? n0 + (lane & 15) : -1;
     const uint64_t seed = a.p_drop > 0.f ? (uint64_t)*a.seed : 0;
     const auto mul = [](float x, float y) { return x * y; };
@@ -375,42 +396,47 @@ __global__ __launch_bounds__(256) void pref_bwd(PrefArgs a) {
     Fld<D> gC = gA;
     Fld<D> gFE;
     {   // fusion view: x3 = fp * FE
-        const Fld<D> sf = fmap<D>(mv<D>(a.W[kWfp], a.b[kWfp], C, lane), sigm);
+        const float* W = stage_w<D>(wl, a.W[kWfp]);
+        const Fld<D> sf = fmap<D>(mv<D, kLd<D>>(W, a.b[kWfp], C, lane), sigm);
         const Fld<D> mf = a.p_drop > 0.f ? drop_scale<D>(seed, 2, row, g, a.p_drop, a.drop_scale) : Fld<D>{};
         const Fld<D> fp = a.p_drop > 0.f ? fmap2<D>(sf, mf, mul) : sf;
         Fld<D> dp = fmap2<D>(g1, FE, mul);
         if (a.p_drop > 0.f) dp = fmap2<D>(dp, mf, mul);
         const Fld<D> dz = fmap2<D>(dp, sf, sig_bwd);
         fstore<D>(a.dz[kWfp], row, g, dz);
-        gC = fmap2<D>(gC, mvt<D>(a.W[kWfp], dz, lane), add);
+        gC = fmap2<D>(gC, mvt<D, kLd<D>>(W, dz, lane), add);
         gFE = fmap2<D>(g1, fp, mul);
     }
 #pragma unroll 1
     for (int v = 0; v < 2; ++v) {  // v = 0: image view, 1: text view
         const int w1 = v ? kW1t : kW1v, w2 = v ? kW2t : kW2v, wp = v ? kWtp : kWip;
-        const Fld<D> h = fmap<D>(mv<D>(a.W[w1], a.b[w1], FE, lane), tanh_);
+        const Fld<D> h = fmap<D>(mv<D, kLd<D>>(stage_w<D>(wl, a.W[w1]), a.b[w1], FE, lane), tanh_);
         fstore<D>(v ? a.ht : a.hv, row, g, h);
-        const Fld<D> s = softmax_row<D>(mv<D>(a.W[w2], nullptr, h, lane));
-        const Fld<D> sp = fmap<D>(mv<D>(a.W[wp], a.b[wp], C, lane), sigm);
-        const Fld<D> mp = a.p_drop > 0.f ? drop_scale<D>(seed, v, row, g, a.p_drop, a.drop_scale) : Fld<D>{};
-        const Fld<D> pp = a.p_drop > 0.f ? fmap2<D>(sp, mp, mul) : sp;
+        const Fld<D> s = softmax_row<D>(mv<D, kLd<D>>(stage_w<D>(wl, a.W[w2]), nullptr, h, lane));
         const Fld<D> E = fload<D>(v ? a.TE : a.IE, row, g);
-        // x = pp * (s * E)
-        Fld<D> dpp = fmap3<D>(g1, s, E, [](float u, float q, float e) { return u * (q * e); });
-        if (a.p_drop > 0.f) dpp = fmap2<D>(dpp, mp, mul);
-        const Fld<D> dzp = fmap2<D>(dpp, sp, sig_bwd);
-        fstore<D>(a.dz[wp], row, g, dzp);
-        gC = fmap2<D>(gC, mvt<D>(a.W[wp], dzp, lane), add);
+        Fld<D> pp;
+        {
+            const float* W = stage_w<D>(wl, a.W[wp]);
+            const Fld<D> sp = fmap<D>(mv<D, kLd<D>>(W, a.b[wp], C, lane), sigm);
+            const Fld<D> mp = a.p_drop > 0.f ? drop_scale<D>(seed, v, row, g, a.p_drop, a.drop_scale) : Fld<D>{};
+            pp = a.p_drop > 0.f ? fmap2<D>(sp, mp, mul) : sp;
+            // x = pp * (s * E)
+            Fld<D> dpp = fmap3<D>(g1, s, E, [](float u, float q, float e) { return u * (q * e); });
+            if (a.p_drop > 0.f) dpp = fmap2<D>(dpp, mp, mul);
+            const Fld<D> dzp = fmap2<D>(dpp, sp, sig_bwd);
+            fstore<D>(a.dz[wp], row, g, dzp);
+            gC = fmap2<D>(gC, mvt<D, kLd<D>>(W, dzp, lane), add);
+        }
         const Fld<D> da = fmap2<D>(g1, pp, mul);          // d (s * E)
         fstore<D>(v ? a.gTE : a.gIE, row, g, fmap2<D>(da, s, mul));
         const Fld<D> dsm = fmap2<D>(da, E, mul);          // d softmax output
         const float dot = rsum<D>(fmap2<D>(dsm, s, mul));
         const Fld<D> dq = fmap2<D>(s, dsm, [&](float y, float gy) { return y * (gy - dot); });
         fstore<D>(a.dz[w2], row, g, dq);
-        const Fld<D> dh = mvt<D>(a.W[w2], dq, lane);
+        const Fld<D> dh = mvt<D, kLd<D>>(stage_w<D>(wl, a.W[w2]), dq, lane);
         const Fld<D> dz1 = fmap2<D>(dh, h, [](float gy, float y) { return gy * (1.f - y * y); });
         fstore<D>(a.dz[w1], row, g, dz1);
-        gFE = fmap2<D>(gFE, mvt<D>(a.W[w1], dz1, lane), add);
+        gFE = fmap2<D>(gFE, mvt<D, kLd<D>>(stage_w<D>(wl, a.W[w1]), dz1, lane), add);
     }
     fstore<D>(a.gC, row, g, gC);
     fstore<D>(a.gFE, row, g, gFE);
@@ -432,43 +458,88 @@ struct WgArgs {
     float* part;                // [n_pairs][n_splits][D*D + D]
 };
 
-// block (split, pair); wave w owns output row tiles to = w, w+4, ..; lane (k, g)
+// block (split, pair): rows [r0, r1) in chunks of 32, each chunk's dz and x rows
+// staged in LDS (row stride D + 16: the 4 K-rows x 16 columns of an MFMA operand
+// read fall in 64 distinct banks), the next chunk's float4s loaded into registers
+// while this one is multiplied.  Wave w owns output row tiles to = w, w + 4, ..;
+// D[o][k]: lane (k, g) reg r holds o = 16 to + 4 g + r, k = 16 tk + c.
+constexpr int kWgChunk = 32;
+
 template <int D>
 __global__ __launch_bounds__(256) void wgrad_part(WgArgs a) {
-    constexpr int T = D / 16, TPW = (T + 3) / 4;
+    constexpr int T = D / 16, TPW = (T + 3) / 4, LD = D + 16;
+    constexpr int Q = D / 4;                          // float4s per row
+    constexpr int PER = kWgChunk * Q / 256;           // float4s per thread per array
+    __shared__ __attribute__((aligned(16))) float zl[kWgChunk * LD];
+    __shared__ __attribute__((aligned(16))) float xl[kWgChunk * LD];
     const int split = blockIdx.x, pr = blockIdx.y;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
     const float* __restrict__ dz = a.dz[pr];
     const float* __restrict__ x = a.x[pr];
     const int64_t r0 = (int64_t)split * kWgRows, r1 = min(a.n, r0 + kWgRows);
     float* out = a.part + ((int64_t)pr * a.n_splits + split) * (D * D + D);
-#pragma unroll 1
+    floatx4 acc[TPW][T];
+#pragma unroll
+    for (int q = 0; q < TPW; ++q)
+#pragma unroll
+        for (int tk = 0; tk < T; ++tk) acc[q][tk] = floatx4{0.f, 0.f, 0.f, 0.f};
+    float bs[TPW];
+#pragma unroll
+    for (int q = 0; q < TPW; ++q) bs[q] = 0.f;
+    float4 pz[PER], px[PER];
+    auto fetch = [&](int64_t cb) {
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int e = threadIdx.x + 256 * i;
+            const int rr = e / Q, c4 = e - rr * Q;
+            const bool ok = cb + rr < r1;
+            pz[i] = ok ? ld4(dz + (cb + rr) * D + 4 * c4) : f4(0.f);
+            px[i] = ok ? ld4(x + (cb + rr) * D + 4 * c4) : f4(0.f);
+        }
+    };
+    if (r0 < r1) fetch(r0);
+    for (int64_t cb = r0; cb < r1; cb += kWgChunk) {
+        __syncthreads();  // the previous chunk's readers are done
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int e = threadIdx.x + 256 * i;
+            const int rr = e / Q, c4 = e - rr * Q;
+            *reinterpret_cast<float4*>(zl + rr * LD + 4 * c4) = pz[i];
+            *reinterpret_cast<float4*>(xl + rr * LD + 4 * c4) = px[i];
+        }
+        __syncthreads();
+        if (cb + kWgChunk < r1) fetch(cb + kWgChunk);
+#pragma unroll
+        for (int s = 0; s < kWgChunk / 4; ++s) {
+            const float* zr = zl + (4 * s + g) * LD + c;
+            const float* xr = xl + (4 * s + g) * LD + c;
+            float bv[T];
+#pragma unroll
+            for (int tk = 0; tk < T; ++tk) bv[tk] = xr[16 * tk];
+#pragma unroll
+            for (int q = 0; q < TPW; ++q) {
+                const int to = w + 4 * q;
+                if (to < T) {
+                    const float av = zr[16 * to];  // A[o = 16to + c][K = row 4s + g]
+                    bs[q] += av;
+#pragma unroll
+                    for (int tk = 0; tk < T; ++tk) acc[q][tk] = mfma4(av, bv[tk], acc[q][tk]);
+                }
+            }
+        }
+    }
+#pragma unroll
     for (int q = 0; q < TPW; ++q) {
         const int to = w + 4 * q;
         if (to >= T) break;
-        floatx4 acc[T];
-#pragma unroll
-        for (int tk = 0; tk < T; ++tk) acc[tk] = floatx4{0.f, 0.f, 0.f, 0.f};
-        float bs = 0.f;
-        for (int64_t r = r0; r < r1; r += 4) {
-            const int64_t rr = r + g;
-            const bool ok = rr < r1;
-            const float av = ok ? dz[rr * D + 16 * to + c] : 0.f;  // A[o = 16to + c][K = rr]
-            bs += av;
-#pragma unroll
-            for (int tk = 0; tk < T; ++tk) {
-                const float bv = ok ? x[rr * D + 16 * tk + c] : 0.f;  // B[K = rr][k = 16tk + c]
-                acc[tk] = mfma4(av, bv, acc[tk]);
-            }
-        }
-        // D[o][k]: lane (k, g) reg r holds o = 16to + 4g + r, k = 16tk + c
 #pragma unroll
         for (int tk = 0; tk < T; ++tk)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) out[(16 * to + 4 * g + r) * D + 16 * tk + c] = acc[tk][r];
-        bs += __shfl_xor(bs, 16, kWave);
-        bs += __shfl_xor(bs, 32, kWave);
-        if (g == 0) out[D * D + 16 * to + c] = bs;
+            for (int r = 0; r < 4; ++r) out[(16 * to + 4 * g + r) * D + 16 * tk + c] = acc[q][tk][r];
+        float b = bs[q];
+        b += __shfl_xor(b, 16, kWave);
+        b += __shfl_xor(b, 32, kWave);
+        if (g == 0) out[D * D + 16 * to + c] = b;
     }
 }
 
@@ -540,14 +611,23 @@ __global__ __launch_bounds__(64 * kNceWaves) void nce_fwd(NceArgs a) {
     const Fld<D> X = nce_load_norm<D>(a, term, 0, bo, g, &nn1);  // own view1 rows (B operand)
     const int64_t ntile = (B + 15) / 16;
     float es = 0.f;  // exp sum of own row c over the other rows 4g + r of this wave's tiles
+    auto rows_of = [&](int64_t mt) {
+        const int64_t bm = mt * 16 + c;
+        return (mt < ntile && bm < B) ? a.idx[term][bm] + a.off[term] : (int64_t)-1;
+    };
+    auto normalize = [&](const Fld<D>& x) {
+        const float den = fmaxf(sqrtf(rsum<D>(fmap<D>(x, [](float v) { return v * v; }))), 1e-12f);
+        return fmap<D>(x, [&](float v) { return v / den; });
+    };
+    Fld<D> Y = normalize(fload<D>(a.src2, rows_of(w), g));  // other view2 rows (A operand)
     for (int64_t mt = w; mt < ntile; mt += kNceWaves) {
+        const Fld<D> Yn = fload<D>(a.src2, rows_of(mt + kNceWaves), g);  // next tile, in flight
         const int64_t m0 = mt * 16;
-        const int64_t bm = m0 + c < B ? m0 + c : -1;
-        const Fld<D> Y = nce_load_norm<D>(a, term, 1, bm, g, nullptr);  // other view2 rows (A operand)
         const floatx4 s = tile_dot<D>(Y, X);  // s[r] = S[own c][other m0 + 4g + r] * tau
 #pragma unroll
         for (int r = 0; r < 4; ++r)
             if (m0 + 4 * g + r < B) es += expf(s[r] / a.tau);
+        Y = normalize(Yn);
     }
     es += __shfl_xor(es, 16, kWave);
     es += __shfl_xor(es, 32, kWave);
@@ -586,7 +666,9 @@ __global__ __launch_bounds__(64) void nce_mean(NceArgs a) {
 template <int D>
 __global__ __launch_bounds__(64 * kNceWaves) void nce_bwd(NceArgs a) {
     constexpr int T = D / 16;
-    __shared__ floatx4 red[kNceWaves][64][T];
+    constexpr int TILE = 16 * kLd<D>;  // one wave's other-tile copy (rows padded)
+    static_assert(kNceWaves * 64 * T * 4 <= kNceWaves * TILE, "reduction fits the tile buffer");
+    __shared__ __attribute__((aligned(16))) float sm[kNceWaves * TILE];
     const int term = blockIdx.z, mode = blockIdx.y;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
     const int64_t B = a.B;
@@ -596,45 +678,68 @@ __global__ __launch_bounds__(64 * kNceWaves) void nce_bwd(NceArgs a) {
     const float* oth_n = a.nrm + ((int64_t)(term * 2 + (mode ^ 1)) * B) * D;
     const float* ttl = a.ttl + term * B;
     const Fld<D> X = fload<D>(own_n, bo, g);
-    const float inv_tau = 1.f / a.tau;
     const float ttl_own = (mode == 0 && bo >= 0) ? ttl[bo] : 1.f;
+    float* tl = sm + w * TILE;
     Fld<D> O = fzero<D>();
     const int64_t ntile = (B + 15) / 16;
+    auto row_of = [&](int64_t mt) { return (mt < ntile && mt * 16 + c < B) ? mt * 16 + c : (int64_t)-1; };
+    auto ttl_of = [&](int64_t mt) {  // mode 1: the divisor of the other rows 4g + r
+        floatx4 t = {1.f, 1.f, 1.f, 1.f};
+        if (mode == 1)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int64_t m = mt * 16 + 4 * g + r;
+                if (mt < ntile && m < B) t[r] = ttl[m];
+            }
+        return t;
+    };
+    Fld<D> Y = fload<D>(oth_n, row_of(w), g);
+    floatx4 tv = ttl_of(w);
     for (int64_t mt = w; mt < ntile; mt += kNceWaves) {
+        const Fld<D> Yn = fload<D>(oth_n, row_of(mt + kNceWaves), g);  // next tile, in flight
+        const floatx4 tvn = ttl_of(mt + kNceWaves);
         const int64_t m0 = mt * 16;
-        const int64_t bm = m0 + c < B ? m0 + c : -1;
-        const Fld<D> Y = fload<D>(oth_n, bm, g);
         const floatx4 s = tile_dot<D>(Y, X);
         // P for own row c and other rows m0 + 4g + r
         floatx4 p;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const int64_t m = m0 + 4 * g + r;
-            const float den = mode == 0 ? ttl_own : (m < B ? ttl[m] : 1.f);
-            p[r] = m < B ? expf(s[r] / a.tau) / den : 0.f;
+            const bool ok = m0 + 4 * g + r < B;
+            p[r] = ok ? expf(s[r] / a.tau) / (mode == 0 ? ttl_own : tv[r]) : 0.f;
         }
-        // O^T[k][own] += sum_m Y^T[k][m] P^T[m][own]: K slot (r, g) = other row m0 + 4g + r
+        // O^T[k][own] += sum_m Y^T[k][m] P^T[m][own] (K slot (r, g) = other row m0 + 4g + r):
+        // the A operand is the tile transposed, through this wave's LDS copy
+#pragma unroll
+        for (int t = 0; t < T; ++t)
+            *reinterpret_cast<floatx4*>(tl + (lane & 15) * kLd<D> + 16 * t + 4 * g) = Y.f[t];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const int64_t m = m0 + 4 * g + r;
-            const float* yr = oth_n + (m < B ? m : 0) * D + c;
+            const float* yr = tl + (4 * g + r) * kLd<D> + c;
 #pragma unroll
-            for (int tk = 0; tk < T; ++tk) O.f[tk] = mfma4(m < B ? yr[16 * tk] : 0.f, p[r], O.f[tk]);
+            for (int tk = 0; tk < T; ++tk) O.f[tk] = mfma4(yr[16 * tk], p[r], O.f[tk]);
         }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        Y = Yn;
+        tv = tvn;
     }
+    __syncthreads();
+    floatx4* red = reinterpret_cast<floatx4*>(sm);  // [wave][lane][T]
 #pragma unroll
-    for (int t = 0; t < T; ++t) red[w][lane][t] = O.f[t];
+    for (int t = 0; t < T; ++t) red[(w * 64 + lane) * T + t] = O.f[t];
     __syncthreads();
     if (w != 0) return;
 #pragma unroll
     for (int t = 0; t < T; ++t) {
-        floatx4 s = red[0][lane][t];
+        floatx4 s = red[lane * T + t];
 #pragma unroll
-        for (int i = 1; i < kNceWaves; ++i) s += red[i][lane][t];
+        for (int i = 1; i < kNceWaves; ++i) s += red[(i * 64 + lane) * T + t];
         O.f[t] = s;
     }
     if (bo < 0) return;
-    const float coef = a.gloss[term] * inv_tau / (float)B;
+    const float coef = a.gloss[term] * (1.f / a.tau) / (float)B;
     const Fld<D> Z = fload<D>(oth_n, bo, g);  // the own row's other view
     const Fld<D> dn = fmap2<D>(O, Z, [&](float o, float z) { return coef * (o - z); });
     // F.normalize backward: (dn - y <y, dn>) / |x|, or dn / eps when |x| <= eps
@@ -666,6 +771,7 @@ struct AdamList {
     const int64_t* step[kAdamMax];
     int64_t n[kAdamMax];
     int64_t blk[kAdamMax + 1];
+    uint32_t vec4;       // bit i: tensor i is float4-aligned with n % 4 == 0
     int32_t count;
     float lr, beta1, beta2, eps, wd;
 };
@@ -688,6 +794,24 @@ __global__ __launch_bounds__(256) void adam_multi(AdamList L) {
     float* __restrict__ v = L.v[t];
     const int64_t base = ((int64_t)blockIdx.x - L.blk[t]) * kAdamPerBlock;
     const int64_t n = L.n[t];
+    if ((L.vec4 >> t) & 1u) {
+#pragma unroll
+        for (int k = 0; k < kAdamPerBlock / 1024; ++k) {
+            const int64_t i = base + 4 * (k * 256 + threadIdx.x);
+            if (i < n) {
+                float4 pp = ld4(p + i), mm = ld4(m + i), vv = ld4(v + i);
+                const float4 gg = ld4(gr + i);
+                adam_elem(c, pp.x, mm.x, vv.x, gg.x);
+                adam_elem(c, pp.y, mm.y, vv.y, gg.y);
+                adam_elem(c, pp.z, mm.z, vv.z, gg.z);
+                adam_elem(c, pp.w, mm.w, vv.w, gg.w);
+                st4(p + i, pp);
+                st4(m + i, mm);
+                st4(v + i, vv);
+            }
+        }
+        return;
+    }
 #pragma unroll
     for (int k = 0; k < kAdamPerBlock / 256; ++k) {
         const int64_t i = base + k * 256 + threadIdx.x;
@@ -699,6 +823,144 @@ __global__ __launch_bounds__(256) void adam_multi(AdamList L) {
             v[i] = vv;
         }
     }
+}
+
+// ---------------------------------------------------------------------------
+// model-level mirror gradient (reference src/common/trainer.py:268-348)
+// ---------------------------------------------------------------------------
+// The scale alpha_eff = clamp(max(base, rel * rms(p) / (lr * rms(g) + 1e-12)), base * max)
+// from ONE pass over every (p, g) pair (per-block f64 sums of squares, reduced in
+// block order: deterministic), and p += float(alpha * mult) * g over the list in one
+// launch (the reference's per-parameter p.add_(-alpha * lr * g) and its restore).
+struct PairList {
+    float* y[kAdamMax];
+    const float* x[kAdamMax];
+    int64_t n[kAdamMax];
+    int64_t blk[kAdamMax + 1];
+    int32_t count;
+};
+
+__device__ __forceinline__ int list_slot(const PairList& L) {
+    int t = 0;
+    while (t + 1 < L.count && (int64_t)blockIdx.x >= L.blk[t + 1]) ++t;
+    return t;
+}
+
+// partial[block] = (sum g^2, sum p^2) over the block's 2048 elements (x = g, y = p)
+__global__ __launch_bounds__(256) void mg_sumsq(PairList L, double* partial) {
+    const int t = list_slot(L);
+    const int64_t base = ((int64_t)blockIdx.x - L.blk[t]) * kAdamPerBlock;
+    double sg = 0.0, sp = 0.0;
+    for (int k = 0; k < kAdamPerBlock / 256; ++k) {
+        const int64_t i = base + k * 256 + threadIdx.x;
+        if (i < L.n[t]) {
+            const double gv = L.x[t][i], pv = L.y[t][i];
+            sg += gv * gv;
+            sp += pv * pv;
+        }
+    }
+    __shared__ double red[2][4];
+    sg = group_sum_d<64>(sg);
+    sp = group_sum_d<64>(sp);
+    if ((threadIdx.x & 63) == 0) {
+        red[0][threadIdx.x >> 6] = sg;
+        red[1][threadIdx.x >> 6] = sp;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        partial[2 * blockIdx.x] = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+        partial[2 * blockIdx.x + 1] = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+    }
+}
+
+// one wave: the block sums in order (lane-strided, then a fixed tree), then the
+// reference's scalar arithmetic: rms values as f32 tensor results, the rest in f64
+__global__ __launch_bounds__(64) void mg_alpha_final(const double* partial, int64_t n_blocks, int64_t numel,
+                                                     double base, double lr, double rel, double max_scale,
+                                                     double* alpha) {
+    double sg = 0.0, sp = 0.0;
+    for (int64_t b = threadIdx.x; b < n_blocks; b += 64) {
+        sg += partial[2 * b];
+        sp += partial[2 * b + 1];
+    }
+    sg = group_sum_d<64>(sg);
+    sp = group_sum_d<64>(sp);
+    if (threadIdx.x != 0) return;
+    const float sq = (float)sqrt((double)numel);
+    const double grad_rms = (double)((float)sqrt(sg) / sq);
+    const double param_rms = (double)((float)sqrt(sp) / sq + 1e-12f);
+    double a = rel * param_rms / (lr * grad_rms + 1e-12);
+    a = a > base ? a : base;  // Python max(base, x): keeps base when x is NaN
+    const double cap = base * max_scale;
+    *alpha = a < cap ? a : cap;
+}
+
+// y += float(alpha * mult) * x
+__global__ __launch_bounds__(256) void axpy_multi(PairList L, const double* alpha, double mult) {
+#pragma clang fp contract(off)  // two roundings, as torch's mul then add_ (device code contracts by default)
+    const int t = list_slot(L);
+    const float s = (float)(*alpha * mult);
+    const int64_t base = ((int64_t)blockIdx.x - L.blk[t]) * kAdamPerBlock;
+    float* __restrict__ y = L.y[t];
+    const float* __restrict__ x = L.x[t];
+#pragma unroll
+    for (int k = 0; k < kAdamPerBlock / 256; ++k) {
+        const int64_t i = base + k * 256 + threadIdx.x;
+        if (i < L.n[t]) y[i] = y[i] + x[i] * s;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// spectral filter weights: unit normalisation w / (|w| + 1e-8) (smore.py:221-229)
+// ---------------------------------------------------------------------------
+// three [nb][2] (re, im) weights -> out [3][nb][2]
+__global__ __launch_bounds__(256) void unit_w_fwd(const float* w0, const float* w1, const float* w2, int nb,
+                                                  int normalize, float* out) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= 3 * nb) return;
+    const float* w = i < nb ? w0 : (i < 2 * nb ? w1 : w2);
+    const int b = i % nb;
+    const float re = w[2 * b], im = w[2 * b + 1];
+    if (normalize) {
+        const float den = hypotf(re, im) + 1e-8f;  // torch.abs(complex) + 1e-8, then a complex / real division
+        out[2 * i] = re / den;
+        out[2 * i + 1] = im / den;
+    } else {
+        out[2 * i] = re;
+        out[2 * i + 1] = im;
+    }
+}
+
+// d w from the spectral backward's per-block partials [nblk][3][nb][2] (summed in
+// block order) through the normalisation: w~ = w / den, den = |w| + eps:
+// d w = g / den - <g, w> w / (|w| den^2)  (|w| = 0: torch's sgn(0) = 0, no second term)
+__global__ __launch_bounds__(256) void unit_w_bwd(const float* part, int nblk, const float* w0, const float* w1,
+                                                  const float* w2, int nb, int normalize, float* g0, float* g1,
+                                                  float* g2) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= 3 * nb) return;
+    float ga = 0.f, gb = 0.f;
+    for (int k = 0; k < nblk; ++k) {
+        ga += part[((int64_t)k * 3 * nb + i) * 2];
+        gb += part[((int64_t)k * 3 * nb + i) * 2 + 1];
+    }
+    const int m = i / nb, b = i % nb;
+    const float* w = m == 0 ? w0 : (m == 1 ? w1 : w2);
+    float* g = m == 0 ? g0 : (m == 1 ? g1 : g2);
+    if (normalize) {
+        const float re = w[2 * b], im = w[2 * b + 1];
+        const float r = hypotf(re, im), den = r + 1e-8f;
+        float da = ga / den, db = gb / den;
+        if (r > 0.f) {
+            const float k = (ga * re + gb * im) / (den * den) / r;
+            da -= k * re;
+            db -= k * im;
+        }
+        ga = da;
+        gb = db;
+    }
+    g[2 * b] = ga;
+    g[2 * b + 1] = gb;
 }
 
 }  // namespace sf
@@ -936,6 +1198,8 @@ int rsx_adam_multi(int32_t count, float* const* p, const float* const* g, float*
             L.step[k] = step_dev[i];
             L.n[k] = n[i];
             L.blk[k] = blocks;
+            const uintptr_t al = (uintptr_t)p[i] | (uintptr_t)g[i] | (uintptr_t)m[i] | (uintptr_t)v[i];
+            if ((n[i] & 3) == 0 && (al & 15) == 0) L.vec4 |= 1u << k;
             blocks += (n[i] + sf::kAdamPerBlock - 1) / sf::kAdamPerBlock;
             ++k;
         }
@@ -946,6 +1210,93 @@ int rsx_adam_multi(int32_t count, float* const* p, const float* const* g, float*
         if (rc) return rc;
     }
     return RSX_OK;
+}
+
+// the pair lists of up to 32 tensors each, in launch order; returns blocks per list
+static int build_pair_lists(int32_t count, float* const* y, const float* const* x, const int64_t* n,
+                            sf::PairList* lists, int n_lists, int64_t* blocks_out) {
+    int li = 0;
+    for (int32_t c0 = 0; c0 < count; c0 += sf::kAdamMax, ++li) {
+        if (li >= n_lists) return RSX_ERR_ARG;
+        sf::PairList& L = lists[li];
+        L = sf::PairList{};
+        int64_t blocks = 0;
+        int k = 0;
+        for (int32_t i = c0; i < count && i < c0 + sf::kAdamMax; ++i) {
+            if (n[i] < 0 || (n[i] > 0 && (!y[i] || !x[i]))) return RSX_ERR_ARG;
+            if (n[i] == 0) continue;
+            L.y[k] = y[i];
+            L.x[k] = x[i];
+            L.n[k] = n[i];
+            L.blk[k] = blocks;
+            blocks += (n[i] + sf::kAdamPerBlock - 1) / sf::kAdamPerBlock;
+            ++k;
+        }
+        L.blk[k] = blocks;
+        L.count = k;
+        blocks_out[li] = blocks;
+    }
+    return RSX_OK;
+}
+
+size_t rsx_mg_alpha_ws_bytes(int32_t count, const int64_t* n) {
+    int64_t blocks = 0;
+    for (int32_t i = 0; i < count; ++i) blocks += (n[i] + sf::kAdamPerBlock - 1) / sf::kAdamPerBlock;
+    return (size_t)(blocks > 0 ? blocks : 1) * 2 * sizeof(double);
+}
+
+int rsx_mg_alpha(int32_t count, const float* const* params, const float* const* grads, const int64_t* n,
+                 double base, double lr, double rel_step, double max_scale, double* alpha_out, void* ws,
+                 size_t ws_bytes, rsx_stream_t stream) {
+    if (count <= 0 || count > 8 * sf::kAdamMax || !params || !grads || !n || !alpha_out) return RSX_ERR_ARG;
+    if (!ws || ws_bytes < rsx_mg_alpha_ws_bytes(count, n)) return RSX_ERR_WORKSPACE;
+    sf::PairList lists[8];
+    int64_t blocks[8] = {0};
+    const int rc = build_pair_lists(count, const_cast<float* const*>(params), grads, n, lists, 8, blocks);
+    if (rc) return rc;
+    hipStream_t s = as_stream(stream);
+    double* part = static_cast<double*>(ws);
+    int64_t off = 0, numel = 0;
+    for (int32_t i = 0; i < count; ++i) numel += n[i];
+    for (int li = 0; li * sf::kAdamMax < count; ++li) {
+        if (blocks[li] > 0) hipLaunchKernelGGL(sf::mg_sumsq, dim3((unsigned)blocks[li]), dim3(256), 0, s, lists[li], part + 2 * off);
+        off += blocks[li];
+    }
+    hipLaunchKernelGGL(sf::mg_alpha_final, dim3(1), dim3(64), 0, s, part, off, numel, base, lr, rel_step, max_scale,
+                       alpha_out);
+    return last_rc();
+}
+
+int rsx_axpy_multi(int32_t count, float* const* y, const float* const* x, const int64_t* n,
+                   const double* alpha_dev, double mult, rsx_stream_t stream) {
+    if (count < 0 || count > 8 * sf::kAdamMax || !alpha_dev || (count > 0 && (!y || !x || !n))) return RSX_ERR_ARG;
+    sf::PairList lists[8];
+    int64_t blocks[8] = {0};
+    const int rc = build_pair_lists(count, y, x, n, lists, 8, blocks);
+    if (rc) return rc;
+    hipStream_t s = as_stream(stream);
+    for (int li = 0; li * sf::kAdamMax < count; ++li)
+        if (blocks[li] > 0) hipLaunchKernelGGL(sf::axpy_multi, dim3((unsigned)blocks[li]), dim3(256), 0, s, lists[li], alpha_dev, mult);
+    return last_rc();
+}
+
+int rsx_smore_unit_weights(const float* wv, const float* wt, const float* wf, int32_t d, int32_t normalize,
+                           float* out, rsx_stream_t stream) {
+    if (!wv || !wt || !wf || !out || d <= 0) return RSX_ERR_ARG;
+    const int nb = d / 2 + 1;
+    hipLaunchKernelGGL(sf::unit_w_fwd, dim3((3 * nb + 255) / 256), dim3(256), 0, as_stream(stream), wv, wt, wf, nb,
+                       normalize, out);
+    return last_rc();
+}
+
+int rsx_smore_unit_weights_bwd(const float* partials, int64_t n_blocks, const float* wv, const float* wt,
+                               const float* wf, int32_t d, int32_t normalize, float* gv, float* gt, float* gf,
+                               rsx_stream_t stream) {
+    if (!partials || n_blocks < 0 || !wv || !wt || !wf || !gv || !gt || !gf || d <= 0) return RSX_ERR_ARG;
+    const int nb = d / 2 + 1;
+    hipLaunchKernelGGL(sf::unit_w_bwd, dim3((3 * nb + 255) / 256), dim3(256), 0, as_stream(stream), partials,
+                       (int)n_blocks, wv, wt, wf, nb, normalize, gv, gt, gf);
+    return last_rc();
 }
 
 }  // extern "C"

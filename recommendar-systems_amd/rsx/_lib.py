@@ -134,6 +134,11 @@ def _declare(lib):
         "rsx_smore_infonce_fwd": (C.c_int, [P, P, P, P, I64, I64, I32, F32, P, P, C.c_size_t, P]),
         "rsx_smore_infonce_bwd": (C.c_int, [P, P, P, P, I64, I64, I32, F32, P, P, P, P, C.c_size_t, P]),
         "rsx_adam_multi": (C.c_int, [I32, P, P, P, P, P, P, F32, F32, F32, F32, F32, P]),
+        "rsx_smore_unit_weights": (C.c_int, [P, P, P, I32, I32, P, P]),
+        "rsx_mg_alpha_ws_bytes": (C.c_size_t, [I32, P]),
+        "rsx_mg_alpha": (C.c_int, [I32, P, P, P, C.c_double, C.c_double, C.c_double, C.c_double, P, P, C.c_size_t, P]),
+        "rsx_axpy_multi": (C.c_int, [I32, P, P, P, P, C.c_double, P]),
+        "rsx_smore_unit_weights_bwd": (C.c_int, [P, I64, P, P, P, I32, I32, P, P, P, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -152,7 +157,9 @@ EXPORTED = ["rsx_version", "rsx_csr_schedule_host", "rsx_spmm", "rsx_rowwise", "
             "rsx_comm_init_host",
             "rsx_comm_allreduce_f32", "rsx_sharded_lightgcn_step", "rsx_sharded_lightgcn_forward",
             "rsx_smore_gates", "rsx_smore_pref", "rsx_smore_wgrad_ws_bytes", "rsx_smore_wgrad",
-            "rsx_smore_infonce_ws_bytes", "rsx_smore_infonce_fwd", "rsx_smore_infonce_bwd", "rsx_adam_multi"]
+            "rsx_smore_infonce_ws_bytes", "rsx_smore_infonce_fwd", "rsx_smore_infonce_bwd", "rsx_adam_multi",
+            "rsx_smore_unit_weights", "rsx_smore_unit_weights_bwd", "rsx_mg_alpha_ws_bytes", "rsx_mg_alpha",
+            "rsx_axpy_multi"]
 
 
 def lib_path() -> str:

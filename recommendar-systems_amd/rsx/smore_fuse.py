@@ -248,3 +248,31 @@ def adam_multi(params, grads, exp_avgs, exp_avg_sqs, steps, lr, betas=(0.9, 0.99
     L.check(L.lib().rsx_adam_multi(n, _arr(params), _arr(grads), _arr(exp_avgs), _arr(exp_avg_sqs), _arr(steps),
                                    sizes, float(lr), float(betas[0]), float(betas[1]), float(eps),
                                    float(weight_decay), ops._stream()), "rsx_adam_multi")
+
+
+# ---------------------------------------------------------------------------
+# model-level mirror gradient
+# ---------------------------------------------------------------------------
+def mg_alpha(params, grads, base, lr, rel_step, max_scale):
+    """alpha_eff of the reference's mirror gradient (trainer.py:290-307) as a 0-d f64
+    device tensor, from one pass over the (param, grad) pairs (two launches)."""
+    n = len(params)
+    sizes = (C.c_int64 * n)(*[p.numel() for p in params])
+    lib = L.lib()
+    dev = params[0].device
+    ws = torch.empty(max(int(lib.rsx_mg_alpha_ws_bytes(n, sizes)), 16), dtype=torch.uint8, device=dev)
+    alpha = torch.empty((), dtype=torch.float64, device=dev)
+    L.check(lib.rsx_mg_alpha(n, _arr([p.detach() for p in params]), _arr(grads), sizes, float(base), float(lr),
+                             float(rel_step), float(max_scale), _p(alpha), _p(ws), ws.numel(), ops._stream()),
+            "rsx_mg_alpha")
+    return alpha
+
+
+def axpy_multi(ys, xs, alpha, mult):
+    """y += float(alpha * mult) * x for every pair (alpha: 0-d f64 device tensor)."""
+    n = len(ys)
+    if n == 0:
+        return
+    sizes = (C.c_int64 * n)(*[y.numel() for y in ys])
+    L.check(L.lib().rsx_axpy_multi(n, _arr([y.detach() for y in ys]), _arr(xs), sizes, _p(alpha), float(mult),
+                                   ops._stream()), "rsx_axpy_multi")

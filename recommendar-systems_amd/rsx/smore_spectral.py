@@ -8,8 +8,9 @@ irfft's.  Backward: one launch for the spectral part (d img, d txt, d w), then t
 projection gradients:
 d Wv = d img^T V on the split-K kernel (rsx_linear_wgrad), d V = d img Wv as a
 library GEMM, d bv = colsum.
-The unit normalisation of the complex weights (:221-229) stays a torch op on the
-(d/2+1)-sized parameters so autograd handles it exactly as the reference does.
+The unit normalisation of the complex weights (:221-229) and its backward are two
+small launches (rsx_smore_unit_weights / _bwd, which also sums the spectral
+backward's per-block weight partials) instead of ~40 torch complex-op kernels.
 """
 from __future__ import annotations
 
@@ -41,12 +42,16 @@ def _wgrad(g, x):
 
 class _Spectral(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, V, Wv, bv, T, Wt, bt, wv, wt, wf):
+    def forward(ctx, V, Wv, bv, T, Wt, bt, rv, rt, rf, normalize):
         n, dv = V.shape
         dt = T.shape[1]
         d = Wv.shape[0]
-        args = [x.contiguous() for x in (V, Wv, bv, T, Wt, bt, wv, wt, wf)]
-        V, Wv, bv, T, Wt, bt, wv, wt, wf = args
+        args = [x.contiguous() for x in (V, Wv, bv, T, Wt, bt, rv, rt, rf)]
+        V, Wv, bv, T, Wt, bt, rv, rt, rf = args
+        unit = torch.empty(3, d // 2 + 1, 2, device=V.device, dtype=torch.float32)
+        L.check(L.lib().rsx_smore_unit_weights(ops._p(rv), ops._p(rt), ops._p(rf), d, int(bool(normalize)),
+                                               ops._p(unit), ops._stream()), "rsx_smore_unit_weights")
+        wv, wt, wf = unit[0], unit[1], unit[2]
         img = torch.empty(n, d, device=V.device, dtype=torch.float32)
         txt = torch.empty_like(img)
         cv, ct, cf = torch.empty_like(img), torch.empty_like(img), torch.empty_like(img)
@@ -58,14 +63,15 @@ class _Spectral(torch.autograd.Function):
         L.check(lib.rsx_smore_spectral_fwd(p(V), dv, p(Wv), p(bv), p(T), dt, p(Wt), p(bt), p(wv), p(wt), p(wf),
                                            n, d, p(img), p(txt), p(cv), p(ct), p(cf), p(spec), p(ws), ws.numel(),
                                            ops._stream()), "rsx_smore_spectral_fwd")
-        ctx.save_for_backward(V, Wv, T, Wt, wv, wt, wf, spec)
-        ctx.nd = (n, d)
+        ctx.save_for_backward(V, Wv, T, Wt, unit, rv, rt, rf, spec)
+        ctx.nd = (n, d, int(bool(normalize)))
         return cv, ct, cf, img, txt
 
     @staticmethod
     def backward(ctx, g_cv, g_ct, g_cf, g_img_out, g_txt_out):
-        V, Wv, T, Wt, wv, wt, wf, spec = ctx.saved_tensors
-        n, d = ctx.nd
+        V, Wv, T, Wt, unit, rv, rt, rf, spec = ctx.saved_tensors
+        wv, wt, wf = unit[0], unit[1], unit[2]
+        n, d, normalize = ctx.nd
         p = ops._p
         lib = L.lib()
         gi = torch.empty(n, d, device=V.device, dtype=torch.float32)
@@ -80,7 +86,10 @@ class _Spectral(torch.autograd.Function):
             gi = gi + g_img_out
         if g_txt_out is not None:
             gt = gt + g_txt_out
-        gw = part.view(-1, 3, d // 2 + 1, 2).sum(0)
+        nb = d // 2 + 1
+        grv, grt, grf = torch.empty_like(rv), torch.empty_like(rt), torch.empty_like(rf)
+        L.check(lib.rsx_smore_unit_weights_bwd(p(part), part.numel() // (6 * nb), p(rv), p(rt), p(rf), d, normalize,
+                                               p(grv), p(grt), p(grf), ops._stream()), "rsx_smore_unit_weights_bwd")
         need = ctx.needs_input_grad
         gV = gi @ Wv if need[0] else None
         gWv = _wgrad(gi, V) if need[1] else None
@@ -88,13 +97,12 @@ class _Spectral(torch.autograd.Function):
         gT = gt @ Wt if need[3] else None
         gWt = _wgrad(gt, T) if need[4] else None
         gbt = gt.sum(0) if need[5] else None
-        return gV, gWv, gbv, gT, gWt, gbt, gw[0], gw[1], gw[2]
+        return gV, gWv, gbv, gT, gWt, gbt, grv, grt, grf, None
 
 
 def spectral(V, Wv, bv, T, Wt, bt, wv, wt, wf, normalize=True):
     """(conv_v, conv_t, conv_f, img, txt) through the fused HIP pass."""
-    return _Spectral.apply(V, Wv, bv, T, Wt, bt, unit_weight(wv, normalize), unit_weight(wt, normalize),
-                           unit_weight(wf, normalize))
+    return _Spectral.apply(V, Wv, bv, T, Wt, bt, wv, wt, wf, bool(normalize))
 
 
 def spectral_available() -> bool:

@@ -356,6 +356,17 @@ class Trainer:
             self.optimizer.zero_grad(set_to_none=True)
         except TypeError:
             self.optimizer.zero_grad()
+            self._grads_zeroed_in_place = True
+
+    def _mg_fused(self) -> bool:
+        """Mirror-gradient bookkeeping on the fused kernels (rsx_mg_alpha / rsx_axpy_multi):
+        f32 CUDA parameters and an optimizer whose zero_grad drops the tensors."""
+        from .optim import RsxAdam
+
+        if getattr(self, "_grads_zeroed_in_place", False) or not isinstance(self.optimizer, RsxAdam):
+            return False
+        ps = [p for p in self.model.parameters() if p.requires_grad]
+        return bool(ps) and all(p.is_cuda and p.dtype == torch.float32 and p.is_contiguous() for p in ps)
 
     def _mirror_gradient(self, loss_func, inter):
         """Model-level mirror gradient (reference trainer.py:268-348)."""
@@ -375,18 +386,28 @@ class Trainer:
         self._zero_grad()
         cur = loss_func(inter)
         (sum(cur) if isinstance(cur, tuple) else cur).backward()
+        fused = self._mg_fused()
         params, grads = [], []
         for p in m.parameters():
             if p.requires_grad and p.grad is not None:
                 params.append(p)
-                grads.append(p.grad.detach().clone())
+                # the fused path keeps the gradient tensors themselves: _zero_grad sets
+                # .grad to None (it never zeroes them in place), so they stay g(theta)
+                grads.append(p.grad.detach() if fused else p.grad.detach().clone())
+        base = float(getattr(m, "mg_alpha", 0.5))
         with torch.no_grad():
-            base = float(getattr(m, "mg_alpha", 0.5))
-            alpha = _mg_alpha(params, grads, base, lr, self.mg_target_rel_step, self.mg_alpha_max_scale)
-            m._alpha_eff = alpha
-            if params:
-                down = (alpha * -lr).float()  # -alpha * lr, rounded to f32 as the scalar of a f32 op
-                torch._foreach_add_(params, torch._foreach_mul(grads, down))
+            if fused and params:
+                from .smore_fuse import axpy_multi, mg_alpha
+
+                alpha = mg_alpha(params, grads, base, lr, self.mg_target_rel_step, self.mg_alpha_max_scale)
+                m._alpha_eff = alpha
+                axpy_multi(params, grads, alpha, -lr)  # theta' = theta - alpha lr g
+            else:
+                alpha = _mg_alpha(params, grads, base, lr, self.mg_target_rel_step, self.mg_alpha_max_scale)
+                m._alpha_eff = alpha
+                if params:
+                    down = (alpha * -lr).float()  # -alpha * lr, rounded to f32 as the scalar of a f32 op
+                    torch._foreach_add_(params, torch._foreach_mul(grads, down))
         self._zero_grad()
         mir = loss_func(inter)
         mirror = sum(mir) if isinstance(mir, tuple) else mir
@@ -397,7 +418,10 @@ class Trainer:
             if live:
                 torch._foreach_mul_(live, -beta)
             if params:
-                torch._foreach_add_(params, torch._foreach_mul(grads, (alpha * lr).float()))
+                if fused:
+                    axpy_multi(params, grads, alpha, lr)  # restore theta
+                else:
+                    torch._foreach_add_(params, torch._foreach_mul(grads, (alpha * lr).float()))
         self.optimizer.step()
         self._zero_grad()
         self._mg_last = (step_id, mirror.detach(), alpha)

@@ -220,3 +220,26 @@ def test_adam_multi_vs_torch(cuda):
         ob.step()
     for x, y in zip(a, b):
         np.testing.assert_allclose(y.detach().cpu().numpy(), x.detach().cpu().numpy(), rtol=0, atol=1e-6)
+
+
+def test_mg_alpha_and_axpy_vs_torch(cuda):
+    """rsx_mg_alpha (f64 sums of squares) against the trainer's torch restatement of the
+    reference's alpha (f32 norms of the concatenations): equal to f32 rounding of the
+    rms values; rsx_axpy_multi == p + g * float(alpha * mult) bit for bit."""
+    from rsx import smore_fuse as SF
+    from rsx.trainer import _mg_alpha
+
+    shapes = [(7050, 4096), (64, 64), (64,), (1, 33, 2), (19445, 64)] + [(5, 7)] * 40
+    gen = torch.Generator().manual_seed(9)
+    ps = [torch.randn(*s, generator=gen).to(cuda) * 0.1 for s in shapes]
+    gs = [torch.randn(*s, generator=gen).to(cuda) * 1e-3 for s in shapes]
+    for lr, base in ((1e-3, 0.5), (1e-1, 0.5), (1e-3, 50.0)):
+        a = SF.mg_alpha(ps, gs, base, lr, 1e-3, 20.0).item()
+        b = _mg_alpha(ps, gs, base, lr, 1e-3, 20.0).item()
+        assert abs(a - b) <= 1e-6 * abs(b), (a, b)
+    alpha = SF.mg_alpha(ps, gs, 0.5, 1e-3, 1e-3, 20.0)
+    want = [p + g * float(alpha.item() * -1e-3) for p, g in zip(ps, gs)]
+    ys = [p.clone() for p in ps]
+    SF.axpy_multi(ys, gs, alpha, -1e-3)
+    for y, w in zip(ys, want):
+        assert torch.equal(y, w)
