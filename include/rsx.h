@@ -574,12 +574,19 @@ size_t rsx_comm_unique_id_bytes(void);
 int rsx_comm_get_unique_id(void* id_host);
 int rsx_comm_init(rsx_comm_t* out, const void* id_host, int32_t rank, int32_t world);
 int rsx_comm_destroy(rsx_comm_t comm);
-/* Test hook: a communicator whose exchanges call `fn(buf, n, ctx)` on the host
- * (after synchronising the caller's stream) instead of RCCL — lets a host-side
- * collective (e.g. torch gloo) drive the sharded step with several ranks on one
- * GPU.  `fn` returns 0 on success. */
-typedef int (*rsx_host_allreduce_fn)(float* buf, int64_t n, void* ctx);
-int rsx_comm_init_host(rsx_comm_t* out, int32_t rank, int32_t world, rsx_host_allreduce_fn fn, void* ctx);
+/* Test hook: a communicator whose exchanges call `fn(op, buf, count, dtype, ctx)`
+ * on the host (after synchronising the caller's stream) instead of RCCL — lets a
+ * host-side collective (e.g. torch gloo) drive the sharded step with several ranks
+ * on one GPU.  In place on device memory `buf`:
+ *   op RSX_COLL_ALLREDUCE      buf[0, count) := sum over ranks
+ *   op RSX_COLL_ALLGATHER      buf[r count, (r+1) count) := rank r's slice, every r
+ *   op RSX_COLL_REDUCESCATTER  buf[rank count, (rank+1) count) := sum over ranks of
+ *                              that slice (buf holds world * count elements)
+ * dtype RSX_COLL_F32 / RSX_COLL_I64.  `fn` returns 0 on success. */
+enum { RSX_COLL_ALLREDUCE = 0, RSX_COLL_ALLGATHER = 1, RSX_COLL_REDUCESCATTER = 2 };
+enum { RSX_COLL_F32 = 0, RSX_COLL_I64 = 1 };
+typedef int (*rsx_host_collective_fn)(int32_t op, void* buf, int64_t count, int32_t dtype, void* ctx);
+int rsx_comm_init_host(rsx_comm_t* out, int32_t rank, int32_t world, rsx_host_collective_fn fn, void* ctx);
 /* buf[0, n) := sum over ranks, in place, ordered after the work queued on `stream`
  * and before the work queued on it afterwards. */
 int rsx_comm_allreduce_f32(rsx_comm_t comm, float* buf, int64_t n, rsx_stream_t stream);
@@ -604,6 +611,19 @@ int rsx_comm_allreduce_f32(rsx_comm_t comm, float* buf, int64_t n, rsx_stream_t 
  * then be zero between steps.  The loss is this rank's mean BPR + its regulariser; the
  * objective is the sum over ranks (data-parallel batches of `batch` per rank).
  * rsx_sharded_lightgcn_forward fills final_emb only (evaluation).
+ *
+ * Sparse exchange (union_items != NULL, K = 2 or 3 with row_tag): the step first
+ * all-gathers every rank's (pos, neg) item ids into union_items [world][2 union_cap];
+ * the last forward layer's item rows are computed only on that union (item_tag
+ * [n_items] int32, zero-filled once) and summed as a compact [world 2 batch, d]
+ * block (cbuf0), G's item rows likewise (cbuf1) — the loss reads nothing else; the
+ * item gradient t is REDUCE-SCATTERED over n_items_pad = world * ceil(n_items /
+ * world) rows (t and the item block of p, m, v padded to that; pad rows zero), each
+ * rank runs Adam on its own n_items_pad / world item rows, and the updated item
+ * rows are ALL-GATHERED back into every replica.  Per step: 2(K-1) dense
+ * all-reduces + one reduce-scatter + one all-gather of n_items*d floats (the
+ * volume of 2K-1 dense all-reduces for K = 3, against 2K+1) plus two
+ * compact all-reduces of world*2*batch rows.
  */
 typedef struct rsx_sharded_lgcn_step {
     const rsx_csr* adj_u;
@@ -636,6 +656,13 @@ typedef struct rsx_sharded_lgcn_step {
      * the regulariser gradient as per-row occurrence counts; the user rows' Adam and
      * the last item partial apply and clear them; r is not used. */
     int32_t* reg_cnt;
+    /* optional sparse exchange (see above) */
+    int64_t* union_items;       /* [world][2 union_cap] */
+    int32_t* item_tag;          /* [n_items] */
+    float* cbuf0; float* cbuf1; /* [world 2 union_cap, d] each */
+    int64_t n_items_pad;        /* rows of t and of p/m/v's item block (>= n_items) */
+    int64_t union_cap;          /* per-rank slice of union_items: 2 union_cap ids (>= batch; the
+                                 * unused tail is zero-filled, so every rank sends the same count) */
 } rsx_sharded_lgcn_step;
 
 int rsx_sharded_lightgcn_step(const rsx_sharded_lgcn_step* st, rsx_stream_t stream);

@@ -46,6 +46,8 @@ struct Rccl {
     decltype(&ncclCommInitRank) init_rank = nullptr;
     decltype(&ncclCommDestroy) destroy = nullptr;
     decltype(&ncclAllReduce) all_reduce = nullptr;
+    decltype(&ncclAllGather) all_gather = nullptr;
+    decltype(&ncclReduceScatter) reduce_scatter = nullptr;
     bool ok = false;
 };
 
@@ -60,7 +62,9 @@ const Rccl& rccl() {
         x.init_rank = reinterpret_cast<decltype(&ncclCommInitRank)>(dlsym(h, "ncclCommInitRank"));
         x.destroy = reinterpret_cast<decltype(&ncclCommDestroy)>(dlsym(h, "ncclCommDestroy"));
         x.all_reduce = reinterpret_cast<decltype(&ncclAllReduce)>(dlsym(h, "ncclAllReduce"));
-        x.ok = x.get_unique_id && x.init_rank && x.destroy && x.all_reduce;
+        x.all_gather = reinterpret_cast<decltype(&ncclAllGather)>(dlsym(h, "ncclAllGather"));
+        x.reduce_scatter = reinterpret_cast<decltype(&ncclReduceScatter)>(dlsym(h, "ncclReduceScatter"));
+        x.ok = x.get_unique_id && x.init_rank && x.destroy && x.all_reduce && x.all_gather && x.reduce_scatter;
         return x;
     }();
     return r;
@@ -79,18 +83,18 @@ struct rsx_comm_s {
     hipEvent_t join[rsx::kJoinEvents] = {};
     int next = 0;
     int32_t rank = 0, world = 1;
-    rsx_host_allreduce_fn host_fn = nullptr;  // test hook: host-side collective instead of RCCL
+    rsx_host_collective_fn host_fn = nullptr;  // test hook: host-side collective instead of RCCL
     void* host_ctx = nullptr;
 };
 
 namespace rsx {
 namespace {
 
-// In-place sum of a[0, n) over the communicator, after the work queued so far on
-// `s`; returns the join event the reader must wait on (nullptr on error, rc set).
-// A host-hook communicator synchronises `s`, calls the hook and returns an event
-// recorded on `s`.
-hipEvent_t exchange(rsx_comm_t c, float* a, int64_t n, hipStream_t s, int* rc) {
+// In-place collective `op` (RSX_COLL_*) on buf over the communicator, after the
+// work queued so far on `s`; returns the join event the reader must wait on
+// (nullptr on error, rc set).  A host-hook communicator synchronises `s`, calls the
+// hook and returns an event recorded on `s`.
+hipEvent_t collective(rsx_comm_t c, int op, void* buf, int64_t count, int dtype, hipStream_t s, int* rc) {
     hipError_t e;
     hipEvent_t j = c->join[c->next];
     c->next = (c->next + 1) % kJoinEvents;
@@ -99,7 +103,7 @@ hipEvent_t exchange(rsx_comm_t c, float* a, int64_t n, hipStream_t s, int* rc) {
             *rc = hip_rc(e);
             return nullptr;
         }
-        if (c->host_fn(a, n, c->host_ctx)) {
+        if (c->host_fn(op, buf, count, dtype, c->host_ctx)) {
             *rc = RSX_ERR_COMM;
             return nullptr;
         }
@@ -113,7 +117,14 @@ hipEvent_t exchange(rsx_comm_t c, float* a, int64_t n, hipStream_t s, int* rc) {
         *rc = hip_rc(e);
         return nullptr;
     }
-    if (rccl().all_reduce(a, a, (size_t)n, ncclFloat32, ncclSum, c->nccl, c->stream) != ncclSuccess) {
+    const ncclDataType_t ty = dtype == RSX_COLL_I64 ? ncclInt64 : ncclFloat32;
+    const size_t es = dtype == RSX_COLL_I64 ? 8 : 4;
+    char* own = static_cast<char*>(buf) + (size_t)c->rank * (size_t)count * es;
+    ncclResult_t r;
+    if (op == RSX_COLL_ALLGATHER) r = rccl().all_gather(own, buf, (size_t)count, ty, c->nccl, c->stream);
+    else if (op == RSX_COLL_REDUCESCATTER) r = rccl().reduce_scatter(buf, own, (size_t)count, ty, ncclSum, c->nccl, c->stream);
+    else r = rccl().all_reduce(buf, buf, (size_t)count, ty, ncclSum, c->nccl, c->stream);
+    if (r != ncclSuccess) {
         *rc = RSX_ERR_COMM;
         return nullptr;
     }
@@ -122,6 +133,39 @@ hipEvent_t exchange(rsx_comm_t c, float* a, int64_t n, hipStream_t s, int* rc) {
         return nullptr;
     }
     return j;
+}
+
+hipEvent_t exchange(rsx_comm_t c, float* a, int64_t n, hipStream_t s, int* rc) {
+    return collective(c, RSX_COLL_ALLREDUCE, a, n, RSX_COLL_F32, s, rc);
+}
+
+// ---- row lists of the sparse exchange -------------------------------------------
+__global__ __launch_bounds__(256) void tag_rows_k(const int64_t* ids, int64_t n, int32_t* tag_arr,
+                                                  const int32_t* tag_dev, int32_t tag) {
+    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (j < n) tag_arr[ids[j]] = tag_dev ? *tag_dev : tag;
+}
+
+// mode 0: dst[j] = src[ids[j]] (gather), 1: dst[ids[j]] = src[j] (scatter; duplicate
+// ids carry identical rows), 2: dst[ids[j]] = 0
+__global__ __launch_bounds__(256) void rows_k(const float* src, float* dst, const int64_t* ids, int64_t n, int d,
+                                              int mode) {
+    const int q = d / 4;
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= n * q) return;
+    const int64_t j = e / q;
+    const int c = (int)(e - j * q) * 4;
+    const int64_t i = ids[j];
+    if (mode == 0) st4(dst + j * d + c, ld4(src + i * d + c));
+    else if (mode == 1) st4(dst + i * d + c, ld4(src + j * d + c));
+    else st4(dst + i * d + c, f4(0.f));
+}
+
+int rows_op(const float* src, float* dst, const int64_t* ids, int64_t n, int d, int mode, hipStream_t s) {
+    if (n <= 0) return 0;
+    const int64_t tot = n * (d / 4);
+    hipLaunchKernelGGL(rows_k, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, src, dst, ids, n, d, mode);
+    return last_rc();
 }
 
 int wait(hipStream_t s, hipEvent_t j) { return hip_rc(hipStreamWaitEvent(s, j, 0)); }
@@ -218,6 +262,20 @@ int sharded_stored_layers(const rsx_sharded_lgcn_step& st, bool train, hipStream
     float* bufs[2] = {st.h0, st.h1};
     hipEvent_t joins[4] = {};
     int rc = 0;
+    // sparse exchange: the union of every rank's (pos, neg) items, gathered first
+    const bool sparse = train && st.union_items;
+    const int64_t cap = st.union_cap;
+    const int64_t nU = sparse ? (int64_t)st.comm->world * 2 * cap : 0;
+    hipEvent_t jU = nullptr;
+    if (sparse) {
+        int64_t* mine = st.union_items + (int64_t)st.comm->rank * 2 * cap;
+        RSX_TRY(hip_rc(hipMemcpyAsync(mine, st.triplets + st.batch, (size_t)(2 * st.batch) * sizeof(int64_t),
+                                      hipMemcpyDeviceToDevice, s)));
+        if (cap > st.batch)  // a partial batch: item 0 stands in (its rows come out right anyway)
+            RSX_TRY(hip_rc(hipMemsetAsync(mine + 2 * st.batch, 0, (size_t)(2 * (cap - st.batch)) * sizeof(int64_t), s)));
+        if (!(jU = collective(st.comm, RSX_COLL_ALLGATHER, st.union_items, 2 * cap, RSX_COLL_I64, s, &rc)))
+            return rc;
+    }
     // ---- forward (the first item partial's launch also tags the batch rows when training)
     const float* x = st.p;
     for (int k = 1; k < K; ++k) {
@@ -249,8 +307,25 @@ int sharded_stored_layers(const rsx_sharded_lgcn_step& st, bool train, hipStream
             e.r_add = st.h0 + off;
             e.aux = K == 3 ? st.h1 + off : nullptr;
         }
-        RSX_TRY(spmm_dispatch(*st.adj_i, x, d, e, st.slab_i, s));
-        if (!(joins[K] = exchange(st.comm, st.final_emb + off, ni * d, s, &rc))) return rc;
+        if (sparse) {  // only the union rows: tagged, computed, gathered, summed, scattered
+            RSX_TRY(wait(s, jU));
+            hipLaunchKernelGGL(tag_rows_k, dim3((unsigned)((nU + 255) / 256)), dim3(256), 0, s, st.union_items, nU,
+                               st.item_tag, st.tag_dev, tag);
+            RSX_TRY(last_rc());
+            e.row_tag = st.item_tag;
+            e.tag = tag;
+            e.tag_dev = st.tag_dev;
+            e.tag_flags = RSX_TAG_ROWS;
+            RSX_TRY(spmm_dispatch(*st.adj_i, x, d, e, st.slab_i, s));
+            RSX_TRY(rows_op(st.final_emb + off, st.cbuf0, st.union_items, nU, d, 0, s));
+            if (!(joins[K] = exchange(st.comm, st.cbuf0, nU * d, s, &rc))) return rc;
+            e.row_tag = nullptr;
+            e.tag_dev = nullptr;
+            e.tag_flags = 0;
+        } else {
+            RSX_TRY(spmm_dispatch(*st.adj_i, x, d, e, st.slab_i, s));
+            if (!(joins[K] = exchange(st.comm, st.final_emb + off, ni * d, s, &rc))) return rc;
+        }
         e.f = st.final_emb;
         e.s_in = st.p;
         e.r_add = st.h0;
@@ -263,6 +338,7 @@ int sharded_stored_layers(const rsx_sharded_lgcn_step& st, bool train, hipStream
         }
         RSX_TRY(spmm_dispatch(*st.adj_u, x, d, e, st.slab_u, s));
         RSX_TRY(wait(s, joins[K]));
+        if (sparse) RSX_TRY(rows_op(st.cbuf0, st.final_emb + off, st.union_items, nU, d, 1, s));
     }
     if (!train) return 0;
     // ---- loss: G' = dL/dfinal / (K+1), R = d reg / d ego on this rank's batch rows
@@ -277,9 +353,17 @@ int sharded_stored_layers(const rsx_sharded_lgcn_step& st, bool train, hipStream
                          (float)(K + 1)));
     // G'_I summed (R_I is not: every rank adds its own R_I to its last item partial,
     // whose exchange then sums them; one n_items*d exchange less per step)
-    hipEvent_t j0 = exchange(st.comm, st.g + off, ni * d, s, &rc);
-    if (!j0) return rc;
-    RSX_TRY(wait(s, j0));
+    if (sparse) {  // G'_I is nonzero on this rank's batch items only: sum the union rows
+        RSX_TRY(rows_op(st.g + off, st.cbuf1, st.union_items, nU, d, 0, s));
+        hipEvent_t j0 = exchange(st.comm, st.cbuf1, nU * d, s, &rc);
+        if (!j0) return rc;
+        RSX_TRY(wait(s, j0));
+        RSX_TRY(rows_op(st.cbuf1, st.g + off, st.union_items, nU, d, 1, s));
+    } else {
+        hipEvent_t j0 = exchange(st.comm, st.g + off, ni * d, s, &rc);
+        if (!j0) return rc;
+        RSX_TRY(wait(s, j0));
+    }
     // ---- backward
     x = st.g;
     for (int k = 1; k < K; ++k) {
@@ -317,7 +401,16 @@ int sharded_stored_layers(const rsx_sharded_lgcn_step& st, bool train, hipStream
             e.r_add = st.r + off;
         }
         RSX_TRY(spmm_dispatch(*st.adj_i, x, d, e, st.slab_i, s));
-        hipEvent_t jt = exchange(st.comm, st.t, ni * d, s, &rc);
+        const int64_t q = sparse ? st.n_items_pad / st.comm->world : 0;  // item rows per owner
+        hipEvent_t jt;
+        if (sparse) {
+            // G'_I and R_I live on the union rows only: cleared there, after their last reader
+            RSX_TRY(rows_op(nullptr, st.g + off, st.union_items, nU, d, 2, s));
+            if (!st.reg_cnt) RSX_TRY(rows_op(nullptr, st.r + off, st.union_items, nU, d, 2, s));
+            jt = collective(st.comm, RSX_COLL_REDUCESCATTER, st.t, q * d, RSX_COLL_F32, s, &rc);
+        } else {
+            jt = exchange(st.comm, st.t, ni * d, s, &rc);
+        }
         if (!jt) return rc;
         if (K >= 2) RSX_TRY(wait(s, joins[K - 1]));
         rsx_epilogue u = epi(RSX_EPI_ADAM);  // user rows: g = (G'_U + A_U H^{K-1}_I) + R_U
@@ -341,15 +434,32 @@ int sharded_stored_layers(const rsx_sharded_lgcn_step& st, bool train, hipStream
         u.tag_flags = RSX_TAG_SPARSE_S | RSX_TAG_SPARSE_R | RSX_TAG_ZERO;
         RSX_TRY(spmm_dispatch(*st.adj_u, x, d, u, st.slab_u, s));
         RSX_TRY(wait(s, jt));
-        rsx_epilogue a = epi(RSX_EPI_ADAM);  // item rows, identical on every rank
-        a.s_in = st.t;
-        a.p = st.p + off;
-        a.m = st.m + off;
-        a.v = st.v + off;
-        a.adam = st.adam;
-        a.zero0 = st.g + off;  // the summed G'_I and this rank's R_I: cleared densely
-        a.zero1 = st.reg_cnt ? nullptr : st.r + off;
-        RSX_TRY(rowwise_dispatch(ni, d, a, s));
+        if (sparse) {
+            // this rank's item rows [rank q, (rank+1) q) ∩ [0, n_items): Adam on the owner only,
+            // then every replica receives the updated rows
+            const int64_t r0 = (int64_t)st.comm->rank * q;
+            const int64_t nown = r0 < ni ? (ni - r0 < q ? ni - r0 : q) : 0;
+            rsx_epilogue a = epi(RSX_EPI_ADAM);
+            a.s_in = st.t + r0 * d;
+            a.p = st.p + off + r0 * d;
+            a.m = st.m + off + r0 * d;
+            a.v = st.v + off + r0 * d;
+            a.adam = st.adam;
+            if (nown > 0) RSX_TRY(rowwise_dispatch(nown, d, a, s));
+            hipEvent_t jp = collective(st.comm, RSX_COLL_ALLGATHER, st.p + off, q * d, RSX_COLL_F32, s, &rc);
+            if (!jp) return rc;
+            RSX_TRY(wait(s, jp));  // the next step (and any reader) sees every updated replica
+        } else {
+            rsx_epilogue a = epi(RSX_EPI_ADAM);  // item rows, identical on every rank
+            a.s_in = st.t;
+            a.p = st.p + off;
+            a.m = st.m + off;
+            a.v = st.v + off;
+            a.adam = st.adam;
+            a.zero0 = st.g + off;  // the summed G'_I and this rank's R_I: cleared densely
+            a.zero1 = st.reg_cnt ? nullptr : st.r + off;
+            RSX_TRY(rowwise_dispatch(ni, d, a, s));
+        }
     }
     return 0;
 }
@@ -363,6 +473,13 @@ bool valid(const rsx_sharded_lgcn_step* st) {
     if (st->n_layers >= 2 && (!st->s || !st->h0 || !st->h1)) return false;
     if (st->n_layers == 1 && !st->h0) return false;
     if ((st->adj_u->n_long > 0 && !st->slab_u) || (st->adj_i->n_long > 0 && !st->slab_i)) return false;
+    if (st->union_items) {
+        const int64_t w = st->comm->world;
+        if (!st->item_tag || !st->cbuf0 || !st->cbuf1 || st->n_items_pad < st->n_items || st->n_items_pad % w ||
+            st->union_cap < st->batch ||
+            !st->row_tag || (st->n_layers != 2 && st->n_layers != 3) || st->d % 4)
+            return false;
+    }
     return true;
 }
 
@@ -407,7 +524,7 @@ int rsx_comm_init(rsx_comm_t* out, const void* id_host, int32_t rank, int32_t wo
     return RSX_OK;
 }
 
-int rsx_comm_init_host(rsx_comm_t* out, int32_t rank, int32_t world, rsx_host_allreduce_fn fn, void* ctx) {
+int rsx_comm_init_host(rsx_comm_t* out, int32_t rank, int32_t world, rsx_host_collective_fn fn, void* ctx) {
     if (!out || !fn || world < 1 || rank < 0 || rank >= world) return RSX_ERR_ARG;
     rsx_comm_s* c = new rsx_comm_s();
     c->rank = rank;

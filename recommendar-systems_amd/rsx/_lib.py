@@ -81,10 +81,13 @@ class ShardedStep(C.Structure):
                 ("p", P), ("m", P), ("v", P), ("s", P), ("h0", P), ("h1", P), ("final_emb", P), ("g", P),
                 ("r", P), ("t", P), ("slab_u", P), ("slab_i", P), ("triplets", P), ("batch", I64),
                 ("adam", Adam), ("loss_out", P), ("loss_acc", P), ("ws", P), ("ws_bytes", C.c_size_t),
-                ("comm", P), ("row_tag", P), ("tag", I64), ("tag_dev", P), ("reg_cnt", P)]
+                ("comm", P), ("row_tag", P), ("tag", I64), ("tag_dev", P), ("reg_cnt", P),
+                ("union_items", P), ("item_tag", P), ("cbuf0", P), ("cbuf1", P), ("n_items_pad", I64), ("union_cap", I64)]
 
 
-HOST_ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, P, I64, P)
+RSX_COLL_ALLREDUCE, RSX_COLL_ALLGATHER, RSX_COLL_REDUCESCATTER = 0, 1, 2
+RSX_COLL_F32, RSX_COLL_I64 = 0, 1
+HOST_COLLECTIVE_FN = C.CFUNCTYPE(C.c_int, I32, P, I64, I32, P)
 
 
 _LIB = None
@@ -122,7 +125,7 @@ def _declare(lib):
         "rsx_comm_get_unique_id": (C.c_int, [P]),
         "rsx_comm_init": (C.c_int, [C.POINTER(P), P, I32, I32]),
         "rsx_comm_destroy": (C.c_int, [P]),
-        "rsx_comm_init_host": (C.c_int, [C.POINTER(P), I32, I32, HOST_ALLREDUCE_FN, P]),
+        "rsx_comm_init_host": (C.c_int, [C.POINTER(P), I32, I32, HOST_COLLECTIVE_FN, P]),
         "rsx_comm_allreduce_f32": (C.c_int, [P, P, I64, P]),
         "rsx_sharded_lightgcn_step": (C.c_int, [C.POINTER(ShardedStep), P]),
         "rsx_sharded_lightgcn_forward": (C.c_int, [C.POINTER(ShardedStep), P]),

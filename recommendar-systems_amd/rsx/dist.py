@@ -49,6 +49,20 @@ the last one — 2K SpMM launches + one item Adam per step instead of 2K SpMMs +
 (`_native_step`).  With a non-RCCL group
 (gloo, tests) the native step's exchanges go through a host hook
 (`rsx_comm_init_host`) so several ranks can share one GPU.
+
+Sparse exchange (`sparse=True`; by default for K = 2, 3 once the item block
+n_items * d * 4 reaches 16 MiB, RSX_SPARSE_MIN_BYTES).  The loss reads the
+final rows of the batch items only, and G = dL/dfinal is nonzero on them only:
+every rank all-gathers the (pos, neg) ids of every rank's batch (the union U,
+world * 2 * batch ids), and the last layer's item rows and G's item rows are
+summed as compact [|U|, d] blocks instead of [n_items, d].  The item gradient is
+reduce-scattered over n_items_pad = world * ceil(n_items / world) rows, each
+rank runs Adam on its own slice of item rows (its moments only there), and the
+updated slices are all-gathered into every replica.  Per K = 3 step that is 4
+dense all-reduces + 1 reduce-scatter + 1 all-gather of n_items * d floats (the
+volume of 5 all-reduces, against 7) + 2 compact all-reduces.  The Python
+sequence below states the same schedule with torch collectives (over gloo,
+reduce-scatter and all-gather are emulated with all-reduce / all_gather).
 """
 from __future__ import annotations
 
@@ -103,7 +117,7 @@ class ShardedLightGCNEngine:
     def __init__(self, train_u: np.ndarray, train_i: np.ndarray, n_users: int, n_items: int, dim: int,
                  n_layers: int, reg: float, lr: float, device, user_emb: np.ndarray, item_emb: np.ndarray,
                  seed: int = 0, batch: int = 2048, chunk: int = 32, weight_decay: float = 0.0, group=None,
-                 backend=None, native: bool | None = None):
+                 backend=None, native: bool | None = None, sparse: bool | None = None):
         if n_layers < 1:
             raise RuntimeError("sharded LightGCN needs n_layers >= 1")
         self.group = group
@@ -133,15 +147,37 @@ class ShardedLightGCNEngine:
         # replicated items: every rank starts from rank 0's item table
         it = torch.from_numpy(np.ascontiguousarray(item_emb, dtype=np.float32))
         it = self._broadcast_host(it)
-        p = torch.cat([torch.from_numpy(np.ascontiguousarray(user_emb, dtype=np.float32)), it])
-        self.p = self.be.tensor(p)
+        if sparse is None:
+            # bandwidth regime only: the sparse schedule trades 7 dense all-reduces for 4 + a
+            # reduce-scatter + an all-gather + 3 small collectives, which pays once the item
+            # block is large (C4: 1 GB) and costs latency when it is small (C2: 4.7 MB)
+            sparse = self.K in (2, 3) and ni * d * 4 >= int(os.environ.get("RSX_SPARSE_MIN_BYTES", 16 << 20))
+        self.sparse = bool(sparse)
+        if self.sparse and self.K not in (2, 3):
+            raise RuntimeError("the sparse exchange schedule is implemented for n_layers 2 and 3")
+        # item rows padded to a multiple of the world size (reduce-scatter / all-gather slices)
+        self.n_items_pad = -(-ni // self.world) * self.world
+        self.q = self.n_items_pad // self.world  # item rows per owner
+        pad = self.n_items_pad - ni
+        p = torch.cat([torch.from_numpy(np.ascontiguousarray(user_emb, dtype=np.float32)), it,
+                       torch.zeros(pad, d, dtype=torch.float32)])
+        self._p_full = self.be.tensor(p)
+        self.p = self._p_full[: nu + ni]
         if hasattr(self.be, "zeros"):
             z = lambda rows=n: self.be.zeros(rows, d)  # noqa: E731
         else:
             z = lambda rows=n: self.be.tensor(torch.zeros(rows, d, dtype=torch.float32))  # noqa: E731
         self.m, self.v, self.s, self.h0, self.h1 = z(), z(), z(), z(), z()
         self.final, self.g, self.r = z(), z(), z()
-        self.t = z(ni)
+        self.t = z(self.n_items_pad)  # pad rows stay zero
+        self.union_cap = self.batch
+        if self.sparse:
+            mk = (lambda a: self.be.tensor(a)) if not hasattr(self.be, "zeros") else \
+                (lambda a: a.to(self.be.device))  # noqa: E731
+            self.union = mk(torch.zeros(self.world * 2 * self.union_cap, dtype=torch.int64))
+            self.item_tag = mk(torch.zeros(ni, dtype=torch.int32))
+            self.cbuf0 = z(self.world * 2 * self.union_cap)
+            self.cbuf1 = z(self.world * 2 * self.union_cap)
         self.loss_acc = self.be.tensor(torch.zeros(1, dtype=torch.float64))
         self.step_count = 0
         self.sampler = self.be.sampler(tu, ti, nu, seed)
@@ -182,20 +218,20 @@ class ShardedLightGCNEngine:
                 L.check(lib.rsx_comm_init(C.byref(comm), buf, self.rank, self.world), "rsx_comm_init")
         else:
             nu = self.n_users
-            views = [self.t] + [getattr(self, k)[nu:] for k in ("h0", "h1", "final", "g", "r")]
-            self._views = {(v.data_ptr(), v.numel()): v for v in views}
+            views = [self.t, self._p_full[nu:]] + [getattr(self, k)[nu:] for k in ("h0", "h1", "final", "g", "r")]
+            if self.sparse:
+                views += [self.union, self.cbuf0, self.cbuf1]
+            self._views = {v.data_ptr(): v.view(-1) for v in views}
 
-            def host_allreduce(ptr, n, _ctx):
+            def host_collective(op, ptr, count, dtype, _ctx):
                 try:
-                    v = self._views[(ptr, n)]
-                    x = v.cpu()
-                    dist.all_reduce(x, group=self.group)
-                    v.copy_(x)
+                    v = self._views[ptr]
+                    self._host_coll(op, v, count)
                     return 0
                 except Exception:  # noqa: BLE001
                     return 1
 
-            self._host_cb = L.HOST_ALLREDUCE_FN(host_allreduce)  # kept alive with the engine
+            self._host_cb = L.HOST_COLLECTIVE_FN(host_collective)  # kept alive with the engine
             L.check(lib.rsx_comm_init_host(C.byref(comm), self.rank, self.world, self._host_cb, None),
                     "rsx_comm_init_host")
         self._comm = comm
@@ -216,6 +252,11 @@ class ShardedLightGCNEngine:
         st.ws, st.ws_bytes = self.ws.data_ptr(), self.ws.numel()
         st.comm = comm.value
         st.row_tag = self.row_tag.data_ptr() if self.row_tag is not None else None
+        st.n_items_pad = self.n_items_pad
+        st.union_cap = self.union_cap
+        if self.sparse and self.row_tag is not None:
+            st.union_items, st.item_tag = self.union.data_ptr(), self.item_tag.data_ptr()
+            st.cbuf0, st.cbuf1 = self.cbuf0.data_ptr(), self.cbuf1.data_ptr()
         # the one-launch BPR (regulariser as per-row occurrence counts, applied and
         # cleared by the user Adam layer and the last item partial), as the single engine
         self.reg_cnt = None
@@ -274,20 +315,40 @@ class ShardedLightGCNEngine:
         t = trip.contiguous()
         self._keep = t
         nb = lib.rsx_bpr_ws_bytes(B)
-        if nb > self.ws.numel():  # a given batch larger than the engine's
-            # a captured graph holds the old workspace pointer: drop it (and re-warm)
+        grow_union = self.sparse and B > self.union_cap
+        if nb > self.ws.numel() or grow_union:  # a given batch larger than the engine's
+            # a captured graph holds the old workspace pointers: drop it (and re-warm)
             # before that memory returns to the caching allocator
             if self._graph is not None:
                 torch.cuda.synchronize(self.be.device)
                 self._graph = None
             self._graph_warm = False
-            self.ws = torch.empty(nb, dtype=torch.uint8, device=self.be.device)
-            st.ws, st.ws_bytes = self.ws.data_ptr(), self.ws.numel()
+            if nb > self.ws.numel():
+                self.ws = torch.empty(nb, dtype=torch.uint8, device=self.be.device)
+                st.ws, st.ws_bytes = self.ws.data_ptr(), self.ws.numel()
+            if grow_union:  # every rank must step with the same batch size (collective counts)
+                self._grow_union(B)
         st.triplets, st.batch = t.data_ptr(), B
         self._step_dev.add_(1)
         L.check(lib.rsx_sharded_lightgcn_step(C.byref(st), ops._stream()), "rsx_sharded_lightgcn_step")
         if graph:
             self._graph_warm = True
+
+    def _grow_union(self, B):
+        """Union-exchange buffers for batches of up to B pairs per rank."""
+        self.union_cap = int(B)
+        dev = self.union.device
+        self.union = torch.zeros(self.world * 2 * B, dtype=torch.int64, device=dev)
+        self.cbuf0 = torch.zeros(self.world * 2 * B, self.d, dtype=torch.float32, device=dev)
+        self.cbuf1 = torch.zeros_like(self.cbuf0)
+        if getattr(self, "_views", None) is not None:
+            for v in (self.union, self.cbuf0, self.cbuf1):
+                self._views[v.data_ptr()] = v.view(-1)
+        if getattr(self, "_st", None) is not None:
+            st = self._st
+            st.union_cap = self.union_cap
+            st.union_items = self.union.data_ptr()
+            st.cbuf0, st.cbuf1 = self.cbuf0.data_ptr(), self.cbuf1.data_ptr()
 
     def close(self):
         """Release the rsx communicator (before destroy_process_group)."""
@@ -323,13 +384,63 @@ class ShardedLightGCNEngine:
     def _ar(self, x):
         return dist.all_reduce(x, group=self.group, async_op=True)
 
+    def _host_coll(self, op, v, count):
+        """One in-place collective on the flat tensor v (the host hook's statement of
+        RSX_COLL_*): the exchange goes through host copies over this group."""
+        w, r = self.world, self.rank
+        if op == L.RSX_COLL_ALLREDUCE:
+            x = v[:count].cpu()
+            dist.all_reduce(x, group=self.group)
+            v[:count].copy_(x)
+        elif op == L.RSX_COLL_ALLGATHER:
+            mine = v[r * count:(r + 1) * count].cpu()
+            parts = [torch.empty_like(mine) for _ in range(w)]
+            dist.all_gather(parts, mine, group=self.group)
+            v[: w * count].copy_(torch.cat(parts))
+        elif op == L.RSX_COLL_REDUCESCATTER:
+            x = v[: w * count].cpu()
+            dist.all_reduce(x, group=self.group)  # gloo has no reduce-scatter: keep this rank's slice
+            v[r * count:(r + 1) * count].copy_(x[r * count:(r + 1) * count])
+        else:
+            raise ValueError(op)
+
+    def _coll(self, op, v, count):
+        """The same collectives issued from Python on device (or CPU) tensors."""
+        if dist.get_backend(self.group) == "nccl":
+            w, r = self.world, self.rank
+            if op == L.RSX_COLL_ALLREDUCE:
+                dist.all_reduce(v[:count], group=self.group)
+            elif op == L.RSX_COLL_ALLGATHER:
+                dist.all_gather_into_tensor(v[: w * count], v[r * count:(r + 1) * count].clone(), group=self.group)
+            else:
+                out = torch.empty(count, dtype=v.dtype, device=v.device)
+                dist.reduce_scatter_tensor(out, v[: w * count], group=self.group)
+                v[r * count:(r + 1) * count].copy_(out)
+            return
+        if v.is_cuda:
+            self._host_coll(op, v, count)
+            return
+        w, r = self.world, self.rank
+        if op == L.RSX_COLL_ALLREDUCE:
+            dist.all_reduce(v[:count], group=self.group)
+        elif op == L.RSX_COLL_ALLGATHER:
+            parts = [torch.empty(count, dtype=v.dtype) for _ in range(w)]
+            dist.all_gather(parts, v[r * count:(r + 1) * count].clone(), group=self.group)
+            v[: w * count].copy_(torch.cat(parts))
+        else:
+            x = v[: w * count].clone()
+            dist.all_reduce(x, group=self.group)
+            v[r * count:(r + 1) * count].copy_(x[r * count:(r + 1) * count])
+
     # --------------------------------------------------------------- forward
-    def _propagate(self, zero_grads: bool):
+    def _propagate(self, zero_grads: bool, union=None):
         """Forward layers with every item all-reduce issued as soon as its partial
         exists: layer k+1's item partial needs only users^k (local), so it is
         computed and its exchange queued before waiting for layer k's; the comm
         stream then runs the K exchanges back to back while the compute stream
-        does the user-row SpMMs.  Per-element arithmetic = one layer at a time."""
+        does the user-row SpMMs.  Per-element arithmetic = one layer at a time.
+        `union` (sparse schedule): the last layer's item rows are summed on those
+        rows only (the final item rows elsewhere are left unsummed: nothing reads them)."""
         be, nu, ni, d, K = self.be, self.n_users, self.n_items, self.d, self.K
         p, s, f = self.p, self.s, self.final
         bufs = (self.h0, self.h1)
@@ -339,7 +450,8 @@ class ShardedLightGCNEngine:
 
         def item_partial(k):  # items^k partial = R_g^T users^{k-1}; exchange queued
             be.spmm(self.A_I, ys[k - 1], d, L.RSX_EPI_STORE, y=ys[k][nu:])
-            works[k] = self._ar(ys[k][nu:])
+            if not (union is not None and k == K):
+                works[k] = self._ar(ys[k][nu:])
 
         item_partial(1)
         for k in range(1, K + 1):
@@ -350,12 +462,20 @@ class ShardedLightGCNEngine:
             else:
                 zero = dict(zero0=self.g[:nu], zero1=self.r[:nu]) if zero_grads else {}
                 be.spmm(self.A_U, ys[k - 1], d, L.RSX_EPI_FINAL, beta=beta, f=f[:nu], s_in=s_in[:nu], **zero)
-            works.pop(k).wait()
+            if k < K or union is None:
+                works.pop(k).wait()
             if k < K:
                 be.rowwise(ni, d, L.RSX_EPI_ADD, y=s[nu:], s_in=s_in[nu:], r_add=ys[k][nu:])
-            else:
+            elif union is None:
                 zi = dict(zero0=self.g[nu:], zero1=self.r[nu:]) if zero_grads else {}
                 be.rowwise(ni, d, L.RSX_EPI_ADD, beta=beta, y=f[nu:], s_in=s_in[nu:], r_add=ys[k][nu:], **zi)
+            else:
+                cb = ys[k][nu:].index_select(0, union)
+                self._coll(L.RSX_COLL_ALLREDUCE, cb.view(-1), cb.numel())
+                f[nu:].index_copy_(0, union, ((s_in[nu:].index_select(0, union) + cb) * beta))
+                if zero_grads:
+                    self.g[nu:].zero_()
+                    self.r[nu:].zero_()
 
     def forward(self):
         if not self._fwd_valid:
@@ -384,7 +504,18 @@ class ShardedLightGCNEngine:
             self._native_step(triplets[:3])
             self._fwd_valid = False
             return
-        self._propagate(zero_grads=True)
+        union = None
+        if self.sparse:  # every rank's (pos, neg) ids, padded to the fixed slice with item 0
+            B = int(triplets.shape[1])
+            if B > self.union_cap:  # every rank must step with the same batch size
+                self._grow_union(B)
+            cap = self.union_cap
+            mine = self.union[self.rank * 2 * cap:(self.rank + 1) * 2 * cap]
+            mine.zero_()
+            mine[: 2 * B].copy_(triplets[1:3].reshape(-1))
+            self._coll(L.RSX_COLL_ALLGATHER, self.union, 2 * cap)
+            union = self.union
+        self._propagate(zero_grads=True, union=union)
         self.loss_out = be.bpr(self.final, self.p, nu, ni, triplets, self.reg, self.g, self.r, self.loss_acc)
         adam = be.adam(self.lr, self.step_count, self.wd)
         beta = 1.0 / (K + 1)
@@ -394,18 +525,26 @@ class ShardedLightGCNEngine:
         # are per-rank partials: their exchange and layer 1's item partial (which
         # needs only G's local user rows) are queued together, and so on per layer
         ys = [g] + [bufs[(k - 1) & 1] for k in range(1, K + 1)]
-        works = {0: self._ar(g[nu:])}
+        if union is not None:  # G's item rows are nonzero on the batch items only
+            cb = g[nu:].index_select(0, union)
+            self._coll(L.RSX_COLL_ALLREDUCE, cb.view(-1), cb.numel())
+            g[nu:].index_copy_(0, union, cb)
+            works = {}
+        else:
+            works = {0: self._ar(g[nu:])}
 
         def item_partial(k):
             if k < K:
                 be.spmm(self.A_I, ys[k - 1], d, L.RSX_EPI_STORE, y=ys[k][nu:])
                 works[k] = self._ar(ys[k][nu:])
             else:  # t = H_I^K/(K+1) + R_I: this rank's share of the item gradient beyond s_I/(K+1)
-                be.spmm(self.A_I, ys[k - 1], d, L.RSX_EPI_ADD, alpha=beta, y=t, r_add=r[nu:])
-                works[k] = self._ar(t)
+                be.spmm(self.A_I, ys[k - 1], d, L.RSX_EPI_ADD, alpha=beta, y=t[:ni], r_add=r[nu:])
+                if union is None:
+                    works[k] = self._ar(t[:ni])
 
         item_partial(1)
-        works.pop(0).wait()
+        if 0 in works:
+            works.pop(0).wait()
         for k in range(1, K + 1):
             s_in = g if k == 1 else s
             if k < K:
@@ -416,7 +555,18 @@ class ShardedLightGCNEngine:
             else:
                 be.spmm(self.A_U, ys[k - 1], d, L.RSX_EPI_ADAM, beta=beta, adam=adam, s_in=s_in[:nu], r_add=r[:nu],
                         p=self.p[:nu], m=self.m[:nu], v=self.v[:nu])
-                works.pop(k).wait()
-                be.rowwise(ni, d, L.RSX_EPI_ADAM, beta=beta, adam=adam, s_in=s_in[nu:], r_add=t,
-                           p=self.p[nu:], m=self.m[nu:], v=self.v[nu:])
+                if union is None:
+                    works.pop(k).wait()
+                    be.rowwise(ni, d, L.RSX_EPI_ADAM, beta=beta, adam=adam, s_in=s_in[nu:], r_add=t[:ni],
+                               p=self.p[nu:], m=self.m[nu:], v=self.v[nu:])
+                else:  # reduce-scatter the item gradient; Adam on this rank's item rows; all-gather them
+                    q = self.q
+                    self._coll(L.RSX_COLL_REDUCESCATTER, t.view(-1), q * d)
+                    r0 = self.rank * q
+                    r1 = min(ni, r0 + q)
+                    if r1 > r0:
+                        sl = slice(nu + r0, nu + r1)
+                        be.rowwise(r1 - r0, d, L.RSX_EPI_ADAM, beta=beta, adam=adam, s_in=s_in[sl],
+                                   r_add=t[r0:r1], p=self.p[sl], m=self.m[sl], v=self.v[sl])
+                    self._coll(L.RSX_COLL_ALLGATHER, self._p_full[nu:].view(-1), q * d)
         self._fwd_valid = False

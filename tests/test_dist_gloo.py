@@ -1,4 +1,4 @@
-"""Row-sharded LightGCN (rsx.dist) on 2 CPU processes over gloo.
+"""Row-sharded LightGCN (rsx.dist) on 2, 4 and 8 CPU processes over gloo.
 
 The HIP kernels cannot run here, so the engine's compute backend is replaced by
 a CPU restatement of the same C-ABI epilogue semantics (include/rsx.h); what is
@@ -129,9 +129,10 @@ def _local_graph(rank):
     return tu, ti, trip
 
 
-def _worker(rank, world, port, out_dir):
+def _worker(rank, world, port, out_dir, sparse=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(1)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from rsx.dist import ShardedLightGCNEngine
 
@@ -139,7 +140,9 @@ def _worker(rank, world, port, out_dir):
     I0 = torch.nn.init.xavier_uniform_(torch.empty(NI, D)).numpy() if rank == 0 else np.zeros((NI, D), np.float32)
     U0 = torch.nn.init.xavier_uniform_(torch.empty(NU, D), generator=torch.Generator().manual_seed(rank)).numpy()
     tu, ti, trip = _local_graph(rank)
-    eng = ShardedLightGCNEngine(tu, ti, NU, NI, D, K, REG, LR, "cpu", U0, I0, backend=CpuBackend())
+    eng = ShardedLightGCNEngine(tu, ti, NU, NI, D, K, REG, LR, "cpu", U0, I0, backend=CpuBackend(), batch=32,
+                                sparse=sparse)
+    assert eng.sparse == sparse
     f0 = eng.forward().clone()
     eng.step(triplets=torch.from_numpy(trip))
     np.savez(os.path.join(out_dir, f"r{rank}.npz"), p=eng.p.numpy(), f0=f0.numpy(), U0=U0,
@@ -155,10 +158,12 @@ def _free_port():
     return p
 
 
-def test_sharded_step_matches_global_objective():
-    world = 2
+@pytest.mark.parametrize("world,sparse", [(2, False), (2, True), (4, True), (8, True), (8, False)])
+def test_sharded_step_matches_global_objective(world, sparse):
+    """sparse: the union-row exchange of the last layer / G's item rows and the
+    reduce-scatter + owner Adam + all-gather of the item gradient (rsx/dist.py)."""
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(world, _free_port(), d), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, _free_port(), d, sparse), nprocs=world, join=True)
         res = [dict(np.load(os.path.join(d, f"r{r}.npz"))) for r in range(world)]
     # global graph: users of rank g offset by g*NU
     gu, gi, trips = [], [], []
@@ -192,5 +197,6 @@ def test_sharded_step_matches_global_objective():
         np.testing.assert_allclose(p[:NU], u.detach().numpy()[r * NU:(r + 1) * NU], rtol=0, atol=2e-6)
         np.testing.assert_allclose(p[NU:], i.detach().numpy(), rtol=0, atol=2e-6)
     # item replicas stay identical
-    assert np.array_equal(res[0]["p"][NU:], res[1]["p"][NU:])
+    for r in range(1, world):
+        assert np.array_equal(res[0]["p"][NU:], res[r]["p"][NU:])
     assert abs(sum(float(x["loss"][0]) for x in res) - loss.item()) < 1e-5

@@ -17,7 +17,7 @@ from test_dist_gloo import D, K, LR, NI, NU, REG, _local_graph
 pytestmark = pytest.mark.gpu
 
 
-def _worker(rank, world, port, out_dir, native):
+def _worker(rank, world, port, out_dir, native, sparse):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -28,8 +28,9 @@ def _worker(rank, world, port, out_dir, native):
     U0 = torch.nn.init.xavier_uniform_(torch.empty(NU, D), generator=torch.Generator().manual_seed(rank)).numpy()
     tu, ti, trip = _local_graph(rank)
     # native: csrc/dist.hip's one-call step, its exchanges through the host hook (gloo)
-    eng = ShardedLightGCNEngine(tu, ti, NU, NI, D, K, REG, LR, "cuda:0", U0, I0, batch=16, native=native)
-    assert eng.native == native
+    eng = ShardedLightGCNEngine(tu, ti, NU, NI, D, K, REG, LR, "cuda:0", U0, I0, batch=16, native=native,
+                                sparse=sparse)
+    assert eng.native == native and eng.sparse == sparse
     f0 = eng.forward().cpu().clone()
     eng.step(triplets=torch.from_numpy(trip).cuda())
     p1 = eng.p.cpu().numpy()
@@ -50,11 +51,13 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("native", [False, True])
-def test_sharded_hip_step_matches_global_objective(native):
+@pytest.mark.parametrize("native,sparse", [(False, False), (True, False), (False, True), (True, True)])
+def test_sharded_hip_step_matches_global_objective(native, sparse):
+    """sparse: the union-row exchange + reduce-scatter / owner Adam / all-gather schedule
+    (csrc/dist.hip with the host hook's collectives when native)."""
     world = 2
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(world, _free_port(), d, native), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, _free_port(), d, native, sparse), nprocs=world, join=True)
         res = [dict(np.load(os.path.join(d, f"r{r}.npz"))) for r in range(world)]
     gu, gi, trips = [], [], []
     for r in range(world):
@@ -88,6 +91,9 @@ def test_sharded_hip_step_matches_global_objective(native):
     assert np.isfinite(res[0]["after"]).all()
 
 
+SPARSE = True  # the one-rank RCCL run exercises the sparse schedule's collectives (all-gather, reduce-scatter)
+
+
 def _native_worker(rank, world, port, out_dir):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -102,7 +108,7 @@ def _native_worker(rank, world, port, out_dir):
     res = {}
     for native in ("graph", True, False):
         eng = ShardedLightGCNEngine(tu, ti, NU, NI, D, K, REG, LR, "cuda:0", U0, I0, batch=16,
-                                    native=bool(native))
+                                    native=bool(native), sparse=SPARSE)
         assert eng.native == bool(native)
         if native is True:
             eng.use_graph = False  # the eagerly issued native step

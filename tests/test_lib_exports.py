@@ -32,9 +32,9 @@ def test_struct_layouts_match_header():
     assert C.sizeof(L.Csr) == 8 * 3 + 8 * 3 + 4 * 2 + 8 + 8 + 8 + 8 + 8
     assert C.sizeof(L.Adam) == 4 * 6 + 8 + 8
     assert C.sizeof(L.Epilogue) == 4 * 4 + 8 * 14 + C.sizeof(L.Adam) + 8 + 4 + 4 + 8 + 8 + 8
-    # gcc on include/rsx.h: sizeof(rsx_lgcn_step) = 240, sizeof(rsx_sharded_lgcn_step) = 272
+    # gcc on include/rsx.h: sizeof(rsx_lgcn_step) = 240, sizeof(rsx_sharded_lgcn_step) = 320
     assert C.sizeof(L.LgcnStep) == 240
-    assert C.sizeof(L.ShardedStep) == 272
+    assert C.sizeof(L.ShardedStep) == 320
 
 
 def test_comm_unique_id_size():
