@@ -112,6 +112,10 @@ class TopKEvaluator:
             return self.evaluate_device(topk, eval_data)
         return self.evaluate_arrays(topk.cpu().numpy(), eval_data.get_eval_items(), eval_data.get_eval_len_list())
 
+    def evaluate_sharded(self, pos, topk, eval_data) -> dict:
+        """A user-sharded evaluation's dict (sharded_metric_dict: sums all-gathered)."""
+        return sharded_metric_dict(pos, topk, eval_data, self.metrics, self.topk)
+
     def evaluate_device(self, topk, eval_data) -> dict:
         """The same dict from device-resident top-k lists (device_metric_dict)."""
         erp, ecol = eval_data.eval_csr()
@@ -187,3 +191,54 @@ def _gain(k: int, device):
         ranks = np.arange(1, k + 1, dtype=np.float64)
         g = _GAIN[key] = torch.from_numpy(1.0 / np.log2(ranks + 1)).to(device)
     return g
+
+
+def _collect(t):
+    """all_gather of a small float64 tensor; returns the per-rank tensors on the host, in rank order."""
+    import torch
+    import torch.distributed as dist
+
+    x = t if dist.get_backend() == "nccl" else t.cpu()
+    parts = [torch.empty_like(x) for _ in range(dist.get_world_size())]
+    dist.all_gather(parts, x)
+    return [q.cpu() for q in parts]
+
+
+def sharded_metric_dict(pos, topk, eval_data, metrics, topk_list) -> dict:
+    """The metric dict of a user-sharded evaluation: this rank ranked the evaluation
+    users at positions `pos` of eval_data's user list (top-k rows `topk`).  Each rank
+    sums its users' per-user values in user order (rsx_topk_metrics), the [5, n_cut]
+    sums are all-gathered and added in rank order, then divided by the global user
+    count (and |held-out items| for recall2) and rounded as the reference does."""
+    import torch
+
+    from . import ops
+
+    erp, ecol = eval_data.eval_csr()
+    cache = getattr(eval_data, "_shard_csr", None)
+    if cache is None or cache[0] is not pos and not torch.equal(cache[0], pos):
+        lens = (erp[1:] - erp[:-1]).index_select(0, pos)
+        rp = torch.zeros(pos.numel() + 1, dtype=torch.int64, device=erp.device)
+        rp[1:] = torch.cumsum(lens, 0)
+        starts = erp[:-1].index_select(0, pos)
+        seg = torch.repeat_interleave(torch.arange(pos.numel(), device=erp.device), lens)
+        idx = starts.index_select(0, seg) + (torch.arange(int(rp[-1].item()), device=erp.device) - rp[:-1].index_select(0, seg))
+        cache = eval_data._shard_csr = (pos, rp, ecol.index_select(0, idx).contiguous())
+    _, rp, col = cache
+    k = topk.shape[1]
+    cuts = sorted(set(int(c) for c in topk_list))
+    sums = ops.topk_metrics(topk.contiguous(), rp, col, cuts, _gain(k, topk.device), exact=True)
+    tot = None
+    for part in _collect(sums):
+        tot = part.clone() if tot is None else tot + part
+    s = tot.numpy()
+    n = int(eval_data.eval_u.numel())
+    pos_total = int(np.asarray(eval_data.get_eval_len_list()).sum())
+    rows = {"recall": 0, "precision": 1, "ndcg": 2, "map": 3, "recall2": 4}
+    col_of = {c: j for j, c in enumerate(cuts)}
+    out = {}
+    for m in metrics:
+        for kk in topk_list:
+            den = pos_total if m == "recall2" else n
+            out[f"{m}@{kk}"] = float(np.round(s[rows[m], col_of[int(kk)]] / den, 4))
+    return out

@@ -15,6 +15,19 @@ below update the same storage:
   torch optimizer works unchanged;
 * fused path (`fused_step`): one `rsx_lightgcn_step` call per batch, Adam in
   the last backward SpMM's epilogue (used by rsx.trainer.Trainer).
+
+Sharded (torch.distributed initialised with world > 1, e.g. `torchrun
+--nproc-per-node 8 main.py -m LightGCN -d sports`, or config `rsx_sharded: True`):
+rank r owns the contiguous user block [r N/W, (r+1) N/W) and a
+rsx.dist.ShardedLightGCNEngine (items replicated).  The initial
+tables are the reference's (every rank draws the full xavier tables from the
+same seed and keeps its users), the parameters are the local user block and the
+item replica.  Training is data-parallel over the user shards: every rank samples
+its own users' interactions on the device (`fused_step_index`, the same number of
+batches per epoch on every rank: the largest shard's, smaller shards wrap
+around) and the step minimises the sum of the ranks' reference losses.
+Evaluation ranks each rank's own evaluation users against all items
+(`full_sort_topk_local`); rsx.trainer all-gathers the metric sums.
 """
 from __future__ import annotations
 
@@ -28,6 +41,14 @@ from . import _lib as L
 from . import ops
 from .engine import LightGCNEngine
 from .recommender import GeneralRecommender
+
+
+def _world():
+    import torch.distributed as dist
+
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_world_size(), dist.get_rank()
+    return 1, 0
 
 
 def propagate_mean(engine, x: torch.Tensor) -> torch.Tensor:
@@ -92,6 +113,11 @@ class LightGCN(GeneralRecommender):
         i0 = nn.init.xavier_uniform_(torch.empty(self.n_items, self.latent_dim))
         im = self.interaction_matrix
         wd = config["weight_decay"] or 0.0
+        world, rank = _world()
+        self.sharded = world > 1 or bool(config["rsx_sharded"])
+        if self.sharded:
+            self._init_sharded(config, im, u0, i0, world, rank, float(wd))
+            return
         self.engine = LightGCNEngine(im.row.astype(np.int64), im.col.astype(np.int64), self.n_users, self.n_items,
                                      self.latent_dim, self.n_layers, self.reg_weight,
                                      lr=config["learning_rate"] or 1e-3, device=self.device, user_emb=u0.numpy(),
@@ -102,6 +128,34 @@ class LightGCN(GeneralRecommender):
         self.embedding_dict = nn.ParameterDict({
             "user_emb": nn.Parameter(self.engine.p[:nu]),
             "item_emb": nn.Parameter(self.engine.p[nu:]),
+        })
+
+    def _init_sharded(self, config, im, u0, i0, world, rank, wd):
+        import torch.distributed as dist
+
+        from .dist import ShardedLightGCNEngine
+
+        nu = self.n_users
+        a, b = rank * nu // world, (rank + 1) * nu // world
+        self.user_range = (a, b)
+        rows, cols = im.row.astype(np.int64), im.col.astype(np.int64)
+        sel = (rows >= a) & (rows < b)
+        B = int(config["train_batch_size"])
+        self.engine = ShardedLightGCNEngine(rows[sel] - a, cols[sel], b - a, self.n_items, self.latent_dim,
+                                            self.n_layers, self.reg_weight, lr=config["learning_rate"] or 1e-3,
+                                            device=self.device, user_emb=u0.numpy()[a:b], item_emb=i0.numpy(),
+                                            seed=int(config["seed"] or 0) + rank, batch=B,
+                                            chunk=int(config["rsx_chunk"] or 32), weight_decay=wd)
+        nb = torch.tensor([-(-self.engine.n_inter // B)], dtype=torch.int64)
+        if dist.get_backend() == "nccl":
+            nb = nb.to(self.device)
+        dist.all_reduce(nb, op=dist.ReduceOp.MAX)
+        self.steps_per_epoch = int(nb.item())
+        self._local_batches = max(1, -(-self.engine.n_inter // B))
+        nl = b - a
+        self.embedding_dict = nn.ParameterDict({
+            "user_emb": nn.Parameter(self.engine.p[:nl]),
+            "item_emb": nn.Parameter(self.engine.p[nl:]),
         })
 
     # -- reference API -----------------------------------------------------------
@@ -117,6 +171,8 @@ class LightGCN(GeneralRecommender):
         return final[: self.n_users], final[self.n_users:]
 
     def calculate_loss(self, interaction):
+        if self.sharded:
+            raise NotImplementedError("the sharded LightGCN trains through fused_step_index (rsx.trainer's fused path)")
         self.engine.invalidate()
         final = _Propagate.apply(self.embedding_dict["user_emb"], self.embedding_dict["item_emb"], self.engine)
         return _BprLoss.apply(final, self.embedding_dict["user_emb"], self.embedding_dict["item_emb"],
@@ -128,13 +184,35 @@ class LightGCN(GeneralRecommender):
             return self.engine.forward()
 
     def full_sort_predict(self, interaction):
+        if self.sharded:
+            raise NotImplementedError("the sharded LightGCN evaluates through full_sort_topk_local")
         f = self._final()
         return ops.score_dense(f[: self.n_users], interaction[0].contiguous(), f[self.n_users:])
 
     # -- rsx fast paths ----------------------------------------------------------
     def fused_step(self, interaction, lr: float):
+        if self.sharded:
+            raise NotImplementedError("the sharded LightGCN samples on the device: fused_step_index")
         self.engine.set_lr(lr)
         self.engine.step(triplets=interaction)
+
+    def fused_step_index(self, epoch: int, i: int, lr: float):
+        """Sharded training: this rank's batch i of `epoch` from its device sampler
+        (i modulo its own batch count: every rank runs steps_per_epoch batches)."""
+        self.engine.lr = float(lr)
+        B = self.engine.batch
+        self.engine.step(epoch=epoch, start=(i % self._local_batches) * B)
+
+    def full_sort_topk_local(self, eval_users: torch.Tensor, k: int, eval_data):
+        """(row positions in eval_users, top-k item ids) for this rank's evaluation users
+        (global ids in [user_range)), ranked against every item with the training mask."""
+        a, b = self.user_range
+        pos = torch.nonzero((eval_users >= a) & (eval_users < b)).flatten()
+        local = (eval_users.index_select(0, pos) - a).contiguous()
+        f = self._final()
+        nl = b - a
+        _, topk = ops.fullsort_topk(f[:nl], local, f[nl:], eval_data.mask_rowptr[a:], eval_data.mask_col, k)
+        return pos, topk
 
     def full_sort_topk(self, interaction, k: int, eval_data):
         f = self._final()

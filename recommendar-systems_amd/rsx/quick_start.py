@@ -16,11 +16,31 @@ from .logger import init_logger
 from .utils import dict2str, get_model, get_trainer, init_seed
 
 
+def _init_distributed(config):
+    """torchrun (WORLD_SIZE > 1): one process per GPU, a process group over RCCL
+    ("nccl"; config rsx_dist_backend overrides, e.g. gloo for several ranks on one
+    GPU); the user-sharded LightGCN picks it up (rsx.lightgcn)."""
+    import torch
+    import torch.distributed as dist
+
+    if int(os.environ.get("WORLD_SIZE", "1")) <= 1 or dist.is_initialized():
+        return
+    backend = config["rsx_dist_backend"] or "nccl"
+    dev = config["device"]
+    if dev.type == "cuda":
+        torch.cuda.set_device(dev)
+    kw = {"device_id": dev} if backend == "nccl" else {}
+    dist.init_process_group(backend, **kw)
+
+
 def quick_start(model, dataset, config_dict, save_model=True, mg=False, log=True):
     config = Config(model, dataset, config_dict, mg)
+    _init_distributed(config)
     if log:
         init_logger(config)
     logger = getLogger()
+    if int(os.environ.get("RANK", "0")) != 0:  # one log per job: rank 0's
+        logger.setLevel("WARNING")
     logger.info("██Server: \t" + platform.node())
     logger.info("██Dir: \t" + os.getcwd() + "\n")
     logger.info(config)

@@ -252,10 +252,22 @@ class Trainer:
         acc.zero_()
         lr = self.current_lr()
         n = 0
-        for batch in train_data:
-            self.model.fused_step(batch, lr)
-            n += 1
-        total = float(acc.item())  # one host sync per epoch
+        if getattr(self.model, "sharded", False):
+            # user-sharded model (torchrun): every rank runs the same number of steps on its
+            # own users' device-sampled batches; the epoch loss is the sum over ranks
+            import torch.distributed as dist
+
+            for i in range(self.model.steps_per_epoch):
+                self.model.fused_step_index(epoch_idx, i, lr)
+                n += 1
+            tot = acc.clone() if dist.get_backend() == "nccl" else acc.cpu()
+            dist.all_reduce(tot)
+            total = float(tot.item())
+        else:
+            for batch in train_data:
+                self.model.fused_step(batch, lr)
+                n += 1
+            total = float(acc.item())  # one host sync per epoch
         if np.isnan(total):
             self.logger.info(f"Loss is nan at epoch: {epoch_idx}. Exiting.")
             return torch.tensor(float("nan")), torch.tensor(0.0)
@@ -491,6 +503,10 @@ class Trainer:
         self.model.eval()
         k = max(self.config["topk"])
         mats = []
+        if getattr(self.model, "sharded", False):
+            # each rank ranks its own evaluation users; the metric sums are all-gathered
+            pos, topk = self.model.full_sort_topk_local(eval_data.eval_u, k, eval_data)
+            return self.evaluator.evaluate_sharded(pos, topk, eval_data)
         fused = hasattr(self.model, "full_sort_topk") and hasattr(eval_data, "mask_rowptr")
         if fused:
             # one fused launch over every evaluation user: the score matrix is never
