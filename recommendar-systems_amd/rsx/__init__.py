@@ -6,3 +6,5 @@ the reference's `GeneralRecommender` / `Trainer` / YAML surface
 (reference `src/common/abstract_recommender.py`, `src/common/trainer.py`).
 """
 __version__ = "0.1.0"
+
+from . import torch_ops  # noqa: E402,F401  registers torch.ops.rsx.* (SURVEY 8(b)2)
