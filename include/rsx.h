@@ -550,6 +550,24 @@ int rsx_adam_multi(int32_t count, float* const* p, const float* const* g, float*
                    float weight_decay, rsx_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
+/* SMORE kNN item graph (knn.hip)                                             */
+/* ------------------------------------------------------------------------ */
+/*
+ * build_sim + build_knn_normalized_graph(sparse, 'sym') (reference
+ * src/utils/utils.py:134-181, called at src/models/smore.py:58-61,69-71) from the
+ * raw feature table feat [n, f] f32 (device): rows L2-normalised (x / ||x||), the
+ * cosine similarities on f32 MFMA with the per-row top-k kept in registers (the
+ * n x n matrix is never formed), k <= 32:
+ *   vals [n, k]    kept similarities, (value desc, index asc) per row (self included)
+ *   idx  [n, k]    int64 neighbour ids
+ *   weights [n, k] d_r^-1/2 * v * d_c^-1/2, d = the row's kept-value sum (inf -> 0)
+ * Workspace rsx_knn_ws_bytes(n, f) (the normalised table).
+ */
+size_t rsx_knn_ws_bytes(int64_t n, int32_t f);
+int rsx_knn_graph(const float* feat, int64_t n, int32_t f, int32_t k, float* vals, int64_t* idx, float* weights,
+                  void* ws, size_t ws_bytes, rsx_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
 /* Row-sharded LightGCN over RCCL (one process per GPU)                       */
 /* ------------------------------------------------------------------------ */
 /*

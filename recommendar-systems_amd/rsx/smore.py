@@ -102,31 +102,28 @@ def knn_graph(feat: np.ndarray, k: int):
     return r.numpy().astype(np.int64), c.numpy().astype(np.int64), w.numpy().astype(np.float32)
 
 
-def knn_graph_device(feat: torch.Tensor, k: int, chunk_bytes: int = 1 << 30):
-    """build_sim + build_knn_normalized_graph(sparse, 'sym') on the device: the dense
-    cosine similarity as a library GEMM (MFMA) in row chunks of <= chunk_bytes (2.1
-    GB for all of Amazon-clothing: nothing at 288 GB of HBM), torch.topk per row, and
-    the sym-norm in the reference's CPU order (deg = the row's kept values added in
-    rank order, as its index_add over row-major edges; 1/sqrt(deg), ATen's pow(-0.5);
-    (d_r * v) * d_c).  The similarities are GPU GEMM sums, so values can differ from
-    the CPU build in the last bits and neighbours at exact near-ties can swap
-    (tests/test_gpu_smore.py pins that).  Returns host (rows, cols, vals) like knn_graph."""
-    x = feat.to(torch.float32)
-    xn = x.div(torch.norm(x, p=2, dim=-1, keepdim=True))
-    n = xn.shape[0]
-    step = max(1, chunk_bytes // (4 * max(n, 1)))
-    vs, ids = [], []
-    for s in range(0, n, step):
-        v, i = torch.topk(xn[s:s + step] @ xn.t(), k, dim=-1)
-        vs.append(v)
-        ids.append(i)
-    v, i = torch.cat(vs), torch.cat(ids)
-    deg = v[:, 0].clone()
-    for j in range(1, k):
-        deg = deg + v[:, j]
-    dis = 1.0 / torch.sqrt(deg)
-    dis = torch.where(torch.isinf(dis), torch.zeros_like(dis), dis)
-    w = dis[:, None] * v * dis[i]
+def knn_graph_device(feat: torch.Tensor, k: int):
+    """build_sim + build_knn_normalized_graph(sparse, 'sym') on the device through the
+    hand-written builder rsx_knn_graph (csrc/knn.hip: row normalisation, the cosine
+    similarities on f32 MFMA with the per-row top-k kept in registers — the n x n
+    matrix is never formed — and the sym-norm in the reference's order: deg = the
+    row's kept values added in rank order, 1/sqrt(deg), (d_r * v) * d_c).  The
+    similarities are f32 MFMA sums, so values can differ from the CPU build in the
+    last bits and neighbours at exact near-ties can swap (tests/test_gpu_smore.py
+    pins that).  Returns host (rows, cols, vals) like knn_graph."""
+    import ctypes as C
+
+    x = feat.detach().to(torch.float32).contiguous()
+    n, f = x.shape
+    if k > 32 or k > n:
+        raise ValueError(f"rsx_knn_graph: k = {k} (supported: k <= 32 and k <= n = {n})")
+    lib = L.lib()
+    v = torch.empty(n, k, dtype=torch.float32, device=x.device)
+    i = torch.empty(n, k, dtype=torch.int64, device=x.device)
+    w = torch.empty(n, k, dtype=torch.float32, device=x.device)
+    ws = torch.empty(max(int(lib.rsx_knn_ws_bytes(n, f)), 4), dtype=torch.uint8, device=x.device)
+    L.check(lib.rsx_knn_graph(ops._p(x), n, f, k, ops._p(v), ops._p(i), ops._p(w), ops._p(ws), ws.numel(),
+                              ops._stream()), "rsx_knn_graph")
     r = np.repeat(np.arange(n, dtype=np.int64), k)
     return r, i.reshape(-1).cpu().numpy().astype(np.int64), w.reshape(-1).cpu().numpy().astype(np.float32)
 

@@ -270,7 +270,7 @@ def test_rsx_adam_matches_torch_single_tensor(cuda):
         np.testing.assert_allclose(y.detach().cpu().numpy(), x.detach().cpu().numpy(), rtol=0, atol=1e-6)
 
 
-@pytest.mark.parametrize("src", ["golden_image", "golden_text", "random"])
+@pytest.mark.parametrize("src", ["golden_image", "golden_text", "random", "wide", "ragged"])
 def test_knn_graph_device_vs_host(cuda, golden, src):
     """SMORE's kNN item graph built on the device (GEMM + topk + sym-norm) against the
     CPU restatement of the reference's build (knn_graph, pinned bit for bit to the
@@ -283,6 +283,12 @@ def test_knn_graph_device_vs_host(cuda, golden, src):
     if src == "random":
         f = np.random.default_rng(3).standard_normal((1500, 768)).astype(np.float32)
         k = 20
+    elif src == "wide":  # baby's raw image width, several 256-row panels and 128-row blocks
+        f = np.random.default_rng(4).standard_normal((2000, 4096)).astype(np.float32)
+        k = 20
+    elif src == "ragged":  # features not a multiple of the 32-wide chunk, the largest k
+        f = np.random.default_rng(5).standard_normal((777, 100)).astype(np.float32)
+        k = 32
     else:
         z = golden("smore_small")
         f = z["v_feat" if src == "golden_image" else "t_feat"].astype(np.float32)
