@@ -568,6 +568,39 @@ int rsx_knn_graph(const float* feat, int64_t n, int32_t f, int32_t k, float* val
                   void* ws, size_t ws_bytes, rsx_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
+/* Graph builders on the device (graph.hip)                                   */
+/* ------------------------------------------------------------------------ */
+/*
+ * rsx_adj_build: the normalised symmetric user-item adjacency from the interaction
+ * list (u, i) [n_edges] int64 (duplicates collapse), CSR over n = n_users + n_items
+ * rows (users first, item column ids offset by n_users), columns sorted per row:
+ *   mode 0  LightGCN / LayerGCN eval graph (src/models/lightgcn.py:65-103):
+ *           (d_r + 1e-7)^-1/2 (d_c + 1e-7)^-1/2 in float64, cast to float32;
+ *   mode 1  SMORE (src/models/smore.py:176-207): float32 d^-1/2, inf -> 0, d_r*1*d_c
+ *           (d^-1/2 correctly rounded from float64; the reference's numpy float32
+ *           power is a vectorised <= 1-ulp powf, so rsx.ops.adj_build re-derives the
+ *           n per-node factors with numpy for bit equality).
+ * rowptr [n+1]; col, val have capacity 2 n_edges (nnz = rowptr[n], twice the number
+ * of distinct pairs).  Workspace rsx_adj_build_ws_bytes.
+ *
+ * rsx_edge_dropout_build: LayerGCN's per-epoch graph (src/models/layergcn.py:51-81)
+ * from the kept-edge mask keep [n_edges] (uint8) over the training edges (e_u, e_i)
+ * and the symmetric template of all edges sorted by (row, col) (t_rowptr [n+1],
+ * t_col [2 n_edges], t_eid [2 n_edges]: the edge each entry comes from): values
+ * float32 1/sqrt(1e-7 + kept degree) products, the kept entries compacted in order.
+ * rowptr [n+1]; col, val capacity 2 n_edges.
+ */
+size_t rsx_adj_build_ws_bytes(int64_t n_edges, int64_t n_users, int64_t n_items);
+int rsx_adj_build(const int64_t* u, const int64_t* i, int64_t n_edges, int64_t n_users, int64_t n_items,
+                  int32_t mode, int64_t* rowptr, int32_t* col, float* val, void* ws, size_t ws_bytes,
+                  rsx_stream_t stream);
+size_t rsx_edge_dropout_ws_bytes(int64_t n_edges, int64_t n_users, int64_t n_items);
+int rsx_edge_dropout_build(const int64_t* e_u, const int64_t* e_i, const uint8_t* keep, int64_t n_edges,
+                           int64_t n_users, int64_t n_items, const int64_t* t_rowptr, const int32_t* t_col,
+                           const int64_t* t_eid, int64_t* rowptr, int32_t* col, float* val, void* ws,
+                           size_t ws_bytes, rsx_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
 /* Row-sharded LightGCN over RCCL (one process per GPU)                       */
 /* ------------------------------------------------------------------------ */
 /*

@@ -143,6 +143,10 @@ def _declare(lib):
         "rsx_axpy_multi": (C.c_int, [I32, P, P, P, P, C.c_double, P]),
         "rsx_knn_ws_bytes": (C.c_size_t, [I64, I32]),
         "rsx_knn_graph": (C.c_int, [P, I64, I32, I32, P, P, P, P, C.c_size_t, P]),
+        "rsx_adj_build_ws_bytes": (C.c_size_t, [I64, I64, I64]),
+        "rsx_adj_build": (C.c_int, [P, P, I64, I64, I64, I32, P, P, P, P, C.c_size_t, P]),
+        "rsx_edge_dropout_ws_bytes": (C.c_size_t, [I64, I64, I64]),
+        "rsx_edge_dropout_build": (C.c_int, [P, P, P, I64, I64, I64, P, P, P, P, P, P, P, C.c_size_t, P]),
         "rsx_smore_unit_weights_bwd": (C.c_int, [P, I64, P, P, P, I32, I32, P, P, P, P]),
     }
     for name, (res, args) in sig.items():
@@ -164,7 +168,8 @@ EXPORTED = ["rsx_version", "rsx_csr_schedule_host", "rsx_spmm", "rsx_rowwise", "
             "rsx_smore_gates", "rsx_smore_pref", "rsx_smore_wgrad_ws_bytes", "rsx_smore_wgrad",
             "rsx_smore_infonce_ws_bytes", "rsx_smore_infonce_fwd", "rsx_smore_infonce_bwd", "rsx_adam_multi",
             "rsx_smore_unit_weights", "rsx_smore_unit_weights_bwd", "rsx_mg_alpha_ws_bytes", "rsx_mg_alpha",
-            "rsx_axpy_multi", "rsx_knn_ws_bytes", "rsx_knn_graph"]
+            "rsx_axpy_multi", "rsx_knn_ws_bytes", "rsx_knn_graph", "rsx_adj_build_ws_bytes", "rsx_adj_build",
+            "rsx_edge_dropout_ws_bytes", "rsx_edge_dropout_build"]
 
 
 def lib_path() -> str:

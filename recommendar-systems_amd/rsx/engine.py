@@ -21,6 +21,18 @@ from . import _lib as L
 from . import graph, ops
 
 
+def lightgcn_adj(train_u, train_i, n_users: int, n_items: int, device, chunk: int = 32) -> "ops.DeviceCSR":
+    """The normalised adjacency (reference lightgcn.py:65-103) built on the device
+    (rsx_adj_build, csrc/graph.hip; bit-equal to graph.lightgcn_norm_adj, which
+    RSX_GRAPH_BUILDER=host selects)."""
+    n = n_users + n_items
+    if os.environ.get("RSX_GRAPH_BUILDER", "device") == "host":
+        rp, col, val = graph.lightgcn_norm_adj(train_u, train_i, n_users, n_items)
+        return ops.DeviceCSR(rp, col, val, n, device, chunk)
+    rp, col, val = ops.adj_build(train_u, train_i, n_users, n_items, ops.ADJ_LIGHTGCN, device)
+    return ops.DeviceCSR.from_device(rp, col, val, n, chunk)
+
+
 class LightGCNEngine:
     def __init__(self, train_u: np.ndarray, train_i: np.ndarray, n_users: int, n_items: int, dim: int,
                  n_layers: int, reg: float, lr: float, device, user_emb: np.ndarray | None = None,
@@ -31,8 +43,7 @@ class LightGCNEngine:
         self.reg, self.lr, self.wd = float(reg), float(lr), float(weight_decay)
         n = self.n_users + self.n_items
         if adj is None:
-            rp, col, val = graph.lightgcn_norm_adj(train_u, train_i, self.n_users, self.n_items)
-            adj = ops.DeviceCSR(rp, col, val, n, self.device, chunk)
+            adj = lightgcn_adj(train_u, train_i, self.n_users, self.n_items, self.device, chunk)
         self.adj = adj
         if user_emb is None:
             # xavier_uniform_ as reference lightgcn.py:56-63 (CPU RNG, caller seeds)

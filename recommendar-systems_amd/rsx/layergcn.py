@@ -19,6 +19,8 @@ E^0 with g = A dZ^1 + (cosine terms) + reg.  Loss: sum-BPR + reg * L2
 """
 from __future__ import annotations
 
+import os
+
 import random
 
 import numpy as np
@@ -27,6 +29,7 @@ import torch.nn as nn
 
 from . import _lib as L
 from . import graph, ops
+from .engine import lightgcn_adj
 from .recommender import GeneralRecommender
 
 
@@ -39,8 +42,7 @@ class LayerGCNEngine:
             raise RuntimeError("LayerGCN needs n_layers >= 1")
         self.reg, self.lr, self.wd, self.chunk = float(reg), float(lr), float(weight_decay), int(chunk)
         n = self.n_users + self.n_items
-        rp, col, val = graph.lightgcn_norm_adj(train_u, train_i, self.n_users, self.n_items)
-        self.norm_adj = ops.DeviceCSR(rp, col, val, n, self.device, chunk)
+        self.norm_adj = lightgcn_adj(train_u, train_i, self.n_users, self.n_items, self.device, chunk)
         self.train_adj = self.norm_adj
         dev = self.device
         self.p = torch.from_numpy(np.concatenate([user_emb, item_emb]).astype(np.float32)).to(dev)
@@ -155,7 +157,15 @@ class DeviceEdgeDropout:
         return torch.zeros(self.n_edges, dtype=torch.bool, device=self.device).index_fill_(0, keep, True)
 
     def build(self, mask: torch.Tensor, keep_len: int):
-        """(rowptr, col, val) device tensors of the symmetric masked adjacency."""
+        """(rowptr, col, val) device tensors of the symmetric masked adjacency: kept
+        degrees, f32 values and the template's compaction in one rsx_edge_dropout_build
+        (csrc/graph.hip); RSX_GRAPH_BUILDER=host keeps the torch-op statement below."""
+        if os.environ.get("RSX_GRAPH_BUILDER", "device") != "host":
+            if not hasattr(self, "_t_col32"):
+                self._t_col32 = self.t_col.contiguous()
+            rp, col, val = ops.edge_dropout_build(self.u, self.i, mask, self.n_users, self.n_items, self.t_rowptr,
+                                                  self._t_col32, self.t_eid)
+            return rp, col[: 2 * keep_len], val[: 2 * keep_len]
         mf = mask.to(torch.float32)
         ru = torch.zeros(self.n_users, dtype=torch.float32, device=self.device).index_add_(0, self.u, mf)
         ci = torch.zeros(self.n_items, dtype=torch.float32, device=self.device).index_add_(0, self.i, mf)

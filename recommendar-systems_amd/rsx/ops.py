@@ -378,3 +378,60 @@ class DeviceSampler:
                                             self.all_items.data_ptr(), self.all_items.numel(), self.seed,
                                             epoch, start, batch, _pi(out), _stream()), "rsx_sample_triplets")
         return out
+
+
+# ---------------------------------------------------------------------------
+# graph builders on the device (csrc/graph.hip)
+# ---------------------------------------------------------------------------
+ADJ_LIGHTGCN, ADJ_SMORE = 0, 1
+
+
+def adj_build(u, i, n_users: int, n_items: int, mode: int, device):
+    """(rowptr int64 [n+1], col int32 [nnz], val f32 [nnz]) device tensors of the
+    normalised symmetric adjacency (rsx_adj_build): mode ADJ_LIGHTGCN = reference
+    lightgcn.py:65-103, ADJ_SMORE = smore.py:176-207; equal to rsx.graph's host
+    builders bit for bit.  u, i: host arrays or device int64 tensors."""
+    dev = torch.device(device)
+    u = torch.as_tensor(u, dtype=torch.int64).to(dev).contiguous()
+    i = torch.as_tensor(i, dtype=torch.int64).to(dev).contiguous()
+    E = u.numel()
+    n = n_users + n_items
+    lib = L.lib()
+    rowptr = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    col = torch.empty(max(2 * E, 1), dtype=torch.int32, device=dev)
+    val = torch.empty(max(2 * E, 1), dtype=torch.float32, device=dev)
+    ws = torch.empty(int(lib.rsx_adj_build_ws_bytes(E, n_users, n_items)), dtype=torch.uint8, device=dev)
+    L.check(lib.rsx_adj_build(_p(u), _p(i), E, n_users, n_items, mode, _p(rowptr), _p(col), _p(val), _p(ws),
+                              ws.numel(), _stream()), "rsx_adj_build")
+    nnz = int(rowptr[-1].item())
+    col, val = col[:nnz], val[:nnz]
+    if mode == ADJ_SMORE:
+        # the reference's d^-1/2 is numpy's float32 power (smore.py:194-198), a vectorised
+        # <= 1-ulp powf, not the correctly rounded value the kernel's f64 pow gives: the n
+        # per-node factors come from numpy itself, the per-edge products stay on the device
+        deg = np.diff(rowptr.cpu().numpy()).astype(np.float32)
+        with np.errstate(divide="ignore"):
+            dinv = np.power(deg, np.float32(-0.5)).astype(np.float32)
+        dinv[np.isinf(dinv)] = 0.0
+        d = torch.from_numpy(dinv).to(dev)
+        rows = torch.repeat_interleave(torch.arange(n, device=dev), rowptr[1:] - rowptr[:-1])
+        val = (d[rows] * 1.0) * d[col.long()]
+    return rowptr, col, val
+
+
+def edge_dropout_build(e_u, e_i, keep, n_users: int, n_items: int, t_rowptr, t_col, t_eid):
+    """(rowptr, col, val) of LayerGCN's masked graph (rsx_edge_dropout_build)."""
+    _gpu(e_u, e_i, keep, t_rowptr, t_col, t_eid)
+    E = e_u.numel()
+    n = n_users + n_items
+    dev = e_u.device
+    lib = L.lib()
+    keep8 = keep.to(torch.uint8).contiguous()
+    rowptr = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    col = torch.empty(max(2 * E, 1), dtype=torch.int32, device=dev)
+    val = torch.empty(max(2 * E, 1), dtype=torch.float32, device=dev)
+    ws = _ws(dev, int(lib.rsx_edge_dropout_ws_bytes(E, n_users, n_items)))
+    L.check(lib.rsx_edge_dropout_build(_p(e_u), _p(e_i), _p(keep8), E, n_users, n_items, _p(t_rowptr), _p(t_col),
+                                       _p(t_eid), _p(rowptr), _p(col), _p(val), _p(ws), ws.numel(), _stream()),
+            "rsx_edge_dropout_build")
+    return rowptr, col, val

@@ -221,11 +221,18 @@ class SMORE(GeneralRecommender):
         nn.init.xavier_uniform_(self.item_id_embedding.weight)
         nu, ni = self.n_users, self.n_items
         im = self.interaction_matrix
-        rp, col, val = graph.smore_norm_adj(im.row.astype(np.int64), im.col.astype(np.int64), nu, ni)
-        self.norm_adj_csr = ops.DeviceCSR(rp, col, val, nu + ni, self.device, chunk)
-        rrp, rcol, rval = graph.csr_block(rp, col, val, 0, nu, nu, nu + ni)
-        rows = np.repeat(np.arange(nu), np.diff(rrp))
-        self.R = _DevGraph(rows, rcol.astype(np.int64), rval, nu, ni, self.device, chunk)
+        if os.environ.get("RSX_GRAPH_BUILDER", "device") == "host":
+            rp, col, val = graph.smore_norm_adj(im.row.astype(np.int64), im.col.astype(np.int64), nu, ni)
+            self.norm_adj_csr = ops.DeviceCSR(rp, col, val, nu + ni, self.device, chunk)
+        else:  # rsx_adj_build (csrc/graph.hip), bit-equal to graph.smore_norm_adj
+            drp, dcol, dval = ops.adj_build(im.row.astype(np.int64), im.col.astype(np.int64), nu, ni,
+                                            ops.ADJ_SMORE, self.device)
+            self.norm_adj_csr = ops.DeviceCSR.from_device(drp, dcol, dval, nu + ni, chunk)
+            rp, col, val = self.norm_adj_csr.rowptr_host, dcol.cpu().numpy(), dval.cpu().numpy()
+        # R = the user rows' item block (users first: rows [0, nu), item columns rebased)
+        e = int(rp[nu])
+        rows = np.repeat(np.arange(nu), np.diff(rp[: nu + 1]))
+        self.R = _DevGraph(rows, col[:e].astype(np.int64) - nu, val[:e], nu, ni, self.device, chunk)
         root = os.path.abspath((config["data_path"] or "") + (config["dataset"] or ""))
         self.knn_mode = config["rsx_knn"] or config["rsx_sampler"] or "device"
         if self.knn_mode not in ("device", "host"):
