@@ -489,6 +489,24 @@ int rsx_smore_pref(int32_t backward, const float* const* W, const float* const* 
                    const float* g_side, float* g_content, float* g_image, float* g_text, float* g_fusion,
                    float* hv, float* ht, float* const* dz, rsx_stream_t stream);
 /*
+ * The same block on the batch rows only (the training forward: only the rows of the
+ * batch's users, positives and negatives reach the BPR and InfoNCE terms, and the
+ * block is row-local).  Logical row r < n is table row rows[r] (rows may repeat):
+ *   forward: all_out / side_out [n, d] compact; content_out / fusion_out (optional)
+ *            receive the gathered content / fusion rows (the InfoNCE content rows and
+ *            a weight-gradient input); the dropout key is the table row.
+ *   backward: g_all / g_side / g_content_in (gradient of content_out, optional) are
+ *            compact; g_content / g_image / g_text / g_fusion are full [N, d] tables
+ *            the row gradients are ADDED into (zero them first); hv / ht / dz compact.
+ */
+int rsx_smore_pref_rows(int32_t backward, const float* const* W, const float* const* b, const float* content,
+                        const float* image_emb, const float* text_emb, const float* fusion_emb, const int64_t* rows,
+                        int64_t n, int32_t d, float p_drop, const int64_t* seed_dev, float* all_out,
+                        float* side_out, float* content_out, float* fusion_out, const float* g_all,
+                        const float* g_side, const float* g_content_in, float* g_content, float* g_image,
+                        float* g_text, float* g_fusion, float* hv, float* ht, float* const* dz,
+                        rsx_stream_t stream);
+/*
  * dW[p] = dz[p]^T x[p] ([d, d]) and db[p] = colsum(dz[p]) (db[p] may be NULL) for up to
  * 8 pairs of [n, d] row sets: row-split partials + one ordered reduction.
  */
@@ -548,6 +566,12 @@ int rsx_smore_unit_weights_bwd(const float* partials, int64_t n_blocks, const fl
 int rsx_adam_multi(int32_t count, float* const* p, const float* const* g, float* const* m, float* const* v,
                    const int64_t* const* step_dev, const int64_t* n, float lr, float beta1, float beta2, float eps,
                    float weight_decay, rsx_stream_t stream);
+/* The same with the gradient taken as g * grad_scale (an f32 product, as the
+ * reference's p.grad.mul_(-mg_beta) before the mirror-gradient step,
+ * src/common/trainer.py:327-330, folded into the update). */
+int rsx_adam_multi_scaled(int32_t count, float* const* p, const float* const* g, float* const* m, float* const* v,
+                          const int64_t* const* step_dev, const int64_t* n, float lr, float beta1, float beta2,
+                          float eps, float weight_decay, float grad_scale, rsx_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
 /* SMORE kNN item graph (knn.hip)                                             */

@@ -344,19 +344,42 @@ struct PrefArgs {
     float* hv;               // recomputed tanh rows of the query MLPs (wgrad inputs)
     float* ht;
     float* dz[kNW];          // pre-activation gradients (wgrad rows)
+    // batch rows (rsx_smore_pref_rows): logical row r reads C / IE / TE / FE at rows[r];
+    // row-r outputs (all, side, c_out, fe_out, dz, hv, ht) and inputs (g_all, g_side,
+    // g_cin) are compact; gC / gIE / gTE / gFE are added into full tables at rows[r]
+    const int64_t* rows;
+    float* c_out;            // forward: the gathered content / fusion rows (optional)
+    float* fe_out;
+    const float* g_cin;      // backward: gradient of c_out (optional), added into gC
 };
+
+// the table row of logical row r (r < 0: none)
+__device__ __forceinline__ int64_t src_row(const PrefArgs& a, int64_t r) { return (r >= 0 && a.rows) ? a.rows[r] : r; }
+
+// Y[row] += x (float atomics: rows repeat within a batch)
+template <int D>
+__device__ __forceinline__ void fatomic(float* Y, int64_t row, int g, const Fld<D>& x) {
+    if (row < 0 || !Y) return;
+#pragma unroll
+    for (int t = 0; t < D / 16; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) unsafeAtomicAdd(Y + row * D + 16 * t + 4 * g + r, x.f[t][r]);
+}
 
 template <int D>
 __global__ __launch_bounds__(256) void pref_fwd(PrefArgs a) {
     __shared__ __attribute__((aligned(16))) float wl[D * kLd<D>];
     const int lane = threadIdx.x & 63, g = lane >> 4;
     const int64_t n0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 16;
-    const int64_t row = n0 + (lane & 15) < a.n ? n0 + (lane & 15) : -1;
+    const int64_t out = n0 + (lane & 15) < a.n ? n0 + (lane & 15) : -1;
+    const int64_t row = src_row(a, out);
     const uint64_t seed = a.p_drop > 0.f ? (uint64_t)*a.seed : 0;
     const auto mul = [](float x, float y) { return x * y; };
     const auto lin = [&](int k, const Fld<D>& x) { return mv<D, kLd<D>>(stage_w<D>(wl, a.W[k]), a.b[k], x, lane); };
     const Fld<D> FE = fload<D>(a.FE, row, g);
     const Fld<D> C = fload<D>(a.C, row, g);
+    fstore<D>(a.c_out, out, g, C);
+    fstore<D>(a.fe_out, out, g, FE);
     // agg_img = ip * (softmax(query_v(FE)) * IE)
     Fld<D> h = fmap<D>(lin(kW1v, FE), tanh_);
     Fld<D> s = softmax_row<D>(lin(kW2v, h));
@@ -373,8 +396,8 @@ __global__ __launch_bounds__(256) void pref_fwd(PrefArgs a) {
     // side = mean(stack([x1, x2, fp * FE]))  (sum, then * 1/3 as torch's mean)
     const Fld<D> sd = fmap3<D>(x1, x2, fmap2<D>(fp, FE, mul),
                                [](float u, float v, float w) { return ((u + v) + w) * (1.f / 3.f); });
-    fstore<D>(a.side, row, g, sd);
-    fstore<D>(a.all, row, g, fmap2<D>(C, sd, [](float u, float v) { return u + v; }));
+    fstore<D>(a.side, out, g, sd);
+    fstore<D>(a.all, out, g, fmap2<D>(C, sd, [](float u, float v) { return u + v; }));
 }
 
 template <int D>
@@ -382,18 +405,19 @@ __global__ __launch_bounds__(256) void pref_bwd(PrefArgs a) {
     __shared__ __attribute__((aligned(16))) float wl[D * kLd<D>];
     const int lane = threadIdx.x & 63, g = lane >> 4;
     const int64_t n0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 16;
-    const int64_t row = n0 + (lane & 15) < a.n ? n0 + (lane & 15) : -1;
+    const int64_t out = n0 + (lane & 15) < a.n ? n0 + (lane & 15) : -1;
+    const int64_t row = src_row(a, out);
     const uint64_t seed = a.p_drop > 0.f ? (uint64_t)*a.seed : 0;
     const auto mul = [](float x, float y) { return x * y; };
     const auto add = [](float x, float y) { return x + y; };
     const auto sig_bwd = [](float gy, float y) { return gy * ((1.f - y) * y); };
-    const Fld<D> gA = fload<D>(a.g_all, row, g);
+    const Fld<D> gA = fload<D>(a.g_all, out, g);
     // d side = g_all + g_side;  each of the three stacked views gets d side / 3
-    const Fld<D> g1 = a.g_side ? fmap2<D>(gA, fload<D>(a.g_side, row, g), [](float u, float v) { return (u + v) * (1.f / 3.f); })
+    const Fld<D> g1 = a.g_side ? fmap2<D>(gA, fload<D>(a.g_side, out, g), [](float u, float v) { return (u + v) * (1.f / 3.f); })
                                : fmap<D>(gA, [](float u) { return u * (1.f / 3.f); });
     const Fld<D> FE = fload<D>(a.FE, row, g);
     const Fld<D> C = fload<D>(a.C, row, g);
-    Fld<D> gC = gA;
+    Fld<D> gC = a.g_cin ? fmap2<D>(gA, fload<D>(a.g_cin, out, g), add) : gA;
     Fld<D> gFE;
     {   // fusion view: x3 = fp * FE
         const float* W = stage_w<D>(wl, a.W[kWfp]);
@@ -403,7 +427,7 @@ __global__ __launch_bounds__(256) void pref_bwd(PrefArgs a) {
         Fld<D> dp = fmap2<D>(g1, FE, mul);
         if (a.p_drop > 0.f) dp = fmap2<D>(dp, mf, mul);
         const Fld<D> dz = fmap2<D>(dp, sf, sig_bwd);
-        fstore<D>(a.dz[kWfp], row, g, dz);
+        fstore<D>(a.dz[kWfp], out, g, dz);
         gC = fmap2<D>(gC, mvt<D, kLd<D>>(W, dz, lane), add);
         gFE = fmap2<D>(g1, fp, mul);
     }
@@ -411,7 +435,7 @@ __global__ __launch_bounds__(256) void pref_bwd(PrefArgs a) {
     for (int v = 0; v < 2; ++v) {  // v = 0: image view, 1: text view
         const int w1 = v ? kW1t : kW1v, w2 = v ? kW2t : kW2v, wp = v ? kWtp : kWip;
         const Fld<D> h = fmap<D>(mv<D, kLd<D>>(stage_w<D>(wl, a.W[w1]), a.b[w1], FE, lane), tanh_);
-        fstore<D>(v ? a.ht : a.hv, row, g, h);
+        fstore<D>(v ? a.ht : a.hv, out, g, h);
         const Fld<D> s = softmax_row<D>(mv<D, kLd<D>>(stage_w<D>(wl, a.W[w2]), nullptr, h, lane));
         const Fld<D> E = fload<D>(v ? a.TE : a.IE, row, g);
         Fld<D> pp;
@@ -424,22 +448,28 @@ __global__ __launch_bounds__(256) void pref_bwd(PrefArgs a) {
             Fld<D> dpp = fmap3<D>(g1, s, E, [](float u, float q, float e) { return u * (q * e); });
             if (a.p_drop > 0.f) dpp = fmap2<D>(dpp, mp, mul);
             const Fld<D> dzp = fmap2<D>(dpp, sp, sig_bwd);
-            fstore<D>(a.dz[wp], row, g, dzp);
+            fstore<D>(a.dz[wp], out, g, dzp);
             gC = fmap2<D>(gC, mvt<D, kLd<D>>(W, dzp, lane), add);
         }
         const Fld<D> da = fmap2<D>(g1, pp, mul);          // d (s * E)
-        fstore<D>(v ? a.gTE : a.gIE, row, g, fmap2<D>(da, s, mul));
+        if (a.rows) fatomic<D>(v ? a.gTE : a.gIE, row, g, fmap2<D>(da, s, mul));
+        else fstore<D>(v ? a.gTE : a.gIE, row, g, fmap2<D>(da, s, mul));
         const Fld<D> dsm = fmap2<D>(da, E, mul);          // d softmax output
         const float dot = rsum<D>(fmap2<D>(dsm, s, mul));
         const Fld<D> dq = fmap2<D>(s, dsm, [&](float y, float gy) { return y * (gy - dot); });
-        fstore<D>(a.dz[w2], row, g, dq);
+        fstore<D>(a.dz[w2], out, g, dq);
         const Fld<D> dh = mvt<D, kLd<D>>(stage_w<D>(wl, a.W[w2]), dq, lane);
         const Fld<D> dz1 = fmap2<D>(dh, h, [](float gy, float y) { return gy * (1.f - y * y); });
-        fstore<D>(a.dz[w1], row, g, dz1);
+        fstore<D>(a.dz[w1], out, g, dz1);
         gFE = fmap2<D>(gFE, mvt<D, kLd<D>>(stage_w<D>(wl, a.W[w1]), dz1, lane), add);
     }
-    fstore<D>(a.gC, row, g, gC);
-    fstore<D>(a.gFE, row, g, gFE);
+    if (a.rows) {
+        fatomic<D>(a.gC, row, g, gC);
+        fatomic<D>(a.gFE, row, g, gFE);
+    } else {
+        fstore<D>(a.gC, row, g, gC);
+        fstore<D>(a.gFE, row, g, gFE);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -774,6 +804,7 @@ struct AdamList {
     uint32_t vec4;       // bit i: tensor i is float4-aligned with n % 4 == 0
     int32_t count;
     float lr, beta1, beta2, eps, wd;
+    float gscale;        // the gradient is g * gscale (f32 product, as torch's grad.mul_(s)); 1 = none
 };
 
 __global__ __launch_bounds__(256) void adam_multi(AdamList L) {
@@ -800,7 +831,8 @@ __global__ __launch_bounds__(256) void adam_multi(AdamList L) {
             const int64_t i = base + 4 * (k * 256 + threadIdx.x);
             if (i < n) {
                 float4 pp = ld4(p + i), mm = ld4(m + i), vv = ld4(v + i);
-                const float4 gg = ld4(gr + i);
+                float4 gg = ld4(gr + i);
+                if (L.gscale != 1.f) gg = mul4(L.gscale, gg);
                 adam_elem(c, pp.x, mm.x, vv.x, gg.x);
                 adam_elem(c, pp.y, mm.y, vv.y, gg.y);
                 adam_elem(c, pp.z, mm.z, vv.z, gg.z);
@@ -817,7 +849,7 @@ __global__ __launch_bounds__(256) void adam_multi(AdamList L) {
         const int64_t i = base + k * 256 + threadIdx.x;
         if (i < n) {
             float pp = p[i], mm = m[i], vv = v[i];
-            adam_elem(c, pp, mm, vv, gr[i]);
+            adam_elem(c, pp, mm, vv, L.gscale != 1.f ? gr[i] * L.gscale : gr[i]);
             p[i] = pp;
             m[i] = mm;
             v[i] = vv;
@@ -873,19 +905,40 @@ __global__ __launch_bounds__(256) void mg_sumsq(PairList L, double* partial) {
     }
 }
 
-// one wave: the block sums in order (lane-strided, then a fixed tree), then the
-// reference's scalar arithmetic: rms values as f32 tensor results, the rest in f64
-__global__ __launch_bounds__(64) void mg_alpha_final(const double* partial, int64_t n_blocks, int64_t numel,
-                                                     double base, double lr, double rel, double max_scale,
-                                                     double* alpha) {
-    double sg = 0.0, sp = 0.0;
-    for (int64_t b = threadIdx.x; b < n_blocks; b += 64) {
-        sg += partial[2 * b];
-        sp += partial[2 * b + 1];
+// one 1024-thread block: the block sums thread-strided (independent loads in flight),
+// then a fixed tree (deterministic), then the reference's scalar arithmetic: rms
+// values as f32 tensor results, the rest in f64
+constexpr int kMgFinal = 1024;
+__global__ __launch_bounds__(kMgFinal) void mg_alpha_final(const double* partial, int64_t n_blocks, int64_t numel,
+                                                           double base, double lr, double rel, double max_scale,
+                                                           double* alpha) {
+    double sg0 = 0.0, sp0 = 0.0, sg1 = 0.0, sp1 = 0.0;
+    int64_t b = threadIdx.x;
+    for (; b + kMgFinal < n_blocks; b += 2 * kMgFinal) {
+        sg0 += partial[2 * b];
+        sp0 += partial[2 * b + 1];
+        sg1 += partial[2 * (b + kMgFinal)];
+        sp1 += partial[2 * (b + kMgFinal) + 1];
     }
-    sg = group_sum_d<64>(sg);
-    sp = group_sum_d<64>(sp);
+    if (b < n_blocks) {
+        sg0 += partial[2 * b];
+        sp0 += partial[2 * b + 1];
+    }
+    double sg = group_sum_d<64>(sg0 + sg1);
+    double sp = group_sum_d<64>(sp0 + sp1);
+    __shared__ double red[2][kMgFinal / 64];
+    if ((threadIdx.x & 63) == 0) {
+        red[0][threadIdx.x >> 6] = sg;
+        red[1][threadIdx.x >> 6] = sp;
+    }
+    __syncthreads();
     if (threadIdx.x != 0) return;
+    sg = 0.0;
+    sp = 0.0;
+    for (int w = 0; w < kMgFinal / 64; ++w) {
+        sg += red[0][w];
+        sp += red[1][w];
+    }
     const float sq = (float)sqrt((double)numel);
     const double grad_rms = (double)((float)sqrt(sg) / sq);
     const double param_rms = (double)((float)sqrt(sp) / sq + 1e-12f);
@@ -931,19 +984,32 @@ __global__ __launch_bounds__(256) void unit_w_fwd(const float* w0, const float* 
     }
 }
 
-// d w from the spectral backward's per-block partials [nblk][3][nb][2] (summed in
-// block order) through the normalisation: w~ = w / den, den = |w| + eps:
-// d w = g / den - <g, w> w / (|w| den^2)  (|w| = 0: torch's sgn(0) = 0, no second term)
+// d w from the spectral backward's per-block partials [nblk][3][nb][2] through the
+// normalisation: w~ = w / den, den = |w| + eps:
+// d w = g / den - <g, w> w / (|w| den^2)  (|w| = 0: torch's sgn(0) = 0, no second term).
+// One block per weight entry i: the partials thread-strided over the blocks, then a
+// fixed tree (deterministic).
 __global__ __launch_bounds__(256) void unit_w_bwd(const float* part, int nblk, const float* w0, const float* w1,
                                                   const float* w2, int nb, int normalize, float* g0, float* g1,
                                                   float* g2) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= 3 * nb) return;
+    const int i = blockIdx.x;
     float ga = 0.f, gb = 0.f;
-    for (int k = 0; k < nblk; ++k) {
-        ga += part[((int64_t)k * 3 * nb + i) * 2];
-        gb += part[((int64_t)k * 3 * nb + i) * 2 + 1];
+    for (int k = threadIdx.x; k < nblk; k += 256) {
+        const float2 v = *reinterpret_cast<const float2*>(part + ((int64_t)k * 3 * nb + i) * 2);
+        ga += v.x;
+        gb += v.y;
     }
+    ga = group_sum<64>(ga);
+    gb = group_sum<64>(gb);
+    __shared__ float red[2][4];
+    if ((threadIdx.x & 63) == 0) {
+        red[0][threadIdx.x >> 6] = ga;
+        red[1][threadIdx.x >> 6] = gb;
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    ga = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+    gb = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
     const int m = i / nb, b = i % nb;
     const float* w = m == 0 ? w0 : (m == 1 ? w1 : w2);
     float* g = m == 0 ? g0 : (m == 1 ? g1 : g2);
@@ -1022,6 +1088,18 @@ int rsx_smore_pref(int32_t backward, const float* const* W, const float* const* 
                    float p_drop, const int64_t* seed_dev, float* all_out, float* side_out, const float* g_all,
                    const float* g_side, float* g_content, float* g_image, float* g_text, float* g_fusion,
                    float* hv, float* ht, float* const* dz, rsx_stream_t stream) {
+    return rsx_smore_pref_rows(backward, W, b, content, image_emb, text_emb, fusion_emb, nullptr, n, d, p_drop,
+                               seed_dev, all_out, side_out, nullptr, nullptr, g_all, g_side, nullptr, g_content,
+                               g_image, g_text, g_fusion, hv, ht, dz, stream);
+}
+
+int rsx_smore_pref_rows(int32_t backward, const float* const* W, const float* const* b, const float* content,
+                        const float* image_emb, const float* text_emb, const float* fusion_emb, const int64_t* rows,
+                        int64_t n, int32_t d, float p_drop, const int64_t* seed_dev, float* all_out,
+                        float* side_out, float* content_out, float* fusion_out, const float* g_all,
+                        const float* g_side, const float* g_content_in, float* g_content, float* g_image,
+                        float* g_text, float* g_fusion, float* hv, float* ht, float* const* dz,
+                        rsx_stream_t stream) {
     if (n < 0 || !W || !b || !content || !image_emb || !text_emb || !fusion_emb) return RSX_ERR_ARG;
     if (p_drop < 0.f || p_drop >= 1.f || (p_drop > 0.f && !seed_dev)) return RSX_ERR_ARG;
     if (n == 0) return RSX_OK;
@@ -1055,6 +1133,10 @@ int rsx_smore_pref(int32_t backward, const float* const* W, const float* const* 
     a.gFE = g_fusion;
     a.hv = hv;
     a.ht = ht;
+    a.rows = rows;
+    a.c_out = backward ? nullptr : content_out;
+    a.fe_out = backward ? nullptr : fusion_out;
+    a.g_cin = backward ? g_content_in : nullptr;
     const dim3 grid((unsigned)(((n + 15) / 16 + 3) / 4));
     hipStream_t s = as_stream(stream);
     switch (d) {
@@ -1177,6 +1259,12 @@ int rsx_smore_infonce_bwd(const float* side, const float* content, const int64_t
 int rsx_adam_multi(int32_t count, float* const* p, const float* const* g, float* const* m, float* const* v,
                    const int64_t* const* step_dev, const int64_t* n, float lr, float beta1, float beta2, float eps,
                    float weight_decay, rsx_stream_t stream) {
+    return rsx_adam_multi_scaled(count, p, g, m, v, step_dev, n, lr, beta1, beta2, eps, weight_decay, 1.f, stream);
+}
+
+int rsx_adam_multi_scaled(int32_t count, float* const* p, const float* const* g, float* const* m, float* const* v,
+                          const int64_t* const* step_dev, const int64_t* n, float lr, float beta1, float beta2,
+                          float eps, float weight_decay, float grad_scale, rsx_stream_t stream) {
     if (count < 0 || (count > 0 && (!p || !g || !m || !v || !step_dev || !n))) return RSX_ERR_ARG;
     hipStream_t s = as_stream(stream);
     for (int32_t c0 = 0; c0 < count; c0 += sf::kAdamMax) {
@@ -1186,6 +1274,7 @@ int rsx_adam_multi(int32_t count, float* const* p, const float* const* g, float*
         L.beta2 = beta2;
         L.eps = eps;
         L.wd = weight_decay;
+        L.gscale = grad_scale;
         int64_t blocks = 0;
         int k = 0;
         for (int32_t i = c0; i < count && k < sf::kAdamMax; ++i) {
@@ -1262,8 +1351,8 @@ int rsx_mg_alpha(int32_t count, const float* const* params, const float* const* 
         if (blocks[li] > 0) hipLaunchKernelGGL(sf::mg_sumsq, dim3((unsigned)blocks[li]), dim3(256), 0, s, lists[li], part + 2 * off);
         off += blocks[li];
     }
-    hipLaunchKernelGGL(sf::mg_alpha_final, dim3(1), dim3(64), 0, s, part, off, numel, base, lr, rel_step, max_scale,
-                       alpha_out);
+    hipLaunchKernelGGL(sf::mg_alpha_final, dim3(1), dim3(sf::kMgFinal), 0, s, part, off, numel, base, lr, rel_step,
+                       max_scale, alpha_out);
     return last_rc();
 }
 
@@ -1294,7 +1383,7 @@ int rsx_smore_unit_weights_bwd(const float* partials, int64_t n_blocks, const fl
                                rsx_stream_t stream) {
     if (!partials || n_blocks < 0 || !wv || !wt || !wf || !gv || !gt || !gf || d <= 0) return RSX_ERR_ARG;
     const int nb = d / 2 + 1;
-    hipLaunchKernelGGL(sf::unit_w_bwd, dim3((3 * nb + 255) / 256), dim3(256), 0, as_stream(stream), partials,
+    hipLaunchKernelGGL(sf::unit_w_bwd, dim3(3 * nb), dim3(256), 0, as_stream(stream), partials,
                        (int)n_blocks, wv, wt, wf, nb, normalize, gv, gt, gf);
     return last_rc();
 }

@@ -24,6 +24,9 @@ from .smore_fuse import adam_multi
 class RsxAdam(torch.optim.Optimizer):
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
+        # the next step() takes every gradient as g * grad_scale (then resets it to 1):
+        # the mirror gradient's p.grad.mul_(-beta) folded into the update
+        self.grad_scale = 1.0
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -31,6 +34,7 @@ class RsxAdam(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        gs, self.grad_scale = float(self.grad_scale), 1.0
         for group in self.param_groups:
             live = [p for p in group["params"] if p.grad is not None]
             for p in live:
@@ -54,11 +58,13 @@ class RsxAdam(torch.optim.Optimizer):
                                                     for p in live],
                            [self.state[p]["exp_avg"] for p in live], [self.state[p]["exp_avg_sq"] for p in live],
                            steps, group["lr"], betas=group["betas"], eps=group["eps"],
-                           weight_decay=group["weight_decay"])
+                           weight_decay=group["weight_decay"], grad_scale=gs)
                 continue
             for p in live:
                 st = self.state[p]
                 g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
+                if gs != 1.0:
+                    g = g * gs
                 ops.adam_(p.data, g, st["exp_avg"], st["exp_avg_sq"], 0, group["lr"], betas=group["betas"],
                           eps=group["eps"], weight_decay=group["weight_decay"], step_dev=st["step"])
         return loss

@@ -278,6 +278,9 @@ class SMORE(GeneralRecommender):
         self.diag_grad = bool(config.get("diag_grad", True))
         self.use_hip_spectral = bool(config.get("rsx_smore_spectral", True))
         self.use_fused = bool(config.get("rsx_smore_fused", True)) and SF.supported(d)
+        # training loss on the batch rows only (rsx_smore_batch_rows: False = full tables)
+        self.batch_rows = bool(config.get("rsx_smore_batch_rows", True))
+        self._bidx = {}
         # dropout masks of the fused preference block: a hash of (seed, call, row,
         # feature); the seed word lives on the device and advances once per training
         # forward (graph-capture safe).  Derived from the config seed, not torch's RNG,
@@ -343,7 +346,8 @@ class SMORE(GeneralRecommender):
             return self._forward_all_fused(train)
         return self._forward_all_torch(train)
 
-    def _forward_all_fused(self, train=False):
+    def _views_fused(self, train=False):
+        """Everything before the preference block: (content, image, text, fusion tables, dropout seed)."""
         cv, ct, cf = self._projected_spectrum()
         item_id = self.item_id_embedding.weight
         img_i, txt_i, fus_i = SF.gates(cv, ct, cf, item_id, self.gate_v, self.gate_t, self.gate_f,
@@ -359,9 +363,13 @@ class SMORE(GeneralRecommender):
             self._drop_seed.add_(1)
         else:
             seed = self._drop_seed
-        all_embeds, side = SF.preference(self, content, image_embeds, text_embeds, fusion_embeds, seed)
         if train:
             self._last["conv"] = (cv.detach(), ct.detach(), cf.detach())
+        return content, image_embeds, text_embeds, fusion_embeds, seed
+
+    def _forward_all_fused(self, train=False):
+        content, image_embeds, text_embeds, fusion_embeds, seed = self._views_fused(train)
+        all_embeds, side = SF.preference(self, content, image_embeds, text_embeds, fusion_embeds, seed)
         return all_embeds, side, content
 
     def _forward_all_torch(self, train=False):
@@ -410,7 +418,38 @@ class SMORE(GeneralRecommender):
         ttl = torch.exp(torch.matmul(view1, view2.transpose(0, 1)) / temperature).sum(dim=1)
         return torch.mean(-torch.log(pos / ttl))
 
+    def _batch_index(self, B: int):
+        """(ar, trip): arange(B) and the compact triplets (b, b, B + b) of the batch rows
+        [users; B + positives; 2B + negatives] (cached per batch size)."""
+        c = self._bidx.get(B)
+        if c is None:
+            ar = torch.arange(B, dtype=torch.int64, device=self.device)
+            c = self._bidx[B] = (ar, torch.stack([ar, ar, ar + B]).contiguous())
+        return c
+
+    def _calculate_loss_rows(self, interaction):
+        """The training loss with the preference block on the batch rows only: the BPR
+        and InfoNCE terms read all / side / content at the batch's users, positives
+        and negatives alone, and the block is row-local (smore.py:320-341), so its
+        other rows are never computed.  Same loss and gradients as the full-table
+        form (duplicate rows are computed once per occurrence, their gradients added)."""
+        users, pos, neg = interaction[0], interaction[1], interaction[2]
+        nu, B = self.n_users, users.numel()
+        content, image_embeds, text_embeds, fusion_embeds, seed = self._views_fused(train=True)
+        rows = torch.cat([users, pos + nu, neg + nu])
+        all_c, side_c, content_c = SF.preference_rows(self, content, image_embeds, text_embeds, fusion_embeds,
+                                                      rows, seed)
+        self.global_step += 1
+        ar, trip = self._batch_index(B)
+        bpr = _BprLoss.apply(all_c, None, None, trip, L.RSX_BPR_SMORE, float(self.reg_weight),
+                             float(self.batch_size), B, 2 * B)
+        cl_items, cl_users = SF.infonce2(side_c, content_c, ar, ar, B, self.cl_temp)
+        self._last["cl"] = (cl_items.detach(), cl_users.detach())
+        return bpr + self.cl_loss * (cl_items + cl_users)
+
     def calculate_loss(self, interaction):
+        if self.use_fused and self.batch_rows:
+            return self._calculate_loss_rows(interaction)
         users, pos, neg = interaction[0], interaction[1], interaction[2]
         all_embeds, side, content = self._forward_all(train=True)
         self.global_step += 1

@@ -154,6 +154,67 @@ def preference(model, content, image_embeds, text_embeds, fusion_embeds, seed):
                        *[x.bias for x in lin])
 
 
+class _PrefRows(torch.autograd.Function):
+    """The preference block on the batch rows `rows` (int64 [n], may repeat): from the
+    full content / view tables to compact (all, side, content) rows; the backward adds
+    the row gradients into full zero tables (rsx_smore_pref_rows)."""
+
+    @staticmethod
+    def forward(ctx, C_, IE, TE, FE, rows, p_drop, seed, *wb):
+        W = [_c(x) for x in wb[:7]]
+        b = [None if x is None else _c(x) for x in wb[7:]]
+        C_, IE, TE, FE, rows = _c(C_), _c(IE), _c(TE), _c(FE), _c(rows)
+        n, d = rows.numel(), C_.shape[1]
+        out = torch.empty(4, n, d, dtype=torch.float32, device=C_.device)
+        all_, side, c_rows, f_rows = out.unbind(0)
+        L.check(L.lib().rsx_smore_pref_rows(0, _arr(W), _arr(b), _p(C_), _p(IE), _p(TE), _p(FE), _p(rows), n, d,
+                                            float(p_drop), _p(seed), _p(all_), _p(side), _p(c_rows), _p(f_rows),
+                                            None, None, None, None, None, None, None, None, None, None,
+                                            ops._stream()), "rsx_smore_pref_rows")
+        ctx.save_for_backward(C_, IE, TE, FE, rows, seed, c_rows, f_rows, *W,
+                              *[x if x is not None else torch.empty(0) for x in b])
+        ctx.has_b = [x is not None for x in b]
+        ctx.p_drop = float(p_drop)
+        return all_, side, c_rows
+
+    @staticmethod
+    def backward(ctx, g_all, g_side, g_crows):
+        sv = ctx.saved_tensors
+        C_, IE, TE, FE, rows, seed, c_rows, f_rows = sv[:8]
+        W = list(sv[8:15])
+        b = [x if h else None for x, h in zip(sv[15:22], ctx.has_b)]
+        n, d = rows.numel(), C_.shape[1]
+        if g_all is None:
+            g_all = torch.zeros_like(c_rows)
+        g_all = _c(g_all)
+        g_side = None if g_side is None else _c(g_side)
+        g_crows = None if g_crows is None else _c(g_crows)
+        gfull = torch.zeros(4, *C_.shape, dtype=torch.float32, device=C_.device)
+        gC, gIE, gTE, gFE = gfull.unbind(0)
+        scratch = torch.empty(9, n, d, dtype=torch.float32, device=C_.device)
+        hv, ht, *dz = scratch.unbind(0)
+        L.check(L.lib().rsx_smore_pref_rows(1, _arr(W), _arr(b), _p(C_), _p(IE), _p(TE), _p(FE), _p(rows), n, d,
+                                            ctx.p_drop, _p(seed), None, None, None, None, _p(g_all), _p(g_side),
+                                            _p(g_crows), _p(gC), _p(gIE), _p(gTE), _p(gFE), _p(hv), _p(ht),
+                                            _arr(dz), ops._stream()), "rsx_smore_pref_rows")
+        xs = [f_rows, hv, f_rows, ht, c_rows, c_rows, c_rows]
+        grads = _wgrad([(dz[i], xs[i], ctx.has_b[i]) for i in range(7)], d, C_.device)
+        gW = [g[0] for g in grads]
+        gb = [g[1] for g in grads]
+        return (gC, gIE, gTE, gFE, None, None, None, *gW, *gb)
+
+
+def preference_rows(model, content, image_embeds, text_embeds, fusion_embeds, rows, seed):
+    """(all, side, content) rows of the reference's preference block at table rows
+    `rows` only (the training loss reads no other row; the block is row-local)."""
+    m = model
+    lin = [m.query_v[0], m.query_v[2], m.query_t[0], m.query_t[2], m.gate_image_prefer[0], m.gate_text_prefer[0],
+           m.gate_fusion_prefer[0]]
+    p = float(m.dropout.p) if m.training else 0.0
+    return _PrefRows.apply(content, image_embeds, text_embeds, fusion_embeds, rows, p, seed,
+                           *[x.weight for x in lin], *[x.bias for x in lin])
+
+
 # ---------------------------------------------------------------------------
 # item view -> [users; items] table
 # ---------------------------------------------------------------------------
@@ -236,8 +297,10 @@ def infonce2(side, content, users, pos, n_users, tau):
 # ---------------------------------------------------------------------------
 # multi-tensor Adam
 # ---------------------------------------------------------------------------
-def adam_multi(params, grads, exp_avgs, exp_avg_sqs, steps, lr, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
-    """torch.optim.Adam's update over many tensors in one launch (per 32 tensors)."""
+def adam_multi(params, grads, exp_avgs, exp_avg_sqs, steps, lr, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0,
+               grad_scale=1.0):
+    """torch.optim.Adam's update over many tensors in one launch (per 32 tensors); the
+    gradients are taken as g * grad_scale (f32 product) when grad_scale != 1."""
     n = len(params)
     if n == 0:
         return
@@ -245,9 +308,10 @@ def adam_multi(params, grads, exp_avgs, exp_avg_sqs, steps, lr, betas=(0.9, 0.99
         if not (t.is_cuda and t.is_contiguous() and t.dtype == torch.float32):
             raise RuntimeError("adam_multi: contiguous f32 GPU tensors only")
     sizes = (C.c_int64 * n)(*[p.numel() for p in params])
-    L.check(L.lib().rsx_adam_multi(n, _arr(params), _arr(grads), _arr(exp_avgs), _arr(exp_avg_sqs), _arr(steps),
-                                   sizes, float(lr), float(betas[0]), float(betas[1]), float(eps),
-                                   float(weight_decay), ops._stream()), "rsx_adam_multi")
+    L.check(L.lib().rsx_adam_multi_scaled(n, _arr(params), _arr(grads), _arr(exp_avgs), _arr(exp_avg_sqs),
+                                          _arr(steps), sizes, float(lr), float(betas[0]), float(betas[1]), float(eps),
+                                          float(weight_decay), float(grad_scale), ops._stream()),
+            "rsx_adam_multi_scaled")
 
 
 # ---------------------------------------------------------------------------

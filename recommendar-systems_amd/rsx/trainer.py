@@ -427,7 +427,9 @@ class Trainer:
         with torch.no_grad():
             beta = float(getattr(m, "mg_beta", 0.2))
             live = [p.grad for p in m.parameters() if p.requires_grad and p.grad is not None]
-            if live:
+            if fused:  # folded into the Adam launch below (g * -beta, the same f32 product)
+                self.optimizer.grad_scale = -beta
+            elif live:
                 torch._foreach_mul_(live, -beta)
             if params:
                 if fused:

@@ -127,6 +127,36 @@ def test_smore_first_step(tmp_path, golden, fx):
         assert np.all(np.abs(got - want) <= bound), n
 
 
+@pytest.mark.parametrize("fx,p_drop", [("smore_small", 0.0), ("smore_small", 0.1), ("smore_d128_small", 0.1)])
+def test_smore_batch_rows_loss_equals_full_tables(tmp_path, golden, fx, p_drop):
+    """The training loss with the preference block on the batch rows only
+    (rsx_smore_batch_rows, the default) against the full-table form: the same loss and
+    every parameter gradient, with the same dropout masks (keyed by the table row), on
+    a batch with repeated users and items."""
+    z, c, train, valid, test = _setup(tmp_path, golden, fx)
+    c["dropout_rate"] = p_drop
+    m = _model(c, train)
+    m.train()
+    trip = torch.from_numpy(z["epoch0_triplets"][:, :512].astype(np.int64)).cuda()
+    trip[0, :40] = trip[0, 0]
+    trip[1, 100:140] = trip[2, 7]
+    out = []
+    for rows in (True, False):
+        m.batch_rows = rows
+        m._drop_seed.fill_(12345)
+        m.zero_grad(set_to_none=True)
+        loss = m.calculate_loss(trip)
+        loss.backward()
+        out.append((loss.item(), {n: p.grad.detach().cpu().numpy().copy() for n, p in m.named_parameters()
+                                  if p.grad is not None}))
+    (la, ga), (lb, gb) = out
+    assert abs(la - lb) <= 1e-6 * abs(lb)
+    assert ga.keys() == gb.keys()
+    for n in gb:
+        scale = max(np.abs(gb[n]).max(), 1e-12)
+        np.testing.assert_allclose(ga[n], gb[n], rtol=0, atol=2e-5 * scale, err_msg=n)
+
+
 @pytest.mark.parametrize("fx", list(FIXTURES))
 def test_smore_one_epoch_with_mirror_gradient(tmp_path, golden, fx):
     from rsx.trainer import Trainer
