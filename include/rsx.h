@@ -92,10 +92,10 @@ int rsx_csr_schedule_host(const int64_t* rowptr_host, int64_t n_rows, int32_t ch
  *   RSX_EPI_STORE     y = alpha*acc
  *   RSX_EPI_LAYERSUM  y = alpha*acc;  s_out = s_in + alpha*acc
  *                     (running layer sum of lightgcn.py:124-125 / Horner backward)
- *   RSX_EPI_FINAL     f = (((s_in + r_add) + aux) + alpha*acc) * beta (NULL terms
- *                     skipped);  zero0/zero1 rows := 0  (last layer: mean over K+1
- *                     layers, lightgcn.py:124-125, from a running sum in s_in or
- *                     from the stored layers E0 = s_in, E1 = r_add, E2 = aux)
+ *   RSX_EPI_FINAL     f = ((((s_in + r_add) + aux) + e0) + alpha*acc) * beta (NULL
+ *                     terms skipped);  zero0/zero1 rows := 0  (last layer: mean over
+ *                     K+1 layers, lightgcn.py:124-125, from a running sum in s_in or
+ *                     from the stored layers E0 = s_in, E1 = r_add, E2 = aux, E3 = e0)
  *   RSX_EPI_ADAM      g = (s_in + alpha*acc) * beta + r_add;  Adam(p, m, v, g)
  *                     (last backward layer fused with torch.optim.Adam,
  *                      src/common/trainer.py:133,238)
@@ -451,6 +451,16 @@ int rsx_topk_metrics_fast(const int64_t* topk_idx, int64_t n_users, int32_t k_ma
  * over blocks, partials are summed in block order (deterministic).
  * out_dim, in_dim multiples of 32.
  */
+/*
+ * The whole backward of a Linear applied to many rows in one pass over them
+ * (the SMORE modality projections image_trs / text_trs, src/models/smore.py:256-259):
+ * dw = g^T x [out, in], dx = g W [n, in] (W [out, in], nn.Linear layout) and, when db
+ * is non-NULL, db = colsum(g) [out].  out_dim in {32, 64, 128}, in_dim a multiple
+ * of 32.  Deterministic (split-K partials added in a fixed order).
+ */
+size_t rsx_linear_bwd_ws_bytes(int64_t n, int32_t out_dim, int32_t in_dim);
+int rsx_linear_bwd(const float* g, const float* x, const float* W, int64_t n, int32_t out_dim, int32_t in_dim,
+                   float* dw, float* dx, float* db, void* ws, size_t ws_bytes, rsx_stream_t stream);
 size_t rsx_linear_wgrad_ws_bytes(int64_t n, int32_t out_dim, int32_t in_dim);
 int rsx_linear_wgrad(const float* g, const float* x, int64_t n, int32_t out_dim, int32_t in_dim, float* dw,
                      void* ws, size_t ws_bytes, rsx_stream_t stream);

@@ -35,10 +35,10 @@ struct WgPlan {
     int slots() const { return splits * rw; }
 };
 
-static WgPlan wg_plan(int64_t n, int out_dim, int in_dim) {
+static WgPlan wg_plan(int64_t n, int out_dim, int in_dim, int max_ig = 4) {
     WgPlan p;
     const int it = in_dim / 32, ot = out_dim / 32;
-    p.ig = (it % 4 == 0) ? 4 : (it % 2 == 0) ? 2 : 1;
+    p.ig = (it % 4 == 0 && max_ig >= 4) ? 4 : (it % 2 == 0 && max_ig >= 2) ? 2 : 1;
     p.otb = ot % 4 == 0 ? 4 : ot % 2 == 0 ? 2 : 1;
     p.rw = 4 / p.otb;
     p.nob = ot / p.otb;
@@ -66,18 +66,29 @@ static WgPlan wg_plan(int64_t n, int out_dim, int in_dim) {
 // x[:, i cols] slices with float4 loads into LDS (double-buffered, the next chunk's
 // loads in flight during this chunk's MFMAs), then row group r computes its 16
 // rows from LDS: A = g[2u + h][wo + j], B_q = x[2u + h][32q + j].
-template <int IG, int OTB>
+//
+// DX (the fused projection backward, one block column of o: nob == 1): the same
+// pass also writes the input gradient dx = g W of the chunk's rows and the block's
+// IC columns (W [out, in] row-major, its [out x IC] slice staged once in LDS;
+// 16x16x4 f32 MFMA tiles from the g chunk already in LDS) and, in the blocks of
+// the first i column, the bias-gradient partials colsum(g) (the av values the dW
+// MFMAs read, summed per lane) into the slot's tail [out] floats.
+template <int IG, int OTB, bool DX = false>
 __global__ __launch_bounds__(256) void wgrad_partial(const float* __restrict__ g, const float* __restrict__ x,
                                                      int64_t n, int out_dim, int in_dim, int64_t rows, int64_t nob,
-                                                     int64_t nib, float* __restrict__ part) {
+                                                     int64_t nib, float* __restrict__ part,
+                                                     const float* __restrict__ W = nullptr, float* __restrict__ dx = nullptr,
+                                                     int do_db = 0) {
     constexpr int RW = 4 / OTB;
     constexpr int OC = 32 * OTB, IC = 32 * IG;   // block's o / i columns
     constexpr int CH = kWgChunk * RW;            // rows per block step
     constexpr int GP = OC + 4, XP = IC + 4;      // padded LDS rows
+    constexpr int WP = IC + 16;                  // W slice rows (16x16x4 B reads: 4 rows x 16 banks apart)
     constexpr int NG = CH * OC / 4, NX = CH * IC / 4;  // float4s per step
     constexpr int PER = (NG + NX + 255) / 256;
     __shared__ float gs[2][CH * GP];
     __shared__ float xs[2][CH * XP];
+    __shared__ float wl[DX ? OC * WP : 1];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, j = lane & 31, h = lane >> 5;
     const int64_t bo = blockIdx.x % nob, bi = (blockIdx.x / nob) % nib, s = blockIdx.x / (nob * nib);
     const int ob = (int)bo * OC, ib = (int)bi * IC;
@@ -136,7 +147,20 @@ __global__ __launch_bounds__(256) void wgrad_partial(const float* __restrict__ g
         if (nst > 1) gload(1, st[1]);
         sstore(0, st[0]);
     }
+    if constexpr (DX) {  // W[:, ib : ib + IC] (out_dim == OC)
+        for (int e = threadIdx.x; e < OC * IC / 4; e += 256) {
+            const int o = e / (IC / 4), c = (e % (IC / 4)) * 4;
+            const float4 v = ld4(W + (int64_t)o * in_dim + ib + c);
+            float* d = wl + o * WP + c;
+            d[0] = v.x;
+            d[1] = v.y;
+            d[2] = v.z;
+            d[3] = v.w;
+        }
+    }
     __syncthreads();
+    const bool db_blk = DX && do_db && bi == 0;
+    float dbacc = 0.f;
     // one block step on buffer / register slot B (a template constant: st[] stays in
     // registers); step c+1's data (loaded a step ago) goes to the other buffer after
     // this step's MFMAs, step c+2's loads are issued into the slot just freed
@@ -156,6 +180,37 @@ __global__ __launch_bounds__(256) void wgrad_partial(const float* __restrict__ g
         for (int u = 0; u < 8; ++u)
 #pragma unroll
             for (int q = 0; q < IG; ++q) acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv[u][q], acc[q], 0, 0, 0);
+        if constexpr (DX) {
+            if (db_blk) {
+#pragma unroll
+                for (int u = 0; u < 8; ++u) dbacc += av[u];
+            }
+            // dx[CH x IC] = g_chunk[CH x OC] W_slice[OC x IC]: CH/16 x IC/16 tiles of 16x16,
+            // wave w takes tiles w, w + 4, ...; lane (n = lane & 15, q4 = lane >> 4)
+            constexpr int NT = (CH / 16) * (IC / 16);
+            const int64_t c0 = r0 + c * CH;
+            const int n16 = lane & 15, q4 = lane >> 4;
+#pragma unroll 1
+            for (int t = wave; t < NT; t += 4) {
+                const int mt = t / (IC / 16), nt = t % (IC / 16);
+                const float* ga = gs[B] + (mt * 16 + n16) * GP + q4;
+                const float* wb = wl + q4 * WP + nt * 16 + n16;
+                typedef float floatx4_t __attribute__((ext_vector_type(4)));
+                floatx4_t d0 = {0.f, 0.f, 0.f, 0.f}, d1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
+                for (int k = 0; k < OC; k += 8) {
+                    d0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ga[k], wb[k * WP], d0, 0, 0, 0);
+                    d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ga[k + 4], wb[(k + 4) * WP], d1, 0, 0, 0);
+                }
+                const floatx4_t d = d0 + d1;
+                // lane holds rows 4 q4 + r of the tile, column n16
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int64_t row = c0 + mt * 16 + 4 * q4 + r;
+                    if (row < r1) dx[row * in_dim + ib + nt * 16 + n16] = d[r];
+                }
+            }
+        }
         if (c + 1 < nst) sstore(B ^ 1, st[B ^ 1]);
         __syncthreads();
     };
@@ -164,7 +219,14 @@ __global__ __launch_bounds__(256) void wgrad_partial(const float* __restrict__ g
         if (c + 1 < nst) step(c + 1, std::integral_constant<int, 1>{});
     }
     // C layout: lane holds column ib + 32q + j, rows ob + wo + (e&3) + 8(e>>2) + 4h
-    float* dst = part + (s * RW + r) * (int64_t)out_dim * in_dim;
+    const int64_t slot_sz = (int64_t)out_dim * in_dim + (DX && do_db ? out_dim : 0);
+    float* dst = part + (s * RW + r) * slot_sz;
+    if constexpr (DX) {
+        if (db_blk) {  // the slot's bias partial: rows 2u + h summed per half, halves added
+            dbacc += __shfl_xor(dbacc, 32, 64);
+            if (h == 0) dst[(int64_t)out_dim * in_dim + wo + j] = dbacc;
+        }
+    }
 #pragma unroll
     for (int q = 0; q < IG; ++q)
 #pragma unroll
@@ -197,6 +259,31 @@ __global__ __launch_bounds__(256) void wgrad_reduce(const float* __restrict__ pa
     if (wave == 0 && e < sz) dw[e] = ((q[0][lane] + q[1][lane]) + q[2][lane]) + q[3][lane];
 }
 
+// as wgrad_reduce with slots `stride` floats apart (the fused backward's slots carry
+// the bias partials after the sz weight partials)
+__global__ __launch_bounds__(256) void wgrad_reduce_strided(const float* __restrict__ part, int S, int64_t sz,
+                                                            int64_t stride, float* __restrict__ out) {
+    __shared__ float q[4][64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t e = (int64_t)blockIdx.x * 64 + lane;
+    const int b = (int)((int64_t)S * wave / 4), en = (int)((int64_t)S * (wave + 1) / 4);
+    float acc = 0.f;
+    if (e < sz) {
+        int p = b;
+        for (; p + 8 <= en; p += 8) {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = part[(int64_t)(p + u) * stride + e];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) acc += v[u];
+        }
+        for (; p < en; ++p) acc += part[(int64_t)p * stride + e];
+    }
+    q[wave][lane] = acc;
+    __syncthreads();
+    if (wave == 0 && e < sz) out[e] = ((q[0][lane] + q[1][lane]) + q[2][lane]) + q[3][lane];
+}
+
 }  // namespace rsx
 
 using namespace rsx;
@@ -205,6 +292,63 @@ extern "C" size_t rsx_linear_wgrad_ws_bytes(int64_t n, int32_t out_dim, int32_t 
     if (n <= 0 || out_dim <= 0 || in_dim <= 0 || (out_dim % 32) || (in_dim % 32)) return 0;
     const WgPlan p = wg_plan(n, out_dim, in_dim);
     return (size_t)p.slots() * (size_t)out_dim * (size_t)in_dim * sizeof(float);
+}
+
+// the fused backward stages a W slice too: IC <= 64 keeps two blocks per CU in LDS
+constexpr int kBwdMaxIg = 2;
+
+extern "C" size_t rsx_linear_bwd_ws_bytes(int64_t n, int32_t out_dim, int32_t in_dim) {
+    if (n <= 0 || (out_dim != 32 && out_dim != 64 && out_dim != 128) || in_dim <= 0 || (in_dim % 32)) return 0;
+    const WgPlan p = wg_plan(n, out_dim, in_dim, kBwdMaxIg);
+    return (size_t)p.slots() * ((size_t)out_dim * (size_t)in_dim + (size_t)out_dim) * sizeof(float);
+}
+
+// dW = g^T x, dx = g W, db = colsum(g) (db may be NULL) in one pass over the rows;
+// out_dim in {32, 64, 128} (one block column of o), in_dim a multiple of 32.
+extern "C" int rsx_linear_bwd(const float* g, const float* x, const float* W, int64_t n, int32_t out_dim,
+                              int32_t in_dim, float* dw, float* dx, float* db, void* ws, size_t ws_bytes,
+                              rsx_stream_t stream) {
+    if (n < 0 || out_dim <= 0 || in_dim <= 0 || !dw || !W || (n > 0 && !dx)) return RSX_ERR_ARG;
+    if ((out_dim != 32 && out_dim != 64 && out_dim != 128) || (in_dim % 32)) return RSX_ERR_UNSUPPORTED;
+    if (n > 0 && (!g || !x)) return RSX_ERR_ARG;
+    hipStream_t s = as_stream(stream);
+    const int64_t sz = (int64_t)out_dim * in_dim;
+    if (n == 0) {
+        hipLaunchKernelGGL(wgrad_reduce, dim3((unsigned)((sz + 63) / 64)), dim3(256), 0, s, (const float*)nullptr, 0,
+                           sz, dw);
+        if (db) hipLaunchKernelGGL(wgrad_reduce, dim3((unsigned)((out_dim + 63) / 64)), dim3(256), 0, s,
+                                   (const float*)nullptr, 0, (int64_t)out_dim, db);
+        return last_rc();
+    }
+    if (ws_bytes < rsx_linear_bwd_ws_bytes(n, out_dim, in_dim) || !ws) return RSX_ERR_WORKSPACE;
+    const WgPlan p = wg_plan(n, out_dim, in_dim, kBwdMaxIg);
+    if (p.nob != 1) return RSX_ERR_UNSUPPORTED;
+    float* part = static_cast<float*>(ws);
+    const dim3 grid((unsigned)(p.nob * p.nib * p.splits));
+    const int do_db = db != nullptr;
+#define RSX_WGX(IG, OTB)                                                                                        \
+    hipLaunchKernelGGL((wgrad_partial<IG, OTB, true>), grid, dim3(256), 0, s, g, x, n, (int)out_dim, (int)in_dim,  \
+                       p.rows, p.nob, p.nib, part, W, dx, do_db)
+    const int key = p.ig * 8 + p.otb;
+    switch (key) {
+        case 4 * 8 + 4: RSX_WGX(4, 4); break;
+        case 4 * 8 + 2: RSX_WGX(4, 2); break;
+        case 4 * 8 + 1: RSX_WGX(4, 1); break;
+        case 2 * 8 + 4: RSX_WGX(2, 4); break;
+        case 2 * 8 + 2: RSX_WGX(2, 2); break;
+        case 2 * 8 + 1: RSX_WGX(2, 1); break;
+        case 1 * 8 + 4: RSX_WGX(1, 4); break;
+        case 1 * 8 + 2: RSX_WGX(1, 2); break;
+        default: RSX_WGX(1, 1); break;
+    }
+#undef RSX_WGX
+    // slots of sz + out_dim floats: dw from the first sz, db from the tails
+    hipLaunchKernelGGL(wgrad_reduce_strided, dim3((unsigned)((sz + 63) / 64)), dim3(256), 0, s, (const float*)part,
+                       p.slots(), sz, sz + (do_db ? out_dim : 0), dw);
+    if (do_db)
+        hipLaunchKernelGGL(wgrad_reduce_strided, dim3((unsigned)((out_dim + 63) / 64)), dim3(256), 0, s,
+                           (const float*)(part + sz), p.slots(), (int64_t)out_dim, sz + out_dim, db);
+    return last_rc();
 }
 
 extern "C" int rsx_linear_wgrad(const float* g, const float* x, int64_t n, int32_t out_dim, int32_t in_dim, float* dw,

@@ -629,6 +629,32 @@ __device__ __forceinline__ Fld<D> nce_load_norm(const NceArgs& a, int term, int 
     return fmap<D>(x, [&](float v) { return v / den; });
 }
 
+// The batch rows of both views normalised once (F.normalize, eps 1e-12): nrm[term][view]
+// [B][D] and |x| (for the backward), and the positive pair's dot (n1 * n2).sum(-1) kept
+// in lrow until nce_fwd turns it into the row loss.  One wave per 16 rows.
+template <int D>
+__global__ __launch_bounds__(64) void nce_norm(NceArgs a) {
+    const int term = blockIdx.y;
+    const int lane = threadIdx.x, g = lane >> 4;
+    const int64_t B = a.B;
+    const int64_t bo = (int64_t)blockIdx.x * 16 + (lane & 15) < B ? (int64_t)blockIdx.x * 16 + (lane & 15) : -1;
+    float n1 = 0.f, n2 = 0.f;
+    const Fld<D> X1 = nce_load_norm<D>(a, term, 0, bo, g, &n1);
+    const Fld<D> X2 = nce_load_norm<D>(a, term, 1, bo, g, &n2);
+    fstore<D>(a.nrm + ((int64_t)(term * 2 + 0) * B) * D, bo, g, X1);
+    fstore<D>(a.nrm + ((int64_t)(term * 2 + 1) * B) * D, bo, g, X2);
+    const float dot = rsum<D>(fmap2<D>(X1, X2, [](float u, float v) { return u * v; }));
+    if (g == 0 && bo >= 0) {
+        a.norms[(term * 2 + 0) * B + bo] = n1;
+        a.norms[(term * 2 + 1) * B + bo] = n2;
+        a.lrow[term * B + bo] = dot;
+    }
+}
+
+// ttl[own] = sum over the other rows m of exp(<n1[own], n2[m]> / tau): a block owns 16
+// rows, its waves stride over the 16-row tiles of the other view (contiguous normalised
+// rows, two tiles in flight ahead of the one being multiplied); then the row loss
+// -log(exp(dot / tau) / ttl).
 template <int D>
 __global__ __launch_bounds__(64 * kNceWaves) void nce_fwd(NceArgs a) {
     __shared__ float part[kNceWaves][16];
@@ -637,47 +663,33 @@ __global__ __launch_bounds__(64 * kNceWaves) void nce_fwd(NceArgs a) {
     const int64_t B = a.B;
     const int64_t n0 = (int64_t)blockIdx.x * 16;
     const int64_t bo = n0 + c < B ? n0 + c : -1;
-    float nn1 = 0.f;
-    const Fld<D> X = nce_load_norm<D>(a, term, 0, bo, g, &nn1);  // own view1 rows (B operand)
+    const float* n1 = a.nrm + ((int64_t)(term * 2 + 0) * B) * D;
+    const float* n2 = a.nrm + ((int64_t)(term * 2 + 1) * B) * D;
+    const Fld<D> X = fload<D>(n1, bo, g);  // own view1 rows (B operand)
     const int64_t ntile = (B + 15) / 16;
+    auto row_of = [&](int64_t mt) { return (mt < ntile && mt * 16 + c < B) ? mt * 16 + c : (int64_t)-1; };
     float es = 0.f;  // exp sum of own row c over the other rows 4g + r of this wave's tiles
-    auto rows_of = [&](int64_t mt) {
-        const int64_t bm = mt * 16 + c;
-        return (mt < ntile && bm < B) ? a.idx[term][bm] + a.off[term] : (int64_t)-1;
-    };
-    auto normalize = [&](const Fld<D>& x) {
-        const float den = fmaxf(sqrtf(rsum<D>(fmap<D>(x, [](float v) { return v * v; }))), 1e-12f);
-        return fmap<D>(x, [&](float v) { return v / den; });
-    };
-    Fld<D> Y = normalize(fload<D>(a.src2, rows_of(w), g));  // other view2 rows (A operand)
+    Fld<D> Y0 = fload<D>(n2, row_of(w), g);
+    Fld<D> Y1 = fload<D>(n2, row_of(w + kNceWaves), g);
     for (int64_t mt = w; mt < ntile; mt += kNceWaves) {
-        const Fld<D> Yn = fload<D>(a.src2, rows_of(mt + kNceWaves), g);  // next tile, in flight
+        const Fld<D> Y2 = fload<D>(n2, row_of(mt + 2 * kNceWaves), g);  // two tiles ahead, in flight
         const int64_t m0 = mt * 16;
-        const floatx4 s = tile_dot<D>(Y, X);  // s[r] = S[own c][other m0 + 4g + r] * tau
+        const floatx4 sv = tile_dot<D>(Y0, X);  // s[r] = <own c, other m0 + 4g + r>
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-            if (m0 + 4 * g + r < B) es += expf(s[r] / a.tau);
-        Y = normalize(Yn);
+            if (m0 + 4 * g + r < B) es += expf(sv[r] / a.tau);
+        Y0 = Y1;
+        Y1 = Y2;
     }
     es += __shfl_xor(es, 16, kWave);
     es += __shfl_xor(es, 32, kWave);
     if (lane < 16) part[w][lane] = es;
-    float dot = 0.f;
-    if (w == 0) {  // own rows' normalised views and norms, kept for the backward
-        fstore<D>(a.nrm + ((int64_t)(term * 2 + 0) * B) * D, bo, g, X);
-        if (g == 0 && bo >= 0) a.norms[(term * 2 + 0) * B + bo] = nn1;
-        float nn2 = 0.f;
-        const Fld<D> X2 = nce_load_norm<D>(a, term, 1, bo, g, &nn2);
-        fstore<D>(a.nrm + ((int64_t)(term * 2 + 1) * B) * D, bo, g, X2);
-        if (g == 0 && bo >= 0) a.norms[(term * 2 + 1) * B + bo] = nn2;
-        dot = rsum<D>(fmap2<D>(X, X2, [](float u, float v) { return u * v; }));  // (n1 * n2).sum(-1)
-    }
     __syncthreads();
     if (w == 0 && lane < 16 && bo >= 0) {
         float ttl = 0.f;
 #pragma unroll
         for (int i = 0; i < kNceWaves; ++i) ttl += part[i][lane];
-        const float pos = expf(dot / a.tau);
+        const float pos = expf(a.lrow[term * B + bo] / a.tau);
         a.ttl[term * B + bo] = ttl;
         a.lrow[term * B + bo] = -logf(pos / ttl);
     }
@@ -1232,8 +1244,13 @@ int rsx_smore_infonce_fwd(const float* side, const float* content, const int64_t
     hipStream_t s = as_stream(stream);
     if (batch == 0) return hip_rc(hipMemsetAsync(loss_out, 0xff, 8, s));  // mean of nothing: NaN
     const dim3 grid((unsigned)((batch + 15) / 16), 2);
-    if (d == 64) hipLaunchKernelGGL(sf::nce_fwd<64>, grid, dim3(64 * sf::kNceWaves), 0, s, a);
-    else hipLaunchKernelGGL(sf::nce_fwd<128>, grid, dim3(64 * sf::kNceWaves), 0, s, a);
+    if (d == 64) {
+        hipLaunchKernelGGL(sf::nce_norm<64>, grid, dim3(64), 0, s, a);
+        hipLaunchKernelGGL(sf::nce_fwd<64>, grid, dim3(64 * sf::kNceWaves), 0, s, a);
+    } else {
+        hipLaunchKernelGGL(sf::nce_norm<128>, grid, dim3(64), 0, s, a);
+        hipLaunchKernelGGL(sf::nce_fwd<128>, grid, dim3(64 * sf::kNceWaves), 0, s, a);
+    }
     hipLaunchKernelGGL(sf::nce_mean, dim3(2), dim3(64), 0, s, a);
     return last_rc();
 }

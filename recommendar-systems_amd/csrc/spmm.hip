@@ -60,6 +60,7 @@ __device__ __forceinline__ EpiIn epi_load(const rsx_epilogue& e, int64_t row, in
         if (s_in) in.a = ld4(s_in + off);
         if (r_add) in.b = ld4(r_add + off);
         if (e.aux) in.c = ld4(e.aux + off);
+        if (e.e0) in.d = ld4(e.e0 + off);
     } else if constexpr (KIND == RSX_EPI_ADD) {
         if (s_in) in.a = ld4(s_in + off);
         if (r_add) in.b = ld4(r_add + off);
@@ -125,11 +126,12 @@ __device__ __forceinline__ void epilogue(const rsx_epilogue& e, int64_t row, flo
         const float4 s = e.s_in ? add4(in.a, acc) : acc;
         st4(e.s_out + off, s);
     } else if constexpr (KIND == RSX_EPI_FINAL) {
-        // ((s_in + r_add) + aux) + acc: the stored layers summed in layer order
+        // (((s_in + r_add) + aux) + e0) + acc: the stored layers summed in layer order
         float4 t = in.a;
         if (e.r_add) t = add4(t, in.b);
         if (e.aux) t = add4(t, in.c);
-        const float4 s = (e.s_in || e.r_add || e.aux) ? add4(t, acc) : acc;
+        if (e.e0) t = add4(t, in.d);
+        const float4 s = (e.s_in || e.r_add || e.aux || e.e0) ? add4(t, acc) : acc;
         st4(e.f + off, mul4(e.beta, s));
     } else if constexpr (KIND == RSX_EPI_AXPBY) {
         float4 s = acc;

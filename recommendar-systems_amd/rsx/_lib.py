@@ -121,6 +121,8 @@ def _declare(lib):
         "rsx_topk_metrics_fast": (C.c_int, [P, I64, I32, P, P, P, I32, P, P, P, C.c_size_t, P]),
         "rsx_linear_wgrad_ws_bytes": (C.c_size_t, [I64, I32, I32]),
         "rsx_linear_wgrad": (C.c_int, [P, P, I64, I32, I32, P, P, C.c_size_t, P]),
+        "rsx_linear_bwd_ws_bytes": (C.c_size_t, [I64, I32, I32]),
+        "rsx_linear_bwd": (C.c_int, [P, P, P, I64, I32, I32, P, P, P, P, C.c_size_t, P]),
         "rsx_comm_unique_id_bytes": (C.c_size_t, []),
         "rsx_comm_get_unique_id": (C.c_int, [P]),
         "rsx_comm_init": (C.c_int, [C.POINTER(P), P, I32, I32]),
@@ -164,7 +166,7 @@ EXPORTED = ["rsx_version", "rsx_csr_schedule_host", "rsx_spmm", "rsx_rowwise", "
             "rsx_smore_spectral_spec_floats", "rsx_smore_spectral_fwd_ws_bytes", "rsx_smore_spectral_fwd",
             "rsx_smore_spectral_bwd",
             "rsx_smore_spectral_bwd_partials",
-            "rsx_topk_metrics_ws_bytes", "rsx_topk_metrics", "rsx_topk_metrics_fast", "rsx_linear_wgrad_ws_bytes", "rsx_linear_wgrad",
+            "rsx_topk_metrics_ws_bytes", "rsx_topk_metrics", "rsx_topk_metrics_fast", "rsx_linear_wgrad_ws_bytes", "rsx_linear_wgrad", "rsx_linear_bwd_ws_bytes", "rsx_linear_bwd",
             "rsx_comm_unique_id_bytes", "rsx_comm_get_unique_id", "rsx_comm_init", "rsx_comm_destroy",
             "rsx_comm_init_host",
             "rsx_comm_allreduce_f32", "rsx_sharded_lightgcn_step", "rsx_sharded_lightgcn_forward",

@@ -289,6 +289,26 @@ def topk_metrics(topk_idx: torch.Tensor, eval_rowptr: torch.Tensor, eval_col: to
     return out
 
 
+def linear_bwd_supported(out_dim: int, in_dim: int) -> bool:
+    return out_dim in (32, 64, 128) and in_dim % 32 == 0
+
+
+def linear_bwd(g: torch.Tensor, x: torch.Tensor, W: torch.Tensor, bias: bool = True):
+    """(dW = g^T x, dx = g W, db = colsum g | None) of a Linear over many rows in one
+    pass (rsx_linear_bwd; deterministic)."""
+    g, x, W = g.contiguous(), x.contiguous(), W.contiguous()
+    n, o = g.shape
+    i = x.shape[1]
+    lib = L.lib()
+    dw = torch.empty(o, i, dtype=torch.float32, device=g.device)
+    dx = torch.empty(n, i, dtype=torch.float32, device=g.device)
+    db = torch.empty(o, dtype=torch.float32, device=g.device) if bias else None
+    ws = _ws(g.device, lib.rsx_linear_bwd_ws_bytes(n, o, i))
+    L.check(lib.rsx_linear_bwd(_p(g), _p(x), _p(W), n, o, i, _p(dw), _p(dx), _p(db), _p(ws), ws.numel(), _stream()),
+            "rsx_linear_bwd")
+    return dw, dx, db
+
+
 def linear_wgrad(g: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
     """dW = g^T x for nn.Linear over many rows (rsx_linear_wgrad): split-K over row
     blocks with an ordered partial sum, where a library GEMM would see a 64x64

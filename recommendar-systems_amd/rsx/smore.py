@@ -79,6 +79,64 @@ class _PropMean(torch.autograd.Function):
         return _prop_mean(ctx.A, g, ctx.K), None, None
 
 
+class _RowTags:
+    """Batch-row tags for the tagged propagation: row r is in the batch when
+    row_tag[r] == *tag_dev; `mark` bumps the device tag and tags the batch's rows
+    (two device ops, no host sync: graph-capture safe)."""
+
+    def __init__(self, n: int, device):
+        self.row_tag = torch.zeros(n, dtype=torch.int32, device=device)
+        self.tag_dev = torch.zeros(1, dtype=torch.int32, device=device)
+
+    def mark(self, rows: torch.Tensor):
+        self.tag_dev.add_(1)
+        self.row_tag[rows] = self.tag_dev
+
+
+class _PropMeanRows(torch.autograd.Function):
+    """mean_{k=0..K} A^k x for a symmetric A, needed at the tagged rows only (K <= 4;
+    the batch rows of the SMORE training loss): E^1..E^{K-1} stored (no running sum),
+    the last layer and the mean on the tagged rows only, in the running sum's order
+    (((E0 + E1) + E2) + E3) + A E3 (other rows of the output are left unwritten).  The
+    backward is Horner on the incoming gradient G, which is zero off the tagged rows:
+    H = G + A H from H = G, the first layer gathering only the tagged rows of G, every
+    layer reading G on the tagged rows only, the last scaled by 1/(K+1) (the dense
+    path's arithmetic: the same mean operator applied to G)."""
+
+    @staticmethod
+    def forward(ctx, x, A, K, tags):
+        x = x.contiguous()
+        n, d = x.shape
+        out = torch.empty_like(x)
+        hs = torch.empty(max(K - 1, 1), n, d, dtype=torch.float32, device=x.device)
+        cur = x
+        for k in range(1, K):
+            A.spmm_epi(cur, ops.epi(L.RSX_EPI_STORE, y=hs[k - 1]), d)
+            cur = hs[k - 1]
+        stored = dict(zip(("s_in", "r_add", "aux", "e0"), [x] + [hs[i] for i in range(K - 1)]))
+        e = ops.epi(L.RSX_EPI_FINAL, beta=1.0 / (K + 1), f=out, row_tag=tags.row_tag, tag_dev=tags.tag_dev, **stored)
+        e.tag_flags = L.RSX_TAG_ROWS
+        A.spmm_epi(cur, e, d)
+        ctx.A, ctx.K, ctx.tags = A, K, tags
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        A, K, tags = ctx.A, ctx.K, ctx.tags
+        g = g.contiguous()
+        d = g.shape[1]
+        bufs = torch.empty(2, *g.shape, dtype=torch.float32, device=g.device)
+        h = g
+        for k in range(1, K + 1):
+            y = bufs[k & 1]
+            e = ops.epi(L.RSX_EPI_ADD, beta=1.0 / (K + 1) if k == K else 1.0, y=y, s_in=g, row_tag=tags.row_tag,
+                        tag_dev=tags.tag_dev)
+            e.tag_flags = L.RSX_TAG_SPARSE_S | (L.RSX_TAG_SPARSE_X if k == 1 else 0)
+            A.spmm_epi(h, e, d)
+            h = y
+        return h, None, None, None
+
+
 def knn_graph(feat: np.ndarray, k: int):
     """build_sim + build_knn_normalized_graph(sparse, 'sym') (src/utils/utils.py:134-181) on the CPU,
     float32 as the reference: cosine similarities, top-k per row, deg = sum of kept values,
@@ -281,6 +339,7 @@ class SMORE(GeneralRecommender):
         # training loss on the batch rows only (rsx_smore_batch_rows: False = full tables)
         self.batch_rows = bool(config.get("rsx_smore_batch_rows", True))
         self._bidx = {}
+        self._tags = None
         # dropout masks of the fused preference block: a hash of (seed, call, row,
         # feature); the seed word lives on the device and advances once per training
         # forward (graph-capture safe).  Derived from the config seed, not torch's RNG,
@@ -346,14 +405,21 @@ class SMORE(GeneralRecommender):
             return self._forward_all_fused(train)
         return self._forward_all_torch(train)
 
-    def _views_fused(self, train=False):
-        """Everything before the preference block: (content, image, text, fusion tables, dropout seed)."""
+    def _views_fused(self, train=False, rows=None):
+        """Everything before the preference block: (content, image, text, fusion tables,
+        dropout seed).  With `rows` (the batch rows) content is exact on those rows only."""
         cv, ct, cf = self._projected_spectrum()
         item_id = self.item_id_embedding.weight
         img_i, txt_i, fus_i = SF.gates(cv, ct, cf, item_id, self.gate_v, self.gate_t, self.gate_f,
                                        self.inject_scale, self.inject_mode == "mul")
         ego = torch.cat([self.user_embedding.weight, item_id], dim=0)
-        content = _PropMean.apply(ego, self.norm_adj_csr, self.n_ui_layers)
+        if rows is not None and 1 <= self.n_ui_layers <= 4:
+            if self._tags is None:
+                self._tags = _RowTags(self.n_users + self.n_items, self.device)
+            self._tags.mark(rows)
+            content = _PropMeanRows.apply(ego, self.norm_adj_csr, self.n_ui_layers, self._tags)
+        else:
+            content = _PropMean.apply(ego, self.norm_adj_csr, self.n_ui_layers)
         nu, L_ = self.n_users, self.n_layers
         image_embeds = SF.view_prop(img_i, self.image_graph, self.R, L_, nu)
         text_embeds = SF.view_prop(txt_i, self.text_graph, self.R, L_, nu)
@@ -435,8 +501,8 @@ class SMORE(GeneralRecommender):
         form (duplicate rows are computed once per occurrence, their gradients added)."""
         users, pos, neg = interaction[0], interaction[1], interaction[2]
         nu, B = self.n_users, users.numel()
-        content, image_embeds, text_embeds, fusion_embeds, seed = self._views_fused(train=True)
         rows = torch.cat([users, pos + nu, neg + nu])
+        content, image_embeds, text_embeds, fusion_embeds, seed = self._views_fused(train=True, rows=rows)
         all_c, side_c, content_c = SF.preference_rows(self, content, image_embeds, text_embeds, fusion_embeds,
                                                       rows, seed)
         self.global_step += 1

@@ -91,13 +91,16 @@ class _Spectral(torch.autograd.Function):
         L.check(lib.rsx_smore_unit_weights_bwd(p(part), part.numel() // (6 * nb), p(rv), p(rt), p(rf), d, normalize,
                                                p(grv), p(grt), p(grf), ops._stream()), "rsx_smore_unit_weights_bwd")
         need = ctx.needs_input_grad
-        gV = gi @ Wv if need[0] else None
-        gWv = _wgrad(gi, V) if need[1] else None
-        gbv = gi.sum(0) if need[2] else None
-        gT = gt @ Wt if need[3] else None
-        gWt = _wgrad(gt, T) if need[4] else None
-        gbt = gt.sum(0) if need[5] else None
-        return gV, gWv, gbv, gT, gWt, gbt, grv, grt, grf, None
+        grads = []
+        for g, X, Wx, k in ((gi, V, Wv, 0), (gt, T, Wt, 3)):
+            if need[k] and need[k + 1] and ops.linear_bwd_supported(g.shape[1], X.shape[1]):
+                # d W, d X and d b in one pass over the rows (rsx_linear_bwd)
+                dW, dX, db = ops.linear_bwd(g, X, Wx, bias=need[k + 2])
+                grads += [dX, dW, db]
+            else:
+                grads += [g @ Wx if need[k] else None, _wgrad(g, X) if need[k + 1] else None,
+                          g.sum(0) if need[k + 2] else None]
+        return (*grads, grv, grt, grf, None)
 
 
 def spectral(V, Wv, bv, T, Wt, bt, wv, wt, wf, normalize=True):

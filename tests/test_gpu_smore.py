@@ -157,6 +157,41 @@ def test_smore_batch_rows_loss_equals_full_tables(tmp_path, golden, fx, p_drop):
         np.testing.assert_allclose(ga[n], gb[n], rtol=0, atol=2e-5 * scale, err_msg=n)
 
 
+@pytest.mark.parametrize("K,d", [(1, 64), (2, 64), (3, 128), (4, 64), (4, 128)])
+def test_prop_mean_rows_vs_dense(cuda, K, d):
+    """The tagged mean propagation of the SMORE training loss (_PropMeanRows: stored
+    layers, last layer + mean on the batch rows) equals the dense one (_PropMean) bit
+    for bit on the batch rows; its Horner backward from a gradient that is zero off
+    the batch rows equals the dense backward within f32 reassociation."""
+    from rsx import graph, ops, synth
+    from rsx.smore import _PropMean, _PropMeanRows, _RowTags
+
+    df = synth.amazon_like(2500, 700, 25000, seed=11)
+    tr = df[df.x_label == 0]
+    nu, ni = int(df.userID.max()) + 1, 700
+    rp, col, val = graph.smore_norm_adj(tr.userID.values.astype(np.int64), tr.itemID.values.astype(np.int64), nu, ni)
+    A = ops.DeviceCSR(rp, col, val, nu + ni, cuda, 32)
+    assert A.n_long > 0
+    gen = torch.Generator().manual_seed(K * 100 + d)
+    x = torch.randn(nu + ni, d, generator=gen).to(cuda).requires_grad_()
+    users = torch.randint(0, nu, (300,), generator=gen)
+    items = torch.randint(0, ni, (600,), generator=gen)
+    items[:50] = int(np.argmax(np.bincount(tr.itemID.values, minlength=ni)))  # a hub row, repeated
+    rows = torch.cat([users, nu + items]).to(cuda)
+    tags = _RowTags(nu + ni, cuda)
+    tags.mark(torch.arange(nu + ni, device=cuda)[:7])  # stale tags of an earlier batch
+    tags.mark(rows)
+    out_t = _PropMeanRows.apply(x, A, K, tags)
+    out_d = _PropMean.apply(x, A, K)
+    assert torch.equal(out_t[rows], out_d[rows])
+    g = torch.zeros(nu + ni, d, device=cuda)
+    g[rows] = torch.randn(rows.numel(), d, generator=gen).to(cuda)
+    gt, = torch.autograd.grad(out_t, x, g)
+    gd, = torch.autograd.grad(out_d, x, g)
+    scale = gd.abs().max().item()
+    np.testing.assert_allclose(gt.cpu().numpy(), gd.cpu().numpy(), rtol=0, atol=2e-6 * scale)
+
+
 @pytest.mark.parametrize("fx", list(FIXTURES))
 def test_smore_one_epoch_with_mirror_gradient(tmp_path, golden, fx):
     from rsx.trainer import Trainer
@@ -260,6 +295,30 @@ def test_linear_wgrad_vs_torch(cuda, n, o, i):
     scale = (g.abs().double().t() @ x.abs().double()).float()
     assert torch.all((got - want).abs() <= 2e-6 * scale + 1e-6), (got - want).abs().max()
     assert torch.equal(got, ops.linear_wgrad(g, x))  # deterministic
+
+
+@pytest.mark.parametrize("n,o,i", [(7050, 64, 4096), (7050, 64, 384), (23033, 128, 768), (1000, 128, 96),
+                                   (37, 32, 64), (513, 32, 160), (0, 64, 64)])
+def test_linear_bwd_vs_torch(cuda, n, o, i):
+    """rsx_linear_bwd (the projections' whole backward in one pass): dW = g^T x,
+    dx = g W and db = colsum g against f64 products (tolerance relative to the
+    magnitude of each sum); deterministic."""
+    from rsx import ops
+
+    gen = torch.Generator(device="cpu").manual_seed(n + 7 * o + i)
+    g = torch.randn(n, o, generator=gen).to(cuda)
+    x = torch.randn(n, i, generator=gen).to(cuda)
+    W = torch.randn(o, i, generator=gen).to(cuda)
+    dw, dx, db = ops.linear_bwd(g, x, W)
+    gd, xd, Wd = g.double(), x.double(), W.double()
+    for got, want, scale in ((dw, gd.t() @ xd, gd.abs().t() @ xd.abs()), (dx, gd @ Wd, gd.abs() @ Wd.abs()),
+                             (db, gd.sum(0), gd.abs().sum(0))):
+        assert got.shape == want.shape
+        assert torch.all((got.double() - want).abs() <= 2e-6 * scale + 1e-6), (got.double() - want).abs().max()
+    dw2, dx2, db2 = ops.linear_bwd(g, x, W)
+    assert torch.equal(dw, dw2) and torch.equal(dx, dx2) and torch.equal(db, db2)
+    _, _, none = ops.linear_bwd(g, x, W, bias=False)
+    assert none is None
 
 
 def test_rsx_linear_matches_nn_linear(cuda):
