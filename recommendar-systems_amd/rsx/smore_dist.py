@@ -276,6 +276,69 @@ class ShardedSMORE(nn.Module):
             dist.all_reduce(h, group=self.group)
             p.grad.copy_(h.to(p.grad.device))
 
+    # -- training with the model-level mirror gradient ----------------------------
+    @torch.no_grad()
+    def mg_alpha(self, params, grads, base, lr, rel_step, max_scale):
+        """alpha_eff of the reference's mirror gradient (src/common/trainer.py:290-307)
+        over the GLOBAL parameter vector: sums of squares of the row-sharded tensors
+        all-reduced, the replicated ones counted once, then the reference's arithmetic
+        (rms values rounded to f32 as its float() of f32 tensors, the rest in f64)."""
+        dev = params[0].device
+        sh = torch.zeros(3, dtype=torch.float64, device=dev)  # sum g^2, sum p^2, numel (sharded)
+        rep = torch.zeros(3, dtype=torch.float64, device=dev)
+        names = {id(p): n for n, p in self.named_parameters()}
+        for p, g in zip(params, grads):
+            acc = sh if names.get(id(p)) in SHARDED else rep
+            acc[0] += g.double().pow(2).sum()
+            acc[1] += p.detach().double().pow(2).sum()
+            acc[2] += p.numel()
+        h = _host_if_gloo(sh, self.group).clone()
+        dist.all_reduce(h, group=self.group)
+        tot = h.to(dev) + rep
+        n = float(tot[2].item())
+        grad_rms = float(torch.tensor(float(tot[0].sqrt()), dtype=torch.float32) / (n ** 0.5))
+        param_rms = float(torch.tensor(float(tot[1].sqrt()), dtype=torch.float32) / (n ** 0.5) + 1e-12)
+        alpha = max(base, rel_step * param_rms / (lr * grad_rms + 1e-12))
+        return min(alpha, base * max_scale)
+
+    def train_batch(self, inter, opt, lr, step_id, mg_interval=3, mg_alpha=0.5, mg_beta=0.2, rel_step=1e-3,
+                    max_scale=20.0):
+        """One batch of the reference Trainer on a mirror-gradient model (src/common/
+        trainer.py:186-201, 244-336) over the process group: loss, backward, gradient
+        sync, Adam; then, when step_id % mg_interval == 0, the mirror gradient: g(theta)
+        again, theta' = theta - alpha lr g, g(theta') scaled by -beta, theta restored,
+        Adam.  `opt` holds this rank's parameters (Adam is per element, so the sharded
+        rows' update is the single-process update of those rows).  Returns 1/W of the
+        batch loss (a float)."""
+        opt.zero_grad(set_to_none=True)
+        loss = self.calculate_loss(inter)
+        value = float(loss.detach())
+        loss.backward()
+        self.sync_grads()
+        opt.step()
+        if mg_interval > 0 and step_id % mg_interval == 0:
+            opt.zero_grad(set_to_none=True)
+            self.calculate_loss(inter).backward()
+            self.sync_grads()
+            params = [p for p in self.parameters() if p.requires_grad and p.grad is not None]
+            grads = [p.grad.detach().clone() for p in params]
+            alpha = self.mg_alpha(params, grads, mg_alpha, lr, rel_step, max_scale)
+            with torch.no_grad():
+                for p, g in zip(params, grads):
+                    p.add_(-alpha * lr * g)
+            opt.zero_grad(set_to_none=True)
+            self.calculate_loss(inter).backward()
+            self.sync_grads()
+            with torch.no_grad():
+                for p in self.parameters():
+                    if p.requires_grad and p.grad is not None:
+                        p.grad.mul_(-mg_beta)
+                for p, g in zip(params, grads):
+                    p.add_(+alpha * lr * g)
+            opt.step()
+            opt.zero_grad(set_to_none=True)
+        return value
+
     @torch.no_grad()
     def full_sort_topk_local(self, k: int, mask_rowptr, mask_col):
         """Top-k item ids of this rank's users (global user ids ua..ub-1, in order)."""

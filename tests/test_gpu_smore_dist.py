@@ -99,3 +99,62 @@ def test_sharded_smore_hip_matches_single_process(cuda, fx):
         assert not bad, bad
         assert np.array_equal(x["got"], res[0]["got"])
         assert np.abs(x["got"] - x["want"]).max() <= 1e-4
+
+
+def _mg_worker(rank, world, port, root, out, fx):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import rsx_oracle as O
+    import test_gpu_smore as T
+    from rsx.smore_dist import SHARDED, HipSmoreBackend, ShardedSMORE, graphs_from_rsx
+
+    z, c, train, valid, test = T._setup(Path(root) / f"r{rank}", _golden, fx)
+    m = T._model(c, train)
+    m.train()
+    trip = torch.from_numpy(z["epoch0_triplets"][:, :512].astype(np.int64)).cuda()
+    params = {n: p.detach().clone() for n, p in m.named_parameters()}
+    cfg = dict(reg_weight=c["reg_weight"], batch_size=c["train_batch_size"], n_ui_layers=c["n_ui_layers"],
+               n_layers=c["n_layers"], cl_loss=c["cl_loss"], cl_temp=m.cl_temp, dropout_rate=0.0)
+    sm = ShardedSMORE(params, graphs_from_rsx(m), m.n_users, m.n_items, cfg, HipSmoreBackend("cuda:0"))
+    sm.train()
+    lr = c["learning_rate"]
+    opt = torch.optim.Adam(sm.parameters(), lr=lr)
+    losses = [sm.train_batch(trip, opt, lr, s + 1, mg_interval=1, mg_alpha=m.mg_alpha, mg_beta=m.mg_beta)
+              for s in range(2)]
+    m.mg_interval = 1
+    ref_opt = torch.optim.Adam(m.parameters(), lr=lr)
+    ref_losses = [O.smore_train_batch(m, ref_opt, trip, lr) for _ in range(2)]
+    (ua, ub), (ia, ib) = sm.own_u, sm.own_i
+    ref_params = dict(m.named_parameters())
+    err = {}
+    for n, p in sm.named_parameters():
+        want = ref_params[n].detach()
+        part = SHARDED.get(n)
+        if part == "u":
+            want = want[ua:ub]
+        elif part == "i":
+            want = want[ia:ib]
+        err[n] = (p.detach() - want).abs().max().item()
+    np.savez(os.path.join(out, f"r{rank}.npz"), loss=np.array(losses) * world, ref=np.array(ref_losses),
+             names=np.array(list(err)), errs=np.array(list(err.values())))
+    dist.destroy_process_group()
+
+
+def test_sharded_smore_hip_mirror_gradient(cuda):
+    """Two batches with the mirror gradient firing on each (mg_interval 1) on 2 ranks
+    with the HIP backend against the single-process rsx SMORE run through the
+    oracle's Trainer batch (smore_train_batch): losses, and every parameter's rows
+    within 1e-4 (Adam's first steps move each element by about lr)."""
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "oracle"))
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "out")
+        os.makedirs(out)
+        mp.spawn(_mg_worker, args=(world, _free_port(), d, out, "smore_small"), nprocs=world, join=True)
+        res = [dict(np.load(os.path.join(out, f"r{r}.npz"))) for r in range(world)]
+    for x in res:
+        np.testing.assert_allclose(x["loss"], x["ref"], rtol=2e-5)
+        bad = {n: e for n, e in zip(x["names"], x["errs"]) if not e <= 1e-4}
+        assert not bad, bad

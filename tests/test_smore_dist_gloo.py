@@ -159,3 +159,41 @@ def test_sharded_smore_step_matches_single_process(world):
                 assert np.array_equal(x["p." + name], p), name
         _close(g, ref_g[name], "grad " + name)
         np.testing.assert_allclose(p, ref_p[name], rtol=0, atol=2e-6, err_msg=name)
+
+
+def _mg_worker(rank, world, port, out, steps):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from rsx.smore_dist import ShardedSMORE
+
+    _, init, graphs, batch, nu, ni = reference_setup()
+    sm = ShardedSMORE(init, graphs, nu, ni, dict(reg_weight=1e-5, batch_size=2048, n_ui_layers=4, n_layers=1),
+                      TorchSmoreBackend())
+    opt = torch.optim.Adam(sm.parameters(), lr=1e-3)
+    losses = [sm.train_batch(batch, opt, 1e-3, step + 1, mg_interval=1) for step in range(steps)]
+    params = {n: p.detach().clone().numpy() for n, p in sm.named_parameters()}
+    np.savez(os.path.join(out, f"r{rank}.npz"), loss=np.array(losses), **{"p." + k: v for k, v in params.items()})
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_smore_mirror_gradient_matches_single_process(world):
+    """Two batches with the model-level mirror gradient firing on each (mg_interval 1):
+    the sharded model's loss and every parameter (rows concatenated over the ranks)
+    against the oracle's single-process Trainer batch (smore_train_batch)."""
+    from rsx.smore_dist import SHARDED
+
+    steps = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_mg_worker, args=(world, _free_port(), d, steps), nprocs=world, join=True)
+        res = [dict(np.load(os.path.join(d, f"r{r}.npz"))) for r in range(world)]
+    m, _, _, batch, nu, ni = reference_setup()
+    m.mg_interval = 1
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+    ref_losses = [O.smore_train_batch(m, opt, batch, 1e-3) for _ in range(steps)]
+    np.testing.assert_allclose(sum(x["loss"] for x in res), ref_losses, rtol=1e-5)
+    for name, p in m.named_parameters():
+        want = p.detach().numpy()
+        got = np.concatenate([x["p." + name] for x in res]) if name in SHARDED else res[0]["p." + name]
+        np.testing.assert_allclose(got, want, rtol=0, atol=2e-5, err_msg=name)
