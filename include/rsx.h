@@ -78,6 +78,18 @@ int rsx_csr_schedule_host(const int64_t* rowptr_host, int64_t n_rows, int32_t ch
                           int32_t* work_host, int32_t* long_host,
                           int64_t* n_work, int64_t* n_long, int64_t* n_slots);
 
+/*
+ * The work schedule of a CSR built on the device, without a host round trip, for a
+ * graph whose every row holds at most as many nonzeros as the same row of a template
+ * CSR with a schedule (a per-epoch edge-dropout graph, reference
+ * src/models/layergcn.py:51-81, against the full training graph): the template's
+ * layout is kept (same n_work / n_long / n_slots / long_rows / slab), `work`
+ * [tmpl->n_work][4] receives the new begin/end of every item; a long row's chunks past
+ * its new end are empty (they contribute zero partials).  rowptr: device, the new
+ * graph's [n_rows + 1].
+ */
+int rsx_csr_schedule_rebind(const rsx_csr* tmpl, const int64_t* rowptr, int32_t* work, rsx_stream_t stream);
+
 /* ------------------------------------------------------------------------ */
 /* SpMM with fused row epilogues                                              */
 /* ------------------------------------------------------------------------ */

@@ -561,6 +561,28 @@ __global__ RSX_SPMM_ATTR __launch_bounds__(kBlock) void spmm_main(rsx_csr a, con
     }
 }
 
+// The schedule of a CSR whose rows are a subset of a template's nonzeros (every row's
+// degree <= the template's: an edge-dropout graph of the template) in the template's
+// work layout: whole rows keep their item, a long row keeps its chunk items and its
+// fixup (the chunks past the row's new end become empty items: zero partials).
+__global__ __launch_bounds__(256) void schedule_rebind_kernel(rsx_csr t, const int64_t* __restrict__ rp,
+                                                              int32_t* __restrict__ work) {
+    const int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (w >= t.n_work) return;
+    const int4 wk = reinterpret_cast<const int4*>(t.work)[w];
+    int4 out;
+    if (wk.y < 0) {
+        out = make_int4(wk.x, -1, (int)rp[wk.x], (int)rp[wk.x + 1]);
+    } else {
+        const int4 lr = reinterpret_cast<const int4*>(t.long_rows)[wk.x];
+        const int64_t e = rp[lr.x + 1];
+        int64_t b = rp[lr.x] + (int64_t)(wk.y - lr.y) * t.chunk;
+        if (b > e) b = e;
+        out = make_int4(wk.x, wk.y, (int)b, (int)(b + t.chunk < e ? b + t.chunk : e));
+    }
+    reinterpret_cast<int4*>(work)[w] = out;
+}
+
 // acc = 0 for every row (stand-alone Adam, K = 0 forward, first LayerGCN backward step).
 template <int D, int KIND>
 __global__ __launch_bounds__(kBlock) void rowwise_kernel(int64_t n_rows, rsx_epilogue e) {
@@ -727,6 +749,14 @@ int rsx_csr_schedule_host(const int64_t* rowptr_host, int64_t n_rows, int32_t ch
     *n_long = nl;
     *n_slots = ns;
     return RSX_OK;
+}
+
+int rsx_csr_schedule_rebind(const rsx_csr* tmpl, const int64_t* rowptr, int32_t* work, rsx_stream_t stream) {
+    if (!tmpl || !rowptr || !work || !tmpl->work || (tmpl->n_long > 0 && !tmpl->long_rows)) return RSX_ERR_ARG;
+    if (tmpl->n_work == 0) return RSX_OK;
+    hipLaunchKernelGGL(rsx::schedule_rebind_kernel, dim3((unsigned)((tmpl->n_work + 255) / 256)), dim3(256), 0,
+                       rsx::as_stream(stream), *tmpl, rowptr, work);
+    return rsx::last_rc();
 }
 
 int rsx_spmm(const rsx_csr* a, const float* x, int32_t d, const rsx_epilogue* epi, float* slab,

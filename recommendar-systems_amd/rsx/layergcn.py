@@ -148,6 +148,7 @@ class DeviceEdgeDropout:
         self.t_rowptr = torch.from_numpy(rowptr).to(self.device)
         self.t_col = torch.from_numpy(cols[order].astype(np.int32)).to(self.device)
         self.t_eid = torch.from_numpy(eid[order].astype(np.int64)).to(self.device)
+        self._tmpl = None
 
     def keep_mask(self, keep_len: int, pruning_random: bool) -> torch.Tensor:
         if pruning_random:
@@ -182,9 +183,19 @@ class DeviceEdgeDropout:
         return rowptr, col[:nnz], val[:nnz]
 
     def epoch_graph(self, dropout: float, pruning_random: bool) -> "ops.DeviceCSR":
+        """The epoch's masked graph.  Its work schedule is rewritten on the device over
+        the layout of the full training graph's (every masked row is a subset of the
+        template row: rsx_csr_schedule_rebind), so the rebuild has no host round trip;
+        RSX_EPOCH_SCHEDULE=host schedules it on the host from a copy of rowptr."""
         keep_len = int(self.n_edges * (1.0 - dropout))
         rowptr, col, val = self.build(self.keep_mask(keep_len, pruning_random), keep_len)
-        return ops.DeviceCSR.from_device(rowptr, col, val, self.n_users + self.n_items, self.chunk)
+        if os.environ.get("RSX_EPOCH_SCHEDULE", "device") == "host":
+            return ops.DeviceCSR.from_device(rowptr, col, val, self.n_users + self.n_items, self.chunk)
+        if self._tmpl is None:  # the full symmetric template's schedule (host, once)
+            self._tmpl = ops.DeviceCSR(self.t_rowptr.cpu().numpy(), self.t_col.to(torch.int32).contiguous(),
+                                       torch.zeros(self.t_col.numel(), dtype=torch.float32, device=self.device),
+                                       self.n_users + self.n_items, self.device, self.chunk)
+        return ops.DeviceCSR.rebind(self._tmpl, rowptr, col, val)
 
 
 def reference_edge_dropout(edge_indices: torch.Tensor, edge_values: torch.Tensor, dropout: float,

@@ -102,6 +102,34 @@ class DeviceCSR:
         return cls(rowptr.cpu().numpy(), col, val, n_cols, col.device, chunk)
 
     @classmethod
+    def rebind(cls, tmpl: "DeviceCSR", rowptr: torch.Tensor, col: torch.Tensor, val: torch.Tensor) -> "DeviceCSR":
+        """A device-built CSR whose every row has at most the template's nonzeros (an
+        edge-dropout graph of it) on the template's work layout: the schedule is
+        rewritten on the device (rsx_csr_schedule_rebind), nothing comes to the host,
+        and the template's long-row table and partial-sum slabs are shared (a graph
+        and its template must not run in the same launch)."""
+        self = cls.__new__(cls)
+        self.device = tmpl.device
+        self.n_rows, self.n_cols, self.chunk = tmpl.n_rows, tmpl.n_cols, tmpl.chunk
+        self.nnz = int(col.numel())
+        self.n_work, self.n_long, self.n_slots = tmpl.n_work, tmpl.n_long, tmpl.n_slots
+        self.rowptr_host = None
+        self.rowptr = rowptr.contiguous()
+        if col.dtype != torch.int32 or val.dtype != torch.float32 or not (col.is_contiguous() and val.is_contiguous()):
+            raise RuntimeError("DeviceCSR.rebind: contiguous int32 col / float32 val expected")
+        self.col, self.val = col, val
+        self.work = torch.empty_like(tmpl.work)
+        L.check(L.lib().rsx_csr_schedule_rebind(C.byref(tmpl.struct), _p(self.rowptr), _p(self.work), _stream()),
+                "rsx_csr_schedule_rebind")
+        self.long_rows = tmpl.long_rows
+        self.struct = L.Csr(self.n_rows, self.n_cols, self.nnz, self.rowptr.data_ptr(), self.col.data_ptr(),
+                            self.val.data_ptr(), self.chunk, 0, self.n_work, self.work.data_ptr(), self.n_long,
+                            self.long_rows.data_ptr(), self.n_slots)
+        self._slabs = tmpl._slabs
+        self._tmpl = tmpl
+        return self
+
+    @classmethod
     def from_scipy(cls, m, device, chunk: int = 32):
         m = m.tocsr()
         m.sort_indices()

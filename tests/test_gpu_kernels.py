@@ -379,6 +379,39 @@ def test_device_edge_dropout_graph_equals_host_builder(cuda, seed):
         x = torch.randn(nu + ni, 64, device=cuda)
         ref = torch.sparse_csr_tensor(A.rowptr, A.col.long(), A.val, (nu + ni, nu + ni)).to_dense() @ x
         assert torch.allclose(A.spmm(x), ref, rtol=1e-5, atol=1e-6)
+        # the device-rebound schedule (template layout) == a fresh host schedule, bit for bit
+        assert A.rowptr_host is None and A.n_long > 0
+        B = ops.DeviceCSR.from_device(A.rowptr, A.col, A.val, nu + ni, 32)
+        for d in (32, 64, 128):
+            xd = torch.randn(nu + ni, d, device=cuda)
+            assert torch.equal(A.spmm(xd), B.spmm(xd)), d
+
+
+@pytest.mark.parametrize("drop", [0.1, 0.5, 0.97])
+def test_schedule_rebind_on_random_subgraphs(cuda, drop):
+    """rsx_csr_schedule_rebind: a CSR whose rows are random subsets of a template's
+    (long rows that shrink below a chunk or to nothing included) multiplied on the
+    rebound template layout equals the product on its own host schedule, bit for bit."""
+    rng = np.random.default_rng(int(drop * 100))
+    n = 1500
+    deg = np.minimum(rng.zipf(1.3, n), 700)
+    rows = np.repeat(np.arange(n), deg)
+    cols = rng.integers(0, n, rows.size)
+    t_rp = np.zeros(n + 1, np.int64)
+    t_rp[1:] = np.cumsum(deg)
+    T = ops.DeviceCSR(t_rp, cols.astype(np.int32), np.ones(rows.size, np.float32), n, cuda, 32)
+    keep = rng.random(rows.size) >= drop
+    keep[t_rp[np.argmax(deg)]:t_rp[np.argmax(deg) + 1]] = False  # the largest hub loses every edge
+    rp = np.zeros(n + 1, np.int64)
+    rp[1:] = np.cumsum(np.bincount(rows[keep], minlength=n))
+    col = torch.from_numpy(cols[keep].astype(np.int32)).to(cuda)
+    val = torch.from_numpy(rng.standard_normal(int(keep.sum())).astype(np.float32)).to(cuda)
+    A = ops.DeviceCSR.rebind(T, torch.from_numpy(rp).to(cuda), col, val)
+    B = ops.DeviceCSR(rp, col, val, n, cuda, 32)
+    assert T.n_long > 0 and B.n_work <= A.n_work
+    for d in (64, 256):
+        x = torch.randn(n, d, device=cuda)
+        assert torch.equal(A.spmm(x), B.spmm(x)), d
 
 
 @pytest.mark.parametrize("K,d", [(2, 64), (3, 64), (3, 128), (2, 256), (3, 32)])
