@@ -387,7 +387,7 @@ def main():
     dev = torch.device("cuda", local)
 
     from rsx.engine import LightGCNEngine
-    from rsx import graph, ops
+    from rsx import _lib as L, graph, ops
 
     torch.manual_seed(999 + rank)
     if big:  # xavier_uniform_ bound for [n, d]: sqrt(6 / (n + d)); drawn on the device
@@ -533,13 +533,51 @@ def main():
     spmm_ms = time_kernel(run_parts, 50)
     alg = spmm_bytes(nu + ni, nnz, d)
     achieved = alg / (spmm_ms * 1e-3) / 1e9
-    traffic = None
-    tfile = os.path.join(HERE, "profiles", "spmm_traffic.json")
-    if os.path.exists(tfile) and args.workload == "c2" and not sharded:  # PMC bytes measured for the C2 launch
-        try:
-            traffic = json.load(open(tfile)).get("bytes_per_launch")
-        except Exception:  # noqa: BLE001
-            traffic = None
+
+    def pmc_bytes(name):  # PMC bytes per launch measured for the C2 kernel (profiles/*.json)
+        tfile = os.path.join(HERE, "profiles", name)
+        if os.path.exists(tfile) and args.workload == "c2" and not sharded:
+            try:
+                return json.load(open(tfile)).get("bytes_per_launch")
+            except Exception:  # noqa: BLE001
+                return None
+        return None
+
+    traffic = pmc_bytes("spmm_traffic.json")
+    store = {"bound": "hbm", "kernel": f"spmm_main<{d},STORE> (hub-row fixups in-launch) one propagation layer",
+             "launches_per_step": 2 if not sharded else None,
+             "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+             "traffic": traffic, "algorithmic_bytes_per_launch": alg, "avg_launch_ms": spmm_ms,
+             "note": ("the sports/baby working set (<50 MB) is Infinity-Cache resident" if not big else
+                      "C4 shard: tables of GBs, gathers from HBM")}
+    roof, kernels = store, [store]
+    if not sharded:
+        # the step's largest single launch: the last backward layer with Adam fused into
+        # its epilogue, exactly as the tagged step issues it (rows of the last batch
+        # tagged; sparse G' and clears on those rows), on scratch copies of p, m, v
+        pc, mc, vc, gc = eng.p.clone(), eng.m.clone(), eng.v.clone(), eng.g.clone()
+        adam_e = ops.epi(L.RSX_EPI_ADAM, s_in=gc, p=pc, m=mc, v=vc, zero0=gc, row_tag=eng.row_tag,
+                         adam=ops.adam_struct(eng.lr, max(eng.step_count, 1)))
+        adam_e.tag = max(eng.step_count, 1)
+        adam_e.tag_flags = L.RSX_TAG_SPARSE_S | L.RSX_TAG_SPARSE_R | L.RSX_TAG_ZERO
+        xh = eng.h1
+
+        def adam_layer():
+            eng.adj.spmm_epi(xh, adam_e, d)
+
+        adam_ms = time_kernel(adam_layer, 50)
+        # S_spmm + Adam's row streams (reads p, m, v; writes m, v: p's write
+        # is S's Y) = S + 20 N d; G' is read on the batch rows only (+ 12 B d per row)
+        adam_alg = alg + 20 * (nu + ni) * d + 12 * 3 * args.batch * d
+        adam_ach = adam_alg / (adam_ms * 1e-3) / 1e9
+        roof = {"bound": "hbm", "kernel": f"spmm_main<{d},ADAM> (last backward layer + Adam, batch-row tags; "
+                                          "the step's largest launch)",
+                "launches_per_step": 1, "achieved": adam_ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": adam_ach / HBM_PEAK_GBS, "traffic": pmc_bytes("spmm_adam_traffic.json"),
+                "algorithmic_bytes_per_launch": adam_alg, "avg_launch_ms": adam_ms,
+                "note": store["note"]}
+        kernels = [roof, store]
+        del pc, mc, vc, gc
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -579,12 +617,8 @@ def main():
                          "kernel_ms_all_eval_users": fs_ms,
                          "kernel_tflops": fs_flops / (fs_ms * 1e-3) / 1e12,
                          "mfma_f32_peak_tflops": 157.3},
-            "roofline": {"bound": "hbm", "kernel": f"spmm_main<{d},STORE> (hub-row fixups in-launch) one propagation layer",
-                         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "algorithmic_bytes_per_launch": alg, "avg_launch_ms": spmm_ms,
-                         "note": ("the sports/baby working set (<50 MB) is Infinity-Cache resident" if not big else
-                                  "C4 shard: tables of GBs, gathers from HBM")},
+            "roofline": roof,
+            "roofline_kernels": kernels,
             "cpu_baseline": cpu,
             "epoch": epoch_rate,
             "gpu_ms_per_step_events": gpu_ms / args.steps,
