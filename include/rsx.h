@@ -195,6 +195,9 @@ typedef struct rsx_epilogue {
     const float* reg_k;
     /* optional: the tag is read from device memory (graph-captured steps) */
     const int32_t* tag_dev;
+    /* ADAM (optional): when *halt != 0 the parameters and moments are left unchanged
+     * (a NaN loss stopped training, rsx_lgcn_step.halt) */
+    const int32_t* halt;
 } rsx_epilogue;
 
 #define RSX_TAG_ROWS 1
@@ -362,6 +365,11 @@ typedef struct rsx_lgcn_step {
      * per-row occurrence counts (+ a done counter and three scales in the tail) that
      * the Adam layer applies and clears; R is not used. */
     int32_t* reg_cnt;
+    /* Optional with reg_cnt: [2] int32, zero-filled.  The first step whose loss is NaN
+     * sets halt[0] = 1 and halt[1] = its tag; from then on the Adam layer leaves the
+     * parameters and moments unchanged, so they stay those of the last finite step (the
+     * reference checks the loss before backward and stops, src/common/trainer.py:201-203). */
+    int32_t* halt;
 } rsx_lgcn_step;
 
 int rsx_lightgcn_step(const rsx_lgcn_step* st, rsx_stream_t stream);

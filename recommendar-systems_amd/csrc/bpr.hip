@@ -36,6 +36,8 @@ struct BprArgs {
     double* part;    // [n_blocks][4]
     int32_t* reg_cnt;  // bpr_fused: [n_rows][3] occurrence counts + [4] tail (done counter, ku, kp, kn)
     int64_t n_rows;
+    int32_t* halt;     // bpr_fused (optional): [2] set to {1, tag} by the first NaN loss
+    int32_t tag;
 };
 
 __device__ __forceinline__ float softplus_neg(float x) {
@@ -360,13 +362,18 @@ __global__ __launch_bounds__(kBprBlock) void bpr_fused(BprArgs a) {
         k[2] = nn > 0 ? (float)((double)a.reg / (B * nn)) : 0.f;
         if (a.loss_out) a.loss_out[0] = (float)loss;
         if (a.loss_acc) a.loss_acc[0] += loss;
+        if (a.halt && loss != loss && a.halt[0] == 0) {
+            a.halt[1] = a.tag;
+            a.halt[0] = 1;
+        }
         *done = 0;  // re-armed for the next launch (stream order)
     }
 }
 
 int bpr_fused_call(const float* fin, const float* ego, int64_t n_users, int64_t n_items, int32_t d,
                    const int64_t* trip, int64_t batch, float reg, float g_div, float* g_fin, int32_t* reg_cnt,
-                   float* loss_out, double* loss_acc, void* ws, size_t ws_bytes, hipStream_t s);
+                   float* loss_out, double* loss_acc, void* ws, size_t ws_bytes, hipStream_t s,
+                   int32_t* halt = nullptr, int32_t tag = 0);
 
 template <int D>
 static int launch_bpr(const BprArgs& a, hipStream_t s) {
@@ -425,7 +432,8 @@ int bpr_call(int32_t variant, const float* fin, const float* ego, int64_t n_user
 
 int bpr_fused_call(const float* fin, const float* ego, int64_t n_users, int64_t n_items, int32_t d,
                    const int64_t* trip, int64_t batch, float reg, float g_div, float* g_fin, int32_t* reg_cnt,
-                   float* loss_out, double* loss_acc, void* ws, size_t ws_bytes, hipStream_t s) {
+                   float* loss_out, double* loss_acc, void* ws, size_t ws_bytes, hipStream_t s, int32_t* halt,
+                   int32_t tag) {
     if (!fin || !ego || !trip || !g_fin || !reg_cnt || batch <= 0 || !ws) return RSX_ERR_ARG;
     if (ws_bytes < bpr_ws(batch)) return RSX_ERR_WORKSPACE;
     BprArgs a = {};
@@ -447,6 +455,8 @@ int bpr_fused_call(const float* fin, const float* ego, int64_t n_users, int64_t 
     a.part = reinterpret_cast<double*>(w + (((size_t)batch * sizeof(float) + 255) & ~(size_t)255));
     a.reg_cnt = reg_cnt;
     a.n_rows = n_users + n_items;
+    a.halt = halt;
+    a.tag = tag;
     switch (d) {
         case 32: hipLaunchKernelGGL((bpr_fused<32>), dim3((unsigned)((batch + 31) / 32)), dim3(kBprBlock), 0, s, a); break;
         case 64: hipLaunchKernelGGL((bpr_fused<64>), dim3((unsigned)((batch + 15) / 16)), dim3(kBprBlock), 0, s, a); break;

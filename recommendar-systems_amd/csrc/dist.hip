@@ -37,7 +37,8 @@ int bpr_call(int32_t variant, const float* fin, const float* ego, int64_t n_user
              float* loss_out, double* loss_acc, void* ws, size_t ws_bytes, hipStream_t s, float g_div = 1.f);
 int bpr_fused_call(const float* fin, const float* ego, int64_t n_users, int64_t n_items, int32_t d,
                    const int64_t* trip, int64_t batch, float reg, float g_div, float* g_fin, int32_t* reg_cnt,
-                   float* loss_out, double* loss_acc, void* ws, size_t ws_bytes, hipStream_t s);
+                   float* loss_out, double* loss_acc, void* ws, size_t ws_bytes, hipStream_t s, int32_t* halt = nullptr,
+                   int32_t tag = 0);
 
 namespace {
 

@@ -169,9 +169,11 @@ __device__ __forceinline__ void epilogue(const rsx_epilogue& e, int64_t row, flo
         g.y = adam_elem(c, p.y, m.y, v.y, g.y);
         g.z = adam_elem(c, p.z, m.z, v.z, g.z);
         g.w = adam_elem(c, p.w, m.w, v.w, g.w);
-        st4(e.p + off, p);
-        st4(e.m + off, m);
-        st4(e.v + off, v);
+        if (!(e.halt && *e.halt)) {  // a NaN loss halted training: parameters stay as they are
+            st4(e.p + off, p);
+            st4(e.m + off, m);
+            st4(e.v + off, v);
+        }
         if (e.g_out) st4(e.g_out + off, g);
     } else if constexpr (KIND == RSX_EPI_LAYERGCN) {
         // F.cosine_similarity(z, e0, dim=-1, eps=1e-8) = <z/max(|z|,eps), e/max(|e|,eps)>

@@ -124,7 +124,8 @@ __global__ __launch_bounds__(256) void tag_rows_kernel(const int64_t* __restrict
 
 int bpr_fused_call(const float* fin, const float* ego, int64_t n_users, int64_t n_items, int32_t d,
                    const int64_t* trip, int64_t batch, float reg, float g_div, float* g_fin, int32_t* reg_cnt,
-                   float* loss_out, double* loss_acc, void* ws, size_t ws_bytes, hipStream_t s);
+                   float* loss_out, double* loss_acc, void* ws, size_t ws_bytes, hipStream_t s, int32_t* halt = nullptr,
+                   int32_t tag = 0);
 
 int tag_rows(const int64_t* trip, int64_t batch, int64_t n_users, int32_t* row_tag, int32_t tag, hipStream_t s,
              const int32_t* tag_dev) {
@@ -227,7 +228,8 @@ static int lgcn_step_stored_layers(const rsx_lgcn_step& st, int64_t batch, int32
     }
     if (st.reg_cnt) {  // one launch; the regulariser gradient as occurrence counts for the Adam layer
         if ((rc = bpr_fused_call(st.final_emb, st.p, st.n_users, st.n_items, d, st.triplets, batch, st.reg,
-                                 (float)(K + 1), st.g, st.reg_cnt, st.loss_out, st.loss_acc, st.ws, st.ws_bytes, s)))
+                                 (float)(K + 1), st.g, st.reg_cnt, st.loss_out, st.loss_acc, st.ws, st.ws_bytes, s,
+                                 st.halt, tag)))
             return rc;
     } else if ((rc = bpr_call(RSX_BPR_LIGHTGCN, st.final_emb, st.p, st.n_users, st.n_items, d, st.triplets, batch,
                               st.reg, (float)batch, st.g, st.r, st.loss_out, st.loss_acc, st.ws, st.ws_bytes, s,
@@ -264,6 +266,7 @@ static int lgcn_step_stored_layers(const rsx_lgcn_step& st, int64_t batch, int32
     e.row_tag = st.row_tag;
     e.tag = tag;
     e.tag_flags = RSX_TAG_SPARSE_S | RSX_TAG_SPARSE_R | RSX_TAG_ZERO;
+    e.halt = st.reg_cnt ? st.halt : nullptr;  // set by the one-launch BPR above
     return spmm_dispatch(A, x, d, e, st.slab, s);
 }
 

@@ -51,7 +51,7 @@ class Epilogue(C.Structure):
                 ("y", P), ("s_in", P), ("s_out", P), ("f", P), ("zero0", P), ("zero1", P), ("r_add", P),
                 ("p", P), ("m", P), ("v", P), ("g_out", P), ("e0", P), ("aux", P), ("aux_w", P),
                 ("adam", Adam), ("row_tag", P), ("tag", I32), ("tag_flags", I32), ("reg_cnt", P), ("reg_k", P),
-                ("tag_dev", P)]
+                ("tag_dev", P), ("halt", P)]
 
 
 RSX_TAG_ROWS = 1
@@ -72,7 +72,7 @@ class LgcnStep(C.Structure):
                 ("p", P), ("m", P), ("v", P), ("s", P), ("h0", P), ("h1", P), ("final_emb", P), ("g", P),
                 ("r", P), ("slab", P), ("triplets", P), ("batch", I64), ("sample", C.POINTER(SamplerArgs)),
                 ("adam", Adam), ("loss_out", P), ("loss_acc", P), ("ws", P), ("ws_bytes", C.c_size_t),
-                ("row_tag", P), ("tag", I64), ("reg_cnt", P)]
+                ("row_tag", P), ("tag", I64), ("reg_cnt", P), ("halt", P)]
 
 
 class ShardedStep(C.Structure):

@@ -222,3 +222,13 @@ class LightGCN(GeneralRecommender):
     @property
     def device_loss_acc(self):
         return self.engine.loss_acc
+
+    @property
+    def device_halt(self):
+        """(halt flag [2] int32 on the device, engine step count) of the single engine's
+        tagged step: {1, tag of the step} once a batch loss was NaN (the parameters stay
+        those of the last finite step), or None where the step has no flag."""
+        e = self.engine
+        if self.sharded or not getattr(e, "use_tags", False) or not getattr(e, "use_reg_cnt", False):
+            return None
+        return e.halt, e.step_count

@@ -10,8 +10,11 @@ Training pass, two modes:
 * fused (model.supports_fused_step and config rsx_fused_step, no classic mirror
   gradient): `model.fused_step(batch, lr)` per batch — forward, loss, backward
   and Adam on the device; the loss is summed on the device and read once per
-  epoch (the reference syncs `loss.item()` every batch, trainer.py:196-200; a
-  NaN loss therefore stops training at the end of the epoch, not mid-epoch);
+  epoch (the reference syncs `loss.item()` every batch, trainer.py:196-200).  A
+  NaN batch loss sets the step's device halt flag (LightGCN's tagged step): its
+  own and every later Adam update of the epoch are skipped, so the parameters are
+  those of the batch before it, as in the reference, which checks before backward
+  and stops (trainer.py:201-203); the epoch-end read reports that batch index;
 * autograd: calculate_loss / backward / torch optimizer exactly as the
   reference, including classic MG (`mg=True`) and the model-level mirror
   gradient (model.mg_enable, trainer.py:268-348).
@@ -264,10 +267,18 @@ class Trainer:
             dist.all_reduce(tot)
             total = float(tot.item())
         else:
+            halt = getattr(self.model, "device_halt", None)
             for batch in train_data:
                 self.model.fused_step(batch, lr)
                 n += 1
             total = float(acc.item())  # one host sync per epoch
+            if halt is not None:
+                flag, s0 = halt  # (device flag, engine step count before this epoch)
+                h = flag.cpu().tolist()
+                if h[0]:  # the step's NaN gate: the batch, and the parameters of the batch before it
+                    b = h[1] - s0 - 1
+                    self.logger.info(f"Loss is nan at epoch: {epoch_idx}, batch index: {b}. Exiting.")
+                    return torch.tensor(float("nan")), torch.tensor(0.0)
         if np.isnan(total):
             self.logger.info(f"Loss is nan at epoch: {epoch_idx}. Exiting.")
             return torch.tensor(float("nan")), torch.tensor(0.0)

@@ -455,6 +455,42 @@ def test_batch_row_tags_equal_dense_step(cuda, K, d):
     np.testing.assert_allclose(a.forward().cpu().numpy(), b.forward().cpu().numpy(), rtol=0, atol=1e-6)
 
 
+def test_nan_loss_halts_the_fused_step(cuda):
+    """A batch whose loss is NaN sets the tagged step's halt flag to {1, its tag}; that
+    step's Adam update and every later one are skipped, so p / m / v stay bit for bit
+    those after the last finite batch (the reference stops before backward)."""
+    from rsx import synth
+    from rsx.engine import LightGCNEngine
+
+    df = synth.amazon_like(2000, 600, 20000, seed=8)
+    tr = df[df.x_label == 0]
+    tu, ti = tr.userID.values.astype(np.int64), tr.itemID.values.astype(np.int64)
+    nu, ni = int(df.userID.max()) + 1, 600
+    torch.manual_seed(9)
+    U0 = torch.nn.init.xavier_uniform_(torch.empty(nu, 64)).numpy()
+    I0 = torch.nn.init.xavier_uniform_(torch.empty(ni, 64)).numpy()
+    eng = LightGCNEngine(tu, ti, nu, ni, 64, 3, 1e-2, 1e-3, cuda, U0, I0, seed=0, batch=512)
+    assert eng.use_tags and eng.use_reg_cnt
+    g = torch.Generator().manual_seed(3)
+    trip = lambda: torch.stack([torch.randint(0, nu, (512,), generator=g), torch.randint(0, ni, (512,), generator=g),  # noqa: E731
+                                torch.randint(0, ni, (512,), generator=g)]).to(cuda)
+    for _ in range(2):
+        eng.step(triplets=trip())
+    torch.cuda.synchronize()
+    assert eng.halt.tolist() == [0, 0]
+    eng.p[5, 3] = float("nan")  # user 5's row poisons any batch that holds user 5
+    snap = [x.clone() for x in (eng.p, eng.m, eng.v)]
+    bad = trip()
+    bad[0, 7] = 5
+    eng.step(triplets=bad)
+    eng.step(triplets=trip())
+    torch.cuda.synchronize()
+    assert eng.halt.tolist() == [1, 3]
+    assert np.isnan(eng.loss_out.item())
+    for a, b in zip((eng.p, eng.m, eng.v), snap):
+        assert torch.equal(a.view(torch.int32), b.view(torch.int32))
+
+
 def test_tagged_step_vs_fixture(cuda, golden):
     """The engine's default step (batch-row tags, stored layers, one-launch BPR with the
     regulariser as counts) against the reference's first LightGCN step (fixture)."""

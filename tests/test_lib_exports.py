@@ -5,6 +5,7 @@ import os
 import re
 
 import numpy as np
+import pytest
 
 from rsx import _lib as L
 
@@ -27,14 +28,25 @@ def test_exports_every_declared_symbol():
     assert lib.rsx_version().decode().startswith("rsx ")
 
 
-def test_struct_layouts_match_header():
-    # sizes the C compiler gives these structs on x86-64 (checked by hand against rsx.h)
-    assert C.sizeof(L.Csr) == 8 * 3 + 8 * 3 + 4 * 2 + 8 + 8 + 8 + 8 + 8
-    assert C.sizeof(L.Adam) == 4 * 6 + 8 + 8
-    assert C.sizeof(L.Epilogue) == 4 * 4 + 8 * 14 + C.sizeof(L.Adam) + 8 + 4 + 4 + 8 + 8 + 8
-    # gcc on include/rsx.h: sizeof(rsx_lgcn_step) = 240, sizeof(rsx_sharded_lgcn_step) = 320
-    assert C.sizeof(L.LgcnStep) == 240
-    assert C.sizeof(L.ShardedStep) == 320
+def test_struct_layouts_match_header(tmp_path):
+    """The ctypes mirrors have the sizes gcc gives the C structs of include/rsx.h (a
+    field added on one side only shifts every later field)."""
+    import shutil
+    import subprocess
+
+    cc = shutil.which("gcc") or shutil.which("cc")
+    if cc is None:
+        pytest.skip("no C compiler")
+    inc = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "include")
+    src = tmp_path / "sz.c"
+    src.write_text('#include "rsx.h"\n#include <stdio.h>\nint main(void){printf("%zu %zu %zu %zu %zu %zu",'
+                   ' sizeof(rsx_csr), sizeof(rsx_adam), sizeof(rsx_epilogue), sizeof(rsx_lgcn_step),'
+                   ' sizeof(rsx_sharded_lgcn_step), sizeof(rsx_sampler_args)); return 0;}\n')
+    exe = tmp_path / "sz"
+    subprocess.run([cc, "-I", inc, str(src), "-o", str(exe)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    assert got == [C.sizeof(L.Csr), C.sizeof(L.Adam), C.sizeof(L.Epilogue), C.sizeof(L.LgcnStep),
+                   C.sizeof(L.ShardedStep), C.sizeof(L.SamplerArgs)]
 
 
 def test_comm_unique_id_size():
