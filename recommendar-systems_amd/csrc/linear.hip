@@ -10,6 +10,7 @@
 // strip over its rows (fp32 MFMA, exact f32 fma chains, next chunk prefetched, one
 // g value feeding IG MFMAs) and writes it to its partial slot; a second pass adds
 // the slots in a fixed order.  Deterministic: the result depends only on the shapes.
+#include <cstdlib>
 #include <type_traits>
 
 #include "rsx_common.hpp"
@@ -35,7 +36,13 @@ struct WgPlan {
     int slots() const { return splits * rw; }
 };
 
-static WgPlan wg_plan(int64_t n, int out_dim, int in_dim, int max_ig = 4) {
+static int lin_env(const char* name, int dflt) {
+    const char* v = getenv(name);
+    const int x = v ? atoi(v) : 0;
+    return x > 0 ? x : dflt;
+}
+
+static WgPlan wg_plan(int64_t n, int out_dim, int in_dim, int max_ig = 4, int64_t target_waves = kWgTargetWaves) {
     WgPlan p;
     const int it = in_dim / 32, ot = out_dim / 32;
     p.ig = (it % 4 == 0 && max_ig >= 4) ? 4 : (it % 2 == 0 && max_ig >= 2) ? 2 : 1;
@@ -44,7 +51,7 @@ static WgPlan wg_plan(int64_t n, int out_dim, int in_dim, int max_ig = 4) {
     p.nob = ot / p.otb;
     p.nib = it / p.ig;
     const int64_t grid_waves = p.nob * p.nib * 4;
-    int64_t s = (kWgTargetWaves + grid_waves - 1) / grid_waves;
+    int64_t s = (target_waves + grid_waves - 1) / grid_waves;
     // partials: at most a quarter of the input bytes (or 4 MB)
     const int64_t in_bytes = n * (int64_t)(out_dim + in_dim) * 4;
     const int64_t slot_bytes = (int64_t)out_dim * in_dim * 4;
@@ -295,11 +302,19 @@ extern "C" size_t rsx_linear_wgrad_ws_bytes(int64_t n, int32_t out_dim, int32_t 
 }
 
 // the fused backward stages a W slice too: IC <= 64 keeps two blocks per CU in LDS
-constexpr int kBwdMaxIg = 2;
+// (RSX_LBWD_IG / RSX_LBWD_WAVES: tuning overrides)
+static int bwd_ig() {
+    static const int v = lin_env("RSX_LBWD_IG", 2);
+    return v;
+}
+static int64_t bwd_waves() {
+    static const int v = lin_env("RSX_LBWD_WAVES", kWgTargetWaves);
+    return v;
+}
 
 extern "C" size_t rsx_linear_bwd_ws_bytes(int64_t n, int32_t out_dim, int32_t in_dim) {
     if (n <= 0 || (out_dim != 32 && out_dim != 64 && out_dim != 128) || in_dim <= 0 || (in_dim % 32)) return 0;
-    const WgPlan p = wg_plan(n, out_dim, in_dim, kBwdMaxIg);
+    const WgPlan p = wg_plan(n, out_dim, in_dim, bwd_ig(), bwd_waves());
     return (size_t)p.slots() * ((size_t)out_dim * (size_t)in_dim + (size_t)out_dim) * sizeof(float);
 }
 
@@ -321,7 +336,7 @@ extern "C" int rsx_linear_bwd(const float* g, const float* x, const float* W, in
         return last_rc();
     }
     if (ws_bytes < rsx_linear_bwd_ws_bytes(n, out_dim, in_dim) || !ws) return RSX_ERR_WORKSPACE;
-    const WgPlan p = wg_plan(n, out_dim, in_dim, kBwdMaxIg);
+    const WgPlan p = wg_plan(n, out_dim, in_dim, bwd_ig(), bwd_waves());
     if (p.nob != 1) return RSX_ERR_UNSUPPORTED;
     float* part = static_cast<float*>(ws);
     const dim3 grid((unsigned)(p.nob * p.nib * p.splits));
