@@ -220,11 +220,18 @@ def bench_model(args):
         one_step()
     torch.cuda.synchronize()
     n = 0
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    ev0.record()
     for _ in range(args.steps):
         n += one_step()
+    ev1.record()
+    t_issue = time.perf_counter() - t0
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
+    log(f"[bench] {w['model']}: {wall * 1e3 / args.steps:.3f} ms/step wall, host issue {t_issue * 1e3 / args.steps:.3f} "
+        f"ms/step, events {ev0.elapsed_time(ev1) / args.steps:.3f} ms/step, graph replays "
+        f"{getattr(getattr(t, '_graph', None), 'replays', None)}")
     model.eval()
     t.evaluate(valid)
     torch.cuda.synchronize()
