@@ -209,6 +209,15 @@ typedef struct rsx_epilogue {
 int rsx_spmm(const rsx_csr* a, const float* x, int32_t d, const rsx_epilogue* epi,
              float* slab, rsx_stream_t stream);
 
+/* Up to 4 independent products Y_p = A_p X_p of one epilogue kind (STORE, ADD or
+ * AXPBY) and one width d in a single launch (SMORE's three item views through their
+ * kNN graphs, or through R: src/models/smore.py:299-317): every product's work
+ * blocks, then every product's hub-row fixups.  Each product is exactly what
+ * rsx_spmm(a[p], x[p], d, &epis[p], slabs[p]) computes (no product may write
+ * another's inputs). */
+int rsx_spmm_batch(int32_t count, const rsx_csr* const* a, const float* const* x, int32_t d,
+                   const rsx_epilogue* epis, float* const* slabs, rsx_stream_t stream);
+
 /* Row-wise epilogue with acc = 0 over rows [0, n_rows): e.g. a stand-alone Adam
  * step (kind RSX_EPI_ADAM, s_in = grad, beta = 1) — torch.optim.Adam in
  * src/common/trainer.py:133,238 — or the K = 0 forward. */

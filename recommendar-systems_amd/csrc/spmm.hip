@@ -516,6 +516,10 @@ __device__ __forceinline__ void spmm_item(const rsx_csr& a, const float* __restr
     }
 }
 
+template <int D, int KIND>
+__device__ __forceinline__ void spmm_main_body(const rsx_csr& a, const float* __restrict__ x, const rsx_epilogue& e,
+                                               float* __restrict__ slab, int64_t n_main, int64_t bid);
+
 // Work blocks [0, n_main): each group walks work items w, w + n_main*GPB, ...
 // (the next descriptor is loaded before the current item is processed); blocks
 // [n_main, n_main + n_long) are the long rows' fixups (fix_only: every block is one).
@@ -546,8 +550,49 @@ __global__ RSX_SPMM_ATTR __launch_bounds__(kBlock) void spmm_main(rsx_csr a, con
         fixup_block<D, KIND>(a, e, slab, (int64_t)blockIdx.x - n_main);
         return;
     }
+    spmm_main_body<D, KIND>(a, x, e, slab, n_main, (int64_t)blockIdx.x);
+}
+
+// Up to kBatchMax independent products of one epilogue kind and width in ONE launch
+// (SMORE's three item views through their kNN graphs, or through R): every
+// problem's work blocks first, then every problem's hub-row fixup blocks, so no
+// fixup can be dispatched ahead of the partials it waits for.
+constexpr int kBatchMax = 4;
+struct SpmmBatch {
+    rsx_csr a[kBatchMax];
+    const float* x[kBatchMax];
+    rsx_epilogue e[kBatchMax];
+    float* slab[kBatchMax];
+    int64_t n_main[kBatchMax];
+    int64_t main_off[kBatchMax + 1];
+    int64_t fix_off[kBatchMax + 1];
+    int32_t count;
+};
+
+template <int D, int KIND>
+__global__ __launch_bounds__(kBlock) void spmm_batch(SpmmBatch b) {
+    int64_t bid = blockIdx.x;
+    const int64_t nm = b.main_off[b.count];
+    int p = 0;
+    if (bid < nm) {
+        while (p + 1 < b.count && bid >= b.main_off[p + 1]) ++p;
+        spmm_main_body<D, KIND>(b.a[p], b.x[p], b.e[p], b.slab[p], b.n_main[p], bid - b.main_off[p]);
+        return;
+    }
+    bid -= nm;
+    while (p + 1 < b.count && bid >= b.fix_off[p + 1]) ++p;
+    fixup_block<D, KIND>(b.a[p], b.e[p], b.slab[p], bid - b.fix_off[p]);
+}
+
+// The work blocks of spmm_main: block `bid` of n_main walks work items w, w + n_main*GPB, ...
+template <int D, int KIND>
+__device__ __forceinline__ void spmm_main_body(const rsx_csr& a, const float* __restrict__ x, const rsx_epilogue& e,
+                                               float* __restrict__ slab, int64_t n_main, int64_t bid) {
+    constexpr int G = D / 4;
+    constexpr int GPB = kBlock / G;
+    const int li = threadIdx.x % G;
     const int64_t stride = n_main * GPB;
-    int64_t w = (int64_t)blockIdx.x * GPB + threadIdx.x / G;
+    int64_t w = bid * GPB + threadIdx.x / G;
     if (w >= a.n_work) return;  // whole groups leave together
     const int4* work = reinterpret_cast<const int4*>(a.work);
     int4 wk = work[w];
@@ -629,6 +674,42 @@ static int launch_spmm(const rsx_csr& a, const float* x, const rsx_epilogue& e, 
         hipLaunchKernelGGL((spmm_main<D, KIND>), dim3((unsigned)a.n_long), dim3(kBlock), 0, s, a, x, e, slab,
                            n_main, 1, TagJob{});
     return last_rc();
+}
+
+template <int D, int KIND>
+static int launch_batch(SpmmBatch& b, hipStream_t s) {
+    constexpr int GPB = kBlock / (D / 4);
+    int64_t nm = 0, nf = 0;
+    for (int p = 0; p < b.count; ++p) {
+        int64_t n_main = (b.a[p].n_work + GPB - 1) / GPB;
+        if (n_main > spmm_max_blocks()) n_main = spmm_max_blocks();
+        b.n_main[p] = n_main;
+        b.main_off[p] = nm;
+        b.fix_off[p] = nf;
+        nm += n_main;
+        nf += b.a[p].n_long;
+    }
+    b.main_off[b.count] = nm;
+    b.fix_off[b.count] = nf;
+    if (nf > kInlineFixups) {  // too many fixup blocks to ride along: one launch per product
+        for (int p = 0; p < b.count; ++p) {
+            const int rc = launch_spmm<D, KIND>(b.a[p], b.x[p], b.e[p], b.slab[p], s, TagJob{});
+            if (rc) return rc;
+        }
+        return 0;
+    }
+    if (nm + nf > 0) hipLaunchKernelGGL((spmm_batch<D, KIND>), dim3((unsigned)(nm + nf)), dim3(kBlock), 0, s, b);
+    return last_rc();
+}
+
+template <int D>
+static int batch_d(SpmmBatch& b, int kind, hipStream_t s) {
+    switch (kind) {
+        case RSX_EPI_STORE: return launch_batch<D, RSX_EPI_STORE>(b, s);
+        case RSX_EPI_ADD: return launch_batch<D, RSX_EPI_ADD>(b, s);
+        case RSX_EPI_AXPBY: return launch_batch<D, RSX_EPI_AXPBY>(b, s);
+        default: return RSX_ERR_UNSUPPORTED;
+    }
 }
 
 template <int D, int KIND>
@@ -765,6 +846,32 @@ int rsx_spmm(const rsx_csr* a, const float* x, int32_t d, const rsx_epilogue* ep
              rsx_stream_t stream) {
     if (!a || !x || !epi) return RSX_ERR_ARG;
     return rsx::spmm_dispatch(*a, x, d, *epi, slab, rsx::as_stream(stream));
+}
+
+int rsx_spmm_batch(int32_t count, const rsx_csr* const* a, const float* const* x, int32_t d, const rsx_epilogue* epis,
+                   float* const* slabs, rsx_stream_t stream) {
+    using namespace rsx;
+    if (count < 0 || count > kBatchMax || (count > 0 && (!a || !x || !epis || !slabs))) return RSX_ERR_ARG;
+    if (count == 0) return RSX_OK;
+    SpmmBatch b{};
+    b.count = count;
+    const int kind = epis[0].kind;
+    for (int p = 0; p < count; ++p) {
+        if (!a[p] || !x[p] || epis[p].kind != kind) return RSX_ERR_ARG;
+        if (a[p]->n_long > 0 && !slabs[p]) return RSX_ERR_WORKSPACE;
+        b.a[p] = *a[p];
+        b.x[p] = x[p];
+        b.e[p] = epis[p];
+        b.slab[p] = slabs[p];
+    }
+    hipStream_t s = as_stream(stream);
+    switch (d) {
+        case 32: return batch_d<32>(b, kind, s);
+        case 64: return batch_d<64>(b, kind, s);
+        case 128: return batch_d<128>(b, kind, s);
+        case 256: return batch_d<256>(b, kind, s);
+        default: return RSX_ERR_UNSUPPORTED;
+    }
 }
 
 int rsx_rowwise(int64_t n_rows, int32_t d, const rsx_epilogue* epi, rsx_stream_t stream) {

@@ -99,6 +99,7 @@ def _declare(lib):
         "rsx_csr_schedule_host": (C.c_int, [P, I64, I32, P, P, C.POINTER(I64), C.POINTER(I64), C.POINTER(I64)]),
         "rsx_spmm": (C.c_int, [C.POINTER(Csr), P, I32, C.POINTER(Epilogue), P, P]),
         "rsx_csr_schedule_rebind": (C.c_int, [C.POINTER(Csr), P, P, P]),
+        "rsx_spmm_batch": (C.c_int, [I32, P, P, I32, P, P, P]),
         "rsx_rowwise": (C.c_int, [I64, I32, C.POINTER(Epilogue), P]),
         "rsx_bpr_ws_bytes": (C.c_size_t, [I64]),
         "rsx_bpr": (C.c_int, [I32, P, P, I64, I64, I32, P, I64, F32, F32, P, P, P, P, P, C.c_size_t, P]),
@@ -161,7 +162,7 @@ def _declare(lib):
         fn.argtypes = args
 
 
-EXPORTED = ["rsx_version", "rsx_csr_schedule_host", "rsx_csr_schedule_rebind", "rsx_spmm", "rsx_rowwise", "rsx_bpr_ws_bytes", "rsx_bpr",
+EXPORTED = ["rsx_version", "rsx_csr_schedule_host", "rsx_csr_schedule_rebind", "rsx_spmm_batch", "rsx_spmm", "rsx_rowwise", "rsx_bpr_ws_bytes", "rsx_bpr",
             "rsx_fullsort_ws_bytes", "rsx_fullsort_plan", "rsx_fullsort_topk", "rsx_score_dense", "rsx_sample_triplets",
             "rsx_gather_rows", "rsx_lightgcn_step", "rsx_lightgcn_forward", "rsx_sample_epoch",
             "rsx_smore_spectral_spec_floats", "rsx_smore_spectral_fwd_ws_bytes", "rsx_smore_spectral_fwd",

@@ -136,15 +136,18 @@ class DeviceCSR:
         return cls(m.indptr.astype(np.int64), m.indices.astype(np.int32), m.data.astype(np.float32), m.shape[1],
                    device, chunk)
 
-    def slab(self, d: int):
+    def slab(self, d: int, k: int = 0):
+        """The partial-sum slab for width d (k > 0: another one, for a second product
+        over this graph in the same launch)."""
         if self.n_slots == 0:
             return None
-        s = self._slabs.get(d)
+        key = d if k == 0 else (d, k)
+        s = self._slabs.get(key)
         if s is None:
             # partial-sum slots, then one int32 arrival counter per long row (zero; the
             # kernel re-arms them), see rsx_spmm in include/rsx.h
             s = torch.zeros(self.n_slots * d + self.n_long, dtype=torch.float32, device=self.device)
-            self._slabs[d] = s
+            self._slabs[key] = s
         return s
 
     def spmm_epi(self, x: torch.Tensor, epi: "L.Epilogue", d: int):
@@ -160,6 +163,24 @@ class DeviceCSR:
         y = out if out is not None else torch.empty(self.n_rows, d, dtype=torch.float32, device=x.device)
         self.spmm_epi(x, epi(L.RSX_EPI_STORE, alpha=alpha, y=y), d)
         return y
+
+
+def spmm_batch(csrs, xs, epis, d: int):
+    """Y_p = A_p X_p with epilogue epis[p] for up to 4 products in one launch (rsx_spmm_batch)."""
+    n = len(csrs)
+    for x in xs:
+        _gpu(x)
+    arr_a = (C.c_void_p * n)(*[C.addressof(a.struct) for a in csrs])
+    arr_x = (C.c_void_p * n)(*[x.data_ptr() for x in xs])
+    arr_e = (L.Epilogue * n)(*epis)
+    seen = {}
+    slabs = []
+    for a in csrs:  # a graph used twice in one launch: a slab per product
+        k = seen.get(id(a), 0)
+        seen[id(a)] = k + 1
+        slabs.append(_pi(a.slab(d, k)))
+    arr_s = (C.c_void_p * n)(*slabs)
+    L.check(L.lib().rsx_spmm_batch(n, arr_a, arr_x, d, arr_e, arr_s, _stream()), "rsx_spmm_batch")
 
 
 def epi(kind: int, alpha: float = 1.0, beta: float = 1.0, adam: "L.Adam | None" = None, **ptrs) -> "L.Epilogue":

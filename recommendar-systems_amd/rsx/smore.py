@@ -340,6 +340,7 @@ class SMORE(GeneralRecommender):
         self.batch_rows = bool(config.get("rsx_smore_batch_rows", True))
         self._bidx = {}
         self._tags = None
+        self.batch_views = bool(config.get("rsx_smore_batch_views", True))
         # dropout masks of the fused preference block: a hash of (seed, call, row,
         # feature); the seed word lives on the device and advances once per training
         # forward (graph-capture safe).  Derived from the config seed, not torch's RNG,
@@ -421,9 +422,13 @@ class SMORE(GeneralRecommender):
         else:
             content = _PropMean.apply(ego, self.norm_adj_csr, self.n_ui_layers)
         nu, L_ = self.n_users, self.n_layers
-        image_embeds = SF.view_prop(img_i, self.image_graph, self.R, L_, nu)
-        text_embeds = SF.view_prop(txt_i, self.text_graph, self.R, L_, nu)
-        fusion_embeds = SF.view_prop(fus_i, self.fusion_graph, self.R, L_, nu)
+        if self.batch_views:  # the three views' products batched into shared launches
+            image_embeds, text_embeds, fusion_embeds = SF.view_prop3(
+                (img_i, txt_i, fus_i), (self.image_graph, self.text_graph, self.fusion_graph), self.R, L_, nu)
+        else:
+            image_embeds = SF.view_prop(img_i, self.image_graph, self.R, L_, nu)
+            text_embeds = SF.view_prop(txt_i, self.text_graph, self.R, L_, nu)
+            fusion_embeds = SF.view_prop(fus_i, self.fusion_graph, self.R, L_, nu)
         if self.training and self.dropout.p > 0:
             seed = self._drop_seed.clone()
             self._drop_seed.add_(1)

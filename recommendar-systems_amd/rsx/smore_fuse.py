@@ -255,6 +255,52 @@ def view_prop(x, G, R, n_layers, n_users):
     return _ViewProp.apply(x, G, R, int(n_layers), int(n_users))
 
 
+class _ViewProp3(torch.autograd.Function):
+    """The three item views (image, text, fusion) through _ViewProp's chain together:
+    each layer's three item-graph products, the three R products, and in the backward
+    the three R^T and item-graph transposes, each set as ONE rsx_spmm_batch launch."""
+
+    @staticmethod
+    def forward(ctx, x0, x1, x2, Gs, R, n_layers, n_users):
+        xs = [_c(x) for x in (x0, x1, x2)]
+        ni, d = xs[0].shape
+        outs = [torch.empty(n_users + ni, d, dtype=torch.float32, device=xs[0].device) for _ in range(3)]
+        cur = xs
+        for k in range(n_layers):
+            dst = [o[n_users:] if k == n_layers - 1 else torch.empty_like(x) for o, x in zip(outs, xs)]
+            ops.spmm_batch([G.A for G in Gs], cur, [ops.epi(L.RSX_EPI_STORE, y=y) for y in dst], d)
+            cur = dst
+        if n_layers == 0:
+            for o, x in zip(outs, xs):
+                o[n_users:].copy_(x)
+        ops.spmm_batch([R.A] * 3, [o[n_users:] for o in outs], [ops.epi(L.RSX_EPI_STORE, y=o[:n_users]) for o in outs],
+                       d)
+        ctx.Gs, ctx.R, ctx.L, ctx.nu = Gs, R, n_layers, n_users
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        nu = ctx.nu
+        ref = next(g for g in grads if g is not None)
+        gs = [_c(g) if g is not None else torch.zeros_like(ref) for g in grads]
+        d = ref.shape[1]
+        gi = [torch.empty_like(g[nu:]) for g in gs]
+        # d items = g_items + R^T g_users (ADD epilogue), the three views in one launch
+        ops.spmm_batch([ctx.R.AT] * 3, [g[:nu] for g in gs],
+                       [ops.epi(L.RSX_EPI_ADD, y=y, r_add=g[nu:]) for y, g in zip(gi, gs)], d)
+        for _ in range(ctx.L):
+            nxt = [torch.empty_like(x) for x in gi]
+            ops.spmm_batch([G.AT for G in ctx.Gs], gi, [ops.epi(L.RSX_EPI_STORE, y=y) for y in nxt], d)
+            gi = nxt
+        return gi[0], gi[1], gi[2], None, None, None, None
+
+
+def view_prop3(xs, Gs, R, n_layers, n_users):
+    """(image, text, fusion) [R G^L x; G^L x] tables of the three views (one launch per
+    layer for all three graphs, one for the three R products)."""
+    return _ViewProp3.apply(xs[0], xs[1], xs[2], tuple(Gs), R, int(n_layers), int(n_users))
+
+
 # ---------------------------------------------------------------------------
 # InfoNCE x 2
 # ---------------------------------------------------------------------------

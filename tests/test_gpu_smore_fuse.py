@@ -168,6 +168,37 @@ def test_view_prop_vs_torch(cuda):
         _close(gx, gi, f"grad L={L_}", 1e-5)
 
 
+@pytest.mark.parametrize("d,L_", [(64, 1), (128, 2), (64, 0)])
+def test_view_prop3_equals_three_view_props(cuda, d, L_):
+    """The three views batched into shared launches (rsx_spmm_batch; R used by all
+    three products of one launch, each with its own partial-sum slab) equal three
+    separate view_prop chains bit for bit, forward and backward, on graphs with hub
+    rows (in-launch fixups)."""
+    from rsx import smore_fuse as SF
+    from rsx.smore import _DevGraph
+
+    rng = np.random.default_rng(7 + d + L_)
+    nu, ni = 900, 400
+
+    def graph(nr, nc, nnz, zipf):
+        r = rng.integers(0, nr, nnz)
+        c = (rng.zipf(zipf, nnz) - 1) % nc
+        key = np.unique(r * nc + c, return_index=True)[1]
+        return _DevGraph(r[key], c[key], rng.random(key.size).astype(np.float32), nr, nc, cuda, 32)
+
+    Gs = [graph(ni, ni, 6000, 1.3), graph(ni, ni, 5000, 1.6), graph(ni, ni, 9000, 1.2)]
+    R = graph(nu, ni, 12000, 1.4)
+    assert R.AT.n_long > 0 and any(G.AT.n_long > 0 for G in Gs)
+    xs = [torch.randn(ni, d, device=cuda, requires_grad=True) for _ in range(3)]
+    ups = [torch.randn(nu + ni, d, device=cuda) for _ in range(3)]
+    outs = SF.view_prop3(xs, Gs, R, L_, nu)
+    g3 = torch.autograd.grad(sum((o * u).sum() for o, u in zip(outs, ups)), xs)
+    for x, G, o, u, g in zip(xs, Gs, outs, ups, g3):
+        o1 = SF.view_prop(x, G, R, L_, nu)
+        (g1,) = torch.autograd.grad((o1 * u).sum(), [x])
+        assert torch.equal(o, o1) and torch.equal(g, g1)
+
+
 def _infonce_ref(v1, v2, tau):
     """The reference's InfoNCE (smore.py:380-387)."""
     v1, v2 = F.normalize(v1, dim=1), F.normalize(v2, dim=1)
