@@ -383,6 +383,39 @@ typedef struct rsx_lgcn_step {
 
 int rsx_lightgcn_step(const rsx_lgcn_step* st, rsx_stream_t stream);
 
+/*
+ * One LayerGCN training batch (reference src/models/layergcn.py:127-177 with the
+ * autograd backward and src/common/trainer.py:238 Adam) as ONE call: K layers
+ * E^k = c_k * (A E^{k-1}) with c_k = cos(A E^{k-1}, E^0) (RSX_EPI_LAYERGCN, out =
+ * sum_k E^k; the pre-scale rows and c_k saved in zs[k-1] / cs[k-1]), BPR-sum + L2
+ * (RSX_BPR_LAYERGCN: g = d/d out, r = d reg / d E^0), the cosine-gate backward
+ * (RSX_EPI_LAYERGCN_BWD, rowwise for layer K, fused into the SpMMs of layers K-1..1),
+ * the last product fused with Adam.  `adj` is the epoch's (edge-dropout) training
+ * graph; g, r are zeroed by the last forward layer.  Same kernels and order as the
+ * Python-issued sequence, one host call instead of 2K + 3.
+ */
+typedef struct rsx_layergcn_step_args {
+    const rsx_csr* adj;
+    int64_t n_users, n_items;
+    int32_t d, n_layers;
+    float reg;
+    int32_t pad0;
+    float* p; float* m; float* v;
+    float* out; float* g; float* r; float* acc;
+    float* h0; float* h1;
+    float* const* zs;   /* [n_layers] -> [N, d] */
+    float* const* cs;   /* [n_layers] -> [N] */
+    float* slab;
+    const int64_t* triplets;  /* [3][batch] */
+    int64_t batch;
+    rsx_adam adam;
+    float* loss_out;    /* [1] or NULL */
+    double* loss_acc;   /* [1] or NULL */
+    void* ws; size_t ws_bytes;  /* >= rsx_bpr_ws_bytes(batch) */
+} rsx_layergcn_step_args;
+
+int rsx_layergcn_step(const rsx_layergcn_step_args* st, rsx_stream_t stream);
+
 /* Forward only (evaluation): final_emb = mean_k A^k p, using s, h0, h1 as scratch. */
 int rsx_lightgcn_forward(const rsx_csr* adj, int32_t d, int32_t n_layers, const float* p,
                          float* s, float* h0, float* h1, float* final_emb, float* slab,
@@ -576,13 +609,16 @@ int rsx_smore_infonce_bwd(const float* side, const float* content, const int64_t
  *     squares in f64, per-block partials reduced in order: deterministic);
  *   rsx_axpy_multi: y[i] += float(*alpha_dev * mult) * x[i] (the mirror step with
  *     mult = -lr, its restore with mult = +lr), one launch per 32 tensors.
+ * lr_dev (optional, device f64): the learning rate is read there instead (lr is
+ * ignored; axpy uses mult * *lr_dev), so a captured step stays valid when the
+ * LambdaLR schedule changes lr between epochs.
  */
 size_t rsx_mg_alpha_ws_bytes(int32_t count, const int64_t* n);
 int rsx_mg_alpha(int32_t count, const float* const* params, const float* const* grads, const int64_t* n,
                  double base, double lr, double rel_step, double max_scale, double* alpha_out, void* ws,
-                 size_t ws_bytes, rsx_stream_t stream);
+                 size_t ws_bytes, const double* lr_dev, rsx_stream_t stream);
 int rsx_axpy_multi(int32_t count, float* const* y, const float* const* x, const int64_t* n,
-                   const double* alpha_dev, double mult, rsx_stream_t stream);
+                   const double* alpha_dev, double mult, const double* lr_dev, rsx_stream_t stream);
 /*
  * SMORE's spectral filter weights (reference src/models/smore.py:221-229): three
  * [d/2+1][2] (re, im) parameters -> out [3][d/2+1][2], each w / (|w| + 1e-8) when
@@ -607,10 +643,12 @@ int rsx_adam_multi(int32_t count, float* const* p, const float* const* g, float*
                    float weight_decay, rsx_stream_t stream);
 /* The same with the gradient taken as g * grad_scale (an f32 product, as the
  * reference's p.grad.mul_(-mg_beta) before the mirror-gradient step,
- * src/common/trainer.py:327-330, folded into the update). */
+ * src/common/trainer.py:327-330, folded into the update); lr_dev (optional, device
+ * f64): the learning rate read on the device (rounded to f32) instead of lr. */
 int rsx_adam_multi_scaled(int32_t count, float* const* p, const float* const* g, float* const* m, float* const* v,
                           const int64_t* const* step_dev, const int64_t* n, float lr, float beta1, float beta2,
-                          float eps, float weight_decay, float grad_scale, rsx_stream_t stream);
+                          float eps, float weight_decay, float grad_scale, const double* lr_dev,
+                          rsx_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
 /* SMORE kNN item graph (knn.hip)                                             */

@@ -408,7 +408,7 @@ int bpr_call(int32_t variant, const float* fin, const float* ego, int64_t n_user
     if (variant != RSX_BPR_SMORE && !ego) return RSX_ERR_ARG;
     if (variant < 0 || variant > 2) return RSX_ERR_ARG;
     if (ws_bytes < bpr_ws(batch)) return RSX_ERR_WORKSPACE;
-    BprArgs a;
+    BprArgs a = {};
     a.variant = variant;
     a.fin = fin;
     a.ego = ego;

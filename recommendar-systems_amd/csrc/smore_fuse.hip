@@ -817,13 +817,14 @@ struct AdamList {
     int32_t count;
     float lr, beta1, beta2, eps, wd;
     float gscale;        // the gradient is g * gscale (f32 product, as torch's grad.mul_(s)); 1 = none
+    const double* lr_dev;  // if non-NULL the learning rate is read here (graph replays across lr changes)
 };
 
 __global__ __launch_bounds__(256) void adam_multi(AdamList L) {
     int t = 0;
     while (t + 1 < L.count && (int64_t)blockIdx.x >= L.blk[t + 1]) ++t;
     rsx_adam cfg;
-    cfg.lr = L.lr;
+    cfg.lr = L.lr_dev ? (float)*L.lr_dev : L.lr;
     cfg.beta1 = L.beta1;
     cfg.beta2 = L.beta2;
     cfg.eps = L.eps;
@@ -923,7 +924,7 @@ __global__ __launch_bounds__(256) void mg_sumsq(PairList L, double* partial) {
 constexpr int kMgFinal = 1024;
 __global__ __launch_bounds__(kMgFinal) void mg_alpha_final(const double* partial, int64_t n_blocks, int64_t numel,
                                                            double base, double lr, double rel, double max_scale,
-                                                           double* alpha) {
+                                                           double* alpha, const double* lr_dev) {
     double sg0 = 0.0, sp0 = 0.0, sg1 = 0.0, sp1 = 0.0;
     int64_t b = threadIdx.x;
     for (; b + kMgFinal < n_blocks; b += 2 * kMgFinal) {
@@ -954,6 +955,7 @@ __global__ __launch_bounds__(kMgFinal) void mg_alpha_final(const double* partial
     const float sq = (float)sqrt((double)numel);
     const double grad_rms = (double)((float)sqrt(sg) / sq);
     const double param_rms = (double)((float)sqrt(sp) / sq + 1e-12f);
+    if (lr_dev) lr = *lr_dev;
     double a = rel * param_rms / (lr * grad_rms + 1e-12);
     a = a > base ? a : base;  // Python max(base, x): keeps base when x is NaN
     const double cap = base * max_scale;
@@ -961,10 +963,10 @@ __global__ __launch_bounds__(kMgFinal) void mg_alpha_final(const double* partial
 }
 
 // y += float(alpha * mult) * x
-__global__ __launch_bounds__(256) void axpy_multi(PairList L, const double* alpha, double mult) {
+__global__ __launch_bounds__(256) void axpy_multi(PairList L, const double* alpha, double mult, const double* lr_dev) {
 #pragma clang fp contract(off)  // two roundings, as torch's mul then add_ (device code contracts by default)
     const int t = list_slot(L);
-    const float s = (float)(*alpha * mult);
+    const float s = (float)(*alpha * (lr_dev ? mult * *lr_dev : mult));
     const int64_t base = ((int64_t)blockIdx.x - L.blk[t]) * kAdamPerBlock;
     float* __restrict__ y = L.y[t];
     const float* __restrict__ x = L.x[t];
@@ -1276,12 +1278,14 @@ int rsx_smore_infonce_bwd(const float* side, const float* content, const int64_t
 int rsx_adam_multi(int32_t count, float* const* p, const float* const* g, float* const* m, float* const* v,
                    const int64_t* const* step_dev, const int64_t* n, float lr, float beta1, float beta2, float eps,
                    float weight_decay, rsx_stream_t stream) {
-    return rsx_adam_multi_scaled(count, p, g, m, v, step_dev, n, lr, beta1, beta2, eps, weight_decay, 1.f, stream);
+    return rsx_adam_multi_scaled(count, p, g, m, v, step_dev, n, lr, beta1, beta2, eps, weight_decay, 1.f, nullptr,
+                                 stream);
 }
 
 int rsx_adam_multi_scaled(int32_t count, float* const* p, const float* const* g, float* const* m, float* const* v,
                           const int64_t* const* step_dev, const int64_t* n, float lr, float beta1, float beta2,
-                          float eps, float weight_decay, float grad_scale, rsx_stream_t stream) {
+                          float eps, float weight_decay, float grad_scale, const double* lr_dev,
+                          rsx_stream_t stream) {
     if (count < 0 || (count > 0 && (!p || !g || !m || !v || !step_dev || !n))) return RSX_ERR_ARG;
     hipStream_t s = as_stream(stream);
     for (int32_t c0 = 0; c0 < count; c0 += sf::kAdamMax) {
@@ -1292,6 +1296,7 @@ int rsx_adam_multi_scaled(int32_t count, float* const* p, const float* const* g,
         L.eps = eps;
         L.wd = weight_decay;
         L.gscale = grad_scale;
+        L.lr_dev = lr_dev;
         int64_t blocks = 0;
         int k = 0;
         for (int32_t i = c0; i < count && k < sf::kAdamMax; ++i) {
@@ -1353,7 +1358,7 @@ size_t rsx_mg_alpha_ws_bytes(int32_t count, const int64_t* n) {
 
 int rsx_mg_alpha(int32_t count, const float* const* params, const float* const* grads, const int64_t* n,
                  double base, double lr, double rel_step, double max_scale, double* alpha_out, void* ws,
-                 size_t ws_bytes, rsx_stream_t stream) {
+                 size_t ws_bytes, const double* lr_dev, rsx_stream_t stream) {
     if (count <= 0 || count > 8 * sf::kAdamMax || !params || !grads || !n || !alpha_out) return RSX_ERR_ARG;
     if (!ws || ws_bytes < rsx_mg_alpha_ws_bytes(count, n)) return RSX_ERR_WORKSPACE;
     sf::PairList lists[8];
@@ -1369,12 +1374,12 @@ int rsx_mg_alpha(int32_t count, const float* const* params, const float* const* 
         off += blocks[li];
     }
     hipLaunchKernelGGL(sf::mg_alpha_final, dim3(1), dim3(sf::kMgFinal), 0, s, part, off, numel, base, lr, rel_step,
-                       max_scale, alpha_out);
+                       max_scale, alpha_out, lr_dev);
     return last_rc();
 }
 
 int rsx_axpy_multi(int32_t count, float* const* y, const float* const* x, const int64_t* n,
-                   const double* alpha_dev, double mult, rsx_stream_t stream) {
+                   const double* alpha_dev, double mult, const double* lr_dev, rsx_stream_t stream) {
     if (count < 0 || count > 8 * sf::kAdamMax || !alpha_dev || (count > 0 && (!y || !x || !n))) return RSX_ERR_ARG;
     sf::PairList lists[8];
     int64_t blocks[8] = {0};
@@ -1382,7 +1387,7 @@ int rsx_axpy_multi(int32_t count, float* const* y, const float* const* x, const 
     if (rc) return rc;
     hipStream_t s = as_stream(stream);
     for (int li = 0; li * sf::kAdamMax < count; ++li)
-        if (blocks[li] > 0) hipLaunchKernelGGL(sf::axpy_multi, dim3((unsigned)blocks[li]), dim3(256), 0, s, lists[li], alpha_dev, mult);
+        if (blocks[li] > 0) hipLaunchKernelGGL(sf::axpy_multi, dim3((unsigned)blocks[li]), dim3(256), 0, s, lists[li], alpha_dev, mult, lr_dev);
     return last_rc();
 }
 

@@ -309,6 +309,75 @@ int rsx_sample_epoch(const int32_t* inter_u, const int32_t* inter_i, int64_t n_i
     return rsx::sample_call(s, n_inter, out, rsx::as_stream(stream), batch);
 }
 
+int rsx_layergcn_step(const rsx_layergcn_step_args* st, rsx_stream_t stream) {
+    using namespace rsx;
+    if (!st || !st->adj || !st->p || !st->m || !st->v || !st->out || !st->g || !st->r || !st->acc || !st->h0 ||
+        !st->h1 || !st->zs || !st->cs || !st->triplets || st->batch <= 0 || st->n_layers < 1)
+        return RSX_ERR_ARG;
+    const rsx_csr& A = *st->adj;
+    const int d = st->d, K = st->n_layers;
+    const int64_t n = st->n_users + st->n_items;
+    if (A.n_rows != n) return RSX_ERR_ARG;
+    for (int k = 0; k < K; ++k)
+        if (!st->zs[k] || !st->cs[k]) return RSX_ERR_ARG;
+    hipStream_t s = as_stream(stream);
+    float* h[2] = {st->h0, st->h1};
+    int rc;
+    // forward: E^k = cos-gated A E^{k-1}; out = sum_k E^k; the last layer zeroes g, r
+    const float* x = st->p;
+    for (int k = 1; k <= K; ++k) {
+        rsx_epilogue e = epi0(RSX_EPI_LAYERGCN);
+        e.e0 = st->p;
+        e.y = h[(k - 1) & 1];
+        e.s_out = st->out;
+        e.s_in = k > 1 ? st->out : nullptr;
+        e.aux = st->zs[k - 1];
+        e.aux_w = st->cs[k - 1];
+        if (k == K) {
+            e.zero0 = st->g;
+            e.zero1 = st->r;
+        }
+        if ((rc = spmm_dispatch(A, x, d, e, st->slab, s))) return rc;
+        x = h[(k - 1) & 1];
+    }
+    if ((rc = bpr_call(RSX_BPR_LAYERGCN, st->out, st->p, st->n_users, st->n_items, d, st->triplets, st->batch,
+                       st->reg, (float)st->batch, st->g, st->r, st->loss_out, st->loss_acc, st->ws, st->ws_bytes, s)))
+        return rc;
+    // dE^K = g -> dZ^K (rowwise), the ego-cosine terms into acc
+    {
+        rsx_epilogue e = epi0(RSX_EPI_LAYERGCN_BWD);
+        e.r_add = st->g;
+        e.aux = st->zs[K - 1];
+        e.aux_w = st->cs[K - 1];
+        e.e0 = st->p;
+        e.y = h[0];
+        e.s_out = st->acc;
+        if ((rc = rowwise_dispatch(n, d, e, s))) return rc;
+    }
+    const float* hz = h[0];
+    for (int k = K - 1; k >= 1; --k) {
+        rsx_epilogue e = epi0(RSX_EPI_LAYERGCN_BWD);
+        e.r_add = st->g;
+        e.aux = st->zs[k - 1];
+        e.aux_w = st->cs[k - 1];
+        e.e0 = st->p;
+        e.y = h[(K - k) & 1];
+        e.s_in = st->acc;
+        e.s_out = st->acc;
+        if ((rc = spmm_dispatch(A, hz, d, e, st->slab, s))) return rc;
+        hz = h[(K - k) & 1];
+    }
+    // dE^0 = A dZ^1 + cosine terms + reg -> Adam
+    rsx_epilogue e = epi0(RSX_EPI_ADAM);
+    e.s_in = st->acc;
+    e.r_add = st->r;
+    e.p = st->p;
+    e.m = st->m;
+    e.v = st->v;
+    e.adam = st->adam;
+    return spmm_dispatch(A, hz, d, e, st->slab, s);
+}
+
 int rsx_lightgcn_forward(const rsx_csr* adj, int32_t d, int32_t n_layers, const float* p, float* s, float* h0,
                          float* h1, float* final_emb, float* slab, rsx_stream_t stream) {
     if (!adj || !p || !final_emb || n_layers < 0) return RSX_ERR_ARG;

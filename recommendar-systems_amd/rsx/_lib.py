@@ -75,6 +75,14 @@ class LgcnStep(C.Structure):
                 ("row_tag", P), ("tag", I64), ("reg_cnt", P), ("halt", P)]
 
 
+class LayerGcnStep(C.Structure):
+    _fields_ = [("adj", C.POINTER(Csr)), ("n_users", I64), ("n_items", I64), ("d", I32), ("n_layers", I32),
+                ("reg", F32), ("pad0", I32),
+                ("p", P), ("m", P), ("v", P), ("out", P), ("g", P), ("r", P), ("acc", P), ("h0", P), ("h1", P),
+                ("zs", P), ("cs", P), ("slab", P), ("triplets", P), ("batch", I64), ("adam", Adam),
+                ("loss_out", P), ("loss_acc", P), ("ws", P), ("ws_bytes", C.c_size_t)]
+
+
 class ShardedStep(C.Structure):
     _fields_ = [("adj_u", C.POINTER(Csr)), ("adj_i", C.POINTER(Csr)), ("n_users", I64), ("n_items", I64),
                 ("d", I32), ("n_layers", I32), ("reg", F32), ("pad0", I32),
@@ -111,6 +119,7 @@ def _declare(lib):
         "rsx_gather_rows": (C.c_int, [P, P, I64, I64, I32, P, P]),
         "rsx_sample_epoch": (C.c_int, [P, P, I64, P, P, P, I64, C.c_uint64, I64, I64, P, P]),
         "rsx_lightgcn_step": (C.c_int, [C.POINTER(LgcnStep), P]),
+        "rsx_layergcn_step": (C.c_int, [C.POINTER(LayerGcnStep), P]),
         "rsx_lightgcn_forward": (C.c_int, [C.POINTER(Csr), I32, I32, P, P, P, P, P, P, P]),
         "rsx_smore_spectral_spec_floats": (C.c_size_t, [I64, I32]),
         "rsx_smore_spectral_fwd_ws_bytes": (C.c_size_t, [I64, I32, I32, I32]),
@@ -143,11 +152,11 @@ def _declare(lib):
         "rsx_smore_infonce_fwd": (C.c_int, [P, P, P, P, I64, I64, I32, F32, P, P, C.c_size_t, P]),
         "rsx_smore_infonce_bwd": (C.c_int, [P, P, P, P, I64, I64, I32, F32, P, P, P, P, C.c_size_t, P]),
         "rsx_adam_multi": (C.c_int, [I32, P, P, P, P, P, P, F32, F32, F32, F32, F32, P]),
-        "rsx_adam_multi_scaled": (C.c_int, [I32, P, P, P, P, P, P, F32, F32, F32, F32, F32, F32, P]),
+        "rsx_adam_multi_scaled": (C.c_int, [I32, P, P, P, P, P, P, F32, F32, F32, F32, F32, F32, P, P]),
         "rsx_smore_unit_weights": (C.c_int, [P, P, P, I32, I32, P, P]),
         "rsx_mg_alpha_ws_bytes": (C.c_size_t, [I32, P]),
-        "rsx_mg_alpha": (C.c_int, [I32, P, P, P, C.c_double, C.c_double, C.c_double, C.c_double, P, P, C.c_size_t, P]),
-        "rsx_axpy_multi": (C.c_int, [I32, P, P, P, P, C.c_double, P]),
+        "rsx_mg_alpha": (C.c_int, [I32, P, P, P, C.c_double, C.c_double, C.c_double, C.c_double, P, P, C.c_size_t, P, P]),
+        "rsx_axpy_multi": (C.c_int, [I32, P, P, P, P, C.c_double, P, P]),
         "rsx_knn_ws_bytes": (C.c_size_t, [I64, I32]),
         "rsx_knn_graph": (C.c_int, [P, I64, I32, I32, P, P, P, P, C.c_size_t, P]),
         "rsx_adj_build_ws_bytes": (C.c_size_t, [I64, I64, I64]),
@@ -164,7 +173,7 @@ def _declare(lib):
 
 EXPORTED = ["rsx_version", "rsx_csr_schedule_host", "rsx_csr_schedule_rebind", "rsx_spmm_batch", "rsx_spmm", "rsx_rowwise", "rsx_bpr_ws_bytes", "rsx_bpr",
             "rsx_fullsort_ws_bytes", "rsx_fullsort_plan", "rsx_fullsort_topk", "rsx_score_dense", "rsx_sample_triplets",
-            "rsx_gather_rows", "rsx_lightgcn_step", "rsx_lightgcn_forward", "rsx_sample_epoch",
+            "rsx_gather_rows", "rsx_lightgcn_step", "rsx_layergcn_step", "rsx_lightgcn_forward", "rsx_sample_epoch",
             "rsx_smore_spectral_spec_floats", "rsx_smore_spectral_fwd_ws_bytes", "rsx_smore_spectral_fwd",
             "rsx_smore_spectral_bwd",
             "rsx_smore_spectral_bwd_partials",

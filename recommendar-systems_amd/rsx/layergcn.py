@@ -19,6 +19,7 @@ E^0 with g = A dZ^1 + (cosine terms) + reg.  Loss: sum-BPR + reg * L2
 """
 from __future__ import annotations
 
+import ctypes as C
 import os
 
 import random
@@ -88,10 +89,44 @@ class LayerGCNEngine:
             self._eval_valid = True
         return self._eval_out
 
+    def _c_step(self, triplets: torch.Tensor):
+        """The batch as one rsx_layergcn_step call (the same kernels and order as the
+        Python-issued sequence below; host cost one ctypes call)."""
+        st = getattr(self, "_cst", None)
+        if st is None:
+            st = self._cst = L.LayerGcnStep()
+            st.n_users, st.n_items, st.d, st.n_layers, st.reg = self.n_users, self.n_items, self.d, self.K, self.reg
+            for name in ("p", "m", "v", "out", "g", "r", "acc"):
+                setattr(st, name, getattr(self, name).data_ptr())
+            st.h0, st.h1 = self.h[0].data_ptr(), self.h[1].data_ptr()
+            self._zs_arr = (C.c_void_p * self.K)(*[z.data_ptr() for z in self.zs])
+            self._cs_arr = (C.c_void_p * self.K)(*[c.data_ptr() for c in self.cs])
+            st.zs, st.cs = C.cast(self._zs_arr, C.c_void_p), C.cast(self._cs_arr, C.c_void_p)
+            st.loss_acc = self.loss_acc.data_ptr()
+            st.loss_out = None
+        A = self.train_adj
+        if getattr(self, "_cst_adj", None) is not A:  # a new epoch graph
+            st.adj = C.pointer(A.struct)
+            slab = A.slab(self.d)
+            st.slab = slab.data_ptr() if slab is not None else None
+            self._cst_adj = A
+        trip = triplets[:3].contiguous()
+        B = trip.shape[1]
+        ws = ops._ws(self.device, L.lib().rsx_bpr_ws_bytes(B))
+        st.ws, st.ws_bytes = ws.data_ptr(), ws.numel()
+        st.triplets, st.batch = trip.data_ptr(), B
+        st.adam = ops.adam_struct(self.lr, self.step_count, weight_decay=self.wd)
+        self._keep = trip
+        L.check(L.lib().rsx_layergcn_step(C.byref(st), ops._stream()), "rsx_layergcn_step")
+        self._eval_valid = False
+
     def step(self, triplets: torch.Tensor):
         d, K, n = self.d, self.K, self.n_users + self.n_items
         A = self.train_adj
         self.step_count += 1
+        if os.environ.get("RSX_LAYERGCN_CSTEP", "1") != "0":
+            self._c_step(triplets)
+            return
         self._forward(A, self.out, zero_grads=True, save=True)
         ops.bpr(L.RSX_BPR_LAYERGCN, self.out, self.p, self.n_users, self.n_items, triplets[:3].contiguous(),
                 self.reg, g_final=self.g, g_ego=self.r, loss_acc=self.loss_acc)

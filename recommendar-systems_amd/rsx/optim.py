@@ -27,6 +27,9 @@ class RsxAdam(torch.optim.Optimizer):
         # the next step() takes every gradient as g * grad_scale (then resets it to 1):
         # the mirror gradient's p.grad.mul_(-beta) folded into the update
         self.grad_scale = 1.0
+        # optional 1-element f64 device tensor holding the learning rate (set by
+        # rsx.trainer for graph-captured steps: a new lr then needs no new capture)
+        self.lr_dev = None
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -58,7 +61,8 @@ class RsxAdam(torch.optim.Optimizer):
                                                     for p in live],
                            [self.state[p]["exp_avg"] for p in live], [self.state[p]["exp_avg_sq"] for p in live],
                            steps, group["lr"], betas=group["betas"], eps=group["eps"],
-                           weight_decay=group["weight_decay"], grad_scale=gs)
+                           weight_decay=group["weight_decay"], grad_scale=gs,
+                           lr_dev=self.lr_dev if len(self.param_groups) == 1 else None)
                 continue
             for p in live:
                 st = self.state[p]

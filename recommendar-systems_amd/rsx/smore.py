@@ -255,6 +255,9 @@ class SMORE(GeneralRecommender):
     # a training batch has no host syncs and global_step advances once per
     # calculate_loss: the Trainer may capture it in a HIP graph (rsx.trainer._GraphStep)
     supports_graph_step = True
+    # no per-epoch buffer rebuilds (pre_epoch_processing is a no-op): the captured
+    # steps stay valid across epochs
+    graph_step_persistent = True
 
     def __init__(self, config, dataset):
         super().__init__(config, dataset)

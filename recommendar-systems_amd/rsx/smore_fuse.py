@@ -344,9 +344,10 @@ def infonce2(side, content, users, pos, n_users, tau):
 # multi-tensor Adam
 # ---------------------------------------------------------------------------
 def adam_multi(params, grads, exp_avgs, exp_avg_sqs, steps, lr, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0,
-               grad_scale=1.0):
+               grad_scale=1.0, lr_dev=None):
     """torch.optim.Adam's update over many tensors in one launch (per 32 tensors); the
-    gradients are taken as g * grad_scale (f32 product) when grad_scale != 1."""
+    gradients are taken as g * grad_scale (f32 product) when grad_scale != 1; with
+    lr_dev (a 1-element f64 device tensor) the learning rate is read from it."""
     n = len(params)
     if n == 0:
         return
@@ -356,14 +357,14 @@ def adam_multi(params, grads, exp_avgs, exp_avg_sqs, steps, lr, betas=(0.9, 0.99
     sizes = (C.c_int64 * n)(*[p.numel() for p in params])
     L.check(L.lib().rsx_adam_multi_scaled(n, _arr(params), _arr(grads), _arr(exp_avgs), _arr(exp_avg_sqs),
                                           _arr(steps), sizes, float(lr), float(betas[0]), float(betas[1]), float(eps),
-                                          float(weight_decay), float(grad_scale), ops._stream()),
+                                          float(weight_decay), float(grad_scale), _p(lr_dev), ops._stream()),
             "rsx_adam_multi_scaled")
 
 
 # ---------------------------------------------------------------------------
 # model-level mirror gradient
 # ---------------------------------------------------------------------------
-def mg_alpha(params, grads, base, lr, rel_step, max_scale):
+def mg_alpha(params, grads, base, lr, rel_step, max_scale, lr_dev=None):
     """alpha_eff of the reference's mirror gradient (trainer.py:290-307) as a 0-d f64
     device tensor, from one pass over the (param, grad) pairs (two launches)."""
     n = len(params)
@@ -373,16 +374,18 @@ def mg_alpha(params, grads, base, lr, rel_step, max_scale):
     ws = torch.empty(max(int(lib.rsx_mg_alpha_ws_bytes(n, sizes)), 16), dtype=torch.uint8, device=dev)
     alpha = torch.empty((), dtype=torch.float64, device=dev)
     L.check(lib.rsx_mg_alpha(n, _arr([p.detach() for p in params]), _arr(grads), sizes, float(base), float(lr),
-                             float(rel_step), float(max_scale), _p(alpha), _p(ws), ws.numel(), ops._stream()),
+                             float(rel_step), float(max_scale), _p(alpha), _p(ws), ws.numel(), _p(lr_dev),
+                             ops._stream()),
             "rsx_mg_alpha")
     return alpha
 
 
-def axpy_multi(ys, xs, alpha, mult):
-    """y += float(alpha * mult) * x for every pair (alpha: 0-d f64 device tensor)."""
+def axpy_multi(ys, xs, alpha, mult, lr_dev=None):
+    """y += float(alpha * mult) * x for every pair (alpha: 0-d f64 device tensor; with
+    lr_dev, a 1-element f64 device tensor, the scale is float(alpha * (mult * lr)))."""
     n = len(ys)
     if n == 0:
         return
     sizes = (C.c_int64 * n)(*[y.numel() for y in ys])
     L.check(L.lib().rsx_axpy_multi(n, _arr([y.detach() for y in ys]), _arr(xs), sizes, _p(alpha), float(mult),
-                                   ops._stream()), "rsx_axpy_multi")
+                                   _p(lr_dev), ops._stream()), "rsx_axpy_multi")

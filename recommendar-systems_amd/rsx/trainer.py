@@ -84,8 +84,9 @@ class _GraphStep:
     graph ("kind"), the host counter is advanced by what the capture advanced it
     by, and batches that log diagnostics run eagerly.  A kind is captured only
     after one eager batch of that kind at full size, so lazily allocated
-    workspaces exist outside the graph's memory pool.  A change of lr (baked into
-    the captured Adam launches) drops the graphs.  Partial batches run eagerly.
+    workspaces exist outside the graph's memory pool.  The learning rate is read
+    on the device (Trainer._sync_lr), so the LambdaLR schedule keeps the graphs
+    (without a device lr, a change of lr drops them).  Partial batches run eagerly.
 
     Contract for a model to opt in (`supports_graph_step = True`): calculate_loss
     increments `global_step` by one (if it has one), and no host syncs or
@@ -123,9 +124,9 @@ class _GraphStep:
         if kind is None:
             return None
         lr = self.t.optimizer.param_groups[0]["lr"]
-        if lr != self.lr:
+        if lr != self.lr and getattr(self.t, "_lr_dev", None) is None:  # lr baked into the captured launches
             self.graphs.clear()
-            self.lr = lr
+        self.lr = lr
         if kind not in self.seen:
             self.seen.add(kind)
             return None
@@ -322,15 +323,32 @@ class Trainer:
                 and (loss_func is None or loss_func == m.calculate_loss) and torch.cuda.is_available())
 
     def reset_graph_step(self):
-        """Drop the captured steps (at each epoch start: pre_epoch_processing may
-        have rebuilt buffers the graphs point at)."""
+        """Drop the captured steps at an epoch start (pre_epoch_processing may have
+        rebuilt buffers the graphs point at), unless the model declares its buffers
+        stable across epochs (`graph_step_persistent`); the learning rate lives on the
+        device (_sync_lr), so the LambdaLR schedule needs no new capture."""
+        if getattr(self.model, "graph_step_persistent", False) and getattr(self, "_lr_dev", None) is not None:
+            return
         self._graph = None
+
+    def _sync_lr(self):
+        """The learning rate as a device f64 scalar that the captured Adam, alpha and
+        axpy launches read (refreshed outside any capture, when the schedule moves it)."""
+        lr = float(self.optimizer.param_groups[0]["lr"])
+        if getattr(self, "_lr_dev", None) is None:
+            self._lr_dev = torch.tensor([lr], dtype=torch.float64, device=self.device)
+            self._lr_host = lr
+            self.optimizer.lr_dev = self._lr_dev
+        elif lr != self._lr_host:
+            self._lr_dev.fill_(lr)
+            self._lr_host = lr
 
     def train_step(self, interaction, batch_idx, loss_func=None):
         """One batch: replayed from a captured graph when possible (see _GraphStep),
         else `_train_batch`.  Returns (losses, loss), detached."""
         loss_func = loss_func or self.model.calculate_loss
         if self.graph_step_enabled(loss_func):
+            self._sync_lr()
             if self._graph is None:
                 self._graph = _GraphStep(self, loss_func)
             out = self._graph.step(interaction)
@@ -422,9 +440,10 @@ class Trainer:
             if fused and params:
                 from .smore_fuse import axpy_multi, mg_alpha
 
-                alpha = mg_alpha(params, grads, base, lr, self.mg_target_rel_step, self.mg_alpha_max_scale)
+                lr_dev = getattr(self, "_lr_dev", None)  # graph-step runs: lr read on the device
+                alpha = mg_alpha(params, grads, base, lr, self.mg_target_rel_step, self.mg_alpha_max_scale, lr_dev)
                 m._alpha_eff = alpha
-                axpy_multi(params, grads, alpha, -lr)  # theta' = theta - alpha lr g
+                axpy_multi(params, grads, alpha, -1.0 if lr_dev is not None else -lr, lr_dev)  # theta - alpha lr g
             else:
                 alpha = _mg_alpha(params, grads, base, lr, self.mg_target_rel_step, self.mg_alpha_max_scale)
                 m._alpha_eff = alpha
@@ -444,7 +463,7 @@ class Trainer:
                 torch._foreach_mul_(live, -beta)
             if params:
                 if fused:
-                    axpy_multi(params, grads, alpha, lr)  # restore theta
+                    axpy_multi(params, grads, alpha, 1.0 if lr_dev is not None else lr, lr_dev)  # restore theta
                 else:
                     torch._foreach_add_(params, torch._foreach_mul(grads, (alpha * lr).float()))
         self.optimizer.step()

@@ -455,6 +455,38 @@ def test_batch_row_tags_equal_dense_step(cuda, K, d):
     np.testing.assert_allclose(a.forward().cpu().numpy(), b.forward().cpu().numpy(), rtol=0, atol=1e-6)
 
 
+@pytest.mark.parametrize("K", [1, 2, 3])
+def test_layergcn_c_step_equals_python_sequence(cuda, K, monkeypatch):
+    """rsx_layergcn_step (the LayerGCN batch as one C call) against the Python-issued
+    kernel sequence it replaces: loss and parameters / moments after 3 batches (the
+    BPR scatter adds repeated rows in either order: atol 1e-6)."""
+    from rsx import synth
+    from rsx.layergcn import LayerGCNEngine
+
+    df = synth.amazon_like(1500, 500, 15000, seed=12)
+    tr = df[df.x_label == 0]
+    tu, ti = tr.userID.values.astype(np.int64), tr.itemID.values.astype(np.int64)
+    nu, ni = int(df.userID.max()) + 1, 500
+    torch.manual_seed(2)
+    U0 = torch.nn.init.xavier_uniform_(torch.empty(nu, 64)).numpy()
+    I0 = torch.nn.init.xavier_uniform_(torch.empty(ni, 64)).numpy()
+    engs = [LayerGCNEngine(tu, ti, nu, ni, 64, K, 1e-4, 1e-3, cuda, U0, I0) for _ in range(2)]
+    assert engs[0].norm_adj.n_long > 0
+    g = torch.Generator().manual_seed(4)
+    for _ in range(3):
+        t = torch.stack([torch.randint(0, nu, (512,), generator=g), torch.randint(0, ni, (512,), generator=g),
+                         torch.randint(0, ni, (512,), generator=g)]).to(cuda)
+        for e, flag in zip(engs, ("1", "0")):
+            monkeypatch.setenv("RSX_LAYERGCN_CSTEP", flag)
+            e.step(t)
+    torch.cuda.synchronize()
+    a, b = engs
+    np.testing.assert_allclose(a.loss_acc.item(), b.loss_acc.item(), rtol=1e-9)
+    for name in ("p", "m", "v"):
+        np.testing.assert_allclose(getattr(a, name).cpu().numpy(), getattr(b, name).cpu().numpy(), rtol=0,
+                                   atol=1e-6, err_msg=name)
+
+
 def test_nan_loss_halts_the_fused_step(cuda):
     """A batch whose loss is NaN sets the tagged step's halt flag to {1, its tag}; that
     step's Adam update and every later one are skipped, so p / m / v stay bit for bit
