@@ -601,6 +601,19 @@ int rsx_smore_infonce_fwd(const float* side, const float* content, const int64_t
 int rsx_smore_infonce_bwd(const float* side, const float* content, const int64_t* users, const int64_t* pos_items,
                           int64_t n_users, int64_t batch, int32_t d, float tau, const float* g_loss, float* g_side,
                           float* g_content, void* ws, size_t ws_bytes, rsx_stream_t stream);
+/* The same forward, also writing the model's loss total_out[0] = add_loss[0] + cl *
+ * (cl_items + cl_users) in f32 (the reference's bpr + cl_loss * (cl_items + cl_users),
+ * src/models/smore.py:411; add_loss = the BPR part); and the backward with the two
+ * upstream gradients read as g_loss[term * g_stride] * g_scale (g_stride 0: one
+ * gradient, the total's, for both terms, g_scale = cl). */
+int rsx_smore_infonce_fwd_total(const float* side, const float* content, const int64_t* users,
+                                const int64_t* pos_items, int64_t n_users, int64_t batch, int32_t d, float tau,
+                                float* loss_out, const float* add_loss, float cl, float* total_out, void* ws,
+                                size_t ws_bytes, rsx_stream_t stream);
+int rsx_smore_infonce_bwd_scaled(const float* side, const float* content, const int64_t* users,
+                                 const int64_t* pos_items, int64_t n_users, int64_t batch, int32_t d, float tau,
+                                 const float* g_loss, int32_t g_stride, float g_scale, float* g_side,
+                                 float* g_content, void* ws, size_t ws_bytes, rsx_stream_t stream);
 /*
  * Model-level mirror gradient (reference src/common/trainer.py:285-336) over `count`
  * (param, grad) pairs of n[i] floats:

@@ -614,7 +614,12 @@ struct NceArgs {
     float* ttl;              // ws: [2][B]
     float* lrow;             // ws: [2][B]
     float* loss;             // [2]: cl_items, cl_users
-    const float* gloss;      // backward: [2] upstream gradients of the two losses
+    const float* add_loss;   // forward (optional): total = add_loss[0] + cl * (cl_items + cl_users)
+    float cl;
+    float* total;
+    const float* gloss;      // backward: upstream gradients of the two losses, gloss[term * gstride] * gscale
+    int32_t gstride;
+    float gscale;
     float* g1;               // d src1 [N, D] (accumulated)
     float* g2;               // d src2
 };
@@ -695,14 +700,22 @@ __global__ __launch_bounds__(64 * kNceWaves) void nce_fwd(NceArgs a) {
     }
 }
 
-// the two means (cl_items, cl_users): one wave per term, rows summed in a fixed order
-__global__ __launch_bounds__(64) void nce_mean(NceArgs a) {
-    const int term = blockIdx.x, lane = threadIdx.x;
+// the two means (cl_items, cl_users): one wave per term, rows summed in a fixed order;
+// optionally the model's total loss add_loss + cl * (cl_items + cl_users) in f32, in
+// the reference's order (smore.py:411: bpr + cl_loss * (cl_items + cl_users))
+__global__ __launch_bounds__(128) void nce_mean(NceArgs a) {
+    const int term = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const float* l = a.lrow + (int64_t)term * a.B;
     double acc = 0.0;
     for (int64_t i = lane; i < a.B; i += 64) acc += (double)l[i];
     acc = group_sum_d<64>(acc);
-    if (lane == 0) a.loss[term] = (float)(acc / (double)a.B);
+    __shared__ float m[2];
+    if (lane == 0) {
+        m[term] = (float)(acc / (double)a.B);
+        a.loss[term] = m[term];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && a.total) a.total[0] = a.add_loss[0] + a.cl * (m[0] + m[1]);
 }
 
 template <int D>
@@ -781,7 +794,7 @@ __global__ __launch_bounds__(64 * kNceWaves) void nce_bwd(NceArgs a) {
         O.f[t] = s;
     }
     if (bo < 0) return;
-    const float coef = a.gloss[term] * (1.f / a.tau) / (float)B;
+    const float coef = (a.gloss[term * a.gstride] * a.gscale) * (1.f / a.tau) / (float)B;
     const Fld<D> Z = fload<D>(oth_n, bo, g);  // the own row's other view
     const Fld<D> dn = fmap2<D>(O, Z, [&](float o, float z) { return coef * (o - z); });
     // F.normalize backward: (dn - y <y, dn>) / |x|, or dn / eps when |x| <= eps
@@ -1238,11 +1251,22 @@ static int nce_setup(sf::NceArgs& a, const float* side, const float* content, co
 int rsx_smore_infonce_fwd(const float* side, const float* content, const int64_t* users, const int64_t* pos_items,
                           int64_t n_users, int64_t batch, int32_t d, float tau, float* loss_out, void* ws,
                           size_t ws_bytes, rsx_stream_t stream) {
+    return rsx_smore_infonce_fwd_total(side, content, users, pos_items, n_users, batch, d, tau, loss_out, nullptr, 0.f,
+                                       nullptr, ws, ws_bytes, stream);
+}
+
+int rsx_smore_infonce_fwd_total(const float* side, const float* content, const int64_t* users,
+                                const int64_t* pos_items, int64_t n_users, int64_t batch, int32_t d, float tau,
+                                float* loss_out, const float* add_loss, float cl, float* total_out, void* ws,
+                                size_t ws_bytes, rsx_stream_t stream) {
     sf::NceArgs a{};
     int rc = nce_setup(a, side, content, users, pos_items, n_users, batch, d, tau, ws, ws_bytes);
     if (rc) return rc;
-    if (!loss_out) return RSX_ERR_ARG;
+    if (!loss_out || (total_out && !add_loss)) return RSX_ERR_ARG;
     a.loss = loss_out;
+    a.add_loss = add_loss;
+    a.cl = cl;
+    a.total = total_out;
     hipStream_t s = as_stream(stream);
     if (batch == 0) return hip_rc(hipMemsetAsync(loss_out, 0xff, 8, s));  // mean of nothing: NaN
     const dim3 grid((unsigned)((batch + 15) / 16), 2);
@@ -1253,19 +1277,29 @@ int rsx_smore_infonce_fwd(const float* side, const float* content, const int64_t
         hipLaunchKernelGGL(sf::nce_norm<128>, grid, dim3(64), 0, s, a);
         hipLaunchKernelGGL(sf::nce_fwd<128>, grid, dim3(64 * sf::kNceWaves), 0, s, a);
     }
-    hipLaunchKernelGGL(sf::nce_mean, dim3(2), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(sf::nce_mean, dim3(1), dim3(128), 0, s, a);
     return last_rc();
 }
 
 int rsx_smore_infonce_bwd(const float* side, const float* content, const int64_t* users, const int64_t* pos_items,
                           int64_t n_users, int64_t batch, int32_t d, float tau, const float* g_loss, float* g_side,
                           float* g_content, void* ws, size_t ws_bytes, rsx_stream_t stream) {
+    return rsx_smore_infonce_bwd_scaled(side, content, users, pos_items, n_users, batch, d, tau, g_loss, 1, 1.f,
+                                        g_side, g_content, ws, ws_bytes, stream);
+}
+
+int rsx_smore_infonce_bwd_scaled(const float* side, const float* content, const int64_t* users,
+                                 const int64_t* pos_items, int64_t n_users, int64_t batch, int32_t d, float tau,
+                                 const float* g_loss, int32_t g_stride, float g_scale, float* g_side,
+                                 float* g_content, void* ws, size_t ws_bytes, rsx_stream_t stream) {
     sf::NceArgs a{};
     int rc = nce_setup(a, side, content, users, pos_items, n_users, batch, d, tau, ws, ws_bytes);
     if (rc) return rc;
-    if (!g_loss || !g_side || !g_content) return RSX_ERR_ARG;
+    if (!g_loss || !g_side || !g_content || g_stride < 0) return RSX_ERR_ARG;
     if (batch == 0) return RSX_OK;
     a.gloss = g_loss;
+    a.gstride = g_stride;
+    a.gscale = g_scale;
     a.g1 = g_side;
     a.g2 = g_content;
     hipStream_t s = as_stream(stream);

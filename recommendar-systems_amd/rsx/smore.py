@@ -342,6 +342,7 @@ class SMORE(GeneralRecommender):
         # training loss on the batch rows only (rsx_smore_batch_rows: False = full tables)
         self.batch_rows = bool(config.get("rsx_smore_batch_rows", True))
         self._bidx = {}
+        self._rows_off = {}
         self._tags = None
         self.batch_views = bool(config.get("rsx_smore_batch_views", True))
         # dropout masks of the fused preference block: a hash of (seed, call, row,
@@ -433,10 +434,10 @@ class SMORE(GeneralRecommender):
             text_embeds = SF.view_prop(txt_i, self.text_graph, self.R, L_, nu)
             fusion_embeds = SF.view_prop(fus_i, self.fusion_graph, self.R, L_, nu)
         if self.training and self.dropout.p > 0:
-            seed = self._drop_seed.clone()
+            # advanced before use (not after): the backward of this forward, which runs
+            # before the next forward, reads the same value, so no copy is kept
             self._drop_seed.add_(1)
-        else:
-            seed = self._drop_seed
+        seed = self._drop_seed
         if train:
             self._last["conv"] = (cv.detach(), ct.detach(), cf.detach())
         return content, image_embeds, text_embeds, fusion_embeds, seed
@@ -499,6 +500,8 @@ class SMORE(GeneralRecommender):
         if c is None:
             ar = torch.arange(B, dtype=torch.int64, device=self.device)
             c = self._bidx[B] = (ar, torch.stack([ar, ar, ar + B]).contiguous())
+            self._rows_off[B] = torch.cat([torch.zeros(B, dtype=torch.int64, device=self.device),
+                                           torch.full((2 * B,), self.n_users, dtype=torch.int64, device=self.device)])
         return c
 
     def _calculate_loss_rows(self, interaction):
@@ -507,19 +510,17 @@ class SMORE(GeneralRecommender):
         and negatives alone, and the block is row-local (smore.py:320-341), so its
         other rows are never computed.  Same loss and gradients as the full-table
         form (duplicate rows are computed once per occurrence, their gradients added)."""
-        users, pos, neg = interaction[0], interaction[1], interaction[2]
-        nu, B = self.n_users, users.numel()
-        rows = torch.cat([users, pos + nu, neg + nu])
+        nu, B = self.n_users, interaction.shape[1]
+        ar, trip = self._batch_index(B)
+        rows = interaction[:3].reshape(-1) + self._rows_off[B]  # [users; nu + positives; nu + negatives]
         content, image_embeds, text_embeds, fusion_embeds, seed = self._views_fused(train=True, rows=rows)
         all_c, side_c, content_c = SF.preference_rows(self, content, image_embeds, text_embeds, fusion_embeds,
                                                       rows, seed)
         self.global_step += 1
-        ar, trip = self._batch_index(B)
-        bpr = _BprLoss.apply(all_c, None, None, trip, L.RSX_BPR_SMORE, float(self.reg_weight),
-                             float(self.batch_size), B, 2 * B)
-        cl_items, cl_users = SF.infonce2(side_c, content_c, ar, ar, B, self.cl_temp)
-        self._last["cl"] = (cl_items.detach(), cl_users.detach())
-        return bpr + self.cl_loss * (cl_items + cl_users)
+        total, parts = SF.smore_loss_rows(all_c, side_c, content_c, trip, ar, B, self.reg_weight, self.batch_size,
+                                          self.cl_loss, self.cl_temp)
+        self._last["cl"] = (parts[0], parts[1])
+        return total
 
     def calculate_loss(self, interaction):
         if self.use_fused and self.batch_rows:

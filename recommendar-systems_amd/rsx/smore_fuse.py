@@ -340,6 +340,50 @@ def infonce2(side, content, users, pos, n_users, tau):
     return _InfoNCE2.apply(side, content, users, pos, n_users, tau)
 
 
+class _SmoreLossRows(torch.autograd.Function):
+    """The SMORE training loss on compact batch rows ([users; positives; negatives]):
+    BPR (RSX_BPR_SMORE, gradients computed with the loss) + cl * (InfoNCE(items) +
+    InfoNCE(users)), the total formed by the InfoNCE mean kernel in the reference's
+    f32 order; backward: the BPR gradient times the upstream gradient, the InfoNCE
+    backward with the upstream gradient x cl read on the device (no loss-combination
+    kernels either way)."""
+
+    @staticmethod
+    def forward(ctx, all_c, side_c, content_c, trip, ar, B, reg, batch_cfg, cl, tau):
+        side_c, content_c = _c(side_c), _c(content_c)
+        d = side_c.shape[1]
+        bl, gf, _ = ops.bpr(L.RSX_BPR_SMORE, all_c.contiguous(), None, B, 2 * B, trip, reg, batch_cfg)
+        lib = L.lib()
+        ws = torch.empty(max(int(lib.rsx_smore_infonce_ws_bytes(B, d)), 4), dtype=torch.uint8, device=side_c.device)
+        out = torch.empty(3, dtype=torch.float32, device=side_c.device)  # cl_items, cl_users, total
+        L.check(lib.rsx_smore_infonce_fwd_total(_p(side_c), _p(content_c), _p(ar), _p(ar), int(B), int(B), d,
+                                                float(tau), _p(out), _p(bl), float(cl), _p(out[2:]), _p(ws),
+                                                ws.numel(), ops._stream()), "rsx_smore_infonce_fwd_total")
+        ctx.save_for_backward(side_c, content_c, ar, ws, gf)
+        ctx.cfg = (int(B), float(tau), float(cl))
+        parts = out[:2]
+        ctx.mark_non_differentiable(parts)
+        return out[2], parts
+
+    @staticmethod
+    def backward(ctx, g_total, g_parts):
+        side_c, content_c, ar, ws, gf = ctx.saved_tensors
+        B, tau, cl = ctx.cfg
+        g_all = gf * g_total
+        gsc = torch.zeros(2, *side_c.shape, dtype=torch.float32, device=side_c.device)
+        gt = g_total.contiguous()
+        L.check(L.lib().rsx_smore_infonce_bwd_scaled(_p(side_c), _p(content_c), _p(ar), _p(ar), B, B,
+                                                     side_c.shape[1], tau, _p(gt), 0, cl, _p(gsc[0]), _p(gsc[1]),
+                                                     _p(ws), ws.numel(), ops._stream()), "rsx_smore_infonce_bwd_scaled")
+        return g_all, gsc[0], gsc[1], None, None, None, None, None, None, None
+
+
+def smore_loss_rows(all_c, side_c, content_c, trip, ar, B, reg, batch_cfg, cl, tau):
+    """(total loss, [cl_items, cl_users]) of SMORE's training loss on compact batch rows."""
+    return _SmoreLossRows.apply(all_c, side_c, content_c, trip, ar, int(B), float(reg), float(batch_cfg), float(cl),
+                                float(tau))
+
+
 # ---------------------------------------------------------------------------
 # multi-tensor Adam
 # ---------------------------------------------------------------------------

@@ -65,6 +65,9 @@ class _Spectral(torch.autograd.Function):
                                            ops._stream()), "rsx_smore_spectral_fwd")
         ctx.save_for_backward(V, Wv, T, Wt, unit, rv, rt, rf, spec)
         ctx.nd = (n, d, int(bool(normalize)))
+        # img / txt are diagnostics outputs that usually get no gradient: no zero-filled
+        # stand-ins for them (nor for an unused conv) in the backward
+        ctx.set_materialize_grads(False)
         return cv, ct, cf, img, txt
 
     @staticmethod
