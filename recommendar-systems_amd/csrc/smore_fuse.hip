@@ -417,9 +417,13 @@ __global__ __launch_bounds__(256) void pref_bwd(PrefArgs a) {
                                : fmap<D>(gA, [](float u) { return u * (1.f / 3.f); });
     const Fld<D> FE = fload<D>(a.FE, row, g);
     const Fld<D> C = fload<D>(a.C, row, g);
-    Fld<D> gC = a.g_cin ? fmap2<D>(gA, fload<D>(a.g_cin, out, g), add) : gA;
-    Fld<D> gFE;
-    {   // fusion view: x3 = fp * FE
+    // batch-row mode: blockIdx.y = 0 the fusion view (+ the pass-through terms), 1 the
+    // image view, 2 the text view, each adding its share of gC / gFE (atomics): three
+    // shorter chains in parallel instead of one long one (otherwise part = -1: all)
+    const int part = gridDim.y > 1 ? (int)blockIdx.y : -1;
+    Fld<D> gC = part > 0 ? fzero<D>() : a.g_cin ? fmap2<D>(gA, fload<D>(a.g_cin, out, g), add) : gA;
+    Fld<D> gFE = fzero<D>();
+    if (part <= 0) {   // fusion view: x3 = fp * FE
         const float* W = stage_w<D>(wl, a.W[kWfp]);
         const Fld<D> sf = fmap<D>(mv<D, kLd<D>>(W, a.b[kWfp], C, lane), sigm);
         const Fld<D> mf = a.p_drop > 0.f ? drop_scale<D>(seed, 2, row, g, a.p_drop, a.drop_scale) : Fld<D>{};
@@ -433,6 +437,7 @@ __global__ __launch_bounds__(256) void pref_bwd(PrefArgs a) {
     }
 #pragma unroll 1
     for (int v = 0; v < 2; ++v) {  // v = 0: image view, 1: text view
+        if (part >= 0 && part != v + 1) continue;  // block-uniform
         const int w1 = v ? kW1t : kW1v, w2 = v ? kW2t : kW2v, wp = v ? kWtp : kWip;
         const Fld<D> h = fmap<D>(mv<D, kLd<D>>(stage_w<D>(wl, a.W[w1]), a.b[w1], FE, lane), tanh_);
         fstore<D>(v ? a.ht : a.hv, out, g, h);
@@ -1164,7 +1169,8 @@ int rsx_smore_pref_rows(int32_t backward, const float* const* W, const float* co
     a.c_out = backward ? nullptr : content_out;
     a.fe_out = backward ? nullptr : fusion_out;
     a.g_cin = backward ? g_content_in : nullptr;
-    const dim3 grid((unsigned)(((n + 15) / 16 + 3) / 4));
+    // batch-row backward: the three views' chains as three block rows (gradients are atomics there)
+    const dim3 grid((unsigned)(((n + 15) / 16 + 3) / 4), backward && rows ? 3 : 1);
     hipStream_t s = as_stream(stream);
     switch (d) {
         case 64:
