@@ -490,8 +490,20 @@ struct WgArgs {
     int32_t n_pairs;
     int32_t n_splits;
     int64_t n;
+    int64_t rows;               // rows per split (wg_rows)
     float* part;                // [n_pairs][n_splits][D*D + D]
 };
+
+// rows per split: enough blocks to fill the chip (~512 over all pairs; the batch-row
+// preference block has only 3B rows), at least 64 (d = 64) / 128 (d = 128) rows and
+// at most kWgRows, a multiple of the 32-row chunk
+inline int64_t wg_rows(int64_t n, int d, int n_pairs) {
+    int64_t r = (n * (n_pairs > 0 ? n_pairs : 1) + 511) / 512;
+    const int64_t lo = d <= 64 ? 64 : 128;
+    if (r < lo) r = lo;
+    if (r > kWgRows) r = kWgRows;
+    return (r + 31) / 32 * 32;
+}
 
 // block (split, pair): rows [r0, r1) in chunks of 32, each chunk's dz and x rows
 // staged in LDS (row stride D + 16: the 4 K-rows x 16 columns of an MFMA operand
@@ -511,7 +523,7 @@ __global__ __launch_bounds__(256) void wgrad_part(WgArgs a) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
     const float* __restrict__ dz = a.dz[pr];
     const float* __restrict__ x = a.x[pr];
-    const int64_t r0 = (int64_t)split * kWgRows, r1 = min(a.n, r0 + kWgRows);
+    const int64_t r0 = (int64_t)split * a.rows, r1 = min(a.n, r0 + a.rows);
     float* out = a.part + ((int64_t)pr * a.n_splits + split) * (D * D + D);
     floatx4 acc[TPW][T];
 #pragma unroll
@@ -578,14 +590,35 @@ __global__ __launch_bounds__(256) void wgrad_part(WgArgs a) {
     }
 }
 
+// element e = blockIdx.x * 64 + lane of pair blockIdx.y: wave w adds splits
+// [w S/4, (w+1) S/4) in order with 8 loads in flight, the four quarters are added in
+// wave order (deterministic)
 template <int D>
 __global__ __launch_bounds__(256) void wgrad_reduce(WgArgs a) {
+    constexpr int64_t SZ = D * D + D;
+    __shared__ float q[4][64];
     const int pr = blockIdx.y;
-    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (e >= D * D + D) return;
-    const float* p = a.part + (int64_t)pr * a.n_splits * (D * D + D) + e;
-    float s = 0.f;
-    for (int i = 0; i < a.n_splits; ++i) s += p[(int64_t)i * (D * D + D)];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t e = (int64_t)blockIdx.x * 64 + lane;
+    const int S = a.n_splits;
+    const int b = S * wave / 4, en = S * (wave + 1) / 4;
+    float acc = 0.f;
+    if (e < SZ) {
+        const float* p = a.part + (int64_t)pr * S * SZ + e;
+        int i = b;
+        for (; i + 8 <= en; i += 8) {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = p[(int64_t)(i + u) * SZ];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) acc += v[u];
+        }
+        for (; i < en; ++i) acc += p[(int64_t)i * SZ];
+    }
+    q[wave][lane] = acc;
+    __syncthreads();
+    if (wave != 0 || e >= SZ) return;
+    const float s = ((q[0][lane] + q[1][lane]) + q[2][lane]) + q[3][lane];
     if (e < D * D) a.dw[pr][e] = s;
     else if (a.db[pr]) a.db[pr][e - D * D] = s;
 }
@@ -1187,7 +1220,8 @@ int rsx_smore_pref_rows(int32_t backward, const float* const* W, const float* co
 }
 
 size_t rsx_smore_wgrad_ws_bytes(int64_t n, int32_t d, int32_t n_pairs) {
-    const int64_t splits = (n + sf::kWgRows - 1) / sf::kWgRows;
+    const int64_t rows = sf::wg_rows(n, d, n_pairs);
+    const int64_t splits = (n + rows - 1) / rows;
     return (size_t)(n_pairs > 0 ? n_pairs : 0) * (size_t)(splits > 0 ? splits : 1) * (size_t)(d * d + d) * 4;
 }
 
@@ -1214,10 +1248,11 @@ int rsx_smore_wgrad(int32_t n_pairs, const float* const* dz, const float* const*
     }
     a.n_pairs = n_pairs;
     a.n = n;
-    a.n_splits = (int32_t)((n + sf::kWgRows - 1) / sf::kWgRows);
+    a.rows = sf::wg_rows(n, d, n_pairs);
+    a.n_splits = (int32_t)((n + a.rows - 1) / a.rows);
     a.part = static_cast<float*>(ws);
     const dim3 g1((unsigned)a.n_splits, (unsigned)n_pairs);
-    const dim3 g2((unsigned)((d * d + d + 255) / 256), (unsigned)n_pairs);
+    const dim3 g2((unsigned)((d * d + d + 63) / 64), (unsigned)n_pairs);
     if (d == 64) {
         hipLaunchKernelGGL(sf::wgrad_part<64>, g1, dim3(256), 0, s, a);
         hipLaunchKernelGGL(sf::wgrad_reduce<64>, g2, dim3(256), 0, s, a);
