@@ -570,9 +570,9 @@ struct SpmmBatch {
 };
 
 template <int D, int KIND>
-__global__ __launch_bounds__(kBlock) void spmm_batch(SpmmBatch b) {
+__global__ __launch_bounds__(kBlock) void spmm_batch(SpmmBatch b, int fix_only) {
     int64_t bid = blockIdx.x;
-    const int64_t nm = b.main_off[b.count];
+    const int64_t nm = fix_only ? 0 : b.main_off[b.count];
     int p = 0;
     if (bid < nm) {
         while (p + 1 < b.count && bid >= b.main_off[p + 1]) ++p;
@@ -691,14 +691,17 @@ static int launch_batch(SpmmBatch& b, hipStream_t s) {
     }
     b.main_off[b.count] = nm;
     b.fix_off[b.count] = nf;
-    if (nf > kInlineFixups) {  // too many fixup blocks to ride along: one launch per product
-        for (int p = 0; p < b.count; ++p) {
-            const int rc = launch_spmm<D, KIND>(b.a[p], b.x[p], b.e[p], b.slab[p], s, TagJob{});
-            if (rc) return rc;
+    if (nf > kInlineFixups) {  // too many fixup blocks to ride along: every product's fixups in a second launch
+        if (nm > 0) {
+            const int64_t f = b.fix_off[b.count];
+            b.fix_off[b.count] = 0;  // (the first launch has no fixup blocks: nm blocks only)
+            hipLaunchKernelGGL((spmm_batch<D, KIND>), dim3((unsigned)nm), dim3(kBlock), 0, s, b, 0);
+            b.fix_off[b.count] = f;
         }
-        return 0;
+        hipLaunchKernelGGL((spmm_batch<D, KIND>), dim3((unsigned)nf), dim3(kBlock), 0, s, b, 1);
+        return last_rc();
     }
-    if (nm + nf > 0) hipLaunchKernelGGL((spmm_batch<D, KIND>), dim3((unsigned)(nm + nf)), dim3(kBlock), 0, s, b);
+    if (nm + nf > 0) hipLaunchKernelGGL((spmm_batch<D, KIND>), dim3((unsigned)(nm + nf)), dim3(kBlock), 0, s, b, 0);
     return last_rc();
 }
 

@@ -199,6 +199,40 @@ def test_view_prop3_equals_three_view_props(cuda, d, L_):
         assert torch.equal(o, o1) and torch.equal(g, g1)
 
 
+@pytest.mark.parametrize("kind", ["store", "add"])
+def test_spmm_batch_many_fixups(cuda, kind):
+    """rsx_spmm_batch with more hub-row fixups than ride along in one launch (> 1024 over
+    the three products: the work blocks, then every product's fixups in a second
+    launch), a graph repeated within the batch: each product equals its own rsx_spmm
+    launch bit for bit."""
+    from rsx import _lib as L
+    from rsx import ops
+
+    rng = np.random.default_rng(5)
+    csrs = []
+    for k in range(3):
+        n = 1500
+        deg = np.where(rng.random(n) < 0.4, rng.integers(33, 200, n), rng.integers(0, 32, n))
+        rp = np.zeros(n + 1, np.int64)
+        rp[1:] = np.cumsum(deg)
+        col = rng.integers(0, n, int(rp[-1])).astype(np.int32)
+        val = rng.standard_normal(int(rp[-1])).astype(np.float32)
+        csrs.append(ops.DeviceCSR(rp, col, val, n, cuda, 32))
+    csrs[2] = csrs[0]  # the same graph twice in one launch (separate slabs)
+    assert sum(a.n_long for a in csrs) > 1024
+    d = 64
+    xs = [torch.randn(1500, d, device=cuda) for _ in range(3)]
+    adds = [torch.randn(1500, d, device=cuda) for _ in range(3)]
+    outs = [torch.empty(1500, d, device=cuda) for _ in range(3)]
+    mk = (lambda y, r: ops.epi(L.RSX_EPI_STORE, y=y)) if kind == "store" else \
+        (lambda y, r: ops.epi(L.RSX_EPI_ADD, y=y, r_add=r))
+    ops.spmm_batch(csrs, xs, [mk(y, r) for y, r in zip(outs, adds)], d)
+    for a, x, r, y in zip(csrs, xs, adds, outs):
+        want = torch.empty_like(y)
+        a.spmm_epi(x, mk(want, r), d)
+        assert torch.equal(y, want)
+
+
 def _infonce_ref(v1, v2, tau):
     """The reference's InfoNCE (smore.py:380-387)."""
     v1, v2 = F.normalize(v1, dim=1), F.normalize(v2, dim=1)
