@@ -51,7 +51,9 @@ static WgPlan wg_plan(int64_t n, int out_dim, int in_dim, int max_ig = 4, int64_
     p.nob = ot / p.otb;
     p.nib = it / p.ig;
     const int64_t grid_waves = p.nob * p.nib * 4;
-    int64_t s = (target_waves + grid_waves - 1) / grid_waves;
+    // splits rounded down: a grid just over the resident count pays a whole second
+    // round for its last few blocks (C5's 768-wide projections: 516 blocks on 512 slots)
+    int64_t s = target_waves / grid_waves;
     // partials: at most a quarter of the input bytes (or 4 MB)
     const int64_t in_bytes = n * (int64_t)(out_dim + in_dim) * 4;
     const int64_t slot_bytes = (int64_t)out_dim * in_dim * 4;
