@@ -622,8 +622,12 @@ def main():
                          "s_per_eval": eval_s,
                          "s_per_eval_includes": "forward + fused top-50 + recall/ndcg/precision/map tail + D2H",
                          "kernel_ms_all_eval_users": fs_ms,
-                         "kernel_tflops": fs_flops / (fs_ms * 1e-3) / 1e12,
-                         "mfma_f32_peak_tflops": 157.3},
+                         # the dense f32 score matrix's flops / kernel time: the screened kernel
+                         # (csrc/fullsort.hip fs_screen) runs two bf16 MFMA passes over all pairs and
+                         # exact f32 dots for the candidates only, so this is an f32-equivalent rate
+                         "kernel_tflops_f32_equivalent": fs_flops / (fs_ms * 1e-3) / 1e12,
+                         "screen_bf16_mfma_tflops": 2 * 2.0 * (d + 16) * ni * vu_d.numel() / (fs_ms * 1e-3) / 1e12,
+                         "mfma_f32_peak_tflops": 157.3, "mfma_bf16_dense_peak_tflops": 2516.6},
             "roofline": roof,
             "roofline_kernels": kernels,
             "cpu_baseline": cpu,

@@ -23,6 +23,7 @@
 // so the strict "> threshold" filter drops nothing the canonical order would keep.
 // Kernel 2 (fs_select): one wavefront per user takes the exact top-K over every
 // chunk's list (each already cut to its top k) and rank-sorts it.
+#include <algorithm>
 #include <climits>
 #include <cstdlib>
 
@@ -111,6 +112,10 @@ struct FsArgs {
     float* out_val;
     int64_t* out_idx;
     int mode;  // profiling ablation (RSX_FS_MODE): 0 full, 1 scores only, 2 no compaction, 3 no final emit
+    const __bf16* Ib;  // fs_screen: bf16 item rows + norm block (kScreenRow), padded to whole 32-item tiles
+    int n_lists;       // candidate lists per user: n_chunks (fs_tiles), n_chunks * seg_slots (fs_screen)
+    int seg_slots;     // fs_screen: segments per (user block, chunk) (1: unsegmented)
+    int64_t seg_waves; // fs_screen: waves per chunk of the balanced split (0: one per user block)
 };
 
 
@@ -548,6 +553,431 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D <= 64 ? 2 
     if (uvalid && h == 0) a.ccount[bslot * a.n_chunks + chunk] = cnt;
 }
 
+// ---------------------------------------------------------------------------
+// Screened full-sort (k <= 64): bf16 MFMA bounds, exact f32 scores for the
+// candidates only.
+//
+// fs_tiles spends most of its time on f32 MFMA (1/16 of the bf16 rate) and on
+// inserting scores that a low running threshold lets through.  fs_screen scores
+// every (user, item) pair twice with v_mfma_f32_32x32x16_bf16 and computes the
+// exact f32 score only for the few items that can reach the user's top k:
+//  * bound: with bf16 (round-to-nearest) operands, exact products and f32
+//    accumulation, |s~ - s| <= eps * sum_j |u_j||v_j| <= eps * |u| * |v_i| for the
+//    exact f32 score s (an fmaf chain) and eps = 2^-7 + 2^-16 + 2 D 2^-23 < kScreenEps;
+//    the margin eps |u| |v_i| rides in the MFMA as one more K block: the item's bf16
+//    row carries |v_i| and the user's carries -+eps |u|, both rounded up, so the
+//    accumulator holds the bound itself;
+//  * pass 1: each lane keeps, per accumulator slot, the two largest lower bounds
+//    s~ - eps |u||v_i| (masked items: exactly -1e10) -- 64 distinct items per user --
+//    and the k-th largest of them, L, is a lower bound of the user's exact k-th
+//    score (k items are known to score >= L);
+//  * pass 2: an item whose upper bound s~ + eps |u||v_i| is >= L (> the running
+//    threshold) gets its exact score by an fmaf chain over d in order (bitwise the
+//    score_dense kernel's; the user row from LDS), and enters the candidate row as
+//    fs_tiles' 64-bit key if that score is >= L; rows that fill up are compacted
+//    exactly as in fs_tiles.
+// The candidate rows, counts and fs_select are fs_tiles'; the top k is exact.
+// ---------------------------------------------------------------------------
+#ifndef RSX_FS_SCREEN_WPE
+#define RSX_FS_SCREEN_WPE 2  // fs_screen waves per SIMD requested at d <= 64
+#endif
+#ifndef RSX_FS_ABUF
+#define RSX_FS_ABUF 1  // fs_screen item-operand buffers (2: the next tile's loads issued before the MFMAs)
+#endif
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+constexpr float kScreenEps = 0.0080f;
+
+template <int D>
+constexpr int kScreenRow = D + 16;  // bf16 elements per screened item row: the row, then |v| and 15 zeros
+
+__device__ __forceinline__ unsigned pack_bf16x2(float lo, float hi) {
+    const bf16x2 v = {(__bf16)lo, (__bf16)hi};
+    return __builtin_bit_cast(unsigned, v);
+}
+__device__ __forceinline__ bf16x8 pack_bf16x8(float4 p, float4 q) {
+    const u32x4 w = {pack_bf16x2(p.x, p.y), pack_bf16x2(p.z, p.w), pack_bf16x2(q.x, q.y), pack_bf16x2(q.z, q.w)};
+    return __builtin_bit_cast(bf16x8, w);
+}
+// bf16 bits of the smallest bf16 >= x (x >= 0 finite)
+__device__ __forceinline__ unsigned bf16_up(float x) { return (__float_as_uint(x) + 0xffffu) >> 16; }
+
+// bf16 copy of every item row with its L2 norm appended (rounded up); rows [ni, ni_pad)
+// are zero.  D/4 threads a row.
+template <int D>
+__global__ __launch_bounds__(256) void fs_prep(const float* __restrict__ I, int64_t ni, int64_t ni_pad,
+                                               __bf16* __restrict__ Ib) {
+    constexpr int G = D / 4;
+    constexpr int DP = kScreenRow<D>;
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t row = t / G;
+    const int c = (int)(t % G);
+    const float4 v = row < ni ? ld4(I + row * D + 4 * c) : f4(0.f);
+    float ss = v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+#pragma unroll
+    for (int o = G / 2; o > 0; o >>= 1) ss += __shfl_xor(ss, o, kWave);  // the row's G threads: one aligned lane group
+    if (row >= ni_pad) return;
+    __bf16* r = Ib + row * DP;
+    *reinterpret_cast<uint2*>(r + 4 * c) = make_uint2(pack_bf16x2(v.x, v.y), pack_bf16x2(v.z, v.w));
+    if (c == 0) {
+        const u32x4 z = {0u, 0u, 0u, 0u};
+        u32x4 w = z;
+        w[0] = bf16_up(sqrtf(ss) * 1.0001f);  // element D (low half of the first word)
+        *reinterpret_cast<u32x4*>(r + D) = w;
+        *reinterpret_cast<u32x4*>(r + D + 8) = z;
+    }
+}
+
+// exact score <U row, I row>: fmaf chain over d in order (as score_dense)
+template <int D>
+__device__ __forceinline__ float exact_dot(const float* __restrict__ u, const float* __restrict__ v) {
+    float acc = 0.f;
+#pragma unroll 4  // blocks of 16 d: the loads of a block in flight together, few registers
+    for (int c = 0; c < D; c += 4) {
+        const float4 x = *reinterpret_cast<const float4*>(u + c), y = ld4(v + c);
+        acc = fmaf(x.x, y.x, acc);
+        acc = fmaf(x.y, y.y, acc);
+        acc = fmaf(x.z, y.z, acc);
+        acc = fmaf(x.w, y.w, acc);
+    }
+    return acc;
+}
+
+// One segment of fs_screen: user block ub, item tiles [ta, tz) of chunk `chunk`, into
+// candidate list `li` of the block's users (lists per user: a.n_lists).
+template <int D>
+__device__ __forceinline__ void screen_segment(const FsArgs& a, int64_t ub, int chunk, int li, int ta, int tz,
+                                               float* urows, unsigned* queue, int* lcnt, unsigned* lomax) {
+    constexpr int HALF = D / 2;
+    constexpr int NM = D / 16;  // bf16 MFMAs per 32x32 tile over the row (8 operand elements per lane each)
+    constexpr int DP = kScreenRow<D>;
+    constexpr int US = D + 4;   // LDS user row stride (floats)
+    const int lane = threadIdx.x, j = lane & 31, h = lane >> 5;
+    const int64_t ublock = ub * 32;
+    const int64_t bslot = ublock + j;
+    const bool uvalid = bslot < a.nb;
+    const int64_t urow = uvalid ? (a.users ? a.users[bslot] : bslot) : 0;
+    const int64_t c0 = (int64_t)chunk * a.chunk_items;
+    const int64_t i0 = c0 + (int64_t)ta * 32;
+    const int64_t i1 = min(min(a.ni, c0 + a.chunk_items), c0 + (int64_t)tz * 32);
+    const int ntiles = tz - ta;
+    u64* const base = a.cand + (ublock * a.n_lists + li) * (int64_t)kCap;
+    const int64_t rowstep = (int64_t)a.n_lists * kCap;
+
+    // B operand: lane (user j, half h) holds u_j[h D/2 + 8 s .. + 8) for MFMA s (the A
+    // operand takes the item rows with the same split, so each MFMA sums 16 of the d);
+    // the f32 row also goes to LDS for the exact scores
+    u32x4 bu[NM + 1];
+    float ss = 0.f;
+    float* const myrow = urows + j * US;
+#pragma unroll
+    for (int s = 0; s < NM; ++s) {
+        const float4 p = uvalid ? ld4(a.U + urow * D + h * HALF + 8 * s) : f4(0.f);
+        const float4 q = uvalid ? ld4(a.U + urow * D + h * HALF + 8 * s + 4) : f4(0.f);
+        ss += p.x * p.x + p.y * p.y + p.z * p.z + p.w * p.w + q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w;
+        bu[s] = u32x4{pack_bf16x2(p.x, p.y), pack_bf16x2(p.z, p.w), pack_bf16x2(q.x, q.y), pack_bf16x2(q.z, q.w)};
+        *reinterpret_cast<float4*>(myrow + h * HALF + 8 * s) = p;
+        *reinterpret_cast<float4*>(myrow + h * HALF + 8 * s + 4) = q;
+    }
+    ss += __shfl_xor(ss, 32, kWave);
+    // margin block: element 0 of lane half 0 carries -eps |u| (pass 1; +eps |u| in pass 2)
+    const unsigned cmb = bf16_up(kScreenEps * sqrtf(ss) * 1.0001f);
+    bu[NM] = u32x4{h == 0 ? (cmb | 0x8000u) : 0u, 0u, 0u, 0u};
+    __syncthreads();  // urows (the previous segment's readers are done: see the end)
+
+    // train-item mask: a per-lane cursor over the user's sorted columns, the column
+    // after the current one prefetched (its load lands while tiles go by; kept as the
+    // raw int32 so that nothing uses it before the next masked item is consumed)
+    int64_t mp = 0, me = 0;
+    int next_mask = INT_MAX, after = INT_MAX;
+    if (uvalid && a.mrp) {
+        int64_t lo = a.mrp[urow], hi = a.mrp[urow + 1];
+        me = hi;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if ((int64_t)a.mcol[mid] < i0) lo = mid + 1; else hi = mid;
+        }
+        mp = lo;
+        next_mask = mp < me ? a.mcol[mp] : INT_MAX;
+        after = mp + 1 < me ? a.mcol[mp + 1] : INT_MAX;
+    }
+    const int64_t mp0 = mp;
+    const int nm0 = next_mask, af0 = after;
+    auto mask_bits = [&](int64_t tb) __attribute__((always_inline)) -> unsigned {
+        unsigned mb = 0;
+        while ((int64_t)next_mask < tb + 32) {
+            mb |= 1u << (unsigned)((int64_t)next_mask - tb);
+            ++mp;
+            next_mask = after;
+            after = mp + 1 < me ? a.mcol[mp + 1] : INT_MAX;
+        }
+        return mb;
+    };
+    // A operand: item i0 + 32 t + j, half h (the padded bf16 copy: no clamps), one
+    // buffer refilled with the next tile as soon as the MFMAs have read it
+    u32x4 ra[RSX_FS_ABUF][NM + 1];
+    auto load_a = [&](auto par, int t) __attribute__((always_inline)) {
+        constexpr int P = decltype(par)::value % RSX_FS_ABUF;
+        const __bf16* row = a.Ib + (i0 + (int64_t)t * 32 + j) * DP;
+        const u32x4* p = reinterpret_cast<const u32x4*>(row + h * HALF);
+#pragma unroll
+        for (int s = 0; s < NM; ++s) ra[P][s] = p[s];
+        ra[P][NM] = *reinterpret_cast<const u32x4*>(row + D + 8 * h);
+    };
+    auto tile = [&](auto par, int t, floatx16& acc) __attribute__((always_inline)) {
+        constexpr int P = decltype(par)::value % RSX_FS_ABUF;
+        // unconditional (the last tile reloads itself): a conditional load would make the
+        // compiler's wait before the MFMAs cover the prefetch too
+        const int tn = t + 1 < ntiles ? t + 1 : t;
+        if constexpr (RSX_FS_ABUF == 2) load_a(IntC<P ^ 1>{}, tn);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+        for (int s = 0; s <= NM; ++s)
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, ra[P][s]),
+                                                          __builtin_bit_cast(bf16x8, bu[s]), acc, 0, 0, 0);
+        if constexpr (RSX_FS_ABUF == 1) load_a(IntC<0>{}, tn);
+    };
+
+    // pass 1: the two largest lower bounds per slot
+    float t1[16], t2[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) t1[r] = t2[r] = -INFINITY;
+    auto pass1 = [&](auto par, int t) __attribute__((always_inline)) {
+        // the mask cursor first: its loads' waits then precede the next tile's prefetch
+        const int64_t tb = i0 + (int64_t)t * 32;
+        const unsigned mb = mask_bits(tb);
+        floatx16 acc;
+        tile(par, t, acc);
+        const int rem = (int)(i1 - tb);
+        // top two by median-of-three (t1 >= t2): t2 = med3(t1, t2, x), t1 = med3(t1, x, +inf)
+        if (rem >= 32 && __ballot(mb != 0u) == 0ull) {  // wave-uniform: no masked or missing item
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                t2[r] = __builtin_amdgcn_fmed3f(t1[r], t2[r], acc[r]);
+                t1[r] = __builtin_amdgcn_fmed3f(t1[r], acc[r], INFINITY);
+            }
+        } else {
+            // slot r <-> item io(r) + 4 h: shift the mask and the bound by 4 h once, so the
+            // per-slot tests take immediates (no per-slot constants held in registers)
+            const unsigned mbh = mb >> (4 * h);
+            const int remh = rem - 4 * h;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int io = (r & 3) + 8 * (r >> 2);
+                const float l = io >= remh ? -INFINITY : (((mbh >> io) & 1u) ? -1e10f : acc[r]);
+                t2[r] = __builtin_amdgcn_fmed3f(t1[r], t2[r], l);
+                t1[r] = __builtin_amdgcn_fmed3f(t1[r], l, INFINITY);
+            }
+        }
+    };
+    if (ntiles > 0) load_a(IntC<0>{}, 0);
+    for (int t = 0; t < ntiles; t += 2) {
+        pass1(IntC<0>{}, t);
+        if (t + 1 < ntiles) pass1(IntC<1>{}, t + 1);
+    }
+    // L = the k-th largest of the lane pair's 64 bounds (radix search on ordered words)
+    unsigned th = 0;
+    for (int bit = 31; bit >= 0; --bit) {
+        const unsigned c = th | (1u << bit);
+        int n = 0;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) n += (int)(ord_f32(t1[r]) >= c) + (int)(ord_f32(t2[r]) >= c);
+        n += __shfl_xor(n, 32, kWave);
+        if (n >= a.k) th = c;
+    }
+    // running strict filter "> tau" keeping every score >= L (the ordered word below L's;
+    // -0.0 == +0.0 as floats, so a bound that lands on a zero filters with a negative denormal)
+    float tau = -INFINITY;
+    if (th > ord_f32(-INFINITY)) {
+        const float tb = unord_f32(th - 1);
+        tau = tb == 0.f ? -__FLT_DENORM_MIN__ : tb;
+    }
+    if (a.mode == 5) {  // profiling ablation: pass 1 only
+        if (uvalid && h == 0) a.ccount[bslot * a.n_lists + li] = 0;
+        if (tau == 1234.5f) a.out_val[0] = tau;
+        __syncthreads();
+        return;
+    }
+
+    // pass 2: candidates by upper bound go to a queue in LDS (item << 6 | masked << 5 | user);
+    // groups of 64 get their exact scores one per lane (all lanes busy), and the kept
+    // keys enter the users' candidate rows (fs_tiles' rows and compaction), counts and
+    // row maxima kept in LDS
+    bu[NM] = u32x4{h == 0 ? cmb : 0u, 0u, 0u, 0u};
+    mp = mp0;
+    next_mask = nm0;
+    after = af0;
+    int cnt = 0;
+    unsigned omax = 0;
+    if (lane < 32) {
+        lcnt[lane] = 0;
+        lomax[lane] = 0u;
+    }
+    int qn = 0;  // queued candidates (wave-uniform)
+    auto compact = [&]() __attribute__((always_inline)) {
+        u64 need = __ballot(h == 0 && cnt > kCap - 64);  // room for a whole group after this
+        while (need) {
+            const int jj = __ffsll((long long)need) - 1;
+            need &= need - 1;
+            const int nn = __builtin_amdgcn_readlane(cnt, jj);
+            const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)ord_f32(tau), jj);
+            const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)omax, jj);
+            int kept;
+            const float nt = compact_slot(base + (int64_t)jj * rowstep, nn, a.k, lane, &kept, lo, hi, RSX_FS_SLACK);
+            if (j == jj) {
+                tau = nt;
+                cnt = kept;
+            }
+            if (lane == jj) lcnt[jj] = kept;
+        }
+    };
+    const u64 ltm = lanemask_lt(lane);
+    auto drain = [&](bool all) __attribute__((always_inline)) {
+        int g = 0;
+        while (qn - g >= 64 || (all && qn > g)) {
+            const int n = min(64, qn - g);
+            __syncthreads();  // queue writes, counts
+            const unsigned e = lane < n ? queue[g + lane] : 0u;
+            const int ju = (int)(e & 31u);
+            const float tj = __shfl(tau, ju, kWave);
+            if (lane < n) {
+                const int64_t item = (int64_t)(e >> 6);
+                const float sc = (e & 32u) ? -1e10f
+                                 : a.mode == 6 ? unord_f32(ord_f32(tj) + 1u + (unsigned)lane)  // ablation: no dots
+                                               : exact_dot<D>(urows + ju * US, a.I + item * D);
+                if (sc > tj) {
+                    const int pos = atomicAdd(&lcnt[ju], 1);
+                    const u64 key = make_key(sc, (int)item);
+                    atomicMax(&lomax[ju], (unsigned)(key >> 32));
+                    base[(int64_t)ju * rowstep + pos] = key;
+                }
+            }
+            __syncthreads();
+            cnt = lcnt[j];
+            omax = lomax[j];
+            compact();
+            g += n;
+        }
+        const int rest = qn - g;
+        if (g > 0 && rest > 0) {
+            __syncthreads();
+            const unsigned v = lane < rest ? queue[g + lane] : 0u;
+            __syncthreads();
+            if (lane < rest) queue[lane] = v;
+        }
+        qn = rest;
+    };
+    auto pass2 = [&](auto par, int t) __attribute__((always_inline)) {
+        const int64_t tb = i0 + (int64_t)t * 32;
+        const unsigned mb = mask_bits(tb);
+        floatx16 acc;
+        tile(par, t, acc);
+        const int rem = (int)(i1 - tb);
+        const unsigned ebase = ((unsigned)(tb + 4 * h) << 6) | (unsigned)j;
+        // one ballot per slot; its lanes append at queue[qn + their rank] (branch-free tests)
+        auto push = [&](bool c, unsigned e) __attribute__((always_inline)) {
+            const u64 bal = __ballot(c);
+            if (bal) {
+                const int rk = __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
+                if (c) queue[qn + rk] = e;
+                qn += popc64(bal);
+            }
+        };
+        const float tv = uvalid ? tau : INFINITY;  // invalid users take nothing
+        if (rem >= 32 && __ballot(mb != 0u) == 0ull) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) push(acc[r] > tv, ebase + ((unsigned)((r & 3) + 8 * (r >> 2)) << 6));
+        } else {
+            const unsigned mbh = mb >> (4 * h);
+            const int remh = rem - 4 * h;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int io = (r & 3) + 8 * (r >> 2);
+                const bool msk = (mbh >> io) & 1u;
+                const float v = msk ? -1e10f : acc[r];
+                push((v > tv) & (io < remh), (ebase + ((unsigned)io << 6)) | (msk ? 32u : 0u));
+            }
+        }
+        if (qn >= 64) drain(false);
+    };
+    if (ntiles > 0) load_a(IntC<0>{}, 0);
+    for (int t = 0; t < ntiles; t += 2) {
+        pass2(IntC<0>{}, t);
+        if (t + 1 < ntiles) pass2(IntC<1>{}, t + 1);
+    }
+    drain(true);
+    __syncthreads();
+    cnt = lcnt[j];
+    omax = lomax[j];
+    if (a.n_lists > 8) {  // lists cut to their top k (fs_select<16, 2>)
+        u64 need = __ballot(h == 0 && cnt > a.k);
+        while (need) {
+            const int jj = __ffsll((long long)need) - 1;
+            need &= need - 1;
+            const int nn = __builtin_amdgcn_readlane(cnt, jj);
+            const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)ord_f32(tau), jj);
+            const unsigned hi = max((unsigned)__builtin_amdgcn_readlane((int)omax, jj),
+                                    (unsigned)__builtin_amdgcn_readlane((int)omax, jj + 32));
+            int kept;
+            compact_slot(base + (int64_t)jj * rowstep, nn, a.k, lane, &kept, lo, hi);
+            if (j == jj) cnt = kept;
+        }
+    }
+    if (uvalid && h == 0) a.ccount[bslot * a.n_lists + li] = cnt;
+    __syncthreads();  // LDS reuse by the next segment
+}
+
+// Balanced full-sort screening: the (user block, item tile) pairs of each chunk are
+// split evenly over the chunk's waves (a.seg_waves of them; 0: one wave per (user
+// block, chunk)), so that every SIMD gets the same work whatever the user count --
+// 2,226 whole (block, chunk) waves on 2,048 resident slots would take two rounds.  A
+// wave's range covers whole or partial tile ranges of consecutive user blocks; segment
+// s of (block, chunk) writes list chunk * S + s (S = a.seg_slots), and the last segment
+// of a (block, chunk) zeroes the counts of the lists after it.
+template <int D>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D <= 64 ? RSX_FS_SCREEN_WPE : 1))) void fs_screen(FsArgs a) {
+    constexpr int US = D + 4;
+    __shared__ __attribute__((aligned(16))) float urows[32 * US];
+    __shared__ unsigned queue[64 * 17];  // pass 2 candidates: < 64 pending + one tile's (<= 16 per lane)
+    __shared__ int lcnt[32];
+    __shared__ unsigned lomax[32];
+    const int64_t n_ub = (a.nb + 31) / 32;
+    const int64_t nper = a.seg_waves ? a.seg_waves : n_ub;  // waves per chunk
+    int64_t w;
+    int chunk;
+    if ((8 % a.n_chunks) == 0) {  // one chunk per XCD: blocks are dealt round-robin to the 8 XCDs
+        const int64_t b = blockIdx.x, xcd = b & 7, slot = b >> 3;
+        chunk = (int)(xcd % a.n_chunks);
+        w = slot * (8 / a.n_chunks) + xcd / a.n_chunks;
+    } else {
+        chunk = (int)(blockIdx.x % a.n_chunks);
+        w = blockIdx.x / a.n_chunks;
+    }
+    if (w >= nper) return;
+    const int64_t c0 = (int64_t)chunk * a.chunk_items;
+    const int nt = (int)((min(a.ni, c0 + a.chunk_items) - c0 + 31) / 32);
+    const int64_t T = n_ub * nt;
+    const int64_t lo = a.seg_waves ? w * T / nper : w * nt, hi = a.seg_waves ? (w + 1) * T / nper : (w + 1) * nt;
+    const int S = a.seg_slots;
+    for (int64_t x = lo; x < hi;) {
+        const int64_t ub = x / nt;
+        const int t0 = (int)(x - ub * nt);
+        const int t1 = (int)min((int64_t)nt, t0 + (hi - x));
+        const int64_t wf = ((ub * nt + 1) * nper + T - 1) / T - 1;  // the wave whose range holds tile 0 of ub
+        const int seg = a.seg_waves ? (int)(w - wf) : 0;
+        screen_segment<D>(a, ub, chunk, chunk * S + seg, t0, t1, urows, queue, lcnt, lomax);
+        if (t1 == nt) {  // the block's last segment in this chunk: the later lists are empty
+            const int j = threadIdx.x & 31;
+            const int64_t bslot = ub * 32 + j;
+            if (threadIdx.x < 32 && bslot < a.nb)
+                for (int q = seg + 1; q < S; ++q) a.ccount[bslot * a.n_lists + chunk * S + q] = 0;
+        }
+        x += t1 - t0;
+    }
+}
+
 // Exact k-th largest of the nonzero keys held E per lane (radix search with ballots,
 // score word first, index word only for a tie at the boundary).
 template <int E>
@@ -612,9 +1042,9 @@ __global__ __launch_bounds__(256) void fs_select(FsArgs a) {
     u64 e[E];
 #pragma unroll
     for (int c = 0; c < SMAX; ++c) {
-        const bool in = c < a.n_chunks;
-        const int n = in ? a.ccount[b * a.n_chunks + c] : 0;
-        const u64* src = a.cand + (b * a.n_chunks + c) * kCap;
+        const bool in = c < a.n_lists;
+        const int n = in ? a.ccount[b * a.n_lists + c] : 0;
+        const u64* src = a.cand + (b * a.n_lists + c) * kCap;
 #pragma unroll
         for (int q = 0; q < PER; ++q) e[PER * c + q] = lane + 64 * q < n ? src[lane + 64 * q] : 0ull;
     }
@@ -671,31 +1101,117 @@ static void fs_plan(int64_t nb, int64_t ni, int d, int* nw, int* n_chunks, int64
     *n_chunks = (int)((ni + per - 1) / per);
 }
 
+static bool fs_use_screen(int k, int d, int64_t ni) {
+    static int on = -1;
+    if (on < 0) {
+        const char* e = getenv("RSX_FS_SCREEN");  // 0: the f32-MFMA fs_tiles path
+        on = e ? atoi(e) != 0 : 1;
+    }
+    return on && k <= 64 && (d == 32 || d == 64 || d == 128 || d == 256) && ni < (1ll << 26);  // queue entry: item << 6
+}
+
+static size_t fs_align(size_t x) { return (x + 255) / 256 * 256; }
+
+// The lists layout of a call: fs_tiles keeps one list per (user, chunk); fs_screen
+// splits each chunk's (user block, tile) pairs evenly over the resident wave slots
+// when there are more (block, chunk) waves than slots (SEGMENTS, fs_screen's header).
+struct FsLayout {
+    int n_chunks;
+    int64_t chunk_items;
+    bool screen;
+    int n_lists, seg_slots;
+    int64_t seg_waves;  // waves per chunk (0: one per user block)
+    int64_t blocks;
+};
+
+static int fs_cus() {
+    static int n = 0;
+    if (!n) {
+        int dev = 0, v = 0;
+        n = (hipGetDevice(&dev) == hipSuccess &&
+             hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+                ? v
+                : 256;
+        (void)hipGetLastError();
+    }
+    return n;
+}
+
+static FsLayout fs_layout(int64_t nb, int64_t ni, int k, int d) {
+    FsLayout L{};
+    int nw;
+    fs_plan(nb, ni, d, &nw, &L.n_chunks, &L.chunk_items);
+    L.screen = fs_use_screen(k, d, ni);
+    L.n_lists = L.n_chunks;
+    L.seg_slots = 1;
+    const int64_t n_ub = (nb + 31) / 32;
+    const int C = L.n_chunks;
+    L.blocks = n_ub * C;
+    if (L.screen && (8 % C) == 0) {
+        const int64_t slots = (int64_t)fs_cus() * 4 * (d <= 128 ? 2 : 1);  // fs_screen: 2 waves per SIMD, 1 at d = 256
+        const int64_t wc = slots / C;
+        if (n_ub * C > slots && wc >= 1) {
+            int S = 1;
+            bool ok = true;
+            for (int c = 0; c < C; ++c) {
+                const int64_t nt = (std::min(ni, (int64_t)(c + 1) * L.chunk_items) - (int64_t)c * L.chunk_items + 31) / 32;
+                const int64_t m = n_ub * nt / wc;  // shortest wave range (tiles)
+                if (m < 1) ok = false;
+                else S = (int)std::max<int64_t>(S, (nt + m - 1) / m + 1);
+            }
+            if (ok && C * S <= 8) {
+                L.seg_waves = wc;
+                L.seg_slots = S;
+                L.n_lists = C * S;
+                L.blocks = wc * C;
+            }
+        }
+    }
+    if ((8 % C) == 0) L.blocks = (L.blocks + 7) / 8 * 8;  // whole rounds of the XCD-aware mapping
+    return L;
+}
+
+// lists cut to their top k before fs_select (fs_tiles: more than 2 chunks; fs_screen: more than 8 lists)
+static bool fs_lists_cut(const FsLayout& L) { return L.screen ? L.n_lists > 8 : L.n_chunks > 2; }
+
+// workspace: candidate rows | counts | (screen) bf16 item copy
 size_t fs_ws(int64_t nb, int64_t ni, int k, int d) {
-    int nw, nc;
-    int64_t per;
-    fs_plan(nb, ni, d, &nw, &nc, &per);
-    return (size_t)nb * nc * kCap * sizeof(u64) + (size_t)nb * nc * sizeof(int) + 512;
+    const FsLayout L = fs_layout(nb, ni, k, d);
+    size_t bytes = fs_align((size_t)nb * L.n_lists * kCap * sizeof(u64) + (size_t)nb * L.n_lists * sizeof(int) + 512);
+    if (L.screen) {
+        const size_t ni_pad = (size_t)(ni + 31) / 32 * 32;
+        bytes += fs_align(ni_pad * (d + 16) * sizeof(__bf16));
+    }
+    return bytes;
 }
 
 template <int D>
-static int launch_fs(FsArgs& a, hipStream_t s) {
-    const int64_t waves = (a.nb + 31) / 32;
-    int64_t nblk = waves * a.n_chunks;
-    if ((8 % a.n_chunks) == 0) nblk = (nblk + 7) / 8 * 8;  // whole rounds of the XCD-aware mapping
-    if (a.mode == 4)
-        hipLaunchKernelGGL((fs_tiles<D, 4>), dim3((unsigned)nblk), dim3(64), 0, s, a);
-    else if (a.mode == 1)
-        hipLaunchKernelGGL((fs_tiles<D, 1>), dim3((unsigned)nblk), dim3(64), 0, s, a);
-    else
-        hipLaunchKernelGGL((fs_tiles<D, 0>), dim3((unsigned)nblk), dim3(64), 0, s, a);
+static int launch_fs(FsArgs& a, const FsLayout& L, hipStream_t s) {
+    const dim3 grid((unsigned)L.blocks);
+    if (a.Ib) {  // screened path
+        const int64_t ni_pad = (a.ni + 31) / 32 * 32;
+        const int64_t nthr = ni_pad * (D / 4);
+        hipLaunchKernelGGL((fs_prep<D>), dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, s, a.I, a.ni, ni_pad,
+                           const_cast<__bf16*>(a.Ib));
+        hipLaunchKernelGGL((fs_screen<D>), grid, dim3(64), 0, s, a);
+    } else if (a.mode == 4) {
+        hipLaunchKernelGGL((fs_tiles<D, 4>), grid, dim3(64), 0, s, a);
+    } else if (a.mode == 1) {
+        hipLaunchKernelGGL((fs_tiles<D, 1>), grid, dim3(64), 0, s, a);
+    } else {
+        hipLaunchKernelGGL((fs_tiles<D, 0>), grid, dim3(64), 0, s, a);
+    }
     const dim3 sg((unsigned)((a.nb + 3) / 4));
-    if (a.mode == 0) {
-        // <= 2 chunks: raw lists (<= kCap keys, kNK per lane); more: lists cut to top k
-        if (a.n_chunks <= 1) hipLaunchKernelGGL((fs_select<1, kNK>), sg, dim3(256), 0, s, a);
-        else if (a.n_chunks <= 2) hipLaunchKernelGGL((fs_select<2, kNK>), sg, dim3(256), 0, s, a);
-        else if (a.n_chunks <= 4) hipLaunchKernelGGL((fs_select<4, 2>), sg, dim3(256), 0, s, a);
-        else if (a.n_chunks <= 8) hipLaunchKernelGGL((fs_select<8, 2>), sg, dim3(256), 0, s, a);
+    if (a.Ib || a.mode == 0) {
+        // raw lists (<= kCap keys, kNK per lane) or lists cut to their top k (<= 2 per lane)
+        const int n = a.n_lists;
+        if (!fs_lists_cut(L)) {
+            if (n <= 1) hipLaunchKernelGGL((fs_select<1, kNK>), sg, dim3(256), 0, s, a);
+            else if (n <= 2) hipLaunchKernelGGL((fs_select<2, kNK>), sg, dim3(256), 0, s, a);
+            else if (n <= 4) hipLaunchKernelGGL((fs_select<4, kNK>), sg, dim3(256), 0, s, a);
+            else hipLaunchKernelGGL((fs_select<8, kNK>), sg, dim3(256), 0, s, a);
+        } else if (n <= 4) hipLaunchKernelGGL((fs_select<4, 2>), sg, dim3(256), 0, s, a);
+        else if (n <= 8) hipLaunchKernelGGL((fs_select<8, 2>), sg, dim3(256), 0, s, a);
         else hipLaunchKernelGGL((fs_select<16, 2>), sg, dim3(256), 0, s, a);
     }
     return last_rc();
@@ -710,8 +1226,12 @@ int fs_call(const float* U, const int64_t* users, int64_t nb, const float* I, in
     if (nb == 0) return RSX_OK;
     if (!ws || ws_bytes < fs_ws(nb, ni, k, d)) return RSX_ERR_WORKSPACE;
     FsArgs a;
-    int nw;
-    fs_plan(nb, ni, d, &nw, &a.n_chunks, &a.chunk_items);
+    const FsLayout L = fs_layout(nb, ni, k, d);
+    a.n_chunks = L.n_chunks;
+    a.chunk_items = L.chunk_items;
+    a.n_lists = L.n_lists;
+    a.seg_slots = L.seg_slots;
+    a.seg_waves = L.seg_waves;
     a.U = U;
     a.users = users;
     a.nb = nb;
@@ -721,9 +1241,15 @@ int fs_call(const float* U, const int64_t* users, int64_t nb, const float* I, in
     a.mcol = mcol;
     a.k = k;
     a.cand = static_cast<u64*>(ws);
-    a.ccount = reinterpret_cast<int*>(static_cast<char*>(ws) + (size_t)nb * a.n_chunks * kCap * sizeof(u64));
+    a.ccount = reinterpret_cast<int*>(static_cast<char*>(ws) + (size_t)nb * a.n_lists * kCap * sizeof(u64));
     a.out_val = out_val;
     a.out_idx = out_idx;
+    a.Ib = nullptr;
+    if (L.screen) {
+        char* p = static_cast<char*>(ws) +
+                  fs_align((size_t)nb * a.n_lists * kCap * sizeof(u64) + (size_t)nb * a.n_lists * sizeof(int) + 512);
+        a.Ib = reinterpret_cast<const __bf16*>(p);
+    }
     {
         static int mode = -1;
         if (mode < 0) {
@@ -733,10 +1259,10 @@ int fs_call(const float* U, const int64_t* users, int64_t nb, const float* I, in
         a.mode = mode;
     }
     switch (d) {
-        case 32: return launch_fs<32>(a, s);
-        case 64: return launch_fs<64>(a, s);
-        case 128: return launch_fs<128>(a, s);
-        case 256: return launch_fs<256>(a, s);
+        case 32: return launch_fs<32>(a, L, s);
+        case 64: return launch_fs<64>(a, L, s);
+        case 128: return launch_fs<128>(a, L, s);
+        case 256: return launch_fs<256>(a, L, s);
         default: return RSX_ERR_UNSUPPORTED;
     }
 }
@@ -782,9 +1308,13 @@ __global__ void gather_rows_k(const float* __restrict__ src, const int64_t* __re
 extern "C" {
 
 size_t rsx_fullsort_ws_bytes(int64_t n_batch, int64_t n_items, int32_t k) {
-    // worst case over d (the plan depends on d only through NW)
-    size_t a = rsx::fs_ws(n_batch, n_items, k, 64), b = rsx::fs_ws(n_batch, n_items, k, 128);
-    return a > b ? a : b;
+    // worst case over d (the plan's chunk count and the screened path's bf16 item copy depend on d)
+    size_t w = 0;
+    for (int d : {32, 64, 128, 256}) {
+        const size_t b = rsx::fs_ws(n_batch, n_items, k, d);
+        w = b > w ? b : w;
+    }
+    return w;
 }
 
 int rsx_fullsort_plan(int64_t n_batch, int64_t n_items, int32_t d, int32_t* n_chunks, int64_t* chunk_items) {

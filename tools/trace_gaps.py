@@ -17,7 +17,8 @@ print(f"{n} periods: span {span / n:.1f} us, busy {busy / n:.1f} us, idle {(span
       f"launches {len(seg) / n:.1f} per period")
 by = defaultdict(lambda: [0.0, 0])
 for r in seg:
-    k = r["Kernel_Name"].split("(")[0][:70]
+    name = r["Kernel_Name"]
+    k = name[:150] if "at::native" in name else name.split("(")[0][:70]
     by[k][0] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
     by[k][1] += 1
 for k, (t, c) in sorted(by.items(), key=lambda x: -x[1][0])[: int(sys.argv[4]) if len(sys.argv) > 4 else 30]:
