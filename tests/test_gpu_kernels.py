@@ -209,6 +209,45 @@ def test_fullsort_random_sizes(cuda, d):
     np.testing.assert_allclose(val.cpu().numpy(), cv, rtol=1e-4, atol=1e-4)
 
 
+@pytest.mark.parametrize("d", [32, 64, 128, 256])
+@pytest.mark.parametrize("k", [1, 17, 50, 64])
+def test_fullsort_screen_exact_vs_dense_scores(cuda, d, k):
+    """The screened full-sort (k <= 64: bf16 bounds, exact f32 scores for candidates only)
+    against the canonical top-k of score_dense's scores: both are the same fmaf chain over
+    d, so the lists must match bit for bit -- an item the bounds wrongly dropped would
+    show.  Heavy-tailed row norms (the margin eps |u||v_i| spans 1e-3..1e3 of a typical
+    score), a zero user (every score ties at 0), negated users, masked runs, and a user
+    count that needs the balanced split of the (user block, tile) work."""
+    from helpers import canonical_topk_fast
+
+    g = torch.Generator().manual_seed(d * 100 + k)
+    nu, ni, nb = 36000, 6007, 35598  # 2 item chunks, more (block, chunk) waves than resident slots
+    U = torch.randn(nu, d, generator=g) * torch.exp(torch.randn(nu, 1, generator=g))
+    I = torch.randn(ni, d, generator=g) * torch.exp(2.0 * torch.randn(ni, 1, generator=g))
+    U[7] = 0.0
+    U[8:40] = -U[8:40]
+    users = torch.randperm(nu, generator=g)[:nb]
+    users[0] = 7
+    rng = np.random.default_rng(d + k)
+    tu = np.repeat(np.arange(nu), 5)
+    ti = rng.integers(0, ni, size=tu.size)
+    heavy = int(users[1])
+    tu = np.concatenate([tu, np.full(ni - 30, heavy)])
+    ti = np.concatenate([ti, np.arange(30, ni)])
+    rp, mc = graph.history_csr(tu, ti, nu)
+    Ud, Id, ud = U.to(cuda), I.to(cuda), users.to(cuda)
+    val, idx = ops.fullsort_topk(Ud, ud, Id, torch.from_numpy(rp).to(cuda), torch.from_numpy(mc).to(cuda), k)
+    rows = np.concatenate([np.arange(64), rng.choice(np.arange(64, nb), size=1200, replace=False)])
+    scores = ops.score_dense(Ud, ud[torch.from_numpy(rows).to(cuda)].contiguous(), Id).cpu().numpy()
+    for b, u in enumerate(users.numpy()[rows]):
+        scores[b, mc[rp[u]:rp[u + 1]]] = -1e10
+    cv, ci = canonical_topk_fast(scores, k)
+    idx, val = idx.cpu().numpy()[rows], val.cpu().numpy()[rows]
+    bad = np.nonzero(np.any(idx != ci, axis=1))[0]
+    assert bad.size == 0, f"rows {bad[:5]}: {idx[bad[0]][:8]} vs {ci[bad[0]][:8]}"
+    assert np.array_equal(val.view(np.uint32), cv.view(np.uint32))
+
+
 def test_score_dense_and_gather(cuda):
     g = torch.Generator().manual_seed(1)
     U = torch.randn(50, 64, generator=g)
