@@ -256,10 +256,13 @@ int rsx_bpr(int32_t variant, const float* final_emb, const float* ego_emb, int64
 /*
  * Replaces  scores = u_emb[users] @ item_emb^T            (lightgcn.py:164 etc.)
  *           scores[mask] = -1e10; topk(scores, k)          (src/common/trainer.py:521-526)
- * without materialising the score matrix.  f32 MFMA (v_mfma_f32_32x32x2_f32,
- * exact f32 fma chains) computes 32x32 score tiles; each row keeps a running
- * top-K in LDS behind a threshold filter; a merge pass orders the result by
- * (score desc, item index asc).  Masked (user, item) pairs — the user's
+ * without materialising the score matrix.  k <= 64 (default): bf16 MFMA tiles
+ * bound every score within eps |u| |v_i| (eps < 2^-7 + 2^-16 + 2 d 2^-23); a first
+ * pass bounds the user's k-th score from below, a second computes exact f32 scores
+ * (an fmaf chain over d in order: rsx_score_dense's bits) only for items whose upper
+ * bound reaches it; k 65..96 (or env RSX_FS_SCREEN=0): exact f32 MFMA tiles with a
+ * running threshold.  Per-user candidate rows in the workspace; a merge pass orders
+ * the result by (score desc, item index asc).  Masked (user, item) pairs — the user's
  * training items, CSR mask_rowptr/mask_col over user ids with sorted columns —
  * score exactly -1e10 as in the reference.
  *   user_emb: [*, d] rows selected by users[b] (int64); item_emb: [n_items, d]
