@@ -1029,39 +1029,121 @@ __device__ __forceinline__ u64 kth_largest_n(const u64 (&e)[E], int k) {
     return ((u64)th << 32) | tl;
 }
 
-// One wavefront per user: the exact top-k over every chunk's raw candidates,
-// ordered by (score desc, index asc).  S = chunks per user (<= SMAX); every list
-// holds <= k <= 96 keys (fs_tiles compacts every list to its top k), i.e. <= 2 per lane.
-template <int SMAX, int PER>
+// The user's candidate lists as one virtual array: key p lives in list c(p) at offset
+// p - off[c] (off[] the lists' prefix sums, wave-uniform).
+template <int SMAX>
+struct FsLists {
+    const u64* src;  // the user's first list; list c at src + c * kCap
+    int off[SMAX + 1];
+    __device__ __forceinline__ u64 at(int p) const {
+        int c = 0;
+#pragma unroll
+        for (int q = 1; q < SMAX; ++q) c += p >= off[q];
+        int o = off[0];
+#pragma unroll
+        for (int q = 1; q < SMAX; ++q) o = c == q ? off[q] : o;
+        return src[c * kCap + (p - o)];
+    }
+};
+
+__device__ __forceinline__ unsigned wave_sum_u(unsigned x) {
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) x += (unsigned)__shfl_xor((int)x, o, kWave);
+    return x;
+}
+
+// Exact k-th largest of `total` keys of the lists (any count): the radix search of
+// kth_largest_n re-reading the keys (L2) each round -- users with very many keys.
+template <int SMAX>
+__device__ u64 kth_largest_lists(const FsLists<SMAX>& Ls, int total, int k, int lane) {
+    unsigned hi = 0u, lo = 0xffffffffu;
+    for (int p = lane; p < total; p += 64) {
+        const unsigned w = (unsigned)(Ls.at(p) >> 32);
+        hi = max(hi, w);
+        lo = min(lo, w);
+    }
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) {
+        hi = max(hi, (unsigned)__shfl_xor((int)hi, o, kWave));
+        lo = min(lo, (unsigned)__shfl_xor((int)lo, o, kWave));
+    }
+    const unsigned diff = lo ^ hi;
+    const int top = diff ? 31 - __builtin_clz(diff) : -1;
+    unsigned th = top >= 31 ? 0u : (hi >> (top + 1)) << (top + 1);
+    for (int bit = top; bit >= 0; --bit) {
+        const unsigned c = th | (1u << bit);
+        unsigned n = 0;
+        for (int p = lane; p < total; p += 64) n += (unsigned)(Ls.at(p) >> 32) >= c;
+        if ((int)wave_sum_u(n) >= k) th = c;
+    }
+    unsigned gt = 0, eq = 0;
+    for (int p = lane; p < total; p += 64) {
+        const unsigned w = (unsigned)(Ls.at(p) >> 32);
+        gt += w > th;
+        eq += w == th;
+    }
+    const int need = k - (int)wave_sum_u(gt);
+    if ((int)wave_sum_u(eq) == need) return (u64)th << 32;
+    unsigned tl = 0;
+    for (int bit = 31; bit >= 0; --bit) {
+        const unsigned c = tl | (1u << bit);
+        unsigned n = 0;
+        for (int p = lane; p < total; p += 64) {
+            const u64 x = Ls.at(p);
+            n += (unsigned)(x >> 32) == th && (unsigned)x >= c;
+        }
+        if ((int)wave_sum_u(n) >= need) tl = c;
+    }
+    return ((u64)th << 32) | tl;
+}
+
+// One wavefront per user: the exact top-k over the user's candidate lists (a.n_lists
+// <= SMAX of them: raw rows of <= kCap keys, or rows cut to the top k), ordered by
+// (score desc, index asc).  The lists are read as one array of the keys that exist:
+// <= 512 of them (<= 4 lists; 1024 for more) go to 8 (16) registers a lane in one round
+// trip and the k-th key is searched there; more are searched in place.
+template <int SMAX>
 __global__ __launch_bounds__(256) void fs_select(FsArgs a) {
-    constexpr int E = PER * SMAX;
+    constexpr int kDenseE = SMAX <= 4 ? 8 : 16;  // keys per lane held in registers
     __shared__ u64 top[4][kCap];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int64_t b = (int64_t)blockIdx.x * 4 + wv;
     if (b >= a.nb) return;  // wave-uniform
-    u64 e[E];
-#pragma unroll
-    for (int c = 0; c < SMAX; ++c) {
-        const bool in = c < a.n_lists;
-        const int n = in ? a.ccount[b * a.n_lists + c] : 0;
-        const u64* src = a.cand + (b * a.n_lists + c) * kCap;
-#pragma unroll
-        for (int q = 0; q < PER; ++q) e[PER * c + q] = lane + 64 * q < n ? src[lane + 64 * q] : 0ull;
-    }
+    FsLists<SMAX> Ls;
+    Ls.src = a.cand + b * a.n_lists * (int64_t)kCap;
     int total = 0;
 #pragma unroll
-    for (int m = 0; m < E; ++m) total += popc64(__ballot(e[m] != 0ull));
+    for (int c = 0; c < SMAX; ++c) {
+        Ls.off[c] = total;
+        total += c < a.n_lists ? a.ccount[b * a.n_lists + c] : 0;
+    }
+    Ls.off[SMAX] = total;
     const int k = a.k;
-    const u64 T = total > k ? kth_largest_n<E>(e, k) : 1ull;
+    const bool dense = total <= 64 * kDenseE;
+    u64 e[kDenseE];
+#pragma unroll
+    for (int m = 0; m < kDenseE; ++m) e[m] = dense && lane + 64 * m < total ? Ls.at(lane + 64 * m) : 0ull;
+    u64 T = 1ull;
+    if (total > k) T = dense ? kth_largest_n<kDenseE>(e, k) : kth_largest_lists<SMAX>(Ls, total, k, lane);
     // gather the winners (exactly min(k, total)) into LDS
     const u64 lt = lanemask_lt(lane);
     int base = 0;
+    if (dense) {
 #pragma unroll
-    for (int m = 0; m < E; ++m) {
-        const bool kp = e[m] != 0ull && e[m] >= T;
-        const u64 bal = __ballot(kp);
-        if (kp) top[wv][base + popc64(bal & lt)] = e[m];
-        base += popc64(bal);
+        for (int m = 0; m < kDenseE; ++m) {
+            const bool kp = e[m] != 0ull && e[m] >= T;
+            const u64 bal = __ballot(kp);
+            if (kp) top[wv][base + popc64(bal & lt)] = e[m];
+            base += popc64(bal);
+        }
+    } else {
+        for (int p0 = 0; p0 < total; p0 += 64) {
+            const u64 x = p0 + lane < total ? Ls.at(p0 + lane) : 0ull;
+            const bool kp = x != 0ull && x >= T;
+            const u64 bal = __ballot(kp);
+            if (kp) top[wv][base + popc64(bal & lt)] = x;
+            base += popc64(bal);
+        }
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -1171,9 +1253,6 @@ static FsLayout fs_layout(int64_t nb, int64_t ni, int k, int d) {
     return L;
 }
 
-// lists cut to their top k before fs_select (fs_tiles: more than 2 chunks; fs_screen: more than 8 lists)
-static bool fs_lists_cut(const FsLayout& L) { return L.screen ? L.n_lists > 8 : L.n_chunks > 2; }
-
 // workspace: candidate rows | counts | (screen) bf16 item copy
 size_t fs_ws(int64_t nb, int64_t ni, int k, int d) {
     const FsLayout L = fs_layout(nb, ni, k, d);
@@ -1203,16 +1282,11 @@ static int launch_fs(FsArgs& a, const FsLayout& L, hipStream_t s) {
     }
     const dim3 sg((unsigned)((a.nb + 3) / 4));
     if (a.Ib || a.mode == 0) {
-        // raw lists (<= kCap keys, kNK per lane) or lists cut to their top k (<= 2 per lane)
         const int n = a.n_lists;
-        if (!fs_lists_cut(L)) {
-            if (n <= 1) hipLaunchKernelGGL((fs_select<1, kNK>), sg, dim3(256), 0, s, a);
-            else if (n <= 2) hipLaunchKernelGGL((fs_select<2, kNK>), sg, dim3(256), 0, s, a);
-            else if (n <= 4) hipLaunchKernelGGL((fs_select<4, kNK>), sg, dim3(256), 0, s, a);
-            else hipLaunchKernelGGL((fs_select<8, kNK>), sg, dim3(256), 0, s, a);
-        } else if (n <= 4) hipLaunchKernelGGL((fs_select<4, 2>), sg, dim3(256), 0, s, a);
-        else if (n <= 8) hipLaunchKernelGGL((fs_select<8, 2>), sg, dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((fs_select<16, 2>), sg, dim3(256), 0, s, a);
+        if (n <= 2) hipLaunchKernelGGL((fs_select<2>), sg, dim3(256), 0, s, a);
+        else if (n <= 4) hipLaunchKernelGGL((fs_select<4>), sg, dim3(256), 0, s, a);
+        else if (n <= 8) hipLaunchKernelGGL((fs_select<8>), sg, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((fs_select<16>), sg, dim3(256), 0, s, a);
     }
     return last_rc();
 }
