@@ -278,8 +278,10 @@ __global__ __launch_bounds__(256) void gates_fwd(GateArgs a) {
     const int64_t n0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 16;
     const int64_t row = n0 + (lane & 15) < a.n ? n0 + (lane & 15) : -1;
     const Fld<D> it = fload<D>(a.item, row, g);
+    // grid.y = 3: one gate per block row (three times the waves of one block per row tile)
+    const int m0 = gridDim.y > 1 ? (int)blockIdx.y : 0, m1 = gridDim.y > 1 ? m0 + 1 : 3;
 #pragma unroll 1
-    for (int m = 0; m < 3; ++m) {
+    for (int m = m0; m < m1; ++m) {
         const Fld<D> cv = fload<D>(a.conv[m], row, g);
         const Fld<D> s = fmap<D>(mv<D, kLd<D>>(stage_w<D>(wl, a.W[m]), a.b[m], cv, lane), sigm);
         const Fld<D> o = a.mul ? fmap2<D>(it, s, [](float x, float y) { return x * y; })
@@ -296,8 +298,19 @@ __global__ __launch_bounds__(256) void gates_bwd(GateArgs a) {
     const int64_t row = n0 + (lane & 15) < a.n ? n0 + (lane & 15) : -1;
     const Fld<D> it = fload<D>(a.item, row, g);
     Fld<D> gi = fzero<D>();
+    // grid.y = 3 (residual mode): one gate per block row; g_item = sum of the three
+    // upstream gradients (no sigmoid in it) is formed by the gate-0 blocks, in gate order
+    const bool split = gridDim.y > 1;
+    const int m0 = split ? (int)blockIdx.y : 0, m1 = split ? m0 + 1 : 3;
+    if (split && blockIdx.y == 0) {
 #pragma unroll 1
-    for (int m = 0; m < 3; ++m) {
+        for (int m = 0; m < 3; ++m)
+            gi = fmap2<D>(gi, a.gout[m] ? fload<D>(a.gout[m], row, g) : fzero<D>(),
+                          [](float acc, float x) { return acc + x; });
+        fstore<D>(a.g_item, row, g, gi);
+    }
+#pragma unroll 1
+    for (int m = m0; m < m1; ++m) {
         const Fld<D> go = a.gout[m] ? fload<D>(a.gout[m], row, g) : fzero<D>();
         const Fld<D> cv = fload<D>(a.conv[m], row, g);
         const float* W = stage_w<D>(wl, a.W[m]);
@@ -314,7 +327,7 @@ __global__ __launch_bounds__(256) void gates_bwd(GateArgs a) {
         fstore<D>(a.dz[m], row, g, dz);
         fstore<D>(a.g_conv[m], row, g, mvt<D, kLd<D>>(W, dz, lane));
     }
-    fstore<D>(a.g_item, row, g, gi);
+    if (!split) fstore<D>(a.g_item, row, g, gi);
 }
 
 // ---------------------------------------------------------------------------
@@ -1132,7 +1145,9 @@ int rsx_smore_gates(int32_t backward, const float* const* conv, const float* ite
     a.scale = scale;
     a.mul = mul;
     a.g_item = g_item;
-    const dim3 grid((unsigned)(((n + 15) / 16 + 3) / 4));
+    // one gate per block row, except the mul-mode backward (its g_item needs all three
+    // sigmoids of a row: one block runs the three gates)
+    const dim3 grid((unsigned)(((n + 15) / 16 + 3) / 4), (backward && mul) ? 1u : 3u);
     hipStream_t s = as_stream(stream);
     switch (d) {
         case 64:
