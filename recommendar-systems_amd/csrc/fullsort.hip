@@ -1219,17 +1219,39 @@ static int fs_cus() {
     return n;
 }
 
+// fs_screen's item chunks: the most chunks that still fit every (32-user block, chunk)
+// wave in one round of resident slots, when that fills >= 80 % of them (one list per
+// chunk, no split); otherwise enough chunks to exceed the slots, split evenly below
+// (fs_layout).  At most 16 chunks.
+static void screen_plan(int64_t nb, int64_t ni, int d, int* n_chunks, int64_t* chunk_items) {
+    const int64_t n_ub = (nb + 31) / 32;
+    const int64_t slots = (int64_t)fs_cus() * 4 * (d <= 128 ? 2 : 1);  // fs_screen: 2 waves per SIMD, 1 at d = 256
+    int64_t c = slots / n_ub;
+    if (c < 1 || n_ub * c * 5 < slots * 4) c = (slots + n_ub - 1) / n_ub;
+    if (c < 1) c = 1;
+    if (c > 16) c = 16;
+    int64_t per = (ni + c - 1) / c;
+    per = (per + 31) / 32 * 32;
+    *chunk_items = per;
+    *n_chunks = (int)((ni + per - 1) / per);
+}
+
 static FsLayout fs_layout(int64_t nb, int64_t ni, int k, int d) {
     FsLayout L{};
     int nw;
-    fs_plan(nb, ni, d, &nw, &L.n_chunks, &L.chunk_items);
     L.screen = fs_use_screen(k, d, ni);
+    if (L.screen) screen_plan(nb, ni, d, &L.n_chunks, &L.chunk_items);
+    else fs_plan(nb, ni, d, &nw, &L.n_chunks, &L.chunk_items);
     L.n_lists = L.n_chunks;
     L.seg_slots = 1;
     const int64_t n_ub = (nb + 31) / 32;
     const int C = L.n_chunks;
     L.blocks = n_ub * C;
-    if (L.screen && (8 % C) == 0) {
+    static const int seg_env = [] {
+        const char* e = getenv("RSX_FS_SEG");  // 0: no balanced split (tuning)
+        return e ? atoi(e) : 1;
+    }();
+    if (L.screen && seg_env && (8 % C) == 0) {
         const int64_t slots = (int64_t)fs_cus() * 4 * (d <= 128 ? 2 : 1);  // fs_screen: 2 waves per SIMD, 1 at d = 256
         const int64_t wc = slots / C;
         if (n_ub * C > slots && wc >= 1) {
@@ -1393,11 +1415,9 @@ size_t rsx_fullsort_ws_bytes(int64_t n_batch, int64_t n_items, int32_t k) {
 
 int rsx_fullsort_plan(int64_t n_batch, int64_t n_items, int32_t d, int32_t* n_chunks, int64_t* chunk_items) {
     if (!n_chunks || !chunk_items || n_batch < 0 || n_items <= 0) return RSX_ERR_ARG;
-    int nw, nc;
-    int64_t per;
-    rsx::fs_plan(n_batch, n_items, d, &nw, &nc, &per);
-    *n_chunks = nc;
-    *chunk_items = per;
+    const rsx::FsLayout L = rsx::fs_layout(n_batch, n_items, 50, d);  // the plan of k <= 64 calls
+    *n_chunks = L.n_chunks;
+    *chunk_items = L.chunk_items;
     return RSX_OK;
 }
 

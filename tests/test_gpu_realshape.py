@@ -5,7 +5,7 @@ many-small-chunks plan and the SpMM's in-launch hub fixups.  These tests run the
 production plans and check them on the CPU:
 
 * full-sort at the C2 shape (35,598 users x 18,357 items, d=64: 2 chunks of 9,184
-  items), the C5 shape (39,387 x 23,033, d=128: 1 chunk), a 15-chunk plan and a
+  items), the C5 shape (39,387 x 23,033, d=128: 2 chunks), a 16-chunk plan and a
   C4-like chunk (d=256, 2 chunks of 200,000 items).  Integer-valued embeddings make
   every score exact in f32, so the top-k indices must equal the oracle's canonical
   top-k (score desc, index asc) bit for bit, including runs of tied scores across
@@ -85,9 +85,10 @@ def _run_fullsort(cuda, U, users, I, rp, mc, k=50):
     return val.cpu().numpy(), idx.cpu().numpy()
 
 
-# (n_users, n_items, d, expected item chunks): C2 sports, C5 clothing, a 15-chunk
-# plan (fs_select<16,2> over lists cut to top k), a C4-like 200k-item chunk at d=256
-SHAPES = [(35598, 18357, 64, 2), (39387, 23033, 128, 1), (4096, 18357, 64, 15), (16384, 400000, 256, 2)]
+# (n_users, n_items, d, expected item chunks): C2 sports and C5 clothing (2 chunks, the
+# balanced split of the screened kernel: 4 lists a user), a 16-chunk plan (fs_select<16>
+# over lists cut to top k), a C4-like 200k-item chunk at d=256
+SHAPES = [(35598, 18357, 64, 2), (39387, 23033, 128, 2), (4096, 18357, 64, 16), (16384, 400000, 256, 2)]
 
 
 @pytest.mark.parametrize("pattern", ["ties", "ramp"])
