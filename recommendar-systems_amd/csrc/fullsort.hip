@@ -582,8 +582,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D <= 64 ? 2 
 #define RSX_FS_SCREEN_WPE 2  // fs_screen waves per SIMD requested at d <= 64
 #endif
 #ifndef RSX_FS_ABUF
-#define RSX_FS_ABUF 1  // fs_screen item-operand buffers (2: the next tile's loads issued before the MFMAs)
+#define RSX_FS_ABUF 3  // fs_screen item-operand buffers at d <= 64 (a ring: loads NB - 1 tiles ahead; 1 at d > 64)
 #endif
+template <int D>
+constexpr int kAbuf = D <= 64 ? RSX_FS_ABUF : 1;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
@@ -600,6 +602,19 @@ __device__ __forceinline__ bf16x8 pack_bf16x8(float4 p, float4 q) {
     const u32x4 w = {pack_bf16x2(p.x, p.y), pack_bf16x2(p.z, p.w), pack_bf16x2(q.x, q.y), pack_bf16x2(q.z, q.w)};
     return __builtin_bit_cast(bf16x8, w);
 }
+// v_max_f32 / v_med3_f32 as single instructions: the builtins' IEEE-mode lowering adds a
+// canonicalising max per operand (scores are finite here)
+__device__ __forceinline__ float vmax(float a, float b) {
+    float r;
+    asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ float vmed3(float a, float b, float c) {
+    float r;
+    asm("v_med3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
 // bf16 bits of the smallest bf16 >= x (x >= 0 finite)
 __device__ __forceinline__ unsigned bf16_up(float x) { return (__float_as_uint(x) + 0xffffu) >> 16; }
 
@@ -714,11 +729,14 @@ __device__ __forceinline__ void screen_segment(const FsArgs& a, int64_t ub, int 
         }
         return mb;
     };
-    // A operand: item i0 + 32 t + j, half h (the padded bf16 copy: no clamps), one
-    // buffer refilled with the next tile as soon as the MFMAs have read it
-    u32x4 ra[RSX_FS_ABUF][NM + 1];
+    // A operand: item i0 + 32 t + j, half h (the padded bf16 copy: no clamps).  NB > 1:
+    // a ring of NB buffers, tile t's MFMAs preceded by the loads of tile t + NB - 1 (two
+    // tiles of latency cover at two waves per SIMD); NB = 1: one buffer refilled with
+    // the next tile as soon as the MFMAs have read it
+    constexpr int NB = kAbuf<D>;
+    u32x4 ra[NB][NM + 1];
     auto load_a = [&](auto par, int t) __attribute__((always_inline)) {
-        constexpr int P = decltype(par)::value % RSX_FS_ABUF;
+        constexpr int P = decltype(par)::value % NB;
         const __bf16* row = a.Ib + (i0 + (int64_t)t * 32 + j) * DP;
         const u32x4* p = reinterpret_cast<const u32x4*>(row + h * HALF);
 #pragma unroll
@@ -726,18 +744,34 @@ __device__ __forceinline__ void screen_segment(const FsArgs& a, int64_t ub, int 
         ra[P][NM] = *reinterpret_cast<const u32x4*>(row + D + 8 * h);
     };
     auto tile = [&](auto par, int t, floatx16& acc) __attribute__((always_inline)) {
-        constexpr int P = decltype(par)::value % RSX_FS_ABUF;
-        // unconditional (the last tile reloads itself): a conditional load would make the
-        // compiler's wait before the MFMAs cover the prefetch too
-        const int tn = t + 1 < ntiles ? t + 1 : t;
-        if constexpr (RSX_FS_ABUF == 2) load_a(IntC<P ^ 1>{}, tn);
+        constexpr int P = decltype(par)::value % NB;
+        // unconditional (past the end the last tile reloads itself): a conditional load
+        // would make the compiler's wait before the MFMAs cover the prefetch too
+        const int ta = t + (NB > 1 ? NB - 1 : 1);
+        const int tn = ta < ntiles ? ta : ntiles - 1;
+        if constexpr (NB > 1) load_a(IntC<(P + NB - 1) % NB>{}, tn);
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[r] = 0.f;
 #pragma unroll
         for (int s = 0; s <= NM; ++s)
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, ra[P][s]),
                                                           __builtin_bit_cast(bf16x8, bu[s]), acc, 0, 0, 0);
-        if constexpr (RSX_FS_ABUF == 1) load_a(IntC<0>{}, tn);
+        if constexpr (NB == 1) load_a(IntC<0>{}, tn);
+    };
+    // the first NB - 1 tiles' loads, then tiles in groups of NB (ring slots by template)
+    auto prime = [&]() __attribute__((always_inline)) {
+        if (ntiles <= 0) return;
+        load_a(IntC<0>{}, 0);
+        if constexpr (NB > 2) load_a(IntC<1>{}, ntiles > 1 ? 1 : 0);
+    };
+    auto sweep = [&](auto&& body) __attribute__((always_inline)) {
+        for (int t = 0; t < ntiles; t += NB) {
+            body(IntC<0>{}, t);
+            if constexpr (NB > 1)
+                if (t + 1 < ntiles) body(IntC<1>{}, t + 1);
+            if constexpr (NB > 2)
+                if (t + 2 < ntiles) body(IntC<2>{}, t + 2);
+        }
     };
 
     // pass 1: the two largest lower bounds per slot
@@ -751,12 +785,12 @@ __device__ __forceinline__ void screen_segment(const FsArgs& a, int64_t ub, int 
         floatx16 acc;
         tile(par, t, acc);
         const int rem = (int)(i1 - tb);
-        // top two by median-of-three (t1 >= t2): t2 = med3(t1, t2, x), t1 = med3(t1, x, +inf)
+        // top two by median-of-three (t1 >= t2): t2 = med3(t1, t2, x), t1 = max(t1, x)
         if (rem >= 32 && __ballot(mb != 0u) == 0ull) {  // wave-uniform: no masked or missing item
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                t2[r] = __builtin_amdgcn_fmed3f(t1[r], t2[r], acc[r]);
-                t1[r] = __builtin_amdgcn_fmed3f(t1[r], acc[r], INFINITY);
+                t2[r] = vmed3(t1[r], t2[r], acc[r]);
+                t1[r] = vmax(t1[r], acc[r]);
             }
         } else {
             // slot r <-> item io(r) + 4 h: shift the mask and the bound by 4 h once, so the
@@ -767,16 +801,13 @@ __device__ __forceinline__ void screen_segment(const FsArgs& a, int64_t ub, int 
             for (int r = 0; r < 16; ++r) {
                 const int io = (r & 3) + 8 * (r >> 2);
                 const float l = io >= remh ? -INFINITY : (((mbh >> io) & 1u) ? -1e10f : acc[r]);
-                t2[r] = __builtin_amdgcn_fmed3f(t1[r], t2[r], l);
-                t1[r] = __builtin_amdgcn_fmed3f(t1[r], l, INFINITY);
+                t2[r] = vmed3(t1[r], t2[r], l);
+                t1[r] = vmax(t1[r], l);
             }
         }
     };
-    if (ntiles > 0) load_a(IntC<0>{}, 0);
-    for (int t = 0; t < ntiles; t += 2) {
-        pass1(IntC<0>{}, t);
-        if (t + 1 < ntiles) pass1(IntC<1>{}, t + 1);
-    }
+    prime();
+    sweep(pass1);
     // L = the k-th largest of the lane pair's 64 bounds (radix search on ordered words)
     unsigned th = 0;
     for (int bit = 31; bit >= 0; --bit) {
@@ -902,11 +933,8 @@ __device__ __forceinline__ void screen_segment(const FsArgs& a, int64_t ub, int 
         }
         if (qn >= 64) drain(false);
     };
-    if (ntiles > 0) load_a(IntC<0>{}, 0);
-    for (int t = 0; t < ntiles; t += 2) {
-        pass2(IntC<0>{}, t);
-        if (t + 1 < ntiles) pass2(IntC<1>{}, t + 1);
-    }
+    prime();
+    sweep(pass2);
     drain(true);
     __syncthreads();
     cnt = lcnt[j];
