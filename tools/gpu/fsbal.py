@@ -1,4 +1,5 @@
-"""Full-sort timing vs the number of 32-user waves (sports item count, d = 64).
+"""Full-sort timing vs the number of 32-user waves (sports item count, d = 64; env FS_NI,
+FS_D for other shapes).
 
 Random tables and a random train mask; prints ms per call and TF/s for each user
 count, to show how the kernel's time follows waves per SIMD.
@@ -14,13 +15,14 @@ from rsx import ops  # noqa: E402
 
 
 def main():
-    ni, d, k = 18357, 64, 50
+    ni, d, k = int(os.environ.get("FS_NI", 18357)), int(os.environ.get("FS_D", 64)), 50
     nbs = [int(x) for x in sys.argv[1:]] or [32768, 35598, 40960, 49152]
     g = torch.Generator().manual_seed(0)
     dev = torch.device("cuda:0")
-    items = (torch.randn(ni, d, generator=g) * 0.1).to(dev)
+    gd = torch.Generator(device=dev).manual_seed(0)
+    items = torch.randn(ni, d, generator=gd, device=dev) * 0.1
     for nb in nbs:
-        users = (torch.randn(nb, d, generator=g) * 0.1).to(dev)
+        users = torch.randn(nb, d, generator=gd, device=dev) * 0.1
         per = 8
         col = torch.randint(0, ni, (nb, per), generator=g).sort(1).values
         rp = torch.arange(0, nb * per + 1, per, dtype=torch.int64)
