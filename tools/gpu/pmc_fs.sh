@@ -6,7 +6,7 @@ OUT=${OUT:-gpurun_out/pmcfs}
 mkdir -p $OUT
 for m in ${MODES:-0 5}; do
   RSX_FS_MODE=$m timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_VALU_MFMA_BUSY_CYCLES \
-    --kernel-include-regex "fs_screen" --output-format csv -d $OUT/m$m -o run -- python tools/gpu/fsbal.py 32768 > $OUT/m$m.log 2>&1 || exit 1
+    --kernel-include-regex "fs_screen" --output-format csv -d $OUT/m$m -o run -- python tools/gpu/fsbal.py ${NBS:-32768} > $OUT/m$m.log 2>&1 || exit 1
 done
 python - <<'PY'
 import csv, glob, os, collections
