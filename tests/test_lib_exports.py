@@ -85,3 +85,19 @@ def test_schedule_host_splits_hub_rows():
     big = np.array([0, 1 << 31], dtype=np.int64)
     assert lib.rsx_csr_schedule_host(big.ctypes.data_as(C.c_void_p), 1, 32, None, None, C.byref(nw),
                                      C.byref(nl), C.byref(ns)) == 1001
+
+
+@pytest.mark.parametrize("nb,ni,d,chunks,per", [
+    (35598, 18357, 64, 2, 9184),      # C2: two chunks, the balanced split (2,226 waves > 2,048 slots)
+    (19445, 7050, 64, 3, 2368),       # baby: three chunks fill 89 % of the slots in one round
+    (39387, 23033, 128, 2, 11520),    # C5
+    (4096, 18357, 64, 16, 1152),      # few users: 16 chunks (lists cut to top k)
+    (16384, 400000, 256, 2, 200000),  # C4-like d = 256 (one wave per SIMD)
+    (40, 500, 64, 16, 32),            # tiny: at most 16 chunks
+])
+def test_fullsort_plan_host(nb, ni, d, chunks, per):
+    """The screened full-sort's item-chunk plan (csrc/fullsort.hip screen_plan, 256 CUs
+    assumed without a GPU), as rsx_fullsort_plan reports it."""
+    nc, pi = C.c_int32(), C.c_int64()
+    L.check(L.lib().rsx_fullsort_plan(nb, ni, d, C.byref(nc), C.byref(pi)), "rsx_fullsort_plan")
+    assert (nc.value, pi.value) == (chunks, per)
