@@ -567,8 +567,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D <= 64 ? 2 
 //    the margin eps |u| |v_i| rides in the MFMA as one more K block: the item's bf16
 //    row carries |v_i| and the user's carries -+eps |u|, both rounded up, so the
 //    accumulator holds the bound itself;
-//  * pass 1: each lane keeps, per accumulator slot, the two largest lower bounds
-//    s~ - eps |u||v_i| (masked items: exactly -1e10) -- 64 distinct items per user --
+//  * pass 1: each lane keeps, per accumulator slot, the three largest lower bounds
+//    s~ - eps |u||v_i| (masked items: exactly -1e10) -- 96 distinct items per user --
 //    and the k-th largest of them, L, is a lower bound of the user's exact k-th
 //    score (k items are known to score >= L);
 //  * pass 2: an item whose upper bound s~ + eps |u||v_i| is >= L (> the running
@@ -582,7 +582,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D <= 64 ? 2 
 #define RSX_FS_SCREEN_WPE 2  // fs_screen waves per SIMD requested at d <= 64
 #endif
 #ifndef RSX_FS_ABUF
-#define RSX_FS_ABUF 3  // fs_screen item-operand buffers at d <= 64 (a ring: loads NB - 1 tiles ahead; 1 at d > 64)
+#define RSX_FS_ABUF 1  // fs_screen item-operand buffers at d <= 64 (a ring: loads NB - 1 tiles ahead; 1 at d > 64)
+#endif
+#ifndef RSX_FS_TOP
+#define RSX_FS_TOP 3  // fs_screen pass-1 samples per accumulator slot (2 or 3): 32 * TOP distinct items a user
 #endif
 template <int D>
 constexpr int kAbuf = D <= 64 ? RSX_FS_ABUF : 1;
@@ -774,10 +777,10 @@ __device__ __forceinline__ void screen_segment(const FsArgs& a, int64_t ub, int 
         }
     };
 
-    // pass 1: the two largest lower bounds per slot
-    float t1[16], t2[16];
+    // pass 1: the RSX_FS_TOP largest lower bounds per slot (t3 unused at 2)
+    float t1[16], t2[16], t3[16];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) t1[r] = t2[r] = -INFINITY;
+    for (int r = 0; r < 16; ++r) t1[r] = t2[r] = t3[r] = -INFINITY;
     auto pass1 = [&](auto par, int t) __attribute__((always_inline)) {
         // the mask cursor first: its loads' waits then precede the next tile's prefetch
         const int64_t tb = i0 + (int64_t)t * 32;
@@ -789,6 +792,7 @@ __device__ __forceinline__ void screen_segment(const FsArgs& a, int64_t ub, int 
         if (rem >= 32 && __ballot(mb != 0u) == 0ull) {  // wave-uniform: no masked or missing item
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
+                if constexpr (RSX_FS_TOP == 3) t3[r] = vmed3(t2[r], t3[r], acc[r]);
                 t2[r] = vmed3(t1[r], t2[r], acc[r]);
                 t1[r] = vmax(t1[r], acc[r]);
             }
@@ -801,6 +805,7 @@ __device__ __forceinline__ void screen_segment(const FsArgs& a, int64_t ub, int 
             for (int r = 0; r < 16; ++r) {
                 const int io = (r & 3) + 8 * (r >> 2);
                 const float l = io >= remh ? -INFINITY : (((mbh >> io) & 1u) ? -1e10f : acc[r]);
+                if constexpr (RSX_FS_TOP == 3) t3[r] = vmed3(t2[r], t3[r], l);
                 t2[r] = vmed3(t1[r], t2[r], l);
                 t1[r] = vmax(t1[r], l);
             }
@@ -808,13 +813,16 @@ __device__ __forceinline__ void screen_segment(const FsArgs& a, int64_t ub, int 
     };
     prime();
     sweep(pass1);
-    // L = the k-th largest of the lane pair's 64 bounds (radix search on ordered words)
+    // L = the k-th largest of the lane pair's 32 * RSX_FS_TOP bounds (radix search on
+    // ordered words)
     unsigned th = 0;
     for (int bit = 31; bit >= 0; --bit) {
         const unsigned c = th | (1u << bit);
         int n = 0;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) n += (int)(ord_f32(t1[r]) >= c) + (int)(ord_f32(t2[r]) >= c);
+        for (int r = 0; r < 16; ++r)
+            n += (int)(ord_f32(t1[r]) >= c) + (int)(ord_f32(t2[r]) >= c) +
+                 (RSX_FS_TOP == 3 ? (int)(ord_f32(t3[r]) >= c) : 0);
         n += __shfl_xor(n, 32, kWave);
         if (n >= a.k) th = c;
     }
