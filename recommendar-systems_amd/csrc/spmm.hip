@@ -642,15 +642,24 @@ __global__ __launch_bounds__(kBlock) void rowwise_kernel(int64_t n_rows, rsx_epi
     epilogue<KIND, D>(e, row, f4(0.f), li);
 }
 
-// Work blocks per launch: enough to fill the chip once (later items are walked by
-// the same groups); RSX_SPMM_MAXB overrides (tuning).
-static int64_t spmm_max_blocks() {
-    static int64_t v = [] {
-        const char* f = getenv("RSX_SPMM_MAXB");
-        const long long x = f ? atoll(f) : 0;
-        return (int64_t)(x > 0 ? x : 2048);
-    }();
-    return v;
+// Work blocks per launch (n = the blocks the work list would need): enough to fill
+// the chip once, later items walked by the same groups.  A d = 64 list needing more
+// than one 2,048-block round gets 1,536 longer-lived blocks (C2 step 133.6-135.0 us
+// against 135.8-137.8 at 2,048 and 152 at 1,024; its ADAM layer 33.5 vs 35.2-35.9
+// us), while a list that fits one round launches whole (baby: 111 us/step whole,
+// 115 capped at 1,536; tools/gpu/maxb_sweep.sh, ab_legs.sh).  RSX_SPMM_MAXB
+// overrides (tuning), RSX_SPMM_MAXB_ADAM for the Adam-epilogue kind alone.
+static int64_t env_blocks(const char* name) {
+    const char* f = getenv(name);
+    const long long x = f ? atoll(f) : 0;
+    return (int64_t)(x > 0 ? x : 0);
+}
+static int64_t spmm_max_blocks(int kind, int d, int64_t n) {
+    static const int64_t all = env_blocks("RSX_SPMM_MAXB");
+    static const int64_t adam = env_blocks("RSX_SPMM_MAXB_ADAM");
+    if (kind == RSX_EPI_ADAM && adam > 0) return adam;
+    if (all > 0) return all;
+    return d <= 64 && n > 2048 ? 1536 : 2048;
 }
 
 // Fixup blocks ride in the same launch only while they cannot fill the chip (so
@@ -663,7 +672,7 @@ static int launch_spmm(const rsx_csr& a, const float* x, const rsx_epilogue& e, 
                        hipStream_t s, const TagJob& tj) {
     constexpr int GPB = kBlock / (D / 4);
     int64_t n_main = (a.n_work + GPB - 1) / GPB;
-    if (n_main > spmm_max_blocks()) n_main = spmm_max_blocks();
+    n_main = std::min(n_main, spmm_max_blocks(KIND, D, n_main));
     const bool inl = a.n_long <= kInlineFixups;
     const int64_t n_tag = tj.batch > 0 ? (3 * tj.batch + kBlock - 1) / kBlock : 0;
     const int64_t nb = n_main + (inl ? a.n_long : 0) + n_tag;
@@ -682,7 +691,7 @@ static int launch_batch(SpmmBatch& b, hipStream_t s) {
     int64_t nm = 0, nf = 0;
     for (int p = 0; p < b.count; ++p) {
         int64_t n_main = (b.a[p].n_work + GPB - 1) / GPB;
-        if (n_main > spmm_max_blocks()) n_main = spmm_max_blocks();
+        n_main = std::min(n_main, spmm_max_blocks(KIND, D, n_main));
         b.n_main[p] = n_main;
         b.main_off[p] = nm;
         b.fix_off[p] = nf;
