@@ -349,6 +349,117 @@ def _json_line(out):
 _STDOUT_FD = 1
 
 
+def _free_port():
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch(argv, n):
+    """`bench.py --gpus N` without an external launcher: start N rank processes of this
+    script (one per GPU, LOCAL_RANK = rank) with the torch.distributed env a torchrun
+    launch would give them, relay rank 0's JSON line, and return the worst exit code.
+    This process never touches the GPU (no HIP call before or after the children), so
+    nothing here initialises a device that a child then shares.  Replaces the
+    reference's one-device pinning (src/utils/configurator.py:114-118)."""
+    import subprocess
+    import tempfile
+
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    out_path = tempfile.mkstemp(prefix="rsx_bench_rank0_", suffix=".json")[1]
+    procs = []
+    base = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=port, WORLD_SIZE=str(n),
+                LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", RSX_BENCH_LAUNCHER="bench.py --gpus")
+    base.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on these hosts (RCCL peer maps)
+    with open(out_path, "wb") as f0:
+        for r in range(n):
+            env = dict(base, RANK=str(r), LOCAL_RANK=str(r))
+            procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env,
+                                          stdout=f0 if r == 0 else sys.stderr.fileno(), stderr=None))
+        rcs = [None] * n
+        import time as _t
+
+        while any(rc is None for rc in rcs):
+            for r, p in enumerate(procs):
+                if rcs[r] is None:
+                    rcs[r] = p.poll()
+            failed = [r for r, rc in enumerate(rcs) if rc not in (None, 0)]
+            if failed:  # one rank died: its peers would block in a collective forever
+                for r, p in enumerate(procs):
+                    if rcs[r] is None:
+                        p.terminate()
+                for r, p in enumerate(procs):
+                    try:
+                        rcs[r] = p.wait(timeout=30)
+                    except subprocess.TimeoutExpired:
+                        p.kill()
+                        rcs[r] = p.wait()
+                log(f"[bench] launcher: rank(s) {failed} failed, exit codes {rcs}")
+                break
+            _t.sleep(0.05)
+    with open(out_path, "rb") as f0:
+        line = f0.read()
+    os.unlink(out_path)
+    if line:
+        os.write(_STDOUT_FD, line)
+    bad = [rc for rc in rcs if rc]
+    return bad[0] if bad else 0
+
+
+def _rank_report(wall_s, gpu_ms, steps, world, dev):
+    """Every rank's (ms/step wall, ms/step device events), gathered to rank order."""
+    mine = torch.tensor([wall_s * 1e3 / steps, gpu_ms / steps], dtype=torch.float64, device=dev)
+    if world == 1:
+        return [{"rank": 0, "ms_per_step": float(mine[0]), "gpu_ms_per_step_events": float(mine[1])}]
+    parts = [torch.empty_like(mine) for _ in range(world)]
+    torch.distributed.all_gather(parts, mine)
+    return [{"rank": r, "ms_per_step": float(p[0]), "gpu_ms_per_step_events": float(p[1])}
+            for r, p in enumerate(parts)]
+
+
+def dry_run(args):
+    """The N-rank launch and reporting without a GPU (CPU tests): gloo group, the
+    world size observed by an all-reduce of ones, K timed CPU 'steps' per rank
+    (a fixed small matmul), max-over-ranks time, per-rank report on rank 0."""
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if os.environ.get("RSX_BENCH_DRY_FAIL_RANK") == str(rank):  # test hook: a rank that dies
+        raise SystemExit(3)
+    if world > 1:
+        dist.init_process_group("gloo")
+    ones = torch.ones(1)
+    if world > 1:
+        dist.all_reduce(ones)
+    x = torch.randn(64, 64)
+
+    def step():
+        return x @ x
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    per_rank = _rank_report(wall, 0.0, args.steps, world, torch.device("cpu"))
+    tmax = max(p["ms_per_step"] for p in per_rank) * args.steps / 1e3
+    if rank == 0:
+        _json_line({"metric": METRIC, "value": None, "unit": "interactions/s", "n_gpus": world,
+                    "steps": args.steps, "warmup": args.warmup, "ms_per_step": tmax * 1e3 / args.steps,
+                    "dry_run": True, "launcher": os.environ.get("RSX_BENCH_LAUNCHER", "external"),
+                    "world_size_observed": int(ones.item()), "per_rank": per_rank})
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     global _STDOUT_FD
     # RCCL / HIP print banners on fd 1 at communicator init: keep fd 1 for the JSON line
@@ -371,7 +482,18 @@ def main():
     ap.add_argument("--eval-users", type=int, default=None, help="default: all valid users (c4: 32768 per rank)")
     ap.add_argument("--c4-chunks", type=int, default=None,
                     help="c4: build only the first N of the 8 1.25M-user chunks (1 = one rank's share at 8 GPUs)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU only: exercise the N-rank launch and report (gloo), no GPU work")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no external launcher (torchrun sets WORLD_SIZE): start the N ranks here
+        raise SystemExit(launch(sys.argv[1:], args.gpus))
+    if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) != args.gpus:
+        log(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']}; the world size wins")
+    if args.dry_run:
+        args.steps = args.steps if args.steps is not None else 3
+        args.warmup = args.warmup if args.warmup is not None else 1
+        return dry_run(args)
     big = args.workload == "c4"
     args.steps = args.steps if args.steps is not None else (20 if big else 200)
     args.warmup = args.warmup if args.warmup is not None else (3 if big else 20)
@@ -384,6 +506,12 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # c4 is the strong-scaling leg: the graph AND the global batch (--batch) are fixed, each
+    # rank draws its share of the batch from its own users; c2/baby are weak scaling: every
+    # rank owns its own sports/baby-shaped user block and a batch of --batch
+    B = args.batch // world if big else args.batch
+    if big and B * world != args.batch:
+        raise SystemExit(f"--batch {args.batch} does not split evenly over {world} ranks")
     tu, ti, vu_all, vi_all, nu, ni, d, desc = load_graph(args.workload, rank, world, args.c4_chunks)
     if big and args.c4_chunks:
         desc += f" [only {args.c4_chunks} of 8 user chunks built]"
@@ -415,9 +543,9 @@ def main():
         from rsx.dist import ShardedLightGCNEngine
 
         eng = ShardedLightGCNEngine(tu, ti, nu, ni, d, 3, 1e-2, 1e-3, dev, U0, I0, seed=rank,
-                                    batch=args.batch)
+                                    batch=B)
     else:
-        eng = LightGCNEngine(tu, ti, nu, ni, d, 3, 1e-2, 1e-3, dev, U0, I0, seed=0, batch=args.batch)
+        eng = LightGCNEngine(tu, ti, nu, ni, d, 3, 1e-2, 1e-3, dev, U0, I0, seed=0, batch=B)
     del U0, I0
     E = eng.n_inter
     parts = [eng.adj] if hasattr(eng, "adj") else [eng.A_U, eng.A_I]
@@ -428,10 +556,10 @@ def main():
     done = {"inter": 0}
 
     def one_step():
-        b = min(args.batch, E - pos["start"])
+        b = min(B, E - pos["start"])
         eng.step(epoch=pos["epoch"], start=pos["start"])
         done["inter"] += b
-        pos["start"] += args.batch
+        pos["start"] += B
         if pos["start"] >= E:
             pos["start"] = 0
             pos["epoch"] += 1
@@ -453,6 +581,14 @@ def main():
         torch.distributed.barrier()
     wall = time.perf_counter() - t0
     gpu_ms = ev0.elapsed_time(ev1)
+    per_rank = _rank_report(wall, gpu_ms, args.steps, world, dev)
+    rccl_world = None
+    if sharded and getattr(eng, "_comm", None) is not None:
+        # the world the step's own communicator spans: an all-reduce of ones on rsx_comm
+        ones = torch.ones(1, dtype=torch.float32, device=dev)
+        L.check(L.lib().rsx_comm_allreduce_f32(eng._comm, ones.data_ptr(), 1, ops._stream()),
+                "rsx_comm_allreduce_f32")
+        rccl_world = int(round(float(ones.item())))
     t_rank = torch.tensor([wall, float(done["inter"])], dtype=torch.float64, device=dev)
     if world > 1:
         tmax = t_rank[:1].clone()
@@ -486,7 +622,7 @@ def main():
             torch.distributed.all_reduce(er[:1], op=torch.distributed.ReduceOp.MAX)
             torch.distributed.all_reduce(er[1:], op=torch.distributed.ReduceOp.SUM)
         epoch_rate = {"interactions_per_s": float(er[1] / er[0]), "s_per_epoch": float(er[0]),
-                      "batches_per_rank": -(-E // args.batch),
+                      "batches_per_rank": -(-E // B),
                       "includes": "the epoch's device sampling launch (shuffle + negatives), every batch's step"}
 
     # full-sort evaluation throughput (forward once + fused MFMA scores/mask/top-50)
@@ -582,7 +718,7 @@ def main():
         adam_ms = time_kernel(adam_layer, 50)
         # S_spmm + Adam's row streams (reads p, m, v; writes m, v: p's write
         # is S's Y) = S + 20 N d; G' is read on the batch rows only (+ 12 B d per row)
-        adam_alg = alg + 20 * (nu + ni) * d + 12 * 3 * args.batch * d
+        adam_alg = alg + 20 * (nu + ni) * d + 12 * 3 * B * d
         adam_ach = adam_alg / (adam_ms * 1e-3) / 1e9
         roof = {"bound": "hbm", "kernel": f"spmm_main<{d},ADAM> (last backward layer + Adam, batch-row tags; "
                                           "the step's largest launch)",
@@ -622,7 +758,11 @@ def main():
                     ("synthetic C4 graph (rsx.synth.chunk_graph: 8 seeded 1.25M-user chunks, Zipf(0.8) items, "
                      "5+Geometric degrees mean 10, reference split rule); xavier-uniform-bound init"),
             "config": {"workload": desc, "model": "LightGCN", "n_layers": 3, "embedding_size": d,
-                       "global_batch": args.batch * world,
+                       "global_batch": B * world, "per_rank_batch": B,
+                       "leg": ("the metric's leg: C2 per rank, weak scaling (per-GPU work fixed as N grows)"
+                               if args.workload == "c2" else
+                               "strong-scaling leg: the fixed C4 graph and global batch split over the ranks"
+                               if big else "baby per rank, weak scaling"),
                        "parallelism": f"rowshard{world}" if sharded else "single"},
             "fullsort_items_per_s": items_per_s,
             "fullsort": {"eval_users": int(n_eval), "n_items": ni, "k": 50,
@@ -639,6 +779,9 @@ def main():
             "roofline_kernels": kernels,
             "cpu_baseline": cpu,
             "epoch": epoch_rate,
+            "launcher": os.environ.get("RSX_BENCH_LAUNCHER", "torchrun" if world > 1 else "single process"),
+            "rccl_world_size": rccl_world,
+            "per_rank": per_rank,
             "gpu_ms_per_step_events": gpu_ms / args.steps,
             "train_loss_mean": loss_mean,
         }

@@ -377,7 +377,7 @@ typedef struct rsx_lgcn_step {
      * per-row occurrence counts (+ a done counter and three scales in the tail) that
      * the Adam layer applies and clears; R is not used. */
     int32_t* reg_cnt;
-    /* Optional with reg_cnt: [2] int32, zero-filled.  The first step whose loss is NaN
+    /* Optional (any path: tagged, dense, K >= 4): [2] int32, zero-filled.  The first step whose loss is NaN
      * sets halt[0] = 1 and halt[1] = its tag; from then on the Adam layer leaves the
      * parameters and moments unchanged, so they stay those of the last finite step (the
      * reference checks the loss before backward and stops, src/common/trainer.py:201-203). */
@@ -627,14 +627,25 @@ int rsx_smore_infonce_bwd_scaled(const float* side, const float* content, const 
  *     mult = -lr, its restore with mult = +lr), one launch per 32 tensors.
  * lr_dev (optional, device f64): the learning rate is read there instead (lr is
  * ignored; axpy uses mult * *lr_dev), so a captured step stays valid when the
- * LambdaLR schedule changes lr between epochs.
+ * LambdaLR schedule changes lr between epochs.  halt (optional, device int32, set by
+ * rsx_nan_gate): when *halt != 0 nothing is updated.
  */
 size_t rsx_mg_alpha_ws_bytes(int32_t count, const int64_t* n);
 int rsx_mg_alpha(int32_t count, const float* const* params, const float* const* grads, const int64_t* n,
                  double base, double lr, double rel_step, double max_scale, double* alpha_out, void* ws,
                  size_t ws_bytes, const double* lr_dev, rsx_stream_t stream);
 int rsx_axpy_multi(int32_t count, float* const* y, const float* const* x, const int64_t* n,
-                   const double* alpha_dev, double mult, const double* lr_dev, rsx_stream_t stream);
+                   const double* alpha_dev, double mult, const double* lr_dev, const int32_t* halt,
+                   rsx_stream_t stream);
+/*
+ * The batch loss's NaN check (reference src/common/trainer.py:192-203: a NaN loss ends
+ * training before backward) without a host sync: counter[0] += 1 (the batch's 1-based
+ * index in the epoch), and on the first NaN *loss halt = {1, that index}.  The
+ * optimizer launches that take `halt` (rsx_adam_multi_scaled, rsx_axpy_multi) then
+ * leave every parameter and moment as it was, so the parameters stay those before the
+ * NaN batch; the trainer reads halt once at the end of the epoch.  Capturable.
+ */
+int rsx_nan_gate(const float* loss, int32_t* halt, int32_t* counter, rsx_stream_t stream);
 /*
  * SMORE's spectral filter weights (reference src/models/smore.py:221-229): three
  * [d/2+1][2] (re, im) parameters -> out [3][d/2+1][2], each w / (|w| + 1e-8) when
@@ -660,11 +671,12 @@ int rsx_adam_multi(int32_t count, float* const* p, const float* const* g, float*
 /* The same with the gradient taken as g * grad_scale (an f32 product, as the
  * reference's p.grad.mul_(-mg_beta) before the mirror-gradient step,
  * src/common/trainer.py:327-330, folded into the update); lr_dev (optional, device
- * f64): the learning rate read on the device (rounded to f32) instead of lr. */
+ * f64): the learning rate read on the device (rounded to f32) instead of lr; halt
+ * (optional, rsx_nan_gate's flag): when *halt != 0 nothing is updated. */
 int rsx_adam_multi_scaled(int32_t count, float* const* p, const float* const* g, float* const* m, float* const* v,
                           const int64_t* const* step_dev, const int64_t* n, float lr, float beta1, float beta2,
                           float eps, float weight_decay, float grad_scale, const double* lr_dev,
-                          rsx_stream_t stream);
+                          const int32_t* halt, rsx_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
 /* SMORE kNN item graph (knn.hip)                                             */
@@ -693,10 +705,16 @@ int rsx_knn_graph(const float* feat, int64_t n, int32_t f, int32_t k, float* val
  * rows (users first, item column ids offset by n_users), columns sorted per row:
  *   mode 0  LightGCN / LayerGCN eval graph (src/models/lightgcn.py:65-103):
  *           (d_r + 1e-7)^-1/2 (d_c + 1e-7)^-1/2 in float64, cast to float32;
- *   mode 1  SMORE (src/models/smore.py:176-207): float32 d^-1/2, inf -> 0, d_r*1*d_c
- *           (d^-1/2 correctly rounded from float64; the reference's numpy float32
- *           power is a vectorised <= 1-ulp powf, so rsx.ops.adj_build re-derives the
- *           n per-node factors with numpy for bit equality).
+ *   mode 1  SMORE (src/models/smore.py:176-207): float32 d^-1/2, inf -> 0, d_r*1*d_c.
+ * dinv_table (device, optional): [table_len] float64, the per-node factor of every
+ * degree 0 .. table_len-1 (mode 0: (deg + 1e-7)^-1/2; mode 1: the float32 value
+ * widened).  The caller computes it with the same host pow the reference uses
+ * (numpy's; np.power is not guaranteed to be correctly rounded, and neither is the
+ * device's pow), so every edge value equals the reference's bit for bit whatever the
+ * degree range (rsx.ops.adj_build builds it from a degree bound).  A node whose
+ * degree is >= table_len, or dinv_table NULL, falls back to the device's float64
+ * pow (correctly rounded to within an ulp: bit-equal on the graphs tested, not
+ * guaranteed).
  * rowptr [n+1]; col, val have capacity 2 n_edges (nnz = rowptr[n], twice the number
  * of distinct pairs).  Workspace rsx_adj_build_ws_bytes.
  *
@@ -709,8 +727,8 @@ int rsx_knn_graph(const float* feat, int64_t n, int32_t f, int32_t k, float* val
  */
 size_t rsx_adj_build_ws_bytes(int64_t n_edges, int64_t n_users, int64_t n_items);
 int rsx_adj_build(const int64_t* u, const int64_t* i, int64_t n_edges, int64_t n_users, int64_t n_items,
-                  int32_t mode, int64_t* rowptr, int32_t* col, float* val, void* ws, size_t ws_bytes,
-                  rsx_stream_t stream);
+                  int32_t mode, const double* dinv_table, int64_t table_len, int64_t* rowptr, int32_t* col,
+                  float* val, void* ws, size_t ws_bytes, rsx_stream_t stream);
 size_t rsx_edge_dropout_ws_bytes(int64_t n_edges, int64_t n_users, int64_t n_items);
 int rsx_edge_dropout_build(const int64_t* e_u, const int64_t* e_i, const uint8_t* keep, int64_t n_edges,
                            int64_t n_users, int64_t n_items, const int64_t* t_rowptr, const int32_t* t_col,

@@ -191,6 +191,10 @@ __global__ __launch_bounds__(kBprBlock) void bpr_bwd(BprArgs a, int n_part) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         if (a.loss_out) a.loss_out[0] = (float)loss;
         if (a.loss_acc) a.loss_acc[0] += loss;
+        if (a.halt && loss != loss && a.halt[0] == 0) {  // the first NaN batch: later Adam layers skip
+            a.halt[1] = a.tag;
+            a.halt[0] = 1;
+        }
     }
     const int li = threadIdx.x % G;
     const int64_t b = (int64_t)blockIdx.x * GPB + threadIdx.x / G;
@@ -403,7 +407,8 @@ size_t bpr_ws(int64_t batch) {
 
 int bpr_call(int32_t variant, const float* fin, const float* ego, int64_t n_users, int64_t n_items, int32_t d,
              const int64_t* trip, int64_t batch, float reg, float batch_cfg, float* g_fin, float* g_ego,
-             float* loss_out, double* loss_acc, void* ws, size_t ws_bytes, hipStream_t s, float g_div) {
+             float* loss_out, double* loss_acc, void* ws, size_t ws_bytes, hipStream_t s, float g_div,
+             int32_t* halt, int32_t tag) {
     if (!fin || !trip || !g_fin || batch <= 0 || !ws) return RSX_ERR_ARG;
     if (variant != RSX_BPR_SMORE && !ego) return RSX_ERR_ARG;
     if (variant < 0 || variant > 2) return RSX_ERR_ARG;
@@ -427,6 +432,8 @@ int bpr_call(int32_t variant, const float* fin, const float* ego, int64_t n_user
     a.coef = reinterpret_cast<float*>(w);
     size_t off = ((size_t)batch * sizeof(float) + 255) & ~(size_t)255;
     a.part = reinterpret_cast<double*>(w + off);
+    a.halt = halt;
+    a.tag = tag;
     return bpr_dispatch(a, d, s);
 }
 
@@ -477,7 +484,7 @@ int rsx_bpr(int32_t variant, const float* final_emb, const float* ego_emb, int64
             int32_t d, const int64_t* triplets, int64_t batch, float reg, float batch_cfg, float* g_final,
             float* g_ego, float* loss_out, double* loss_acc, void* ws, size_t ws_bytes, rsx_stream_t stream) {
     return rsx::bpr_call(variant, final_emb, ego_emb, n_users, n_items, d, triplets, batch, reg, batch_cfg,
-                         g_final, g_ego, loss_out, loss_acc, ws, ws_bytes, rsx::as_stream(stream), 1.f);
+                         g_final, g_ego, loss_out, loss_acc, ws, ws_bytes, rsx::as_stream(stream), 1.f, nullptr, 0);
 }
 
 }  // extern "C"

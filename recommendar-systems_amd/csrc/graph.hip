@@ -16,9 +16,9 @@
 //
 // Build: keys u<<32|i radix-sorted and de-duplicated (hipCUB), integer degrees by
 // atomics (exact in any order), rowptr by an exclusive scan; the user rows are the
-// unique keys in order; the item rows are the keys i<<32|u radix-sorted.  x^-1/2 is
-// evaluated with pow in float64 (the host's correctly rounded pow / powf; in f32 mode
-// the float64 result is rounded once to float32).
+// unique keys in order; the item rows are the keys i<<32|u radix-sorted.  x^-1/2 comes
+// from the caller's table of the host pow's values per degree (numpy's, as the
+// reference), with the device's float64 pow only beyond the table.
 #include <hipcub/hipcub.hpp>
 
 #include "rsx_common.hpp"
@@ -46,11 +46,16 @@ __global__ __launch_bounds__(256) void degrees(const uint64_t* uk, const int64_t
     atomicAdd(reinterpret_cast<unsigned long long*>(deg + nu + (k & 0xFFFFFFFFull)), 1ull);
 }
 
-// d^-1/2 per node: mode 0 float64 (deg + 1e-7), mode 1 float32 (inf -> 0), stored as double
-__global__ __launch_bounds__(256) void dinv_k(const int64_t* deg, int64_t n, int mode, double* dinv) {
+// d^-1/2 per node: mode 0 float64 (deg + 1e-7), mode 1 float32 (inf -> 0), stored as double;
+// from the caller's host-computed table where the degree is in it (bit-equal to the
+// reference's numpy pow by construction), else the device's float64 pow
+__global__ __launch_bounds__(256) void dinv_k(const int64_t* deg, int64_t n, int mode, const double* table,
+                                              int64_t table_len, double* dinv) {
     const int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (v >= n) return;
-    if (mode == 0) {
+    if (table && deg[v] < table_len) {
+        dinv[v] = table[deg[v]];
+    } else if (mode == 0) {
         dinv[v] = pow((double)deg[v] + 1e-7, -0.5);
     } else {
         const float x = (float)deg[v];
@@ -186,10 +191,10 @@ size_t rsx_adj_build_ws_bytes(int64_t n_edges, int64_t n_users, int64_t n_items)
 }
 
 int rsx_adj_build(const int64_t* u, const int64_t* i, int64_t n_edges, int64_t n_users, int64_t n_items,
-                  int32_t mode, int64_t* rowptr, int32_t* col, float* val, void* ws, size_t ws_bytes,
-                  rsx_stream_t stream) {
+                  int32_t mode, const double* dinv_table, int64_t table_len, int64_t* rowptr, int32_t* col,
+                  float* val, void* ws, size_t ws_bytes, rsx_stream_t stream) {
     if (n_edges < 0 || (n_edges > 0 && (!u || !i || !col || !val)) || n_users < 0 || n_items < 0 ||
-        (mode != 0 && mode != 1) || !rowptr)
+        (mode != 0 && mode != 1) || !rowptr || table_len < 0 || (table_len > 0 && !dinv_table))
         return RSX_ERR_ARG;
     if (n_users >= (int64_t(1) << 31) || n_items >= (int64_t(1) << 31) || 2 * n_edges >= (int64_t(1) << 31) ||
         n_edges >= INT32_MAX)
@@ -212,7 +217,8 @@ int rsx_adj_build(const int64_t* u, const int64_t* i, int64_t n_edges, int64_t n
     hipLaunchKernelGGL(gb::degrees, dim3(gb::blocks(E)), dim3(256), 0, s, w.k0, w.n_unique, E, n_users, w.deg);
     tb = w.temp_bytes;
     if (hipcub::DeviceScan::ExclusiveSum(w.temp, tb, w.deg, rowptr, (int)(n + 1), s) != hipSuccess) return last_rc();
-    hipLaunchKernelGGL(gb::dinv_k, dim3(gb::blocks(n)), dim3(256), 0, s, w.deg, n, mode, w.dinv);
+    hipLaunchKernelGGL(gb::dinv_k, dim3(gb::blocks(n)), dim3(256), 0, s, w.deg, n, mode,
+                       table_len > 0 ? dinv_table : nullptr, table_len, w.dinv);
     hipLaunchKernelGGL(gb::user_rows, dim3(gb::blocks(E)), dim3(256), 0, s, w.k0, w.n_unique, E, n_users, w.dinv,
                        mode, col, val, w.k2);
     tb = w.temp_bytes;

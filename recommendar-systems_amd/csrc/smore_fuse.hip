@@ -882,9 +882,11 @@ struct AdamList {
     float lr, beta1, beta2, eps, wd;
     float gscale;        // the gradient is g * gscale (f32 product, as torch's grad.mul_(s)); 1 = none
     const double* lr_dev;  // if non-NULL the learning rate is read here (graph replays across lr changes)
+    const int32_t* halt;   // if non-NULL and *halt != 0 (a NaN loss, rsx_nan_gate) nothing is updated
 };
 
 __global__ __launch_bounds__(256) void adam_multi(AdamList L) {
+    if (L.halt && *L.halt) return;
     int t = 0;
     while (t + 1 < L.count && (int64_t)blockIdx.x >= L.blk[t + 1]) ++t;
     rsx_adam cfg;
@@ -931,6 +933,19 @@ __global__ __launch_bounds__(256) void adam_multi(AdamList L) {
             m[i] = mm;
             v[i] = vv;
         }
+    }
+}
+
+// the batch loss's NaN check (reference src/common/trainer.py:192-203) on the device:
+// one lane counts the batch and, on the first NaN loss, records {1, its 1-based index}
+__global__ void nan_gate(const float* loss, int32_t* halt, int32_t* counter) {
+    if (threadIdx.x != 0) return;
+    const int32_t c = counter[0] + 1;
+    counter[0] = c;
+    const float x = loss[0];
+    if (x != x && halt[0] == 0) {
+        halt[1] = c;
+        halt[0] = 1;
     }
 }
 
@@ -1027,8 +1042,10 @@ __global__ __launch_bounds__(kMgFinal) void mg_alpha_final(const double* partial
 }
 
 // y += float(alpha * mult) * x
-__global__ __launch_bounds__(256) void axpy_multi(PairList L, const double* alpha, double mult, const double* lr_dev) {
+__global__ __launch_bounds__(256) void axpy_multi(PairList L, const double* alpha, double mult, const double* lr_dev,
+                                                   const int32_t* halt) {
 #pragma clang fp contract(off)  // two roundings, as torch's mul then add_ (device code contracts by default)
+    if (halt && *halt) return;
     const int t = list_slot(L);
     const float s = (float)(*alpha * (lr_dev ? mult * *lr_dev : mult));
     const int64_t base = ((int64_t)blockIdx.x - L.blk[t]) * kAdamPerBlock;
@@ -1369,13 +1386,19 @@ int rsx_adam_multi(int32_t count, float* const* p, const float* const* g, float*
                    const int64_t* const* step_dev, const int64_t* n, float lr, float beta1, float beta2, float eps,
                    float weight_decay, rsx_stream_t stream) {
     return rsx_adam_multi_scaled(count, p, g, m, v, step_dev, n, lr, beta1, beta2, eps, weight_decay, 1.f, nullptr,
-                                 stream);
+                                 nullptr, stream);
+}
+
+int rsx_nan_gate(const float* loss, int32_t* halt, int32_t* counter, rsx_stream_t stream) {
+    if (!loss || !halt || !counter) return RSX_ERR_ARG;
+    hipLaunchKernelGGL(sf::nan_gate, dim3(1), dim3(64), 0, as_stream(stream), loss, halt, counter);
+    return last_rc();
 }
 
 int rsx_adam_multi_scaled(int32_t count, float* const* p, const float* const* g, float* const* m, float* const* v,
                           const int64_t* const* step_dev, const int64_t* n, float lr, float beta1, float beta2,
                           float eps, float weight_decay, float grad_scale, const double* lr_dev,
-                          rsx_stream_t stream) {
+                          const int32_t* halt, rsx_stream_t stream) {
     if (count < 0 || (count > 0 && (!p || !g || !m || !v || !step_dev || !n))) return RSX_ERR_ARG;
     hipStream_t s = as_stream(stream);
     for (int32_t c0 = 0; c0 < count; c0 += sf::kAdamMax) {
@@ -1387,6 +1410,7 @@ int rsx_adam_multi_scaled(int32_t count, float* const* p, const float* const* g,
         L.wd = weight_decay;
         L.gscale = grad_scale;
         L.lr_dev = lr_dev;
+        L.halt = halt;
         int64_t blocks = 0;
         int k = 0;
         for (int32_t i = c0; i < count && k < sf::kAdamMax; ++i) {
@@ -1469,7 +1493,8 @@ int rsx_mg_alpha(int32_t count, const float* const* params, const float* const* 
 }
 
 int rsx_axpy_multi(int32_t count, float* const* y, const float* const* x, const int64_t* n,
-                   const double* alpha_dev, double mult, const double* lr_dev, rsx_stream_t stream) {
+                   const double* alpha_dev, double mult, const double* lr_dev, const int32_t* halt,
+                   rsx_stream_t stream) {
     if (count < 0 || count > 8 * sf::kAdamMax || !alpha_dev || (count > 0 && (!y || !x || !n))) return RSX_ERR_ARG;
     sf::PairList lists[8];
     int64_t blocks[8] = {0};
@@ -1477,7 +1502,8 @@ int rsx_axpy_multi(int32_t count, float* const* y, const float* const* x, const 
     if (rc) return rc;
     hipStream_t s = as_stream(stream);
     for (int li = 0; li * sf::kAdamMax < count; ++li)
-        if (blocks[li] > 0) hipLaunchKernelGGL(sf::axpy_multi, dim3((unsigned)blocks[li]), dim3(256), 0, s, lists[li], alpha_dev, mult, lr_dev);
+        if (blocks[li] > 0) hipLaunchKernelGGL(sf::axpy_multi, dim3((unsigned)blocks[li]), dim3(256), 0, s, lists[li], alpha_dev, mult, lr_dev,
+                               halt);
     return last_rc();
 }
 

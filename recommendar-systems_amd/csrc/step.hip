@@ -30,7 +30,8 @@ int spmm_dispatch_tagging(const rsx_csr& a, const float* x, int d, const rsx_epi
 int rowwise_dispatch(int64_t n, int d, const rsx_epilogue& e, hipStream_t s);
 int bpr_call(int32_t variant, const float* fin, const float* ego, int64_t n_users, int64_t n_items, int32_t d,
              const int64_t* trip, int64_t batch, float reg, float batch_cfg, float* g_fin, float* g_ego,
-             float* loss_out, double* loss_acc, void* ws, size_t ws_bytes, hipStream_t s, float g_div = 1.f);
+             float* loss_out, double* loss_acc, void* ws, size_t ws_bytes, hipStream_t s, float g_div = 1.f,
+             int32_t* halt = nullptr, int32_t tag = 0);
 
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     z += 0x9e3779b97f4a7c15ull;
@@ -233,7 +234,7 @@ static int lgcn_step_stored_layers(const rsx_lgcn_step& st, int64_t batch, int32
             return rc;
     } else if ((rc = bpr_call(RSX_BPR_LIGHTGCN, st.final_emb, st.p, st.n_users, st.n_items, d, st.triplets, batch,
                               st.reg, (float)batch, st.g, st.r, st.loss_out, st.loss_acc, st.ws, st.ws_bytes, s,
-                              (float)(K + 1)))) {
+                              (float)(K + 1), st.halt, tag))) {
         return rc;
     }
     // backward: H = G' + A H, H_0 = G'
@@ -266,7 +267,7 @@ static int lgcn_step_stored_layers(const rsx_lgcn_step& st, int64_t batch, int32
     e.row_tag = st.row_tag;
     e.tag = tag;
     e.tag_flags = RSX_TAG_SPARSE_S | RSX_TAG_SPARSE_R | RSX_TAG_ZERO;
-    e.halt = st.reg_cnt ? st.halt : nullptr;  // set by the one-launch BPR above
+    e.halt = st.halt;  // set by the BPR above on a NaN loss
     return spmm_dispatch(A, x, d, e, st.slab, s);
 }
 
@@ -417,7 +418,8 @@ int rsx_lightgcn_step(const rsx_lgcn_step* st, rsx_stream_t stream) {
         return rc;
     // BPR loss + gradients
     if ((rc = bpr_call(RSX_BPR_LIGHTGCN, st->final_emb, st->p, st->n_users, st->n_items, d, st->triplets, batch,
-                       st->reg, (float)batch, st->g, st->r, st->loss_out, st->loss_acc, st->ws, st->ws_bytes, s)))
+                       st->reg, (float)batch, st->g, st->r, st->loss_out, st->loss_acc, st->ws, st->ws_bytes, s, 1.f,
+                       st->halt, (int32_t)st->tag)))
         return rc;
     // backward (Horner) with Adam fused into the last layer
     const float beta = 1.f / (float)(K + 1);
@@ -429,6 +431,7 @@ int rsx_lightgcn_step(const rsx_lgcn_step* st, rsx_stream_t stream) {
         e.m = st->m;
         e.v = st->v;
         e.adam = st->adam;
+        e.halt = st->halt;
         return rowwise_dispatch(A.n_rows, d, e, s);
     }
     const float* x = st->g;
@@ -444,6 +447,7 @@ int rsx_lightgcn_step(const rsx_lgcn_step* st, rsx_stream_t stream) {
             e.m = st->m;
             e.v = st->v;
             e.adam = st->adam;
+            e.halt = st->halt;  // set by the BPR above on a NaN loss
             if (tags) {  // K >= 2: nothing reads G or R after this layer
                 e.row_tag = st->row_tag;
                 e.tag = tag;

@@ -155,15 +155,16 @@ def _declare(lib):
         "rsx_smore_infonce_bwd_scaled": (C.c_int, [P, P, P, P, I64, I64, I32, F32, P, I32, F32, P, P, P, C.c_size_t,
                                                    P]),
         "rsx_adam_multi": (C.c_int, [I32, P, P, P, P, P, P, F32, F32, F32, F32, F32, P]),
-        "rsx_adam_multi_scaled": (C.c_int, [I32, P, P, P, P, P, P, F32, F32, F32, F32, F32, F32, P, P]),
+        "rsx_adam_multi_scaled": (C.c_int, [I32, P, P, P, P, P, P, F32, F32, F32, F32, F32, F32, P, P, P]),
+        "rsx_nan_gate": (C.c_int, [P, P, P, P]),
         "rsx_smore_unit_weights": (C.c_int, [P, P, P, I32, I32, P, P]),
         "rsx_mg_alpha_ws_bytes": (C.c_size_t, [I32, P]),
         "rsx_mg_alpha": (C.c_int, [I32, P, P, P, C.c_double, C.c_double, C.c_double, C.c_double, P, P, C.c_size_t, P, P]),
-        "rsx_axpy_multi": (C.c_int, [I32, P, P, P, P, C.c_double, P, P]),
+        "rsx_axpy_multi": (C.c_int, [I32, P, P, P, P, C.c_double, P, P, P]),
         "rsx_knn_ws_bytes": (C.c_size_t, [I64, I32]),
         "rsx_knn_graph": (C.c_int, [P, I64, I32, I32, P, P, P, P, C.c_size_t, P]),
         "rsx_adj_build_ws_bytes": (C.c_size_t, [I64, I64, I64]),
-        "rsx_adj_build": (C.c_int, [P, P, I64, I64, I64, I32, P, P, P, P, C.c_size_t, P]),
+        "rsx_adj_build": (C.c_int, [P, P, I64, I64, I64, I32, P, I64, P, P, P, P, C.c_size_t, P]),
         "rsx_edge_dropout_ws_bytes": (C.c_size_t, [I64, I64, I64]),
         "rsx_edge_dropout_build": (C.c_int, [P, P, P, I64, I64, I64, P, P, P, P, P, P, P, C.c_size_t, P]),
         "rsx_smore_unit_weights_bwd": (C.c_int, [P, I64, P, P, P, I32, I32, P, P, P, P]),
@@ -188,7 +189,7 @@ EXPORTED = ["rsx_version", "rsx_csr_schedule_host", "rsx_csr_schedule_rebind", "
             "rsx_smore_infonce_ws_bytes", "rsx_smore_infonce_fwd", "rsx_smore_infonce_bwd", "rsx_smore_infonce_fwd_total", "rsx_smore_infonce_bwd_scaled", "rsx_adam_multi", "rsx_adam_multi_scaled",
             "rsx_smore_unit_weights", "rsx_smore_unit_weights_bwd", "rsx_mg_alpha_ws_bytes", "rsx_mg_alpha",
             "rsx_axpy_multi", "rsx_knn_ws_bytes", "rsx_knn_graph", "rsx_adj_build_ws_bytes", "rsx_adj_build",
-            "rsx_edge_dropout_ws_bytes", "rsx_edge_dropout_build"]
+            "rsx_edge_dropout_ws_bytes", "rsx_edge_dropout_build", "rsx_nan_gate"]
 
 
 def lib_path() -> str:

@@ -117,7 +117,7 @@ class ShardedLightGCNEngine:
     def __init__(self, train_u: np.ndarray, train_i: np.ndarray, n_users: int, n_items: int, dim: int,
                  n_layers: int, reg: float, lr: float, device, user_emb: np.ndarray, item_emb: np.ndarray,
                  seed: int = 0, batch: int = 2048, chunk: int = 32, weight_decay: float = 0.0, group=None,
-                 backend=None, native: bool | None = None, sparse: bool | None = None):
+                 backend=None, native: bool | None = None, sparse: bool | None = None, union_cap: int | None = None):
         if n_layers < 1:
             raise RuntimeError("sharded LightGCN needs n_layers >= 1")
         self.group = group
@@ -170,7 +170,9 @@ class ShardedLightGCNEngine:
         self.m, self.v, self.s, self.h0, self.h1 = z(), z(), z(), z(), z()
         self.final, self.g, self.r = z(), z(), z()
         self.t = z(self.n_items_pad)  # pad rows stay zero
-        self.union_cap = self.batch
+        # the union exchange's per-rank slice: equal on every rank (ranks may step with
+        # different batch sizes; the largest bounds the slice)
+        self.union_cap = int(union_cap or self.batch)
         if self.sparse:
             mk = (lambda a: self.be.tensor(a)) if not hasattr(self.be, "zeros") else \
                 (lambda a: a.to(self.be.device))  # noqa: E731

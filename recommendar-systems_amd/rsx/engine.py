@@ -73,7 +73,7 @@ class LightGCNEngine:
         # one-launch BPR with the regulariser gradient as per-row counts (tagged step only)
         self.reg_cnt = torch.zeros(3 * n + 4, dtype=torch.int32, device=dev)
         self.use_reg_cnt = os.environ.get("RSX_BPR_FUSED", "1") != "0"
-        # NaN halt flag of the tagged step with the one-launch BPR: {halted, tag of the NaN step}
+        # NaN halt flag of the step (every path: tagged, dense, K >= 4): {halted, tag of the NaN step}
         self.halt = torch.zeros(2, dtype=torch.int32, device=dev)
         self._st = L.LgcnStep()
         self._sa = L.SamplerArgs()
@@ -103,7 +103,7 @@ class LightGCNEngine:
         st.ws, st.ws_bytes = self.ws.data_ptr(), self.ws.numel()
         st.row_tag = self.row_tag.data_ptr() if self.use_tags else None
         st.reg_cnt = self.reg_cnt.data_ptr() if (self.use_tags and self.use_reg_cnt) else None
-        st.halt = self.halt.data_ptr() if (self.use_tags and self.use_reg_cnt) else None
+        st.halt = self.halt.data_ptr()
 
     def set_lr(self, lr: float):
         self.lr = float(lr)

@@ -23,9 +23,10 @@ rsx.dist.ShardedLightGCNEngine (items replicated).  The initial
 tables are the reference's (every rank draws the full xavier tables from the
 same seed and keeps its users), the parameters are the local user block and the
 item replica.  Training is data-parallel over the user shards: every rank samples
-its own users' interactions on the device (`fused_step_index`, the same number of
-batches per epoch on every rank: the largest shard's, smaller shards wrap
-around) and the step minimises the sum of the ranks' reference losses.
+its own users' interactions on the device (`fused_step_index`); every rank runs
+the same number of steps per epoch, ceil(E / (W B)), with a batch sized so that
+it visits each of its interactions exactly once (B_r = ceil(E_r / steps) ~ B), and
+the step minimises the sum of the ranks' reference losses.
 Evaluation ranks each rank's own evaluation users against all items
 (`full_sort_topk_local`); rsx.trainer all-gathers the metric sums.
 """
@@ -141,17 +142,29 @@ class LightGCN(GeneralRecommender):
         rows, cols = im.row.astype(np.int64), im.col.astype(np.int64)
         sel = (rows >= a) & (rows < b)
         B = int(config["train_batch_size"])
+        # every rank visits each of its interactions once per epoch in the same number of
+        # steps: steps = ceil(E / (W B)) over the global count E, and rank r's batch is
+        # B_r = ceil(E_r / steps) (~B; its last batch is the partial one).  Contiguous user
+        # ranges hold unequal interaction counts, so a fixed B per rank would make the small
+        # shards wrap around and re-train their batches within the epoch.
+        e_r = int(sel.sum())
+        if e_r == 0:
+            raise RuntimeError(f"rank {rank}: no training interactions in users [{a}, {b})")
+        cnt = torch.tensor([e_r], dtype=torch.int64)
+        if dist.get_backend() == "nccl":
+            cnt = cnt.to(self.device)
+        dist.all_reduce(cnt)
+        steps = -(-int(cnt.item()) // (world * B))
+        b_r = -(-e_r // steps)
+        cap = torch.tensor([b_r], dtype=torch.int64, device=cnt.device)
+        dist.all_reduce(cap, op=dist.ReduceOp.MAX)
         self.engine = ShardedLightGCNEngine(rows[sel] - a, cols[sel], b - a, self.n_items, self.latent_dim,
                                             self.n_layers, self.reg_weight, lr=config["learning_rate"] or 1e-3,
                                             device=self.device, user_emb=u0.numpy()[a:b], item_emb=i0.numpy(),
-                                            seed=int(config["seed"] or 0) + rank, batch=B,
-                                            chunk=int(config["rsx_chunk"] or 32), weight_decay=wd)
-        nb = torch.tensor([-(-self.engine.n_inter // B)], dtype=torch.int64)
-        if dist.get_backend() == "nccl":
-            nb = nb.to(self.device)
-        dist.all_reduce(nb, op=dist.ReduceOp.MAX)
-        self.steps_per_epoch = int(nb.item())
-        self._local_batches = max(1, -(-self.engine.n_inter // B))
+                                            seed=int(config["seed"] or 0) + rank, batch=b_r,
+                                            chunk=int(config["rsx_chunk"] or 32), weight_decay=wd,
+                                            union_cap=int(cap.item()))
+        self.steps_per_epoch = steps
         nl = b - a
         self.embedding_dict = nn.ParameterDict({
             "user_emb": nn.Parameter(self.engine.p[:nl]),
@@ -197,11 +210,10 @@ class LightGCN(GeneralRecommender):
         self.engine.step(triplets=interaction)
 
     def fused_step_index(self, epoch: int, i: int, lr: float):
-        """Sharded training: this rank's batch i of `epoch` from its device sampler
-        (i modulo its own batch count: every rank runs steps_per_epoch batches)."""
+        """Sharded training: this rank's batch i (of steps_per_epoch, the same count on every
+        rank) of `epoch` from its device sampler."""
         self.engine.lr = float(lr)
-        B = self.engine.batch
-        self.engine.step(epoch=epoch, start=(i % self._local_batches) * B)
+        self.engine.step(epoch=epoch, start=i * self.engine.batch)
 
     def full_sort_topk_local(self, eval_users: torch.Tensor, k: int, eval_data):
         """(row positions in eval_users, top-k item ids) for this rank's evaluation users
@@ -226,9 +238,9 @@ class LightGCN(GeneralRecommender):
     @property
     def device_halt(self):
         """(halt flag [2] int32 on the device, engine step count) of the single engine's
-        tagged step: {1, tag of the step} once a batch loss was NaN (the parameters stay
-        those of the last finite step), or None where the step has no flag."""
+        step: {1, tag of the step} once a batch loss was NaN (the parameters stay those of
+        the last finite step), or None where the step has no flag (sharded engine)."""
         e = self.engine
-        if self.sharded or not getattr(e, "use_tags", False) or not getattr(e, "use_reg_cnt", False):
+        if self.sharded:
             return None
         return e.halt, e.step_count

@@ -455,37 +455,45 @@ class DeviceSampler:
 ADJ_LIGHTGCN, ADJ_SMORE = 0, 1
 
 
+def dinv_table(max_deg: int, mode: int) -> np.ndarray:
+    """The per-node factor of every degree 0..max_deg with the reference's own host
+    arithmetic: mode ADJ_LIGHTGCN (deg + 1e-7)^-1/2 in float64 numpy
+    (lightgcn.py:93-96), ADJ_SMORE numpy's float32 power with inf -> 0
+    (smore.py:194-198), widened to float64 for the kernel."""
+    deg = np.arange(max_deg + 1)
+    if mode == ADJ_LIGHTGCN:
+        return np.power(deg.astype(np.float64) + 1e-7, -0.5)
+    with np.errstate(divide="ignore"):
+        d = np.power(deg.astype(np.float32), np.float32(-0.5)).astype(np.float32)
+    d[np.isinf(d)] = 0.0
+    return d.astype(np.float64)
+
+
 def adj_build(u, i, n_users: int, n_items: int, mode: int, device):
     """(rowptr int64 [n+1], col int32 [nnz], val f32 [nnz]) device tensors of the
     normalised symmetric adjacency (rsx_adj_build): mode ADJ_LIGHTGCN = reference
     lightgcn.py:65-103, ADJ_SMORE = smore.py:176-207; equal to rsx.graph's host
-    builders bit for bit.  u, i: host arrays or device int64 tensors."""
+    builders bit for bit (the per-degree factors are the host pow's, a table up to a
+    degree bound: the largest raw interaction count of any user or item).  u, i: host
+    arrays or device int64 tensors."""
     dev = torch.device(device)
     u = torch.as_tensor(u, dtype=torch.int64).to(dev).contiguous()
     i = torch.as_tensor(i, dtype=torch.int64).to(dev).contiguous()
     E = u.numel()
     n = n_users + n_items
     lib = L.lib()
+    bound = 0
+    if E:
+        bound = int(torch.stack([torch.bincount(u).max(), torch.bincount(i).max()]).max().item())
+    table = torch.from_numpy(dinv_table(bound, mode)).to(dev)
     rowptr = torch.empty(n + 1, dtype=torch.int64, device=dev)
     col = torch.empty(max(2 * E, 1), dtype=torch.int32, device=dev)
     val = torch.empty(max(2 * E, 1), dtype=torch.float32, device=dev)
     ws = torch.empty(int(lib.rsx_adj_build_ws_bytes(E, n_users, n_items)), dtype=torch.uint8, device=dev)
-    L.check(lib.rsx_adj_build(_p(u), _p(i), E, n_users, n_items, mode, _p(rowptr), _p(col), _p(val), _p(ws),
-                              ws.numel(), _stream()), "rsx_adj_build")
+    L.check(lib.rsx_adj_build(_p(u), _p(i), E, n_users, n_items, mode, _p(table), table.numel(), _p(rowptr),
+                              _p(col), _p(val), _p(ws), ws.numel(), _stream()), "rsx_adj_build")
     nnz = int(rowptr[-1].item())
-    col, val = col[:nnz], val[:nnz]
-    if mode == ADJ_SMORE:
-        # the reference's d^-1/2 is numpy's float32 power (smore.py:194-198), a vectorised
-        # <= 1-ulp powf, not the correctly rounded value the kernel's f64 pow gives: the n
-        # per-node factors come from numpy itself, the per-edge products stay on the device
-        deg = np.diff(rowptr.cpu().numpy()).astype(np.float32)
-        with np.errstate(divide="ignore"):
-            dinv = np.power(deg, np.float32(-0.5)).astype(np.float32)
-        dinv[np.isinf(dinv)] = 0.0
-        d = torch.from_numpy(dinv).to(dev)
-        rows = torch.repeat_interleave(torch.arange(n, device=dev), rowptr[1:] - rowptr[:-1])
-        val = (d[rows] * 1.0) * d[col.long()]
-    return rowptr, col, val
+    return rowptr, col[:nnz], val[:nnz]
 
 
 def edge_dropout_build(e_u, e_i, keep, n_users: int, n_items: int, t_rowptr, t_col, t_eid):

@@ -17,7 +17,6 @@ from __future__ import annotations
 
 import torch
 
-from . import ops
 from .smore_fuse import adam_multi
 
 
@@ -30,6 +29,16 @@ class RsxAdam(torch.optim.Optimizer):
         # optional 1-element f64 device tensor holding the learning rate (set by
         # rsx.trainer for graph-captured steps: a new lr then needs no new capture)
         self.lr_dev = None
+        # optional int32 [2] device flag of rsx.smore_fuse.nan_gate (set by rsx.trainer):
+        # once a batch loss was NaN no update changes any parameter or moment
+        self.halt = None
+
+    def lr_on_device(self) -> bool:
+        """Whether every update reads the learning rate from `lr_dev` (one group of
+        contiguous parameters: the rsx_adam_multi path); otherwise a captured step has
+        the host lr baked into its launches."""
+        return (self.lr_dev is not None and len(self.param_groups) == 1
+                and all(p.is_contiguous() for p in self.param_groups[0]["params"]))
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -56,19 +65,22 @@ class RsxAdam(torch.optim.Optimizer):
                 continue
             steps = [self.state[p]["step"] for p in live]
             torch._foreach_add_(steps, 1)
+            grads = [p.grad if p.grad.is_contiguous() else p.grad.contiguous() for p in live]
             if all(p.is_contiguous() for p in live):
-                adam_multi([p.data for p in live], [p.grad if p.grad.is_contiguous() else p.grad.contiguous()
-                                                    for p in live],
+                adam_multi([p.data for p in live], grads,
                            [self.state[p]["exp_avg"] for p in live], [self.state[p]["exp_avg_sq"] for p in live],
                            steps, group["lr"], betas=group["betas"], eps=group["eps"],
                            weight_decay=group["weight_decay"], grad_scale=gs,
-                           lr_dev=self.lr_dev if len(self.param_groups) == 1 else None)
+                           lr_dev=self.lr_dev if len(self.param_groups) == 1 else None, halt=self.halt)
                 continue
-            for p in live:
-                st = self.state[p]
-                g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
-                if gs != 1.0:
-                    g = g * gs
-                ops.adam_(p.data, g, st["exp_avg"], st["exp_avg_sq"], 0, group["lr"], betas=group["betas"],
-                          eps=group["eps"], weight_decay=group["weight_decay"], step_dev=st["step"])
+            # a non-contiguous parameter: the same launch on contiguous copies, copied back
+            ts = [[t.contiguous() for t in (p.data, self.state[p]["exp_avg"], self.state[p]["exp_avg_sq"])]
+                  for p in live]
+            adam_multi([t[0] for t in ts], grads, [t[1] for t in ts], [t[2] for t in ts], steps, group["lr"],
+                       betas=group["betas"], eps=group["eps"], weight_decay=group["weight_decay"], grad_scale=gs,
+                       halt=self.halt)
+            for p, (pc, mc, vc) in zip(live, ts):
+                for dst, src in ((p.data, pc), (self.state[p]["exp_avg"], mc), (self.state[p]["exp_avg_sq"], vc)):
+                    if dst.data_ptr() != src.data_ptr():
+                        dst.copy_(src)
         return loss

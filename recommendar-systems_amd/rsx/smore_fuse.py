@@ -388,10 +388,11 @@ def smore_loss_rows(all_c, side_c, content_c, trip, ar, B, reg, batch_cfg, cl, t
 # multi-tensor Adam
 # ---------------------------------------------------------------------------
 def adam_multi(params, grads, exp_avgs, exp_avg_sqs, steps, lr, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0,
-               grad_scale=1.0, lr_dev=None):
+               grad_scale=1.0, lr_dev=None, halt=None):
     """torch.optim.Adam's update over many tensors in one launch (per 32 tensors); the
     gradients are taken as g * grad_scale (f32 product) when grad_scale != 1; with
-    lr_dev (a 1-element f64 device tensor) the learning rate is read from it."""
+    lr_dev (a 1-element f64 device tensor) the learning rate is read from it; with
+    halt (nan_gate's int32 flag) nothing is updated once it is set."""
     n = len(params)
     if n == 0:
         return
@@ -401,7 +402,8 @@ def adam_multi(params, grads, exp_avgs, exp_avg_sqs, steps, lr, betas=(0.9, 0.99
     sizes = (C.c_int64 * n)(*[p.numel() for p in params])
     L.check(L.lib().rsx_adam_multi_scaled(n, _arr(params), _arr(grads), _arr(exp_avgs), _arr(exp_avg_sqs),
                                           _arr(steps), sizes, float(lr), float(betas[0]), float(betas[1]), float(eps),
-                                          float(weight_decay), float(grad_scale), _p(lr_dev), ops._stream()),
+                                          float(weight_decay), float(grad_scale), _p(lr_dev), _p(halt),
+                                          ops._stream()),
             "rsx_adam_multi_scaled")
 
 
@@ -424,12 +426,23 @@ def mg_alpha(params, grads, base, lr, rel_step, max_scale, lr_dev=None):
     return alpha
 
 
-def axpy_multi(ys, xs, alpha, mult, lr_dev=None):
+def nan_gate(loss, halt, counter):
+    """The batch loss's NaN check on the device (rsx_nan_gate; reference
+    src/common/trainer.py:192-203): counter += 1, and on the first NaN loss
+    halt = {1, counter}; the optimizer launches given `halt` then update nothing."""
+    loss = loss.detach().reshape(1)
+    if loss.dtype != torch.float32 or not loss.is_cuda:
+        raise RuntimeError("nan_gate: a float32 GPU loss")
+    L.check(L.lib().rsx_nan_gate(_p(loss), _p(halt), _p(counter), ops._stream()), "rsx_nan_gate")
+
+
+def axpy_multi(ys, xs, alpha, mult, lr_dev=None, halt=None):
     """y += float(alpha * mult) * x for every pair (alpha: 0-d f64 device tensor; with
-    lr_dev, a 1-element f64 device tensor, the scale is float(alpha * (mult * lr)))."""
+    lr_dev, a 1-element f64 device tensor, the scale is float(alpha * (mult * lr)));
+    with halt (nan_gate's flag) nothing is updated once it is set."""
     n = len(ys)
     if n == 0:
         return
     sizes = (C.c_int64 * n)(*[y.numel() for y in ys])
     L.check(L.lib().rsx_axpy_multi(n, _arr([y.detach() for y in ys]), _arr(xs), sizes, _p(alpha), float(mult),
-                                   _p(lr_dev), ops._stream()), "rsx_axpy_multi")
+                                   _p(lr_dev), _p(halt), ops._stream()), "rsx_axpy_multi")

@@ -33,19 +33,46 @@ from torch import Tensor
 from . import _lib as L
 from . import graph, ops
 
-_CACHE: dict = {}
+import os
+from collections import OrderedDict
+
+# graph cache, least recently used first.  Bounded two ways, because a caller such as
+# the reference's LayerGCN builds a fresh masked_adj every epoch (src/models/layergcn.py:
+# 51-70) and would otherwise pin one graph per epoch: at most _PER_SHAPE graphs of one
+# (n_rows, n_cols, transpose) shape (a model's train and eval graph), and at most
+# _CACHE_BYTES of graph memory (held tensors + work schedule + transposed copies) in all.
+_CACHE: "OrderedDict" = OrderedDict()
 _CACHE_MAX = 32
+_PER_SHAPE = 2
+_CACHE_BYTES = int(os.environ.get("RSX_TORCH_OPS_CACHE_BYTES", 4 << 30))
 
 
 def _key(*ts):
     return tuple((t.data_ptr(), t.numel(), t._version) for t in ts)
 
 
+def _graph_bytes(A, transpose):
+    """Device bytes a cache entry keeps alive: the CSR arrays (held, or transposed
+    copies) and the work schedule (16 B per work item, 16 B per split row)."""
+    b = 8 * (A.n_rows + 1) + 8 * A.nnz + 16 * (A.n_work + A.n_long)
+    return b * (2 if transpose else 1)
+
+
+def _evict(shape):
+    same = [k for k in _CACHE if k[1:] == shape]
+    while len(same) >= _PER_SHAPE:
+        _CACHE.pop(same.pop(0))
+    while _CACHE and (len(_CACHE) >= _CACHE_MAX or sum(v[4] for v in _CACHE.values()) > _CACHE_BYTES):
+        _CACHE.popitem(last=False)
+
+
 def _csr(rowptr: Tensor, col: Tensor, val: Tensor, n_cols: int, transpose: bool = False):
     """The cached DeviceCSR of (rowptr, col, val) (or of its transpose)."""
-    key = (_key(rowptr, col, val), int(n_cols), bool(transpose))
+    shape = (_n_rows(rowptr), int(n_cols), bool(transpose))
+    key = (_key(rowptr, col, val),) + shape
     hit = _CACHE.get(key)
     if hit is not None:
+        _CACHE.move_to_end(key)
         return hit[0]
     if col.dtype != torch.int32 or val.dtype != torch.float32 or rowptr.dtype != torch.int64:
         raise RuntimeError("rsx CSR: rowptr int64, col int32, val float32")
@@ -57,9 +84,9 @@ def _csr(rowptr: Tensor, col: Tensor, val: Tensor, n_cols: int, transpose: bool 
         A = ops.DeviceCSR(trp, tcol, tval, rp.size - 1, val.device)
     else:
         A = ops.DeviceCSR.from_device(rowptr, col.contiguous(), val.contiguous(), int(n_cols))
-    if len(_CACHE) >= _CACHE_MAX:
-        _CACHE.pop(next(iter(_CACHE)))
-    _CACHE[key] = (A, rowptr, col, val)  # the tensors are held: their storage cannot be reused
+    _evict(shape)
+    # the tensors are held: their storage cannot be reused while the entry lives
+    _CACHE[key] = (A, rowptr, col, val, _graph_bytes(A, transpose))
     return A
 
 

@@ -123,9 +123,10 @@ class _GraphStep:
         kind = self._kind()
         if kind is None:
             return None
-        lr = self.t.optimizer.param_groups[0]["lr"]
-        if lr != self.lr and getattr(self.t, "_lr_dev", None) is None:  # lr baked into the captured launches
-            self.graphs.clear()
+        opt = self.t.optimizer
+        lr = tuple(g["lr"] for g in opt.param_groups)
+        if lr != self.lr and not getattr(opt, "lr_on_device", lambda: False)():
+            self.graphs.clear()  # the lr is baked into the captured launches
         self.lr = lr
         if kind not in self.seen:
             self.seen.add(kind)
@@ -269,6 +270,8 @@ class Trainer:
             total = float(tot.item())
         else:
             halt = getattr(self.model, "device_halt", None)
+            if halt is not None:
+                halt[0].zero_()  # a halt of an earlier fit() does not carry into this epoch
             for batch in train_data:
                 self.model.fused_step(batch, lr)
                 n += 1
@@ -288,23 +291,52 @@ class Trainer:
     def _check_nan(self, loss):
         return bool(torch.isnan(loss))
 
+    def _nan_gate_on(self) -> bool:
+        """The device NaN gate (rsx_nan_gate + the halt flag of RsxAdam / axpy_multi)
+        replaces the reference's per-batch host check when every update goes through
+        the rsx optimizer kernels."""
+        from .optim import RsxAdam
+
+        return isinstance(self.optimizer, RsxAdam) and torch.cuda.is_available() and \
+            bool(self.config.get("rsx_nan_gate", True))
+
+    def _arm_nan_gate(self):
+        if getattr(self, "_halt", None) is None:
+            dev = next(iter(self.model.parameters())).device
+            self._halt = torch.zeros(2, dtype=torch.int32, device=dev)
+            self._nan_ctr = torch.zeros(1, dtype=torch.int32, device=dev)
+        self._halt.zero_()
+        self._nan_ctr.zero_()
+        self.optimizer.halt = self._halt
+
     def _train_epoch_autograd(self, train_data, epoch_idx, loss_func=None):
         """Reference _train_epoch (trainer.py:170-260).  Per-batch losses stay on the
         device and are summed once at the end of the epoch (the reference calls
-        .item() per batch, a host sync each); a NaN batch loss ends the epoch at the
-        next check, every `rsx_nan_check_every` batches (reference: every batch)."""
+        .item() per batch, a host sync each).  A NaN batch loss (reference :192-203:
+        checked before backward, training stops) is caught on the device by the NaN
+        gate: from that batch on no optimizer or mirror-gradient launch changes a
+        parameter, and the epoch-end read reports the batch index.  Without the rsx
+        optimizer the loss is checked on the host after every batch, as the reference."""
         loss_func = loss_func or self.model.calculate_loss
         parts = []
         loss_batches = []
-        every = max(int(self.config.get("rsx_nan_check_every", 64) or 64), 1)
+        gate = self._gate = self._nan_gate_on()
+        if gate:
+            self._arm_nan_gate()
         self.reset_graph_step()
         for batch_idx, interaction in enumerate(train_data):
             losses, loss = self.train_step(interaction, batch_idx, loss_func)
             parts.append(torch.stack(list(losses)) if isinstance(losses, tuple) else loss)
             loss_batches.append(loss)
-            if (batch_idx + 1) % every == 0 and self._check_nan(loss_batches[-1]):
+            if not gate and self._check_nan(loss_batches[-1]):
                 self.logger.info(f"Loss is nan at epoch: {epoch_idx}, batch index: {batch_idx}. Exiting.")
                 return loss_batches[-1], torch.tensor(0.0)
+        if gate:
+            h = self._halt.cpu().tolist()  # one read per epoch
+            if h[0]:
+                b = h[1] - 1
+                self.logger.info(f"Loss is nan at epoch: {epoch_idx}, batch index: {b}. Exiting.")
+                return loss_batches[b], torch.tensor(0.0)
         if not parts:
             return 0.0, loss_batches
         host = torch.stack(parts).double().cpu().numpy()  # one sync per epoch
@@ -327,7 +359,8 @@ class Trainer:
         rebuilt buffers the graphs point at), unless the model declares its buffers
         stable across epochs (`graph_step_persistent`); the learning rate lives on the
         device (_sync_lr), so the LambdaLR schedule needs no new capture."""
-        if getattr(self.model, "graph_step_persistent", False) and getattr(self, "_lr_dev", None) is not None:
+        if getattr(self.model, "graph_step_persistent", False) and getattr(self, "_lr_dev", None) is not None \
+                and getattr(self.optimizer, "lr_on_device", lambda: False)():
             return
         self._graph = None
 
@@ -371,6 +404,10 @@ class Trainer:
         second = interaction.clone() if hasattr(interaction, "clone") else interaction
         losses = loss_func(interaction)
         loss = sum(losses) if isinstance(losses, tuple) else losses
+        if getattr(self, "_gate", False):
+            from .smore_fuse import nan_gate
+
+            nan_gate(loss, self._halt, self._nan_ctr)
         if not getattr(self.model, "mg_enable", False):
             if self.mg and batch_idx % self.beta == 0:
                 (self.alpha1 * loss).backward()
@@ -443,7 +480,8 @@ class Trainer:
                 lr_dev = getattr(self, "_lr_dev", None)  # graph-step runs: lr read on the device
                 alpha = mg_alpha(params, grads, base, lr, self.mg_target_rel_step, self.mg_alpha_max_scale, lr_dev)
                 m._alpha_eff = alpha
-                axpy_multi(params, grads, alpha, -1.0 if lr_dev is not None else -lr, lr_dev)  # theta - alpha lr g
+                halt = self._halt if getattr(self, "_gate", False) else None
+                axpy_multi(params, grads, alpha, -1.0 if lr_dev is not None else -lr, lr_dev, halt)  # theta - alpha lr g
             else:
                 alpha = _mg_alpha(params, grads, base, lr, self.mg_target_rel_step, self.mg_alpha_max_scale)
                 m._alpha_eff = alpha
@@ -463,7 +501,7 @@ class Trainer:
                 torch._foreach_mul_(live, -beta)
             if params:
                 if fused:
-                    axpy_multi(params, grads, alpha, 1.0 if lr_dev is not None else lr, lr_dev)  # restore theta
+                    axpy_multi(params, grads, alpha, 1.0 if lr_dev is not None else lr, lr_dev, halt)  # restore theta
                 else:
                     torch._foreach_add_(params, torch._foreach_mul(grads, (alpha * lr).float()))
         self.optimizer.step()

@@ -129,7 +129,7 @@ def _local_graph(rank):
     return tu, ti, trip
 
 
-def _worker(rank, world, port, out_dir, sparse=False):
+def _worker(rank, world, port, out_dir, sparse=False, k=K):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     torch.set_num_threads(1)
@@ -140,7 +140,7 @@ def _worker(rank, world, port, out_dir, sparse=False):
     I0 = torch.nn.init.xavier_uniform_(torch.empty(NI, D)).numpy() if rank == 0 else np.zeros((NI, D), np.float32)
     U0 = torch.nn.init.xavier_uniform_(torch.empty(NU, D), generator=torch.Generator().manual_seed(rank)).numpy()
     tu, ti, trip = _local_graph(rank)
-    eng = ShardedLightGCNEngine(tu, ti, NU, NI, D, K, REG, LR, "cpu", U0, I0, backend=CpuBackend(), batch=32,
+    eng = ShardedLightGCNEngine(tu, ti, NU, NI, D, k, REG, LR, "cpu", U0, I0, backend=CpuBackend(), batch=32,
                                 sparse=sparse)
     assert eng.sparse == sparse
     f0 = eng.forward().clone()
@@ -158,12 +158,15 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world,sparse", [(2, False), (2, True), (4, True), (8, True), (8, False)])
-def test_sharded_step_matches_global_objective(world, sparse):
+@pytest.mark.parametrize("world,sparse,k", [(2, False, 3), (2, True, 3), (4, True, 3), (8, True, 3), (8, False, 3),
+                                            (2, False, 4), (4, False, 4), (2, True, 2), (2, False, 1)])
+def test_sharded_step_matches_global_objective(world, sparse, k):
     """sparse: the union-row exchange of the last layer / G's item rows and the
-    reduce-scatter + owner Adam + all-gather of the item gradient (rsx/dist.py)."""
+    reduce-scatter + owner Adam + all-gather of the item gradient (rsx/dist.py).
+    k = 4: the reference's default depth (src/configs/model/LightGCN.yaml:3)."""
+    K = k
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(world, _free_port(), d, sparse), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, _free_port(), d, sparse, k), nprocs=world, join=True)
         res = [dict(np.load(os.path.join(d, f"r{r}.npz"))) for r in range(world)]
     # global graph: users of rank g offset by g*NU
     gu, gi, trips = [], [], []

@@ -17,7 +17,7 @@ from test_dist_gloo import D, K, LR, NI, NU, REG, _local_graph
 pytestmark = pytest.mark.gpu
 
 
-def _worker(rank, world, port, out_dir, native, sparse):
+def _worker(rank, world, port, out_dir, native, sparse, k=K):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -28,7 +28,7 @@ def _worker(rank, world, port, out_dir, native, sparse):
     U0 = torch.nn.init.xavier_uniform_(torch.empty(NU, D), generator=torch.Generator().manual_seed(rank)).numpy()
     tu, ti, trip = _local_graph(rank)
     # native: csrc/dist.hip's one-call step, its exchanges through the host hook (gloo)
-    eng = ShardedLightGCNEngine(tu, ti, NU, NI, D, K, REG, LR, "cuda:0", U0, I0, batch=16, native=native,
+    eng = ShardedLightGCNEngine(tu, ti, NU, NI, D, k, REG, LR, "cuda:0", U0, I0, batch=16, native=native,
                                 sparse=sparse)
     assert eng.native == native and eng.sparse == sparse
     f0 = eng.forward().cpu().clone()
@@ -51,13 +51,16 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("native,sparse", [(False, False), (True, False), (False, True), (True, True)])
-def test_sharded_hip_step_matches_global_objective(native, sparse):
+@pytest.mark.parametrize("native,sparse,k", [(False, False, 3), (True, False, 3), (False, True, 3), (True, True, 3),
+                                             (True, False, 4), (False, False, 4)])
+def test_sharded_hip_step_matches_global_objective(native, sparse, k):
     """sparse: the union-row exchange + reduce-scatter / owner Adam / all-gather schedule
-    (csrc/dist.hip with the host hook's collectives when native)."""
+    (csrc/dist.hip with the host hook's collectives when native).  k = 4: the
+    reference's default depth, the native step's dense (untagged) form."""
     world = 2
+    K = k
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(world, _free_port(), d, native, sparse), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, _free_port(), d, native, sparse, k), nprocs=world, join=True)
         res = [dict(np.load(os.path.join(d, f"r{r}.npz"))) for r in range(world)]
     gu, gi, trips = [], [], []
     for r in range(world):

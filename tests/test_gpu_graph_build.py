@@ -24,6 +24,24 @@ def _graphs(golden):
     i = rng.integers(0, 300, 6000)
     u[:100], i[:100] = u[100:200], i[100:200]  # duplicate pairs
     yield "dups_isolated", u, i, 520, 330  # users 500..519 and items 300..329 have no edges
+    # every degree 1..4000 on the user side (user k has k items) and item degrees up to
+    # 4000: the per-degree factors across the whole range a C4-like hub graph reaches
+    nu, ni = 4000, 4000
+    u = np.repeat(np.arange(nu), np.arange(1, nu + 1))
+    i = np.concatenate([np.arange(k) for k in range(1, nu + 1)])
+    yield "all_degrees", u, i, nu, ni
+
+
+def test_dinv_table_is_the_host_pow():
+    """The per-degree factor table equals the host builders' own expressions elementwise."""
+    deg = np.arange(100001)
+    t0 = ops.dinv_table(100000, ops.ADJ_LIGHTGCN)
+    assert np.array_equal(t0.view(np.uint64), np.power(deg.astype(np.float64) + 1e-7, -0.5).view(np.uint64))
+    t1 = ops.dinv_table(100000, ops.ADJ_SMORE)
+    with np.errstate(divide="ignore"):
+        want = np.power(deg.astype(np.float32), np.float32(-0.5)).astype(np.float32)
+    want[np.isinf(want)] = 0
+    assert np.array_equal(t1.astype(np.float32).view(np.uint32), want.view(np.uint32)) and t1[0] == 0
 
 
 @pytest.mark.parametrize("mode", [ops.ADJ_LIGHTGCN, ops.ADJ_SMORE])

@@ -526,10 +526,15 @@ def test_layergcn_c_step_equals_python_sequence(cuda, K, monkeypatch):
                                    atol=1e-6, err_msg=name)
 
 
-def test_nan_loss_halts_the_fused_step(cuda):
-    """A batch whose loss is NaN sets the tagged step's halt flag to {1, its tag}; that
-    step's Adam update and every later one are skipped, so p / m / v stay bit for bit
-    those after the last finite batch (the reference stops before backward)."""
+@pytest.mark.parametrize("K,tags,fused_bpr", [(3, True, True), (3, True, False), (3, False, False),
+                                               (4, True, True), (4, False, False), (5, True, False)])
+def test_nan_loss_halts_the_fused_step(cuda, K, tags, fused_bpr):
+    """A batch whose loss is NaN sets the step's halt flag to {1, its tag}; that step's
+    Adam update and every later one are skipped, so p / m / v stay bit for bit those
+    after the last finite batch (the reference stops before backward,
+    src/common/trainer.py:192-203).  Every step path: the stored-layer step (K = 2, 3),
+    the tag_rows + dense path (K >= 4, the reference's default depth), the untagged
+    dense path, with the one-launch or the two-launch BPR."""
     from rsx import synth
     from rsx.engine import LightGCNEngine
 
@@ -540,8 +545,9 @@ def test_nan_loss_halts_the_fused_step(cuda):
     torch.manual_seed(9)
     U0 = torch.nn.init.xavier_uniform_(torch.empty(nu, 64)).numpy()
     I0 = torch.nn.init.xavier_uniform_(torch.empty(ni, 64)).numpy()
-    eng = LightGCNEngine(tu, ti, nu, ni, 64, 3, 1e-2, 1e-3, cuda, U0, I0, seed=0, batch=512)
-    assert eng.use_tags and eng.use_reg_cnt
+    eng = LightGCNEngine(tu, ti, nu, ni, 64, K, 1e-2, 1e-3, cuda, U0, I0, seed=0, batch=512)
+    eng.use_tags, eng.use_reg_cnt = tags, fused_bpr
+    eng._fill_static()
     g = torch.Generator().manual_seed(3)
     trip = lambda: torch.stack([torch.randint(0, nu, (512,), generator=g), torch.randint(0, ni, (512,), generator=g),  # noqa: E731
                                 torch.randint(0, ni, (512,), generator=g)]).to(cuda)

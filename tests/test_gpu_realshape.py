@@ -172,20 +172,31 @@ def test_spmm_out_of_launch_fixups_vs_torch(cuda, d):
     assert torch.equal(y, A.spmm(x.to(cuda)).cpu())  # deterministic
 
 
-@pytest.mark.parametrize("tags", [True, False])
-def test_lightgcn_d256_k3_hub_graph_vs_oracle(cuda, tags):
-    """Three B=2048 LightGCN steps at d=256, K=3 on a power-law graph with > 1,024 hub
-    rows against the oracle's CPU training step, same triplets: every loss within rtol
-    1e-5; after the first step every parameter within Adam's rounding bound (the first
-    update is -lr g/(|g|+eps), so a gradient rounding difference delta moves it by at
-    most lr |s(g+delta) - s(g)|, s(x) = x/(|x|+eps); delta = 2e-5 of the row's largest
-    gradient: f32 sums in another order)."""
+def _adam_first_step_bound(g, lr):
+    """|p_gpu - p_cpu| bound after one Adam step: the first update is -lr g/(|g|+eps), so a
+    gradient rounding difference delta moves it by at most lr |s(g+delta) - s(g)|,
+    s(x) = x/(|x|+eps); delta = 2e-5 of the row's largest gradient (f32 sums in another
+    order)."""
+    delta = 2e-5 * np.abs(g).max(axis=1, keepdims=True) + 1e-30
+    s = lambda x: x / (np.abs(x) + 1e-8)  # noqa: E731
+    return lr * np.maximum(np.abs(s(g + delta) - s(g)), np.abs(s(g - delta) - s(g))) + 2e-7
+
+
+@pytest.mark.parametrize("d,K,tags", [(256, 3, True), (256, 3, False), (64, 4, True), (64, 4, False),
+                                      (256, 4, True), (64, 5, True)])
+def test_lightgcn_hub_graph_vs_oracle(cuda, d, K, tags):
+    """Three B=2048 LightGCN steps on a power-law graph with > 1,024 hub rows against
+    the oracle's CPU training step, same triplets: every loss within rtol 1e-5; after
+    the first step every parameter within Adam's rounding bound.  K = 4 is the
+    reference's own default depth (src/configs/model/LightGCN.yaml:3, n_layers [4]):
+    the step then takes the tag_rows + dense-forward + Horner path
+    (csrc/step.hip rsx_lightgcn_step, K >= 4) instead of the stored-layer step."""
     from rsx.engine import LightGCNEngine
 
     df = synth.amazon_like(20000, 4000, 300000, seed=1)
     tr = df[df.x_label == 0]
     tu, ti = tr.userID.values.astype(np.int64), tr.itemID.values.astype(np.int64)
-    nu, ni, d, K, lr, reg = int(df.userID.max()) + 1, 4000, 256, 3, 1e-3, 1e-2
+    nu, ni, lr, reg = int(df.userID.max()) + 1, 4000, 1e-3, 1e-2
     torch.manual_seed(999)
     U0 = torch.nn.init.xavier_uniform_(torch.empty(nu, d)).numpy()
     I0 = torch.nn.init.xavier_uniform_(torch.empty(ni, d)).numpy()
@@ -205,7 +216,40 @@ def test_lightgcn_d256_k3_hub_graph_vs_oracle(cuda, tags):
             g = np.concatenate([cpu.u.grad.numpy(), cpu.i.grad.numpy()])
             p_cpu = np.concatenate([cpu.u.detach().numpy(), cpu.i.detach().numpy()])
             p_gpu = eng.p.cpu().numpy()
-            delta = 2e-5 * np.abs(g).max(axis=1, keepdims=True) + 1e-30
-            s = lambda x: x / (np.abs(x) + 1e-8)  # noqa: E731
-            bound = lr * np.maximum(np.abs(s(g + delta) - s(g)), np.abs(s(g - delta) - s(g))) + 2e-7
+            bound = _adam_first_step_bound(g, lr)
             assert np.all(np.abs(p_gpu - p_cpu) <= bound), np.abs(p_gpu - p_cpu).max()
+    assert eng.halt.tolist() == [0, 0]
+
+
+@pytest.mark.parametrize("K", [2, 4])
+def test_layergcn_c_step_vs_oracle(cuda, K):
+    """The LayerGCN batch as one C call (rsx_layergcn_step) against the oracle's CPU
+    LayerGCN training step on a hub graph, same triplets, dropout 0 (the eval graph):
+    losses rtol 1e-5 over three steps, step-1 parameters within Adam's rounding bound.
+    K = 4 is LayerGCN.yaml's default n_layers (src/configs/model/LayerGCN.yaml:2)."""
+    from rsx.layergcn import LayerGCNEngine
+
+    df = synth.amazon_like(6000, 1500, 80000, seed=4)
+    tr = df[df.x_label == 0]
+    tu, ti = tr.userID.values.astype(np.int64), tr.itemID.values.astype(np.int64)
+    nu, ni, d, lr, reg = int(df.userID.max()) + 1, 1500, 64, 1e-3, 1e-2
+    torch.manual_seed(7)
+    U0 = torch.nn.init.xavier_uniform_(torch.empty(nu, d)).numpy()
+    I0 = torch.nn.init.xavier_uniform_(torch.empty(ni, d)).numpy()
+    eng = LayerGCNEngine(tu, ti, nu, ni, d, K, reg, lr, cuda, U0, I0)
+    assert eng.norm_adj.n_long > 0
+    cpu = O.LayerGCNCPU(tu, ti, nu, ni, U0, I0, K, reg, 0.0, lr=lr)
+    cpu.pre_epoch()
+    samp = O.ReferenceSampler(tu, ti, seed=5)
+    prev = 0.0
+    for step in range(3):
+        trip = samp.next(2048)
+        want = cpu.step(trip)
+        eng.step(trip.to(cuda))
+        now = eng.loss_acc.item()  # the step's loss is added to the f64 accumulator
+        assert abs((now - prev) - want) <= 1e-5 * abs(want), (step, now - prev, want)
+        prev = now
+        if step == 0:
+            g = np.concatenate([cpu.u.grad.numpy(), cpu.i.grad.numpy()])
+            p_cpu = np.concatenate([cpu.u.detach().numpy(), cpu.i.detach().numpy()])
+            assert np.all(np.abs(eng.p.cpu().numpy() - p_cpu) <= _adam_first_step_bound(g, lr))

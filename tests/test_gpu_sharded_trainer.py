@@ -56,12 +56,25 @@ def _worker(rank, world, port, root, out):
     assert m.sharded
     t = Trainer(c, m)
     assert t.fused
+    # every rank visits each of its interactions exactly once per epoch in the common
+    # step count (no wrap-around re-training of a small shard's batches)
+    E, Bm = m.engine.n_inter, m.engine.batch
+    assert (m.steps_per_epoch - 1) * Bm < E <= m.steps_per_epoch * Bm
+    seen = []
+    step0 = m.engine.step
+
+    def spy(triplets=None, epoch=0, start=0):
+        seen.append((epoch, start))
+        return step0(triplets=triplets, epoch=epoch, start=start)
+
+    m.engine.step = spy
     losses = []
     for epoch in range(2):
         loss, n = t._train_epoch(train, epoch)
         assert not torch.is_tensor(loss) and n == m.steps_per_epoch
         losses.append(loss)
         t._epoch_for_lr += 1
+    assert seen == [(e, i * Bm) for e in range(2) for i in range(m.steps_per_epoch)]
     vres = t.evaluate(valid)
     f = m._final().cpu()
     a, b = m.user_range

@@ -213,6 +213,47 @@ def test_smore_one_epoch_with_mirror_gradient(tmp_path, golden, fx):
             assert abs(res[k] - ref[k]) <= 1e-4 + 1e-12, (tag, k, res[k], ref[k])
 
 
+@pytest.mark.parametrize("graph", [True, False])
+def test_smore_nan_loss_halts_the_step(tmp_path, golden, graph):
+    """A NaN batch loss inside an epoch of graph-replayed (or eager) SMORE batches with
+    the mirror gradient: the device NaN gate (rsx_nan_gate) stops every later Adam and
+    mirror-gradient launch, so every parameter and Adam moment stays bit for bit what
+    it was before the NaN batch, and the epoch reports that batch index (reference
+    src/common/trainer.py:192-203: checked before backward, training stops)."""
+    from rsx.trainer import Trainer
+
+    z, c, train, valid, test = _setup(tmp_path, golden)
+    c["rsx_graph_step"] = graph
+    m = _model(c, train)
+    t = Trainer(c, m)
+    m.pre_epoch_processing()
+    loss0, _ = t._train_epoch(train, 0)  # captures the graphs (both batch kinds)
+    assert not torch.is_tensor(loss0)
+    snap = {}
+    bad = 3
+
+    def poisoned():
+        for i, b in enumerate(train):
+            if i == bad:
+                m.user_embedding.weight.data[b[0, 0]] = float("nan")
+                snap["p"] = [p.detach().clone() for p in m.parameters()]
+                snap["s"] = [(st["exp_avg"].clone(), st["exp_avg_sq"].clone())
+                             for st in (t.optimizer.state[p] for p in m.parameters())]
+            yield b
+
+    m.pre_epoch_processing()
+    loss1, _ = t._train_epoch(poisoned(), 1)
+    assert torch.is_tensor(loss1) and torch.isnan(loss1)
+    assert t._halt.tolist() == [1, bad + 1]
+    if graph:
+        assert t._graph is not None and t._graph.replays > 0
+    eq = lambda a, b: torch.equal(a.view(torch.int32), b.view(torch.int32))  # noqa: E731  NaN-safe bitwise
+    for p, q in zip(m.parameters(), snap["p"]):
+        assert eq(p.detach(), q)
+    for p, (em, ev) in zip(m.parameters(), snap["s"]):
+        assert eq(t.optimizer.state[p]["exp_avg"], em) and eq(t.optimizer.state[p]["exp_avg_sq"], ev)
+
+
 def test_smore_graph_step_equals_eager(tmp_path, golden):
     """Two epochs with the training batch replayed from captured HIP graphs
     (rsx_graph_step) == the same epochs run eagerly: the host step counter and the

@@ -174,3 +174,29 @@ def test_smore_spectral_op_and_grad(cuda):
         _close(a, b, "spectral", 1e-4)
     for a, b in zip(gg, wg):
         _close(a, b, "spectral grad", 1e-4)
+
+
+def test_graph_cache_stays_bounded_over_fresh_epoch_graphs(adj, cuda):
+    """A fresh masked graph every epoch (the reference LayerGCN's pre_epoch_processing,
+    src/models/layergcn.py:51-70) through torch.ops.rsx: the op's graph cache keeps at
+    most two graphs of one shape, so device memory stays flat across epochs."""
+    from rsx import torch_ops
+
+    (rp, col, val), _, nu, ni, _ = adj
+    n = nu + ni
+    torch_ops._CACHE.clear()
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(n, 64, device=cuda)
+    mem = []
+    for epoch in range(8):
+        keep = torch.rand(col.numel(), generator=g) >= 0.1
+        rows = torch.repeat_interleave(torch.arange(n), torch.diff(rp.cpu()))[keep]
+        rpk = torch.zeros(n + 1, dtype=torch.int64)
+        rpk[1:] = torch.cumsum(torch.bincount(rows, minlength=n), 0)
+        y = torch.ops.rsx.propagate_layergcn(rpk.to(cuda), col[keep.to(cuda)].contiguous(),
+                                             val[keep.to(cuda)].contiguous(), x, 2)
+        del y, rpk, rows, keep
+        torch.cuda.synchronize()
+        assert sum(1 for k in torch_ops._CACHE if k[1:] == (n, n, False)) <= torch_ops._PER_SHAPE
+        mem.append(torch.cuda.memory_allocated(cuda))
+    assert max(mem[3:]) <= mem[2] + (1 << 20), mem
