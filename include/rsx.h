@@ -456,8 +456,8 @@ int rsx_smore_spectral_fwd(const float* V, int32_t dv, const float* Wv, const fl
  * [n_items, d] and per-block partial sums of d wv / d wt / d wf into
  * g_w_partial [rsx_smore_spectral_bwd_partials(n, d)] floats laid out
  * [ceil(n/64)][3][d/2+1][2] (sum over the first axis for the weight gradients).
- * The projection gradients d Wv = d img^T V (rsx_linear_wgrad), d V = d img Wv,
- * d bv = colsum(d img) (and the text twins) are left to the caller.
+ * The projection gradients d Wv = d img^T V, d V = d img Wv, d bv = colsum(d img)
+ * (and the text twins) are left to the caller: rsx_linear_bwd, one pass each.
  */
 size_t rsx_smore_spectral_bwd_partials(int64_t n_items, int32_t d);
 int rsx_smore_spectral_bwd(const float* spec, const float* wv, const float* wt, const float* wf,
@@ -514,14 +514,16 @@ int rsx_topk_metrics_fast(const int64_t* topk_idx, int64_t n_users, int32_t k_ma
  * gradient of SMORE's gate / query / preference layers
  * (src/models/smore.py:106-120, applied to all users+items).  The rows are split
  * over blocks, partials are summed in block order (deterministic).
- * out_dim, in_dim multiples of 32.
+ * out_dim a multiple of 32, in_dim a multiple of 4 (a ragged last 32-column tile is
+ * masked).
  */
 /*
  * The whole backward of a Linear applied to many rows in one pass over them
  * (the SMORE modality projections image_trs / text_trs, src/models/smore.py:256-259):
  * dw = g^T x [out, in], dx = g W [n, in] (W [out, in], nn.Linear layout) and, when db
  * is non-NULL, db = colsum(g) [out].  out_dim in {32, 64, 128}, in_dim a multiple
- * of 32.  Deterministic (split-K partials added in a fixed order).
+ * of 4 (e.g. the golden fixture's 48 / 24-wide features; a ragged last 32-column tile
+ * is masked).  Deterministic (split-K partials added in a fixed order).
  */
 size_t rsx_linear_bwd_ws_bytes(int64_t n, int32_t out_dim, int32_t in_dim);
 int rsx_linear_bwd(const float* g, const float* x, const float* W, int64_t n, int32_t out_dim, int32_t in_dim,

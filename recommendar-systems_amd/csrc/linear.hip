@@ -42,9 +42,11 @@ static int lin_env(const char* name, int dflt) {
     return x > 0 ? x : dflt;
 }
 
+// in_dim: a multiple of 4 (float4 rows); the i tiles cover ceil(in_dim / 32) * 32 columns and
+// the kernel masks the columns past in_dim (loads as zeros, no stores)
 static WgPlan wg_plan(int64_t n, int out_dim, int in_dim, int max_ig = 4, int64_t target_waves = kWgTargetWaves) {
     WgPlan p;
-    const int it = in_dim / 32, ot = out_dim / 32;
+    const int it = (in_dim + 31) / 32, ot = out_dim / 32;
     p.ig = (it % 4 == 0 && max_ig >= 4) ? 4 : (it % 2 == 0 && max_ig >= 2) ? 2 : 1;
     p.otb = ot % 4 == 0 ? 4 : ot % 2 == 0 ? 2 : 1;
     p.rw = 4 / p.otb;
@@ -127,7 +129,7 @@ __global__ __launch_bounds__(256) void wgrad_partial(const float* __restrict__ g
                 const int e2 = e - NG;
                 const int rr = e2 / (IC / 4), cc = (e2 % (IC / 4)) * 4;
                 const int64_t row = c0 + rr;
-                if (row < r1) t = ld4(x + row * in_dim + ib + cc);
+                if (row < r1 && ib + cc < in_dim) t = ld4(x + row * in_dim + ib + cc);
             }
             v[k] = t;
         }
@@ -159,7 +161,7 @@ __global__ __launch_bounds__(256) void wgrad_partial(const float* __restrict__ g
     if constexpr (DX) {  // W[:, ib : ib + IC] (out_dim == OC)
         for (int e = threadIdx.x; e < OC * IC / 4; e += 256) {
             const int o = e / (IC / 4), c = (e % (IC / 4)) * 4;
-            const float4 v = ld4(W + (int64_t)o * in_dim + ib + c);
+            const float4 v = ib + c < in_dim ? ld4(W + (int64_t)o * in_dim + ib + c) : f4(0.f);
             float* d = wl + o * WP + c;
             d[0] = v.x;
             d[1] = v.y;
@@ -216,7 +218,7 @@ __global__ __launch_bounds__(256) void wgrad_partial(const float* __restrict__ g
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int64_t row = c0 + mt * 16 + 4 * q4 + r;
-                    if (row < r1) dx[row * in_dim + ib + nt * 16 + n16] = d[r];
+                    if (row < r1 && ib + nt * 16 + n16 < in_dim) dx[row * in_dim + ib + nt * 16 + n16] = d[r];
                 }
             }
         }
@@ -237,10 +239,12 @@ __global__ __launch_bounds__(256) void wgrad_partial(const float* __restrict__ g
         }
     }
 #pragma unroll
-    for (int q = 0; q < IG; ++q)
+    for (int q = 0; q < IG; ++q) {
+        if (ib + 32 * q + j >= in_dim) continue;  // the padded columns of a ragged last i tile
 #pragma unroll
         for (int e = 0; e < 16; ++e)
             dst[(int64_t)(ob + wo + (e & 3) + 8 * (e >> 2) + 4 * h) * in_dim + ib + 32 * q + j] = acc[q][e];
+    }
 }
 
 // element e = blockIdx.x*64 + lane; wave w adds slots [w*S/4, (w+1)*S/4) in
@@ -298,7 +302,7 @@ __global__ __launch_bounds__(256) void wgrad_reduce_strided(const float* __restr
 using namespace rsx;
 
 extern "C" size_t rsx_linear_wgrad_ws_bytes(int64_t n, int32_t out_dim, int32_t in_dim) {
-    if (n <= 0 || out_dim <= 0 || in_dim <= 0 || (out_dim % 32) || (in_dim % 32)) return 0;
+    if (n <= 0 || out_dim <= 0 || in_dim <= 0 || (out_dim % 32) || (in_dim % 4)) return 0;
     const WgPlan p = wg_plan(n, out_dim, in_dim);
     return (size_t)p.slots() * (size_t)out_dim * (size_t)in_dim * sizeof(float);
 }
@@ -315,18 +319,18 @@ static int64_t bwd_waves() {
 }
 
 extern "C" size_t rsx_linear_bwd_ws_bytes(int64_t n, int32_t out_dim, int32_t in_dim) {
-    if (n <= 0 || (out_dim != 32 && out_dim != 64 && out_dim != 128) || in_dim <= 0 || (in_dim % 32)) return 0;
+    if (n <= 0 || (out_dim != 32 && out_dim != 64 && out_dim != 128) || in_dim <= 0 || (in_dim % 4)) return 0;
     const WgPlan p = wg_plan(n, out_dim, in_dim, bwd_ig(), bwd_waves());
     return (size_t)p.slots() * ((size_t)out_dim * (size_t)in_dim + (size_t)out_dim) * sizeof(float);
 }
 
 // dW = g^T x, dx = g W, db = colsum(g) (db may be NULL) in one pass over the rows;
-// out_dim in {32, 64, 128} (one block column of o), in_dim a multiple of 32.
+// out_dim in {32, 64, 128} (one block column of o), in_dim a multiple of 4.
 extern "C" int rsx_linear_bwd(const float* g, const float* x, const float* W, int64_t n, int32_t out_dim,
                               int32_t in_dim, float* dw, float* dx, float* db, void* ws, size_t ws_bytes,
                               rsx_stream_t stream) {
     if (n < 0 || out_dim <= 0 || in_dim <= 0 || !dw || !W || (n > 0 && !dx)) return RSX_ERR_ARG;
-    if ((out_dim != 32 && out_dim != 64 && out_dim != 128) || (in_dim % 32)) return RSX_ERR_UNSUPPORTED;
+    if ((out_dim != 32 && out_dim != 64 && out_dim != 128) || (in_dim % 4)) return RSX_ERR_UNSUPPORTED;
     if (n > 0 && (!g || !x)) return RSX_ERR_ARG;
     hipStream_t s = as_stream(stream);
     const int64_t sz = (int64_t)out_dim * in_dim;
@@ -371,7 +375,7 @@ extern "C" int rsx_linear_bwd(const float* g, const float* x, const float* W, in
 extern "C" int rsx_linear_wgrad(const float* g, const float* x, int64_t n, int32_t out_dim, int32_t in_dim, float* dw,
                                 void* ws, size_t ws_bytes, rsx_stream_t stream) {
     if (n < 0 || out_dim <= 0 || in_dim <= 0 || !dw) return RSX_ERR_ARG;
-    if ((out_dim % 32) || (in_dim % 32)) return RSX_ERR_UNSUPPORTED;
+    if ((out_dim % 32) || (in_dim % 4)) return RSX_ERR_UNSUPPORTED;
     if (n > 0 && (!g || !x)) return RSX_ERR_ARG;
     hipStream_t s = as_stream(stream);
     const int64_t sz = (int64_t)out_dim * in_dim;

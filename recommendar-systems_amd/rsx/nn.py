@@ -1,12 +1,12 @@
-"""nn.Linear whose weight gradient runs on rsx_linear_wgrad.
+"""nn.Linear container for SMORE's gate / query / preference layers.
 
-SMORE applies several Linear(d, d) layers to every user+item row (26k rows at
-Amazon-baby; reference src/models/smore.py:106-120).  Their AddmmBackward weight
-gradient g^T x has a d x d output and a 26k-long reduction, which a library GEMM
-runs on a couple of workgroups (~130 us each, ~3 ms per SMORE step under the
-mirror gradient).  RsxLinear keeps nn.Linear's parameters, initialisation and
-state-dict names, and routes only that product to the split-K kernel; the input
-gradient and the bias gradient stay torch ops.
+RsxLinear keeps nn.Linear's parameters, initialisation order and state-dict names
+(reference src/models/smore.py:106-120), so `init_seed` reproduces the reference's
+weights and checkpoints load unchanged.  The SMORE training and evaluation path
+never calls these modules: the fused kernels (csrc/smore_fuse.hip, rsx.smore_fuse)
+read their weight / bias tensors directly.  `forward` remains for API callers that
+apply a layer themselves (a library GEMM; with its weight gradient on the split-K
+kernel rsx_linear_wgrad when the widths allow).
 """
 from __future__ import annotations
 

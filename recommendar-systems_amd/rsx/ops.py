@@ -339,7 +339,7 @@ def topk_metrics(topk_idx: torch.Tensor, eval_rowptr: torch.Tensor, eval_col: to
 
 
 def linear_bwd_supported(out_dim: int, in_dim: int) -> bool:
-    return out_dim in (32, 64, 128) and in_dim % 32 == 0
+    return out_dim in (32, 64, 128) and in_dim % 4 == 0
 
 
 def linear_bwd(g: torch.Tensor, x: torch.Tensor, W: torch.Tensor, bias: bool = True):

@@ -12,14 +12,17 @@ Same class name, constructor, YAML keys, module names and creation order (so
   aggregation R — HIP SpMM with autograd (backward = SpMM with the transposed
   CSR, the kNN graphs are not symmetric);
 * projection + spectral denoise / fusion (smore.py:209-252,256-272) — the fused
-  HIP pass rsx_smore_spectral (forward and backward, see csrc/smore.hip) when the
-  library has it, else the op-for-op torch.fft form;
+  HIP pass rsx_smore_spectral (forward and backward, see csrc/smore.hip);
 * BPR part of the loss — the fused HIP BPR kernel (variant SMORE);
 * gates + inject, the item views' propagation into [R x; x], the preference
   block (query MLPs, softmax over d, dropout'd preference gates, mean, content +
   side) and both InfoNCE terms — fused HIP kernels with autograd (rsx.smore_fuse,
-  csrc/smore_fuse.hip) for d in {64, 128}; the op-for-op torch form otherwise or
-  with rsx_smore_fused: False.
+  csrc/smore_fuse.hip).
+
+The kernels are instantiated for embedding_size 64 and 128 (the SMORE.yaml default
+and C5's CLIP width) with both modalities present and feature widths that are
+multiples of 32; any other shape raises RuntimeError (RSX_ERR_UNSUPPORTED) at
+construction: there is no torch fallback on this path.
 
 Diagnostics that the reference gathers with per-step `.item()` calls
 (spectrum band energies, gate statistics, CL values) are computed lazily, only
@@ -238,7 +241,8 @@ class _DevGraph:
 
 
 def spectrum_torch(img, txt, wv, wt, wf, normalize=True):
-    """Reference spectrum_convolution (smore.py:209-237) with torch.fft."""
+    """Reference spectrum_convolution (smore.py:209-237) with torch.fft: the fp32
+    statement the tests check the HIP pass against (not called by the model)."""
     d = img.shape[1]
     fi = torch.fft.rfft(img, dim=1, norm="ortho")
     ft = torch.fft.rfft(txt, dim=1, norm="ortho")
@@ -249,6 +253,19 @@ def spectrum_torch(img, txt, wv, wt, wf, normalize=True):
     ct = torch.fft.irfft(ft * cw[1], n=d, dim=1, norm="ortho")
     cf = torch.fft.irfft(ft * fi * cw[2], n=d, dim=1, norm="ortho")
     return cv, ct, cf
+
+
+def _require_supported(d, v_feat, t_feat):
+    """The shapes the SMORE kernels are instantiated for; anything else is refused
+    (RSX_ERR_UNSUPPORTED) rather than run on torch ops."""
+    from .smore_spectral import spectral_supported
+
+    if v_feat is None or t_feat is None:
+        raise RuntimeError("RSX_ERR_UNSUPPORTED: rsx SMORE needs both the image and the text features")
+    dv, dt = int(v_feat.shape[1]), int(t_feat.shape[1])
+    if not (SF.supported(d) and spectral_supported(d, dv, dt)):
+        raise RuntimeError(f"RSX_ERR_UNSUPPORTED: rsx SMORE kernels are built for embedding_size 64 / 128 and "
+                           f"feature widths that are multiples of 32 (got d={d}, image {dv}, text {dt})")
 
 
 class SMORE(GeneralRecommender):
@@ -337,8 +354,7 @@ class SMORE(GeneralRecommender):
         self.diag_spectrum = bool(config.get("diag_spectrum", True))
         self.diag_gate = bool(config.get("diag_gate", True))
         self.diag_grad = bool(config.get("diag_grad", True))
-        self.use_hip_spectral = bool(config.get("rsx_smore_spectral", True))
-        self.use_fused = bool(config.get("rsx_smore_fused", True)) and SF.supported(d)
+        _require_supported(d, self.v_feat, self.t_feat)
         # training loss on the batch rows only (rsx_smore_batch_rows: False = full tables)
         self.batch_rows = bool(config.get("rsx_smore_batch_rows", True))
         self._bidx = {}
@@ -382,20 +398,22 @@ class SMORE(GeneralRecommender):
 
     # --------------------------------------------------------------- forward
     def spectrum_convolution(self, image_embeds, text_embeds):
-        cv, ct, cf = spectrum_torch(image_embeds, text_embeds, self.image_complex_weight,
+        """Reference API (smore.py:209-237) on already projected tables: the fused HIP
+        pass with an identity projection (x I + 0 is exact in f32)."""
+        from .smore_spectral import spectral
+
+        d = self.embedding_dim
+        eye = torch.eye(d, device=image_embeds.device, dtype=torch.float32)
+        zero = torch.zeros(d, device=image_embeds.device, dtype=torch.float32)
+        cv, ct, cf, _, _ = spectral(image_embeds, eye, zero, text_embeds, eye, zero, self.image_complex_weight,
                                     self.text_complex_weight, self.fusion_complex_weight, self.spectral_weight_norm)
         self._last["spec_in"] = (image_embeds.detach(), text_embeds.detach())
         return cv, ct, cf
 
     def _projected_spectrum(self):
-        from .smore_spectral import spectral_fused, spectral_supported
+        from .smore_spectral import spectral_fused
 
-        if (self.use_hip_spectral and self.v_feat is not None and self.t_feat is not None
-                and spectral_supported(self.embedding_dim, self.v_feat.shape[1], self.t_feat.shape[1])):
-            return spectral_fused(self)
-        img = self.image_trs(self.image_embedding.weight)
-        txt = self.text_trs(self.text_embedding.weight)
-        return self.spectrum_convolution(img, txt)
+        return spectral_fused(self)
 
     def forward(self, adj=None, train=False):
         """Reference signature: (users, items) or, with train=True, (users, items, side, content)."""
@@ -406,9 +424,7 @@ class SMORE(GeneralRecommender):
         return users, items
 
     def _forward_all(self, train=False):
-        if self.use_fused:
-            return self._forward_all_fused(train)
-        return self._forward_all_torch(train)
+        return self._forward_all_fused(train)
 
     def _views_fused(self, train=False, rows=None):
         """Everything before the preference block: (content, image, text, fusion tables,
@@ -447,51 +463,14 @@ class SMORE(GeneralRecommender):
         all_embeds, side = SF.preference(self, content, image_embeds, text_embeds, fusion_embeds, seed)
         return all_embeds, side, content
 
-    def _forward_all_torch(self, train=False):
-        cv, ct, cf = self._projected_spectrum()
-        item_id = self.item_id_embedding.weight
-        if self.inject_mode == "mul":
-            img_i = item_id * self.gate_v(cv)
-            txt_i = item_id * self.gate_t(ct)
-            fus_i = item_id * self.gate_f(cf)
-        else:
-            img_i = item_id + self.inject_scale * self.gate_v(cv)
-            txt_i = item_id + self.inject_scale * self.gate_t(ct)
-            fus_i = item_id + self.inject_scale * self.gate_f(cf)
-        ego = torch.cat([self.user_embedding.weight, item_id], dim=0)
-        content = _PropMean.apply(ego, self.norm_adj_csr, self.n_ui_layers)
-        for _ in range(self.n_layers):
-            img_i = self.image_graph(img_i)
-        image_embeds = torch.cat([self.R(img_i), img_i], dim=0)
-        for _ in range(self.n_layers):
-            txt_i = self.text_graph(txt_i)
-        text_embeds = torch.cat([self.R(txt_i), txt_i], dim=0)
-        for _ in range(self.n_layers):
-            fus_i = self.fusion_graph(fus_i)
-        fusion_embeds = torch.cat([self.R(fus_i), fus_i], dim=0)
-        soft_v = self.softmax(self.query_v(fusion_embeds))
-        soft_t = self.softmax(self.query_t(fusion_embeds))
-        agg_img = soft_v * image_embeds
-        agg_txt = soft_t * text_embeds
-        ip = self.dropout(self.gate_image_prefer(content))
-        tp = self.dropout(self.gate_text_prefer(content))
-        fp = self.dropout(self.gate_fusion_prefer(content))
-        agg_img = torch.multiply(ip, agg_img)
-        agg_txt = torch.multiply(tp, agg_txt)
-        fusion_embeds = torch.multiply(fp, fusion_embeds)
-        side = torch.mean(torch.stack([agg_img, agg_txt, fusion_embeds]), dim=0)
-        all_embeds = content + side
-        if train:
-            self._last["conv"] = (cv.detach(), ct.detach(), cf.detach())
-        return all_embeds, side, content
-
     # ------------------------------------------------------------------ loss
     @staticmethod
     def InfoNCE(view1, view2, temperature):
-        view1, view2 = F.normalize(view1, dim=1), F.normalize(view2, dim=1)
-        pos = torch.exp((view1 * view2).sum(dim=-1) / temperature)
-        ttl = torch.exp(torch.matmul(view1, view2.transpose(0, 1)) / temperature).sum(dim=1)
-        return torch.mean(-torch.log(pos / ttl))
+        """Reference API (smore.py:395-401): mean -log(exp(<v1,v2>/t) / sum_j exp(<v1,v2_j>/t))
+        of the L2-normalised rows, on the fused HIP kernels (rsx_smore_infonce_*)."""
+        ar = torch.arange(view1.shape[0], dtype=torch.int64, device=view1.device)
+        cl, _ = SF.infonce2(view1.contiguous(), view2.contiguous(), ar, ar, 0, temperature)
+        return cl
 
     def _batch_index(self, B: int):
         """(ar, trip): arange(B) and the compact triplets (b, b, B + b) of the batch rows
@@ -523,7 +502,7 @@ class SMORE(GeneralRecommender):
         return total
 
     def calculate_loss(self, interaction):
-        if self.use_fused and self.batch_rows:
+        if self.batch_rows:
             return self._calculate_loss_rows(interaction)
         users, pos, neg = interaction[0], interaction[1], interaction[2]
         all_embeds, side, content = self._forward_all(train=True)
@@ -531,11 +510,7 @@ class SMORE(GeneralRecommender):
         nu = self.n_users
         bpr = _BprLoss.apply(all_embeds, None, None, interaction[:3].contiguous(), L.RSX_BPR_SMORE,
                              float(self.reg_weight), float(self.batch_size), nu, self.n_items)
-        if self.use_fused:
-            cl_items, cl_users = SF.infonce2(side, content, users, pos, nu, self.cl_temp)
-        else:
-            cl_items = self.InfoNCE(side[nu:][pos], content[nu:][pos], self.cl_temp)
-            cl_users = self.InfoNCE(side[:nu][users], content[:nu][users], self.cl_temp)
+        cl_items, cl_users = SF.infonce2(side, content, users, pos, nu, self.cl_temp)
         self._last["cl"] = (cl_items.detach(), cl_users.detach())
         return bpr + self.cl_loss * (cl_items + cl_users)
 

@@ -5,9 +5,8 @@ text_trs and :209-237 spectrum_convolution), with autograd.
 Forward: two launches (fp32 MFMA): img = V Wv^T + bv, txt = T Wt^T + bt, then
 their rfft's (saved for the backward), the three filtered spectra and the three
 irfft's.  Backward: one launch for the spectral part (d img, d txt, d w), then the
-projection gradients:
-d Wv = d img^T V on the split-K kernel (rsx_linear_wgrad), d V = d img Wv as a
-library GEMM, d bv = colsum.
+projection gradients of each modality in one pass over its rows (rsx_linear_bwd,
+csrc/linear.hip): d Wv = d img^T V split-K, d V = d img Wv, d bv = colsum d img.
 The unit normalisation of the complex weights (:221-229) and its backward are two
 small launches (rsx_smore_unit_weights / _bwd, which also sums the spectral
 backward's per-block weight partials) instead of ~40 torch complex-op kernels.
@@ -21,7 +20,8 @@ from . import ops
 
 
 def spectral_supported(d: int, dv: int, dt: int) -> bool:
-    return d in (64, 128) and dv % 4 == 0 and dt % 4 == 0
+    """The shapes rsx_smore_spectral_fwd/bwd and rsx_linear_bwd are built for."""
+    return d in (64, 128) and ops.linear_bwd_supported(d, dv) and ops.linear_bwd_supported(d, dt)
 
 
 def unit_weight(w: torch.Tensor, normalize: bool) -> torch.Tensor:
@@ -30,14 +30,6 @@ def unit_weight(w: torch.Tensor, normalize: bool) -> torch.Tensor:
     if normalize:
         cw = cw / (torch.abs(cw) + 1e-8)
     return torch.view_as_real(cw).reshape(-1, 2)
-
-
-def _wgrad(g, x):
-    """d W = g^T x (a d x dv output over the n items): the split-K kernel when the
-    widths allow it (rsx_linear_wgrad), else a library GEMM."""
-    if g.shape[1] % 32 == 0 and x.shape[1] % 32 == 0:
-        return ops.linear_wgrad(g, x)
-    return g.t() @ x
 
 
 class _Spectral(torch.autograd.Function):
@@ -96,13 +88,12 @@ class _Spectral(torch.autograd.Function):
         need = ctx.needs_input_grad
         grads = []
         for g, X, Wx, k in ((gi, V, Wv, 0), (gt, T, Wt, 3)):
-            if need[k] and need[k + 1] and ops.linear_bwd_supported(g.shape[1], X.shape[1]):
-                # d W, d X and d b in one pass over the rows (rsx_linear_bwd)
-                dW, dX, db = ops.linear_bwd(g, X, Wx, bias=need[k + 2])
-                grads += [dX, dW, db]
-            else:
-                grads += [g @ Wx if need[k] else None, _wgrad(g, X) if need[k + 1] else None,
-                          g.sum(0) if need[k + 2] else None]
+            if not (need[k] or need[k + 1] or need[k + 2]):
+                grads += [None, None, None]
+                continue
+            # d W, d X and d b in one pass over the rows (rsx_linear_bwd)
+            dW, dX, db = ops.linear_bwd(g, X, Wx, bias=need[k + 2])
+            grads += [dX if need[k] else None, dW if need[k + 1] else None, db if need[k + 2] else None]
         return (*grads, grv, grt, grf, None)
 
 

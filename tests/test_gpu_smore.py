@@ -339,7 +339,8 @@ def test_linear_wgrad_vs_torch(cuda, n, o, i):
 
 
 @pytest.mark.parametrize("n,o,i", [(7050, 64, 4096), (7050, 64, 384), (23033, 128, 768), (1000, 128, 96),
-                                   (37, 32, 64), (513, 32, 160), (0, 64, 64)])
+                                   (37, 32, 64), (513, 32, 160), (0, 64, 64),
+                                   (200, 64, 48), (200, 64, 24), (777, 128, 100), (3000, 64, 4)])
 def test_linear_bwd_vs_torch(cuda, n, o, i):
     """rsx_linear_bwd (the projections' whole backward in one pass): dW = g^T x,
     dx = g W and db = colsum g against f64 products (tolerance relative to the
