@@ -155,10 +155,20 @@ WORKLOADS = {
 
 
 def bench_model(args):
-    """C1 / C3 through the drop-in surface (Config -> RecDataset -> loaders -> model ->
-    Trainer): a step = one training batch exactly as Trainer runs it."""
+    """C1 / C3 / C5 through the drop-in surface (Config -> RecDataset -> loaders -> model ->
+    Trainer): a step = one training batch exactly as Trainer runs it.  SMORE (c3, c5) at
+    WORLD_SIZE > 1: the users-sharded model (rsx.smore_dist: items replicated, one item
+    all-reduce per UI layer over RCCL), every rank stepping on its own batch."""
     import tempfile
 
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     from rsx import synth
     from rsx.config import Config
     from rsx.data import EvalDataLoader, RecDataset, TrainDataLoader
@@ -196,13 +206,20 @@ def bench_model(args):
     build_s = time.perf_counter() - t_build
     t = Trainer(c, model)
     model.train()
+    sharded = bool(getattr(model, "sharded", False))
+    if sharded:
+        t._gate = t._nan_gate_on()  # as Trainer._train_epoch_autograd arms it
+        if t._gate:
+            t._arm_nan_gate()
 
     def batches():
+        ep = 0
         while True:
             model.pre_epoch_processing()
             t.reset_graph_step()  # as Trainer._train_epoch does at each epoch start
-            for b in train:
+            for b in (model.local_batches(ep) if sharded else train):
                 yield b
+            ep += 1
 
     it = batches()
     idx = {"i": 0}
@@ -225,6 +242,8 @@ def bench_model(args):
     for _ in range(n_warm):
         one_step()
     torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
     n = 0
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
@@ -234,10 +253,24 @@ def bench_model(args):
     ev1.record()
     t_issue = time.perf_counter() - t0
     torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
     wall = time.perf_counter() - t0
-    log(f"[bench] {w['model']}: {wall * 1e3 / args.steps:.3f} ms/step wall, host issue {t_issue * 1e3 / args.steps:.3f} "
-        f"ms/step, events {ev0.elapsed_time(ev1) / args.steps:.3f} ms/step, graph replays "
-        f"{getattr(getattr(t, '_graph', None), 'replays', None)}")
+    log(f"[bench] rank {rank}/{world} {w['model']}: {wall * 1e3 / args.steps:.3f} ms/step wall, host issue "
+        f"{t_issue * 1e3 / args.steps:.3f} ms/step, events {ev0.elapsed_time(ev1) / args.steps:.3f} ms/step, "
+        f"graph replays {getattr(getattr(t, '_graph', None), 'replays', None)}")
+    dev = torch.device("cuda", torch.cuda.current_device())
+    per_rank = _rank_report(wall, ev0.elapsed_time(ev1), args.steps, world, dev)
+    rccl_world = None
+    if world > 1:
+        tot = torch.tensor([float(n)], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(tot)
+        n = float(tot.item())
+        wall = max(p["ms_per_step"] for p in per_rank) * args.steps / 1e3
+        if getattr(getattr(model, "comm", None), "handle", None) is not None:
+            ones = torch.ones(1, dtype=torch.float32, device=dev)
+            model.comm.allreduce_(ones)
+            rccl_world = int(round(float(ones.item())))
     model.eval()
     t.evaluate(valid)
     torch.cuda.synchronize()
@@ -246,12 +279,18 @@ def bench_model(args):
     torch.cuda.synchronize()
     eval_s = time.perf_counter() - te0
     n_eval = int(len(valid.get_eval_users()))
+    if world > 1:
+        ev_t = torch.tensor([eval_s], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(ev_t, op=torch.distributed.ReduceOp.MAX)
+        eval_s = float(ev_t.item())
 
     # roofline: one propagation SpMM (STORE) over the model's training graph, d columns
     d = int(c["embedding_size"])
     if w["model"] == "SMORE":
         A = model.norm_adj_csr
         x = torch.cat([model.user_embedding.weight, model.item_id_embedding.weight]).detach().contiguous()
+        if sharded:  # the full graph over a full-size operand (this rank holds its user rows only)
+            x = torch.randn(A.n_cols, d, device=x.device)
         kname = f"spmm_main<{d},STORE> UI-graph propagation layer"
     else:
         A = model.engine.train_adj
@@ -265,7 +304,7 @@ def bench_model(args):
             "algorithmic_bytes_per_launch": alg, "avg_launch_ms": spmm_ms,
             "note": "baby/clothing working sets are Infinity-Cache resident"}
     cpu = None
-    if not args.no_cpu_baseline:
+    if not args.no_cpu_baseline and world == 1:
         tr_df = df[df.x_label == 0]
         tu_, ti_ = tr_df.userID.values.astype(np.int64), tr_df.itemID.values.astype(np.int64)
         nu_ = int(df.userID.max()) + 1
@@ -276,20 +315,28 @@ def bench_model(args):
             cpu = cpu_baseline_layergcn(tu_, ti_, nu_, ni, int(c["n_layers"]), float(c["reg_weight"]),
                                         float(c["dropout"]), args.cpu_budget, -(-tu_.size // args.batch))
     out = {
-        "metric": METRIC, "value": n / wall, "unit": "interactions/s", "n_gpus": 1, "steps": args.steps,
+        "metric": METRIC, "value": n / wall, "unit": "interactions/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "warmup_steps_run": n_warm, "ms_per_step": wall * 1e3 / args.steps,
         "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32",
         "data": f"synthetic Amazon-{w['dataset']}-shaped graph (rsx.synth seed 0)"
                 + ("; N(0,1) features" if w["model"] == "SMORE" else ""),
         "config": {"workload": w["desc"], "model": w["model"], "embedding_size": int(c["embedding_size"]),
-                   "global_batch": args.batch, "parallelism": "single", "fused_step": bool(t.fused),
+                   "global_batch": int(getattr(model, "local_batch", args.batch)) * world,
+                   "parallelism": f"usershard{world}" if sharded else "single", "fused_step": bool(t.fused),
                    "graph_step": t._graph is not None and t._graph.replays > 0},
+        "launcher": os.environ.get("RSX_BENCH_LAUNCHER", "torchrun" if world > 1 else "single process"),
+        "rccl_world_size": rccl_world, "per_rank": per_rank,
         "fullsort_items_per_s": n_eval * ni / eval_s,
         "fullsort": {"eval_users": n_eval, "n_items": ni, "s_per_eval_incl_forward_and_metrics": eval_s},
         "model_build_s": build_s, "roofline": roof, "cpu_baseline": cpu,
     }
-    _json_line(out)
+    if rank == 0:
+        _json_line(out)
+    if world > 1:
+        if getattr(model, "comm", None) is not None:
+            model.comm.close()
+        torch.distributed.destroy_process_group()
 
 
 def _c4_chunk(args):
@@ -499,8 +546,8 @@ def main():
     args.warmup = args.warmup if args.warmup is not None else (3 if big else 20)
     args.eval_users = args.eval_users if args.eval_users is not None else (32768 if big else 0)
     if args.workload in ("c1", "c3", "c5"):
-        if int(os.environ.get("WORLD_SIZE", "1")) != 1:
-            raise SystemExit("--workload c1/c3/c5 are single-GPU legs")
+        if int(os.environ.get("WORLD_SIZE", "1")) != 1 and args.workload == "c1":
+            raise SystemExit("--workload c1 is a single-GPU leg")
         return bench_model(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -152,6 +152,7 @@ class DeviceCSR:
 
     def spmm_epi(self, x: torch.Tensor, epi: "L.Epilogue", d: int):
         _gpu(x)
+        _check_x(self, x, d)
         rc = L.lib().rsx_spmm(C.byref(self.struct), _p(x), d, C.byref(epi), _p(self.slab(d)), _stream())
         L.check(rc, "rsx_spmm")
 
@@ -165,11 +166,20 @@ class DeviceCSR:
         return y
 
 
+def _check_x(A, x, d: int):
+    """The kernel gathers rows 0..n_cols-1 of x with d contiguous floats each: check that
+    before the launch (an out-of-range gather would fault the GPU)."""
+    if x.dim() != 2 or x.shape[1] != d or x.shape[0] < A.n_cols or not x.is_contiguous() \
+            or x.dtype != torch.float32:
+        raise RuntimeError(f"spmm: x {tuple(x.shape)} {x.dtype} does not cover the {A.n_cols} x {d} operand")
+
+
 def spmm_batch(csrs, xs, epis, d: int):
     """Y_p = A_p X_p with epilogue epis[p] for up to 4 products in one launch (rsx_spmm_batch)."""
     n = len(csrs)
-    for x in xs:
+    for a, x in zip(csrs, xs):
         _gpu(x)
+        _check_x(a, x, d)
     arr_a = (C.c_void_p * n)(*[C.addressof(a.struct) for a in csrs])
     arr_x = (C.c_void_p * n)(*[x.data_ptr() for x in xs])
     arr_e = (L.Epilogue * n)(*epis)

@@ -101,13 +101,15 @@ class _PropMeanRows(torch.autograd.Function):
     the batch rows of the SMORE training loss): E^1..E^{K-1} stored (no running sum),
     the last layer and the mean on the tagged rows only, in the running sum's order
     (((E0 + E1) + E2) + E3) + A E3 (other rows of the output are left unwritten).  The
-    backward is Horner on the incoming gradient G, which is zero off the tagged rows:
+    backward is Horner on the incoming gradient G, which is zero off the tagged rows
+    (`rows`: the forward's rows, re-tagged in the backward, so several forwards may run
+    before their backwards, as in a sum of batch losses):
     H = G + A H from H = G, the first layer gathering only the tagged rows of G, every
     layer reading G on the tagged rows only, the last scaled by 1/(K+1) (the dense
     path's arithmetic: the same mean operator applied to G)."""
 
     @staticmethod
-    def forward(ctx, x, A, K, tags):
+    def forward(ctx, x, A, K, tags, rows=None):
         x = x.contiguous()
         n, d = x.shape
         out = torch.empty_like(x)
@@ -120,12 +122,16 @@ class _PropMeanRows(torch.autograd.Function):
         e = ops.epi(L.RSX_EPI_FINAL, beta=1.0 / (K + 1), f=out, row_tag=tags.row_tag, tag_dev=tags.tag_dev, **stored)
         e.tag_flags = L.RSX_TAG_ROWS
         A.spmm_epi(cur, e, d)
-        ctx.A, ctx.K, ctx.tags = A, K, tags
+        ctx.A, ctx.K, ctx.tags, ctx.rows = A, K, tags, rows
         return out
 
     @staticmethod
     def backward(ctx, g):
         A, K, tags = ctx.A, ctx.K, ctx.tags
+        if ctx.rows is not None:
+            # re-tag this forward's rows: a later forward (another calculate_loss before this
+            # backward) may have moved the tag on, and G is zero off exactly these rows
+            tags.mark(ctx.rows)
         g = g.contiguous()
         d = g.shape[1]
         bufs = torch.empty(2, *g.shape, dtype=torch.float32, device=g.device)
@@ -137,7 +143,7 @@ class _PropMeanRows(torch.autograd.Function):
             e.tag_flags = L.RSX_TAG_SPARSE_S | (L.RSX_TAG_SPARSE_X if k == 1 else 0)
             A.spmm_epi(h, e, d)
             h = y
-        return h, None, None, None
+        return h, None, None, None, None
 
 
 def knn_graph(feat: np.ndarray, k: int):
@@ -369,6 +375,78 @@ class SMORE(GeneralRecommender):
                                        device=self.device)
         self._last = {}
         self.to(self.device)
+        from .lightgcn import _world
+
+        world, rank = _world()
+        flag = config["rsx_sharded"]  # None: shard whenever the process group has > 1 rank
+        self.sharded = bool(flag) if flag is not None else world > 1
+        if self.sharded:
+            self._init_sharded(config, rp, col, val, (rows, col[:e].astype(np.int64) - nu, val[:e]), world, rank)
+
+    def _init_sharded(self, config, rp, col, val, r_coo, world, rank):
+        """Users sharded over the process group, the item side replicated (rsx.smore_dist):
+        this rank keeps its rows of the user table (drawn in full first, so every rank
+        holds the reference's initial weights), its rows of the UI graph and of R, and
+        samples its own users' interactions on the device."""
+        from .smore_dist import Comm, HipSmoreBackend, SmoreShard
+
+        nu, ni = self.n_users, self.n_items
+        self.comm = Comm(None, self.device)
+        graphs = {"norm_adj": (np.asarray(rp), np.asarray(col), np.asarray(val)),
+                  "R": graph.to_csr(r_coo[0], r_coo[1], r_coo[2], nu, ni),
+                  "image": self.image_graph, "text": self.text_graph, "fusion": self.fusion_graph}
+        self._shard = SmoreShard(graphs, nu, ni, self.n_ui_layers, self.n_layers,
+                                 HipSmoreBackend(self.device, int(config["rsx_chunk"] or 32)), self.comm)
+        a, b = self._shard.own_u
+        self.user_range = (a, b)
+        w = self.user_embedding.weight.detach()[a:b].clone()
+        self.user_embedding = nn.Embedding(b - a, self.embedding_dim, _weight=w, device=self.device)
+        # the step's collectives are captured with it only over RCCL (a gloo group's are host calls)
+        self.supports_graph_step = self.comm.native
+        # this rank's interactions, visited once per epoch in the common step count
+        im = self.interaction_matrix
+        rows, cols = im.row.astype(np.int64), im.col.astype(np.int64)
+        sel = (rows >= a) & (rows < b)
+        e_r = int(sel.sum())
+        if e_r == 0:
+            raise RuntimeError(f"rank {rank}: no training interactions in users [{a}, {b})")
+        B = int(config["train_batch_size"])
+        cnt = torch.tensor([float(e_r), 0.0], dtype=torch.float32, device=self.device)
+        self.comm.allreduce_(cnt)
+        steps = -(-int(round(cnt[0].item())) // (world * B))
+        self.local_batch = -(-e_r // steps)
+        self.steps_per_epoch = steps
+        self._sampler = ops.DeviceSampler(rows[sel] - a, cols[sel], b - a, self.device,
+                                          seed=int(config["seed"] or 0) + rank)
+        self._epoch_buf = None
+        self._epoch_of_buf = None
+        self._gate_buf = torch.zeros(1, dtype=torch.float32, device=self.device)
+
+    def local_batches(self, epoch: int):
+        """This rank's training batches of `epoch` (device-sampled [3, B_r] triplets: users
+        as local row ids, items global): steps_per_epoch of them on every rank."""
+        if self._epoch_of_buf != epoch:
+            self._epoch_buf = self._sampler.sample_epoch(epoch, self.local_batch, out=self._epoch_buf)
+            self._epoch_of_buf = epoch
+        for j in range(self.steps_per_epoch):
+            yield ops.DeviceSampler.batch_view(self._epoch_buf, self._sampler.n_inter, self.local_batch, j)
+
+    def gate_loss(self, loss):
+        """The NaN gate's input on a sharded model: the loss summed over the ranks, so a NaN
+        batch on any rank stops every rank's updates (the replicas stay equal)."""
+        if not self.sharded:
+            return loss
+        self._gate_buf.copy_(loss.detach().reshape(1))
+        return self.comm.allreduce_(self._gate_buf)
+
+    def mg_alpha_global(self, params, grads, base, lr, rel_step, max_scale, lr_dev=None):
+        """The mirror gradient's alpha over the global parameter vector (sharded model)."""
+        return self._shard.mg_alpha(self, params, grads, base, lr, rel_step, max_scale, lr_dev)
+
+    def full_sort_topk_local(self, eval_users, k: int, eval_data):
+        """(positions in eval_users of this rank's users, their top-k item ids)."""
+        return self._shard.full_sort_topk_local(self, self._drop_seed, eval_users, k, eval_data.mask_rowptr,
+                                                eval_data.mask_col)
 
     # ---------------------------------------------------------------- graphs
     def _cached_knn(self, root, name, feat, k):
@@ -385,15 +463,23 @@ class SMORE(GeneralRecommender):
         f = feat.detach().cpu().numpy()
         sig = np.array([f.shape[0], f.shape[1], float(np.float64(f[:4].sum())), float(np.float64(f[-4:].sum()))])
         if os.path.exists(path):
-            z = np.load(path)
-            if np.array_equal(z["sig"], sig):
-                return z["r"], z["c"], z["v"]
+            try:
+                z = np.load(path)
+                if np.array_equal(z["sig"], sig):
+                    return z["r"], z["c"], z["v"]
+            except (OSError, ValueError, KeyError, EOFError):  # another rank still writing it: rebuild
+                pass
         r, c, v = knn_graph_device(feat.detach().to(self.device), k) if device_build else knn_graph(f, k)
-        try:
-            os.makedirs(root, exist_ok=True)
-            np.savez(path, r=r, c=c, v=v, sig=sig)
-        except OSError:
-            pass
+        from .lightgcn import _world
+
+        if _world()[1] == 0:  # one writer per job (every rank builds the same graph)
+            try:
+                os.makedirs(root, exist_ok=True)
+                tmp = f"{path}.{os.getpid()}.tmp.npz"
+                np.savez(tmp, r=r, c=c, v=v, sig=sig)
+                os.replace(tmp, path)
+            except OSError:
+                pass
         return r, c, v
 
     # --------------------------------------------------------------- forward
@@ -438,7 +524,7 @@ class SMORE(GeneralRecommender):
             if self._tags is None:
                 self._tags = _RowTags(self.n_users + self.n_items, self.device)
             self._tags.mark(rows)
-            content = _PropMeanRows.apply(ego, self.norm_adj_csr, self.n_ui_layers, self._tags)
+            content = _PropMeanRows.apply(ego, self.norm_adj_csr, self.n_ui_layers, self._tags, rows)
         else:
             content = _PropMean.apply(ego, self.norm_adj_csr, self.n_ui_layers)
         nu, L_ = self.n_users, self.n_layers
@@ -502,6 +588,11 @@ class SMORE(GeneralRecommender):
         return total
 
     def calculate_loss(self, interaction):
+        if self.sharded:  # this rank's batch (users as local row ids): rsx.smore_dist
+            if self.training and self.dropout.p > 0:
+                self._drop_seed.add_(1)
+            self.global_step += 1
+            return self._shard.loss(self, interaction, self._drop_seed)
         if self.batch_rows:
             return self._calculate_loss_rows(interaction)
         users, pos, neg = interaction[0], interaction[1], interaction[2]
@@ -515,11 +606,15 @@ class SMORE(GeneralRecommender):
         return bpr + self.cl_loss * (cl_items + cl_users)
 
     def full_sort_predict(self, interaction):
+        if self.sharded:
+            raise NotImplementedError("the sharded SMORE evaluates through full_sort_topk_local")
         with torch.no_grad():
             u, i = self.forward(self.norm_adj_csr)
         return ops.score_dense(u.contiguous(), interaction[0].contiguous(), i.contiguous())
 
     def full_sort_topk(self, interaction, k, eval_data):
+        if self.sharded:
+            raise NotImplementedError("the sharded SMORE evaluates through full_sort_topk_local")
         with torch.no_grad():
             if getattr(self, "_eval_cache", None) is None:
                 u, i = self.forward(self.norm_adj_csr)

@@ -1,39 +1,51 @@
-"""SMORE sharded over the ranks of a process group ("the same
-scheme ... shard the projection by item rows and all-gather the projected NI x d").
+"""SMORE over the ranks of a process group: users sharded, the item side replicated
+("replicate the item-side tables and kNN graphs", 141 MB at
+Amazon-clothing).  Reference model: src/models/smore.py:24-411; the multi-GPU
+scheme replaces the reference's one-device pinning (src/utils/configurator.py:114-118).
 
-Partition: users and items are split into contiguous per-rank ranges; a rank owns
-its users' and items' rows of every table — the user and item-id embeddings and
-the raw image / text feature tables (Embedding.from_pretrained(freeze=False): the
-largest parameters, 7050 x 4096 at Amazon-baby).  The small weights (projections,
-gates, query MLPs, spectral filters) are replicated and their gradients summed.
+Partition.  Rank r owns the contiguous user block [a_r, b_r): its rows of the user
+embedding (the only row-sharded parameter), of the normalised UI adjacency and of R.
+Everything item-side is replicated and bit-identical on every rank: the item-id
+embedding, the raw image / text feature tables (trainable, the largest
+parameters), the projections, spectral filters, gates and preference weights, and
+the kNN item graphs.
 
-Forward (reference src/models/smore.py:256-349), per rank:
-  * projection + spectral fusion and the modality gates on its own item rows
-    (row-local, smore.py:256-272);
-  * the UI backbone, n_ui_layers times: all-gather the [users; items] table, multiply
-    by this rank's rows of the normalised adjacency (smore.py:276-287);
-  * each item view: all-gather the item rows, multiply by this rank's rows of the
-    kNN graph, n_layers times; then this rank's users through R (smore.py:289-317);
-  * the preference block on its own rows (smore.py:320-341).
-Loss: the all_embeds / side / content tables are all-gathered and every rank
-evaluates the reference loss on the whole batch (BPR + regulariser + both InfoNCE
-terms, smore.py:352-411), scaled by 1/W: the gathers' backward (an all-reduce of the
-full gradient, then this rank's slice) sums the W copies into exactly the
-single-process gradient of the owned rows; `sync_grads` sums the replicated
-weights' gradients.  One step therefore equals the single-process step (the
-gloo tests compare them), up to f32 summation order.
+Step (per rank, on its own batch of its own users' interactions; the objective is
+the sum over ranks of the reference loss of each rank's batch, i.e. data-parallel
+batches of B per GPU):
+  * projection + spectral fusion and the modality gates on every item (replicated);
+  * the UI backbone, n_ui_layers times: users^k = A_U items^{k-1} (local rows),
+    items^k = sum_g A_I,g users_g^{k-1} — ONE all-reduce of the item partial
+    [n_items, d] per layer;
+  * the three item views through their kNN graphs (replicated), their user rows
+    through the rank's rows of R;
+  * the preference block and the loss (BPR + both InfoNCE terms) on the batch rows
+    only ([users; positives; negatives], rsx.smore._calculate_loss_rows' form).
+Backward: the UI backbone's gradient is the same operator on (G_U, sum_g G_I,g) —
+one all-reduce of G's item rows, then one per layer; the three views' item-row
+gradients (their own rows plus R^T of the user rows) are summed over the ranks in
+ONE all-reduce before the replicated kNN / gate / spectral / projection backward,
+which then runs identically everywhere; the preference weights' gradients (the only
+replicated weights fed by rank-local rows) are summed in one all-reduce.  Every
+replicated parameter therefore receives the complete, identical gradient and the
+replicas stay bit-identical under the per-element Adam; no table is ever gathered.
 
-The gather is an autograd Function over torch.distributed (all_gather forward,
-all_reduce + slice backward: works over gloo and RCCL; device tensors over gloo
-travel through host copies).  Compute goes through a backend: `HipSmoreBackend`
-(the rsx kernels: fused spectral pass, gates, preference, InfoNCE, SpMM, BPR) or
-a torch restatement (tests on the CPU).  Dropout masks (p > 0) are drawn per local
-row, so they differ from a single-process run's (same distribution).
+Exchange per forward + backward pass at C5 (n_items 23,033, d 128: X = 11.8 MB):
+4 (UI forward) + 1 + 4 (UI backward) + 3 (views, one call) all-reduces of X + a
+0.5 MB weight all-reduce = 12 X per pass, ~2.9 passes per step with the mirror
+gradient (DESIGN.md §6 models the time).
 
-Evaluation: each rank ranks its own users against the gathered item table
-(`full_sort_topk_local`); rsx.evaluator.sharded_metric_dict all-gathers the sums.
+Collectives go through `Comm`: over "nccl" an rsx communicator (csrc/dist.hip,
+RCCL, stream-ordered, captured with the step's HIP graph), otherwise (gloo, tests)
+torch.distributed on host copies.  Compute goes through a backend: `HipSmoreBackend`
+(the rsx kernels) or, in the CPU tests, a torch restatement.
+
+Evaluation: every rank ranks its own users against the (replicated) item rows;
+rsx.evaluator.sharded_metric_dict all-gathers the metric sums.
 """
 from __future__ import annotations
+
+import ctypes as C
 
 import numpy as np
 import torch
@@ -43,63 +55,111 @@ import torch.nn as nn
 from . import _lib as L
 from . import graph, ops
 
-# parameters split by rows: (name, "u" users | "i" items)
-SHARDED = {"user_embedding.weight": "u", "item_id_embedding.weight": "i", "image_embedding.weight": "i",
-           "text_embedding.weight": "i"}
+# the row-sharded parameter (its rows [a_r, b_r) live on rank r); everything else is replicated
+SHARDED = {"user_embedding.weight": "u"}
+# the preference block's Linear layers: replicated weights fed by rank-local rows
+PREF = ("query_v.0", "query_v.2", "query_t.0", "query_t.2", "gate_image_prefer.0", "gate_text_prefer.0",
+        "gate_fusion_prefer.0")
 
 
 def ranges(n: int, world: int):
     return [(r * n // world, (r + 1) * n // world) for r in range(world)]
 
 
-def _host_if_gloo(t, group):
-    return t.cpu() if (t.is_cuda and dist.get_backend(group) != "nccl") else t
+class Comm:
+    """In-place f32 sum all-reduce over the process group.  "nccl": an rsx
+    communicator (RCCL through csrc/dist.hip: rsx_comm_allreduce_f32 on the caller's
+    stream, capturable in a HIP graph); other backends: torch.distributed on host
+    copies (gloo; several ranks may share one GPU)."""
+
+    def __init__(self, group=None, device=None):
+        self.group = group
+        if not (dist.is_available() and dist.is_initialized()):  # rsx_sharded without a group: one rank
+            self.world, self.rank, self.native, self.handle = 1, 0, False, None
+            return
+        self.world, self.rank = dist.get_world_size(group), dist.get_rank(group)
+        self.native = dist.get_backend(group) == "nccl"
+        self.handle = None
+        if self.native and self.world > 1:
+            lib = L.lib()
+            nb = int(lib.rsx_comm_unique_id_bytes())
+            buf = (C.c_uint8 * nb)()
+            if self.rank == 0:
+                L.check(lib.rsx_comm_get_unique_id(buf), "rsx_comm_get_unique_id")
+            uid = torch.tensor(bytearray(bytes(buf)), dtype=torch.uint8, device=device)
+            dist.broadcast(uid, src=dist.get_global_rank(group, 0) if group else 0, group=group)
+            C.memmove(buf, bytes(uid.cpu().numpy().tobytes()), nb)
+            h = C.c_void_p()
+            with torch.cuda.device(device):
+                L.check(lib.rsx_comm_init(C.byref(h), buf, self.rank, self.world), "rsx_comm_init")
+            self.handle = h
+
+    def allreduce_(self, t: torch.Tensor) -> torch.Tensor:
+        if self.world == 1:
+            return t
+        if t.dtype != torch.float32 or not t.is_contiguous():
+            raise RuntimeError("Comm.allreduce_: contiguous float32 tensors")
+        if self.handle is not None:
+            L.check(L.lib().rsx_comm_allreduce_f32(self.handle, t.data_ptr(), t.numel(), ops._stream()),
+                    "rsx_comm_allreduce_f32")
+            return t
+        h = t.cpu() if t.is_cuda else t
+        dist.all_reduce(h, group=self.group)
+        if h is not t:
+            t.copy_(h)
+        return t
+
+    def close(self):
+        if self.handle is not None:
+            torch.cuda.synchronize()
+            L.lib().rsx_comm_destroy(self.handle)
+            self.handle = None
 
 
-class _Gather(torch.autograd.Function):
-    """x = this rank's rows [a_r, b_r) -> the full [n, ...] table (all ranks' rows in
-    rank order); backward: the full gradient all-reduced, this rank's slice."""
+class _AllReduceGrad(torch.autograd.Function):
+    """Identity forward; backward: the gradients of all inputs summed over the ranks in
+    one all-reduce (replicated tensors fed by rank-local work)."""
 
     @staticmethod
-    def forward(ctx, x, rng, group):
-        r = dist.get_rank(group)
-        mx = max(b - a for a, b in rng)
-        buf = x.new_zeros((mx,) + tuple(x.shape[1:]))
-        buf[: x.shape[0]] = x
-        hb = _host_if_gloo(buf, group)
-        parts = [torch.empty_like(hb) for _ in rng]
-        dist.all_gather(parts, hb.contiguous(), group=group)
-        full = torch.cat([p[: b - a] for p, (a, b) in zip(parts, rng)]).to(x.device)
-        ctx.rng, ctx.r, ctx.group = rng, r, group
-        return full
+    def forward(ctx, comm, *ts):
+        ctx.comm = comm
+        ctx.shapes = [t.shape for t in ts]
+        return tuple(t.view_as(t) for t in ts)
+
+    @staticmethod
+    def backward(ctx, *gs):
+        ref = next(g for g in gs if g is not None)
+        flat = torch.cat([(g if g is not None else torch.zeros(s, dtype=ref.dtype, device=ref.device)).reshape(-1)
+                          for g, s in zip(gs, ctx.shapes)])
+        ctx.comm.allreduce_(flat)
+        out, o = [], 0
+        for s in ctx.shapes:
+            n = int(np.prod(s)) if len(s) else 1
+            out.append(flat[o:o + n].view(s))
+            o += n
+        return (None, *out)
+
+
+def allreduce_grad(comm, *ts):
+    return _AllReduceGrad.apply(comm, *ts)
+
+
+class _UIProp(torch.autograd.Function):
+    """content = mean_{k=0..K} A^k E0 of the users-sharded UI graph, rows [own users;
+    all items] (the item rows identical on every rank).  A is symmetric, so the
+    backward is the same operator applied to (G_U, sum over ranks of G_I)."""
+
+    @staticmethod
+    def forward(ctx, x, core):
+        ctx.core = core
+        return core.ui_mean(x.contiguous())
 
     @staticmethod
     def backward(ctx, g):
-        h = _host_if_gloo(g.contiguous(), ctx.group).clone()
-        dist.all_reduce(h, group=ctx.group)
-        a, b = ctx.rng[ctx.r]
-        return h[a:b].to(g.device), None, None
-
-
-def gather(x, rng, group=None):
-    return _Gather.apply(x, rng, group)
-
-
-def csr_rows(rowptr, col, val, r0: int, r1: int):
-    """Rows [r0, r1) of a host CSR (columns unchanged)."""
-    a, b = int(rowptr[r0]), int(rowptr[r1])
-    return rowptr[r0:r1 + 1] - a, col[a:b], val[a:b]
-
-
-def stack_csr(*blocks):
-    """Row-concatenation of host CSR blocks with the same columns."""
-    rps, cols, vals, off = [np.zeros(1, np.int64)], [], [], 0
-    for rp, c, v in blocks:
-        rps.append(rp[1:] + off)
-        off += int(rp[-1])
-        cols.append(c)
-        vals.append(v)
-    return np.concatenate(rps), np.concatenate(cols), np.concatenate(vals)
+        core = ctx.core
+        g = g.contiguous().clone()
+        core.comm.allreduce_(g[core.nu_own:])
+        return core.ui_mean(g), None
 
 
 # ---------------------------------------------------------------------------
@@ -112,248 +172,263 @@ class HipSmoreBackend:
         self.device = ops.require_device(device)
         self.chunk = chunk
 
-    def operator(self, rowptr, col, val, n_cols):
-        """(A, A^T) device CSRs of a local row block (the backward multiplies by A^T)."""
-        n_rows = rowptr.size - 1
+    def operator(self, rowptr, col, val, n_cols, transpose=False):
+        """A device CSR of a local row block (and, with transpose, the pair (A, A^T) for a
+        product whose backward multiplies by A^T)."""
         A = ops.DeviceCSR(rowptr, col, val, n_cols, self.device, self.chunk)
+        if not transpose:
+            return A
+        n_rows = rowptr.size - 1
         rows = np.repeat(np.arange(n_rows, dtype=np.int64), np.diff(rowptr))
         AT = ops.DeviceCSR(*graph.to_csr(col.astype(np.int64), rows, val, n_cols, n_rows), n_rows, self.device,
                            self.chunk)
-        return A, AT
+        return _Pair(A, AT)
 
-    def spmm(self, op, x):
-        from .smore import _SpMM
+    def ui_mean(self, core, x):
+        """mean over layers with the running sums in the SpMM epilogues (users) and one
+        all-reduce of every item partial (its running sum a row-wise ADD after it)."""
+        nu, K, d = core.nu_own, core.K, x.shape[1]
+        ni = x.shape[0] - nu
+        out = torch.empty_like(x)
+        s = torch.empty_like(x)
+        bufs = torch.empty(2, *x.shape, dtype=torch.float32, device=x.device)
+        cur = x
+        beta = 1.0 / (K + 1)
+        for k in range(1, K + 1):
+            y = bufs[k & 1]
+            s_in = x if k == 1 else s
+            # item partial = A_I users^{k-1}, summed over the ranks
+            core.A_I.spmm_epi(cur[:nu], ops.epi(L.RSX_EPI_STORE, y=y[nu:]), d)
+            core.comm.allreduce_(y[nu:])
+            if k < K:
+                core.A_U.spmm_epi(cur[nu:], ops.epi(L.RSX_EPI_LAYERSUM, y=y[:nu], s_in=s_in[:nu], s_out=s[:nu]), d)
+                ops.rowwise(ni, d, ops.epi(L.RSX_EPI_ADD, y=s[nu:], s_in=s_in[nu:], r_add=y[nu:]))
+            else:
+                core.A_U.spmm_epi(cur[nu:], ops.epi(L.RSX_EPI_FINAL, beta=beta, f=out[:nu], s_in=s_in[:nu]), d)
+                ops.rowwise(ni, d, ops.epi(L.RSX_EPI_ADD, beta=beta, y=out[nu:], s_in=s_in[nu:], r_add=y[nu:]))
+            cur = y
+        if K == 0:
+            out.copy_(x)
+        return out
 
-        return _SpMM.apply(x, op[0], op[1])
-
-    def spectral(self, m, V, T):
+    def spectral(self, m):
         from .smore_spectral import spectral
 
-        return spectral(V, m.image_trs.weight, m.image_trs.bias, T, m.text_trs.weight, m.text_trs.bias,
-                        m.image_complex_weight, m.text_complex_weight, m.fusion_complex_weight, True)[:3]
+        return spectral(m.image_embedding.weight, m.image_trs.weight, m.image_trs.bias, m.text_embedding.weight,
+                        m.text_trs.weight, m.text_trs.bias, m.image_complex_weight, m.text_complex_weight,
+                        m.fusion_complex_weight, getattr(m, "spectral_weight_norm", True))[:3]
 
     def gates(self, m, cv, ct, cf, item):
         from . import smore_fuse as SF
 
         return SF.gates(cv, ct, cf, item, m.gate_v, m.gate_t, m.gate_f, m.inject_scale, False)
 
-    def preference(self, m, C, IE, TE, FE):
+    def views(self, core, xs):
         from . import smore_fuse as SF
 
-        return SF.preference(m, C, IE, TE, FE, m._seed)
+        return SF.view_prop3(xs, core.G, core.R, core.L, core.nu_own, comm=core.comm)
 
-    def loss(self, m, all_e, side, content, inter):
+    def pref_rows(self, m, content, views, rows, seed, weights):
         from . import smore_fuse as SF
-        from .lightgcn import _BprLoss
 
-        nu = m.n_users
-        bpr = _BprLoss.apply(all_e, None, None, inter[:3].contiguous(), L.RSX_BPR_SMORE, float(m.reg_weight),
-                             float(m.batch_size), nu, m.n_items)
-        ci, cu = SF.infonce2(side, content, inter[0].contiguous(), inter[1].contiguous(), nu, m.cl_temp)
-        return bpr + m.cl_loss * (ci + cu)
+        return SF.preference_rows(m, content, *views, rows, seed, weights=weights)
 
-    def mean_layers(self, layers):
-        return torch.stack(layers, dim=1).mean(dim=1)
+    def pref_full(self, m, content, views, seed):
+        from . import smore_fuse as SF
+
+        return SF.preference(m, content, *views, seed)
+
+    def loss_rows(self, m, all_c, side_c, content_c, trip, ar, B):
+        from . import smore_fuse as SF
+
+        total, parts = SF.smore_loss_rows(all_c, side_c, content_c, trip, ar, B, m.reg_weight, m.batch_size,
+                                          m.cl_loss, m.cl_temp)
+        return total
+
+
+class _Pair:
+    """(A, A^T) device CSRs: the forward product and its transpose for the backward."""
+
+    def __init__(self, A, AT):
+        self.A, self.AT = A, AT
 
 
 # ---------------------------------------------------------------------------
-# the sharded model
+# the sharded computation
 # ---------------------------------------------------------------------------
-class ShardedSMORE(nn.Module):
-    """SMORE over the process group; parameters named as the reference's, the
-    row-sharded ones holding this rank's rows (see the module docstring)."""
+class SmoreShard:
+    """The users-sharded SMORE step and evaluation over a parameter holder `m` that has
+    the reference's module layout (rsx.smore.SMORE in sharded mode, or a test container):
+    m.user_embedding.weight holds this rank's user rows, the rest the full tables."""
 
-    def __init__(self, params: dict, graphs: dict, n_users: int, n_items: int, cfg: dict, backend, group=None):
-        super().__init__()
-        self.group = group
-        self.world, self.rank = dist.get_world_size(group), dist.get_rank(group)
-        self.be = backend
+    def __init__(self, graphs: dict, n_users: int, n_items: int, n_ui_layers: int, n_layers: int, backend,
+                 comm: Comm):
+        self.be, self.comm = backend, comm
+        self.world, self.rank = comm.world, comm.rank
         self.n_users, self.n_items = int(n_users), int(n_items)
-        self.urng, self.irng = ranges(self.n_users, self.world), ranges(self.n_items, self.world)
-        (ua, ub), (ia, ib) = self.urng[self.rank], self.irng[self.rank]
-        self.own_u, self.own_i = (ua, ub), (ia, ib)
-        self.reg_weight = float(cfg.get("reg_weight", 1e-5))
-        self.cl_loss = float(cfg.get("cl_loss", 0.01))
-        self.cl_temp = float(cfg.get("cl_temp", 0.2))
-        self.batch_size = float(cfg.get("batch_size", 2048))
-        self.n_ui_layers = int(cfg.get("n_ui_layers", 4))
-        self.n_layers = int(cfg.get("n_layers", 1))
-        self.inject_scale = float(cfg.get("inject_scale", 0.7))
-        d = params["user_embedding.weight"].shape[1]
-        dev = getattr(backend, "device", torch.device("cpu"))
-        mods = {}
-        for name, full in params.items():  # nn containers in the reference's layout
-            full = torch.as_tensor(full, dtype=torch.float32)
-            part = SHARDED.get(name)
-            if part == "u":
-                full = full[ua:ub]
-            elif part == "i":
-                full = full[ia:ib]
-            mods[name] = nn.Parameter(full.clone().to(dev))
-        self.user_embedding = nn.Module()
-        self.item_id_embedding = nn.Module()
-        self.image_embedding = nn.Module()
-        self.text_embedding = nn.Module()
-        lin = lambda i, o, b=True: nn.Linear(i, o, bias=b, device=dev)  # noqa: E731
-        dv, dt = params["image_trs.weight"].shape[1], params["text_trs.weight"].shape[1]
-        self.image_trs, self.text_trs = lin(dv, d), lin(dt, d)
-        self.query_v = nn.Sequential(lin(d, d), nn.Tanh(), lin(d, d, False))
-        self.query_t = nn.Sequential(lin(d, d), nn.Tanh(), lin(d, d, False))
-        for g in ("gate_v", "gate_t", "gate_f", "gate_image_prefer", "gate_text_prefer", "gate_fusion_prefer"):
-            setattr(self, g, nn.Sequential(lin(d, d), nn.Sigmoid()))
-        self.dropout = nn.Dropout(p=float(cfg.get("dropout_rate", 0.0)))
-        for name, p in mods.items():  # the given values replace the fresh modules' parameters
-            obj = self
-            *path, leaf = name.split(".")
-            for k in path:
-                obj = obj[int(k)] if k.isdigit() else getattr(obj, k)
-            obj._parameters.pop(leaf, None)
-            obj.register_parameter(leaf, p)
-        self._seed = torch.tensor([int(cfg.get("seed", 999)) * 1000003 + 17 + self.rank], dtype=torch.int64,
-                                  device=dev)
-        # this rank's rows of every operator: UI adjacency (own users, then own items; all
-        # N columns), each kNN graph (own items; item columns), R (own users; item columns)
+        self.urng = ranges(self.n_users, self.world)
+        a, b = self.urng[self.rank]
+        self.own_u = (a, b)
+        self.nu_own = b - a
+        self.K, self.L = int(n_ui_layers), int(n_layers)
         nu, ni = self.n_users, self.n_items
         rp, col, val = graphs["norm_adj"]
-        ui = stack_csr(csr_rows(rp, col, val, ua, ub), csr_rows(rp, col, val, nu + ia, nu + ib))
-        self.A_ui = backend.operator(*ui, nu + ni)
-        self.G = {}
-        for v in ("image", "text", "fusion"):
-            grp, gcol, gval = graphs[v]
-            self.G[v] = backend.operator(*csr_rows(grp, gcol, gval, ia, ib), ni)
+        # A_U: own user rows, item columns rebased to 0..ni; A_I: item rows, own-user columns rebased to 0..nu_own
+        up, uc, uv = csr_rows(rp, col, val, a, b)
+        self.A_U = backend.operator(up, uc.astype(np.int64) - nu, uv, ni)
+        ip, ic, iv = csr_rows(rp, col, val, nu, nu + ni)
+        rows = np.repeat(np.arange(ni, dtype=np.int64), np.diff(ip))
+        keep = (ic >= a) & (ic < b)
+        self.A_I = backend.operator(*graph.to_csr(rows[keep], ic[keep].astype(np.int64) - a, iv[keep], ni,
+                                                  self.nu_own), self.nu_own)
+        # the kNN item graphs (replicated): prebuilt (A, A^T) pairs or host CSRs
+        self.G = tuple(graphs[v] if hasattr(graphs[v], "AT") else backend.operator(*graphs[v], ni, transpose=True)
+                       for v in ("image", "text", "fusion"))
         rrp, rcol, rval = graphs["R"]
-        self.R = backend.operator(*csr_rows(rrp, rcol, rval, ua, ub), ni)
+        self.R = backend.operator(*csr_rows(rrp, rcol, rval, a, b), ni, transpose=True)
+        self._rows_cache = {}
 
-    # -- gathers ----------------------------------------------------------------
-    def _users(self, x):
-        return gather(x, self.urng, self.group)
+    # -- pieces -----------------------------------------------------------------
+    def ui_mean(self, x):
+        return self.be.ui_mean(self, x)
 
-    def _items(self, x):
-        return gather(x, self.irng, self.group)
+    def _item_side(self, m):
+        cv, ct, cf = self.be.spectral(m)
+        return self.be.gates(m, cv, ct, cf, m.item_id_embedding.weight)
 
-    def _table(self, x):
-        """[own users; own items] -> the full [users; items] table."""
-        nu_own = self.own_u[1] - self.own_u[0]
-        return torch.cat([self._users(x[:nu_own]), self._items(x[nu_own:])])
+    def _content_views(self, m):
+        img, txt, fus = self._item_side(m)
+        ego = torch.cat([m.user_embedding.weight, m.item_id_embedding.weight])
+        content = _UIProp.apply(ego, self)
+        return content, self.be.views(self, (img, txt, fus))
 
-    # -- forward ----------------------------------------------------------------
-    def forward_local(self):
-        """(all_embeds, side, content) of this rank's rows [own users; own items]."""
-        be = self.be
-        cv, ct, cf = be.spectral(self, self.image_embedding.weight, self.text_embedding.weight)
-        item = self.item_id_embedding.weight
-        img, txt, fus = be.gates(self, cv, ct, cf, item)
-        x = torch.cat([self.user_embedding.weight, item])
-        layers = [x]
-        for _ in range(self.n_ui_layers):
-            x = be.spmm(self.A_ui, self._table(x))
-            layers.append(x)
-        content = be.mean_layers(layers)
-        views = []
-        for v, xi in (("image", img), ("text", txt), ("fusion", fus)):
-            for _ in range(self.n_layers):
-                xi = be.spmm(self.G[v], self._items(xi))
-            views.append(torch.cat([be.spmm(self.R, self._items(xi)), xi]))
-        all_e, side = be.preference(self, content, *views)
-        return all_e, side, content
+    def pref_weights(self, m):
+        """The preference block's weights and biases, their gradients summed over the ranks."""
+        lin = [m.get_submodule(n) for n in PREF]
+        ws = [x.weight for x in lin] + [x.bias for x in lin if x.bias is not None]
+        out = allreduce_grad(self.comm, *ws)
+        w, b = list(out[:7]), iter(out[7:])
+        return w + [next(b) if x.bias is not None else None for x in lin]
 
-    def calculate_loss(self, interaction):
-        """1/W of the reference loss of the whole batch (every rank holds the same batch)."""
-        all_e, side, content = self.forward_local()
-        return self.be.loss(self, self._table(all_e), self._table(side), self._table(content),
-                            interaction) / self.world
+    def _rows(self, B, device):
+        c = self._rows_cache.get(B)
+        if c is None:
+            ar = torch.arange(B, dtype=torch.int64, device=device)
+            off = torch.cat([torch.zeros(B, dtype=torch.int64, device=device),
+                             torch.full((2 * B,), self.nu_own, dtype=torch.int64, device=device)])
+            c = self._rows_cache[B] = (ar, torch.stack([ar, ar, ar + B]).contiguous(), off)
+        return c
 
-    def replicated_parameters(self):
-        return [p for n, p in self.named_parameters() if n not in SHARDED]
+    # -- training ---------------------------------------------------------------
+    def loss(self, m, inter, seed):
+        """The reference loss of this rank's batch `inter` [3, B] (users as local row ids
+        0..nu_own-1, items global): BPR + reg + cl * (InfoNCE(items) + InfoNCE(users)) on
+        the batch rows, with the collectives above in its backward."""
+        B = int(inter.shape[1])
+        ar, trip, off = self._rows(B, inter.device)
+        rows = inter[:3].reshape(-1) + off
+        content, views = self._content_views(m)
+        all_c, side_c, content_c = self.be.pref_rows(m, content, views, rows, seed, self.pref_weights(m))
+        return self.be.loss_rows(m, all_c, side_c, content_c, trip, ar, B)
+
+    # -- evaluation ---------------------------------------------------------------
+    @torch.no_grad()
+    def tables(self, m, seed):
+        """all_embeds rows [own users; all items] (evaluation forward, no dropout)."""
+        content, views = self._content_views(m)
+        all_e, _ = self.be.pref_full(m, content, views, seed)
+        return all_e
 
     @torch.no_grad()
-    def sync_grads(self):
-        """Sum the replicated weights' gradients over the ranks (each rank's covers its rows)."""
-        for p in self.replicated_parameters():
-            if p.grad is None:
-                continue
-            h = _host_if_gloo(p.grad, self.group).clone()
-            dist.all_reduce(h, group=self.group)
-            p.grad.copy_(h.to(p.grad.device))
+    def full_sort_topk_local(self, m, seed, eval_users, k, mask_rowptr, mask_col):
+        """(positions in eval_users of this rank's users, their top-k item ids)."""
+        a, b = self.own_u
+        pos = torch.nonzero((eval_users >= a) & (eval_users < b)).flatten()
+        local = (eval_users.index_select(0, pos) - a).contiguous()
+        f = self.tables(m, seed)
+        nl = self.nu_own
+        _, topk = ops.fullsort_topk(f[:nl].contiguous(), local, f[nl:].contiguous(), mask_rowptr[a:], mask_col, k)
+        return pos, topk
 
-    # -- training with the model-level mirror gradient ----------------------------
+    # -- mirror gradient -----------------------------------------------------------
     @torch.no_grad()
-    def mg_alpha(self, params, grads, base, lr, rel_step, max_scale):
-        """alpha_eff of the reference's mirror gradient (src/common/trainer.py:290-307)
-        over the GLOBAL parameter vector: sums of squares of the row-sharded tensors
-        all-reduced, the replicated ones counted once, then the reference's arithmetic
-        (rms values rounded to f32 as its float() of f32 tensors, the rest in f64)."""
+    def mg_alpha(self, m, params, grads, base, lr, rel_step, max_scale, lr_dev=None):
+        """alpha_eff of the reference's mirror gradient (src/common/trainer.py:290-307) over
+        the GLOBAL parameter vector, as a 0-d f64 device tensor (no host sync): sums of
+        squares of the row-sharded user table summed over the ranks (one all-reduce),
+        the replicated parameters counted once."""
+        sharded = {id(m.user_embedding.weight)}
+        sh_g = [g for p, g in zip(params, grads) if id(p) in sharded]
+        sh_p = [p.detach() for p in params if id(p) in sharded]
+        rp_g = [g for p, g in zip(params, grads) if id(p) not in sharded]
+        rp_p = [p.detach() for p in params if id(p) not in sharded]
         dev = params[0].device
-        sh = torch.zeros(3, dtype=torch.float64, device=dev)  # sum g^2, sum p^2, numel (sharded)
-        rep = torch.zeros(3, dtype=torch.float64, device=dev)
-        names = {id(p): n for n, p in self.named_parameters()}
-        for p, g in zip(params, grads):
-            acc = sh if names.get(id(p)) in SHARDED else rep
-            acc[0] += g.double().pow(2).sum()
-            acc[1] += p.detach().double().pow(2).sum()
-            acc[2] += p.numel()
-        h = _host_if_gloo(sh, self.group).clone()
-        dist.all_reduce(h, group=self.group)
-        tot = h.to(dev) + rep
-        n = float(tot[2].item())
-        grad_rms = float(torch.tensor(float(tot[0].sqrt()), dtype=torch.float32) / (n ** 0.5))
-        param_rms = float(torch.tensor(float(tot[1].sqrt()), dtype=torch.float32) / (n ** 0.5) + 1e-12)
-        alpha = max(base, rel_step * param_rms / (lr * grad_rms + 1e-12))
-        return min(alpha, base * max_scale)
 
-    def train_batch(self, inter, opt, lr, step_id, mg_interval=3, mg_alpha=0.5, mg_beta=0.2, rel_step=1e-3,
-                    max_scale=20.0):
-        """One batch of the reference Trainer on a mirror-gradient model (src/common/
-        trainer.py:186-201, 244-336) over the process group: loss, backward, gradient
-        sync, Adam; then, when step_id % mg_interval == 0, the mirror gradient: g(theta)
-        again, theta' = theta - alpha lr g, g(theta') scaled by -beta, theta restored,
-        Adam.  `opt` holds this rank's parameters (Adam is per element, so the sharded
-        rows' update is the single-process update of those rows).  Returns 1/W of the
-        batch loss (a float)."""
-        opt.zero_grad(set_to_none=True)
-        loss = self.calculate_loss(inter)
-        value = float(loss.detach())
-        loss.backward()
-        self.sync_grads()
-        opt.step()
-        if mg_interval > 0 and step_id % mg_interval == 0:
-            opt.zero_grad(set_to_none=True)
-            self.calculate_loss(inter).backward()
-            self.sync_grads()
-            params = [p for p in self.parameters() if p.requires_grad and p.grad is not None]
-            grads = [p.grad.detach().clone() for p in params]
-            alpha = self.mg_alpha(params, grads, mg_alpha, lr, rel_step, max_scale)
-            with torch.no_grad():
-                for p, g in zip(params, grads):
-                    p.add_(-alpha * lr * g)
-            opt.zero_grad(set_to_none=True)
-            self.calculate_loss(inter).backward()
-            self.sync_grads()
-            with torch.no_grad():
-                for p in self.parameters():
-                    if p.requires_grad and p.grad is not None:
-                        p.grad.mul_(-mg_beta)
-                for p, g in zip(params, grads):
-                    p.add_(+alpha * lr * g)
-            opt.step()
-            opt.zero_grad(set_to_none=True)
-        return value
+        def sq(ts):
+            if not ts:
+                return torch.zeros((), dtype=torch.float64, device=dev)
+            return torch.stack([n.double() for n in torch._foreach_norm(ts)]).pow(2).sum()
 
-    @torch.no_grad()
-    def full_sort_topk_local(self, k: int, mask_rowptr, mask_col):
-        """Top-k item ids of this rank's users (global user ids ua..ub-1, in order)."""
-        all_e, _, _ = self.forward_local()
-        nu_own = self.own_u[1] - self.own_u[0]
-        items = self._items(all_e[nu_own:].contiguous())
-        users = torch.arange(nu_own, device=all_e.device)
-        return ops.fullsort_topk(all_e[:nu_own].contiguous(), users, items.contiguous(),
-                                 mask_rowptr[self.own_u[0]:], mask_col, k)[1]
+        part = torch.stack([sq(sh_g), sq(sh_p), torch.tensor(float(sum(p.numel() for p in sh_p)), dtype=torch.float64,
+                                                             device=dev)]).float()
+        self.comm.allreduce_(part)
+        tot = part.double() + torch.stack([sq(rp_g), sq(rp_p), torch.tensor(float(sum(p.numel() for p in rp_p)),
+                                                                               dtype=torch.float64, device=dev)])
+        n = tot[2]
+        grad_rms = (tot[0].sqrt().float() / n.sqrt().float()).double()
+        param_rms = (tot[1].sqrt().float() / n.sqrt().float() + 1e-12).double()
+        lr_t = lr_dev[0] if lr_dev is not None else torch.tensor(float(lr), dtype=torch.float64, device=dev)
+        alpha = rel_step * param_rms / (lr_t * grad_rms + 1e-12)
+        alpha = torch.where(alpha > base, alpha, torch.full_like(alpha, base))
+        return torch.clamp(alpha, max=base * max_scale)
+
+
+def csr_rows(rowptr, col, val, r0: int, r1: int):
+    """Rows [r0, r1) of a host CSR (columns unchanged)."""
+    a, b = int(rowptr[r0]), int(rowptr[r1])
+    return rowptr[r0:r1 + 1] - a, col[a:b], val[a:b]
 
 
 def graphs_from_rsx(model):
-    """Host CSRs of a single-process rsx.smore.SMORE's operators (for ShardedSMORE)."""
+    """Host CSRs of a single-process rsx.smore.SMORE's operators."""
     def host(A):
         return A.rowptr_host, A.col.cpu().numpy(), A.val.cpu().numpy()
 
     return {"norm_adj": host(model.norm_adj_csr), "image": host(model.image_graph.A),
             "text": host(model.text_graph.A), "fusion": host(model.fusion_graph.A), "R": host(model.R.A)}
+
+
+def param_container(params: dict, cfg: dict, user_range, device="cpu"):
+    """An nn.Module with the reference's SMORE parameter layout holding `params` (full
+    tables; the user table cut to `user_range`) — the parameter holder of the CPU
+    tests and of tools that drive SmoreShard without rsx.smore.SMORE."""
+    m = nn.Module()
+    a, b = user_range
+    d = params["user_embedding.weight"].shape[1]
+    lin = lambda i, o, bias=True: nn.Linear(i, o, bias=bias, device=device)  # noqa: E731
+    dv, dt = params["image_trs.weight"].shape[1], params["text_trs.weight"].shape[1]
+    for name in ("user_embedding", "item_id_embedding", "image_embedding", "text_embedding"):
+        setattr(m, name, nn.Module())
+    m.image_trs, m.text_trs = lin(dv, d), lin(dt, d)
+    m.query_v = nn.Sequential(lin(d, d), nn.Tanh(), lin(d, d, False))
+    m.query_t = nn.Sequential(lin(d, d), nn.Tanh(), lin(d, d, False))
+    for g in ("gate_v", "gate_t", "gate_f", "gate_image_prefer", "gate_text_prefer", "gate_fusion_prefer"):
+        setattr(m, g, nn.Sequential(lin(d, d), nn.Sigmoid()))
+    m.dropout = nn.Dropout(p=float(cfg.get("dropout_rate", 0.0)))
+    for name, full in params.items():
+        full = torch.as_tensor(full, dtype=torch.float32)
+        if SHARDED.get(name) == "u":
+            full = full[a:b]
+        obj = m
+        *path, leaf = name.split(".")
+        for k in path:
+            obj = obj[int(k)] if k.isdigit() else getattr(obj, k)
+        obj._parameters.pop(leaf, None)
+        obj.register_parameter(leaf, nn.Parameter(full.clone().to(device)))
+    m.reg_weight = float(cfg.get("reg_weight", 1e-5))
+    m.cl_loss = float(cfg.get("cl_loss", 0.01))
+    m.cl_temp = float(cfg.get("cl_temp", 0.2))
+    m.batch_size = float(cfg.get("batch_size", 2048))
+    m.inject_scale = float(cfg.get("inject_scale", 0.7))
+    m.spectral_weight_norm = True
+    return m

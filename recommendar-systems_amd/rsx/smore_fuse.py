@@ -204,15 +204,18 @@ class _PrefRows(torch.autograd.Function):
         return (gC, gIE, gTE, gFE, None, None, None, *gW, *gb)
 
 
-def preference_rows(model, content, image_embeds, text_embeds, fusion_embeds, rows, seed):
+def preference_rows(model, content, image_embeds, text_embeds, fusion_embeds, rows, seed, weights=None):
     """(all, side, content) rows of the reference's preference block at table rows
-    `rows` only (the training loss reads no other row; the block is row-local)."""
+    `rows` only (the training loss reads no other row; the block is row-local).
+    `weights`: the 7 weights then the 7 biases (None where absent) to use instead of
+    the model's own tensors (the sharded model passes them through a gradient sum)."""
     m = model
-    lin = [m.query_v[0], m.query_v[2], m.query_t[0], m.query_t[2], m.gate_image_prefer[0], m.gate_text_prefer[0],
-           m.gate_fusion_prefer[0]]
+    if weights is None:
+        lin = [m.query_v[0], m.query_v[2], m.query_t[0], m.query_t[2], m.gate_image_prefer[0],
+               m.gate_text_prefer[0], m.gate_fusion_prefer[0]]
+        weights = [x.weight for x in lin] + [x.bias for x in lin]
     p = float(m.dropout.p) if m.training else 0.0
-    return _PrefRows.apply(content, image_embeds, text_embeds, fusion_embeds, rows, p, seed,
-                           *[x.weight for x in lin], *[x.bias for x in lin])
+    return _PrefRows.apply(content, image_embeds, text_embeds, fusion_embeds, rows, p, seed, *weights)
 
 
 # ---------------------------------------------------------------------------
@@ -261,7 +264,7 @@ class _ViewProp3(torch.autograd.Function):
     the three R^T and item-graph transposes, each set as ONE rsx_spmm_batch launch."""
 
     @staticmethod
-    def forward(ctx, x0, x1, x2, Gs, R, n_layers, n_users):
+    def forward(ctx, x0, x1, x2, Gs, R, n_layers, n_users, comm):
         xs = [_c(x) for x in (x0, x1, x2)]
         ni, d = xs[0].shape
         outs = [torch.empty(n_users + ni, d, dtype=torch.float32, device=xs[0].device) for _ in range(3)]
@@ -275,7 +278,7 @@ class _ViewProp3(torch.autograd.Function):
                 o[n_users:].copy_(x)
         ops.spmm_batch([R.A] * 3, [o[n_users:] for o in outs], [ops.epi(L.RSX_EPI_STORE, y=o[:n_users]) for o in outs],
                        d)
-        ctx.Gs, ctx.R, ctx.L, ctx.nu = Gs, R, n_layers, n_users
+        ctx.Gs, ctx.R, ctx.L, ctx.nu, ctx.comm = Gs, R, n_layers, n_users, comm
         return tuple(outs)
 
     @staticmethod
@@ -284,21 +287,26 @@ class _ViewProp3(torch.autograd.Function):
         ref = next(g for g in grads if g is not None)
         gs = [_c(g) if g is not None else torch.zeros_like(ref) for g in grads]
         d = ref.shape[1]
-        gi = [torch.empty_like(g[nu:]) for g in gs]
+        gbuf = torch.empty(3, ref.shape[0] - nu, d, dtype=torch.float32, device=ref.device)
+        gi = list(gbuf.unbind(0))
         # d items = g_items + R^T g_users (ADD epilogue), the three views in one launch
         ops.spmm_batch([ctx.R.AT] * 3, [g[:nu] for g in gs],
                        [ops.epi(L.RSX_EPI_ADD, y=y, r_add=g[nu:]) for y, g in zip(gi, gs)], d)
+        if ctx.comm is not None:  # users sharded (rsx.smore_dist): the item rows' gradient summed over the ranks
+            ctx.comm.allreduce_(gbuf)
         for _ in range(ctx.L):
             nxt = [torch.empty_like(x) for x in gi]
             ops.spmm_batch([G.AT for G in ctx.Gs], gi, [ops.epi(L.RSX_EPI_STORE, y=y) for y in nxt], d)
             gi = nxt
-        return gi[0], gi[1], gi[2], None, None, None, None
+        return gi[0], gi[1], gi[2], None, None, None, None, None
 
 
-def view_prop3(xs, Gs, R, n_layers, n_users):
+def view_prop3(xs, Gs, R, n_layers, n_users, comm=None):
     """(image, text, fusion) [R G^L x; G^L x] tables of the three views (one launch per
-    layer for all three graphs, one for the three R products)."""
-    return _ViewProp3.apply(xs[0], xs[1], xs[2], tuple(Gs), R, int(n_layers), int(n_users))
+    layer for all three graphs, one for the three R products).  With `comm` (R = this
+    rank's user rows) the item rows' gradients are summed over the ranks in one
+    all-reduce before the item-graph backward."""
+    return _ViewProp3.apply(xs[0], xs[1], xs[2], tuple(Gs), R, int(n_layers), int(n_users), comm)
 
 
 # ---------------------------------------------------------------------------

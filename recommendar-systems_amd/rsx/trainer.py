@@ -324,6 +324,9 @@ class Trainer:
         if gate:
             self._arm_nan_gate()
         self.reset_graph_step()
+        sharded = bool(getattr(self.model, "sharded", False)) and hasattr(self.model, "local_batches")
+        if sharded:  # users sharded over the ranks: this rank's own device-sampled batches
+            train_data = self.model.local_batches(epoch_idx)
         for batch_idx, interaction in enumerate(train_data):
             losses, loss = self.train_step(interaction, batch_idx, loss_func)
             parts.append(torch.stack(list(losses)) if isinstance(losses, tuple) else loss)
@@ -339,7 +342,19 @@ class Trainer:
                 return loss_batches[b], torch.tensor(0.0)
         if not parts:
             return 0.0, loss_batches
-        host = torch.stack(parts).double().cpu().numpy()  # one sync per epoch
+        host = torch.stack(parts).double()
+        if sharded:  # the epoch loss of the job: every rank's batches
+            import torch.distributed as dist
+
+            host = host.float().contiguous()
+            if dist.get_backend() == "nccl":
+                dist.all_reduce(host)
+            else:
+                h = host.cpu()
+                dist.all_reduce(h)
+                host = h
+            host = host.double()
+        host = host.cpu().numpy()  # one sync per epoch
         if np.isnan(host).any():
             self.logger.info(f"Loss is nan at epoch: {epoch_idx}. Exiting.")
             return torch.tensor(float("nan")), torch.tensor(0.0)
@@ -407,7 +422,8 @@ class Trainer:
         if getattr(self, "_gate", False):
             from .smore_fuse import nan_gate
 
-            nan_gate(loss, self._halt, self._nan_ctr)
+            gl = self.model.gate_loss(loss) if hasattr(self.model, "gate_loss") else loss
+            nan_gate(gl, self._halt, self._nan_ctr)
         if not getattr(self.model, "mg_enable", False):
             if self.mg and batch_idx % self.beta == 0:
                 (self.alpha1 * loss).backward()
@@ -478,7 +494,12 @@ class Trainer:
                 from .smore_fuse import axpy_multi, mg_alpha
 
                 lr_dev = getattr(self, "_lr_dev", None)  # graph-step runs: lr read on the device
-                alpha = mg_alpha(params, grads, base, lr, self.mg_target_rel_step, self.mg_alpha_max_scale, lr_dev)
+                if getattr(m, "sharded", False) and hasattr(m, "mg_alpha_global"):  # over the global vector
+                    alpha = m.mg_alpha_global(params, grads, base, lr, self.mg_target_rel_step,
+                                              self.mg_alpha_max_scale, lr_dev)
+                else:
+                    alpha = mg_alpha(params, grads, base, lr, self.mg_target_rel_step, self.mg_alpha_max_scale,
+                                     lr_dev)
                 m._alpha_eff = alpha
                 halt = self._halt if getattr(self, "_gate", False) else None
                 axpy_multi(params, grads, alpha, -1.0 if lr_dev is not None else -lr, lr_dev, halt)  # theta - alpha lr g

@@ -181,7 +181,7 @@ def test_prop_mean_rows_vs_dense(cuda, K, d):
     tags = _RowTags(nu + ni, cuda)
     tags.mark(torch.arange(nu + ni, device=cuda)[:7])  # stale tags of an earlier batch
     tags.mark(rows)
-    out_t = _PropMeanRows.apply(x, A, K, tags)
+    out_t = _PropMeanRows.apply(x, A, K, tags, rows)
     out_d = _PropMean.apply(x, A, K)
     assert torch.equal(out_t[rows], out_d[rows])
     g = torch.zeros(nu + ni, d, device=cuda)
@@ -211,6 +211,25 @@ def test_smore_one_epoch_with_mirror_gradient(tmp_path, golden, fx):
         ref = metric_dict(z, tag)
         for k in ref:
             assert abs(res[k] - ref[k]) <= 1e-4 + 1e-12, (tag, k, res[k], ref[k])
+
+
+def test_smore_two_losses_before_one_backward(tmp_path, golden):
+    """calculate_loss twice (two batches) and ONE backward of their sum = the two
+    backwards one at a time: the batch-row propagation re-tags its forward's rows in its
+    backward, so a later forward's tags cannot hide the earlier batch's rows."""
+    z, c, train, valid, test = _setup(tmp_path, golden)
+    m = _model(c, train)
+    m.train()
+    t = torch.from_numpy(z["epoch0_triplets"][:, :1024].astype(np.int64)).cuda()
+    b1, b2 = t[:, :512].contiguous(), t[:, 512:].contiguous()
+    (m.calculate_loss(b1) + m.calculate_loss(b2)).backward()
+    joint = {n: p.grad.clone() for n, p in m.named_parameters()}
+    m.zero_grad(set_to_none=True)
+    m.calculate_loss(b1).backward()
+    m.calculate_loss(b2).backward()
+    for n, p in m.named_parameters():
+        scale = max(p.grad.abs().max().item(), 1e-12)
+        assert (p.grad - joint[n]).abs().max().item() <= 1e-5 * scale, n
 
 
 @pytest.mark.parametrize("graph", [True, False])

@@ -1,12 +1,17 @@
-"""SMORE sharded over 2 and 4 CPU ranks (rsx.smore_dist, gloo) against the single-process
-objective: the oracle's SMORE restatement (oracle/rsx_oracle.py:SMORECPU, pinned to the
-reference's own forward / loss by tests/test_oracle_smore.py) on the golden fixture's
-data and initial weights.  The HIP kernels cannot run here, so the sharded model's
-compute backend is a torch restatement of the same ops; what is under test is the
-partition (user / item row ranges, local operator row blocks), the differentiable
-gathers and the replicated-gradient sum.  One batch: the loss equals the
-single-process loss, every parameter's gradient (the sharded rows gathered) equals
-the single-process gradient, and one Adam step gives the same parameters."""
+"""SMORE with users sharded over 2 and 4 CPU ranks and the item side replicated
+(rsx.smore_dist, gloo) against the single-process objective: the oracle's SMORE
+restatement (oracle/rsx_oracle.py:SMORECPU, pinned to the reference's own forward /
+loss by tests/test_oracle_smore.py) on the golden fixture's data and initial weights.
+
+Each rank trains on its own batch of its own users' interactions, so the objective is
+the sum over ranks of the reference loss of each rank's batch (data-parallel batches).
+The HIP kernels cannot run here, so the sharded model's compute backend is a torch
+restatement of the same ops; what is under test is the partition (user row blocks of
+the UI graph and of R, the replicated item side), the collective schedule (one
+all-reduce of the item partial per UI layer, the views' item-row gradients summed in
+one all-reduce, the preference weights' gradients summed) and that the replicas stay
+identical.  One batch: losses, every gradient and one Adam step; and two batches with
+the model-level mirror gradient (global alpha over the sharded parameter vector)."""
 import os
 import socket
 import tempfile
@@ -23,21 +28,39 @@ import rsx_oracle as O
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
+def _sp(rowptr, col, val, n_cols):
+    rows = np.repeat(np.arange(rowptr.size - 1), np.diff(rowptr))
+    return torch.sparse_coo_tensor(torch.from_numpy(np.vstack([rows, col.astype(np.int64)])),
+                                   torch.from_numpy(val.astype(np.float32)), (rowptr.size - 1, n_cols)).coalesce()
+
+
+class _Pair:
+    def __init__(self, A):
+        self.A, self.AT = A, A.t().coalesce()
+
+
 class TorchSmoreBackend:
     """torch restatement of the ops rsx.smore_dist.HipSmoreBackend runs (reference
-    src/models/smore.py:209-411)."""
+    src/models/smore.py:209-411), with the same collectives."""
 
-    def operator(self, rowptr, col, val, n_cols):
-        rows = np.repeat(np.arange(rowptr.size - 1), np.diff(rowptr))
-        return torch.sparse_coo_tensor(torch.from_numpy(np.vstack([rows, col.astype(np.int64)])),
-                                       torch.from_numpy(val.astype(np.float32)),
-                                       (rowptr.size - 1, n_cols)).coalesce()
+    def operator(self, rowptr, col, val, n_cols, transpose=False):
+        A = _sp(rowptr, col, val, n_cols)
+        return _Pair(A) if transpose else A
 
-    def spmm(self, op, x):
-        return torch.sparse.mm(op, x)
+    def ui_mean(self, core, x):
+        nu, K = core.nu_own, core.K
+        s, cur = x.clone(), x
+        for _ in range(K):
+            u = torch.sparse.mm(core.A_U, cur[nu:])
+            i = torch.sparse.mm(core.A_I, cur[:nu]).contiguous()
+            core.comm.allreduce_(i)
+            cur = torch.cat([u, i])
+            s = s + cur
+        return s / (K + 1)
 
-    def spectral(self, m, V, T):
-        img, txt = F.linear(V, m.image_trs.weight, m.image_trs.bias), F.linear(T, m.text_trs.weight, m.text_trs.bias)
+    def spectral(self, m):
+        img = F.linear(m.image_embedding.weight, m.image_trs.weight, m.image_trs.bias)
+        txt = F.linear(m.text_embedding.weight, m.text_trs.weight, m.text_trs.bias)
         fi, ft = torch.fft.rfft(img, dim=1, norm="ortho"), torch.fft.rfft(txt, dim=1, norm="ortho")
 
         def unit(w):
@@ -53,28 +76,46 @@ class TorchSmoreBackend:
         return (item + m.inject_scale * m.gate_v(cv), item + m.inject_scale * m.gate_t(ct),
                 item + m.inject_scale * m.gate_f(cf))
 
-    def preference(self, m, C, IE, TE, FE):
-        agg_img = torch.softmax(m.query_v(FE), dim=-1) * IE
-        agg_txt = torch.softmax(m.query_t(FE), dim=-1) * TE
-        ip, tp, fp = (m.dropout(m.gate_image_prefer(C)), m.dropout(m.gate_text_prefer(C)),
-                      m.dropout(m.gate_fusion_prefer(C)))
+    def views(self, core, xs):
+        from rsx.smore_dist import allreduce_grad
+
+        outs = []
+        for x, G in zip(xs, core.G):
+            for _ in range(core.L):
+                x = torch.sparse.mm(G.A, x)
+            outs.append(x)
+        outs = allreduce_grad(core.comm, *outs)
+        return tuple(torch.cat([torch.sparse.mm(core.R.A, x), x]) for x in outs)
+
+    @staticmethod
+    def _pref(C, IE, TE, FE, w):
+        (qv0, qv2, qt0, qt2, gi, gt, gf), (bqv0, _, bqt0, _, bgi, bgt, bgf) = w[:7], w[7:]
+        agg_img = torch.softmax(F.linear(torch.tanh(F.linear(FE, qv0, bqv0)), qv2), dim=-1) * IE
+        agg_txt = torch.softmax(F.linear(torch.tanh(F.linear(FE, qt0, bqt0)), qt2), dim=-1) * TE
+        ip, tp, fp = (torch.sigmoid(F.linear(C, gi, bgi)), torch.sigmoid(F.linear(C, gt, bgt)),
+                      torch.sigmoid(F.linear(C, gf, bgf)))
         side = torch.mean(torch.stack([ip * agg_img, tp * agg_txt, fp * FE]), dim=0)
         return C + side, side
 
-    def loss(self, m, all_e, side, content, inter):
-        nu = m.n_users
-        users, pos, neg = inter[0], inter[1], inter[2]
-        ua, ia = all_e[:nu], all_e[nu:]
-        u, p, n = ua[users], ia[pos], ia[neg]
+    def pref_rows(self, m, content, views, rows, seed, weights):
+        C = content[rows]
+        a, s = self._pref(C, *(v[rows] for v in views), weights)
+        return a, s, C
+
+    def pref_full(self, m, content, views, seed):
+        from rsx.smore_dist import PREF
+
+        lin = [m.get_submodule(n) for n in PREF]
+        return self._pref(content, *views, [x.weight for x in lin] + [x.bias for x in lin])
+
+    def loss_rows(self, m, all_c, side_c, content_c, trip, ar, B):
+        u, p, n = all_c[:B], all_c[B:2 * B], all_c[2 * B:]
         ps, ns = (u * p).sum(dim=1), (u * n).sum(dim=1)
         reg = (0.5 * (u ** 2).sum() + 0.5 * (p ** 2).sum() + 0.5 * (n ** 2).sum()) / m.batch_size
         mf = -torch.mean(F.logsigmoid(ps - ns))
-        su, si, cu, ci = side[:nu], side[nu:], content[:nu], content[nu:]
-        cl = O.SMORECPU.info_nce(si[pos], ci[pos], m.cl_temp) + O.SMORECPU.info_nce(su[users], cu[users], m.cl_temp)
-        return mf + m.reg_weight * reg + 0.0 + m.cl_loss * cl
-
-    def mean_layers(self, layers):
-        return torch.stack(layers, dim=1).mean(dim=1)
+        cl = (O.SMORECPU.info_nce(side_c[B:2 * B], content_c[B:2 * B], m.cl_temp)
+              + O.SMORECPU.info_nce(side_c[:B], content_c[:B], m.cl_temp))
+        return mf + m.reg_weight * reg + m.cl_loss * cl
 
 
 def _csr(sp):
@@ -94,27 +135,48 @@ def reference_setup():
                    dropout=0.0, batch_size=2048, init=init)
     graphs = {"norm_adj": _csr(m.norm_adj), "R": _csr(m.R), "image": _csr(m.image_original_adj),
               "text": _csr(m.text_original_adj), "fusion": _csr(m.fusion_adj)}
-    batch = torch.from_numpy(z["epoch0_triplets"][:, :300].astype(np.int64))
-    return m, init, graphs, batch, nu, ni
+    return m, init, graphs, z, nu, ni
 
 
-def _worker(rank, world, port, out):
+def rank_batches(z, nu, world, per=120):
+    """Each rank's batch: the first `per` fixture triplets whose user is in its block
+    (global ids)."""
+    from rsx.smore_dist import ranges
+
+    t = z["epoch0_triplets"].astype(np.int64)
+    out = []
+    for a, b in ranges(nu, world):
+        sel = np.nonzero((t[0] >= a) & (t[0] < b))[0][:per]
+        out.append(torch.from_numpy(t[:, sel].copy()))
+    return out
+
+
+CFG = dict(reg_weight=1e-5, batch_size=2048, cl_loss=0.01, cl_temp=0.2, dropout_rate=0.0)
+
+
+def _setup_rank(rank, world, port):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.set_num_threads(1)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from rsx.smore_dist import ShardedSMORE
+    from rsx.smore_dist import Comm, SmoreShard, param_container
 
-    _, init, graphs, batch, nu, ni = reference_setup()
-    sm = ShardedSMORE(init, graphs, nu, ni, dict(reg_weight=1e-5, batch_size=2048, n_ui_layers=4, n_layers=1),
-                      TorchSmoreBackend())
-    loss = sm.calculate_loss(batch)
+    _, init, graphs, z, nu, ni = reference_setup()
+    core = SmoreShard(graphs, nu, ni, 4, 1, TorchSmoreBackend(), Comm())
+    m = param_container(init, CFG, core.own_u)
+    inter = rank_batches(z, nu, world)[rank].clone()
+    inter[0] -= core.own_u[0]  # local user rows
+    return core, m, inter
+
+
+def _worker(rank, world, port, out):
+    core, m, inter = _setup_rank(rank, world, port)
+    loss = core.loss(m, inter, None)
     loss.backward()
-    sm.sync_grads()
-    grads = {n: p.grad.clone().numpy() for n, p in sm.named_parameters()}
-    opt = torch.optim.Adam(sm.parameters(), lr=1e-3)
+    grads = {n: p.grad.clone().numpy() for n, p in m.named_parameters()}
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3)
     opt.step()
-    params = {n: p.detach().clone().numpy() for n, p in sm.named_parameters()}
-    np.savez(os.path.join(out, f"r{rank}.npz"), loss=loss.detach().numpy(), own=np.array([*sm.own_u, *sm.own_i]),
+    params = {n: p.detach().clone().numpy() for n, p in m.named_parameters()}
+    np.savez(os.path.join(out, f"r{rank}.npz"), loss=loss.detach().numpy(), own=np.array(core.own_u),
              **{"g." + k: v for k, v in grads.items()}, **{"p." + k: v for k, v in params.items()})
     dist.destroy_process_group()
 
@@ -140,14 +202,14 @@ def test_sharded_smore_step_matches_single_process(world):
     with tempfile.TemporaryDirectory() as d:
         mp.spawn(_worker, args=(world, _free_port(), d), nprocs=world, join=True)
         res = [dict(np.load(os.path.join(d, f"r{r}.npz"))) for r in range(world)]
-    m, _, _, batch, nu, ni = reference_setup()
-    loss = m.calculate_loss(batch)
+    m, _, _, z, nu, ni = reference_setup()
+    batches = rank_batches(z, nu, world)
+    loss = sum(m.calculate_loss(b) for b in batches)
     loss.backward()
     ref_g = {n: p.grad.clone().numpy() for n, p in m.named_parameters()}
     opt = torch.optim.Adam(m.parameters(), lr=1e-3)
     opt.step()
     ref_p = {n: p.detach().clone().numpy() for n, p in m.named_parameters()}
-    # every rank's loss is 1/W of the single-process loss
     assert abs(sum(float(x["loss"]) for x in res) - loss.item()) <= 1e-5 * abs(loss.item())
     for name in ref_g:
         if name in SHARDED:
@@ -156,42 +218,91 @@ def test_sharded_smore_step_matches_single_process(world):
         else:
             g, p = res[0]["g." + name], res[0]["p." + name]
             for x in res[1:]:  # replicas stay identical
+                assert np.array_equal(x["g." + name], g), name
                 assert np.array_equal(x["p." + name], p), name
         _close(g, ref_g[name], "grad " + name)
-        np.testing.assert_allclose(p, ref_p[name], rtol=0, atol=2e-6, err_msg=name)
+        # Adam's first update is -lr g/(|g|+eps): a gradient rounding difference delta (here
+        # 2e-5 of the tensor's scale: f32 sums in another order) moves it by at most
+        # lr |s(g + delta) - s(g)|, s(x) = x / (|x| + eps) -- large only where g ~ 0
+        gr = ref_g[name]
+        delta = 2e-5 * np.abs(gr).max() + 1e-30
+        sfn = lambda x: x / (np.abs(x) + 1e-8)  # noqa: E731
+        bound = 1e-3 * np.maximum(np.abs(sfn(gr + delta) - sfn(gr)), np.abs(sfn(gr - delta) - sfn(gr))) + 2e-7
+        assert np.all(np.abs(p - ref_p[name]) <= bound), (name, np.abs(p - ref_p[name]).max())
+
+
+def _shard_train_batch(core, m, inter, opt, lr, step_id, mg_interval, base=0.5, beta=0.2):
+    """rsx.trainer.Trainer._train_batch + _mirror_gradient on the sharded model
+    (reference src/common/trainer.py:186-201, 244-336): loss, backward, Adam, then the
+    mirror gradient with alpha over the global parameter vector (SmoreShard.mg_alpha)."""
+    opt.zero_grad(set_to_none=True)
+    loss = core.loss(m, inter, None)
+    value = float(loss.detach())
+    loss.backward()
+    opt.step()
+    if step_id % mg_interval == 0:
+        opt.zero_grad(set_to_none=True)
+        core.loss(m, inter, None).backward()
+        params = [p for p in m.parameters() if p.grad is not None]
+        grads = [p.grad.detach().clone() for p in params]
+        alpha = float(core.mg_alpha(m, params, grads, base, lr, 1e-3, 20.0))
+        with torch.no_grad():
+            for p, g in zip(params, grads):
+                p.add_(-alpha * lr * g)
+        opt.zero_grad(set_to_none=True)
+        core.loss(m, inter, None).backward()
+        with torch.no_grad():
+            for p in m.parameters():
+                if p.grad is not None:
+                    p.grad.mul_(-beta)
+            for p, g in zip(params, grads):
+                p.add_(alpha * lr * g)
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+    return value
 
 
 def _mg_worker(rank, world, port, out, steps):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    torch.set_num_threads(1)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    from rsx.smore_dist import ShardedSMORE
-
-    _, init, graphs, batch, nu, ni = reference_setup()
-    sm = ShardedSMORE(init, graphs, nu, ni, dict(reg_weight=1e-5, batch_size=2048, n_ui_layers=4, n_layers=1),
-                      TorchSmoreBackend())
-    opt = torch.optim.Adam(sm.parameters(), lr=1e-3)
-    losses = [sm.train_batch(batch, opt, 1e-3, step + 1, mg_interval=1) for step in range(steps)]
-    params = {n: p.detach().clone().numpy() for n, p in sm.named_parameters()}
+    core, m, inter = _setup_rank(rank, world, port)
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+    losses = [_shard_train_batch(core, m, inter, opt, 1e-3, s + 1, 1) for s in range(steps)]
+    params = {n: p.detach().clone().numpy() for n, p in m.named_parameters()}
     np.savez(os.path.join(out, f"r{rank}.npz"), loss=np.array(losses), **{"p." + k: v for k, v in params.items()})
     dist.destroy_process_group()
+
+
+class _SumOfBatches:
+    """The single-process objective sum_g L(batch_g) as one 'model' for the oracle's
+    Trainer batch (smore_train_batch): global_step advances once per call."""
+
+    def __init__(self, m):
+        self.m, self.global_step, self.mg_interval = m, 0, 1
+        self.mg_alpha, self.mg_beta = m.mg_alpha, m.mg_beta
+
+    def calculate_loss(self, batches):
+        self.global_step += 1
+        return sum(self.m.calculate_loss(b) for b in batches)
+
+    def parameters(self):
+        return self.m.parameters()
 
 
 @pytest.mark.parametrize("world", [2, 4])
 def test_sharded_smore_mirror_gradient_matches_single_process(world):
     """Two batches with the model-level mirror gradient firing on each (mg_interval 1):
-    the sharded model's loss and every parameter (rows concatenated over the ranks)
-    against the oracle's single-process Trainer batch (smore_train_batch)."""
+    the ranks' losses and every parameter (user rows concatenated over the ranks)
+    against the oracle's single-process Trainer batch on the sum of the rank batches."""
     from rsx.smore_dist import SHARDED
 
     steps = 2
     with tempfile.TemporaryDirectory() as d:
         mp.spawn(_mg_worker, args=(world, _free_port(), d, steps), nprocs=world, join=True)
         res = [dict(np.load(os.path.join(d, f"r{r}.npz"))) for r in range(world)]
-    m, _, _, batch, nu, ni = reference_setup()
-    m.mg_interval = 1
+    m, _, _, z, nu, ni = reference_setup()
+    batches = rank_batches(z, nu, world)
+    s = _SumOfBatches(m)
     opt = torch.optim.Adam(m.parameters(), lr=1e-3)
-    ref_losses = [O.smore_train_batch(m, opt, batch, 1e-3) for _ in range(steps)]
+    ref_losses = [O.smore_train_batch(s, opt, batches, 1e-3) for _ in range(steps)]
     np.testing.assert_allclose(sum(x["loss"] for x in res), ref_losses, rtol=1e-5)
     for name, p in m.named_parameters():
         want = p.detach().numpy()
