@@ -166,9 +166,9 @@ def bench_model(args):
     if world > 1:
         import torch.distributed as dist
 
-        local = int(os.environ.get("LOCAL_RANK", "0"))
+        local = _local_device()
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        _init_group(local)
     from rsx import synth
     from rsx.config import Config
     from rsx.data import EvalDataLoader, RecDataset, TrainDataLoader
@@ -190,6 +190,8 @@ def bench_model(args):
     cfg = dict(data_path=root + "/", train_batch_size=args.batch, rsx_sampler="device",
                is_multimodal_model=w["model"] == "SMORE", **w["cfg"])
     c = Config(w["model"], w["dataset"], cfg)
+    if world > 1:
+        c["device"] = torch.device("cuda", _local_device())  # (the rehearsal mode puts every rank on GPU 0)
     for k in c["hyper_parameters"]:
         if isinstance(c[k], list):
             c[k] = c[k][0]
@@ -396,6 +398,25 @@ def _json_line(out):
 _STDOUT_FD = 1
 
 
+def _local_device() -> int:
+    """This rank's GPU: LOCAL_RANK (one process per GPU).  RSX_BENCH_SAME_DEVICE=1 puts every
+    rank on GPU 0 -- only with RSX_BENCH_BACKEND=gloo (RCCL refuses two ranks on one GPU):
+    a rehearsal of the N-rank code paths on a one-GPU box, not a measurement."""
+    if os.environ.get("RSX_BENCH_SAME_DEVICE") == "1":
+        return 0
+    return int(os.environ.get("LOCAL_RANK", "0"))
+
+
+def _init_group(local: int):
+    import torch.distributed as dist
+
+    backend = os.environ.get("RSX_BENCH_BACKEND", "nccl")
+    if backend == "nccl":
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        dist.init_process_group(backend)
+
+
 def _free_port():
     import socket
 
@@ -460,6 +481,8 @@ def _rank_report(wall_s, gpu_ms, steps, world, dev):
     mine = torch.tensor([wall_s * 1e3 / steps, gpu_ms / steps], dtype=torch.float64, device=dev)
     if world == 1:
         return [{"rank": 0, "ms_per_step": float(mine[0]), "gpu_ms_per_step_events": float(mine[1])}]
+    if torch.distributed.get_backend() != "nccl":
+        mine = mine.cpu()  # gloo gathers host tensors only
     parts = [torch.empty_like(mine) for _ in range(world)]
     torch.distributed.all_gather(parts, mine)
     return [{"rank": r, "ms_per_step": float(p[0]), "gpu_ms_per_step_events": float(p[1])}
@@ -552,7 +575,7 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = _local_device()
     # c4 is the strong-scaling leg: the graph AND the global batch (--batch) are fixed, each
     # rank draws its share of the batch from its own users; c2/baby are weak scaling: every
     # rank owns its own sports/baby-shaped user block and a batch of --batch
@@ -572,7 +595,7 @@ def main():
             os.environ.setdefault("RANK", "0")
             os.environ.setdefault("WORLD_SIZE", "1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        _init_group(local)
     dev = torch.device("cuda", local)
 
     from rsx.engine import LightGCNEngine
@@ -656,9 +679,15 @@ def main():
         torch.cuda.synchronize()
         if world > 1:
             torch.distributed.barrier()
+        # every rank runs the same number of steps (its collectives pair with its peers'):
+        # the largest per-rank batch count; a rank with fewer batches wraps into its next epoch
+        nb = torch.tensor([float(-(-E // B))], dtype=torch.float64, device=dev)
+        if world > 1:
+            torch.distributed.all_reduce(nb, op=torch.distributed.ReduceOp.MAX)
+        nb = int(nb.item())
         done["inter"] = 0
         t_ep = time.perf_counter()
-        while pos["epoch"] == ep0:
+        for _ in range(nb):
             one_step()
         torch.cuda.synchronize()
         if world > 1:
@@ -669,7 +698,7 @@ def main():
             torch.distributed.all_reduce(er[:1], op=torch.distributed.ReduceOp.MAX)
             torch.distributed.all_reduce(er[1:], op=torch.distributed.ReduceOp.SUM)
         epoch_rate = {"interactions_per_s": float(er[1] / er[0]), "s_per_epoch": float(er[0]),
-                      "batches_per_rank": -(-E // B),
+                      "batches_per_rank": nb,
                       "includes": "the epoch's device sampling launch (shuffle + negatives), every batch's step"}
 
     # full-sort evaluation throughput (forward once + fused MFMA scores/mask/top-50)

@@ -531,3 +531,32 @@ class LayerGCNCPU:
         loss.backward()
         self.opt.step()
         return v
+
+
+# ---------------------------------------------------------------------------
+# full-sort scores as the kernels compute them (oracle/fs_oracle.c, C fmaf chain)
+# ---------------------------------------------------------------------------
+def fmaf_scores(U: np.ndarray, users: np.ndarray, I: np.ndarray) -> np.ndarray:
+    """[len(users), n_items] f32: the fmaf chain over d in order of U[users[b]] . I[i]
+    -- the exact score the rsx full-sort ranks by (csrc/fullsort.hip exact_dot), computed
+    on the CPU by oracle/fs_oracle.c (src/common/trainer.py:509-528 ranks U I^T)."""
+    import ctypes as C
+    import os
+
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_build", "libfsoracle.so")
+    if not os.path.exists(path):
+        import subprocess
+
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        subprocess.run(["gcc", "-O2", "-fopenmp", "-ffp-contract=off", "-fPIC", "-shared", "-o", path,
+                        os.path.join(os.path.dirname(path), "..", "fs_oracle.c"), "-lm"], check=True)
+    lib = C.CDLL(path)
+    U = np.ascontiguousarray(U, dtype=np.float32)
+    I = np.ascontiguousarray(I, dtype=np.float32)
+    users = np.ascontiguousarray(users, dtype=np.int64)
+    out = np.empty((users.size, I.shape[0]), dtype=np.float32)
+    P = C.c_void_p
+    lib.rsx_oracle_fmaf_scores.argtypes = [P, P, C.c_int64, P, C.c_int64, C.c_int32, P]
+    lib.rsx_oracle_fmaf_scores(U.ctypes.data, users.ctypes.data, users.size, I.ctypes.data, I.shape[0],
+                               U.shape[1], out.ctypes.data)
+    return out

@@ -577,6 +577,33 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D <= 64 ? 2 
 //    fs_tiles' 64-bit key if that score is >= L; rows that fill up are compacted
 //    exactly as in fs_tiles.
 // The candidate rows, counts and fs_select are fs_tiles'; the top k is exact.
+//
+// Invariants the exactness rests on (a change to either pass must keep every one;
+// tests/test_gpu_realshape.py::test_fullsort_screen_exact_vs_cpu_fmaf anchors them on
+// the CPU's fmaf scores, test_gpu_kernels.py::test_fullsort_screen_exact_vs_dense_scores
+// on score_dense's):
+//  (i)   bound: for every unmasked item, lo_i <= s_i <= hi_i with lo/hi the pass-1 /
+//        pass-2 accumulators (the margin block rounds |v_i| and eps |u| up);
+//  (ii)  key score: a masked item's score is exactly -1e10 in both passes (not its
+//        bound), an item past the chunk end is -inf in pass 1 and never queued;
+//  (iii) threshold: L = the k-th largest of >= k DISTINCT items' lower scores (pass 1
+//        samples distinct items per slot), so at least k items score >= L and every
+//        top-k item scores >= L; tau starts just below L and only rises to a k-th
+//        largest exact key of the user's row, so "score > tau" never rejects a top-k item;
+//  (iv)  queue completeness: pass 2 queues EVERY item whose upper score (hi_i, or -1e10
+//        for a masked item) exceeds the user's tau when its tile is scanned -- masked
+//        items included: a user whose unmasked items number fewer than k in the chunk
+//        has L = -1e10 and needs its masked items in the candidate row (they fill the
+//        top k as -1e10 in index order).  The round-2 "leaner masked-tile branch" that
+//        was reverted skipped masked items in pass 2 and broke exactly this: pass 1 stays
+//        correct, the row misses its -1e10 entries.  Rebuilt (tools/fs_lean_variant.py)
+//        and run on the GPU: it fails the CPU-anchored test on the masked-heavy users only
+//        (rows 1, 2 at every plan, k 50 / 64) and the dense-scores test on its masked-heavy
+//        user at k 50 / 64 only (30 unmasked items: k 1 / 17 need no -1e10 entry); every
+//        other row stays exact (profiles/r03/fs_invariant/);
+//  (v)   drain order: a queued item is scored against the user's tau at drain time
+//        (tau only rises), and a row is compacted to its exact top k+slack keys before
+//        it could overflow; fs_select then merges the user's lists exactly.
 // ---------------------------------------------------------------------------
 #ifndef RSX_FS_SCREEN_WPE
 #define RSX_FS_SCREEN_WPE 2  // fs_screen waves per SIMD requested at d <= 64

@@ -112,6 +112,44 @@ def test_fullsort_production_plans_exact(cuda, nb, ni, d, chunks, pattern):
     assert np.all(val[:6, 10:] == np.float32(-1e10))
 
 
+@pytest.mark.parametrize("k", [50, 64])
+@pytest.mark.parametrize("nb,ni,d,chunks", SHAPES)
+def test_fullsort_screen_exact_vs_cpu_fmaf(cuda, nb, ni, d, chunks, k):
+    """Real-valued, heavy-tailed tables at every production plan, anchored on the CPU:
+    the screened kernel's top-k must equal, index for index and bit for bit in value,
+    the canonical top-k (score desc, index asc) of the scores oracle/fs_oracle.c computes
+    with C's fmaf chain (the reference ranks U I^T with the train items at -1e10,
+    src/common/trainer.py:509-528).  The tables stress the screen's invariants
+    (csrc/fullsort.hip, "Screened full-sort"): row norms over six orders of magnitude
+    (the margin eps |u||v_i| from 1e-3 to 1e3 of a typical score), exact duplicate item
+    rows (score ties at the k boundary: the index order decides), a zero user (every
+    score 0), negated users, and users whose train items mask all but 10 items (the top
+    k holds -1e10 entries: masked items must reach the candidate rows as -1e10)."""
+    assert _plan(nb, ni, d)[0] == chunks
+    rng = np.random.default_rng(nb + d + k)
+    U = (rng.standard_normal((nb, d)) * np.exp(rng.standard_normal((nb, 1)))).astype(np.float32)
+    I = (rng.standard_normal((ni, d)) * np.exp(1.5 * rng.standard_normal((ni, 1)))).astype(np.float32)
+    dup = rng.choice(ni, size=ni // 50, replace=False)
+    I[dup] = I[rng.choice(ni, size=dup.size)]  # exact score ties
+    U[3] = 0.0
+    U[8:40] = -U[8:40]
+    users = rng.permutation(nb).astype(np.int64)
+    heavy = users[[1, 2]]
+    rp, mc = _history(nb, ni, rng, heavy)
+    val, idx = _run_fullsort(cuda, U, users, I, rp, mc, k)
+    rows = np.concatenate([[0, 1, 2, int(np.nonzero(users == 3)[0][0])],
+                           rng.choice(np.arange(3, nb), size=300 if d < 256 else 60, replace=False)])
+    s = O.fmaf_scores(U, users[rows], I)
+    for b, r in enumerate(rows):
+        u = users[r]
+        s[b, mc[rp[u]:rp[u + 1]]] = -1e10
+    cv, ci = canonical_topk_fast(s, k)
+    bad = np.nonzero(np.any(idx[rows] != ci, axis=1))[0]
+    assert bad.size == 0, f"rows {rows[bad[:5]]}: {idx[rows[bad[0]]][:8]} vs {ci[bad[0]][:8]}"
+    assert np.array_equal(val[rows].view(np.uint32), cv.view(np.uint32))
+    assert np.sum(cv[1] == -1e10) > 0 and np.sum(cv[2] == -1e10) > 0  # the masked-heavy users' top k
+
+
 def test_fullsort_sports_trained_tables(cuda):
     """Scores of a LightGCN table trained for 60 batches on the sports-shaped graph (the
     bench's evaluation: all 35,598 users, the train-item mask), modulo near-ties."""
