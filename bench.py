@@ -78,7 +78,7 @@ def _timed_loop(step, budget_s, min_steps=3, max_steps=200):
             return steps, el
 
 
-def cpu_baseline(df_train, nu, ni, budget_s=12.0, d=64, shape="sports", scale=1):
+def cpu_baseline(df_train, nu, ni, budget_s=12.0, d=64, shape="sports", scale=1, K=3):
     """Reference-identical CPU LightGCN (oracle restatement) on this host's cores:
     Python negative sampler + torch.sparse.mm propagation + autograd + Adam.  With
     scale > 1 the graph is a 1/scale slice and the rate is divided by scale."""
@@ -88,13 +88,13 @@ def cpu_baseline(df_train, nu, ni, budget_s=12.0, d=64, shape="sports", scale=1)
     torch.manual_seed(999)
     U0 = torch.nn.init.xavier_uniform_(torch.empty(nu, d)).numpy()
     I0 = torch.nn.init.xavier_uniform_(torch.empty(ni, d)).numpy()
-    cpu = O.LightGCNCPU(A, U0, I0, 3, 1e-2)
+    cpu = O.LightGCNCPU(A, U0, I0, K, 1e-2)
     smp = O.ReferenceSampler(tu, ti)
     if scale == 1:
         cpu.step(smp.next(2048))  # warm
     steps, el = _timed_loop(lambda: cpu.step(smp.next(2048)), budget_s, min_steps=1 if scale > 1 else 3)
-    what = (f"{steps} LightGCN K=3 d={d} B=2048 steps on the same {shape}-shaped graph" if scale == 1 else
-            f"{steps} LightGCN K=3 d={d} B=2048 step(s) on a 1/{scale} user slice ({nu:,} users x {ni:,} items, "
+    what = (f"{steps} LightGCN K={K} d={d} B=2048 steps on the same {shape}-shaped graph" if scale == 1 else
+            f"{steps} LightGCN K={K} d={d} B=2048 step(s) on a 1/{scale} user slice ({nu:,} users x {ni:,} items, "
             f"{len(tu):,} train interactions), rate divided by {scale}")
     return {"value": steps * 2048 / el / scale, "unit": "interactions/s", "cores": torch.get_num_threads(),
             "kind": "port",
@@ -552,6 +552,8 @@ def main():
     ap.add_argument("--eval-users", type=int, default=None, help="default: all valid users (c4: 32768 per rank)")
     ap.add_argument("--c4-chunks", type=int, default=None,
                     help="c4: build only the first N of the 8 1.25M-user chunks (1 = one rank's share at 8 GPUs)")
+    ap.add_argument("--n-layers", type=int, default=3,
+                    help="LightGCN depth (c2/baby/c4; default 3 = configs C2/C4; the reference's YAML default is 4)")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU only: exercise the N-rank launch and report (gloo), no GPU work")
     args = ap.parse_args()
@@ -612,10 +614,10 @@ def main():
     if sharded:
         from rsx.dist import ShardedLightGCNEngine
 
-        eng = ShardedLightGCNEngine(tu, ti, nu, ni, d, 3, 1e-2, 1e-3, dev, U0, I0, seed=rank,
+        eng = ShardedLightGCNEngine(tu, ti, nu, ni, d, args.n_layers, 1e-2, 1e-3, dev, U0, I0, seed=rank,
                                     batch=B)
     else:
-        eng = LightGCNEngine(tu, ti, nu, ni, d, 3, 1e-2, 1e-3, dev, U0, I0, seed=0, batch=B)
+        eng = LightGCNEngine(tu, ti, nu, ni, d, args.n_layers, 1e-2, 1e-3, dev, U0, I0, seed=0, batch=B)
     del U0, I0
     E = eng.n_inter
     parts = [eng.adj] if hasattr(eng, "adj") else [eng.A_U, eng.A_I]
@@ -808,10 +810,12 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         if not big:
-            cpu = cpu_baseline((tu, ti), nu, ni, args.cpu_budget, shape="sports" if args.workload == "c2" else "baby")
+            cpu = cpu_baseline((tu, ti), nu, ni, args.cpu_budget, shape="sports" if args.workload == "c2" else "baby",
+                               K=args.n_layers)
         else:  # C4: a 1/10 user slice (the first 1M users of the graph) over all 1M items, per step
             m = tu < 1_000_000
-            cpu = cpu_baseline((tu[m], ti[m]), 1_000_000, ni, args.cpu_budget, d=d, shape="C4", scale=10)
+            cpu = cpu_baseline((tu[m], ti[m]), 1_000_000, ni, args.cpu_budget, d=d, shape="C4", scale=10,
+                               K=args.n_layers)
 
     if rank == 0:
         ms = wall * 1e3 / args.steps
@@ -833,7 +837,7 @@ def main():
                     if not big else
                     ("synthetic C4 graph (rsx.synth.chunk_graph: 8 seeded 1.25M-user chunks, Zipf(0.8) items, "
                      "5+Geometric degrees mean 10, reference split rule); xavier-uniform-bound init"),
-            "config": {"workload": desc, "model": "LightGCN", "n_layers": 3, "embedding_size": d,
+            "config": {"workload": desc, "model": "LightGCN", "n_layers": args.n_layers, "embedding_size": d,
                        "global_batch": B * world, "per_rank_batch": B,
                        "leg": ("the metric's leg: C2 per rank, weak scaling (per-GPU work fixed as N grows)"
                                if args.workload == "c2" else

@@ -377,7 +377,7 @@ typedef struct rsx_lgcn_step {
      * per-row occurrence counts (+ a done counter and three scales in the tail) that
      * the Adam layer applies and clears; R is not used. */
     int32_t* reg_cnt;
-    /* Optional (any path: tagged, dense, K >= 4): [2] int32, zero-filled.  The first step whose loss is NaN
+    /* Optional (any path: tagged or dense, any K): [2] int32, zero-filled.  The first step whose loss is NaN
      * sets halt[0] = 1 and halt[1] = its tag; from then on the Adam layer leaves the
      * parameters and moments unchanged, so they stay those of the last finite step (the
      * reference checks the loss before backward and stops, src/common/trainer.py:201-203). */

@@ -15,7 +15,7 @@
 //   loss      BPR fwd+bwd: G += dL/dF (batch rows), R += d reg / d E^0;
 //   backward  H_k = A H_{k-1} (H_0 = G), S = sum H; the last layer
 //             applies Adam to E^0 with g = S/(K+1) + R in its epilogue.
-// With batch-row tags (rsx_lgcn_step.row_tag, K = 2, 3) the step stores the
+// With batch-row tags (rsx_lgcn_step.row_tag, K = 2..4) the step stores the
 // layers instead of a running sum, computes the last forward layer on the batch
 // rows only and runs the backward as the reference autograd's recursion on
 // G' = G/(K+1) (lgcn_step_stored_layers below): about 110 MB less traffic per
@@ -186,9 +186,10 @@ static int lgcn_forward(const rsx_csr& A, int d, int K, const float* p, float* s
     return 0;
 }
 
-// The batch-tagged LightGCN step for K = 2, 3: the forward keeps E^1..E^{K-1} in
-// h0 / h1 (no running sum) and computes the last layer and the mean on the batch
-// rows only; BPR writes G' = dL/dfinal / (K+1) (each layer's share of the mean,
+// The batch-tagged LightGCN step for K = 2, 3, 4 (4: the reference's default depth,
+// src/configs/model/LightGCN.yaml:3): the forward keeps E^1..E^{K-1} in h0 / h1 / s
+// (no running sum: s is free in this form) and computes the last layer and the mean on
+// the batch rows only; BPR writes G' = dL/dfinal / (K+1) (each layer's share of the mean,
 // MeanBackward); the backward is Horner on G', the reference autograd's own
 // recursion  dE^{k-1} = G' + A dE^k  (A symmetric), so no layer sum is stored
 // either: layer 1 gathers only the batch rows of G' (the rest are zero) and every
@@ -198,12 +199,13 @@ static int lgcn_step_stored_layers(const rsx_lgcn_step& st, int64_t batch, int32
     const rsx_csr& A = *st.adj;
     const int d = st.d, K = st.n_layers;
     int rc;
-    float* bufs[2] = {st.h0, st.h1};
+    float* layers[3] = {st.h0, st.h1, st.s};  // E^1, E^2, E^3
+    float* bufs[2] = {st.h0, st.h1};         // the backward's ping-pong
     // forward: E^k = A E^{k-1} stored (k < K), then F = mean on the tagged rows
     const float* x = st.p;
     for (int k = 1; k < K; ++k) {
         rsx_epilogue e = epi0(RSX_EPI_STORE);
-        e.y = bufs[k - 1];
+        e.y = layers[k - 1];
         TagJob tj;  // layer 1 also tags the batch rows (nothing reads the tags before the last layer)
         if (k == 1) {
             tj.trip = st.triplets;
@@ -213,15 +215,16 @@ static int lgcn_step_stored_layers(const rsx_lgcn_step& st, int64_t batch, int32
             tj.tag = tag;
         }
         if ((rc = spmm_dispatch_tagging(A, x, d, e, st.slab, s, tj))) return rc;
-        x = bufs[k - 1];
+        x = layers[k - 1];
     }
     {
-        rsx_epilogue e = epi0(RSX_EPI_FINAL);
+        rsx_epilogue e = epi0(RSX_EPI_FINAL);  // ((((E0 + E1) + E2) + E3) + A E^{K-1}) / (K+1)
         e.beta = 1.f / (float)(K + 1);
         e.f = st.final_emb;
         e.s_in = st.p;                        // E^0
         e.r_add = st.h0;                      // E^1
-        e.aux = K == 3 ? st.h1 : nullptr;     // E^2
+        e.aux = K >= 3 ? st.h1 : nullptr;     // E^2
+        e.e0 = K == 4 ? st.s : nullptr;       // E^3
         e.row_tag = st.row_tag;
         e.tag = tag;
         e.tag_flags = RSX_TAG_ROWS;
@@ -241,13 +244,13 @@ static int lgcn_step_stored_layers(const rsx_lgcn_step& st, int64_t batch, int32
     x = st.g;
     for (int k = 1; k < K; ++k) {
         rsx_epilogue e = epi0(RSX_EPI_ADD);
-        e.y = bufs[k - 1];
+        e.y = bufs[(k - 1) & 1];
         e.s_in = st.g;
         e.row_tag = st.row_tag;
         e.tag = tag;
         e.tag_flags = RSX_TAG_SPARSE_S | (k == 1 ? RSX_TAG_SPARSE_X : 0);
         if ((rc = spmm_dispatch(A, x, d, e, st.slab, s))) return rc;
-        x = bufs[k - 1];
+        x = bufs[(k - 1) & 1];
     }
     rsx_epilogue e = epi0(RSX_EPI_ADAM);
     e.s_in = st.g;
@@ -409,7 +412,7 @@ int rsx_lightgcn_step(const rsx_lgcn_step* st, rsx_stream_t stream) {
     const int32_t tag = (int32_t)st->tag;
     if (tags) {
         if (st->tag <= 0 || st->tag > INT32_MAX) return RSX_ERR_ARG;
-        if (K <= 3) return lgcn_step_stored_layers(*st, batch, tag, s);  // tags written by its layer 1
+        if (K <= 4) return lgcn_step_stored_layers(*st, batch, tag, s);  // tags written by its layer 1
         if ((rc = tag_rows(st->triplets, batch, st->n_users, st->row_tag, tag, s, nullptr))) return rc;
     }
     // forward (dense path: the last layer zeroes g and r)

@@ -453,7 +453,7 @@ def test_schedule_rebind_on_random_subgraphs(cuda, drop):
         assert torch.equal(A.spmm(x), B.spmm(x)), d
 
 
-@pytest.mark.parametrize("K,d", [(2, 64), (3, 64), (3, 128), (2, 256), (3, 32)])
+@pytest.mark.parametrize("K,d", [(2, 64), (3, 64), (3, 128), (2, 256), (3, 32), (4, 64), (4, 256)])
 def test_batch_row_tags_equal_dense_step(cuda, K, d):
     """rsx_lgcn_step.row_tag (last forward layer on the batch rows, sparse G, G/R
     cleared on the batch rows) gives the dense path's parameters and losses on a
