@@ -139,6 +139,92 @@ def cpu_baseline_smore(tu, ti, nu, ni, v, t, d, image_k, text_k, dropout, budget
                       f"and features (oracle.SMORECPU: torch CPU forward/autograd/Adam)"}
 
 
+MFMA_F32_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: dense f32 MFMA (no xf32 on gfx950)
+
+
+def _roof_hbm(name, nbytes, ms, note, calls):
+    gbs = nbytes / (ms * 1e-3) / 1e9
+    return {"bound": "hbm", "kernel": name, "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": gbs / HBM_PEAK_GBS, "traffic": None, "algorithmic_bytes_per_launch": nbytes, "avg_launch_ms": ms,
+            "launches_per_pass": calls, "note": note}
+
+
+def _roof_mfma(name, flops, ms, note, calls):
+    tfs = flops / (ms * 1e-3) / 1e12
+    return {"bound": "mfma", "kernel": name, "achieved": tfs, "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",
+            "frac": tfs / MFMA_F32_PEAK_TFS, "traffic": None, "algorithmic_flops_per_launch": flops,
+            "avg_launch_ms": ms, "launches_per_pass": calls, "note": note}
+
+
+def smore_kernel_rooflines(model, B, d):
+    """SMORE's dominant launches per forward/backward pass, each timed alone (HIP events on
+    the stream the kernels use) on the model's own operands, with its algorithmic work:
+      * the three item views' kNN products in one launch (spmm_batch STORE): per view
+        4(NI+1) + 8 nnz + 4 NI d (X read once) + 4 NI d (Y written) bytes;
+      * the projections' backward (rsx_linear_bwd, one per modality): dW = g^T X and
+        dX = g W, 4 NI d dv flop;
+      * the preference block's backward on the 3B batch rows (pref_rows bwd + its batched
+        weight gradients): 7 Linear(d, d) x (dX + dW) = 28 (3B) d^2 flop;
+      * the InfoNCE backward of both terms (nce_bwd): 2 terms x 2 products (d side,
+        d content) x 2 B^2 d flop = 8 B^2 d.
+    Sorted by their share of a pass (time x launches per pass)."""
+    from rsx import _lib as L
+    from rsx import ops
+    from rsx import smore_fuse as SF
+
+    dev = model.item_id_embedding.weight.device
+    ni = model.n_items
+    g = torch.Generator(device="cpu").manual_seed(5)
+    out = []
+    # views: the item-graph layer of the three views, one launch
+    Gs = [model.image_graph.A, model.text_graph.A, model.fusion_graph.A]
+    xs = [torch.randn(ni, d, generator=g).to(dev) for _ in range(3)]
+    ys = [torch.empty(ni, d, device=dev) for _ in range(3)]
+    epis = [ops.epi(L.RSX_EPI_STORE, y=y) for y in ys]
+    ms = time_kernel(lambda: ops.spmm_batch(Gs, xs, epis, d), 30)
+    nbytes = sum(4 * (ni + 1) + 8 * A.nnz + 8 * ni * d for A in Gs)
+    out.append(_roof_hbm(f"spmm_batch<{d},STORE> three kNN item-view products (one launch)", nbytes, ms,
+                         "kNN graphs and item tables are Infinity-Cache resident at clothing", 2))
+    # projection backward, image modality
+    V = model.image_embedding.weight.detach()
+    W = model.image_trs.weight.detach()
+    gi = torch.randn(ni, d, generator=g).to(dev)
+    ms = time_kernel(lambda: ops.linear_bwd(gi, V, W), 20)
+    out.append(_roof_mfma(f"rsx_linear_bwd (wgrad_partial<DX>) projection backward {ni}x{V.shape[1]}->{d}",
+                          4.0 * ni * d * V.shape[1], ms, "f32 MFMA 32x32x2 (dW) + 16x16x4 (dX)", 2))
+    # preference block backward on 3B rows
+    nu = model.n_users if not getattr(model, "sharded", False) else model.user_embedding.weight.shape[0]
+    n = nu + ni
+    tabs = [torch.randn(n, d, generator=g).to(dev).requires_grad_() for _ in range(4)]
+    rows = torch.randint(0, n, (3 * B,), generator=g).to(dev)
+    seed = torch.zeros(1, dtype=torch.int64, device=dev)
+    outs = SF.preference_rows(model, *tabs, rows, seed)
+    gos = [torch.randn_like(o) for o in outs]
+
+    def pref_bwd():
+        torch.autograd.grad(outs, tabs, gos, retain_graph=True)
+
+    ms = time_kernel(pref_bwd, 20)
+    out.append(_roof_mfma(f"pref_rows<{d}> backward + weight gradients ({3 * B} batch rows)", 28.0 * 3 * B * d * d,
+                          ms, "16x16x4 f32 MFMA row tiles; one 16-row tile per wave", 1))
+    # InfoNCE backward of both terms (compact rows)
+    side = torch.randn(3 * B, d, generator=g).to(dev).requires_grad_()
+    cont = torch.randn(3 * B, d, generator=g).to(dev).requires_grad_()
+    allc = torch.randn(3 * B, d, generator=g).to(dev).requires_grad_()
+    ar = torch.arange(B, device=dev)
+    trip = torch.stack([ar, ar, ar + B]).contiguous()
+    tot, _ = SF.smore_loss_rows(allc, side, cont, trip, ar, B, 1e-5, 2048.0, 0.01, 0.2)
+
+    def nce_bwd():
+        torch.autograd.grad(tot, [side, cont], retain_graph=True)
+
+    ms = time_kernel(nce_bwd, 20)
+    out.append(_roof_mfma(f"nce_bwd<{d}> InfoNCE backward, both terms (B = {B})", 8.0 * B * B * d, ms,
+                          "f32 MFMA; the B x B similarity tiles recomputed flash-style", 1))
+    out.sort(key=lambda r: -r["avg_launch_ms"] * r["launches_per_pass"])
+    return out
+
+
 WORKLOADS = {
     "c1": dict(model="LayerGCN", dataset="baby", desc="C1: LayerGCN K=2 d=64, baby-shaped (19,445 users x 7,050 items), "
                                                     "B=2048, device sampler, fused step (reference config: CPU)",
@@ -305,6 +391,12 @@ def bench_model(args):
             "unit": "GB/s", "frac": alg / (spmm_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
             "algorithmic_bytes_per_launch": alg, "avg_launch_ms": spmm_ms,
             "note": "baby/clothing working sets are Infinity-Cache resident"}
+    kernels = [roof]
+    if w["model"] == "SMORE":
+        # the step's dominant launches (rocprof: profiles/r02/legs/prof_c{3,5}), each timed
+        # alone on the model's own operands; the largest-share one is the line's roofline
+        kernels = smore_kernel_rooflines(model, args.batch, d) + [roof]
+        roof = kernels[0]
     cpu = None
     if not args.no_cpu_baseline and world == 1:
         tr_df = df[df.x_label == 0]
@@ -331,7 +423,7 @@ def bench_model(args):
         "rccl_world_size": rccl_world, "per_rank": per_rank,
         "fullsort_items_per_s": n_eval * ni / eval_s,
         "fullsort": {"eval_users": n_eval, "n_items": ni, "s_per_eval_incl_forward_and_metrics": eval_s},
-        "model_build_s": build_s, "roofline": roof, "cpu_baseline": cpu,
+        "model_build_s": build_s, "roofline": roof, "roofline_kernels": kernels, "cpu_baseline": cpu,
     }
     if rank == 0:
         _json_line(out)

@@ -261,6 +261,14 @@ def spectrum_torch(img, txt, wv, wt, wf, normalize=True):
     return cv, ct, cf
 
 
+class _nullctx:
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *a):
+        return False
+
+
 def _require_supported(d, v_feat, t_feat):
     """The shapes the SMORE kernels are instantiated for; anything else is refused
     (RSX_ERR_UNSUPPORTED) rather than run on torch ops."""
@@ -422,6 +430,15 @@ class SMORE(GeneralRecommender):
         self._epoch_of_buf = None
         self._gate_buf = torch.zeros(1, dtype=torch.float32, device=self.device)
 
+    def _side_stream(self):
+        """The UI backbone's stream (one per model), or None (RSX_SMORE_STREAMS=0)."""
+        if os.environ.get("RSX_SMORE_STREAMS", "1") == "0":
+            return None
+        st = getattr(self, "_ui_stream", None)
+        if st is None:
+            st = self._ui_stream = torch.cuda.Stream(device=self.device)
+        return st
+
     def local_batches(self, epoch: int):
         """This rank's training batches of `epoch` (device-sampled [3, B_r] triplets: users
         as local row ids, items global): steps_per_epoch of them on every rank."""
@@ -514,19 +531,37 @@ class SMORE(GeneralRecommender):
 
     def _views_fused(self, train=False, rows=None):
         """Everything before the preference block: (content, image, text, fusion tables,
-        dropout seed).  With `rows` (the batch rows) content is exact on those rows only."""
-        cv, ct, cf = self._projected_spectrum()
+        dropout seed).  With `rows` (the batch rows) content is exact on those rows only.
+
+        The UI backbone (content) does not depend on the item side (projection, spectral
+        fusion, gates) before the views meet it in the preference block, so it runs on a
+        side stream concurrently with it; its backward then runs on that stream too
+        (autograd keeps each op's backward on its forward's stream), overlapping the
+        item side's backward.  Both are latency-bound chains of mid-size launches, and
+        in a captured step the two streams become parallel branches of the HIP graph.
+        RSX_SMORE_STREAMS=0 keeps everything on one stream."""
         item_id = self.item_id_embedding.weight
+        main = torch.cuda.current_stream()
+        side = self._side_stream()
+        if side is not None:
+            side.wait_stream(main)
+            if rows is not None:
+                rows.record_stream(side)  # made on this stream, read on the side stream (also in the backward)
+        with torch.cuda.stream(side) if side is not None else _nullctx():
+            ego = torch.cat([self.user_embedding.weight, item_id], dim=0)
+            if rows is not None and 1 <= self.n_ui_layers <= 4:
+                if self._tags is None:
+                    self._tags = _RowTags(self.n_users + self.n_items, self.device)
+                self._tags.mark(rows)
+                content = _PropMeanRows.apply(ego, self.norm_adj_csr, self.n_ui_layers, self._tags, rows)
+            else:
+                content = _PropMean.apply(ego, self.norm_adj_csr, self.n_ui_layers)
+        cv, ct, cf = self._projected_spectrum()
         img_i, txt_i, fus_i = SF.gates(cv, ct, cf, item_id, self.gate_v, self.gate_t, self.gate_f,
                                        self.inject_scale, self.inject_mode == "mul")
-        ego = torch.cat([self.user_embedding.weight, item_id], dim=0)
-        if rows is not None and 1 <= self.n_ui_layers <= 4:
-            if self._tags is None:
-                self._tags = _RowTags(self.n_users + self.n_items, self.device)
-            self._tags.mark(rows)
-            content = _PropMeanRows.apply(ego, self.norm_adj_csr, self.n_ui_layers, self._tags, rows)
-        else:
-            content = _PropMean.apply(ego, self.norm_adj_csr, self.n_ui_layers)
+        if side is not None:
+            main.wait_stream(side)
+            content.record_stream(main)  # allocated on the side stream, read on this one
         nu, L_ = self.n_users, self.n_layers
         if self.batch_views:  # the three views' products batched into shared launches
             image_embeds, text_embeds, fusion_embeds = SF.view_prop3(
