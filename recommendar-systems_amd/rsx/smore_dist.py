@@ -165,12 +165,31 @@ class _UIProp(torch.autograd.Function):
 # ---------------------------------------------------------------------------
 # backends
 # ---------------------------------------------------------------------------
+class _Null:
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *a):
+        return False
+
+
 class HipSmoreBackend:
     """The rsx kernels (the single-process rsx.smore.SMORE's path)."""
 
     def __init__(self, device, chunk=32):
         self.device = ops.require_device(device)
         self.chunk = chunk
+        self._side = None
+
+    def side_stream(self):
+        """The UI backbone's stream (RSX_SMORE_STREAMS=0: none)."""
+        import os
+
+        if os.environ.get("RSX_SMORE_STREAMS", "1") == "0":
+            return None
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=self.device)
+        return self._side
 
     def operator(self, rowptr, col, val, n_cols, transpose=False):
         """A device CSR of a local row block (and, with transpose, the pair (A, A^T) for a
@@ -297,9 +316,21 @@ class SmoreShard:
         return self.be.gates(m, cv, ct, cf, m.item_id_embedding.weight)
 
     def _content_views(self, m):
+        """The UI backbone (with its per-layer all-reduces) on a side stream of the HIP
+        backend, concurrent with the replicated item side, so its exchanges hide behind
+        the projection / spectral / gate kernels (and likewise in the backward, which
+        autograd runs on the same streams)."""
+        side = self.be.side_stream() if hasattr(self.be, "side_stream") else None
+        main = torch.cuda.current_stream() if side is not None else None
+        if side is not None:
+            side.wait_stream(main)
+        with torch.cuda.stream(side) if side is not None else _Null():
+            ego = torch.cat([m.user_embedding.weight, m.item_id_embedding.weight])
+            content = _UIProp.apply(ego, self)
         img, txt, fus = self._item_side(m)
-        ego = torch.cat([m.user_embedding.weight, m.item_id_embedding.weight])
-        content = _UIProp.apply(ego, self)
+        if side is not None:
+            main.wait_stream(side)
+            content.record_stream(main)
         return content, self.be.views(self, (img, txt, fus))
 
     def pref_weights(self, m):
