@@ -116,6 +116,7 @@ struct FsArgs {
     int n_lists;       // candidate lists per user: n_chunks (fs_tiles), n_chunks * seg_slots (fs_screen)
     int seg_slots;     // fs_screen: segments per (user block, chunk) (1: unsegmented)
     int64_t seg_waves; // fs_screen: waves per chunk of the balanced split (0: one per user block)
+    unsigned* lbound;  // fs_screen two-phase: [nb] ordered words, max over the user's segments of their L
 };
 
 
@@ -604,12 +605,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D <= 64 ? 2 
 //  (v)   drain order: a queued item is scored against the user's tau at drain time
 //        (tau only rises), and a row is compacted to its exact top k+slack keys before
 //        it could overflow; fs_select then merges the user's lists exactly.
+// Round 3 refinements, each keeping (i)-(v):
+//  * two phases (default; RSX_FS_2PHASE=0: one launch): pass 1 of every segment max-es its
+//    L into a per-user word, pass 2 starts every segment of the user from the largest --
+//    each segment's L is a lower bound of the user's k-th score (iii), so their max is;
+//  * mask-free pass 1 (when every user of the wave has k + m <= 32 * RSX_FS_TOP, m = its
+//    masked items in the segment): masked items are sampled by their bounds and L is the
+//    (k + m)-th largest sample -- at most m of the k + m distinct items above it are
+//    masked, so (iii) holds without a per-slot mask select;
+//  * pass 2 with every tau >= -1e10 (wave-uniform test): a masked item's key -1e10 never
+//    exceeds tau, so (iv) needs no masked entry; items are tested by their raw upper
+//    bound (a masked hit is queued with its mask bit and scored -1e10 at the drain, below
+//    tau); a wave with some tau < -1e10 takes the exact masked select of (iv).
 // ---------------------------------------------------------------------------
 #ifndef RSX_FS_SCREEN_WPE
 #define RSX_FS_SCREEN_WPE 2  // fs_screen waves per SIMD requested at d <= 64
 #endif
 #ifndef RSX_FS_ABUF
-#define RSX_FS_ABUF 1  // fs_screen item-operand buffers at d <= 64 (a ring: loads NB - 1 tiles ahead; 1 at d > 64)
+#define RSX_FS_ABUF 2  // fs_screen item-operand buffers at d <= 64 (a ring: loads NB - 1 tiles ahead; 1 at d > 64)
 #endif
 #ifndef RSX_FS_TOP
 #define RSX_FS_TOP 3  // fs_screen pass-1 samples per accumulator slot (2 or 3): 32 * TOP distinct items a user
@@ -691,9 +704,19 @@ __device__ __forceinline__ float exact_dot(const float* __restrict__ u, const fl
 
 // One segment of fs_screen: user block ub, item tiles [ta, tz) of chunk `chunk`, into
 // candidate list `li` of the block's users (lists per user: a.n_lists).
-template <int D>
+// train-item mask list: each lane's next kMaskCap masked columns in LDS (stride kMaskCap + 1:
+// conflict-free), refilled from global only when a lane runs out -- the tile loops hold no
+// global load of their own besides the item operands, so their waits count those exactly
+constexpr int kMaskCap = 16;
+constexpr int kMaskStride = kMaskCap + 1;
+
+// PH: 0 both passes in one launch (the segment's own L); 1 pass 1 only, the segment's L
+// max-ed into a.lbound[user]; 2 pass 2 only, from tau = the user's a.lbound (every
+// segment of the user: chunks and split ranges)
+template <int D, int PH>
 __device__ __forceinline__ void screen_segment(const FsArgs& a, int64_t ub, int chunk, int li, int ta, int tz,
-                                               float* urows, unsigned* queue, int* lcnt, unsigned* lomax) {
+                                               float* urows, unsigned* queue, int* lcnt, unsigned* lomax,
+                                               int* mlds) {
     constexpr int HALF = D / 2;
     constexpr int NM = D / 16;  // bf16 MFMAs per 32x32 tile over the row (8 operand elements per lane each)
     constexpr int DP = kScreenRow<D>;
@@ -731,31 +754,54 @@ __device__ __forceinline__ void screen_segment(const FsArgs& a, int64_t ub, int 
     bu[NM] = u32x4{h == 0 ? (cmb | 0x8000u) : 0u, 0u, 0u, 0u};
     __syncthreads();  // urows (the previous segment's readers are done: see the end)
 
-    // train-item mask: a per-lane cursor over the user's sorted columns, the column
-    // after the current one prefetched (its load lands while tiles go by; kept as the
-    // raw int32 so that nothing uses it before the next masked item is consumed)
-    int64_t mp = 0, me = 0;
-    int next_mask = INT_MAX, after = INT_MAX;
+    // train-item mask: a per-lane cursor over the user's sorted columns [mp, me), the
+    // next kMaskCap of them staged in this lane's LDS list (mpos = the column index of
+    // entry 0, mfill entries, cursor mcur); next_mask = the current column (INT_MAX: none)
+    int64_t mp = 0, me = 0, mq = 0;
     if (uvalid && a.mrp) {
         int64_t lo = a.mrp[urow], hi = a.mrp[urow + 1];
         me = hi;
-        while (lo < hi) {
-            const int64_t mid = (lo + hi) >> 1;
-            if ((int64_t)a.mcol[mid] < i0) lo = mid + 1; else hi = mid;
-        }
-        mp = lo;
-        next_mask = mp < me ? a.mcol[mp] : INT_MAX;
-        after = mp + 1 < me ? a.mcol[mp + 1] : INT_MAX;
+        auto first_ge = [&](int64_t l, int64_t r, int64_t x) __attribute__((always_inline)) {
+            while (l < r) {
+                const int64_t mid = (l + r) >> 1;
+                if ((int64_t)a.mcol[mid] < x) l = mid + 1; else r = mid;
+            }
+            return l;
+        };
+        mp = first_ge(lo, hi, i0);
+        mq = first_ge(mp, hi, i1);
     }
+    // m = the user's masked items in [i0, i1).  MASK-FREE pass 1 (wave-uniform, when every
+    // user has k + m <= the 32 * RSX_FS_TOP samples): masked items are sampled by their
+    // bounds like any other, and L is the (k + m)-th largest sample -- of the k + m distinct
+    // items at or above it at most m are masked, so k unmasked items score >= L
+    const int kk = a.k + (int)(mq - mp);
+    const bool mfree = __ballot(uvalid && kk > 32 * RSX_FS_TOP) == 0ull;
+    int* const ml = mlds + lane * kMaskStride;
+    int64_t mpos = mp;
+    int mfill = 0, mcur = 0;
+    auto mfetch = [&]() __attribute__((always_inline)) {  // entries [mpos, mpos + mfill) into the list
+        mfill = (int)min((int64_t)kMaskCap, me - mpos);
+        mcur = 0;
+        if (mfill <= 0) return;
+        int v[kMaskCap];  // every load issued before the first use (one wait, not one per entry)
+#pragma unroll
+        for (int q = 0; q < kMaskCap; ++q) v[q] = a.mcol[mpos + min(q, mfill - 1)];
+#pragma unroll
+        for (int q = 0; q < kMaskCap; ++q) ml[q] = v[q];  // (entries past mfill: never read)
+    };
+    mfetch();
+    int next_mask = mfill > 0 ? ml[0] : INT_MAX;
     const int64_t mp0 = mp;
-    const int nm0 = next_mask, af0 = after;
     auto mask_bits = [&](int64_t tb) __attribute__((always_inline)) -> unsigned {
         unsigned mb = 0;
         while ((int64_t)next_mask < tb + 32) {
             mb |= 1u << (unsigned)((int64_t)next_mask - tb);
-            ++mp;
-            next_mask = after;
-            after = mp + 1 < me ? a.mcol[mp + 1] : INT_MAX;
+            if (++mcur == mfill) {
+                mpos += mfill;
+                mfetch();
+            }
+            next_mask = mcur < mfill ? ml[mcur] : INT_MAX;
         }
         return mb;
     };
@@ -811,12 +857,12 @@ __device__ __forceinline__ void screen_segment(const FsArgs& a, int64_t ub, int 
     auto pass1 = [&](auto par, int t) __attribute__((always_inline)) {
         // the mask cursor first: its loads' waits then precede the next tile's prefetch
         const int64_t tb = i0 + (int64_t)t * 32;
-        const unsigned mb = mask_bits(tb);
+        const unsigned mb = mfree ? 0u : mask_bits(tb);
         floatx16 acc;
         tile(par, t, acc);
         const int rem = (int)(i1 - tb);
         // top two by median-of-three (t1 >= t2): t2 = med3(t1, t2, x), t1 = max(t1, x)
-        if (rem >= 32 && __ballot(mb != 0u) == 0ull) {  // wave-uniform: no masked or missing item
+        if (rem >= 32 && (mfree || __ballot(mb != 0u) == 0ull)) {  // wave-uniform: no masked or missing item
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 if constexpr (RSX_FS_TOP == 3) t3[r] = vmed3(t2[r], t3[r], acc[r]);
@@ -838,20 +884,28 @@ __device__ __forceinline__ void screen_segment(const FsArgs& a, int64_t ub, int 
             }
         }
     };
-    prime();
-    sweep(pass1);
-    // L = the k-th largest of the lane pair's 32 * RSX_FS_TOP bounds (radix search on
-    // ordered words)
     unsigned th = 0;
-    for (int bit = 31; bit >= 0; --bit) {
-        const unsigned c = th | (1u << bit);
-        int n = 0;
+    if constexpr (PH != 2) {
+        prime();
+        sweep(pass1);
+        // L = the k-th largest of the lane pair's 32 * RSX_FS_TOP bounds (radix search on
+        // ordered words)
+        for (int bit = 31; bit >= 0; --bit) {
+            const unsigned c = th | (1u << bit);
+            int n = 0;
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
-            n += (int)(ord_f32(t1[r]) >= c) + (int)(ord_f32(t2[r]) >= c) +
-                 (RSX_FS_TOP == 3 ? (int)(ord_f32(t3[r]) >= c) : 0);
-        n += __shfl_xor(n, 32, kWave);
-        if (n >= a.k) th = c;
+            for (int r = 0; r < 16; ++r)
+                n += (int)(ord_f32(t1[r]) >= c) + (int)(ord_f32(t2[r]) >= c) +
+                     (RSX_FS_TOP == 3 ? (int)(ord_f32(t3[r]) >= c) : 0);
+            n += __shfl_xor(n, 32, kWave);
+            if (n >= (mfree ? kk : a.k)) th = c;
+        }
+        if constexpr (PH == 1) {  // every segment's L is a lower bound of the user's k-th score: keep the largest
+            if (uvalid && h == 0) atomicMax(a.lbound + bslot, th);
+            return;
+        }
+    } else {
+        th = uvalid ? a.lbound[bslot] : 0u;
     }
     // running strict filter "> tau" keeping every score >= L (the ordered word below L's;
     // -0.0 == +0.0 as floats, so a bound that lands on a zero filters with a negative denormal)
@@ -860,7 +914,7 @@ __device__ __forceinline__ void screen_segment(const FsArgs& a, int64_t ub, int 
         const float tb = unord_f32(th - 1);
         tau = tb == 0.f ? -__FLT_DENORM_MIN__ : tb;
     }
-    if (a.mode == 5) {  // profiling ablation: pass 1 only
+    if (PH == 0 && a.mode == 5) {  // profiling ablation: pass 1 only
         if (uvalid && h == 0) a.ccount[bslot * a.n_lists + li] = 0;
         if (tau == 1234.5f) a.out_val[0] = tau;
         __syncthreads();
@@ -872,9 +926,9 @@ __device__ __forceinline__ void screen_segment(const FsArgs& a, int64_t ub, int 
     // keys enter the users' candidate rows (fs_tiles' rows and compaction), counts and
     // row maxima kept in LDS
     bu[NM] = u32x4{h == 0 ? cmb : 0u, 0u, 0u, 0u};
-    mp = mp0;
-    next_mask = nm0;
-    after = af0;
+    mpos = mp0;
+    mfetch();
+    next_mask = mfill > 0 ? ml[0] : INT_MAX;
     int cnt = 0;
     unsigned omax = 0;
     if (lane < 32) {
@@ -952,9 +1006,16 @@ __device__ __forceinline__ void screen_segment(const FsArgs& a, int64_t ub, int 
             }
         };
         const float tv = uvalid ? tau : INFINITY;  // invalid users take nothing
-        if (rem >= 32 && __ballot(mb != 0u) == 0ull) {
+        if (rem >= 32 && __ballot(tv < -1e10f) == 0ull) {
+            // every tau >= -1e10: a masked item (key -1e10) never needs queueing, so items are
+            // tested by their raw upper bounds and a hit carries its mask bit (the drain
+            // scores it -1e10, below tau)
+            const unsigned mbh = mb >> (4 * h);
 #pragma unroll
-            for (int r = 0; r < 16; ++r) push(acc[r] > tv, ebase + ((unsigned)((r & 3) + 8 * (r >> 2)) << 6));
+            for (int r = 0; r < 16; ++r) {
+                const int io = (r & 3) + 8 * (r >> 2);
+                push(acc[r] > tv, (ebase + ((unsigned)io << 6)) | (((mbh >> io) & 1u) << 5));
+            }
         } else {
             const unsigned mbh = mb >> (4 * h);
             const int remh = rem - 4 * h;
@@ -999,13 +1060,14 @@ __device__ __forceinline__ void screen_segment(const FsArgs& a, int64_t ub, int 
 // wave's range covers whole or partial tile ranges of consecutive user blocks; segment
 // s of (block, chunk) writes list chunk * S + s (S = a.seg_slots), and the last segment
 // of a (block, chunk) zeroes the counts of the lists after it.
-template <int D>
+template <int D, int PH>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D <= 64 ? RSX_FS_SCREEN_WPE : 1))) void fs_screen(FsArgs a) {
     constexpr int US = D + 4;
     __shared__ __attribute__((aligned(16))) float urows[32 * US];
     __shared__ unsigned queue[64 * 17];  // pass 2 candidates: < 64 pending + one tile's (<= 16 per lane)
     __shared__ int lcnt[32];
     __shared__ unsigned lomax[32];
+    __shared__ int mlds[64 * kMaskStride];
     const int64_t n_ub = (a.nb + 31) / 32;
     const int64_t nper = a.seg_waves ? a.seg_waves : n_ub;  // waves per chunk
     int64_t w;
@@ -1030,8 +1092,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D <= 64 ? RS
         const int t1 = (int)min((int64_t)nt, t0 + (hi - x));
         const int64_t wf = ((ub * nt + 1) * nper + T - 1) / T - 1;  // the wave whose range holds tile 0 of ub
         const int seg = a.seg_waves ? (int)(w - wf) : 0;
-        screen_segment<D>(a, ub, chunk, chunk * S + seg, t0, t1, urows, queue, lcnt, lomax);
-        if (t1 == nt) {  // the block's last segment in this chunk: the later lists are empty
+        screen_segment<D, PH>(a, ub, chunk, chunk * S + seg, t0, t1, urows, queue, lcnt, lomax, mlds);
+        if (PH != 1 && t1 == nt) {  // the block's last segment in this chunk: the later lists are empty
             const int j = threadIdx.x & 31;
             const int64_t bslot = ub * 32 + j;
             if (threadIdx.x < 32 && bslot < a.nb)
@@ -1345,6 +1407,7 @@ size_t fs_ws(int64_t nb, int64_t ni, int k, int d) {
     if (L.screen) {
         const size_t ni_pad = (size_t)(ni + 31) / 32 * 32;
         bytes += fs_align(ni_pad * (d + 16) * sizeof(__bf16));
+        bytes += fs_align((size_t)nb * sizeof(unsigned));  // lbound
     }
     return bytes;
 }
@@ -1357,7 +1420,14 @@ static int launch_fs(FsArgs& a, const FsLayout& L, hipStream_t s) {
         const int64_t nthr = ni_pad * (D / 4);
         hipLaunchKernelGGL((fs_prep<D>), dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, s, a.I, a.ni, ni_pad,
                            const_cast<__bf16*>(a.Ib));
-        hipLaunchKernelGGL((fs_screen<D>), grid, dim3(64), 0, s, a);
+        if (a.lbound) {  // two phases: every segment of a user filters by the best of their thresholds
+            (void)hipMemsetAsync(a.lbound, 0, (size_t)a.nb * sizeof(unsigned), s);
+            hipLaunchKernelGGL((fs_screen<D, 1>), grid, dim3(64), 0, s, a);
+            if (a.mode != 5) hipLaunchKernelGGL((fs_screen<D, 2>), grid, dim3(64), 0, s, a);
+            else return last_rc();
+        } else {
+            hipLaunchKernelGGL((fs_screen<D, 0>), grid, dim3(64), 0, s, a);
+        }
     } else if (a.mode == 4) {
         hipLaunchKernelGGL((fs_tiles<D, 4>), grid, dim3(64), 0, s, a);
     } else if (a.mode == 1) {
@@ -1404,10 +1474,17 @@ int fs_call(const float* U, const int64_t* users, int64_t nb, const float* I, in
     a.out_val = out_val;
     a.out_idx = out_idx;
     a.Ib = nullptr;
+    a.lbound = nullptr;
     if (L.screen) {
         char* p = static_cast<char*>(ws) +
                   fs_align((size_t)nb * a.n_lists * kCap * sizeof(u64) + (size_t)nb * a.n_lists * sizeof(int) + 512);
         a.Ib = reinterpret_cast<const __bf16*>(p);
+        const size_t ni_pad = (size_t)(ni + 31) / 32 * 32;
+        static const int two = [] {
+            const char* e = getenv("RSX_FS_2PHASE");  // 0: both passes in one launch, per-segment thresholds
+            return e ? atoi(e) : 1;
+        }();
+        a.lbound = two ? reinterpret_cast<unsigned*>(p + fs_align(ni_pad * (d + 16) * sizeof(__bf16))) : nullptr;
     }
     {
         static int mode = -1;
