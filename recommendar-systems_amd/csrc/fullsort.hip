@@ -116,7 +116,9 @@ struct FsArgs {
     int n_lists;       // candidate lists per user: n_chunks (fs_tiles), n_chunks * seg_slots (fs_screen)
     int seg_slots;     // fs_screen: segments per (user block, chunk) (1: unsegmented)
     int64_t seg_waves; // fs_screen: waves per chunk of the balanced split (0: one per user block)
-    unsigned* lbound;  // fs_screen two-phase: [nb] ordered words, max over the user's segments of their L
+    unsigned* lbound;  // fs_screen two-phase: [nb] the user's L as an ordered word (fs_thresh)
+    uint16_t* samp;    // two-phase pass 1: [nb][n_lists][96] the segments' samples (ordered words' high halves)
+    uint16_t* mcnt1;   // two-phase pass 1: [nb][n_lists] masked items sampled by value (0xffff: no segment)
 };
 
 
@@ -636,6 +638,7 @@ constexpr float kScreenEps = 0.0080f;
 
 template <int D>
 constexpr int kScreenRow = D + 16;  // bf16 elements per screened item row: the row, then |v| and 15 zeros
+constexpr int kScreenPadTiles = 2;  // 32-row tiles past ni_pad in the bf16 copy (read ahead, never used)
 
 __device__ __forceinline__ unsigned pack_bf16x2(float lo, float hi) {
     const bf16x2 v = {(__bf16)lo, (__bf16)hi};
@@ -687,6 +690,33 @@ __global__ __launch_bounds__(256) void fs_prep(const float* __restrict__ I, int6
     }
 }
 
+// ND exact scores at once (one per candidate, the chains interleaved: each is exact_dot's
+// fmaf chain over d in order, bit for bit; the interleave only hides the FMA latency)
+template <int D, int ND>
+__device__ __forceinline__ void exact_dots(const float* const (&u)[ND], const float* const (&v)[ND], float (&out)[ND]) {
+    float acc[ND];
+#pragma unroll
+    for (int n = 0; n < ND; ++n) acc[n] = 0.f;
+#pragma unroll 4
+    for (int c = 0; c < D; c += 4) {
+        float4 x[ND], y[ND];
+#pragma unroll
+        for (int n = 0; n < ND; ++n) {
+            x[n] = *reinterpret_cast<const float4*>(u[n] + c);
+            y[n] = ld4(v[n] + c);
+        }
+#pragma unroll
+        for (int n = 0; n < ND; ++n) {
+            acc[n] = fmaf(x[n].x, y[n].x, acc[n]);
+            acc[n] = fmaf(x[n].y, y[n].y, acc[n]);
+            acc[n] = fmaf(x[n].z, y[n].z, acc[n]);
+            acc[n] = fmaf(x[n].w, y[n].w, acc[n]);
+        }
+    }
+#pragma unroll
+    for (int n = 0; n < ND; ++n) out[n] = acc[n];
+}
+
 // exact score <U row, I row>: fmaf chain over d in order (as score_dense)
 template <int D>
 __device__ __forceinline__ float exact_dot(const float* __restrict__ u, const float* __restrict__ v) {
@@ -704,10 +734,14 @@ __device__ __forceinline__ float exact_dot(const float* __restrict__ u, const fl
 
 // One segment of fs_screen: user block ub, item tiles [ta, tz) of chunk `chunk`, into
 // candidate list `li` of the block's users (lists per user: a.n_lists).
-// train-item mask list: each lane's next kMaskCap masked columns in LDS (stride kMaskCap + 1:
-// conflict-free), refilled from global only when a lane runs out -- the tile loops hold no
-// global load of their own besides the item operands, so their waits count those exactly
-constexpr int kMaskCap = 16;
+// train-item mask lists: a user's masked columns of the segment in LDS (up to kMaskCap,
+// stride kMaskCap + 1: conflict-free; screen_segment's LDS form)
+#ifndef RSX_FS_DRAIN
+#define RSX_FS_DRAIN 1  // pass-2 candidates scored per lane per drain (interleaved exact dots; 2: same time)
+#endif
+constexpr int kDrainPer = RSX_FS_DRAIN;
+constexpr int kQueueCap = 64 * kDrainPer + 1024;  // < 64 kDrainPer pending + one tile's (<= 16 per lane)
+constexpr int kMaskCap = 32;
 constexpr int kMaskStride = kMaskCap + 1;
 
 // PH: 0 both passes in one launch (the segment's own L); 1 pass 1 only, the segment's L
@@ -745,8 +779,10 @@ __device__ __forceinline__ void screen_segment(const FsArgs& a, int64_t ub, int 
         const float4 q = uvalid ? ld4(a.U + urow * D + h * HALF + 8 * s + 4) : f4(0.f);
         ss += p.x * p.x + p.y * p.y + p.z * p.z + p.w * p.w + q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w;
         bu[s] = u32x4{pack_bf16x2(p.x, p.y), pack_bf16x2(p.z, p.w), pack_bf16x2(q.x, q.y), pack_bf16x2(q.z, q.w)};
-        *reinterpret_cast<float4*>(myrow + h * HALF + 8 * s) = p;
-        *reinterpret_cast<float4*>(myrow + h * HALF + 8 * s + 4) = q;
+        if constexpr (PH != 1) {  // the f32 row for the exact scores (pass 2)
+            *reinterpret_cast<float4*>(myrow + h * HALF + 8 * s) = p;
+            *reinterpret_cast<float4*>(myrow + h * HALF + 8 * s + 4) = q;
+        }
     }
     ss += __shfl_xor(ss, 32, kWave);
     // margin block: element 0 of lane half 0 carries -eps |u| (pass 1; +eps |u| in pass 2)
@@ -754,9 +790,7 @@ __device__ __forceinline__ void screen_segment(const FsArgs& a, int64_t ub, int 
     bu[NM] = u32x4{h == 0 ? (cmb | 0x8000u) : 0u, 0u, 0u, 0u};
     __syncthreads();  // urows (the previous segment's readers are done: see the end)
 
-    // train-item mask: a per-lane cursor over the user's sorted columns [mp, me), the
-    // next kMaskCap of them staged in this lane's LDS list (mpos = the column index of
-    // entry 0, mfill entries, cursor mcur); next_mask = the current column (INT_MAX: none)
+    // train-item mask: the user's sorted columns; [mp, mq) are the segment's
     int64_t mp = 0, me = 0, mq = 0;
     if (uvalid && a.mrp) {
         int64_t lo = a.mrp[urow], hi = a.mrp[urow + 1];
@@ -775,70 +809,93 @@ __device__ __forceinline__ void screen_segment(const FsArgs& a, int64_t ub, int 
     // user has k + m <= the 32 * RSX_FS_TOP samples): masked items are sampled by their
     // bounds like any other, and L is the (k + m)-th largest sample -- of the k + m distinct
     // items at or above it at most m are masked, so k unmasked items score >= L
-    const int kk = a.k + (int)(mq - mp);
+    const int64_t mcount = mq - mp;
+    const int kk = a.k + (int)mcount;
     const bool mfree = __ballot(uvalid && kk > 32 * RSX_FS_TOP) == 0ull;
-    int* const ml = mlds + lane * kMaskStride;
-    int64_t mpos = mp;
-    int mfill = 0, mcur = 0;
-    auto mfetch = [&]() __attribute__((always_inline)) {  // entries [mpos, mpos + mfill) into the list
-        mfill = (int)min((int64_t)kMaskCap, me - mpos);
-        mcur = 0;
-        if (mfill <= 0) return;
-        int v[kMaskCap];  // every load issued before the first use (one wait, not one per entry)
+    // The mask cursor, in one of two forms chosen per segment (wave-uniform):
+    //  LDS: every user's m <= kMaskCap -- the segment's columns staged once in the user's
+    //       LDS list (both lane halves read it; INT_MAX-terminated): the tile loops then
+    //       hold no global load besides the item operands, so their waits count those;
+    //  GLOBAL: a per-lane cursor over the columns, the one after the current prefetched.
+    const bool mlds_ok = __ballot(mcount > kMaskCap) == 0ull;
+    int* const ml = mlds + j * kMaskStride;
+    if (mlds_ok) {
+        int v[kMaskCap / 2];  // lane half h loads entries h, h + 2, ..: every load before the first store
+        if (mcount > 0) {
 #pragma unroll
-        for (int q = 0; q < kMaskCap; ++q) v[q] = a.mcol[mpos + min(q, mfill - 1)];
+            for (int q = 0; q < kMaskCap / 2; ++q) v[q] = a.mcol[mp + min((int64_t)(2 * q + h), mcount - 1)];
+        }
 #pragma unroll
-        for (int q = 0; q < kMaskCap; ++q) ml[q] = v[q];  // (entries past mfill: never read)
-    };
-    mfetch();
-    int next_mask = mfill > 0 ? ml[0] : INT_MAX;
+        for (int q = 0; q < kMaskCap / 2; ++q) ml[2 * q + h] = 2 * q + h < mcount ? v[q] : INT_MAX;
+        if (h == 0) ml[kMaskCap] = INT_MAX;
+    }
     const int64_t mp0 = mp;
-    auto mask_bits = [&](int64_t tb) __attribute__((always_inline)) -> unsigned {
+    int next_mask = INT_MAX, after = INT_MAX, mcur = 0;
+    auto mask_start = [&]() __attribute__((always_inline)) {  // (every variable assigned on every path)
+        const int nm = mlds_ok ? ml[0] : (mp0 < me ? a.mcol[mp0] : INT_MAX);
+        const int af = (!mlds_ok && mp0 + 1 < me) ? a.mcol[mp0 + 1] : INT_MAX;
+        mcur = 0;
+        mp = mp0;
+        next_mask = nm;
+        after = af;
+    };
+    __syncthreads();  // the lists (lanes read their partner half's entries)
+    mask_start();
+    // the tile's mask bits, form M: 0 none (mask-free pass 1), 1 LDS, 2 GLOBAL
+    auto mask_bits = [&](auto form, int64_t tb) __attribute__((always_inline)) -> unsigned {
+        constexpr int M = decltype(form)::value;
         unsigned mb = 0;
-        while ((int64_t)next_mask < tb + 32) {
-            mb |= 1u << (unsigned)((int64_t)next_mask - tb);
-            if (++mcur == mfill) {
-                mpos += mfill;
-                mfetch();
+        if constexpr (M == 1) {
+            while ((int64_t)next_mask < tb + 32) {
+                mb |= 1u << (unsigned)((int64_t)next_mask - tb);
+                next_mask = ml[++mcur];
             }
-            next_mask = mcur < mfill ? ml[mcur] : INT_MAX;
+        } else if constexpr (M == 2) {
+            while ((int64_t)next_mask < tb + 32) {
+                mb |= 1u << (unsigned)((int64_t)next_mask - tb);
+                ++mp;
+                next_mask = after;
+                after = mp + 1 < me ? a.mcol[mp + 1] : INT_MAX;
+            }
         }
         return mb;
     };
-    // A operand: item i0 + 32 t + j, half h (the padded bf16 copy: no clamps).  NB > 1:
-    // a ring of NB buffers, tile t's MFMAs preceded by the loads of tile t + NB - 1 (two
-    // tiles of latency cover at two waves per SIMD); NB = 1: one buffer refilled with
-    // the next tile as soon as the MFMAs have read it
+    // A operand: item i0 + 32 t + j, half h (the padded bf16 copy: no clamps), loaded
+    // in tile order through one stepping pointer.  NB > 1: a ring of NB buffers, tile
+    // t's MFMAs preceded by the loads of tile t + NB - 1 (two tiles of latency cover at
+    // two waves per SIMD); NB = 1: one buffer refilled with the next tile as soon as the
+    // MFMAs have read it.  Every tile issues its load unconditionally (a conditional
+    // load would make the compiler's wait before the MFMAs cover the prefetch too): the
+    // last NB - 1 loads read past the segment, into the copy's kScreenPadTiles tiles
     constexpr int NB = kAbuf<D>;
     u32x4 ra[NB][NM + 1];
-    auto load_a = [&](auto par, int t) __attribute__((always_inline)) {
+    const __bf16* const a0 = a.Ib + (i0 + j) * DP;
+    const __bf16* anext = a0;
+    auto load_a = [&](auto par) __attribute__((always_inline)) {
         constexpr int P = decltype(par)::value % NB;
-        const __bf16* row = a.Ib + (i0 + (int64_t)t * 32 + j) * DP;
-        const u32x4* p = reinterpret_cast<const u32x4*>(row + h * HALF);
+        const u32x4* p = reinterpret_cast<const u32x4*>(anext + h * HALF);
 #pragma unroll
         for (int s = 0; s < NM; ++s) ra[P][s] = p[s];
-        ra[P][NM] = *reinterpret_cast<const u32x4*>(row + D + 8 * h);
+        ra[P][NM] = *reinterpret_cast<const u32x4*>(anext + D + 8 * h);
+        anext += 32 * DP;
     };
     auto tile = [&](auto par, int t, floatx16& acc) __attribute__((always_inline)) {
         constexpr int P = decltype(par)::value % NB;
-        // unconditional (past the end the last tile reloads itself): a conditional load
-        // would make the compiler's wait before the MFMAs cover the prefetch too
-        const int ta = t + (NB > 1 ? NB - 1 : 1);
-        const int tn = ta < ntiles ? ta : ntiles - 1;
-        if constexpr (NB > 1) load_a(IntC<(P + NB - 1) % NB>{}, tn);
+        if constexpr (NB > 1) load_a(IntC<(P + NB - 1) % NB>{});
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[r] = 0.f;
 #pragma unroll
         for (int s = 0; s <= NM; ++s)
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, ra[P][s]),
                                                           __builtin_bit_cast(bf16x8, bu[s]), acc, 0, 0, 0);
-        if constexpr (NB == 1) load_a(IntC<0>{}, tn);
+        if constexpr (NB == 1) load_a(IntC<0>{});
     };
     // the first NB - 1 tiles' loads, then tiles in groups of NB (ring slots by template)
     auto prime = [&]() __attribute__((always_inline)) {
+        anext = a0;
         if (ntiles <= 0) return;
-        load_a(IntC<0>{}, 0);
-        if constexpr (NB > 2) load_a(IntC<1>{}, ntiles > 1 ? 1 : 0);
+        load_a(IntC<0>{});
+        if constexpr (NB > 2) load_a(IntC<1>{});
     };
     auto sweep = [&](auto&& body) __attribute__((always_inline)) {
         for (int t = 0; t < ntiles; t += NB) {
@@ -854,22 +911,17 @@ __device__ __forceinline__ void screen_segment(const FsArgs& a, int64_t ub, int 
     float t1[16], t2[16], t3[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) t1[r] = t2[r] = t3[r] = -INFINITY;
-    auto pass1 = [&](auto par, int t) __attribute__((always_inline)) {
+    auto pass1 = [&](auto form, auto par, int t) __attribute__((always_inline)) {
         // the mask cursor first: its loads' waits then precede the next tile's prefetch
         const int64_t tb = i0 + (int64_t)t * 32;
-        const unsigned mb = mfree ? 0u : mask_bits(tb);
+        const unsigned mb = mask_bits(form, tb);
         floatx16 acc;
         tile(par, t, acc);
         const int rem = (int)(i1 - tb);
-        // top two by median-of-three (t1 >= t2): t2 = med3(t1, t2, x), t1 = max(t1, x)
-        if (rem >= 32 && (mfree || __ballot(mb != 0u) == 0ull)) {  // wave-uniform: no masked or missing item
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                if constexpr (RSX_FS_TOP == 3) t3[r] = vmed3(t2[r], t3[r], acc[r]);
-                t2[r] = vmed3(t1[r], t2[r], acc[r]);
-                t1[r] = vmax(t1[r], acc[r]);
-            }
-        } else {
+        // a tile with a missing item (the chunk's last) or, outside the mask-free form, a
+        // masked one: those slots first take their key (-inf / -1e10) in place, then every
+        // tile runs the same update (one code path: no register shuffles between forms)
+        if (rem < 32 || (decltype(form)::value != 0 && __ballot(mb != 0u) != 0ull)) {  // wave-uniform
             // slot r <-> item io(r) + 4 h: shift the mask and the bound by 4 h once, so the
             // per-slot tests take immediates (no per-slot constants held in registers)
             const unsigned mbh = mb >> (4 * h);
@@ -877,17 +929,49 @@ __device__ __forceinline__ void screen_segment(const FsArgs& a, int64_t ub, int 
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int io = (r & 3) + 8 * (r >> 2);
-                const float l = io >= remh ? -INFINITY : (((mbh >> io) & 1u) ? -1e10f : acc[r]);
-                if constexpr (RSX_FS_TOP == 3) t3[r] = vmed3(t2[r], t3[r], l);
-                t2[r] = vmed3(t1[r], t2[r], l);
-                t1[r] = vmax(t1[r], l);
+                acc[r] = io >= remh ? -INFINITY : (((mbh >> io) & 1u) ? -1e10f : acc[r]);
             }
+        }
+        // top three by median-of-three (t1 >= t2 >= t3): t3 = med3(t2, t3, x),
+        // t2 = med3(t1, t2, x), t1 = max(t1, x)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            if constexpr (RSX_FS_TOP == 3) t3[r] = vmed3(t2[r], t3[r], acc[r]);
+            t2[r] = vmed3(t1[r], t2[r], acc[r]);
+            t1[r] = vmax(t1[r], acc[r]);
         }
     };
     unsigned th = 0;
     if constexpr (PH != 2) {
         prime();
-        sweep(pass1);
+        if (mfree) sweep([&](auto par, int t) __attribute__((always_inline)) { pass1(IntC<0>{}, par, t); });
+        else if (mlds_ok) sweep([&](auto par, int t) __attribute__((always_inline)) { pass1(IntC<1>{}, par, t); });
+        else sweep([&](auto par, int t) __attribute__((always_inline)) { pass1(IntC<2>{}, par, t); });
+        if constexpr (PH == 1) {  // publish the samples; fs_thresh takes L over all the user's segments
+            if (uvalid) {
+                // high half of the ordered word (rounding down: a lower bound stays one); -inf
+                // (a missing item) as 0, which counts as no sample
+                auto s16 = [](float x) __attribute__((always_inline)) -> unsigned {
+                    return x == -INFINITY ? 0u : ord_f32(x) >> 16;
+                };
+                uint4* dst = reinterpret_cast<uint4*>(a.samp + ((bslot * a.n_lists + li) * 96 + h * 48));
+#pragma unroll
+                for (int q = 0; q < 6; ++q) {
+                    unsigned w[4];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int v0 = 8 * q + 2 * e, v1 = v0 + 1;  // sample v: t1 / t2 / t3 [v % 16] by v / 16
+                        const float x0 = v0 < 16 ? t1[v0] : v0 < 32 ? t2[v0 - 16] : t3[v0 - 32];
+                        const float x1 = v1 < 16 ? t1[v1] : v1 < 32 ? t2[v1 - 16] : t3[v1 - 32];
+                        w[e] = s16(RSX_FS_TOP == 3 || v0 < 32 ? x0 : -INFINITY) |
+                               (s16(RSX_FS_TOP == 3 || v1 < 32 ? x1 : -INFINITY) << 16);
+                    }
+                    dst[q] = make_uint4(w[0], w[1], w[2], w[3]);
+                }
+                if (h == 0) a.mcnt1[bslot * a.n_lists + li] = (uint16_t)(mfree ? min(mcount, (int64_t)0xfffe) : 0);
+            }
+            return;
+        }
         // L = the k-th largest of the lane pair's 32 * RSX_FS_TOP bounds (radix search on
         // ordered words)
         for (int bit = 31; bit >= 0; --bit) {
@@ -899,10 +983,6 @@ __device__ __forceinline__ void screen_segment(const FsArgs& a, int64_t ub, int 
                      (RSX_FS_TOP == 3 ? (int)(ord_f32(t3[r]) >= c) : 0);
             n += __shfl_xor(n, 32, kWave);
             if (n >= (mfree ? kk : a.k)) th = c;
-        }
-        if constexpr (PH == 1) {  // every segment's L is a lower bound of the user's k-th score: keep the largest
-            if (uvalid && h == 0) atomicMax(a.lbound + bslot, th);
-            return;
         }
     } else {
         th = uvalid ? a.lbound[bslot] : 0u;
@@ -926,9 +1006,7 @@ __device__ __forceinline__ void screen_segment(const FsArgs& a, int64_t ub, int 
     // keys enter the users' candidate rows (fs_tiles' rows and compaction), counts and
     // row maxima kept in LDS
     bu[NM] = u32x4{h == 0 ? cmb : 0u, 0u, 0u, 0u};
-    mpos = mp0;
-    mfetch();
-    next_mask = mfill > 0 ? ml[0] : INT_MAX;
+    mask_start();
     int cnt = 0;
     unsigned omax = 0;
     if (lane < 32) {
@@ -936,8 +1014,9 @@ __device__ __forceinline__ void screen_segment(const FsArgs& a, int64_t ub, int 
         lomax[lane] = 0u;
     }
     int qn = 0;  // queued candidates (wave-uniform)
+    int nq = 0;  // mode 9 (profiling): candidates queued by this segment
     auto compact = [&]() __attribute__((always_inline)) {
-        u64 need = __ballot(h == 0 && cnt > kCap - 64);  // room for a whole group after this
+        u64 need = __ballot(h == 0 && cnt > kCap - 64 * kDrainPer);  // room for a whole drain group after this
         while (need) {
             const int jj = __ffsll((long long)need) - 1;
             need &= need - 1;
@@ -955,23 +1034,38 @@ __device__ __forceinline__ void screen_segment(const FsArgs& a, int64_t ub, int 
     };
     const u64 ltm = lanemask_lt(lane);
     auto drain = [&](bool all) __attribute__((always_inline)) {
+        constexpr int G = 64 * kDrainPer;  // candidates per drain group: kDrainPer per lane
         int g = 0;
-        while (qn - g >= 64 || (all && qn > g)) {
-            const int n = min(64, qn - g);
+        while (qn - g >= G || (all && qn > g)) {
+            const int n = min(G, qn - g);
             __syncthreads();  // queue writes, counts
-            const unsigned e = lane < n ? queue[g + lane] : 0u;
-            const int ju = (int)(e & 31u);
-            const float tj = __shfl(tau, ju, kWave);
-            if (lane < n) {
-                const int64_t item = (int64_t)(e >> 6);
-                const float sc = (e & 32u) ? -1e10f
-                                 : a.mode == 6 ? unord_f32(ord_f32(tj) + 1u + (unsigned)lane)  // ablation: no dots
-                                               : exact_dot<D>(urows + ju * US, a.I + item * D);
-                if (sc > tj) {
-                    const int pos = atomicAdd(&lcnt[ju], 1);
-                    const u64 key = make_key(sc, (int)item);
-                    atomicMax(&lomax[ju], (unsigned)(key >> 32));
-                    base[(int64_t)ju * rowstep + pos] = key;
+            unsigned e[kDrainPer];
+            int ju[kDrainPer];
+            float tj[kDrainPer], sc[kDrainPer];
+            const float* up[kDrainPer];
+            const float* vp[kDrainPer];
+#pragma unroll
+            for (int q = 0; q < kDrainPer; ++q) {
+                e[q] = lane + 64 * q < n ? queue[g + lane + 64 * q] : 0u;
+                ju[q] = (int)(e[q] & 31u);
+                tj[q] = __shfl(tau, ju[q], kWave);
+                up[q] = urows + ju[q] * US;
+                vp[q] = a.I + (int64_t)(e[q] >> 6) * D;
+            }
+            if (a.mode == 6) {  // profiling ablation: no dots
+#pragma unroll
+                for (int q = 0; q < kDrainPer; ++q) sc[q] = unord_f32(ord_f32(tj[q]) + 1u + (unsigned)lane);
+            } else if (lane < n) {  // (lanes past n hold item 0: valid addresses, results unused)
+                exact_dots<D, kDrainPer>(up, vp, sc);
+            }
+#pragma unroll
+            for (int q = 0; q < kDrainPer; ++q) {
+                const float v = (e[q] & 32u) ? -1e10f : sc[q];
+                if (lane + 64 * q < n && v > tj[q]) {
+                    const int pos = atomicAdd(&lcnt[ju[q]], 1);
+                    const u64 key = make_key(v, (int)(e[q] >> 6));
+                    atomicMax(&lomax[ju[q]], (unsigned)(key >> 32));
+                    base[(int64_t)ju[q] * rowstep + pos] = key;
                 }
             }
             __syncthreads();
@@ -981,56 +1075,59 @@ __device__ __forceinline__ void screen_segment(const FsArgs& a, int64_t ub, int 
             g += n;
         }
         const int rest = qn - g;
-        if (g > 0 && rest > 0) {
+        if (g > 0 && rest > 0) {  // rest < G: the unscored tail to the queue's front
+            unsigned v[kDrainPer];
             __syncthreads();
-            const unsigned v = lane < rest ? queue[g + lane] : 0u;
+#pragma unroll
+            for (int q = 0; q < kDrainPer; ++q) v[q] = lane + 64 * q < rest ? queue[g + lane + 64 * q] : 0u;
             __syncthreads();
-            if (lane < rest) queue[lane] = v;
+#pragma unroll
+            for (int q = 0; q < kDrainPer; ++q)
+                if (lane + 64 * q < rest) queue[lane + 64 * q] = v[q];
         }
         qn = rest;
     };
-    auto pass2 = [&](auto par, int t) __attribute__((always_inline)) {
+    auto pass2 = [&](auto form, auto par, int t) __attribute__((always_inline)) {
         const int64_t tb = i0 + (int64_t)t * 32;
-        const unsigned mb = mask_bits(tb);
+        const unsigned mb = mask_bits(form, tb);
         floatx16 acc;
         tile(par, t, acc);
         const int rem = (int)(i1 - tb);
         const unsigned ebase = ((unsigned)(tb + 4 * h) << 6) | (unsigned)j;
         // one ballot per slot; its lanes append at queue[qn + their rank] (branch-free tests)
         auto push = [&](bool c, unsigned e) __attribute__((always_inline)) {
-            const u64 bal = __ballot(c);
+            const u64 bal = __ballot(c) & (a.mode == 8 ? 0ull : ~0ull);  // 8: profiling ablation, no candidates
             if (bal) {
                 const int rk = __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
                 if (c) queue[qn + rk] = e;
                 qn += popc64(bal);
+                if (a.mode == 9) nq += popc64(bal);
             }
         };
         const float tv = uvalid ? tau : INFINITY;  // invalid users take nothing
-        if (rem >= 32 && __ballot(tv < -1e10f) == 0ull) {
-            // every tau >= -1e10: a masked item (key -1e10) never needs queueing, so items are
-            // tested by their raw upper bounds and a hit carries its mask bit (the drain
-            // scores it -1e10, below tau)
-            const unsigned mbh = mb >> (4 * h);
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int io = (r & 3) + 8 * (r >> 2);
-                push(acc[r] > tv, (ebase + ((unsigned)io << 6)) | (((mbh >> io) & 1u) << 5));
-            }
-        } else {
-            const unsigned mbh = mb >> (4 * h);
+        // every tau >= -1e10 (wave-uniform): a masked item (key -1e10) never needs queueing,
+        // so the items are tested by their raw upper bounds and a hit carries its mask bit
+        // (the drain scores it -1e10, below tau); otherwise -- and on the chunk's last tile
+        // -- masked slots take -1e10 and missing ones -inf in place first
+        const unsigned mbh = mb >> (4 * h);
+        if (rem < 32 || __ballot(tv < -1e10f) != 0ull) {
             const int remh = rem - 4 * h;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int io = (r & 3) + 8 * (r >> 2);
-                const bool msk = (mbh >> io) & 1u;
-                const float v = msk ? -1e10f : acc[r];
-                push((v > tv) & (io < remh), (ebase + ((unsigned)io << 6)) | (msk ? 32u : 0u));
+                acc[r] = io >= remh ? -INFINITY : (((mbh >> io) & 1u) ? -1e10f : acc[r]);
             }
         }
-        if (qn >= 64) drain(false);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int io = (r & 3) + 8 * (r >> 2);
+            push(acc[r] > tv, (ebase + ((unsigned)io << 6)) | (((mbh >> io) & 1u) << 5));
+        }
+        if (qn >= 64 * kDrainPer) drain(false);
     };
     prime();
-    sweep(pass2);
+    if (mlds_ok) sweep([&](auto par, int t) __attribute__((always_inline)) { pass2(IntC<1>{}, par, t); });
+    else sweep([&](auto par, int t) __attribute__((always_inline)) { pass2(IntC<2>{}, par, t); });
     drain(true);
     __syncthreads();
     cnt = lcnt[j];
@@ -1050,6 +1147,12 @@ __device__ __forceinline__ void screen_segment(const FsArgs& a, int64_t ub, int 
         }
     }
     if (uvalid && h == 0) a.ccount[bslot * a.n_lists + li] = cnt;
+    if (a.mode == 9 && lane == 0) {  // profiling: queued / kept candidate totals into out_idx[0], [1]
+        atomicAdd(reinterpret_cast<unsigned long long*>(a.out_idx), (unsigned long long)nq);
+        int kept = 0;
+        for (int q = 0; q < 32; ++q) kept += lcnt[q];
+        atomicAdd(reinterpret_cast<unsigned long long*>(a.out_idx) + 1, (unsigned long long)kept);
+    }
     __syncthreads();  // LDS reuse by the next segment
 }
 
@@ -1063,11 +1166,11 @@ __device__ __forceinline__ void screen_segment(const FsArgs& a, int64_t ub, int 
 template <int D, int PH>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D <= 64 ? RSX_FS_SCREEN_WPE : 1))) void fs_screen(FsArgs a) {
     constexpr int US = D + 4;
-    __shared__ __attribute__((aligned(16))) float urows[32 * US];
-    __shared__ unsigned queue[64 * 17];  // pass 2 candidates: < 64 pending + one tile's (<= 16 per lane)
+    __shared__ __attribute__((aligned(16))) float urows[PH == 1 ? 4 : 32 * US];  // pass 2's f32 user rows
+    __shared__ unsigned queue[PH == 1 ? 1 : kQueueCap];  // pass 2 candidates
     __shared__ int lcnt[32];
     __shared__ unsigned lomax[32];
-    __shared__ int mlds[64 * kMaskStride];
+    __shared__ int mlds[32 * kMaskStride];
     const int64_t n_ub = (a.nb + 31) / 32;
     const int64_t nper = a.seg_waves ? a.seg_waves : n_ub;  // waves per chunk
     int64_t w;
@@ -1101,6 +1204,46 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D <= 64 ? RS
         }
         x += t1 - t0;
     }
+}
+
+// The user's L of the two-phase screen: the (k + M)-th largest of every sample its pass-1
+// segments published (M = their masked items sampled by value).  The segments cover
+// disjoint item ranges, so the samples are distinct items and at most M of the k + M at
+// or above L are masked: k unmasked items score >= L (invariant (iii) over the union).
+// One wave per user; 16-bit radix search; fewer than k + M samples: no threshold (0).
+// NW: sample pairs (u32 words) per lane, nl * 48 <= 64 NW
+template <int NW>
+__global__ __launch_bounds__(256) void fs_thresh(const uint16_t* __restrict__ samp, const uint16_t* __restrict__ mcnt,
+                                                 int nl, int64_t nb, int k, unsigned* __restrict__ lbound) {
+    const int lane = threadIdx.x & 63;
+    const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (b >= nb) return;  // whole waves
+    const unsigned m = lane < nl ? (unsigned)mcnt[b * nl + lane] : 0xffffu;
+    const u64 valid = __ballot(m != 0xffffu);  // bit l: list l has a segment
+    int mm = m != 0xffffu ? (int)m : 0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mm += __shfl_xor(mm, o, kWave);
+    const int kk = k + mm;
+    const int nwords = nl * 48;
+    const unsigned* __restrict__ w32 = reinterpret_cast<const unsigned*>(samp) + b * nwords;
+    unsigned v[2 * NW];
+#pragma unroll
+    for (int q = 0; q < NW; ++q) {  // every load before the first use
+        const int e = lane + 64 * q;
+        const unsigned x = e < nwords ? w32[e] : 0u;
+        const bool ok = e < nwords && ((valid >> (e / 48)) & 1ull);
+        v[2 * q] = ok ? (x & 0xffffu) : 0u;
+        v[2 * q + 1] = ok ? (x >> 16) : 0u;
+    }
+    unsigned th = 0;
+    for (int bit = 15; bit >= 0; --bit) {
+        const unsigned c = th | (1u << bit);
+        int n = 0;
+#pragma unroll
+        for (int q = 0; q < 2 * NW; ++q) n += popc64(__ballot(v[q] >= c));
+        if (n >= kk) th = c;
+    }
+    if (lane == 0) lbound[b] = th << 16;
 }
 
 // Exact k-th largest of the nonzero keys held E per lane (radix search with ballots,
@@ -1348,9 +1491,9 @@ static int fs_cus() {
 // wave in one round of resident slots, when that fills >= 80 % of them (one list per
 // chunk, no split); otherwise enough chunks to exceed the slots, split evenly below
 // (fs_layout).  At most 16 chunks.
-static void screen_plan(int64_t nb, int64_t ni, int d, int* n_chunks, int64_t* chunk_items) {
+static void screen_plan(int64_t nb, int64_t ni, int wps, int* n_chunks, int64_t* chunk_items) {
     const int64_t n_ub = (nb + 31) / 32;
-    const int64_t slots = (int64_t)fs_cus() * 4 * (d <= 128 ? 2 : 1);  // fs_screen: 2 waves per SIMD, 1 at d = 256
+    const int64_t slots = (int64_t)fs_cus() * 4 * wps;
     int64_t c = slots / n_ub;
     if (c < 1 || n_ub * c * 5 < slots * 4) c = (slots + n_ub - 1) / n_ub;
     if (c < 1) c = 1;
@@ -1361,11 +1504,23 @@ static void screen_plan(int64_t nb, int64_t ni, int d, int* n_chunks, int64_t* c
     *n_chunks = (int)((ni + per - 1) / per);
 }
 
-static FsLayout fs_layout(int64_t nb, int64_t ni, int k, int d) {
+// resident fs_screen waves per SIMD a layout plans for: pass 1 (and the one-launch form)
+// 2 at d <= 128 (register budget), 1 at d = 256; the pass-2 launch of the two-phase form
+// holds no pass-1 samples (fewer registers): RSX_FS_WPS2 (tuning)
+static int fs_wps(int d, int phase) {
+    static const int w2 = [] {
+        const char* e = getenv("RSX_FS_WPS2");
+        return e ? atoi(e) : 0;
+    }();
+    if (phase == 2 && w2 > 0) return w2;
+    return d <= 128 ? 2 : 1;
+}
+
+static FsLayout fs_layout(int64_t nb, int64_t ni, int k, int d, int wps) {
     FsLayout L{};
     int nw;
     L.screen = fs_use_screen(k, d, ni);
-    if (L.screen) screen_plan(nb, ni, d, &L.n_chunks, &L.chunk_items);
+    if (L.screen) screen_plan(nb, ni, wps, &L.n_chunks, &L.chunk_items);
     else fs_plan(nb, ni, d, &nw, &L.n_chunks, &L.chunk_items);
     L.n_lists = L.n_chunks;
     L.seg_slots = 1;
@@ -1377,7 +1532,7 @@ static FsLayout fs_layout(int64_t nb, int64_t ni, int k, int d) {
         return e ? atoi(e) : 1;
     }();
     if (L.screen && seg_env && (8 % C) == 0) {
-        const int64_t slots = (int64_t)fs_cus() * 4 * (d <= 128 ? 2 : 1);  // fs_screen: 2 waves per SIMD, 1 at d = 256
+        const int64_t slots = (int64_t)fs_cus() * 4 * wps;
         const int64_t wc = slots / C;
         if (n_ub * C > slots && wc >= 1) {
             int S = 1;
@@ -1401,30 +1556,55 @@ static FsLayout fs_layout(int64_t nb, int64_t ni, int k, int d) {
 }
 
 // workspace: candidate rows | counts | (screen) bf16 item copy
+// candidate lists per user: the pass-2 layout's (two-phase) or the one-launch layout's
+static int fs_lists(int64_t nb, int64_t ni, int k, int d) {
+    return std::max(fs_layout(nb, ni, k, d, fs_wps(d, 1)).n_lists, fs_layout(nb, ni, k, d, fs_wps(d, 2)).n_lists);
+}
+
 size_t fs_ws(int64_t nb, int64_t ni, int k, int d) {
-    const FsLayout L = fs_layout(nb, ni, k, d);
-    size_t bytes = fs_align((size_t)nb * L.n_lists * kCap * sizeof(u64) + (size_t)nb * L.n_lists * sizeof(int) + 512);
+    const FsLayout L = fs_layout(nb, ni, k, d, fs_wps(d, 1));
+    const int nl = fs_lists(nb, ni, k, d);
+    size_t bytes = fs_align((size_t)nb * nl * kCap * sizeof(u64) + (size_t)nb * nl * sizeof(int) + 512);
     if (L.screen) {
         const size_t ni_pad = (size_t)(ni + 31) / 32 * 32;
-        bytes += fs_align(ni_pad * (d + 16) * sizeof(__bf16));
+        bytes += fs_align((ni_pad + 32 * kScreenPadTiles) * (d + 16) * sizeof(__bf16));
         bytes += fs_align((size_t)nb * sizeof(unsigned));  // lbound
+        bytes += fs_align((size_t)nb * L.n_lists * 96 * sizeof(uint16_t));  // samp (pass-1 layout)
+        bytes += fs_align((size_t)nb * L.n_lists * sizeof(uint16_t));       // mcnt1
     }
     return bytes;
 }
 
+// L: the one-launch / pass-1 layout; L2: the pass-2 layout of the two-phase form (its own
+// chunks and segments: pass 1 only publishes per-user thresholds, pass 2 writes the lists)
 template <int D>
-static int launch_fs(FsArgs& a, const FsLayout& L, hipStream_t s) {
+static int launch_fs(FsArgs& a, const FsLayout& L, const FsLayout& L2, hipStream_t s) {
     const dim3 grid((unsigned)L.blocks);
     if (a.Ib) {  // screened path
         const int64_t ni_pad = (a.ni + 31) / 32 * 32;
         const int64_t nthr = ni_pad * (D / 4);
         hipLaunchKernelGGL((fs_prep<D>), dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, s, a.I, a.ni, ni_pad,
                            const_cast<__bf16*>(a.Ib));
-        if (a.lbound) {  // two phases: every segment of a user filters by the best of their thresholds
-            (void)hipMemsetAsync(a.lbound, 0, (size_t)a.nb * sizeof(unsigned), s);
+        if (a.mode == 9) (void)hipMemsetAsync(a.out_idx, 0, 2 * sizeof(int64_t), s);  // profiling counters
+        if (a.lbound) {  // two phases: every segment of a user filters by the user's L over all of them
+            (void)hipMemsetAsync(a.mcnt1, 0xff, (size_t)a.nb * L.n_lists * sizeof(uint16_t), s);
             hipLaunchKernelGGL((fs_screen<D, 1>), grid, dim3(64), 0, s, a);
-            if (a.mode != 5) hipLaunchKernelGGL((fs_screen<D, 2>), grid, dim3(64), 0, s, a);
-            else return last_rc();
+            {
+                const dim3 tg((unsigned)((a.nb + 3) / 4));
+                const uint16_t* sp = a.samp;
+                const uint16_t* mc = a.mcnt1;
+                const int nl = L.n_lists;  // <= 16
+                if (nl <= 4) hipLaunchKernelGGL((fs_thresh<3>), tg, dim3(256), 0, s, sp, mc, nl, a.nb, a.k, a.lbound);
+                else if (nl <= 8) hipLaunchKernelGGL((fs_thresh<6>), tg, dim3(256), 0, s, sp, mc, nl, a.nb, a.k, a.lbound);
+                else hipLaunchKernelGGL((fs_thresh<12>), tg, dim3(256), 0, s, sp, mc, nl, a.nb, a.k, a.lbound);
+            }
+            if (a.mode == 5) return last_rc();
+            a.n_chunks = L2.n_chunks;
+            a.chunk_items = L2.chunk_items;
+            a.n_lists = L2.n_lists;
+            a.seg_slots = L2.seg_slots;
+            a.seg_waves = L2.seg_waves;
+            hipLaunchKernelGGL((fs_screen<D, 2>), dim3((unsigned)L2.blocks), dim3(64), 0, s, a);
         } else {
             hipLaunchKernelGGL((fs_screen<D, 0>), grid, dim3(64), 0, s, a);
         }
@@ -1436,6 +1616,7 @@ static int launch_fs(FsArgs& a, const FsLayout& L, hipStream_t s) {
         hipLaunchKernelGGL((fs_tiles<D, 0>), grid, dim3(64), 0, s, a);
     }
     const dim3 sg((unsigned)((a.nb + 3) / 4));
+    if (a.mode == 9) return last_rc();  // profiling: out_idx holds the candidate counts
     if (a.Ib || a.mode == 0) {
         const int n = a.n_lists;
         if (n <= 2) hipLaunchKernelGGL((fs_select<2>), sg, dim3(256), 0, s, a);
@@ -1455,7 +1636,8 @@ int fs_call(const float* U, const int64_t* users, int64_t nb, const float* I, in
     if (nb == 0) return RSX_OK;
     if (!ws || ws_bytes < fs_ws(nb, ni, k, d)) return RSX_ERR_WORKSPACE;
     FsArgs a;
-    const FsLayout L = fs_layout(nb, ni, k, d);
+    const FsLayout L = fs_layout(nb, ni, k, d, fs_wps(d, 1));
+    const int nl = fs_lists(nb, ni, k, d);
     a.n_chunks = L.n_chunks;
     a.chunk_items = L.chunk_items;
     a.n_lists = L.n_lists;
@@ -1470,21 +1652,27 @@ int fs_call(const float* U, const int64_t* users, int64_t nb, const float* I, in
     a.mcol = mcol;
     a.k = k;
     a.cand = static_cast<u64*>(ws);
-    a.ccount = reinterpret_cast<int*>(static_cast<char*>(ws) + (size_t)nb * a.n_lists * kCap * sizeof(u64));
+    a.ccount = reinterpret_cast<int*>(static_cast<char*>(ws) + (size_t)nb * nl * kCap * sizeof(u64));
     a.out_val = out_val;
     a.out_idx = out_idx;
     a.Ib = nullptr;
     a.lbound = nullptr;
+    a.samp = nullptr;
+    a.mcnt1 = nullptr;
     if (L.screen) {
-        char* p = static_cast<char*>(ws) +
-                  fs_align((size_t)nb * a.n_lists * kCap * sizeof(u64) + (size_t)nb * a.n_lists * sizeof(int) + 512);
+        char* p = static_cast<char*>(ws) + fs_align((size_t)nb * nl * kCap * sizeof(u64) + (size_t)nb * nl * sizeof(int) + 512);
         a.Ib = reinterpret_cast<const __bf16*>(p);
         const size_t ni_pad = (size_t)(ni + 31) / 32 * 32;
         static const int two = [] {
             const char* e = getenv("RSX_FS_2PHASE");  // 0: both passes in one launch, per-segment thresholds
             return e ? atoi(e) : 1;
         }();
-        a.lbound = two ? reinterpret_cast<unsigned*>(p + fs_align(ni_pad * (d + 16) * sizeof(__bf16))) : nullptr;
+        char* q = p + fs_align((ni_pad + 32 * kScreenPadTiles) * (d + 16) * sizeof(__bf16));
+        a.lbound = two ? reinterpret_cast<unsigned*>(q) : nullptr;
+        q += fs_align((size_t)nb * sizeof(unsigned));
+        a.samp = reinterpret_cast<uint16_t*>(q);
+        q += fs_align((size_t)nb * L.n_lists * 96 * sizeof(uint16_t));
+        a.mcnt1 = reinterpret_cast<uint16_t*>(q);
     }
     {
         static int mode = -1;
@@ -1494,11 +1682,12 @@ int fs_call(const float* U, const int64_t* users, int64_t nb, const float* I, in
         }
         a.mode = mode;
     }
+    const FsLayout L2 = a.lbound ? fs_layout(nb, ni, k, d, fs_wps(d, 2)) : L;
     switch (d) {
-        case 32: return launch_fs<32>(a, L, s);
-        case 64: return launch_fs<64>(a, L, s);
-        case 128: return launch_fs<128>(a, L, s);
-        case 256: return launch_fs<256>(a, L, s);
+        case 32: return launch_fs<32>(a, L, L2, s);
+        case 64: return launch_fs<64>(a, L, L2, s);
+        case 128: return launch_fs<128>(a, L, L2, s);
+        case 256: return launch_fs<256>(a, L, L2, s);
         default: return RSX_ERR_UNSUPPORTED;
     }
 }
@@ -1555,7 +1744,7 @@ size_t rsx_fullsort_ws_bytes(int64_t n_batch, int64_t n_items, int32_t k) {
 
 int rsx_fullsort_plan(int64_t n_batch, int64_t n_items, int32_t d, int32_t* n_chunks, int64_t* chunk_items) {
     if (!n_chunks || !chunk_items || n_batch < 0 || n_items <= 0) return RSX_ERR_ARG;
-    const rsx::FsLayout L = rsx::fs_layout(n_batch, n_items, 50, d);  // the plan of k <= 64 calls
+    const rsx::FsLayout L = rsx::fs_layout(n_batch, n_items, 50, d, rsx::fs_wps(d, 1));  // the plan of k <= 64 calls (pass 1)
     *n_chunks = L.n_chunks;
     *chunk_items = L.chunk_items;
     return RSX_OK;

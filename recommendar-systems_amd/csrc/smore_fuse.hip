@@ -184,15 +184,22 @@ __device__ __forceinline__ Fld<D> mvt(const float* __restrict__ W, const Fld<D>&
 template <int D>
 constexpr int kLd = D + 4;
 
+// Staged by LDS-DMA (global_load_lds, 4 B a lane: a wave-instruction moves 64 consecutive
+// floats of one row, so the padded rows stay intact): every piece of the block's share is
+// in flight at once and no VGPR holds it -- a register-staged loop here waited out one
+// L2 round trip per float4 (the store needs the load), 16 of them per thread at d = 128.
 template <int D>
 __device__ __forceinline__ const float* stage_w(float* __restrict__ lds, const float* __restrict__ W) {
+    static_assert(D % 64 == 0, "stage_w: rows of whole 64-float pieces");
     __syncthreads();  // the previous weight's readers are done
-    constexpr int Q = D / 4;
-    for (int i = threadIdx.x; i < D * Q; i += blockDim.x) {
-        const int row = i / Q, c4 = i - row * Q;
-        *reinterpret_cast<float4*>(lds + row * kLd<D> + 4 * c4) = ld4(W + (int64_t)row * D + 4 * c4);
+    constexpr int PR = D / 64;        // pieces per row
+    const int lane = threadIdx.x & 63;
+    const int nw = blockDim.x >> 6;
+    for (int pc = threadIdx.x >> 6; pc < D * PR; pc += nw) {  // wave-uniform
+        const int row = pc / PR, c0 = (pc - row * PR) * 64;
+        __builtin_amdgcn_global_load_lds(W + (int64_t)row * D + c0 + lane, lds + row * kLd<D> + c0, 4, 0, 0);
     }
-    __syncthreads();
+    __syncthreads();  // (waits for the DMA: vmcnt(0) before the barrier)
     return lds;
 }
 
