@@ -42,6 +42,19 @@ __device__ __forceinline__ double group_sum_d(double x) {
 inline int hip_rc(hipError_t e) { return static_cast<int>(e); }
 inline int last_rc() { return static_cast<int>(hipGetLastError()); }
 inline hipStream_t as_stream(rsx_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
+// the current device's CU count (cached per process; 256 when the query fails)
+inline int device_cus() {
+    static int n = 0;
+    if (!n) {
+        int dev = 0, v = 0;
+        n = (hipGetDevice(&dev) == hipSuccess &&
+             hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+                ? v
+                : 256;
+        (void)hipGetLastError();
+    }
+    return n;
+}
 
 // Batch-row tagging carried by an SpMM launch (extra blocks after the work and
 // fixup blocks): row_tag[u] = row_tag[n_users + i] = tag for every triplet.

@@ -276,24 +276,32 @@ struct GateArgs {
     float* g_item;          // backward outputs
     float* g_conv[3];
     float* dz[3];           // pre-activation gradients (wgrad rows)
+    int64_t nbx;            // 64-row blocks of n (grid.x may be fewer: blocks stride over them)
 };
 
+// Blocks stride over the 64-row blocks (grid.x <= a.nbx): a gate's weight is staged once
+// per block (grid.y = 3: one gate per block row), not once per 64 rows.
 template <int D>
 __global__ __launch_bounds__(256) void gates_fwd(GateArgs a) {
     __shared__ __attribute__((aligned(16))) float wl[D * kLd<D>];
     const int lane = threadIdx.x & 63, g = lane >> 4;
-    const int64_t n0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 16;
-    const int64_t row = n0 + (lane & 15) < a.n ? n0 + (lane & 15) : -1;
-    const Fld<D> it = fload<D>(a.item, row, g);
-    // grid.y = 3: one gate per block row (three times the waves of one block per row tile)
-    const int m0 = gridDim.y > 1 ? (int)blockIdx.y : 0, m1 = gridDim.y > 1 ? m0 + 1 : 3;
+    const bool split = gridDim.y > 1;
+    if (split) stage_w<D>(wl, a.W[blockIdx.y]);
 #pragma unroll 1
-    for (int m = m0; m < m1; ++m) {
-        const Fld<D> cv = fload<D>(a.conv[m], row, g);
-        const Fld<D> s = fmap<D>(mv<D, kLd<D>>(stage_w<D>(wl, a.W[m]), a.b[m], cv, lane), sigm);
-        const Fld<D> o = a.mul ? fmap2<D>(it, s, [](float x, float y) { return x * y; })
-                               : fmap2<D>(it, s, [&](float x, float y) { return x + a.scale * y; });
-        fstore<D>(a.out[m], row, g, o);
+    for (int64_t bx = blockIdx.x; bx < a.nbx; bx += gridDim.x) {  // block-uniform
+        const int64_t n0 = (bx * 4 + (threadIdx.x >> 6)) * 16;
+        const int64_t row = n0 + (lane & 15) < a.n ? n0 + (lane & 15) : -1;
+        const Fld<D> it = fload<D>(a.item, row, g);
+        const int m0 = split ? (int)blockIdx.y : 0, m1 = split ? m0 + 1 : 3;
+#pragma unroll 1
+        for (int m = m0; m < m1; ++m) {
+            const Fld<D> cv = fload<D>(a.conv[m], row, g);
+            const float* W = split ? wl : stage_w<D>(wl, a.W[m]);
+            const Fld<D> s = fmap<D>(mv<D, kLd<D>>(W, a.b[m], cv, lane), sigm);
+            const Fld<D> o = a.mul ? fmap2<D>(it, s, [](float x, float y) { return x * y; })
+                                   : fmap2<D>(it, s, [&](float x, float y) { return x + a.scale * y; });
+            fstore<D>(a.out[m], row, g, o);
+        }
     }
 }
 
@@ -301,13 +309,16 @@ template <int D>
 __global__ __launch_bounds__(256) void gates_bwd(GateArgs a) {
     __shared__ __attribute__((aligned(16))) float wl[D * kLd<D>];
     const int lane = threadIdx.x & 63, g = lane >> 4;
-    const int64_t n0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 16;
-    const int64_t row = n0 + (lane & 15) < a.n ? n0 + (lane & 15) : -1;
-    const Fld<D> it = fload<D>(a.item, row, g);
-    Fld<D> gi = fzero<D>();
     // grid.y = 3 (residual mode): one gate per block row; g_item = sum of the three
     // upstream gradients (no sigmoid in it) is formed by the gate-0 blocks, in gate order
     const bool split = gridDim.y > 1;
+    if (split) stage_w<D>(wl, a.W[blockIdx.y]);
+#pragma unroll 1
+    for (int64_t bx = blockIdx.x; bx < a.nbx; bx += gridDim.x) {  // block-uniform
+    const int64_t n0 = (bx * 4 + (threadIdx.x >> 6)) * 16;
+    const int64_t row = n0 + (lane & 15) < a.n ? n0 + (lane & 15) : -1;
+    const Fld<D> it = fload<D>(a.item, row, g);
+    Fld<D> gi = fzero<D>();
     const int m0 = split ? (int)blockIdx.y : 0, m1 = split ? m0 + 1 : 3;
     if (split && blockIdx.y == 0) {
 #pragma unroll 1
@@ -320,7 +331,7 @@ __global__ __launch_bounds__(256) void gates_bwd(GateArgs a) {
     for (int m = m0; m < m1; ++m) {
         const Fld<D> go = a.gout[m] ? fload<D>(a.gout[m], row, g) : fzero<D>();
         const Fld<D> cv = fload<D>(a.conv[m], row, g);
-        const float* W = stage_w<D>(wl, a.W[m]);
+        const float* W = split ? wl : stage_w<D>(wl, a.W[m]);
         const Fld<D> s = fmap<D>(mv<D, kLd<D>>(W, a.b[m], cv, lane), sigm);
         Fld<D> ds;
         if (a.mul) {
@@ -335,6 +346,7 @@ __global__ __launch_bounds__(256) void gates_bwd(GateArgs a) {
         fstore<D>(a.g_conv[m], row, g, mvt<D, kLd<D>>(W, dz, lane));
     }
     if (!split) fstore<D>(a.g_item, row, g, gi);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1171,7 +1183,18 @@ int rsx_smore_gates(int32_t backward, const float* const* conv, const float* ite
     a.g_item = g_item;
     // one gate per block row, except the mul-mode backward (its g_item needs all three
     // sigmoids of a row: one block runs the three gates)
-    const dim3 grid((unsigned)(((n + 15) / 16 + 3) / 4), (backward && mul) ? 1u : 3u);
+    a.nbx = ((n + 15) / 16 + 3) / 4;
+    // blocks: the row blocks, at most RSX_GATE_BLOCKS (default: 2 per CU -- the LDS
+    // weight copy allows two; each block then strides over its row blocks)
+    const unsigned gy = (backward && mul) ? 1u : 3u;
+    static const int64_t cap_env = [] {
+        const char* e = getenv("RSX_GATE_BLOCKS");
+        return e ? (int64_t)atoll(e) : (int64_t)0;
+    }();
+    int64_t gx = a.nbx;
+    const int64_t cap = cap_env > 0 ? cap_env : (int64_t)(2 * device_cus()) / gy;
+    if (cap > 0 && gx > cap) gx = cap;
+    const dim3 grid((unsigned)gx, gy);
     hipStream_t s = as_stream(stream);
     switch (d) {
         case 64:
