@@ -851,6 +851,12 @@ typedef struct rsx_sharded_lgcn_step {
     int64_t n_items_pad;        /* rows of t and of p/m/v's item block (>= n_items) */
     int64_t union_cap;          /* per-rank slice of union_items: 2 union_cap ids (>= batch; the
                                  * unused tail is zero-filled, so every rank sends the same count) */
+    /* optional, dense schedule with row_tag and n_layers 2 or 3: [2 n_items, d] floats.
+     * The step then sums two layers' item partials per collective (an item partial
+     * needs only the rank's own user rows): 4 collectives per step at K = 3 (3 at
+     * K = 2) instead of 2K + 1, the same bytes, the compute between rounds serialised
+     * (csrc/dist.hip:sharded_fused_rounds; rsx.dist enables it with RSX_SHARDED_FUSED=1). */
+    float* xch;
 } rsx_sharded_lgcn_step;
 
 int rsx_sharded_lightgcn_step(const rsx_sharded_lgcn_step* st, rsx_stream_t stream);

@@ -466,6 +466,200 @@ int sharded_stored_layers(const rsx_sharded_lgcn_step& st, bool train, hipStream
     return 0;
 }
 
+// Fused-round step for K = 2, 3 (dense schedule, batch-row tags; st.xch = [2 n_items, d]).
+// The bipartite graph splits each K-layer chain into two interleaved ones: an item
+// partial needs only the rank's own user rows, so two layers' partials can be summed in
+// ONE collective.  Forward: [E^1_I | E^2_I] then the final item rows (K = 3), or
+// [E^1_I | final item rows] (K = 2: the final partial adds the rank's OWN E^1 partial,
+// the sum over ranks is then the mean's E^1 term).  Backward (Horner on G' = dL/dfinal
+// / (K+1)): [sum G'_I | H^1_I] then [H^2_I | item gradient] (K = 3) or the item gradient
+// (K = 2); every item partial adds the rank's own G'_I, so the sums carry G'_I once.
+// 4 collectives per step at K = 3 (3 at K = 2) instead of 2K+1, the same bytes; the
+// summed halves are copied to the layer buffers the next products read.
+int sharded_fused_rounds(const rsx_sharded_lgcn_step& st, hipStream_t s) {
+    const int d = st.d, K = st.n_layers;
+    const int64_t nu = st.n_users, ni = st.n_items, off = nu * (int64_t)d, X = ni * (int64_t)d;
+    const bool root = st.comm->rank == 0;
+    const float beta = 1.f / (float)(K + 1);
+    const int32_t tag = (int32_t)st.tag;
+    float* A = st.xch;
+    float* B = st.xch + X;
+    int rc = 0;
+    auto copy = [&](float* dst, const float* src) -> int {
+        return hip_rc(hipMemcpyAsync(dst, src, (size_t)X * sizeof(float), hipMemcpyDeviceToDevice, s));
+    };
+    auto tags = [&](rsx_epilogue& e, int flags) {
+        e.row_tag = st.row_tag;
+        e.tag = tag;
+        e.tag_dev = st.tag_dev;
+        e.tag_flags = flags;
+    };
+    // ---- forward
+    {
+        rsx_epilogue e = epi(RSX_EPI_STORE);  // E^1 item partial (this launch also tags the batch rows)
+        e.y = A;
+        TagJob tj;
+        tj.trip = st.triplets;
+        tj.batch = st.batch;
+        tj.n_users = nu;
+        tj.row_tag = st.row_tag;
+        tj.tag = tag;
+        tj.tag_dev = st.tag_dev;
+        RSX_TRY(spmm_dispatch_tagging(*st.adj_i, st.p, d, e, st.slab_i, s, tj));
+        rsx_epilogue u = epi(RSX_EPI_STORE);  // E^1 user rows (local: E^0 items are replicated)
+        u.y = st.h0;
+        RSX_TRY(spmm_dispatch(*st.adj_u, st.p, d, u, st.slab_u, s));
+    }
+    if (K == 3) {
+        rsx_epilogue e = epi(RSX_EPI_STORE);  // E^2 item partial from the own E^1 user rows
+        e.y = B;
+        RSX_TRY(spmm_dispatch(*st.adj_i, st.h0, d, e, st.slab_i, s));
+        hipEvent_t j1 = exchange(st.comm, A, 2 * X, s, &rc);
+        if (!j1) return rc;
+        RSX_TRY(wait(s, j1));
+        RSX_TRY(copy(st.h0 + off, A));  // E^1 items
+        RSX_TRY(copy(st.h1 + off, B));  // E^2 items
+        rsx_epilogue u = epi(RSX_EPI_STORE);  // E^2 user rows
+        u.y = st.h1;
+        RSX_TRY(spmm_dispatch(*st.adj_u, st.h0, d, u, st.slab_u, s));
+        rsx_epilogue f = epi(RSX_EPI_FINAL);  // final item partial; rank 0 adds the summed E^0..E^2 rows
+        f.beta = beta;
+        f.f = st.final_emb + off;
+        if (root) {
+            f.s_in = st.p + off;
+            f.r_add = st.h0 + off;
+            f.aux = st.h1 + off;
+        }
+        RSX_TRY(spmm_dispatch(*st.adj_i, st.h1, d, f, st.slab_i, s));
+        hipEvent_t j2 = exchange(st.comm, st.final_emb + off, X, s, &rc);
+        if (!j2) return rc;
+        rsx_epilogue fu = epi(RSX_EPI_FINAL);  // final user rows, batch rows only
+        fu.beta = beta;
+        fu.f = st.final_emb;
+        fu.s_in = st.p;
+        fu.r_add = st.h0;
+        fu.aux = st.h1;
+        tags(fu, RSX_TAG_ROWS);
+        RSX_TRY(spmm_dispatch(*st.adj_u, st.h1, d, fu, st.slab_u, s));
+        RSX_TRY(wait(s, j2));
+    } else {
+        rsx_epilogue f = epi(RSX_EPI_FINAL);  // final item partial: (rank 0: E^0) + own E^1 partial + own E^2 partial
+        f.beta = beta;
+        f.f = B;
+        if (root) f.s_in = st.p + off;
+        f.r_add = A;
+        RSX_TRY(spmm_dispatch(*st.adj_i, st.h0, d, f, st.slab_i, s));
+        hipEvent_t j1 = exchange(st.comm, A, 2 * X, s, &rc);
+        if (!j1) return rc;
+        RSX_TRY(wait(s, j1));
+        RSX_TRY(copy(st.h0 + off, A));             // E^1 items
+        RSX_TRY(copy(st.final_emb + off, B));      // the final item rows
+        rsx_epilogue fu = epi(RSX_EPI_FINAL);
+        fu.beta = beta;
+        fu.f = st.final_emb;
+        fu.s_in = st.p;
+        fu.r_add = st.h0;
+        tags(fu, RSX_TAG_ROWS);
+        RSX_TRY(spmm_dispatch(*st.adj_u, st.h0, d, fu, st.slab_u, s));
+    }
+    // ---- loss: G' (this rank's batch rows), R (counts with reg_cnt)
+    const float* reg_k = st.reg_cnt ? reinterpret_cast<const float*>(st.reg_cnt + 3 * (nu + ni) + 1) : nullptr;
+    if (st.reg_cnt)
+        RSX_TRY(bpr_fused_call(st.final_emb, st.p, nu, ni, d, st.triplets, st.batch, st.reg, (float)(K + 1), st.g,
+                               st.reg_cnt, st.loss_out, st.loss_acc, st.ws, st.ws_bytes, s));
+    else
+        RSX_TRY(bpr_call(RSX_BPR_LIGHTGCN, st.final_emb, st.p, nu, ni, d, st.triplets, st.batch, st.reg,
+                         (float)st.batch, st.g, st.r, st.loss_out, st.loss_acc, st.ws, st.ws_bytes, s,
+                         (float)(K + 1)));
+    // ---- backward round 1: [sum G'_I | H^1_I = sum (G'_I + A_I G'_U)]
+    RSX_TRY(copy(A, st.g + off));
+    {
+        rsx_epilogue e = epi(RSX_EPI_ADD);
+        e.y = B;
+        e.s_in = st.g + off;  // own G'_I
+        tags(e, RSX_TAG_SPARSE_X);  // X = G': this rank's batch users only
+        RSX_TRY(spmm_dispatch(*st.adj_i, st.g, d, e, st.slab_i, s));
+    }
+    hipEvent_t b1 = exchange(st.comm, A, 2 * X, s, &rc);
+    if (!b1) return rc;
+    RSX_TRY(wait(s, b1));
+    RSX_TRY(copy(st.h1 + off, A));  // sum G'_I (h1's item rows are free in the backward)
+    RSX_TRY(copy(st.h0 + off, B));  // H^1_I
+    auto h_users = [&](float* y, const float* x) -> int {  // H users = G'_U + A_U (x's item rows)
+        rsx_epilogue u = epi(RSX_EPI_ADD);
+        u.y = y;
+        u.s_in = st.g;
+        tags(u, RSX_TAG_SPARSE_S);
+        return spmm_dispatch(*st.adj_u, x, d, u, st.slab_u, s);
+    };
+    auto item_grad = [&](float* y, const float* x) -> int {  // own G'_I + A_I (x's user rows) + own R_I
+        rsx_epilogue e = epi(RSX_EPI_ADD);
+        e.y = y;
+        e.s_in = st.g + off;
+        if (st.reg_cnt) {  // own R_I from the counts (cleared here)
+            e.reg_cnt = st.reg_cnt + 3 * nu;
+            e.reg_k = reg_k;
+            e.p = st.p + off;
+        } else {
+            e.r_add = st.r + off;
+        }
+        return spmm_dispatch(*st.adj_i, x, d, e, st.slab_i, s);
+    };
+    RSX_TRY(h_users(st.h0, st.h1));  // H^1_U = G'_U + A_U sum G'_I
+    const float* gI;                  // the summed item gradient
+    const float* xa;                  // the buffer whose item rows the user Adam layer reads
+    if (K == 3) {
+        RSX_TRY(h_users(st.h1, st.h0));  // H^2_U = G'_U + A_U H^1_I (h1's item rows: sum G'_I, read above)
+        rsx_epilogue e = epi(RSX_EPI_ADD);  // H^2_I partial: own G'_I + A_I H^1_U
+        e.y = A;
+        e.s_in = st.g + off;
+        RSX_TRY(spmm_dispatch(*st.adj_i, st.h0, d, e, st.slab_i, s));
+        RSX_TRY(item_grad(B, st.h1));  // own G'_I + A_I H^2_U + own R_I
+        hipEvent_t b2 = exchange(st.comm, A, 2 * X, s, &rc);
+        if (!b2) return rc;
+        RSX_TRY(wait(s, b2));
+        RSX_TRY(copy(st.h1 + off, A));  // H^2_I
+        gI = B;
+        xa = st.h1;
+    } else {
+        RSX_TRY(item_grad(A, st.h0));  // own G'_I + A_I H^1_U + own R_I
+        hipEvent_t b2 = exchange(st.comm, A, X, s, &rc);
+        if (!b2) return rc;
+        RSX_TRY(wait(s, b2));
+        gI = A;
+        xa = st.h0;
+    }
+    {
+        rsx_epilogue u = epi(RSX_EPI_ADAM);  // user rows: g = (G'_U + A_U H^{K-1}_I) + R_U
+        u.s_in = st.g;
+        u.r_add = st.r;
+        u.p = st.p;
+        u.m = st.m;
+        u.v = st.v;
+        u.adam = st.adam;
+        u.zero0 = st.g;
+        u.zero1 = st.r;
+        if (st.reg_cnt) {
+            u.r_add = nullptr;
+            u.zero1 = nullptr;
+            u.reg_cnt = st.reg_cnt;
+            u.reg_k = reg_k;
+        }
+        tags(u, RSX_TAG_SPARSE_S | RSX_TAG_SPARSE_R | RSX_TAG_ZERO);
+        RSX_TRY(spmm_dispatch(*st.adj_u, xa, d, u, st.slab_u, s));
+        rsx_epilogue a = epi(RSX_EPI_ADAM);  // item rows, identical on every rank
+        a.s_in = gI;
+        a.p = st.p + off;
+        a.m = st.m + off;
+        a.v = st.v + off;
+        a.adam = st.adam;
+        a.zero0 = st.g + off;  // own G'_I and R_I: cleared densely
+        a.zero1 = st.reg_cnt ? nullptr : st.r + off;
+        RSX_TRY(rowwise_dispatch(ni, d, a, s));
+    }
+    return 0;
+}
+
 bool valid(const rsx_sharded_lgcn_step* st) {
     if (!st || !st->adj_u || !st->adj_i || !st->comm || !st->p || !st->final_emb || st->n_layers < 1 ||
         st->n_layers > 30 || st->n_users < 0 || st->n_items <= 0)
@@ -580,6 +774,7 @@ int rsx_sharded_lightgcn_step(const rsx_sharded_lgcn_step* st, rsx_stream_t stre
     const int d = st->d, K = st->n_layers;
     if (st->row_tag && (K == 2 || K == 3)) {
         if (!st->tag_dev && (st->tag <= 0 || st->tag > INT32_MAX)) return RSX_ERR_ARG;
+        if (st->xch && !st->union_items) return sharded_fused_rounds(*st, s);
         return sharded_stored_layers(*st, true, s);
     }
     const int64_t nu = st->n_users, ni = st->n_items, off = nu * (int64_t)d;

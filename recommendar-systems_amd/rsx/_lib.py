@@ -90,7 +90,8 @@ class ShardedStep(C.Structure):
                 ("r", P), ("t", P), ("slab_u", P), ("slab_i", P), ("triplets", P), ("batch", I64),
                 ("adam", Adam), ("loss_out", P), ("loss_acc", P), ("ws", P), ("ws_bytes", C.c_size_t),
                 ("comm", P), ("row_tag", P), ("tag", I64), ("tag_dev", P), ("reg_cnt", P),
-                ("union_items", P), ("item_tag", P), ("cbuf0", P), ("cbuf1", P), ("n_items_pad", I64), ("union_cap", I64)]
+                ("union_items", P), ("item_tag", P), ("cbuf0", P), ("cbuf1", P), ("n_items_pad", I64), ("union_cap", I64),
+                ("xch", P)]
 
 
 RSX_COLL_ALLREDUCE, RSX_COLL_ALLGATHER, RSX_COLL_REDUCESCATTER = 0, 1, 2

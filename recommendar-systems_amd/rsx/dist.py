@@ -208,6 +208,15 @@ class ShardedLightGCNEngine:
         handshake), or — any other backend, tests — the host hook driving this group's
         all_reduce on host copies of the exchanged rows."""
         lib = L.lib()
+        # the fused-round schedule (RSX_SHARDED_FUSED=1; dense, K = 2, 3, batch-row tags):
+        # two layers' item partials per collective, 4 collectives per K = 3 step instead of
+        # 7 (csrc/dist.hip:sharded_fused_rounds).  Off by default: it saves three collective
+        # latencies but serialises the compute the per-layer schedule hides behind its
+        # exchanges (one rank: 0.236 vs 0.219 ms/step; DESIGN.md §6)
+        self.xch = None
+        if (not self.sparse and self.row_tag is not None and self.K in (2, 3)
+                and os.environ.get("RSX_SHARDED_FUSED", "0") == "1"):
+            self.xch = torch.zeros(2 * self.n_items, self.d, dtype=torch.float32, device=self.be.device)
         comm = C.c_void_p()
         if dist.get_backend(self.group) == "nccl":
             nb = int(lib.rsx_comm_unique_id_bytes())
@@ -223,6 +232,8 @@ class ShardedLightGCNEngine:
             views = [self.t, self._p_full[nu:]] + [getattr(self, k)[nu:] for k in ("h0", "h1", "final", "g", "r")]
             if self.sparse:
                 views += [self.union, self.cbuf0, self.cbuf1]
+            if self.xch is not None:
+                views.append(self.xch)
             self._views = {v.data_ptr(): v.view(-1) for v in views}
 
             def host_collective(op, ptr, count, dtype, _ctx):
@@ -259,6 +270,7 @@ class ShardedLightGCNEngine:
         if self.sparse and self.row_tag is not None:
             st.union_items, st.item_tag = self.union.data_ptr(), self.item_tag.data_ptr()
             st.cbuf0, st.cbuf1 = self.cbuf0.data_ptr(), self.cbuf1.data_ptr()
+        st.xch = self.xch.data_ptr() if self.xch is not None else None
         # the one-launch BPR (regulariser as per-row occurrence counts, applied and
         # cleared by the user Adam layer and the last item partial), as the single engine
         self.reg_cnt = None

@@ -17,9 +17,10 @@ from test_dist_gloo import D, K, LR, NI, NU, REG, _local_graph
 pytestmark = pytest.mark.gpu
 
 
-def _worker(rank, world, port, out_dir, native, sparse, k=K):
+def _worker(rank, world, port, out_dir, native, sparse, k=K, fused=True):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
+    os.environ["RSX_SHARDED_FUSED"] = "1" if fused else "0"
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from rsx.dist import ShardedLightGCNEngine
 
@@ -31,6 +32,8 @@ def _worker(rank, world, port, out_dir, native, sparse, k=K):
     eng = ShardedLightGCNEngine(tu, ti, NU, NI, D, k, REG, LR, "cuda:0", U0, I0, batch=16, native=native,
                                 sparse=sparse)
     assert eng.native == native and eng.sparse == sparse
+    if native:  # the fused-round schedule: dense, K = 2, 3 (csrc/dist.hip:sharded_fused_rounds)
+        assert (getattr(eng, "xch", None) is not None) == (fused and not sparse and k in (2, 3))
     f0 = eng.forward().cpu().clone()
     eng.step(triplets=torch.from_numpy(trip).cuda())
     p1 = eng.p.cpu().numpy()
@@ -51,16 +54,20 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("native,sparse,k", [(False, False, 3), (True, False, 3), (False, True, 3), (True, True, 3),
-                                             (True, False, 4), (False, False, 4)])
-def test_sharded_hip_step_matches_global_objective(native, sparse, k):
+@pytest.mark.parametrize("native,sparse,k,fused", [(False, False, 3, True), (True, False, 3, True),
+                                                   (True, False, 3, False), (True, False, 2, True),
+                                                   (False, True, 3, True), (True, True, 3, True),
+                                                   (True, False, 4, True), (False, False, 4, True)])
+def test_sharded_hip_step_matches_global_objective(native, sparse, k, fused):
     """sparse: the union-row exchange + reduce-scatter / owner Adam / all-gather schedule
-    (csrc/dist.hip with the host hook's collectives when native).  k = 4: the
-    reference's default depth, the native step's dense (untagged) form."""
+    (csrc/dist.hip with the host hook's collectives when native).  Native dense K = 2, 3:
+    the fused-round schedule (two layers' item partials per collective), fused=False the
+    one-exchange-per-layer stored-layer step.  k = 4: the reference's default depth, the
+    native step's dense (untagged) form."""
     world = 2
     K = k
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(world, _free_port(), d, native, sparse, k), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, _free_port(), d, native, sparse, k, fused), nprocs=world, join=True)
         res = [dict(np.load(os.path.join(d, f"r{r}.npz"))) for r in range(world)]
     gu, gi, trips = [], [], []
     for r in range(world):
@@ -94,12 +101,10 @@ def test_sharded_hip_step_matches_global_objective(native, sparse, k):
     assert np.isfinite(res[0]["after"]).all()
 
 
-SPARSE = True  # the one-rank RCCL run exercises the sparse schedule's collectives (all-gather, reduce-scatter)
-
-
-def _native_worker(rank, world, port, out_dir):
+def _native_worker(rank, world, port, out_dir, SPARSE=True):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
+    os.environ["RSX_SHARDED_FUSED"] = "0" if SPARSE else "1"  # dense: the fused-round schedule, graph-captured
     torch.cuda.set_device(0)
     dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
     from rsx.dist import ShardedLightGCNEngine
@@ -156,12 +161,14 @@ def _native_worker(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
-def test_native_sharded_step_equals_python_sequence():
+@pytest.mark.parametrize("sparse", [True, False])
+def test_native_sharded_step_equals_python_sequence(sparse):
     """csrc/dist.hip's one-call step over an RCCL communicator (one rank here: the box
     has one GPU) equals the Python-issued sequence it restates: the forward bit for
-    bit, training within 1e-5."""
+    bit, training within 1e-5.  sparse: the sparse schedule's collectives (all-gather,
+    reduce-scatter); dense: the fused-round schedule, graph-captured too."""
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_native_worker, args=(1, _free_port(), d), nprocs=1, join=True)
+        mp.spawn(_native_worker, args=(1, _free_port(), d, sparse), nprocs=1, join=True)
         z = dict(np.load(os.path.join(d, "native.npz")))
     # forward before any step: same kernels, same order -> bit-identical; after the
     # steps the BPR gradient scatter's float atomics (duplicate rows in a batch, as the
