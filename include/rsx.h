@@ -571,7 +571,9 @@ int rsx_smore_pref(int32_t backward, const float* const* W, const float* const* 
  * block is row-local).  Logical row r < n is table row rows[r] (rows may repeat):
  *   forward: all_out / side_out [n, d] compact; content_out / fusion_out (optional)
  *            receive the gathered content / fusion rows (the InfoNCE content rows and
- *            a weight-gradient input); the dropout key is the table row.
+ *            a weight-gradient input); the dropout key is the table row.  With the
+ *            scratch hv ([n, d], optional) the three views' chains run as three block
+ *            rows and a combine pass adds them (the same arithmetic, shorter chains).
  *   backward: g_all / g_side / g_content_in (gradient of content_out, optional) are
  *            compact; g_content / g_image / g_text / g_fusion are full [N, d] tables
  *            the row gradients are ADDED into (zero them first); hv / ht / dz compact.
@@ -596,7 +598,9 @@ int rsx_smore_wgrad(int32_t n_pairs, const float* const* dz, const float* const*
  *   loss_out[1] = InfoNCE(side[users], content[users], tau)                   (cl_users)
  * InfoNCE(a, b) = mean_i -log(exp(<a_i, b_i>/tau) / sum_j exp(<a_i, b_j>/tau)) on
  * F.normalize'd rows.  The workspace [rsx_smore_infonce_ws_bytes] written by the
- * forward (normalised rows, norms, row sums) is read by the backward, which ADDS
+ * forward (normalised rows, norms, row sums and, for batch <= 4096, the two terms'
+ * [batch x batch] exp(S / tau) tiles: the backward reads them instead of recomputing
+ * the similarity products) is read by the backward, which ADDS
  * g_loss[0] * d cl_items + g_loss[1] * d cl_users into g_side / g_content [N, d].
  */
 size_t rsx_smore_infonce_ws_bytes(int64_t batch, int32_t d);
@@ -679,6 +683,17 @@ int rsx_adam_multi_scaled(int32_t count, float* const* p, const float* const* g,
                           const int64_t* const* step_dev, const int64_t* n, float lr, float beta1, float beta2,
                           float eps, float weight_decay, float grad_scale, const double* lr_dev,
                           const int32_t* halt, rsx_stream_t stream);
+/* The same with the mirror gradient's restore folded in (reference
+ * src/common/trainer.py:332-335, `p.add_(+alpha_eff * lr * g)` then optimizer.step()):
+ * each p first becomes p + rx * float(*ralpha * rmult) (with lr_dev:
+ * float(*ralpha * (rmult * *lr_dev))), two roundings as rsx_axpy_multi, then the Adam
+ * update of rsx_adam_multi_scaled — bit-equal to rsx_axpy_multi followed by it, with
+ * one pass over p instead of two.  rx[i]: tensor i's saved gradient g(theta); rx and
+ * ralpha are both NULL (no restore) or both given. */
+int rsx_adam_multi_mg(int32_t count, float* const* p, const float* const* g, float* const* m, float* const* v,
+                      const int64_t* const* step_dev, const int64_t* n, float lr, float beta1, float beta2, float eps,
+                      float weight_decay, float grad_scale, const double* lr_dev, const int32_t* halt,
+                      const float* const* rx, const double* ralpha, double rmult, rsx_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
 /* SMORE kNN item graph (knn.hip)                                             */

@@ -509,6 +509,134 @@ __global__ __launch_bounds__(256) void pref_bwd(PrefArgs a) {
     }
 }
 
+// The batch-row forward as three block rows (blockIdx.y): 0 the fusion view x3 = fp * FE
+// (into `side`) and the gathered C / FE rows, 1 the image view x1 (into `all`), 2 the text
+// view x2 (into the scratch `hv`): three chains of <= 3 matrix products instead of one
+// of 7; pref_combine then forms side = ((x1 + x2) + x3) / 3 and all = C + side, pref_fwd's
+// arithmetic element for element.
+template <int D>
+__global__ __launch_bounds__(256) void pref_fwd_rows(PrefArgs a) {
+    __shared__ __attribute__((aligned(16))) float wl[D * kLd<D>];
+    const int lane = threadIdx.x & 63, g = lane >> 4;
+    const int64_t n0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 16;
+    const int64_t out = n0 + (lane & 15) < a.n ? n0 + (lane & 15) : -1;
+    const int64_t row = src_row(a, out);
+    const uint64_t seed = a.p_drop > 0.f ? (uint64_t)*a.seed : 0;
+    const auto mul = [](float x, float y) { return x * y; };
+    const auto lin = [&](int k, const Fld<D>& x) { return mv<D, kLd<D>>(stage_w<D>(wl, a.W[k]), a.b[k], x, lane); };
+    const int part = (int)blockIdx.y;
+    if (part == 0) {
+        const Fld<D> C = fload<D>(a.C, row, g);
+        fstore<D>(a.c_out, out, g, C);
+        Fld<D> fp = fmap<D>(lin(kWfp, C), sigm);
+        if (a.p_drop > 0.f) fp = fmap2<D>(fp, drop_scale<D>(seed, 2, row, g, a.p_drop, a.drop_scale), mul);
+        const Fld<D> FE = fload<D>(a.FE, row, g);
+        fstore<D>(a.fe_out, out, g, FE);
+        fstore<D>(a.side, out, g, fmap2<D>(fp, FE, mul));
+        return;
+    }
+    const int v = part - 1;
+    Fld<D> s;
+    {
+        const Fld<D> h = fmap<D>(lin(v ? kW1t : kW1v, fload<D>(a.FE, row, g)), tanh_);
+        s = softmax_row<D>(lin(v ? kW2t : kW2v, h));
+    }
+    Fld<D> pg = fmap<D>(lin(v ? kWtp : kWip, fload<D>(a.C, row, g)), sigm);
+    if (a.p_drop > 0.f) pg = fmap2<D>(pg, drop_scale<D>(seed, v, row, g, a.p_drop, a.drop_scale), mul);
+    const Fld<D> x = fmap3<D>(pg, s, fload<D>(v ? a.TE : a.IE, row, g), [](float p, float q, float e) { return p * (q * e); });
+    fstore<D>(v ? a.hv : a.all, out, g, x);
+}
+
+// side = ((x1 + x2) + x3) * (1/3), all = C + side over the compact rows (float4 a thread)
+template <int D>
+__global__ __launch_bounds__(256) void pref_combine(PrefArgs a) {
+    const int64_t e = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+    if (e >= a.n * D) return;
+    const int64_t r = e / D, f = e % D;
+    const float4 x1 = ld4(a.all + e), x2 = ld4(a.hv + e), x3 = ld4(a.side + e);
+    const float4 c = a.c_out ? ld4(a.c_out + e) : ld4(a.C + src_row(a, r) * D + f);
+    const float4 sd = make_float4(((x1.x + x2.x) + x3.x) * (1.f / 3.f), ((x1.y + x2.y) + x3.y) * (1.f / 3.f),
+                                  ((x1.z + x2.z) + x3.z) * (1.f / 3.f), ((x1.w + x2.w) + x3.w) * (1.f / 3.f));
+    st4(a.side + e, sd);
+    st4(a.all + e, make_float4(c.x + sd.x, c.y + sd.y, c.z + sd.z, c.w + sd.w));
+}
+
+// The batch-row backward (rsx_smore_pref_rows, gradients added by atomics): blockIdx.y = 0
+// the fusion view + the pass-through terms, 1 the image view, 2 the text view — the same
+// arithmetic as pref_bwd's split form, ordered so that few row fields are live at once
+// (at d = 128 a field is 32 VGPRs a lane: pref_bwd's order keeps ~9 of them across its
+// matrix products and spills): the gate product first (C then dead), the query MLP from
+// FE (dead after), tanh rows reloaded from the hv / ht rows this kernel wrote, each view's
+// gC / gFE share added as soon as it is formed.
+template <int D>
+__global__ __launch_bounds__(256) void pref_bwd_rows(PrefArgs a) {
+    __shared__ __attribute__((aligned(16))) float wl[D * kLd<D>];
+    const int lane = threadIdx.x & 63, g = lane >> 4;
+    const int64_t n0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 16;
+    const int64_t out = n0 + (lane & 15) < a.n ? n0 + (lane & 15) : -1;
+    const int64_t row = src_row(a, out);
+    const uint64_t seed = a.p_drop > 0.f ? (uint64_t)*a.seed : 0;
+    const auto mul = [](float x, float y) { return x * y; };
+    const auto add = [](float x, float y) { return x + y; };
+    const auto sig_bwd = [](float gy, float y) { return gy * ((1.f - y) * y); };
+    const auto g1_of = [&]() __attribute__((always_inline)) {  // d side / 3 (each stacked view's share)
+        const Fld<D> gA = fload<D>(a.g_all, out, g);
+        return a.g_side ? fmap2<D>(gA, fload<D>(a.g_side, out, g), [](float u, float v) { return (u + v) * (1.f / 3.f); })
+                        : fmap<D>(gA, [](float u) { return u * (1.f / 3.f); });
+    };
+    const int part = (int)blockIdx.y;
+    if (part == 0) {  // fusion view x3 = fp * FE, and d all -> d content
+        const float* W = stage_w<D>(wl, a.W[kWfp]);
+        const Fld<D> sf = fmap<D>(mv<D, kLd<D>>(W, a.b[kWfp], fload<D>(a.C, row, g), lane), sigm);
+        const Fld<D> mf = a.p_drop > 0.f ? drop_scale<D>(seed, 2, row, g, a.p_drop, a.drop_scale) : Fld<D>{};
+        const Fld<D> g1 = g1_of();
+        Fld<D> dp = fmap2<D>(g1, fload<D>(a.FE, row, g), mul);
+        if (a.p_drop > 0.f) dp = fmap2<D>(dp, mf, mul);
+        const Fld<D> dz = fmap2<D>(dp, sf, sig_bwd);
+        fstore<D>(a.dz[kWfp], out, g, dz);
+        const Fld<D> fp = a.p_drop > 0.f ? fmap2<D>(sf, mf, mul) : sf;
+        fatomic<D>(a.gFE, row, g, fmap2<D>(g1, fp, mul));
+        const Fld<D> gA = fload<D>(a.g_all, out, g);
+        const Fld<D> gC = a.g_cin ? fmap2<D>(gA, fload<D>(a.g_cin, out, g), add) : gA;
+        fatomic<D>(a.gC, row, g, fmap2<D>(gC, mvt<D, kLd<D>>(W, dz, lane), add));
+        return;
+    }
+    const int v = part - 1;  // 0: image view, 1: text view
+    const int w1 = v ? kW1t : kW1v, w2 = v ? kW2t : kW2v, wp = v ? kWtp : kWip;
+    // the view's preference gate on C (dropout mask applied after the sigmoid)
+    const Fld<D> sp = fmap<D>(mv<D, kLd<D>>(stage_w<D>(wl, a.W[wp]), a.b[wp], fload<D>(a.C, row, g), lane), sigm);
+    Fld<D> s;
+    {
+        const Fld<D> h = fmap<D>(mv<D, kLd<D>>(stage_w<D>(wl, a.W[w1]), a.b[w1], fload<D>(a.FE, row, g), lane), tanh_);
+        fstore<D>(v ? a.ht : a.hv, out, g, h);
+        s = softmax_row<D>(mv<D, kLd<D>>(stage_w<D>(wl, a.W[w2]), nullptr, h, lane));
+    }
+    const Fld<D> mp = a.p_drop > 0.f ? drop_scale<D>(seed, v, row, g, a.p_drop, a.drop_scale) : Fld<D>{};
+    const Fld<D> pp = a.p_drop > 0.f ? fmap2<D>(sp, mp, mul) : sp;
+    const Fld<D> g1 = g1_of();
+    Fld<D> da;  // d (s * E)
+    {
+        const Fld<D> E = fload<D>(v ? a.TE : a.IE, row, g);
+        // x = pp * (s * E)
+        Fld<D> dpp = fmap3<D>(g1, s, E, [](float u, float q, float e) { return u * (q * e); });
+        if (a.p_drop > 0.f) dpp = fmap2<D>(dpp, mp, mul);
+        const Fld<D> dzp = fmap2<D>(dpp, sp, sig_bwd);
+        fstore<D>(a.dz[wp], out, g, dzp);
+        fatomic<D>(a.gC, row, g, mvt<D, kLd<D>>(stage_w<D>(wl, a.W[wp]), dzp, lane));
+        da = fmap2<D>(g1, pp, mul);
+        fatomic<D>(v ? a.gTE : a.gIE, row, g, fmap2<D>(da, s, mul));
+        da = fmap2<D>(da, E, mul);  // d softmax output
+    }
+    const float dot = rsum<D>(fmap2<D>(da, s, mul));
+    const Fld<D> dq = fmap2<D>(s, da, [&](float y, float gy) { return y * (gy - dot); });
+    fstore<D>(a.dz[w2], out, g, dq);
+    const Fld<D> dh = mvt<D, kLd<D>>(stage_w<D>(wl, a.W[w2]), dq, lane);
+    const Fld<D> h = fload<D>(v ? a.ht : a.hv, out, g);  // this lane's own store above
+    const Fld<D> dz1 = fmap2<D>(dh, h, [](float gy, float y) { return gy * (1.f - y * y); });
+    fstore<D>(a.dz[w1], out, g, dz1);
+    fatomic<D>(a.gFE, row, g, mvt<D, kLd<D>>(stage_w<D>(wl, a.W[w1]), dz1, lane));
+}
+
 // ---------------------------------------------------------------------------
 // batched weight gradients: dW_p = dZ_p^T X_p, db_p = colsum(dZ_p)
 // ---------------------------------------------------------------------------
@@ -692,7 +820,10 @@ struct NceArgs {
     float gscale;
     float* g1;               // d src1 [N, D] (accumulated)
     float* g2;               // d src2
+    float* E;                // ws (B <= kNceStoreMax): [2][B][B] exp(S / tau), written by the forward,
+                             // read by the backward instead of recomputing S (NULL: recompute)
 };
+constexpr int64_t kNceStoreMax = 4096;
 
 template <int D>
 __device__ __forceinline__ Fld<D> nce_load_norm(const NceArgs& a, int term, int view, int64_t b, int g, float* nrm_out) {
@@ -750,9 +881,22 @@ __global__ __launch_bounds__(64 * kNceWaves) void nce_fwd(NceArgs a) {
         const Fld<D> Y2 = fload<D>(n2, row_of(mt + 2 * kNceWaves), g);  // two tiles ahead, in flight
         const int64_t m0 = mt * 16;
         const floatx4 sv = tile_dot<D>(Y0, X);  // s[r] = <own c, other m0 + 4g + r>
+        floatx4 ev;
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-            if (m0 + 4 * g + r < B) es += expf(sv[r] / a.tau);
+        for (int r = 0; r < 4; ++r) {
+            ev[r] = m0 + 4 * g + r < B ? expf(sv[r] / a.tau) : 0.f;
+            es += ev[r];  // (+0 for a column past B: the sum is unchanged)
+        }
+        if (a.E && bo >= 0) {  // E[term][own][m0 + 4g .. +3] for the backward
+            float* er = a.E + ((int64_t)term * B + bo) * B + m0 + 4 * g;
+            if ((B & 3) == 0 && m0 + 4 * g + 3 < B) {
+                *reinterpret_cast<floatx4*>(er) = ev;
+            } else {
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    if (m0 + 4 * g + r < B) er[r] = ev[r];
+            }
+        }
         Y0 = Y1;
         Y1 = Y2;
     }
@@ -818,19 +962,47 @@ __global__ __launch_bounds__(64 * kNceWaves) void nce_bwd(NceArgs a) {
             }
         return t;
     };
+    // exp(S / tau) of own row c and other rows mt*16 + 4g + r as the forward wrote it
+    // (E[term][view1 row][view2 row]; 0 past B or for a missing own row)
+    const float* eb = a.E ? a.E + (int64_t)term * B * B : nullptr;
+    auto e_of = [&](int64_t mt) {
+        floatx4 ev = {0.f, 0.f, 0.f, 0.f};
+        if (!eb || bo < 0 || mt >= ntile) return ev;
+        const int64_t m0 = mt * 16 + 4 * g;
+        if (mode == 0) {
+            const float* er = eb + bo * B + m0;
+            if ((B & 3) == 0 && m0 + 3 < B) {
+                ev = *reinterpret_cast<const floatx4*>(er);
+            } else {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) ev[r] = m0 + r < B ? er[r] : 0.f;
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) ev[r] = m0 + r < B ? eb[(m0 + r) * B + bo] : 0.f;
+        }
+        return ev;
+    };
     Fld<D> Y = fload<D>(oth_n, row_of(w), g);
     floatx4 tv = ttl_of(w);
+    floatx4 ev = e_of(w);
     for (int64_t mt = w; mt < ntile; mt += kNceWaves) {
         const Fld<D> Yn = fload<D>(oth_n, row_of(mt + kNceWaves), g);  // next tile, in flight
         const floatx4 tvn = ttl_of(mt + kNceWaves);
+        const floatx4 evn = e_of(mt + kNceWaves);
         const int64_t m0 = mt * 16;
-        const floatx4 s = tile_dot<D>(Y, X);
         // P for own row c and other rows m0 + 4g + r
         floatx4 p;
+        if (eb) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const bool ok = m0 + 4 * g + r < B;
-            p[r] = ok ? expf(s[r] / a.tau) / (mode == 0 ? ttl_own : tv[r]) : 0.f;
+            for (int r = 0; r < 4; ++r) p[r] = (bo >= 0 && m0 + 4 * g + r < B) ? ev[r] / (mode == 0 ? ttl_own : tv[r]) : 0.f;
+        } else {
+            const floatx4 s = tile_dot<D>(Y, X);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const bool ok = m0 + 4 * g + r < B;
+                p[r] = ok ? expf(s[r] / a.tau) / (mode == 0 ? ttl_own : tv[r]) : 0.f;
+            }
         }
         // O^T[k][own] += sum_m Y^T[k][m] P^T[m][own] (K slot (r, g) = other row m0 + 4g + r):
         // the A operand is the tile transposed, through this wave's LDS copy
@@ -849,6 +1021,7 @@ __global__ __launch_bounds__(64 * kNceWaves) void nce_bwd(NceArgs a) {
         __builtin_amdgcn_wave_barrier();
         Y = Yn;
         tv = tvn;
+        ev = evn;
     }
     __syncthreads();
     floatx4* red = reinterpret_cast<floatx4*>(sm);  // [wave][lane][T]
@@ -902,7 +1075,18 @@ struct AdamList {
     float gscale;        // the gradient is g * gscale (f32 product, as torch's grad.mul_(s)); 1 = none
     const double* lr_dev;  // if non-NULL the learning rate is read here (graph replays across lr changes)
     const int32_t* halt;   // if non-NULL and *halt != 0 (a NaN loss, rsx_nan_gate) nothing is updated
+    // the mirror gradient's restore folded in (rsx_adam_multi_mg): with ralpha non-NULL,
+    // p = p + rx * float(*ralpha * rmult [* lr]) first (axpy_multi's two roundings), then Adam
+    const float* rx[kAdamMax];
+    const double* ralpha;
+    double rmult;
 };
+
+// y + x * s with two roundings (torch's mul then add_; no contraction): axpy_multi's arithmetic
+__device__ __forceinline__ float restore1(float y, float x, float s) {
+#pragma clang fp contract(off)
+    return y + x * s;
+}
 
 __global__ __launch_bounds__(256) void adam_multi(AdamList L) {
     if (L.halt && *L.halt) return;
@@ -923,6 +1107,8 @@ __global__ __launch_bounds__(256) void adam_multi(AdamList L) {
     float* __restrict__ v = L.v[t];
     const int64_t base = ((int64_t)blockIdx.x - L.blk[t]) * kAdamPerBlock;
     const int64_t n = L.n[t];
+    const float* __restrict__ rx = L.ralpha ? L.rx[t] : nullptr;
+    const float rs = rx ? (float)(*L.ralpha * (L.lr_dev ? L.rmult * *L.lr_dev : L.rmult)) : 0.f;
     if ((L.vec4 >> t) & 1u) {
 #pragma unroll
         for (int k = 0; k < kAdamPerBlock / 1024; ++k) {
@@ -930,6 +1116,11 @@ __global__ __launch_bounds__(256) void adam_multi(AdamList L) {
             if (i < n) {
                 float4 pp = ld4(p + i), mm = ld4(m + i), vv = ld4(v + i);
                 float4 gg = ld4(gr + i);
+                if (rx) {
+                    const float4 xx = ld4(rx + i);
+                    pp = make_float4(restore1(pp.x, xx.x, rs), restore1(pp.y, xx.y, rs), restore1(pp.z, xx.z, rs),
+                                     restore1(pp.w, xx.w, rs));
+                }
                 if (L.gscale != 1.f) gg = mul4(L.gscale, gg);
                 adam_elem(c, pp.x, mm.x, vv.x, gg.x);
                 adam_elem(c, pp.y, mm.y, vv.y, gg.y);
@@ -947,6 +1138,7 @@ __global__ __launch_bounds__(256) void adam_multi(AdamList L) {
         const int64_t i = base + k * 256 + threadIdx.x;
         if (i < n) {
             float pp = p[i], mm = m[i], vv = v[i];
+            if (rx) pp = restore1(pp, rx[i], rs);
             adam_elem(c, pp, mm, vv, L.gscale != 1.f ? gr[i] * L.gscale : gr[i]);
             p[i] = pp;
             m[i] = mm;
@@ -981,6 +1173,7 @@ struct PairList {
     int64_t n[kAdamMax];
     int64_t blk[kAdamMax + 1];
     int32_t count;
+    uint32_t vec4;  // bit i: pair i is float4-aligned with n % 4 == 0
 };
 
 __device__ __forceinline__ int list_slot(const PairList& L) {
@@ -994,12 +1187,30 @@ __global__ __launch_bounds__(256) void mg_sumsq(PairList L, double* partial) {
     const int t = list_slot(L);
     const int64_t base = ((int64_t)blockIdx.x - L.blk[t]) * kAdamPerBlock;
     double sg = 0.0, sp = 0.0;
-    for (int k = 0; k < kAdamPerBlock / 256; ++k) {
-        const int64_t i = base + k * 256 + threadIdx.x;
-        if (i < L.n[t]) {
-            const double gv = L.x[t][i], pv = L.y[t][i];
-            sg += gv * gv;
-            sp += pv * pv;
+    if ((L.vec4 >> t) & 1u) {  // float4 loads, both of a thread's chunks in flight together
+        float4 gv[kAdamPerBlock / 1024], pv[kAdamPerBlock / 1024];
+#pragma unroll
+        for (int k = 0; k < kAdamPerBlock / 1024; ++k) {
+            const int64_t i = base + 4 * (k * 256 + threadIdx.x);
+            const bool ok = i < L.n[t];
+            gv[k] = ok ? ld4(L.x[t] + i) : f4(0.f);
+            pv[k] = ok ? ld4(L.y[t] + i) : f4(0.f);
+        }
+#pragma unroll
+        for (int k = 0; k < kAdamPerBlock / 1024; ++k) {
+            sg += (double)gv[k].x * gv[k].x + (double)gv[k].y * gv[k].y + (double)gv[k].z * gv[k].z +
+                  (double)gv[k].w * gv[k].w;
+            sp += (double)pv[k].x * pv[k].x + (double)pv[k].y * pv[k].y + (double)pv[k].z * pv[k].z +
+                  (double)pv[k].w * pv[k].w;
+        }
+    } else {
+        for (int k = 0; k < kAdamPerBlock / 256; ++k) {
+            const int64_t i = base + k * 256 + threadIdx.x;
+            if (i < L.n[t]) {
+                const double gv = L.x[t][i], pv = L.y[t][i];
+                sg += gv * gv;
+                sp += pv * pv;
+            }
         }
     }
     __shared__ double red[2][4];
@@ -1070,6 +1281,17 @@ __global__ __launch_bounds__(256) void axpy_multi(PairList L, const double* alph
     const int64_t base = ((int64_t)blockIdx.x - L.blk[t]) * kAdamPerBlock;
     float* __restrict__ y = L.y[t];
     const float* __restrict__ x = L.x[t];
+    if ((L.vec4 >> t) & 1u) {
+#pragma unroll
+        for (int k = 0; k < kAdamPerBlock / 1024; ++k) {
+            const int64_t i = base + 4 * (k * 256 + threadIdx.x);
+            if (i < L.n[t]) {
+                const float4 yy = ld4(y + i), xx = ld4(x + i);
+                st4(y + i, make_float4(yy.x + xx.x * s, yy.y + xx.y * s, yy.z + xx.z * s, yy.w + xx.w * s));
+            }
+        }
+        return;
+    }
 #pragma unroll
     for (int k = 0; k < kAdamPerBlock / 256; ++k) {
         const int64_t i = base + k * 256 + threadIdx.x;
@@ -1264,16 +1486,30 @@ int rsx_smore_pref_rows(int32_t backward, const float* const* W, const float* co
     a.c_out = backward ? nullptr : content_out;
     a.fe_out = backward ? nullptr : fusion_out;
     a.g_cin = backward ? g_content_in : nullptr;
-    // batch-row backward: the three views' chains as three block rows (gradients are atomics there)
-    const dim3 grid((unsigned)(((n + 15) / 16 + 3) / 4), backward && rows ? 3 : 1);
+    // batch-row backward: the three views' chains as three block rows (gradients are atomics
+    // there); batch-row forward with the scratch hv: likewise, then pref_combine
+    const bool split_fwd = !backward && rows && hv;
+    const dim3 grid((unsigned)(((n + 15) / 16 + 3) / 4), (backward && rows) || split_fwd ? 3 : 1);
     hipStream_t s = as_stream(stream);
+    if (split_fwd) {
+        if (n == 0) return RSX_OK;
+        if (d == 64) hipLaunchKernelGGL(sf::pref_fwd_rows<64>, grid, dim3(256), 0, s, a);
+        else if (d == 128) hipLaunchKernelGGL(sf::pref_fwd_rows<128>, grid, dim3(256), 0, s, a);
+        else return RSX_ERR_UNSUPPORTED;
+        const dim3 gc((unsigned)((n * d / 4 + 255) / 256));
+        if (d == 64) hipLaunchKernelGGL(sf::pref_combine<64>, gc, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL(sf::pref_combine<128>, gc, dim3(256), 0, s, a);
+        return last_rc();
+    }
     switch (d) {
         case 64:
-            if (backward) hipLaunchKernelGGL(sf::pref_bwd<64>, grid, dim3(256), 0, s, a);
+            if (backward && rows) hipLaunchKernelGGL(sf::pref_bwd_rows<64>, grid, dim3(256), 0, s, a);
+            else if (backward) hipLaunchKernelGGL(sf::pref_bwd<64>, grid, dim3(256), 0, s, a);
             else hipLaunchKernelGGL(sf::pref_fwd<64>, grid, dim3(256), 0, s, a);
             break;
         case 128:
-            if (backward) hipLaunchKernelGGL(sf::pref_bwd<128>, grid, dim3(256), 0, s, a);
+            if (backward && rows) hipLaunchKernelGGL(sf::pref_bwd_rows<128>, grid, dim3(256), 0, s, a);
+            else if (backward) hipLaunchKernelGGL(sf::pref_bwd<128>, grid, dim3(256), 0, s, a);
             else hipLaunchKernelGGL(sf::pref_fwd<128>, grid, dim3(256), 0, s, a);
             break;
         default: return RSX_ERR_UNSUPPORTED;
@@ -1326,7 +1562,8 @@ int rsx_smore_wgrad(int32_t n_pairs, const float* const* dz, const float* const*
 }
 
 size_t rsx_smore_infonce_ws_bytes(int64_t batch, int32_t d) {
-    return (size_t)(4 * batch * d + 4 * batch + 2 * batch + 2 * batch) * 4;
+    const int64_t e = batch <= sf::kNceStoreMax ? 2 * batch * batch : 0;  // the stored exp(S / tau) tiles
+    return (size_t)(4 * batch * d + 4 * batch + 2 * batch + 2 * batch + e) * 4;
 }
 
 static int nce_setup(sf::NceArgs& a, const float* side, const float* content, const int64_t* users,
@@ -1348,6 +1585,7 @@ static int nce_setup(sf::NceArgs& a, const float* side, const float* content, co
     a.norms = a.nrm + 4 * batch * d;
     a.ttl = a.norms + 4 * batch;
     a.lrow = a.ttl + 2 * batch;
+    a.E = batch <= sf::kNceStoreMax ? a.lrow + 2 * batch : nullptr;
     return RSX_OK;
 }
 
@@ -1429,7 +1667,16 @@ int rsx_adam_multi_scaled(int32_t count, float* const* p, const float* const* g,
                           const int64_t* const* step_dev, const int64_t* n, float lr, float beta1, float beta2,
                           float eps, float weight_decay, float grad_scale, const double* lr_dev,
                           const int32_t* halt, rsx_stream_t stream) {
+    return rsx_adam_multi_mg(count, p, g, m, v, step_dev, n, lr, beta1, beta2, eps, weight_decay, grad_scale, lr_dev,
+                             halt, nullptr, nullptr, 0.0, stream);
+}
+
+int rsx_adam_multi_mg(int32_t count, float* const* p, const float* const* g, float* const* m, float* const* v,
+                      const int64_t* const* step_dev, const int64_t* n, float lr, float beta1, float beta2, float eps,
+                      float weight_decay, float grad_scale, const double* lr_dev, const int32_t* halt,
+                      const float* const* rx, const double* ralpha, double rmult, rsx_stream_t stream) {
     if (count < 0 || (count > 0 && (!p || !g || !m || !v || !step_dev || !n))) return RSX_ERR_ARG;
+    if ((rx != nullptr) != (ralpha != nullptr)) return RSX_ERR_ARG;
     hipStream_t s = as_stream(stream);
     for (int32_t c0 = 0; c0 < count; c0 += sf::kAdamMax) {
         sf::AdamList L{};
@@ -1441,19 +1688,24 @@ int rsx_adam_multi_scaled(int32_t count, float* const* p, const float* const* g,
         L.gscale = grad_scale;
         L.lr_dev = lr_dev;
         L.halt = halt;
+        L.ralpha = ralpha;
+        L.rmult = rmult;
         int64_t blocks = 0;
         int k = 0;
         for (int32_t i = c0; i < count && k < sf::kAdamMax; ++i) {
             if (n[i] < 0 || (n[i] > 0 && (!p[i] || !g[i] || !m[i] || !v[i] || !step_dev[i]))) return RSX_ERR_ARG;
+            if (n[i] > 0 && rx && !rx[i]) return RSX_ERR_ARG;
             if (n[i] == 0) continue;
             L.p[k] = p[i];
             L.g[k] = g[i];
             L.m[k] = m[i];
             L.v[k] = v[i];
+            L.rx[k] = rx ? rx[i] : nullptr;
             L.step[k] = step_dev[i];
             L.n[k] = n[i];
             L.blk[k] = blocks;
-            const uintptr_t al = (uintptr_t)p[i] | (uintptr_t)g[i] | (uintptr_t)m[i] | (uintptr_t)v[i];
+            const uintptr_t al = (uintptr_t)p[i] | (uintptr_t)g[i] | (uintptr_t)m[i] | (uintptr_t)v[i] |
+                                 (uintptr_t)(rx ? rx[i] : nullptr);
             if ((n[i] & 3) == 0 && (al & 15) == 0) L.vec4 |= 1u << k;
             blocks += (n[i] + sf::kAdamPerBlock - 1) / sf::kAdamPerBlock;
             ++k;
@@ -1484,6 +1736,7 @@ static int build_pair_lists(int32_t count, float* const* y, const float* const* 
             L.x[k] = x[i];
             L.n[k] = n[i];
             L.blk[k] = blocks;
+            if ((n[i] & 3) == 0 && (((uintptr_t)y[i] | (uintptr_t)x[i]) & 15) == 0) L.vec4 |= 1u << k;
             blocks += (n[i] + sf::kAdamPerBlock - 1) / sf::kAdamPerBlock;
             ++k;
         }

@@ -157,6 +157,8 @@ def _declare(lib):
                                                    P]),
         "rsx_adam_multi": (C.c_int, [I32, P, P, P, P, P, P, F32, F32, F32, F32, F32, P]),
         "rsx_adam_multi_scaled": (C.c_int, [I32, P, P, P, P, P, P, F32, F32, F32, F32, F32, F32, P, P, P]),
+        "rsx_adam_multi_mg": (C.c_int, [I32, P, P, P, P, P, P, F32, F32, F32, F32, F32, F32, P, P, P, P, C.c_double,
+                                        P]),
         "rsx_nan_gate": (C.c_int, [P, P, P, P]),
         "rsx_smore_unit_weights": (C.c_int, [P, P, P, I32, I32, P, P]),
         "rsx_mg_alpha_ws_bytes": (C.c_size_t, [I32, P]),
@@ -187,7 +189,7 @@ EXPORTED = ["rsx_version", "rsx_csr_schedule_host", "rsx_csr_schedule_rebind", "
             "rsx_comm_init_host",
             "rsx_comm_allreduce_f32", "rsx_sharded_lightgcn_step", "rsx_sharded_lightgcn_forward",
             "rsx_smore_gates", "rsx_smore_pref", "rsx_smore_pref_rows", "rsx_smore_wgrad_ws_bytes", "rsx_smore_wgrad",
-            "rsx_smore_infonce_ws_bytes", "rsx_smore_infonce_fwd", "rsx_smore_infonce_bwd", "rsx_smore_infonce_fwd_total", "rsx_smore_infonce_bwd_scaled", "rsx_adam_multi", "rsx_adam_multi_scaled",
+            "rsx_smore_infonce_ws_bytes", "rsx_smore_infonce_fwd", "rsx_smore_infonce_bwd", "rsx_smore_infonce_fwd_total", "rsx_smore_infonce_bwd_scaled", "rsx_adam_multi", "rsx_adam_multi_scaled", "rsx_adam_multi_mg",
             "rsx_smore_unit_weights", "rsx_smore_unit_weights_bwd", "rsx_mg_alpha_ws_bytes", "rsx_mg_alpha",
             "rsx_axpy_multi", "rsx_knn_ws_bytes", "rsx_knn_graph", "rsx_adj_build_ws_bytes", "rsx_adj_build",
             "rsx_edge_dropout_ws_bytes", "rsx_edge_dropout_build", "rsx_nan_gate"]

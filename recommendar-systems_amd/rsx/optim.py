@@ -17,7 +17,7 @@ from __future__ import annotations
 
 import torch
 
-from .smore_fuse import adam_multi
+from .smore_fuse import adam_multi, axpy_multi
 
 
 class RsxAdam(torch.optim.Optimizer):
@@ -32,6 +32,11 @@ class RsxAdam(torch.optim.Optimizer):
         # optional int32 [2] device flag of rsx.smore_fuse.nan_gate (set by rsx.trainer):
         # once a batch loss was NaN no update changes any parameter or moment
         self.halt = None
+        # the mirror gradient's restore for the next step() (then reset): (params, xs,
+        # alpha, mult, lr_dev, halt) — p += float(alpha * mult [* lr]) * x folded into the
+        # Adam launch when the step updates exactly `params` with the same lr_dev / halt
+        # (rsx.trainer); otherwise rsx_axpy_multi applies it before the update
+        self.restore = None
 
     def lr_on_device(self) -> bool:
         """Whether every update reads the learning rate from `lr_dev` (one group of
@@ -47,6 +52,19 @@ class RsxAdam(torch.optim.Optimizer):
             with torch.enable_grad():
                 loss = closure()
         gs, self.grad_scale = float(self.grad_scale), 1.0
+        restore, self.restore = self.restore, None
+        rmap = None
+        if restore is not None:
+            rps, rxs, ralpha, rmult, rlr, rhalt = restore
+            live_all = [p for g in self.param_groups for p in g["params"] if p.grad is not None]
+            fold = (len(self.param_groups) == 1 and len(rps) == len(live_all) and rlr is self.lr_dev
+                    and rhalt is self.halt
+                    and {id(p) for p in rps} == {id(p) for p in live_all}
+                    and all(p.is_contiguous() for p in live_all))
+            if fold:
+                rmap = {id(p): x for p, x in zip(rps, rxs)}
+            else:  # the restore as its own pass, then the plain update
+                axpy_multi(rps, rxs, ralpha, rmult, rlr, rhalt)
         for group in self.param_groups:
             live = [p for p in group["params"] if p.grad is not None]
             for p in live:
@@ -71,7 +89,8 @@ class RsxAdam(torch.optim.Optimizer):
                            [self.state[p]["exp_avg"] for p in live], [self.state[p]["exp_avg_sq"] for p in live],
                            steps, group["lr"], betas=group["betas"], eps=group["eps"],
                            weight_decay=group["weight_decay"], grad_scale=gs,
-                           lr_dev=self.lr_dev if len(self.param_groups) == 1 else None, halt=self.halt)
+                           lr_dev=self.lr_dev if len(self.param_groups) == 1 else None, halt=self.halt,
+                           restore=None if rmap is None else ([rmap[id(p)] for p in live], ralpha, rmult))
                 continue
             # a non-contiguous parameter: the same launch on contiguous copies, copied back
             ts = [[t.contiguous() for t in (p.data, self.state[p]["exp_avg"], self.state[p]["exp_avg_sq"])]

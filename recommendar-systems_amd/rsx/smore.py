@@ -336,9 +336,12 @@ class SMORE(GeneralRecommender):
         if self.t_feat is not None:
             self.text_embedding = nn.Embedding.from_pretrained(self.t_feat.clone(), freeze=False)
             txt_g = self._cached_knn(root, "text", self.t_feat, self.text_knn_k)
-        self.image_graph = _DevGraph(*img_g, ni, ni, self.device, chunk)
-        self.text_graph = _DevGraph(*txt_g, ni, ni, self.device, chunk)
-        self.fusion_graph = _DevGraph(*max_pool_union(img_g, txt_g, ni), ni, ni, self.device, chunk)
+        # kNN rows hold k (<= ~40 in the fusion union) nonzeros: a 64-wide work item takes a
+        # whole row, so the views' products need no hub-row partials or fixup blocks
+        kchunk = int(config["rsx_knn_chunk"] or 64)
+        self.image_graph = _DevGraph(*img_g, ni, ni, self.device, kchunk)
+        self.text_graph = _DevGraph(*txt_g, ni, ni, self.device, kchunk)
+        self.fusion_graph = _DevGraph(*max_pool_union(img_g, txt_g, ni), ni, ni, self.device, kchunk)
         if self.v_feat is not None:
             self.image_trs = nn.Linear(self.v_feat.shape[1], d)
         if self.t_feat is not None:
@@ -564,8 +567,10 @@ class SMORE(GeneralRecommender):
             content.record_stream(main)  # allocated on the side stream, read on this one
         nu, L_ = self.n_users, self.n_layers
         if self.batch_views:  # the three views' products batched into shared launches
+            tags = self._tags if rows is not None and 1 <= self.n_ui_layers <= 4 else None
             image_embeds, text_embeds, fusion_embeds = SF.view_prop3(
-                (img_i, txt_i, fus_i), (self.image_graph, self.text_graph, self.fusion_graph), self.R, L_, nu)
+                (img_i, txt_i, fus_i), (self.image_graph, self.text_graph, self.fusion_graph), self.R, L_, nu,
+                tags=tags)
         else:
             image_embeds = SF.view_prop(img_i, self.image_graph, self.R, L_, nu)
             text_embeds = SF.view_prop(txt_i, self.text_graph, self.R, L_, nu)

@@ -165,11 +165,11 @@ class _PrefRows(torch.autograd.Function):
         b = [None if x is None else _c(x) for x in wb[7:]]
         C_, IE, TE, FE, rows = _c(C_), _c(IE), _c(TE), _c(FE), _c(rows)
         n, d = rows.numel(), C_.shape[1]
-        out = torch.empty(4, n, d, dtype=torch.float32, device=C_.device)
-        all_, side, c_rows, f_rows = out.unbind(0)
+        out = torch.empty(5, n, d, dtype=torch.float32, device=C_.device)
+        all_, side, c_rows, f_rows, x2 = out.unbind(0)  # x2: the split forward's scratch
         L.check(L.lib().rsx_smore_pref_rows(0, _arr(W), _arr(b), _p(C_), _p(IE), _p(TE), _p(FE), _p(rows), n, d,
                                             float(p_drop), _p(seed), _p(all_), _p(side), _p(c_rows), _p(f_rows),
-                                            None, None, None, None, None, None, None, None, None, None,
+                                            None, None, None, None, None, None, None, _p(x2), None, None,
                                             ops._stream()), "rsx_smore_pref_rows")
         ctx.save_for_backward(C_, IE, TE, FE, rows, seed, c_rows, f_rows, *W,
                               *[x if x is not None else torch.empty(0) for x in b])
@@ -264,7 +264,7 @@ class _ViewProp3(torch.autograd.Function):
     the three R^T and item-graph transposes, each set as ONE rsx_spmm_batch launch."""
 
     @staticmethod
-    def forward(ctx, x0, x1, x2, Gs, R, n_layers, n_users, comm):
+    def forward(ctx, x0, x1, x2, Gs, R, n_layers, n_users, comm, tags):
         xs = [_c(x) for x in (x0, x1, x2)]
         ni, d = xs[0].shape
         outs = [torch.empty(n_users + ni, d, dtype=torch.float32, device=xs[0].device) for _ in range(3)]
@@ -276,8 +276,12 @@ class _ViewProp3(torch.autograd.Function):
         if n_layers == 0:
             for o, x in zip(outs, xs):
                 o[n_users:].copy_(x)
-        ops.spmm_batch([R.A] * 3, [o[n_users:] for o in outs], [ops.epi(L.RSX_EPI_STORE, y=o[:n_users]) for o in outs],
-                       d)
+        epis = [ops.epi(L.RSX_EPI_STORE, y=o[:n_users]) for o in outs]
+        if tags is not None:  # user rows on the tagged (batch) users only; the rest are left unwritten
+            for e in epis:
+                e.row_tag, e.tag_dev = tags.row_tag.data_ptr(), tags.tag_dev.data_ptr()
+                e.tag_flags = L.RSX_TAG_ROWS
+        ops.spmm_batch([R.A] * 3, [o[n_users:] for o in outs], epis, d)
         ctx.Gs, ctx.R, ctx.L, ctx.nu, ctx.comm = Gs, R, n_layers, n_users, comm
         return tuple(outs)
 
@@ -298,15 +302,17 @@ class _ViewProp3(torch.autograd.Function):
             nxt = [torch.empty_like(x) for x in gi]
             ops.spmm_batch([G.AT for G in ctx.Gs], gi, [ops.epi(L.RSX_EPI_STORE, y=y) for y in nxt], d)
             gi = nxt
-        return gi[0], gi[1], gi[2], None, None, None, None, None
+        return gi[0], gi[1], gi[2], None, None, None, None, None, None
 
 
-def view_prop3(xs, Gs, R, n_layers, n_users, comm=None):
+def view_prop3(xs, Gs, R, n_layers, n_users, comm=None, tags=None):
     """(image, text, fusion) [R G^L x; G^L x] tables of the three views (one launch per
     layer for all three graphs, one for the three R products).  With `comm` (R = this
     rank's user rows) the item rows' gradients are summed over the ranks in one
-    all-reduce before the item-graph backward."""
-    return _ViewProp3.apply(xs[0], xs[1], xs[2], tuple(Gs), R, int(n_layers), int(n_users), comm)
+    all-reduce before the item-graph backward.  With `tags` (the batch-row tags of the
+    training loss, rsx.smore._RowTags over [users; items]) the user rows are computed on
+    the tagged users only: the preference block reads no other user row of a view."""
+    return _ViewProp3.apply(xs[0], xs[1], xs[2], tuple(Gs), R, int(n_layers), int(n_users), comm, tags)
 
 
 # ---------------------------------------------------------------------------
@@ -396,18 +402,30 @@ def smore_loss_rows(all_c, side_c, content_c, trip, ar, B, reg, batch_cfg, cl, t
 # multi-tensor Adam
 # ---------------------------------------------------------------------------
 def adam_multi(params, grads, exp_avgs, exp_avg_sqs, steps, lr, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0,
-               grad_scale=1.0, lr_dev=None, halt=None):
+               grad_scale=1.0, lr_dev=None, halt=None, restore=None):
     """torch.optim.Adam's update over many tensors in one launch (per 32 tensors); the
     gradients are taken as g * grad_scale (f32 product) when grad_scale != 1; with
     lr_dev (a 1-element f64 device tensor) the learning rate is read from it; with
-    halt (nan_gate's int32 flag) nothing is updated once it is set."""
+    halt (nan_gate's int32 flag) nothing is updated once it is set.  restore = (xs,
+    alpha, mult): the mirror gradient's restore p += float(alpha * mult [* lr]) * x
+    (axpy_multi's arithmetic) folded into the same launch (rsx_adam_multi_mg)."""
     n = len(params)
     if n == 0:
         return
-    for t in (*params, *grads, *exp_avgs, *exp_avg_sqs):
+    xs = list(restore[0]) if restore is not None else []
+    for t in (*params, *grads, *exp_avgs, *exp_avg_sqs, *xs):
         if not (t.is_cuda and t.is_contiguous() and t.dtype == torch.float32):
             raise RuntimeError("adam_multi: contiguous f32 GPU tensors only")
     sizes = (C.c_int64 * n)(*[p.numel() for p in params])
+    if restore is not None:
+        if len(xs) != n or any(x.numel() != p.numel() for x, p in zip(xs, params)):
+            raise RuntimeError("adam_multi: one restore tensor per parameter, of its size")
+        L.check(L.lib().rsx_adam_multi_mg(n, _arr(params), _arr(grads), _arr(exp_avgs), _arr(exp_avg_sqs),
+                                          _arr(steps), sizes, float(lr), float(betas[0]), float(betas[1]), float(eps),
+                                          float(weight_decay), float(grad_scale), _p(lr_dev), _p(halt), _arr(xs),
+                                          _p(restore[1]), float(restore[2]), ops._stream()),
+                "rsx_adam_multi_mg")
+        return
     L.check(L.lib().rsx_adam_multi_scaled(n, _arr(params), _arr(grads), _arr(exp_avgs), _arr(exp_avg_sqs),
                                           _arr(steps), sizes, float(lr), float(betas[0]), float(betas[1]), float(eps),
                                           float(weight_decay), float(grad_scale), _p(lr_dev), _p(halt),

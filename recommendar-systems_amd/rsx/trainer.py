@@ -521,8 +521,8 @@ class Trainer:
             elif live:
                 torch._foreach_mul_(live, -beta)
             if params:
-                if fused:
-                    axpy_multi(params, grads, alpha, 1.0 if lr_dev is not None else lr, lr_dev, halt)  # restore theta
+                if fused:  # restore theta, folded into the Adam launch below (rsx_adam_multi_mg)
+                    self.optimizer.restore = (params, grads, alpha, 1.0 if lr_dev is not None else lr, lr_dev, halt)
                 else:
                     torch._foreach_add_(params, torch._foreach_mul(grads, (alpha * lr).float()))
         self.optimizer.step()

@@ -308,3 +308,43 @@ def test_mg_alpha_and_axpy_vs_torch(cuda):
     SF.axpy_multi(ys, gs, alpha, -1e-3)
     for y, w in zip(ys, want):
         assert torch.equal(y, w)
+
+
+@pytest.mark.gpu
+def test_adam_multi_mg_equals_axpy_then_adam(cuda):
+    """rsx_adam_multi_mg (the mirror gradient's restore folded into the Adam launch) ==
+    rsx_axpy_multi then rsx_adam_multi_scaled, bit for bit: parameters and both
+    moments, float4 and ragged tensors, host lr and device lr, with grad_scale; and a
+    set halt flag leaves everything unchanged."""
+    from rsx import smore_fuse as SF
+
+    shapes = [(7050, 768), (128, 128), (128,), (1, 65, 2), (23033, 128), (5, 7), (3,)]
+    gen = torch.Generator().manual_seed(11)
+    mk = lambda s, sc: torch.randn(*s, generator=gen).to(cuda) * sc  # noqa: E731
+    ps = [mk(s, 0.1) for s in shapes]
+    gs = [mk(s, 1e-3) for s in shapes]
+    xs = [mk(s, 1e-3) for s in shapes]
+    ms = [mk(s, 1e-4) for s in shapes]
+    vs = [mk(s, 1e-6).abs() for s in shapes]
+    alpha = torch.tensor(3.7, dtype=torch.float64, device=cuda)
+    for lr_dev in (None, torch.tensor([2e-3], dtype=torch.float64, device=cuda)):
+        mult = 1.0 if lr_dev is not None else 1e-3
+        ref = [[t.clone() for t in ts] for ts in (ps, ms, vs)]
+        got = [[t.clone() for t in ts] for ts in (ps, ms, vs)]
+        st_a = [torch.full((), 3, dtype=torch.int64, device=cuda) for _ in shapes]
+        st_b = [t.clone() for t in st_a]
+        SF.axpy_multi(ref[0], xs, alpha, mult, lr_dev)
+        SF.adam_multi(ref[0], gs, ref[1], ref[2], st_a, 1e-3, grad_scale=-0.2, lr_dev=lr_dev)
+        SF.adam_multi(got[0], gs, got[1], got[2], st_b, 1e-3, grad_scale=-0.2, lr_dev=lr_dev,
+                      restore=(xs, alpha, mult))
+        for name, a, b in zip(("p", "m", "v"), ref, got):
+            for i, (x, y) in enumerate(zip(a, b)):
+                assert torch.equal(x, y), (name, i, shapes[i], lr_dev is not None, (x - y).abs().max().item(),
+                                           (x != y).sum().item())
+    halt = torch.tensor([1, 4], dtype=torch.int32, device=cuda)
+    got = [t.clone() for t in ps]
+    st = [torch.full((), 3, dtype=torch.int64, device=cuda) for _ in shapes]
+    SF.adam_multi(got, gs, [t.clone() for t in ms], [t.clone() for t in vs], st, 1e-3, halt=halt,
+                  restore=(xs, alpha, 1e-3))
+    for x, y in zip(got, ps):
+        assert torch.equal(x, y)
