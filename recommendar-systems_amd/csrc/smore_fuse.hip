@@ -160,6 +160,65 @@ __device__ __forceinline__ Fld<D> mv(const float* __restrict__ W, const float* b
     return z;
 }
 
+// mv / mvt with a bounded register footprint: the weight operands of step t+1 are
+// loaded while step t's MFMAs run, and a scheduling barrier keeps the compiler from
+// hoisting every step's loads to the top (which needs D*D/16 registers at d = 128 and
+// makes two waves a SIMD spill).  Same products, same accumulation order.
+template <int D, int LD>
+__device__ __forceinline__ Fld<D> mv_p(const float* __restrict__ W, const float* b, const Fld<D>& x, int lane) {
+    constexpr int T = D / 16;
+    const int c = lane & 15, g = lane >> 4;
+    Fld<D> z = fvec<D>(b, g);
+    const float* wr = W + c * LD + 4 * g;
+    float4 w[2][T];
+#pragma unroll
+    for (int to = 0; to < T; ++to) w[0][to] = ld4(wr + 16 * to * LD);
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        if (t + 1 < T) {
+#pragma unroll
+            for (int to = 0; to < T; ++to) w[(t + 1) & 1][to] = ld4(wr + 16 * to * LD + 16 * (t + 1));
+        }
+        const float4* wc = w[t & 1];
+#pragma unroll
+        for (int to = 0; to < T; ++to) z.f[to] = mfma4(wc[to].x, x.f[t][0], z.f[to]);
+#pragma unroll
+        for (int to = 0; to < T; ++to) z.f[to] = mfma4(wc[to].y, x.f[t][1], z.f[to]);
+#pragma unroll
+        for (int to = 0; to < T; ++to) z.f[to] = mfma4(wc[to].z, x.f[t][2], z.f[to]);
+#pragma unroll
+        for (int to = 0; to < T; ++to) z.f[to] = mfma4(wc[to].w, x.f[t][3], z.f[to]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    return z;
+}
+
+template <int D, int LD>
+__device__ __forceinline__ Fld<D> mvt_p(const float* __restrict__ W, const Fld<D>& x, int lane) {
+    constexpr int T = D / 16;
+    const int c = lane & 15, g = lane >> 4;
+    Fld<D> z = fzero<D>();
+    float wv[2][T];
+    auto load = [&](int t, int r, float(&dst)[T]) __attribute__((always_inline)) {
+        const float* wr = W + (16 * t + 4 * g + r) * LD + c;
+#pragma unroll
+        for (int tk = 0; tk < T; ++tk) dst[tk] = wr[16 * tk];
+    };
+    load(0, 0, wv[0]);
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int q = t * 4 + r;
+            if (q + 1 < 4 * T) load((q + 1) >> 2, (q + 1) & 3, wv[(q + 1) & 1]);
+#pragma unroll
+            for (int tk = 0; tk < T; ++tk) z.f[tk] = mfma4(wv[q & 1][tk], x.f[t][r], z.f[tk]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    return z;
+}
+
 // z[n][k] = sum_o W[o][k] x[n][o]  (the input gradient of a Linear)
 template <int D, int LD>
 __device__ __forceinline__ Fld<D> mvt(const float* __restrict__ W, const Fld<D>& x, int lane) {
@@ -297,7 +356,7 @@ __global__ __launch_bounds__(256) void gates_fwd(GateArgs a) {
         for (int m = m0; m < m1; ++m) {
             const Fld<D> cv = fload<D>(a.conv[m], row, g);
             const float* W = split ? wl : stage_w<D>(wl, a.W[m]);
-            const Fld<D> s = fmap<D>(mv<D, kLd<D>>(W, a.b[m], cv, lane), sigm);
+            const Fld<D> s = fmap<D>(mv_p<D, kLd<D>>(W, a.b[m], cv, lane), sigm);
             const Fld<D> o = a.mul ? fmap2<D>(it, s, [](float x, float y) { return x * y; })
                                    : fmap2<D>(it, s, [&](float x, float y) { return x + a.scale * y; });
             fstore<D>(a.out[m], row, g, o);
@@ -332,7 +391,7 @@ __global__ __launch_bounds__(256) void gates_bwd(GateArgs a) {
         const Fld<D> go = a.gout[m] ? fload<D>(a.gout[m], row, g) : fzero<D>();
         const Fld<D> cv = fload<D>(a.conv[m], row, g);
         const float* W = split ? wl : stage_w<D>(wl, a.W[m]);
-        const Fld<D> s = fmap<D>(mv<D, kLd<D>>(W, a.b[m], cv, lane), sigm);
+        const Fld<D> s = fmap<D>(mv_p<D, kLd<D>>(W, a.b[m], cv, lane), sigm);
         Fld<D> ds;
         if (a.mul) {
             gi = fmap3<D>(gi, go, s, [](float acc, float x, float y) { return acc + x * y; });
@@ -343,9 +402,43 @@ __global__ __launch_bounds__(256) void gates_bwd(GateArgs a) {
         }
         const Fld<D> dz = fmap2<D>(ds, s, [](float x, float y) { return x * ((1.f - y) * y); });
         fstore<D>(a.dz[m], row, g, dz);
-        fstore<D>(a.g_conv[m], row, g, mvt<D, kLd<D>>(W, dz, lane));
+        fstore<D>(a.g_conv[m], row, g, mvt_p<D, kLd<D>>(W, dz, lane));
     }
     if (!split) fstore<D>(a.g_item, row, g, gi);
+    }
+}
+
+// gates_bwd in residual mode (out = item + scale * sigmoid(Linear(conv)), one gate per
+// block row): the same arithmetic with no item row or g_item accumulator held across the
+// gate's two matrix products (the gate-0 blocks form g_item first), so fewer fields
+// are live: d = 128 fits two waves a SIMD.
+template <int D>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void gates_bwd_res(GateArgs a) {
+    __shared__ __attribute__((aligned(16))) float wl[D * kLd<D>];
+    const int lane = threadIdx.x & 63, g = lane >> 4;
+    const int m = (int)blockIdx.y;
+    const float* W = stage_w<D>(wl, a.W[m]);
+#pragma unroll 1
+    for (int64_t bx = blockIdx.x; bx < a.nbx; bx += gridDim.x) {  // block-uniform
+        const int64_t n0 = (bx * 4 + (threadIdx.x >> 6)) * 16;
+        const int64_t row = n0 + (lane & 15) < a.n ? n0 + (lane & 15) : -1;
+        if (m == 0) {  // g_item = sum of the three upstream gradients, in gate order
+            Fld<D> gi = fzero<D>();
+#pragma unroll 1
+            for (int q = 0; q < 3; ++q)
+                gi = fmap2<D>(gi, a.gout[q] ? fload<D>(a.gout[q], row, g) : fzero<D>(),
+                              [](float acc, float x) { return acc + x; });
+            fstore<D>(a.g_item, row, g, gi);
+        }
+        Fld<D> dz;
+        {
+            const Fld<D> s = fmap<D>(mv_p<D, kLd<D>>(W, a.b[m], fload<D>(a.conv[m], row, g), lane), sigm);
+            const Fld<D> go = a.gout[m] ? fload<D>(a.gout[m], row, g) : fzero<D>();
+            dz = fmap2<D>(fmap<D>(go, [&](float x) { return a.scale * x; }), s,
+                          [](float x, float y) { return x * ((1.f - y) * y); });
+        }
+        fstore<D>(a.dz[m], row, g, dz);
+        fstore<D>(a.g_conv[m], row, g, mvt_p<D, kLd<D>>(W, dz, lane));
     }
 }
 
@@ -407,7 +500,7 @@ __global__ __launch_bounds__(256) void pref_fwd(PrefArgs a) {
     const int64_t row = src_row(a, out);
     const uint64_t seed = a.p_drop > 0.f ? (uint64_t)*a.seed : 0;
     const auto mul = [](float x, float y) { return x * y; };
-    const auto lin = [&](int k, const Fld<D>& x) { return mv<D, kLd<D>>(stage_w<D>(wl, a.W[k]), a.b[k], x, lane); };
+    const auto lin = [&](int k, const Fld<D>& x) { return mv_p<D, kLd<D>>(stage_w<D>(wl, a.W[k]), a.b[k], x, lane); };
     const Fld<D> FE = fload<D>(a.FE, row, g);
     const Fld<D> C = fload<D>(a.C, row, g);
     fstore<D>(a.c_out, out, g, C);
@@ -457,28 +550,28 @@ __global__ __launch_bounds__(256) void pref_bwd(PrefArgs a) {
     Fld<D> gFE = fzero<D>();
     if (part <= 0) {   // fusion view: x3 = fp * FE
         const float* W = stage_w<D>(wl, a.W[kWfp]);
-        const Fld<D> sf = fmap<D>(mv<D, kLd<D>>(W, a.b[kWfp], C, lane), sigm);
+        const Fld<D> sf = fmap<D>(mv_p<D, kLd<D>>(W, a.b[kWfp], C, lane), sigm);
         const Fld<D> mf = a.p_drop > 0.f ? drop_scale<D>(seed, 2, row, g, a.p_drop, a.drop_scale) : Fld<D>{};
         const Fld<D> fp = a.p_drop > 0.f ? fmap2<D>(sf, mf, mul) : sf;
         Fld<D> dp = fmap2<D>(g1, FE, mul);
         if (a.p_drop > 0.f) dp = fmap2<D>(dp, mf, mul);
         const Fld<D> dz = fmap2<D>(dp, sf, sig_bwd);
         fstore<D>(a.dz[kWfp], out, g, dz);
-        gC = fmap2<D>(gC, mvt<D, kLd<D>>(W, dz, lane), add);
+        gC = fmap2<D>(gC, mvt_p<D, kLd<D>>(W, dz, lane), add);
         gFE = fmap2<D>(g1, fp, mul);
     }
 #pragma unroll 1
     for (int v = 0; v < 2; ++v) {  // v = 0: image view, 1: text view
         if (part >= 0 && part != v + 1) continue;  // block-uniform
         const int w1 = v ? kW1t : kW1v, w2 = v ? kW2t : kW2v, wp = v ? kWtp : kWip;
-        const Fld<D> h = fmap<D>(mv<D, kLd<D>>(stage_w<D>(wl, a.W[w1]), a.b[w1], FE, lane), tanh_);
+        const Fld<D> h = fmap<D>(mv_p<D, kLd<D>>(stage_w<D>(wl, a.W[w1]), a.b[w1], FE, lane), tanh_);
         fstore<D>(v ? a.ht : a.hv, out, g, h);
-        const Fld<D> s = softmax_row<D>(mv<D, kLd<D>>(stage_w<D>(wl, a.W[w2]), nullptr, h, lane));
+        const Fld<D> s = softmax_row<D>(mv_p<D, kLd<D>>(stage_w<D>(wl, a.W[w2]), nullptr, h, lane));
         const Fld<D> E = fload<D>(v ? a.TE : a.IE, row, g);
         Fld<D> pp;
         {
             const float* W = stage_w<D>(wl, a.W[wp]);
-            const Fld<D> sp = fmap<D>(mv<D, kLd<D>>(W, a.b[wp], C, lane), sigm);
+            const Fld<D> sp = fmap<D>(mv_p<D, kLd<D>>(W, a.b[wp], C, lane), sigm);
             const Fld<D> mp = a.p_drop > 0.f ? drop_scale<D>(seed, v, row, g, a.p_drop, a.drop_scale) : Fld<D>{};
             pp = a.p_drop > 0.f ? fmap2<D>(sp, mp, mul) : sp;
             // x = pp * (s * E)
@@ -486,7 +579,7 @@ __global__ __launch_bounds__(256) void pref_bwd(PrefArgs a) {
             if (a.p_drop > 0.f) dpp = fmap2<D>(dpp, mp, mul);
             const Fld<D> dzp = fmap2<D>(dpp, sp, sig_bwd);
             fstore<D>(a.dz[wp], out, g, dzp);
-            gC = fmap2<D>(gC, mvt<D, kLd<D>>(W, dzp, lane), add);
+            gC = fmap2<D>(gC, mvt_p<D, kLd<D>>(W, dzp, lane), add);
         }
         const Fld<D> da = fmap2<D>(g1, pp, mul);          // d (s * E)
         if (a.rows) fatomic<D>(v ? a.gTE : a.gIE, row, g, fmap2<D>(da, s, mul));
@@ -495,10 +588,10 @@ __global__ __launch_bounds__(256) void pref_bwd(PrefArgs a) {
         const float dot = rsum<D>(fmap2<D>(dsm, s, mul));
         const Fld<D> dq = fmap2<D>(s, dsm, [&](float y, float gy) { return y * (gy - dot); });
         fstore<D>(a.dz[w2], out, g, dq);
-        const Fld<D> dh = mvt<D, kLd<D>>(stage_w<D>(wl, a.W[w2]), dq, lane);
+        const Fld<D> dh = mvt_p<D, kLd<D>>(stage_w<D>(wl, a.W[w2]), dq, lane);
         const Fld<D> dz1 = fmap2<D>(dh, h, [](float gy, float y) { return gy * (1.f - y * y); });
         fstore<D>(a.dz[w1], out, g, dz1);
-        gFE = fmap2<D>(gFE, mvt<D, kLd<D>>(stage_w<D>(wl, a.W[w1]), dz1, lane), add);
+        gFE = fmap2<D>(gFE, mvt_p<D, kLd<D>>(stage_w<D>(wl, a.W[w1]), dz1, lane), add);
     }
     if (a.rows) {
         fatomic<D>(a.gC, row, g, gC);
@@ -523,7 +616,7 @@ __global__ __launch_bounds__(256) void pref_fwd_rows(PrefArgs a) {
     const int64_t row = src_row(a, out);
     const uint64_t seed = a.p_drop > 0.f ? (uint64_t)*a.seed : 0;
     const auto mul = [](float x, float y) { return x * y; };
-    const auto lin = [&](int k, const Fld<D>& x) { return mv<D, kLd<D>>(stage_w<D>(wl, a.W[k]), a.b[k], x, lane); };
+    const auto lin = [&](int k, const Fld<D>& x) { return mv_p<D, kLd<D>>(stage_w<D>(wl, a.W[k]), a.b[k], x, lane); };
     const int part = (int)blockIdx.y;
     if (part == 0) {
         const Fld<D> C = fload<D>(a.C, row, g);
@@ -569,7 +662,7 @@ __global__ __launch_bounds__(256) void pref_combine(PrefArgs a) {
 // FE (dead after), tanh rows reloaded from the hv / ht rows this kernel wrote, each view's
 // gC / gFE share added as soon as it is formed.
 template <int D>
-__global__ __launch_bounds__(256) void pref_bwd_rows(PrefArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void pref_bwd_rows(PrefArgs a) {
     __shared__ __attribute__((aligned(16))) float wl[D * kLd<D>];
     const int lane = threadIdx.x & 63, g = lane >> 4;
     const int64_t n0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 16;
@@ -587,7 +680,7 @@ __global__ __launch_bounds__(256) void pref_bwd_rows(PrefArgs a) {
     const int part = (int)blockIdx.y;
     if (part == 0) {  // fusion view x3 = fp * FE, and d all -> d content
         const float* W = stage_w<D>(wl, a.W[kWfp]);
-        const Fld<D> sf = fmap<D>(mv<D, kLd<D>>(W, a.b[kWfp], fload<D>(a.C, row, g), lane), sigm);
+        const Fld<D> sf = fmap<D>(mv_p<D, kLd<D>>(W, a.b[kWfp], fload<D>(a.C, row, g), lane), sigm);
         const Fld<D> mf = a.p_drop > 0.f ? drop_scale<D>(seed, 2, row, g, a.p_drop, a.drop_scale) : Fld<D>{};
         const Fld<D> g1 = g1_of();
         Fld<D> dp = fmap2<D>(g1, fload<D>(a.FE, row, g), mul);
@@ -598,18 +691,18 @@ __global__ __launch_bounds__(256) void pref_bwd_rows(PrefArgs a) {
         fatomic<D>(a.gFE, row, g, fmap2<D>(g1, fp, mul));
         const Fld<D> gA = fload<D>(a.g_all, out, g);
         const Fld<D> gC = a.g_cin ? fmap2<D>(gA, fload<D>(a.g_cin, out, g), add) : gA;
-        fatomic<D>(a.gC, row, g, fmap2<D>(gC, mvt<D, kLd<D>>(W, dz, lane), add));
+        fatomic<D>(a.gC, row, g, fmap2<D>(gC, mvt_p<D, kLd<D>>(W, dz, lane), add));
         return;
     }
     const int v = part - 1;  // 0: image view, 1: text view
     const int w1 = v ? kW1t : kW1v, w2 = v ? kW2t : kW2v, wp = v ? kWtp : kWip;
     // the view's preference gate on C (dropout mask applied after the sigmoid)
-    const Fld<D> sp = fmap<D>(mv<D, kLd<D>>(stage_w<D>(wl, a.W[wp]), a.b[wp], fload<D>(a.C, row, g), lane), sigm);
+    const Fld<D> sp = fmap<D>(mv_p<D, kLd<D>>(stage_w<D>(wl, a.W[wp]), a.b[wp], fload<D>(a.C, row, g), lane), sigm);
     Fld<D> s;
     {
-        const Fld<D> h = fmap<D>(mv<D, kLd<D>>(stage_w<D>(wl, a.W[w1]), a.b[w1], fload<D>(a.FE, row, g), lane), tanh_);
+        const Fld<D> h = fmap<D>(mv_p<D, kLd<D>>(stage_w<D>(wl, a.W[w1]), a.b[w1], fload<D>(a.FE, row, g), lane), tanh_);
         fstore<D>(v ? a.ht : a.hv, out, g, h);
-        s = softmax_row<D>(mv<D, kLd<D>>(stage_w<D>(wl, a.W[w2]), nullptr, h, lane));
+        s = softmax_row<D>(mv_p<D, kLd<D>>(stage_w<D>(wl, a.W[w2]), nullptr, h, lane));
     }
     const Fld<D> mp = a.p_drop > 0.f ? drop_scale<D>(seed, v, row, g, a.p_drop, a.drop_scale) : Fld<D>{};
     const Fld<D> pp = a.p_drop > 0.f ? fmap2<D>(sp, mp, mul) : sp;
@@ -622,7 +715,7 @@ __global__ __launch_bounds__(256) void pref_bwd_rows(PrefArgs a) {
         if (a.p_drop > 0.f) dpp = fmap2<D>(dpp, mp, mul);
         const Fld<D> dzp = fmap2<D>(dpp, sp, sig_bwd);
         fstore<D>(a.dz[wp], out, g, dzp);
-        fatomic<D>(a.gC, row, g, mvt<D, kLd<D>>(stage_w<D>(wl, a.W[wp]), dzp, lane));
+        fatomic<D>(a.gC, row, g, mvt_p<D, kLd<D>>(stage_w<D>(wl, a.W[wp]), dzp, lane));
         da = fmap2<D>(g1, pp, mul);
         fatomic<D>(v ? a.gTE : a.gIE, row, g, fmap2<D>(da, s, mul));
         da = fmap2<D>(da, E, mul);  // d softmax output
@@ -630,11 +723,11 @@ __global__ __launch_bounds__(256) void pref_bwd_rows(PrefArgs a) {
     const float dot = rsum<D>(fmap2<D>(da, s, mul));
     const Fld<D> dq = fmap2<D>(s, da, [&](float y, float gy) { return y * (gy - dot); });
     fstore<D>(a.dz[w2], out, g, dq);
-    const Fld<D> dh = mvt<D, kLd<D>>(stage_w<D>(wl, a.W[w2]), dq, lane);
+    const Fld<D> dh = mvt_p<D, kLd<D>>(stage_w<D>(wl, a.W[w2]), dq, lane);
     const Fld<D> h = fload<D>(v ? a.ht : a.hv, out, g);  // this lane's own store above
     const Fld<D> dz1 = fmap2<D>(dh, h, [](float gy, float y) { return gy * (1.f - y * y); });
     fstore<D>(a.dz[w1], out, g, dz1);
-    fatomic<D>(a.gFE, row, g, mvt<D, kLd<D>>(stage_w<D>(wl, a.W[w1]), dz1, lane));
+    fatomic<D>(a.gFE, row, g, mvt_p<D, kLd<D>>(stage_w<D>(wl, a.W[w1]), dz1, lane));
 }
 
 // ---------------------------------------------------------------------------
@@ -946,7 +1039,6 @@ __global__ __launch_bounds__(64 * kNceWaves) void nce_bwd(NceArgs a) {
     const float* own_n = a.nrm + ((int64_t)(term * 2 + mode) * B) * D;
     const float* oth_n = a.nrm + ((int64_t)(term * 2 + (mode ^ 1)) * B) * D;
     const float* ttl = a.ttl + term * B;
-    const Fld<D> X = fload<D>(own_n, bo, g);
     const float ttl_own = (mode == 0 && bo >= 0) ? ttl[bo] : 1.f;
     float* tl = sm + w * TILE;
     Fld<D> O = fzero<D>();
@@ -983,6 +1075,7 @@ __global__ __launch_bounds__(64 * kNceWaves) void nce_bwd(NceArgs a) {
         }
         return ev;
     };
+    const Fld<D> X = fload<D>(own_n, bo, g);
     Fld<D> Y = fload<D>(oth_n, row_of(w), g);
     floatx4 tv = ttl_of(w);
     floatx4 ev = e_of(w);
@@ -1373,6 +1466,7 @@ __global__ __launch_bounds__(256) void unit_w_bwd(const float* part, int nblk, c
 // ---------------------------------------------------------------------------
 using namespace rsx;
 
+
 extern "C" {
 
 int rsx_smore_gates(int32_t backward, const float* const* conv, const float* item, const float* const* W,
@@ -1420,11 +1514,13 @@ int rsx_smore_gates(int32_t backward, const float* const* conv, const float* ite
     hipStream_t s = as_stream(stream);
     switch (d) {
         case 64:
-            if (backward) hipLaunchKernelGGL(sf::gates_bwd<64>, grid, dim3(256), 0, s, a);
+            if (backward && !mul) hipLaunchKernelGGL(sf::gates_bwd_res<64>, grid, dim3(256), 0, s, a);
+            else if (backward) hipLaunchKernelGGL(sf::gates_bwd<64>, grid, dim3(256), 0, s, a);
             else hipLaunchKernelGGL(sf::gates_fwd<64>, grid, dim3(256), 0, s, a);
             break;
         case 128:
-            if (backward) hipLaunchKernelGGL(sf::gates_bwd<128>, grid, dim3(256), 0, s, a);
+            if (backward && !mul) hipLaunchKernelGGL(sf::gates_bwd_res<128>, grid, dim3(256), 0, s, a);
+            else if (backward) hipLaunchKernelGGL(sf::gates_bwd<128>, grid, dim3(256), 0, s, a);
             else hipLaunchKernelGGL(sf::gates_fwd<128>, grid, dim3(256), 0, s, a);
             break;
         default: return RSX_ERR_UNSUPPORTED;

@@ -199,6 +199,46 @@ def test_view_prop3_equals_three_view_props(cuda, d, L_):
         assert torch.equal(o, o1) and torch.equal(g, g1)
 
 
+@pytest.mark.parametrize("d", [64, 128])
+def test_view_prop3_tagged_users(cuda, d):
+    """view_prop3 with the batch-row tags (the R products on the tagged users only: the
+    preference block reads no other user row) against the full form: the tagged users'
+    and every item row of the forward bit for bit, and the input gradients bit for bit
+    for an upstream gradient that is zero off the tagged users (the batch-row preference
+    block's); kNN graphs in 64-wide work items."""
+    from rsx import smore_fuse as SF
+    from rsx.smore import _DevGraph, _RowTags
+
+    rng = np.random.default_rng(d)
+    nu, ni = 1200, 500
+
+    def graph(nr, nc, nnz, zipf, chunk):
+        r = rng.integers(0, nr, nnz)
+        c = (rng.zipf(zipf, nnz) - 1) % nc
+        key = np.unique(r * nc + c, return_index=True)[1]
+        return _DevGraph(r[key], c[key], rng.random(key.size).astype(np.float32), nr, nc, cuda, chunk)
+
+    Gs = [graph(ni, ni, 6000, 1.3, 64), graph(ni, ni, 5000, 1.6, 64), graph(ni, ni, 9000, 1.2, 64)]
+    R = graph(nu, ni, 14000, 1.4, 32)
+    tags = _RowTags(nu + ni, cuda)
+    users = torch.from_numpy(rng.integers(0, nu, 300)).to(cuda)
+    tags.mark(torch.cat([users, nu + torch.from_numpy(rng.integers(0, ni, 600)).to(cuda)]))
+    xs = [torch.randn(ni, d, device=cuda, requires_grad=True) for _ in range(3)]
+    outs = SF.view_prop3(xs, Gs, R, 1, nu, tags=tags)
+    full = SF.view_prop3(xs, Gs, R, 1, nu)
+    rows = torch.cat([torch.unique(users), torch.arange(nu, nu + ni, device=cuda)])
+    for o, f in zip(outs, full):
+        assert torch.equal(o[rows], f[rows])
+    m = torch.zeros(nu + ni, 1, device=cuda)
+    m[users] = 1.0
+    m[nu:] = 1.0
+    ups = [torch.randn(nu + ni, d, device=cuda) * m for _ in range(3)]
+    gt = torch.autograd.grad(sum((o * w).sum() for o, w in zip(outs, ups)), xs)
+    gf = torch.autograd.grad(sum((o * w).sum() for o, w in zip(full, ups)), xs)
+    for a, b in zip(gt, gf):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("kind", ["store", "add"])
 def test_spmm_batch_many_fixups(cuda, kind):
     """rsx_spmm_batch with more hub-row fixups than ride along in one launch (> 1024 over

@@ -1,14 +1,16 @@
-# C3 / C5 step time: the batch-row preference forward split (RSX_PREF_SPLIT) x the two
-# projections' backward on two streams (RSX_PROJ_STREAM)
+# SMORE GPU tests, then the C5 / C3 bench lines and one step's kernel sequence of each
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-OUT=${OUT:-gpurun_out/sab}
+export TMPDIR=/tmp
+OUT=${OUT:-gpurun_out/ab}
 mkdir -p $OUT
-for w in c3 c5; do
-  for sp in 0 1; do
-    for ps in 0 1; do
-      RSX_PREF_SPLIT=$sp RSX_PROJ_STREAM=$ps timeout -k 10 200 python bench.py --workload $w --steps 20 --warmup 5 --no-cpu-baseline > $OUT/${w}_s${sp}_p${ps}.json 2> $OUT/${w}_s${sp}_p${ps}.err || exit 1
-      python -c "import json; d=json.load(open('$OUT/${w}_s${sp}_p${ps}.json')); print('$w split=$sp proj_stream=$ps', round(d['ms_per_step'], 3))"
-    done
+timeout -k 10 600 python -u -m pytest tests/test_gpu_smore.py tests/test_gpu_smore_fuse.py tests/test_gpu_smore_dist.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $OUT/pytest.log 2>&1
+rc=$?; tail -3 $OUT/pytest.log; [ $rc -eq 0 ] || exit $rc
+for w in c5 c3; do
+  for v in ${VARIANTS:-1}; do
+    RSX_SMORE_WGRAD_STREAM=$v timeout -k 10 300 python bench.py --workload $w --no-cpu-baseline --steps 30 --warmup 6 > $OUT/${w}_w$v.json 2> $OUT/${w}_w$v.err || exit 1
+    python -c "import json;d=json.load(open('$OUT/${w}_w$v.json'));print('$w wgrad-stream=$v', d['ms_per_step'])"
   done
 done
+OUT=$OUT/seq bash tools/gpu/c5_seq.sh
+LEG=c3 OUT=$OUT/seq3 bash tools/gpu/c5_seq.sh

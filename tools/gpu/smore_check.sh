@@ -9,3 +9,4 @@ rc=$?; tail -3 $OUT/pytest.log; [ $rc -eq 0 ] || exit $rc
 OUT=$OUT/seq bash tools/gpu/c5_seq.sh
 timeout -k 10 300 python bench.py --workload c3 --no-cpu-baseline --steps 30 --warmup 6 > gpurun_out/sc/c3.json 2> gpurun_out/sc/c3.err || exit 1
 python -c "import json;d=json.load(open('gpurun_out/sc/c3.json'));print('c3', d['ms_per_step'])"
+timeout -k 10 120 python tools/gpu/micro_gemm.py > gpurun_out/sc/micro_gemm.json 2>&1; cat gpurun_out/sc/micro_gemm.json
