@@ -345,7 +345,27 @@ __global__ __launch_bounds__(256) void gates_fwd(GateArgs a) {
     __shared__ __attribute__((aligned(16))) float wl[D * kLd<D>];
     const int lane = threadIdx.x & 63, g = lane >> 4;
     const bool split = gridDim.y > 1;
-    if (split) stage_w<D>(wl, a.W[blockIdx.y]);
+    if (split) {  // one gate per block row: the next row block's rows load during this one's product
+        const int m = (int)blockIdx.y;
+        const float* W = stage_w<D>(wl, a.W[m]);
+        auto row_of = [&](int64_t bx) {
+            const int64_t r = (bx * 4 + (threadIdx.x >> 6)) * 16 + (lane & 15);
+            return bx < a.nbx && r < a.n ? r : (int64_t)-1;
+        };
+        Fld<D> cvn = fload<D>(a.conv[m], row_of(blockIdx.x), g);
+#pragma unroll 1
+        for (int64_t bx = blockIdx.x; bx < a.nbx; bx += gridDim.x) {  // block-uniform
+            const int64_t row = row_of(bx);
+            const Fld<D> cv = cvn;
+            const Fld<D> it = fload<D>(a.item, row, g);
+            cvn = fload<D>(a.conv[m], row_of(bx + gridDim.x), g);
+            const Fld<D> s = fmap<D>(mv_p<D, kLd<D>>(W, a.b[m], cv, lane), sigm);
+            const Fld<D> o = a.mul ? fmap2<D>(it, s, [](float x, float y) { return x * y; })
+                                   : fmap2<D>(it, s, [&](float x, float y) { return x + a.scale * y; });
+            fstore<D>(a.out[m], row, g, o);
+        }
+        return;
+    }
 #pragma unroll 1
     for (int64_t bx = blockIdx.x; bx < a.nbx; bx += gridDim.x) {  // block-uniform
         const int64_t n0 = (bx * 4 + (threadIdx.x >> 6)) * 16;
@@ -418,10 +438,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void g
     const int lane = threadIdx.x & 63, g = lane >> 4;
     const int m = (int)blockIdx.y;
     const float* W = stage_w<D>(wl, a.W[m]);
+    auto row_of = [&](int64_t bx) {
+        const int64_t r = (bx * 4 + (threadIdx.x >> 6)) * 16 + (lane & 15);
+        return bx < a.nbx && r < a.n ? r : (int64_t)-1;
+    };
+    // the next row block's conv rows are loaded while this one's products run
+    Fld<D> cvn = fload<D>(a.conv[m], row_of(blockIdx.x), g);
 #pragma unroll 1
     for (int64_t bx = blockIdx.x; bx < a.nbx; bx += gridDim.x) {  // block-uniform
-        const int64_t n0 = (bx * 4 + (threadIdx.x >> 6)) * 16;
-        const int64_t row = n0 + (lane & 15) < a.n ? n0 + (lane & 15) : -1;
+        const int64_t row = row_of(bx);
         if (m == 0) {  // g_item = sum of the three upstream gradients, in gate order
             Fld<D> gi = fzero<D>();
 #pragma unroll 1
@@ -432,8 +457,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void g
         }
         Fld<D> dz;
         {
-            const Fld<D> s = fmap<D>(mv_p<D, kLd<D>>(W, a.b[m], fload<D>(a.conv[m], row, g), lane), sigm);
-            const Fld<D> go = a.gout[m] ? fload<D>(a.gout[m], row, g) : fzero<D>();
+            const Fld<D> cv = cvn;
+            const Fld<D> go = a.gout[m] ? fload<D>(a.gout[m], row, g) : fzero<D>();  // in flight during the product
+            cvn = fload<D>(a.conv[m], row_of(bx + gridDim.x), g);
+            const Fld<D> s = fmap<D>(mv_p<D, kLd<D>>(W, a.b[m], cv, lane), sigm);
             dz = fmap2<D>(fmap<D>(go, [&](float x) { return a.scale * x; }), s,
                           [](float x, float y) { return x * ((1.f - y) * y); });
         }
