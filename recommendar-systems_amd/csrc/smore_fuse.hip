@@ -682,8 +682,10 @@ __global__ __launch_bounds__(256) void pref_combine(PrefArgs a) {
 }
 
 // The batch-row backward (rsx_smore_pref_rows, gradients added by atomics): blockIdx.y = 0
-// the fusion view + the pass-through terms, 1 the image view, 2 the text view — the same
-// arithmetic as pref_bwd's split form, ordered so that few row fields are live at once
+// the fusion view + the pass-through terms, 1 / 2 the image / text view's query chain,
+// 3 / 4 the image / text view's preference gate — the same arithmetic as pref_bwd's split
+// form (each block row recomputes the forward values it needs), ordered so that few row
+// fields are live at once
 // (at d = 128 a field is 32 VGPRs a lane: pref_bwd's order keeps ~9 of them across its
 // matrix products and spills): the gate product first (C then dead), the query MLP from
 // FE (dead after), tanh rows reloaded from the hv / ht rows this kernel wrote, each view's
@@ -721,32 +723,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
         fatomic<D>(a.gC, row, g, fmap2<D>(gC, mvt_p<D, kLd<D>>(W, dz, lane), add));
         return;
     }
-    const int v = part - 1;  // 0: image view, 1: text view
+    // parts 1 / 2: the image / text view's query chain (d IE / d TE, d FE); parts 3 / 4 the
+    // same view's preference gate (d C): each recomputes the forward values it needs (the
+    // gate sigmoid, resp. the softmax), so the longest chain is 5 products instead of 6
+    const int v = (part - 1) & 1;  // 0: image view, 1: text view
+    const bool gate_part = part >= 3;
     const int w1 = v ? kW1t : kW1v, w2 = v ? kW2t : kW2v, wp = v ? kWtp : kWip;
     // the view's preference gate on C (dropout mask applied after the sigmoid)
     const Fld<D> sp = fmap<D>(mv_p<D, kLd<D>>(stage_w<D>(wl, a.W[wp]), a.b[wp], fload<D>(a.C, row, g), lane), sigm);
     Fld<D> s;
     {
         const Fld<D> h = fmap<D>(mv_p<D, kLd<D>>(stage_w<D>(wl, a.W[w1]), a.b[w1], fload<D>(a.FE, row, g), lane), tanh_);
-        fstore<D>(v ? a.ht : a.hv, out, g, h);
+        if (!gate_part) fstore<D>(v ? a.ht : a.hv, out, g, h);
         s = softmax_row<D>(mv_p<D, kLd<D>>(stage_w<D>(wl, a.W[w2]), nullptr, h, lane));
     }
     const Fld<D> mp = a.p_drop > 0.f ? drop_scale<D>(seed, v, row, g, a.p_drop, a.drop_scale) : Fld<D>{};
-    const Fld<D> pp = a.p_drop > 0.f ? fmap2<D>(sp, mp, mul) : sp;
     const Fld<D> g1 = g1_of();
-    Fld<D> da;  // d (s * E)
-    {
-        const Fld<D> E = fload<D>(v ? a.TE : a.IE, row, g);
-        // x = pp * (s * E)
-        Fld<D> dpp = fmap3<D>(g1, s, E, [](float u, float q, float e) { return u * (q * e); });
+    if (gate_part) {
+        // x = pp * (s * E): d pp, through the dropout mask and the sigmoid
+        Fld<D> dpp = fmap3<D>(g1, s, fload<D>(v ? a.TE : a.IE, row, g), [](float u, float q, float e) { return u * (q * e); });
         if (a.p_drop > 0.f) dpp = fmap2<D>(dpp, mp, mul);
         const Fld<D> dzp = fmap2<D>(dpp, sp, sig_bwd);
         fstore<D>(a.dz[wp], out, g, dzp);
         fatomic<D>(a.gC, row, g, mvt_p<D, kLd<D>>(stage_w<D>(wl, a.W[wp]), dzp, lane));
-        da = fmap2<D>(g1, pp, mul);
-        fatomic<D>(v ? a.gTE : a.gIE, row, g, fmap2<D>(da, s, mul));
-        da = fmap2<D>(da, E, mul);  // d softmax output
+        return;
     }
+    const Fld<D> pp = a.p_drop > 0.f ? fmap2<D>(sp, mp, mul) : sp;
+    Fld<D> da = fmap2<D>(g1, pp, mul);  // d (s * E)
+    fatomic<D>(v ? a.gTE : a.gIE, row, g, fmap2<D>(da, s, mul));
+    da = fmap2<D>(da, fload<D>(v ? a.TE : a.IE, row, g), mul);  // d softmax output
     const float dot = rsum<D>(fmap2<D>(da, s, mul));
     const Fld<D> dq = fmap2<D>(s, da, [&](float y, float gy) { return y * (gy - dot); });
     fstore<D>(a.dz[w2], out, g, dq);
@@ -1612,7 +1617,7 @@ int rsx_smore_pref_rows(int32_t backward, const float* const* W, const float* co
     // batch-row backward: the three views' chains as three block rows (gradients are atomics
     // there); batch-row forward with the scratch hv: likewise, then pref_combine
     const bool split_fwd = !backward && rows && hv;
-    const dim3 grid((unsigned)(((n + 15) / 16 + 3) / 4), (backward && rows) || split_fwd ? 3 : 1);
+    const dim3 grid((unsigned)(((n + 15) / 16 + 3) / 4), backward && rows ? 5 : split_fwd ? 3 : 1);
     hipStream_t s = as_stream(stream);
     if (split_fwd) {
         if (n == 0) return RSX_OK;
