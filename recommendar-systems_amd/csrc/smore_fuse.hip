@@ -508,10 +508,18 @@ struct PrefArgs {
 // the table row of logical row r (r < 0: none)
 __device__ __forceinline__ int64_t src_row(const PrefArgs& a, int64_t r) { return (r >= 0 && a.rows) ? a.rows[r] : r; }
 
-// Y[row] += x (float atomics: rows repeat within a batch)
+// Y[row] += x (float atomics: rows repeat within a batch).  RSX_PREF_PLAIN_STORES=1 (a timing
+// variant only, tools/build_variant.py: wrong where rows repeat) stores instead, to price the atomics.
+#ifndef RSX_PREF_PLAIN_STORES
+#define RSX_PREF_PLAIN_STORES 0
+#endif
 template <int D>
 __device__ __forceinline__ void fatomic(float* Y, int64_t row, int g, const Fld<D>& x) {
     if (row < 0 || !Y) return;
+    if (RSX_PREF_PLAIN_STORES) {
+        fstore<D>(Y, row, g, x);
+        return;
+    }
 #pragma unroll
     for (int t = 0; t < D / 16; ++t)
 #pragma unroll
