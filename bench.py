@@ -10,12 +10,15 @@ A step = one training batch end to end on the device: triplet sampling
 (shuffle + rejection negatives), 3-layer propagation, BPR loss + backward,
 Horner backward propagation, Adam — one `rsx_lightgcn_step` C-ABI call.
 
-N>1 (one process per GPU, torchrun): weak scaling of the row-sharded design
-(SURVEY 8e): every rank owns a sports-shaped block of users (its own
-interactions, rank-seeded) over the SAME 18,357 items; user rows stay local,
-item rows are reduced across ranks after every propagation layer
-(all-reduce of the item partial sums over RCCL/xGMI) and the item-side
-gradient likewise.  value = all ranks' interactions / max-over-ranks time.
+N>1 (one process per GPU, torchrun or `--gpus N`): weak scaling, data-parallel
+by default (`--dist dp`, rsx.dp / csrc/dp.hip): every rank holds the same
+sports-shaped graph and a bit-identical replica of the tables, and trains its own
+2048 triplets of the global batch of N*2048 (the reference objective at that
+batch); per step the ranks all-gather their triplets and their loss-gradient rows
+(~1.6 MB per rank) over RCCL/xGMI and run the same backward and Adam.
+`--dist rowshard`: the row-sharded design (rsx.dist): every rank owns
+its own sports-shaped block of users over the same items, the item partials
+all-reduced per layer.  value = all ranks' interactions / max-over-ranks time.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
 Prints ONE JSON line on rank 0.
@@ -441,17 +444,18 @@ def _c4_chunk(args):
     return c, u, i, lab
 
 
-def load_graph(workload, rank, world, c4_chunks=None):
+def load_graph(workload, rank, world, c4_chunks=None, replicated=False):
     """(train users, train items, valid users, valid items, n_users, n_items, d, desc) of
     this rank.  c2: every rank owns its own sports-shaped block of users (rank-seeded)
-    over the same items (weak scaling).  c4: the fixed 10M-user graph, whose 8
-    user chunks are dealt to the ranks in contiguous ranges (local user ids)."""
+    over the same items (row-sharded weak scaling), or with `replicated` every rank the
+    same graph (data-parallel).  c4: the fixed 10M-user graph, whose 8 user chunks are
+    dealt to the ranks in contiguous ranges (local user ids)."""
     from rsx import synth
 
     if workload in ("c2", "baby"):
         shape = "sports" if workload == "c2" else "baby"
         nu0, ni, ne0 = synth.SHAPES[shape]
-        df = synth.amazon_like(nu0, ni, ne0, seed=rank)
+        df = synth.amazon_like(nu0, ni, ne0, seed=0 if replicated else rank)
         tr, va = df[df.x_label == 0], df[df.x_label == 1]
         desc = (f"C2: LightGCN K=3 d=64, sports-shaped (35,598 users x 18,357 items per rank), B=2048 per rank, "
                 f"device sampler, fused step" if workload == "c2" else
@@ -640,6 +644,11 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sharded", action="store_true",
                     help="use the row-sharded engine even at N=1 (measures its host/launch overhead)")
+    ap.add_argument("--dist", choices=["dp", "rowshard"], default=None,
+                    help="N>1 scheme for c2/baby: dp (default: the graph replicated, the global batch split, "
+                         "rsx.dp) or rowshard (users row-sharded, rsx.dist); c4 is always rowshard")
+    ap.add_argument("--dp", action="store_true",
+                    help="use the data-parallel engine even at N=1 (measures its exchange-free overhead)")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--eval-users", type=int, default=None, help="default: all valid users (c4: 32768 per rank)")
     ap.add_argument("--c4-chunks", type=int, default=None,
@@ -676,11 +685,18 @@ def main():
     B = args.batch // world if big else args.batch
     if big and B * world != args.batch:
         raise SystemExit(f"--batch {args.batch} does not split evenly over {world} ranks")
-    tu, ti, vu_all, vi_all, nu, ni, d, desc = load_graph(args.workload, rank, world, args.c4_chunks)
+    scheme = args.dist or ("rowshard" if big else "dp")
+    if big and scheme != "rowshard":
+        raise SystemExit("--workload c4 is the row-sharded strong-scaling leg")
+    dp = not big and not args.sharded and (args.dp or (world > 1 and scheme == "dp"))
+    tu, ti, vu_all, vi_all, nu, ni, d, desc = load_graph(args.workload, rank, world, args.c4_chunks, replicated=dp)
     if big and args.c4_chunks:
         desc += f" [only {args.c4_chunks} of 8 user chunks built]"
-    sharded = world > 1 or big or args.sharded
-    if sharded:
+    if dp:
+        desc = desc.replace("per rank), B=2048 per rank", "), the graph replicated on every rank, "
+                                                              f"B={B} per rank, global batch {B * world}")
+    sharded = (world > 1 or big or args.sharded) and not dp
+    if sharded or dp:
         import torch.distributed as dist
 
         if world == 1:  # a one-rank group for the sharded engine
@@ -703,7 +719,12 @@ def main():
         U0 = torch.nn.init.xavier_uniform_(torch.empty(nu, d)).numpy()
         I0 = torch.nn.init.xavier_uniform_(torch.empty(ni, d)).numpy()
 
-    if sharded:
+    if dp:
+        from rsx.dp import DataParallelLightGCNEngine
+
+        eng = DataParallelLightGCNEngine(tu, ti, nu, ni, d, args.n_layers, 1e-2, 1e-3, dev, U0, I0, seed=0,
+                                         batch=B)
+    elif sharded:
         from rsx.dist import ShardedLightGCNEngine
 
         eng = ShardedLightGCNEngine(tu, ti, nu, ni, d, args.n_layers, 1e-2, 1e-3, dev, U0, I0, seed=rank,
@@ -720,6 +741,17 @@ def main():
     done = {"inter": 0}
 
     def one_step():
+        if dp:  # global step j: this rank's slice j W + rank of the epoch (S W balanced slices)
+            S = eng.steps_per_epoch()
+            j = pos["start"]
+            a, e = ops.DeviceSampler.slice_bounds(E, S * world, j * world + rank)
+            eng.step_index(pos["epoch"], j)
+            done["inter"] += e - a
+            pos["start"] += 1
+            if pos["start"] >= S:
+                pos["start"] = 0
+                pos["epoch"] += 1
+            return
         b = min(B, E - pos["start"])
         eng.step(epoch=pos["epoch"], start=pos["start"])
         done["inter"] += b
@@ -747,7 +779,7 @@ def main():
     gpu_ms = ev0.elapsed_time(ev1)
     per_rank = _rank_report(wall, gpu_ms, args.steps, world, dev)
     rccl_world = None
-    if sharded and getattr(eng, "_comm", None) is not None:
+    if (sharded or dp) and getattr(eng, "_comm", None) is not None:
         # the world the step's own communicator spans: an all-reduce of ones on rsx_comm
         ones = torch.ones(1, dtype=torch.float32, device=dev)
         L.check(L.lib().rsx_comm_allreduce_f32(eng._comm, ones.data_ptr(), 1, ops._stream()),
@@ -775,7 +807,7 @@ def main():
             torch.distributed.barrier()
         # every rank runs the same number of steps (its collectives pair with its peers'):
         # the largest per-rank batch count; a rank with fewer batches wraps into its next epoch
-        nb = torch.tensor([float(-(-E // B))], dtype=torch.float64, device=dev)
+        nb = torch.tensor([float(eng.steps_per_epoch() if dp else -(-E // B))], dtype=torch.float64, device=dev)
         if world > 1:
             torch.distributed.all_reduce(nb, op=torch.distributed.ReduceOp.MAX)
         nb = int(nb.item())
@@ -799,6 +831,8 @@ def main():
     vusers = np.unique(vu_all)
     if args.eval_users:
         vusers = vusers[: args.eval_users]
+    if dp and world > 1:  # the replicas split the evaluation users (metric sums would be gathered)
+        vusers = vusers[rank * vusers.size // world:(rank + 1) * vusers.size // world]
     rp, mc = graph.history_csr(tu, ti, nu)
     rp_d, mc_d = torch.from_numpy(rp).to(dev), torch.from_numpy(mc).to(dev)
     vu_d = torch.from_numpy(vusers.astype(np.int64)).to(dev)
@@ -871,7 +905,7 @@ def main():
              "note": ("the sports/baby working set (<50 MB) is Infinity-Cache resident" if not big else
                       "C4 shard: tables of GBs, gathers from HBM")}
     roof, kernels = store, [store]
-    if not sharded:
+    if not sharded and hasattr(eng, "adj"):
         # the step's largest single launch: the last backward layer with Adam fused into
         # its epilogue, exactly as the tagged step issues it (rows of the last batch
         # tagged; sparse G' and clears on those rows), on scratch copies of p, m, v
@@ -931,11 +965,15 @@ def main():
                      "5+Geometric degrees mean 10, reference split rule); xavier-uniform-bound init"),
             "config": {"workload": desc, "model": "LightGCN", "n_layers": args.n_layers, "embedding_size": d,
                        "global_batch": B * world, "per_rank_batch": B,
-                       "leg": ("the metric's leg: C2 per rank, weak scaling (per-GPU work fixed as N grows)"
+                       "leg": ("the metric's leg: C2, weak scaling (per-GPU work fixed as N grows)"
                                if args.workload == "c2" else
                                "strong-scaling leg: the fixed C4 graph and global batch split over the ranks"
-                               if big else "baby per rank, weak scaling"),
-                       "parallelism": f"rowshard{world}" if sharded else "single"},
+                               if big else "baby, weak scaling"),
+                       "parallelism": (f"dp{world}" if dp else f"rowshard{world}" if sharded else "single"),
+                       "scheme": ("data-parallel: graph + tables replicated, global batch N*B, per step an "
+                                  "all-gather of the ranks' triplets and loss-gradient rows (rsx.dp)" if dp else
+                                  "row-sharded users, replicated items, item partials all-reduced per layer "
+                                  "(rsx.dist)" if sharded else "one GPU")},
             "fullsort_items_per_s": items_per_s,
             "fullsort": {"eval_users": int(n_eval), "n_items": ni, "k": 50,
                          "s_per_eval": eval_s,
@@ -960,7 +998,7 @@ def main():
         _json_line(out)
     if hasattr(eng, "close"):
         eng.close()
-    if sharded:
+    if sharded or dp:
         torch.distributed.destroy_process_group()
 
 

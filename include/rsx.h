@@ -311,6 +311,17 @@ int rsx_sample_epoch(const int32_t* inter_u, const int32_t* inter_i, int64_t n_i
                      int64_t n_all_items, uint64_t seed, int64_t epoch, int64_t batch, int64_t* out,
                      rsx_stream_t stream);
 
+/* The same epoch stream cut into n_slices balanced slices instead of fixed batches:
+ * slice j = epoch positions [floor(j n_inter / S), floor((j+1) n_inter / S)) (sizes
+ * differ by at most one; 1 <= S <= n_inter), stored [3][Bj] contiguous at
+ * out + 3*floor(j n_inter / S).  The sharded trainers' epochs: every rank runs the
+ * same step count S and visits each of its interactions once (replaces the reference
+ * DataLoader's per-epoch batch walk, src/utils/dataloader.py:226-258). */
+int rsx_sample_epoch_slices(const int32_t* inter_u, const int32_t* inter_i, int64_t n_inter,
+                            const int64_t* hist_rowptr, const int32_t* hist_col, const int32_t* all_items,
+                            int64_t n_all_items, uint64_t seed, int64_t epoch, int64_t n_slices, int64_t* out,
+                            rsx_stream_t stream);
+
 /* Gather rows: out[b] = src[idx[b] + offset]  (u_embeddings = user_all[user] etc.). */
 int rsx_gather_rows(const float* src, const int64_t* idx, int64_t n, int64_t offset, int32_t d,
                     float* out, rsx_stream_t stream);
@@ -876,6 +887,58 @@ typedef struct rsx_sharded_lgcn_step {
 
 int rsx_sharded_lightgcn_step(const rsx_sharded_lgcn_step* st, rsx_stream_t stream);
 int rsx_sharded_lightgcn_forward(const rsx_sharded_lgcn_step* st, rsx_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
+/* Data-parallel LightGCN over RCCL (one process per GPU, graph replicated)   */
+/* ------------------------------------------------------------------------ */
+/*
+ * Every rank holds the whole graph and a bit-identical replica of p, m, v; a step
+ * trains the global batch of all ranks' triplets (rank r its own [3][batch]): the
+ * reference objective at batch sum_r batch_r (src/models/lightgcn.py:132-156 with the
+ * mean and the Frobenius norms over the global batch; src/common/trainer.py:186-238
+ * at batch W B).  The step is lgcn_step_stored_layers' (K = 2..4) with two
+ * exchanges, both all-gathers: every rank's triplets (`slots`, [world][3 cap + 1]
+ * int64: count, users, positives, negatives) and every rank's G' = dL/dfinal/(K+1)
+ * at its own occurrence rows plus its four f64 loss totals (`blocks`, [world]
+ * [rsx_dp_block_floats(cap, d)] floats).  Each rank merges the blocks into the same
+ * G' (per row a sum over ranks in rank order, led through `pos` [world][N] int64,
+ * zero-filled once), counts every triplet's rows (reg_cnt, the global regulariser),
+ * tags the union of the ranks' batch rows (row_tag; own_tag: this rank's, for its
+ * last forward layer) and runs the same backward and Adam.  tag_dev: the step's tag
+ * on the device (> 0, fresh per step, e.g. the low word of adam.step_dev), so the
+ * step captures once in a hipGraph.  g and reg_cnt must be zero between steps (true
+ * from zero-filled buffers and after every step).
+ */
+typedef struct rsx_dp_lgcn_step {
+    const rsx_csr* adj;         /* the whole graph */
+    int64_t n_users, n_items;
+    int32_t d, n_layers;        /* n_layers 2..4 */
+    float reg;
+    int32_t pad0;
+    float* p; float* m; float* v;
+    float* s; float* h0; float* h1;   /* E^1, E^2 (h0, h1), E^3 (s, K = 4 only) */
+    float* final_emb; float* g;
+    float* slab;
+    int64_t* triplets;          /* this rank's [3][batch] */
+    int64_t batch;              /* 1 <= batch <= cap */
+    rsx_adam adam;
+    float* loss_out;            /* [1]: the global batch's loss */
+    double* loss_acc;           /* [1] or NULL */
+    void* ws; size_t ws_bytes;  /* >= rsx_bpr_ws_bytes(batch) */
+    rsx_comm_t comm;
+    int32_t* row_tag;           /* [N] */
+    int32_t* own_tag;           /* [N] */
+    const int32_t* tag_dev;     /* [1] */
+    int32_t* reg_cnt;           /* [3 N + 4] */
+    int32_t* halt;              /* [2] or NULL: set by a NaN global loss (as rsx_lgcn_step.halt) */
+    int64_t cap;                /* per-rank batch capacity (every rank the same) */
+    int64_t* slots;             /* [world][3 cap + 1] */
+    float* blocks;              /* [world][rsx_dp_block_floats(cap, d)] */
+    int64_t* pos;               /* [world][N] */
+} rsx_dp_lgcn_step;
+
+int rsx_dp_lightgcn_step(const rsx_dp_lgcn_step* st, rsx_stream_t stream);
+size_t rsx_dp_block_floats(int64_t cap, int32_t d);
 
 #ifdef __cplusplus
 }

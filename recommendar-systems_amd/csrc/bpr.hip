@@ -38,6 +38,15 @@ struct BprArgs {
     int64_t n_rows;
     int32_t* halt;     // bpr_fused (optional): [2] set to {1, tag} by the first NaN loss
     int32_t tag;
+    // bpr_fused, data-parallel form (dp_tot != NULL): the loss is the mean over the GLOBAL
+    // batch, B_glob = the sum of every rank's count in the gathered triplet slots
+    // (dp_slots[r * dp_slot_len], r < dp_world); no occurrence counts are written (the
+    // merge counts every rank's triplets) and the last block stores this rank's four f64
+    // totals (loss terms, |U|^2, |P|^2, |N|^2) at dp_tot instead of finishing the loss
+    const int64_t* dp_slots;
+    int64_t dp_slot_len;
+    int32_t dp_world;
+    double* dp_tot;
 };
 
 __device__ __forceinline__ float softplus_neg(float x) {
@@ -244,6 +253,11 @@ __global__ __launch_bounds__(kBprBlock) void bpr_fused(BprArgs a) {
     const int li = threadIdx.x % G;
     const int64_t b = (int64_t)blockIdx.x * GPB + threadIdx.x / G;
     double t_loss = 0.0, t_u = 0.0, t_p = 0.0, t_n = 0.0;
+    int64_t bdiv = a.batch;  // the mean's batch: this launch's, or the global batch (dp)
+    if (a.dp_tot) {
+        bdiv = 0;
+        for (int r = 0; r < a.dp_world; ++r) bdiv += a.dp_slots[(int64_t)r * a.dp_slot_len];
+    }
     if (b < a.batch) {
         const int64_t u = a.trip[b];
         const int64_t p = a.trip[a.batch + b] + a.n_users;
@@ -275,7 +289,7 @@ __global__ __launch_bounds__(kBprBlock) void bpr_fused(BprArgs a) {
         const float delta = sp - sn;
         const float sg = 1.f / (1.f + expf(-delta));
         const float term = -logf(1e-10f + sg);
-        const float coef = -(sg * (1.f - sg)) / (1e-10f + sg) / (float)a.batch;
+        const float coef = -(sg * (1.f - sg)) / (1e-10f + sg) / (float)bdiv;
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
             const int col = li + c * G;
@@ -290,9 +304,11 @@ __global__ __launch_bounds__(kBprBlock) void bpr_fused(BprArgs a) {
             atomicAdd(a.g_fin + n * D + col, gn);
         }
         if (li == 0) {
-            atomicAdd(a.reg_cnt + 3 * u + 0, 1);
-            atomicAdd(a.reg_cnt + 3 * p + 1, 1);
-            atomicAdd(a.reg_cnt + 3 * n + 2, 1);
+            if (!a.dp_tot) {
+                atomicAdd(a.reg_cnt + 3 * u + 0, 1);
+                atomicAdd(a.reg_cnt + 3 * p + 1, 1);
+                atomicAdd(a.reg_cnt + 3 * n + 2, 1);
+            }
             t_loss = (double)term;
         }
         t_u = (double)qu;
@@ -355,6 +371,12 @@ __global__ __launch_bounds__(kBprBlock) void bpr_fused(BprArgs a) {
             }
             __syncthreads();
         }
+    }
+    if (a.dp_tot) {  // this rank's totals for the merge (csrc/dp.hip), which finishes the loss
+        if (threadIdx.x < 4) a.dp_tot[threadIdx.x] = tr[threadIdx.x][0];
+        __syncthreads();
+        if (threadIdx.x == 0) *done = 0;
+        return;
     }
     if (threadIdx.x == 0) {
         const double B = (double)a.batch;
@@ -437,10 +459,10 @@ int bpr_call(int32_t variant, const float* fin, const float* ego, int64_t n_user
     return bpr_dispatch(a, d, s);
 }
 
-int bpr_fused_call(const float* fin, const float* ego, int64_t n_users, int64_t n_items, int32_t d,
+int bpr_fused_args(const float* fin, const float* ego, int64_t n_users, int64_t n_items, int32_t d,
                    const int64_t* trip, int64_t batch, float reg, float g_div, float* g_fin, int32_t* reg_cnt,
                    float* loss_out, double* loss_acc, void* ws, size_t ws_bytes, hipStream_t s, int32_t* halt,
-                   int32_t tag) {
+                   int32_t tag, const int64_t* dp_slots, int64_t dp_slot_len, int32_t dp_world, double* dp_tot) {
     if (!fin || !ego || !trip || !g_fin || !reg_cnt || batch <= 0 || !ws) return RSX_ERR_ARG;
     if (ws_bytes < bpr_ws(batch)) return RSX_ERR_WORKSPACE;
     BprArgs a = {};
@@ -464,6 +486,10 @@ int bpr_fused_call(const float* fin, const float* ego, int64_t n_users, int64_t 
     a.n_rows = n_users + n_items;
     a.halt = halt;
     a.tag = tag;
+    a.dp_slots = dp_slots;
+    a.dp_slot_len = dp_slot_len;
+    a.dp_world = dp_world;
+    a.dp_tot = dp_tot;
     switch (d) {
         case 32: hipLaunchKernelGGL((bpr_fused<32>), dim3((unsigned)((batch + 31) / 32)), dim3(kBprBlock), 0, s, a); break;
         case 64: hipLaunchKernelGGL((bpr_fused<64>), dim3((unsigned)((batch + 15) / 16)), dim3(kBprBlock), 0, s, a); break;
@@ -472,6 +498,14 @@ int bpr_fused_call(const float* fin, const float* ego, int64_t n_users, int64_t 
         default: return RSX_ERR_UNSUPPORTED;
     }
     return last_rc();
+}
+
+int bpr_fused_call(const float* fin, const float* ego, int64_t n_users, int64_t n_items, int32_t d,
+                   const int64_t* trip, int64_t batch, float reg, float g_div, float* g_fin, int32_t* reg_cnt,
+                   float* loss_out, double* loss_acc, void* ws, size_t ws_bytes, hipStream_t s, int32_t* halt,
+                   int32_t tag) {
+    return bpr_fused_args(fin, ego, n_users, n_items, d, trip, batch, reg, g_div, g_fin, reg_cnt, loss_out, loss_acc,
+                          ws, ws_bytes, s, halt, tag, nullptr, 0, 0, nullptr);
 }
 
 }  // namespace rsx

@@ -90,7 +90,18 @@ struct rsx_comm_s {
 };
 
 namespace rsx {
-namespace {
+
+int comm_rank(rsx_comm_t c) { return c->rank; }
+int comm_world(rsx_comm_t c) { return c->world; }
+// The stream the communicator's exchanges run on (host-hook communicators: the caller's):
+// small kernels that only feed later exchanges can run there, off the compute stream.
+hipStream_t comm_stream(rsx_comm_t c, hipStream_t s) { return c->host_fn ? s : c->stream; }
+// The next event of the communicator's ring (for a fence the caller records itself).
+hipEvent_t comm_event(rsx_comm_t c) {
+    hipEvent_t j = c->join[c->next];
+    c->next = (c->next + 1) % kJoinEvents;
+    return j;
+}
 
 // In-place collective `op` (RSX_COLL_*) on buf over the communicator, after the
 // work queued so far on `s`; returns the join event the reader must wait on
@@ -140,6 +151,8 @@ hipEvent_t collective(rsx_comm_t c, int op, void* buf, int64_t count, int dtype,
 hipEvent_t exchange(rsx_comm_t c, float* a, int64_t n, hipStream_t s, int* rc) {
     return collective(c, RSX_COLL_ALLREDUCE, a, n, RSX_COLL_F32, s, rc);
 }
+
+namespace {
 
 // ---- row lists of the sparse exchange -------------------------------------------
 __global__ __launch_bounds__(256) void tag_rows_k(const int64_t* ids, int64_t n, int32_t* tag_arr,

@@ -29,6 +29,15 @@
 
 #include "rsx_common.hpp"
 
+// Profiling ablations (RSX_FS_MODE 1, 4, 5, 6, 8, 9: scores only, pass 1 only, no exact dots,
+// no candidates, candidate counters in out_idx ...) return wrong top-k lists by design: they
+// exist only in an ablation build (tools/build_variant.py fs_abl -DRSX_FS_ABLATION=1).  The
+// product library compiles every FS_ABL(x) to false, and refuses a set RSX_FS_MODE.
+#ifndef RSX_FS_ABLATION
+#define RSX_FS_ABLATION 0
+#endif
+#define FS_ABL(x) (RSX_FS_ABLATION && a.mode == (x))
+
 namespace rsx {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
@@ -111,7 +120,7 @@ struct FsArgs {
     int* ccount;  // [nb][n_chunks]
     float* out_val;
     int64_t* out_idx;
-    int mode;  // profiling ablation (RSX_FS_MODE): 0 full, 1 scores only, 2 no compaction, 3 no final emit
+    int mode;  // profiling ablation (RSX_FS_MODE, ablation builds only, see FS_ABL): 0 = the product
     const __bf16* Ib;  // fs_screen: bf16 item rows + norm block (kScreenRow), padded to whole 32-item tiles
     int n_lists;       // candidate lists per user: n_chunks (fs_tiles), n_chunks * seg_slots (fs_screen)
     int seg_slots;     // fs_screen: segments per (user block, chunk) (1: unsegmented)
@@ -994,7 +1003,7 @@ __device__ __forceinline__ void screen_segment(const FsArgs& a, int64_t ub, int 
         const float tb = unord_f32(th - 1);
         tau = tb == 0.f ? -__FLT_DENORM_MIN__ : tb;
     }
-    if (PH == 0 && a.mode == 5) {  // profiling ablation: pass 1 only
+    if (PH == 0 && FS_ABL(5)) {  // profiling ablation: pass 1 only
         if (uvalid && h == 0) a.ccount[bslot * a.n_lists + li] = 0;
         if (tau == 1234.5f) a.out_val[0] = tau;
         __syncthreads();
@@ -1052,7 +1061,7 @@ __device__ __forceinline__ void screen_segment(const FsArgs& a, int64_t ub, int 
                 up[q] = urows + ju[q] * US;
                 vp[q] = a.I + (int64_t)(e[q] >> 6) * D;
             }
-            if (a.mode == 6) {  // profiling ablation: no dots
+            if (FS_ABL(6)) {  // profiling ablation: no dots
 #pragma unroll
                 for (int q = 0; q < kDrainPer; ++q) sc[q] = unord_f32(ord_f32(tj[q]) + 1u + (unsigned)lane);
             } else if (lane < n) {  // (lanes past n hold item 0: valid addresses, results unused)
@@ -1096,12 +1105,12 @@ __device__ __forceinline__ void screen_segment(const FsArgs& a, int64_t ub, int 
         const unsigned ebase = ((unsigned)(tb + 4 * h) << 6) | (unsigned)j;
         // one ballot per slot; its lanes append at queue[qn + their rank] (branch-free tests)
         auto push = [&](bool c, unsigned e) __attribute__((always_inline)) {
-            const u64 bal = __ballot(c) & (a.mode == 8 ? 0ull : ~0ull);  // 8: profiling ablation, no candidates
+            const u64 bal = __ballot(c) & (FS_ABL(8) ? 0ull : ~0ull);  // 8: profiling ablation, no candidates
             if (bal) {
                 const int rk = __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
                 if (c) queue[qn + rk] = e;
                 qn += popc64(bal);
-                if (a.mode == 9) nq += popc64(bal);
+                if (FS_ABL(9)) nq += popc64(bal);
             }
         };
         const float tv = uvalid ? tau : INFINITY;  // invalid users take nothing
@@ -1147,7 +1156,7 @@ __device__ __forceinline__ void screen_segment(const FsArgs& a, int64_t ub, int 
         }
     }
     if (uvalid && h == 0) a.ccount[bslot * a.n_lists + li] = cnt;
-    if (a.mode == 9 && lane == 0) {  // profiling: queued / kept candidate totals into out_idx[0], [1]
+    if (FS_ABL(9) && lane == 0) {  // profiling: queued / kept candidate totals into out_idx[0], [1]
         atomicAdd(reinterpret_cast<unsigned long long*>(a.out_idx), (unsigned long long)nq);
         int kept = 0;
         for (int q = 0; q < 32; ++q) kept += lcnt[q];
@@ -1440,9 +1449,9 @@ static void fs_plan(int64_t nb, int64_t ni, int d, int* nw, int* n_chunks, int64
     int64_t s = (target + waves - 1) / waves;
     if (s < 1) s = 1;
     if (s > 16) s = 16;
-    if (const char* f = getenv("RSX_FS_CHUNKS")) {  // tuning override
-        const int v = atoi(f);
-        if (v >= 1 && v <= 16) s = v;
+    {  // tuning override
+        static const int v = env_knob("RSX_FS_CHUNKS", 0, 1, 16);
+        if (v) s = v;
     }
     int64_t per = (ni + s - 1) / s;
     per = (per + 31) / 32 * 32;
@@ -1452,11 +1461,7 @@ static void fs_plan(int64_t nb, int64_t ni, int d, int* nw, int* n_chunks, int64
 }
 
 static bool fs_use_screen(int k, int d, int64_t ni) {
-    static int on = -1;
-    if (on < 0) {
-        const char* e = getenv("RSX_FS_SCREEN");  // 0: the f32-MFMA fs_tiles path
-        on = e ? atoi(e) != 0 : 1;
-    }
+    static const int on = env_knob("RSX_FS_SCREEN", 1, 0, 1);  // 0: the f32-MFMA fs_tiles path
     return on && k <= 64 && (d == 32 || d == 64 || d == 128 || d == 256) && ni < (1ll << 26);  // queue entry: item << 6
 }
 
@@ -1508,10 +1513,7 @@ static void screen_plan(int64_t nb, int64_t ni, int wps, int* n_chunks, int64_t*
 // 2 at d <= 128 (register budget), 1 at d = 256; the pass-2 launch of the two-phase form
 // holds no pass-1 samples (fewer registers): RSX_FS_WPS2 (tuning)
 static int fs_wps(int d, int phase) {
-    static const int w2 = [] {
-        const char* e = getenv("RSX_FS_WPS2");
-        return e ? atoi(e) : 0;
-    }();
+    static const int w2 = env_knob("RSX_FS_WPS2", 0, 1, 4);
     if (phase == 2 && w2 > 0) return w2;
     return d <= 128 ? 2 : 1;
 }
@@ -1527,10 +1529,7 @@ static FsLayout fs_layout(int64_t nb, int64_t ni, int k, int d, int wps) {
     const int64_t n_ub = (nb + 31) / 32;
     const int C = L.n_chunks;
     L.blocks = n_ub * C;
-    static const int seg_env = [] {
-        const char* e = getenv("RSX_FS_SEG");  // 0: no balanced split (tuning)
-        return e ? atoi(e) : 1;
-    }();
+    static const int seg_env = env_knob("RSX_FS_SEG", 1, 0, 1);  // 0: no balanced split (tuning)
     if (L.screen && seg_env && (8 % C) == 0) {
         const int64_t slots = (int64_t)fs_cus() * 4 * wps;
         const int64_t wc = slots / C;
@@ -1585,7 +1584,7 @@ static int launch_fs(FsArgs& a, const FsLayout& L, const FsLayout& L2, hipStream
         const int64_t nthr = ni_pad * (D / 4);
         hipLaunchKernelGGL((fs_prep<D>), dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, s, a.I, a.ni, ni_pad,
                            const_cast<__bf16*>(a.Ib));
-        if (a.mode == 9) (void)hipMemsetAsync(a.out_idx, 0, 2 * sizeof(int64_t), s);  // profiling counters
+        if (FS_ABL(9)) (void)hipMemsetAsync(a.out_idx, 0, 2 * sizeof(int64_t), s);  // profiling counters
         if (a.lbound) {  // two phases: every segment of a user filters by the user's L over all of them
             (void)hipMemsetAsync(a.mcnt1, 0xff, (size_t)a.nb * L.n_lists * sizeof(uint16_t), s);
             hipLaunchKernelGGL((fs_screen<D, 1>), grid, dim3(64), 0, s, a);
@@ -1598,7 +1597,7 @@ static int launch_fs(FsArgs& a, const FsLayout& L, const FsLayout& L2, hipStream
                 else if (nl <= 8) hipLaunchKernelGGL((fs_thresh<6>), tg, dim3(256), 0, s, sp, mc, nl, a.nb, a.k, a.lbound);
                 else hipLaunchKernelGGL((fs_thresh<12>), tg, dim3(256), 0, s, sp, mc, nl, a.nb, a.k, a.lbound);
             }
-            if (a.mode == 5) return last_rc();
+            if (FS_ABL(5)) return last_rc();
             a.n_chunks = L2.n_chunks;
             a.chunk_items = L2.chunk_items;
             a.n_lists = L2.n_lists;
@@ -1608,16 +1607,16 @@ static int launch_fs(FsArgs& a, const FsLayout& L, const FsLayout& L2, hipStream
         } else {
             hipLaunchKernelGGL((fs_screen<D, 0>), grid, dim3(64), 0, s, a);
         }
-    } else if (a.mode == 4) {
+    } else if (FS_ABL(4)) {
         hipLaunchKernelGGL((fs_tiles<D, 4>), grid, dim3(64), 0, s, a);
-    } else if (a.mode == 1) {
+    } else if (FS_ABL(1)) {
         hipLaunchKernelGGL((fs_tiles<D, 1>), grid, dim3(64), 0, s, a);
     } else {
         hipLaunchKernelGGL((fs_tiles<D, 0>), grid, dim3(64), 0, s, a);
     }
     const dim3 sg((unsigned)((a.nb + 3) / 4));
-    if (a.mode == 9) return last_rc();  // profiling: out_idx holds the candidate counts
-    if (a.Ib || a.mode == 0) {
+    if (FS_ABL(9)) return last_rc();  // profiling: out_idx holds the candidate counts
+    if (a.Ib || !RSX_FS_ABLATION || a.mode == 0) {
         const int n = a.n_lists;
         if (n <= 2) hipLaunchKernelGGL((fs_select<2>), sg, dim3(256), 0, s, a);
         else if (n <= 4) hipLaunchKernelGGL((fs_select<4>), sg, dim3(256), 0, s, a);
@@ -1663,10 +1662,7 @@ int fs_call(const float* U, const int64_t* users, int64_t nb, const float* I, in
         char* p = static_cast<char*>(ws) + fs_align((size_t)nb * nl * kCap * sizeof(u64) + (size_t)nb * nl * sizeof(int) + 512);
         a.Ib = reinterpret_cast<const __bf16*>(p);
         const size_t ni_pad = (size_t)(ni + 31) / 32 * 32;
-        static const int two = [] {
-            const char* e = getenv("RSX_FS_2PHASE");  // 0: both passes in one launch, per-segment thresholds
-            return e ? atoi(e) : 1;
-        }();
+        static const int two = env_knob("RSX_FS_2PHASE", 1, 0, 1);  // 0: both passes in one launch, per-segment thresholds
         char* q = p + fs_align((ni_pad + 32 * kScreenPadTiles) * (d + 16) * sizeof(__bf16));
         a.lbound = two ? reinterpret_cast<unsigned*>(q) : nullptr;
         q += fs_align((size_t)nb * sizeof(unsigned));
@@ -1675,10 +1671,11 @@ int fs_call(const float* U, const int64_t* users, int64_t nb, const float* I, in
         a.mcnt1 = reinterpret_cast<uint16_t*>(q);
     }
     {
-        static int mode = -1;
-        if (mode < 0) {
-            const char* e = getenv("RSX_FS_MODE");
-            mode = e ? atoi(e) : 0;
+        static const int mode = env_knob("RSX_FS_MODE", 0, 0, 9);
+        if (mode != 0 && !RSX_FS_ABLATION) {
+            fprintf(stderr, "librsx: RSX_FS_MODE=%d is a profiling ablation (wrong top-k by design); it runs only in "
+                            "an ablation build (tools/build_variant.py NAME -DRSX_FS_ABLATION=1)\n", mode);
+            return RSX_ERR_UNSUPPORTED;
         }
         a.mode = mode;
     }

@@ -36,11 +36,7 @@ struct WgPlan {
     int slots() const { return splits * rw; }
 };
 
-static int lin_env(const char* name, int dflt) {
-    const char* v = getenv(name);
-    const int x = v ? atoi(v) : 0;
-    return x > 0 ? x : dflt;
-}
+static int lin_env(const char* name, int dflt) { return env_knob(name, dflt, 1, 1 << 20); }
 
 // in_dim: a multiple of 4 (float4 rows); the i tiles cover ceil(in_dim / 32) * 32 columns and
 // the kernel masks the columns past in_dim (loads as zeros, no stores)

@@ -2,6 +2,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
 
 #include "rsx.h"
 
@@ -54,6 +56,21 @@ inline int device_cus() {
         (void)hipGetLastError();
     }
     return n;
+}
+
+// A tuning knob read from the environment: unset -> dflt; an integer in [lo, hi] -> that
+// value; anything else (not an integer, out of range) aborts with the knob's name.
+// Knobs only re-plan launches (grid sizes, splits, phases); none changes a result.
+inline int env_knob(const char* name, int dflt, int lo, int hi) {
+    const char* v = getenv(name);
+    if (!v || !*v) return dflt;
+    char* end = nullptr;
+    const long long x = strtoll(v, &end, 10);
+    if (*end != '\0' || x < lo || x > hi) {
+        fprintf(stderr, "librsx: %s=%s is not a valid value (an integer in [%d, %d])\n", name, v, lo, hi);
+        abort();
+    }
+    return (int)x;
 }
 
 // Batch-row tagging carried by an SpMM launch (extra blocks after the work and

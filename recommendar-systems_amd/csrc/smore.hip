@@ -578,11 +578,7 @@ extern "C" size_t rsx_smore_spectral_spec_floats(int64_t n_items, int32_t d) {
 }
 
 // K splits of a projection: about 1024 blocks over both modalities, >= 512 of K per split
-static int env_int(const char* name, int dflt) {
-    const char* v = getenv(name);
-    const int x = v ? atoi(v) : 0;
-    return x > 0 ? x : dflt;
-}
+static int env_int(const char* name, int dflt) { return env_knob(name, dflt, 1, 1 << 20); }
 
 static int proj_splits(int64_t n, int K) {
     static const int target = env_int("RSX_PROJ_TARGET", 1536), mink = env_int("RSX_PROJ_MINK", 512);

@@ -1543,10 +1543,7 @@ int rsx_smore_gates(int32_t backward, const float* const* conv, const float* ite
     // blocks: the row blocks, at most RSX_GATE_BLOCKS (default: 2 per CU -- the LDS
     // weight copy allows two; each block then strides over its row blocks)
     const unsigned gy = (backward && mul) ? 1u : 3u;
-    static const int64_t cap_env = [] {
-        const char* e = getenv("RSX_GATE_BLOCKS");
-        return e ? (int64_t)atoll(e) : (int64_t)0;
-    }();
+    static const int64_t cap_env = env_knob("RSX_GATE_BLOCKS", 0, 1, 1 << 20);
     int64_t gx = a.nbx;
     const int64_t cap = cap_env > 0 ? cap_env : (int64_t)(2 * device_cus()) / gy;
     if (cap > 0 && gx > cap) gx = cap;
@@ -1828,7 +1825,8 @@ int rsx_adam_multi_mg(int32_t count, float* const* p, const float* const* g, flo
         L.rmult = rmult;
         int64_t blocks = 0;
         int k = 0;
-        for (int32_t i = c0; i < count && k < sf::kAdamMax; ++i) {
+        // the chunk is tensors [c0, c0 + 32): empty ones are skipped, never carried into the next chunk
+        for (int32_t i = c0; i < count && i < c0 + sf::kAdamMax; ++i) {
             if (n[i] < 0 || (n[i] > 0 && (!p[i] || !g[i] || !m[i] || !v[i] || !step_dev[i]))) return RSX_ERR_ARG;
             if (n[i] > 0 && rx && !rx[i]) return RSX_ERR_ARG;
             if (n[i] == 0) continue;

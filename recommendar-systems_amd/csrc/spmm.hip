@@ -649,11 +649,7 @@ __global__ __launch_bounds__(kBlock) void rowwise_kernel(int64_t n_rows, rsx_epi
 // us), while a list that fits one round launches whole (baby: 111 us/step whole,
 // 115 capped at 1,536; tools/gpu/maxb_sweep.sh, ab_legs.sh).  RSX_SPMM_MAXB
 // overrides (tuning), RSX_SPMM_MAXB_ADAM for the Adam-epilogue kind alone.
-static int64_t env_blocks(const char* name) {
-    const char* f = getenv(name);
-    const long long x = f ? atoll(f) : 0;
-    return (int64_t)(x > 0 ? x : 0);
-}
+static int64_t env_blocks(const char* name) { return env_knob(name, 0, 1, 1 << 20); }
 static int64_t spmm_max_blocks(int kind, int d, int64_t n) {
     static const int64_t all = env_blocks("RSX_SPMM_MAXB");
     static const int64_t adam = env_blocks("RSX_SPMM_MAXB_ADAM");

@@ -73,9 +73,11 @@ __device__ __forceinline__ bool in_sorted(const int32_t* a, int64_t lo, int64_t 
 
 // Triplet for epoch position pos = start + t.  Output layout: batch-major, batch
 // j = t / bm holding [3][Bj] contiguous at out + 3*bm*j (Bj = min(bm, count - j*bm));
-// with bm >= count this is the plain [3][count] layout.
+// with bm >= count this is the plain [3][count] layout.  With n_slices > 0 the batches
+// are the n_slices balanced slices [floor(j count / S), floor((j+1) count / S)) instead
+// (sizes differ by at most one), slice j stored [3][Bj] at out + 3*floor(j count / S).
 __global__ __launch_bounds__(256) void sample_kernel(rsx_sampler_args s, int hb, int64_t count, int64_t bm,
-                                                     int64_t* out) {
+                                                     int64_t* out, int64_t n_slices) {
     const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (t >= count) return;
     const uint64_t key = mix64(s.seed ^ mix64((uint64_t)s.epoch + 0x1234567ull));
@@ -91,15 +93,27 @@ __global__ __launch_bounds__(256) void sample_kernel(rsx_sampler_args s, int hb,
         n = s.all_items[st % (uint64_t)s.n_all_items];
         if (!in_sorted(s.hist_col, lo, hi, n)) break;
     }
-    const int64_t jb = t / bm, b = t - jb * bm;
-    const int64_t bj = (count - jb * bm) < bm ? (count - jb * bm) : bm;
-    int64_t* o = out + 3 * bm * jb;
+    int64_t b, bj;
+    int64_t* o;
+    if (n_slices > 0) {
+        const int64_t j = ((t + 1) * n_slices - 1) / count;  // the slice holding t
+        const int64_t a = j * count / n_slices, e_ = (j + 1) * count / n_slices;
+        b = t - a;
+        bj = e_ - a;
+        o = out + 3 * a;
+    } else {
+        const int64_t jb = t / bm;
+        b = t - jb * bm;
+        bj = (count - jb * bm) < bm ? (count - jb * bm) : bm;
+        o = out + 3 * bm * jb;
+    }
     o[b] = u;
     o[bj + b] = p;
     o[2 * bj + b] = n;
 }
 
-int sample_call(const rsx_sampler_args& s, int64_t batch, int64_t* out, hipStream_t st, int64_t bm = 0) {
+int sample_call(const rsx_sampler_args& s, int64_t batch, int64_t* out, hipStream_t st, int64_t bm = 0,
+                int64_t n_slices = 0) {
     if (!s.inter_u || !s.inter_i || !s.hist_rowptr || !s.all_items || s.n_inter <= 0 || s.n_all_items <= 0 ||
         !out || batch <= 0 || s.start < 0 || s.start >= s.n_inter)
         return RSX_ERR_ARG;
@@ -109,7 +123,7 @@ int sample_call(const rsx_sampler_args& s, int64_t batch, int64_t* out, hipStrea
     while ((1ll << bits) < s.n_inter) ++bits;
     if (bits & 1) ++bits;
     hipLaunchKernelGGL(sample_kernel, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, st, s, bits / 2, count,
-                       bm, out);
+                       bm, out, n_slices);
     return last_rc();
 }
 
@@ -311,6 +325,25 @@ int rsx_sample_epoch(const int32_t* inter_u, const int32_t* inter_i, int64_t n_i
     s.start = 0;
     if (batch <= 0) return RSX_ERR_ARG;
     return rsx::sample_call(s, n_inter, out, rsx::as_stream(stream), batch);
+}
+
+int rsx_sample_epoch_slices(const int32_t* inter_u, const int32_t* inter_i, int64_t n_inter,
+                            const int64_t* hist_rowptr, const int32_t* hist_col, const int32_t* all_items,
+                            int64_t n_all_items, uint64_t seed, int64_t epoch, int64_t n_slices, int64_t* out,
+                            rsx_stream_t stream) {
+    rsx_sampler_args s;
+    s.inter_u = inter_u;
+    s.inter_i = inter_i;
+    s.n_inter = n_inter;
+    s.hist_rowptr = hist_rowptr;
+    s.hist_col = hist_col;
+    s.all_items = all_items;
+    s.n_all_items = n_all_items;
+    s.seed = seed;
+    s.epoch = epoch;
+    s.start = 0;
+    if (n_slices <= 0 || n_slices > n_inter) return RSX_ERR_ARG;  // every slice holds >= 1 triplet
+    return rsx::sample_call(s, n_inter, out, rsx::as_stream(stream), n_inter, n_slices);
 }
 
 int rsx_layergcn_step(const rsx_layergcn_step_args* st, rsx_stream_t stream) {

@@ -94,6 +94,15 @@ class ShardedStep(C.Structure):
                 ("xch", P)]
 
 
+class DpStep(C.Structure):
+    _fields_ = [("adj", C.POINTER(Csr)), ("n_users", I64), ("n_items", I64), ("d", I32), ("n_layers", I32),
+                ("reg", F32), ("pad0", I32), ("p", P), ("m", P), ("v", P), ("s", P), ("h0", P), ("h1", P),
+                ("final_emb", P), ("g", P), ("slab", P), ("triplets", P), ("batch", I64), ("adam", Adam),
+                ("loss_out", P), ("loss_acc", P), ("ws", P), ("ws_bytes", C.c_size_t), ("comm", P),
+                ("row_tag", P), ("own_tag", P), ("tag_dev", P), ("reg_cnt", P), ("halt", P), ("cap", I64),
+                ("slots", P), ("blocks", P), ("pos", P)]
+
+
 RSX_COLL_ALLREDUCE, RSX_COLL_ALLGATHER, RSX_COLL_REDUCESCATTER = 0, 1, 2
 RSX_COLL_F32, RSX_COLL_I64 = 0, 1
 HOST_COLLECTIVE_FN = C.CFUNCTYPE(C.c_int, I32, P, I64, I32, P)
@@ -119,7 +128,10 @@ def _declare(lib):
         "rsx_sample_triplets": (C.c_int, [P, P, I64, P, P, P, I64, C.c_uint64, I64, I64, I64, P, P]),
         "rsx_gather_rows": (C.c_int, [P, P, I64, I64, I32, P, P]),
         "rsx_sample_epoch": (C.c_int, [P, P, I64, P, P, P, I64, C.c_uint64, I64, I64, P, P]),
+        "rsx_sample_epoch_slices": (C.c_int, [P, P, I64, P, P, P, I64, C.c_uint64, I64, I64, P, P]),
         "rsx_lightgcn_step": (C.c_int, [C.POINTER(LgcnStep), P]),
+        "rsx_dp_lightgcn_step": (C.c_int, [C.POINTER(DpStep), P]),
+        "rsx_dp_block_floats": (C.c_size_t, [I64, I32]),
         "rsx_layergcn_step": (C.c_int, [C.POINTER(LayerGcnStep), P]),
         "rsx_lightgcn_forward": (C.c_int, [C.POINTER(Csr), I32, I32, P, P, P, P, P, P, P]),
         "rsx_smore_spectral_spec_floats": (C.c_size_t, [I64, I32]),
@@ -181,6 +193,7 @@ def _declare(lib):
 EXPORTED = ["rsx_version", "rsx_csr_schedule_host", "rsx_csr_schedule_rebind", "rsx_spmm_batch", "rsx_spmm", "rsx_rowwise", "rsx_bpr_ws_bytes", "rsx_bpr",
             "rsx_fullsort_ws_bytes", "rsx_fullsort_plan", "rsx_fullsort_topk", "rsx_score_dense", "rsx_sample_triplets",
             "rsx_gather_rows", "rsx_lightgcn_step", "rsx_layergcn_step", "rsx_lightgcn_forward", "rsx_sample_epoch",
+            "rsx_sample_epoch_slices",
             "rsx_smore_spectral_spec_floats", "rsx_smore_spectral_fwd_ws_bytes", "rsx_smore_spectral_fwd",
             "rsx_smore_spectral_bwd",
             "rsx_smore_spectral_bwd_partials",
@@ -188,6 +201,7 @@ EXPORTED = ["rsx_version", "rsx_csr_schedule_host", "rsx_csr_schedule_rebind", "
             "rsx_comm_unique_id_bytes", "rsx_comm_get_unique_id", "rsx_comm_init", "rsx_comm_destroy",
             "rsx_comm_init_host",
             "rsx_comm_allreduce_f32", "rsx_sharded_lightgcn_step", "rsx_sharded_lightgcn_forward",
+            "rsx_dp_lightgcn_step", "rsx_dp_block_floats",
             "rsx_smore_gates", "rsx_smore_pref", "rsx_smore_pref_rows", "rsx_smore_wgrad_ws_bytes", "rsx_smore_wgrad",
             "rsx_smore_infonce_ws_bytes", "rsx_smore_infonce_fwd", "rsx_smore_infonce_bwd", "rsx_smore_infonce_fwd_total", "rsx_smore_infonce_bwd_scaled", "rsx_adam_multi", "rsx_adam_multi_scaled", "rsx_adam_multi_mg",
             "rsx_smore_unit_weights", "rsx_smore_unit_weights_bwd", "rsx_mg_alpha_ws_bytes", "rsx_mg_alpha",

@@ -19,7 +19,7 @@ CSRC = os.path.join(ROOT, "csrc")
 INCLUDE = os.path.join(REPO, "include")
 LIBDIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIBDIR, "librsx.so")
-SOURCES = ["spmm.hip", "bpr.hip", "fullsort.hip", "step.hip", "smore.hip", "metrics.hip", "linear.hip", "dist.hip", "smore_fuse.hip", "knn.hip", "graph.hip"]
+SOURCES = ["spmm.hip", "bpr.hip", "fullsort.hip", "step.hip", "smore.hip", "metrics.hip", "linear.hip", "dist.hip", "dp.hip", "smore_fuse.hip", "knn.hip", "graph.hip"]
 ARCH = os.environ.get("RSX_OFFLOAD_ARCH", "gfx950")
 
 

@@ -284,30 +284,31 @@ class ShardedLightGCNEngine:
         # triplet copy + one graph launch instead of ~20 launches and 7 collectives)
         self._step_dev = torch.zeros(1, dtype=torch.int64, device=self.be.device)
         st.tag_dev = self._step_dev.data_ptr()
-        self._trip_buf = torch.zeros(3, self.batch, dtype=torch.int64, device=self.be.device)
-        self._graph = None
-        self._graph_lr = None
-        self._graph_warm = False
+        # one captured graph per batch size (balanced epoch slices come in two sizes)
+        self._graphs = {}  # B -> (graph, lr, triplet buffer)
+        self._graph_warm = set()
         self.use_graph = (dist.get_backend(self.group) == "nccl" and self.row_tag is not None
                           and os.environ.get("RSX_SHARDED_GRAPH", "1") != "0")
 
     def _native_step(self, trip):
-        """One batch through csrc/dist.hip.  Full batches over RCCL: the first runs
-        eagerly (RCCL sets up its connections on first use), the second is captured
-        into a HIP graph, every later one replays it after copying its triplets into
-        the captured buffer.  Partial batches, a changed lr and host-hook
+        """One batch through csrc/dist.hip.  Over RCCL, per batch size: the first batch runs
+        eagerly (RCCL sets up its connections on first use, workspaces settle), the second
+        is captured into a HIP graph, every later one replays it after copying its
+        triplets into the captured buffer.  A changed lr re-captures; host-hook
         communicators run eagerly."""
         lib, st = L.lib(), self._st
         B = int(trip.shape[1])
         st.adam = ops.adam_struct(self.lr, self.step_count, weight_decay=self.wd, step_dev=self._step_dev)
-        graph = self.use_graph and B == self.batch
-        if graph and self._graph is not None and self._graph_lr == self.lr:
-            self._trip_buf.copy_(trip)
-            self._graph.replay()
+        graph = self.use_graph and B <= self.union_cap
+        cap = self._graphs.get(B) if graph else None
+        if cap is not None and cap[1] == self.lr:
+            cap[2].copy_(trip)
+            cap[0].replay()
             return
-        if graph and self._graph_warm:
-            self._trip_buf.copy_(trip)
-            st.triplets, st.batch = self._trip_buf.data_ptr(), B
+        if graph and B in self._graph_warm:
+            buf = cap[2] if cap is not None else torch.zeros(3, B, dtype=torch.int64, device=self.be.device)
+            buf.copy_(trip)
+            st.triplets, st.batch = buf.data_ptr(), B
             g = torch.cuda.CUDAGraph()
             gc_on = gc.isenabled()
             gc.disable()  # no finalizers inside the capture (see rsx/trainer.py:_capture)
@@ -319,24 +320,23 @@ class ShardedLightGCNEngine:
                 self.use_graph = False
                 torch.cuda.synchronize()
             else:
-                self._graph, self._graph_lr = g, self.lr
+                self._graphs[B] = (g, self.lr, buf)
+                g.replay()
+                return
             finally:
                 if gc_on:
                     gc.enable()
-            if self._graph is g:
-                g.replay()
-                return
         t = trip.contiguous()
         self._keep = t
         nb = lib.rsx_bpr_ws_bytes(B)
         grow_union = self.sparse and B > self.union_cap
         if nb > self.ws.numel() or grow_union:  # a given batch larger than the engine's
-            # a captured graph holds the old workspace pointers: drop it (and re-warm)
+            # captured graphs hold the old workspace pointers: drop them (and re-warm)
             # before that memory returns to the caching allocator
-            if self._graph is not None:
+            if self._graphs:
                 torch.cuda.synchronize(self.be.device)
-                self._graph = None
-            self._graph_warm = False
+                self._graphs.clear()
+            self._graph_warm.clear()
             if nb > self.ws.numel():
                 self.ws = torch.empty(nb, dtype=torch.uint8, device=self.be.device)
                 st.ws, st.ws_bytes = self.ws.data_ptr(), self.ws.numel()
@@ -346,7 +346,7 @@ class ShardedLightGCNEngine:
         self._step_dev.add_(1)
         L.check(lib.rsx_sharded_lightgcn_step(C.byref(st), ops._stream()), "rsx_sharded_lightgcn_step")
         if graph:
-            self._graph_warm = True
+            self._graph_warm.add(B)
 
     def _grow_union(self, B):
         """Union-exchange buffers for batches of up to B pairs per rank."""
@@ -367,7 +367,7 @@ class ShardedLightGCNEngine:
     def close(self):
         """Release the rsx communicator (before destroy_process_group)."""
         if self._comm is not None:
-            self._graph = None  # the captured collectives belong to the communicator
+            self._graphs = {}  # the captured collectives belong to the communicator
             torch.cuda.synchronize(self.be.device)
             L.lib().rsx_comm_destroy(self._comm)
             self._comm = None
@@ -505,6 +505,15 @@ class ShardedLightGCNEngine:
         self._fwd_valid = False
 
     # ------------------------------------------------------------------ step
+    def step_slice(self, epoch: int, j: int, n_slices: int):
+        """Batch j of `epoch` cut into n_slices balanced slices of this rank's interactions
+        (rsx_sample_epoch_slices): every rank runs the same n_slices steps per epoch and
+        visits each of its interactions exactly once; a slice holds >= 1 triplet."""
+        if self._epoch_sampled != (epoch, n_slices):
+            self._epoch_buf = self.sampler.sample_epoch_slices(epoch, n_slices, out=self._epoch_buf)
+            self._epoch_sampled = (epoch, n_slices)
+        self.step(triplets=ops.DeviceSampler.slice_view(self._epoch_buf, self.n_inter, n_slices, j))
+
     def step(self, triplets=None, epoch: int = 0, start: int = 0):
         be, nu, ni, d, K = self.be, self.n_users, self.n_items, self.d, self.K
         self.step_count += 1

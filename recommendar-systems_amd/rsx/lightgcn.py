@@ -24,9 +24,10 @@ tables are the reference's (every rank draws the full xavier tables from the
 same seed and keeps its users), the parameters are the local user block and the
 item replica.  Training is data-parallel over the user shards: every rank samples
 its own users' interactions on the device (`fused_step_index`); every rank runs
-the same number of steps per epoch, ceil(E / (W B)), with a batch sized so that
-it visits each of its interactions exactly once (B_r = ceil(E_r / steps) ~ B), and
-the step minimises the sum of the ranks' reference losses.
+the same number of steps per epoch, ceil(E / (W B)), over its epoch cut into that
+many balanced slices (sizes ceil / floor of E_r / steps ~ B), so it visits each of
+its interactions exactly once, and the step minimises the sum of the ranks'
+reference losses.
 Evaluation ranks each rank's own evaluation users against all items
 (`full_sort_topk_local`); rsx.trainer all-gathers the metric sums.
 """
@@ -143,27 +144,29 @@ class LightGCN(GeneralRecommender):
         sel = (rows >= a) & (rows < b)
         B = int(config["train_batch_size"])
         # every rank visits each of its interactions once per epoch in the same number of
-        # steps: steps = ceil(E / (W B)) over the global count E, and rank r's batch is
-        # B_r = ceil(E_r / steps) (~B; its last batch is the partial one).  Contiguous user
-        # ranges hold unequal interaction counts, so a fixed B per rank would make the small
-        # shards wrap around and re-train their batches within the epoch.
+        # steps: steps = ceil(E / (W B)) over the global count E, and rank r's epoch is cut
+        # into `steps` balanced slices of its E_r interactions (sizes ceil / floor of
+        # E_r / steps, ~B; rsx_sample_epoch_slices).  A rank with fewer interactions than
+        # steps would have empty slices: refused on every rank alike (no rank may leave
+        # the collectives early).
         e_r = int(sel.sum())
-        if e_r == 0:
-            raise RuntimeError(f"rank {rank}: no training interactions in users [{a}, {b})")
-        cnt = torch.tensor([e_r], dtype=torch.int64)
-        if dist.get_backend() == "nccl":
-            cnt = cnt.to(self.device)
-        dist.all_reduce(cnt)
-        steps = -(-int(cnt.item()) // (world * B))
+        dev = self.device if dist.get_backend() == "nccl" else torch.device("cpu")
+        stats = torch.tensor([e_r, -e_r], dtype=torch.int64, device=dev)
+        tot = stats[:1].clone()
+        dist.all_reduce(tot)
+        steps = max(1, -(-int(tot.item()) // (world * B)))
+        dist.all_reduce(stats, op=dist.ReduceOp.MAX)  # [max E_r, -min E_r]
+        if -int(stats[1].item()) < steps:
+            raise RuntimeError(f"sharded LightGCN: a rank holds {-int(stats[1].item())} training interactions, fewer "
+                               f"than the {steps} steps per epoch (world {world}, batch {B}); use fewer ranks")
         b_r = -(-e_r // steps)
-        cap = torch.tensor([b_r], dtype=torch.int64, device=cnt.device)
-        dist.all_reduce(cap, op=dist.ReduceOp.MAX)
+        cap = -(-int(stats[0].item()) // steps)  # the largest slice of any rank
         self.engine = ShardedLightGCNEngine(rows[sel] - a, cols[sel], b - a, self.n_items, self.latent_dim,
                                             self.n_layers, self.reg_weight, lr=config["learning_rate"] or 1e-3,
                                             device=self.device, user_emb=u0.numpy()[a:b], item_emb=i0.numpy(),
                                             seed=int(config["seed"] or 0) + rank, batch=b_r,
                                             chunk=int(config["rsx_chunk"] or 32), weight_decay=wd,
-                                            union_cap=int(cap.item()))
+                                            union_cap=cap)
         self.steps_per_epoch = steps
         nl = b - a
         self.embedding_dict = nn.ParameterDict({
@@ -213,7 +216,7 @@ class LightGCN(GeneralRecommender):
         """Sharded training: this rank's batch i (of steps_per_epoch, the same count on every
         rank) of `epoch` from its device sampler."""
         self.engine.lr = float(lr)
-        self.engine.step(epoch=epoch, start=i * self.engine.batch)
+        self.engine.step_slice(epoch, i, self.steps_per_epoch)
 
     def full_sort_topk_local(self, eval_users: torch.Tensor, k: int, eval_data):
         """(row positions in eval_users, top-k item ids) for this rank's evaluation users

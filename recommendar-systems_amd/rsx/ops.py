@@ -448,6 +448,28 @@ class DeviceSampler:
         b = min(batch, n_inter - j * batch)
         return epoch_buf[3 * batch * j: 3 * batch * j + 3 * b].view(3, b)
 
+    def sample_epoch_slices(self, epoch: int, n_slices: int, out: torch.Tensor | None = None) -> torch.Tensor:
+        """The epoch cut into n_slices balanced slices (rsx_sample_epoch_slices): slice j =
+        positions [j E // S, (j+1) E // S), read with `slice_view`."""
+        if not 1 <= n_slices <= self.n_inter:
+            raise ValueError(f"{n_slices} slices of an epoch of {self.n_inter} interactions")
+        if out is None:
+            out = torch.empty(3 * self.n_inter, dtype=torch.int64, device=self.device)
+        L.check(L.lib().rsx_sample_epoch_slices(self.inter_u.data_ptr(), self.inter_i.data_ptr(), self.n_inter,
+                                                self.hist_rowptr.data_ptr(), self.hist_col.data_ptr(),
+                                                self.all_items.data_ptr(), self.all_items.numel(), self.seed, epoch,
+                                                n_slices, _pi(out), _stream()), "rsx_sample_epoch_slices")
+        return out
+
+    @staticmethod
+    def slice_bounds(n_inter: int, n_slices: int, j: int):
+        return j * n_inter // n_slices, (j + 1) * n_inter // n_slices
+
+    @staticmethod
+    def slice_view(epoch_buf: torch.Tensor, n_inter: int, n_slices: int, j: int) -> torch.Tensor:
+        a, e = DeviceSampler.slice_bounds(n_inter, n_slices, j)
+        return epoch_buf[3 * a: 3 * e].view(3, e - a)
+
     def sample(self, epoch: int, start: int, batch: int, out: torch.Tensor | None = None) -> torch.Tensor:
         count = min(batch, self.n_inter - start)
         if out is None:

@@ -420,13 +420,25 @@ class SMORE(GeneralRecommender):
         rows, cols = im.row.astype(np.int64), im.col.astype(np.int64)
         sel = (rows >= a) & (rows < b)
         e_r = int(sel.sum())
-        if e_r == 0:
-            raise RuntimeError(f"rank {rank}: no training interactions in users [{a}, {b})")
         B = int(config["train_batch_size"])
-        cnt = torch.tensor([float(e_r), 0.0], dtype=torch.float32, device=self.device)
-        self.comm.allreduce_(cnt)
-        steps = -(-int(round(cnt[0].item())) // (world * B))
-        self.local_batch = -(-e_r // steps)
+        # the global count in int64 (an f32 sum is exact only to 2^24 interactions); every
+        # rank's epoch is cut into `steps` balanced slices of its E_r interactions, so a
+        # rank with fewer interactions than steps is refused on every rank alike
+        import torch.distributed as dist
+
+        group = dist.is_available() and dist.is_initialized()
+        cdev = self.device if group and dist.get_backend() == "nccl" else torch.device("cpu")
+        stats = torch.tensor([e_r, -e_r], dtype=torch.int64, device=cdev)
+        tot = stats[:1].clone()
+        if group:
+            dist.all_reduce(tot)
+        steps = max(1, -(-int(tot.item()) // (world * B)))
+        if group:
+            dist.all_reduce(stats, op=dist.ReduceOp.MAX)  # [max E_r, -min E_r]
+        if -int(stats[1].item()) < steps:
+            raise RuntimeError(f"sharded SMORE: a rank holds {-int(stats[1].item())} training interactions, fewer than "
+                               f"the {steps} steps per epoch (world {world}, batch {B}); use fewer ranks")
+        self.local_batch = -(-e_r // steps)  # this rank's largest slice
         self.steps_per_epoch = steps
         self._sampler = ops.DeviceSampler(rows[sel] - a, cols[sel], b - a, self.device,
                                           seed=int(config["seed"] or 0) + rank)
@@ -444,13 +456,15 @@ class SMORE(GeneralRecommender):
         return st
 
     def local_batches(self, epoch: int):
-        """This rank's training batches of `epoch` (device-sampled [3, B_r] triplets: users
-        as local row ids, items global): steps_per_epoch of them on every rank."""
+        """This rank's training batches of `epoch` (device-sampled [3, B_j] triplets: users
+        as local row ids, items global): steps_per_epoch balanced slices of its epoch on
+        every rank (sizes differ by at most one), each interaction visited once."""
+        S = self.steps_per_epoch
         if self._epoch_of_buf != epoch:
-            self._epoch_buf = self._sampler.sample_epoch(epoch, self.local_batch, out=self._epoch_buf)
+            self._epoch_buf = self._sampler.sample_epoch_slices(epoch, S, out=self._epoch_buf)
             self._epoch_of_buf = epoch
-        for j in range(self.steps_per_epoch):
-            yield ops.DeviceSampler.batch_view(self._epoch_buf, self._sampler.n_inter, self.local_batch, j)
+        for j in range(S):
+            yield ops.DeviceSampler.slice_view(self._epoch_buf, self._sampler.n_inter, S, j)
 
     def gate_loss(self, loss):
         """The NaN gate's input on a sharded model: the loss summed over the ranks, so a NaN

@@ -81,12 +81,12 @@ class _GraphStep:
     The control flow of a batch depends on the host counter `model.global_step`
     (mirror gradient when the step after the first calculate_loss is a multiple of
     mg_interval; diagnostics every mg_log_interval steps).  Each branch is its own
-    graph ("kind"), the host counter is advanced by what the capture advanced it
-    by, and batches that log diagnostics run eagerly.  A kind is captured only
-    after one eager batch of that kind at full size, so lazily allocated
+    graph ("kind", per batch shape), the host counter is advanced by what the
+    capture advanced it by, and batches that log diagnostics run eagerly.  A kind is
+    captured only after one eager batch of that kind and shape, so lazily allocated
     workspaces exist outside the graph's memory pool.  The learning rate is read
     on the device (Trainer._sync_lr), so the LambdaLR schedule keeps the graphs
-    (without a device lr, a change of lr drops them).  Partial batches run eagerly.
+    (without a device lr, a change of lr drops them).
 
     Contract for a model to opt in (`supports_graph_step = True`): calculate_loss
     increments `global_step` by one (if it has one), and no host syncs or
@@ -95,7 +95,6 @@ class _GraphStep:
     def __init__(self, trainer, loss_func):
         self.t = trainer
         self.loss_func = loss_func
-        self.shape = None
         self.seen = set()
         self.graphs = {}
         self.lr = None
@@ -116,13 +115,12 @@ class _GraphStep:
         """The batch through a graph: (losses, loss), or None to run it eagerly."""
         if not (torch.is_tensor(inter) and inter.is_cuda):
             return None
-        if self.shape is None:
-            self.shape = tuple(inter.shape)
-        if tuple(inter.shape) != self.shape:
-            return None
         kind = self._kind()
         if kind is None:
             return None
+        # one graph per (batch shape, kind): a sharded epoch's balanced slices come in two
+        # sizes; the loader's last partial batch is a third
+        kind = (tuple(inter.shape), kind)
         opt = self.t.optimizer
         lr = tuple(g["lr"] for g in opt.param_groups)
         if lr != self.lr and not getattr(opt, "lr_on_device", lambda: False)():
@@ -331,7 +329,10 @@ class Trainer:
             losses, loss = self.train_step(interaction, batch_idx, loss_func)
             parts.append(torch.stack(list(losses)) if isinstance(losses, tuple) else loss)
             loss_batches.append(loss)
-            if not gate and self._check_nan(loss_batches[-1]):
+            # sharded: the host check reads the loss summed over the ranks, so a NaN on any
+            # rank stops every rank at the same batch (none is left waiting in a collective)
+            chk = self.model.gate_loss(loss).clone() if (sharded and not gate) else loss
+            if not gate and self._check_nan(chk):
                 self.logger.info(f"Loss is nan at epoch: {epoch_idx}, batch index: {batch_idx}. Exiting.")
                 return loss_batches[-1], torch.tensor(0.0)
         if gate:
@@ -489,12 +490,13 @@ class Trainer:
                 # .grad to None (it never zeroes them in place), so they stay g(theta)
                 grads.append(p.grad.detach() if fused else p.grad.detach().clone())
         base = float(getattr(m, "mg_alpha", 0.5))
+        sharded_m = bool(getattr(m, "sharded", False)) and hasattr(m, "mg_alpha_global")
         with torch.no_grad():
             if fused and params:
                 from .smore_fuse import axpy_multi, mg_alpha
 
                 lr_dev = getattr(self, "_lr_dev", None)  # graph-step runs: lr read on the device
-                if getattr(m, "sharded", False) and hasattr(m, "mg_alpha_global"):  # over the global vector
+                if sharded_m:  # over the global vector
                     alpha = m.mg_alpha_global(params, grads, base, lr, self.mg_target_rel_step,
                                               self.mg_alpha_max_scale, lr_dev)
                 else:
@@ -504,7 +506,11 @@ class Trainer:
                 halt = self._halt if getattr(self, "_gate", False) else None
                 axpy_multi(params, grads, alpha, -1.0 if lr_dev is not None else -lr, lr_dev, halt)  # theta - alpha lr g
             else:
-                alpha = _mg_alpha(params, grads, base, lr, self.mg_target_rel_step, self.mg_alpha_max_scale)
+                if sharded_m:  # every rank the same alpha (the replicated parameters stay equal)
+                    alpha = m.mg_alpha_global(params, grads, base, lr, self.mg_target_rel_step,
+                                              self.mg_alpha_max_scale)
+                else:
+                    alpha = _mg_alpha(params, grads, base, lr, self.mg_target_rel_step, self.mg_alpha_max_scale)
                 m._alpha_eff = alpha
                 if params:
                     down = (alpha * -lr).float()  # -alpha * lr, rounded to f32 as the scalar of a f32 op

@@ -36,6 +36,21 @@ class CpuCSR:
 class CpuSampler:
     def __init__(self, tu, ti):
         self.n_inter = tu.size
+        self.tu, self.ti = np.asarray(tu), np.asarray(ti)
+
+    def sample_epoch_slices(self, epoch, n_slices, out=None):
+        """The layout of rsx_sample_epoch_slices over a seeded permutation (negatives: the
+        position's item + 1, unchecked: only the visiting order is under test here)."""
+        from rsx.ops import DeviceSampler
+
+        E = self.n_inter
+        perm = np.random.default_rng(epoch).permutation(E)
+        out = torch.empty(3 * E, dtype=torch.int64)
+        for j in range(n_slices):
+            a, e = DeviceSampler.slice_bounds(E, n_slices, j)
+            sel = perm[a:e]
+            out[3 * a:3 * e] = torch.from_numpy(np.concatenate([self.tu[sel], self.ti[sel], (self.ti[sel] + 1) % NI]))
+        return out
 
 
 class CpuBackend:
@@ -203,3 +218,127 @@ def test_sharded_step_matches_global_objective(world, sparse, k):
     for r in range(1, world):
         assert np.array_equal(res[0]["p"][NU:], res[r]["p"][NU:])
     assert abs(sum(float(x["loss"][0]) for x in res) - loss.item()) < 1e-5
+
+
+def _slices_worker(rank, world, port, out_dir):
+    """Unequal shards with more steps per epoch than the small shard's batch (the case a
+    fixed per-rank batch walked past the shard's end): every rank runs the common step
+    count over balanced slices of its own interactions and visits each exactly once."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from rsx.dist import ShardedLightGCNEngine
+
+    e_r = [11, 5, 7][rank]
+    tu = np.arange(e_r) % 4
+    ti = (np.arange(e_r) * 3) % NI
+    key = np.unique(tu * 1000 + ti)
+    tu, ti = key // 1000, key % 1000
+    torch.manual_seed(7)
+    I0 = torch.nn.init.xavier_uniform_(torch.empty(NI, D)).numpy()
+    U0 = torch.nn.init.xavier_uniform_(torch.empty(4, D)).numpy()
+    B = 2
+    tot = torch.tensor([tu.size])
+    dist.all_reduce(tot)
+    steps = -(-int(tot.item()) // (world * B))
+    eng = ShardedLightGCNEngine(tu, ti, 4, NI, D, 2, REG, LR, "cpu", U0, I0, backend=CpuBackend(),
+                                batch=-(-tu.size // steps))
+    seen = []
+    real_step = eng.step
+
+    def spy(triplets=None, **kw):
+        seen.append(triplets.clone())
+        return real_step(triplets=triplets, **kw)
+
+    eng.step = spy
+    for j in range(steps):
+        eng.step_slice(0, j, steps)
+    np.savez(os.path.join(out_dir, f"r{rank}.npz"), steps=steps, n=tu.size,
+             users=torch.cat([t[0] for t in seen]).numpy(), items=torch.cat([t[1] for t in seen]).numpy(),
+             sizes=np.array([t.shape[1] for t in seen]), tu=tu, ti=ti)
+    dist.destroy_process_group()
+
+
+def test_balanced_slices_visit_every_interaction_once():
+    world = 3
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_slices_worker, args=(world, _free_port(), d), nprocs=world, join=True)
+        res = [dict(np.load(os.path.join(d, f"r{r}.npz"))) for r in range(world)]
+    steps = int(res[0]["steps"])
+    for r in res:
+        assert len(r["sizes"]) == steps  # the common step count on every rank
+        assert r["sizes"].min() >= 1 and r["sizes"].max() - r["sizes"].min() <= 1
+        got = sorted(zip(r["users"].tolist(), r["items"].tolist()))
+        assert got == sorted(zip(r["tu"].tolist(), r["ti"].tolist()))  # each interaction exactly once
+    assert any(int(r["n"]) < 2 * steps for r in res)  # a shard whose fixed-B walk would overrun
+
+
+@pytest.mark.parametrize("E,S", [(5, 4), (3022, 7), (10, 10), (1, 1), (299_999, 147)])
+def test_slice_bounds_partition(E, S):
+    from rsx.ops import DeviceSampler
+
+    b = [DeviceSampler.slice_bounds(E, S, j) for j in range(S)]
+    assert b[0][0] == 0 and b[-1][1] == E
+    assert all(b[j][1] == b[j + 1][0] for j in range(S - 1))
+    sizes = [e - a for a, e in b]
+    assert min(sizes) >= 1 and max(sizes) - min(sizes) <= 1
+    # the kernel's slice-of-position formula (csrc/step.hip sample_kernel)
+    for t in list(range(min(E, 50))) + list(range(max(0, E - 50), E)):
+        j = ((t + 1) * S - 1) // E
+        assert b[j][0] <= t < b[j][1]
+
+
+def _dp_worker(rank, world, port, out_dir, k):
+    """rsx.dp's data-parallel step (its CPU restatement) on `world` gloo ranks: the
+    graph and tables replicated, rank r's own triplets, one global batch per step."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from rsx.dp import DataParallelLightGCNEngine
+
+    tu, ti, _ = _local_graph(0)  # one graph for every rank
+    torch.manual_seed(7)
+    U0 = torch.nn.init.xavier_uniform_(torch.empty(NU, D)).numpy()
+    I0 = torch.nn.init.xavier_uniform_(torch.empty(NI, D)).numpy()
+    if rank:  # replicas start from rank 0's tables whatever the others hold
+        U0, I0 = U0 * 0 + 1, I0 * 0 - 1
+    eng = DataParallelLightGCNEngine(tu, ti, NU, NI, D, k, REG, LR, "cpu", U0, I0, batch=32, backend="torch")
+    losses = []
+    for s in range(2):
+        _, _, trip = _local_graph(10 * s + rank)  # rank-specific triplets (users < NU, items < NI)
+        eng.step(torch.from_numpy(trip[:, : 20 - rank]))  # unequal rank batches
+        losses.append(float(eng.loss_out[0]))
+    np.savez(os.path.join(out_dir, f"r{rank}.npz"), p=eng.p.numpy(), losses=np.array(losses))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,k", [(2, 3), (4, 3), (2, 2), (3, 4)])
+def test_data_parallel_step_matches_global_batch(world, k):
+    """Two data-parallel steps = two reference steps (loss + torch.optim.Adam) on the
+    global batch (every rank's triplets concatenated, rank order) of the one graph;
+    the replicas stay bit-identical."""
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_dp_worker, args=(world, _free_port(), d, k), nprocs=world, join=True)
+        res = [dict(np.load(os.path.join(d, f"r{r}.npz"))) for r in range(world)]
+    tu, ti, _ = _local_graph(0)
+    A = O.lightgcn_norm_adj_vec(tu, ti, NU, NI)
+    torch.manual_seed(7)
+    u = torch.nn.Parameter(torch.nn.init.xavier_uniform_(torch.empty(NU, D)))
+    i = torch.nn.Parameter(torch.nn.init.xavier_uniform_(torch.empty(NI, D)))
+    opt = torch.optim.Adam([u, i], lr=LR)
+    ref_losses = []
+    for s in range(2):
+        trip = torch.from_numpy(np.concatenate([_local_graph(10 * s + r)[2][:, : 20 - r] for r in range(world)], 1))
+        opt.zero_grad()
+        loss = O.lightgcn_loss(u, i, A, k, trip, REG)
+        loss.backward()
+        opt.step()
+        ref_losses.append(loss.item())
+    for r in range(world):
+        np.testing.assert_allclose(res[r]["losses"], ref_losses, rtol=1e-5)
+        p = res[r]["p"]
+        np.testing.assert_allclose(p[:NU], u.detach().numpy(), rtol=0, atol=2e-6)
+        np.testing.assert_allclose(p[NU:], i.detach().numpy(), rtol=0, atol=2e-6)
+        assert np.array_equal(res[0]["p"], p)  # replicas bit-identical

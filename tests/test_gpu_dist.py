@@ -132,7 +132,7 @@ def _native_worker(rank, world, port, out_dir, SPARSE=True):
         eng.invalidate()
         f1 = eng.forward().cpu().clone()
         if native == "graph":  # full batches after the first were replayed from one capture
-            assert eng._graph is not None
+            assert eng._graphs.get(16) is not None
         res[native] = (f0.numpy(), eng.p.cpu().numpy(), eng.m.cpu().numpy(), np.array(losses), f1.numpy())
         if native is True:  # the bare collective: one rank = identity, stream-ordered
             from rsx import _lib as L
@@ -149,11 +149,11 @@ def _native_worker(rank, world, port, out_dir, SPARSE=True):
             p_before = eng.p.clone()
             big = torch.from_numpy(np.concatenate([trip, trip], axis=1)).cuda()
             eng.step(triplets=big)
-            assert eng._graph is None
+            assert not eng._graphs
             for s in range(0, 3 * 16, 16):
                 eng.step(epoch=1, start=s)
             torch.cuda.synchronize()
-            assert eng._graph is not None and torch.isfinite(eng.p).all()
+            assert eng._graphs.get(16) is not None and torch.isfinite(eng.p).all()
             assert not torch.equal(p_before, eng.p)
         eng.close()
     np.savez(os.path.join(out_dir, "native.npz"), **{f"{k}_{i}": v for k in ("graph", True, False)

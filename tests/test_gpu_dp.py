@@ -1,0 +1,138 @@
+"""Data-parallel LightGCN (rsx.dp, csrc/dp.hip) with the HIP backend.
+
+* 2 and 3 ranks sharing the one GPU of the test box, the step's two all-gathers through
+  the host hook over gloo (RCCL needs one GPU per rank; the 8-GPU RCCL run is the
+  driver's): two steps must equal two reference steps (oracle loss + torch.optim.Adam)
+  on the global batch, and every replica must stay bit-identical;
+* 1 rank over a real RCCL communicator, graph-captured: the step must equal the
+  single-GPU fused step (rsx_lightgcn_step) on the same triplets.
+"""
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import rsx_oracle as O
+from test_dist_gloo import D, LR, NI, NU, REG, _local_graph
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _trip(s, r):
+    return _local_graph(10 * s + r)[2][:, : 20 - r]  # unequal rank batches
+
+
+def _worker(rank, world, port, out_dir, k):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from rsx.dp import DataParallelLightGCNEngine
+
+    tu, ti, _ = _local_graph(0)
+    torch.manual_seed(7)
+    U0 = torch.nn.init.xavier_uniform_(torch.empty(NU, D)).numpy()
+    I0 = torch.nn.init.xavier_uniform_(torch.empty(NI, D)).numpy()
+    if rank:
+        U0, I0 = U0 * 0 + 1, I0 * 0 - 1  # replicas start from rank 0's tables
+    eng = DataParallelLightGCNEngine(tu, ti, NU, NI, D, k, REG, LR, "cuda:0", U0, I0, batch=32)
+    losses, ps = [], []
+    for s in range(2):
+        eng.step(torch.from_numpy(_trip(s, rank)).cuda())
+        losses.append(float(eng.loss_out.item()))
+        ps.append(eng.p.cpu().numpy())
+    # the union's G' rows and counts are cleared after the step
+    assert torch.count_nonzero(eng.g).item() == 0
+    assert torch.count_nonzero(eng.reg_cnt[:-4]).item() == 0
+    # device-sampled epoch: every rank the same number of slices, all finite
+    for j in range(eng.steps_per_epoch()):
+        eng.step_index(0, j)
+    torch.cuda.synchronize()
+    np.savez(os.path.join(out_dir, f"r{rank}.npz"), p1=ps[0], p2=ps[1], losses=np.array(losses),
+             after=eng.p.cpu().numpy(), f=eng.forward().cpu().numpy())
+    eng.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,k", [(2, 3), (3, 3), (2, 2), (2, 4)])
+def test_dp_hip_step_matches_global_batch(world, k):
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker, args=(world, _free_port(), d, k), nprocs=world, join=True)
+        res = [dict(np.load(os.path.join(d, f"r{r}.npz"))) for r in range(world)]
+    tu, ti, _ = _local_graph(0)
+    A = O.lightgcn_norm_adj_vec(tu, ti, NU, NI)
+    torch.manual_seed(7)
+    u = torch.nn.Parameter(torch.nn.init.xavier_uniform_(torch.empty(NU, D)))
+    i = torch.nn.Parameter(torch.nn.init.xavier_uniform_(torch.empty(NI, D)))
+    opt = torch.optim.Adam([u, i], lr=LR)
+    ref_losses, ref_p = [], []
+    for s in range(2):
+        trip = torch.from_numpy(np.concatenate([_trip(s, r) for r in range(world)], 1))
+        opt.zero_grad()
+        loss = O.lightgcn_loss(u, i, A, k, trip, REG)
+        loss.backward()
+        opt.step()
+        ref_losses.append(loss.item())
+        ref_p.append(np.concatenate([u.detach().numpy(), i.detach().numpy()]))
+    for r in range(world):
+        np.testing.assert_allclose(res[r]["losses"], ref_losses, rtol=1e-5)
+        np.testing.assert_allclose(res[r]["p1"], ref_p[0], rtol=0, atol=2e-6)
+        np.testing.assert_allclose(res[r]["p2"], ref_p[1], rtol=0, atol=3e-6)
+        for key in ("p1", "p2", "after", "f"):  # replicas bit-identical, also after an epoch
+            assert np.array_equal(res[0][key], res[r][key]), key
+    assert np.isfinite(res[0]["after"]).all()
+
+
+def _rccl_worker(rank, world, port, out_dir, k):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    from rsx.dp import DataParallelLightGCNEngine
+    from rsx.engine import LightGCNEngine
+
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "lightgcn_small.npz"))
+    nu, ni = int(z["n_users"]), int(z["n_items"])
+    U0, I0 = z["init.embedding_dict.user_emb"], z["init.embedding_dict.item_emb"]
+    dp = DataParallelLightGCNEngine(z["train_u"], z["train_i"], nu, ni, 64, k, 1e-2, 1e-3, "cuda:0", U0, I0,
+                                    batch=512)
+    one = LightGCNEngine(z["train_u"], z["train_i"], nu, ni, 64, k, 1e-2, 1e-3, "cuda:0", U0, I0, batch=512)
+    trips = torch.from_numpy(z["epoch0_triplets"].astype(np.int64)).cuda()
+    la, lb = [], []
+    for s in range(6):  # eager, eager (warm), captured, replayed ...; a partial batch at the end
+        t = trips[:, s * 512:(s + 1) * 512] if s < 5 else trips[:, 5 * 512: 5 * 512 + 300]
+        dp.step(t)
+        one.step(triplets=t)
+        la.append(float(dp.loss_out.item()))
+        lb.append(float(one.loss_out.item()))
+    torch.cuda.synchronize()
+    np.savez(os.path.join(out_dir, "rccl.npz"), la=np.array(la), lb=np.array(lb), pa=dp.p.cpu().numpy(),
+             pb=one.p.cpu().numpy(), ma=dp.m.cpu().numpy(), mb=one.m.cpu().numpy(),
+             graphs=np.array(sorted(dp._graphs)))
+    dp.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("k", [3, 4])
+def test_dp_one_rank_rccl_equals_single_gpu_step(k):
+    """World 1 over RCCL, graph-captured: the same arithmetic as the single-GPU stored-layer
+    step (only the BPR scatter's float atomics order differently run to run)."""
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_rccl_worker, args=(1, _free_port(), d, k), nprocs=1, join=True)
+        z = dict(np.load(os.path.join(d, "rccl.npz")))
+    np.testing.assert_allclose(z["la"], z["lb"], rtol=1e-6)
+    np.testing.assert_allclose(z["pa"], z["pb"], rtol=0, atol=1e-6)
+    np.testing.assert_allclose(z["ma"], z["mb"], rtol=0, atol=1e-7)
+    assert 512 in z["graphs"].tolist()  # full batches replayed from a captured graph

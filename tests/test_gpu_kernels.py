@@ -295,6 +295,29 @@ def test_sample_epoch_matches_per_batch(cuda, golden):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("n_slices", [1, 3, 7, 64, 1000, 5000])
+def test_sample_epoch_slices_recut_the_same_stream(cuda, golden, n_slices):
+    """rsx_sample_epoch_slices: slice j = epoch positions [j E // S, (j+1) E // S) of the
+    same stream rsx_sample_epoch writes (the sharded trainers' balanced epochs, every
+    interaction once, sizes within one of each other)."""
+    z = golden("lightgcn_small")
+    s = ops.DeviceSampler(z["train_u"], z["train_i"], int(z["n_users"]), cuda, seed=9)
+    E = s.n_inter
+    if n_slices > E:
+        with pytest.raises(ValueError):
+            s.sample_epoch_slices(epoch=3, n_slices=n_slices)
+        return
+    plain = s.sample_epoch(epoch=3, batch=E).view(3, E).cpu()
+    buf = s.sample_epoch_slices(epoch=3, n_slices=n_slices)
+    sizes = []
+    for j in range(n_slices):
+        a, e = ops.DeviceSampler.slice_bounds(E, n_slices, j)
+        v = ops.DeviceSampler.slice_view(buf, E, n_slices, j).cpu()
+        assert torch.equal(v, plain[:, a:e])
+        sizes.append(e - a)
+    assert sum(sizes) == E and max(sizes) - min(sizes) <= 1 and min(sizes) >= 1
+
+
 class _EvalStub:
     """The two EvalDataLoader members the device metric path reads."""
 

@@ -39,15 +39,16 @@ def test_struct_layouts_match_header(tmp_path):
         pytest.skip("no C compiler")
     inc = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "include")
     src = tmp_path / "sz.c"
-    src.write_text('#include "rsx.h"\n#include <stdio.h>\nint main(void){printf("%zu %zu %zu %zu %zu %zu %zu",'
+    src.write_text('#include "rsx.h"\n#include <stdio.h>\nint main(void){printf("%zu %zu %zu %zu %zu %zu %zu %zu",'
                    ' sizeof(rsx_csr), sizeof(rsx_adam), sizeof(rsx_epilogue), sizeof(rsx_lgcn_step),'
-                   ' sizeof(rsx_sharded_lgcn_step), sizeof(rsx_sampler_args), sizeof(rsx_layergcn_step_args));'
+                   ' sizeof(rsx_sharded_lgcn_step), sizeof(rsx_sampler_args), sizeof(rsx_layergcn_step_args),'
+                   ' sizeof(rsx_dp_lgcn_step));'
                    ' return 0;}\n')
     exe = tmp_path / "sz"
     subprocess.run([cc, "-I", inc, str(src), "-o", str(exe)], check=True)
     got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
     assert got == [C.sizeof(L.Csr), C.sizeof(L.Adam), C.sizeof(L.Epilogue), C.sizeof(L.LgcnStep),
-                   C.sizeof(L.ShardedStep), C.sizeof(L.SamplerArgs), C.sizeof(L.LayerGcnStep)]
+                   C.sizeof(L.ShardedStep), C.sizeof(L.SamplerArgs), C.sizeof(L.LayerGcnStep), C.sizeof(L.DpStep)]
 
 
 def test_comm_unique_id_size():
