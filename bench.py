@@ -189,12 +189,13 @@ def smore_kernel_rooflines(model, B, d):
     out.append(_roof_hbm(f"spmm_batch<{d},STORE> three kNN item-view products (one launch)", nbytes, ms,
                          "kNN graphs and item tables are Infinity-Cache resident at clothing", 2))
     # projection backward, image modality
-    V = model.image_embedding.weight.detach()
+    V = model.image_embedding.weight.detach()  # this rank's item rows when the item side is sharded
     W = model.image_trs.weight.detach()
-    gi = torch.randn(ni, d, generator=g).to(dev)
+    nv = V.shape[0]
+    gi = torch.randn(nv, d, generator=g).to(dev)
     ms = time_kernel(lambda: ops.linear_bwd(gi, V, W), 20)
-    out.append(_roof_mfma(f"rsx_linear_bwd (wgrad_partial<DX>) projection backward {ni}x{V.shape[1]}->{d}",
-                          4.0 * ni * d * V.shape[1], ms, "f32 MFMA 32x32x2 (dW) + 16x16x4 (dX)", 2))
+    out.append(_roof_mfma(f"rsx_linear_bwd (wgrad_partial<DX>) projection backward {nv}x{V.shape[1]}->{d}",
+                          4.0 * nv * d * V.shape[1], ms, "f32 MFMA 32x32x2 (dW) + 16x16x4 (dX)", 2))
     # preference block backward on 3B rows
     nu = model.n_users if not getattr(model, "sharded", False) else model.user_embedding.weight.shape[0]
     n = nu + ni
@@ -682,9 +683,21 @@ def main():
     # c4 is the strong-scaling leg: the graph AND the global batch (--batch) are fixed, each
     # rank draws its share of the batch from its own users; c2/baby are weak scaling: every
     # rank owns its own sports/baby-shaped user block and a batch of --batch
-    B = args.batch // world if big else args.batch
-    if big and B * world != args.batch:
-        raise SystemExit(f"--batch {args.batch} does not split evenly over {world} ranks")
+    # latency injection (RSX_COMM_SIM=W, rsx.dist.sim_comm_params): ONE rank runs the per-rank
+    # share of a W-rank c4 job (8/W of the 8 user chunks, batch 2048/W) with every collective
+    # replaced by a comm-stream kernel holding the modelled time, CUs and HBM bytes of that
+    # collective at W ranks: the step time is the modelled job's critical path
+    from rsx.dist import sim_comm_params
+
+    sim = sim_comm_params() if big else None
+    w_eff = sim["world"] if sim else world
+    if sim and world != 1:
+        raise SystemExit("RSX_COMM_SIM runs one rank")
+    if sim and args.c4_chunks is None:
+        args.c4_chunks = 8 // w_eff
+    B = args.batch // w_eff if big else args.batch
+    if big and B * w_eff != args.batch:
+        raise SystemExit(f"--batch {args.batch} does not split evenly over {w_eff} ranks")
     scheme = args.dist or ("rowshard" if big else "dp")
     if big and scheme != "rowshard":
         raise SystemExit("--workload c4 is the row-sharded strong-scaling leg")
@@ -692,6 +705,10 @@ def main():
     tu, ti, vu_all, vi_all, nu, ni, d, desc = load_graph(args.workload, rank, world, args.c4_chunks, replicated=dp)
     if big and args.c4_chunks:
         desc += f" [only {args.c4_chunks} of 8 user chunks built]"
+    if sim:
+        desc += (f" [latency-injected model of rank 0 of a {sim['world']}-rank job: its {args.c4_chunks}/8 user "
+                 f"share, batch {B}, every collective a comm-stream kernel of the modelled time at "
+                 f"{sim['busbw_gbs']:.0f} GB/s bus bandwidth + {sim['latency_us']:.0f} us]")
     if dp:
         desc = desc.replace("per rank), B=2048 per rank", "), the graph replicated on every rank, "
                                                               f"B={B} per rank, global batch {B * world}")
@@ -995,6 +1012,15 @@ def main():
             "gpu_ms_per_step_events": gpu_ms / args.steps,
             "train_loss_mean": loss_mean,
         }
+        if sim:
+            X = float(ni) * d * 4
+            lib = L.lib()
+            out["latency_injection"] = dict(sim, per_collective_ms={
+                "allreduce_item_block": 1e3 * lib.rsx_comm_sim_seconds(eng._comm, L.RSX_COLL_ALLREDUCE, X),
+                "reduce_scatter_or_all_gather_item_block":
+                    1e3 * lib.rsx_comm_sim_seconds(eng._comm, L.RSX_COLL_ALLGATHER, X)},
+                note="value / ms_per_step: one rank's share of the modelled job (the job's rate is world x value "
+                     "when every rank holds the same share)")
         _json_line(out)
     if hasattr(eng, "close"):
         eng.close()

@@ -801,9 +801,26 @@ enum { RSX_COLL_ALLREDUCE = 0, RSX_COLL_ALLGATHER = 1, RSX_COLL_REDUCESCATTER = 
 enum { RSX_COLL_F32 = 0, RSX_COLL_I64 = 1 };
 typedef int (*rsx_host_collective_fn)(int32_t op, void* buf, int64_t count, int32_t dtype, void* ctx);
 int rsx_comm_init_host(rsx_comm_t* out, int32_t rank, int32_t world, rsx_host_collective_fn fn, void* ctx);
+/* Latency injection (a one-GPU stand-in for a sim_world-rank job): a communicator of
+ * world 1 whose collectives leave the data as it is (the one-rank result) and instead
+ * run, on the communicator's stream, a kernel of `blocks` 256-thread workgroups that
+ * streams the collective's HBM bytes through a `scratch_mb` scratch buffer and holds
+ * its slots for the modelled time of the collective at sim_world ranks: a ring moves
+ * 2 (W-1)/W X bytes per rank for an all-reduce of X, (W-1)/W X for an all-gather or
+ * reduce-scatter whose whole buffer is X, at `busbw_gbs` GB/s per rank, plus
+ * `latency_us`.  A one-rank step over it has the compute of one rank of the modelled
+ * job and the exchanges' time and CU / HBM footprint on the comm stream, so its
+ * measured step time is the modelled job's critical path.
+ * rsx_comm_sim_seconds: the modelled time of one collective (the buffer's bytes). */
+int rsx_comm_init_sim(rsx_comm_t* out, int32_t sim_world, double busbw_gbs, double latency_us, int32_t blocks,
+                      int64_t scratch_mb);
+double rsx_comm_sim_seconds(rsx_comm_t comm, int32_t op, double bytes);
 /* buf[0, n) := sum over ranks, in place, ordered after the work queued on `stream`
  * and before the work queued on it afterwards. */
 int rsx_comm_allreduce_f32(rsx_comm_t comm, float* buf, int64_t n, rsx_stream_t stream);
+/* buf[r n, (r+1) n) := rank r's slice for every rank r (buf holds world * n floats), in
+ * place, stream-ordered as above. */
+int rsx_comm_allgather_f32(rsx_comm_t comm, float* buf, int64_t n, rsx_stream_t stream);
 
 /*
  * One LightGCN batch on this rank's shard (the sharded twin of rsx_lightgcn_step;

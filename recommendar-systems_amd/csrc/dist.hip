@@ -87,6 +87,16 @@ struct rsx_comm_s {
     int32_t rank = 0, world = 1;
     rsx_host_collective_fn host_fn = nullptr;  // test hook: host-side collective instead of RCCL
     void* host_ctx = nullptr;
+    // latency-injected one-rank communicator (rsx_comm_init_sim): every collective is the
+    // identity on the data (world 1) and a comm-stream kernel that holds `sim_blocks`
+    // workgroups and streams the collective's HBM bytes for the modelled time at sim_world
+    int32_t sim_world = 0;
+    double sim_busbw = 0.0;   // bytes/s per rank, the model's bus bandwidth at sim_world
+    double sim_lat = 0.0;     // seconds per collective
+    int32_t sim_blocks = 0;
+    double sim_tick_hz = 0.0; // the device wall clock
+    float* sim_scratch = nullptr;
+    int64_t sim_scratch_floats = 0;
 };
 
 namespace rsx {
@@ -103,6 +113,31 @@ hipEvent_t comm_event(rsx_comm_t c) {
     return j;
 }
 
+// The latency-injection stand-in for one collective: `blocks` workgroups copy `floats`
+// floats of the scratch (half read, half written: the collective's HBM traffic) and
+// then hold their slots until `ticks` of the device wall clock have passed since the
+// kernel started (block 0's start, shared through the first scratch word is not
+// needed: each block measures from its own start, all start together).
+__global__ __launch_bounds__(256) void sim_collective(float* __restrict__ scratch, int64_t half, int64_t floats,
+                                                      uint64_t ticks) {
+    const uint64_t t0 = wall_clock64();
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < floats / 2; i += stride) {
+        const int64_t k = i % half;
+        scratch[half + k] = scratch[k] + 1.f;
+    }
+    while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(16);
+}
+
+// Modelled time of one collective of `bytes` (the whole buffer: all-reduce X, all-gather
+// / reduce-scatter world * count) over sim_world ranks: a ring moves 2 (W-1)/W X per rank
+// for an all-reduce, (W-1)/W X for the others, at the model's per-rank bus bandwidth.
+static double sim_seconds(const rsx_comm_s* c, int op, double bytes) {
+    const double w = c->sim_world;
+    const double moved = (op == RSX_COLL_ALLREDUCE ? 2.0 : 1.0) * (w - 1.0) / w * bytes;
+    return moved / c->sim_busbw + c->sim_lat;
+}
+
 // In-place collective `op` (RSX_COLL_*) on buf over the communicator, after the
 // work queued so far on `s`; returns the join event the reader must wait on
 // (nullptr on error, rc set).  A host-hook communicator synchronises `s`, calls the
@@ -111,6 +146,25 @@ hipEvent_t collective(rsx_comm_t c, int op, void* buf, int64_t count, int dtype,
     hipError_t e;
     hipEvent_t j = c->join[c->next];
     c->next = (c->next + 1) % kJoinEvents;
+    if (c->sim_world) {  // one rank: the data is already the result; the time is injected
+        if ((e = hipEventRecord(c->fork, s)) != hipSuccess || (e = hipStreamWaitEvent(c->stream, c->fork, 0)) != hipSuccess) {
+            *rc = hip_rc(e);
+            return nullptr;
+        }
+        const double es = dtype == RSX_COLL_I64 ? 8.0 : 4.0;
+        const double bytes = (double)count * es;  // world 1: the whole buffer
+        const double sec = sim_seconds(c, op, bytes);
+        const double moved = (op == RSX_COLL_ALLREDUCE ? 2.0 : 1.0) * (c->sim_world - 1.0) / c->sim_world * bytes;
+        int64_t floats = (int64_t)(2.0 * moved / 4.0);  // the moved bytes read once and written once
+        const int64_t half = c->sim_scratch_floats / 2;
+        hipLaunchKernelGGL(sim_collective, dim3((unsigned)c->sim_blocks), dim3(256), 0, c->stream, c->sim_scratch,
+                           half, floats, (uint64_t)(sec * c->sim_tick_hz));
+        if ((e = hipGetLastError()) != hipSuccess || (e = hipEventRecord(j, c->stream)) != hipSuccess) {
+            *rc = hip_rc(e);
+            return nullptr;
+        }
+        return j;
+    }
     if (c->host_fn) {
         if ((e = hipStreamSynchronize(s)) != hipSuccess) {
             *rc = hip_rc(e);
@@ -751,9 +805,45 @@ int rsx_comm_init_host(rsx_comm_t* out, int32_t rank, int32_t world, rsx_host_co
     return RSX_OK;
 }
 
+int rsx_comm_init_sim(rsx_comm_t* out, int32_t sim_world, double busbw_gbs, double latency_us, int32_t blocks,
+                      int64_t scratch_mb) {
+    if (!out || sim_world < 2 || busbw_gbs <= 0 || latency_us < 0 || blocks < 1 || scratch_mb < 1)
+        return RSX_ERR_ARG;
+    rsx_comm_s* c = new rsx_comm_s();
+    c->rank = 0;
+    c->world = 1;
+    c->sim_world = sim_world;
+    c->sim_busbw = busbw_gbs * 1e9;
+    c->sim_lat = latency_us * 1e-6;
+    c->sim_blocks = blocks;
+    int dev = 0, khz = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev);
+    c->sim_tick_hz = (khz > 0 ? khz : 100000) * 1e3;
+    c->sim_scratch_floats = scratch_mb * (1 << 20) / 4;
+    if (e == hipSuccess) e = hipMalloc(&c->sim_scratch, (size_t)c->sim_scratch_floats * 4);
+    if (e == hipSuccess) e = hipMemset(c->sim_scratch, 0, (size_t)c->sim_scratch_floats * 4);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork, hipEventDisableTiming);
+    for (int i = 0; e == hipSuccess && i < rsx::kJoinEvents; ++i)
+        e = hipEventCreateWithFlags(&c->join[i], hipEventDisableTiming);
+    if (e != hipSuccess) {
+        rsx_comm_destroy(c);
+        return rsx::hip_rc(e);
+    }
+    *out = c;
+    return RSX_OK;
+}
+
+double rsx_comm_sim_seconds(rsx_comm_t c, int32_t op, double bytes) {
+    if (!c || !c->sim_world) return -1.0;
+    return rsx::sim_seconds(c, op, bytes);
+}
+
 int rsx_comm_destroy(rsx_comm_t c) {
     if (!c) return RSX_OK;
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->sim_scratch) (void)hipFree(c->sim_scratch);
     if (c->nccl) rsx::rccl().destroy(c->nccl);
     for (int i = 0; i < rsx::kJoinEvents; ++i)
         if (c->join[i]) (void)hipEventDestroy(c->join[i]);
@@ -768,6 +858,15 @@ int rsx_comm_allreduce_f32(rsx_comm_t c, float* buf, int64_t n, rsx_stream_t str
     int rc = 0;
     hipStream_t s = rsx::as_stream(stream);
     hipEvent_t j = rsx::exchange(c, buf, n, s, &rc);
+    if (!j) return rc;
+    return rsx::wait(s, j);
+}
+
+int rsx_comm_allgather_f32(rsx_comm_t c, float* buf, int64_t count, rsx_stream_t stream) {
+    if (!c || (!buf && count > 0) || count < 0) return RSX_ERR_ARG;
+    int rc = 0;
+    hipStream_t s = rsx::as_stream(stream);
+    hipEvent_t j = rsx::collective(c, RSX_COLL_ALLGATHER, buf, count, RSX_COLL_F32, s, &rc);
     if (!j) return rc;
     return rsx::wait(s, j);
 }

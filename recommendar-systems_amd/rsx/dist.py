@@ -78,6 +78,31 @@ from . import _lib as L
 from . import graph, ops
 
 
+# xGMI link model (MI355X_MICROARCH.md): 7 links per GPU, ~76.5 GB/s per
+# direction each; a W-rank ring on a fully connected node drives min(W-1, 7) of them at
+# an efficiency of 0.8 (RCCL's ring / LL128 protocols on large messages)
+XGMI_LINK_GBS, XGMI_LINKS, RING_EFF, RCCL_LATENCY_US, RCCL_BLOCKS = 76.5, 7, 0.8, 30.0, 32
+
+
+def model_busbw_gbs(world: int) -> float:
+    return min(world - 1, XGMI_LINKS) * XGMI_LINK_GBS * RING_EFF
+
+
+def sim_comm_params():
+    """RSX_COMM_SIM = "W[:busbw_gbs[:latency_us[:blocks]]]": run the one-rank engine over a
+    latency-injected communicator modelling a W-rank job (rsx_comm_init_sim); None if unset."""
+    v = os.environ.get("RSX_COMM_SIM")
+    if not v:
+        return None
+    f = v.split(":")
+    w = int(f[0])
+    if w < 2:
+        raise ValueError(f"RSX_COMM_SIM={v}: the modelled world must be >= 2")
+    return {"world": w, "busbw_gbs": float(f[1]) if len(f) > 1 and f[1] else model_busbw_gbs(w),
+            "latency_us": float(f[2]) if len(f) > 2 and f[2] else RCCL_LATENCY_US,
+            "blocks": int(f[3]) if len(f) > 3 and f[3] else RCCL_BLOCKS, "scratch_mb": 512}
+
+
 class HipBackend:
     """Product backend: rsx HIP kernels on the current torch stream."""
 
@@ -195,6 +220,7 @@ class ShardedLightGCNEngine:
             native = isinstance(self.be, HipBackend) and dist.get_backend(self.group) == "nccl"
         self.native = bool(native)
         self._comm = None
+        self.sim = None  # the latency-injection model (RSX_COMM_SIM), if the communicator is one
         if self.native:
             if not isinstance(self.be, HipBackend):
                 raise RuntimeError("the native sharded step needs the HIP backend")
@@ -218,7 +244,15 @@ class ShardedLightGCNEngine:
                 and os.environ.get("RSX_SHARDED_FUSED", "0") == "1"):
             self.xch = torch.zeros(2 * self.n_items, self.d, dtype=torch.float32, device=self.be.device)
         comm = C.c_void_p()
-        if dist.get_backend(self.group) == "nccl":
+        sim = sim_comm_params()
+        if sim is not None:
+            if self.world != 1:
+                raise RuntimeError("RSX_COMM_SIM models a multi-rank job on ONE rank (world 1)")
+            self.sim = sim
+            with torch.cuda.device(self.be.device):
+                L.check(lib.rsx_comm_init_sim(C.byref(comm), sim["world"], sim["busbw_gbs"], sim["latency_us"],
+                                              sim["blocks"], sim["scratch_mb"]), "rsx_comm_init_sim")
+        elif dist.get_backend(self.group) == "nccl":
             nb = int(lib.rsx_comm_unique_id_bytes())
             buf = (C.c_uint8 * nb)()
             if self.rank == 0:

@@ -407,12 +407,24 @@ class SMORE(GeneralRecommender):
         graphs = {"norm_adj": (np.asarray(rp), np.asarray(col), np.asarray(val)),
                   "R": graph.to_csr(r_coo[0], r_coo[1], r_coo[2], nu, ni),
                   "image": self.image_graph, "text": self.text_graph, "fusion": self.fusion_graph}
+        # the item side sharded by item rows too (projection, spectral fusion, the gates'
+        # inject term; the raw feature tables row-sharded): residual inject mode only (its
+        # inject term is row-local and additive); rsx_smore_item_shard: False replicates it
+        flag = config.get("rsx_smore_item_shard", True)
+        item_shard = bool(flag if flag is not None else True) and self.inject_mode != "mul"
         self._shard = SmoreShard(graphs, nu, ni, self.n_ui_layers, self.n_layers,
-                                 HipSmoreBackend(self.device, int(config["rsx_chunk"] or 32)), self.comm)
+                                 HipSmoreBackend(self.device, int(config["rsx_chunk"] or 32)), self.comm,
+                                 item_shard=item_shard)
         a, b = self._shard.own_u
         self.user_range = (a, b)
         w = self.user_embedding.weight.detach()[a:b].clone()
         self.user_embedding = nn.Embedding(b - a, self.embedding_dim, _weight=w, device=self.device)
+        if self._shard.item_shard:  # this rank's rows of the raw feature tables
+            ia, ib = self._shard.own_i
+            self.image_embedding = nn.Embedding.from_pretrained(
+                self.image_embedding.weight.detach()[ia:ib].clone(), freeze=False)
+            self.text_embedding = nn.Embedding.from_pretrained(
+                self.text_embedding.weight.detach()[ia:ib].clone(), freeze=False)
         # the step's collectives are captured with it only over RCCL (a gloo group's are host calls)
         self.supports_graph_step = self.comm.native
         # this rank's interactions, visited once per epoch in the common step count

@@ -57,6 +57,8 @@ from . import graph, ops
 
 # the row-sharded parameter (its rows [a_r, b_r) live on rank r); everything else is replicated
 SHARDED = {"user_embedding.weight": "u"}
+# with the item side sharded (SmoreShard item_shard): the raw feature tables' rows
+ITEM_SHARDED = {"image_embedding.weight": "i", "text_embedding.weight": "i"}
 # the preference block's Linear layers: replicated weights fed by rank-local rows
 PREF = ("query_v.0", "query_v.2", "query_t.0", "query_t.2", "gate_image_prefer.0", "gate_text_prefer.0",
         "gate_fusion_prefer.0")
@@ -109,6 +111,23 @@ class Comm:
             t.copy_(h)
         return t
 
+    def allgather_(self, t: torch.Tensor, count: int) -> torch.Tensor:
+        """t[r count:(r+1) count] := rank r's slice, every r (t: world * count floats)."""
+        if self.world == 1:
+            return t
+        if t.dtype != torch.float32 or not t.is_contiguous() or t.numel() < self.world * count:
+            raise RuntimeError("Comm.allgather_: a contiguous float32 tensor of world * count elements")
+        if self.handle is not None:
+            L.check(L.lib().rsx_comm_allgather_f32(self.handle, t.data_ptr(), int(count), ops._stream()),
+                    "rsx_comm_allgather_f32")
+            return t
+        flat = t.view(-1)
+        mine = flat[self.rank * count:(self.rank + 1) * count].cpu()
+        parts = [torch.empty_like(mine) for _ in range(self.world)]
+        dist.all_gather(parts, mine, group=self.group)
+        flat[: self.world * count].copy_(torch.cat(parts).to(t.device))
+        return t
+
     def close(self):
         if self.handle is not None:
             torch.cuda.synchronize()
@@ -142,6 +161,48 @@ class _AllReduceGrad(torch.autograd.Function):
 
 def allreduce_grad(comm, *ts):
     return _AllReduceGrad.apply(comm, *ts)
+
+
+class _GatherRows(torch.autograd.Function):
+    """Every rank's rows of k row-sharded tables (rank r: rows [r q, r q + n_r) of each,
+    n_r <= q) gathered into [k, n, d] on every rank in ONE all-gather of [k, q, d] slices
+    (padded); backward: the replicated gradient's own rows (no exchange: the gradient of
+    a replicated consumer is the same on every rank)."""
+
+    @staticmethod
+    def forward(ctx, comm, q, n, *own):
+        k = len(own)
+        n_r, d = own[0].shape
+        W, r = comm.world, comm.rank
+        buf = torch.zeros(W, k, q, d, dtype=torch.float32, device=own[0].device)
+        for j, x in enumerate(own):
+            buf[r, j, :n_r].copy_(x)
+        comm.allgather_(buf, k * q * d)
+        out = buf.permute(1, 0, 2, 3).reshape(k, W * q, d)[:, :n].contiguous()
+        ctx.rq = (r * q, r * q + n_r)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        a, b = ctx.rq
+        return (None, None, None, *[g[j, a:b] for j in range(g.shape[0])])
+
+
+def gather_rows(comm, q, n, *own):
+    return _GatherRows.apply(comm, q, n, *own)
+
+
+def item_ranges(n_items: int, world: int):
+    """Rank r's item rows [r q, min((r+1) q, n_items)), q = ceil(n_items / world): equal
+    slices (the last may be shorter), so one all-gather of q-row slices lines them up."""
+    q = -(-n_items // world)
+    return q, [(min(r * q, n_items), min((r + 1) * q, n_items)) for r in range(world)]
+
+
+# the item side's weights: each rank's gradient covers its own item rows only
+ITEM_W = ("image_trs.weight", "image_trs.bias", "text_trs.weight", "text_trs.bias", "image_complex_weight",
+          "text_complex_weight", "fusion_complex_weight", "gate_v.0.weight", "gate_v.0.bias", "gate_t.0.weight",
+          "gate_t.0.bias", "gate_f.0.weight", "gate_f.0.bias")
 
 
 class _UIProp(torch.autograd.Function):
@@ -242,6 +303,24 @@ class HipSmoreBackend:
 
         return SF.gates(cv, ct, cf, item, m.gate_v, m.gate_t, m.gate_f, m.inject_scale, False)
 
+    def item_side_sharded(self, core, m):
+        """Projection -> spectral -> the gates' inject term on this rank's item rows only
+        (the fused kernels on n_own rows), gathered once; + the replicated item-id table."""
+        from . import smore_fuse as SF
+        from .smore_spectral import spectral
+
+        w = dict(zip(ITEM_W, allreduce_grad(core.comm, *[m.get_parameter(n) for n in ITEM_W])))
+        cv, ct, cf, _, _ = spectral(m.image_embedding.weight, w["image_trs.weight"], w["image_trs.bias"],
+                                    m.text_embedding.weight, w["text_trs.weight"], w["text_trs.bias"],
+                                    w["image_complex_weight"], w["text_complex_weight"], w["fusion_complex_weight"],
+                                    getattr(m, "spectral_weight_norm", True))
+        zero = core.zero_rows(cv)
+        dv, dt, df = SF._Gates.apply(cv, ct, cf, zero, w["gate_v.0.weight"], w["gate_v.0.bias"], w["gate_t.0.weight"],
+                                     w["gate_t.0.bias"], w["gate_f.0.weight"], w["gate_f.0.bias"],
+                                     float(m.inject_scale), False)
+        D = gather_rows(core.comm, core.iq, core.n_items, dv, dt, df)
+        return (D + m.item_id_embedding.weight.unsqueeze(0)).unbind(0)
+
     def views(self, core, xs):
         from . import smore_fuse as SF
 
@@ -281,7 +360,7 @@ class SmoreShard:
     m.user_embedding.weight holds this rank's user rows, the rest the full tables."""
 
     def __init__(self, graphs: dict, n_users: int, n_items: int, n_ui_layers: int, n_layers: int, backend,
-                 comm: Comm):
+                 comm: Comm, item_shard: bool = False):
         self.be, self.comm = backend, comm
         self.world, self.rank = comm.world, comm.rank
         self.n_users, self.n_items = int(n_users), int(n_items)
@@ -306,12 +385,27 @@ class SmoreShard:
         rrp, rcol, rval = graphs["R"]
         self.R = backend.operator(*csr_rows(rrp, rcol, rval, a, b), ni, transpose=True)
         self._rows_cache = {}
+        # the item side (projection, spectral fusion, the gates' inject term) on this rank's
+        # item rows only, the raw feature tables row-sharded with it (rank r: rows
+        # [r q, (r+1) q)); the three inject tables gathered once per forward
+        self.iq, irng = item_ranges(ni, self.world)
+        self.own_i = irng[self.rank]
+        self.item_shard = bool(item_shard) and self.world > 1 and all(b_ > a_ for a_, b_ in irng)
+        self._zero = None
 
     # -- pieces -----------------------------------------------------------------
     def ui_mean(self, x):
         return self.be.ui_mean(self, x)
 
+    def zero_rows(self, like):
+        """A zero [n_own_items, d] table (the gates kernel's item operand: the inject term alone)."""
+        if self._zero is None or self._zero.shape != like.shape or self._zero.device != like.device:
+            self._zero = torch.zeros_like(like)
+        return self._zero
+
     def _item_side(self, m):
+        if self.item_shard:
+            return self.be.item_side_sharded(self, m)
         cv, ct, cf = self.be.spectral(m)
         return self.be.gates(m, cv, ct, cf, m.item_id_embedding.weight)
 
@@ -389,6 +483,8 @@ class SmoreShard:
         squares of the row-sharded user table summed over the ranks (one all-reduce),
         the replicated parameters counted once."""
         sharded = {id(m.user_embedding.weight)}
+        if self.item_shard:  # the raw feature tables: this rank's item rows
+            sharded |= {id(m.image_embedding.weight), id(m.text_embedding.weight)}
         sh_g = [g for p, g in zip(params, grads) if id(p) in sharded]
         sh_p = [p.detach() for p in params if id(p) in sharded]
         rp_g = [g for p, g in zip(params, grads) if id(p) not in sharded]
@@ -429,10 +525,11 @@ def graphs_from_rsx(model):
             "text": host(model.text_graph.A), "fusion": host(model.fusion_graph.A), "R": host(model.R.A)}
 
 
-def param_container(params: dict, cfg: dict, user_range, device="cpu"):
+def param_container(params: dict, cfg: dict, user_range, device="cpu", item_range=None):
     """An nn.Module with the reference's SMORE parameter layout holding `params` (full
-    tables; the user table cut to `user_range`) — the parameter holder of the CPU
-    tests and of tools that drive SmoreShard without rsx.smore.SMORE."""
+    tables; the user table cut to `user_range`, with `item_range` the raw feature tables
+    cut to those item rows) — the parameter holder of the CPU tests and of tools that
+    drive SmoreShard without rsx.smore.SMORE."""
     m = nn.Module()
     a, b = user_range
     d = params["user_embedding.weight"].shape[1]
@@ -450,6 +547,8 @@ def param_container(params: dict, cfg: dict, user_range, device="cpu"):
         full = torch.as_tensor(full, dtype=torch.float32)
         if SHARDED.get(name) == "u":
             full = full[a:b]
+        elif item_range is not None and ITEM_SHARDED.get(name) == "i":
+            full = full[item_range[0]:item_range[1]]
         obj = m
         *path, leaf = name.split(".")
         for k in path:

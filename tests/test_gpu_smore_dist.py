@@ -5,8 +5,11 @@ golden fixture (itself pinned to the reference's first step, tests/test_gpu_smor
 on the objective the sharded run optimises: the sum over ranks of the reference loss
 of each rank's own batch.
 
-* one batch: every rank's loss, every gradient (own user rows; the replicated item
-  side equal on every rank) within 1e-4 of scale;
+* one batch: every rank's loss, every gradient (own user rows; with the item side
+  sharded, own rows of the raw feature tables; the replicated parameters equal on every
+  rank) within 1e-4 of scale, against the single-process rsx SMORE AND directly against
+  the oracle (oracle/rsx_oracle.py:SMORECPU, the reference's restatement) on the sum of
+  the rank batches;
 * the sharded evaluation (each rank ranks its own users; metric sums all-gathered)
   equal to the single-process evaluation of the same weights;
 * one epoch through rsx.trainer.Trainer (device-sampled rank batches, the model-level
@@ -31,7 +34,7 @@ def _golden(name):
     return dict(np.load(os.path.join(GOLD, name + ".npz")))
 
 
-def _models(root, rank, fx):
+def _models(root, rank, fx, item_shard=True):
     """(config, train, valid, sharded model, single-process model), both from the
     reference's initial weights (init_seed before each)."""
     import test_gpu_smore as T
@@ -39,6 +42,7 @@ def _models(root, rank, fx):
     z, c, train, valid, test = T._setup(Path(root) / f"r{rank}", _golden, fx)
     c["rsx_sampler"] = "device"  # the sharded model samples its own users on the device
     c["rsx_knn"] = "host"  # the kNN graphs of the fixture tests (tests/test_gpu_smore.py)
+    c["rsx_smore_item_shard"] = item_shard
     sm = T._model(c, train)
     assert sm.sharded
     c["rsx_sharded"] = False
@@ -63,12 +67,43 @@ def _global_batch(sm, inter):
     return [p[:, : int(s.item())].to(inter.device) for p, s in zip(parts, sizes)]
 
 
-def _worker(rank, world, port, root, out, fx):
+def _own_rows(sm, n, t):
+    """The rows of a (full-table) tensor `t` that rank's parameter `n` holds."""
+    if n == "user_embedding.weight":
+        a, b = sm.user_range
+        return t[a:b]
+    if sm._shard.item_shard and n in ("image_embedding.weight", "text_embedding.weight"):
+        a, b = sm._shard.own_i
+        return t[a:b]
+    return t
+
+
+def _sharded_param(sm, n):
+    return n == "user_embedding.weight" or (sm._shard.item_shard and n in ("image_embedding.weight",
+                                                                            "text_embedding.weight"))
+
+
+def _oracle_grads(z, c, batches):
+    """The oracle's SMORE (the reference restated on the CPU) on the same fixture weights:
+    the per-batch losses and the gradients of their sum."""
+    import rsx_oracle as O
+
+    init = {k[5:]: z[k] for k in z if k.startswith("init.")}
+    m = O.SMORECPU(z["train_u"], z["train_i"], int(z["n_users"]), int(z["n_items"]), z["v_feat"], z["t_feat"],
+                   d=int(c["embedding_size"]), image_k=int(c["image_knn_k"]), text_k=int(c["text_knn_k"]),
+                   dropout=0.0, batch_size=int(c["train_batch_size"]), init=init)
+    losses = [m.calculate_loss(b.cpu()) for b in batches]
+    sum(losses).backward()
+    return [x.item() for x in losses], {n: p.grad.detach() for n, p in m.named_parameters()}
+
+
+def _worker(rank, world, port, root, out, fx, item_shard=True):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from rsx.evaluator import TopKEvaluator
 
-    z, c, train, valid, sm, ref = _models(root, rank, fx)
+    z, c, train, valid, sm, ref = _models(root, rank, fx, item_shard)
+    assert sm._shard.item_shard == item_shard
     sm.train()
     ref.train()
     inter = next(iter(sm.local_batches(0)))
@@ -77,17 +112,17 @@ def _worker(rank, world, port, root, out, fx):
     batches = _global_batch(sm, inter)
     rl = [ref.calculate_loss(b) for b in batches]
     sum(rl).backward()
-    a, b = sm.user_range
-    err = {}
+    ol, og = _oracle_grads(z, c, batches)
+    err, oerr = {}, {}
     refp = dict(ref.named_parameters())
     assert set(refp) == set(n for n, _ in sm.named_parameters())
     for n, p in sm.named_parameters():
-        g = refp[n].grad.detach()
-        if n == "user_embedding.weight":
-            g = g[a:b]
+        g = _own_rows(sm, n, refp[n].grad.detach())
         scale = max(g.abs().max().item(), 1e-12)
         err[n] = (p.grad - g).abs().max().item() / scale
-    grads = {n: p.grad.detach().cpu().numpy() for n, p in sm.named_parameters() if n != "user_embedding.weight"}
+        go = _own_rows(sm, n, og[n]).to(p.device)
+        oerr[n] = (p.grad - go).abs().max().item() / max(go.abs().max().item(), 1e-12)
+    grads = {n: p.grad.detach().cpu().numpy() for n, p in sm.named_parameters() if not _sharded_param(sm, n)}
     # sharded evaluation of the initial weights vs the single-process evaluation
     sm.eval()
     ref.eval()
@@ -97,8 +132,8 @@ def _worker(rank, world, port, root, out, fx):
     got = ev.evaluate_sharded(pos, topk, valid)
     _, full = ref.full_sort_topk([valid.eval_u, None], k, valid)
     want = ev.evaluate_device(full, valid)
-    np.savez(os.path.join(out, f"r{rank}.npz"), loss=loss.item(), ref=rl[rank].item(),
-             names=np.array(list(err)), errs=np.array(list(err.values())),
+    np.savez(os.path.join(out, f"r{rank}.npz"), loss=loss.item(), ref=rl[rank].item(), oracle=ol[rank],
+             names=np.array(list(err)), errs=np.array(list(err.values())), oerrs=np.array(list(oerr.values())),
              keys=np.array(sorted(got)), got=np.array([got[x] for x in sorted(got)]),
              want=np.array([want[x] for x in sorted(got)]), **{"g." + n: v for n, v in grads.items()})
     dist.destroy_process_group()
@@ -120,13 +155,18 @@ def _spawn(fn, world, *args):
         return [dict(np.load(os.path.join(out, f"r{r}.npz"))) for r in range(world)]
 
 
-@pytest.mark.parametrize("fx,world", [("smore_small", 2), ("smore_d128_small", 2), ("smore_small", 4)])
-def test_sharded_smore_hip_matches_single_process(cuda, fx, world):
-    res = _spawn(_worker, world, fx)
+@pytest.mark.parametrize("fx,world,item_shard", [("smore_small", 2, True), ("smore_d128_small", 2, True),
+                                                 ("smore_small", 4, True), ("smore_d128_small", 4, True),
+                                                 ("smore_small", 2, False)])
+def test_sharded_smore_hip_matches_single_process(cuda, fx, world, item_shard):
+    res = _spawn(_worker, world, fx, item_shard)
     for x in res:
         assert abs(float(x["loss"]) - float(x["ref"])) <= 2e-5 * abs(float(x["ref"]))
+        assert abs(float(x["loss"]) - float(x["oracle"])) <= 2e-5 * abs(float(x["oracle"]))
         bad = {n: e for n, e in zip(x["names"], x["errs"]) if not e <= 1e-4}
         assert not bad, bad
+        bad = {n: e for n, e in zip(x["names"], x["oerrs"]) if not e <= 1e-4}
+        assert not bad, ("vs oracle", bad)
         assert np.array_equal(x["got"], res[0]["got"])
         assert np.abs(x["got"] - x["want"]).max() <= 1e-4
         for n in x:  # replicated gradients are bit-identical on every rank
@@ -154,15 +194,12 @@ def _trainer_worker(rank, world, port, root, out, fx):
 
     ref.pre_epoch_processing()
     loss_r, _ = tr._train_epoch(steps, 0, loss_func=joint)
-    a, b = sm.user_range
     refp = dict(ref.named_parameters())
     err = {}
     for n, p in sm.named_parameters():
-        want = refp[n].detach()
-        if n == "user_embedding.weight":
-            want = want[a:b]
+        want = _own_rows(sm, n, refp[n].detach())
         err[n] = (p.detach() - want).abs().max().item()
-    items = {n: p.detach().cpu().numpy() for n, p in sm.named_parameters() if n != "user_embedding.weight"}
+    items = {n: p.detach().cpu().numpy() for n, p in sm.named_parameters() if not _sharded_param(sm, n)}
     np.savez(os.path.join(out, f"r{rank}.npz"), loss=float(loss_s), ref=float(loss_r), steps=len(steps),
              gstep=sm.global_step, rstep=ref.global_step, names=np.array(list(err)), errs=np.array(list(err.values())),
              **{"p." + n: v for n, v in items.items()})

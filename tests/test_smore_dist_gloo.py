@@ -72,6 +72,31 @@ class TorchSmoreBackend:
                 torch.fft.irfft(ft * unit(m.text_complex_weight), n=n, dim=1, norm="ortho"),
                 torch.fft.irfft(ft * fi * unit(m.fusion_complex_weight), n=n, dim=1, norm="ortho"))
 
+    def item_side_sharded(self, core, m):
+        """The item side on this rank's item rows (m's feature tables hold them), the inject
+        terms gathered (rsx.smore_dist.gather_rows) and added to the replicated item table."""
+        from rsx.smore_dist import ITEM_W, allreduce_grad, gather_rows
+
+        w = dict(zip(ITEM_W, allreduce_grad(core.comm, *[m.get_parameter(n) for n in ITEM_W])))
+        img = F.linear(m.image_embedding.weight, w["image_trs.weight"], w["image_trs.bias"])
+        txt = F.linear(m.text_embedding.weight, w["text_trs.weight"], w["text_trs.bias"])
+        fi, ft = torch.fft.rfft(img, dim=1, norm="ortho"), torch.fft.rfft(txt, dim=1, norm="ortho")
+
+        def unit(x):
+            wc = torch.view_as_complex(x)
+            return wc / (torch.abs(wc) + 1e-8)
+
+        n = img.shape[1]
+        cv = torch.fft.irfft(fi * unit(w["image_complex_weight"]), n=n, dim=1, norm="ortho")
+        ct = torch.fft.irfft(ft * unit(w["text_complex_weight"]), n=n, dim=1, norm="ortho")
+        cf = torch.fft.irfft(ft * fi * unit(w["fusion_complex_weight"]), n=n, dim=1, norm="ortho")
+        s = m.inject_scale
+        D = gather_rows(core.comm, core.iq, core.n_items,
+                        s * torch.sigmoid(F.linear(cv, w["gate_v.0.weight"], w["gate_v.0.bias"])),
+                        s * torch.sigmoid(F.linear(ct, w["gate_t.0.weight"], w["gate_t.0.bias"])),
+                        s * torch.sigmoid(F.linear(cf, w["gate_f.0.weight"], w["gate_f.0.bias"])))
+        return (D + m.item_id_embedding.weight.unsqueeze(0)).unbind(0)
+
     def gates(self, m, cv, ct, cf, item):
         return (item + m.inject_scale * m.gate_v(cv), item + m.inject_scale * m.gate_t(ct),
                 item + m.inject_scale * m.gate_f(cf))
@@ -154,22 +179,29 @@ def rank_batches(z, nu, world, per=120):
 CFG = dict(reg_weight=1e-5, batch_size=2048, cl_loss=0.01, cl_temp=0.2, dropout_rate=0.0)
 
 
-def _setup_rank(rank, world, port):
+def _setup_rank(rank, world, port, item_shard=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.set_num_threads(1)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from rsx.smore_dist import Comm, SmoreShard, param_container
 
     _, init, graphs, z, nu, ni = reference_setup()
-    core = SmoreShard(graphs, nu, ni, 4, 1, TorchSmoreBackend(), Comm())
-    m = param_container(init, CFG, core.own_u)
+    core = SmoreShard(graphs, nu, ni, 4, 1, TorchSmoreBackend(), Comm(), item_shard=item_shard)
+    assert core.item_shard == item_shard
+    m = param_container(init, CFG, core.own_u, item_range=core.own_i if item_shard else None)
     inter = rank_batches(z, nu, world)[rank].clone()
     inter[0] -= core.own_u[0]  # local user rows
     return core, m, inter
 
 
-def _worker(rank, world, port, out):
-    core, m, inter = _setup_rank(rank, world, port)
+def _sharded_names(item_shard):
+    from rsx.smore_dist import ITEM_SHARDED, SHARDED
+
+    return set(SHARDED) | (set(ITEM_SHARDED) if item_shard else set())
+
+
+def _worker(rank, world, port, out, item_shard=False):
+    core, m, inter = _setup_rank(rank, world, port, item_shard)
     loss = core.loss(m, inter, None)
     loss.backward()
     grads = {n: p.grad.clone().numpy() for n, p in m.named_parameters()}
@@ -195,12 +227,13 @@ def _close(a, b, name, tol=2e-5):
     assert err <= tol * scale, f"{name}: {err:.3g} vs scale {scale:.3g}"
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_sharded_smore_step_matches_single_process(world):
-    from rsx.smore_dist import SHARDED
-
+@pytest.mark.parametrize("world,item_shard", [(2, False), (4, False), (2, True), (4, True)])
+def test_sharded_smore_step_matches_single_process(world, item_shard):
+    """item_shard: the item side (projection, spectral fusion, the gates' inject term)
+    computed on each rank's item rows, the raw feature tables row-sharded with it."""
+    SHARDED = _sharded_names(item_shard)
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(world, _free_port(), d), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, _free_port(), d, item_shard), nprocs=world, join=True)
         res = [dict(np.load(os.path.join(d, f"r{r}.npz"))) for r in range(world)]
     m, _, _, z, nu, ni = reference_setup()
     batches = rank_batches(z, nu, world)
@@ -262,8 +295,8 @@ def _shard_train_batch(core, m, inter, opt, lr, step_id, mg_interval, base=0.5, 
     return value
 
 
-def _mg_worker(rank, world, port, out, steps):
-    core, m, inter = _setup_rank(rank, world, port)
+def _mg_worker(rank, world, port, out, steps, item_shard=False):
+    core, m, inter = _setup_rank(rank, world, port, item_shard)
     opt = torch.optim.Adam(m.parameters(), lr=1e-3)
     losses = [_shard_train_batch(core, m, inter, opt, 1e-3, s + 1, 1) for s in range(steps)]
     params = {n: p.detach().clone().numpy() for n, p in m.named_parameters()}
@@ -287,16 +320,15 @@ class _SumOfBatches:
         return self.m.parameters()
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_sharded_smore_mirror_gradient_matches_single_process(world):
+@pytest.mark.parametrize("world,item_shard", [(2, False), (4, False), (4, True)])
+def test_sharded_smore_mirror_gradient_matches_single_process(world, item_shard):
     """Two batches with the model-level mirror gradient firing on each (mg_interval 1):
     the ranks' losses and every parameter (user rows concatenated over the ranks)
     against the oracle's single-process Trainer batch on the sum of the rank batches."""
-    from rsx.smore_dist import SHARDED
-
+    SHARDED = _sharded_names(item_shard)
     steps = 2
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_mg_worker, args=(world, _free_port(), d, steps), nprocs=world, join=True)
+        mp.spawn(_mg_worker, args=(world, _free_port(), d, steps, item_shard), nprocs=world, join=True)
         res = [dict(np.load(os.path.join(d, f"r{r}.npz"))) for r in range(world)]
     m, _, _, z, nu, ni = reference_setup()
     batches = rank_batches(z, nu, world)
