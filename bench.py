@@ -1001,6 +1001,12 @@ def main():
                          # exact f32 dots for the candidates only, so this is an f32-equivalent rate
                          "kernel_tflops_f32_equivalent": fs_flops / (fs_ms * 1e-3) / 1e12,
                          "screen_bf16_mfma_tflops": 2 * 2.0 * (d + 16) * ni * vu_d.numel() / (fs_ms * 1e-3) / 1e12,
+                         # north_star's "MFMA utilisation for the full-sort GEMM": the MFMA work the
+                         # screened kernel issues (two bf16 passes over every pair) per second over the
+                         # dense bf16 peak; the f32-equivalent rate above is the algorithm's, not the
+                         # matrix cores' (the kernel is issue-bound on its selection work)
+                         "mfma_util": 2 * 2.0 * (d + 16) * ni * vu_d.numel() / (fs_ms * 1e-3) / 1e12 / 2516.6,
+                         "mfma_util_note": "bf16 MFMA work / kernel time / 2516.6 TF/s dense bf16 peak",
                          "mfma_f32_peak_tflops": 157.3, "mfma_bf16_dense_peak_tflops": 2516.6},
             "roofline": roof,
             "roofline_kernels": kernels,

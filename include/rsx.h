@@ -588,14 +588,19 @@ int rsx_smore_pref(int32_t backward, const float* const* W, const float* const* 
  *   backward: g_all / g_side / g_content_in (gradient of content_out, optional) are
  *            compact; g_content / g_image / g_text / g_fusion are full [N, d] tables
  *            the row gradients are ADDED into (zero them first); hv / ht / dz compact.
+ *            With `occ` ([rsx_smore_pref_rows_occ_floats(n, d)] scratch, backward only)
+ *            no float atomics: the row gradients are written per occurrence and each
+ *            table row of `rows` is SET to their sum in a fixed order (deterministic run
+ *            to run); the other rows are untouched (zero them first).
  */
 int rsx_smore_pref_rows(int32_t backward, const float* const* W, const float* const* b, const float* content,
                         const float* image_emb, const float* text_emb, const float* fusion_emb, const int64_t* rows,
                         int64_t n, int32_t d, float p_drop, const int64_t* seed_dev, float* all_out,
                         float* side_out, float* content_out, float* fusion_out, const float* g_all,
                         const float* g_side, const float* g_content_in, float* g_content, float* g_image,
-                        float* g_text, float* g_fusion, float* hv, float* ht, float* const* dz,
+                        float* g_text, float* g_fusion, float* hv, float* ht, float* const* dz, float* occ,
                         rsx_stream_t stream);
+size_t rsx_smore_pref_rows_occ_floats(int64_t n, int32_t d);
 /*
  * dW[p] = dz[p]^T x[p] ([d, d]) and db[p] = colsum(dz[p]) (db[p] may be NULL) for up to
  * 8 pairs of [n, d] row sets: row-split partials + one ordered reduction.

@@ -503,7 +503,15 @@ struct PrefArgs {
     float* c_out;            // forward: the gathered content / fusion rows (optional)
     float* fe_out;
     const float* g_cin;      // backward: gradient of c_out (optional), added into gC
+    // backward (batch rows, optional): [kOcc][n][D] per-occurrence row gradients instead of
+    // float atomics into the tables; pref_segsum then sums them per table row in a fixed order
+    float* occ;
 };
+
+// the per-occurrence slots of pref_bwd_rows (occ): the three gC shares (parts 0, 3, 4),
+// the three gFE shares (parts 0, 1, 2), gIE, gTE
+constexpr int kOccC0 = 0, kOccC3 = 1, kOccC4 = 2, kOccF0 = 3, kOccF1 = 4, kOccF2 = 5, kOccI = 6, kOccT = 7,
+              kOcc = 8;
 
 // the table row of logical row r (r < 0: none)
 __device__ __forceinline__ int64_t src_row(const PrefArgs& a, int64_t r) { return (r >= 0 && a.rows) ? a.rows[r] : r; }
@@ -524,6 +532,15 @@ __device__ __forceinline__ void fatomic(float* Y, int64_t row, int g, const Fld<
     for (int t = 0; t < D / 16; ++t)
 #pragma unroll
         for (int r = 0; r < 4; ++r) unsafeAtomicAdd(Y + row * D + 16 * t + 4 * g + r, x.f[t][r]);
+}
+
+// a row gradient of logical row `out` (table row `row`): into the per-occurrence slot, or
+// added into the table
+template <int D>
+__device__ __forceinline__ void radd(const PrefArgs& a, int slot, float* Y, int64_t row, int64_t out, int g,
+                                     const Fld<D>& x) {
+    if (a.occ) fstore<D>(a.occ + (int64_t)slot * a.n * D, out, g, x);
+    else fatomic<D>(Y, row, g, x);
 }
 
 template <int D>
@@ -725,10 +742,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
         const Fld<D> dz = fmap2<D>(dp, sf, sig_bwd);
         fstore<D>(a.dz[kWfp], out, g, dz);
         const Fld<D> fp = a.p_drop > 0.f ? fmap2<D>(sf, mf, mul) : sf;
-        fatomic<D>(a.gFE, row, g, fmap2<D>(g1, fp, mul));
+        radd<D>(a, kOccF0, a.gFE, row, out, g, fmap2<D>(g1, fp, mul));
         const Fld<D> gA = fload<D>(a.g_all, out, g);
         const Fld<D> gC = a.g_cin ? fmap2<D>(gA, fload<D>(a.g_cin, out, g), add) : gA;
-        fatomic<D>(a.gC, row, g, fmap2<D>(gC, mvt_p<D, kLd<D>>(W, dz, lane), add));
+        radd<D>(a, kOccC0, a.gC, row, out, g, fmap2<D>(gC, mvt_p<D, kLd<D>>(W, dz, lane), add));
         return;
     }
     // parts 1 / 2: the image / text view's query chain (d IE / d TE, d FE); parts 3 / 4 the
@@ -753,12 +770,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
         if (a.p_drop > 0.f) dpp = fmap2<D>(dpp, mp, mul);
         const Fld<D> dzp = fmap2<D>(dpp, sp, sig_bwd);
         fstore<D>(a.dz[wp], out, g, dzp);
-        fatomic<D>(a.gC, row, g, mvt_p<D, kLd<D>>(stage_w<D>(wl, a.W[wp]), dzp, lane));
+        radd<D>(a, v ? kOccC4 : kOccC3, a.gC, row, out, g, mvt_p<D, kLd<D>>(stage_w<D>(wl, a.W[wp]), dzp, lane));
         return;
     }
     const Fld<D> pp = a.p_drop > 0.f ? fmap2<D>(sp, mp, mul) : sp;
     Fld<D> da = fmap2<D>(g1, pp, mul);  // d (s * E)
-    fatomic<D>(v ? a.gTE : a.gIE, row, g, fmap2<D>(da, s, mul));
+    radd<D>(a, v ? kOccT : kOccI, v ? a.gTE : a.gIE, row, out, g, fmap2<D>(da, s, mul));
     da = fmap2<D>(da, fload<D>(v ? a.TE : a.IE, row, g), mul);  // d softmax output
     const float dot = rsum<D>(fmap2<D>(da, s, mul));
     const Fld<D> dq = fmap2<D>(s, da, [&](float y, float gy) { return y * (gy - dot); });
@@ -767,7 +784,57 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
     const Fld<D> h = fload<D>(v ? a.ht : a.hv, out, g);  // this lane's own store above
     const Fld<D> dz1 = fmap2<D>(dh, h, [](float gy, float y) { return gy * (1.f - y * y); });
     fstore<D>(a.dz[w1], out, g, dz1);
-    fatomic<D>(a.gFE, row, g, mvt_p<D, kLd<D>>(stage_w<D>(wl, a.W[w1]), dz1, lane));
+    radd<D>(a, v ? kOccF2 : kOccF1, a.gFE, row, out, g, mvt_p<D, kLd<D>>(stage_w<D>(wl, a.W[w1]), dz1, lane));
+}
+
+// The per-occurrence row gradients of pref_bwd_rows summed per table row, deterministic:
+// one wave per occurrence j; the first occurrence of its row (no earlier j' with the same
+// row: a ballot scan) sums every occurrence of the row in ascending order, each
+// occurrence's shares in slot order, and stores the row of gC / gIE / gTE / gFE.  The
+// rows array is 3B entries (L2 resident); a leader's scan is n / 64 ballots.
+template <int D>
+__global__ __launch_bounds__(256) void pref_segsum(const int64_t* __restrict__ rows, int64_t n,
+                                                   const float* __restrict__ occ, float* __restrict__ gC,
+                                                   float* __restrict__ gIE, float* __restrict__ gTE,
+                                                   float* __restrict__ gFE) {
+    constexpr int PL = D / 64;  // columns per lane: lane + 64 p
+    const int lane = threadIdx.x & 63;
+    const int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (j >= n) return;
+    const int64_t x = rows[j];
+    for (int64_t c = 0; c < j; c += 64) {
+        const int64_t k = c + lane;
+        if (__ballot(k < j && rows[k] == x)) return;  // an earlier occurrence leads
+    }
+    const int64_t sl = n * D;
+    float aC[PL], aF[PL], aI[PL], aT[PL];
+#pragma unroll
+    for (int p = 0; p < PL; ++p) aC[p] = aF[p] = aI[p] = aT[p] = 0.f;
+    for (int64_t c = j; c < n; c += 64) {
+        const int64_t k = c + lane;
+        uint64_t m = __ballot(k < n && rows[k] == x);
+        while (m) {
+            const int b = __builtin_ctzll(m);
+            m &= m - 1;
+            const float* o = occ + (c + b) * D + lane;
+#pragma unroll
+            for (int p = 0; p < PL; ++p) {
+                const int64_t q = 64 * p;
+                aC[p] = ((aC[p] + o[kOccC0 * sl + q]) + o[kOccC3 * sl + q]) + o[kOccC4 * sl + q];
+                aF[p] = ((aF[p] + o[kOccF0 * sl + q]) + o[kOccF1 * sl + q]) + o[kOccF2 * sl + q];
+                aI[p] += o[kOccI * sl + q];
+                aT[p] += o[kOccT * sl + q];
+            }
+        }
+    }
+#pragma unroll
+    for (int p = 0; p < PL; ++p) {
+        const int64_t col = x * D + lane + 64 * p;
+        gC[col] = aC[p];
+        gFE[col] = aF[p];
+        gIE[col] = aI[p];
+        gTE[col] = aT[p];
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1572,7 +1639,7 @@ int rsx_smore_pref(int32_t backward, const float* const* W, const float* const* 
                    float* hv, float* ht, float* const* dz, rsx_stream_t stream) {
     return rsx_smore_pref_rows(backward, W, b, content, image_emb, text_emb, fusion_emb, nullptr, n, d, p_drop,
                                seed_dev, all_out, side_out, nullptr, nullptr, g_all, g_side, nullptr, g_content,
-                               g_image, g_text, g_fusion, hv, ht, dz, stream);
+                               g_image, g_text, g_fusion, hv, ht, dz, nullptr, stream);
 }
 
 int rsx_smore_pref_rows(int32_t backward, const float* const* W, const float* const* b, const float* content,
@@ -1580,9 +1647,10 @@ int rsx_smore_pref_rows(int32_t backward, const float* const* W, const float* co
                         int64_t n, int32_t d, float p_drop, const int64_t* seed_dev, float* all_out,
                         float* side_out, float* content_out, float* fusion_out, const float* g_all,
                         const float* g_side, const float* g_content_in, float* g_content, float* g_image,
-                        float* g_text, float* g_fusion, float* hv, float* ht, float* const* dz,
+                        float* g_text, float* g_fusion, float* hv, float* ht, float* const* dz, float* occ,
                         rsx_stream_t stream) {
     if (n < 0 || !W || !b || !content || !image_emb || !text_emb || !fusion_emb) return RSX_ERR_ARG;
+    if (occ && (!backward || !rows)) return RSX_ERR_ARG;
     if (p_drop < 0.f || p_drop >= 1.f || (p_drop > 0.f && !seed_dev)) return RSX_ERR_ARG;
     if (n == 0) return RSX_OK;
     sf::PrefArgs a{};
@@ -1619,6 +1687,7 @@ int rsx_smore_pref_rows(int32_t backward, const float* const* W, const float* co
     a.c_out = backward ? nullptr : content_out;
     a.fe_out = backward ? nullptr : fusion_out;
     a.g_cin = backward ? g_content_in : nullptr;
+    a.occ = occ;
     // batch-row backward: the three views' chains as three block rows (gradients are atomics
     // there); batch-row forward with the scratch hv: likewise, then pref_combine
     const bool split_fwd = !backward && rows && hv;
@@ -1647,8 +1716,15 @@ int rsx_smore_pref_rows(int32_t backward, const float* const* W, const float* co
             break;
         default: return RSX_ERR_UNSUPPORTED;
     }
+    if (occ) {  // the per-occurrence rows summed per table row (deterministic)
+        const dim3 sg((unsigned)((n + 3) / 4));
+        if (d == 64) hipLaunchKernelGGL(sf::pref_segsum<64>, sg, dim3(256), 0, s, rows, n, occ, g_content, g_image, g_text, g_fusion);
+        else hipLaunchKernelGGL(sf::pref_segsum<128>, sg, dim3(256), 0, s, rows, n, occ, g_content, g_image, g_text, g_fusion);
+    }
     return last_rc();
 }
+
+size_t rsx_smore_pref_rows_occ_floats(int64_t n, int32_t d) { return (size_t)sf::kOcc * (size_t)n * (size_t)d; }
 
 size_t rsx_smore_wgrad_ws_bytes(int64_t n, int32_t d, int32_t n_pairs) {
     const int64_t rows = sf::wg_rows(n, d, n_pairs);

@@ -156,8 +156,9 @@ def preference(model, content, image_embeds, text_embeds, fusion_embeds, seed):
 
 class _PrefRows(torch.autograd.Function):
     """The preference block on the batch rows `rows` (int64 [n], may repeat): from the
-    full content / view tables to compact (all, side, content) rows; the backward adds
-    the row gradients into full zero tables (rsx_smore_pref_rows)."""
+    full content / view tables to compact (all, side, content) rows; the backward writes
+    the row gradients per occurrence and sums them per table row in a fixed order into
+    full zero tables (rsx_smore_pref_rows with occ: deterministic, no float atomics)."""
 
     @staticmethod
     def forward(ctx, C_, IE, TE, FE, rows, p_drop, seed, *wb):
@@ -169,7 +170,7 @@ class _PrefRows(torch.autograd.Function):
         all_, side, c_rows, f_rows, x2 = out.unbind(0)  # x2: the split forward's scratch
         L.check(L.lib().rsx_smore_pref_rows(0, _arr(W), _arr(b), _p(C_), _p(IE), _p(TE), _p(FE), _p(rows), n, d,
                                             float(p_drop), _p(seed), _p(all_), _p(side), _p(c_rows), _p(f_rows),
-                                            None, None, None, None, None, None, None, _p(x2), None, None,
+                                            None, None, None, None, None, None, None, _p(x2), None, None, None,
                                             ops._stream()), "rsx_smore_pref_rows")
         ctx.save_for_backward(C_, IE, TE, FE, rows, seed, c_rows, f_rows, *W,
                               *[x if x is not None else torch.empty(0) for x in b])
@@ -191,12 +192,15 @@ class _PrefRows(torch.autograd.Function):
         g_crows = None if g_crows is None else _c(g_crows)
         gfull = torch.zeros(4, *C_.shape, dtype=torch.float32, device=C_.device)
         gC, gIE, gTE, gFE = gfull.unbind(0)
-        scratch = torch.empty(9, n, d, dtype=torch.float32, device=C_.device)
-        hv, ht, *dz = scratch.unbind(0)
+        # hv, ht, dz[7] and the per-occurrence row gradients (deterministic sums, no atomics)
+        occ_n = int(L.lib().rsx_smore_pref_rows_occ_floats(n, d))
+        scratch = torch.empty(9 * n * d + occ_n, dtype=torch.float32, device=C_.device)
+        hv, ht, *dz = scratch[: 9 * n * d].view(9, n, d).unbind(0)
+        occ = scratch[9 * n * d:]
         L.check(L.lib().rsx_smore_pref_rows(1, _arr(W), _arr(b), _p(C_), _p(IE), _p(TE), _p(FE), _p(rows), n, d,
                                             ctx.p_drop, _p(seed), None, None, None, None, _p(g_all), _p(g_side),
                                             _p(g_crows), _p(gC), _p(gIE), _p(gTE), _p(gFE), _p(hv), _p(ht),
-                                            _arr(dz), ops._stream()), "rsx_smore_pref_rows")
+                                            _arr(dz), _p(occ), ops._stream()), "rsx_smore_pref_rows")
         xs = [f_rows, hv, f_rows, ht, c_rows, c_rows, c_rows]
         grads = _wgrad([(dz[i], xs[i], ctx.has_b[i]) for i in range(7)], d, C_.device)
         gW = [g[0] for g in grads]

@@ -64,17 +64,23 @@ def _worker(rank, world, port, root, out):
     step0 = m.engine.step
 
     def spy(triplets=None, epoch=0, start=0):
-        seen.append((epoch, start))
+        seen.append(triplets[:2].cpu().numpy().copy())
         return step0(triplets=triplets, epoch=epoch, start=start)
 
     m.engine.step = spy
     losses = []
+    inter = np.stack([m.engine.sampler.inter_u.cpu().numpy(), m.engine.sampler.inter_i.cpu().numpy()])
     for epoch in range(2):
+        seen.clear()
         loss, n = t._train_epoch(train, epoch)
         assert not torch.is_tensor(loss) and n == m.steps_per_epoch
         losses.append(loss)
         t._epoch_for_lr += 1
-    assert seen == [(e, i * Bm) for e in range(2) for i in range(m.steps_per_epoch)]
+        # the common step count, balanced slices (sizes within one), each interaction once
+        sizes = [x.shape[1] for x in seen]
+        assert len(seen) == m.steps_per_epoch and max(sizes) - min(sizes) <= 1 and max(sizes) <= Bm
+        got = np.concatenate(seen, axis=1)
+        assert sorted(map(tuple, got.T.tolist())) == sorted(map(tuple, inter.T.tolist()))
     vres = t.evaluate(valid)
     f = m._final().cpu()
     a, b = m.user_range

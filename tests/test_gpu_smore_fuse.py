@@ -129,6 +129,47 @@ def test_preference_vs_torch(cuda, d, n, p):
     _close(ea, m.ref(C_, IE, TE, FE, None)[0], "eval all")
 
 
+@pytest.mark.parametrize("d,N,n,p", [(64, 3000, 6144, 0.0), (128, 5000, 6144, 0.1), (128, 700, 999, 0.0)])
+def test_preference_rows_vs_torch_and_deterministic(cuda, d, N, n, p):
+    """The batch-row preference block (rsx_smore_pref_rows with per-occurrence row
+    gradients + pref_segsum): repeated rows (a batch's popular items), gradients of the
+    full tables vs torch autograd of the gathered rows (1e-4 of scale), and bit-identical
+    gradients on a second run (no float atomics: a fixed summation order per row)."""
+    from rsx import smore_fuse as SF
+
+    gen = torch.Generator().manual_seed(d + n)
+    mk = lambda: torch.randn(N, d, generator=gen).to(cuda).requires_grad_()  # noqa: E731
+    C_, IE, TE, FE = mk(), mk(), mk(), mk()
+    m = _PrefModel(d, gen, cuda, p).train()
+    hot = torch.randint(0, 40, (n // 3,), generator=gen)  # heavy repeats
+    rows = torch.cat([hot, torch.randint(0, N, (n - n // 3,), generator=gen)])[torch.randperm(n, generator=gen)]
+    rows = rows.to(cuda)
+    seed = torch.tensor([777], dtype=torch.int64, device=cuda)
+    up = [torch.randn(n, d, generator=gen).to(cuda) for _ in range(3)]
+    params = [C_, IE, TE, FE] + list(m.parameters())
+
+    def run():
+        a, s_, c = SF.preference_rows(m, C_, IE, TE, FE, rows, seed)
+        return a, s_, c, torch.autograd.grad((a * up[0]).sum() + (s_ * up[1]).sum() + (c * up[2]).sum(), params)
+
+    ga, gs, gc, gg = run()
+    masks = None
+    if p > 0:  # the kernel's dropout key is the table row
+        full = [torch.from_numpy(_drop_mask_np(777, k, N, d, p)).to(cuda) for k in range(3)]
+        masks = [x[rows] for x in full]
+    wa, ws = m.ref(C_[rows], IE[rows], TE[rows], FE[rows], masks)
+    wc = C_[rows]
+    wg = torch.autograd.grad((wa * up[0]).sum() + (ws * up[1]).sum() + (wc * up[2]).sum(), params)
+    _close(ga, wa, "all")
+    _close(gs, ws, "side")
+    names = ["content", "image", "text", "fusion"] + [k for k, _ in m.named_parameters()]
+    for name, a, b in zip(names, gg, wg):
+        _close(a, b, name)
+    _, _, _, gg2 = run()
+    for name, a, b in zip(names[:4], gg, gg2):
+        assert torch.equal(a, b), name  # the table gradients: bit-stable run to run
+
+
 def test_view_prop_vs_torch(cuda):
     from rsx import smore_fuse as SF
     from rsx.smore import _DevGraph
