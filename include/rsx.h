@@ -823,6 +823,11 @@ double rsx_comm_sim_seconds(rsx_comm_t comm, int32_t op, double bytes);
 /* buf[0, n) := sum over ranks, in place, ordered after the work queued on `stream`
  * and before the work queued on it afterwards. */
 int rsx_comm_allreduce_f32(rsx_comm_t comm, float* buf, int64_t n, rsx_stream_t stream);
+/* The same all-reduce without the wait: the caller's stream goes on (work that does not
+ * read buf overlaps the exchange) until rsx_comm_wait(comm, stream), which orders the
+ * stream after the last started all-reduce (one in flight per communicator). */
+int rsx_comm_allreduce_f32_start(rsx_comm_t comm, float* buf, int64_t n, rsx_stream_t stream);
+int rsx_comm_wait(rsx_comm_t comm, rsx_stream_t stream);
 /* buf[r n, (r+1) n) := rank r's slice for every rank r (buf holds world * n floats), in
  * place, stream-ordered as above. */
 int rsx_comm_allgather_f32(rsx_comm_t comm, float* buf, int64_t n, rsx_stream_t stream);

@@ -90,6 +90,7 @@ struct rsx_comm_s {
     // latency-injected one-rank communicator (rsx_comm_init_sim): every collective is the
     // identity on the data (world 1) and a comm-stream kernel that holds `sim_blocks`
     // workgroups and streams the collective's HBM bytes for the modelled time at sim_world
+    hipEvent_t pending = nullptr;  // the join event of the last rsx_comm_allreduce_f32_start
     int32_t sim_world = 0;
     double sim_busbw = 0.0;   // bytes/s per rank, the model's bus bandwidth at sim_world
     double sim_lat = 0.0;     // seconds per collective
@@ -860,6 +861,23 @@ int rsx_comm_allreduce_f32(rsx_comm_t c, float* buf, int64_t n, rsx_stream_t str
     hipEvent_t j = rsx::exchange(c, buf, n, s, &rc);
     if (!j) return rc;
     return rsx::wait(s, j);
+}
+
+int rsx_comm_allreduce_f32_start(rsx_comm_t c, float* buf, int64_t n, rsx_stream_t stream) {
+    if (!c || (!buf && n > 0) || n < 0) return RSX_ERR_ARG;
+    int rc = 0;
+    hipEvent_t j = rsx::exchange(c, buf, n, rsx::as_stream(stream), &rc);
+    if (!j) return rc;
+    c->pending = j;
+    return RSX_OK;
+}
+
+int rsx_comm_wait(rsx_comm_t c, rsx_stream_t stream) {
+    if (!c) return RSX_ERR_ARG;
+    if (!c->pending) return RSX_OK;
+    const int rc = rsx::wait(rsx::as_stream(stream), c->pending);
+    c->pending = nullptr;
+    return rc;
 }
 
 int rsx_comm_allgather_f32(rsx_comm_t c, float* buf, int64_t count, rsx_stream_t stream) {

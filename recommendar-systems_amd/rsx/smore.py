@@ -570,7 +570,13 @@ class SMORE(GeneralRecommender):
         item side's backward.  Both are latency-bound chains of mid-size launches, and
         in a captured step the two streams become parallel branches of the HIP graph.
         RSX_SMORE_STREAMS=0 keeps everything on one stream."""
-        item_id = self.item_id_embedding.weight
+        # the leaves enter the graph through views made on THIS stream, so every leaf has one
+        # consumer on one stream: its AccumulateGrad runs on the stream of the node that
+        # produces its gradient (a leaf read on both streams had its accumulator bound to
+        # the side stream while the gates' backward fed it from this one: torch's
+        # AccumulateGrad stream-mismatch warning, and a cross-stream sync per backward)
+        item_id = self.item_id_embedding.weight.view_as(self.item_id_embedding.weight)
+        user_w = self.user_embedding.weight.view_as(self.user_embedding.weight)
         main = torch.cuda.current_stream()
         side = self._side_stream()
         if side is not None:
@@ -578,7 +584,7 @@ class SMORE(GeneralRecommender):
             if rows is not None:
                 rows.record_stream(side)  # made on this stream, read on the side stream (also in the backward)
         with torch.cuda.stream(side) if side is not None else _nullctx():
-            ego = torch.cat([self.user_embedding.weight, item_id], dim=0)
+            ego = torch.cat([user_w, item_id], dim=0)
             if rows is not None and 1 <= self.n_ui_layers <= 4:
                 if self._tags is None:
                     self._tags = _RowTags(self.n_users + self.n_items, self.device)

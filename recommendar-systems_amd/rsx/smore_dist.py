@@ -111,6 +111,23 @@ class Comm:
             t.copy_(h)
         return t
 
+    def allreduce_start_(self, t: torch.Tensor):
+        """allreduce_ without the wait (RCCL: on the communicator's stream; the caller's
+        stream runs on until wait()); host collectives are synchronous."""
+        if self.world == 1:
+            return t
+        if self.handle is not None:
+            if t.dtype != torch.float32 or not t.is_contiguous():
+                raise RuntimeError("Comm.allreduce_start_: contiguous float32 tensors")
+            L.check(L.lib().rsx_comm_allreduce_f32_start(self.handle, t.data_ptr(), t.numel(), ops._stream()),
+                    "rsx_comm_allreduce_f32_start")
+            return t
+        return self.allreduce_(t)
+
+    def wait(self):
+        if self.handle is not None:
+            L.check(L.lib().rsx_comm_wait(self.handle, ops._stream()), "rsx_comm_wait")
+
     def allgather_(self, t: torch.Tensor, count: int) -> torch.Tensor:
         """t[r count:(r+1) count] := rank r's slice, every r (t: world * count floats)."""
         if self.world == 1:
@@ -277,14 +294,18 @@ class HipSmoreBackend:
         for k in range(1, K + 1):
             y = bufs[k & 1]
             s_in = x if k == 1 else s
-            # item partial = A_I users^{k-1}, summed over the ranks
+            # item partial = A_I users^{k-1}, summed over the ranks; the exchange runs on the
+            # communicator's stream while this layer's user rows (they read the previous
+            # layer's items only) are computed
             core.A_I.spmm_epi(cur[:nu], ops.epi(L.RSX_EPI_STORE, y=y[nu:]), d)
-            core.comm.allreduce_(y[nu:])
+            core.comm.allreduce_start_(y[nu:])
             if k < K:
                 core.A_U.spmm_epi(cur[nu:], ops.epi(L.RSX_EPI_LAYERSUM, y=y[:nu], s_in=s_in[:nu], s_out=s[:nu]), d)
+                core.comm.wait()
                 ops.rowwise(ni, d, ops.epi(L.RSX_EPI_ADD, y=s[nu:], s_in=s_in[nu:], r_add=y[nu:]))
             else:
                 core.A_U.spmm_epi(cur[nu:], ops.epi(L.RSX_EPI_FINAL, beta=beta, f=out[:nu], s_in=s_in[:nu]), d)
+                core.comm.wait()
                 ops.rowwise(ni, d, ops.epi(L.RSX_EPI_ADD, beta=beta, y=out[nu:], s_in=s_in[nu:], r_add=y[nu:]))
             cur = y
         if K == 0:
@@ -303,7 +324,7 @@ class HipSmoreBackend:
 
         return SF.gates(cv, ct, cf, item, m.gate_v, m.gate_t, m.gate_f, m.inject_scale, False)
 
-    def item_side_sharded(self, core, m):
+    def item_side_sharded(self, core, m, item):
         """Projection -> spectral -> the gates' inject term on this rank's item rows only
         (the fused kernels on n_own rows), gathered once; + the replicated item-id table."""
         from . import smore_fuse as SF
@@ -319,7 +340,7 @@ class HipSmoreBackend:
                                      w["gate_t.0.bias"], w["gate_f.0.weight"], w["gate_f.0.bias"],
                                      float(m.inject_scale), False)
         D = gather_rows(core.comm, core.iq, core.n_items, dv, dt, df)
-        return (D + m.item_id_embedding.weight.unsqueeze(0)).unbind(0)
+        return (D + item.unsqueeze(0)).unbind(0)
 
     def views(self, core, xs):
         from . import smore_fuse as SF
@@ -403,11 +424,12 @@ class SmoreShard:
             self._zero = torch.zeros_like(like)
         return self._zero
 
-    def _item_side(self, m):
+    def _item_side(self, m, item=None):
+        item = m.item_id_embedding.weight if item is None else item
         if self.item_shard:
-            return self.be.item_side_sharded(self, m)
+            return self.be.item_side_sharded(self, m, item)
         cv, ct, cf = self.be.spectral(m)
-        return self.be.gates(m, cv, ct, cf, m.item_id_embedding.weight)
+        return self.be.gates(m, cv, ct, cf, item)
 
     def _content_views(self, m):
         """The UI backbone (with its per-layer all-reduces) on a side stream of the HIP
@@ -416,12 +438,15 @@ class SmoreShard:
         autograd runs on the same streams)."""
         side = self.be.side_stream() if hasattr(self.be, "side_stream") else None
         main = torch.cuda.current_stream() if side is not None else None
+        # every leaf enters through a view made here, on one stream (rsx.smore._views_fused)
+        uw = m.user_embedding.weight.view_as(m.user_embedding.weight)
+        iw = m.item_id_embedding.weight.view_as(m.item_id_embedding.weight)
         if side is not None:
             side.wait_stream(main)
         with torch.cuda.stream(side) if side is not None else _Null():
-            ego = torch.cat([m.user_embedding.weight, m.item_id_embedding.weight])
+            ego = torch.cat([uw, iw])
             content = _UIProp.apply(ego, self)
-        img, txt, fus = self._item_side(m)
+        img, txt, fus = self._item_side(m, iw)
         if side is not None:
             main.wait_stream(side)
             content.record_stream(main)

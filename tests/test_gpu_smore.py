@@ -213,6 +213,34 @@ def test_smore_one_epoch_with_mirror_gradient(tmp_path, golden, fx):
             assert abs(res[k] - ref[k]) <= 1e-4 + 1e-12, (tag, k, res[k], ref[k])
 
 
+@pytest.mark.parametrize("graph", [True, False])
+def test_smore_training_emits_no_accumulate_grad_stream_warning(tmp_path, golden, graph):
+    """Two epochs of SMORE batches (the UI backbone on its side stream; eager, captured
+    and replayed batches) raise no warning from torch's autograd engine: in particular
+    not the AccumulateGrad stream-mismatch one (a leaf's gradient produced on another
+    stream than its accumulator's, an extra cross-stream sync per backward)."""
+    import warnings
+
+    from rsx.trainer import Trainer
+
+    z, c, train, valid, test = _setup(tmp_path, golden)
+    c["rsx_graph_step"] = graph
+    m = _model(c, train)
+    t = Trainer(c, m)
+    torch.autograd.graph.set_warn_on_accumulate_grad_stream_mismatch(True)
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        for ep in range(2):
+            m.pre_epoch_processing()
+            loss, _ = t._train_epoch(train, ep)
+            assert not torch.is_tensor(loss)
+        torch.cuda.synchronize()
+    bad = [str(x.message)[:160] for x in w if "AccumulateGrad" in str(x.message) or "stream" in str(x.message)]
+    assert not bad, bad
+    if graph:
+        assert t._graph is not None and t._graph.replays > 0
+
+
 def test_smore_two_losses_before_one_backward(tmp_path, golden):
     """calculate_loss twice (two batches) and ONE backward of their sum = the two
     backwards one at a time: the batch-row propagation re-tags its forward's rows in its

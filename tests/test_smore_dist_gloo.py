@@ -72,7 +72,7 @@ class TorchSmoreBackend:
                 torch.fft.irfft(ft * unit(m.text_complex_weight), n=n, dim=1, norm="ortho"),
                 torch.fft.irfft(ft * fi * unit(m.fusion_complex_weight), n=n, dim=1, norm="ortho"))
 
-    def item_side_sharded(self, core, m):
+    def item_side_sharded(self, core, m, item):
         """The item side on this rank's item rows (m's feature tables hold them), the inject
         terms gathered (rsx.smore_dist.gather_rows) and added to the replicated item table."""
         from rsx.smore_dist import ITEM_W, allreduce_grad, gather_rows
@@ -95,7 +95,7 @@ class TorchSmoreBackend:
                         s * torch.sigmoid(F.linear(cv, w["gate_v.0.weight"], w["gate_v.0.bias"])),
                         s * torch.sigmoid(F.linear(ct, w["gate_t.0.weight"], w["gate_t.0.bias"])),
                         s * torch.sigmoid(F.linear(cf, w["gate_f.0.weight"], w["gate_f.0.bias"])))
-        return (D + m.item_id_embedding.weight.unsqueeze(0)).unbind(0)
+        return (D + item.unsqueeze(0)).unbind(0)
 
     def gates(self, m, cv, ct, cf, item):
         return (item + m.inject_scale * m.gate_v(cv), item + m.inject_scale * m.gate_t(ct),
