@@ -382,6 +382,13 @@ int sharded_stored_layers(const rsx_sharded_lgcn_step& st, bool train, hipStream
             hipLaunchKernelGGL(tag_rows_k, dim3((unsigned)((nU + 255) / 256)), dim3(256), 0, s, st.union_items, nU,
                                st.item_tag, st.tag_dev, tag);
             RSX_TRY(last_rc());
+            // the union items in row_tag's item block as well: after the compact exchange G'_I
+            // is nonzero exactly there, so the first backward user-row product gathers only
+            // those item rows (RSX_TAG_SPARSE_X) -- the item block of row_tag is read by no
+            // other product of this step (its user block holds this rank's batch users)
+            hipLaunchKernelGGL(tag_rows_k, dim3((unsigned)((nU + 255) / 256)), dim3(256), 0, s, st.union_items, nU,
+                               st.row_tag + nu, st.tag_dev, tag);
+            RSX_TRY(last_rc());
             e.row_tag = st.item_tag;
             e.tag = tag;
             e.tag_dev = st.tag_dev;
@@ -455,7 +462,8 @@ int sharded_stored_layers(const rsx_sharded_lgcn_step& st, bool train, hipStream
         u.row_tag = st.row_tag;
         u.tag = tag;
         u.tag_dev = st.tag_dev;
-        u.tag_flags = RSX_TAG_SPARSE_S;
+        // k = 1, sparse schedule: X = G' whose item rows are nonzero on the union items only
+        u.tag_flags = RSX_TAG_SPARSE_S | (k == 1 && sparse ? RSX_TAG_SPARSE_X : 0);
         RSX_TRY(spmm_dispatch(*st.adj_u, x, d, u, st.slab_u, s));
         x = bufs[k - 1];
     }
