@@ -635,6 +635,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D <= 64 ? 2 
 #ifndef RSX_FS_ABUF
 #define RSX_FS_ABUF 2  // fs_screen item-operand buffers at d <= 64 (a ring: loads NB - 1 tiles ahead; 1 at d > 64)
 #endif
+#ifndef RSX_FS_P1PIPE
+#define RSX_FS_P1PIPE 0  // 1: fs_screen pass 1 software-pipelined over two accumulators (A/B variant)
+#endif
 #ifndef RSX_FS_TOP
 #define RSX_FS_TOP 3  // fs_screen pass-1 samples per accumulator slot (2 or 3): 32 * TOP distinct items a user
 #endif
@@ -920,12 +923,16 @@ __device__ __forceinline__ void screen_segment(const FsArgs& a, int64_t ub, int 
     float t1[16], t2[16], t3[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) t1[r] = t2[r] = t3[r] = -INFINITY;
-    auto pass1 = [&](auto form, auto par, int t) __attribute__((always_inline)) {
+    // pass 1 of one tile in two halves: p1_issue (the mask cursor, then the tile's MFMAs)
+    // and p1_update (the missing / masked slots' keys, the per-slot top three)
+    auto p1_issue = [&](auto form, auto par, int t, floatx16& acc) __attribute__((always_inline)) -> unsigned {
         // the mask cursor first: its loads' waits then precede the next tile's prefetch
-        const int64_t tb = i0 + (int64_t)t * 32;
-        const unsigned mb = mask_bits(form, tb);
-        floatx16 acc;
+        const unsigned mb = mask_bits(form, i0 + (int64_t)t * 32);
         tile(par, t, acc);
+        return mb;
+    };
+    auto p1_update = [&](auto form, int t, floatx16& acc, unsigned mb) __attribute__((always_inline)) {
+        const int64_t tb = i0 + (int64_t)t * 32;
         const int rem = (int)(i1 - tb);
         // a tile with a missing item (the chunk's last) or, outside the mask-free form, a
         // masked one: those slots first take their key (-inf / -1e10) in place, then every
@@ -950,12 +957,74 @@ __device__ __forceinline__ void screen_segment(const FsArgs& a, int64_t ub, int 
             t1[r] = vmax(t1[r], acc[r]);
         }
     };
+    auto pass1 = [&](auto form, auto par, int t) __attribute__((always_inline)) {
+        floatx16 acc;
+        const unsigned mb = p1_issue(form, par, t, acc);
+        p1_update(form, t, acc, mb);
+    };
+    // Software-pipelined pass 1 (NB <= 2): tile t + 1's MFMAs are issued before tile t's
+    // top-three update, into a second accumulator, so the update's VALU fills the matrix
+    // pipe's dependent-MFMA gaps of the same wave instead of following the chain (one
+    // accumulator serialises MFMA chain -> VALU -> next chain: ~48 VALU per tile behind
+    // 5 dependent MFMAs).  Same tiles, same order of updates: the same samples.
+    auto sweep1 = [&](auto form) __attribute__((always_inline)) {
+        // the mask-free form of the two-phase pass-1 kernel at d <= 64 (the other forms and
+        // kernels would spill past the two-waves-per-SIMD register budget)
+        if constexpr (RSX_FS_P1PIPE && NB <= 2 && decltype(form)::value == 0 && PH == 1 && D <= 64) {
+            if (ntiles <= 0) return;
+            // every tile but the segment's last is full: the loop's tiles take the top-three
+            // update with no masking (one basic block: the next tile's MFMAs and this tile's
+            // VALU interleave, one MFMA per ~9 updates); the last tile the masked form
+            auto upd = [&](floatx16& acc) __attribute__((always_inline)) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    if constexpr (RSX_FS_TOP == 3) t3[r] = vmed3(t2[r], t3[r], acc[r]);
+                    t2[r] = vmed3(t1[r], t2[r], acc[r]);
+                    t1[r] = vmax(t1[r], acc[r]);
+                }
+            };
+#define RSX_P1_INTERLEAVE()                                     \
+    do {                                                        \
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);      \
+        __builtin_amdgcn_sched_group_barrier(0x002, 10, 0);     \
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);      \
+        __builtin_amdgcn_sched_group_barrier(0x002, 10, 0);     \
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);      \
+        __builtin_amdgcn_sched_group_barrier(0x002, 10, 0);     \
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);      \
+        __builtin_amdgcn_sched_group_barrier(0x002, 10, 0);     \
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);      \
+        __builtin_amdgcn_sched_group_barrier(0x002, 10, 0);     \
+    } while (0)
+            floatx16 acc0, acc1;
+            unsigned mb0 = p1_issue(form, IntC<0>{}, 0, acc0), mb1 = 0;
+            int t = 0;
+            for (; t + 2 < ntiles; t += 2) {  // tiles t, t + 1 full
+                mb1 = p1_issue(form, IntC<1>{}, t + 1, acc1);
+                upd(acc0);
+                RSX_P1_INTERLEAVE();
+                mb0 = p1_issue(form, IntC<0>{}, t + 2, acc0);
+                upd(acc1);
+                RSX_P1_INTERLEAVE();
+            }
+#undef RSX_P1_INTERLEAVE
+            if (t + 1 < ntiles) {  // tiles t (full) and t + 1 (the last)
+                mb1 = p1_issue(form, IntC<1>{}, t + 1, acc1);
+                upd(acc0);
+                p1_update(form, t + 1, acc1, mb1);
+            } else {
+                p1_update(form, t, acc0, mb0);
+            }
+        } else {
+            sweep([&](auto par, int t) __attribute__((always_inline)) { pass1(form, par, t); });
+        }
+    };
     unsigned th = 0;
     if constexpr (PH != 2) {
         prime();
-        if (mfree) sweep([&](auto par, int t) __attribute__((always_inline)) { pass1(IntC<0>{}, par, t); });
-        else if (mlds_ok) sweep([&](auto par, int t) __attribute__((always_inline)) { pass1(IntC<1>{}, par, t); });
-        else sweep([&](auto par, int t) __attribute__((always_inline)) { pass1(IntC<2>{}, par, t); });
+        if (mfree) sweep1(IntC<0>{});
+        else if (mlds_ok) sweep1(IntC<1>{});
+        else sweep1(IntC<2>{});
         if constexpr (PH == 1) {  // publish the samples; fs_thresh takes L over all the user's segments
             if (uvalid) {
                 // high half of the ordered word (rounding down: a lower bound stays one); -inf
