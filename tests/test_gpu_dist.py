@@ -181,3 +181,60 @@ def test_native_sharded_step_equals_python_sequence(sparse):
         # the graph-replayed native step = the eagerly issued one (up to the BPR atomics' order)
         np.testing.assert_allclose(z[f"graph_{i}"], z[f"True_{i}"], rtol=1e-6, atol=1e-6, err_msg=str(i))
     assert np.isfinite(z["True_1"]).all()
+
+
+def _sim_worker(rank, world, port, out_dir):
+    """The one-rank sharded engine over the latency-injected communicator (RSX_COMM_SIM):
+    every collective is the one-rank identity plus a comm-stream kernel holding the
+    modelled time, so the trained tables equal the plain one-rank engine's and the step
+    takes at least the modelled exchange time."""
+    import time
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    from rsx import _lib as L
+    from rsx.dist import ShardedLightGCNEngine
+
+    torch.manual_seed(7)
+    I0 = torch.nn.init.xavier_uniform_(torch.empty(NI, D)).numpy()
+    U0 = torch.nn.init.xavier_uniform_(torch.empty(NU, D)).numpy()
+    tu, ti, trip = _local_graph(0)
+    out = {}
+    for sim in (None, "4:1.0:200"):  # 4 ranks at 1 GB/s bus bandwidth + 200 us per collective
+        if sim:
+            os.environ["RSX_COMM_SIM"] = sim
+        else:
+            os.environ.pop("RSX_COMM_SIM", None)
+        eng = ShardedLightGCNEngine(tu, ti, NU, NI, D, K, REG, LR, "cuda:0", U0, I0, batch=16, sparse=True)
+        assert (eng.sim is not None) == bool(sim)
+        for s in range(0, 4 * 16, 16):  # eager, eager, captured, replayed
+            eng.step(epoch=0, start=s)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for s in range(4 * 16, 8 * 16, 16):
+            eng.step(epoch=0, start=s)
+        torch.cuda.synchronize()
+        out[f"ms_{bool(sim)}"] = (time.perf_counter() - t0) * 1e3 / 4
+        out[f"p_{bool(sim)}"] = eng.p.cpu().numpy()
+        if sim:
+            X = NI * D * 4.0
+            out["model_ar_ms"] = 1e3 * L.lib().rsx_comm_sim_seconds(eng._comm, L.RSX_COLL_ALLREDUCE, X)
+        eng.close()
+    os.environ.pop("RSX_COMM_SIM", None)
+    np.savez(os.path.join(out_dir, "sim.npz"), **out)
+    dist.destroy_process_group()
+
+
+def test_latency_injected_comm_is_data_identity_and_takes_the_modelled_time():
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_sim_worker, args=(1, _free_port(), d), nprocs=1, join=True)
+        z = dict(np.load(os.path.join(d, "sim.npz")))
+    np.testing.assert_allclose(z["p_True"], z["p_False"], rtol=0, atol=1e-6)
+    # model: 2 (W-1)/W X / busbw + latency for an all-reduce of the item block X
+    X = NI * D * 4.0
+    assert abs(float(z["model_ar_ms"]) - (1e3 * 2 * 0.75 * X / 1e9 + 0.2)) < 1e-6
+    # a K = 3 sparse step issues 4 dense all-reduce-volume collectives + RS + AG + compact
+    # ones: at least the 200 us latency of each of its >= 8 collectives on the comm stream
+    assert float(z["ms_True"]) >= float(z["ms_False"]) + 8 * 0.2 * 0.9, (z["ms_True"], z["ms_False"])
