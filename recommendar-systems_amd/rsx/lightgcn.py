@@ -30,6 +30,10 @@ its interactions exactly once, and the step minimises the sum of the ranks'
 reference losses.
 Evaluation ranks each rank's own evaluation users against all items
 (`full_sort_topk_local`); rsx.trainer all-gathers the metric sums.
+
+Config `rsx_dist: dp` selects the data-parallel engine instead (rsx.dp: the whole graph
+and the tables on every rank, the global batch of every rank's triplets per step, two
+small all-gathers a step), the evaluation users split over the ranks.
 """
 from __future__ import annotations
 
@@ -117,6 +121,10 @@ class LightGCN(GeneralRecommender):
         wd = config["weight_decay"] or 0.0
         world, rank = _world()
         self.sharded = world > 1 or bool(config["rsx_sharded"])
+        self.dp = self.sharded and str(config["rsx_dist"] or "rowshard").lower() == "dp"
+        if self.dp:
+            self._init_dp(config, im, u0, i0, world, rank, float(wd))
+            return
         if self.sharded:
             self._init_sharded(config, im, u0, i0, world, rank, float(wd))
             return
@@ -174,6 +182,25 @@ class LightGCN(GeneralRecommender):
             "item_emb": nn.Parameter(self.engine.p[nl:]),
         })
 
+    def _init_dp(self, config, im, u0, i0, world, rank, wd):
+        """Data-parallel (config rsx_dist: dp, rsx.dp): the whole graph and the tables on
+        every rank, each rank trains its slice of every global batch (the reference
+        objective at batch W * train_batch_size); the replicas stay bit-identical."""
+        from .dp import DataParallelLightGCNEngine
+
+        self.engine = DataParallelLightGCNEngine(
+            im.row.astype(np.int64), im.col.astype(np.int64), self.n_users, self.n_items, self.latent_dim,
+            self.n_layers, self.reg_weight, lr=config["learning_rate"] or 1e-3, device=self.device,
+            user_emb=u0.numpy(), item_emb=i0.numpy(), seed=int(config["seed"] or 0),
+            batch=int(config["train_batch_size"]), chunk=int(config["rsx_chunk"] or 32), weight_decay=wd)
+        self.steps_per_epoch = self.engine.steps_per_epoch()
+        nu = self.n_users
+        self.user_range = (rank * nu // world, (rank + 1) * nu // world)  # this rank's evaluation users
+        self.embedding_dict = nn.ParameterDict({
+            "user_emb": nn.Parameter(self.engine.p[:nu]),
+            "item_emb": nn.Parameter(self.engine.p[nu:]),
+        })
+
     # -- reference API -----------------------------------------------------------
     def train(self, mode: bool = True):
         self.engine.invalidate()
@@ -216,6 +243,9 @@ class LightGCN(GeneralRecommender):
         """Sharded training: this rank's batch i (of steps_per_epoch, the same count on every
         rank) of `epoch` from its device sampler."""
         self.engine.lr = float(lr)
+        if self.dp:
+            self.engine.step_index(epoch, i)
+            return
         self.engine.step_slice(epoch, i, self.steps_per_epoch)
 
     def full_sort_topk_local(self, eval_users: torch.Tensor, k: int, eval_data):
@@ -223,8 +253,13 @@ class LightGCN(GeneralRecommender):
         (global ids in [user_range)), ranked against every item with the training mask."""
         a, b = self.user_range
         pos = torch.nonzero((eval_users >= a) & (eval_users < b)).flatten()
-        local = (eval_users.index_select(0, pos) - a).contiguous()
         f = self._final()
+        if self.dp:  # replicated tables: this rank's slice of the users, global ids
+            nu = self.n_users
+            users = eval_users.index_select(0, pos).contiguous()
+            _, topk = ops.fullsort_topk(f[:nu], users, f[nu:], eval_data.mask_rowptr, eval_data.mask_col, k)
+            return pos, topk
+        local = (eval_users.index_select(0, pos) - a).contiguous()
         nl = b - a
         _, topk = ops.fullsort_topk(f[:nl], local, f[nl:], eval_data.mask_rowptr[a:], eval_data.mask_col, k)
         return pos, topk

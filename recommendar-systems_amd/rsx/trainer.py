@@ -263,9 +263,12 @@ class Trainer:
             for i in range(self.model.steps_per_epoch):
                 self.model.fused_step_index(epoch_idx, i, lr)
                 n += 1
-            tot = acc.clone() if dist.get_backend() == "nccl" else acc.cpu()
-            dist.all_reduce(tot)
-            total = float(tot.item())
+            if getattr(self.model, "dp", False):  # data-parallel: every rank holds the global batches' loss
+                total = float(acc.item())
+            else:
+                tot = acc.clone() if dist.get_backend() == "nccl" else acc.cpu()
+                dist.all_reduce(tot)
+                total = float(tot.item())
         else:
             halt = getattr(self.model, "device_halt", None)
             if halt is not None:

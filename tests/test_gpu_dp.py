@@ -136,3 +136,83 @@ def test_dp_one_rank_rccl_equals_single_gpu_step(k):
     np.testing.assert_allclose(z["pa"], z["pb"], rtol=0, atol=1e-6)
     np.testing.assert_allclose(z["ma"], z["mb"], rtol=0, atol=1e-7)
     assert 512 in z["graphs"].tolist()  # full batches replayed from a captured graph
+
+
+def _trainer_worker(rank, world, port, root, out):
+    """LightGCN with config rsx_dist: dp through the reference's training flow (rsx.trainer
+    fused epochs + sharded evaluation), two ranks on one GPU over gloo."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import test_gpu_sharded_trainer as TS
+    from rsx.lightgcn import LightGCN
+    from rsx.trainer import Trainer
+    from rsx.utils import init_seed
+
+    c, train, valid = TS._setup(root, rsx_dist="dp")
+    init_seed(c["seed"])
+    train.pretrain_setup()
+    m = LightGCN(c, train)
+    assert m.sharded and m.dp
+    t = Trainer(c, m)
+    assert t.fused
+    seen = []
+    step0 = m.engine.step
+
+    def spy(triplets):
+        seen.append(triplets[:2].cpu().numpy().copy())
+        return step0(triplets)
+
+    m.engine.step = spy
+    losses = []
+    for epoch in range(2):
+        seen.clear()
+        loss, n = t._train_epoch(train, epoch)
+        assert not torch.is_tensor(loss) and n == m.steps_per_epoch
+        losses.append(loss)
+        t._epoch_for_lr += 1
+        if epoch == 0:
+            mine = np.concatenate(seen, axis=1)
+    vres = t.evaluate(valid)
+    f = m._final().cpu()
+    np.savez(os.path.join(out, f"r{rank}.npz"), f=f.numpy(), p=m.engine.p.cpu().numpy(), losses=np.array(losses),
+             keys=np.array(sorted(vres)), vals=np.array([vres[k] for k in sorted(vres)]), mine=mine,
+             inter=np.stack([m.engine.sampler.inter_u.cpu().numpy(), m.engine.sampler.inter_i.cpu().numpy()]))
+    dist.barrier()
+    m.engine.close()
+    dist.destroy_process_group()
+
+
+def test_dp_trainer_fit_and_evaluate(cuda):
+    """Every rank: the same losses, the same (bit-identical) tables and metric dict; the
+    dict equals a single-process evaluation of those tables; one epoch's rank slices
+    cover every training interaction exactly once."""
+    import shutil
+
+    from rsx import ops
+    from rsx.evaluator import TopKEvaluator
+    import test_gpu_sharded_trainer as TS
+
+    world = 2
+    with tempfile.TemporaryDirectory() as root:
+        os.makedirs(os.path.join(root, "baby"))
+        shutil.copy(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "gold_small.inter"),
+                    os.path.join(root, "baby", "baby.inter"))
+        out = os.path.join(root, "out")
+        os.makedirs(out)
+        mp.spawn(_trainer_worker, args=(world, _free_port(), root, out), nprocs=world, join=True)
+        res = [dict(np.load(os.path.join(out, f"r{r}.npz"))) for r in range(world)]
+        c, _, valid = TS._setup(root)
+    for x in res[1:]:
+        for key in ("f", "p", "losses", "vals"):
+            assert np.array_equal(res[0][key], x[key]), key
+    assert np.isfinite(res[0]["losses"]).all()
+    got_pairs = sorted(map(tuple, np.concatenate([x["mine"] for x in res], axis=1).T.tolist()))
+    assert got_pairs == sorted(map(tuple, res[0]["inter"].T.tolist()))
+    f = torch.from_numpy(res[0]["f"]).to(cuda)
+    nu = int(valid.mask_rowptr.numel() - 1)
+    k = max(c["topk"])
+    _, topk = ops.fullsort_topk(f[:nu], valid.eval_u, f[nu:], valid.mask_rowptr, valid.mask_col, k)
+    want = TopKEvaluator(c).evaluate_device(topk, valid)
+    got = dict(zip(res[0]["keys"], res[0]["vals"]))
+    for key in want:
+        assert abs(got[key] - want[key]) <= 1e-4 + 1e-12, (key, got[key], want[key])
