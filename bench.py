@@ -947,8 +947,26 @@ def main():
                 "frac": adam_ach / HBM_PEAK_GBS, "traffic": pmc_bytes("spmm_adam_traffic.json"),
                 "algorithmic_bytes_per_launch": adam_alg, "avg_launch_ms": adam_ms,
                 "note": store["note"]}
-        kernels = [roof, store]
-        del pc, mc, vc, gc
+        # the backward's Horner layer H = G' + A H (ADD epilogue, G' read on the batch rows):
+        # two per step at K = 3, the first gathering only G's batch rows
+        yh = torch.empty_like(eng.h0)
+        add_e = ops.epi(L.RSX_EPI_ADD, y=yh, s_in=gc, row_tag=eng.row_tag)
+        add_e.tag = max(eng.step_count, 1)
+        add_e.tag_flags = L.RSX_TAG_SPARSE_S
+
+        def add_layer():
+            eng.adj.spmm_epi(eng.h0, add_e, d)
+
+        add_ms = time_kernel(add_layer, 50)
+        add_alg = alg + 12 * 3 * B * d
+        add_ach = add_alg / (add_ms * 1e-3) / 1e9
+        addk = {"bound": "hbm", "kernel": f"spmm_main<{d},ADD> (a backward Horner layer H = G' + A H, dense X, "
+                                         "G' on the batch rows)",
+                "launches_per_step": 1 if args.n_layers == 3 else None, "achieved": add_ach, "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": add_ach / HBM_PEAK_GBS, "traffic": None,
+                "algorithmic_bytes_per_launch": add_alg, "avg_launch_ms": add_ms, "note": store["note"]}
+        kernels = [roof, store, addk]
+        del pc, mc, vc, gc, yh
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

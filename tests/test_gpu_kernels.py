@@ -508,9 +508,11 @@ def test_batch_row_tags_equal_dense_step(cuda, K, d):
     n = nu + ni
     assert a.use_reg_cnt and torch.count_nonzero(a.reg_cnt[: 3 * n + 1]).item() == 0
     np.testing.assert_allclose(a.loss_acc.item(), b.loss_acc.item(), rtol=1e-9)
-    for name in ("p", "m", "v"):
+    # the moments carry the atomics-order rounding of g (~1e-7 here); Adam's step normalises
+    # g by its RMS, which amplifies that rounding where g ~ 0 (up to ~lr per step): p 1e-5
+    for name, tol in (("p", 1e-5), ("m", 1e-6), ("v", 1e-6)):
         np.testing.assert_allclose(getattr(a, name).cpu().numpy(), getattr(b, name).cpu().numpy(), rtol=0,
-                                   atol=1e-6, err_msg=name)
+                                   atol=tol, err_msg=name)
     # the forward for evaluation (dense) is unaffected
     a.invalidate()
     b.invalidate()
@@ -544,9 +546,11 @@ def test_layergcn_c_step_equals_python_sequence(cuda, K, monkeypatch):
     torch.cuda.synchronize()
     a, b = engs
     np.testing.assert_allclose(a.loss_acc.item(), b.loss_acc.item(), rtol=1e-9)
-    for name in ("p", "m", "v"):
+    # the moments carry the atomics-order rounding of g (~1e-7 here); Adam's step normalises
+    # g by its RMS, which amplifies that rounding where g ~ 0 (up to ~lr per step): p 1e-5
+    for name, tol in (("p", 1e-5), ("m", 1e-6), ("v", 1e-6)):
         np.testing.assert_allclose(getattr(a, name).cpu().numpy(), getattr(b, name).cpu().numpy(), rtol=0,
-                                   atol=1e-6, err_msg=name)
+                                   atol=tol, err_msg=name)
 
 
 @pytest.mark.parametrize("K,tags,fused_bpr", [(3, True, True), (3, True, False), (3, False, False),

@@ -6,7 +6,7 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 OUT=${OUT:-gpurun_out/r04dp}
 mkdir -p $OUT
-timeout -k 10 900 python -u -m pytest tests/test_gpu_smore.py tests/test_gpu_sharded_trainer.py tests/test_gpu_dp.py tests/test_gpu_smore_fuse.py tests/test_gpu_smore_dist.py tests/test_gpu_dist.py tests/test_gpu_kernels.py -m gpu -x -q --timeout 200 --timeout-method thread -p no:cacheprovider > $OUT/pytest.log 2>&1
+timeout -k 10 900 python -u -m pytest tests/test_gpu_kernels.py -m gpu -x -q --timeout 200 --timeout-method thread -p no:cacheprovider > $OUT/pytest.log 2>&1
 rc=$?; tail -15 $OUT/pytest.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python bench.py --no-cpu-baseline --steps 200 > $OUT/c2.json 2> $OUT/c2.err || { tail -20 $OUT/c2.err; exit 1; }
 timeout -k 10 300 python bench.py --no-cpu-baseline --steps 200 --dp > $OUT/c2_dp1.json 2> $OUT/c2_dp1.err || { tail -20 $OUT/c2_dp1.err; exit 1; }
