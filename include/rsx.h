@@ -910,6 +910,19 @@ typedef struct rsx_sharded_lgcn_step {
      * K = 2) instead of 2K + 1, the same bytes, the compute between rounds serialised
      * (csrc/dist.hip:sharded_fused_rounds; rsx.dist enables it with RSX_SHARDED_FUSED=1). */
     float* xch;
+    /* optional (the stored-layer step, n_layers 2 or 3): the first forward item partial
+     * issued as n_head > 1 row pieces of adj_i, each piece's rows all-reduced as soon as
+     * that piece is computed, so the step's first exchange starts after 1/n_head of the
+     * product instead of after all of it (nothing else of the step can hide it).
+     * head_i[p] (host array) is the CSR of item rows [head_row0[p], head_row0[p+1]) of
+     * adj_i with its own work schedule (row ids local to the piece, nonzero offsets
+     * into adj_i's col/val) and its own slab head_slab[p]; results are bit-identical to
+     * the one-launch product (same chunks, same fixup order). */
+    int32_t n_head;
+    int32_t pad1;
+    const rsx_csr* head_i;
+    const int64_t* head_row0;   /* host, [n_head + 1] */
+    float* const* head_slab;    /* host, [n_head] (NULL entries for pieces without long rows) */
 } rsx_sharded_lgcn_step;
 
 int rsx_sharded_lightgcn_step(const rsx_sharded_lgcn_step* st, rsx_stream_t stream);

@@ -360,8 +360,20 @@ int sharded_stored_layers(const rsx_sharded_lgcn_step& st, bool train, hipStream
             tj.tag = tag;
             tj.tag_dev = st.tag_dev;
         }
-        RSX_TRY(spmm_dispatch_tagging(*st.adj_i, x, d, e, st.slab_i, s, tj));   // item partial of E^k
-        if (!(joins[k] = exchange(st.comm, bufs[k - 1] + off, ni * d, s, &rc))) return rc;
+        if (k == 1 && st.n_head > 1) {
+            // the step's head: nothing but this product can run before the first exchange,
+            // so it goes in row pieces, each piece's item rows summed as soon as they exist
+            // (the comm stream is in order: the last piece's join covers every piece)
+            for (int32_t p = 0; p < st.n_head; ++p) {
+                const int64_t r0 = st.head_row0[p], r1 = st.head_row0[p + 1];
+                e.y = bufs[0] + off + r0 * d;
+                RSX_TRY(spmm_dispatch_tagging(st.head_i[p], x, d, e, st.head_slab[p], s, p == 0 ? tj : TagJob{}));
+                if (!(joins[1] = exchange(st.comm, e.y, (r1 - r0) * d, s, &rc))) return rc;
+            }
+        } else {
+            RSX_TRY(spmm_dispatch_tagging(*st.adj_i, x, d, e, st.slab_i, s, tj));   // item partial of E^k
+            if (!(joins[k] = exchange(st.comm, bufs[k - 1] + off, ni * d, s, &rc))) return rc;
+        }
         if (k >= 2) RSX_TRY(wait(s, joins[k - 1]));                  // E^{k-1} items summed
         e.y = bufs[k - 1];
         RSX_TRY(spmm_dispatch(*st.adj_u, x, d, e, st.slab_u, s));   // E^k user rows
@@ -751,6 +763,18 @@ bool valid(const rsx_sharded_lgcn_step* st) {
             st->union_cap < st->batch ||
             !st->row_tag || (st->n_layers != 2 && st->n_layers != 3) || st->d % 4)
             return false;
+    }
+    if (st->n_head > 1) {  // the head pieces tile adj_i's rows in order
+        if (!st->head_i || !st->head_row0 || !st->head_slab || st->head_row0[0] != 0 ||
+            st->head_row0[st->n_head] != st->n_items)
+            return false;
+        for (int32_t p = 0; p < st->n_head; ++p) {
+            const rsx_csr& h = st->head_i[p];
+            if (st->head_row0[p + 1] <= st->head_row0[p] || h.n_rows != st->head_row0[p + 1] - st->head_row0[p] ||
+                h.n_cols != st->adj_i->n_cols || h.col != st->adj_i->col || h.val != st->adj_i->val ||
+                (h.n_long > 0 && !st->head_slab[p]))
+                return false;
+        }
     }
     return true;
 }

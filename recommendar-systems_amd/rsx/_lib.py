@@ -91,7 +91,8 @@ class ShardedStep(C.Structure):
                 ("adam", Adam), ("loss_out", P), ("loss_acc", P), ("ws", P), ("ws_bytes", C.c_size_t),
                 ("comm", P), ("row_tag", P), ("tag", I64), ("tag_dev", P), ("reg_cnt", P),
                 ("union_items", P), ("item_tag", P), ("cbuf0", P), ("cbuf1", P), ("n_items_pad", I64), ("union_cap", I64),
-                ("xch", P)]
+                ("xch", P), ("n_head", I32), ("pad1", I32), ("head_i", C.POINTER(Csr)), ("head_row0", P),
+                ("head_slab", P)]
 
 
 class DpStep(C.Structure):

@@ -103,6 +103,16 @@ def sim_comm_params():
             "blocks": int(f[3]) if len(f) > 3 and f[3] else RCCL_BLOCKS, "scratch_mb": 512}
 
 
+def head_pieces_knob(default: int) -> int:
+    """RSX_SHARDED_HEAD: row pieces of the step's first item partial (1 = one launch)."""
+    v = os.environ.get("RSX_SHARDED_HEAD")
+    if v is None or v == "":
+        return default
+    if not v.isdigit() or not 1 <= int(v) <= 64:
+        raise ValueError(f"RSX_SHARDED_HEAD={v!r}: an integer in [1, 64] expected")
+    return int(v)
+
+
 class HipBackend:
     """Product backend: rsx HIP kernels on the current torch stream."""
 
@@ -243,6 +253,21 @@ class ShardedLightGCNEngine:
         if (not self.sparse and self.row_tag is not None and self.K in (2, 3)
                 and os.environ.get("RSX_SHARDED_FUSED", "0") == "1"):
             self.xch = torch.zeros(2 * self.n_items, self.d, dtype=torch.float32, device=self.be.device)
+        # the step's head in row pieces (rsx_sharded_lgcn_step.n_head): the first item
+        # partial's rows all-reduced piece by piece, so the first exchange starts after
+        # 1/n_head of that product.  Default: 4 in the bandwidth regime (the sparse
+        # schedule: C4's 1 GB item block, where one product is ~2 ms per 1.25M users),
+        # off where latency bounds the exchanges (C2); RSX_SHARDED_HEAD overrides.
+        self.head = []
+        n_head = head_pieces_knob(4 if self.sparse else 1)
+        if n_head > 1 and self.row_tag is not None and self.xch is None and self.A_I.rowptr_host is not None:
+            rp = self.A_I.rowptr_host
+            cuts = np.searchsorted(rp, np.arange(1, n_head) * rp[-1] / n_head, side="left")
+            row0 = np.unique(np.concatenate([[0], np.clip(cuts, 1, self.n_items - 1), [self.n_items]]))
+            row0 = row0.astype(np.int64)
+            if row0.size - 1 > 1:
+                self.head = [ops.DeviceCSR.row_slice(self.A_I, int(a), int(b)) for a, b in zip(row0[:-1], row0[1:])]
+                self.head_row0 = row0
         comm = C.c_void_p()
         sim = sim_comm_params()
         if sim is not None:
@@ -268,6 +293,8 @@ class ShardedLightGCNEngine:
                 views += [self.union, self.cbuf0, self.cbuf1]
             if self.xch is not None:
                 views.append(self.xch)
+            if self.head:  # the head pieces' item rows of E^1
+                views += [self.h0[nu + int(a): nu + int(b)] for a, b in zip(self.head_row0[:-1], self.head_row0[1:])]
             self._views = {v.data_ptr(): v.view(-1) for v in views}
 
             def host_collective(op, ptr, count, dtype, _ctx):
@@ -305,6 +332,16 @@ class ShardedLightGCNEngine:
             st.union_items, st.item_tag = self.union.data_ptr(), self.item_tag.data_ptr()
             st.cbuf0, st.cbuf1 = self.cbuf0.data_ptr(), self.cbuf1.data_ptr()
         st.xch = self.xch.data_ptr() if self.xch is not None else None
+        if self.head:
+            self._head_structs = (L.Csr * len(self.head))(*[h.struct for h in self.head])
+            self._head_row0 = (C.c_int64 * self.head_row0.size)(*[int(x) for x in self.head_row0])
+            slabs = [h.slab(self.d) for h in self.head]
+            self._head_slab_keep = slabs
+            self._head_slab = (C.c_void_p * len(slabs))(*[s.data_ptr() if s is not None else None for s in slabs])
+            st.n_head = len(self.head)
+            st.head_i = C.cast(self._head_structs, C.POINTER(L.Csr))
+            st.head_row0 = C.cast(self._head_row0, C.c_void_p)
+            st.head_slab = C.cast(self._head_slab, C.c_void_p)
         # the one-launch BPR (regulariser as per-row occurrence counts, applied and
         # cleared by the user Adam layer and the last item partial), as the single engine
         self.reg_cnt = None

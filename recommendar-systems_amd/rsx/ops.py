@@ -130,6 +130,41 @@ class DeviceCSR:
         return self
 
     @classmethod
+    def row_slice(cls, parent: "DeviceCSR", r0: int, r1: int) -> "DeviceCSR":
+        """Rows [r0, r1) of a host-scheduled CSR as a CSR of its own: its own work
+        schedule (row ids local to the slice, nonzero offsets into the parent's col / val,
+        which are shared) and its own slabs.  A product over it writes rows y[0 : r1-r0]
+        bit-identically to the parent's rows r0..r1 (same chunks, same fixup order)."""
+        if parent.rowptr_host is None or not 0 <= r0 < r1 <= parent.n_rows:
+            raise RuntimeError("DeviceCSR.row_slice: a host-scheduled CSR and 0 <= r0 < r1 <= n_rows")
+        lib = L.lib()
+        rp = np.ascontiguousarray(parent.rowptr_host[r0:r1 + 1])
+        nw, nl, ns = C.c_int64(), C.c_int64(), C.c_int64()
+        L.check(lib.rsx_csr_schedule_host(rp.ctypes.data_as(C.c_void_p), r1 - r0, parent.chunk, None, None,
+                                          C.byref(nw), C.byref(nl), C.byref(ns)), "rsx_csr_schedule_host")
+        work = np.zeros((max(nw.value, 1), 4), dtype=np.int32)
+        longr = np.zeros((max(nl.value, 1), 4), dtype=np.int32)
+        L.check(lib.rsx_csr_schedule_host(rp.ctypes.data_as(C.c_void_p), r1 - r0, parent.chunk,
+                                          work.ctypes.data_as(C.c_void_p), longr.ctypes.data_as(C.c_void_p),
+                                          C.byref(nw), C.byref(nl), C.byref(ns)), "rsx_csr_schedule_host")
+        self = cls.__new__(cls)
+        self.device = parent.device
+        self.n_rows, self.n_cols, self.chunk = r1 - r0, parent.n_cols, parent.chunk
+        self.nnz = int(rp[-1] - rp[0])
+        self.n_work, self.n_long, self.n_slots = nw.value, nl.value, ns.value
+        self.rowptr_host = rp
+        self.rowptr = parent.rowptr[r0:r1 + 1]
+        self.col, self.val = parent.col, parent.val
+        self.work = torch.from_numpy(work).to(self.device)
+        self.long_rows = torch.from_numpy(longr).to(self.device)
+        self.struct = L.Csr(self.n_rows, self.n_cols, self.nnz, self.rowptr.data_ptr(), self.col.data_ptr(),
+                            self.val.data_ptr(), self.chunk, 0, self.n_work, self.work.data_ptr(), self.n_long,
+                            self.long_rows.data_ptr(), self.n_slots)
+        self._slabs = {}
+        self._parent = parent
+        return self
+
+    @classmethod
     def from_scipy(cls, m, device, chunk: int = 32):
         m = m.tocsr()
         m.sort_indices()

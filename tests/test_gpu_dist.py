@@ -17,10 +17,12 @@ from test_dist_gloo import D, K, LR, NI, NU, REG, _local_graph
 pytestmark = pytest.mark.gpu
 
 
-def _worker(rank, world, port, out_dir, native, sparse, k=K, fused=True):
+def _worker(rank, world, port, out_dir, native, sparse, k=K, fused=True, head=None):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     os.environ["RSX_SHARDED_FUSED"] = "1" if fused else "0"
+    if head is not None:  # the step's first item partial in `head` row pieces (rsx_sharded_lgcn_step.n_head)
+        os.environ["RSX_SHARDED_HEAD"] = str(head)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from rsx.dist import ShardedLightGCNEngine
 
@@ -34,6 +36,8 @@ def _worker(rank, world, port, out_dir, native, sparse, k=K, fused=True):
     assert eng.native == native and eng.sparse == sparse
     if native:  # the fused-round schedule: dense, K = 2, 3 (csrc/dist.hip:sharded_fused_rounds)
         assert (getattr(eng, "xch", None) is not None) == (fused and not sparse and k in (2, 3))
+        if head is not None:
+            assert len(eng.head) == head
     f0 = eng.forward().cpu().clone()
     eng.step(triplets=torch.from_numpy(trip).cuda())
     p1 = eng.p.cpu().numpy()
@@ -57,17 +61,23 @@ def _free_port():
 @pytest.mark.parametrize("native,sparse,k,fused", [(False, False, 3, True), (True, False, 3, True),
                                                    (True, False, 3, False), (True, False, 2, True),
                                                    (False, True, 3, True), (True, True, 3, True),
-                                                   (True, False, 4, True), (False, False, 4, True)])
+                                                   (True, False, 4, True), (False, False, 4, True),
+                                                   (True, True, 3, "head3"), (True, False, 3, "head3"),
+                                                   (True, True, 2, "head3")])
 def test_sharded_hip_step_matches_global_objective(native, sparse, k, fused):
     """sparse: the union-row exchange + reduce-scatter / owner Adam / all-gather schedule
     (csrc/dist.hip with the host hook's collectives when native).  Native dense K = 2, 3:
     the fused-round schedule (two layers' item partials per collective), fused=False the
     one-exchange-per-layer stored-layer step.  k = 4: the reference's default depth, the
-    native step's dense (untagged) form."""
+    native step's dense (untagged) form.  "head3": the stored-layer step with its first
+    item partial in 3 row pieces, each all-reduced as soon as it is computed."""
     world = 2
     K = k
+    head = None
+    if fused == "head3":
+        fused, head = False, 3
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(world, _free_port(), d, native, sparse, k, fused), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, _free_port(), d, native, sparse, k, fused, head), nprocs=world, join=True)
         res = [dict(np.load(os.path.join(d, f"r{r}.npz"))) for r in range(world)]
     gu, gi, trips = [], [], []
     for r in range(world):
