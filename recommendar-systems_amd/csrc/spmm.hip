@@ -245,7 +245,7 @@ template <int T>
 __device__ __forceinline__ int row_bcast(int x) {
     return __builtin_amdgcn_update_dpp(0, x, 0x150 + T, 0xf, 0xf, false);
 }
-template <int H>
+template <int H, int D = 64>
 __device__ __forceinline__ float4 gather8(float4 acc, int cm, float vm, int n, const float* xl) {
     const int vi = __float_as_int(vm);
     int c[8];
@@ -260,7 +260,7 @@ __device__ __forceinline__ float4 gather8(float4 acc, int cm, float vm, int n, c
     c[7] = row_bcast<8 * H + 7>(cm); v[7] = __int_as_float(row_bcast<8 * H + 7>(vi));
     float4 xv[8];
 #pragma unroll
-    for (int t = 0; t < 8; ++t) xv[t] = (8 * H + t < n && c[t] >= 0) ? ld4(xl + (int64_t)c[t] * 64) : f4(0.f);
+    for (int t = 0; t < 8; ++t) xv[t] = (8 * H + t < n && c[t] >= 0) ? ld4(xl + (int64_t)c[t] * D) : f4(0.f);
 #pragma unroll
     for (int t = 0; t < 8; ++t) acc = fma4(v[t], xv[t], acc);
     return acc;
@@ -378,6 +378,11 @@ __device__ __forceinline__ void st4_sc1(float* p, float4 v) {
 #ifndef RSX_SPMM_PF
 #define RSX_SPMM_PF 1
 #endif
+// d >= 128: (col, val) loaded 16 entries per lane-row and DPP-broadcast (0: the
+// per-entry wave-uniform loads; a compile-time A/B switch, tools/build_variant.py)
+#ifndef RSX_SPMM_WIDE_BCAST
+#define RSX_SPMM_WIDE_BCAST 1
+#endif
 
 // (col, val) of the next work item's first 16 nonzeros, loaded while the current
 // item's first gathers are in flight (d = 64): the next item starts with its
@@ -461,6 +466,23 @@ __device__ __forceinline__ void spmm_item(const rsx_csr& a, const float* __restr
 #endif
             if (n > 8) acc = gather8<1>(acc, cm, vm, n, xl);
 #endif
+        }
+    } else if constexpr (RSX_SPMM_WIDE_BCAST && D >= 128) {
+        // d = 128 / 256: a group spans 2 / 4 DPP rows.  Lane li loads entry j + (li & 15):
+        // the rows of a group load the same 16 (col, val) entries (one coalesced request
+        // each), and row_newbcast:t hands entry t to every lane of its row -- two vector
+        // loads per 16 nonzeros instead of two wave-uniform loads per nonzero, so the
+        // memory pipe carries the neighbour-row gathers only.  Same fma chain in nonzero
+        // order as the per-entry loop below: bit-identical results.
+        const int q = li & 15;
+        for (; j < end; j += 16) {
+            const bool mine = j + q < end;
+            int cm = mine ? col[j + q] : 0;
+            const float vm = mine ? val[j + q] : 0.f;
+            if (sparse_x && mine && e.row_tag[cm] != tag_of(e)) cm = -1;  // zero X row: no gather
+            const int n = end - j;
+            acc = gather8<0, D>(acc, cm, vm, n, xl);
+            if (n > 8) acc = gather8<1, D>(acc, cm, vm, n, xl);
         }
     } else {
         for (; j + kUnroll <= end; j += kUnroll) {

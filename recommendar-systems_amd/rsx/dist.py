@@ -170,6 +170,7 @@ class ShardedLightGCNEngine:
         # global item degrees (sum of every rank's interactions)
         deg_i = torch.from_numpy(np.bincount(ii, minlength=ni).astype(np.int64))
         deg_i = self._allreduce_host(deg_i)
+        self._deg_i_global = deg_i.numpy().astype(np.int64)  # the same on every rank
         deg_u = np.bincount(uu, minlength=nu).astype(np.float64)
         du = np.power(deg_u + 1e-7, -0.5)
         di = np.power(deg_i.numpy().astype(np.float64) + 1e-7, -0.5)
@@ -261,7 +262,8 @@ class ShardedLightGCNEngine:
         self.head = []
         n_head = head_pieces_knob(4 if self.sparse else 1)
         if n_head > 1 and self.row_tag is not None and self.xch is None and self.A_I.rowptr_host is not None:
-            rp = self.A_I.rowptr_host
+            # cut by the GLOBAL item degrees (every rank the same pieces: the collectives match)
+            rp = np.concatenate([[0], np.cumsum(self._deg_i_global)])
             cuts = np.searchsorted(rp, np.arange(1, n_head) * rp[-1] / n_head, side="left")
             row0 = np.unique(np.concatenate([[0], np.clip(cuts, 1, self.n_items - 1), [self.n_items]]))
             row0 = row0.astype(np.int64)
@@ -295,7 +297,13 @@ class ShardedLightGCNEngine:
                 views.append(self.xch)
             if self.head:  # the head pieces' item rows of E^1
                 views += [self.h0[nu + int(a): nu + int(b)] for a, b in zip(self.head_row0[:-1], self.head_row0[1:])]
-            self._views = {v.data_ptr(): v.view(-1) for v in views}
+            # one view per start pointer: the largest (the first head piece starts where the
+            # whole item block of h0 does; collectives use the first `count` floats)
+            self._views = {}
+            for v in views:
+                f = v.view(-1)
+                if f.numel() > self._views.get(v.data_ptr(), f[:0]).numel():
+                    self._views[v.data_ptr()] = f
 
             def host_collective(op, ptr, count, dtype, _ctx):
                 try:
