@@ -42,6 +42,10 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 // double-buffered.  Waves: item tile (w & 1) x feature tiles {w >> 1, + 2, ...}.
 constexpr int kPjItems = 64, kPjK = 32, kPjPad = 36;
 
+__device__ __forceinline__ float f4_at(const float4& v, int i) {  // i: a compile-time constant after unrolling
+    return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w;
+}
+
 struct SpecProjArgs {
     const float* X[2];  // V [n, K0], T [n, K1]
     int32_t K[2];
@@ -122,16 +126,26 @@ __global__ __launch_bounds__(256) void smore_proj(SpecProjArgs a) {
     auto step = [&](int c, auto bc) __attribute__((always_inline)) {
         constexpr int B = decltype(bc)::value;
         if (c + 2 < nch) gload(c + 2, st[B]);
-        const float* xb = xs[B] + (it * 32 + j) * kPjPad + h;
+        // the chunk's K order permuted (A and B alike): MFMA step u, lane half h takes
+        // k = 16 h + u, so a lane's 16 operands of a chunk are contiguous in its LDS row
+        // (four 16-B reads per operand instead of sixteen 4-B reads; rows padded to 36
+        // floats: 16 lanes' 16-B reads hit distinct banks)
+        float4 av[4], bv[TPW][4];
+        const float* xb = xs[B] + (it * 32 + j) * kPjPad + 16 * h;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) av[r] = *reinterpret_cast<const float4*>(xb + 4 * r);
+#pragma unroll
+        for (int q = 0; q < TPW; ++q) {
+            const float* wb = ws[B] + (((wave >> 1) + 2 * q) * 32 + j) * kPjPad + 16 * h;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) bv[q][r] = *reinterpret_cast<const float4*>(wb + 4 * r);
+        }
 #pragma unroll
         for (int u = 0; u < kPjK / 2; ++u) {
-            const float av = xb[2 * u];
+            const float a_u = f4_at(av[u >> 2], u & 3);
 #pragma unroll
-            for (int q = 0; q < TPW; ++q) {
-                const int ft = (wave >> 1) + 2 * q;
-                acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, ws[B][(ft * 32 + j) * kPjPad + 2 * u + h], acc[q],
-                                                              0, 0, 0);
-            }
+            for (int q = 0; q < TPW; ++q)
+                acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(a_u, f4_at(bv[q][u >> 2], u & 3), acc[q], 0, 0, 0);
         }
         if (c + 1 < nch) sstore(B ^ 1, st[B ^ 1]);
         __syncthreads();
@@ -577,7 +591,10 @@ extern "C" size_t rsx_smore_spectral_spec_floats(int64_t n_items, int32_t d) {
     return (size_t)n_items * 2 * 16 * (size_t)mt;
 }
 
-// K splits of a projection: about 1024 blocks over both modalities, >= 512 of K per split
+// K splits of a projection: about 1536 blocks over both modalities, >= 512 of K per split
+// (C5's 768-wide features: one split; two -- 1,440 blocks in 2.8 rounds of the 512 resident
+// d = 128 blocks instead of 720 in 1.4 -- measured no faster once smore_spec_fwd sums them:
+// proj 148.7 -> 138.3 us, spec_fwd 73.6 -> 82.5)
 static int env_int(const char* name, int dflt) { return env_knob(name, dflt, 1, 1 << 20); }
 
 static int proj_splits(int64_t n, int K) {
