@@ -1039,10 +1039,23 @@ def main():
         if sim:
             X = float(ni) * d * 4
             lib = L.lib()
+            # one stand-alone injected all-reduce of the item block, timed on the device: the
+            # stand-in must take the modelled time (its HBM copy must not be the bound)
+            import ctypes as _C
+            buf = torch.zeros(ni * d, dtype=torch.float32, device=dev)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            e0.record()
+            L.check(lib.rsx_comm_allreduce_f32(eng._comm, _C.c_void_p(buf.data_ptr()), ni * d, ops._stream()),
+                    "rsx_comm_allreduce_f32")
+            e1.record()
+            torch.cuda.synchronize()
+            del buf
             out["latency_injection"] = dict(sim, per_collective_ms={
                 "allreduce_item_block": 1e3 * lib.rsx_comm_sim_seconds(eng._comm, L.RSX_COLL_ALLREDUCE, X),
                 "reduce_scatter_or_all_gather_item_block":
                     1e3 * lib.rsx_comm_sim_seconds(eng._comm, L.RSX_COLL_ALLGATHER, X)},
+                measured_allreduce_item_block_ms=e0.elapsed_time(e1),
                 note="value / ms_per_step: one rank's share of the modelled job (the job's rate is world x value "
                      "when every rank holds the same share)")
         _json_line(out)

@@ -122,10 +122,25 @@ hipEvent_t comm_event(rsx_comm_t c) {
 __global__ __launch_bounds__(256) void sim_collective(float* __restrict__ scratch, int64_t half, int64_t floats,
                                                       uint64_t ticks) {
     const uint64_t t0 = wall_clock64();
+    // float4 copies, four in flight per lane, in passes over the scratch's halves (a
+    // per-element loop with one dependent load at a time ran at ~0.2 TB/s on 32 blocks
+    // and took several times the modelled collective time at C4's 1 GB item block)
     const int64_t stride = (int64_t)gridDim.x * 256;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < floats / 2; i += stride) {
-        const int64_t k = i % half;
-        scratch[half + k] = scratch[k] + 1.f;
+    const int64_t h4 = half / 4;
+    const float4* __restrict__ src = reinterpret_cast<const float4*>(scratch);
+    float4* __restrict__ dst = reinterpret_cast<float4*>(scratch + half);
+    for (int64_t todo = floats / 8; todo > 0;) {
+        const int64_t n = todo < h4 ? todo : h4;
+        int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+        for (; i + 3 * stride < n; i += 4 * stride) {
+            const float4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], e = src[i + 3 * stride];
+            dst[i] = add4(a, f4(1.f));
+            dst[i + stride] = add4(b, f4(1.f));
+            dst[i + 2 * stride] = add4(c, f4(1.f));
+            dst[i + 3 * stride] = add4(e, f4(1.f));
+        }
+        for (; i < n; i += stride) dst[i] = add4(src[i], f4(1.f));
+        todo -= n;
     }
     while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(16);
 }
