@@ -690,6 +690,8 @@ def main():
     from rsx.dist import sim_comm_params
 
     sim = sim_comm_params() if big else None
+    if sim:  # time this rank's share of the modelled job (csrc/dist.hip: the owner Adam on 1/W items)
+        os.environ.setdefault("RSX_COMM_SIM_SHARE", "1")
     w_eff = sim["world"] if sim else world
     if sim and world != 1:
         raise SystemExit("RSX_COMM_SIM runs one rank")

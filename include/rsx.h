@@ -593,6 +593,13 @@ int rsx_smore_pref(int32_t backward, const float* const* W, const float* const* 
  *            table row of `rows` is SET to their sum in a fixed order (deterministic run
  *            to run); the other rows are untouched (zero them first).
  */
+/*
+ * Batch-row tags (the SMORE loss rows, src/models/smore.py:366-411): row_tag[rows[j]] =
+ * *tag_dev for j < n (stream-ordered, graph-capturable; the caller bumps *tag_dev first).
+ * A product with row_tag / tag_dev then treats exactly these rows as tagged.
+ */
+int rsx_tag_rows(int32_t* row_tag, const int64_t* rows, int64_t n, const int32_t* tag_dev, rsx_stream_t stream);
+
 int rsx_smore_pref_rows(int32_t backward, const float* const* W, const float* const* b, const float* content,
                         const float* image_emb, const float* text_emb, const float* fusion_emb, const int64_t* rows,
                         int64_t n, int32_t d, float p_drop, const int64_t* seed_dev, float* all_out,
@@ -923,6 +930,18 @@ typedef struct rsx_sharded_lgcn_step {
     const rsx_csr* head_i;
     const int64_t* head_row0;   /* host, [n_head + 1] */
     float* const* head_slab;    /* host, [n_head] (NULL entries for pieces without long rows) */
+    /* optional with the sparse exchange (training): the last stored forward layer's item
+     * rows E^{K-1}_I are read only by the final rows of the batch users (their neighbour
+     * items) and of the union items, so they are summed over exactly those rows: every
+     * rank lists its batch users' neighbour items and its own (pos, neg) items in its
+     * nbr_cap slice of nbr_items (unused slots item 0), the lists are all-gathered, and
+     * one compact [world nbr_cap, d] all-reduce (cbufN) replaces the dense one of
+     * n_items*d floats.  nbr_cap >= 2 union_cap + the largest neighbour count of any
+     * union_cap of this rank's users (the host bounds it); nbr_count is a device int. */
+    int64_t* nbr_items;         /* [world][nbr_cap] */
+    int32_t* nbr_count;         /* [1] */
+    float* cbufN;               /* [world nbr_cap, d] */
+    int64_t nbr_cap;
 } rsx_sharded_lgcn_step;
 
 int rsx_sharded_lightgcn_step(const rsx_sharded_lgcn_step* st, rsx_stream_t stream);

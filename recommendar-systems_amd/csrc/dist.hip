@@ -102,6 +102,18 @@ struct rsx_comm_s {
 
 namespace rsx {
 
+// The communicator's stream at the device's greatest priority (RSX_COMM_PRIORITY=0: the
+// default priority): a collective queued behind a chip-filling product gets its
+// workgroups dispatched as soon as slots free up, instead of after that product's queued
+// blocks (RCCL's kernels, and the latency-injected stand-in, hold a few dozen CUs).
+hipError_t comm_stream_create(hipStream_t* s) {
+    static const int64_t prio_on = env_knob("RSX_COMM_PRIORITY", 1, 0, 1);
+    int least = 0, greatest = 0;
+    if (prio_on && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
+        return hipStreamCreateWithPriority(s, hipStreamNonBlocking, greatest);
+    return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+}
+
 int comm_rank(rsx_comm_t c) { return c->rank; }
 int comm_world(rsx_comm_t c) { return c->world; }
 // The stream the communicator's exchanges run on (host-hook communicators: the caller's):
@@ -246,6 +258,30 @@ __global__ __launch_bounds__(256) void rows_k(const float* src, float* dst, cons
     else st4(dst + i * d + c, f4(0.f));
 }
 
+// This rank's list for the sparse last-layer exchange: its (pos, neg) items (the union
+// share), then every neighbour item of its batch users (A_U row u: cols = n_users + item),
+// appended at a claimed position; the caller zero-fills the slice first (unused slots
+// stay item 0).  One wave per batch user; claims past `cap` are dropped and counted in
+// *cnt (the host bound makes that impossible; a test checks the counter).
+__global__ __launch_bounds__(256) void nbr_list_k(const int64_t* __restrict__ trip, int64_t batch,
+                                                  const int64_t* __restrict__ rowptr, const int32_t* __restrict__ col,
+                                                  int64_t n_users, int64_t* __restrict__ out, int64_t cap,
+                                                  int32_t* __restrict__ cnt) {
+    const int lane = threadIdx.x & 63;
+    const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (w >= batch) return;
+    if (lane < 2) out[2 * w + lane] = trip[(1 + lane) * batch + w];  // pos, neg of triplet w
+    const int64_t u = trip[w];
+    const int64_t b = rowptr[u], e = rowptr[u + 1];
+    int32_t base = 0;
+    if (lane == 0) base = atomicAdd(cnt, (int32_t)(e - b));
+    base = __shfl(base, 0, 64);
+    for (int64_t j = b + lane; j < e; j += 64) {
+        const int64_t p = 2 * batch + base + (j - b);
+        if (p < cap) out[p] = (int64_t)col[j] - n_users;
+    }
+}
+
 int rows_op(const float* src, float* dst, const int64_t* ids, int64_t n, int d, int mode, hipStream_t s) {
     if (n <= 0) return 0;
     const int64_t tot = n * (d / 4);
@@ -361,6 +397,19 @@ int sharded_stored_layers(const rsx_sharded_lgcn_step& st, bool train, hipStream
         if (!(jU = collective(st.comm, RSX_COLL_ALLGATHER, st.union_items, 2 * cap, RSX_COLL_I64, s, &rc)))
             return rc;
     }
+    // sparse last forward layer: this rank's (pos, neg) + batch users' neighbour items, gathered
+    const bool nbr = sparse && st.nbr_items;  // (valid() checked the buffers and the cap)
+    const int64_t nQ = nbr ? (int64_t)st.comm->world * st.nbr_cap : 0;
+    hipEvent_t jN = nullptr;
+    if (nbr) {
+        int64_t* mine = st.nbr_items + (int64_t)st.comm->rank * st.nbr_cap;
+        RSX_TRY(hip_rc(hipMemsetAsync(mine, 0, (size_t)st.nbr_cap * sizeof(int64_t), s)));
+        RSX_TRY(hip_rc(hipMemsetAsync(st.nbr_count, 0, sizeof(int32_t), s)));
+        hipLaunchKernelGGL(nbr_list_k, dim3((unsigned)((st.batch + 3) / 4)), dim3(256), 0, s, st.triplets, st.batch,
+                           st.adj_u->rowptr, st.adj_u->col, nu, mine, st.nbr_cap, st.nbr_count);
+        RSX_TRY(last_rc());
+        if (!(jN = collective(st.comm, RSX_COLL_ALLGATHER, st.nbr_items, st.nbr_cap, RSX_COLL_I64, s, &rc))) return rc;
+    }
     // ---- forward (the first item partial's launch also tags the batch rows when training)
     const float* x = st.p;
     for (int k = 1; k < K; ++k) {
@@ -375,7 +424,14 @@ int sharded_stored_layers(const rsx_sharded_lgcn_step& st, bool train, hipStream
             tj.tag = tag;
             tj.tag_dev = st.tag_dev;
         }
-        if (k == 1 && st.n_head > 1) {
+        if (k == K - 1 && nbr) {
+            // E^{K-1}_I is read on the listed rows only (the batch users' final rows gather
+            // their neighbour items, the union items' final rows add it): summed there alone
+            RSX_TRY(spmm_dispatch_tagging(*st.adj_i, x, d, e, st.slab_i, s, tj));
+            RSX_TRY(wait(s, jN));
+            RSX_TRY(rows_op(bufs[k - 1] + off, st.cbufN, st.nbr_items, nQ, d, 0, s));
+            if (!(joins[k] = exchange(st.comm, st.cbufN, nQ * d, s, &rc))) return rc;
+        } else if (k == 1 && st.n_head > 1) {
             // the step's head: nothing but this product can run before the first exchange,
             // so it goes in row pieces, each piece's item rows summed as soon as they exist
             // (the comm stream is in order: the last piece's join covers every piece)
@@ -395,6 +451,7 @@ int sharded_stored_layers(const rsx_sharded_lgcn_step& st, bool train, hipStream
         x = bufs[k - 1];
     }
     RSX_TRY(wait(s, joins[K - 1]));
+    if (nbr) RSX_TRY(rows_op(st.cbufN, bufs[K - 2] + off, st.nbr_items, nQ, d, 1, s));  // summed rows back
     {
         rsx_epilogue e = epi(RSX_EPI_FINAL);
         e.beta = beta;
@@ -543,7 +600,12 @@ int sharded_stored_layers(const rsx_sharded_lgcn_step& st, bool train, hipStream
             // this rank's item rows [rank q, (rank+1) q) ∩ [0, n_items): Adam on the owner only,
             // then every replica receives the updated rows
             const int64_t r0 = (int64_t)st.comm->rank * q;
-            const int64_t nown = r0 < ni ? (ni - r0 < q ? ni - r0 : q) : 0;
+            int64_t nown = r0 < ni ? (ni - r0 < q ? ni - r0 : q) : 0;
+            // latency injection with RSX_COMM_SIM_SHARE=1 (bench.py): the one rank times ITS
+            // share of the modelled W-rank job, so the owner Adam covers ceil(n_items / W) rows
+            // (the parameters then differ from a one-rank run: a timing mode, not a training one)
+            static const int64_t sim_share = env_knob("RSX_COMM_SIM_SHARE", 0, 0, 1);
+            if (sim_share && st.comm->sim_world > 1) nown = (ni + st.comm->sim_world - 1) / st.comm->sim_world;
             rsx_epilogue a = epi(RSX_EPI_ADAM);
             a.s_in = st.t + r0 * d;
             a.p = st.p + off + r0 * d;
@@ -779,6 +841,8 @@ bool valid(const rsx_sharded_lgcn_step* st) {
             !st->row_tag || (st->n_layers != 2 && st->n_layers != 3) || st->d % 4)
             return false;
     }
+    if (st->nbr_items && (!st->union_items || !st->nbr_count || !st->cbufN || st->nbr_cap < 2 * st->union_cap))
+        return false;
     if (st->n_head > 1) {  // the head pieces tile adj_i's rows in order
         if (!st->head_i || !st->head_row0 || !st->head_slab || st->head_row0[0] != 0 ||
             st->head_row0[st->n_head] != st->n_items)
@@ -818,7 +882,7 @@ int rsx_comm_init(rsx_comm_t* out, const void* id_host, int32_t rank, int32_t wo
     c->world = world;
     ncclUniqueId id;
     memcpy(&id, id_host, sizeof(id));
-    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    hipError_t e = rsx::comm_stream_create(&c->stream);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork, hipEventDisableTiming);
     for (int i = 0; e == hipSuccess && i < rsx::kJoinEvents; ++i)
         e = hipEventCreateWithFlags(&c->join[i], hipEventDisableTiming);
@@ -871,7 +935,7 @@ int rsx_comm_init_sim(rsx_comm_t* out, int32_t sim_world, double busbw_gbs, doub
     c->sim_scratch_floats = scratch_mb * (1 << 20) / 4;
     if (e == hipSuccess) e = hipMalloc(&c->sim_scratch, (size_t)c->sim_scratch_floats * 4);
     if (e == hipSuccess) e = hipMemset(c->sim_scratch, 0, (size_t)c->sim_scratch_floats * 4);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = rsx::comm_stream_create(&c->stream);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork, hipEventDisableTiming);
     for (int i = 0; e == hipSuccess && i < rsx::kJoinEvents; ++i)
         e = hipEventCreateWithFlags(&c->join[i], hipEventDisableTiming);

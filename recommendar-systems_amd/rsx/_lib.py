@@ -92,7 +92,7 @@ class ShardedStep(C.Structure):
                 ("comm", P), ("row_tag", P), ("tag", I64), ("tag_dev", P), ("reg_cnt", P),
                 ("union_items", P), ("item_tag", P), ("cbuf0", P), ("cbuf1", P), ("n_items_pad", I64), ("union_cap", I64),
                 ("xch", P), ("n_head", I32), ("pad1", I32), ("head_i", C.POINTER(Csr)), ("head_row0", P),
-                ("head_slab", P)]
+                ("head_slab", P), ("nbr_items", P), ("nbr_count", P), ("cbufN", P), ("nbr_cap", I64)]
 
 
 class DpStep(C.Structure):
@@ -166,6 +166,7 @@ def _declare(lib):
         "rsx_smore_pref_rows": (C.c_int, [I32, P, P, P, P, P, P, P, I64, I32, F32, P, P, P, P, P, P, P, P, P, P, P,
                                           P, P, P, P, P, P]),
         "rsx_smore_pref_rows_occ_floats": (C.c_size_t, [I64, I32]),
+        "rsx_tag_rows": (C.c_int, [P, P, I64, P, P]),
         "rsx_smore_wgrad_ws_bytes": (C.c_size_t, [I64, I32, I32]),
         "rsx_smore_wgrad": (C.c_int, [I32, P, P, P, P, I64, I32, P, C.c_size_t, P]),
         "rsx_smore_infonce_ws_bytes": (C.c_size_t, [I64, I32]),
@@ -210,7 +211,7 @@ EXPORTED = ["rsx_version", "rsx_csr_schedule_host", "rsx_csr_schedule_rebind", "
             "rsx_comm_allreduce_f32", "rsx_sharded_lightgcn_step", "rsx_sharded_lightgcn_forward",
             "rsx_dp_lightgcn_step", "rsx_dp_block_floats", "rsx_comm_init_sim", "rsx_comm_sim_seconds",
             "rsx_comm_allgather_f32", "rsx_comm_allreduce_f32_start", "rsx_comm_wait",
-            "rsx_smore_gates", "rsx_smore_pref", "rsx_smore_pref_rows", "rsx_smore_pref_rows_occ_floats", "rsx_smore_wgrad_ws_bytes", "rsx_smore_wgrad",
+            "rsx_smore_gates", "rsx_smore_pref", "rsx_smore_pref_rows", "rsx_smore_pref_rows_occ_floats", "rsx_tag_rows", "rsx_smore_wgrad_ws_bytes", "rsx_smore_wgrad",
             "rsx_smore_infonce_ws_bytes", "rsx_smore_infonce_fwd", "rsx_smore_infonce_bwd", "rsx_smore_infonce_fwd_total", "rsx_smore_infonce_bwd_scaled", "rsx_adam_multi", "rsx_adam_multi_scaled", "rsx_adam_multi_mg",
             "rsx_smore_unit_weights", "rsx_smore_unit_weights_bwd", "rsx_mg_alpha_ws_bytes", "rsx_mg_alpha",
             "rsx_axpy_multi", "rsx_knn_ws_bytes", "rsx_knn_graph", "rsx_adj_build_ws_bytes", "rsx_adj_build",

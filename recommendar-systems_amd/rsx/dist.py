@@ -216,6 +216,7 @@ class ShardedLightGCNEngine:
             self.item_tag = mk(torch.zeros(ni, dtype=torch.int32))
             self.cbuf0 = z(self.world * 2 * self.union_cap)
             self.cbuf1 = z(self.world * 2 * self.union_cap)
+            self.nbr = None  # the sparse last-layer exchange's buffers (native step, _init_native)
         self.loss_acc = self.be.tensor(torch.zeros(1, dtype=torch.float64))
         self.step_count = 0
         self.sampler = self.be.sampler(tu, ti, nu, seed)
@@ -270,6 +271,12 @@ class ShardedLightGCNEngine:
             if row0.size - 1 > 1:
                 self.head = [ops.DeviceCSR.row_slice(self.A_I, int(a), int(b)) for a, b in zip(row0[:-1], row0[1:])]
                 self.head_row0 = row0
+        # the last stored forward layer's item rows summed on the rows the loss reads only
+        # (rsx_sharded_lgcn_step.nbr_items; RSX_SHARDED_NBR=0 keeps its dense all-reduce)
+        self.nbr = None
+        if (self.sparse and self.row_tag is not None and self.A_U.rowptr_host is not None
+                and os.environ.get("RSX_SHARDED_NBR", "1") != "0"):
+            self._alloc_nbr(self.union_cap)
         comm = C.c_void_p()
         sim = sim_comm_params()
         if sim is not None:
@@ -295,6 +302,8 @@ class ShardedLightGCNEngine:
                 views += [self.union, self.cbuf0, self.cbuf1]
             if self.xch is not None:
                 views.append(self.xch)
+            if self.nbr is not None:
+                views += [self.nbr["ids"], self.nbr["buf"]]
             if self.head:  # the head pieces' item rows of E^1
                 views += [self.h0[nu + int(a): nu + int(b)] for a, b in zip(self.head_row0[:-1], self.head_row0[1:])]
             # one view per start pointer: the largest (the first head piece starts where the
@@ -340,6 +349,7 @@ class ShardedLightGCNEngine:
             st.union_items, st.item_tag = self.union.data_ptr(), self.item_tag.data_ptr()
             st.cbuf0, st.cbuf1 = self.cbuf0.data_ptr(), self.cbuf1.data_ptr()
         st.xch = self.xch.data_ptr() if self.xch is not None else None
+        self._set_nbr_struct()
         if self.head:
             self._head_structs = (L.Csr * len(self.head))(*[h.struct for h in self.head])
             self._head_row0 = (C.c_int64 * self.head_row0.size)(*[int(x) for x in self.head_row0])
@@ -427,6 +437,29 @@ class ShardedLightGCNEngine:
         if graph:
             self._graph_warm.add(B)
 
+    def _alloc_nbr(self, B):
+        cap = self._nbr_cap(B)
+        sim = sim_comm_params()
+        if sim is not None and self.world == 1:
+            # one rank modelling a W-rank job: its list padded to the job's W slices (item 0),
+            # so the injected compact all-reduce moves the modelled job's bytes
+            cap *= sim["world"]
+        dev = self.be.device
+        self.nbr = {"cap": cap, "ids": torch.zeros(self.world * cap, dtype=torch.int64, device=dev),
+                    "count": torch.zeros(1, dtype=torch.int32, device=dev),
+                    "buf": torch.zeros(self.world * cap, self.d, dtype=torch.float32, device=dev)}
+
+    def _set_nbr_struct(self):
+        st = getattr(self, "_st", None)
+        if st is None:
+            return
+        if self.nbr is None:
+            st.nbr_items = st.nbr_count = st.cbufN = None
+            st.nbr_cap = 0
+        else:
+            st.nbr_items, st.nbr_count = self.nbr["ids"].data_ptr(), self.nbr["count"].data_ptr()
+            st.cbufN, st.nbr_cap = self.nbr["buf"].data_ptr(), self.nbr["cap"]
+
     def _grow_union(self, B):
         """Union-exchange buffers for batches of up to B pairs per rank."""
         self.union_cap = int(B)
@@ -434,8 +467,11 @@ class ShardedLightGCNEngine:
         self.union = torch.zeros(self.world * 2 * B, dtype=torch.int64, device=dev)
         self.cbuf0 = torch.zeros(self.world * 2 * B, self.d, dtype=torch.float32, device=dev)
         self.cbuf1 = torch.zeros_like(self.cbuf0)
+        if getattr(self, "nbr", None) is not None:
+            self._alloc_nbr(B)
+            self._set_nbr_struct()
         if getattr(self, "_views", None) is not None:
-            for v in (self.union, self.cbuf0, self.cbuf1):
+            for v in (self.union, self.cbuf0, self.cbuf1) + ((self.nbr["ids"], self.nbr["buf"]) if self.nbr else ()):
                 self._views[v.data_ptr()] = v.view(-1)
         if getattr(self, "_st", None) is not None:
             st = self._st
@@ -458,13 +494,22 @@ class ShardedLightGCNEngine:
             pass
 
     # ------------------------------------------------------------------ comms
-    def _allreduce_host(self, t):
+    def _allreduce_host(self, t, op=dist.ReduceOp.SUM):
         if dist.get_backend(self.group) == "nccl":
             x = t.to(torch.device("cuda", torch.cuda.current_device()))
-            dist.all_reduce(x, group=self.group)
+            dist.all_reduce(x, op=op, group=self.group)
             return x.cpu()
-        dist.all_reduce(t, group=self.group)
+        dist.all_reduce(t, op=op, group=self.group)
         return t
+
+    def _nbr_cap(self, B):
+        """rsx_sharded_lgcn_step.nbr_cap for batches of up to B triplets per rank: 2 B union
+        items + the largest neighbour count any B of this rank's users can have (the sum of
+        the B largest user degrees), the maximum over the ranks (the slices line up)."""
+        deg = np.diff(self.A_U.rowptr_host)
+        top = int(np.sort(deg)[::-1][:B].sum()) if deg.size else 0
+        cap = torch.tensor([2 * int(B) + top], dtype=torch.int64)
+        return int(self._allreduce_host(cap, op=dist.ReduceOp.MAX).item())
 
     def _broadcast_host(self, t):
         if dist.get_backend(self.group) == "nccl":

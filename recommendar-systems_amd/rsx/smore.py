@@ -82,6 +82,33 @@ class _PropMean(torch.autograd.Function):
         return _prop_mean(ctx.A, g, ctx.K), None, None
 
 
+class _Joined(torch.autograd.Function):
+    """torch.cat([U, I]) without the copy when U and I are adjacent row blocks of one
+    buffer (SMORE keeps its user and item-id tables so: rsx.smore.SMORE.__init__): the
+    output aliases their storage (a new tensor, not an autograd view of either input);
+    backward: the two row blocks of the gradient, as cat's."""
+
+    @staticmethod
+    def forward(ctx, u, i):
+        ctx.nu = u.shape[0]
+        out = torch.empty(0, dtype=u.dtype, device=u.device)
+        out.set_(u.untyped_storage(), u.storage_offset(), (u.shape[0] + i.shape[0], u.shape[1]), (u.shape[1], 1))
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        return g[: ctx.nu], g[ctx.nu:]
+
+
+def _ego(u: torch.Tensor, i: torch.Tensor) -> torch.Tensor:
+    """[U; I] (the reference's torch.cat([user_embeds, item_embeds]), smore.py:278)."""
+    adjacent = (u.device == i.device and u.dtype == i.dtype and u.is_contiguous() and i.is_contiguous()
+                and u.dim() == 2 and i.dim() == 2 and u.shape[1] == i.shape[1]
+                and u.untyped_storage().data_ptr() == i.untyped_storage().data_ptr()
+                and i.storage_offset() == u.storage_offset() + u.numel())
+    return _Joined.apply(u, i) if adjacent else torch.cat([u, i], dim=0)
+
+
 class _RowTags:
     """Batch-row tags for the tagged propagation: row r is in the batch when
     row_tag[r] == *tag_dev; `mark` bumps the device tag and tags the batch's rows
@@ -93,7 +120,9 @@ class _RowTags:
 
     def mark(self, rows: torch.Tensor):
         self.tag_dev.add_(1)
-        self.row_tag[rows] = self.tag_dev
+        rows = rows.to(torch.int64).contiguous()
+        L.check(L.lib().rsx_tag_rows(ops._p(self.row_tag), ops._p(rows), rows.numel(), ops._p(self.tag_dev),
+                                     ops._stream()), "rsx_tag_rows")
 
 
 class _PropMeanRows(torch.autograd.Function):
@@ -312,6 +341,15 @@ class SMORE(GeneralRecommender):
         nn.init.xavier_uniform_(self.user_embedding.weight)
         nn.init.xavier_uniform_(self.item_id_embedding.weight)
         nu, ni = self.n_users, self.n_items
+        if torch.device(self.device).type == "cuda":
+            # the two tables as adjacent row blocks of one device buffer (drawn on the CPU as
+            # the reference does, then copied): the UI backbone's ego table [U; I] is that
+            # buffer itself (_ego), no per-forward concatenation copy
+            joint = torch.empty(nu + ni, d, dtype=torch.float32, device=self.device)
+            joint[:nu].copy_(self.user_embedding.weight.detach())
+            joint[nu:].copy_(self.item_id_embedding.weight.detach())
+            self.user_embedding.weight = nn.Parameter(joint[:nu])
+            self.item_id_embedding.weight = nn.Parameter(joint[nu:])
         im = self.interaction_matrix
         if os.environ.get("RSX_GRAPH_BUILDER", "device") == "host":
             rp, col, val = graph.smore_norm_adj(im.row.astype(np.int64), im.col.astype(np.int64), nu, ni)
@@ -584,7 +622,7 @@ class SMORE(GeneralRecommender):
             if rows is not None:
                 rows.record_stream(side)  # made on this stream, read on the side stream (also in the backward)
         with torch.cuda.stream(side) if side is not None else _nullctx():
-            ego = torch.cat([user_w, item_id], dim=0)
+            ego = _ego(user_w, item_id)
             if rows is not None and 1 <= self.n_ui_layers <= 4:
                 if self._tags is None:
                     self._tags = _RowTags(self.n_users + self.n_items, self.device)
