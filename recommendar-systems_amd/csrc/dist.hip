@@ -537,8 +537,23 @@ int sharded_stored_layers(const rsx_sharded_lgcn_step& st, bool train, hipStream
             e.tag_dev = st.tag_dev;
             e.tag_flags = RSX_TAG_SPARSE_X;
         }
-        RSX_TRY(spmm_dispatch(*st.adj_i, x, d, e, st.slab_i, s));
-        if (!(joins[k] = exchange(st.comm, bufs[k - 1] + off, ni * d, s, &rc))) return rc;
+        if (k == 1 && st.n_head > 1) {
+            // the backward's head: its first exchange waits for this product alone, so it
+            // goes in the same row pieces as the forward's (the pieces' epilogue rows are
+            // local: y and G'_I offset by the piece's first row; SPARSE_X reads columns)
+            float* y0 = e.y;
+            const float* s0 = e.s_in;
+            for (int32_t p = 0; p < st.n_head; ++p) {
+                const int64_t r0 = st.head_row0[p], r1 = st.head_row0[p + 1];
+                e.y = y0 + r0 * d;
+                if (s0) e.s_in = s0 + r0 * d;
+                RSX_TRY(spmm_dispatch(st.head_i[p], x, d, e, st.head_slab[p], s));
+                if (!(joins[1] = exchange(st.comm, e.y, (r1 - r0) * d, s, &rc))) return rc;
+            }
+        } else {
+            RSX_TRY(spmm_dispatch(*st.adj_i, x, d, e, st.slab_i, s));
+            if (!(joins[k] = exchange(st.comm, bufs[k - 1] + off, ni * d, s, &rc))) return rc;
+        }
         if (k >= 2) RSX_TRY(wait(s, joins[k - 1]));
         rsx_epilogue u = epi(RSX_EPI_ADD);  // H^k users = G'_U + A_U H^{k-1}_I (G'_U on batch users only)
         u.y = bufs[k - 1];
@@ -595,7 +610,7 @@ int sharded_stored_layers(const rsx_sharded_lgcn_step& st, bool train, hipStream
         u.tag_dev = st.tag_dev;
         u.tag_flags = RSX_TAG_SPARSE_S | RSX_TAG_SPARSE_R | RSX_TAG_ZERO;
         RSX_TRY(spmm_dispatch(*st.adj_u, x, d, u, st.slab_u, s));
-        RSX_TRY(wait(s, jt));
+        if (!sparse) RSX_TRY(wait(s, jt));  // (sparse: the owner Adam runs behind jt on the comm stream)
         if (sparse) {
             // this rank's item rows [rank q, (rank+1) q) ∩ [0, n_items): Adam on the owner only,
             // then every replica receives the updated rows
@@ -612,8 +627,14 @@ int sharded_stored_layers(const rsx_sharded_lgcn_step& st, bool train, hipStream
             a.m = st.m + off + r0 * d;
             a.v = st.v + off + r0 * d;
             a.adam = st.adam;
-            if (nown > 0) RSX_TRY(rowwise_dispatch(nown, d, a, s));
-            hipEvent_t jp = collective(st.comm, RSX_COLL_ALLGATHER, st.p + off, q * d, RSX_COLL_F32, s, &rc);
+            // the owner Adam and the all-gather follow the reduce-scatter on the comm stream:
+            // they read only its output and the item rows of p / m / v, which nothing on the
+            // compute stream touches now (the user Adam there updates user rows), so the
+            // all-gather no longer waits for the user-row Adam product
+            hipStream_t cs = comm_stream(st.comm, s);
+            if (cs != s) RSX_TRY(wait(cs, jt));
+            if (nown > 0) RSX_TRY(rowwise_dispatch(nown, d, a, cs));
+            hipEvent_t jp = collective(st.comm, RSX_COLL_ALLGATHER, st.p + off, q * d, RSX_COLL_F32, cs, &rc);
             if (!jp) return rc;
             RSX_TRY(wait(s, jp));  // the next step (and any reader) sees every updated replica
         } else {

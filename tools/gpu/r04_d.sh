@@ -22,6 +22,7 @@ run sim_w8 RSX_COMM_SIM=8 || exit 1
 run sim_w8_eager RSX_COMM_SIM=8 RSX_SHARDED_GRAPH=0 || exit 1
 run sim_w8_nonbr RSX_COMM_SIM=8 RSX_SHARDED_NBR=0 || exit 1
 run sim_w8_lowprio RSX_COMM_SIM=8 RSX_COMM_PRIORITY=0 || exit 1
+run sim_w8_head1 RSX_COMM_SIM=8 RSX_SHARDED_HEAD=1 || exit 1
 run sim_w4 RSX_COMM_SIM=4 || exit 1
 run sim_w2 RSX_COMM_SIM=2 || exit 1
 W=8 OUT=$OUT/trace_w8 bash tools/gpu/c4_simtrace.sh
