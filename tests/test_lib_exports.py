@@ -102,3 +102,43 @@ def test_fullsort_plan_host(nb, ni, d, chunks, per):
     nc, pi = C.c_int32(), C.c_int64()
     L.check(L.lib().rsx_fullsort_plan(nb, ni, d, C.byref(nc), C.byref(pi)), "rsx_fullsort_plan")
     assert (nc.value, pi.value) == (chunks, per)
+
+
+def test_row_slice_schedules_cover_the_parent_rows():
+    """DeviceCSR.row_slice (the sharded step's head pieces, rsx_sharded_lgcn_step.n_head):
+    each piece's schedule is the host schedule of its rows, row ids local to the piece,
+    nonzero offsets into the parent's col / val; the pieces' work items together cover
+    every nonzero of the parent once, in the same chunks."""
+    from rsx import ops
+    from rsx.dist import head_pieces_knob
+
+    rng = np.random.default_rng(5)
+    deg = np.concatenate([rng.integers(0, 12, 300), [0, 33, 64, 65, 200, 1000]])
+    rng.shuffle(deg)
+    rowptr = np.concatenate([[0], np.cumsum(deg)]).astype(np.int64)
+    nnz = int(rowptr[-1])
+    col = rng.integers(0, 500, nnz).astype(np.int32)
+    val = rng.random(nnz).astype(np.float32)
+    parent = ops.DeviceCSR(rowptr, col, val, 500, "cpu", chunk=32)
+    cuts = [0, 77, 150, 151, rowptr.size - 1]
+    seen = np.zeros(nnz, np.int32)
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        piece = ops.DeviceCSR.row_slice(parent, a, b)
+        assert piece.n_rows == b - a and piece.col is parent.col and piece.val is parent.val
+        work = piece.work.numpy()[: piece.n_work]
+        lr = piece.long_rows.numpy()[: piece.n_long]
+        n_chunks = int(lr[:, 2].sum()) if piece.n_long else 0
+        for i, (x, slot, s, e) in enumerate(work):
+            r = (lr[x, 0] if i < n_chunks else x) + a  # the parent's row
+            assert rowptr[r] <= s <= e <= rowptr[r + 1] and e - s <= 32
+            seen[s:e] += 1
+    assert (seen == 1).all()
+    assert head_pieces_knob(4) == 4
+    import os
+
+    os.environ["RSX_SHARDED_HEAD"] = "x"
+    try:
+        with pytest.raises(ValueError):
+            head_pieces_knob(4)
+    finally:
+        del os.environ["RSX_SHARDED_HEAD"]
