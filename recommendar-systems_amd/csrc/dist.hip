@@ -102,18 +102,6 @@ struct rsx_comm_s {
 
 namespace rsx {
 
-// The communicator's stream at the device's greatest priority (RSX_COMM_PRIORITY=0: the
-// default priority): a collective queued behind a chip-filling product gets its
-// workgroups dispatched as soon as slots free up, instead of after that product's queued
-// blocks (RCCL's kernels, and the latency-injected stand-in, hold a few dozen CUs).
-hipError_t comm_stream_create(hipStream_t* s) {
-    static const int64_t prio_on = env_knob("RSX_COMM_PRIORITY", 1, 0, 1);
-    int least = 0, greatest = 0;
-    if (prio_on && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
-        return hipStreamCreateWithPriority(s, hipStreamNonBlocking, greatest);
-    return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
-}
-
 int comm_rank(rsx_comm_t c) { return c->rank; }
 int comm_world(rsx_comm_t c) { return c->world; }
 // The stream the communicator's exchanges run on (host-hook communicators: the caller's):
@@ -174,8 +162,12 @@ hipEvent_t collective(rsx_comm_t c, int op, void* buf, int64_t count, int dtype,
     hipError_t e;
     hipEvent_t j = c->join[c->next];
     c->next = (c->next + 1) % kJoinEvents;
+    // a call issued on the comm stream itself (work queued behind an earlier exchange) needs no
+    // fork: a stream waiting on its own event breaks HIP graph capture (instantiation fault)
+    const bool fork = s != c->stream;
     if (c->sim_world) {  // one rank: the data is already the result; the time is injected
-        if ((e = hipEventRecord(c->fork, s)) != hipSuccess || (e = hipStreamWaitEvent(c->stream, c->fork, 0)) != hipSuccess) {
+        if (fork && ((e = hipEventRecord(c->fork, s)) != hipSuccess ||
+                     (e = hipStreamWaitEvent(c->stream, c->fork, 0)) != hipSuccess)) {
             *rc = hip_rc(e);
             return nullptr;
         }
@@ -208,7 +200,8 @@ hipEvent_t collective(rsx_comm_t c, int op, void* buf, int64_t count, int dtype,
         }
         return j;
     }
-    if ((e = hipEventRecord(c->fork, s)) != hipSuccess || (e = hipStreamWaitEvent(c->stream, c->fork, 0)) != hipSuccess) {
+    if (fork && ((e = hipEventRecord(c->fork, s)) != hipSuccess ||
+                 (e = hipStreamWaitEvent(c->stream, c->fork, 0)) != hipSuccess)) {
         *rc = hip_rc(e);
         return nullptr;
     }
@@ -631,8 +624,9 @@ int sharded_stored_layers(const rsx_sharded_lgcn_step& st, bool train, hipStream
             // they read only its output and the item rows of p / m / v, which nothing on the
             // compute stream touches now (the user Adam there updates user rows), so the
             // all-gather no longer waits for the user-row Adam product
-            hipStream_t cs = comm_stream(st.comm, s);
-            if (cs != s) RSX_TRY(wait(cs, jt));
+            static const int64_t on_comm = env_knob("RSX_SHARDED_COMM_ADAM", 1, 0, 1);
+            hipStream_t cs = on_comm ? comm_stream(st.comm, s) : s;  // (jt completes on cs itself)
+            if (cs == s) RSX_TRY(wait(s, jt));
             if (nown > 0) RSX_TRY(rowwise_dispatch(nown, d, a, cs));
             hipEvent_t jp = collective(st.comm, RSX_COLL_ALLGATHER, st.p + off, q * d, RSX_COLL_F32, cs, &rc);
             if (!jp) return rc;
@@ -903,7 +897,7 @@ int rsx_comm_init(rsx_comm_t* out, const void* id_host, int32_t rank, int32_t wo
     c->world = world;
     ncclUniqueId id;
     memcpy(&id, id_host, sizeof(id));
-    hipError_t e = rsx::comm_stream_create(&c->stream);
+    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork, hipEventDisableTiming);
     for (int i = 0; e == hipSuccess && i < rsx::kJoinEvents; ++i)
         e = hipEventCreateWithFlags(&c->join[i], hipEventDisableTiming);
@@ -956,7 +950,7 @@ int rsx_comm_init_sim(rsx_comm_t* out, int32_t sim_world, double busbw_gbs, doub
     c->sim_scratch_floats = scratch_mb * (1 << 20) / 4;
     if (e == hipSuccess) e = hipMalloc(&c->sim_scratch, (size_t)c->sim_scratch_floats * 4);
     if (e == hipSuccess) e = hipMemset(c->sim_scratch, 0, (size_t)c->sim_scratch_floats * 4);
-    if (e == hipSuccess) e = rsx::comm_stream_create(&c->stream);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork, hipEventDisableTiming);
     for (int i = 0; e == hipSuccess && i < rsx::kJoinEvents; ++i)
         e = hipEventCreateWithFlags(&c->join[i], hipEventDisableTiming);

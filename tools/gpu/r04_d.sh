@@ -1,5 +1,5 @@
 # round 4, batch D: the sharded-step GPU tests (neighbour-row exchange of the last forward
-# layer, high-priority comm stream), then C4 under latency injection: W = 8 with / without
+# layer, owner Adam on the comm stream), then C4 under latency injection: W = 8 with / without
 # the neighbour exchange and graph-replayed / eager, W = 4 and 2, and a W = 8 step trace
 set -o pipefail
 cd $GRAFT_REPO_ROOT
@@ -21,7 +21,7 @@ print('$name', 'ms/step', round(d['ms_per_step'], 3), li.get('measured_allreduce
 run sim_w8 RSX_COMM_SIM=8 || exit 1
 run sim_w8_eager RSX_COMM_SIM=8 RSX_SHARDED_GRAPH=0 || exit 1
 run sim_w8_nonbr RSX_COMM_SIM=8 RSX_SHARDED_NBR=0 || exit 1
-run sim_w8_lowprio RSX_COMM_SIM=8 RSX_COMM_PRIORITY=0 || exit 1
+run sim_w8_adam_compute RSX_COMM_SIM=8 RSX_SHARDED_COMM_ADAM=0 || exit 1
 run sim_w8_head1 RSX_COMM_SIM=8 RSX_SHARDED_HEAD=1 || exit 1
 run sim_w4 RSX_COMM_SIM=4 || exit 1
 run sim_w2 RSX_COMM_SIM=2 || exit 1
