@@ -255,13 +255,14 @@ class ShardedLightGCNEngine:
         if (not self.sparse and self.row_tag is not None and self.K in (2, 3)
                 and os.environ.get("RSX_SHARDED_FUSED", "0") == "1"):
             self.xch = torch.zeros(2 * self.n_items, self.d, dtype=torch.float32, device=self.be.device)
-        # the step's head in row pieces (rsx_sharded_lgcn_step.n_head): the first item
-        # partial's rows all-reduced piece by piece, so the first exchange starts after
-        # 1/n_head of that product.  Default: 4 in the bandwidth regime (the sparse
-        # schedule: C4's 1 GB item block, where one product is ~2 ms per 1.25M users),
-        # off where latency bounds the exchanges (C2); RSX_SHARDED_HEAD overrides.
+        # the step's heads in row pieces (rsx_sharded_lgcn_step.n_head): the first forward
+        # and backward item partials' rows all-reduced piece by piece.  Off by default: in
+        # the graph-replayed C4 step at a modelled 8-rank job (latency injection) 4 pieces
+        # took 28.5 ms/step against 25.2 without (the replay spreads the extra launches and
+        # collectives over the hardware queues, and a piece can queue behind an exchange);
+        # RSX_SHARDED_HEAD=n turns them on.
         self.head = []
-        n_head = head_pieces_knob(4 if self.sparse else 1)
+        n_head = head_pieces_knob(1)
         if n_head > 1 and self.row_tag is not None and self.xch is None and self.A_I.rowptr_host is not None:
             # cut by the GLOBAL item degrees (every rank the same pieces: the collectives match)
             rp = np.concatenate([[0], np.cumsum(self._deg_i_global)])

@@ -24,12 +24,12 @@ run() {  # name, timeout, env..., -- args
 }
 if [ "${PART:-1}" = 1 ]; then
 EXTRA="" run sim_w8 500 RSX_COMM_SIM=8 || exit 1
-EXTRA="" run sim_w8_head1 500 RSX_COMM_SIM=8 RSX_SHARDED_HEAD=1 || exit 1
-EXTRA="--c4-chunks 1 --batch 256" run compute_w8 500 RSX_SHARDED_HEAD=1 || exit 1
+EXTRA="" run sim_w8_head4 500 RSX_COMM_SIM=8 RSX_SHARDED_HEAD=4 || exit 1
+EXTRA="--c4-chunks 1 --batch 256" run compute_w8 500 RSX_X=0 || exit 1
 EXTRA="" run sim_w4 600 RSX_COMM_SIM=4 || exit 1
-EXTRA="--c4-chunks 2 --batch 512" run compute_w4 600 RSX_SHARDED_HEAD=1 || exit 1
+EXTRA="--c4-chunks 2 --batch 512" run compute_w4 600 RSX_X=0 || exit 1
 EXTRA="" run sim_w2 800 RSX_COMM_SIM=2 || exit 1
-EXTRA="--c4-chunks 4 --batch 1024" run compute_w2 800 RSX_SHARDED_HEAD=1 || exit 1
+EXTRA="--c4-chunks 4 --batch 1024" run compute_w2 800 RSX_X=0 || exit 1
 fi
 if [ "${PART:-1}" = 2 ]; then
 # the N = 1 anchor: the whole 10M-user graph on one GPU, with its CPU baseline
