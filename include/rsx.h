@@ -942,9 +942,19 @@ typedef struct rsx_sharded_lgcn_step {
     int32_t* nbr_count;         /* [1] */
     float* cbufN;               /* [world nbr_cap, d] */
     int64_t nbr_cap;
+    /* optional with the sparse exchange: 1 = the all-gather of the owners' updated item rows
+     * is issued at the START of the next step (on the comm stream, waited on only before the
+     * first product that reads item rows of p, so it overlaps the first item partial) instead
+     * of at the end of this one.  Between steps the item rows owned by other ranks are then
+     * one step old on this rank: call rsx_sharded_lightgcn_flush before reading p (forward,
+     * evaluation, checkpoints).  Issuing it when nothing is pending is harmless (idempotent). */
+    int32_t defer_ag;
+    int32_t pad2;
 } rsx_sharded_lgcn_step;
 
 int rsx_sharded_lightgcn_step(const rsx_sharded_lgcn_step* st, rsx_stream_t stream);
+/* the deferred parameter all-gather of a defer_ag step (see above), stream-ordered */
+int rsx_sharded_lightgcn_flush(const rsx_sharded_lgcn_step* st, rsx_stream_t stream);
 int rsx_sharded_lightgcn_forward(const rsx_sharded_lgcn_step* st, rsx_stream_t stream);
 
 /* ------------------------------------------------------------------------ */

@@ -403,6 +403,13 @@ int sharded_stored_layers(const rsx_sharded_lgcn_step& st, bool train, hipStream
         RSX_TRY(last_rc());
         if (!(jN = collective(st.comm, RSX_COLL_ALLGATHER, st.nbr_items, st.nbr_cap, RSX_COLL_I64, s, &rc))) return rc;
     }
+    // the previous step's owner rows, all-gathered while the first item partial runs (that
+    // product reads user rows only); waited on before the first product reading item rows
+    hipEvent_t jAG = nullptr;
+    if (sparse && st.defer_ag) {
+        const int64_t q = st.n_items_pad / st.comm->world;
+        if (!(jAG = collective(st.comm, RSX_COLL_ALLGATHER, st.p + off, q * d, RSX_COLL_F32, s, &rc))) return rc;
+    }
     // ---- forward (the first item partial's launch also tags the batch rows when training)
     const float* x = st.p;
     for (int k = 1; k < K; ++k) {
@@ -439,6 +446,7 @@ int sharded_stored_layers(const rsx_sharded_lgcn_step& st, bool train, hipStream
             if (!(joins[k] = exchange(st.comm, bufs[k - 1] + off, ni * d, s, &rc))) return rc;
         }
         if (k >= 2) RSX_TRY(wait(s, joins[k - 1]));                  // E^{k-1} items summed
+        if (k == 1 && jAG) RSX_TRY(wait(s, jAG));                     // p's item rows current
         e.y = bufs[k - 1];
         RSX_TRY(spmm_dispatch(*st.adj_u, x, d, e, st.slab_u, s));   // E^k user rows
         x = bufs[k - 1];
@@ -628,9 +636,17 @@ int sharded_stored_layers(const rsx_sharded_lgcn_step& st, bool train, hipStream
             hipStream_t cs = on_comm ? comm_stream(st.comm, s) : s;  // (jt completes on cs itself)
             if (cs == s) RSX_TRY(wait(s, jt));
             if (nown > 0) RSX_TRY(rowwise_dispatch(nown, d, a, cs));
-            hipEvent_t jp = collective(st.comm, RSX_COLL_ALLGATHER, st.p + off, q * d, RSX_COLL_F32, cs, &rc);
-            if (!jp) return rc;
-            RSX_TRY(wait(s, jp));  // the next step (and any reader) sees every updated replica
+            if (st.defer_ag) {  // the all-gather opens the next step (or rsx_sharded_lightgcn_flush)
+                if (cs != s) {
+                    hipEvent_t ja = comm_event(st.comm);
+                    RSX_TRY(hip_rc(hipEventRecord(ja, cs)));
+                    RSX_TRY(wait(s, ja));
+                }
+            } else {
+                hipEvent_t jp = collective(st.comm, RSX_COLL_ALLGATHER, st.p + off, q * d, RSX_COLL_F32, cs, &rc);
+                if (!jp) return rc;
+                RSX_TRY(wait(s, jp));  // the next step (and any reader) sees every updated replica
+            }
         } else {
             rsx_epilogue a = epi(RSX_EPI_ADAM);  // item rows, identical on every rank
             a.s_in = st.t;
@@ -1020,6 +1036,19 @@ int rsx_sharded_lightgcn_forward(const rsx_sharded_lgcn_step* st, rsx_stream_t s
     if (st->row_tag && (st->n_layers == 2 || st->n_layers == 3))
         return rsx::sharded_stored_layers(*st, false, rsx::as_stream(stream));
     return rsx::sharded_forward(*st, false, rsx::as_stream(stream));
+}
+
+int rsx_sharded_lightgcn_flush(const rsx_sharded_lgcn_step* st, rsx_stream_t stream) {
+    using namespace rsx;
+    if (!valid(st)) return RSX_ERR_ARG;
+    if (!st->union_items || !st->defer_ag) return RSX_OK;  // nothing is ever deferred
+    hipStream_t s = as_stream(stream);
+    int rc = 0;
+    const int64_t q = st->n_items_pad / st->comm->world;
+    hipEvent_t j = collective(st->comm, RSX_COLL_ALLGATHER, st->p + st->n_users * (int64_t)st->d, q * st->d,
+                              RSX_COLL_F32, s, &rc);
+    if (!j) return rc;
+    return wait(s, j);
 }
 
 int rsx_sharded_lightgcn_step(const rsx_sharded_lgcn_step* st, rsx_stream_t stream) {

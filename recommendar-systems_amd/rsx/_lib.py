@@ -92,7 +92,7 @@ class ShardedStep(C.Structure):
                 ("comm", P), ("row_tag", P), ("tag", I64), ("tag_dev", P), ("reg_cnt", P),
                 ("union_items", P), ("item_tag", P), ("cbuf0", P), ("cbuf1", P), ("n_items_pad", I64), ("union_cap", I64),
                 ("xch", P), ("n_head", I32), ("pad1", I32), ("head_i", C.POINTER(Csr)), ("head_row0", P),
-                ("head_slab", P), ("nbr_items", P), ("nbr_count", P), ("cbufN", P), ("nbr_cap", I64)]
+                ("head_slab", P), ("nbr_items", P), ("nbr_count", P), ("cbufN", P), ("nbr_cap", I64), ("defer_ag", I32), ("pad2", I32)]
 
 
 class DpStep(C.Structure):
@@ -161,6 +161,7 @@ def _declare(lib):
         "rsx_comm_allreduce_f32": (C.c_int, [P, P, I64, P]),
         "rsx_sharded_lightgcn_step": (C.c_int, [C.POINTER(ShardedStep), P]),
         "rsx_sharded_lightgcn_forward": (C.c_int, [C.POINTER(ShardedStep), P]),
+        "rsx_sharded_lightgcn_flush": (C.c_int, [C.POINTER(ShardedStep), P]),
         "rsx_smore_gates": (C.c_int, [I32, P, P, P, P, I64, I32, F32, I32, P, P, P, P, P, P]),
         "rsx_smore_pref": (C.c_int, [I32, P, P, P, P, P, P, I64, I32, F32, P, P, P, P, P, P, P, P, P, P, P, P, P]),
         "rsx_smore_pref_rows": (C.c_int, [I32, P, P, P, P, P, P, P, I64, I32, F32, P, P, P, P, P, P, P, P, P, P, P,
@@ -208,7 +209,7 @@ EXPORTED = ["rsx_version", "rsx_csr_schedule_host", "rsx_csr_schedule_rebind", "
             "rsx_topk_metrics_ws_bytes", "rsx_topk_metrics", "rsx_topk_metrics_fast", "rsx_linear_wgrad_ws_bytes", "rsx_linear_wgrad", "rsx_linear_bwd_ws_bytes", "rsx_linear_bwd",
             "rsx_comm_unique_id_bytes", "rsx_comm_get_unique_id", "rsx_comm_init", "rsx_comm_destroy",
             "rsx_comm_init_host",
-            "rsx_comm_allreduce_f32", "rsx_sharded_lightgcn_step", "rsx_sharded_lightgcn_forward",
+            "rsx_comm_allreduce_f32", "rsx_sharded_lightgcn_step", "rsx_sharded_lightgcn_forward", "rsx_sharded_lightgcn_flush",
             "rsx_dp_lightgcn_step", "rsx_dp_block_floats", "rsx_comm_init_sim", "rsx_comm_sim_seconds",
             "rsx_comm_allgather_f32", "rsx_comm_allreduce_f32_start", "rsx_comm_wait",
             "rsx_smore_gates", "rsx_smore_pref", "rsx_smore_pref_rows", "rsx_smore_pref_rows_occ_floats", "rsx_tag_rows", "rsx_smore_wgrad_ws_bytes", "rsx_smore_wgrad",

@@ -198,7 +198,9 @@ class ShardedLightGCNEngine:
         p = torch.cat([torch.from_numpy(np.ascontiguousarray(user_emb, dtype=np.float32)), it,
                        torch.zeros(pad, d, dtype=torch.float32)])
         self._p_full = self.be.tensor(p)
-        self.p = self._p_full[: nu + ni]
+        self._p = self._p_full[: nu + ni]
+        self.defer_ag = False  # the native sparse step's deferred parameter all-gather (_init_native)
+        self._ag_dirty = False
         if hasattr(self.be, "zeros"):
             z = lambda rows=n: self.be.zeros(rows, d)  # noqa: E731
         else:
@@ -331,8 +333,14 @@ class ShardedLightGCNEngine:
         st.adj_u = C.pointer(self.A_U.struct)
         st.adj_i = C.pointer(self.A_I.struct)
         st.n_users, st.n_items, st.d, st.n_layers, st.reg = self.n_users, self.n_items, self.d, self.K, self.reg
-        for name in ("p", "m", "v", "s", "h0", "h1", "g", "r", "t"):
+        for name in ("m", "v", "s", "h0", "h1", "g", "r", "t"):
             setattr(st, name, getattr(self, name).data_ptr())
+        st.p = self._p.data_ptr()
+        # the parameter all-gather deferred to the next step (include/rsx.h defer_ag; the
+        # sparse schedule only; RSX_SHARDED_DEFER_AG=0 keeps it at the end of the step)
+        self.defer_ag = bool(self.sparse and self.row_tag is not None
+                             and os.environ.get("RSX_SHARDED_DEFER_AG", "1") != "0")
+        st.defer_ag = int(self.defer_ag)
         st.final_emb = self.final.data_ptr()
         su, si = self.A_U.slab(self.d), self.A_I.slab(self.d)
         st.slab_u = su.data_ptr() if su is not None else 0
@@ -483,6 +491,7 @@ class ShardedLightGCNEngine:
     def close(self):
         """Release the rsx communicator (before destroy_process_group)."""
         if self._comm is not None:
+            self.flush()
             self._graphs = {}  # the captured collectives belong to the communicator
             torch.cuda.synchronize(self.be.device)
             L.lib().rsx_comm_destroy(self._comm)
@@ -581,7 +590,7 @@ class ShardedLightGCNEngine:
         `union` (sparse schedule): the last layer's item rows are summed on those
         rows only (the final item rows elsewhere are left unsummed: nothing reads them)."""
         be, nu, ni, d, K = self.be, self.n_users, self.n_items, self.d, self.K
-        p, s, f = self.p, self.s, self.final
+        p, s, f = self._p, self.s, self.final
         bufs = (self.h0, self.h1)
         beta = 1.0 / (K + 1)
         ys = [p] + [bufs[(k - 1) & 1] for k in range(1, K + 1)]  # ys[k]: users^k | items^k
@@ -616,7 +625,22 @@ class ShardedLightGCNEngine:
                     self.g[nu:].zero_()
                     self.r[nu:].zero_()
 
+    @property
+    def p(self):
+        """The [users; items] parameter table (deferred item rows all-gathered first)."""
+        self.flush()
+        return self._p
+
+    def flush(self):
+        """Complete a deferred parameter all-gather (defer_ag: the sparse native step issues
+        it at the start of the next step), so every replica's item rows are current."""
+        if self._ag_dirty and self._comm is not None:
+            L.check(L.lib().rsx_sharded_lightgcn_flush(C.byref(self._st), ops._stream()),
+                    "rsx_sharded_lightgcn_flush")
+        self._ag_dirty = False
+
     def forward(self):
+        self.flush()
         if not self._fwd_valid:
             if self.native:
                 L.check(L.lib().rsx_sharded_lightgcn_forward(C.byref(self._st), ops._stream()),
@@ -651,6 +675,7 @@ class ShardedLightGCNEngine:
         if self.native:
             self._native_step(triplets[:3])
             self._fwd_valid = False
+            self._ag_dirty = self.defer_ag
             return
         union = None
         if self.sparse:  # every rank's (pos, neg) ids, padded to the fixed slice with item 0
@@ -664,7 +689,7 @@ class ShardedLightGCNEngine:
             self._coll(L.RSX_COLL_ALLGATHER, self.union, 2 * cap)
             union = self.union
         self._propagate(zero_grads=True, union=union)
-        self.loss_out = be.bpr(self.final, self.p, nu, ni, triplets, self.reg, self.g, self.r, self.loss_acc)
+        self.loss_out = be.bpr(self.final, self._p, nu, ni, triplets, self.reg, self.g, self.r, self.loss_acc)
         adam = be.adam(self.lr, self.step_count, self.wd)
         beta = 1.0 / (K + 1)
         g, s, r, t = self.g, self.s, self.r, self.t
@@ -702,11 +727,11 @@ class ShardedLightGCNEngine:
                 be.rowwise(ni, d, L.RSX_EPI_ADD, y=s[nu:], s_in=s_in[nu:], r_add=ys[k][nu:])
             else:
                 be.spmm(self.A_U, ys[k - 1], d, L.RSX_EPI_ADAM, beta=beta, adam=adam, s_in=s_in[:nu], r_add=r[:nu],
-                        p=self.p[:nu], m=self.m[:nu], v=self.v[:nu])
+                        p=self._p[:nu], m=self.m[:nu], v=self.v[:nu])
                 if union is None:
                     works.pop(k).wait()
                     be.rowwise(ni, d, L.RSX_EPI_ADAM, beta=beta, adam=adam, s_in=s_in[nu:], r_add=t[:ni],
-                               p=self.p[nu:], m=self.m[nu:], v=self.v[nu:])
+                               p=self._p[nu:], m=self.m[nu:], v=self.v[nu:])
                 else:  # reduce-scatter the item gradient; Adam on this rank's item rows; all-gather them
                     q = self.q
                     self._coll(L.RSX_COLL_REDUCESCATTER, t.view(-1), q * d)
@@ -715,6 +740,6 @@ class ShardedLightGCNEngine:
                     if r1 > r0:
                         sl = slice(nu + r0, nu + r1)
                         be.rowwise(r1 - r0, d, L.RSX_EPI_ADAM, beta=beta, adam=adam, s_in=s_in[sl],
-                                   r_add=t[r0:r1], p=self.p[sl], m=self.m[sl], v=self.v[sl])
+                                   r_add=t[r0:r1], p=self._p[sl], m=self.m[sl], v=self.v[sl])
                     self._coll(L.RSX_COLL_ALLGATHER, self._p_full[nu:].view(-1), q * d)
         self._fwd_valid = False

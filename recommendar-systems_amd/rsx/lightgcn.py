@@ -248,6 +248,14 @@ class LightGCN(GeneralRecommender):
             return
         self.engine.step_slice(epoch, i, self.steps_per_epoch)
 
+    def state_dict(self, *args, **kwargs):
+        """The parameters as the reference's state dict; the sharded engine's deferred item
+        rows are all-gathered first (rsx.dist.ShardedLightGCNEngine.flush)."""
+        eng = self.__dict__.get("engine")
+        if eng is not None and hasattr(eng, "flush"):
+            eng.flush()
+        return super().state_dict(*args, **kwargs)
+
     def full_sort_topk_local(self, eval_users: torch.Tensor, k: int, eval_data):
         """(row positions in eval_users, top-k item ids) for this rank's evaluation users
         (global ids in [user_range)), ranked against every item with the training mask."""
