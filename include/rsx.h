@@ -983,7 +983,10 @@ typedef struct rsx_dp_lgcn_step {
     int64_t n_users, n_items;
     int32_t d, n_layers;        /* n_layers 2..4 */
     float reg;
-    int32_t pad0;
+    /* nonzero: the step's first launch increments *adam.step_dev itself (whose low word
+     * is then tag_dev), so a captured step needs no separate counter launch; zero: the
+     * caller has already incremented it */
+    int32_t inc_step;
     float* p; float* m; float* v;
     float* s; float* h0; float* h1;   /* E^1, E^2 (h0, h1), E^3 (s, K = 4 only) */
     float* final_emb; float* g;

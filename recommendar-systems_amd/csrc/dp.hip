@@ -48,12 +48,14 @@ namespace {
 constexpr int kHdr = 8;  // block header: four f64 loss totals
 
 // slot = [B, users[cap], positives[cap], negatives[cap]] (tail zero)
+// (step: the Adam counter the step increments first, or NULL)
 __global__ __launch_bounds__(256) void dp_pack(const int64_t* __restrict__ trip, int64_t B, int64_t cap,
-                                               int64_t* __restrict__ slot) {
+                                               int64_t* __restrict__ slot, int64_t* __restrict__ step) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i > 3 * cap) return;
     if (i == 0) {
         slot[0] = B;
+        if (step) step[0] += 1;
         return;
     }
     const int64_t j = i - 1, k = j / cap, t = j - k * cap;
@@ -184,7 +186,7 @@ int dp_step(const rsx_dp_lgcn_step& st, hipStream_t s) {
     // (1) this rank's triplets into its slot; every rank's gathered while the forward runs,
     // then indexed (union tags, counts, pos) on the comm stream
     hipLaunchKernelGGL(dp_pack, dim3((unsigned)((L + 255) / 256)), dim3(256), 0, s, st.triplets, B, cap,
-                       st.slots + rank * L);
+                       st.slots + rank * L, st.inc_step ? const_cast<int64_t*>(st.adam.step_dev) : nullptr);
     DP_TRY(last_rc());
     if (!collective(st.comm, RSX_COLL_ALLGATHER, st.slots, L, RSX_COLL_I64, s, &rc)) return rc;
     hipStream_t cs = comm_stream(st.comm, s);
@@ -300,6 +302,8 @@ bool dp_valid(const rsx_dp_lgcn_step* st) {
     if (st->adj->n_rows != st->n_users + st->n_items || st->adj->n_cols != st->adj->n_rows) return false;
     if (st->adj->n_long > 0 && !st->slab) return false;
     if (3 * st->cap > 0x7fffffffll) return false;  // occurrence index in pos's low word
+    if (st->inc_step && (!st->adam.step_dev || (const void*)st->adam.step_dev != (const void*)st->tag_dev))
+        return false;  // the incremented counter is the tag every later launch reads
     return true;
 }
 

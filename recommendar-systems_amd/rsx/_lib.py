@@ -97,7 +97,7 @@ class ShardedStep(C.Structure):
 
 class DpStep(C.Structure):
     _fields_ = [("adj", C.POINTER(Csr)), ("n_users", I64), ("n_items", I64), ("d", I32), ("n_layers", I32),
-                ("reg", F32), ("pad0", I32), ("p", P), ("m", P), ("v", P), ("s", P), ("h0", P), ("h1", P),
+                ("reg", F32), ("inc_step", I32), ("p", P), ("m", P), ("v", P), ("s", P), ("h0", P), ("h1", P),
                 ("final_emb", P), ("g", P), ("slab", P), ("triplets", P), ("batch", I64), ("adam", Adam),
                 ("loss_out", P), ("loss_acc", P), ("ws", P), ("ws_bytes", C.c_size_t), ("comm", P),
                 ("row_tag", P), ("own_tag", P), ("tag_dev", P), ("reg_cnt", P), ("halt", P), ("cap", I64),

@@ -151,6 +151,7 @@ class DataParallelLightGCNEngine:
         st.comm = self._comm.value
         st.row_tag, st.own_tag = self.row_tag.data_ptr(), self.own_tag.data_ptr()
         st.tag_dev = self._step_dev.data_ptr()
+        st.inc_step = 1  # dp_pack increments the counter (no separate add launch a step)
         st.reg_cnt, st.halt = self.reg_cnt.data_ptr(), self.halt.data_ptr()
         st.cap = cap
         st.slots, st.blocks, st.pos = self.slots.data_ptr(), self.blocks.data_ptr(), self.pos.data_ptr()
@@ -208,7 +209,6 @@ class DataParallelLightGCNEngine:
             gc.disable()
             try:
                 with torch.cuda.graph(g):
-                    self._step_dev.add_(1)
                     L.check(lib.rsx_dp_lightgcn_step(C.byref(st), ops._stream()), "rsx_dp_lightgcn_step")
             except Exception:  # noqa: BLE001  capture refused: eager from now on
                 self.use_graph = False
@@ -224,7 +224,6 @@ class DataParallelLightGCNEngine:
         t = triplets[:3].contiguous()
         self._keep = t
         st.triplets, st.batch = t.data_ptr(), B
-        self._step_dev.add_(1)
         L.check(lib.rsx_dp_lightgcn_step(C.byref(st), ops._stream()), "rsx_dp_lightgcn_step")
         self._warm.add(B)
         self._fwd_valid = False
