@@ -187,6 +187,10 @@ __global__ __launch_bounds__(256) void wgrad_partial(const float* __restrict__ g
         for (int u = 0; u < 8; ++u)
 #pragma unroll
             for (int q = 0; q < IG; ++q) acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv[u][q], acc[q], 0, 0, 0);
+        // every LDS operand read issued before the first MFMA (one latency per step, not
+        // one per MFMA pair)
+        __builtin_amdgcn_sched_group_barrier(0x100, 8 + 8 * IG, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 8 * IG, 0);
         if constexpr (DX) {
             if (db_blk) {
 #pragma unroll
@@ -204,11 +208,22 @@ __global__ __launch_bounds__(256) void wgrad_partial(const float* __restrict__ g
                 const float* wb = wl + q4 * WP + nt * 16 + n16;
                 typedef float floatx4_t __attribute__((ext_vector_type(4)));
                 floatx4_t d0 = {0.f, 0.f, 0.f, 0.f}, d1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 8
-                for (int k = 0; k < OC; k += 8) {
-                    d0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ga[k], wb[k * WP], d0, 0, 0, 0);
-                    d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ga[k + 4], wb[(k + 4) * WP], d1, 0, 0, 0);
+                // the tile's OC/4 operand pairs read from LDS ahead of its MFMAs (a read per
+                // MFMA pair waited on one at a time left the 16x16x4 chain latency-bound);
+                // d0 takes k = 0, 8, ..., d1 k = 4, 12, ... as before
+                float ar[OC / 4], br[OC / 4];
+#pragma unroll
+                for (int k = 0; k < OC / 4; ++k) {
+                    ar[k] = ga[4 * k];
+                    br[k] = wb[4 * k * WP];
                 }
+#pragma unroll
+                for (int k = 0; k < OC / 4; k += 2) {
+                    d0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ar[k], br[k], d0, 0, 0, 0);
+                    d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ar[k + 1], br[k + 1], d1, 0, 0, 0);
+                }
+                __builtin_amdgcn_sched_group_barrier(0x100, OC / 2, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, OC / 4, 0);
                 const floatx4_t d = d0 + d1;
                 // lane holds rows 4 q4 + r of the tile, column n16
 #pragma unroll

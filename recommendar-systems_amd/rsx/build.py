@@ -30,16 +30,27 @@ def _hipcc() -> str:
     raise RuntimeError("hipcc not found: librsx.so needs ROCm's hipcc (gfx950)")
 
 
-def _flags():
+# Per-source code-generation flags.  -amdgpu-mfma-vgpr-form: MFMA accumulators in the
+# architectural VGPRs.  Without it the register allocator keeps a loop-carried
+# accumulator in VGPRs and copies it into AGPRs and back around every MFMA block
+# (wgrad_partial<2,4,DX>: 64 v_accvgpr moves per two-chunk step, 156 VGPRs + AGPRs);
+# with it the kernel has no AGPR traffic and 118 VGPRs.  Same instructions otherwise,
+# so the results are bit-identical.
+SOURCE_FLAGS = {
+    "linear.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"],
+}
+
+
+def _flags(src: str | None = None):
     return [f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", f"-I{INCLUDE}", f"-I{CSRC}",
-            "-Wno-unused-result"]
+            "-Wno-unused-result", *SOURCE_FLAGS.get(src, [])]
 
 
 def _needs_build() -> bool:
     if not os.path.exists(LIB):
         return True
     t = os.path.getmtime(LIB)
-    deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + [os.path.join(INCLUDE, "rsx.h")]
+    deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + [os.path.join(INCLUDE, "rsx.h"), __file__]
     return any(os.path.getmtime(p) > t for p in deps if os.path.isfile(p))
 
 
@@ -54,7 +65,7 @@ def build(force: bool = False, verbose: bool = True) -> str:
 
     def compile_one(src):
         obj = os.path.join(objdir, src.replace(".hip", ".o"))
-        cmd = [hipcc, *_flags(), "-c", os.path.join(CSRC, src), "-o", obj]
+        cmd = [hipcc, *_flags(src), "-c", os.path.join(CSRC, src), "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")

@@ -1,4 +1,5 @@
-"""Build a variant of librsx.so with extra -D flags into rsx/lib/variants/<name>/
+"""Build a variant of librsx.so with extra flags (-D..., -mllvm ...) on every source into
+rsx/lib/variants/<name>/
 (for side-by-side timing on the GPU box via RSX_LIB=...).
 usage: python tools/build_variant.py NAME -DFOO=1 [-DBAR=2 ...]"""
 import os
@@ -14,7 +15,7 @@ os.makedirs(out, exist_ok=True)
 objs = []
 for src in B.SOURCES:
     obj = os.path.join(out, src.replace(".hip", ".o"))
-    subprocess.run([B._hipcc(), *B._flags(), *defs, "-c", os.path.join(B.CSRC, src), "-o", obj], check=True)
+    subprocess.run([B._hipcc(), *B._flags(src), *defs, "-c", os.path.join(B.CSRC, src), "-o", obj], check=True)
     objs.append(obj)
 subprocess.run([B._hipcc(), f"--offload-arch={B.ARCH}", "-shared", "-fPIC", "-o", os.path.join(out, "librsx.so"), "-ldl",
                 *objs], check=True)
