@@ -790,43 +790,97 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
 // The per-occurrence row gradients of pref_bwd_rows summed per table row, deterministic:
 // one wave per occurrence j; the first occurrence of its row (no earlier j' with the same
 // row: a ballot scan) sums every occurrence of the row in ascending order, each
-// occurrence's shares in slot order, and stores the row of gC / gIE / gTE / gFE.  The
-// rows array is 3B entries (L2 resident); a leader's scan is n / 64 ballots.
-template <int D>
-__global__ __launch_bounds__(256) void pref_segsum(const int64_t* __restrict__ rows, int64_t n,
-                                                   const float* __restrict__ occ, float* __restrict__ gC,
-                                                   float* __restrict__ gIE, float* __restrict__ gTE,
-                                                   float* __restrict__ gFE) {
+// occurrence's shares in slot order, and stores the row of gC / gIE / gTE / gFE.  Both
+// scans test U chunks of 64 rows per step (loads in flight together: a chunk at a time
+// made every wave a chain of ~n / 64 dependent round trips).  The row ids come from
+// `RowAt`: the global int64 array, or (pref_segsum_lds) the block's int32 copy in LDS.
+constexpr int kSegList = 128;  // a wave's occurrence list (LDS int32)
+template <int D, typename RowAt>
+__device__ __forceinline__ void segsum_one(int64_t j, int64_t n, RowAt row_at, const float* __restrict__ occ,
+                                           float* __restrict__ gC, float* __restrict__ gIE, float* __restrict__ gTE,
+                                           float* __restrict__ gFE, int32_t* lst) {
     constexpr int PL = D / 64;  // columns per lane: lane + 64 p
+    constexpr int UC = 8, US = 4, UB = 4;
     const int lane = threadIdx.x & 63;
-    const int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (j >= n) return;
-    const int64_t x = rows[j];
-    for (int64_t c = 0; c < j; c += 64) {
-        const int64_t k = c + lane;
-        if (__ballot(k < j && rows[k] == x)) return;  // an earlier occurrence leads
+    const int64_t x = row_at(j);
+    for (int64_t c = 0; c < j; c += 64 * UC) {
+        int64_t r[UC];
+#pragma unroll
+        for (int u = 0; u < UC; ++u) {
+            const int64_t k = c + 64 * u + lane;
+            r[u] = k < j ? row_at(k) : -1;
+        }
+        bool hit = false;
+#pragma unroll
+        for (int u = 0; u < UC; ++u) hit |= r[u] == x;
+        if (__ballot(hit)) return;  // an earlier occurrence leads
     }
     const int64_t sl = n * D;
     float aC[PL], aF[PL], aI[PL], aT[PL];
 #pragma unroll
     for (int p = 0; p < PL; ++p) aC[p] = aF[p] = aI[p] = aT[p] = 0.f;
-    for (int64_t c = j; c < n; c += 64) {
-        const int64_t k = c + lane;
-        uint64_t m = __ballot(k < n && rows[k] == x);
-        while (m) {
-            const int b = __builtin_ctzll(m);
-            m &= m - 1;
-            const float* o = occ + (c + b) * D + lane;
+    // the row's occurrences are listed (ascending) in the wave's LDS list, then summed UB
+    // at a time with their loads issued together (a hot row's occurrences one by one were
+    // a chain of dependent loads: the launch's tail)
+    int cnt = 0;  // wave-uniform
+    auto flush = [&]() __attribute__((always_inline)) {
+        for (int i0 = 0; i0 < cnt; i0 += UB) {
+            float v[UB][8][PL];
 #pragma unroll
-            for (int p = 0; p < PL; ++p) {
-                const int64_t q = 64 * p;
-                aC[p] = ((aC[p] + o[kOccC0 * sl + q]) + o[kOccC3 * sl + q]) + o[kOccC4 * sl + q];
-                aF[p] = ((aF[p] + o[kOccF0 * sl + q]) + o[kOccF1 * sl + q]) + o[kOccF2 * sl + q];
-                aI[p] += o[kOccI * sl + q];
-                aT[p] += o[kOccT * sl + q];
+            for (int t = 0; t < UB; ++t) {
+                const int64_t k = i0 + t < cnt ? (int64_t)lst[i0 + t] : j;  // (a padded slot reloads j, unused)
+                const float* o = occ + k * D + lane;
+#pragma unroll
+                for (int p = 0; p < PL; ++p) {
+                    const int64_t q = 64 * p;
+                    v[t][0][p] = o[kOccC0 * sl + q];
+                    v[t][1][p] = o[kOccC3 * sl + q];
+                    v[t][2][p] = o[kOccC4 * sl + q];
+                    v[t][3][p] = o[kOccF0 * sl + q];
+                    v[t][4][p] = o[kOccF1 * sl + q];
+                    v[t][5][p] = o[kOccF2 * sl + q];
+                    v[t][6][p] = o[kOccI * sl + q];
+                    v[t][7][p] = o[kOccT * sl + q];
+                }
+            }
+#pragma unroll
+            for (int t = 0; t < UB; ++t) {
+                if (i0 + t >= cnt) break;
+#pragma unroll
+                for (int p = 0; p < PL; ++p) {
+                    aC[p] = ((aC[p] + v[t][0][p]) + v[t][1][p]) + v[t][2][p];
+                    aF[p] = ((aF[p] + v[t][3][p]) + v[t][4][p]) + v[t][5][p];
+                    aI[p] += v[t][6][p];
+                    aT[p] += v[t][7][p];
+                }
+            }
+        }
+        cnt = 0;
+    };
+    for (int64_t c0 = j; c0 < n; c0 += 64 * US) {
+        uint64_t mu[US];
+        {
+            int64_t r[US];
+#pragma unroll
+            for (int u = 0; u < US; ++u) {
+                const int64_t k = c0 + 64 * u + lane;
+                r[u] = k < n ? row_at(k) : -1;
+            }
+#pragma unroll
+            for (int u = 0; u < US; ++u) mu[u] = __ballot(r[u] == x);
+        }
+#pragma unroll
+        for (int u = 0; u < US; ++u) {  // the chunks in order: occurrences ascending
+            uint64_t m = mu[u];
+            while (m) {
+                const int b = __builtin_ctzll(m);
+                m &= m - 1;
+                if (lane == 0) lst[cnt] = (int32_t)(c0 + 64 * u + b);
+                if (++cnt == kSegList) flush();
             }
         }
     }
+    flush();
 #pragma unroll
     for (int p = 0; p < PL; ++p) {
         const int64_t col = x * D + lane + 64 * p;
@@ -835,6 +889,34 @@ __global__ __launch_bounds__(256) void pref_segsum(const int64_t* __restrict__ r
         gIE[col] = aI[p];
         gTE[col] = aT[p];
     }
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void pref_segsum(const int64_t* __restrict__ rows, int64_t n,
+                                                   const float* __restrict__ occ, float* __restrict__ gC,
+                                                   float* __restrict__ gIE, float* __restrict__ gTE,
+                                                   float* __restrict__ gFE) {
+    __shared__ int32_t lst[4][kSegList];
+    const int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (j >= n) return;
+    segsum_one<D>(j, n, [&](int64_t k) { return rows[k]; }, occ, gC, gIE, gTE, gFE, lst[threadIdx.x >> 6]);
+}
+
+// 16 occurrences a block share one int32 copy of the row ids in LDS (n <= kSegLds):
+// every wave's scans read LDS instead of re-reading the int64 ids from L2
+constexpr int kSegLds = 16384, kSegWaves = 16;
+template <int D>
+__global__ __launch_bounds__(64 * kSegWaves) void pref_segsum_lds(const int64_t* __restrict__ rows, int64_t n,
+                                                                  const float* __restrict__ occ,
+                                                                  float* __restrict__ gC, float* __restrict__ gIE,
+                                                                  float* __restrict__ gTE, float* __restrict__ gFE) {
+    __shared__ int32_t rl[kSegLds];
+    __shared__ int32_t lst[kSegWaves][kSegList];
+    for (int64_t k = threadIdx.x; k < n; k += 64 * kSegWaves) rl[k] = (int32_t)rows[k];
+    __syncthreads();
+    const int64_t j = (int64_t)blockIdx.x * kSegWaves + (threadIdx.x >> 6);
+    if (j >= n) return;
+    segsum_one<D>(j, n, [&](int64_t k) { return (int64_t)rl[k]; }, occ, gC, gIE, gTE, gFE, lst[threadIdx.x >> 6]);
 }
 
 // Batch-row tags (rsx_tag_rows): row_tag[rows[j]] = *tag_dev for every j (duplicates
@@ -1791,6 +1873,13 @@ int rsx_tag_rows(int32_t* row_tag, const int64_t* rows, int64_t n, const int32_t
     return last_rc();
 }
 
+// RSX_SEGSUM_GLOBAL=1: the per-row sums read the row ids from global memory even when
+// they fit the LDS copy (timing A/B; the two kernels give identical results)
+static bool seg_global() {
+    static const bool v = env_knob("RSX_SEGSUM_GLOBAL", 0, 0, 1) != 0;
+    return v;
+}
+
 int rsx_smore_pref_rows(int32_t backward, const float* const* W, const float* const* b, const float* content,
                         const float* image_emb, const float* text_emb, const float* fusion_emb, const int64_t* rows,
                         int64_t n, int32_t d, float p_drop, const int64_t* seed_dev, float* all_out,
@@ -1866,9 +1955,16 @@ int rsx_smore_pref_rows(int32_t backward, const float* const* W, const float* co
         default: return RSX_ERR_UNSUPPORTED;
     }
     if (occ) {  // the per-occurrence rows summed per table row (deterministic)
-        const dim3 sg((unsigned)((n + 3) / 4));
-        if (d == 64) hipLaunchKernelGGL(sf::pref_segsum<64>, sg, dim3(256), 0, s, rows, n, occ, g_content, g_image, g_text, g_fusion);
-        else hipLaunchKernelGGL(sf::pref_segsum<128>, sg, dim3(256), 0, s, rows, n, occ, g_content, g_image, g_text, g_fusion);
+        if (n > 0x7fffffffll) return RSX_ERR_UNSUPPORTED;  // occurrence indices listed as int32
+        if (n <= sf::kSegLds && !seg_global()) {  // row ids < 2^31 (table rows)
+            const dim3 sg((unsigned)((n + sf::kSegWaves - 1) / sf::kSegWaves)), sb(64 * sf::kSegWaves);
+            if (d == 64) hipLaunchKernelGGL(sf::pref_segsum_lds<64>, sg, sb, 0, s, rows, n, occ, g_content, g_image, g_text, g_fusion);
+            else hipLaunchKernelGGL(sf::pref_segsum_lds<128>, sg, sb, 0, s, rows, n, occ, g_content, g_image, g_text, g_fusion);
+        } else {
+            const dim3 sg((unsigned)((n + 3) / 4));
+            if (d == 64) hipLaunchKernelGGL(sf::pref_segsum<64>, sg, dim3(256), 0, s, rows, n, occ, g_content, g_image, g_text, g_fusion);
+            else hipLaunchKernelGGL(sf::pref_segsum<128>, sg, dim3(256), 0, s, rows, n, occ, g_content, g_image, g_text, g_fusion);
+        }
     }
     return last_rc();
 }

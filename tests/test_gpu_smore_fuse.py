@@ -129,7 +129,9 @@ def test_preference_vs_torch(cuda, d, n, p):
     _close(ea, m.ref(C_, IE, TE, FE, None)[0], "eval all")
 
 
-@pytest.mark.parametrize("d,N,n,p", [(64, 3000, 6144, 0.0), (128, 5000, 6144, 0.1), (128, 700, 999, 0.0)])
+# n = 20000 > the LDS copy's 16384 ids: pref_segsum's global-memory form
+@pytest.mark.parametrize("d,N,n,p", [(64, 3000, 6144, 0.0), (128, 5000, 6144, 0.1), (128, 700, 999, 0.0),
+                                     (64, 9000, 20000, 0.0)])
 def test_preference_rows_vs_torch_and_deterministic(cuda, d, N, n, p):
     """The batch-row preference block (rsx_smore_pref_rows with per-occurrence row
     gradients + pref_segsum): repeated rows (a batch's popular items), gradients of the
