@@ -832,7 +832,8 @@ double rsx_comm_sim_seconds(rsx_comm_t comm, int32_t op, double bytes);
 int rsx_comm_allreduce_f32(rsx_comm_t comm, float* buf, int64_t n, rsx_stream_t stream);
 /* The same all-reduce without the wait: the caller's stream goes on (work that does not
  * read buf overlaps the exchange) until rsx_comm_wait(comm, stream), which orders the
- * stream after the last started all-reduce (one in flight per communicator). */
+ * stream after the started all-reduce.  One in flight per communicator: a second start
+ * before the wait returns RSX_ERR_ARG (its join would otherwise replace the first's). */
 int rsx_comm_allreduce_f32_start(rsx_comm_t comm, float* buf, int64_t n, rsx_stream_t stream);
 int rsx_comm_wait(rsx_comm_t comm, rsx_stream_t stream);
 /* buf[r n, (r+1) n) := rank r's slice for every rank r (buf holds world * n floats), in
@@ -950,6 +951,12 @@ typedef struct rsx_sharded_lgcn_step {
      * evaluation, checkpoints).  Issuing it when nothing is pending is harmless (idempotent). */
     int32_t defer_ag;
     int32_t pad2;
+    /* optional [1] device int32, zero-filled: the sparse exchange's row lists never
+     * dereference an id outside [0, n_items); such an id sets bit 0 instead (the lists are
+     * built from the triplets, so it means a corrupt batch), and a neighbour list longer than
+     * nbr_cap sets bit 1 (impossible under the host bound: each distinct batch user is listed
+     * once).  The host reads it at its sync points (rsx.dist: flush / forward / close). */
+    int32_t* err;
 } rsx_sharded_lgcn_step;
 
 int rsx_sharded_lightgcn_step(const rsx_sharded_lgcn_step* st, rsx_stream_t stream);
@@ -1011,6 +1018,43 @@ typedef struct rsx_dp_lgcn_step {
 
 int rsx_dp_lightgcn_step(const rsx_dp_lgcn_step* st, rsx_stream_t stream);
 size_t rsx_dp_block_floats(int64_t cap, int32_t d);
+
+/* ------------------------------------------------------------------------ */
+/* CPU kernels (host memory): the CPU dispatch key of torch.ops.rsx.*        */
+/* ------------------------------------------------------------------------ */
+/*
+ * the custom operators carry CPU and HIP kernels, so the reference's
+ * CPU configuration (C1: "CPU PyTorch reference path, no GPU") runs through the same
+ * operator boundary.  Host pointers, synchronous, rows split over RSX_CPU_THREADS workers
+ * (default: the hardware threads); each output row is written by one worker in a fixed
+ * order (results independent of the thread count).  Same formulas as the HIP kernels:
+ *   rsx_cpu_spmm              y = A x (CSR, f32)                     torch.sparse.mm
+ *   rsx_cpu_propagate_mean    out = (x + A x + ... + A^K x) / (K+1)  lightgcn.py:117-130
+ *   rsx_cpu_layergcn_forward  out = sum_k c_k A E^{k-1}, c_k the cosine gate;
+ *                             zs [K][n][d], cs [K][n] optional saves  layergcn.py:127-140
+ *   rsx_cpu_layergcn_backward dx from G = d/d out and the saves (RSX_EPI_LAYERGCN_BWD)
+ *   rsx_cpu_bpr               rsx_bpr's variants; gradients ADDED     loss.py:33-61
+ *   rsx_cpu_fullsort_topk     rsx_fullsort_topk's contract (scores, mask -1e10, top-k in
+ *                             (score desc, item asc) order)          trainer.py:509-528
+ *   rsx_cpu_adam              torch.optim.Adam, `step` already incremented  trainer.py:238
+ */
+int rsx_cpu_spmm(const int64_t* rowptr, const int32_t* col, const float* val, int64_t n_rows, const float* x,
+                 int32_t d, float* y);
+int rsx_cpu_propagate_mean(const int64_t* rowptr, const int32_t* col, const float* val, int64_t n, const float* x,
+                           int32_t d, int32_t n_layers, float* out);
+int rsx_cpu_layergcn_forward(const int64_t* rowptr, const int32_t* col, const float* val, int64_t n, const float* x,
+                             int32_t d, int32_t n_layers, float* out, float* zs, float* cs);
+int rsx_cpu_layergcn_backward(const int64_t* rowptr, const int32_t* col, const float* val, int64_t n,
+                              const float* x, int32_t d, int32_t n_layers, const float* G, const float* zs,
+                              const float* cs, float* dx);
+int rsx_cpu_bpr(int32_t variant, const float* final_emb, const float* ego_emb, int64_t n_users, int64_t n_items,
+                int32_t d, const int64_t* triplets, int64_t batch, float reg, float batch_cfg, float* g_final,
+                float* g_ego, float* loss_out);
+int rsx_cpu_fullsort_topk(const float* user_emb, const int64_t* users, int64_t n_batch, const float* item_emb,
+                          int64_t n_items, int32_t d, const int64_t* mask_rowptr, const int32_t* mask_col, int32_t k,
+                          float* scores_out, int64_t* idx_out);
+int rsx_cpu_adam(float* p, const float* g, float* m, float* v, int64_t n, int64_t step, float lr, float beta1,
+                 float beta2, float eps, float weight_decay);
 
 #ifdef __cplusplus
 }

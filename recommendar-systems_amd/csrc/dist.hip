@@ -80,7 +80,13 @@ constexpr int kJoinEvents = 64;  // > 2K+2 exchanges in flight per step for any 
 
 struct rsx_comm_s {
     ncclComm_t nccl = nullptr;
-    hipStream_t stream = nullptr;  // exchanges run here, ordered
+    hipStream_t stream = nullptr;  // exchanges run here, ordered (eagerly issued steps)
+    // exchanges of a step being captured into a hipGraph run here instead: a stream at
+    // the default priority (nullptr when `stream` is one).  A captured fork / join on a
+    // greatest-priority stream made graph replays segfault in hipGraphLaunch (round 4 /
+    // round 5: the latency-injected sharded step, DESIGN.md §6 "The round-4 faults"),
+    // and a replayed graph's kernels do not run on the captured streams anyway
+    hipStream_t stream_cap = nullptr;
     hipEvent_t fork = nullptr;     // compute -> comm (waited right after it is recorded)
     hipEvent_t join[rsx::kJoinEvents] = {};
     int next = 0;
@@ -98,15 +104,47 @@ struct rsx_comm_s {
     double sim_tick_hz = 0.0; // the device wall clock
     float* sim_scratch = nullptr;
     int64_t sim_scratch_floats = 0;
+    // RSX_COMM_SIM_POISON=1 (tests): each stand-in collective overwrites its buffer with
+    // poison (f32 NaN / i64 -1) for the modelled time and restores it at the end, so a
+    // reader not ordered after the join sees NaN / an out-of-range id and a writer not
+    // ordered before the fork is overwritten by the restore: a stream-order race detector
+    int32_t sim_poison = 0;
+    float* sim_save = nullptr;  // [scratch floats / 2]: the poisoned buffer's saved words
 };
 
 namespace rsx {
 
+// The communicator's stream at the device's greatest priority (RSX_COMM_PRIORITY=0: the
+// default priority): a collective queued behind a chip-filling product gets its
+// workgroups dispatched as soon as slots free up, instead of after that product's queued
+// blocks (RCCL's kernels, and the latency-injected stand-in, hold a few dozen CUs).
+// Correctness never depends on it: every cross-stream read / write is fenced by the
+// fork / join events (tests/test_gpu_dist.py runs the poisoned stand-in with it on).
+hipError_t comm_streams_create(rsx_comm_s* c) {
+    const int prio_on = env_knob("RSX_COMM_PRIORITY", 1, 0, 1);  // read per communicator
+    int least = 0, greatest = 0;
+    if (prio_on && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess && greatest != least) {
+        hipError_t e = hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, greatest);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream_cap, hipStreamNonBlocking);
+        return e;
+    }
+    return hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+}
+
 int comm_rank(rsx_comm_t c) { return c->rank; }
 int comm_world(rsx_comm_t c) { return c->world; }
-// The stream the communicator's exchanges run on (host-hook communicators: the caller's):
-// small kernels that only feed later exchanges can run there, off the compute stream.
-hipStream_t comm_stream(rsx_comm_t c, hipStream_t s) { return c->host_fn ? s : c->stream; }
+// The stream the communicator's exchanges run on, for work issued from `s` (host-hook
+// communicators: `s` itself): the priority stream for eager issue, the capture stream
+// while `s` is being captured; a call issued on either comm stream stays on it.  Small
+// kernels that only feed later exchanges can run there, off the compute stream.
+hipStream_t comm_stream(rsx_comm_t c, hipStream_t s) {
+    if (c->host_fn || s == c->stream || (c->stream_cap && s == c->stream_cap)) return s;
+    if (c->stream_cap) {
+        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(s, &cap) == hipSuccess && cap == hipStreamCaptureStatusActive) return c->stream_cap;
+    }
+    return c->stream;
+}
 // The next event of the communicator's ring (for a fence the caller records itself).
 hipEvent_t comm_event(rsx_comm_t c) {
     hipEvent_t j = c->join[c->next];
@@ -117,21 +155,33 @@ hipEvent_t comm_event(rsx_comm_t c) {
 // The latency-injection stand-in for one collective: `blocks` workgroups copy `floats`
 // floats of the scratch (half read, half written: the collective's HBM traffic) and
 // then hold their slots until `ticks` of the device wall clock have passed since the
-// kernel started (block 0's start, shared through the first scratch word is not
-// needed: each block measures from its own start, all start together).
+// kernel started (each block measures from its own start; all start together).
+// Poison mode (`save` != nullptr, tests): each thread first saves its words of the
+// collective's buffer and overwrites them with `poison` (published device-wide by a
+// release fence), and restores them after the wait, so for the modelled time the
+// buffer holds NaN (f32) / -1 (i64 ids) — what an unfenced reader would see.
 __global__ __launch_bounds__(256) void sim_collective(float* __restrict__ scratch, int64_t half, int64_t floats,
-                                                      uint64_t ticks) {
+                                                      uint64_t ticks, uint32_t* __restrict__ buf,
+                                                      uint32_t* __restrict__ save, int64_t words, uint32_t poison) {
     const uint64_t t0 = wall_clock64();
+    const int64_t tid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    if (save) {
+        for (int64_t i = tid; i < words; i += stride) {
+            save[i] = buf[i];
+            buf[i] = poison;
+        }
+        __threadfence();
+    }
     // float4 copies, four in flight per lane, in passes over the scratch's halves (a
     // per-element loop with one dependent load at a time ran at ~0.2 TB/s on 32 blocks
     // and took several times the modelled collective time at C4's 1 GB item block)
-    const int64_t stride = (int64_t)gridDim.x * 256;
     const int64_t h4 = half / 4;
     const float4* __restrict__ src = reinterpret_cast<const float4*>(scratch);
     float4* __restrict__ dst = reinterpret_cast<float4*>(scratch + half);
     for (int64_t todo = floats / 8; todo > 0;) {
         const int64_t n = todo < h4 ? todo : h4;
-        int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+        int64_t i = tid;
         for (; i + 3 * stride < n; i += 4 * stride) {
             const float4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], e = src[i + 3 * stride];
             dst[i] = add4(a, f4(1.f));
@@ -143,6 +193,8 @@ __global__ __launch_bounds__(256) void sim_collective(float* __restrict__ scratc
         todo -= n;
     }
     while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(16);
+    if (save)
+        for (int64_t i = tid; i < words; i += stride) buf[i] = save[i];
 }
 
 // Modelled time of one collective of `bytes` (the whole buffer: all-reduce X, all-gather
@@ -162,12 +214,14 @@ hipEvent_t collective(rsx_comm_t c, int op, void* buf, int64_t count, int dtype,
     hipError_t e;
     hipEvent_t j = c->join[c->next];
     c->next = (c->next + 1) % kJoinEvents;
+    const hipStream_t cs = comm_stream(c, s);
     // a call issued on the comm stream itself (work queued behind an earlier exchange) needs no
-    // fork: a stream waiting on its own event breaks HIP graph capture (instantiation fault)
-    const bool fork = s != c->stream;
+    // fork: a captured stream waiting on an event recorded on itself makes the graph's replay
+    // segfault in hipGraphLaunch (tools/gpu/exp/selfwait.hip)
+    const bool fork = s != cs;
     if (c->sim_world) {  // one rank: the data is already the result; the time is injected
         if (fork && ((e = hipEventRecord(c->fork, s)) != hipSuccess ||
-                     (e = hipStreamWaitEvent(c->stream, c->fork, 0)) != hipSuccess)) {
+                     (e = hipStreamWaitEvent(cs, c->fork, 0)) != hipSuccess)) {
             *rc = hip_rc(e);
             return nullptr;
         }
@@ -177,9 +231,14 @@ hipEvent_t collective(rsx_comm_t c, int op, void* buf, int64_t count, int dtype,
         const double moved = (op == RSX_COLL_ALLREDUCE ? 2.0 : 1.0) * (c->sim_world - 1.0) / c->sim_world * bytes;
         int64_t floats = (int64_t)(2.0 * moved / 4.0);  // the moved bytes read once and written once
         const int64_t half = c->sim_scratch_floats / 2;
-        hipLaunchKernelGGL(sim_collective, dim3((unsigned)c->sim_blocks), dim3(256), 0, c->stream, c->sim_scratch,
-                           half, floats, (uint64_t)(sec * c->sim_tick_hz));
-        if ((e = hipGetLastError()) != hipSuccess || (e = hipEventRecord(j, c->stream)) != hipSuccess) {
+        // poison mode: the whole buffer the collective writes (world 1: count elements)
+        const int64_t words = (int64_t)bytes / 4;
+        const bool poison = c->sim_poison && words <= c->sim_scratch_floats / 2;
+        hipLaunchKernelGGL(sim_collective, dim3((unsigned)c->sim_blocks), dim3(256), 0, cs, c->sim_scratch,
+                           half, floats, (uint64_t)(sec * c->sim_tick_hz), poison ? static_cast<uint32_t*>(buf) : nullptr,
+                           poison ? reinterpret_cast<uint32_t*>(c->sim_save) : nullptr, words,
+                           dtype == RSX_COLL_I64 ? 0xffffffffu : 0x7fc00000u);
+        if ((e = hipGetLastError()) != hipSuccess || (e = hipEventRecord(j, cs)) != hipSuccess) {
             *rc = hip_rc(e);
             return nullptr;
         }
@@ -201,7 +260,7 @@ hipEvent_t collective(rsx_comm_t c, int op, void* buf, int64_t count, int dtype,
         return j;
     }
     if (fork && ((e = hipEventRecord(c->fork, s)) != hipSuccess ||
-                 (e = hipStreamWaitEvent(c->stream, c->fork, 0)) != hipSuccess)) {
+                 (e = hipStreamWaitEvent(cs, c->fork, 0)) != hipSuccess)) {
         *rc = hip_rc(e);
         return nullptr;
     }
@@ -209,14 +268,14 @@ hipEvent_t collective(rsx_comm_t c, int op, void* buf, int64_t count, int dtype,
     const size_t es = dtype == RSX_COLL_I64 ? 8 : 4;
     char* own = static_cast<char*>(buf) + (size_t)c->rank * (size_t)count * es;
     ncclResult_t r;
-    if (op == RSX_COLL_ALLGATHER) r = rccl().all_gather(own, buf, (size_t)count, ty, c->nccl, c->stream);
-    else if (op == RSX_COLL_REDUCESCATTER) r = rccl().reduce_scatter(buf, own, (size_t)count, ty, ncclSum, c->nccl, c->stream);
-    else r = rccl().all_reduce(buf, buf, (size_t)count, ty, ncclSum, c->nccl, c->stream);
+    if (op == RSX_COLL_ALLGATHER) r = rccl().all_gather(own, buf, (size_t)count, ty, c->nccl, cs);
+    else if (op == RSX_COLL_REDUCESCATTER) r = rccl().reduce_scatter(buf, own, (size_t)count, ty, ncclSum, c->nccl, cs);
+    else r = rccl().all_reduce(buf, buf, (size_t)count, ty, ncclSum, c->nccl, cs);
     if (r != ncclSuccess) {
         *rc = RSX_ERR_COMM;
         return nullptr;
     }
-    if ((e = hipEventRecord(j, c->stream)) != hipSuccess) {
+    if ((e = hipEventRecord(j, cs)) != hipSuccess) {
         *rc = hip_rc(e);
         return nullptr;
     }
@@ -231,54 +290,79 @@ namespace {
 
 // ---- row lists of the sparse exchange -------------------------------------------
 __global__ __launch_bounds__(256) void tag_rows_k(const int64_t* ids, int64_t n, int32_t* tag_arr,
-                                                  const int32_t* tag_dev, int32_t tag) {
+                                                  const int32_t* tag_dev, int32_t tag, int64_t n_rows, int32_t* err) {
     const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (j < n) tag_arr[ids[j]] = tag_dev ? *tag_dev : tag;
+    if (j >= n) return;
+    const int64_t i = ids[j];
+    if (i < 0 || i >= n_rows) {
+        if (err) atomicOr(err, 1);
+        return;
+    }
+    tag_arr[i] = tag_dev ? *tag_dev : tag;
 }
 
 // mode 0: dst[j] = src[ids[j]] (gather), 1: dst[ids[j]] = src[j] (scatter; duplicate
-// ids carry identical rows), 2: dst[ids[j]] = 0
+// ids carry identical rows), 2: dst[ids[j]] = 0.  An id outside [0, n_rows) is never
+// dereferenced: it sets err bit 0 (rsx_sharded_lgcn_step.err) instead of faulting.
 __global__ __launch_bounds__(256) void rows_k(const float* src, float* dst, const int64_t* ids, int64_t n, int d,
-                                              int mode) {
+                                              int mode, int64_t n_rows, int32_t* err) {
     const int q = d / 4;
     const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (e >= n * q) return;
     const int64_t j = e / q;
     const int c = (int)(e - j * q) * 4;
     const int64_t i = ids[j];
+    if (i < 0 || i >= n_rows) {
+        if (err) atomicOr(err, 1);
+        return;
+    }
     if (mode == 0) st4(dst + j * d + c, ld4(src + i * d + c));
     else if (mode == 1) st4(dst + i * d + c, ld4(src + j * d + c));
     else st4(dst + i * d + c, f4(0.f));
 }
 
 // This rank's list for the sparse last-layer exchange: its (pos, neg) items (the union
-// share), then every neighbour item of its batch users (A_U row u: cols = n_users + item),
-// appended at a claimed position; the caller zero-fills the slice first (unused slots
-// stay item 0).  One wave per batch user; claims past `cap` are dropped and counted in
-// *cnt (the host bound makes that impossible; a test checks the counter).
+// share), then every neighbour item of its DISTINCT batch users (A_U row u: cols =
+// n_users + item), appended at a claimed position; the caller zero-fills the slice first
+// (unused slots stay item 0).  One wave per triplet; a user repeated in the batch is
+// listed once: the wave that swaps the step's tag into row_tag[u] first lists it (the
+// first item partial's tag blocks later write the same tags), so the list holds at most
+// 2 batch + the sum of the batch's distinct users' degrees <= the host bound (2 union_cap
+// + the union_cap largest degrees).  A claim past `cap` is dropped and sets err bit 1.
 __global__ __launch_bounds__(256) void nbr_list_k(const int64_t* __restrict__ trip, int64_t batch,
                                                   const int64_t* __restrict__ rowptr, const int32_t* __restrict__ col,
                                                   int64_t n_users, int64_t* __restrict__ out, int64_t cap,
-                                                  int32_t* __restrict__ cnt) {
+                                                  int32_t* __restrict__ cnt, int32_t* __restrict__ row_tag,
+                                                  const int32_t* __restrict__ tag_dev, int32_t tag,
+                                                  int32_t* __restrict__ err) {
     const int lane = threadIdx.x & 63;
     const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (w >= batch) return;
     if (lane < 2) out[2 * w + lane] = trip[(1 + lane) * batch + w];  // pos, neg of triplet w
     const int64_t u = trip[w];
     const int64_t b = rowptr[u], e = rowptr[u + 1];
-    int32_t base = 0;
-    if (lane == 0) base = atomicAdd(cnt, (int32_t)(e - b));
+    int32_t base = -1;
+    if (lane == 0) {
+        const int32_t t = tag_dev ? *tag_dev : tag;
+        if (atomicExch(row_tag + u, t) != t) {
+            base = atomicAdd(cnt, (int32_t)(e - b));
+            if (2 * batch + base + (e - b) > cap && err) atomicOr(err, 2);
+        }
+    }
     base = __shfl(base, 0, 64);
+    if (base < 0) return;  // a repeated user: listed by its first triplet's wave
     for (int64_t j = b + lane; j < e; j += 64) {
         const int64_t p = 2 * batch + base + (j - b);
         if (p < cap) out[p] = (int64_t)col[j] - n_users;
     }
 }
 
-int rows_op(const float* src, float* dst, const int64_t* ids, int64_t n, int d, int mode, hipStream_t s) {
+int rows_op(const float* src, float* dst, const int64_t* ids, int64_t n, int d, int mode, int64_t n_rows,
+            int32_t* err, hipStream_t s) {
     if (n <= 0) return 0;
     const int64_t tot = n * (d / 4);
-    hipLaunchKernelGGL(rows_k, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, src, dst, ids, n, d, mode);
+    hipLaunchKernelGGL(rows_k, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, src, dst, ids, n, d, mode,
+                       n_rows, err);
     return last_rc();
 }
 
@@ -399,7 +483,8 @@ int sharded_stored_layers(const rsx_sharded_lgcn_step& st, bool train, hipStream
         RSX_TRY(hip_rc(hipMemsetAsync(mine, 0, (size_t)st.nbr_cap * sizeof(int64_t), s)));
         RSX_TRY(hip_rc(hipMemsetAsync(st.nbr_count, 0, sizeof(int32_t), s)));
         hipLaunchKernelGGL(nbr_list_k, dim3((unsigned)((st.batch + 3) / 4)), dim3(256), 0, s, st.triplets, st.batch,
-                           st.adj_u->rowptr, st.adj_u->col, nu, mine, st.nbr_cap, st.nbr_count);
+                           st.adj_u->rowptr, st.adj_u->col, nu, mine, st.nbr_cap, st.nbr_count, st.row_tag,
+                           st.tag_dev, tag, st.err);
         RSX_TRY(last_rc());
         if (!(jN = collective(st.comm, RSX_COLL_ALLGATHER, st.nbr_items, st.nbr_cap, RSX_COLL_I64, s, &rc))) return rc;
     }
@@ -429,7 +514,7 @@ int sharded_stored_layers(const rsx_sharded_lgcn_step& st, bool train, hipStream
             // their neighbour items, the union items' final rows add it): summed there alone
             RSX_TRY(spmm_dispatch_tagging(*st.adj_i, x, d, e, st.slab_i, s, tj));
             RSX_TRY(wait(s, jN));
-            RSX_TRY(rows_op(bufs[k - 1] + off, st.cbufN, st.nbr_items, nQ, d, 0, s));
+            RSX_TRY(rows_op(bufs[k - 1] + off, st.cbufN, st.nbr_items, nQ, d, 0, ni, st.err, s));
             if (!(joins[k] = exchange(st.comm, st.cbufN, nQ * d, s, &rc))) return rc;
         } else if (k == 1 && st.n_head > 1) {
             // the step's head: nothing but this product can run before the first exchange,
@@ -452,7 +537,7 @@ int sharded_stored_layers(const rsx_sharded_lgcn_step& st, bool train, hipStream
         x = bufs[k - 1];
     }
     RSX_TRY(wait(s, joins[K - 1]));
-    if (nbr) RSX_TRY(rows_op(st.cbufN, bufs[K - 2] + off, st.nbr_items, nQ, d, 1, s));  // summed rows back
+    if (nbr) RSX_TRY(rows_op(st.cbufN, bufs[K - 2] + off, st.nbr_items, nQ, d, 1, ni, st.err, s));  // summed rows back
     {
         rsx_epilogue e = epi(RSX_EPI_FINAL);
         e.beta = beta;
@@ -465,21 +550,21 @@ int sharded_stored_layers(const rsx_sharded_lgcn_step& st, bool train, hipStream
         if (sparse) {  // only the union rows: tagged, computed, gathered, summed, scattered
             RSX_TRY(wait(s, jU));
             hipLaunchKernelGGL(tag_rows_k, dim3((unsigned)((nU + 255) / 256)), dim3(256), 0, s, st.union_items, nU,
-                               st.item_tag, st.tag_dev, tag);
+                               st.item_tag, st.tag_dev, tag, ni, st.err);
             RSX_TRY(last_rc());
             // the union items in row_tag's item block as well: after the compact exchange G'_I
             // is nonzero exactly there, so the first backward user-row product gathers only
             // those item rows (RSX_TAG_SPARSE_X) -- the item block of row_tag is read by no
             // other product of this step (its user block holds this rank's batch users)
             hipLaunchKernelGGL(tag_rows_k, dim3((unsigned)((nU + 255) / 256)), dim3(256), 0, s, st.union_items, nU,
-                               st.row_tag + nu, st.tag_dev, tag);
+                               st.row_tag + nu, st.tag_dev, tag, ni, st.err);
             RSX_TRY(last_rc());
             e.row_tag = st.item_tag;
             e.tag = tag;
             e.tag_dev = st.tag_dev;
             e.tag_flags = RSX_TAG_ROWS;
             RSX_TRY(spmm_dispatch(*st.adj_i, x, d, e, st.slab_i, s));
-            RSX_TRY(rows_op(st.final_emb + off, st.cbuf0, st.union_items, nU, d, 0, s));
+            RSX_TRY(rows_op(st.final_emb + off, st.cbuf0, st.union_items, nU, d, 0, ni, st.err, s));
             if (!(joins[K] = exchange(st.comm, st.cbuf0, nU * d, s, &rc))) return rc;
             e.row_tag = nullptr;
             e.tag_dev = nullptr;
@@ -500,7 +585,7 @@ int sharded_stored_layers(const rsx_sharded_lgcn_step& st, bool train, hipStream
         }
         RSX_TRY(spmm_dispatch(*st.adj_u, x, d, e, st.slab_u, s));
         RSX_TRY(wait(s, joins[K]));
-        if (sparse) RSX_TRY(rows_op(st.cbuf0, st.final_emb + off, st.union_items, nU, d, 1, s));
+        if (sparse) RSX_TRY(rows_op(st.cbuf0, st.final_emb + off, st.union_items, nU, d, 1, ni, st.err, s));
     }
     if (!train) return 0;
     // ---- loss: G' = dL/dfinal / (K+1), R = d reg / d ego on this rank's batch rows
@@ -516,11 +601,11 @@ int sharded_stored_layers(const rsx_sharded_lgcn_step& st, bool train, hipStream
     // G'_I summed (R_I is not: every rank adds its own R_I to its last item partial,
     // whose exchange then sums them; one n_items*d exchange less per step)
     if (sparse) {  // G'_I is nonzero on this rank's batch items only: sum the union rows
-        RSX_TRY(rows_op(st.g + off, st.cbuf1, st.union_items, nU, d, 0, s));
+        RSX_TRY(rows_op(st.g + off, st.cbuf1, st.union_items, nU, d, 0, ni, st.err, s));
         hipEvent_t j0 = exchange(st.comm, st.cbuf1, nU * d, s, &rc);
         if (!j0) return rc;
         RSX_TRY(wait(s, j0));
-        RSX_TRY(rows_op(st.cbuf1, st.g + off, st.union_items, nU, d, 1, s));
+        RSX_TRY(rows_op(st.cbuf1, st.g + off, st.union_items, nU, d, 1, ni, st.err, s));
     } else {
         hipEvent_t j0 = exchange(st.comm, st.g + off, ni * d, s, &rc);
         if (!j0) return rc;
@@ -583,8 +668,8 @@ int sharded_stored_layers(const rsx_sharded_lgcn_step& st, bool train, hipStream
         hipEvent_t jt;
         if (sparse) {
             // G'_I and R_I live on the union rows only: cleared there, after their last reader
-            RSX_TRY(rows_op(nullptr, st.g + off, st.union_items, nU, d, 2, s));
-            if (!st.reg_cnt) RSX_TRY(rows_op(nullptr, st.r + off, st.union_items, nU, d, 2, s));
+            RSX_TRY(rows_op(nullptr, st.g + off, st.union_items, nU, d, 2, ni, st.err, s));
+            if (!st.reg_cnt) RSX_TRY(rows_op(nullptr, st.r + off, st.union_items, nU, d, 2, ni, st.err, s));
             jt = collective(st.comm, RSX_COLL_REDUCESCATTER, st.t, q * d, RSX_COLL_F32, s, &rc);
         } else {
             jt = exchange(st.comm, st.t, ni * d, s, &rc);
@@ -632,7 +717,7 @@ int sharded_stored_layers(const rsx_sharded_lgcn_step& st, bool train, hipStream
             // they read only its output and the item rows of p / m / v, which nothing on the
             // compute stream touches now (the user Adam there updates user rows), so the
             // all-gather no longer waits for the user-row Adam product
-            static const int64_t on_comm = env_knob("RSX_SHARDED_COMM_ADAM", 1, 0, 1);
+            const int on_comm = env_knob("RSX_SHARDED_COMM_ADAM", 1, 0, 1);  // read per issue (tests flip it)
             hipStream_t cs = on_comm ? comm_stream(st.comm, s) : s;  // (jt completes on cs itself)
             if (cs == s) RSX_TRY(wait(s, jt));
             if (nown > 0) RSX_TRY(rowwise_dispatch(nown, d, a, cs));
@@ -913,7 +998,7 @@ int rsx_comm_init(rsx_comm_t* out, const void* id_host, int32_t rank, int32_t wo
     c->world = world;
     ncclUniqueId id;
     memcpy(&id, id_host, sizeof(id));
-    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    hipError_t e = rsx::comm_streams_create(c);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork, hipEventDisableTiming);
     for (int i = 0; e == hipSuccess && i < rsx::kJoinEvents; ++i)
         e = hipEventCreateWithFlags(&c->join[i], hipEventDisableTiming);
@@ -966,7 +1051,9 @@ int rsx_comm_init_sim(rsx_comm_t* out, int32_t sim_world, double busbw_gbs, doub
     c->sim_scratch_floats = scratch_mb * (1 << 20) / 4;
     if (e == hipSuccess) e = hipMalloc(&c->sim_scratch, (size_t)c->sim_scratch_floats * 4);
     if (e == hipSuccess) e = hipMemset(c->sim_scratch, 0, (size_t)c->sim_scratch_floats * 4);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    c->sim_poison = (int32_t)rsx::env_knob("RSX_COMM_SIM_POISON", 0, 0, 1);
+    if (e == hipSuccess && c->sim_poison) e = hipMalloc(&c->sim_save, (size_t)(c->sim_scratch_floats / 2) * 4);
+    if (e == hipSuccess) e = rsx::comm_streams_create(c);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork, hipEventDisableTiming);
     for (int i = 0; e == hipSuccess && i < rsx::kJoinEvents; ++i)
         e = hipEventCreateWithFlags(&c->join[i], hipEventDisableTiming);
@@ -986,12 +1073,15 @@ double rsx_comm_sim_seconds(rsx_comm_t c, int32_t op, double bytes) {
 int rsx_comm_destroy(rsx_comm_t c) {
     if (!c) return RSX_OK;
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->stream_cap) (void)hipStreamSynchronize(c->stream_cap);
     if (c->sim_scratch) (void)hipFree(c->sim_scratch);
+    if (c->sim_save) (void)hipFree(c->sim_save);
     if (c->nccl) rsx::rccl().destroy(c->nccl);
     for (int i = 0; i < rsx::kJoinEvents; ++i)
         if (c->join[i]) (void)hipEventDestroy(c->join[i]);
     if (c->fork) (void)hipEventDestroy(c->fork);
     if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->stream_cap) (void)hipStreamDestroy(c->stream_cap);
     delete c;
     return RSX_OK;
 }
@@ -1007,6 +1097,7 @@ int rsx_comm_allreduce_f32(rsx_comm_t c, float* buf, int64_t n, rsx_stream_t str
 
 int rsx_comm_allreduce_f32_start(rsx_comm_t c, float* buf, int64_t n, rsx_stream_t stream) {
     if (!c || (!buf && n > 0) || n < 0) return RSX_ERR_ARG;
+    if (c->pending) return RSX_ERR_ARG;  // one exchange in flight: every start pairs with one rsx_comm_wait
     int rc = 0;
     hipEvent_t j = rsx::exchange(c, buf, n, rsx::as_stream(stream), &rc);
     if (!j) return rc;

@@ -92,7 +92,8 @@ class ShardedStep(C.Structure):
                 ("comm", P), ("row_tag", P), ("tag", I64), ("tag_dev", P), ("reg_cnt", P),
                 ("union_items", P), ("item_tag", P), ("cbuf0", P), ("cbuf1", P), ("n_items_pad", I64), ("union_cap", I64),
                 ("xch", P), ("n_head", I32), ("pad1", I32), ("head_i", C.POINTER(Csr)), ("head_row0", P),
-                ("head_slab", P), ("nbr_items", P), ("nbr_count", P), ("cbufN", P), ("nbr_cap", I64), ("defer_ag", I32), ("pad2", I32)]
+                ("head_slab", P), ("nbr_items", P), ("nbr_count", P), ("cbufN", P), ("nbr_cap", I64), ("defer_ag", I32), ("pad2", I32),
+                ("err", P)]
 
 
 class DpStep(C.Structure):
@@ -192,6 +193,13 @@ def _declare(lib):
         "rsx_edge_dropout_ws_bytes": (C.c_size_t, [I64, I64, I64]),
         "rsx_edge_dropout_build": (C.c_int, [P, P, P, I64, I64, I64, P, P, P, P, P, P, P, C.c_size_t, P]),
         "rsx_smore_unit_weights_bwd": (C.c_int, [P, I64, P, P, P, I32, I32, P, P, P, P]),
+        "rsx_cpu_spmm": (C.c_int, [P, P, P, I64, P, I32, P]),
+        "rsx_cpu_propagate_mean": (C.c_int, [P, P, P, I64, P, I32, I32, P]),
+        "rsx_cpu_layergcn_forward": (C.c_int, [P, P, P, I64, P, I32, I32, P, P, P]),
+        "rsx_cpu_layergcn_backward": (C.c_int, [P, P, P, I64, P, I32, I32, P, P, P, P]),
+        "rsx_cpu_bpr": (C.c_int, [I32, P, P, I64, I64, I32, P, I64, F32, F32, P, P, P]),
+        "rsx_cpu_fullsort_topk": (C.c_int, [P, P, I64, P, I64, I32, P, P, I32, P, P]),
+        "rsx_cpu_adam": (C.c_int, [P, P, P, P, I64, I64, F32, F32, F32, F32, F32]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -216,7 +224,9 @@ EXPORTED = ["rsx_version", "rsx_csr_schedule_host", "rsx_csr_schedule_rebind", "
             "rsx_smore_infonce_ws_bytes", "rsx_smore_infonce_fwd", "rsx_smore_infonce_bwd", "rsx_smore_infonce_fwd_total", "rsx_smore_infonce_bwd_scaled", "rsx_adam_multi", "rsx_adam_multi_scaled", "rsx_adam_multi_mg",
             "rsx_smore_unit_weights", "rsx_smore_unit_weights_bwd", "rsx_mg_alpha_ws_bytes", "rsx_mg_alpha",
             "rsx_axpy_multi", "rsx_knn_ws_bytes", "rsx_knn_graph", "rsx_adj_build_ws_bytes", "rsx_adj_build",
-            "rsx_edge_dropout_ws_bytes", "rsx_edge_dropout_build", "rsx_nan_gate"]
+            "rsx_edge_dropout_ws_bytes", "rsx_edge_dropout_build", "rsx_nan_gate",
+            "rsx_cpu_spmm", "rsx_cpu_propagate_mean", "rsx_cpu_layergcn_forward", "rsx_cpu_layergcn_backward",
+            "rsx_cpu_bpr", "rsx_cpu_fullsort_topk", "rsx_cpu_adam"]
 
 
 def lib_path() -> str:

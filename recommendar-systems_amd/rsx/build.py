@@ -19,7 +19,9 @@ CSRC = os.path.join(ROOT, "csrc")
 INCLUDE = os.path.join(REPO, "include")
 LIBDIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIBDIR, "librsx.so")
-SOURCES = ["spmm.hip", "bpr.hip", "fullsort.hip", "step.hip", "smore.hip", "metrics.hip", "linear.hip", "dist.hip", "dp.hip", "smore_fuse.hip", "knn.hip", "graph.hip"]
+SOURCES = ["spmm.hip", "bpr.hip", "fullsort.hip", "step.hip", "smore.hip", "metrics.hip", "linear.hip", "dist.hip",
+           "dp.hip", "smore_fuse.hip", "knn.hip", "graph.hip",
+           "cpu_ops.cpp"]  # host-only C++ (the torch.ops.rsx CPU kernels), compiled as plain C++
 ARCH = os.environ.get("RSX_OFFLOAD_ARCH", "gfx950")
 
 
@@ -64,8 +66,12 @@ def build(force: bool = False, verbose: bool = True) -> str:
     srcs = [s for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
 
     def compile_one(src):
-        obj = os.path.join(objdir, src.replace(".hip", ".o"))
-        cmd = [hipcc, *_flags(src), "-c", os.path.join(CSRC, src), "-o", obj]
+        obj = os.path.join(objdir, os.path.splitext(src)[0] + ".o")
+        if src.endswith(".cpp"):  # host code: no device pass
+            cmd = [hipcc, "-x", "c++", "-O3", "-fPIC", "-std=c++17", "-pthread", f"-I{INCLUDE}", f"-I{CSRC}", "-c",
+                   os.path.join(CSRC, src), "-o", obj]
+        else:
+            cmd = [hipcc, *_flags(src), "-c", os.path.join(CSRC, src), "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")
@@ -74,7 +80,7 @@ def build(force: bool = False, verbose: bool = True) -> str:
     with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
         objs = list(ex.map(compile_one, srcs))
     tmp = LIB + ".tmp"
-    cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs, "-ldl"]
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-pthread", "-o", tmp, *objs, "-ldl"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stderr}")

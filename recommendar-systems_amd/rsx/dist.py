@@ -358,6 +358,9 @@ class ShardedLightGCNEngine:
             st.union_items, st.item_tag = self.union.data_ptr(), self.item_tag.data_ptr()
             st.cbuf0, st.cbuf1 = self.cbuf0.data_ptr(), self.cbuf1.data_ptr()
         st.xch = self.xch.data_ptr() if self.xch is not None else None
+        # the sparse exchange's row-list error bits (include/rsx.h rsx_sharded_lgcn_step.err)
+        self.err = torch.zeros(1, dtype=torch.int32, device=self.be.device)
+        st.err = self.err.data_ptr()
         self._set_nbr_struct()
         if self.head:
             self._head_structs = (L.Csr * len(self.head))(*[h.struct for h in self.head])
@@ -627,17 +630,32 @@ class ShardedLightGCNEngine:
 
     @property
     def p(self):
-        """The [users; items] parameter table (deferred item rows all-gathered first)."""
-        self.flush()
+        """The [users; items] parameter table, read as it is: no collective (a rank-0-only
+        checkpoint must not block).  With the deferred all-gather (defer_ag) the item rows
+        owned by other ranks are one step old until every rank has called flush(), which
+        the Trainer does at the end of each epoch and forward() does before evaluation."""
         return self._p
 
     def flush(self):
         """Complete a deferred parameter all-gather (defer_ag: the sparse native step issues
-        it at the start of the next step), so every replica's item rows are current."""
+        it at the start of the next step), so every replica's item rows are current.  It is
+        a collective when one is pending: every rank must call it at the same point (the
+        Trainer does, at the end of each epoch and before evaluation)."""
         if self._ag_dirty and self._comm is not None:
             L.check(L.lib().rsx_sharded_lightgcn_flush(C.byref(self._st), ops._stream()),
                     "rsx_sharded_lightgcn_flush")
         self._ag_dirty = False
+        self.check_err()
+
+    def check_err(self):
+        """Raise if a step's sparse row lists met an out-of-range id or overflowed (bits of
+        rsx_sharded_lgcn_step.err; reading it synchronises the stream)."""
+        err = getattr(self, "err", None)
+        if err is not None and self.native:
+            e = int(err.item())
+            if e:
+                raise RuntimeError(f"sharded LightGCN step: row-list error bits {e:#x} "
+                                   "(1: an item id outside [0, n_items); 2: neighbour list over nbr_cap)")
 
     def forward(self):
         self.flush()

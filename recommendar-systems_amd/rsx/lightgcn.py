@@ -248,14 +248,6 @@ class LightGCN(GeneralRecommender):
             return
         self.engine.step_slice(epoch, i, self.steps_per_epoch)
 
-    def state_dict(self, *args, **kwargs):
-        """The parameters as the reference's state dict; the sharded engine's deferred item
-        rows are all-gathered first (rsx.dist.ShardedLightGCNEngine.flush)."""
-        eng = self.__dict__.get("engine")
-        if eng is not None and hasattr(eng, "flush"):
-            eng.flush()
-        return super().state_dict(*args, **kwargs)
-
     def full_sort_topk_local(self, eval_users: torch.Tensor, k: int, eval_data):
         """(row positions in eval_users, top-k item ids) for this rank's evaluation users
         (global ids in [user_range)), ranked against every item with the training mask."""
@@ -283,10 +275,12 @@ class LightGCN(GeneralRecommender):
 
     @property
     def device_halt(self):
-        """(halt flag [2] int32 on the device, engine step count) of the single engine's
-        step: {1, tag of the step} once a batch loss was NaN (the parameters stay those of
-        the last finite step), or None where the step has no flag (sharded engine)."""
+        """(halt flag [2] int32 on the device, engine step count) of the single or
+        data-parallel engine's step: {1, tag of the step} once a (global) batch loss was NaN
+        (the parameters stay those of the last finite step; the tag is the engine's step
+        count, so the Trainer reports the batch index), or None where the step has no flag
+        (row-sharded engine)."""
         e = self.engine
-        if self.sharded:
+        if self.sharded and not getattr(self, "dp", False):
             return None
         return e.halt, e.step_count

@@ -13,12 +13,16 @@ through the dispatcher instead of importing the rsx model classes:
 (reference call sites: src/models/lightgcn.py:117-166, src/models/layergcn.py:127-188,
 src/models/smore.py:209-272, src/common/loss.py:33-61, src/common/trainer.py:238,509-528).
 
-Graphs are plain CSR tensors on the GPU (rowptr int64 [N+1], col int32 [nnz],
-val f32 [nnz]); the nnz-balanced work schedule (and, for spmm_csr's backward, the
+Graphs are plain CSR tensors (rowptr int64 [N+1], col int32 [nnz], val f32 [nnz]);
+on the GPU the nnz-balanced work schedule (and, for spmm_csr's backward, the
 transposed CSR) is built once per graph and cached, keyed by the tensors (held,
 so their storage cannot be reused while cached).  The adjacency is a constant of
-the reference models (no gradient to `val`).  Every op is registered for the CUDA
-(ROCm) device type only: CPU tensors raise (no CPU fallback on the product path).
+the reference models (no gradient to `val`).  Each op has two kernels, chosen by the
+dispatcher from the tensors' device: CUDA (ROCm) tensors run the HIP kernels, CPU
+tensors the C++ CPU kernels of the same library (csrc/cpu_ops.cpp, include/rsx.h
+"CPU kernels": the reference's CPU configuration, BASELINE C1).  Neither is a fallback
+for the other: a GPU tensor never reaches a CPU kernel (the HIP library failing to load
+raises).  smore_spectral is GPU-only (CPU tensors raise NotImplementedError).
 Backward passes that need forward intermediates recompute the forward (a few
 SpMMs), so the ops hold no hidden state between forward and backward.
 """
@@ -94,6 +98,36 @@ def _n_rows(rowptr):
     return rowptr.shape[0] - 1
 
 
+def _cp(t):
+    """Host pointer of a contiguous CPU tensor (None for None)."""
+    return None if t is None else t.data_ptr()
+
+
+def _cpu_csr(rowptr, col, val):
+    if col.dtype != torch.int32 or val.dtype != torch.float32 or rowptr.dtype != torch.int64:
+        raise RuntimeError("rsx CSR: rowptr int64, col int32, val float32")
+    return rowptr.contiguous(), col.contiguous(), val.contiguous()
+
+
+def _cpu_spmm(rowptr, col, val, x):
+    rowptr, col, val = _cpu_csr(rowptr, col, val)
+    x = x.contiguous()
+    if x.dtype != torch.float32 or x.dim() != 2:
+        raise RuntimeError("rsx::spmm_csr: x must be float32 [n_cols, d]")
+    y = x.new_empty(_n_rows(rowptr), x.shape[1])
+    L.check(L.lib().rsx_cpu_spmm(_cp(rowptr), _cp(col), _cp(val), _n_rows(rowptr), _cp(x), x.shape[1], _cp(y)),
+            "rsx_cpu_spmm")
+    return y
+
+
+def _cpu_transpose(rowptr, col, val, n_cols):
+    """(rowptr, col, val) of A^T on the host (graph.to_csr: rows sorted, columns in order)."""
+    rp = rowptr.numpy()
+    rows = np.repeat(np.arange(rp.size - 1, dtype=np.int64), np.diff(rp))
+    trp, tcol, tval = graph.to_csr(col.numpy().astype(np.int64), rows, val.numpy(), int(n_cols), rp.size - 1)
+    return torch.from_numpy(trp), torch.from_numpy(tcol.astype(np.int32)), torch.from_numpy(tval.astype(np.float32))
+
+
 # ---------------------------------------------------------------------------
 # SpMM
 # ---------------------------------------------------------------------------
@@ -116,11 +150,18 @@ def _spmm_setup(ctx, inputs, output):
 
 def _spmm_bwd(ctx, g):
     rowptr, col, val = ctx.saved_tensors
+    if not g.is_cuda:  # the CPU kernel on the host transpose
+        return None, None, None, _cpu_spmm(*_cpu_transpose(rowptr, col, val, ctx.n_cols), g), None
     AT = _csr(rowptr, col, val, ctx.n_cols, transpose=True)
     return None, None, None, AT.spmm(g.contiguous()), None
 
 
 spmm_csr.register_autograd(_spmm_bwd, setup_context=_spmm_setup)
+
+
+@spmm_csr.register_kernel("cpu")
+def _(rowptr, col, val, x, n_cols):
+    return _cpu_spmm(rowptr, col, val, x)
 
 
 # ---------------------------------------------------------------------------
@@ -151,6 +192,16 @@ def _pm_bwd(ctx, g):
 
 
 propagate_mean.register_autograd(_pm_bwd, setup_context=_pm_setup)
+
+
+@propagate_mean.register_kernel("cpu")
+def _(rowptr, col, val, x, n_layers):
+    rowptr, col, val = _cpu_csr(rowptr, col, val)
+    x = x.contiguous()
+    out = torch.empty_like(x)
+    L.check(L.lib().rsx_cpu_propagate_mean(_cp(rowptr), _cp(col), _cp(val), _n_rows(rowptr), _cp(x), x.shape[1],
+                                           int(n_layers), _cp(out)), "rsx_cpu_propagate_mean")
+    return out
 
 
 # ---------------------------------------------------------------------------
@@ -192,10 +243,27 @@ def _lg_setup(ctx, inputs, output):
     ctx.K = K
 
 
+def _lg_bwd_cpu(rowptr, col, val, x, K, G):
+    rowptr, col, val = _cpu_csr(rowptr, col, val)
+    n, d = x.shape
+    zs = x.new_empty(K, n, d)
+    cs = x.new_empty(K, n)
+    out = torch.empty_like(x)
+    lib = L.lib()
+    L.check(lib.rsx_cpu_layergcn_forward(_cp(rowptr), _cp(col), _cp(val), n, _cp(x), d, K, _cp(out), _cp(zs),
+                                         _cp(cs)), "rsx_cpu_layergcn_forward")
+    dx = torch.empty_like(x)
+    L.check(lib.rsx_cpu_layergcn_backward(_cp(rowptr), _cp(col), _cp(val), n, _cp(x), d, K, _cp(G), _cp(zs), _cp(cs),
+                                          _cp(dx)), "rsx_cpu_layergcn_backward")
+    return dx
+
+
 def _lg_bwd(ctx, G):
     rowptr, col, val, x = ctx.saved_tensors
     K = ctx.K
     x = x.contiguous()
+    if not x.is_cuda:
+        return None, None, None, _lg_bwd_cpu(rowptr, col, val, x, K, G.contiguous()), None
     A = _csr(rowptr, col, val, _n_rows(rowptr))
     _, zs, cs = _lgcn_forward(A, x, K, True)  # recompute the pre-scale rows and cosine weights
     n, d = x.shape
@@ -216,6 +284,18 @@ def _lg_bwd(ctx, G):
 
 
 propagate_layergcn.register_autograd(_lg_bwd, setup_context=_lg_setup)
+
+
+@propagate_layergcn.register_kernel("cpu")
+def _(rowptr, col, val, x, n_layers):
+    if n_layers < 1:
+        raise RuntimeError("propagate_layergcn: n_layers >= 1")
+    rowptr, col, val = _cpu_csr(rowptr, col, val)
+    x = x.contiguous()
+    out = torch.empty_like(x)
+    L.check(L.lib().rsx_cpu_layergcn_forward(_cp(rowptr), _cp(col), _cp(val), x.shape[0], _cp(x), x.shape[1],
+                                             int(n_layers), _cp(out), None, None), "rsx_cpu_layergcn_forward")
+    return out
 
 
 # ---------------------------------------------------------------------------
@@ -243,9 +323,34 @@ def _bpr_setup(ctx, inputs, output):
     ctx.cfg = (n_users, reg, variant, batch_cfg, ego is not None)
 
 
+def _cpu_bpr(final, ego, triplets, n_users, reg, variant, batch_cfg, grads):
+    final = final.contiguous()
+    ego = ego.contiguous() if ego is not None else None
+    trip = triplets[:3].contiguous()
+    if trip.dtype != torch.int64:
+        raise RuntimeError("rsx::bpr_loss: triplets must be int64 [3, B]")
+    B = trip.shape[1]
+    ni = final.shape[0] - n_users
+    gf = torch.zeros_like(final) if grads else None
+    ge = torch.zeros_like(ego) if (grads and ego is not None and variant != L.RSX_BPR_SMORE) else None
+    loss = final.new_empty(1)
+    L.check(L.lib().rsx_cpu_bpr(int(variant), _cp(final), _cp(ego), int(n_users), ni, final.shape[1], _cp(trip), B,
+                                float(reg), float(batch_cfg) if batch_cfg > 0 else float(B), _cp(gf), _cp(ge),
+                                _cp(loss)), "rsx_cpu_bpr")
+    return loss, gf, ge
+
+
+@bpr_loss.register_kernel("cpu")
+def _(final, ego, triplets, n_users, reg, variant, batch_cfg):
+    return _cpu_bpr(final, ego, triplets, n_users, reg, variant, batch_cfg, False)[0][0].clone()
+
+
 def _bpr_bwd(ctx, go):
     final, ego, triplets = ctx.saved_tensors
     n_users, reg, variant, batch_cfg, has_ego = ctx.cfg
+    if not final.is_cuda:
+        _, gf, ge = _cpu_bpr(final, ego if has_ego else None, triplets, n_users, reg, variant, batch_cfg, True)
+        return go * gf, (go * ge if ge is not None else None), None, None, None, None, None
     ni = final.shape[0] - n_users
     _, gf, ge = ops.bpr(int(variant), final.contiguous(), ego.contiguous() if has_ego else None, int(n_users), ni,
                         triplets, float(reg), float(batch_cfg) if batch_cfg > 0 else None)
@@ -267,6 +372,20 @@ def fullsort_topk(user_emb: Tensor, users: Tensor, item_emb: Tensor, mask_rowptr
                              mask_rowptr.contiguous(), mask_col.contiguous(), int(k))
 
 
+@fullsort_topk.register_kernel("cpu")
+def _(user_emb, users, item_emb, mask_rowptr, mask_col, k):
+    ue, it = user_emb.contiguous(), item_emb.contiguous()
+    users = users.contiguous()
+    nb = users.numel()
+    val = ue.new_empty(nb, int(k))
+    idx = torch.empty(nb, int(k), dtype=torch.int64)
+    if nb:
+        L.check(L.lib().rsx_cpu_fullsort_topk(_cp(ue), _cp(users), nb, _cp(it), it.shape[0], it.shape[1],
+                                              _cp(mask_rowptr.contiguous()), _cp(mask_col.contiguous()), int(k),
+                                              _cp(val), _cp(idx)), "rsx_cpu_fullsort_topk")
+    return val, idx
+
+
 @fullsort_topk.register_fake
 def _(user_emb, users, item_emb, mask_rowptr, mask_col, k):
     nb = users.shape[0]
@@ -284,6 +403,16 @@ def adam_(p: Tensor, g: Tensor, m: Tensor, v: Tensor, step: Tensor, lr: float, b
     from .smore_fuse import adam_multi
 
     adam_multi([p], [g.contiguous()], [m], [v], [step], lr, betas=(beta1, beta2), eps=eps, weight_decay=weight_decay)
+
+
+@adam_.register_kernel("cpu")
+def _(p, g, m, v, step, lr, beta1, beta2, eps, weight_decay):
+    for t in (p, m, v):
+        if not t.is_contiguous() or t.dtype != torch.float32:
+            raise RuntimeError("rsx::adam_: p, m, v must be contiguous float32")
+    g = g.contiguous()
+    L.check(L.lib().rsx_cpu_adam(_cp(p), _cp(g), _cp(m), _cp(v), p.numel(), int(step), float(lr), float(beta1),
+                                 float(beta2), float(eps), float(weight_decay)), "rsx_cpu_adam")
 
 
 # ---------------------------------------------------------------------------

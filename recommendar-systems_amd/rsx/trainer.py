@@ -255,14 +255,25 @@ class Trainer:
         acc.zero_()
         lr = self.current_lr()
         n = 0
+        # the step's device NaN gate (single engine, data-parallel engine): cleared per epoch,
+        # so a halt of an earlier fit() does not carry into this one
+        halt = getattr(self.model, "device_halt", None)
+        if halt is not None:
+            halt[0].zero_()
         if getattr(self.model, "sharded", False):
-            # user-sharded model (torchrun): every rank runs the same number of steps on its
-            # own users' device-sampled batches; the epoch loss is the sum over ranks
+            # user-sharded / data-parallel model (torchrun): every rank runs the same number
+            # of steps on its own device-sampled batches; the epoch loss is the sum over ranks
             import torch.distributed as dist
 
             for i in range(self.model.steps_per_epoch):
                 self.model.fused_step_index(epoch_idx, i, lr)
                 n += 1
+            # the row-sharded engine's deferred parameter all-gather is a collective: every
+            # rank completes it here, at the same point, so that a later read of the
+            # parameters (a rank-0 checkpoint, state_dict) needs no exchange
+            flush = getattr(getattr(self.model, "engine", None), "flush", None)
+            if flush is not None:
+                flush()
             if getattr(self.model, "dp", False):  # data-parallel: every rank holds the global batches' loss
                 total = float(acc.item())
             else:
@@ -270,20 +281,17 @@ class Trainer:
                 dist.all_reduce(tot)
                 total = float(tot.item())
         else:
-            halt = getattr(self.model, "device_halt", None)
-            if halt is not None:
-                halt[0].zero_()  # a halt of an earlier fit() does not carry into this epoch
             for batch in train_data:
                 self.model.fused_step(batch, lr)
                 n += 1
             total = float(acc.item())  # one host sync per epoch
-            if halt is not None:
-                flag, s0 = halt  # (device flag, engine step count before this epoch)
-                h = flag.cpu().tolist()
-                if h[0]:  # the step's NaN gate: the batch, and the parameters of the batch before it
-                    b = h[1] - s0 - 1
-                    self.logger.info(f"Loss is nan at epoch: {epoch_idx}, batch index: {b}. Exiting.")
-                    return torch.tensor(float("nan")), torch.tensor(0.0)
+        if halt is not None:
+            flag, s0 = halt  # (device flag, engine step count before this epoch)
+            h = flag.cpu().tolist()
+            if h[0]:  # the step's NaN gate: the batch, and the parameters of the batch before it
+                b = h[1] - s0 - 1
+                self.logger.info(f"Loss is nan at epoch: {epoch_idx}, batch index: {b}. Exiting.")
+                return torch.tensor(float("nan")), torch.tensor(0.0)
         if np.isnan(total):
             self.logger.info(f"Loss is nan at epoch: {epoch_idx}. Exiting.")
             return torch.tensor(float("nan")), torch.tensor(0.0)

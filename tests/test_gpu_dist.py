@@ -40,10 +40,14 @@ def _worker(rank, world, port, out_dir, native, sparse, k=K, fused=True, head=No
             assert len(eng.head) == head
     f0 = eng.forward().cpu().clone()
     eng.step(triplets=torch.from_numpy(trip).cuda())
+    if rank == 0:  # a one-rank read of the parameters (a checkpoint) issues no collective
+        _ = eng.p.cpu()
+    eng.flush()  # every rank: the deferred all-gather of the owners' item rows
     p1 = eng.p.cpu().numpy()
     # device-sampled steps run too (epoch buffer + slices)
     for s in range(0, eng.n_inter, 16):
         eng.step(epoch=0, start=s)
+    eng.flush()
     torch.cuda.synchronize()
     np.savez(os.path.join(out_dir, f"r{rank}.npz"), p=p1, f0=f0.numpy(), U0=U0, I0=I0,
              after=eng.p.cpu().numpy())
@@ -140,7 +144,7 @@ def _native_worker(rank, world, port, out_dir, SPARSE=True):
         if getattr(eng, "reg_cnt", None) is not None:  # the one-launch BPR's occurrence counts are all cleared
             assert torch.count_nonzero(eng.reg_cnt[:-4]).item() == 0
         eng.invalidate()
-        f1 = eng.forward().cpu().clone()
+        f1 = eng.forward().cpu().clone()  # (forward flushes first: every rank calls it)
         if native == "graph":  # full batches after the first were replayed from one capture
             assert eng._graphs.get(16) is not None
         res[native] = (f0.numpy(), eng.p.cpu().numpy(), eng.m.cpu().numpy(), np.array(losses), f1.numpy())
@@ -227,6 +231,7 @@ def _sim_worker(rank, world, port, out_dir):
             eng.step(epoch=0, start=s)
         torch.cuda.synchronize()
         out[f"ms_{bool(sim)}"] = (time.perf_counter() - t0) * 1e3 / 4
+        eng.flush()
         out[f"p_{bool(sim)}"] = eng.p.cpu().numpy()
         if sim:
             X = NI * D * 4.0
@@ -248,3 +253,115 @@ def test_latency_injected_comm_is_data_identity_and_takes_the_modelled_time():
     # a K = 3 sparse step issues 4 dense all-reduce-volume collectives + RS + AG + compact
     # ones: at least the 200 us latency of each of its >= 8 collectives on the comm stream
     assert float(z["ms_True"]) >= float(z["ms_False"]) + 8 * 0.2 * 0.9, (z["ms_True"], z["ms_False"])
+
+
+def _hub_graph():
+    """_local_graph's shape plus a hub user: user 0 holds 30 items (the others ~4), so a
+    batch repeating user 0 lists 16 x 30 neighbour claims unless users are deduplicated."""
+    rng = np.random.default_rng(5)
+    tu = np.concatenate([np.repeat(np.arange(NU), 4), np.zeros(30, np.int64)])
+    ti = np.concatenate([np.concatenate([rng.choice(NI, 4, replace=False) for _ in range(NU)]), np.arange(30)])
+    key = np.unique(tu * 1000 + ti)
+    return key // 1000, key % 1000
+
+
+def _hub_batches(tu, ti, n=6, B=16):
+    """n batches of B triplets (user, positive, sampled negative); batch 0 is user 0 sixteen
+    times, the others mix user 0 with random users (duplicates included)."""
+    rng = np.random.default_rng(11)
+    hist = {}
+    for u, i in zip(tu.tolist(), ti.tolist()):
+        hist.setdefault(u, []).append(i)
+    out = []
+    for b in range(n):
+        users = np.zeros(B, np.int64) if b == 0 else np.concatenate([[0, 0, 0], rng.integers(0, NU, B - 3)])
+        pos = np.array([rng.choice(hist[int(u)]) for u in users], np.int64)
+        neg = []
+        for u in users:
+            x = int(rng.integers(NI))
+            while x in hist[int(u)]:
+                x = int(rng.integers(NI))
+            neg.append(x)
+        out.append(np.stack([users, pos, np.array(neg, np.int64)]))
+    return out
+
+
+def _order_worker(rank, world, port, out_dir):
+    """The sparse native step over the POISONED latency-injected communicator (every
+    collective's buffer reads NaN / id -1 for its modelled time, then is restored): each
+    combination of the owner-Adam placement and the deferred all-gather, graph-replayed
+    and eager, with the comm stream at the greatest priority."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ["RSX_COMM_SIM"] = "4:1.0:100"  # 4 modelled ranks, 1 GB/s, 100 us per collective
+    os.environ["RSX_COMM_SIM_POISON"] = "1"
+    os.environ["RSX_COMM_PRIORITY"] = "1"
+    os.environ.pop("RSX_COMM_SIM_SHARE", None)
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    from rsx.dist import ShardedLightGCNEngine
+
+    torch.manual_seed(7)
+    I0 = torch.nn.init.xavier_uniform_(torch.empty(NI, D)).numpy()
+    U0 = torch.nn.init.xavier_uniform_(torch.empty(NU, D)).numpy()
+    tu, ti = _hub_graph()
+    batches = [torch.from_numpy(b).cuda() for b in _hub_batches(tu, ti)]
+    out = {"U0": U0, "I0": I0}
+    for comm_adam in (0, 1):
+        for defer in (0, 1):
+            for graph in (True, False):
+                os.environ["RSX_SHARDED_COMM_ADAM"] = str(comm_adam)
+                os.environ["RSX_SHARDED_DEFER_AG"] = str(defer)
+                eng = ShardedLightGCNEngine(tu, ti, NU, NI, D, K, REG, LR, "cuda:0", U0, I0, batch=16, sparse=True)
+                assert eng.sim is not None and eng.nbr is not None and eng.defer_ag == bool(defer)
+                eng.use_graph = graph
+                counts = []
+                for t in batches:
+                    eng.step(triplets=t)
+                    counts.append(int(eng.nbr["count"].item()))
+                eng.flush()  # raises on a row-list error bit
+                torch.cuda.synchronize()
+                key = f"a{comm_adam}_d{defer}_g{int(graph)}"
+                out[f"p_{key}"] = eng.p.cpu().numpy()
+                out[f"cnt_{key}"] = np.array(counts)
+                out[f"err_{key}"] = int(eng.err.item())
+                out[f"replays_{key}"] = int(16 in eng._graphs)
+                eng.close()
+    np.savez(os.path.join(out_dir, "order.npz"), **out)
+    dist.destroy_process_group()
+
+
+def test_sparse_step_stream_order_under_poisoned_collectives():
+    """Pins the stream order of csrc/dist.hip's sparse step (round-4 faults):
+    every collective runs on the comm stream (priority on) as a stand-in that poisons its
+    buffer for the modelled time, so a reader or writer not fenced by the fork / join
+    events sees NaN / an id of -1 (row lists: error bit, never a fault).  Graph-replayed
+    = eager, both = the unsharded objective (one rank: the whole graph) after 6 Adam steps;
+    the neighbour list holds each distinct batch user once (a repeated hub
+    user overflowed nbr_cap)."""
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_order_worker, args=(1, _free_port(), d), nprocs=1, join=True)
+        z = dict(np.load(os.path.join(d, "order.npz")))
+    tu, ti = _hub_graph()
+    A = O.lightgcn_norm_adj_vec(tu, ti, NU, NI)
+    u = torch.nn.Parameter(torch.from_numpy(z["U0"].copy()))
+    i = torch.nn.Parameter(torch.from_numpy(z["I0"].copy()))
+    opt = torch.optim.Adam([u, i], lr=LR)
+    batches = _hub_batches(tu, ti)
+    for t in batches:
+        opt.zero_grad()
+        O.lightgcn_loss(u, i, A, K, torch.from_numpy(t), REG).backward()
+        opt.step()
+    ref = torch.cat([u, i]).detach().numpy()
+    deg = np.bincount(tu, minlength=NU)
+    want = [2 * 16 + int(deg[np.unique(t[0])].sum()) for t in batches]
+    for comm_adam in (0, 1):
+        for defer in (0, 1):
+            key_g, key_e = f"a{comm_adam}_d{defer}_g1", f"a{comm_adam}_d{defer}_g0"
+            assert z[f"replays_{key_g}"] == 1 and z[f"err_{key_g}"] == 0 and z[f"err_{key_e}"] == 0
+            for key in (key_g, key_e):
+                # the claim counter: every distinct batch user's degree once (2 B ids first)
+                assert (z[f"cnt_{key}"] + 2 * 16).tolist() == want, key
+                np.testing.assert_allclose(z[f"p_{key}"], ref, rtol=0, atol=2e-5, err_msg=key)
+            # replayed = eager up to the BPR gradient atomics' order (repeated rows)
+            np.testing.assert_allclose(z[f"p_{key_g}"], z[f"p_{key_e}"], rtol=0, atol=1e-5, err_msg=key_g)
