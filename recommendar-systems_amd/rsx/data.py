@@ -156,6 +156,8 @@ class TrainDataLoader(_Loader):
         self.all_uids = df[dataset.uid_field].unique()
         self.all_item_len = len(self.all_items)
         self.sampler_kind = (config.get("rsx_sampler", "device") or "device").lower()
+        if torch.device(self.device).type == "cpu":  # the CPU configuration: the reference's own host stream
+            self.sampler_kind = "host"
         self.history_items_per_u = {u: set(g.values) for u, g in df.groupby(dataset.uid_field)[dataset.iid_field]}
         self._dev_sampler = None
         self._epoch = -1

@@ -247,7 +247,9 @@ class LayerGCN(GeneralRecommender):
 
     def __init__(self, config, dataset):
         super().__init__(config, dataset)
-        ops.require_device(self.device)
+        self.cpu = torch.device(self.device).type == "cpu"  # the CPU configuration (BASELINE C1, rsx.cpu_engine)
+        if not self.cpu:
+            ops.require_device(self.device)
         self.interaction_matrix = dataset.inter_matrix(form="coo").astype(np.float32)
         self.latent_dim = config["embedding_size"]
         self.n_layers = config["n_layers"]
@@ -257,10 +259,18 @@ class LayerGCN(GeneralRecommender):
         u0 = nn.init.xavier_uniform_(torch.empty(self.n_users, self.latent_dim))
         i0 = nn.init.xavier_uniform_(torch.empty(self.n_items, self.latent_dim))
         im = self.interaction_matrix
-        self.engine = LayerGCNEngine(im.row.astype(np.int64), im.col.astype(np.int64), self.n_users, self.n_items,
-                                     self.latent_dim, self.n_layers, self.reg_weight, config["learning_rate"] or 1e-3,
-                                     self.device, u0.numpy(), i0.numpy(), chunk=int(config["rsx_chunk"] or 32),
-                                     weight_decay=float(config["weight_decay"] or 0.0))
+        if self.cpu:
+            from .cpu_engine import CpuGCNEngine
+
+            self.engine = CpuGCNEngine("layergcn", im.row, im.col, self.n_users, self.n_items, self.latent_dim,
+                                       self.n_layers, self.reg_weight, config["learning_rate"] or 1e-3, u0.numpy(),
+                                       i0.numpy(), weight_decay=float(config["weight_decay"] or 0.0))
+        else:
+            self.engine = LayerGCNEngine(im.row.astype(np.int64), im.col.astype(np.int64), self.n_users,
+                                         self.n_items, self.latent_dim, self.n_layers, self.reg_weight,
+                                         config["learning_rate"] or 1e-3, self.device, u0.numpy(), i0.numpy(),
+                                         chunk=int(config["rsx_chunk"] or 32),
+                                         weight_decay=float(config["weight_decay"] or 0.0))
         nu = self.n_users
         self.user_embeddings = nn.Parameter(self.engine.p[:nu])
         self.item_embeddings = nn.Parameter(self.engine.p[nu:])
@@ -272,6 +282,8 @@ class LayerGCN(GeneralRecommender):
         mode = config["rsx_edge_dropout"] or config["rsx_sampler"] or "device"
         if mode not in ("device", "host"):
             raise ValueError(f"rsx_edge_dropout must be 'device' or 'host', got {mode!r}")
+        if self.cpu:  # the reference's own per-epoch draw and host graph (layergcn.py:51-89)
+            mode = "host"
         self.edge_dropout_mode = mode
         self._dev_dropout = None
 
@@ -309,6 +321,8 @@ class LayerGCN(GeneralRecommender):
 
     def full_sort_predict(self, interaction):
         f = self._final()
+        if self.cpu:  # reference layergcn.py:179-188 on the CPU tables
+            return torch.matmul(f[: self.n_users][interaction[0]], f[self.n_users:].t())
         return ops.score_dense(f[: self.n_users], interaction[0].contiguous(), f[self.n_users:])
 
     def fused_step(self, interaction, lr: float):
@@ -317,6 +331,10 @@ class LayerGCN(GeneralRecommender):
 
     def full_sort_topk(self, interaction, k: int, eval_data):
         f = self._final()
+        if self.cpu:
+            return torch.ops.rsx.fullsort_topk(f[: self.n_users].contiguous(), interaction[0].contiguous(),
+                                               f[self.n_users:].contiguous(), eval_data.mask_rowptr,
+                                               eval_data.mask_col, k)
         return ops.fullsort_topk(f[: self.n_users], interaction[0].contiguous(), f[self.n_users:],
                                  eval_data.mask_rowptr, eval_data.mask_col, k)
 

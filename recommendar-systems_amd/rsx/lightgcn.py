@@ -109,7 +109,9 @@ class LightGCN(GeneralRecommender):
 
     def __init__(self, config, dataset):
         super().__init__(config, dataset)
-        ops.require_device(self.device)
+        self.cpu = torch.device(self.device).type == "cpu"  # the CPU configuration (rsx.cpu_engine)
+        if not self.cpu:
+            ops.require_device(self.device)
         self.interaction_matrix = dataset.inter_matrix(form="coo").astype(np.float32)
         self.latent_dim = config["embedding_size"]
         self.n_layers = config["n_layers"]
@@ -120,6 +122,19 @@ class LightGCN(GeneralRecommender):
         im = self.interaction_matrix
         wd = config["weight_decay"] or 0.0
         world, rank = _world()
+        if self.cpu:  # torch.ops.rsx's CPU kernels; one process (the reference's CPU run)
+            from .cpu_engine import CpuGCNEngine
+
+            self.sharded = self.dp = False
+            self.engine = CpuGCNEngine("lightgcn", im.row, im.col, self.n_users, self.n_items, self.latent_dim,
+                                       self.n_layers, self.reg_weight, config["learning_rate"] or 1e-3, u0.numpy(),
+                                       i0.numpy(), weight_decay=float(wd))
+            nu = self.n_users
+            self.embedding_dict = nn.ParameterDict({
+                "user_emb": nn.Parameter(self.engine.p[:nu]),
+                "item_emb": nn.Parameter(self.engine.p[nu:]),
+            })
+            return
         self.sharded = world > 1 or bool(config["rsx_sharded"])
         self.dp = self.sharded and str(config["rsx_dist"] or "rowshard").lower() == "dp"
         if self.dp:
@@ -210,10 +225,15 @@ class LightGCN(GeneralRecommender):
         return torch.cat([self.embedding_dict["user_emb"], self.embedding_dict["item_emb"]], 0)
 
     def forward(self):
+        if self.cpu:
+            final = self.engine._prop(self.engine.norm_adj, self.get_ego_embeddings())
+            return final[: self.n_users], final[self.n_users:]
         final = _Propagate.apply(self.embedding_dict["user_emb"], self.embedding_dict["item_emb"], self.engine)
         return final[: self.n_users], final[self.n_users:]
 
     def calculate_loss(self, interaction):
+        if self.cpu:  # the same ops on CPU tensors (autograd reaches both parameters)
+            return self.engine.loss(self.get_ego_embeddings(), interaction, self.engine.norm_adj)
         if self.sharded:
             raise NotImplementedError("the sharded LightGCN trains through fused_step_index (rsx.trainer's fused path)")
         self.engine.invalidate()
@@ -230,6 +250,8 @@ class LightGCN(GeneralRecommender):
         if self.sharded:
             raise NotImplementedError("the sharded LightGCN evaluates through full_sort_topk_local")
         f = self._final()
+        if self.cpu:  # reference lightgcn.py:158-166 on the CPU tables
+            return torch.matmul(f[: self.n_users][interaction[0]], f[self.n_users:].t())
         return ops.score_dense(f[: self.n_users], interaction[0].contiguous(), f[self.n_users:])
 
     # -- rsx fast paths ----------------------------------------------------------
@@ -266,6 +288,10 @@ class LightGCN(GeneralRecommender):
 
     def full_sort_topk(self, interaction, k: int, eval_data):
         f = self._final()
+        if self.cpu:
+            return torch.ops.rsx.fullsort_topk(f[: self.n_users].contiguous(), interaction[0].contiguous(),
+                                               f[self.n_users:].contiguous(), eval_data.mask_rowptr,
+                                               eval_data.mask_col, k)
         return ops.fullsort_topk(f[: self.n_users], interaction[0].contiguous(), f[self.n_users:],
                                  eval_data.mask_rowptr, eval_data.mask_col, k)
 
@@ -281,6 +307,6 @@ class LightGCN(GeneralRecommender):
         count, so the Trainer reports the batch index), or None where the step has no flag
         (row-sharded engine)."""
         e = self.engine
-        if self.sharded and not getattr(self, "dp", False):
+        if getattr(self, "cpu", False) or (self.sharded and not getattr(self, "dp", False)):
             return None
         return e.halt, e.step_count

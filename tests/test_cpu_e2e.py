@@ -1,0 +1,125 @@
+"""End-to-end parity of the CPU configuration (BASELINE C1: "CPU PyTorch reference path,
+plumbing, no GPU"): the reference's training flow (quick_start order, seed 999, the
+reference's host triplet stream and edge-dropout draws) through the drop-in rsx models
+on a CPU device, i.e. through torch.ops.rsx's CPU kernels (rsx.cpu_engine,
+csrc/cpu_ops.cpp), compared with what the reference itself produced on the same data
+(tests/golden, captured by tools/capture_golden.py).  Same tolerances as the GPU e2e
+test (tests/test_gpu_e2e.py): parameters after 2-3 epochs of Adam within atol 5e-5,
+metric dicts within 1e-4, the masked epoch graphs bit for bit."""
+import os
+import shutil
+
+import numpy as np
+import pytest
+import torch
+
+from helpers import coo_sorted, csr_to_sorted, metric_dict, params
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _setup(tmp_path, model, extra):
+    from rsx.config import Config
+    from rsx.data import EvalDataLoader, RecDataset, TrainDataLoader
+
+    d = tmp_path / "data" / "baby"
+    d.mkdir(parents=True)
+    shutil.copy(os.path.join(GOLD, "gold_small.inter"), d / "baby.inter")
+    cfg = dict(data_path=str(tmp_path / "data") + "/", train_batch_size=512, eval_batch_size=256,
+               is_multimodal_model=False, use_gpu=False)
+    cfg.update(extra)
+    c = Config(model, "baby", cfg)
+    assert c["device"].type == "cpu"
+    for k in c["hyper_parameters"]:
+        if isinstance(c[k], list):
+            c[k] = c[k][0]
+    ds = RecDataset(c)
+    tr, va, te = ds.split()
+    for x in (ds, tr, va, te):
+        str(x)
+    train = TrainDataLoader(c, tr, batch_size=512, shuffle=True)
+    valid = EvalDataLoader(c, va, additional_dataset=tr, batch_size=256)
+    test = EvalDataLoader(c, te, additional_dataset=tr, batch_size=256)
+    return c, train, valid, test
+
+
+def _run(tmp_path, model, extra, epochs, fused=True):
+    from rsx.cpu_engine import CpuGCNEngine
+    from rsx.trainer import Trainer
+    from rsx.utils import get_model, init_seed
+
+    c, train, valid, test = _setup(tmp_path, model, dict(extra, rsx_fused_step=fused))
+    assert train.sampler_kind == "host"  # the reference's stream on the CPU
+    init_seed(c["seed"])
+    train.pretrain_setup()
+    m = get_model(model)(c, train)
+    assert isinstance(m.engine, CpuGCNEngine)
+    t = Trainer(c, m)
+    graphs = []
+    for epoch in range(epochs):
+        m.cur_epoch = epoch
+        m.pre_epoch_processing()
+        graphs.append(m.engine.train_adj)
+        loss, _ = t._train_epoch(train, epoch)
+        assert not torch.is_tensor(loss)
+        if t.lr_scheduler is not None:
+            t.lr_scheduler.step()
+        t._epoch_for_lr += 1
+    return m, t.evaluate(valid), t.evaluate(test), graphs
+
+
+def _compare_metrics(res, ref):
+    assert res.keys() == ref.keys()
+    for k in ref:
+        assert abs(res[k] - ref[k]) <= 1e-4 + 1e-12, (k, res[k], ref[k])
+
+
+@pytest.mark.parametrize("fx,dropout", [("layergcn_small", 0.0), ("layergcn_drop_small", 0.1)])
+def test_cpu_layergcn_two_epochs_vs_reference(tmp_path, golden, fx, dropout):
+    z = golden(fx)
+    m, vres, tres, graphs = _run(tmp_path, "LayerGCN", dict(n_layers=[2], reg_weight=[1e-2], dropout=[dropout]), 2)
+    if dropout > 0:
+        for e, (rp, col, val) in enumerate(graphs):
+            ref = coo_sorted(z[f"e{e}_masked_idx"].astype(np.int64), z[f"e{e}_masked_val"])
+            mine = csr_to_sorted(rp.numpy(), col.numpy(), val.numpy())
+            for x, y in zip(ref, mine):
+                assert np.array_equal(x, y), e
+    pu, pi = params(z, "epoch1_param.", "LayerGCN")
+    np.testing.assert_allclose(m.user_embeddings.detach().numpy(), pu, rtol=0, atol=5e-5)
+    np.testing.assert_allclose(m.item_embeddings.detach().numpy(), pi, rtol=0, atol=5e-5)
+    _compare_metrics(vres, metric_dict(z, "epoch1_valid"))
+    _compare_metrics(tres, metric_dict(z, "epoch1_test"))
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_cpu_lightgcn_three_epochs_vs_reference(tmp_path, golden, fused):
+    """fused: the engine's step; False: the reference Trainer's autograd + torch Adam on
+    calculate_loss (the ops' autograd through both parameters)."""
+    z = golden("lightgcn_small")
+    m, vres, tres, _ = _run(tmp_path, "LightGCN", dict(n_layers=[3], reg_weight=[1e-2]), 3, fused=fused)
+    pu, pi = params(z, "epoch2_param.", "LightGCN")
+    np.testing.assert_allclose(m.embedding_dict["user_emb"].detach().numpy(), pu, rtol=0, atol=5e-5)
+    np.testing.assert_allclose(m.embedding_dict["item_emb"].detach().numpy(), pi, rtol=0, atol=5e-5)
+    _compare_metrics(vres, metric_dict(z, "epoch2_valid"))
+    _compare_metrics(tres, metric_dict(z, "epoch2_test"))
+
+
+def test_main_layergcn_baby_trains_without_a_gpu(tmp_path):
+    """`main.py -m LayerGCN -d baby` on a GPU-less box: the CLI, a baby-shaped dataset
+    (rsx.synth), one grid point, two epochs through the CPU kernels, a result dict."""
+    import subprocess
+    import sys
+
+    from rsx import synth
+
+    df = synth.shaped("baby", seed=0)
+    synth.write_inter(df, str(tmp_path / "data"), "baby")
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    main = os.path.join(repo, "recommendar-systems_amd", "main.py")
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", RSX_CPU_THREADS="8")
+    r = subprocess.run([sys.executable, main, "-m", "LayerGCN", "-d", "baby", f"data_path={tmp_path / 'data'}/",
+                        "epochs=2", "n_layers=[2]", "dropout=[0.1]", "reg_weight=[1e-2]", "is_multimodal_model=False",
+                        "use_gpu=False"], cwd=tmp_path, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    log = "".join(open(os.path.join(tmp_path, "log", f)).read() for f in os.listdir(tmp_path / "log"))
+    assert "epoch 1 training" in log and "recall@20" in log and "All Over" in log
