@@ -279,6 +279,11 @@ def bench_model(args):
         np.save(os.path.join(root, w["dataset"], ft), feats[1])
     cfg = dict(data_path=root + "/", train_batch_size=args.batch, rsx_sampler="device",
                is_multimodal_model=w["model"] == "SMORE", **w["cfg"])
+    from rsx.dist import sim_comm_params
+
+    sim = sim_comm_params() if (world == 1 and w["model"] == "SMORE") else None
+    if sim:  # rank 0 of a modelled W-rank users-sharded job (rsx.smore_dist.Comm's latency injection)
+        cfg["rsx_sharded"] = True
     c = Config(w["model"], w["dataset"], cfg)
     if world > 1:
         c["device"] = torch.device("cuda", _local_device())  # (the rehearsal mode puts every rank on GPU 0)
@@ -429,11 +434,21 @@ def bench_model(args):
         "fullsort": {"eval_users": n_eval, "n_items": ni, "s_per_eval_incl_forward_and_metrics": eval_s},
         "model_build_s": build_s, "roofline": roof, "roofline_kernels": kernels, "cpu_baseline": cpu,
     }
+    if sim:
+        Wm = int(sim["world"])
+        out["config"]["parallelism"] = f"usershard{Wm} (latency-injected, rank 0 of {Wm})"
+        out["config"]["global_batch"] = int(getattr(model, "local_batch", args.batch)) * Wm
+        out["latency_injection"] = dict(
+            sim, modelled_job={"world": Wm, "interactions_per_s": Wm * n / wall, "ms_per_step": wall * 1e3 / args.steps},
+            note="value / ms_per_step: rank 0 of the modelled job (its 1/W of the users and item rows, a batch of "
+                 "its own; every collective a comm-stream stand-in of the modelled time): the job's rate is world x "
+                 "value; the fullsort figures are this rank's users only")
     if rank == 0:
         _json_line(out)
-    if world > 1:
+    if world > 1 or sim:
         if getattr(model, "comm", None) is not None:
             model.comm.close()
+    if world > 1:
         torch.distributed.destroy_process_group()
 
 
@@ -687,10 +702,12 @@ def main():
     # share of a W-rank c4 job (8/W of the 8 user chunks, batch 2048/W) with every collective
     # replaced by a comm-stream kernel holding the modelled time, CUs and HBM bytes of that
     # collective at W ranks: the step time is the modelled job's critical path
+    # (c2 / baby: the data-parallel leg's rank 0 of a W-rank job, csrc/dp.hip's sim mode: the
+    # job's global batch and union through the step, the two all-gathers modelled)
     from rsx.dist import sim_comm_params
 
-    sim = sim_comm_params() if big else None
-    if sim:  # time this rank's share of the modelled job (csrc/dist.hip: the owner Adam on 1/W items)
+    sim = sim_comm_params()
+    if sim and big:  # time this rank's share of the modelled job (csrc/dist.hip: the owner Adam on 1/W items)
         os.environ.setdefault("RSX_COMM_SIM_SHARE", "1")
     w_eff = sim["world"] if sim else world
     if sim and world != 1:
@@ -703,14 +720,19 @@ def main():
     scheme = args.dist or ("rowshard" if big else "dp")
     if big and scheme != "rowshard":
         raise SystemExit("--workload c4 is the row-sharded strong-scaling leg")
-    dp = not big and not args.sharded and (args.dp or (world > 1 and scheme == "dp"))
+    dp = not big and not args.sharded and (args.dp or ((world > 1 or sim is not None) and scheme == "dp"))
     tu, ti, vu_all, vi_all, nu, ni, d, desc = load_graph(args.workload, rank, world, args.c4_chunks, replicated=dp)
     if big and args.c4_chunks:
         desc += f" [only {args.c4_chunks} of 8 user chunks built]"
-    if sim:
+    if sim and big:
         desc += (f" [latency-injected model of rank 0 of a {sim['world']}-rank job: its {args.c4_chunks}/8 user "
                  f"share, batch {B}, every collective a comm-stream kernel of the modelled time at "
                  f"{sim['busbw_gbs']:.0f} GB/s bus bandwidth + {sim['latency_us']:.0f} us]")
+    elif sim:
+        desc += (f" [latency-injected model of rank 0 of a {sim['world']}-rank data-parallel job: the graph "
+                 f"replicated, B={B} per rank, global batch {B * sim['world']} (the other ranks' triplets in their "
+                 f"slots), both all-gathers comm-stream kernels of the modelled time at {sim['busbw_gbs']:.0f} GB/s "
+                 f"bus bandwidth + {sim['latency_us']:.0f} us]")
     if dp:
         desc = desc.replace("per rank), B=2048 per rank", "), the graph replicated on every rank, "
                                                               f"B={B} per rank, global batch {B * world}")
@@ -1007,8 +1029,8 @@ def main():
                                "strong-scaling leg: the fixed C4 graph and global batch split over the ranks"
                                if big else "baby, weak scaling"),
                        "parallelism": (f"dp{world}" if dp else f"rowshard{world}" if sharded else "single"),
-                       "scheme": ("data-parallel: graph + tables replicated, global batch N*B, per step an "
-                                  "all-gather of the ranks' triplets and loss-gradient rows (rsx.dp)" if dp else
+                       "scheme": ("data-parallel: graph + tables replicated, global batch N*B, per step one "
+                                  "all-gather of the ranks' triplets (rsx.dp)" if dp else
                                   "row-sharded users, replicated items, item partials all-reduced per layer "
                                   "(rsx.dist)" if sharded else "one GPU")},
             "fullsort_items_per_s": items_per_s,
@@ -1038,7 +1060,17 @@ def main():
             "gpu_ms_per_step_events": gpu_ms / args.steps,
             "train_loss_mean": loss_mean,
         }
-        if sim:
+        if sim and dp:
+            lib = L.lib()
+            Wm = sim["world"]
+            out["latency_injection"] = dict(sim, per_collective_ms={
+                "allgather_slots": 1e3 * lib.rsx_comm_sim_seconds(eng._comm, L.RSX_COLL_ALLGATHER,
+                                                                  float(3 * eng.cap + 1) * 8 * Wm)},
+                modelled_job={"world": Wm, "interactions_per_s": Wm * total_inter / wall,
+                              "global_batch": B * Wm, "ms_per_step": ms},
+                note="value / ms_per_step: rank 0 of the modelled data-parallel job (every rank runs the same "
+                     "step on the replicated graph, so the job's rate is world x value)")
+        elif sim:
             X = float(ni) * d * 4
             lib = L.lib()
             # one stand-alone injected all-reduce of the item block, timed on the device: the

@@ -972,18 +972,24 @@ int rsx_sharded_lightgcn_forward(const rsx_sharded_lgcn_step* st, rsx_stream_t s
  * trains the global batch of all ranks' triplets (rank r its own [3][batch]): the
  * reference objective at batch sum_r batch_r (src/models/lightgcn.py:132-156 with the
  * mean and the Frobenius norms over the global batch; src/common/trainer.py:186-238
- * at batch W B).  The step is lgcn_step_stored_layers' (K = 2..4) with two
- * exchanges, both all-gathers: every rank's triplets (`slots`, [world][3 cap + 1]
- * int64: count, users, positives, negatives) and every rank's G' = dL/dfinal/(K+1)
- * at its own occurrence rows plus its four f64 loss totals (`blocks`, [world]
- * [rsx_dp_block_floats(cap, d)] floats).  Each rank merges the blocks into the same
- * G' (per row a sum over ranks in rank order, led through `pos` [world][N] int64,
- * zero-filled once), counts every triplet's rows (reg_cnt, the global regulariser),
- * tags the union of the ranks' batch rows (row_tag; own_tag: this rank's, for its
- * last forward layer) and runs the same backward and Adam.  tag_dev: the step's tag
- * on the device (> 0, fresh per step, e.g. the low word of adam.step_dev), so the
- * step captures once in a hipGraph.  g and reg_cnt must be zero between steps (true
- * from zero-filled buffers and after every step).
+ * at batch W B).  The step is lgcn_step_stored_layers' (K = 2..4) with ONE exchange:
+ * an all-gather of every rank's triplets (`slots`, [world][3 cap + 1] int64: count,
+ * users, positives, negatives), issued on the communicator's stream while the forward
+ * runs.  Every rank then evaluates the whole global batch itself — the last forward
+ * layer on the union of the ranks' batch rows, the BPR loss and G' = dL/dfinal/(K+1)
+ * of every triplet (G' accumulated per row in 64-bit fixed point, so the sum does not
+ * depend on the order of its atomics), the backward and Adam — with the same kernels
+ * on the same inputs, so the replicas stay bit-identical with no other exchange.
+ * row_tag [N] int32 (zero-filled once): the union's tags; reg_cnt [3 N + 4] (zero-
+ * filled once): the global regulariser's occurrence counts; tag_dev: the step's tag on
+ * the device (> 0, fresh per step, e.g. the low word of adam.step_dev), so the step
+ * captures once in a hipGraph.  g, reg_cnt and `work` must be zero-filled before the
+ * first step (every step leaves them so).  `work`: rsx_dp_work_bytes(n_users + n_items,
+ * d, cap, world) bytes (the fixed-point accumulators, the occurrence sort, the loss
+ * partials).  Over a latency-injected communicator (rsx_comm_init_sim, modelled world
+ * W) the one rank times rank 0 of a W-rank job: slots hold W ranks, the caller fills
+ * slots 1..W-1 (the other ranks' triplets), `work` is sized for W, and the stand-in
+ * all-gather moves (W-1)/W of the W-slot buffer.
  */
 typedef struct rsx_dp_lgcn_step {
     const rsx_csr* adj;         /* the whole graph */
@@ -1003,21 +1009,18 @@ typedef struct rsx_dp_lgcn_step {
     rsx_adam adam;
     float* loss_out;            /* [1]: the global batch's loss */
     double* loss_acc;           /* [1] or NULL */
-    void* ws; size_t ws_bytes;  /* >= rsx_bpr_ws_bytes(batch) */
     rsx_comm_t comm;
     int32_t* row_tag;           /* [N] */
-    int32_t* own_tag;           /* [N] */
     const int32_t* tag_dev;     /* [1] */
     int32_t* reg_cnt;           /* [3 N + 4] */
     int32_t* halt;              /* [2] or NULL: set by a NaN global loss (as rsx_lgcn_step.halt) */
     int64_t cap;                /* per-rank batch capacity (every rank the same) */
     int64_t* slots;             /* [world][3 cap + 1] */
-    float* blocks;              /* [world][rsx_dp_block_floats(cap, d)] */
-    int64_t* pos;               /* [world][N] */
+    void* work; size_t work_bytes;  /* >= rsx_dp_work_bytes(...), zero-filled once */
 } rsx_dp_lgcn_step;
 
 int rsx_dp_lightgcn_step(const rsx_dp_lgcn_step* st, rsx_stream_t stream);
-size_t rsx_dp_block_floats(int64_t cap, int32_t d);
+size_t rsx_dp_work_bytes(int64_t n_rows, int32_t d, int64_t cap, int32_t world);
 
 /* ------------------------------------------------------------------------ */
 /* CPU kernels (host memory): the CPU dispatch key of torch.ops.rsx.*        */

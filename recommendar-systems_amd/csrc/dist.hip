@@ -133,6 +133,8 @@ hipError_t comm_streams_create(rsx_comm_s* c) {
 
 int comm_rank(rsx_comm_t c) { return c->rank; }
 int comm_world(rsx_comm_t c) { return c->world; }
+// The modelled world of a latency-injected communicator (0 for a real or host-hook one).
+int comm_sim_world(rsx_comm_t c) { return c->sim_world; }
 // The stream the communicator's exchanges run on, for work issued from `s` (host-hook
 // communicators: `s` itself): the priority stream for eager issue, the capture stream
 // while `s` is being captured; a call issued on either comm stream stays on it.  Small

@@ -7,51 +7,99 @@
 // at batch W * B — mean BPR over the global batch + reg * (|U|_F + |P|_F + |N|_F) / W B
 // with the Frobenius norms over the global batch's rows.
 //
-// What crosses the ranks is small.  The propagation is linear, so the gradient of the
-// embedding table is the backward operator applied to G' = dL/dfinal / (K+1), and G' is
-// nonzero on the batch rows only: rank r's share G'_r lives on its own <= 3B rows.  So a
-// step exchanges (1) every rank's triplets (3B int64, gathered while the forward runs)
-// and (2) every rank's G'_r at its own occurrence rows plus four f64 loss totals
-// (3B d floats): an all-gather of ~1.6 MB per rank at sports shape, against 13.8 MB for
-// an all-reduce of the dense gradient.  Every rank then merges the blocks into the same
-// G' (a deterministic rank-ordered sum per row, below), counts every triplet's rows for
-// the regulariser, and runs the same backward and Adam: the replicas stay bit-identical
-// with no parameter exchange.  Per step: 2 all-gathers; ~2 x 2.2 % of the C2 step's
-// kernels extra (pack, gather, index, merge).
+// Only the triplets cross the ranks.  The propagation is replicated (every rank runs it
+// on the whole graph: on these graphs its cost is per step, not per triplet), so every
+// rank can evaluate the loss of EVERY rank's triplets itself once it knows them: a step
+// all-gathers the ranks' triplets (3B int64 per rank, 48 KB at B = 2048, on the comm
+// stream while the forward runs) and nothing else.  Round 4 all-gathered every rank's
+// dL/dfinal rows instead (1.6 MB per rank, on the critical path between the loss and the
+// backward); that exchange is gone.  Every rank then runs the same kernels on the same
+// inputs: the last forward layer on the union of the ranks' batch rows, the BPR loss of
+// the global batch, its gradient G' = dL/dfinal / (K+1), the backward and Adam — so the
+// replicas stay bit-identical with no parameter exchange, provided every kernel is
+// deterministic.  The SpMMs and the loss reductions are (fixed orders); G' is a sum of
+// per-occurrence terms over rows that repeat in the batch, so it is accumulated in
+// 64-bit fixed point (integer adds commute: the order of the atomics cannot change a
+// bit), at a power-of-two scale from a bound on the batch's rows, then rounded to f32
+// once.  A row with one occurrence gets exactly the f32 term the single-GPU step adds.
 //
-// Merge.  Rank r's block row j is G'_r at the row x of occurrence j (duplicate
-// occurrences in one rank carry identical rows: gathered from the same table row).
-// pos[r][x] = (stamp << 32) | j for SOME occurrence j of x in rank r (a benign race of
-// equal candidates); the occurrence that won pos[r][x], in the lowest rank holding x, is
-// x's leader, and the leader writes G'[x] = sum over ranks r' in rank order of
-// block[r'][pos[r'][x]].  Every rank evaluates the same sums in the same order.  The
-// stamp is the step's tag, so pos is never cleared.
+// Per step on the comm stream (hidden behind the forward): the triplet all-gather, the
+// union tags and global regulariser counts (dp_index), and a stable radix sort of the
+// W 3 B occurrences by row, which lets the gradient pass add each run of equal rows in
+// registers and issue one atomic per run instead of one per occurrence (hot items occur
+// hundreds of times in a global batch).
+#include <hipcub/hipcub.hpp>
+
 #include "rsx_common.hpp"
 
 namespace rsx {
 
 int spmm_dispatch(const rsx_csr& a, const float* x, int d, const rsx_epilogue& e, float* slab, hipStream_t s);
-int spmm_dispatch_tagging(const rsx_csr& a, const float* x, int d, const rsx_epilogue& e, float* slab,
-                          hipStream_t s, const TagJob& tj);
-int bpr_fused_args(const float* fin, const float* ego, int64_t n_users, int64_t n_items, int32_t d,
-                   const int64_t* trip, int64_t batch, float reg, float g_div, float* g_fin, int32_t* reg_cnt,
-                   float* loss_out, double* loss_acc, void* ws, size_t ws_bytes, hipStream_t s, int32_t* halt,
-                   int32_t tag, const int64_t* dp_slots, int64_t dp_slot_len, int32_t dp_world, double* dp_tot);
 int comm_rank(rsx_comm_t c);
 int comm_world(rsx_comm_t c);
+int comm_sim_world(rsx_comm_t c);
 hipStream_t comm_stream(rsx_comm_t c, hipStream_t s);
 hipEvent_t comm_event(rsx_comm_t c);
 hipEvent_t collective(rsx_comm_t c, int op, void* buf, int64_t count, int dtype, hipStream_t s, int* rc);
 
 namespace {
 
-constexpr int kHdr = 8;  // block header: four f64 loss totals
+constexpr int kBlk = 256;
+constexpr int kChunk = 16;  // sorted occurrences per lane group in the gradient pass
+
+// The step's workspace (rsx_dp_lgcn_step.work), carved in this order, 256-B aligned.
+struct Work {
+    unsigned long long* acc;  // [N][d] fixed-point G' accumulators (zero between steps)
+    int32_t *ka, *kb, *va, *vb;  // occurrence keys (rows) / ids, radix-sort double buffers
+    float* coef;              // [W][cap] per-triplet dL/d(s+ - s-)
+    double* part;             // [n_blk_a][5] loss, |U|^2, |P|^2, |N|^2, max |f| partials
+    int32_t* meta;            // [4]: done counter, fixed-point exponent
+    void* temp;               // hipCUB radix-sort temp storage
+    size_t temp_bytes;
+    size_t total;
+};
+
+size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
+
+int key_bits(int64_t N) {  // bits of the sort key: rows 0..N-1, padding N
+    int b = 1;
+    while ((int64_t(1) << b) <= N) ++b;
+    return b;
+}
+
+Work carve(void* base, int64_t N, int d, int64_t cap, int W) {
+    Work w = {};
+    const int64_t n_occ = (int64_t)W * 3 * cap, n_trip = (int64_t)W * cap;
+    const int64_t n_blk = (n_trip + 3) / 4 + 1;  // phase A: >= 4 triplets per block (d <= 256)
+    char* p = static_cast<char*>(base);
+    size_t o = 0;
+    auto take = [&](size_t bytes) {
+        void* q = p ? p + o : nullptr;
+        o += al(bytes);
+        return q;
+    };
+    w.acc = static_cast<unsigned long long*>(take((size_t)N * d * 8));
+    w.ka = static_cast<int32_t*>(take((size_t)n_occ * 4));
+    w.kb = static_cast<int32_t*>(take((size_t)n_occ * 4));
+    w.va = static_cast<int32_t*>(take((size_t)n_occ * 4));
+    w.vb = static_cast<int32_t*>(take((size_t)n_occ * 4));
+    w.coef = static_cast<float*>(take((size_t)n_trip * 4));
+    w.part = static_cast<double*>(take((size_t)n_blk * 5 * 8));
+    w.meta = static_cast<int32_t*>(take(16));
+    hipcub::DoubleBuffer<int32_t> k(w.ka, w.kb), v(w.va, w.vb);
+    size_t tb = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k, v, (int)n_occ, 0, key_bits(N));
+    w.temp = take(tb);
+    w.temp_bytes = tb;
+    w.total = o;
+    return w;
+}
 
 // slot = [B, users[cap], positives[cap], negatives[cap]] (tail zero)
 // (step: the Adam counter the step increments first, or NULL)
-__global__ __launch_bounds__(256) void dp_pack(const int64_t* __restrict__ trip, int64_t B, int64_t cap,
-                                               int64_t* __restrict__ slot, int64_t* __restrict__ step) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+__global__ __launch_bounds__(kBlk) void dp_pack(const int64_t* __restrict__ trip, int64_t B, int64_t cap,
+                                                int64_t* __restrict__ slot, int64_t* __restrict__ step) {
+    const int64_t i = (int64_t)blockIdx.x * kBlk + threadIdx.x;
     if (i > 3 * cap) return;
     if (i == 0) {
         slot[0] = B;
@@ -63,61 +111,137 @@ __global__ __launch_bounds__(256) void dp_pack(const int64_t* __restrict__ trip,
 }
 
 // occurrence i = (r, j = kind cap + t) of the gathered slots -> its table row (or -1)
-__device__ __forceinline__ int64_t occ_row(const int64_t* slots, int64_t L, int64_t cap, int64_t n_users, int64_t i,
-                                           int64_t* r_out, int64_t* j_out) {
+__device__ __forceinline__ int64_t occ_row(const int64_t* slots, int64_t cap, int64_t n_users, int64_t i) {
+    const int64_t L = 3 * cap + 1;
     const int64_t r = i / (3 * cap), j = i - r * 3 * cap;
     const int64_t* slot = slots + r * L;
-    const int64_t t = j % cap;
-    *r_out = r;
-    *j_out = j;
-    if (t >= slot[0]) return -1;
+    if (j % cap >= slot[0]) return -1;
     const int64_t id = slot[1 + j];
     return j < cap ? id : n_users + id;
 }
 
-// Union tags, global occurrence counts (the regulariser's), and pos[r][x] for every
-// occurrence of every rank (runs on the comm stream once the triplets are gathered).
-__global__ __launch_bounds__(256) void dp_index(const int64_t* __restrict__ slots, int32_t W, int64_t cap,
-                                                int64_t n_users, int64_t N, int64_t* __restrict__ pos,
-                                                int32_t* __restrict__ row_tag, int32_t* __restrict__ reg_cnt,
-                                                const int32_t* __restrict__ tag_dev) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+// (comm stream, once the triplets are gathered) union tags, global occurrence counts (the
+// regulariser's), and the sort input: key = row (N for a padding slot), value = occurrence
+__global__ __launch_bounds__(kBlk) void dp_index(const int64_t* __restrict__ slots, int32_t W, int64_t cap,
+                                                 int64_t n_users, int64_t N, int32_t* __restrict__ row_tag,
+                                                 int32_t* __restrict__ reg_cnt, const int32_t* __restrict__ tag_dev,
+                                                 int32_t* __restrict__ key, int32_t* __restrict__ val) {
+    const int64_t i = (int64_t)blockIdx.x * kBlk + threadIdx.x;
     if (i >= (int64_t)W * 3 * cap) return;
-    int64_t r, j;
-    const int64_t x = occ_row(slots, 3 * cap + 1, cap, n_users, i, &r, &j);
+    const int64_t x = occ_row(slots, cap, n_users, i);
+    key[i] = x < 0 ? (int32_t)N : (int32_t)x;
+    val[i] = (int32_t)i;
     if (x < 0) return;
-    const int32_t stamp = *tag_dev;
-    pos[r * N + x] = ((int64_t)stamp << 32) | j;
-    row_tag[x] = stamp;
-    atomicAdd(reg_cnt + 3 * x + j / cap, 1);
+    row_tag[x] = *tag_dev;
+    atomicAdd(reg_cnt + 3 * x + (i % (3 * cap)) / cap, 1);
 }
 
-// One lane group (D/4 lanes, a float4 each) per occurrence: the leaders write the
-// rank-ordered sums.  Block 0 also finishes the global loss (bpr_fused's formula on the
-// summed totals) and the regulariser's three scales.
+// Phase A: every triplet of every rank — s+ - s- from the final rows, the BPR term and its
+// coefficient (bpr_fused's formulas at the global batch size), the regulariser's squared
+// norms on the ego rows and max |f| (the fixed-point scale's bound); per-block f64
+// partials, reduced by the last block in a fixed order into the loss, the regulariser's
+// three scales (reg_cnt's tail, as the single-GPU BPR leaves them) and the exponent.
 template <int D>
-__global__ __launch_bounds__(256) void dp_merge(const int64_t* __restrict__ slots, int32_t W, int64_t cap,
-                                                int64_t n_users, int64_t N, const int64_t* __restrict__ pos,
-                                                const float* __restrict__ blocks, int64_t stride,
-                                                float* __restrict__ g, const int32_t* __restrict__ tag_dev,
-                                                int32_t* __restrict__ reg_cnt, float reg, float* loss_out,
-                                                double* loss_acc, int32_t* halt) {
-    constexpr int G = D / 4, GPB = 256 / G;
-    const int32_t stamp = *tag_dev;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        double tl = 0.0, qu = 0.0, qp = 0.0, qn = 0.0;
-        int64_t bg = 0;
-        for (int r = 0; r < W; ++r) {
-            const double* h = reinterpret_cast<const double*>(blocks + (int64_t)r * stride + 3 * cap * D);
-            tl += h[0];
-            qu += h[1];
-            qp += h[2];
-            qn += h[3];
-            bg += slots[(int64_t)r * (3 * cap + 1)];
+__global__ __launch_bounds__(kBlk) void dp_bpr_coef(const int64_t* __restrict__ slots, int32_t W, int64_t cap,
+                                                    int64_t n_users, int64_t N, const float* __restrict__ fin,
+                                                    const float* __restrict__ ego, float g_div, float reg,
+                                                    float* __restrict__ coef, double* __restrict__ part,
+                                                    int32_t* __restrict__ meta, int32_t* __restrict__ reg_cnt,
+                                                    float* loss_out, double* loss_acc, int32_t* halt,
+                                                    const int32_t* __restrict__ tag_dev) {
+    constexpr int G = D / 4, GPB = kBlk / G;
+    const int li = threadIdx.x % G;
+    const int64_t L = 3 * cap + 1;
+    const int64_t b = (int64_t)blockIdx.x * GPB + threadIdx.x / G;  // triplet slot r cap + t
+    int64_t bg = 0;
+    for (int r = 0; r < W; ++r) bg += slots[(int64_t)r * L];
+    double t_loss = 0.0, t_u = 0.0, t_p = 0.0, t_n = 0.0;
+    float t_max = 0.f;
+    if (b < (int64_t)W * cap) {
+        const int64_t r = b / cap, t = b - r * cap;
+        const int64_t* slot = slots + r * L;
+        if (t < slot[0]) {
+            const int64_t u = slot[1 + t], p = n_users + slot[1 + cap + t], n = n_users + slot[1 + 2 * cap + t];
+            const float4 fu = ld4(fin + u * D + li * 4), fp = ld4(fin + p * D + li * 4), fn = ld4(fin + n * D + li * 4);
+            const float4 eu = ld4(ego + u * D + li * 4), ep = ld4(ego + p * D + li * 4), en = ld4(ego + n * D + li * 4);
+            const float sp = group_sum<G>(dot4(fu, fp)), sn = group_sum<G>(dot4(fu, fn));
+            const float delta = sp - sn;
+            const float sg = 1.f / (1.f + expf(-delta));
+            const float term = -logf(1e-10f + sg);
+            const float c = -(sg * (1.f - sg)) / (1e-10f + sg) / (float)bg;
+            if (li == 0) {
+                coef[b] = c;
+                t_loss = (double)term;
+            }
+            t_u = (double)dot4(eu, eu);
+            t_p = (double)dot4(ep, ep);
+            t_n = (double)dot4(en, en);
+            const float m0 = fmaxf(fmaxf(fabsf(fu.x), fabsf(fu.y)), fmaxf(fabsf(fu.z), fabsf(fu.w)));
+            const float m1 = fmaxf(fmaxf(fabsf(fp.x), fabsf(fp.y)), fmaxf(fabsf(fp.z), fabsf(fp.w)));
+            const float m2 = fmaxf(fmaxf(fabsf(fn.x), fabsf(fn.y)), fmaxf(fabsf(fn.z), fabsf(fn.w)));
+            t_max = fmaxf(m0, fmaxf(m1, m2));
+            if (t_max != t_max) t_max = __builtin_huge_valf();  // NaN rows: the scale's clamp below
+        } else if (li == 0) {
+            coef[b] = 0.f;
         }
+    }
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) {
+        t_loss += __shfl_xor(t_loss, o, kWave);
+        t_u += __shfl_xor(t_u, o, kWave);
+        t_p += __shfl_xor(t_p, o, kWave);
+        t_n += __shfl_xor(t_n, o, kWave);
+        t_max = fmaxf(t_max, __shfl_xor(t_max, o, kWave));
+    }
+    __shared__ double red[kBlk / kWave][5];
+    const int wv = threadIdx.x / kWave;
+    if (threadIdx.x % kWave == 0) {
+        red[wv][0] = t_loss;
+        red[wv][1] = t_u;
+        red[wv][2] = t_p;
+        red[wv][3] = t_n;
+        red[wv][4] = (double)t_max;
+    }
+    __syncthreads();
+    __shared__ int last;
+    if (threadIdx.x < 5) {
+        double v = 0.0;
+        for (int w = 0; w < kBlk / kWave; ++w) v = threadIdx.x == 4 ? fmax(v, red[w][4]) : v + red[w][threadIdx.x];
+        __hip_atomic_store(part + (int64_t)blockIdx.x * 5 + threadIdx.x, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        const int prev = __hip_atomic_fetch_add(meta, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = prev == (int)gridDim.x - 1;
+        if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    __syncthreads();
+    if (!last) return;
+    // the last block: a fixed-order reduction of the per-block partials (every rank the same)
+    __shared__ double tr[5][kBlk];
+    double s[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+    for (int k = threadIdx.x; k < (int)gridDim.x; k += kBlk) {
+        const double* q = part + (int64_t)k * 5;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) s[c] += __hip_atomic_load(q + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s[4] = fmax(s[4], __hip_atomic_load(q + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    }
+#pragma unroll
+    for (int c = 0; c < 5; ++c) tr[c][threadIdx.x] = s[c];
+    __syncthreads();
+    for (int w = kBlk / 2; w > 0; w >>= 1) {
+        if (threadIdx.x < w) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) tr[c][threadIdx.x] += tr[c][threadIdx.x + w];
+            tr[4][threadIdx.x] = fmax(tr[4][threadIdx.x], tr[4][threadIdx.x + w]);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
         const double B = (double)bg;
-        const double nu = sqrt(qu), np = sqrt(qp), nn = sqrt(qn);
-        const double loss = tl / B + (double)reg * (nu + np + nn) / B;
+        const double nu = sqrt(tr[1][0]), np = sqrt(tr[2][0]), nn = sqrt(tr[3][0]);
+        const double loss = tr[0][0] / B + (double)reg * (nu + np + nn) / B;
         float* k = reinterpret_cast<float*>(reg_cnt + 3 * N + 1);
         k[0] = nu > 0 ? (float)((double)reg / (B * nu)) : 0.f;
         k[1] = np > 0 ? (float)((double)reg / (B * np)) : 0.f;
@@ -125,41 +249,112 @@ __global__ __launch_bounds__(256) void dp_merge(const int64_t* __restrict__ slot
         if (loss_out) loss_out[0] = (float)loss;
         if (loss_acc) loss_acc[0] += loss;
         if (halt && loss != loss && halt[0] == 0) {
-            halt[1] = stamp;
+            halt[1] = *tag_dev;
             halt[0] = 1;
         }
+        // |G'(x)| <= (3 B occurrences) * (2 max|f| / B) / g_div: the fixed-point scale 2^e keeps
+        // every accumulated row below 2^61 (NaN / inf rows: e = 0, the halt flag stops Adam)
+        const double bound = 6.0 * tr[4][0] / (double)g_div;
+        int e = 0;
+        if (bound > 0.0 && bound < 1e300) e = 61 - (int)ceil(log2(bound));
+        else if (bound == 0.0) e = 61;
+        meta[1] = e < 0 ? 0 : (e > 900 ? 900 : e);
+        meta[0] = 0;  // re-armed for the next launch (stream order)
     }
-    const int li = threadIdx.x % G;
-    const int64_t i = (int64_t)blockIdx.x * GPB + threadIdx.x / G;
-    if (i >= (int64_t)W * 3 * cap) return;
-    int64_t r, j;
-    const int64_t x = occ_row(slots, 3 * cap + 1, cap, n_users, i, &r, &j);
-    if (x < 0) return;
-    if (pos[r * N + x] != (((int64_t)stamp << 32) | j)) return;  // not this rank's representative of x
-    for (int64_t q = 0; q < r; ++q)
-        if ((int32_t)(pos[q * N + x] >> 32) == stamp) return;  // a lower rank holds x: its leader sums
-    float4 acc = f4(0.f);
-    for (int64_t q = r; q < W; ++q) {
-        const int64_t pq = pos[q * N + x];
-        if ((int32_t)(pq >> 32) != stamp) continue;
-        acc = add4(acc, ld4(blocks + q * stride + (pq & 0xffffffffll) * D + li * 4));
-    }
-    st4(g + x * D + li * 4, acc);
 }
 
-// block[own] rows = G'_own at this rank's occurrences
-__global__ __launch_bounds__(256) void dp_gather(const int64_t* __restrict__ trip, int64_t B, int64_t cap,
-                                                 int64_t n_users, int d, const float* __restrict__ g,
-                                                 float* __restrict__ blk) {
-    const int q = d / 4;
-    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (e >= 3 * B * q) return;
-    const int64_t o = e / q;
-    const int c = (int)(e - o * q) * 4;
-    const int64_t k = o / B, t = o - k * B;
-    const int64_t id = trip[k * B + t];
-    const int64_t x = k == 0 ? id : n_users + id;
-    st4(blk + (k * cap + t) * d + c, ld4(g + x * d + c));
+// Phase B: G' in fixed point.  Lane group c walks sorted occurrences [c kChunk, (c+1)
+// kChunk): each occurrence's term (bpr_fused's f32 arithmetic: coef (f_p - f_n) / g_div
+// for a user, +-coef f_u / g_div for an item) scaled by 2^e and rounded to int64, a run of
+// equal rows summed in registers, one 64-bit integer atomic per run and column.
+template <int D>
+__global__ __launch_bounds__(kBlk) void dp_bpr_grad(const int64_t* __restrict__ slots, int64_t cap, int64_t n_users,
+                                                    int64_t N, int64_t n_occ, const int32_t* __restrict__ key,
+                                                    const int32_t* __restrict__ val, const float* __restrict__ fin,
+                                                    const float* __restrict__ coef, float g_div,
+                                                    const int32_t* __restrict__ meta,
+                                                    unsigned long long* __restrict__ acc) {
+    constexpr int G = D / 4, GPB = kBlk / G;
+    const int li = threadIdx.x % G;
+    const int64_t c0 = ((int64_t)blockIdx.x * GPB + threadIdx.x / G) * kChunk;
+    if (c0 >= n_occ) return;
+    const int64_t c1 = c0 + kChunk < n_occ ? c0 + kChunk : n_occ;
+    const double S = ldexp(1.0, meta[1]);
+    const int64_t L = 3 * cap + 1;
+    long long a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+    int32_t cur = -1;
+    for (int64_t i = c0; i < c1; ++i) {
+        const int32_t x = key[i];
+        if (x >= N) break;  // padding sorts last
+        if (x != cur) {
+            if (cur >= 0) {
+                unsigned long long* q = acc + (int64_t)cur * D + li * 4;
+                atomicAdd(q + 0, (unsigned long long)a0);
+                atomicAdd(q + 1, (unsigned long long)a1);
+                atomicAdd(q + 2, (unsigned long long)a2);
+                atomicAdd(q + 3, (unsigned long long)a3);
+            }
+            cur = x;
+            a0 = a1 = a2 = a3 = 0;
+        }
+        const int64_t o = val[i];
+        const int64_t r = o / (3 * cap), j = o - r * 3 * cap, kind = j / cap, t = j - kind * cap;
+        const int64_t* slot = slots + r * L;
+        const float c = coef[r * cap + t];
+        float4 g;
+        if (kind == 0) {
+            const float4 fp = ld4(fin + (n_users + slot[1 + cap + t]) * D + li * 4);
+            const float4 fn = ld4(fin + (n_users + slot[1 + 2 * cap + t]) * D + li * 4);
+            g = make_float4(c * (fp.x - fn.x), c * (fp.y - fn.y), c * (fp.z - fn.z), c * (fp.w - fn.w));
+        } else {
+            const float4 fu = ld4(fin + slot[1 + t] * D + li * 4);
+            const float cc = kind == 1 ? c : -c;
+            g = make_float4(cc * fu.x, cc * fu.y, cc * fu.z, cc * fu.w);
+        }
+        if (g_div != 1.f) {
+            g.x /= g_div;
+            g.y /= g_div;
+            g.z /= g_div;
+            g.w /= g_div;
+        }
+        a0 += llrint((double)g.x * S);
+        a1 += llrint((double)g.y * S);
+        a2 += llrint((double)g.z * S);
+        a3 += llrint((double)g.w * S);
+    }
+    if (cur >= 0) {
+        unsigned long long* q = acc + (int64_t)cur * D + li * 4;
+        atomicAdd(q + 0, (unsigned long long)a0);
+        atomicAdd(q + 1, (unsigned long long)a1);
+        atomicAdd(q + 2, (unsigned long long)a2);
+        atomicAdd(q + 3, (unsigned long long)a3);
+    }
+}
+
+// Phase C: every union row once (the first of its run in the sorted keys): G'[x] = its
+// accumulator / 2^e rounded to f32, the accumulator cleared for the next step.
+template <int D>
+__global__ __launch_bounds__(kBlk) void dp_bpr_round(int64_t N, int64_t n_occ, const int32_t* __restrict__ key,
+                                                     const int32_t* __restrict__ meta,
+                                                     unsigned long long* __restrict__ acc, float* __restrict__ g) {
+    constexpr int G = D / 4, GPB = kBlk / G;
+    const int li = threadIdx.x % G;
+    const int64_t i = (int64_t)blockIdx.x * GPB + threadIdx.x / G;
+    if (i >= n_occ) return;
+    const int32_t x = key[i];
+    if (x >= N || (i > 0 && key[i - 1] == x)) return;
+    const double inv = ldexp(1.0, -meta[1]);
+    unsigned long long* q = acc + (int64_t)x * D + li * 4;
+    float4 v;
+    v.x = (float)((double)(long long)q[0] * inv);
+    v.y = (float)((double)(long long)q[1] * inv);
+    v.z = (float)((double)(long long)q[2] * inv);
+    v.w = (float)((double)(long long)q[3] * inv);
+    q[0] = 0ull;
+    q[1] = 0ull;
+    q[2] = 0ull;
+    q[3] = 0ull;
+    st4(g + (int64_t)x * D + li * 4, v);
 }
 
 rsx_epilogue epi(int kind) {
@@ -176,47 +371,80 @@ rsx_epilogue epi(int kind) {
         if (rc_) return rc_;   \
     } while (0)
 
+template <int D>
+int dp_loss_kernels(const rsx_dp_lgcn_step& st, const Work& w, int32_t W, hipStream_t s) {
+    constexpr int GPB = kBlk / (D / 4);
+    const int64_t nu = st.n_users, N = st.n_users + st.n_items, cap = st.cap;
+    const int64_t n_trip = (int64_t)W * cap, n_occ = (int64_t)W * 3 * cap;
+    const float g_div = (float)(st.n_layers + 1);
+    const int nb_a = (int)((n_trip + GPB - 1) / GPB);
+    hipLaunchKernelGGL((dp_bpr_coef<D>), dim3(nb_a), dim3(kBlk), 0, s, st.slots, W, cap, nu, N, st.final_emb, st.p,
+                       g_div, st.reg, w.coef, w.part, w.meta, st.reg_cnt, st.loss_out, st.loss_acc, st.halt,
+                       st.tag_dev);
+    DP_TRY(last_rc());
+    const int64_t n_chunks = (n_occ + kChunk - 1) / kChunk;
+    hipLaunchKernelGGL((dp_bpr_grad<D>), dim3((unsigned)((n_chunks + GPB - 1) / GPB)), dim3(kBlk), 0, s, st.slots,
+                       cap, nu, N, n_occ, w.kb, w.vb, st.final_emb, w.coef, g_div, w.meta, w.acc);
+    DP_TRY(last_rc());
+    hipLaunchKernelGGL((dp_bpr_round<D>), dim3((unsigned)((n_occ + GPB - 1) / GPB)), dim3(kBlk), 0, s, N, n_occ, w.kb,
+                       w.meta, w.acc, st.g);
+    return last_rc();
+}
+
 int dp_step(const rsx_dp_lgcn_step& st, hipStream_t s) {
     const rsx_csr& A = *st.adj;
     const int d = st.d, K = st.n_layers;
     const int64_t nu = st.n_users, N = st.n_users + st.n_items, cap = st.cap, B = st.batch;
-    const int32_t W = comm_world(st.comm), rank = comm_rank(st.comm);
-    const int64_t L = 3 * cap + 1, stride = 3 * cap * d + kHdr;
+    // over a latency-injected communicator (rsx_comm_init_sim) the one rank times rank 0 of a
+    // W-rank job: slots hold W ranks (the caller fills the other ranks' triplets), so the
+    // index, sort, loss and backward see the job's global batch; the stand-in all-gather is
+    // given its whole W-slot buffer (the sim's byte count is the buffer's) and moves (W-1)/W
+    // of it, as one rank of the job does
+    const int32_t sim_w = comm_sim_world(st.comm);
+    const int32_t W = sim_w > 0 ? sim_w : comm_world(st.comm), rank = comm_rank(st.comm);
+    const int64_t L = 3 * cap + 1, n_occ = (int64_t)W * 3 * cap;
+    const int64_t ag = sim_w > 0 ? W : 1;  // all-gather count multiplier (sim: the whole buffer)
+    Work w = carve(st.work, N, d, cap, W);
+    if (w.total > st.work_bytes) return RSX_ERR_WORKSPACE;
     int rc = 0;
     // (1) this rank's triplets into its slot; every rank's gathered while the forward runs,
-    // then indexed (union tags, counts, pos) on the comm stream
-    hipLaunchKernelGGL(dp_pack, dim3((unsigned)((L + 255) / 256)), dim3(256), 0, s, st.triplets, B, cap,
+    // then indexed (union tags, global counts) and sorted by row, on the comm stream
+    hipLaunchKernelGGL(dp_pack, dim3((unsigned)((L + kBlk - 1) / kBlk)), dim3(kBlk), 0, s, st.triplets, B, cap,
                        st.slots + rank * L, st.inc_step ? const_cast<int64_t*>(st.adam.step_dev) : nullptr);
     DP_TRY(last_rc());
-    if (!collective(st.comm, RSX_COLL_ALLGATHER, st.slots, L, RSX_COLL_I64, s, &rc)) return rc;
+    if (!collective(st.comm, RSX_COLL_ALLGATHER, st.slots, L * ag, RSX_COLL_I64, s, &rc)) return rc;
     hipStream_t cs = comm_stream(st.comm, s);
-    const int64_t n_occ = (int64_t)W * 3 * cap;
-    hipLaunchKernelGGL(dp_index, dim3((unsigned)((n_occ + 255) / 256)), dim3(256), 0, cs, st.slots, W, cap, nu, N,
-                       st.pos, st.row_tag, st.reg_cnt, st.tag_dev);
+    hipLaunchKernelGGL(dp_index, dim3((unsigned)((n_occ + kBlk - 1) / kBlk)), dim3(kBlk), 0, cs, st.slots, W, cap, nu,
+                       N, st.row_tag, st.reg_cnt, st.tag_dev, w.ka, w.va);
     DP_TRY(last_rc());
-    hipEvent_t j_idx = nullptr;
+    hipEvent_t j_idx = nullptr, j_sort = nullptr;
     if (cs != s) {
         j_idx = comm_event(st.comm);
         DP_TRY(hip_rc(hipEventRecord(j_idx, cs)));
     }
-    // (2) forward: E^1..E^{K-1} stored (layer 1 also tags this rank's batch rows in own_tag),
-    // the last layer and the mean on those rows only (lgcn_step_stored_layers' forward)
+    {
+        hipcub::DoubleBuffer<int32_t> k(w.ka, w.kb), v(w.va, w.vb);
+        size_t tb = w.temp_bytes;
+        DP_TRY(hip_rc(hipcub::DeviceRadixSort::SortPairs(w.temp, tb, k, v, (int)n_occ, 0, key_bits(N), cs)));
+        // the sorted run lands in kb / vb or back in ka / va (the pass count is fixed per
+        // key width): the later kernels read whichever the selector names
+        w.kb = k.Current();
+        w.vb = v.Current();
+    }
+    if (cs != s) {
+        j_sort = comm_event(st.comm);
+        DP_TRY(hip_rc(hipEventRecord(j_sort, cs)));
+    }
+    // (2) forward: E^1..E^{K-1} stored, the last layer and the mean on the union rows only
     float* layers[3] = {st.h0, st.h1, st.s};
     const float* x = st.p;
     for (int k = 1; k < K; ++k) {
         rsx_epilogue e = epi(RSX_EPI_STORE);
         e.y = layers[k - 1];
-        TagJob tj;
-        if (k == 1) {
-            tj.trip = st.triplets;
-            tj.batch = B;
-            tj.n_users = nu;
-            tj.row_tag = st.own_tag;
-            tj.tag_dev = st.tag_dev;
-        }
-        DP_TRY(spmm_dispatch_tagging(A, x, d, e, st.slab, s, tj));
+        DP_TRY(spmm_dispatch(A, x, d, e, st.slab, s));
         x = layers[k - 1];
     }
+    if (j_idx) DP_TRY(hip_rc(hipStreamWaitEvent(s, j_idx, 0)));  // the union tags
     {
         rsx_epilogue e = epi(RSX_EPI_FINAL);
         e.beta = 1.f / (float)(K + 1);
@@ -225,44 +453,21 @@ int dp_step(const rsx_dp_lgcn_step& st, hipStream_t s) {
         e.r_add = st.h0;
         e.aux = K >= 3 ? st.h1 : nullptr;
         e.e0 = K == 4 ? st.s : nullptr;
-        e.row_tag = st.own_tag;
+        e.row_tag = st.row_tag;
         e.tag_dev = st.tag_dev;
         e.tag_flags = RSX_TAG_ROWS;
         DP_TRY(spmm_dispatch(A, x, d, e, st.slab, s));
     }
-    // (3) this rank's BPR share over the global batch: G'_own (table), its totals into its block
-    if (j_idx) DP_TRY(hip_rc(hipStreamWaitEvent(s, j_idx, 0)));  // the slots (global batch size)
-    float* own_blk = st.blocks + rank * stride;
-    DP_TRY(bpr_fused_args(st.final_emb, st.p, nu, st.n_items, d, st.triplets, B, st.reg, (float)(K + 1), st.g,
-                          st.reg_cnt, nullptr, nullptr, st.ws, st.ws_bytes, s, nullptr, 0, st.slots, L, W,
-                          reinterpret_cast<double*>(own_blk + 3 * cap * d)));
-    {
-        const int64_t n = 3 * B * (d / 4);
-        hipLaunchKernelGGL(dp_gather, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, st.triplets, B, cap, nu, d,
-                           st.g, own_blk);
-        DP_TRY(last_rc());
+    // (3) the global batch's loss and G' = dL/dfinal / (K+1) on every rank
+    if (j_sort) DP_TRY(hip_rc(hipStreamWaitEvent(s, j_sort, 0)));
+    switch (d) {
+        case 32: DP_TRY(dp_loss_kernels<32>(st, w, W, s)); break;
+        case 64: DP_TRY(dp_loss_kernels<64>(st, w, W, s)); break;
+        case 128: DP_TRY(dp_loss_kernels<128>(st, w, W, s)); break;
+        case 256: DP_TRY(dp_loss_kernels<256>(st, w, W, s)); break;
+        default: return RSX_ERR_UNSUPPORTED;
     }
-    // (4) every rank's block, merged into the same G' on every rank
-    hipEvent_t jb = collective(st.comm, RSX_COLL_ALLGATHER, st.blocks, stride, RSX_COLL_F32, s, &rc);
-    if (!jb) return rc;
-    DP_TRY(hip_rc(hipStreamWaitEvent(s, jb, 0)));
-    {
-        const int G = d / 4, gpb = 256 / G;
-        const dim3 grid((unsigned)((n_occ + gpb - 1) / gpb));
-#define DP_MERGE(DD)                                                                                                \
-    hipLaunchKernelGGL((dp_merge<DD>), grid, dim3(256), 0, s, st.slots, W, cap, nu, N, st.pos, st.blocks, stride, \
-                       st.g, st.tag_dev, st.reg_cnt, st.reg, st.loss_out, st.loss_acc, st.halt)
-        switch (d) {
-            case 32: DP_MERGE(32); break;
-            case 64: DP_MERGE(64); break;
-            case 128: DP_MERGE(128); break;
-            case 256: DP_MERGE(256); break;
-            default: return RSX_ERR_UNSUPPORTED;
-        }
-#undef DP_MERGE
-        DP_TRY(last_rc());
-    }
-    // (5) backward on the union rows: H = G' + A H from H = G', Adam on g = H^K + R with the
+    // (4) backward on the union rows: H = G' + A H from H = G', Adam on g = H^K + R with the
     // global counts and scales, G' and the counts cleared on the union rows
     x = st.g;
     float* bufs[2] = {st.h0, st.h1};
@@ -294,14 +499,13 @@ int dp_step(const rsx_dp_lgcn_step& st, hipStream_t s) {
 
 bool dp_valid(const rsx_dp_lgcn_step* st) {
     if (!st || !st->adj || !st->comm || !st->p || !st->m || !st->v || !st->h0 || !st->h1 || !st->final_emb ||
-        !st->g || !st->triplets || !st->row_tag || !st->own_tag || !st->tag_dev || !st->reg_cnt || !st->slots ||
-        !st->blocks || !st->pos || !st->ws)
+        !st->g || !st->triplets || !st->row_tag || !st->tag_dev || !st->reg_cnt || !st->slots || !st->work)
         return false;
     if (st->n_layers < 2 || st->n_layers > 4 || (st->n_layers == 4 && !st->s)) return false;
     if (st->batch <= 0 || st->batch > st->cap || st->n_users < 0 || st->n_items <= 0) return false;
     if (st->adj->n_rows != st->n_users + st->n_items || st->adj->n_cols != st->adj->n_rows) return false;
     if (st->adj->n_long > 0 && !st->slab) return false;
-    if (3 * st->cap > 0x7fffffffll) return false;  // occurrence index in pos's low word
+    if (st->n_users + st->n_items >= 0x7fffffffll) return false;  // int32 sort keys
     if (st->inc_step && (!st->adam.step_dev || (const void*)st->adam.step_dev != (const void*)st->tag_dev))
         return false;  // the incremented counter is the tag every later launch reads
     return true;
@@ -315,9 +519,15 @@ extern "C" {
 int rsx_dp_lightgcn_step(const rsx_dp_lgcn_step* st, rsx_stream_t stream) {
     if (!rsx::dp_valid(st)) return RSX_ERR_ARG;
     if (st->d != 32 && st->d != 64 && st->d != 128 && st->d != 256) return RSX_ERR_UNSUPPORTED;
+    const int32_t sim_w = rsx::comm_sim_world(st->comm);
+    const int64_t W = sim_w > 0 ? sim_w : rsx::comm_world(st->comm);
+    if (W * 3 * st->cap >= 0x7fffffffll) return RSX_ERR_ARG;  // int32 occurrence ids
     return rsx::dp_step(*st, rsx::as_stream(stream));
 }
 
-size_t rsx_dp_block_floats(int64_t cap, int32_t d) { return (size_t)(3 * cap * d + rsx::kHdr); }
+size_t rsx_dp_work_bytes(int64_t n_rows, int32_t d, int64_t cap, int32_t world) {
+    if (n_rows <= 0 || d <= 0 || cap <= 0 || world < 1) return 0;
+    return rsx::carve(nullptr, n_rows, d, cap, world).total;
+}
 
 }  // extern "C"

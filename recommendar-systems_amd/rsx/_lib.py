@@ -100,9 +100,8 @@ class DpStep(C.Structure):
     _fields_ = [("adj", C.POINTER(Csr)), ("n_users", I64), ("n_items", I64), ("d", I32), ("n_layers", I32),
                 ("reg", F32), ("inc_step", I32), ("p", P), ("m", P), ("v", P), ("s", P), ("h0", P), ("h1", P),
                 ("final_emb", P), ("g", P), ("slab", P), ("triplets", P), ("batch", I64), ("adam", Adam),
-                ("loss_out", P), ("loss_acc", P), ("ws", P), ("ws_bytes", C.c_size_t), ("comm", P),
-                ("row_tag", P), ("own_tag", P), ("tag_dev", P), ("reg_cnt", P), ("halt", P), ("cap", I64),
-                ("slots", P), ("blocks", P), ("pos", P)]
+                ("loss_out", P), ("loss_acc", P), ("comm", P), ("row_tag", P), ("tag_dev", P), ("reg_cnt", P),
+                ("halt", P), ("cap", I64), ("slots", P), ("work", P), ("work_bytes", C.c_size_t)]
 
 
 RSX_COLL_ALLREDUCE, RSX_COLL_ALLGATHER, RSX_COLL_REDUCESCATTER = 0, 1, 2
@@ -138,7 +137,7 @@ def _declare(lib):
         "rsx_comm_allreduce_f32_start": (C.c_int, [P, P, I64, P]),
         "rsx_comm_wait": (C.c_int, [P, P]),
         "rsx_comm_sim_seconds": (C.c_double, [P, I32, C.c_double]),
-        "rsx_dp_block_floats": (C.c_size_t, [I64, I32]),
+        "rsx_dp_work_bytes": (C.c_size_t, [I64, I32, I64, I32]),
         "rsx_layergcn_step": (C.c_int, [C.POINTER(LayerGcnStep), P]),
         "rsx_lightgcn_forward": (C.c_int, [C.POINTER(Csr), I32, I32, P, P, P, P, P, P, P]),
         "rsx_smore_spectral_spec_floats": (C.c_size_t, [I64, I32]),
@@ -218,7 +217,7 @@ EXPORTED = ["rsx_version", "rsx_csr_schedule_host", "rsx_csr_schedule_rebind", "
             "rsx_comm_unique_id_bytes", "rsx_comm_get_unique_id", "rsx_comm_init", "rsx_comm_destroy",
             "rsx_comm_init_host",
             "rsx_comm_allreduce_f32", "rsx_sharded_lightgcn_step", "rsx_sharded_lightgcn_forward", "rsx_sharded_lightgcn_flush",
-            "rsx_dp_lightgcn_step", "rsx_dp_block_floats", "rsx_comm_init_sim", "rsx_comm_sim_seconds",
+            "rsx_dp_lightgcn_step", "rsx_dp_work_bytes", "rsx_comm_init_sim", "rsx_comm_sim_seconds",
             "rsx_comm_allgather_f32", "rsx_comm_allreduce_f32_start", "rsx_comm_wait",
             "rsx_smore_gates", "rsx_smore_pref", "rsx_smore_pref_rows", "rsx_smore_pref_rows_occ_floats", "rsx_tag_rows", "rsx_smore_wgrad_ws_bytes", "rsx_smore_wgrad",
             "rsx_smore_infonce_ws_bytes", "rsx_smore_infonce_fwd", "rsx_smore_infonce_bwd", "rsx_smore_infonce_fwd_total", "rsx_smore_infonce_bwd_scaled", "rsx_adam_multi", "rsx_adam_multi_scaled", "rsx_adam_multi_mg",

@@ -8,18 +8,21 @@ GLOBAL batch of every rank's triplets (rank r draws its own B): the reference
 LightGCN objective at batch W*B (src/models/lightgcn.py:132-156: mean BPR over the
 global batch, reg * (|U|_F + |P|_F + |N|_F) / (W B) with norms over the global batch).
 
-The exchange rides on linearity: the table's gradient is the backward operator applied
-to G' = dL/dfinal / (K+1), which is nonzero on the batch rows only.  So each step
-all-gathers every rank's triplets (while the forward runs) and every rank's G' rows at
-its own occurrences plus its four loss totals (~1.6 MB per rank at sports shape), and
-every rank merges them into the same G' and runs the same backward and Adam
-(csrc/dp.hip).  No parameter or dense-gradient exchange: replicas stay bit-identical.
+Only the triplets are exchanged.  The propagation is replicated (on these graphs its
+cost is per step, not per triplet), so once every rank knows every rank's triplets (one
+all-gather of 48 KB per rank at B = 2048, hidden behind the forward) each rank evaluates
+the whole global batch itself: the last layer on the union of the batch rows, the loss and
+dL/dfinal of every triplet (accumulated per row in 64-bit fixed point: the sum cannot
+depend on the order of the atomics), the backward and Adam (csrc/dp.hip).  Every rank runs
+the same kernels on the same inputs, so the replicas stay bit-identical with no parameter
+or gradient exchange.  (Round 4 all-gathered every rank's dL/dfinal rows instead: 1.6 MB
+per rank on the critical path between the loss and the backward.)
 
-For the graphs the driver's weak-scaling leg uses (Amazon-sports: the whole step is
-~0.14 ms of kernels on 14 MB tables) this beats row sharding, whose per-layer item
-all-reduces of the full item block dominate; row sharding
-(rsx.dist.ShardedLightGCNEngine) stays the choice when the graph is too large to
-propagate on every rank in time (C4's strong-scaling leg).
+The scaling this buys is the global batch's: a step costs about what one GPU's step of
+batch B costs (the union's last layer and the global batch's loss grow with W), and
+processes W B triplets.  Row sharding (rsx.dist.ShardedLightGCNEngine) splits the
+propagation itself, and stays the choice when the graph is too large to propagate on
+every rank in time (C4's strong-scaling leg).
 
 Epochs: the epoch's interactions (one device-sampled stream, the same seed on every
 rank) cut into S * W balanced slices, S = ceil(E / (W B)); step j of rank r trains
@@ -27,7 +30,7 @@ slice j W + r, so the global batch of step j is slices [j W, (j+1) W) and every
 interaction is visited once per epoch.
 
 `backend="torch"` runs a CPU restatement of the same sequence (gloo tests): the
-per-rank totals, the global norms, the block merge, the backward on the merged G'.
+triplet all-gather, then the global batch's loss and gradient on every rank.
 """
 from __future__ import annotations
 
@@ -43,13 +46,21 @@ from . import _lib as L
 from . import ops
 
 
-def _comm_init(group, device, views):
+def _comm_init(group, device, views, sim=None):
     """An rsx communicator over `group`: RCCL ("nccl": unique-id handshake) or, on any
     other backend (gloo: tests, several ranks on one GPU), the host hook that runs each
-    collective on host copies of the registered device buffers `views` ({ptr: flat})."""
+    collective on host copies of the registered device buffers `views` ({ptr: flat});
+    with `sim` (rsx.dist.sim_comm_params, a one-rank group) the latency-injected stand-in."""
     lib = L.lib()
     comm = C.c_void_p()
     world, rank = dist.get_world_size(group), dist.get_rank(group)
+    if sim is not None:
+        if world != 1:
+            raise RuntimeError("RSX_COMM_SIM models a multi-rank job on ONE rank (world 1)")
+        with torch.cuda.device(device):
+            L.check(lib.rsx_comm_init_sim(C.byref(comm), sim["world"], sim["busbw_gbs"], sim["latency_us"],
+                                          sim["blocks"], sim["scratch_mb"]), "rsx_comm_init_sim")
+        return comm, None
     if dist.get_backend(group) == "nccl":
         nb = int(lib.rsx_comm_unique_id_bytes())
         buf = (C.c_uint8 * nb)()
@@ -118,25 +129,30 @@ class DataParallelLightGCNEngine:
         self.m, self.v, self.h0, self.h1, self.final, self.g = z(), z(), z(), z(), z(), z()
         self.s = z() if self.K == 4 else None
         self.row_tag = torch.zeros(n, dtype=torch.int32, device=dev)
-        self.own_tag = torch.zeros(n, dtype=torch.int32, device=dev)
         self.reg_cnt = torch.zeros(3 * n + 4, dtype=torch.int32, device=dev)
         self.halt = torch.zeros(2, dtype=torch.int32, device=dev)
         self.loss_out = torch.zeros(1, dtype=torch.float32, device=dev)
         self.loss_acc = torch.zeros(1, dtype=torch.float64, device=dev)
         self._step_dev = torch.zeros(1, dtype=torch.int64, device=dev)  # Adam's step; its low word = the tag
         lib = L.lib()
-        W, cap = self.world, self.cap
+        # latency injection (RSX_COMM_SIM=W on a one-rank group, csrc/dp.hip): rank 0 of a
+        # modelled W-rank job, its slots and workspace sized for W ranks
+        from .dist import sim_comm_params
+
+        self.sim = sim_comm_params() if self.world == 1 else None
+        W, cap = (self.sim["world"] if self.sim else self.world), self.cap
+        self.model_world = W
         self.slots = torch.zeros(W * (3 * cap + 1), dtype=torch.int64, device=dev)
-        self.stride = int(lib.rsx_dp_block_floats(cap, d))
-        self.blocks = torch.zeros(W * self.stride, dtype=torch.float32, device=dev)
-        self.pos = torch.zeros(W * n, dtype=torch.int64, device=dev)
-        self.ws = torch.empty(lib.rsx_bpr_ws_bytes(cap), dtype=torch.uint8, device=dev)
+        # the step's workspace: fixed-point G' accumulators, the occurrence sort, loss partials
+        self.work = torch.zeros(int(lib.rsx_dp_work_bytes(n, d, cap, W)), dtype=torch.uint8, device=dev)
         self.sampler = ops.DeviceSampler(tu, ti, nu, dev, seed=seed)
         self.n_inter = self.sampler.n_inter
         self._epoch_buf = None
         self._epoch_key = None
-        self._views = {self.slots.data_ptr(): self.slots, self.blocks.data_ptr(): self.blocks}
-        self._comm, self._host_cb = _comm_init(group, dev, self._views)
+        self._views = {self.slots.data_ptr(): self.slots}
+        self._comm, self._host_cb = _comm_init(group, dev, self._views, self.sim)
+        if self.sim:
+            self._fill_peer_slots()
         st = self._st = L.DpStep()
         st.adj = C.pointer(self.adj.struct)
         st.n_users, st.n_items, st.d, st.n_layers, st.reg = nu, ni, d, self.K, self.reg
@@ -147,14 +163,14 @@ class DataParallelLightGCNEngine:
         slab = self.adj.slab(d)
         st.slab = slab.data_ptr() if slab is not None else None
         st.loss_out, st.loss_acc = self.loss_out.data_ptr(), self.loss_acc.data_ptr()
-        st.ws, st.ws_bytes = self.ws.data_ptr(), self.ws.numel()
         st.comm = self._comm.value
-        st.row_tag, st.own_tag = self.row_tag.data_ptr(), self.own_tag.data_ptr()
+        st.row_tag = self.row_tag.data_ptr()
         st.tag_dev = self._step_dev.data_ptr()
         st.inc_step = 1  # dp_pack increments the counter (no separate add launch a step)
         st.reg_cnt, st.halt = self.reg_cnt.data_ptr(), self.halt.data_ptr()
         st.cap = cap
-        st.slots, st.blocks, st.pos = self.slots.data_ptr(), self.blocks.data_ptr(), self.pos.data_ptr()
+        st.slots = self.slots.data_ptr()
+        st.work, st.work_bytes = self.work.data_ptr(), self.work.numel()
         self.use_graph = dist.get_backend(group) == "nccl" and os.environ.get("RSX_DP_GRAPH", "1") != "0"
         self._graphs = {}
         self._warm = set()
@@ -168,6 +184,22 @@ class DataParallelLightGCNEngine:
         h = t.cpu()
         dist.broadcast(h, src=0, group=self.group)
         return h.to(t.device)
+
+    def _fill_peer_slots(self):
+        """Latency injection: the modelled job's other ranks' slots, once — ranks 1..W-1
+        train slices 1..W-1 of epoch 0 cut into batch-sized balanced slices (a batch each,
+        as in the job), so the step indexes, merges and back-propagates a global batch of
+        the job's size and union (a timing mode: those ranks' own steps are not run)."""
+        W, cap, L_ = self.model_world, self.cap, 3 * self.cap + 1
+        n = max(W, -(-self.n_inter // cap))
+        buf = self.sampler.sample_epoch_slices(0, n)
+        for r in range(1, W):
+            t = ops.DeviceSampler.slice_view(buf, self.n_inter, n, r)
+            b = int(t.shape[1])
+            slot = self.slots[r * L_:(r + 1) * L_]
+            slot[0] = b
+            slot[1:].view(3, cap)[:, :b].copy_(t[:3])
+        torch.cuda.synchronize(self.device)
 
     def steps_per_epoch(self) -> int:
         return -(-self.n_inter // (self.world * self.batch))
@@ -287,9 +319,9 @@ class DataParallelLightGCNEngine:
         return acc / (self.K + 1)
 
     def _torch_step(self, trip):
-        W, r, nu, K = self.world, self.rank, self.n_users, self.K
+        W, nu, K = self.world, self.n_users, self.K
         trip = trip[:3].long()
-        # (1) every rank's triplets
+        # (1) every rank's triplets: the step's only exchange
         counts = [torch.zeros(1, dtype=torch.int64) for _ in range(W)]
         dist.all_gather(counts, torch.tensor([trip.shape[1]]), group=self.group)
         cap = int(max(c.item() for c in counts))
@@ -297,47 +329,25 @@ class DataParallelLightGCNEngine:
         pad[:, : trip.shape[1]] = trip
         trips = [torch.zeros_like(pad) for _ in range(W)]
         dist.all_gather(trips, pad, group=self.group)
-        trips = [t[:, : int(c.item())] for t, c in zip(trips, counts)]
-        Bg = float(sum(int(c.item()) for c in counts))
-        # (2) forward; (3) this rank's share: G'_r on its rows and its four totals
+        glob = torch.cat([t[:, : int(c.item())] for t, c in zip(trips, counts)], 1)
+        Bg = float(glob.shape[1])
+        # (2) forward; (3) the GLOBAL batch's loss and G' = dL/dfinal / (K+1), on every rank
         final = self._torch_forward()
         f = final.clone().requires_grad_(True)
-        u, pi, ni_ = trip[0], trip[1] + nu, trip[2] + nu
+        u, pi, ni_ = glob[0], glob[1] + nu, glob[2] + nu
         sg = torch.sigmoid((f[u] * f[pi]).sum(1) - (f[u] * f[ni_]).sum(1))
         (-torch.log(1e-10 + sg)).sum().div(Bg).backward()
-        gr = f.grad / (K + 1)
+        G = f.grad / (K + 1)
         e = self.p
-        tot = torch.tensor([float((-torch.log(1e-10 + sg.detach())).double().sum()),
-                            float((e[u].double() ** 2).sum()), float((e[pi].double() ** 2).sum()),
-                            float((e[ni_].double() ** 2).sum())], dtype=torch.float64)
-        occ = torch.cat([u, pi, ni_])
-        blk = gr[occ]
-        # (4) every rank's block and totals; the merge: per row, ranks in order
-        tots = [torch.zeros_like(tot) for _ in range(W)]
-        dist.all_gather(tots, tot, group=self.group)
-        occs = [torch.cat([t[0], t[1] + nu, t[2] + nu]) for t in trips]
-        blks = [None] * W
-        dist.all_gather_object(blks, blk, group=self.group)
-        G = torch.zeros_like(self.p)
-        seen = {}
-        for q in range(W):
-            rep = {}
-            for j, x in enumerate(occs[q].tolist()):
-                rep.setdefault(x, j)  # one representative occurrence per (rank, row)
-            for x, j in rep.items():
-                seen[x] = seen[x] + blks[q][j] if x in seen else torch.zeros(self.d) + blks[q][j]
-        for x, row in seen.items():
-            G[x] = row
-        T = torch.stack(tots).sum(0)
-        nrm = T[1:].sqrt()
-        loss = T[0] / Bg + self.reg * nrm.sum() / Bg
+        tl = float((-torch.log(1e-10 + sg.detach())).double().sum())
+        nrm = torch.tensor([float((e[x].double() ** 2).sum()) for x in (u, pi, ni_)], dtype=torch.float64).sqrt()
+        loss = tl / Bg + self.reg * float(nrm.sum()) / Bg
         self.loss_out[0] = float(loss)
         self.loss_acc_host += float(loss)
         k = [float(self.reg / (Bg * x)) if x > 0 else 0.0 for x in nrm.tolist()]
         cnt = torch.zeros(self.p.shape[0], 3)
-        for t in trips:
-            for kind, ids in enumerate((t[0], t[1] + nu, t[2] + nu)):
-                cnt[:, kind].index_add_(0, ids, torch.ones(ids.numel()))
+        for kind, ids in enumerate((u, pi, ni_)):
+            cnt[:, kind].index_add_(0, ids, torch.ones(ids.numel()))
         R = (cnt[:, 0:1] * k[0] + cnt[:, 1:2] * k[1] + cnt[:, 2:3] * k[2]) * self.p
         # (5) backward: H = G' + A H from H = G', g = H^K + R; Adam
         H = G

@@ -198,6 +198,8 @@ def _collect(t):
     import torch
     import torch.distributed as dist
 
+    if not (dist.is_available() and dist.is_initialized()):  # one rank (rsx_sharded without a group)
+        return [t.cpu()]
     x = t if dist.get_backend() == "nccl" else t.cpu()
     parts = [torch.empty_like(x) for _ in range(dist.get_world_size())]
     dist.all_gather(parts, x)

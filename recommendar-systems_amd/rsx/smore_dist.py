@@ -76,6 +76,23 @@ class Comm:
 
     def __init__(self, group=None, device=None):
         self.group = group
+        self.sim = None
+        from .dist import sim_comm_params
+
+        sim = sim_comm_params()
+        one = not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1
+        if sim is not None and one:
+            # latency injection (RSX_COMM_SIM=W): this one process is rank 0 of a modelled
+            # W-rank job — SmoreShard partitions users and item rows W ways, and every
+            # collective is the one-rank identity plus a comm-stream stand-in holding the
+            # modelled time, CUs and HBM bytes of that collective (csrc/dist.hip)
+            self.world, self.rank, self.native, self.sim = int(sim["world"]), 0, True, sim
+            h = C.c_void_p()
+            with torch.cuda.device(device):
+                L.check(L.lib().rsx_comm_init_sim(C.byref(h), sim["world"], sim["busbw_gbs"], sim["latency_us"],
+                                                  sim["blocks"], sim["scratch_mb"]), "rsx_comm_init_sim")
+            self.handle = h
+            return
         if not (dist.is_available() and dist.is_initialized()):  # rsx_sharded without a group: one rank
             self.world, self.rank, self.native, self.handle = 1, 0, False, None
             return
@@ -135,7 +152,9 @@ class Comm:
         if t.dtype != torch.float32 or not t.is_contiguous() or t.numel() < self.world * count:
             raise RuntimeError("Comm.allgather_: a contiguous float32 tensor of world * count elements")
         if self.handle is not None:
-            L.check(L.lib().rsx_comm_allgather_f32(self.handle, t.data_ptr(), int(count), ops._stream()),
+            # (the stand-in is given the whole world * count buffer: its byte count is the buffer's)
+            n = int(count) * (self.world if self.sim else 1)
+            L.check(L.lib().rsx_comm_allgather_f32(self.handle, t.data_ptr(), n, ops._stream()),
                     "rsx_comm_allgather_f32")
             return t
         flat = t.view(-1)
