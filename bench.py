@@ -1041,7 +1041,12 @@ def main():
                          # the dense f32 score matrix's flops / kernel time: the screened kernel
                          # (csrc/fullsort.hip fs_screen) runs two bf16 MFMA passes over all pairs and
                          # exact f32 dots for the candidates only, so this is an f32-equivalent rate
-                         "kernel_tflops_f32_equivalent": fs_flops / (fs_ms * 1e-3) / 1e12,
+                         "algorithmic_tflops_f32_equivalent": fs_flops / (fs_ms * 1e-3) / 1e12,
+                         "algorithmic_tflops_note": ("2*d*n_items*users (the dense f32 score GEMM's flops) / "
+                                                     "kernel time: an ALGORITHMIC rate of the screened "
+                                                     "selection (most pairs never get an f32 dot), not "
+                                                     "hardware utilisation; it may exceed the 157.3 TF/s f32 "
+                                                     "MFMA peak. Utilisation: mfma_util"),
                          "screen_bf16_mfma_tflops": 2 * 2.0 * (d + 16) * ni * vu_d.numel() / (fs_ms * 1e-3) / 1e12,
                          # north_star's "MFMA utilisation for the full-sort GEMM": the MFMA work the
                          # screened kernel issues (two bf16 passes over every pair) per second over the

@@ -462,6 +462,29 @@ int rsx_smore_spectral_fwd(const float* V, int32_t dv, const float* Wv, const fl
                            void* ws, size_t ws_bytes, rsx_stream_t stream);
 
 /*
+ * The whole SMORE item side of smore.py:256-272 (image_trs / text_trs,
+ * spectrum_convolution and, with `item` set, the modality gates
+ *   img_i = item + scale * sigmoid(gate_v(conv_v))   (mul: item * sigmoid(..)),
+ * likewise txt_i / fus_i with gate_t / gate_f) as ONE launch: every block projects
+ * its share and the last block to finish an item tile runs the spectral part and
+ * the gates of that tile.  Same arguments and outputs as rsx_smore_spectral_fwd
+ * (bit-identical values), plus `tile_cnt` [rsx_smore_item_tiles(n)] uint32
+ * arrival counters (zero before the first call; the kernel re-arms them, so one
+ * buffer serves every later call on the same stream) and the gate arguments:
+ * gate_W[3] [d, d] nn.Linear weights, gate_b[3] [d], gate_out[3] [n_items, d]
+ * (all ignored when item == NULL).  Gate outputs equal rsx_smore_gates(0, ...)'s.
+ */
+size_t rsx_smore_item_tiles(int64_t n_items);
+int rsx_smore_item_fwd(const float* V, int32_t dv, const float* Wv, const float* bv,
+                       const float* T, int32_t dt, const float* Wt, const float* bt,
+                       const float* wv, const float* wt, const float* wf,
+                       int64_t n_items, int32_t d, float* img, float* txt,
+                       float* conv_v, float* conv_t, float* conv_f, float* spec,
+                       void* ws, size_t ws_bytes, uint32_t* tile_cnt,
+                       const float* item, const float* const* gate_W, const float* const* gate_b,
+                       float scale, int32_t mul, float* const* gate_out, rsx_stream_t stream);
+
+/*
  * Backward of the spectral part: given the forward's `spec` and d conv_v /
  * d conv_t / d conv_f (each may be NULL = zero), writes d img, d txt
  * [n_items, d] and per-block partial sums of d wv / d wt / d wf into
@@ -469,12 +492,15 @@ int rsx_smore_spectral_fwd(const float* V, int32_t dv, const float* Wv, const fl
  * [ceil(n/64)][3][d/2+1][2] (sum over the first axis for the weight gradients).
  * The projection gradients d Wv = d img^T V, d V = d img Wv, d bv = colsum(d img)
  * (and the text twins) are left to the caller: rsx_linear_bwd, one pass each.
+ * `ws` [rsx_smore_spectral_bwd_ws_bytes(n, d)] carries d Fi / d Ft between the two
+ * passes (frequency side, then feature side).
  */
 size_t rsx_smore_spectral_bwd_partials(int64_t n_items, int32_t d);
+size_t rsx_smore_spectral_bwd_ws_bytes(int64_t n_items, int32_t d);
 int rsx_smore_spectral_bwd(const float* spec, const float* wv, const float* wt, const float* wf,
                            const float* g_v, const float* g_t, const float* g_f,
                            int64_t n_items, int32_t d, float* g_img, float* g_txt,
-                           float* g_w_partial, rsx_stream_t stream);
+                           float* g_w_partial, void* ws, size_t ws_bytes, rsx_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
 /* Evaluation tail: top-K ranking metrics                                     */

@@ -17,7 +17,7 @@
 //    feed the three irfft products directly as B operands (the k index of an MFMA
 //    may be permuted freely as long as A uses the same permutation): no LDS
 //    transposes.  One wave = 16 items, no block-level synchronisation.
-// 3. smore_spec_bwd: dY = irfft^T(d conv) (the same matrices transposed), the
+// 3. smore_spec_bwd_freq / _feat: dY = irfft^T(d conv) (the same matrices transposed), the
 //    complex product rules against the spectra the forward saved, d w per block
 //    (lane-group reductions, waves added in order: deterministic), d img / d txt
 //    = rfft^T(dF).  The projection gradients
@@ -26,6 +26,7 @@
 #include <type_traits>
 
 #include "rsx_common.hpp"
+#include "smore_fld.hpp"
 
 namespace rsx {
 
@@ -56,17 +57,22 @@ struct SpecProjArgs {
     float* out[2][8];   // split s of modality m: [n, d] (s = 0: img / txt themselves)
 };
 
+// LDS floats of one projection block: X and W chunks, double-buffered
 template <int D>
-__global__ __launch_bounds__(256) void smore_proj(SpecProjArgs a) {
+constexpr int kPjLds = 2 * kPjItems * kPjPad + 2 * D * kPjPad;
+
+// Block `bid`'s share of the projection (all 256 threads); returns its item tile.
+// lds: kPjLds<D> floats.
+template <int D>
+__device__ __forceinline__ int proj_block(const SpecProjArgs& a, int bid, float* __restrict__ lds) {
     constexpr int FT = D / 32;            // feature tiles
     constexpr int TPW = 2 * FT / 4;       // tiles per wave (FT/2: 1 for d=64, 2 for d=128)
     constexpr int NX = kPjItems * kPjK / 4, NW = D * kPjK / 4;  // float4s per chunk
     constexpr int PER = (NX + NW) / 256;
     static_assert((NX + NW) % 256 == 0, "chunk split");
-    __shared__ float xs[2][kPjItems * kPjPad];
-    __shared__ float ws[2][D * kPjPad];
+    float (*xs)[kPjItems * kPjPad] = reinterpret_cast<float (*)[kPjItems * kPjPad]>(lds);
+    float (*ws)[D * kPjPad] = reinterpret_cast<float (*)[D * kPjPad]>(lds + 2 * kPjItems * kPjPad);
     // blocks: modality 0 splits, then modality 1 splits, each over the item tiles
-    int bid = blockIdx.x;
     const int nb0 = a.tiles * a.S[0];
     const int m = bid < nb0 ? 0 : 1;
     if (m) bid -= nb0;
@@ -165,6 +171,13 @@ __global__ __launch_bounds__(256) void smore_proj(SpecProjArgs a) {
             if (row < a.n) out[row * D + f] = acc[q][e];
         }
     }
+    return tile;
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void smore_proj(SpecProjArgs a) {
+    __shared__ __attribute__((aligned(16))) float lds[kPjLds<D>];
+    proj_block<D>(a, blockIdx.x, lds);
 }
 
 // ---------------------------------------------------------------------------
@@ -179,29 +192,27 @@ struct Spec {
     static constexpr int OT = D / 16;             // 16-row tiles of the d features
 };
 
-// Keeps the twiddle loads of one MFMA step from being hoisted into earlier steps (or
-// merged with the same loads of another phase): a fully unrolled loop otherwise
-// loads all of them up front, hundreds of live registers and spills.  The LDS
-// tables never escape, so a memory clobber does not order their loads; an opaque
-// index does.  One step is 2-3 x MT MFMAs, ample to cover an LDS read.
-__device__ __forceinline__ void step_fence() { asm volatile("" ::: "memory"); }
 __device__ __forceinline__ int opaque(int x) {
     asm volatile("" : "+v"(x));
     return x;
 }
-// Volatile asm statements keep their order, but the MFMAs around them do not: they
-// can sink below every later step's index asm, which again hoists all loads.  A
-// volatile asm that "rewrites" the coefficients of the previous step must follow
-// the MFMAs that read them, so the next step's loads cannot pass those MFMAs (and
-// still overlap their execution).
+// The coefficient reads of one MFMA step group must not be hoisted into earlier groups
+// (a fully unrolled loop otherwise loads every group up front: hundreds of live
+// registers, spills).  tie() "rewrites" the previous group's coefficients after the
+// MFMAs that read them, and the next group's table offset passes through opaque()
+// after it: volatile asm keeps that order, so the next reads cannot pass those MFMAs
+// (and still overlap their execution).
 template <int N>
-__device__ __forceinline__ void tie(float (&c)[N]) {
+__device__ __forceinline__ void tie(float4 (&c)[N]) {
 #pragma unroll
-    for (int i = 0; i < N; ++i) asm volatile("" : "+v"(c[i]));
+    for (int i = 0; i < N; ++i) asm volatile("" : "+v"(c[i].x), "+v"(c[i].y), "+v"(c[i].z), "+v"(c[i].w));
 }
 
 __device__ __forceinline__ floatx4 mfma16(float a, float b, floatx4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ float f4c(const float4& v, int i) {  // i: a compile-time constant after unrolling
+    return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w;
 }
 
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
@@ -226,8 +237,7 @@ __device__ __forceinline__ void twiddles(float* tw) {
 // rfft matrix: row j (Re of bin j/2 for even j, Im for odd j), feature f
 template <int D>
 __device__ __forceinline__ float fwd_coef(int j, int f, const float* tw) {
-    const int e = opaque((((j >> 1) * f) & (D - 1)) + (j & 1) * D);
-    const float v = tw[e];
+    const float v = tw[(((j >> 1) * f) & (D - 1)) + (j & 1) * D];
     return j < Spec<D>::MR ? v : 0.f;
 }
 
@@ -236,10 +246,72 @@ __device__ __forceinline__ float fwd_coef(int j, int f, const float* tw) {
 template <int D>
 __device__ __forceinline__ float inv_coef(int t, int j, const float* tw) {
     const int b = j >> 1;
-    const int e = opaque(((b * t) & (D - 1)) + (j & 1) * D);
-    const float v = tw[e];
+    const float v = tw[((b * t) & (D - 1)) + (j & 1) * D];
     const float c = (b == 0 || b == D / 2) ? 1.f : 2.f;
     return j < Spec<D>::MR ? c * v : 0.f;
+}
+
+// ---------------------------------------------------------------------------
+// coefficient tables: the DFT matrices as MFMA A operands in LDS, in the order the
+// MFMA steps read them (one conflict-free ds_read_b128 per lane = four steps' operands,
+// at a constant offset: no index arithmetic, no twiddle-table bank conflicts).  The
+// spectrum's last 16-row tile holds 2 real rows (Re / Im of bin D/2: MR = D + 2 =
+// 16 (MT - 1) + 2), so its operands are stored compactly and the other lanes read 0.
+// ---------------------------------------------------------------------------
+template <int D>
+struct Tab {
+    static constexpr int MT = Spec<D>::MT, Q = D / 16;       // Q: step groups (SI / 4) = feature tiles (OT)
+    static constexpr int kMain = (MT - 1) * Q * 64;          // float4s of the full tiles
+    static constexpr int kFloats = 4 * (kMain + 8 * Q);      // + the compact last tile
+};
+
+// k-step layout (rfft over the features / the irfft's transpose): entry (t, q), lane
+// (n, g), component r = coef(spectrum row j = 16 t + n, feature f = g SI + 4 q + r)
+template <int D, class F>
+__device__ __forceinline__ void tab_ks(float4* __restrict__ tab, F coef) {
+    using T = Tab<D>;
+    constexpr int SI = Spec<D>::SI;
+    for (int e = threadIdx.x; e < T::kMain; e += blockDim.x) {
+        const int lane = e & 63, tq = e >> 6, t = tq / T::Q, q = tq % T::Q;
+        const int j = 16 * t + (lane & 15), f0 = (lane >> 4) * SI + 4 * q;
+        tab[e] = make_float4(coef(j, f0), coef(j, f0 + 1), coef(j, f0 + 2), coef(j, f0 + 3));
+    }
+    for (int e = threadIdx.x; e < 8 * T::Q; e += blockDim.x) {
+        const int n = e & 1, g = (e >> 1) & 3, q = e >> 3;
+        const int j = 16 * (T::MT - 1) + n, f0 = g * SI + 4 * q;
+        tab[T::kMain + e] = make_float4(coef(j, f0), coef(j, f0 + 1), coef(j, f0 + 2), coef(j, f0 + 3));
+    }
+}
+template <int D>
+__device__ __forceinline__ float4 ks_at(const float4* __restrict__ tab, int base, int t, int q, int lane) {
+    using T = Tab<D>;
+    if (t < T::MT - 1) return tab[base + (t * T::Q + q) * 64];
+    const float4 v = tab[T::kMain + (q * 4 + (lane >> 4)) * 2 + (lane & 1)];
+    return (lane & 15) < 2 ? v : f4(0.f);
+}
+
+// output-tile layout (rfft^T onto the features / the irfft): entry (tau, t), lane
+// (n, g), component i = coef(spectrum row j = 16 t + 4 g + i, output o = 16 tau + n)
+template <int D, class F>
+__device__ __forceinline__ void tab_ot(float4* __restrict__ tab, F coef) {
+    using T = Tab<D>;
+    for (int e = threadIdx.x; e < T::kMain; e += blockDim.x) {
+        const int lane = e & 63, tt = e >> 6, tau = tt / (T::MT - 1), t = tt % (T::MT - 1);
+        const int j0 = 16 * t + 4 * (lane >> 4), o = 16 * tau + (lane & 15);
+        tab[e] = make_float4(coef(j0, o), coef(j0 + 1, o), coef(j0 + 2, o), coef(j0 + 3, o));
+    }
+    float2* last = reinterpret_cast<float2*>(tab + T::kMain);
+    for (int e = threadIdx.x; e < 16 * T::Q; e += blockDim.x) {
+        const int j0 = 16 * (T::MT - 1), o = 16 * (e >> 4) + (e & 15);
+        last[e] = make_float2(coef(j0, o), coef(j0 + 1, o));
+    }
+}
+template <int D>
+__device__ __forceinline__ float4 ot_at(const float4* __restrict__ tab, int base, int tau, int t, int lane) {
+    using T = Tab<D>;
+    if (t < T::MT - 1) return tab[base + (tau * (T::MT - 1) + t) * 64];
+    const float2 v = reinterpret_cast<const float2*>(tab + T::kMain)[tau * 16 + (lane & 15)];
+    return (lane >> 4) == 0 ? make_float4(v.x, v.y, 0.f, 0.f) : f4(0.f);
 }
 
 // B operand of 16 item rows: lane (g = l>>4, n = l&15) holds x[item][g*SI + s] for
@@ -259,29 +331,33 @@ __device__ __forceinline__ void load_rows(const float* __restrict__ x, int64_t i
     }
 }
 
-// F[t] (t < MT): the spectrum of the 16 items; lane (g, n) holds rows 16t + 4g + i,
-// i.e. the (Re, Im) of bins 8t + 2g and 8t + 2g + 1 of item n
-template <int D>
-__device__ __forceinline__ void rfft16(const float (&xi)[Spec<D>::SI], const float (&xt)[Spec<D>::SI], int g, int n16,
-                                       const float* tw, floatx4 (&fi)[Spec<D>::MT],
-                                       floatx4 (&ft)[Spec<D>::MT]) {
-    constexpr int SI = Spec<D>::SI, MT = Spec<D>::MT;
+// acc[t] += sum_s A_t(s) x[s] over the SI steps (k-step table): the rfft of 16 items
+// (fwd table; two signals) or irfft^T of a gradient (inv table; one signal).  F[t]
+// (t < MT): lane (g, n) holds rows 16t + 4g + i, i.e. the (Re, Im) of bins 8t + 2g and
+// 8t + 2g + 1 of item n
+template <int D, int NS>
+__device__ __forceinline__ void ks_product(const float4* __restrict__ tab, const float (*x[NS])[Spec<D>::SI],
+                                           floatx4 (*acc[NS])[Spec<D>::MT], int lane) {
+    constexpr int MT = Spec<D>::MT, Q = Tab<D>::Q;
 #pragma unroll
-    for (int t = 0; t < MT; ++t) fi[t] = ft[t] = floatx4{0.f, 0.f, 0.f, 0.f};
-    float c[MT];
+    for (int k = 0; k < NS; ++k)
 #pragma unroll
-    for (int t = 0; t < MT; ++t) c[t] = 0.f;
+        for (int t = 0; t < MT; ++t) (*acc[k])[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+    float4 c[MT];
 #pragma unroll
-    for (int s = 0; s < SI; ++s) {
-        const int f = g * SI + s;
+    for (int t = 0; t < MT; ++t) c[t] = f4(0.f);
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
         tie(c);
+        const int base = opaque(lane);
 #pragma unroll
-        for (int t = 0; t < MT; ++t) c[t] = fwd_coef<D>(16 * t + n16, f, tw);
+        for (int t = 0; t < MT; ++t) c[t] = ks_at<D>(tab, base, t, q, lane);
 #pragma unroll
-        for (int t = 0; t < MT; ++t) {
-            fi[t] = mfma16(c[t], xi[s], fi[t]);
-            ft[t] = mfma16(c[t], xt[s], ft[t]);
-        }
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int t = 0; t < MT; ++t)
+#pragma unroll
+                for (int k = 0; k < NS; ++k) (*acc[k])[t] = mfma16(f4c(c[t], r), (*x[k])[4 * q + r], (*acc[k])[t]);
     }
 }
 
@@ -337,26 +413,47 @@ __device__ __forceinline__ void proj_rows(const SpecFwdArgs& a, int m, int64_t i
     }
 }
 
+// LDS of the spectral part (floats): one coefficient table, the twiddles (2 D), the
+// three unit complex weight vectors (3 NB float2s)
 template <int D>
-__global__ __launch_bounds__(256) void smore_spec_fwd(SpecFwdArgs a) {
+constexpr int kSpecLds = Tab<D>::kFloats + 2 * D + 6 * Spec<D>::NB;
+
+template <int D>
+__device__ __forceinline__ void spec_setup(const SpecFwdArgs& a, float* __restrict__ lds) {
+    constexpr int NB = Spec<D>::NB;
+    float* tw = lds + Tab<D>::kFloats;
+    twiddles<D>(tw);
+    float2* ws = reinterpret_cast<float2*>(tw + 2 * D);
+    for (int e = threadIdx.x; e < 3 * NB; e += blockDim.x)
+        ws[e] = make_float2(a.w[e / NB][2 * (e % NB)], a.w[e / NB][2 * (e % NB) + 1]);
+    __syncthreads();
+    tab_ks<D>(reinterpret_cast<float4*>(lds), [&](int j, int f) { return fwd_coef<D>(j, f, tw); });
+    __syncthreads();
+}
+
+// The spectral part of one 64-item tile (4 waves x 16 items; all 256 threads, block-
+// uniform: it rebuilds the LDS table between the rfft and the irfft; spec_setup before)
+template <int D>
+__device__ __forceinline__ void spec_tile(const SpecFwdArgs& a, int64_t tile, float* __restrict__ lds) {
     using S = Spec<D>;
     constexpr int SI = S::SI, MT = S::MT, NB = S::NB, OT = S::OT;
-    __shared__ float tw[2 * D];
-    __shared__ float2 ws[3][NB];
-    twiddles<D>(tw);
-    for (int e = threadIdx.x; e < 3 * NB; e += blockDim.x)
-        ws[e / NB][e % NB] = make_float2(a.w[e / NB][2 * (e % NB)], a.w[e / NB][2 * (e % NB) + 1]);
-    __syncthreads();
+    const float4* tab = reinterpret_cast<const float4*>(lds);
+    const float* tw = lds + Tab<D>::kFloats;
+    const float2(*ws)[NB] = reinterpret_cast<const float2(*)[NB]>(tw + 2 * D);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, n16 = lane & 15, g = lane >> 4;
-    const int64_t item = ((int64_t)blockIdx.x * 4 + wave) * 16 + n16;
+    const int64_t item = (tile * 4 + wave) * 16 + n16;
     const bool iv = item < a.n;  // a wave past the end runs on zeros (MFMAs need the whole wave)
     floatx4 fi[MT], ft[MT], yf[MT];
     {
         float xi[SI], xt[SI];
         proj_rows<D>(a, 0, item, iv, g, xi);
         proj_rows<D>(a, 1, item, iv, g, xt);
-        rfft16<D>(xi, xt, g, n16, tw, fi, ft);
+        const float (*xs[2])[SI] = {&xi, &xt};
+        floatx4 (*accs[2])[MT] = {&fi, &ft};
+        ks_product<D, 2>(tab, xs, accs, lane);
     }
+    __syncthreads();  // every wave is done with the rfft table
+    tab_ot<D>(reinterpret_cast<float4*>(lds), [&](int j, int o) { return inv_coef<D>(o, j, tw); });
     if (iv) {
 #pragma unroll
         for (int t = 0; t < MT; ++t) {
@@ -378,22 +475,21 @@ __global__ __launch_bounds__(256) void smore_spec_fwd(SpecFwdArgs a) {
             set_pair(ft[t], p, bv ? cmul(Ft, ws[1][bb]) : z);
             set_pair(yf[t], p, bv ? cmul(cmul(Ft, Fi), ws[2][bb]) : z);
         }
+    __syncthreads();  // the irfft table is complete
     // conv_m = irfft(Y_m): output tile tau, step (t, i) <-> spectrum row 16t + 4g + i
 #pragma unroll
     for (int tau = 0; tau < OT; ++tau) {
         floatx4 cv{0.f, 0.f, 0.f, 0.f}, ct = cv, cf = cv;
-        const int tq = 16 * tau + n16;
-        float c[4] = {0.f, 0.f, 0.f, 0.f};
+        float4 c[1] = {f4(0.f)};
 #pragma unroll
         for (int t = 0; t < MT; ++t) {
             tie(c);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) c[i] = inv_coef<D>(tq, 16 * t + 4 * g + i, tw);
+            c[0] = ot_at<D>(tab, opaque(lane), tau, t, lane);
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                cv = mfma16(c[i], fi[t][i], cv);
-                ct = mfma16(c[i], ft[t][i], ct);
-                cf = mfma16(c[i], yf[t][i], cf);
+                cv = mfma16(f4c(c[0], i), fi[t][i], cv);
+                ct = mfma16(f4c(c[0], i), ft[t][i], ct);
+                cf = mfma16(f4c(c[0], i), yf[t][i], cf);
             }
         }
         if (iv) {  // lane (g, n) holds features 16 tau + 4g + r of item n
@@ -405,6 +501,13 @@ __global__ __launch_bounds__(256) void smore_spec_fwd(SpecFwdArgs a) {
     }
 }
 
+template <int D>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void smore_spec_fwd(SpecFwdArgs a) {
+    __shared__ __attribute__((aligned(16))) float lds[kSpecLds<D>];
+    spec_setup<D>(a, lds);
+    spec_tile<D>(a, blockIdx.x, lds);
+}
+
 struct SpecBwdArgs {
     const float* spec;  // the forward's saved spectra [n][2][16 MT]
     const float* w[3];
@@ -412,6 +515,7 @@ struct SpecBwdArgs {
     int64_t n;
     float* gx[2];       // d img, d txt [n, d]
     float* gw;          // [gridDim.x][3][d/2+1][2] per-block partials
+    float* dfreq;       // [waves][2][MT][64][4]: dFi, dFt between the two passes
 };
 
 // the sum over the 16 items (lanes n = 0..15 of lane group g) of x, in lane n == 0
@@ -423,81 +527,41 @@ __device__ __forceinline__ float sum16(float x) {
     return x;
 }
 
-// dY = irfft^T(d conv) for the 16 items: dy[t] in the spectrum layout of rfft16
+// The backward in two passes, each small enough in live state to run two waves a SIMD
+// (one pass holding every spectrum of 16 items needed 508 registers and 82 KB of LDS
+// at d = 128: one wave a SIMD, 1.4 rounds of the chip at C5).
+// 1. smore_spec_bwd_freq: dY_f, dY_v, dY_t = irfft^T(d conv_f / _v / _t) (k-step table of
+//    the irfft matrix); dp = dY_f conj(wf) held in registers; dFi = dY_v conj(wv) +
+//    dp conj(Ft), dFt = dY_t conj(wt) + dp conj(Fi) stored per wave, lane-contiguous
+//    (each float4 store a 1 KB run); d w per block.
+// 2. smore_spec_bwd_feat: d img = rfft^T(dFi), d txt = rfft^T(dFt) (output-tile table of
+//    the rfft matrix).
 template <int D>
-__device__ __forceinline__ void irfft_t16(const float* __restrict__ gsrc, int64_t item, bool iv, int g, int n16,
-                                          const float* tw, floatx4 (&dy)[Spec<D>::MT]) {
-    constexpr int SI = Spec<D>::SI, MT = Spec<D>::MT;
-    float gin[SI];
-    load_rows<D>(gsrc, item, iv, g, gin);
-#pragma unroll
-    for (int t = 0; t < MT; ++t) dy[t] = floatx4{0.f, 0.f, 0.f, 0.f};
-    float c[MT];
-#pragma unroll
-    for (int t = 0; t < MT; ++t) c[t] = 0.f;
-#pragma unroll
-    for (int s = 0; s < SI; ++s) {
-        const int f = g * SI + s;
-        tie(c);
-#pragma unroll
-        for (int t = 0; t < MT; ++t) c[t] = inv_coef<D>(f, 16 * t + n16, tw);
-#pragma unroll
-        for (int t = 0; t < MT; ++t) dy[t] = mfma16(c[t], gin[s], dy[t]);
-    }
+__device__ __forceinline__ int64_t dfreq_off(int64_t gwave, int sig, int t, int lane) {
+    return (((gwave * 2 + sig) * Spec<D>::MT + t) * 64 + lane) * 4;
 }
 
-// d x = rfft^T(dF) for the 16 items, stored to gx: output tiles in pairs (two
-// independent accumulators), step (t, i) <-> spectrum row 16t + 4g + i
 template <int D>
-__device__ __forceinline__ void rfft_t16_store(const floatx4 (&df)[Spec<D>::MT], float* __restrict__ gx, int64_t item,
-                                               bool iv, int g, int n16, const float* tw) {
-    constexpr int MT = Spec<D>::MT, OT = Spec<D>::OT;
-#pragma unroll 1
-    for (int tau = 0; tau < OT; tau += 2) {  // rolled: bounds the live coefficients to one pair of tiles
-        floatx4 a0{0.f, 0.f, 0.f, 0.f}, a1 = a0;
-        float c[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int t = 0; t < MT; ++t) {
-            tie(c);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int j = 16 * t + 4 * g + i;
-                c[i] = fwd_coef<D>(j, 16 * tau + n16, tw);
-                c[4 + i] = fwd_coef<D>(j, 16 * tau + 16 + n16, tw);
-            }
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                a0 = mfma16(c[i], df[t][i], a0);
-                a1 = mfma16(c[4 + i], df[t][i], a1);
-            }
-        }
-        if (iv) {
-            const int64_t o = item * D + 16 * tau + 4 * g;
-            st4(gx + o, make_float4(a0[0], a0[1], a0[2], a0[3]));
-            st4(gx + o + 16, make_float4(a1[0], a1[1], a1[2], a1[3]));
-        }
-    }
-}
+constexpr int kBwdFreqLds = Tab<D>::kFloats + 2 * D;
 
-// Order keeps the live state small: the fusion term first (dp = dYf conj(wf) parked
-// in LDS), then the image term (dFi formed in place of dYv and parked in LDS), the
-// text term (dFt -> d txt, after which Fi and Ft are dead), and d img last.
 template <int D>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 64 ? 2 : 1))) void smore_spec_bwd(
-    SpecBwdArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void smore_spec_bwd_freq(SpecBwdArgs a) {
     using S = Spec<D>;
-    constexpr int SI = S::SI, MT = S::MT, NB = S::NB;
-    __shared__ float tw[2 * D];
+    constexpr int MT = S::MT, NB = S::NB, SI = S::SI;
+    __shared__ __attribute__((aligned(16))) float lds[kBwdFreqLds<D>];
     __shared__ float2 ws[3][NB];
     __shared__ float2 dws[4][3][NB];
-    __shared__ float dfs[4][4 * MT][64];  // dFi parked per wave, lane-contiguous
-    __shared__ float dps[4][4 * MT][64];  // dp = dYf conj(wf), likewise
+    float* tw = lds + Tab<D>::kFloats;
     twiddles<D>(tw);
     for (int e = threadIdx.x; e < 3 * NB; e += blockDim.x)
         ws[e / NB][e % NB] = make_float2(a.w[e / NB][2 * (e % NB)], a.w[e / NB][2 * (e % NB) + 1]);
     __syncthreads();
+    tab_ks<D>(reinterpret_cast<float4*>(lds), [&](int j, int f) { return inv_coef<D>(f, j, tw); });
+    __syncthreads();
+    const float4* tab = reinterpret_cast<const float4*>(lds);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, n16 = lane & 15, g = lane >> 4;
-    const int64_t item = ((int64_t)blockIdx.x * 4 + wave) * 16 + n16;
+    const int64_t gwave = (int64_t)blockIdx.x * 4 + wave;
+    const int64_t item = gwave * 16 + n16;
     const bool iv = item < a.n;
     // the forward's spectra of tile t (lane (g, n): bins 8t + 2g, 8t + 2g + 1 of item n)
     auto spec4 = [&](int sig, int t) __attribute__((always_inline)) {
@@ -510,11 +574,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 64 ? 2
         dw.y = sum16(dw.y);
         if (n16 == 0 && bv) dws[wave][m][b] = dw;
     };
-    floatx4 dy[MT];
-    auto dp_at = [&](int t, int p) __attribute__((always_inline)) {
-        return make_float2(dps[wave][4 * t + 2 * p][lane], dps[wave][4 * t + 2 * p + 1][lane]);
+    auto store_df = [&](int sig, const floatx4 (&v)[MT]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int t = 0; t < MT; ++t)
+            st4(a.dfreq + dfreq_off<D>(gwave, sig, t, lane), make_float4(v[t][0], v[t][1], v[t][2], v[t][3]));
     };
-    irfft_t16<D>(a.g[2], item, iv, g, n16, tw, dy);
+    // dY = irfft^T(d conv_m) for the 16 items, in the spectrum layout
+    auto irfft_t = [&](int m, floatx4 (&dy)[MT]) __attribute__((always_inline)) {
+        float gin[SI];
+        load_rows<D>(a.g[m], item, iv, g, gin);
+        const float (*xs[1])[SI] = {&gin};
+        floatx4 (*accs[1])[MT] = {&dy};
+        ks_product<D, 1>(tab, xs, accs, lane);
+    };
+    floatx4 dy[MT], dp[MT];
+    irfft_t(2, dy);
 #pragma unroll
     for (int t = 0; t < MT; ++t) {
         const floatx4 fi4 = spec4(0, t), ft4 = spec4(1, t);
@@ -524,13 +598,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 64 ? 2
             const bool bv = b < NB;
             const float2 dY = pair(dy[t], p);
             put_dw(2, b, bv, cmulc(dY, cmul(pair(ft4, p), pair(fi4, p))));
-            const float2 v = bv ? cmulc(dY, ws[2][bv ? b : 0]) : make_float2(0.f, 0.f);
-            dps[wave][4 * t + 2 * p][lane] = v.x;
-            dps[wave][4 * t + 2 * p + 1][lane] = v.y;
+            set_pair(dp[t], p, bv ? cmulc(dY, ws[2][bv ? b : 0]) : make_float2(0.f, 0.f));
         }
     }
     // image: dFi = dYv conj(wv) + dp conj(Ft)
-    irfft_t16<D>(a.g[0], item, iv, g, n16, tw, dy);
+    irfft_t(0, dy);
 #pragma unroll
     for (int t = 0; t < MT; ++t) {
         const floatx4 fi4 = spec4(0, t), ft4 = spec4(1, t);
@@ -541,16 +613,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 64 ? 2
             const float2 dY = pair(dy[t], p);
             put_dw(0, b, bv, cmulc(dY, pair(fi4, p)));
             const float2 u = bv ? cmulc(dY, ws[0][bv ? b : 0]) : make_float2(0.f, 0.f);
-            const float2 v = cmulc(dp_at(t, p), pair(ft4, p));
+            const float2 v = cmulc(pair(dp[t], p), pair(ft4, p));
             set_pair(dy[t], p, make_float2(u.x + v.x, u.y + v.y));
         }
     }
-#pragma unroll
-    for (int t = 0; t < MT; ++t)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) dfs[wave][4 * t + i][lane] = dy[t][i];
+    store_df(0, dy);
     // text: dFt = dYt conj(wt) + dp conj(Fi)
-    irfft_t16<D>(a.g[1], item, iv, g, n16, tw, dy);
+    irfft_t(1, dy);
 #pragma unroll
     for (int t = 0; t < MT; ++t) {
         const floatx4 fi4 = spec4(0, t), ft4 = spec4(1, t);
@@ -561,16 +630,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 64 ? 2
             const float2 dY = pair(dy[t], p);
             put_dw(1, b, bv, cmulc(dY, pair(ft4, p)));
             const float2 u = bv ? cmulc(dY, ws[1][bv ? b : 0]) : make_float2(0.f, 0.f);
-            const float2 v = cmulc(dp_at(t, p), pair(fi4, p));
+            const float2 v = cmulc(pair(dp[t], p), pair(fi4, p));
             set_pair(dy[t], p, make_float2(u.x + v.x, u.y + v.y));
         }
     }
-    rfft_t16_store<D>(dy, a.gx[1], item, iv, g, n16, tw);
-#pragma unroll
-    for (int t = 0; t < MT; ++t)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) dy[t][i] = dfs[wave][4 * t + i][lane];
-    rfft_t16_store<D>(dy, a.gx[0], item, iv, g, n16, tw);
+    store_df(1, dy);
     __syncthreads();
     // per-block d weight partial, waves added in order (deterministic)
     for (int e = threadIdx.x; e < 3 * NB * 2; e += blockDim.x) {
@@ -578,6 +642,126 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 64 ? 2
         const float2 w0 = dws[0][m][k], w1 = dws[1][m][k], w2 = dws[2][m][k], w3 = dws[3][m][k];
         const float v = c ? ((w0.y + w1.y) + w2.y) + w3.y : ((w0.x + w1.x) + w2.x) + w3.x;
         a.gw[((int64_t)blockIdx.x * 3 + m) * NB * 2 + k * 2 + c] = v;
+    }
+}
+
+template <int D>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void smore_spec_bwd_feat(SpecBwdArgs a) {
+    constexpr int MT = Spec<D>::MT, OT = Spec<D>::OT;
+    __shared__ __attribute__((aligned(16))) float lds[kBwdFreqLds<D>];
+    float* tw = lds + Tab<D>::kFloats;
+    twiddles<D>(tw);
+    __syncthreads();
+    tab_ot<D>(reinterpret_cast<float4*>(lds), [&](int j, int o) { return fwd_coef<D>(j, o, tw); });
+    __syncthreads();
+    const float4* tab = reinterpret_cast<const float4*>(lds);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, n16 = lane & 15, g = lane >> 4;
+    const int64_t gwave = (int64_t)blockIdx.x * 4 + wave;
+    const int64_t item = gwave * 16 + n16;
+    const bool iv = item < a.n;
+#pragma unroll 1
+    for (int sig = 0; sig < 2; ++sig) {
+        floatx4 df[MT];
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+            const float4 v = ld4(a.dfreq + dfreq_off<D>(gwave, sig, t, lane));
+            df[t] = floatx4{v.x, v.y, v.z, v.w};
+        }
+        // d x = rfft^T(dF): output tiles in pairs (two independent accumulators), step
+        // (t, i) <-> spectrum row 16t + 4g + i
+#pragma unroll 1
+        for (int tau = 0; tau < OT; tau += 2) {  // rolled: bounds the live coefficients to one pair of tiles
+            floatx4 a0{0.f, 0.f, 0.f, 0.f}, a1 = a0;
+            float4 c[2] = {f4(0.f), f4(0.f)};
+#pragma unroll
+            for (int t = 0; t < MT; ++t) {
+                tie(c);
+                const int base = opaque(lane);
+                c[0] = ot_at<D>(tab, base, tau, t, lane);
+                c[1] = ot_at<D>(tab, base, tau + 1, t, lane);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    a0 = mfma16(f4c(c[0], i), df[t][i], a0);
+                    a1 = mfma16(f4c(c[1], i), df[t][i], a1);
+                }
+            }
+            if (iv) {
+                const int64_t o = item * D + 16 * tau + 4 * g;
+                st4(a.gx[sig] + o, make_float4(a0[0], a0[1], a0[2], a0[3]));
+                st4(a.gx[sig] + o + 16, make_float4(a1[0], a1[1], a1[2], a1[3]));
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// the item side in one launch: projection -> spectral part -> modality gates
+// ---------------------------------------------------------------------------
+// Every block runs its smore_proj share (an item tile x one modality x one K split) and
+// then counts itself in at its tile; the tile's last arriver (release / acquire at agent
+// scope: the other blocks' projection rows may sit in another XCD's L2) runs the
+// spectral part of those 64 items and, with `item` set, the three modality gates
+// (smore.py:262-272) on the conv rows its own lanes just stored.  The arithmetic is
+// smore_proj + smore_spec_fwd + gates_fwd's, op for op: the results are bit-identical
+// to the three-launch chain, without its two [n, d] round trips through HBM, two
+// launch boundaries or the spectral part's tail (it runs while other tiles project).
+struct ItemFwdArgs {
+    SpecProjArgs p;
+    SpecFwdArgs s;
+    uint32_t* cnt;          // [tiles] arrival counters: zero, re-armed by each tile's last arriver
+    const float* item;      // item_id embedding [n, D] (NULL: no gates)
+    const float* gW[3];     // gate_v/t/f Linear weights [D, D] and biases
+    const float* gb[3];
+    float scale;            // inject_scale (residual mode)
+    int32_t mul;            // inject_mode == "mul"
+    float* gout[3];         // img_i, txt_i, fus_i
+};
+
+template <int D>
+constexpr int kItemLds = kPjLds<D> > kSpecLds<D> ? (kPjLds<D> > D * sf::kLd<D> ? kPjLds<D> : D * sf::kLd<D>)
+                                                 : (kSpecLds<D> > D * sf::kLd<D> ? kSpecLds<D> : D * sf::kLd<D>);
+
+template <int D>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void smore_item_fwd(ItemFwdArgs a) {
+    __shared__ __attribute__((aligned(16))) float lds[kItemLds<D>];
+    __shared__ int last;
+    const int tile = proj_block<D>(a.p, blockIdx.x, lds);
+    // publish (the split-K counter hand-off): every wave drains its projection stores, one
+    // lane releases at agent scope for the block (one L2 write-back per block: a release in
+    // every lane, or __threadfence(), costs several times the whole hand-off) then counts
+    // the block in; the tile's last arriver acquires once and reads the other blocks' rows
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t need = (uint32_t)(a.p.S[0] + a.p.S[1]);
+        const uint32_t prev = __hip_atomic_fetch_add(a.cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = prev + 1 == need;
+        if (last) {
+            __hip_atomic_store(a.cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    }
+    __syncthreads();
+    if (!last) return;  // block-uniform
+    spec_setup<D>(a.s, lds);
+    spec_tile<D>(a.s, tile, lds);
+    if (!a.item) return;
+    // the gates: the conv rows this lane stored above (same lane, same addresses)
+    const int lane = threadIdx.x & 63, g = lane >> 4;
+    const int64_t r = ((int64_t)tile * 4 + (threadIdx.x >> 6)) * 16 + (lane & 15);
+    const int64_t row = r < a.s.n ? r : -1;
+    const sf::Fld<D> it = sf::fload<D>(a.item, row, g);
+#pragma unroll 1
+    for (int m = 0; m < 3; ++m) {
+        const sf::Fld<D> cv = sf::fload<D>(a.s.conv[m], row, g);
+        const float* W = sf::stage_w<D>(lds, a.gW[m]);  // (its barrier: the spectral part's LDS readers are done)
+        const sf::Fld<D> sg = sf::fmap<D>(sf::mv_p<D, sf::kLd<D>>(W, a.gb[m], cv, lane), sf::sigm);
+        const sf::Fld<D> o = a.mul ? sf::fmap2<D>(it, sg, [](float x, float y) { return x * y; })
+                                   : sf::fmap2<D>(it, sg, [&](float x, float y) { return x + a.scale * y; });
+        sf::fstore<D>(a.gout[m], row, g, o);
     }
 }
 
@@ -613,20 +797,17 @@ extern "C" size_t rsx_smore_spectral_fwd_ws_bytes(int64_t n_items, int32_t d, in
     return (size_t)extra * (size_t)n_items * (size_t)d * sizeof(float);
 }
 
-extern "C" int rsx_smore_spectral_fwd(const float* V, int32_t dv, const float* Wv, const float* bv, const float* T,
-                                      int32_t dt, const float* Wt, const float* bt, const float* wv, const float* wt,
-                                      const float* wf, int64_t n_items, int32_t d, float* img, float* txt,
-                                      float* conv_v, float* conv_t, float* conv_f, float* spec, void* ws,
-                                      size_t ws_bytes, rsx_stream_t stream) {
+// the launch arguments of the projection and the spectral part (rc != RSX_OK: invalid)
+static int spectral_args(const float* V, int32_t dv, const float* Wv, const float* bv, const float* T, int32_t dt,
+                         const float* Wt, const float* bt, const float* wv, const float* wt, const float* wf,
+                         int64_t n_items, int32_t d, float* img, float* txt, float* conv_v, float* conv_t,
+                         float* conv_f, float* spec, void* ws, size_t ws_bytes, SpecProjArgs& p, SpecFwdArgs& a) {
     if (n_items < 0 || dv <= 0 || dt <= 0 || (dv & 3) || (dt & 3)) return RSX_ERR_ARG;
     if (!V || !Wv || !bv || !T || !Wt || !bt || !wv || !wt || !wf || !img || !txt || !conv_v || !conv_t || !conv_f ||
         !spec)
         return RSX_ERR_ARG;
     if (d != 64 && d != 128) return RSX_ERR_UNSUPPORTED;
-    if (n_items == 0) return RSX_OK;
     if (ws_bytes < rsx_smore_spectral_fwd_ws_bytes(n_items, d, dv, dt) || (ws_bytes && !ws)) return RSX_ERR_WORKSPACE;
-    SpecProjArgs p;
-    SpecFwdArgs a;
     p.X[0] = V;
     p.X[1] = T;
     p.K[0] = dv;
@@ -663,6 +844,19 @@ extern "C" int rsx_smore_spectral_fwd(const float* V, int32_t dv, const float* W
     a.conv[1] = conv_t;
     a.conv[2] = conv_f;
     a.spec = spec;
+    return RSX_OK;
+}
+
+extern "C" int rsx_smore_spectral_fwd(const float* V, int32_t dv, const float* Wv, const float* bv, const float* T,
+                                      int32_t dt, const float* Wt, const float* bt, const float* wv, const float* wt,
+                                      const float* wf, int64_t n_items, int32_t d, float* img, float* txt,
+                                      float* conv_v, float* conv_t, float* conv_f, float* spec, void* ws,
+                                      size_t ws_bytes, rsx_stream_t stream) {
+    SpecProjArgs p;
+    SpecFwdArgs a;
+    const int rc = spectral_args(V, dv, Wv, bv, T, dt, Wt, bt, wv, wt, wf, n_items, d, img, txt, conv_v, conv_t,
+                                 conv_f, spec, ws, ws_bytes, p, a);
+    if (rc != RSX_OK || n_items == 0) return rc;
     const dim3 gp((unsigned)(p.tiles * (p.S[0] + p.S[1])));
     const dim3 gs((unsigned)((n_items + 63) / 64));
     hipStream_t s = as_stream(stream);
@@ -676,16 +870,62 @@ extern "C" int rsx_smore_spectral_fwd(const float* V, int32_t dv, const float* W
     return last_rc();
 }
 
+extern "C" size_t rsx_smore_item_tiles(int64_t n_items) {
+    return n_items <= 0 ? 0 : (size_t)((n_items + kPjItems - 1) / kPjItems);
+}
+
+extern "C" int rsx_smore_item_fwd(const float* V, int32_t dv, const float* Wv, const float* bv, const float* T,
+                                  int32_t dt, const float* Wt, const float* bt, const float* wv, const float* wt,
+                                  const float* wf, int64_t n_items, int32_t d, float* img, float* txt, float* conv_v,
+                                  float* conv_t, float* conv_f, float* spec, void* ws, size_t ws_bytes,
+                                  uint32_t* tile_cnt, const float* item, const float* const* gate_W,
+                                  const float* const* gate_b, float scale, int32_t mul, float* const* gate_out,
+                                  rsx_stream_t stream) {
+    ItemFwdArgs a;
+    const int rc = spectral_args(V, dv, Wv, bv, T, dt, Wt, bt, wv, wt, wf, n_items, d, img, txt, conv_v, conv_t,
+                                 conv_f, spec, ws, ws_bytes, a.p, a.s);
+    if (rc != RSX_OK) return rc;
+    if (!tile_cnt) return RSX_ERR_ARG;
+    a.cnt = tile_cnt;
+    a.item = item;
+    a.scale = scale;
+    a.mul = mul;
+    if (item && (!gate_W || !gate_b || !gate_out)) return RSX_ERR_ARG;
+    for (int m = 0; m < 3; ++m) {
+        a.gW[m] = item ? gate_W[m] : nullptr;
+        a.gb[m] = item ? gate_b[m] : nullptr;
+        a.gout[m] = item ? gate_out[m] : nullptr;
+        if (item && (!a.gW[m] || !a.gb[m] || !a.gout[m])) return RSX_ERR_ARG;
+    }
+    if (n_items == 0) return RSX_OK;
+    const dim3 grid((unsigned)(a.p.tiles * (a.p.S[0] + a.p.S[1])));
+    hipStream_t s = as_stream(stream);
+    if (d == 64)
+        hipLaunchKernelGGL(smore_item_fwd<64>, grid, dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL(smore_item_fwd<128>, grid, dim3(256), 0, s, a);
+    return last_rc();
+}
+
 extern "C" size_t rsx_smore_spectral_bwd_partials(int64_t n_items, int32_t d) {
     return (size_t)((n_items + 63) / 64) * 3 * (size_t)(d / 2 + 1) * 2;
 }
 
+extern "C" size_t rsx_smore_spectral_bwd_ws_bytes(int64_t n_items, int32_t d) {
+    if (n_items <= 0) return 0;
+    const int mt = d == 64 ? Spec<64>::MT : Spec<128>::MT;
+    const int64_t waves = (n_items + 63) / 64 * 4;
+    return (size_t)waves * 2 * (size_t)mt * 64 * 4 * sizeof(float);
+}
+
 extern "C" int rsx_smore_spectral_bwd(const float* spec, const float* wv, const float* wt, const float* wf,
                                       const float* g_v, const float* g_t, const float* g_f, int64_t n_items, int32_t d,
-                                      float* g_img, float* g_txt, float* g_w_partial, rsx_stream_t stream) {
+                                      float* g_img, float* g_txt, float* g_w_partial, void* ws, size_t ws_bytes,
+                                      rsx_stream_t stream) {
     if (n_items < 0 || !spec || !wv || !wt || !wf || !g_img || !g_txt || !g_w_partial) return RSX_ERR_ARG;
     if (d != 64 && d != 128) return RSX_ERR_UNSUPPORTED;
     if (n_items == 0) return RSX_OK;
+    if (!ws || ws_bytes < rsx_smore_spectral_bwd_ws_bytes(n_items, d)) return RSX_ERR_WORKSPACE;
     SpecBwdArgs a;
     a.spec = spec;
     a.w[0] = wv;
@@ -698,11 +938,15 @@ extern "C" int rsx_smore_spectral_bwd(const float* spec, const float* wv, const 
     a.gx[0] = g_img;
     a.gx[1] = g_txt;
     a.gw = g_w_partial;
+    a.dfreq = static_cast<float*>(ws);
     const dim3 g((unsigned)((n_items + 63) / 64));
     hipStream_t s = as_stream(stream);
-    if (d == 64)
-        hipLaunchKernelGGL(smore_spec_bwd<64>, g, dim3(256), 0, s, a);
-    else
-        hipLaunchKernelGGL(smore_spec_bwd<128>, g, dim3(256), 0, s, a);
+    if (d == 64) {
+        hipLaunchKernelGGL(smore_spec_bwd_freq<64>, g, dim3(256), 0, s, a);
+        hipLaunchKernelGGL(smore_spec_bwd_feat<64>, g, dim3(256), 0, s, a);
+    } else {
+        hipLaunchKernelGGL(smore_spec_bwd_freq<128>, g, dim3(256), 0, s, a);
+        hipLaunchKernelGGL(smore_spec_bwd_feat<128>, g, dim3(256), 0, s, a);
+    }
     return last_rc();
 }

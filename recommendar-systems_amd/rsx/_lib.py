@@ -144,7 +144,11 @@ def _declare(lib):
         "rsx_smore_spectral_fwd_ws_bytes": (C.c_size_t, [I64, I32, I32, I32]),
         "rsx_smore_spectral_fwd": (C.c_int, [P, I32, P, P, P, I32, P, P, P, P, P, I64, I32, P, P, P, P, P, P, P,
                                              C.c_size_t, P]),
-        "rsx_smore_spectral_bwd": (C.c_int, [P, P, P, P, P, P, P, I64, I32, P, P, P, P]),
+        "rsx_smore_item_tiles": (C.c_size_t, [I64]),
+        "rsx_smore_item_fwd": (C.c_int, [P, I32, P, P, P, I32, P, P, P, P, P, I64, I32, P, P, P, P, P, P, P,
+                                         C.c_size_t, P, P, P, P, F32, I32, P, P]),
+        "rsx_smore_spectral_bwd": (C.c_int, [P, P, P, P, P, P, P, I64, I32, P, P, P, P, C.c_size_t, P]),
+        "rsx_smore_spectral_bwd_ws_bytes": (C.c_size_t, [I64, I32]),
         "rsx_smore_spectral_bwd_partials": (C.c_size_t, [I64, I32]),
         "rsx_topk_metrics_ws_bytes": (C.c_size_t, [I64, I32]),
         "rsx_topk_metrics": (C.c_int, [P, I64, I32, P, P, P, I32, P, P, P, C.c_size_t, P]),
@@ -212,7 +216,7 @@ EXPORTED = ["rsx_version", "rsx_csr_schedule_host", "rsx_csr_schedule_rebind", "
             "rsx_sample_epoch_slices",
             "rsx_smore_spectral_spec_floats", "rsx_smore_spectral_fwd_ws_bytes", "rsx_smore_spectral_fwd",
             "rsx_smore_spectral_bwd",
-            "rsx_smore_spectral_bwd_partials",
+            "rsx_smore_spectral_bwd_partials", "rsx_smore_spectral_bwd_ws_bytes", "rsx_smore_item_tiles", "rsx_smore_item_fwd",
             "rsx_topk_metrics_ws_bytes", "rsx_topk_metrics", "rsx_topk_metrics_fast", "rsx_linear_wgrad_ws_bytes", "rsx_linear_wgrad", "rsx_linear_bwd_ws_bytes", "rsx_linear_bwd",
             "rsx_comm_unique_id_bytes", "rsx_comm_get_unique_id", "rsx_comm_init", "rsx_comm_destroy",
             "rsx_comm_init_host",

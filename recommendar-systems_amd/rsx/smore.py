@@ -417,6 +417,9 @@ class SMORE(GeneralRecommender):
         self._rows_off = {}
         self._tags = None
         self.batch_views = bool(config.get("rsx_smore_batch_views", True))
+        # the item side (projections, spectral part, gates) as one launch (rsx_smore_item_fwd);
+        # False: the three-launch chain (same values, bit for bit)
+        self.item_fused = bool(config.get("rsx_smore_item_fused", True))
         # dropout masks of the fused preference block: a hash of (seed, call, row,
         # feature); the seed word lives on the device and advances once per training
         # forward (graph-capture safe).  Derived from the config seed, not torch's RNG,
@@ -630,9 +633,14 @@ class SMORE(GeneralRecommender):
                 content = _PropMeanRows.apply(ego, self.norm_adj_csr, self.n_ui_layers, self._tags, rows)
             else:
                 content = _PropMean.apply(ego, self.norm_adj_csr, self.n_ui_layers)
-        cv, ct, cf = self._projected_spectrum()
-        img_i, txt_i, fus_i = SF.gates(cv, ct, cf, item_id, self.gate_v, self.gate_t, self.gate_f,
-                                       self.inject_scale, self.inject_mode == "mul")
+        if self.item_fused and type(self)._projected_spectrum is SMORE._projected_spectrum:
+            from .smore_spectral import item_side_fused
+
+            (img_i, txt_i, fus_i), (cv, ct, cf) = item_side_fused(self, item_id)
+        else:
+            cv, ct, cf = self._projected_spectrum()
+            img_i, txt_i, fus_i = SF.gates(cv, ct, cf, item_id, self.gate_v, self.gate_t, self.gate_f,
+                                           self.inject_scale, self.inject_mode == "mul")
         if side is not None:
             main.wait_stream(side)
             content.record_stream(main)  # allocated on the side stream, read on this one

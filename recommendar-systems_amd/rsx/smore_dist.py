@@ -343,21 +343,29 @@ class HipSmoreBackend:
 
         return SF.gates(cv, ct, cf, item, m.gate_v, m.gate_t, m.gate_f, m.inject_scale, False)
 
+    def item_side(self, m, item):
+        """spectral + gates as the one-launch item side (rsx_smore_item_fwd)."""
+        from .smore_spectral import item_side
+
+        return item_side(m.image_embedding.weight, m.image_trs.weight, m.image_trs.bias, m.text_embedding.weight,
+                         m.text_trs.weight, m.text_trs.bias, m.image_complex_weight, m.text_complex_weight,
+                         m.fusion_complex_weight, item, m.gate_v, m.gate_t, m.gate_f, m.inject_scale, False,
+                         getattr(m, "spectral_weight_norm", True))[:3]
+
     def item_side_sharded(self, core, m, item):
         """Projection -> spectral -> the gates' inject term on this rank's item rows only
         (the fused kernels on n_own rows), gathered once; + the replicated item-id table."""
-        from . import smore_fuse as SF
-        from .smore_spectral import spectral
+        from .smore_spectral import _ItemSide
 
         w = dict(zip(ITEM_W, allreduce_grad(core.comm, *[m.get_parameter(n) for n in ITEM_W])))
-        cv, ct, cf, _, _ = spectral(m.image_embedding.weight, w["image_trs.weight"], w["image_trs.bias"],
-                                    m.text_embedding.weight, w["text_trs.weight"], w["text_trs.bias"],
-                                    w["image_complex_weight"], w["text_complex_weight"], w["fusion_complex_weight"],
-                                    getattr(m, "spectral_weight_norm", True))
-        zero = core.zero_rows(cv)
-        dv, dt, df = SF._Gates.apply(cv, ct, cf, zero, w["gate_v.0.weight"], w["gate_v.0.bias"], w["gate_t.0.weight"],
+        # the gates' item operand is zero: the kernel writes the inject term alone
+        zero = core.zero_rows(m.image_embedding.weight.shape[0], item.shape[1], item.device)
+        dv, dt, df = _ItemSide.apply(m.image_embedding.weight, w["image_trs.weight"], w["image_trs.bias"],
+                                     m.text_embedding.weight, w["text_trs.weight"], w["text_trs.bias"],
+                                     w["image_complex_weight"], w["text_complex_weight"], w["fusion_complex_weight"],
+                                     zero, w["gate_v.0.weight"], w["gate_v.0.bias"], w["gate_t.0.weight"],
                                      w["gate_t.0.bias"], w["gate_f.0.weight"], w["gate_f.0.bias"],
-                                     float(m.inject_scale), False)
+                                     bool(getattr(m, "spectral_weight_norm", True)), float(m.inject_scale), False)[:3]
         D = gather_rows(core.comm, core.iq, core.n_items, dv, dt, df)
         return (D + item.unsqueeze(0)).unbind(0)
 
@@ -437,16 +445,19 @@ class SmoreShard:
     def ui_mean(self, x):
         return self.be.ui_mean(self, x)
 
-    def zero_rows(self, like):
-        """A zero [n_own_items, d] table (the gates kernel's item operand: the inject term alone)."""
-        if self._zero is None or self._zero.shape != like.shape or self._zero.device != like.device:
-            self._zero = torch.zeros_like(like)
-        return self._zero
+    def zero_rows(self, n, d, device):
+        """A zero [n_own_items, d] table (the gates' item operand: the inject term alone)."""
+        z = self._zero
+        if z is None or z.shape != (n, d) or z.device != torch.device(device):
+            self._zero = z = torch.zeros(n, d, dtype=torch.float32, device=device)
+        return z
 
     def _item_side(self, m, item=None):
         item = m.item_id_embedding.weight if item is None else item
         if self.item_shard:
             return self.be.item_side_sharded(self, m, item)
+        if hasattr(self.be, "item_side"):
+            return self.be.item_side(m, item)
         cv, ct, cf = self.be.spectral(m)
         return self.be.gates(m, cv, ct, cf, item)
 

@@ -77,18 +77,24 @@ class _Gates(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gv, gt, gf):
         cv, ct, cf, item, Wv, Wt, Wf, bv, bt, bf = ctx.saved_tensors
-        scale, mul = ctx.cfg
-        n, d = item.shape
-        gi = torch.empty_like(item)
-        gc = [torch.empty_like(item) for _ in range(3)]
-        dz = [torch.empty_like(item) for _ in range(3)]
-        gouts = [None if g is None else _c(g) for g in (gv, gt, gf)]
-        L.check(L.lib().rsx_smore_gates(1, _arr([cv, ct, cf]), _p(item), _arr([Wv, Wt, Wf]), _arr([bv, bt, bf]), n,
-                                        d, scale, mul, None, _arr(gouts), _p(gi), _arr(gc), _arr(dz),
-                                        ops._stream()), "rsx_smore_gates")
-        (gWv, gbv), (gWt, gbt), (gWf, gbf) = _wgrad([(dz[0], cv, True), (dz[1], ct, True), (dz[2], cf, True)], d,
-                                                    item.device)
-        return gc[0], gc[1], gc[2], gi, gWv, gbv, gWt, gbt, gWf, gbf, None, None
+        gc, gi, wg = _gates_backward((cv, ct, cf), item, (Wv, Wt, Wf), (bv, bt, bf), ctx.cfg, (gv, gt, gf))
+        return (*gc, gi, *wg, None, None)
+
+
+def _gates_backward(conv, item, W, b, cfg, gouts):
+    """(d conv[3], d item, (d Wv, d bv, d Wt, d bt, d Wf, d bf)) of the gates: one launch
+    for the row gradients, one rsx_smore_wgrad pair for the weights."""
+    scale, mul = cfg
+    n, d = item.shape
+    gi = torch.empty_like(item)
+    gc = [torch.empty_like(item) for _ in range(3)]
+    dz = [torch.empty_like(item) for _ in range(3)]
+    gouts = [None if g is None else _c(g) for g in gouts]
+    L.check(L.lib().rsx_smore_gates(1, _arr(list(conv)), _p(item), _arr(list(W)), _arr(list(b)), n, d, scale, mul,
+                                    None, _arr(gouts), _p(gi), _arr(gc), _arr(dz), ops._stream()), "rsx_smore_gates")
+    (gWv, gbv), (gWt, gbt), (gWf, gbf) = _wgrad([(dz[0], conv[0], True), (dz[1], conv[1], True),
+                                                 (dz[2], conv[2], True)], d, item.device)
+    return gc, gi, (gWv, gbv, gWt, gbt, gWf, gbf)
 
 
 def gates(cv, ct, cf, item, gate_v, gate_t, gate_f, scale: float, mul: bool):

@@ -369,6 +369,42 @@ def test_spectral_fused_vs_torch_autograd(cuda, d, n, dv, dt):
         np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), rtol=1e-4, atol=1e-4 * scale, err_msg=name)
 
 
+@pytest.mark.parametrize("d,n,dv,dt,mul", [(64, 1000, 512, 384, False), (128, 333, 768, 768, False),
+                                           (64, 7, 48, 24, True), (64, 200, 4096, 384, False),
+                                           (128, 23033, 768, 768, False), (128, 129, 1024, 96, True)])
+def test_item_side_one_launch_equals_three_launch_chain(cuda, d, n, dv, dt, mul):
+    """rsx_smore_item_fwd (projection -> spectral -> gates in one launch, the tile's last
+    arriving block running the tail) against rsx_smore_spectral_fwd + rsx_smore_gates: every
+    output bit for bit (the same arithmetic), K-split projections (4096-wide: 8 splits of a
+    tile counted in), ragged last tiles, residual and mul inject; called three times so the
+    arrival counters are re-armed; the backward's gradients equal the chain's, bit for bit."""
+    from rsx import smore_fuse as SF
+    from rsx.smore_spectral import item_side, spectral
+
+    g = torch.Generator(device="cpu").manual_seed(3 * d + n)
+    mk = lambda *s: torch.randn(*s, generator=g).to(cuda).requires_grad_()  # noqa: E731
+    V, T = mk(n, dv), mk(n, dt)
+    Wv, Wt = (mk(d, dv) / dv ** 0.5).detach().requires_grad_(), (mk(d, dt) / dt ** 0.5).detach().requires_grad_()
+    bv, bt = mk(d), mk(d)
+    wv, wt, wf = mk(1, d // 2 + 1, 2), mk(1, d // 2 + 1, 2), mk(1, d // 2 + 1, 2)
+    item = mk(n, d)
+    gates = [torch.nn.Sequential(torch.nn.Linear(d, d), torch.nn.Sigmoid()).to(cuda) for _ in range(3)]
+    leaves = [V, Wv, bv, T, Wt, bt, wv, wt, wf, item] + [p for s in gates for p in s.parameters()]
+    up = [torch.randn(n, d, generator=g).to(cuda) for _ in range(3)]
+
+    cv, ct, cf, img, txt = spectral(V, Wv, bv, T, Wt, bt, wv, wt, wf)
+    ref = SF.gates(cv, ct, cf, item, *gates, 0.7, mul)
+    ref_g = torch.autograd.grad(sum((r * u).sum() for r, u in zip(ref, up)), leaves)
+    for rep in range(3):
+        got = item_side(V, Wv, bv, T, Wt, bt, wv, wt, wf, item, *gates, 0.7, mul)
+        for name, a, b in zip(["img_i", "txt_i", "fus_i", "conv_v", "conv_t", "conv_f", "img", "txt"], got,
+                              (*ref, cv, ct, cf, img, txt)):
+            assert torch.equal(a, b), (rep, name, (a - b).abs().max().item())
+    got_g = torch.autograd.grad(sum((r * u).sum() for r, u in zip(got[:3], up)), leaves)
+    for i, (a, b) in enumerate(zip(got_g, ref_g)):
+        assert torch.equal(a, b), (i, (a - b).abs().max().item())
+
+
 @pytest.mark.parametrize("n,o,i", [(26495, 64, 64), (1000, 128, 64), (7, 32, 32), (513, 64, 128), (7050, 64, 4096),
                                    (7050, 64, 384), (0, 64, 64), (65, 32, 32), (300001, 64, 64)])
 def test_linear_wgrad_vs_torch(cuda, n, o, i):
