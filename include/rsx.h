@@ -198,6 +198,10 @@ typedef struct rsx_epilogue {
     /* ADAM (optional): when *halt != 0 the parameters and moments are left unchanged
      * (a NaN loss stopped training, rsx_lgcn_step.halt) */
     const int32_t* halt;
+    /* RSX_TAG_SPARSE_X (optional): the tags of X's rows where they are numbered apart
+     * from the output rows (a rectangular operator, e.g. R^T: items x users); NULL:
+     * row_tag for both */
+    const int32_t* x_tag;
 } rsx_epilogue;
 
 #define RSX_TAG_ROWS 1

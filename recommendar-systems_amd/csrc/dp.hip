@@ -24,12 +24,14 @@
 // once.  A row with one occurrence gets exactly the f32 term the single-GPU step adds.
 //
 // Per step on the comm stream (hidden behind the forward): the triplet all-gather, the
-// union tags and global regulariser counts (dp_index), and a stable radix sort of the
-// W 3 B occurrences by row, which lets the gradient pass add each run of equal rows in
-// registers and issue one atomic per run instead of one per occurrence (hot items occur
-// hundreds of times in a global batch).
-#include <hipcub/hipcub.hpp>
-
+// union tags and global regulariser counts (dp_index), and the W 3 B occurrences bucketed
+// by row (dp_alloc: each union row's first claimer reserves a run of its count;
+// dp_scatter: each occurrence takes a place in its row's run), which lets the gradient
+// pass add each run of equal rows in registers and issue one atomic per run instead of
+// one per occurrence (hot items occur hundreds of times in a global batch).  Where a run
+// lands and its order are not fixed, and need not be: the sums are integer (below).  Two
+// small launches instead of a radix sort's five (merge-sort passes for these sizes,
+// ~43 us at W = 1 and ~47 at W = 8 on the comm stream: the loss waited on them).
 #include "rsx_common.hpp"
 
 namespace rsx {
@@ -50,22 +52,17 @@ constexpr int kChunk = 16;  // sorted occurrences per lane group in the gradient
 // The step's workspace (rsx_dp_lgcn_step.work), carved in this order, 256-B aligned.
 struct Work {
     unsigned long long* acc;  // [N][d] fixed-point G' accumulators (zero between steps)
-    int32_t *ka, *kb, *va, *vb;  // occurrence keys (rows) / ids, radix-sort double buffers
+    int32_t* start;           // [N] a union row's run start + 1 (0: unclaimed; cleared by dp_bpr_round)
+    int32_t* cursor;          // [N] places taken in the row's run (cleared by dp_bpr_round)
+    int32_t* keys;            // [W 3 cap] the row of each run place
+    int32_t* occ;             // [W 3 cap] the occurrence at each run place
     float* coef;              // [W][cap] per-triplet dL/d(s+ - s-)
     double* part;             // [n_blk_a][5] loss, |U|^2, |P|^2, |N|^2, max |f| partials
-    int32_t* meta;            // [4]: done counter, fixed-point exponent
-    void* temp;               // hipCUB radix-sort temp storage
-    size_t temp_bytes;
+    int32_t* meta;            // [4]: done counter, fixed-point exponent, run places taken
     size_t total;
 };
 
 size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
-
-int key_bits(int64_t N) {  // bits of the sort key: rows 0..N-1, padding N
-    int b = 1;
-    while ((int64_t(1) << b) <= N) ++b;
-    return b;
-}
 
 Work carve(void* base, int64_t N, int d, int64_t cap, int W) {
     Work w = {};
@@ -79,31 +76,30 @@ Work carve(void* base, int64_t N, int d, int64_t cap, int W) {
         return q;
     };
     w.acc = static_cast<unsigned long long*>(take((size_t)N * d * 8));
-    w.ka = static_cast<int32_t*>(take((size_t)n_occ * 4));
-    w.kb = static_cast<int32_t*>(take((size_t)n_occ * 4));
-    w.va = static_cast<int32_t*>(take((size_t)n_occ * 4));
-    w.vb = static_cast<int32_t*>(take((size_t)n_occ * 4));
+    w.start = static_cast<int32_t*>(take((size_t)N * 4));
+    w.cursor = static_cast<int32_t*>(take((size_t)N * 4));
+    w.keys = static_cast<int32_t*>(take((size_t)n_occ * 4));
+    w.occ = static_cast<int32_t*>(take((size_t)n_occ * 4));
     w.coef = static_cast<float*>(take((size_t)n_trip * 4));
     w.part = static_cast<double*>(take((size_t)n_blk * 5 * 8));
     w.meta = static_cast<int32_t*>(take(16));
-    hipcub::DoubleBuffer<int32_t> k(w.ka, w.kb), v(w.va, w.vb);
-    size_t tb = 0;
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k, v, (int)n_occ, 0, key_bits(N));
-    w.temp = take(tb);
-    w.temp_bytes = tb;
     w.total = o;
     return w;
 }
 
 // slot = [B, users[cap], positives[cap], negatives[cap]] (tail zero)
 // (step: the Adam counter the step increments first, or NULL)
+// (meta[2], the run places the previous step took, is zeroed here: the step's first
+// launch, ahead of the comm stream's fork)
 __global__ __launch_bounds__(kBlk) void dp_pack(const int64_t* __restrict__ trip, int64_t B, int64_t cap,
-                                                int64_t* __restrict__ slot, int64_t* __restrict__ step) {
+                                                int64_t* __restrict__ slot, int64_t* __restrict__ step,
+                                                int32_t* __restrict__ meta) {
     const int64_t i = (int64_t)blockIdx.x * kBlk + threadIdx.x;
     if (i > 3 * cap) return;
     if (i == 0) {
         slot[0] = B;
         if (step) step[0] += 1;
+        meta[2] = 0;
         return;
     }
     const int64_t j = i - 1, k = j / cap, t = j - k * cap;
@@ -120,20 +116,43 @@ __device__ __forceinline__ int64_t occ_row(const int64_t* slots, int64_t cap, in
     return j < cap ? id : n_users + id;
 }
 
-// (comm stream, once the triplets are gathered) union tags, global occurrence counts (the
-// regulariser's), and the sort input: key = row (N for a padding slot), value = occurrence
+// (comm stream, once the triplets are gathered) union tags and global occurrence counts
+// (the regulariser's, and the runs' lengths)
 __global__ __launch_bounds__(kBlk) void dp_index(const int64_t* __restrict__ slots, int32_t W, int64_t cap,
-                                                 int64_t n_users, int64_t N, int32_t* __restrict__ row_tag,
-                                                 int32_t* __restrict__ reg_cnt, const int32_t* __restrict__ tag_dev,
-                                                 int32_t* __restrict__ key, int32_t* __restrict__ val) {
+                                                 int64_t n_users, int32_t* __restrict__ row_tag,
+                                                 int32_t* __restrict__ reg_cnt, const int32_t* __restrict__ tag_dev) {
     const int64_t i = (int64_t)blockIdx.x * kBlk + threadIdx.x;
     if (i >= (int64_t)W * 3 * cap) return;
     const int64_t x = occ_row(slots, cap, n_users, i);
-    key[i] = x < 0 ? (int32_t)N : (int32_t)x;
-    val[i] = (int32_t)i;
     if (x < 0) return;
     row_tag[x] = *tag_dev;
     atomicAdd(reg_cnt + 3 * x + (i % (3 * cap)) / cap, 1);
+}
+
+// (comm stream) each union row's run: its first claimer reserves count places
+__global__ __launch_bounds__(kBlk) void dp_alloc(const int64_t* __restrict__ slots, int32_t W, int64_t cap,
+                                                 int64_t n_users, const int32_t* __restrict__ reg_cnt,
+                                                 int32_t* __restrict__ start, int32_t* __restrict__ meta) {
+    const int64_t i = (int64_t)blockIdx.x * kBlk + threadIdx.x;
+    if (i >= (int64_t)W * 3 * cap) return;
+    const int64_t x = occ_row(slots, cap, n_users, i);
+    if (x < 0 || atomicCAS(start + x, 0, -1) != 0) return;
+    const int32_t n = reg_cnt[3 * x] + reg_cnt[3 * x + 1] + reg_cnt[3 * x + 2];
+    start[x] = atomicAdd(meta + 2, n) + 1;
+}
+
+// (comm stream) every occurrence takes a place in its row's run
+__global__ __launch_bounds__(kBlk) void dp_scatter(const int64_t* __restrict__ slots, int32_t W, int64_t cap,
+                                                   int64_t n_users, const int32_t* __restrict__ start,
+                                                   int32_t* __restrict__ cursor, int32_t* __restrict__ keys,
+                                                   int32_t* __restrict__ occ) {
+    const int64_t i = (int64_t)blockIdx.x * kBlk + threadIdx.x;
+    if (i >= (int64_t)W * 3 * cap) return;
+    const int64_t x = occ_row(slots, cap, n_users, i);
+    if (x < 0) return;
+    const int32_t p = start[x] - 1 + atomicAdd(cursor + x, 1);
+    keys[p] = (int32_t)x;
+    occ[p] = (int32_t)i;
 }
 
 // Phase A: every triplet of every rank — s+ - s- from the final rows, the BPR term and its
@@ -263,10 +282,15 @@ __global__ __launch_bounds__(kBlk) void dp_bpr_coef(const int64_t* __restrict__ 
     }
 }
 
-// Phase B: G' in fixed point.  Lane group c walks sorted occurrences [c kChunk, (c+1)
-// kChunk): each occurrence's term (bpr_fused's f32 arithmetic: coef (f_p - f_n) / g_div
+// Phase B: G' in fixed point.  Lane group c walks run places [c kChunk, (c+1) kChunk): each occurrence's term (bpr_fused's f32 arithmetic: coef (f_p - f_n) / g_div
 // for a user, +-coef f_u / g_div for an item) scaled by 2^e and rounded to int64, a run of
 // equal rows summed in registers, one 64-bit integer atomic per run and column.
+// The chunk's bookkeeping (sorted key, occurrence -> triplet -> the rows to gather and
+// the coefficient: three dependent loads) is resolved by the group's lanes for all its
+// occurrences at once (lane q holds occurrence q's) and broadcast by shuffles, and the
+// rows of KB occurrences are gathered together before they are added: a lane group
+// walking its occurrences one dependent chain at a time spent ~30 us on 6,144
+// occurrences.
 template <int D>
 __global__ __launch_bounds__(kBlk) void dp_bpr_grad(const int64_t* __restrict__ slots, int64_t cap, int64_t n_users,
                                                     int64_t N, int64_t n_occ, const int32_t* __restrict__ key,
@@ -275,74 +299,119 @@ __global__ __launch_bounds__(kBlk) void dp_bpr_grad(const int64_t* __restrict__ 
                                                     const int32_t* __restrict__ meta,
                                                     unsigned long long* __restrict__ acc) {
     constexpr int G = D / 4, GPB = kBlk / G;
+    constexpr int KP = (kChunk + G - 1) / G;  // occurrences whose bookkeeping one lane holds
+    constexpr int KB = 8;                     // occurrences gathered together
     const int li = threadIdx.x % G;
+    const int gl0 = (threadIdx.x % kWave) - li;  // the group's first lane in the wave
     const int64_t c0 = ((int64_t)blockIdx.x * GPB + threadIdx.x / G) * kChunk;
-    if (c0 >= n_occ) return;
-    const int64_t c1 = c0 + kChunk < n_occ ? c0 + kChunk : n_occ;
+    const int64_t n_pl = meta[2] < n_occ ? meta[2] : n_occ;  // the run places taken this step
+    if (c0 >= n_pl) return;  // group-uniform
     const double S = ldexp(1.0, meta[1]);
     const int64_t L = 3 * cap + 1;
+    // bookkeeping of occurrence q = li + G k of the chunk: its row (N: none), the rows it
+    // gathers (b = -1 when only one) and its signed, scaled coefficient
+    int32_t xq[KP];
+    int64_t aq[KP], bq[KP];
+    float cq[KP];
+#pragma unroll
+    for (int k = 0; k < KP; ++k) {
+        const int q = li + G * k;
+        const int64_t i = c0 + q;
+        xq[k] = (int32_t)N;
+        aq[k] = bq[k] = -1;
+        cq[k] = 0.f;
+        if (q < kChunk && i < n_pl) {
+            const int32_t x = key[i];
+            if (x < N) {
+                const int64_t o = val[i];
+                const int64_t r = o / (3 * cap), j = o - r * 3 * cap, kind = j / cap, t = j - kind * cap;
+                const int64_t* slot = slots + r * L;
+                const float c = coef[r * cap + t];
+                xq[k] = x;
+                if (kind == 0) {
+                    aq[k] = n_users + slot[1 + cap + t];
+                    bq[k] = n_users + slot[1 + 2 * cap + t];
+                    cq[k] = c;
+                } else {
+                    aq[k] = slot[1 + t];
+                    cq[k] = kind == 1 ? c : -c;
+                }
+            }
+        }
+    }
     long long a0 = 0, a1 = 0, a2 = 0, a3 = 0;
     int32_t cur = -1;
-    for (int64_t i = c0; i < c1; ++i) {
-        const int32_t x = key[i];
-        if (x >= N) break;  // padding sorts last
-        if (x != cur) {
-            if (cur >= 0) {
-                unsigned long long* q = acc + (int64_t)cur * D + li * 4;
-                atomicAdd(q + 0, (unsigned long long)a0);
-                atomicAdd(q + 1, (unsigned long long)a1);
-                atomicAdd(q + 2, (unsigned long long)a2);
-                atomicAdd(q + 3, (unsigned long long)a3);
+    auto flush = [&]() __attribute__((always_inline)) {
+        if (cur >= 0) {
+            unsigned long long* q = acc + (int64_t)cur * D + li * 4;
+            atomicAdd(q + 0, (unsigned long long)a0);
+            atomicAdd(q + 1, (unsigned long long)a1);
+            atomicAdd(q + 2, (unsigned long long)a2);
+            atomicAdd(q + 3, (unsigned long long)a3);
+        }
+    };
+#pragma unroll
+    for (int j0 = 0; j0 < kChunk; j0 += KB) {
+        int32_t xs[KB];
+        float cs[KB];
+        bool two[KB];
+        float4 va[KB], vb[KB];
+#pragma unroll
+        for (int u = 0; u < KB; ++u) {
+            const int q = j0 + u, src = gl0 + q % G, k = q / G;
+            xs[u] = __shfl(xq[k], src, kWave);
+            cs[u] = __shfl(cq[k], src, kWave);
+            const int64_t ra = __shfl(aq[k], src, kWave), rb = __shfl(bq[k], src, kWave);
+            two[u] = rb >= 0;
+            va[u] = ra >= 0 ? ld4(fin + ra * D + li * 4) : f4(0.f);
+            vb[u] = rb >= 0 ? ld4(fin + rb * D + li * 4) : f4(0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < KB; ++u) {
+            const int32_t x = xs[u];
+            if (x >= N) break;  // past the places taken (group-uniform)
+            if (x != cur) {
+                flush();
+                cur = x;
+                a0 = a1 = a2 = a3 = 0;
             }
-            cur = x;
-            a0 = a1 = a2 = a3 = 0;
+            const float c = cs[u];
+            float4 g;
+            if (two[u]) {
+                g = make_float4(c * (va[u].x - vb[u].x), c * (va[u].y - vb[u].y), c * (va[u].z - vb[u].z),
+                                c * (va[u].w - vb[u].w));
+            } else {
+                g = make_float4(c * va[u].x, c * va[u].y, c * va[u].z, c * va[u].w);
+            }
+            if (g_div != 1.f) {
+                g.x /= g_div;
+                g.y /= g_div;
+                g.z /= g_div;
+                g.w /= g_div;
+            }
+            a0 += llrint((double)g.x * S);
+            a1 += llrint((double)g.y * S);
+            a2 += llrint((double)g.z * S);
+            a3 += llrint((double)g.w * S);
         }
-        const int64_t o = val[i];
-        const int64_t r = o / (3 * cap), j = o - r * 3 * cap, kind = j / cap, t = j - kind * cap;
-        const int64_t* slot = slots + r * L;
-        const float c = coef[r * cap + t];
-        float4 g;
-        if (kind == 0) {
-            const float4 fp = ld4(fin + (n_users + slot[1 + cap + t]) * D + li * 4);
-            const float4 fn = ld4(fin + (n_users + slot[1 + 2 * cap + t]) * D + li * 4);
-            g = make_float4(c * (fp.x - fn.x), c * (fp.y - fn.y), c * (fp.z - fn.z), c * (fp.w - fn.w));
-        } else {
-            const float4 fu = ld4(fin + slot[1 + t] * D + li * 4);
-            const float cc = kind == 1 ? c : -c;
-            g = make_float4(cc * fu.x, cc * fu.y, cc * fu.z, cc * fu.w);
-        }
-        if (g_div != 1.f) {
-            g.x /= g_div;
-            g.y /= g_div;
-            g.z /= g_div;
-            g.w /= g_div;
-        }
-        a0 += llrint((double)g.x * S);
-        a1 += llrint((double)g.y * S);
-        a2 += llrint((double)g.z * S);
-        a3 += llrint((double)g.w * S);
     }
-    if (cur >= 0) {
-        unsigned long long* q = acc + (int64_t)cur * D + li * 4;
-        atomicAdd(q + 0, (unsigned long long)a0);
-        atomicAdd(q + 1, (unsigned long long)a1);
-        atomicAdd(q + 2, (unsigned long long)a2);
-        atomicAdd(q + 3, (unsigned long long)a3);
-    }
+    flush();
 }
 
-// Phase C: every union row once (the first of its run in the sorted keys): G'[x] = its
-// accumulator / 2^e rounded to f32, the accumulator cleared for the next step.
+// Phase C: every union row once (the first place of its run): G'[x] = its accumulator /
+// 2^e rounded to f32; the accumulator, the run's start and cursor cleared for the next step.
 template <int D>
-__global__ __launch_bounds__(kBlk) void dp_bpr_round(int64_t N, int64_t n_occ, const int32_t* __restrict__ key,
+__global__ __launch_bounds__(kBlk) void dp_bpr_round(int64_t n_occ, const int32_t* __restrict__ key,
+                                                     int32_t* __restrict__ start, int32_t* __restrict__ cursor,
                                                      const int32_t* __restrict__ meta,
                                                      unsigned long long* __restrict__ acc, float* __restrict__ g) {
     constexpr int G = D / 4, GPB = kBlk / G;
     const int li = threadIdx.x % G;
     const int64_t i = (int64_t)blockIdx.x * GPB + threadIdx.x / G;
-    if (i >= n_occ) return;
+    const int64_t n_pl = meta[2] < n_occ ? meta[2] : n_occ;
+    if (i >= n_pl) return;
     const int32_t x = key[i];
-    if (x >= N || (i > 0 && key[i - 1] == x)) return;
+    if (start[x] - 1 != i) return;  // (a first place clears start[x] below: the others then see 0)
     const double inv = ldexp(1.0, -meta[1]);
     unsigned long long* q = acc + (int64_t)x * D + li * 4;
     float4 v;
@@ -355,6 +424,10 @@ __global__ __launch_bounds__(kBlk) void dp_bpr_round(int64_t N, int64_t n_occ, c
     q[2] = 0ull;
     q[3] = 0ull;
     st4(g + (int64_t)x * D + li * 4, v);
+    if (li == 0) {
+        start[x] = 0;
+        cursor[x] = 0;
+    }
 }
 
 rsx_epilogue epi(int kind) {
@@ -384,10 +457,10 @@ int dp_loss_kernels(const rsx_dp_lgcn_step& st, const Work& w, int32_t W, hipStr
     DP_TRY(last_rc());
     const int64_t n_chunks = (n_occ + kChunk - 1) / kChunk;
     hipLaunchKernelGGL((dp_bpr_grad<D>), dim3((unsigned)((n_chunks + GPB - 1) / GPB)), dim3(kBlk), 0, s, st.slots,
-                       cap, nu, N, n_occ, w.kb, w.vb, st.final_emb, w.coef, g_div, w.meta, w.acc);
+                       cap, nu, N, n_occ, w.keys, w.occ, st.final_emb, w.coef, g_div, w.meta, w.acc);
     DP_TRY(last_rc());
-    hipLaunchKernelGGL((dp_bpr_round<D>), dim3((unsigned)((n_occ + GPB - 1) / GPB)), dim3(kBlk), 0, s, N, n_occ, w.kb,
-                       w.meta, w.acc, st.g);
+    hipLaunchKernelGGL((dp_bpr_round<D>), dim3((unsigned)((n_occ + GPB - 1) / GPB)), dim3(kBlk), 0, s, n_occ, w.keys,
+                       w.start, w.cursor, w.meta, w.acc, st.g);
     return last_rc();
 }
 
@@ -408,29 +481,24 @@ int dp_step(const rsx_dp_lgcn_step& st, hipStream_t s) {
     if (w.total > st.work_bytes) return RSX_ERR_WORKSPACE;
     int rc = 0;
     // (1) this rank's triplets into its slot; every rank's gathered while the forward runs,
-    // then indexed (union tags, global counts) and sorted by row, on the comm stream
+    // then indexed (union tags, global counts) and bucketed by row, on the comm stream
     hipLaunchKernelGGL(dp_pack, dim3((unsigned)((L + kBlk - 1) / kBlk)), dim3(kBlk), 0, s, st.triplets, B, cap,
-                       st.slots + rank * L, st.inc_step ? const_cast<int64_t*>(st.adam.step_dev) : nullptr);
+                       st.slots + rank * L, st.inc_step ? const_cast<int64_t*>(st.adam.step_dev) : nullptr, w.meta);
     DP_TRY(last_rc());
     if (!collective(st.comm, RSX_COLL_ALLGATHER, st.slots, L * ag, RSX_COLL_I64, s, &rc)) return rc;
     hipStream_t cs = comm_stream(st.comm, s);
-    hipLaunchKernelGGL(dp_index, dim3((unsigned)((n_occ + kBlk - 1) / kBlk)), dim3(kBlk), 0, cs, st.slots, W, cap, nu,
-                       N, st.row_tag, st.reg_cnt, st.tag_dev, w.ka, w.va);
+    const dim3 go((unsigned)((n_occ + kBlk - 1) / kBlk));
+    hipLaunchKernelGGL(dp_index, go, dim3(kBlk), 0, cs, st.slots, W, cap, nu, st.row_tag, st.reg_cnt, st.tag_dev);
     DP_TRY(last_rc());
     hipEvent_t j_idx = nullptr, j_sort = nullptr;
     if (cs != s) {
         j_idx = comm_event(st.comm);
         DP_TRY(hip_rc(hipEventRecord(j_idx, cs)));
     }
-    {
-        hipcub::DoubleBuffer<int32_t> k(w.ka, w.kb), v(w.va, w.vb);
-        size_t tb = w.temp_bytes;
-        DP_TRY(hip_rc(hipcub::DeviceRadixSort::SortPairs(w.temp, tb, k, v, (int)n_occ, 0, key_bits(N), cs)));
-        // the sorted run lands in kb / vb or back in ka / va (the pass count is fixed per
-        // key width): the later kernels read whichever the selector names
-        w.kb = k.Current();
-        w.vb = v.Current();
-    }
+    hipLaunchKernelGGL(dp_alloc, go, dim3(kBlk), 0, cs, st.slots, W, cap, nu, st.reg_cnt, w.start, w.meta);
+    DP_TRY(last_rc());
+    hipLaunchKernelGGL(dp_scatter, go, dim3(kBlk), 0, cs, st.slots, W, cap, nu, w.start, w.cursor, w.keys, w.occ);
+    DP_TRY(last_rc());
     if (cs != s) {
         j_sort = comm_event(st.comm);
         DP_TRY(hip_rc(hipEventRecord(j_sort, cs)));

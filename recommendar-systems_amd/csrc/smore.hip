@@ -335,29 +335,59 @@ __device__ __forceinline__ void load_rows(const float* __restrict__ x, int64_t i
 // (fwd table; two signals) or irfft^T of a gradient (inv table; one signal).  F[t]
 // (t < MT): lane (g, n) holds rows 16t + 4g + i, i.e. the (Re, Im) of bins 8t + 2g and
 // 8t + 2g + 1 of item n
-template <int D, int NS>
+template <int D, int NS, int T0 = 0, int NT = Spec<D>::MT>
 __device__ __forceinline__ void ks_product(const float4* __restrict__ tab, const float (*x[NS])[Spec<D>::SI],
-                                           floatx4 (*acc[NS])[Spec<D>::MT], int lane) {
-    constexpr int MT = Spec<D>::MT, Q = Tab<D>::Q;
+                                           floatx4 (*acc[NS])[NT], int lane) {
+    constexpr int Q = Tab<D>::Q;  // (tiles T0 .. T0 + NT - 1 of the spectrum only)
 #pragma unroll
     for (int k = 0; k < NS; ++k)
 #pragma unroll
-        for (int t = 0; t < MT; ++t) (*acc[k])[t] = floatx4{0.f, 0.f, 0.f, 0.f};
-    float4 c[MT];
+        for (int t = 0; t < NT; ++t) (*acc[k])[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+    float4 c[NT];
 #pragma unroll
-    for (int t = 0; t < MT; ++t) c[t] = f4(0.f);
+    for (int t = 0; t < NT; ++t) c[t] = f4(0.f);
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
         tie(c);
         const int base = opaque(lane);
 #pragma unroll
-        for (int t = 0; t < MT; ++t) c[t] = ks_at<D>(tab, base, t, q, lane);
+        for (int t = 0; t < NT; ++t) c[t] = ks_at<D>(tab, base, T0 + t, q, lane);
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll
-            for (int t = 0; t < MT; ++t)
+            for (int t = 0; t < NT; ++t)
 #pragma unroll
                 for (int k = 0; k < NS; ++k) (*acc[k])[t] = mfma16(f4c(c[t], r), (*x[k])[4 * q + r], (*acc[k])[t]);
+    }
+}
+
+// ks_product for one signal read straight from its rows [n, D] (the B operand of step
+// 4q + r is x[g SI + 4q + r]: one float4 per step group, the next group's in flight)
+// instead of a register copy of the whole row slice: SI - 8 fewer live registers
+template <int D, int T0, int NT>
+__device__ __forceinline__ void ks_product_rows(const float4* __restrict__ tab, const float* __restrict__ x,
+                                                int64_t item, bool ok, int g, floatx4 (&acc)[NT], int lane) {
+    constexpr int Q = Tab<D>::Q, SI = Spec<D>::SI;
+    const float* p = x + (ok ? item : 0) * D + g * SI;
+    const bool ld = ok && x;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+    float4 c[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) c[t] = f4(0.f);
+    float4 xv = ld ? ld4(p) : f4(0.f);
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        tie(c);
+        const int base = opaque(lane);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) c[t] = ks_at<D>(tab, base, T0 + t, q, lane);
+        const float4 xn = (ld && q + 1 < Q) ? ld4(p + 4 * (q + 1)) : f4(0.f);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int t = 0; t < NT; ++t) acc[t] = mfma16(f4c(c[t], r), f4c(xv, r), acc[t]);
+        xv = xn;
     }
 }
 
@@ -544,10 +574,97 @@ __device__ __forceinline__ int64_t dfreq_off(int64_t gwave, int sig, int t, int 
 template <int D>
 constexpr int kBwdFreqLds = Tab<D>::kFloats + 2 * D;
 
-template <int D>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void smore_spec_bwd_freq(SpecBwdArgs a) {
+// The frequency pass of 16 items on spectrum tiles T0 .. T0 + NT - 1 (one wave; the two
+// halves of a block's 8 waves take the two tile ranges of the same items: twice the
+// waves, each half the MFMA chain and registers)
+template <int D, int T0, int NT>
+__device__ __forceinline__ void freq_tiles(const SpecBwdArgs& a, const float4* __restrict__ tab,
+                                           const float2 (*ws)[Spec<D>::NB], float2 (*dws)[Spec<D>::NB],
+                                           int64_t gwave, int lane) {
     using S = Spec<D>;
     constexpr int MT = S::MT, NB = S::NB, SI = S::SI;
+    const int n16 = lane & 15, g = lane >> 4;
+    const int64_t item = gwave * 16 + n16;
+    const bool iv = item < a.n;
+    // the forward's spectra of tile t (lane (g, n): bins 8t + 2g, 8t + 2g + 1 of item n)
+    auto spec4 = [&](int sig, int t) __attribute__((always_inline)) {
+        const float4 v = iv ? ld4(a.spec + spec_off<D>(item, sig, t, g)) : f4(0.f);
+        return floatx4{v.x, v.y, v.z, v.w};
+    };
+    // d w of bin b (summed over the wave's 16 items) into dws[m][b]
+    auto put_dw = [&](int m, int b, bool bv, float2 dw) __attribute__((always_inline)) {
+        dw.x = sum16(dw.x);
+        dw.y = sum16(dw.y);
+        if (n16 == 0 && bv) dws[m][b] = dw;
+    };
+    auto store_df = [&](int sig, const floatx4 (&v)[NT]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+            st4(a.dfreq + dfreq_off<D>(gwave, sig, T0 + t, lane), make_float4(v[t][0], v[t][1], v[t][2], v[t][3]));
+    };
+    // dY = irfft^T(d conv_m) for the 16 items, in the spectrum layout
+    auto irfft_t = [&](int m, floatx4 (&dy)[NT]) __attribute__((always_inline)) {
+        ks_product_rows<D, T0, NT>(tab, a.g[m], item, iv, g, dy, lane);
+    };
+    floatx4 dy[NT], dp[NT];
+    irfft_t(2, dy);
+#pragma unroll
+    for (int u = 0; u < NT; ++u) {
+        const int t = T0 + u;
+        const floatx4 fi4 = spec4(0, t), ft4 = spec4(1, t);
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            const int b = 8 * t + 2 * g + p;
+            const bool bv = b < NB;
+            const float2 dY = pair(dy[u], p);
+            put_dw(2, b, bv, cmulc(dY, cmul(pair(ft4, p), pair(fi4, p))));
+            set_pair(dp[u], p, bv ? cmulc(dY, ws[2][bv ? b : 0]) : make_float2(0.f, 0.f));
+        }
+    }
+    // image: dFi = dYv conj(wv) + dp conj(Ft)
+    irfft_t(0, dy);
+#pragma unroll
+    for (int u = 0; u < NT; ++u) {
+        const int t = T0 + u;
+        const floatx4 fi4 = spec4(0, t), ft4 = spec4(1, t);
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            const int b = 8 * t + 2 * g + p;
+            const bool bv = b < NB;
+            const float2 dY = pair(dy[u], p);
+            put_dw(0, b, bv, cmulc(dY, pair(fi4, p)));
+            const float2 uu = bv ? cmulc(dY, ws[0][bv ? b : 0]) : make_float2(0.f, 0.f);
+            const float2 v = cmulc(pair(dp[u], p), pair(ft4, p));
+            set_pair(dy[u], p, make_float2(uu.x + v.x, uu.y + v.y));
+        }
+    }
+    store_df(0, dy);
+    // text: dFt = dYt conj(wt) + dp conj(Fi)
+    irfft_t(1, dy);
+#pragma unroll
+    for (int u = 0; u < NT; ++u) {
+        const int t = T0 + u;
+        const floatx4 fi4 = spec4(0, t), ft4 = spec4(1, t);
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            const int b = 8 * t + 2 * g + p;
+            const bool bv = b < NB;
+            const float2 dY = pair(dy[u], p);
+            put_dw(1, b, bv, cmulc(dY, pair(ft4, p)));
+            const float2 uu = bv ? cmulc(dY, ws[1][bv ? b : 0]) : make_float2(0.f, 0.f);
+            const float2 v = cmulc(pair(dp[u], p), pair(fi4, p));
+            set_pair(dy[u], p, make_float2(uu.x + v.x, uu.y + v.y));
+        }
+    }
+    store_df(1, dy);
+    (void)MT;
+    (void)SI;
+}
+
+template <int D>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void smore_spec_bwd_freq(SpecBwdArgs a) {
+    using S = Spec<D>;
+    constexpr int MT = S::MT, NB = S::NB, MTA = (MT + 1) / 2;
     __shared__ __attribute__((aligned(16))) float lds[kBwdFreqLds<D>];
     __shared__ float2 ws[3][NB];
     __shared__ float2 dws[4][3][NB];
@@ -559,84 +676,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void s
     tab_ks<D>(reinterpret_cast<float4*>(lds), [&](int j, int f) { return inv_coef<D>(f, j, tw); });
     __syncthreads();
     const float4* tab = reinterpret_cast<const float4*>(lds);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, n16 = lane & 15, g = lane >> 4;
-    const int64_t gwave = (int64_t)blockIdx.x * 4 + wave;
-    const int64_t item = gwave * 16 + n16;
-    const bool iv = item < a.n;
-    // the forward's spectra of tile t (lane (g, n): bins 8t + 2g, 8t + 2g + 1 of item n)
-    auto spec4 = [&](int sig, int t) __attribute__((always_inline)) {
-        const float4 v = iv ? ld4(a.spec + spec_off<D>(item, sig, t, g)) : f4(0.f);
-        return floatx4{v.x, v.y, v.z, v.w};
-    };
-    // d w of bin b (summed over the wave's 16 items) into dws[wave][m][b]
-    auto put_dw = [&](int m, int b, bool bv, float2 dw) __attribute__((always_inline)) {
-        dw.x = sum16(dw.x);
-        dw.y = sum16(dw.y);
-        if (n16 == 0 && bv) dws[wave][m][b] = dw;
-    };
-    auto store_df = [&](int sig, const floatx4 (&v)[MT]) __attribute__((always_inline)) {
-#pragma unroll
-        for (int t = 0; t < MT; ++t)
-            st4(a.dfreq + dfreq_off<D>(gwave, sig, t, lane), make_float4(v[t][0], v[t][1], v[t][2], v[t][3]));
-    };
-    // dY = irfft^T(d conv_m) for the 16 items, in the spectrum layout
-    auto irfft_t = [&](int m, floatx4 (&dy)[MT]) __attribute__((always_inline)) {
-        float gin[SI];
-        load_rows<D>(a.g[m], item, iv, g, gin);
-        const float (*xs[1])[SI] = {&gin};
-        floatx4 (*accs[1])[MT] = {&dy};
-        ks_product<D, 1>(tab, xs, accs, lane);
-    };
-    floatx4 dy[MT], dp[MT];
-    irfft_t(2, dy);
-#pragma unroll
-    for (int t = 0; t < MT; ++t) {
-        const floatx4 fi4 = spec4(0, t), ft4 = spec4(1, t);
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
-            const int b = 8 * t + 2 * g + p;
-            const bool bv = b < NB;
-            const float2 dY = pair(dy[t], p);
-            put_dw(2, b, bv, cmulc(dY, cmul(pair(ft4, p), pair(fi4, p))));
-            set_pair(dp[t], p, bv ? cmulc(dY, ws[2][bv ? b : 0]) : make_float2(0.f, 0.f));
-        }
-    }
-    // image: dFi = dYv conj(wv) + dp conj(Ft)
-    irfft_t(0, dy);
-#pragma unroll
-    for (int t = 0; t < MT; ++t) {
-        const floatx4 fi4 = spec4(0, t), ft4 = spec4(1, t);
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
-            const int b = 8 * t + 2 * g + p;
-            const bool bv = b < NB;
-            const float2 dY = pair(dy[t], p);
-            put_dw(0, b, bv, cmulc(dY, pair(fi4, p)));
-            const float2 u = bv ? cmulc(dY, ws[0][bv ? b : 0]) : make_float2(0.f, 0.f);
-            const float2 v = cmulc(pair(dp[t], p), pair(ft4, p));
-            set_pair(dy[t], p, make_float2(u.x + v.x, u.y + v.y));
-        }
-    }
-    store_df(0, dy);
-    // text: dFt = dYt conj(wt) + dp conj(Fi)
-    irfft_t(1, dy);
-#pragma unroll
-    for (int t = 0; t < MT; ++t) {
-        const floatx4 fi4 = spec4(0, t), ft4 = spec4(1, t);
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
-            const int b = 8 * t + 2 * g + p;
-            const bool bv = b < NB;
-            const float2 dY = pair(dy[t], p);
-            put_dw(1, b, bv, cmulc(dY, pair(ft4, p)));
-            const float2 u = bv ? cmulc(dY, ws[1][bv ? b : 0]) : make_float2(0.f, 0.f);
-            const float2 v = cmulc(pair(dp[t], p), pair(fi4, p));
-            set_pair(dy[t], p, make_float2(u.x + v.x, u.y + v.y));
-        }
-    }
-    store_df(1, dy);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, ig = wave & 3;
+    const int64_t gwave = (int64_t)blockIdx.x * 4 + ig;
+    if (wave < 4)  // wave-uniform: tiles 0 .. MTA-1, then MTA .. MT-1, of the same 16 items
+        freq_tiles<D, 0, MTA>(a, tab, ws, dws[ig], gwave, lane);
+    else
+        freq_tiles<D, MTA, MT - MTA>(a, tab, ws, dws[ig], gwave, lane);
     __syncthreads();
-    // per-block d weight partial, waves added in order (deterministic)
+    // per-block d weight partial, the four item groups added in order (deterministic; a
+    // bin's dws entry comes from the one wave whose tiles hold it)
     for (int e = threadIdx.x; e < 3 * NB * 2; e += blockDim.x) {
         const int m = e / (2 * NB), k = (e / 2) % NB, c = e & 1;
         const float2 w0 = dws[0][m][k], w1 = dws[1][m][k], w2 = dws[2][m][k], w3 = dws[3][m][k];
@@ -646,8 +694,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void s
 }
 
 template <int D>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void smore_spec_bwd_feat(SpecBwdArgs a) {
-    constexpr int MT = Spec<D>::MT, OT = Spec<D>::OT;
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void smore_spec_bwd_feat(SpecBwdArgs a) {
+    constexpr int MT = Spec<D>::MT, OT = Spec<D>::OT, HT = OT / 2;  // output tiles per half
     __shared__ __attribute__((aligned(16))) float lds[kBwdFreqLds<D>];
     float* tw = lds + Tab<D>::kFloats;
     twiddles<D>(tw);
@@ -656,7 +704,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void s
     __syncthreads();
     const float4* tab = reinterpret_cast<const float4*>(lds);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, n16 = lane & 15, g = lane >> 4;
-    const int64_t gwave = (int64_t)blockIdx.x * 4 + wave;
+    const int ig = wave & 3, h = wave >> 2;  // item group, half of the output tiles
+    const int64_t gwave = (int64_t)blockIdx.x * 4 + ig;
     const int64_t item = gwave * 16 + n16;
     const bool iv = item < a.n;
 #pragma unroll 1
@@ -670,7 +719,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void s
         // d x = rfft^T(dF): output tiles in pairs (two independent accumulators), step
         // (t, i) <-> spectrum row 16t + 4g + i
 #pragma unroll 1
-        for (int tau = 0; tau < OT; tau += 2) {  // rolled: bounds the live coefficients to one pair of tiles
+        for (int tau = h * HT; tau < (h + 1) * HT; tau += 2) {  // rolled: one pair's coefficients live
             floatx4 a0{0.f, 0.f, 0.f, 0.f}, a1 = a0;
             float4 c[2] = {f4(0.f), f4(0.f)};
 #pragma unroll
@@ -942,11 +991,11 @@ extern "C" int rsx_smore_spectral_bwd(const float* spec, const float* wv, const 
     const dim3 g((unsigned)((n_items + 63) / 64));
     hipStream_t s = as_stream(stream);
     if (d == 64) {
-        hipLaunchKernelGGL(smore_spec_bwd_freq<64>, g, dim3(256), 0, s, a);
-        hipLaunchKernelGGL(smore_spec_bwd_feat<64>, g, dim3(256), 0, s, a);
+        hipLaunchKernelGGL(smore_spec_bwd_freq<64>, g, dim3(512), 0, s, a);
+        hipLaunchKernelGGL(smore_spec_bwd_feat<64>, g, dim3(512), 0, s, a);
     } else {
-        hipLaunchKernelGGL(smore_spec_bwd_freq<128>, g, dim3(256), 0, s, a);
-        hipLaunchKernelGGL(smore_spec_bwd_feat<128>, g, dim3(256), 0, s, a);
+        hipLaunchKernelGGL(smore_spec_bwd_freq<128>, g, dim3(512), 0, s, a);
+        hipLaunchKernelGGL(smore_spec_bwd_feat<128>, g, dim3(512), 0, s, a);
     }
     return last_rc();
 }

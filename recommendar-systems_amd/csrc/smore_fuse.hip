@@ -1089,21 +1089,30 @@ __global__ __launch_bounds__(64 * kNceWaves) void nce_bwd(NceArgs a) {
 // The same products in the same K grouping and order as nce_bwd; the waves' partials are
 // summed in wave order through LDS (transposed back to the row layout) and the epilogue
 // is nce_bwd's.
-template <int D>
+template <int D, int NG>
 __global__ __launch_bounds__(64 * kNceWaves) void nce_bwd_t(NceArgs a) {
+    // NG own 16-row groups per block: every other-view tile a wave loads feeds NG groups'
+    // MFMAs (NG = 2 halves the L2 reads of the other view's tiles; same K split over the
+    // waves, same order, so the results are NG = 1's bit for bit)
     constexpr int T = D / 16;
     __shared__ __attribute__((aligned(16))) float red[kNceWaves][16][D];
     const int term = blockIdx.z, mode = blockIdx.y;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
     const int64_t B = a.B;
-    const int64_t n0 = (int64_t)blockIdx.x * 16;
-    const int64_t bo = n0 + c < B ? n0 + c : -1;
+    int64_t bo[NG];
+#pragma unroll
+    for (int h = 0; h < NG; ++h) {
+        const int64_t n0 = ((int64_t)blockIdx.x * NG + h) * 16;
+        bo[h] = n0 + c < B ? n0 + c : -1;
+    }
     const int64_t ntile = (B + 15) / 16;
     const float* own_n = a.nrm + ((int64_t)(term * 2 + mode) * B) * D;
     const float* oth_n = a.nrm + ((int64_t)(term * 2 + (mode ^ 1)) * B) * D;
     const float* othT = a.nrmT + ((int64_t)(term * 2 + (mode ^ 1)) * ntile) * D * 16 + c * 16 + 4 * g;
     const float* ttl = a.ttl + term * B;
-    const float ttl_own = (mode == 0 && bo >= 0) ? ttl[bo] : 1.f;
+    float ttl_own[NG];
+#pragma unroll
+    for (int h = 0; h < NG; ++h) ttl_own[h] = (mode == 0 && bo[h] >= 0) ? ttl[bo[h]] : 1.f;
     const float* eb = a.E + (int64_t)term * B * B;
     auto ttl_of = [&](int64_t mt) {
         floatx4 t = {1.f, 1.f, 1.f, 1.f};
@@ -1115,12 +1124,12 @@ __global__ __launch_bounds__(64 * kNceWaves) void nce_bwd_t(NceArgs a) {
             }
         return t;
     };
-    auto e_of = [&](int64_t mt) {
+    auto e_of = [&](int64_t mt, int64_t own) {
         floatx4 ev = {0.f, 0.f, 0.f, 0.f};
-        if (bo < 0 || mt >= ntile) return ev;
+        if (own < 0 || mt >= ntile) return ev;
         const int64_t m0 = mt * 16 + 4 * g;
         if (mode == 0) {
-            const float* er = eb + bo * B + m0;
+            const float* er = eb + own * B + m0;
             if ((B & 3) == 0 && m0 + 3 < B) {
                 ev = *reinterpret_cast<const floatx4*>(er);
             } else {
@@ -1129,7 +1138,7 @@ __global__ __launch_bounds__(64 * kNceWaves) void nce_bwd_t(NceArgs a) {
             }
         } else {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) ev[r] = m0 + r < B ? eb[(m0 + r) * B + bo] : 0.f;
+            for (int r = 0; r < 4; ++r) ev[r] = m0 + r < B ? eb[(m0 + r) * B + own] : 0.f;
         }
         return ev;
     };
@@ -1139,52 +1148,72 @@ __global__ __launch_bounds__(64 * kNceWaves) void nce_bwd_t(NceArgs a) {
             y[tk] = mt < ntile ? *reinterpret_cast<const floatx4*>(othT + (mt * D + 16 * tk) * 16)
                                : floatx4{0.f, 0.f, 0.f, 0.f};
     };
-    floatx4 O[T];
+    floatx4 O[NG][T];
 #pragma unroll
-    for (int tk = 0; tk < T; ++tk) O[tk] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int h = 0; h < NG; ++h)
+#pragma unroll
+        for (int tk = 0; tk < T; ++tk) O[h][tk] = floatx4{0.f, 0.f, 0.f, 0.f};
     floatx4 Y[T];
     y_of(w, Y);
     floatx4 tv = ttl_of(w);
-    floatx4 ev = e_of(w);
+    floatx4 ev[NG];
+#pragma unroll
+    for (int h = 0; h < NG; ++h) ev[h] = e_of(w, bo[h]);
     for (int64_t mt = w; mt < ntile; mt += kNceWaves) {
         floatx4 Yn[T];
         y_of(mt + kNceWaves, Yn);  // the next tile, in flight
         const floatx4 tvn = ttl_of(mt + kNceWaves);
-        const floatx4 evn = e_of(mt + kNceWaves);
+        floatx4 evn[NG];
+#pragma unroll
+        for (int h = 0; h < NG; ++h) evn[h] = e_of(mt + kNceWaves, bo[h]);
         const int64_t m0 = mt * 16;
-        floatx4 p;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) p[r] = (bo >= 0 && m0 + 4 * g + r < B) ? ev[r] / (mode == 0 ? ttl_own : tv[r]) : 0.f;
+        for (int h = 0; h < NG; ++h) {
+            floatx4 p;
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
+            for (int r = 0; r < 4; ++r)
+                p[r] = (bo[h] >= 0 && m0 + 4 * g + r < B) ? ev[h][r] / (mode == 0 ? ttl_own[h] : tv[r]) : 0.f;
 #pragma unroll
-            for (int tk = 0; tk < T; ++tk) O[tk] = mfma4(p[r], Y[tk][r], O[tk]);
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int tk = 0; tk < T; ++tk) O[h][tk] = mfma4(p[r], Y[tk][r], O[h][tk]);
+        }
 #pragma unroll
         for (int tk = 0; tk < T; ++tk) Y[tk] = Yn[tk];
         tv = tvn;
-        ev = evn;
+#pragma unroll
+        for (int h = 0; h < NG; ++h) ev[h] = evn[h];
     }
-    // lane (c, g) holds O[own 4g + q][feature 16 tk + c]
-#pragma unroll
-    for (int tk = 0; tk < T; ++tk)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) red[w][4 * g + q][16 * tk + c] = O[tk][q];
-    __syncthreads();
-    if (w != 0) return;
+    // the waves' partials summed in wave order, one group at a time through `red`; wave h
+    // finishes group h
     Fld<D> S;
 #pragma unroll
-    for (int t = 0; t < T; ++t) {
-        floatx4 s = *reinterpret_cast<const floatx4*>(&red[0][c][16 * t + 4 * g]);
+    for (int h = 0; h < NG; ++h) {
+        if (h) __syncthreads();  // wave h - 1 has read the previous group
+        // lane (c, g) holds O[own 4g + q][feature 16 tk + c]
 #pragma unroll
-        for (int i = 1; i < kNceWaves; ++i) s += *reinterpret_cast<const floatx4*>(&red[i][c][16 * t + 4 * g]);
-        S.f[t] = s;
+        for (int tk = 0; tk < T; ++tk)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) red[w][4 * g + q][16 * tk + c] = O[h][tk][q];
+        __syncthreads();
+        if (w == h) {
+#pragma unroll
+            for (int t = 0; t < T; ++t) {
+                floatx4 s = *reinterpret_cast<const floatx4*>(&red[0][c][16 * t + 4 * g]);
+#pragma unroll
+                for (int i = 1; i < kNceWaves; ++i) s += *reinterpret_cast<const floatx4*>(&red[i][c][16 * t + 4 * g]);
+                S.f[t] = s;
+            }
+        }
     }
-    if (bo < 0) return;
-    const Fld<D> X = fload<D>(own_n, bo, g);
+    if (w >= NG) return;
+    const int64_t own = bo[w];
+    if (own < 0) return;
+    const Fld<D> X = fload<D>(own_n, own, g);
     const float coef = (a.gloss[term * a.gstride] * a.gscale) * (1.f / a.tau) / (float)B;
-    const Fld<D> Z = fload<D>(oth_n, bo, g);  // the own row's other view
+    const Fld<D> Z = fload<D>(oth_n, own, g);  // the own row's other view
     const Fld<D> dn = fmap2<D>(S, Z, [&](float o, float z) { return coef * (o - z); });
-    const float nx = a.norms[(term * 2 + mode) * B + bo];
+    const float nx = a.norms[(term * 2 + mode) * B + own];
     Fld<D> dv;
     if (nx > 1e-12f) {
         const float yd = rsum<D>(fmap2<D>(X, dn, [](float u, float v) { return u * v; }));
@@ -1192,7 +1221,7 @@ __global__ __launch_bounds__(64 * kNceWaves) void nce_bwd_t(NceArgs a) {
     } else {
         dv = fmap<D>(dn, [](float u) { return u / 1e-12f; });
     }
-    float* dst = (mode == 0 ? a.g1 : a.g2) + (a.idx[term][bo] + a.off[term]) * D;
+    float* dst = (mode == 0 ? a.g1 : a.g2) + (a.idx[term][own] + a.off[term]) * D;
 #pragma unroll
     for (int t = 0; t < T; ++t)
 #pragma unroll
@@ -1823,7 +1852,13 @@ int rsx_smore_infonce_bwd_scaled(const float* side, const float* content, const 
     const dim3 grid((unsigned)((batch + 15) / 16), 2, 2);
     if (a.E && d == 128) {  // the forward's exp tiles and transposed rows (same workspace, same batch);
         // d = 64 stays on nce_bwd (the transposed-tile form measured no faster there: 95-141 vs 88 us)
-        hipLaunchKernelGGL(sf::nce_bwd_t<128>, grid, dim3(64 * sf::kNceWaves), 0, s, a);
+        static const int ng = env_knob("RSX_NCE_GROUPS", 2, 1, 2);
+        if (ng == 2) {
+            const dim3 g2((unsigned)((batch + 31) / 32), 2, 2);
+            hipLaunchKernelGGL((sf::nce_bwd_t<128, 2>), g2, dim3(64 * sf::kNceWaves), 0, s, a);
+        } else {
+            hipLaunchKernelGGL((sf::nce_bwd_t<128, 1>), grid, dim3(64 * sf::kNceWaves), 0, s, a);
+        }
     } else {
         if (d == 64) hipLaunchKernelGGL(sf::nce_bwd<64>, grid, dim3(64 * sf::kNceWaves), 0, s, a);
         else hipLaunchKernelGGL(sf::nce_bwd<128>, grid, dim3(64 * sf::kNceWaves), 0, s, a);

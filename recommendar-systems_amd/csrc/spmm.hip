@@ -406,6 +406,7 @@ __device__ __forceinline__ void spmm_item(const rsx_csr& a, const float* __restr
         if (e.row_tag[r] != tag_of(e)) return;
     }
     const bool sparse_x = tf & RSX_TAG_SPARSE_X;
+    const int32_t* __restrict__ xtag = e.x_tag ? e.x_tag : e.row_tag;
     EpiIn pre;
     if (wk.y < 0) {
         pre = epi_load<KIND, D>(e, wk.x, li);
@@ -437,7 +438,7 @@ __device__ __forceinline__ void spmm_item(const rsx_csr& a, const float* __restr
                 cm = mine ? col[j + li] : 0;
                 vm = mine ? val[j + li] : 0.f;
             }
-            if (sparse_x && mine && e.row_tag[cm] != tag_of(e)) cm = -1;  // zero X row: no gather
+            if (sparse_x && mine && xtag[cm] != tag_of(e)) cm = -1;  // zero X row: no gather
             const int n = end - j;
 #if RSX_SPMM_G16
             acc = gather16(acc, cm, vm, n, xl);
@@ -479,7 +480,7 @@ __device__ __forceinline__ void spmm_item(const rsx_csr& a, const float* __restr
             const bool mine = j + q < end;
             int cm = mine ? col[j + q] : 0;
             const float vm = mine ? val[j + q] : 0.f;
-            if (sparse_x && mine && e.row_tag[cm] != tag_of(e)) cm = -1;  // zero X row: no gather
+            if (sparse_x && mine && xtag[cm] != tag_of(e)) cm = -1;  // zero X row: no gather
             const int n = end - j;
             acc = gather8<0, D>(acc, cm, vm, n, xl);
             if (n > 8) acc = gather8<1, D>(acc, cm, vm, n, xl);
@@ -496,7 +497,7 @@ __device__ __forceinline__ void spmm_item(const rsx_csr& a, const float* __restr
             if (sparse_x) {
 #pragma unroll
                 for (int t = 0; t < kUnroll; ++t)
-                    if (e.row_tag[c[t]] != tag_of(e)) c[t] = -1;
+                    if (xtag[c[t]] != tag_of(e)) c[t] = -1;
             }
             float4 xv[kUnroll];
 #pragma unroll
@@ -512,7 +513,7 @@ __device__ __forceinline__ void spmm_item(const rsx_csr& a, const float* __restr
                 const bool ok = j + t < end;
                 c[t] = ok ? col[j + t] : 0;
                 v[t] = ok ? val[j + t] : 0.f;
-                if (sparse_x && ok && e.row_tag[c[t]] != tag_of(e)) c[t] = -1;
+                if (sparse_x && ok && xtag[c[t]] != tag_of(e)) c[t] = -1;
             }
             float4 xv[kUnroll];
 #pragma unroll

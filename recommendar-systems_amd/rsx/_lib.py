@@ -51,7 +51,7 @@ class Epilogue(C.Structure):
                 ("y", P), ("s_in", P), ("s_out", P), ("f", P), ("zero0", P), ("zero1", P), ("r_add", P),
                 ("p", P), ("m", P), ("v", P), ("g_out", P), ("e0", P), ("aux", P), ("aux_w", P),
                 ("adam", Adam), ("row_tag", P), ("tag", I32), ("tag_flags", I32), ("reg_cnt", P), ("reg_k", P),
-                ("tag_dev", P), ("halt", P)]
+                ("tag_dev", P), ("halt", P), ("x_tag", P)]
 
 
 RSX_TAG_ROWS = 1

@@ -416,10 +416,12 @@ class SMORE(GeneralRecommender):
         self._bidx = {}
         self._rows_off = {}
         self._tags = None
+        self._vtags = None  # the views' backward batch-row tags (rsx.smore_fuse._ViewProp3)
         self.batch_views = bool(config.get("rsx_smore_batch_views", True))
-        # the item side (projections, spectral part, gates) as one launch (rsx_smore_item_fwd);
-        # False: the three-launch chain (same values, bit for bit)
-        self.item_fused = bool(config.get("rsx_smore_item_fused", True))
+        # the item side (projections, spectral part, gates) as one launch (rsx_smore_item_fwd)
+        # instead of the three-launch chain (same values, bit for bit).  Off by default: it
+        # measured slower (C5 235 vs 209 us, C3 111 vs 77: tools/gpu/micro_item.py)
+        self.item_fused = bool(config.get("rsx_smore_item_fused", False))
         # dropout masks of the fused preference block: a hash of (seed, call, row,
         # feature); the seed word lives on the device and advances once per training
         # forward (graph-capture safe).  Derived from the config seed, not torch's RNG,
@@ -600,6 +602,11 @@ class SMORE(GeneralRecommender):
     def _forward_all(self, train=False):
         return self._forward_all_fused(train)
 
+    def _sparse_rows(self, rows) -> bool:
+        """The batch-row path with tag-aware consumers of the preference block's table
+        gradients (the UI backbone's _PropMeanRows, the views' _ViewProp3)."""
+        return rows is not None and 1 <= self.n_ui_layers <= 4 and self.batch_views
+
     def _views_fused(self, train=False, rows=None):
         """Everything before the preference block: (content, image, text, fusion tables,
         dropout seed).  With `rows` (the batch rows) content is exact on those rows only.
@@ -647,10 +654,15 @@ class SMORE(GeneralRecommender):
         nu, L_ = self.n_users, self.n_layers
         if self.batch_views:  # the three views' products batched into shared launches
             # the batch rows' tags (marked above for the UI backbone; the side stream has joined)
-            tags = self._tags if rows is not None and 1 <= self.n_ui_layers <= 4 else None
+            tags = self._tags if self._sparse_rows(rows) else None
+            gtags = None
+            if tags is not None:  # the backward's own tags (the UI backbone re-tags on the side stream)
+                if self._vtags is None:
+                    self._vtags = _RowTags(self.n_users + self.n_items, self.device)
+                gtags = self._vtags
             image_embeds, text_embeds, fusion_embeds = SF.view_prop3(
                 (img_i, txt_i, fus_i), (self.image_graph, self.text_graph, self.fusion_graph), self.R, L_, nu,
-                tags=tags)
+                tags=tags, gtags=gtags, rows=rows if gtags is not None else None)
         else:
             image_embeds = SF.view_prop(img_i, self.image_graph, self.R, L_, nu)
             text_embeds = SF.view_prop(txt_i, self.text_graph, self.R, L_, nu)
@@ -700,7 +712,7 @@ class SMORE(GeneralRecommender):
         rows = interaction[:3].reshape(-1) + self._rows_off[B]  # [users; nu + positives; nu + negatives]
         content, image_embeds, text_embeds, fusion_embeds, seed = self._views_fused(train=True, rows=rows)
         all_c, side_c, content_c = SF.preference_rows(self, content, image_embeds, text_embeds, fusion_embeds,
-                                                      rows, seed)
+                                                      rows, seed, sparse_grads=self._sparse_rows(rows))
         self.global_step += 1
         total, parts = SF.smore_loss_rows(all_c, side_c, content_c, trip, ar, B, self.reg_weight, self.batch_size,
                                           self.cl_loss, self.cl_temp)

@@ -46,6 +46,7 @@ rsx.evaluator.sharded_metric_dict all-gathers the metric sums.
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import numpy as np
 import torch
@@ -54,6 +55,10 @@ import torch.nn as nn
 
 from . import _lib as L
 from . import graph, ops
+
+# the SMORE item side as one launch (rsx_smore_item_fwd) instead of the projection +
+# spectral + gates chain: same values bit for bit, measured slower, so opt-in
+ITEM_FUSED = os.environ.get("RSX_SMORE_ITEM_FUSED", "0") == "1"
 
 # the row-sharded parameter (its rows [a_r, b_r) live on rank r); everything else is replicated
 SHARDED = {"user_embedding.weight": "u"}
@@ -355,17 +360,28 @@ class HipSmoreBackend:
     def item_side_sharded(self, core, m, item):
         """Projection -> spectral -> the gates' inject term on this rank's item rows only
         (the fused kernels on n_own rows), gathered once; + the replicated item-id table."""
-        from .smore_spectral import _ItemSide
+        from . import smore_fuse as SF
+        from .smore_spectral import _ItemSide, spectral
 
         w = dict(zip(ITEM_W, allreduce_grad(core.comm, *[m.get_parameter(n) for n in ITEM_W])))
-        # the gates' item operand is zero: the kernel writes the inject term alone
+        # the gates' item operand is zero: the kernels write the inject term alone
         zero = core.zero_rows(m.image_embedding.weight.shape[0], item.shape[1], item.device)
-        dv, dt, df = _ItemSide.apply(m.image_embedding.weight, w["image_trs.weight"], w["image_trs.bias"],
-                                     m.text_embedding.weight, w["text_trs.weight"], w["text_trs.bias"],
-                                     w["image_complex_weight"], w["text_complex_weight"], w["fusion_complex_weight"],
-                                     zero, w["gate_v.0.weight"], w["gate_v.0.bias"], w["gate_t.0.weight"],
-                                     w["gate_t.0.bias"], w["gate_f.0.weight"], w["gate_f.0.bias"],
-                                     bool(getattr(m, "spectral_weight_norm", True)), float(m.inject_scale), False)[:3]
+        norm = bool(getattr(m, "spectral_weight_norm", True))
+        if ITEM_FUSED:
+            dv, dt, df = _ItemSide.apply(m.image_embedding.weight, w["image_trs.weight"], w["image_trs.bias"],
+                                         m.text_embedding.weight, w["text_trs.weight"], w["text_trs.bias"],
+                                         w["image_complex_weight"], w["text_complex_weight"],
+                                         w["fusion_complex_weight"], zero, w["gate_v.0.weight"], w["gate_v.0.bias"],
+                                         w["gate_t.0.weight"], w["gate_t.0.bias"], w["gate_f.0.weight"],
+                                         w["gate_f.0.bias"], norm, float(m.inject_scale), False)[:3]
+        else:
+            cv, ct, cf, _, _ = spectral(m.image_embedding.weight, w["image_trs.weight"], w["image_trs.bias"],
+                                        m.text_embedding.weight, w["text_trs.weight"], w["text_trs.bias"],
+                                        w["image_complex_weight"], w["text_complex_weight"],
+                                        w["fusion_complex_weight"], norm)
+            dv, dt, df = SF._Gates.apply(cv, ct, cf, zero, w["gate_v.0.weight"], w["gate_v.0.bias"],
+                                         w["gate_t.0.weight"], w["gate_t.0.bias"], w["gate_f.0.weight"],
+                                         w["gate_f.0.bias"], float(m.inject_scale), False)
         D = gather_rows(core.comm, core.iq, core.n_items, dv, dt, df)
         return (D + item.unsqueeze(0)).unbind(0)
 
@@ -456,7 +472,7 @@ class SmoreShard:
         item = m.item_id_embedding.weight if item is None else item
         if self.item_shard:
             return self.be.item_side_sharded(self, m, item)
-        if hasattr(self.be, "item_side"):
+        if ITEM_FUSED and hasattr(self.be, "item_side"):
             return self.be.item_side(m, item)
         cv, ct, cf = self.be.spectral(m)
         return self.be.gates(m, cv, ct, cf, item)

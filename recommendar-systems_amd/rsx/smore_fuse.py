@@ -167,10 +167,11 @@ class _PrefRows(torch.autograd.Function):
     full zero tables (rsx_smore_pref_rows with occ: deterministic, no float atomics)."""
 
     @staticmethod
-    def forward(ctx, C_, IE, TE, FE, rows, p_drop, seed, *wb):
+    def forward(ctx, C_, IE, TE, FE, rows, p_drop, seed, sparse, *wb):
         W = [_c(x) for x in wb[:7]]
         b = [None if x is None else _c(x) for x in wb[7:]]
         C_, IE, TE, FE, rows = _c(C_), _c(IE), _c(TE), _c(FE), _c(rows)
+        ctx.sparse = bool(sparse)
         n, d = rows.numel(), C_.shape[1]
         out = torch.empty(5, n, d, dtype=torch.float32, device=C_.device)
         all_, side, c_rows, f_rows, x2 = out.unbind(0)  # x2: the split forward's scratch
@@ -196,7 +197,11 @@ class _PrefRows(torch.autograd.Function):
         g_all = _c(g_all)
         g_side = None if g_side is None else _c(g_side)
         g_crows = None if g_crows is None else _c(g_crows)
-        gfull = torch.zeros(4, *C_.shape, dtype=torch.float32, device=C_.device)
+        # sparse: every consumer of these tables reads them on the batch rows only (the
+        # tagged UI backbone, _PropMeanRows; the views' tagged R^T product, _ViewProp3), so
+        # the rows the kernel does not write are never read and need no zero fill
+        alloc = torch.empty if ctx.sparse else torch.zeros
+        gfull = alloc(4, *C_.shape, dtype=torch.float32, device=C_.device)
         gC, gIE, gTE, gFE = gfull.unbind(0)
         # hv, ht, dz[7] and the per-occurrence row gradients (deterministic sums, no atomics)
         occ_n = int(L.lib().rsx_smore_pref_rows_occ_floats(n, d))
@@ -211,21 +216,25 @@ class _PrefRows(torch.autograd.Function):
         grads = _wgrad([(dz[i], xs[i], ctx.has_b[i]) for i in range(7)], d, C_.device)
         gW = [g[0] for g in grads]
         gb = [g[1] for g in grads]
-        return (gC, gIE, gTE, gFE, None, None, None, *gW, *gb)
+        return (gC, gIE, gTE, gFE, None, None, None, None, *gW, *gb)
 
 
-def preference_rows(model, content, image_embeds, text_embeds, fusion_embeds, rows, seed, weights=None):
+def preference_rows(model, content, image_embeds, text_embeds, fusion_embeds, rows, seed, weights=None,
+                    sparse_grads=False):
     """(all, side, content) rows of the reference's preference block at table rows
     `rows` only (the training loss reads no other row; the block is row-local).
     `weights`: the 7 weights then the 7 biases (None where absent) to use instead of
-    the model's own tensors (the sharded model passes them through a gradient sum)."""
+    the model's own tensors (the sharded model passes them through a gradient sum).
+    `sparse_grads`: the four table gradients are defined on the batch rows only (their
+    consumers read nothing else: see _PrefRows.backward)."""
     m = model
     if weights is None:
         lin = [m.query_v[0], m.query_v[2], m.query_t[0], m.query_t[2], m.gate_image_prefer[0],
                m.gate_text_prefer[0], m.gate_fusion_prefer[0]]
         weights = [x.weight for x in lin] + [x.bias for x in lin]
     p = float(m.dropout.p) if m.training else 0.0
-    return _PrefRows.apply(content, image_embeds, text_embeds, fusion_embeds, rows, p, seed, *weights)
+    return _PrefRows.apply(content, image_embeds, text_embeds, fusion_embeds, rows, p, seed, bool(sparse_grads),
+                           *weights)
 
 
 # ---------------------------------------------------------------------------
@@ -274,7 +283,7 @@ class _ViewProp3(torch.autograd.Function):
     the three R^T and item-graph transposes, each set as ONE rsx_spmm_batch launch."""
 
     @staticmethod
-    def forward(ctx, x0, x1, x2, Gs, R, n_layers, n_users, comm, tags):
+    def forward(ctx, x0, x1, x2, Gs, R, n_layers, n_users, comm, tags, gtags, rows):
         xs = [_c(x) for x in (x0, x1, x2)]
         ni, d = xs[0].shape
         outs = [torch.empty(n_users + ni, d, dtype=torch.float32, device=xs[0].device) for _ in range(3)]
@@ -293,6 +302,7 @@ class _ViewProp3(torch.autograd.Function):
                 e.tag_flags = L.RSX_TAG_ROWS
         ops.spmm_batch([R.A] * 3, [o[n_users:] for o in outs], epis, d)
         ctx.Gs, ctx.R, ctx.L, ctx.nu, ctx.comm = Gs, R, n_layers, n_users, comm
+        ctx.gtags, ctx.rows = gtags, rows
         return tuple(outs)
 
     @staticmethod
@@ -306,26 +316,38 @@ class _ViewProp3(torch.autograd.Function):
         # d items = g_items + R^T g_users (ADD epilogue), the three views in one launch.
         # (A scatter from the batch users instead, by float atomics, measured slower: 92 us
         # against 104 at C5, and at baby d = 64 three times the gather.)
-        ops.spmm_batch([ctx.R.AT] * 3, [g[:nu] for g in gs],
-                       [ops.epi(L.RSX_EPI_ADD, y=y, r_add=g[nu:]) for y, g in zip(gi, gs)], d)
+        epis = [ops.epi(L.RSX_EPI_ADD, y=y, r_add=g[nu:]) for y, g in zip(gi, gs)]
+        t = ctx.gtags
+        if t is not None:
+            # the incoming gradients are defined on the batch rows only (_PrefRows, sparse):
+            # the users' rows are gathered (x_tag) and the items' rows added (row_tag on the
+            # item block) on the tagged rows only -- re-tagged here, on this stream, as
+            # _PropMeanRows does with its own tags on the side stream
+            t.mark(ctx.rows)
+            for e in epis:
+                e.row_tag, e.x_tag, e.tag_dev = t.row_tag[nu:].data_ptr(), t.row_tag.data_ptr(), t.tag_dev.data_ptr()
+                e.tag_flags = L.RSX_TAG_SPARSE_X | L.RSX_TAG_SPARSE_R
+        ops.spmm_batch([ctx.R.AT] * 3, [g[:nu] for g in gs], epis, d)
         if ctx.comm is not None:  # users sharded (rsx.smore_dist): the item rows' gradient summed over the ranks
             ctx.comm.allreduce_(gbuf)
         for _ in range(ctx.L):
             nxt = [torch.empty_like(x) for x in gi]
             ops.spmm_batch([G.AT for G in ctx.Gs], gi, [ops.epi(L.RSX_EPI_STORE, y=y) for y in nxt], d)
             gi = nxt
-        return gi[0], gi[1], gi[2], None, None, None, None, None, None
+        return gi[0], gi[1], gi[2], None, None, None, None, None, None, None, None
 
 
-def view_prop3(xs, Gs, R, n_layers, n_users, comm=None, tags=None):
+def view_prop3(xs, Gs, R, n_layers, n_users, comm=None, tags=None, gtags=None, rows=None):
     """(image, text, fusion) [R G^L x; G^L x] tables of the three views (one launch per
     layer for all three graphs, one for the three R products).  With `comm` (R = this
     rank's user rows) the item rows' gradients are summed over the ranks in one
     all-reduce before the item-graph backward.  With `tags` (the batch-row tags of the
     training loss, rsx.smore._RowTags over [users; items], already marked) the user rows
     are computed on the tagged users only: the preference block reads no other user row
-    of a view."""
-    return _ViewProp3.apply(xs[0], xs[1], xs[2], tuple(Gs), R, int(n_layers), int(n_users), comm, tags)
+    of a view.  With `gtags` (a _RowTags of its own) and `rows` the backward takes the
+    incoming gradients as defined on `rows` only (preference_rows(sparse_grads=True))
+    and reads nothing else of them."""
+    return _ViewProp3.apply(xs[0], xs[1], xs[2], tuple(Gs), R, int(n_layers), int(n_users), comm, tags, gtags, rows)
 
 
 # ---------------------------------------------------------------------------

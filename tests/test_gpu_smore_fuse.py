@@ -282,6 +282,61 @@ def test_view_prop3_tagged_users(cuda, d):
         assert torch.equal(a, b)
 
 
+class _Poison(torch.autograd.Function):
+    """Identity forward; backward hands on the incoming gradient with every row off
+    `rows` overwritten by NaN (what an unfilled table holds there)."""
+
+    @staticmethod
+    def forward(ctx, x, keep):
+        ctx.save_for_backward(keep)
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        (keep,) = ctx.saved_tensors
+        return torch.where(keep, g, torch.full_like(g, float("nan"))), None
+
+
+@pytest.mark.parametrize("d", [64, 128])
+def test_view_prop3_sparse_gradients_read_only_the_batch_rows(cuda, d):
+    """The views' backward with its own tags (gtags, rows: preference_rows(sparse_grads=
+    True) leaves the table gradients unwritten off the batch rows): NaN in every other row
+    of the upstream gradient changes nothing -- the input gradients equal, bit for bit, the
+    dense backward's for the same gradient zero off the batch rows (users gathered through
+    x_tag, items added through the item block's row tags); repeated batch rows."""
+    from rsx import smore_fuse as SF
+    from rsx.smore import _DevGraph, _RowTags
+
+    rng = np.random.default_rng(11 + d)
+    nu, ni = 1100, 450
+
+    def graph(nr, nc, nnz, zipf, chunk):
+        r = rng.integers(0, nr, nnz)
+        c = (rng.zipf(zipf, nnz) - 1) % nc
+        key = np.unique(r * nc + c, return_index=True)[1]
+        return _DevGraph(r[key], c[key], rng.random(key.size).astype(np.float32), nr, nc, cuda, chunk)
+
+    Gs = [graph(ni, ni, 6000, 1.3, 64), graph(ni, ni, 5000, 1.6, 64), graph(ni, ni, 9000, 1.2, 64)]
+    R = graph(nu, ni, 14000, 1.4, 32)
+    users = torch.from_numpy(rng.integers(0, nu, 256)).to(cuda)
+    items = torch.from_numpy(rng.integers(0, ni, 512)).to(cuda)
+    rows = torch.cat([users, nu + items])
+    tags, gtags = _RowTags(nu + ni, cuda), _RowTags(nu + ni, cuda)
+    tags.mark(rows)
+    keep = torch.zeros(nu + ni, 1, dtype=torch.bool, device=cuda)
+    keep[rows] = True
+    xs = [torch.randn(ni, d, device=cuda, requires_grad=True) for _ in range(3)]
+    ups = [torch.randn(nu + ni, d, device=cuda) * keep for _ in range(3)]
+    for L_ in (1, 2):
+        sp = SF.view_prop3(xs, Gs, R, L_, nu, tags=tags, gtags=gtags, rows=rows)
+        sp = [_Poison.apply(o, keep) for o in sp]
+        dn = SF.view_prop3(xs, Gs, R, L_, nu, tags=tags)
+        gs_ = torch.autograd.grad(sum((o * w).sum() for o, w in zip(sp, ups)), xs)
+        gd = torch.autograd.grad(sum((o * w).sum() for o, w in zip(dn, ups)), xs)
+        for a, b in zip(gs_, gd):
+            assert torch.isfinite(a).all() and torch.equal(a, b), L_
+
+
 @pytest.mark.parametrize("kind", ["store", "add"])
 def test_spmm_batch_many_fixups(cuda, kind):
     """rsx_spmm_batch with more hub-row fixups than ride along in one launch (> 1024 over

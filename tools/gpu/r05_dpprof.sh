@@ -1,4 +1,4 @@
-# round 5: kernel traces of the triplets-only DP step (one real RCCL rank; rank 0 of a
+# round 5: kernel traces of the triplets-only DP step (and the C5 step's launch sequence) (one real RCCL rank; rank 0 of a
 # latency-injected 8-rank job) beside the single-GPU C2 engine, for the per-launch breakdown
 set -o pipefail
 cd $GRAFT_REPO_ROOT
@@ -16,4 +16,8 @@ prof c2 RSX_X=0 || exit 1
 ARGS="--dp --steps 200 --warmup 20 --no-cpu-baseline"
 prof dp1 RSX_X=0 || exit 1
 prof dp_sim8 RSX_COMM_SIM=8 || exit 1
+# the C5 step's launch sequence (every dispatch, 3 timed steps): where its fills and small
+# kernels sit
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/c5seq -o c5seq -- python3 bench.py --workload c5 \
+  --steps 3 --warmup 2 --no-cpu-baseline > $OUT/c5seq.json 2> $OUT/c5seq.err || { tail -20 $OUT/c5seq.err; exit 1; }
 echo done
