@@ -284,6 +284,8 @@ def bench_model(args):
     sim = sim_comm_params() if (world == 1 and w["model"] == "SMORE") else None
     if sim:  # rank 0 of a modelled W-rank users-sharded job (rsx.smore_dist.Comm's latency injection)
         cfg["rsx_sharded"] = True
+    if os.environ.get("RSX_BENCH_GRAPH") == "0":  # diagnosis: the model's batches eagerly
+        cfg["rsx_graph_step"] = False
     c = Config(w["model"], w["dataset"], cfg)
     if world > 1:
         c["device"] = torch.device("cuda", _local_device())  # (the rehearsal mode puts every rank on GPU 0)

@@ -242,9 +242,9 @@ __global__ __launch_bounds__(kBprBlock) void bpr_bwd(BprArgs a, int n_part) {
 // gradient, which needs the batch's global Frobenius norms, is left to the
 // consumer as occurrence counts per row (as user, positive, negative) and three
 // scales ku, kp, kn: R[row] = (c_u ku + c_p kp + c_n kn) ego[row] (the reference
-// sums c equal terms per row).  Every block stores its f64 partials; the last
-// block to arrive (agent-scope release/acquire around one counter) reduces them in
-// bpr_bwd's fixed order, writes the loss and the scales and re-arms the counter.
+// sums c equal terms per row).  Every block stores its f64 partials (sc1); the last
+// block to arrive at one counter reduces them (sc1 loads) in bpr_bwd's fixed order,
+// writes the loss and the scales and re-arms the counter.
 template <int D>
 __global__ __launch_bounds__(kBprBlock) void bpr_fused(BprArgs a) {
     constexpr int G = D / 4;
@@ -338,13 +338,15 @@ __global__ __launch_bounds__(kBprBlock) void bpr_fused(BprArgs a) {
         __hip_atomic_store(a.part + (int64_t)blockIdx.x * 4 + threadIdx.x, v, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
     }
+    // the partials are stored and read sc1 (agent-scope atomics: write-through, L1 bypassed),
+    // so the hand-off needs no per-block L2 write-back fence (MI355X_MICROARCH.md, valid
+    // forms: sc1 stores drained by vmcnt(0) before the counter add, sc1 loads by the last)
+    if (threadIdx.x < 4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the storing lanes (one wave)
     __syncthreads();
     int* done = a.reg_cnt + 3 * a.n_rows;
     if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         const int prev = __hip_atomic_fetch_add(done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         last = prev == (int)gridDim.x - 1;
-        if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     }
     __syncthreads();
     if (!last) return;

@@ -129,16 +129,34 @@ __global__ __launch_bounds__(kBlk) void dp_index(const int64_t* __restrict__ slo
     atomicAdd(reg_cnt + 3 * x + (i % (3 * cap)) / cap, 1);
 }
 
-// (comm stream) each union row's run: its first claimer reserves count places
+// (comm stream) each union row's run: its first claimer reserves count places.  The
+// claims of a wave are summed first (a scan over its lanes) and reserved with one atomic
+// per wave: one counter taking an atomic per union row serialised at its L2 channel
+// (12 us at W = 1, 16 at W = 8)
 __global__ __launch_bounds__(kBlk) void dp_alloc(const int64_t* __restrict__ slots, int32_t W, int64_t cap,
                                                  int64_t n_users, const int32_t* __restrict__ reg_cnt,
                                                  int32_t* __restrict__ start, int32_t* __restrict__ meta) {
     const int64_t i = (int64_t)blockIdx.x * kBlk + threadIdx.x;
-    if (i >= (int64_t)W * 3 * cap) return;
-    const int64_t x = occ_row(slots, cap, n_users, i);
-    if (x < 0 || atomicCAS(start + x, 0, -1) != 0) return;
-    const int32_t n = reg_cnt[3 * x] + reg_cnt[3 * x + 1] + reg_cnt[3 * x + 2];
-    start[x] = atomicAdd(meta + 2, n) + 1;
+    const int lane = threadIdx.x % kWave;
+    int64_t x = -1;
+    int32_t n = 0;
+    if (i < (int64_t)W * 3 * cap) {
+        x = occ_row(slots, cap, n_users, i);
+        if (x >= 0 && atomicCAS(start + x, 0, -1) == 0)
+            n = reg_cnt[3 * x] + reg_cnt[3 * x + 1] + reg_cnt[3 * x + 2];
+        else
+            x = -1;
+    }
+    int32_t inc = n;  // inclusive scan of the wave's claims (every lane of the wave is here)
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+        const int32_t v = __shfl_up(inc, o, kWave);
+        if (lane >= o) inc += v;
+    }
+    int32_t base = 0;
+    if (lane == kWave - 1 && inc > 0) base = atomicAdd(meta + 2, inc);
+    base = __shfl(base, kWave - 1, kWave);
+    if (x >= 0) start[x] = base + (inc - n) + 1;
 }
 
 // (comm stream) every occurrence takes a place in its row's run
@@ -228,12 +246,14 @@ __global__ __launch_bounds__(kBlk) void dp_bpr_coef(const int64_t* __restrict__ 
         for (int w = 0; w < kBlk / kWave; ++w) v = threadIdx.x == 4 ? fmax(v, red[w][4]) : v + red[w][threadIdx.x];
         __hip_atomic_store(part + (int64_t)blockIdx.x * 5 + threadIdx.x, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    // the partials are stored and read sc1 (agent-scope atomics: write-through, L1 bypassed),
+    // so the hand-off needs no L2 write-back fence per block (MI355X_MICROARCH.md, valid
+    // forms: sc1 stores drained by vmcnt(0) before the counter add, sc1 loads by the last)
+    if (threadIdx.x < 5) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the storing lanes (one wave)
     __syncthreads();
     if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         const int prev = __hip_atomic_fetch_add(meta, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         last = prev == (int)gridDim.x - 1;
-        if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     }
     __syncthreads();
     if (!last) return;
@@ -282,35 +302,41 @@ __global__ __launch_bounds__(kBlk) void dp_bpr_coef(const int64_t* __restrict__ 
     }
 }
 
-// Phase B: G' in fixed point.  Lane group c walks run places [c kChunk, (c+1) kChunk): each occurrence's term (bpr_fused's f32 arithmetic: coef (f_p - f_n) / g_div
-// for a user, +-coef f_u / g_div for an item) scaled by 2^e and rounded to int64, a run of
-// equal rows summed in registers, one 64-bit integer atomic per run and column.
-// The chunk's bookkeeping (sorted key, occurrence -> triplet -> the rows to gather and
-// the coefficient: three dependent loads) is resolved by the group's lanes for all its
-// occurrences at once (lane q holds occurrence q's) and broadcast by shuffles, and the
-// rows of KB occurrences are gathered together before they are added: a lane group
-// walking its occurrences one dependent chain at a time spent ~30 us on 6,144
-// occurrences.
+// Phase B: G' in fixed point.  Lane group c takes run places [c kChunk, (c+1) kChunk):
+// each occurrence's term (bpr_fused's f32 arithmetic: coef (f_p - f_n) / g_div for a user,
+// +-coef f_u / g_div for an item) scaled by 2^e and rounded to int64, the terms of a run
+// segment summed in registers.  A run that lies wholly in the chunk (most rows occur once
+// or a few times) is finished here: its sum scaled back and rounded to f32 once, stored
+// as G' -- no atomics; only a run crossing a chunk boundary adds its segments into the
+// int64 accumulators (integer adds commute: any order gives the same bits), which
+// dp_bpr_round then finishes.  The chunk's bookkeeping (place -> occurrence -> triplet ->
+// the rows to gather, the coefficient, the run's first place and length: dependent
+// loads) is resolved by the group's lanes for all its places at once (lane q holds place
+// q's) and broadcast by shuffles, and every gather of the chunk is issued before the first
+// store or atomic (gfx9 counts loads, stores and atomics in one vmcnt: a load issued
+// after them would wait for them).  (The per-run atomics of the previous form, one per
+// run and column, cost ~50 us at W = 8.)
 template <int D>
 __global__ __launch_bounds__(kBlk) void dp_bpr_grad(const int64_t* __restrict__ slots, int64_t cap, int64_t n_users,
                                                     int64_t N, int64_t n_occ, const int32_t* __restrict__ key,
-                                                    const int32_t* __restrict__ val, const float* __restrict__ fin,
+                                                    const int32_t* __restrict__ val,
+                                                    const int32_t* __restrict__ start,
+                                                    const int32_t* __restrict__ cursor, const float* __restrict__ fin,
                                                     const float* __restrict__ coef, float g_div,
                                                     const int32_t* __restrict__ meta,
-                                                    unsigned long long* __restrict__ acc) {
+                                                    unsigned long long* __restrict__ acc, float* __restrict__ gout) {
     constexpr int G = D / 4, GPB = kBlk / G;
-    constexpr int KP = (kChunk + G - 1) / G;  // occurrences whose bookkeeping one lane holds
-    constexpr int KB = 8;                     // occurrences gathered together
+    constexpr int KP = (kChunk + G - 1) / G;  // places whose bookkeeping one lane holds
     const int li = threadIdx.x % G;
     const int gl0 = (threadIdx.x % kWave) - li;  // the group's first lane in the wave
     const int64_t c0 = ((int64_t)blockIdx.x * GPB + threadIdx.x / G) * kChunk;
     const int64_t n_pl = meta[2] < n_occ ? meta[2] : n_occ;  // the run places taken this step
     if (c0 >= n_pl) return;  // group-uniform
-    const double S = ldexp(1.0, meta[1]);
+    const double S = ldexp(1.0, meta[1]), inv = ldexp(1.0, -meta[1]);
     const int64_t L = 3 * cap + 1;
-    // bookkeeping of occurrence q = li + G k of the chunk: its row (N: none), the rows it
-    // gathers (b = -1 when only one) and its signed, scaled coefficient
-    int32_t xq[KP];
+    // bookkeeping of place c0 + q, q = li + G k: its row (N: none), the rows it gathers
+    // (b = -1 when only one), its signed coefficient, its run's first place and length
+    int32_t xq[KP], sq[KP], nq[KP];
     int64_t aq[KP], bq[KP];
     float cq[KP];
 #pragma unroll
@@ -318,31 +344,56 @@ __global__ __launch_bounds__(kBlk) void dp_bpr_grad(const int64_t* __restrict__ 
         const int q = li + G * k;
         const int64_t i = c0 + q;
         xq[k] = (int32_t)N;
+        sq[k] = nq[k] = 0;
         aq[k] = bq[k] = -1;
         cq[k] = 0.f;
         if (q < kChunk && i < n_pl) {
             const int32_t x = key[i];
-            if (x < N) {
-                const int64_t o = val[i];
-                const int64_t r = o / (3 * cap), j = o - r * 3 * cap, kind = j / cap, t = j - kind * cap;
-                const int64_t* slot = slots + r * L;
-                const float c = coef[r * cap + t];
-                xq[k] = x;
-                if (kind == 0) {
-                    aq[k] = n_users + slot[1 + cap + t];
-                    bq[k] = n_users + slot[1 + 2 * cap + t];
-                    cq[k] = c;
-                } else {
-                    aq[k] = slot[1 + t];
-                    cq[k] = kind == 1 ? c : -c;
-                }
+            const int64_t o = val[i];
+            const int64_t r = o / (3 * cap), j = o - r * 3 * cap, kind = j / cap, t = j - kind * cap;
+            const int64_t* slot = slots + r * L;
+            const float c = coef[r * cap + t];
+            xq[k] = x;
+            sq[k] = start[x] - 1;
+            nq[k] = cursor[x];
+            if (kind == 0) {
+                aq[k] = n_users + slot[1 + cap + t];
+                bq[k] = n_users + slot[1 + 2 * cap + t];
+                cq[k] = c;
+            } else {
+                aq[k] = slot[1 + t];
+                cq[k] = kind == 1 ? c : -c;
             }
         }
     }
+    int32_t xs[kChunk], ss[kChunk], ns[kChunk];
+    float cs[kChunk];
+    bool two[kChunk];
+    float4 va[kChunk], vb[kChunk];
+#pragma unroll
+    for (int u = 0; u < kChunk; ++u) {
+        const int src = gl0 + u % G, k = u / G;
+        xs[u] = __shfl(xq[k], src, kWave);
+        ss[u] = __shfl(sq[k], src, kWave);
+        ns[u] = __shfl(nq[k], src, kWave);
+        cs[u] = __shfl(cq[k], src, kWave);
+        const int64_t ra = __shfl(aq[k], src, kWave), rb = __shfl(bq[k], src, kWave);
+        two[u] = rb >= 0;
+        va[u] = ra >= 0 ? ld4(fin + ra * D + li * 4) : f4(0.f);
+        vb[u] = rb >= 0 ? ld4(fin + rb * D + li * 4) : f4(0.f);
+    }
     long long a0 = 0, a1 = 0, a2 = 0, a3 = 0;
-    int32_t cur = -1;
+    int32_t cur = -1, seg0 = 0, segn = 0, cur_s = 0, cur_n = 0;
     auto flush = [&]() __attribute__((always_inline)) {
-        if (cur >= 0) {
+        if (cur < 0) return;
+        if (seg0 == cur_s && segn == cur_n) {  // the whole run: G' here, rounded once
+            float4 v;
+            v.x = (float)((double)a0 * inv);
+            v.y = (float)((double)a1 * inv);
+            v.z = (float)((double)a2 * inv);
+            v.w = (float)((double)a3 * inv);
+            st4(gout + (int64_t)cur * D + li * 4, v);
+        } else {
             unsigned long long* q = acc + (int64_t)cur * D + li * 4;
             atomicAdd(q + 0, (unsigned long long)a0);
             atomicAdd(q + 1, (unsigned long long)a1);
@@ -351,55 +402,44 @@ __global__ __launch_bounds__(kBlk) void dp_bpr_grad(const int64_t* __restrict__ 
         }
     };
 #pragma unroll
-    for (int j0 = 0; j0 < kChunk; j0 += KB) {
-        int32_t xs[KB];
-        float cs[KB];
-        bool two[KB];
-        float4 va[KB], vb[KB];
-#pragma unroll
-        for (int u = 0; u < KB; ++u) {
-            const int q = j0 + u, src = gl0 + q % G, k = q / G;
-            xs[u] = __shfl(xq[k], src, kWave);
-            cs[u] = __shfl(cq[k], src, kWave);
-            const int64_t ra = __shfl(aq[k], src, kWave), rb = __shfl(bq[k], src, kWave);
-            two[u] = rb >= 0;
-            va[u] = ra >= 0 ? ld4(fin + ra * D + li * 4) : f4(0.f);
-            vb[u] = rb >= 0 ? ld4(fin + rb * D + li * 4) : f4(0.f);
+    for (int u = 0; u < kChunk; ++u) {
+        const int32_t x = xs[u];
+        if (x >= N) break;  // past the places taken (group-uniform)
+        if (x != cur) {
+            flush();
+            cur = x;
+            seg0 = (int32_t)(c0 + u);
+            segn = 0;
+            cur_s = ss[u];
+            cur_n = ns[u];
+            a0 = a1 = a2 = a3 = 0;
         }
-#pragma unroll
-        for (int u = 0; u < KB; ++u) {
-            const int32_t x = xs[u];
-            if (x >= N) break;  // past the places taken (group-uniform)
-            if (x != cur) {
-                flush();
-                cur = x;
-                a0 = a1 = a2 = a3 = 0;
-            }
-            const float c = cs[u];
-            float4 g;
-            if (two[u]) {
-                g = make_float4(c * (va[u].x - vb[u].x), c * (va[u].y - vb[u].y), c * (va[u].z - vb[u].z),
-                                c * (va[u].w - vb[u].w));
-            } else {
-                g = make_float4(c * va[u].x, c * va[u].y, c * va[u].z, c * va[u].w);
-            }
-            if (g_div != 1.f) {
-                g.x /= g_div;
-                g.y /= g_div;
-                g.z /= g_div;
-                g.w /= g_div;
-            }
-            a0 += llrint((double)g.x * S);
-            a1 += llrint((double)g.y * S);
-            a2 += llrint((double)g.z * S);
-            a3 += llrint((double)g.w * S);
+        ++segn;
+        const float c = cs[u];
+        float4 g;
+        if (two[u]) {
+            g = make_float4(c * (va[u].x - vb[u].x), c * (va[u].y - vb[u].y), c * (va[u].z - vb[u].z),
+                            c * (va[u].w - vb[u].w));
+        } else {
+            g = make_float4(c * va[u].x, c * va[u].y, c * va[u].z, c * va[u].w);
         }
+        if (g_div != 1.f) {
+            g.x /= g_div;
+            g.y /= g_div;
+            g.z /= g_div;
+            g.w /= g_div;
+        }
+        a0 += llrint((double)g.x * S);
+        a1 += llrint((double)g.y * S);
+        a2 += llrint((double)g.z * S);
+        a3 += llrint((double)g.w * S);
     }
     flush();
 }
 
-// Phase C: every union row once (the first place of its run): G'[x] = its accumulator /
-// 2^e rounded to f32; the accumulator, the run's start and cursor cleared for the next step.
+// Phase C: every union row once (the first place of its run): a run that crossed a chunk
+// boundary gets G'[x] = its accumulator / 2^e rounded to f32 and the accumulator cleared;
+// every run's start and cursor are cleared for the next step.
 template <int D>
 __global__ __launch_bounds__(kBlk) void dp_bpr_round(int64_t n_occ, const int32_t* __restrict__ key,
                                                      int32_t* __restrict__ start, int32_t* __restrict__ cursor,
@@ -412,18 +452,21 @@ __global__ __launch_bounds__(kBlk) void dp_bpr_round(int64_t n_occ, const int32_
     if (i >= n_pl) return;
     const int32_t x = key[i];
     if (start[x] - 1 != i) return;  // (a first place clears start[x] below: the others then see 0)
-    const double inv = ldexp(1.0, -meta[1]);
-    unsigned long long* q = acc + (int64_t)x * D + li * 4;
-    float4 v;
-    v.x = (float)((double)(long long)q[0] * inv);
-    v.y = (float)((double)(long long)q[1] * inv);
-    v.z = (float)((double)(long long)q[2] * inv);
-    v.w = (float)((double)(long long)q[3] * inv);
-    q[0] = 0ull;
-    q[1] = 0ull;
-    q[2] = 0ull;
-    q[3] = 0ull;
-    st4(g + (int64_t)x * D + li * 4, v);
+    const int32_t n = cursor[x];
+    if (i / kChunk != (i + n - 1) / kChunk) {  // finished by dp_bpr_grad otherwise
+        const double inv = ldexp(1.0, -meta[1]);
+        unsigned long long* q = acc + (int64_t)x * D + li * 4;
+        float4 v;
+        v.x = (float)((double)(long long)q[0] * inv);
+        v.y = (float)((double)(long long)q[1] * inv);
+        v.z = (float)((double)(long long)q[2] * inv);
+        v.w = (float)((double)(long long)q[3] * inv);
+        q[0] = 0ull;
+        q[1] = 0ull;
+        q[2] = 0ull;
+        q[3] = 0ull;
+        st4(g + (int64_t)x * D + li * 4, v);
+    }
     if (li == 0) {
         start[x] = 0;
         cursor[x] = 0;
@@ -457,7 +500,8 @@ int dp_loss_kernels(const rsx_dp_lgcn_step& st, const Work& w, int32_t W, hipStr
     DP_TRY(last_rc());
     const int64_t n_chunks = (n_occ + kChunk - 1) / kChunk;
     hipLaunchKernelGGL((dp_bpr_grad<D>), dim3((unsigned)((n_chunks + GPB - 1) / GPB)), dim3(kBlk), 0, s, st.slots,
-                       cap, nu, N, n_occ, w.keys, w.occ, st.final_emb, w.coef, g_div, w.meta, w.acc);
+                       cap, nu, N, n_occ, w.keys, w.occ, w.start, w.cursor, st.final_emb, w.coef, g_div, w.meta,
+                       w.acc, st.g);
     DP_TRY(last_rc());
     hipLaunchKernelGGL((dp_bpr_round<D>), dim3((unsigned)((n_occ + GPB - 1) / GPB)), dim3(kBlk), 0, s, n_occ, w.keys,
                        w.start, w.cursor, w.meta, w.acc, st.g);
@@ -480,13 +524,21 @@ int dp_step(const rsx_dp_lgcn_step& st, hipStream_t s) {
     Work w = carve(st.work, N, d, cap, W);
     if (w.total > st.work_bytes) return RSX_ERR_WORKSPACE;
     int rc = 0;
-    // (1) this rank's triplets into its slot; every rank's gathered while the forward runs,
-    // then indexed (union tags, global counts) and bucketed by row, on the comm stream
-    hipLaunchKernelGGL(dp_pack, dim3((unsigned)((L + kBlk - 1) / kBlk)), dim3(kBlk), 0, s, st.triplets, B, cap,
+    // (1) on the comm stream, while the forward runs: this rank's triplets into its slot,
+    // every rank's gathered, then indexed (union tags, global counts) and bucketed by row.
+    // The forward's first launch depends on nothing of this step (in a replayed graph a
+    // dependency across queues costs ~10 us: the slot pack used to sit ahead of it on the
+    // compute stream)
+    hipStream_t cs = comm_stream(st.comm, s);
+    if (cs != s) {
+        hipEvent_t fork = comm_event(st.comm);
+        DP_TRY(hip_rc(hipEventRecord(fork, s)));
+        DP_TRY(hip_rc(hipStreamWaitEvent(cs, fork, 0)));
+    }
+    hipLaunchKernelGGL(dp_pack, dim3((unsigned)((L + kBlk - 1) / kBlk)), dim3(kBlk), 0, cs, st.triplets, B, cap,
                        st.slots + rank * L, st.inc_step ? const_cast<int64_t*>(st.adam.step_dev) : nullptr, w.meta);
     DP_TRY(last_rc());
-    if (!collective(st.comm, RSX_COLL_ALLGATHER, st.slots, L * ag, RSX_COLL_I64, s, &rc)) return rc;
-    hipStream_t cs = comm_stream(st.comm, s);
+    if (!collective(st.comm, RSX_COLL_ALLGATHER, st.slots, L * ag, RSX_COLL_I64, cs, &rc)) return rc;
     const dim3 go((unsigned)((n_occ + kBlk - 1) / kBlk));
     hipLaunchKernelGGL(dp_index, go, dim3(kBlk), 0, cs, st.slots, W, cap, nu, st.row_tag, st.reg_cnt, st.tag_dev);
     DP_TRY(last_rc());

@@ -3,7 +3,7 @@
 # stand-in holding its modelled time, 32 CUs and HBM bytes), beside their N = 1 lines
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-export TMPDIR=/tmp
+export TMPDIR=/tmp PYTHONFAULTHANDLER=1
 OUT=${OUT:-gpurun_out/r05sims}
 mkdir -p $OUT
 summ() {
