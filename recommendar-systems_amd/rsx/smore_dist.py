@@ -482,7 +482,11 @@ class SmoreShard:
         backend, concurrent with the replicated item side, so its exchanges hide behind
         the projection / spectral / gate kernels (and likewise in the backward, which
         autograd runs on the same streams)."""
-        side = self.be.side_stream() if hasattr(self.be, "side_stream") else None
+        # (not with an rsx communicator: a collective forked from a side stream that joined a
+        # graph capture makes HIP's capture end segfault -- tools/gpu/diag_smore_sim.py,
+        # pattern `side`, DESIGN §6 -- so the native-comm step keeps the UI backbone and its
+        # all-reduces on the capturing stream, where the fork is the DP / row-sharded steps')
+        side = self.be.side_stream() if hasattr(self.be, "side_stream") and not self.comm.native else None
         main = torch.cuda.current_stream() if side is not None else None
         # every leaf enters through a view made here, on one stream (rsx.smore._views_fused)
         uw = m.user_embedding.weight.view_as(m.user_embedding.weight)
@@ -567,15 +571,15 @@ class SmoreShard:
                 return torch.zeros((), dtype=torch.float64, device=dev)
             return torch.stack([n.double() for n in torch._foreach_norm(ts)]).pow(2).sum()
 
-        part = torch.stack([sq(sh_g), sq(sh_p), torch.tensor(float(sum(p.numel() for p in sh_p)), dtype=torch.float64,
-                                                             device=dev)]).float()
+        part = torch.stack([sq(sh_g), sq(sh_p), torch.full((), float(sum(p.numel() for p in sh_p)),
+                                                           dtype=torch.float64, device=dev)]).float()
         self.comm.allreduce_(part)
-        tot = part.double() + torch.stack([sq(rp_g), sq(rp_p), torch.tensor(float(sum(p.numel() for p in rp_p)),
-                                                                               dtype=torch.float64, device=dev)])
+        tot = part.double() + torch.stack([sq(rp_g), sq(rp_p), torch.full((), float(sum(p.numel() for p in rp_p)),
+                                                                             dtype=torch.float64, device=dev)])
         n = tot[2]
         grad_rms = (tot[0].sqrt().float() / n.sqrt().float()).double()
         param_rms = (tot[1].sqrt().float() / n.sqrt().float() + 1e-12).double()
-        lr_t = lr_dev[0] if lr_dev is not None else torch.tensor(float(lr), dtype=torch.float64, device=dev)
+        lr_t = lr_dev[0] if lr_dev is not None else torch.full((), float(lr), dtype=torch.float64, device=dev)
         alpha = rel_step * param_rms / (lr_t * grad_rms + 1e-12)
         alpha = torch.where(alpha > base, alpha, torch.full_like(alpha, base))
         return torch.clamp(alpha, max=base * max_scale)
