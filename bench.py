@@ -1034,7 +1034,9 @@ def main():
                        "scheme": ("data-parallel: graph + tables replicated, global batch N*B, per step one "
                                   "all-gather of the ranks' triplets (rsx.dp)" if dp else
                                   "row-sharded users, replicated items, item partials all-reduced per layer "
-                                  "(rsx.dist)" if sharded else "one GPU")},
+                                  "(rsx.dist)" if sharded else "one GPU"),
+                       **({"dp_issue": "graph replay" if eng.use_graph else "eager (one C-ABI call a step)"}
+                          if dp else {})},
             "fullsort_items_per_s": items_per_s,
             "fullsort": {"eval_users": int(n_eval), "n_items": ni, "k": 50,
                          "s_per_eval": eval_s,

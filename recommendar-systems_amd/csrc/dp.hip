@@ -32,6 +32,8 @@
 // lands and its order are not fixed, and need not be: the sums are integer (below).  Two
 // small launches instead of a radix sort's five (merge-sort passes for these sizes,
 // ~43 us at W = 1 and ~47 at W = 8 on the comm stream: the loss waited on them).
+#include <cmath>
+
 #include "rsx_common.hpp"
 
 namespace rsx {
@@ -178,6 +180,12 @@ __global__ __launch_bounds__(kBlk) void dp_scatter(const int64_t* __restrict__ s
 // norms on the ego rows and max |f| (the fixed-point scale's bound); per-block f64
 // partials, reduced by the last block in a fixed order into the loss, the regulariser's
 // three scales (reg_cnt's tail, as the single-GPU BPR leaves them) and the exponent.
+// A lane group takes kTpg triplets and issues all their row gathers before the first use
+// (the kernel is a chain of dependent loads at ~1 wave a SIMD: the ids, then the rows),
+// which also cuts the blocks, so the last block's partial loads are one round, issued
+// together.
+constexpr int kTpg = 4;  // triplets per lane group in phase A
+
 template <int D>
 __global__ __launch_bounds__(kBlk) void dp_bpr_coef(const int64_t* __restrict__ slots, int32_t W, int64_t cap,
                                                     int64_t n_users, int64_t N, const float* __restrict__ fin,
@@ -188,39 +196,67 @@ __global__ __launch_bounds__(kBlk) void dp_bpr_coef(const int64_t* __restrict__ 
                                                     const int32_t* __restrict__ tag_dev) {
     constexpr int G = D / 4, GPB = kBlk / G;
     const int li = threadIdx.x % G;
-    const int64_t L = 3 * cap + 1;
-    const int64_t b = (int64_t)blockIdx.x * GPB + threadIdx.x / G;  // triplet slot r cap + t
+    const int64_t L = 3 * cap + 1, n_trip = (int64_t)W * cap;
+    const int64_t b0 = ((int64_t)blockIdx.x * GPB + threadIdx.x / G) * kTpg;  // triplet slots r cap + t
     int64_t bg = 0;
     for (int r = 0; r < W; ++r) bg += slots[(int64_t)r * L];
+    int64_t ru[kTpg], rp[kTpg], rn[kTpg];
+#pragma unroll
+    for (int k = 0; k < kTpg; ++k) {
+        ru[k] = -1;
+        const int64_t b = b0 + k;
+        if (b < n_trip) {
+            const int64_t r = b / cap, t = b - r * cap;
+            const int64_t* slot = slots + r * L;
+            if (t < slot[0]) {
+                ru[k] = slot[1 + t];
+                rp[k] = n_users + slot[1 + cap + t];
+                rn[k] = n_users + slot[1 + 2 * cap + t];
+            }
+        }
+    }
+    float4 fu[kTpg], fp[kTpg], fn[kTpg], eu[kTpg], ep[kTpg], en[kTpg];
+#pragma unroll
+    for (int k = 0; k < kTpg; ++k) {
+        if (ru[k] >= 0) {
+            fu[k] = ld4(fin + ru[k] * D + li * 4);
+            fp[k] = ld4(fin + rp[k] * D + li * 4);
+            fn[k] = ld4(fin + rn[k] * D + li * 4);
+            eu[k] = ld4(ego + ru[k] * D + li * 4);
+            ep[k] = ld4(ego + rp[k] * D + li * 4);
+            en[k] = ld4(ego + rn[k] * D + li * 4);
+        } else {
+            fu[k] = fp[k] = fn[k] = eu[k] = ep[k] = en[k] = f4(0.f);
+        }
+    }
     double t_loss = 0.0, t_u = 0.0, t_p = 0.0, t_n = 0.0;
     float t_max = 0.f;
-    if (b < (int64_t)W * cap) {
-        const int64_t r = b / cap, t = b - r * cap;
-        const int64_t* slot = slots + r * L;
-        if (t < slot[0]) {
-            const int64_t u = slot[1 + t], p = n_users + slot[1 + cap + t], n = n_users + slot[1 + 2 * cap + t];
-            const float4 fu = ld4(fin + u * D + li * 4), fp = ld4(fin + p * D + li * 4), fn = ld4(fin + n * D + li * 4);
-            const float4 eu = ld4(ego + u * D + li * 4), ep = ld4(ego + p * D + li * 4), en = ld4(ego + n * D + li * 4);
-            const float sp = group_sum<G>(dot4(fu, fp)), sn = group_sum<G>(dot4(fu, fn));
-            const float delta = sp - sn;
-            const float sg = 1.f / (1.f + expf(-delta));
-            const float term = -logf(1e-10f + sg);
-            const float c = -(sg * (1.f - sg)) / (1e-10f + sg) / (float)bg;
-            if (li == 0) {
-                coef[b] = c;
-                t_loss = (double)term;
-            }
-            t_u = (double)dot4(eu, eu);
-            t_p = (double)dot4(ep, ep);
-            t_n = (double)dot4(en, en);
-            const float m0 = fmaxf(fmaxf(fabsf(fu.x), fabsf(fu.y)), fmaxf(fabsf(fu.z), fabsf(fu.w)));
-            const float m1 = fmaxf(fmaxf(fabsf(fp.x), fabsf(fp.y)), fmaxf(fabsf(fp.z), fabsf(fp.w)));
-            const float m2 = fmaxf(fmaxf(fabsf(fn.x), fabsf(fn.y)), fmaxf(fabsf(fn.z), fabsf(fn.w)));
-            t_max = fmaxf(m0, fmaxf(m1, m2));
-            if (t_max != t_max) t_max = __builtin_huge_valf();  // NaN rows: the scale's clamp below
-        } else if (li == 0) {
-            coef[b] = 0.f;
+#pragma unroll
+    for (int k = 0; k < kTpg; ++k) {
+        const int64_t b = b0 + k;
+        if (b >= n_trip) break;  // (group-uniform)
+        if (ru[k] < 0) {
+            if (li == 0) coef[b] = 0.f;
+            continue;
         }
+        const float sp = group_sum<G>(dot4(fu[k], fp[k])), sn = group_sum<G>(dot4(fu[k], fn[k]));
+        const float delta = sp - sn;
+        const float sg = 1.f / (1.f + expf(-delta));
+        const float term = -logf(1e-10f + sg);
+        const float c = -(sg * (1.f - sg)) / (1e-10f + sg) / (float)bg;
+        if (li == 0) {
+            coef[b] = c;
+            t_loss += (double)term;
+        }
+        t_u += (double)dot4(eu[k], eu[k]);
+        t_p += (double)dot4(ep[k], ep[k]);
+        t_n += (double)dot4(en[k], en[k]);
+        const float m0 = fmaxf(fmaxf(fabsf(fu[k].x), fabsf(fu[k].y)), fmaxf(fabsf(fu[k].z), fabsf(fu[k].w)));
+        const float m1 = fmaxf(fmaxf(fabsf(fp[k].x), fabsf(fp[k].y)), fmaxf(fabsf(fp[k].z), fabsf(fp[k].w)));
+        const float m2 = fmaxf(fmaxf(fabsf(fn[k].x), fabsf(fn[k].y)), fmaxf(fabsf(fn[k].z), fabsf(fn[k].w)));
+        float m = fmaxf(m0, fmaxf(m1, m2));
+        if (m != m) m = __builtin_huge_valf();  // NaN rows: the scale's clamp below
+        t_max = fmaxf(t_max, m);
     }
 #pragma unroll
     for (int o = kWave / 2; o > 0; o >>= 1) {
@@ -230,7 +266,8 @@ __global__ __launch_bounds__(kBlk) void dp_bpr_coef(const int64_t* __restrict__ 
         t_n += __shfl_xor(t_n, o, kWave);
         t_max = fmaxf(t_max, __shfl_xor(t_max, o, kWave));
     }
-    __shared__ double red[kBlk / kWave][5];
+    constexpr int NW = kBlk / kWave;
+    __shared__ double red[NW][5];
     const int wv = threadIdx.x / kWave;
     if (threadIdx.x % kWave == 0) {
         red[wv][0] = t_loss;
@@ -243,7 +280,7 @@ __global__ __launch_bounds__(kBlk) void dp_bpr_coef(const int64_t* __restrict__ 
     __shared__ int last;
     if (threadIdx.x < 5) {
         double v = 0.0;
-        for (int w = 0; w < kBlk / kWave; ++w) v = threadIdx.x == 4 ? fmax(v, red[w][4]) : v + red[w][threadIdx.x];
+        for (int w = 0; w < NW; ++w) v = threadIdx.x == 4 ? fmax(v, red[w][4]) : v + red[w][threadIdx.x];
         __hip_atomic_store(part + (int64_t)blockIdx.x * 5 + threadIdx.x, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     // the partials are stored and read sc1 (agent-scope atomics: write-through, L1 bypassed),
@@ -257,30 +294,50 @@ __global__ __launch_bounds__(kBlk) void dp_bpr_coef(const int64_t* __restrict__ 
     }
     __syncthreads();
     if (!last) return;
-    // the last block: a fixed-order reduction of the per-block partials (every rank the same)
-    __shared__ double tr[5][kBlk];
+    // the last block: a fixed-order reduction of the per-block partials (every rank the same):
+    // thread t sums blocks t, t + kBlk, ... in that order (kU of them loaded at once), then a
+    // fixed shuffle tree per wave and the waves in order
+    constexpr int kU = 4;
     double s[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
-    for (int k = threadIdx.x; k < (int)gridDim.x; k += kBlk) {
-        const double* q = part + (int64_t)k * 5;
+    const int nb = (int)gridDim.x;
+    for (int k0 = threadIdx.x; k0 < nb; k0 += kU * kBlk) {
+        double v[kU][5];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) s[c] += __hip_atomic_load(q + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s[4] = fmax(s[4], __hip_atomic_load(q + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    }
+        for (int j = 0; j < kU; ++j) {
+            const int k = k0 + j * kBlk;
+            const double* q = part + (int64_t)(k < nb ? k : 0) * 5;
 #pragma unroll
-    for (int c = 0; c < 5; ++c) tr[c][threadIdx.x] = s[c];
-    __syncthreads();
-    for (int w = kBlk / 2; w > 0; w >>= 1) {
-        if (threadIdx.x < w) {
-#pragma unroll
-            for (int c = 0; c < 4; ++c) tr[c][threadIdx.x] += tr[c][threadIdx.x + w];
-            tr[4][threadIdx.x] = fmax(tr[4][threadIdx.x], tr[4][threadIdx.x + w]);
+            for (int c = 0; c < 5; ++c) v[j][c] = __hip_atomic_load(q + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < kU; ++j) {
+            if (k0 + j * kBlk >= nb) break;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) s[c] += v[j][c];
+            s[4] = fmax(s[4], v[j][4]);
+        }
     }
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) s[c] += __shfl_xor(s[c], o, kWave);
+        s[4] = fmax(s[4], __shfl_xor(s[4], o, kWave));
+    }
+    __shared__ double tr[NW][5];
+    if (threadIdx.x % kWave == 0) {
+#pragma unroll
+        for (int c = 0; c < 5; ++c) tr[wv][c] = s[c];
+    }
+    __syncthreads();
     if (threadIdx.x == 0) {
+        double r[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+        for (int w = 0; w < NW; ++w) {
+            for (int c = 0; c < 4; ++c) r[c] += tr[w][c];
+            r[4] = fmax(r[4], tr[w][4]);
+        }
         const double B = (double)bg;
-        const double nu = sqrt(tr[1][0]), np = sqrt(tr[2][0]), nn = sqrt(tr[3][0]);
-        const double loss = tr[0][0] / B + (double)reg * (nu + np + nn) / B;
+        const double nu = sqrt(r[1]), np = sqrt(r[2]), nn = sqrt(r[3]);
+        const double loss = r[0] / B + (double)reg * (nu + np + nn) / B;
         float* k = reinterpret_cast<float*>(reg_cnt + 3 * N + 1);
         k[0] = nu > 0 ? (float)((double)reg / (B * nu)) : 0.f;
         k[1] = np > 0 ? (float)((double)reg / (B * np)) : 0.f;
@@ -293,7 +350,7 @@ __global__ __launch_bounds__(kBlk) void dp_bpr_coef(const int64_t* __restrict__ 
         }
         // |G'(x)| <= (3 B occurrences) * (2 max|f| / B) / g_div: the fixed-point scale 2^e keeps
         // every accumulated row below 2^61 (NaN / inf rows: e = 0, the halt flag stops Adam)
-        const double bound = 6.0 * tr[4][0] / (double)g_div;
+        const double bound = 6.0 * r[4] / (double)g_div;
         int e = 0;
         if (bound > 0.0 && bound < 1e300) e = 61 - (int)ceil(log2(bound));
         else if (bound == 0.0) e = 61;
@@ -322,7 +379,7 @@ __global__ __launch_bounds__(kBlk) void dp_bpr_grad(const int64_t* __restrict__ 
                                                     const int32_t* __restrict__ val,
                                                     const int32_t* __restrict__ start,
                                                     const int32_t* __restrict__ cursor, const float* __restrict__ fin,
-                                                    const float* __restrict__ coef, float g_div,
+                                                    const float* __restrict__ coef, float g_div, float g_inv,
                                                     const int32_t* __restrict__ meta,
                                                     unsigned long long* __restrict__ acc, float* __restrict__ gout) {
     constexpr int G = D / 4, GPB = kBlk / G;
@@ -423,7 +480,12 @@ __global__ __launch_bounds__(kBlk) void dp_bpr_grad(const int64_t* __restrict__ 
         } else {
             g = make_float4(c * va[u].x, c * va[u].y, c * va[u].z, c * va[u].w);
         }
-        if (g_div != 1.f) {
+        if (g_inv != 0.f) {  // g_div a power of two: x * 2^-k is x / 2^k rounded the same way
+            g.x *= g_inv;
+            g.y *= g_inv;
+            g.z *= g_inv;
+            g.w *= g_inv;
+        } else if (g_div != 1.f) {
             g.x /= g_div;
             g.y /= g_div;
             g.z /= g_div;
@@ -493,14 +555,16 @@ int dp_loss_kernels(const rsx_dp_lgcn_step& st, const Work& w, int32_t W, hipStr
     const int64_t nu = st.n_users, N = st.n_users + st.n_items, cap = st.cap;
     const int64_t n_trip = (int64_t)W * cap, n_occ = (int64_t)W * 3 * cap;
     const float g_div = (float)(st.n_layers + 1);
-    const int nb_a = (int)((n_trip + GPB - 1) / GPB);
+    int g_exp = 0;
+    const float g_inv = std::frexp(g_div, &g_exp) == 0.5f ? std::ldexp(1.f, 1 - g_exp) : 0.f;  // 1 / g_div if 2^k
+    const int nb_a = (int)((n_trip + GPB * kTpg - 1) / (GPB * kTpg));
     hipLaunchKernelGGL((dp_bpr_coef<D>), dim3(nb_a), dim3(kBlk), 0, s, st.slots, W, cap, nu, N, st.final_emb, st.p,
                        g_div, st.reg, w.coef, w.part, w.meta, st.reg_cnt, st.loss_out, st.loss_acc, st.halt,
                        st.tag_dev);
     DP_TRY(last_rc());
     const int64_t n_chunks = (n_occ + kChunk - 1) / kChunk;
     hipLaunchKernelGGL((dp_bpr_grad<D>), dim3((unsigned)((n_chunks + GPB - 1) / GPB)), dim3(kBlk), 0, s, st.slots,
-                       cap, nu, N, n_occ, w.keys, w.occ, w.start, w.cursor, st.final_emb, w.coef, g_div, w.meta,
+                       cap, nu, N, n_occ, w.keys, w.occ, w.start, w.cursor, st.final_emb, w.coef, g_div, g_inv, w.meta,
                        w.acc, st.g);
     DP_TRY(last_rc());
     hipLaunchKernelGGL((dp_bpr_round<D>), dim3((unsigned)((n_occ + GPB - 1) / GPB)), dim3(kBlk), 0, s, n_occ, w.keys,

@@ -171,7 +171,12 @@ class DataParallelLightGCNEngine:
         st.cap = cap
         st.slots = self.slots.data_ptr()
         st.work, st.work_bytes = self.work.data_ptr(), self.work.numel()
-        self.use_graph = dist.get_backend(group) == "nccl" and os.environ.get("RSX_DP_GRAPH", "1") != "0"
+        # issued eagerly by default: the step is one C-ABI call of ~14 launches, and a replayed
+        # graph measured slower (one real RCCL rank 0.201 vs 0.178 ms a step; latency-injected
+        # W = 2 / 8: 0.206 / 0.234 vs 0.202 / 0.232, profiles/r05/dp/eager_vs_graph/): its
+        # RCCL node, its per-step triplet copy into the captured buffer and the cross-queue
+        # start of its forward branch.  RSX_DP_GRAPH=1 captures it.
+        self.use_graph = dist.get_backend(group) == "nccl" and os.environ.get("RSX_DP_GRAPH", "0") == "1"
         self._graphs = {}
         self._warm = set()
         self._fwd_valid = False

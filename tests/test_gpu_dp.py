@@ -1,10 +1,10 @@
 """Data-parallel LightGCN (rsx.dp, csrc/dp.hip) with the HIP backend.
 
-* 2 and 3 ranks sharing the one GPU of the test box, the step's two all-gathers through
+* 2 and 3 ranks sharing the one GPU of the test box, the step's triplet all-gather through
   the host hook over gloo (RCCL needs one GPU per rank; the 8-GPU RCCL run is the
   driver's): two steps must equal two reference steps (oracle loss + torch.optim.Adam)
   on the global batch, and every replica must stay bit-identical;
-* 1 rank over a real RCCL communicator, graph-captured: the step must equal the
+* 1 rank over a real RCCL communicator, eager and graph-captured: the step must equal the
   single-GPU fused step (rsx_lightgcn_step) on the same triplets.
 """
 import os
@@ -95,9 +95,10 @@ def test_dp_hip_step_matches_global_batch(world, k):
     assert np.isfinite(res[0]["after"]).all()
 
 
-def _rccl_worker(rank, world, port, out_dir, k):
+def _rccl_worker(rank, world, port, out_dir, k, graph="1"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
+    os.environ["RSX_DP_GRAPH"] = graph  # read by the engine's constructor
     torch.cuda.set_device(0)
     dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
     from rsx.dp import DataParallelLightGCNEngine
@@ -125,17 +126,21 @@ def _rccl_worker(rank, world, port, out_dir, k):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("k", [3, 4])
-def test_dp_one_rank_rccl_equals_single_gpu_step(k):
-    """World 1 over RCCL, graph-captured: the same arithmetic as the single-GPU stored-layer
-    step (only the BPR scatter's float atomics order differently run to run)."""
+@pytest.mark.parametrize("k,graph", [(3, "1"), (4, "1"), (3, "0")])
+def test_dp_one_rank_rccl_equals_single_gpu_step(k, graph):
+    """World 1 over RCCL, graph-captured (RSX_DP_GRAPH=1) or issued eagerly (the default):
+    the same arithmetic as the single-GPU stored-layer step (only the BPR scatter's float
+    atomics order differently run to run)."""
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_rccl_worker, args=(1, _free_port(), d, k), nprocs=1, join=True)
+        mp.spawn(_rccl_worker, args=(1, _free_port(), d, k, graph), nprocs=1, join=True)
         z = dict(np.load(os.path.join(d, "rccl.npz")))
     np.testing.assert_allclose(z["la"], z["lb"], rtol=1e-6)
     np.testing.assert_allclose(z["pa"], z["pb"], rtol=0, atol=1e-6)
     np.testing.assert_allclose(z["ma"], z["mb"], rtol=0, atol=1e-7)
-    assert 512 in z["graphs"].tolist()  # full batches replayed from a captured graph
+    if graph == "1":
+        assert 512 in z["graphs"].tolist()  # full batches replayed from a captured graph
+    else:
+        assert z["graphs"].size == 0
 
 
 def _trainer_worker(rank, world, port, root, out):

@@ -1,0 +1,19 @@
+# round 5, eighth GPU batch: the DP step issued eagerly by default (RSX_DP_GRAPH=1 captures
+# it); DP tests (the one-rank RCCL step eager and captured), the DP legs, and an eager
+# kernel trace at a latency-injected W = 8
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp PYTHONFAULTHANDLER=1
+OUT=${OUT:-gpurun_out/r05b8}
+mkdir -p $OUT
+timeout -k 10 500 python -u -m pytest tests/test_gpu_dp.py -m gpu -v --timeout 300 --timeout-method thread \
+  -p no:cacheprovider > $OUT/pytest.log 2>&1
+rc=$?; grep -E "passed|failed|FAILED|Error" $OUT/pytest.log | tail -12; [ $rc -eq 0 ] || exit $rc
+OUT=$OUT PART=dp bash tools/gpu/r05_sims.sh || exit 1
+RSX_COMM_SIM=8 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/trace8 -o t -- \
+  python3 bench.py --dp --steps 60 --warmup 20 --no-cpu-baseline > $OUT/trace8.json 2> $OUT/trace8.err \
+  || { tail -20 $OUT/trace8.err; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/trace1 -o t -- \
+  python3 bench.py --dp --steps 60 --warmup 20 --no-cpu-baseline > $OUT/trace1.json 2> $OUT/trace1.err \
+  || { tail -20 $OUT/trace1.err; exit 1; }
+echo done
