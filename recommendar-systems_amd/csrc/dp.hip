@@ -49,7 +49,6 @@ hipEvent_t collective(rsx_comm_t c, int op, void* buf, int64_t count, int dtype,
 namespace {
 
 constexpr int kBlk = 256;
-constexpr int kChunk = 16;  // sorted occurrences per lane group in the gradient pass
 
 // The step's workspace (rsx_dp_lgcn_step.work), carved in this order, 256-B aligned.
 struct Work {
@@ -180,13 +179,11 @@ __global__ __launch_bounds__(kBlk) void dp_scatter(const int64_t* __restrict__ s
 // norms on the ego rows and max |f| (the fixed-point scale's bound); per-block f64
 // partials, reduced by the last block in a fixed order into the loss, the regulariser's
 // three scales (reg_cnt's tail, as the single-GPU BPR leaves them) and the exponent.
-// A lane group takes kTpg triplets and issues all their row gathers before the first use
-// (the kernel is a chain of dependent loads at ~1 wave a SIMD: the ids, then the rows),
-// which also cuts the blocks, so the last block's partial loads are one round, issued
-// together.
-constexpr int kTpg = 4;  // triplets per lane group in phase A
-
-template <int D>
+// A lane group takes TPG triplets (4 on a large global batch) and issues all their row
+// gathers before the first use (the kernel is a chain of dependent loads at ~1 wave a SIMD:
+// the ids, then the rows), which also cuts the blocks, so the last block's partial loads
+// are one round, issued together; a small batch keeps one triplet a group (more waves).
+template <int D, int TPG>
 __global__ __launch_bounds__(kBlk) void dp_bpr_coef(const int64_t* __restrict__ slots, int32_t W, int64_t cap,
                                                     int64_t n_users, int64_t N, const float* __restrict__ fin,
                                                     const float* __restrict__ ego, float g_div, float reg,
@@ -197,12 +194,12 @@ __global__ __launch_bounds__(kBlk) void dp_bpr_coef(const int64_t* __restrict__ 
     constexpr int G = D / 4, GPB = kBlk / G;
     const int li = threadIdx.x % G;
     const int64_t L = 3 * cap + 1, n_trip = (int64_t)W * cap;
-    const int64_t b0 = ((int64_t)blockIdx.x * GPB + threadIdx.x / G) * kTpg;  // triplet slots r cap + t
+    const int64_t b0 = ((int64_t)blockIdx.x * GPB + threadIdx.x / G) * TPG;  // triplet slots r cap + t
     int64_t bg = 0;
     for (int r = 0; r < W; ++r) bg += slots[(int64_t)r * L];
-    int64_t ru[kTpg], rp[kTpg], rn[kTpg];
+    int64_t ru[TPG], rp[TPG], rn[TPG];
 #pragma unroll
-    for (int k = 0; k < kTpg; ++k) {
+    for (int k = 0; k < TPG; ++k) {
         ru[k] = -1;
         const int64_t b = b0 + k;
         if (b < n_trip) {
@@ -215,9 +212,9 @@ __global__ __launch_bounds__(kBlk) void dp_bpr_coef(const int64_t* __restrict__ 
             }
         }
     }
-    float4 fu[kTpg], fp[kTpg], fn[kTpg], eu[kTpg], ep[kTpg], en[kTpg];
+    float4 fu[TPG], fp[TPG], fn[TPG], eu[TPG], ep[TPG], en[TPG];
 #pragma unroll
-    for (int k = 0; k < kTpg; ++k) {
+    for (int k = 0; k < TPG; ++k) {
         if (ru[k] >= 0) {
             fu[k] = ld4(fin + ru[k] * D + li * 4);
             fp[k] = ld4(fin + rp[k] * D + li * 4);
@@ -232,7 +229,7 @@ __global__ __launch_bounds__(kBlk) void dp_bpr_coef(const int64_t* __restrict__ 
     double t_loss = 0.0, t_u = 0.0, t_p = 0.0, t_n = 0.0;
     float t_max = 0.f;
 #pragma unroll
-    for (int k = 0; k < kTpg; ++k) {
+    for (int k = 0; k < TPG; ++k) {
         const int64_t b = b0 + k;
         if (b >= n_trip) break;  // (group-uniform)
         if (ru[k] < 0) {
@@ -359,7 +356,8 @@ __global__ __launch_bounds__(kBlk) void dp_bpr_coef(const int64_t* __restrict__ 
     }
 }
 
-// Phase B: G' in fixed point.  Lane group c takes run places [c kChunk, (c+1) kChunk):
+// Phase B: G' in fixed point.  Lane group c takes run places [c CH, (c+1) CH) (CH = 16 on a
+// large global batch, 4 on a small one: four times the waves where there are few):
 // each occurrence's term (bpr_fused's f32 arithmetic: coef (f_p - f_n) / g_div for a user,
 // +-coef f_u / g_div for an item) scaled by 2^e and rounded to int64, the terms of a run
 // segment summed in registers.  A run that lies wholly in the chunk (most rows occur once
@@ -373,7 +371,7 @@ __global__ __launch_bounds__(kBlk) void dp_bpr_coef(const int64_t* __restrict__ 
 // store or atomic (gfx9 counts loads, stores and atomics in one vmcnt: a load issued
 // after them would wait for them).  (The per-run atomics of the previous form, one per
 // run and column, cost ~50 us at W = 8.)
-template <int D>
+template <int D, int CH>
 __global__ __launch_bounds__(kBlk) void dp_bpr_grad(const int64_t* __restrict__ slots, int64_t cap, int64_t n_users,
                                                     int64_t N, int64_t n_occ, const int32_t* __restrict__ key,
                                                     const int32_t* __restrict__ val,
@@ -383,10 +381,10 @@ __global__ __launch_bounds__(kBlk) void dp_bpr_grad(const int64_t* __restrict__ 
                                                     const int32_t* __restrict__ meta,
                                                     unsigned long long* __restrict__ acc, float* __restrict__ gout) {
     constexpr int G = D / 4, GPB = kBlk / G;
-    constexpr int KP = (kChunk + G - 1) / G;  // places whose bookkeeping one lane holds
+    constexpr int KP = (CH + G - 1) / G;  // places whose bookkeeping one lane holds
     const int li = threadIdx.x % G;
     const int gl0 = (threadIdx.x % kWave) - li;  // the group's first lane in the wave
-    const int64_t c0 = ((int64_t)blockIdx.x * GPB + threadIdx.x / G) * kChunk;
+    const int64_t c0 = ((int64_t)blockIdx.x * GPB + threadIdx.x / G) * CH;
     const int64_t n_pl = meta[2] < n_occ ? meta[2] : n_occ;  // the run places taken this step
     if (c0 >= n_pl) return;  // group-uniform
     const double S = ldexp(1.0, meta[1]), inv = ldexp(1.0, -meta[1]);
@@ -404,7 +402,7 @@ __global__ __launch_bounds__(kBlk) void dp_bpr_grad(const int64_t* __restrict__ 
         sq[k] = nq[k] = 0;
         aq[k] = bq[k] = -1;
         cq[k] = 0.f;
-        if (q < kChunk && i < n_pl) {
+        if (q < CH && i < n_pl) {
             const int32_t x = key[i];
             const int64_t o = val[i];
             const int64_t r = o / (3 * cap), j = o - r * 3 * cap, kind = j / cap, t = j - kind * cap;
@@ -423,12 +421,12 @@ __global__ __launch_bounds__(kBlk) void dp_bpr_grad(const int64_t* __restrict__ 
             }
         }
     }
-    int32_t xs[kChunk], ss[kChunk], ns[kChunk];
-    float cs[kChunk];
-    bool two[kChunk];
-    float4 va[kChunk], vb[kChunk];
+    int32_t xs[CH], ss[CH], ns[CH];
+    float cs[CH];
+    bool two[CH];
+    float4 va[CH], vb[CH];
 #pragma unroll
-    for (int u = 0; u < kChunk; ++u) {
+    for (int u = 0; u < CH; ++u) {
         const int src = gl0 + u % G, k = u / G;
         xs[u] = __shfl(xq[k], src, kWave);
         ss[u] = __shfl(sq[k], src, kWave);
@@ -459,7 +457,7 @@ __global__ __launch_bounds__(kBlk) void dp_bpr_grad(const int64_t* __restrict__ 
         }
     };
 #pragma unroll
-    for (int u = 0; u < kChunk; ++u) {
+    for (int u = 0; u < CH; ++u) {
         const int32_t x = xs[u];
         if (x >= N) break;  // past the places taken (group-uniform)
         if (x != cur) {
@@ -503,7 +501,7 @@ __global__ __launch_bounds__(kBlk) void dp_bpr_grad(const int64_t* __restrict__ 
 // boundary gets G'[x] = its accumulator / 2^e rounded to f32 and the accumulator cleared;
 // every run's start and cursor are cleared for the next step.
 template <int D>
-__global__ __launch_bounds__(kBlk) void dp_bpr_round(int64_t n_occ, const int32_t* __restrict__ key,
+__global__ __launch_bounds__(kBlk) void dp_bpr_round(int64_t n_occ, int32_t chunk, const int32_t* __restrict__ key,
                                                      int32_t* __restrict__ start, int32_t* __restrict__ cursor,
                                                      const int32_t* __restrict__ meta,
                                                      unsigned long long* __restrict__ acc, float* __restrict__ g) {
@@ -515,7 +513,7 @@ __global__ __launch_bounds__(kBlk) void dp_bpr_round(int64_t n_occ, const int32_
     const int32_t x = key[i];
     if (start[x] - 1 != i) return;  // (a first place clears start[x] below: the others then see 0)
     const int32_t n = cursor[x];
-    if (i / kChunk != (i + n - 1) / kChunk) {  // finished by dp_bpr_grad otherwise
+    if (i / chunk != (i + n - 1) / chunk) {  // finished by dp_bpr_grad otherwise
         const double inv = ldexp(1.0, -meta[1]);
         unsigned long long* q = acc + (int64_t)x * D + li * 4;
         float4 v;
@@ -557,18 +555,32 @@ int dp_loss_kernels(const rsx_dp_lgcn_step& st, const Work& w, int32_t W, hipStr
     const float g_div = (float)(st.n_layers + 1);
     int g_exp = 0;
     const float g_inv = std::frexp(g_div, &g_exp) == 0.5f ? std::ldexp(1.f, 1 - g_exp) : 0.f;  // 1 / g_div if 2^k
-    const int nb_a = (int)((n_trip + GPB * kTpg - 1) / (GPB * kTpg));
-    hipLaunchKernelGGL((dp_bpr_coef<D>), dim3(nb_a), dim3(kBlk), 0, s, st.slots, W, cap, nu, N, st.final_emb, st.p,
-                       g_div, st.reg, w.coef, w.part, w.meta, st.reg_cnt, st.loss_out, st.loss_acc, st.halt,
-                       st.tag_dev);
+    // a small global batch (W = 1, 2 at B = 2048) takes narrower groups: the passes are
+    // chains of dependent loads, and there the waves, not the issue, are few
+    // (RSX_DP_GROUPS: 0 by the batch, 1 narrow, 2 wide -- for the tests of both forms)
+    static const int groups = env_knob("RSX_DP_GROUPS", 0, 0, 2);
+    const bool big = groups ? groups == 2 : n_trip >= 8192;
+    const int tpg = big ? 4 : 1, ch = big ? 16 : 4;
+    const int nb_a = (int)((n_trip + GPB * tpg - 1) / (GPB * tpg));
+    if (big)
+        hipLaunchKernelGGL((dp_bpr_coef<D, 4>), dim3(nb_a), dim3(kBlk), 0, s, st.slots, W, cap, nu, N, st.final_emb,
+                           st.p, g_div, st.reg, w.coef, w.part, w.meta, st.reg_cnt, st.loss_out, st.loss_acc, st.halt,
+                           st.tag_dev);
+    else
+        hipLaunchKernelGGL((dp_bpr_coef<D, 1>), dim3(nb_a), dim3(kBlk), 0, s, st.slots, W, cap, nu, N, st.final_emb,
+                           st.p, g_div, st.reg, w.coef, w.part, w.meta, st.reg_cnt, st.loss_out, st.loss_acc, st.halt,
+                           st.tag_dev);
     DP_TRY(last_rc());
-    const int64_t n_chunks = (n_occ + kChunk - 1) / kChunk;
-    hipLaunchKernelGGL((dp_bpr_grad<D>), dim3((unsigned)((n_chunks + GPB - 1) / GPB)), dim3(kBlk), 0, s, st.slots,
-                       cap, nu, N, n_occ, w.keys, w.occ, w.start, w.cursor, st.final_emb, w.coef, g_div, g_inv, w.meta,
-                       w.acc, st.g);
+    const dim3 gg((unsigned)(((n_occ + ch - 1) / ch + GPB - 1) / GPB));
+    if (big)
+        hipLaunchKernelGGL((dp_bpr_grad<D, 16>), gg, dim3(kBlk), 0, s, st.slots, cap, nu, N, n_occ, w.keys, w.occ,
+                           w.start, w.cursor, st.final_emb, w.coef, g_div, g_inv, w.meta, w.acc, st.g);
+    else
+        hipLaunchKernelGGL((dp_bpr_grad<D, 4>), gg, dim3(kBlk), 0, s, st.slots, cap, nu, N, n_occ, w.keys, w.occ,
+                           w.start, w.cursor, st.final_emb, w.coef, g_div, g_inv, w.meta, w.acc, st.g);
     DP_TRY(last_rc());
-    hipLaunchKernelGGL((dp_bpr_round<D>), dim3((unsigned)((n_occ + GPB - 1) / GPB)), dim3(kBlk), 0, s, n_occ, w.keys,
-                       w.start, w.cursor, w.meta, w.acc, st.g);
+    hipLaunchKernelGGL((dp_bpr_round<D>), dim3((unsigned)((n_occ + GPB - 1) / GPB)), dim3(kBlk), 0, s, n_occ, ch,
+                       w.keys, w.start, w.cursor, w.meta, w.acc, st.g);
     return last_rc();
 }
 

@@ -35,9 +35,10 @@ def _trip(s, r):
     return _local_graph(10 * s + r)[2][:, : 20 - r]  # unequal rank batches
 
 
-def _worker(rank, world, port, out_dir, k):
+def _worker(rank, world, port, out_dir, k, groups="0"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
+    os.environ["RSX_DP_GROUPS"] = groups  # the loss passes' lane-group form (read at the first step)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from rsx.dp import DataParallelLightGCNEngine
 
@@ -66,10 +67,12 @@ def _worker(rank, world, port, out_dir, k):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,k", [(2, 3), (3, 3), (2, 2), (2, 4)])
-def test_dp_hip_step_matches_global_batch(world, k):
+@pytest.mark.parametrize("world,k,groups", [(2, 3, "1"), (3, 3, "2"), (2, 2, "1"), (2, 4, "2"), (2, 3, "2")])
+def test_dp_hip_step_matches_global_batch(world, k, groups):
+    """groups: the loss passes' narrow (1: a triplet / 4 run places a lane group, the small
+    batch form) or wide (2: 4 triplets / 16 places, the large batch form) lane groups."""
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(world, _free_port(), d, k), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, _free_port(), d, k, groups), nprocs=world, join=True)
         res = [dict(np.load(os.path.join(d, f"r{r}.npz"))) for r in range(world)]
     tu, ti, _ = _local_graph(0)
     A = O.lightgcn_norm_adj_vec(tu, ti, NU, NI)
