@@ -412,6 +412,7 @@ class _SmoreLossRows(torch.autograd.Function):
         ctx.cfg = (int(B), float(tau), float(cl))
         parts = out[:2]
         ctx.mark_non_differentiable(parts)
+        ctx.set_materialize_grads(False)  # no zero-filled gradient for the parts (a fill launch)
         return out[2], parts
 
     @staticmethod

@@ -450,12 +450,29 @@ class Trainer:
                 clip_grad_norm_(self.model.parameters(), **self.clip_grad_norm)
             self.optimizer.step()
             return losses, loss
-        loss.backward()
+        self._backward(loss)
         if self.clip_grad_norm:
             clip_grad_norm_(self.model.parameters(), **self.clip_grad_norm)
         self.optimizer.step()
         self._mirror_gradient(loss_func, second)
         return losses, loss
+
+    def _backward(self, loss):
+        """loss.backward() with a cached ones seed for a scalar loss on the device: autograd's
+        own seed is a fill launch per backward (three a mirror-gradient step), and the
+        captured step replays every launch."""
+        if not (torch.is_tensor(loss) and loss.is_cuda and loss.dim() == 0):
+            loss.backward()
+            return
+        key = (loss.device, loss.dtype)
+        seeds = self.__dict__.setdefault("_seeds", {})
+        one = seeds.get(key)
+        if one is None:
+            if _capturing():  # a fill launched inside the capture would be replayed every step
+                loss.backward()
+                return
+            one = seeds[key] = torch.ones((), dtype=loss.dtype, device=loss.device)
+        loss.backward(one)
 
     def _zero_grad(self):
         try:
@@ -491,7 +508,7 @@ class Trainer:
         lr = self.optimizer.param_groups[0].get("lr", 1.0)
         self._zero_grad()
         cur = loss_func(inter)
-        (sum(cur) if isinstance(cur, tuple) else cur).backward()
+        self._backward(sum(cur) if isinstance(cur, tuple) else cur)
         fused = self._mg_fused()
         params, grads = [], []
         for p in m.parameters():
@@ -529,7 +546,7 @@ class Trainer:
         self._zero_grad()
         mir = loss_func(inter)
         mirror = sum(mir) if isinstance(mir, tuple) else mir
-        mirror.backward()
+        self._backward(mirror)
         with torch.no_grad():
             beta = float(getattr(m, "mg_beta", 0.2))
             live = [p.grad for p in m.parameters() if p.requires_grad and p.grad is not None]
