@@ -245,8 +245,11 @@ int rsx_rowwise(int64_t n_rows, int32_t d, const rsx_epilogue* epi, rsx_stream_t
  * NULL for SMORE), loss_out[0] = loss (f32); if loss_acc != NULL, loss is also
  * added into loss_acc[0] (f64, per-epoch accumulator without a host sync).
  * Workspace: rsx_bpr_ws_bytes(B).
+ * RSX_BPR_SMORE_ROWS: RSX_BPR_SMORE on compact batch rows — n_users = B, n_items = 2 B and
+ * triplets (b, b, B + b), so every row of the [3 B, d] g_final is one triplet's: written
+ * (=), not added, and g_final needs no zero fill.
  */
-enum { RSX_BPR_LIGHTGCN = 0, RSX_BPR_LAYERGCN = 1, RSX_BPR_SMORE = 2 };
+enum { RSX_BPR_LIGHTGCN = 0, RSX_BPR_LAYERGCN = 1, RSX_BPR_SMORE = 2, RSX_BPR_SMORE_ROWS = 3 };
 
 size_t rsx_bpr_ws_bytes(int64_t batch);
 int rsx_bpr(int32_t variant, const float* final_emb, const float* ego_emb, int64_t n_users,
@@ -676,6 +679,16 @@ int rsx_smore_infonce_bwd_scaled(const float* side, const float* content, const 
                                  const int64_t* pos_items, int64_t n_users, int64_t batch, int32_t d, float tau,
                                  const float* g_loss, int32_t g_stride, float g_scale, float* g_side,
                                  float* g_content, void* ws, size_t ws_bytes, rsx_stream_t stream);
+/* The backward of the training loss on the compact batch rows ([users; positives;
+ * negatives], 3 batch rows of d; reference src/models/smore.py:366-411): users = positives
+ * = ar = arange(batch), n_users = batch, as rsx_smore_infonce_fwd_total ran them (same ws).
+ * Writes (does not add) g_side / g_content [3 batch, d]: the InfoNCE rows of the users and
+ * positives (each written once), zeros on the negatives' rows; g_all [3 batch, d] =
+ * g_bpr * g_total[0] (the BPR rows' gradient, from rsx_bpr, times the total's upstream
+ * gradient); the InfoNCE part is scaled by g_total[0] * cl.  One launch. */
+int rsx_smore_loss_rows_bwd(const float* side_c, const float* content_c, const int64_t* ar, int64_t batch, int32_t d,
+                            float tau, const float* g_total, float cl, const float* g_bpr, float* g_all,
+                            float* g_side, float* g_content, void* ws, size_t ws_bytes, rsx_stream_t stream);
 /*
  * Model-level mirror gradient (reference src/common/trainer.py:285-336) over `count`
  * (param, grad) pairs of n[i] floats:

@@ -21,6 +21,7 @@ constexpr int kBprBlock = 256;
 
 struct BprArgs {
     int variant;
+    int rows;        // RSX_BPR_SMORE_ROWS: every g_fin row is written by one triplet (stored, not added)
     const float* fin;
     const float* ego;
     int64_t n_users, n_items;
@@ -231,6 +232,12 @@ __global__ __launch_bounds__(kBprBlock) void bpr_bwd(BprArgs a, int n_part) {
             atomicAdd(a.g_ego + p * D + col, kp * a.ego[p * D + col]);
             atomicAdd(a.g_ego + n * D + col, kn * a.ego[n * D + col]);
         }
+        if (a.rows) {
+            a.g_fin[u * D + col] = gu;
+            a.g_fin[p * D + col] = gp;
+            a.g_fin[n * D + col] = gn;
+            continue;
+        }
         atomicAdd(a.g_fin + u * D + col, gu);
         atomicAdd(a.g_fin + p * D + col, gp);
         atomicAdd(a.g_fin + n * D + col, gn);
@@ -434,11 +441,15 @@ int bpr_call(int32_t variant, const float* fin, const float* ego, int64_t n_user
              float* loss_out, double* loss_acc, void* ws, size_t ws_bytes, hipStream_t s, float g_div,
              int32_t* halt, int32_t tag) {
     if (!fin || !trip || !g_fin || batch <= 0 || !ws) return RSX_ERR_ARG;
+    if (variant < 0 || variant > 3) return RSX_ERR_ARG;
+    const int rows = variant == RSX_BPR_SMORE_ROWS;  // SMORE's arithmetic, rows stored
+    if (rows && (n_users != batch || n_items != 2 * batch)) return RSX_ERR_ARG;
+    if (rows) variant = RSX_BPR_SMORE;
     if (variant != RSX_BPR_SMORE && !ego) return RSX_ERR_ARG;
-    if (variant < 0 || variant > 2) return RSX_ERR_ARG;
     if (ws_bytes < bpr_ws(batch)) return RSX_ERR_WORKSPACE;
     BprArgs a = {};
     a.variant = variant;
+    a.rows = rows;
     a.fin = fin;
     a.ego = ego;
     a.n_users = n_users;

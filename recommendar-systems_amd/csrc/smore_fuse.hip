@@ -835,7 +835,39 @@ struct NceArgs {
                              // read by the backward instead of recomputing S (NULL: recompute)
     float* nrmT;             // ws (with E): [2 terms][2 views][ceil(B/16)][D][16] the normalised rows,
                              // each 16-row tile transposed (the backward's MFMA B operand as stored)
+    // backward, the compact batch rows (rsx_smore_loss_rows_bwd): every (term, own row)
+    // destination is distinct, so the rows are stored, not added; and two element-wise jobs
+    // spread over the grid: xo = xg * gloss[0] (xn floats) and z1, z2 zeroed (zn floats each)
+    int32_t rows;
+    const float* xg;
+    float* xo;
+    int64_t xn;
+    float* z1;
+    float* z2;
+    int64_t zn;
 };
+
+// the element-wise jobs of the compact-rows backward, grid-strided over every thread of the
+// launch (uniform no-ops otherwise)
+__device__ __forceinline__ void nce_extra(const NceArgs& a) {
+    if (!a.xo && !a.z1) return;
+    const int64_t nthr = (int64_t)gridDim.x * gridDim.y * gridDim.z * blockDim.x;
+    const int64_t tid =
+        (((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * blockDim.x + threadIdx.x;
+    if (a.xo) {
+        const float sc = a.gloss[0];
+        for (int64_t i = tid; i < a.xn / 4; i += nthr) {
+            const float4 v = ld4(a.xg + 4 * i);
+            st4(a.xo + 4 * i, make_float4(v.x * sc, v.y * sc, v.z * sc, v.w * sc));
+        }
+    }
+    if (a.z1) {
+        for (int64_t i = tid; i < a.zn / 4; i += nthr) {
+            st4(a.z1 + 4 * i, f4(0.f));
+            st4(a.z2 + 4 * i, f4(0.f));
+        }
+    }
+}
 constexpr int64_t kNceStoreMax = 4096;
 
 template <int D>
@@ -973,6 +1005,7 @@ __global__ __launch_bounds__(64 * kNceWaves) void nce_bwd(NceArgs a) {
     constexpr int TILE = 16 * kLd<D>;  // one wave's other-tile copy (rows padded)
     static_assert(kNceWaves * 64 * T * 4 <= kNceWaves * TILE, "reduction fits the tile buffer");
     __shared__ __attribute__((aligned(16))) float sm[kNceWaves * TILE];
+    nce_extra(a);
     const int term = blockIdx.z, mode = blockIdx.y;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
     const int64_t B = a.B;
@@ -1085,6 +1118,11 @@ __global__ __launch_bounds__(64 * kNceWaves) void nce_bwd(NceArgs a) {
         dv = fmap<D>(dn, [](float u) { return u / 1e-12f; });
     }
     float* dst = (mode == 0 ? a.g1 : a.g2) + (a.idx[term][bo] + a.off[term]) * D;
+    if (a.rows) {
+#pragma unroll
+        for (int t = 0; t < T; ++t) st4(dst + 16 * t + 4 * g, make_float4(dv.f[t][0], dv.f[t][1], dv.f[t][2], dv.f[t][3]));
+        return;
+    }
 #pragma unroll
     for (int t = 0; t < T; ++t)
 #pragma unroll
@@ -1106,6 +1144,7 @@ __global__ __launch_bounds__(64 * kNceWaves) void nce_bwd_t(NceArgs a) {
     // waves, same order, so the results are NG = 1's bit for bit)
     constexpr int T = D / 16;
     __shared__ __attribute__((aligned(16))) float red[kNceWaves][16][D];
+    nce_extra(a);
     const int term = blockIdx.z, mode = blockIdx.y;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
     const int64_t B = a.B;
@@ -1232,6 +1271,11 @@ __global__ __launch_bounds__(64 * kNceWaves) void nce_bwd_t(NceArgs a) {
         dv = fmap<D>(dn, [](float u) { return u / 1e-12f; });
     }
     float* dst = (mode == 0 ? a.g1 : a.g2) + (a.idx[term][own] + a.off[term]) * D;
+    if (a.rows) {
+#pragma unroll
+        for (int t = 0; t < T; ++t) st4(dst + 16 * t + 4 * g, make_float4(dv.f[t][0], dv.f[t][1], dv.f[t][2], dv.f[t][3]));
+        return;
+    }
 #pragma unroll
     for (int t = 0; t < T; ++t)
 #pragma unroll
@@ -1780,6 +1824,8 @@ size_t rsx_smore_infonce_ws_bytes(int64_t batch, int32_t d) {
     return (size_t)(4 * batch * d + 4 * batch + 2 * batch + 2 * batch + e) * 4;
 }
 
+static int nce_bwd_launch(sf::NceArgs& a, int64_t batch, int32_t d, hipStream_t s);
+
 static int nce_setup(sf::NceArgs& a, const float* side, const float* content, const int64_t* users,
                      const int64_t* pos_items, int64_t n_users, int64_t batch, int32_t d, float tau, void* ws,
                      size_t ws_bytes) {
@@ -1858,7 +1904,33 @@ int rsx_smore_infonce_bwd_scaled(const float* side, const float* content, const 
     a.gscale = g_scale;
     a.g1 = g_side;
     a.g2 = g_content;
-    hipStream_t s = as_stream(stream);
+    return nce_bwd_launch(a, batch, d, as_stream(stream));
+}
+
+int rsx_smore_loss_rows_bwd(const float* side_c, const float* content_c, const int64_t* ar, int64_t batch, int32_t d,
+                            float tau, const float* g_total, float cl, const float* g_bpr, float* g_all,
+                            float* g_side, float* g_content, void* ws, size_t ws_bytes, rsx_stream_t stream) {
+    sf::NceArgs a{};
+    int rc = nce_setup(a, side_c, content_c, ar, ar, batch, batch, d, tau, ws, ws_bytes);
+    if (rc) return rc;
+    if (!g_total || !g_bpr || !g_all || !g_side || !g_content) return RSX_ERR_ARG;
+    if (batch == 0) return RSX_OK;
+    a.gloss = g_total;
+    a.gstride = 0;
+    a.gscale = cl;
+    a.g1 = g_side;
+    a.g2 = g_content;
+    a.rows = 1;  // rows [users; positives] each written once (ar = arange(batch))
+    a.xg = g_bpr;
+    a.xo = g_all;
+    a.xn = 3 * batch * d;
+    a.z1 = g_side + 2 * batch * d;  // the negatives' rows: no InfoNCE term
+    a.z2 = g_content + 2 * batch * d;
+    a.zn = batch * d;
+    return nce_bwd_launch(a, batch, d, as_stream(stream));
+}
+
+static int nce_bwd_launch(sf::NceArgs& a, int64_t batch, int32_t d, hipStream_t s) {
     const dim3 grid((unsigned)((batch + 15) / 16), 2, 2);
     if (a.E && d == 128) {  // the forward's exp tiles and transposed rows (same workspace, same batch);
         // d = 64 stays on nce_bwd (the transposed-tile form measured no faster there: 95-141 vs 88 us)

@@ -28,6 +28,7 @@ RSX_EPI_ADD = 7
 RSX_BPR_LIGHTGCN = 0
 RSX_BPR_LAYERGCN = 1
 RSX_BPR_SMORE = 2
+RSX_BPR_SMORE_ROWS = 3
 
 _ERRORS = {1001: "RSX_ERR_ARG (bad size or null pointer)",
            1002: "RSX_ERR_UNSUPPORTED (embedding width / k not compiled)",
@@ -180,6 +181,7 @@ def _declare(lib):
         "rsx_smore_infonce_fwd_total": (C.c_int, [P, P, P, P, I64, I64, I32, F32, P, P, F32, P, P, C.c_size_t, P]),
         "rsx_smore_infonce_bwd_scaled": (C.c_int, [P, P, P, P, I64, I64, I32, F32, P, I32, F32, P, P, P, C.c_size_t,
                                                    P]),
+        "rsx_smore_loss_rows_bwd": (C.c_int, [P, P, P, I64, I32, F32, P, F32, P, P, P, P, P, C.c_size_t, P]),
         "rsx_adam_multi": (C.c_int, [I32, P, P, P, P, P, P, F32, F32, F32, F32, F32, P]),
         "rsx_adam_multi_scaled": (C.c_int, [I32, P, P, P, P, P, P, F32, F32, F32, F32, F32, F32, P, P, P]),
         "rsx_adam_multi_mg": (C.c_int, [I32, P, P, P, P, P, P, F32, F32, F32, F32, F32, F32, P, P, P, P, C.c_double,
@@ -224,7 +226,7 @@ EXPORTED = ["rsx_version", "rsx_csr_schedule_host", "rsx_csr_schedule_rebind", "
             "rsx_dp_lightgcn_step", "rsx_dp_work_bytes", "rsx_comm_init_sim", "rsx_comm_sim_seconds",
             "rsx_comm_allgather_f32", "rsx_comm_allreduce_f32_start", "rsx_comm_wait",
             "rsx_smore_gates", "rsx_smore_pref", "rsx_smore_pref_rows", "rsx_smore_pref_rows_occ_floats", "rsx_tag_rows", "rsx_smore_wgrad_ws_bytes", "rsx_smore_wgrad",
-            "rsx_smore_infonce_ws_bytes", "rsx_smore_infonce_fwd", "rsx_smore_infonce_bwd", "rsx_smore_infonce_fwd_total", "rsx_smore_infonce_bwd_scaled", "rsx_adam_multi", "rsx_adam_multi_scaled", "rsx_adam_multi_mg",
+            "rsx_smore_infonce_ws_bytes", "rsx_smore_infonce_fwd", "rsx_smore_infonce_bwd", "rsx_smore_infonce_fwd_total", "rsx_smore_infonce_bwd_scaled", "rsx_smore_loss_rows_bwd", "rsx_adam_multi", "rsx_adam_multi_scaled", "rsx_adam_multi_mg",
             "rsx_smore_unit_weights", "rsx_smore_unit_weights_bwd", "rsx_mg_alpha_ws_bytes", "rsx_mg_alpha",
             "rsx_axpy_multi", "rsx_knn_ws_bytes", "rsx_knn_graph", "rsx_adj_build_ws_bytes", "rsx_adj_build",
             "rsx_edge_dropout_ws_bytes", "rsx_edge_dropout_build", "rsx_nan_gate",

@@ -315,9 +315,9 @@ def bpr(variant: int, final: torch.Tensor, ego: torch.Tensor | None, n_users: in
     B = trip.shape[1]
     d = final.shape[1]
     lib = L.lib()
-    if g_final is None:
-        g_final = torch.zeros_like(final)
-    if g_ego is None and ego is not None and variant != L.RSX_BPR_SMORE:
+    if g_final is None:  # (RSX_BPR_SMORE_ROWS writes every row: no fill)
+        g_final = torch.empty_like(final) if variant == L.RSX_BPR_SMORE_ROWS else torch.zeros_like(final)
+    if g_ego is None and ego is not None and variant not in (L.RSX_BPR_SMORE, L.RSX_BPR_SMORE_ROWS):
         g_ego = torch.zeros_like(ego)
     loss = torch.empty(1, dtype=torch.float32, device=final.device)
     nb = lib.rsx_bpr_ws_bytes(B)

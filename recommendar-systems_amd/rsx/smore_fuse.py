@@ -401,7 +401,8 @@ class _SmoreLossRows(torch.autograd.Function):
     def forward(ctx, all_c, side_c, content_c, trip, ar, B, reg, batch_cfg, cl, tau):
         side_c, content_c = _c(side_c), _c(content_c)
         d = side_c.shape[1]
-        bl, gf, _ = ops.bpr(L.RSX_BPR_SMORE, all_c.contiguous(), None, B, 2 * B, trip, reg, batch_cfg)
+        # compact rows (b, b, B + b): the gradient rows are stored, no zero fill
+        bl, gf, _ = ops.bpr(L.RSX_BPR_SMORE_ROWS, all_c.contiguous(), None, B, 2 * B, trip, reg, batch_cfg)
         lib = L.lib()
         ws = torch.empty(max(int(lib.rsx_smore_infonce_ws_bytes(B, d)), 4), dtype=torch.uint8, device=side_c.device)
         out = torch.empty(3, dtype=torch.float32, device=side_c.device)  # cl_items, cl_users, total
@@ -419,12 +420,17 @@ class _SmoreLossRows(torch.autograd.Function):
     def backward(ctx, g_total, g_parts):
         side_c, content_c, ar, ws, gf = ctx.saved_tensors
         B, tau, cl = ctx.cfg
-        g_all = gf * g_total
-        gsc = torch.zeros(2, *side_c.shape, dtype=torch.float32, device=side_c.device)
+        # one launch: the InfoNCE rows stored (each batch row once), the negatives' rows
+        # zeroed and the BPR rows' gradient times g_total -- no fill or multiply launches
+        if side_c.shape[0] != 3 * B or gf.shape != side_c.shape:
+            raise RuntimeError(f"smore_loss_rows: {tuple(side_c.shape)} side rows, {tuple(gf.shape)} BPR rows for a "
+                               f"batch of {B} (3 B rows each expected)")
+        g_all = torch.empty_like(gf)
+        gsc = torch.empty(2, *side_c.shape, dtype=torch.float32, device=side_c.device)
         gt = g_total.contiguous()
-        L.check(L.lib().rsx_smore_infonce_bwd_scaled(_p(side_c), _p(content_c), _p(ar), _p(ar), B, B,
-                                                     side_c.shape[1], tau, _p(gt), 0, cl, _p(gsc[0]), _p(gsc[1]),
-                                                     _p(ws), ws.numel(), ops._stream()), "rsx_smore_infonce_bwd_scaled")
+        L.check(L.lib().rsx_smore_loss_rows_bwd(_p(side_c), _p(content_c), _p(ar), B, side_c.shape[1], tau, _p(gt), cl,
+                                                _p(gf), _p(g_all), _p(gsc[0]), _p(gsc[1]), _p(ws), ws.numel(),
+                                                ops._stream()), "rsx_smore_loss_rows_bwd")
         return g_all, gsc[0], gsc[1], None, None, None, None, None, None, None
 
 

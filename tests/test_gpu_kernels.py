@@ -111,6 +111,26 @@ def test_bpr_vs_autograd(cuda, golden, variant):
         np.testing.assert_allclose(ge.cpu().numpy(), el.grad.numpy(), rtol=1e-4, atol=1e-7)
 
 
+@pytest.mark.parametrize("d", [64, 128])
+def test_bpr_smore_rows_stores_what_smore_adds(cuda, d):
+    """RSX_BPR_SMORE_ROWS on compact batch rows (triplets (b, b, B + b), n_users = B,
+    n_items = 2B) writes every g_final row: the values RSX_BPR_SMORE adds into zeros,
+    bit for bit, into a buffer that starts as garbage; the same loss; and the variant
+    refuses any other row layout."""
+    B = 300
+    g = torch.Generator().manual_seed(11 + d)
+    fin = (torch.randn(3 * B, d, generator=g) * 0.1).to(cuda)
+    ar = torch.arange(B, device=cuda)
+    trip = torch.stack([ar, ar, ar + B]).contiguous()
+    l0, g0, _ = ops.bpr(L.RSX_BPR_SMORE, fin, None, B, 2 * B, trip, 1e-2, batch_cfg=2048.0)
+    junk = torch.full((3 * B, d), float("nan"), device=cuda)
+    l1, g1, _ = ops.bpr(L.RSX_BPR_SMORE_ROWS, fin, None, B, 2 * B, trip, 1e-2, batch_cfg=2048.0, g_final=junk)
+    assert torch.equal(l0, l1)
+    assert torch.equal(g0 + 0.0, g1 + 0.0)  # (+0.0: a stored -0.0 equals the added +0.0)
+    with pytest.raises(RuntimeError):
+        ops.bpr(L.RSX_BPR_SMORE_ROWS, fin, None, B + 1, 2 * B - 1, trip, 1e-2, batch_cfg=2048.0)
+
+
 def test_adam_vs_torch(cuda):
     g = torch.Generator().manual_seed(3)
     p = torch.randn(300, 64, generator=g)

@@ -486,3 +486,38 @@ def test_adam_multi_mg_equals_axpy_then_adam(cuda):
                   restore=(xs, alpha, 1e-3))
     for x, y in zip(got, ps):
         assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("d", [64, 128])
+def test_loss_rows_backward_one_launch_equals_the_parts(cuda, d):
+    """rsx_smore_loss_rows_bwd (the compact-rows loss backward in one launch) against the
+    parts it replaces: rsx_smore_infonce_bwd_scaled adding into zeros and g_bpr * g_total.
+    The InfoNCE rows equal the added ones bit for bit (stores of the same values; +0.0
+    folds a stored -0.0), the negatives' rows are zero in buffers that start as NaN, and
+    the BPR rows are the same f32 products."""
+    from rsx import _lib as L
+    from rsx import ops
+
+    B = 200
+    g = torch.Generator(device=cuda).manual_seed(d)
+    side = torch.randn(3 * B, d, generator=g, device=cuda)
+    cont = torch.randn(3 * B, d, generator=g, device=cuda)
+    gbpr = torch.randn(3 * B, d, generator=g, device=cuda)
+    gt = torch.tensor([0.75], device=cuda)
+    ar = torch.arange(B, device=cuda)
+    lib, p = L.lib(), ops._p
+    ws = torch.empty(int(lib.rsx_smore_infonce_ws_bytes(B, d)), dtype=torch.uint8, device=cuda)
+    out = torch.empty(3, device=cuda)
+    bl = torch.zeros(1, device=cuda)
+    L.check(lib.rsx_smore_infonce_fwd_total(p(side), p(cont), p(ar), p(ar), B, B, d, 0.2, p(out), p(bl), 0.3,
+                                            p(out[2:]), p(ws), ws.numel(), ops._stream()), "fwd_total")
+    ref = torch.zeros(2, 3 * B, d, device=cuda)
+    L.check(lib.rsx_smore_infonce_bwd_scaled(p(side), p(cont), p(ar), p(ar), B, B, d, 0.2, p(gt), 0, 0.3, p(ref[0]),
+                                             p(ref[1]), p(ws), ws.numel(), ops._stream()), "bwd_scaled")
+    got = torch.full((2, 3 * B, d), float("nan"), device=cuda)
+    gall = torch.full((3 * B, d), float("nan"), device=cuda)
+    L.check(lib.rsx_smore_loss_rows_bwd(p(side), p(cont), p(ar), B, d, 0.2, p(gt), 0.3, p(gbpr), p(gall), p(got[0]),
+                                        p(got[1]), p(ws), ws.numel(), ops._stream()), "loss_rows_bwd")
+    torch.cuda.synchronize()
+    assert torch.equal(got + 0.0, ref + 0.0)
+    assert torch.equal(gall, gbpr * gt)
