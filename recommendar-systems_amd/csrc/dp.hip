@@ -606,11 +606,23 @@ int dp_step(const rsx_dp_lgcn_step& st, hipStream_t s) {
     // dependency across queues costs ~10 us: the slot pack used to sit ahead of it on the
     // compute stream)
     hipStream_t cs = comm_stream(st.comm, s);
+    hipEvent_t fork = nullptr;
     if (cs != s) {
-        hipEvent_t fork = comm_event(st.comm);
+        fork = comm_event(st.comm);
         DP_TRY(hip_rc(hipEventRecord(fork, s)));
-        DP_TRY(hip_rc(hipStreamWaitEvent(cs, fork, 0)));
     }
+    // (2) forward: E^1..E^{K-1} stored -- issued first, so that the GPU starts them while the
+    // host issues the comm branch (its RCCL call among them): a forward issued after the
+    // branch started ~6 us after the previous step's last kernel at one rank
+    float* layers[3] = {st.h0, st.h1, st.s};
+    const float* x = st.p;
+    for (int k = 1; k < K; ++k) {
+        rsx_epilogue e = epi(RSX_EPI_STORE);
+        e.y = layers[k - 1];
+        DP_TRY(spmm_dispatch(A, x, d, e, st.slab, s));
+        x = layers[k - 1];
+    }
+    if (fork) DP_TRY(hip_rc(hipStreamWaitEvent(cs, fork, 0)));
     hipLaunchKernelGGL(dp_pack, dim3((unsigned)((L + kBlk - 1) / kBlk)), dim3(kBlk), 0, cs, st.triplets, B, cap,
                        st.slots + rank * L, st.inc_step ? const_cast<int64_t*>(st.adam.step_dev) : nullptr, w.meta);
     DP_TRY(last_rc());
@@ -631,15 +643,7 @@ int dp_step(const rsx_dp_lgcn_step& st, hipStream_t s) {
         j_sort = comm_event(st.comm);
         DP_TRY(hip_rc(hipEventRecord(j_sort, cs)));
     }
-    // (2) forward: E^1..E^{K-1} stored, the last layer and the mean on the union rows only
-    float* layers[3] = {st.h0, st.h1, st.s};
-    const float* x = st.p;
-    for (int k = 1; k < K; ++k) {
-        rsx_epilogue e = epi(RSX_EPI_STORE);
-        e.y = layers[k - 1];
-        DP_TRY(spmm_dispatch(A, x, d, e, st.slab, s));
-        x = layers[k - 1];
-    }
+    // (2) (issued above) then the last layer and the mean on the union rows only
     if (j_idx) DP_TRY(hip_rc(hipStreamWaitEvent(s, j_idx, 0)));  // the union tags
     {
         rsx_epilogue e = epi(RSX_EPI_FINAL);
