@@ -555,29 +555,35 @@ int dp_loss_kernels(const rsx_dp_lgcn_step& st, const Work& w, int32_t W, hipStr
     const float g_div = (float)(st.n_layers + 1);
     int g_exp = 0;
     const float g_inv = std::frexp(g_div, &g_exp) == 0.5f ? std::ldexp(1.f, 1 - g_exp) : 0.f;  // 1 / g_div if 2^k
-    // a small global batch (W = 1, 2 at B = 2048) takes narrower groups: the passes are
-    // chains of dependent loads, and there the waves, not the issue, are few
-    // (RSX_DP_GROUPS: 0 by the batch, 1 narrow, 2 wide -- for the tests of both forms)
-    static const int groups = env_knob("RSX_DP_GROUPS", 0, 0, 2);
-    const bool big = groups ? groups == 2 : n_trip >= 8192;
-    const int tpg = big ? 4 : 1, ch = big ? 16 : 4;
+    // a smaller global batch takes narrower groups: the passes are chains of dependent
+    // loads, and there the waves, not the issue, are few.  Measured latency-injected at
+    // B = 2048 (profiles/r05/dp/groups/): W = 1, 2 best at 1 triplet / 4 run places a
+    // group, W = 4 at 2 / 8 (0.2040 against 0.2114 ms a step wide), W = 8 at 4 / 16.
+    // (RSX_DP_GROUPS: 0 by the batch, 1 narrow, 2 wide, 3 middle -- for the tests of each
+    // form; RSX_DP_TPG / RSX_DP_CH: 1, 2, 4 triplets / 4, 8, 16 run places, for timing)
+    static const int groups = env_knob("RSX_DP_GROUPS", 0, 0, 3);
+    static const int tpg_knob = env_knob("RSX_DP_TPG", 0, 0, 4), ch_knob = env_knob("RSX_DP_CH", 0, 0, 16);
+    const int form = groups ? groups : n_trip >= 16384 ? 2 : n_trip >= 8192 ? 3 : 1;
+    int tpg = form == 2 ? 4 : form == 3 ? 2 : 1, ch = form == 2 ? 16 : form == 3 ? 8 : 4;
+    if (tpg_knob == 1 || tpg_knob == 2 || tpg_knob == 4) tpg = tpg_knob;
+    if (ch_knob == 4 || ch_knob == 8 || ch_knob == 16) ch = ch_knob;
     const int nb_a = (int)((n_trip + GPB * tpg - 1) / (GPB * tpg));
-    if (big)
-        hipLaunchKernelGGL((dp_bpr_coef<D, 4>), dim3(nb_a), dim3(kBlk), 0, s, st.slots, W, cap, nu, N, st.final_emb,
-                           st.p, g_div, st.reg, w.coef, w.part, w.meta, st.reg_cnt, st.loss_out, st.loss_acc, st.halt,
-                           st.tag_dev);
-    else
-        hipLaunchKernelGGL((dp_bpr_coef<D, 1>), dim3(nb_a), dim3(kBlk), 0, s, st.slots, W, cap, nu, N, st.final_emb,
-                           st.p, g_div, st.reg, w.coef, w.part, w.meta, st.reg_cnt, st.loss_out, st.loss_acc, st.halt,
-                           st.tag_dev);
+#define DP_COEF(T)                                                                                                   \
+    hipLaunchKernelGGL((dp_bpr_coef<D, T>), dim3(nb_a), dim3(kBlk), 0, s, st.slots, W, cap, nu, N, st.final_emb, st.p, \
+                       g_div, st.reg, w.coef, w.part, w.meta, st.reg_cnt, st.loss_out, st.loss_acc, st.halt, st.tag_dev)
+    if (tpg == 4) DP_COEF(4);
+    else if (tpg == 2) DP_COEF(2);
+    else DP_COEF(1);
+#undef DP_COEF
     DP_TRY(last_rc());
     const dim3 gg((unsigned)(((n_occ + ch - 1) / ch + GPB - 1) / GPB));
-    if (big)
-        hipLaunchKernelGGL((dp_bpr_grad<D, 16>), gg, dim3(kBlk), 0, s, st.slots, cap, nu, N, n_occ, w.keys, w.occ,
-                           w.start, w.cursor, st.final_emb, w.coef, g_div, g_inv, w.meta, w.acc, st.g);
-    else
-        hipLaunchKernelGGL((dp_bpr_grad<D, 4>), gg, dim3(kBlk), 0, s, st.slots, cap, nu, N, n_occ, w.keys, w.occ,
-                           w.start, w.cursor, st.final_emb, w.coef, g_div, g_inv, w.meta, w.acc, st.g);
+#define DP_GRAD(C)                                                                                                   \
+    hipLaunchKernelGGL((dp_bpr_grad<D, C>), gg, dim3(kBlk), 0, s, st.slots, cap, nu, N, n_occ, w.keys, w.occ, w.start, \
+                       w.cursor, st.final_emb, w.coef, g_div, g_inv, w.meta, w.acc, st.g)
+    if (ch == 16) DP_GRAD(16);
+    else if (ch == 8) DP_GRAD(8);
+    else DP_GRAD(4);
+#undef DP_GRAD
     DP_TRY(last_rc());
     hipLaunchKernelGGL((dp_bpr_round<D>), dim3((unsigned)((n_occ + GPB - 1) / GPB)), dim3(kBlk), 0, s, n_occ, ch,
                        w.keys, w.start, w.cursor, w.meta, w.acc, st.g);

@@ -308,6 +308,37 @@ __global__ __launch_bounds__(256) void wgrad_reduce_strided(const float* __restr
     if (wave == 0 && e < sz) out[e] = ((q[0][lane] + q[1][lane]) + q[2][lane]) + q[3][lane];
 }
 
+// dW and db of the fused backward in one launch: a slot is sz weight partials followed by
+// out_dim bias partials (stride sz + out_dim), so element e < sz + out_dim of every slot
+// adds up the same way; e < sz goes to dw, the rest to db (wgrad_reduce_strided's order)
+__global__ __launch_bounds__(256) void wgrad_reduce_dwdb(const float* __restrict__ part, int S, int64_t sz,
+                                                         int64_t stride, float* __restrict__ dw,
+                                                         float* __restrict__ db) {
+    __shared__ float q[4][64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t e = (int64_t)blockIdx.x * 64 + lane;
+    const int b = (int)((int64_t)S * wave / 4), en = (int)((int64_t)S * (wave + 1) / 4);
+    float acc = 0.f;
+    if (e < stride) {
+        int p = b;
+        for (; p + 8 <= en; p += 8) {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = part[(int64_t)(p + u) * stride + e];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) acc += v[u];
+        }
+        for (; p < en; ++p) acc += part[(int64_t)p * stride + e];
+    }
+    q[wave][lane] = acc;
+    __syncthreads();
+    if (wave == 0 && e < stride) {
+        const float v = ((q[0][lane] + q[1][lane]) + q[2][lane]) + q[3][lane];
+        if (e < sz) dw[e] = v;
+        else db[e - sz] = v;
+    }
+}
+
 }  // namespace rsx
 
 using namespace rsx;
@@ -374,12 +405,15 @@ extern "C" int rsx_linear_bwd(const float* g, const float* x, const float* W, in
         default: RSX_WGX(1, 1); break;
     }
 #undef RSX_WGX
-    // slots of sz + out_dim floats: dw from the first sz, db from the tails
-    hipLaunchKernelGGL(wgrad_reduce_strided, dim3((unsigned)((sz + 63) / 64)), dim3(256), 0, s, (const float*)part,
-                       p.slots(), sz, sz + (do_db ? out_dim : 0), dw);
-    if (do_db)
-        hipLaunchKernelGGL(wgrad_reduce_strided, dim3((unsigned)((out_dim + 63) / 64)), dim3(256), 0, s,
-                           (const float*)(part + sz), p.slots(), (int64_t)out_dim, sz + out_dim, db);
+    // slots of sz + out_dim floats: dw from the first sz, db from the tails (one launch)
+    if (do_db) {
+        const int64_t st = sz + out_dim;
+        hipLaunchKernelGGL(wgrad_reduce_dwdb, dim3((unsigned)((st + 63) / 64)), dim3(256), 0, s, (const float*)part,
+                           p.slots(), sz, st, dw, db);
+    } else {
+        hipLaunchKernelGGL(wgrad_reduce_strided, dim3((unsigned)((sz + 63) / 64)), dim3(256), 0, s,
+                           (const float*)part, p.slots(), sz, sz, dw);
+    }
     return last_rc();
 }
 

@@ -67,10 +67,12 @@ def _worker(rank, world, port, out_dir, k, groups="0"):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,k,groups", [(2, 3, "1"), (3, 3, "2"), (2, 2, "1"), (2, 4, "2"), (2, 3, "2")])
+@pytest.mark.parametrize("world,k,groups", [(2, 3, "1"), (3, 3, "2"), (2, 2, "1"), (2, 4, "2"), (2, 3, "2"),
+                                           (3, 3, "3"), (2, 4, "3")])
 def test_dp_hip_step_matches_global_batch(world, k, groups):
     """groups: the loss passes' narrow (1: a triplet / 4 run places a lane group, the small
-    batch form) or wide (2: 4 triplets / 16 places, the large batch form) lane groups."""
+    batch form), wide (2: 4 triplets / 16 places, the large batch form) or middle (3: 2 / 8)
+    lane groups."""
     with tempfile.TemporaryDirectory() as d:
         mp.spawn(_worker, args=(world, _free_port(), d, k, groups), nprocs=world, join=True)
         res = [dict(np.load(os.path.join(d, f"r{r}.npz"))) for r in range(world)]
