@@ -19,6 +19,13 @@ namespace rsx {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
+// RSX_LBWD_ABL (timing ablations of the fused backward, tools/build_variant.py only; the
+// product build leaves it 0): 1 skips the dx products, 2 skips the dW products, 3 drops the
+// sched_group_barrier orderings (the compiler's schedule; results unchanged)
+#ifndef RSX_LBWD_ABL
+#define RSX_LBWD_ABL 0
+#endif
+
 constexpr int kWgChunk = 16;         // rows per wave step: 8 MFMA k-steps of 2 rows
 constexpr int kWgTargetWaves = 2048; // two per SIMD (LDS-staged blocks interleave)
 
@@ -183,15 +190,20 @@ __global__ __launch_bounds__(256) void wgrad_partial(const float* __restrict__ g
 #pragma unroll
             for (int q = 0; q < IG; ++q) bv[u][q] = xb[(2 * u + h) * XP + 32 * q];
         }
+        if (!(DX && RSX_LBWD_ABL == 2)) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
+            for (int u = 0; u < 8; ++u)
 #pragma unroll
-            for (int q = 0; q < IG; ++q) acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv[u][q], acc[q], 0, 0, 0);
+                for (int q = 0; q < IG; ++q)
+                    acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv[u][q], acc[q], 0, 0, 0);
+        }
         // every LDS operand read issued before the first MFMA (one latency per step, not
         // one per MFMA pair)
+#if RSX_LBWD_ABL != 3
         __builtin_amdgcn_sched_group_barrier(0x100, 8 + 8 * IG, 0);
         __builtin_amdgcn_sched_group_barrier(0x008, 8 * IG, 0);
-        if constexpr (DX) {
+#endif
+        if constexpr (DX && RSX_LBWD_ABL != 1) {
             if (db_blk) {
 #pragma unroll
                 for (int u = 0; u < 8; ++u) dbacc += av[u];
@@ -222,8 +234,10 @@ __global__ __launch_bounds__(256) void wgrad_partial(const float* __restrict__ g
                     d0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ar[k], br[k], d0, 0, 0, 0);
                     d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ar[k + 1], br[k + 1], d1, 0, 0, 0);
                 }
+#if RSX_LBWD_ABL != 3
                 __builtin_amdgcn_sched_group_barrier(0x100, OC / 2, 0);
                 __builtin_amdgcn_sched_group_barrier(0x008, OC / 4, 0);
+#endif
                 const floatx4_t d = d0 + d1;
                 // lane holds rows 4 q4 + r of the tile, column n16
 #pragma unroll

@@ -14,9 +14,14 @@ out = os.path.join(B.LIBDIR, "variants", name)
 os.makedirs(out, exist_ok=True)
 objs = []
 for src in B.SOURCES:
-    obj = os.path.join(out, src.replace(".hip", ".o"))
-    subprocess.run([B._hipcc(), *B._flags(src), *defs, "-c", os.path.join(B.CSRC, src), "-o", obj], check=True)
+    obj = os.path.join(out, os.path.splitext(src)[0] + ".o")
+    if src.endswith(".cpp"):  # host code, as rsx.build compiles it
+        cmd = [B._hipcc(), "-x", "c++", "-O3", "-fPIC", "-std=c++17", "-pthread", f"-I{B.INCLUDE}", f"-I{B.CSRC}",
+               *defs, "-c", os.path.join(B.CSRC, src), "-o", obj]
+    else:
+        cmd = [B._hipcc(), *B._flags(src), *defs, "-c", os.path.join(B.CSRC, src), "-o", obj]
+    subprocess.run(cmd, check=True)
     objs.append(obj)
-subprocess.run([B._hipcc(), f"--offload-arch={B.ARCH}", "-shared", "-fPIC", "-o", os.path.join(out, "librsx.so"), "-ldl",
-                *objs], check=True)
+subprocess.run([B._hipcc(), f"--offload-arch={B.ARCH}", "-shared", "-fPIC", "-pthread", "-o",
+                os.path.join(out, "librsx.so"), *objs, "-ldl"], check=True)
 print(os.path.join(out, "librsx.so"))
