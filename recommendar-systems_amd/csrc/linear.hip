@@ -97,12 +97,12 @@ __global__ __launch_bounds__(256) void wgrad_partial(const float* __restrict__ g
     constexpr int OC = 32 * OTB, IC = 32 * IG;   // block's o / i columns
     constexpr int CH = kWgChunk * RW;            // rows per block step
     constexpr int GP = OC + 4, XP = IC + 4;      // padded LDS rows
-    constexpr int WP = IC + 16;                  // W slice rows (16x16x4 B reads: 4 rows x 16 banks apart)
+    constexpr int WPT = OC + 4;                  // W^T slice rows (a column of W: o contiguous, 16-B aligned)
     constexpr int NG = CH * OC / 4, NX = CH * IC / 4;  // float4s per step
     constexpr int PER = (NG + NX + 255) / 256;
-    __shared__ float gs[2][CH * GP];
-    __shared__ float xs[2][CH * XP];
-    __shared__ float wl[DX ? OC * WP : 1];
+    __shared__ __attribute__((aligned(16))) float gs[2][CH * GP];
+    __shared__ __attribute__((aligned(16))) float xs[2][CH * XP];
+    __shared__ __attribute__((aligned(16))) float wl[DX ? IC * WPT : 4];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, j = lane & 31, h = lane >> 5;
     const int64_t bo = blockIdx.x % nob, bi = (blockIdx.x / nob) % nib, s = blockIdx.x / (nob * nib);
     const int ob = (int)bo * OC, ib = (int)bi * IC;
@@ -161,15 +161,14 @@ __global__ __launch_bounds__(256) void wgrad_partial(const float* __restrict__ g
         if (nst > 1) gload(1, st[1]);
         sstore(0, st[0]);
     }
-    if constexpr (DX) {  // W[:, ib : ib + IC] (out_dim == OC)
+    if constexpr (DX) {  // W[:, ib : ib + IC]^T (out_dim == OC): wl[col][o], lanes along o
         for (int e = threadIdx.x; e < OC * IC / 4; e += 256) {
-            const int o = e / (IC / 4), c = (e % (IC / 4)) * 4;
+            const int o = e % OC, c = (e / OC) * 4;
             const float4 v = ib + c < in_dim ? ld4(W + (int64_t)o * in_dim + ib + c) : f4(0.f);
-            float* d = wl + o * WP + c;
-            d[0] = v.x;
-            d[1] = v.y;
-            d[2] = v.z;
-            d[3] = v.w;
+            wl[(c + 0) * WPT + o] = v.x;
+            wl[(c + 1) * WPT + o] = v.y;
+            wl[(c + 2) * WPT + o] = v.z;
+            wl[(c + 3) * WPT + o] = v.w;
         }
     }
     __syncthreads();
@@ -209,42 +208,45 @@ __global__ __launch_bounds__(256) void wgrad_partial(const float* __restrict__ g
                 for (int u = 0; u < 8; ++u) dbacc += av[u];
             }
             // dx[CH x IC] = g_chunk[CH x OC] W_slice[OC x IC]: CH/16 x IC/16 tiles of 16x16,
-            // wave w takes tiles w, w + 4, ...; lane (n = lane & 15, q4 = lane >> 4)
+            // wave w takes tiles w, w + 4, ...; lane (n = lane & 15, q4 = lane >> 4).  Each
+            // tile is computed transposed, dx^T = W_slice^T g_chunk^T (A = W^T from the
+            // transposed LDS slice, B = g^T from the chunk), so a lane ends with 4 adjacent
+            // columns of one row (one float4 store, not 4 dword stores); and the K order is
+            // permuted (lane group q4 takes o = q4 OC/4 + k, A and B alike), so a lane's
+            // operands are contiguous: OC/8 ds_read_b128 a tile instead of OC/2 ds_read_b32
             constexpr int NT = (CH / 16) * (IC / 16);
+            constexpr int K4 = OC / 16;  // float4 operand groups per lane
             const int64_t c0 = r0 + c * CH;
             const int n16 = lane & 15, q4 = lane >> 4;
 #pragma unroll 1
             for (int t = wave; t < NT; t += 4) {
                 const int mt = t / (IC / 16), nt = t % (IC / 16);
-                const float* ga = gs[B] + (mt * 16 + n16) * GP + q4;
-                const float* wb = wl + q4 * WP + nt * 16 + n16;
+                const float* gb4 = gs[B] + (mt * 16 + n16) * GP + q4 * (OC / 4);
+                const float* wa4 = wl + (nt * 16 + n16) * WPT + q4 * (OC / 4);
                 typedef float floatx4_t __attribute__((ext_vector_type(4)));
                 floatx4_t d0 = {0.f, 0.f, 0.f, 0.f}, d1 = {0.f, 0.f, 0.f, 0.f};
-                // the tile's OC/4 operand pairs read from LDS ahead of its MFMAs (a read per
-                // MFMA pair waited on one at a time left the 16x16x4 chain latency-bound);
-                // d0 takes k = 0, 8, ..., d1 k = 4, 12, ... as before
-                float ar[OC / 4], br[OC / 4];
+                float4 A4[K4], B4[K4];
 #pragma unroll
-                for (int k = 0; k < OC / 4; ++k) {
-                    ar[k] = ga[4 * k];
-                    br[k] = wb[4 * k * WP];
+                for (int k = 0; k < K4; ++k) {
+                    A4[k] = *reinterpret_cast<const float4*>(wa4 + 4 * k);
+                    B4[k] = *reinterpret_cast<const float4*>(gb4 + 4 * k);
                 }
 #pragma unroll
-                for (int k = 0; k < OC / 4; k += 2) {
-                    d0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ar[k], br[k], d0, 0, 0, 0);
-                    d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ar[k + 1], br[k + 1], d1, 0, 0, 0);
+                for (int k = 0; k < K4; ++k) {
+                    d0 = __builtin_amdgcn_mfma_f32_16x16x4f32(A4[k].x, B4[k].x, d0, 0, 0, 0);
+                    d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(A4[k].y, B4[k].y, d1, 0, 0, 0);
+                    d0 = __builtin_amdgcn_mfma_f32_16x16x4f32(A4[k].z, B4[k].z, d0, 0, 0, 0);
+                    d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(A4[k].w, B4[k].w, d1, 0, 0, 0);
                 }
 #if RSX_LBWD_ABL != 3
-                __builtin_amdgcn_sched_group_barrier(0x100, OC / 2, 0);
-                __builtin_amdgcn_sched_group_barrier(0x008, OC / 4, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 2 * K4, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 4 * K4, 0);
 #endif
                 const floatx4_t d = d0 + d1;
-                // lane holds rows 4 q4 + r of the tile, column n16
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int64_t row = c0 + mt * 16 + 4 * q4 + r;
-                    if (row < r1 && ib + nt * 16 + n16 < in_dim) dx[row * in_dim + ib + nt * 16 + n16] = d[r];
-                }
+                // lane holds columns 4 q4 .. 4 q4 + 3 of the tile, row n16
+                const int64_t row = c0 + mt * 16 + n16;
+                const int col = ib + nt * 16 + 4 * q4;
+                if (row < r1 && col < in_dim) st4(dx + row * in_dim + col, make_float4(d[0], d[1], d[2], d[3]));
             }
         }
         if (c + 1 < nst) sstore(B ^ 1, st[B ^ 1]);
