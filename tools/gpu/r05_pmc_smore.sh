@@ -10,7 +10,7 @@ export TMPDIR=/tmp
 OUT=${OUT:-gpurun_out/r05pmc}
 mkdir -p $OUT
 A="--workload c5 --steps 4 --warmup 2 --no-cpu-baseline"
-RX="pref_bwd_rows|wgrad_part|nce_bwd_t|pref_segsum|linear_bwd|gates_bwd_res|spec_bwd"
+RX=${RX:-"pref_bwd_rows|wgrad_part|nce_bwd_t|pref_segsum|linear_bwd|gates_bwd_res|spec_bwd"}
 timeout -s KILL 60 rocprofv3 -L > $OUT/counters.txt 2>&1 || true
 pass() {  # name, counters
   local name=$1; shift
