@@ -822,12 +822,25 @@ def main():
     gpu_ms = ev0.elapsed_time(ev1)
     per_rank = _rank_report(wall, gpu_ms, args.steps, world, dev)
     rccl_world = None
-    if (sharded or dp) and getattr(eng, "_comm", None) is not None:
+    if (sharded or dp) and getattr(eng, "_comm", None) is not None and (
+            not dp or torch.distributed.get_backend() == "nccl" or sim):
         # the world the step's own communicator spans: an all-reduce of ones on rsx_comm
+        # (the DP engine's host hook -- gloo rehearsals -- moves all-gathers only)
         ones = torch.ones(1, dtype=torch.float32, device=dev)
         L.check(L.lib().rsx_comm_allreduce_f32(eng._comm, ones.data_ptr(), 1, ops._stream()),
                 "rsx_comm_allreduce_f32")
         rccl_world = int(round(float(ones.item())))
+    # data-parallel: the replicas must stay bit-identical with no parameter exchange (§6.1):
+    # an exact integer checksum of every rank's parameter table and Adam moments, compared
+    # across the ranks after the timed steps (outside the timed region)
+    replicas_identical = None
+    if dp and world > 1:
+        ck = torch.stack([t.detach().contiguous().view(torch.int32).to(torch.int64).sum() for t in (eng.p, eng.m, eng.v)])
+        if torch.distributed.get_backend() != "nccl":
+            ck = ck.cpu()
+        cks = [torch.empty_like(ck) for _ in range(world)]
+        torch.distributed.all_gather(cks, ck)
+        replicas_identical = all(torch.equal(cks[0], q) for q in cks[1:])
     t_rank = torch.tensor([wall, float(done["inter"])], dtype=torch.float64, device=dev)
     if world > 1:
         tmax = t_rank[:1].clone()
@@ -1065,6 +1078,7 @@ def main():
             "epoch": epoch_rate,
             "launcher": os.environ.get("RSX_BENCH_LAUNCHER", "torchrun" if world > 1 else "single process"),
             "rccl_world_size": rccl_world,
+            "dp_replicas_bit_identical": replicas_identical,
             "per_rank": per_rank,
             "gpu_ms_per_step_events": gpu_ms / args.steps,
             "train_loss_mean": loss_mean,
