@@ -954,10 +954,26 @@ def main():
         return None
 
     traffic = pmc_bytes("spmm_traffic.json")
+    traffic_note = None
+    if big and d == 256:
+        # C4: the FETCH_SIZE passes of one rank's 1/8 share (1.25M users x 1M items,
+        # profiles/r03/c4/c4_spmm_traffic.json, gfx950-corrected): per STORE product launch,
+        # two products (user rows, item rows) per layer, plus the rows written (the WRITE
+        # pass did not finish: the algorithmic 4 B x rows x d)
+        tfile = os.path.join(HERE, "profiles", "r03", "c4", "c4_spmm_traffic.json")
+        if os.path.exists(tfile) and abs(nu - 1_250_000) <= 1000:
+            try:
+                per = json.load(open(tfile))["per_kind_fetch_bytes_per_launch"]["spmm_main<256, 0>"]
+                traffic = 2 * per + 4.0 * (nu + ni) * d
+                traffic_note = ("PMC FETCH_SIZE of the 1/8-share product launches (profiles/r03/c4/c4_spmm_traffic.json) "
+                                "x 2 products + the written rows")
+            except Exception:  # noqa: BLE001
+                traffic = None
     store = {"bound": "hbm", "kernel": f"spmm_main<{d},STORE> (hub-row fixups in-launch) one propagation layer",
              "launches_per_step": 2 if not sharded else None,
              "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-             "traffic": traffic, "algorithmic_bytes_per_launch": alg, "avg_launch_ms": spmm_ms,
+             "traffic": traffic, **({"traffic_source": traffic_note} if traffic_note else {}),
+             "algorithmic_bytes_per_launch": alg, "avg_launch_ms": spmm_ms,
              "note": ("the sports/baby working set (<50 MB) is Infinity-Cache resident" if not big else
                       "C4 shard: tables of GBs, gathers from HBM")}
     roof, kernels = store, [store]
