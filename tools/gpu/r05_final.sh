@@ -4,7 +4,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-OUT=${OUT:-gpurun_out/r05final2}
+OUT=${OUT:-gpurun_out/r05final3}
 mkdir -p $OUT
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider > $OUT/pytest_gpu.log 2>&1
 rc=$?; grep -E "passed|failed|error" $OUT/pytest_gpu.log | tail -3; [ $rc -eq 0 ] || exit $rc
