@@ -31,11 +31,15 @@ def _free_port():
     return p
 
 
-def _trip(s, r):
-    return _local_graph(10 * s + r)[2][:, : 20 - r]  # unequal rank batches
+def _trip(s, r, hot=False):
+    t = _local_graph(10 * s + r)[2][:, : 20 - r].copy()  # unequal rank batches
+    if hot:  # one positive item for every triplet and one user for half of them: runs of
+        t[1, :] = 0  # equal rows that cross many chunks of the gradient pass
+        t[0, ::2] = 0
+    return t
 
 
-def _worker(rank, world, port, out_dir, k, groups="0"):
+def _worker(rank, world, port, out_dir, k, groups="0", hot=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     os.environ["RSX_DP_GROUPS"] = groups  # the loss passes' lane-group form (read at the first step)
@@ -51,12 +55,18 @@ def _worker(rank, world, port, out_dir, k, groups="0"):
     eng = DataParallelLightGCNEngine(tu, ti, NU, NI, D, k, REG, LR, "cuda:0", U0, I0, batch=32)
     losses, ps = [], []
     for s in range(2):
-        eng.step(torch.from_numpy(_trip(s, rank)).cuda())
+        eng.step(torch.from_numpy(_trip(s, rank, hot)).cuda())
         losses.append(float(eng.loss_out.item()))
         ps.append(eng.p.cpu().numpy())
     # the union's G' rows and counts are cleared after the step
     assert torch.count_nonzero(eng.g).item() == 0
     assert torch.count_nonzero(eng.reg_cnt[:-4]).item() == 0
+    # and the gradient pass's run state (csrc/dp.hip Work: the int64 accumulators and each
+    # row's run start / cursor, carved first, 256-B aligned) is all zero again
+    al = lambda x: (x + 255) & ~255  # noqa: E731
+    n = NU + NI
+    head = al(n * D * 8) + 2 * al(n * 4)
+    assert torch.count_nonzero(eng.work[:head]).item() == 0
     # device-sampled epoch: every rank the same number of slices, all finite
     for j in range(eng.steps_per_epoch()):
         eng.step_index(0, j)
@@ -67,14 +77,17 @@ def _worker(rank, world, port, out_dir, k, groups="0"):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,k,groups", [(2, 3, "1"), (3, 3, "2"), (2, 2, "1"), (2, 4, "2"), (2, 3, "2"),
-                                           (3, 3, "3"), (2, 4, "3")])
-def test_dp_hip_step_matches_global_batch(world, k, groups):
-    """groups: the loss passes' narrow (1: a triplet / 4 run places a lane group, the small
+@pytest.mark.parametrize("world,k,groups,hot", [(2, 3, "1", False), (3, 3, "2", False), (2, 2, "1", False),
+                                               (2, 4, "2", False), (2, 3, "2", False), (3, 3, "3", False),
+                                               (2, 4, "3", False), (2, 3, "1", True), (3, 3, "2", True),
+                                               (2, 3, "3", True)])
+def test_dp_hip_step_matches_global_batch(world, k, groups, hot):
+    """hot: runs of equal rows across many chunks (the gradient pass's last-segment finish).
+    groups: the loss passes' narrow (1: a triplet / 4 run places a lane group, the small
     batch form), wide (2: 4 triplets / 16 places, the large batch form) or middle (3: 2 / 8)
     lane groups."""
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(world, _free_port(), d, k, groups), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, _free_port(), d, k, groups, hot), nprocs=world, join=True)
         res = [dict(np.load(os.path.join(d, f"r{r}.npz"))) for r in range(world)]
     tu, ti, _ = _local_graph(0)
     A = O.lightgcn_norm_adj_vec(tu, ti, NU, NI)
@@ -84,7 +97,7 @@ def test_dp_hip_step_matches_global_batch(world, k, groups):
     opt = torch.optim.Adam([u, i], lr=LR)
     ref_losses, ref_p = [], []
     for s in range(2):
-        trip = torch.from_numpy(np.concatenate([_trip(s, r) for r in range(world)], 1))
+        trip = torch.from_numpy(np.concatenate([_trip(s, r, hot) for r in range(world)], 1))
         opt.zero_grad()
         loss = O.lightgcn_loss(u, i, A, k, trip, REG)
         loss.backward()
