@@ -107,6 +107,35 @@ __global__ __launch_bounds__(kBlk) void dp_pack(const int64_t* __restrict__ trip
     slot[i] = t < B ? trip[k * B + t] : 0;
 }
 
+// one real rank (the slot is the gathered buffer): dp_pack and dp_index in one launch --
+// each occurrence is packed and indexed by the thread that reads it (the same tags and
+// integer counts).  The tag is the Adam counter, which this step increments: here every
+// thread tags with the counter + inc, and dp_alloc, the next launch, does the increment
+// (a thread of this launch may read the counter before or after another one writes it)
+__global__ __launch_bounds__(kBlk) void dp_pack_index(const int64_t* __restrict__ trip, int64_t B, int64_t cap,
+                                                      int64_t n_users, int64_t* __restrict__ slot, int32_t inc,
+                                                      int32_t* __restrict__ meta, int32_t* __restrict__ row_tag,
+                                                      int32_t* __restrict__ reg_cnt,
+                                                      const int32_t* __restrict__ tag_dev) {
+    const int64_t i = (int64_t)blockIdx.x * kBlk + threadIdx.x;
+    if (i > 3 * cap) return;
+    if (i == 0) {
+        slot[0] = B;
+        meta[2] = 0;
+        return;
+    }
+    const int64_t j = i - 1, k = j / cap, t = j - k * cap;
+    if (t >= B) {
+        slot[i] = 0;
+        return;
+    }
+    const int64_t id = trip[k * B + t];
+    slot[i] = id;
+    const int64_t x = k == 0 ? id : n_users + id;
+    row_tag[x] = *tag_dev + inc;
+    atomicAdd(reg_cnt + 3 * x + k, 1);
+}
+
 // occurrence i = (r, j = kind cap + t) of the gathered slots -> its table row (or -1)
 __device__ __forceinline__ int64_t occ_row(const int64_t* slots, int64_t cap, int64_t n_users, int64_t i) {
     const int64_t L = 3 * cap + 1;
@@ -136,9 +165,11 @@ __global__ __launch_bounds__(kBlk) void dp_index(const int64_t* __restrict__ slo
 // (12 us at W = 1, 16 at W = 8)
 __global__ __launch_bounds__(kBlk) void dp_alloc(const int64_t* __restrict__ slots, int32_t W, int64_t cap,
                                                  int64_t n_users, const int32_t* __restrict__ reg_cnt,
-                                                 int32_t* __restrict__ start, int32_t* __restrict__ meta) {
+                                                 int32_t* __restrict__ start, int32_t* __restrict__ meta,
+                                                 int64_t* __restrict__ step) {
     const int64_t i = (int64_t)blockIdx.x * kBlk + threadIdx.x;
     const int lane = threadIdx.x % kWave;
+    if (step && i == 0) step[0] += 1;  // the Adam counter, after dp_pack_index (one real rank)
     int64_t x = -1;
     int32_t n = 0;
     if (i < (int64_t)W * 3 * cap) {
@@ -190,7 +221,9 @@ __global__ __launch_bounds__(kBlk) void dp_bpr_coef(const int64_t* __restrict__ 
                                                     float* __restrict__ coef, double* __restrict__ part,
                                                     int32_t* __restrict__ meta, int32_t* __restrict__ reg_cnt,
                                                     float* loss_out, double* loss_acc, int32_t* halt,
-                                                    const int32_t* __restrict__ tag_dev) {
+                                                    const int32_t* __restrict__ tag_dev,
+                                                    const int32_t* __restrict__ start, int32_t* __restrict__ cursor,
+                                                    int32_t* __restrict__ keys, int32_t* __restrict__ occ) {
     constexpr int G = D / 4, GPB = kBlk / G;
     const int li = threadIdx.x % G;
     const int64_t L = 3 * cap + 1, n_trip = (int64_t)W * cap;
@@ -224,6 +257,17 @@ __global__ __launch_bounds__(kBlk) void dp_bpr_coef(const int64_t* __restrict__ 
             en[k] = ld4(ego + rn[k] * D + li * 4);
         } else {
             fu[k] = fp[k] = fn[k] = eu[k] = ep[k] = en[k] = f4(0.f);
+        }
+    }
+    if (keys && li < 3) {  // one real rank: dp_scatter's places, taken here (lanes 0..2: u, p, n)
+#pragma unroll
+        for (int k = 0; k < TPG; ++k) {
+            if (ru[k] < 0) continue;
+            const int64_t b = b0 + k, r = b / cap, t = b - r * cap;
+            const int64_t x = li == 0 ? ru[k] : li == 1 ? rp[k] : rn[k];
+            const int32_t q = start[x] - 1 + atomicAdd(cursor + x, 1);
+            keys[q] = (int32_t)x;
+            occ[q] = (int32_t)(r * 3 * cap + li * cap + t);
         }
     }
     double t_loss = 0.0, t_u = 0.0, t_p = 0.0, t_n = 0.0;
@@ -548,7 +592,7 @@ rsx_epilogue epi(int kind) {
     } while (0)
 
 template <int D>
-int dp_loss_kernels(const rsx_dp_lgcn_step& st, const Work& w, int32_t W, hipStream_t s) {
+int dp_loss_kernels(const rsx_dp_lgcn_step& st, const Work& w, int32_t W, bool solo, hipStream_t s) {
     constexpr int GPB = kBlk / (D / 4);
     const int64_t nu = st.n_users, N = st.n_users + st.n_items, cap = st.cap;
     const int64_t n_trip = (int64_t)W * cap, n_occ = (int64_t)W * 3 * cap;
@@ -570,7 +614,8 @@ int dp_loss_kernels(const rsx_dp_lgcn_step& st, const Work& w, int32_t W, hipStr
     const int nb_a = (int)((n_trip + GPB * tpg - 1) / (GPB * tpg));
 #define DP_COEF(T)                                                                                                   \
     hipLaunchKernelGGL((dp_bpr_coef<D, T>), dim3(nb_a), dim3(kBlk), 0, s, st.slots, W, cap, nu, N, st.final_emb, st.p, \
-                       g_div, st.reg, w.coef, w.part, w.meta, st.reg_cnt, st.loss_out, st.loss_acc, st.halt, st.tag_dev)
+                       g_div, st.reg, w.coef, w.part, w.meta, st.reg_cnt, st.loss_out, st.loss_acc, st.halt, st.tag_dev, \
+                       w.start, w.cursor, solo ? w.keys : nullptr, w.occ)
     if (tpg == 4) DP_COEF(4);
     else if (tpg == 2) DP_COEF(2);
     else DP_COEF(1);
@@ -612,6 +657,14 @@ int dp_step(const rsx_dp_lgcn_step& st, hipStream_t s) {
     // dependency across queues costs ~10 us: the slot pack used to sit ahead of it on the
     // compute stream)
     hipStream_t cs = comm_stream(st.comm, s);
+    // one real rank: the branch has nothing worth three cross-queue operations to overlap
+    // with (the fork and the two joins idle the compute queue ~20 us, §6.1), so it runs in
+    // line on the compute stream, the all-gather of one slot is the slot itself, the pack
+    // indexes what it packs (dp_pack_index), and the loss pass takes the run places
+    // (dp_bpr_coef; RSX_DP_SOLO=0 keeps the forked branch, for timing)
+    static const int solo_knob = env_knob("RSX_DP_SOLO", 1, 0, 1);
+    const bool solo = solo_knob && sim_w <= 0 && W == 1;
+    if (solo) cs = s;
     hipEvent_t fork = nullptr;
     if (cs != s) {
         fork = comm_event(st.comm);
@@ -629,22 +682,33 @@ int dp_step(const rsx_dp_lgcn_step& st, hipStream_t s) {
         x = layers[k - 1];
     }
     if (fork) DP_TRY(hip_rc(hipStreamWaitEvent(cs, fork, 0)));
-    hipLaunchKernelGGL(dp_pack, dim3((unsigned)((L + kBlk - 1) / kBlk)), dim3(kBlk), 0, cs, st.triplets, B, cap,
-                       st.slots + rank * L, st.inc_step ? const_cast<int64_t*>(st.adam.step_dev) : nullptr, w.meta);
-    DP_TRY(last_rc());
-    if (!collective(st.comm, RSX_COLL_ALLGATHER, st.slots, L * ag, RSX_COLL_I64, cs, &rc)) return rc;
+    int64_t* const step_dev = st.inc_step ? const_cast<int64_t*>(st.adam.step_dev) : nullptr;
     const dim3 go((unsigned)((n_occ + kBlk - 1) / kBlk));
-    hipLaunchKernelGGL(dp_index, go, dim3(kBlk), 0, cs, st.slots, W, cap, nu, st.row_tag, st.reg_cnt, st.tag_dev);
-    DP_TRY(last_rc());
+    if (solo) {
+        hipLaunchKernelGGL(dp_pack_index, dim3((unsigned)((L + kBlk - 1) / kBlk)), dim3(kBlk), 0, s, st.triplets, B,
+                           cap, nu, st.slots, step_dev ? 1 : 0, w.meta, st.row_tag, st.reg_cnt, st.tag_dev);
+        DP_TRY(last_rc());
+    } else {
+        hipLaunchKernelGGL(dp_pack, dim3((unsigned)((L + kBlk - 1) / kBlk)), dim3(kBlk), 0, cs, st.triplets, B, cap,
+                           st.slots + rank * L, step_dev, w.meta);
+        DP_TRY(last_rc());
+        if (!collective(st.comm, RSX_COLL_ALLGATHER, st.slots, L * ag, RSX_COLL_I64, cs, &rc)) return rc;
+        hipLaunchKernelGGL(dp_index, go, dim3(kBlk), 0, cs, st.slots, W, cap, nu, st.row_tag, st.reg_cnt, st.tag_dev);
+        DP_TRY(last_rc());
+    }
     hipEvent_t j_idx = nullptr, j_sort = nullptr;
     if (cs != s) {
         j_idx = comm_event(st.comm);
         DP_TRY(hip_rc(hipEventRecord(j_idx, cs)));
     }
-    hipLaunchKernelGGL(dp_alloc, go, dim3(kBlk), 0, cs, st.slots, W, cap, nu, st.reg_cnt, w.start, w.meta);
+    hipLaunchKernelGGL(dp_alloc, go, dim3(kBlk), 0, cs, st.slots, W, cap, nu, st.reg_cnt, w.start, w.meta,
+                       solo ? step_dev : nullptr);
     DP_TRY(last_rc());
-    hipLaunchKernelGGL(dp_scatter, go, dim3(kBlk), 0, cs, st.slots, W, cap, nu, w.start, w.cursor, w.keys, w.occ);
-    DP_TRY(last_rc());
+    if (!solo) {  // (one real rank: dp_bpr_coef takes the places)
+        hipLaunchKernelGGL(dp_scatter, go, dim3(kBlk), 0, cs, st.slots, W, cap, nu, w.start, w.cursor, w.keys,
+                           w.occ);
+        DP_TRY(last_rc());
+    }
     if (cs != s) {
         j_sort = comm_event(st.comm);
         DP_TRY(hip_rc(hipEventRecord(j_sort, cs)));
@@ -667,10 +731,10 @@ int dp_step(const rsx_dp_lgcn_step& st, hipStream_t s) {
     // (3) the global batch's loss and G' = dL/dfinal / (K+1) on every rank
     if (j_sort) DP_TRY(hip_rc(hipStreamWaitEvent(s, j_sort, 0)));
     switch (d) {
-        case 32: DP_TRY(dp_loss_kernels<32>(st, w, W, s)); break;
-        case 64: DP_TRY(dp_loss_kernels<64>(st, w, W, s)); break;
-        case 128: DP_TRY(dp_loss_kernels<128>(st, w, W, s)); break;
-        case 256: DP_TRY(dp_loss_kernels<256>(st, w, W, s)); break;
+        case 32: DP_TRY(dp_loss_kernels<32>(st, w, W, solo, s)); break;
+        case 64: DP_TRY(dp_loss_kernels<64>(st, w, W, solo, s)); break;
+        case 128: DP_TRY(dp_loss_kernels<128>(st, w, W, solo, s)); break;
+        case 256: DP_TRY(dp_loss_kernels<256>(st, w, W, solo, s)); break;
         default: return RSX_ERR_UNSUPPORTED;
     }
     // (4) backward on the union rows: H = G' + A H from H = G', Adam on g = H^K + R with the

@@ -30,6 +30,13 @@ ARGS="--dp --steps 300 --warmup 30 --no-cpu-baseline"
 run dp_eager_n1 300 RSX_DP_GRAPH=0 || exit 1
 for W in 2 8; do run dp_eager_sim_w$W 300 RSX_DP_GRAPH=0 RSX_COMM_SIM=$W || exit 1; done
 fi
+if [ "${PART:-dp}" = solo ]; then  # one real rank: the comm branch in line vs forked
+ARGS="--dp --steps 300 --warmup 30 --no-cpu-baseline"
+for i in 1 2; do
+  run dp_solo_n1_$i 300 RSX_DP_SOLO=1 || exit 1
+  run dp_forked_n1_$i 300 RSX_DP_SOLO=0 || exit 1
+done
+fi
 if [ "${PART:-dp}" = c5 ]; then
 ARGS="--workload c5 --steps 30 --warmup 6 --no-cpu-baseline"
 run c5_n1 600 RSX_X=0 || exit 1
