@@ -1,10 +1,10 @@
 # round-5 closing evidence: the GPU suite, smoke, the default bench line (with its CPU
 # baseline) and its rocprofv3 kernel stats, the C5 / C3 legs and C5's kernel stats, then the
-# C5 leg under latency injection (tools/gpu/r05_sims.sh PART=c5)
+# C5 leg under latency injection (tools/gpu/r05_sims.sh PART=c5) and the DP legs (PART=dp)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-OUT=${OUT:-gpurun_out/r05final3}
+OUT=${OUT:-gpurun_out/r05final4}
 mkdir -p $OUT
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider > $OUT/pytest_gpu.log 2>&1
 rc=$?; grep -E "passed|failed|error" $OUT/pytest_gpu.log | tail -3; [ $rc -eq 0 ] || exit $rc
@@ -19,5 +19,5 @@ for w in c5 c3; do
 done
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats_c5 -o c5 -- python bench.py --workload c5 --no-cpu-baseline --steps 20 --warmup 6 > $OUT/c5_under_rocprof.json 2> $OUT/c5_prof.err || exit 1
 find $OUT -name '*kernel_trace.csv' -delete
-OUT=$OUT PART=c5 bash tools/gpu/r05_sims.sh || exit 1
+OUT=$OUT PART=c5 bash tools/gpu/r05_sims.sh && OUT=$OUT PART=dp bash tools/gpu/r05_sims.sh || exit 1
 echo done
