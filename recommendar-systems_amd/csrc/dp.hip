@@ -592,7 +592,7 @@ rsx_epilogue epi(int kind) {
     } while (0)
 
 template <int D>
-int dp_loss_kernels(const rsx_dp_lgcn_step& st, const Work& w, int32_t W, bool solo, hipStream_t s) {
+int dp_loss_kernels(const rsx_dp_lgcn_step& st, const Work& w, int32_t W, bool places, hipStream_t s) {
     constexpr int GPB = kBlk / (D / 4);
     const int64_t nu = st.n_users, N = st.n_users + st.n_items, cap = st.cap;
     const int64_t n_trip = (int64_t)W * cap, n_occ = (int64_t)W * 3 * cap;
@@ -615,7 +615,7 @@ int dp_loss_kernels(const rsx_dp_lgcn_step& st, const Work& w, int32_t W, bool s
 #define DP_COEF(T)                                                                                                   \
     hipLaunchKernelGGL((dp_bpr_coef<D, T>), dim3(nb_a), dim3(kBlk), 0, s, st.slots, W, cap, nu, N, st.final_emb, st.p, \
                        g_div, st.reg, w.coef, w.part, w.meta, st.reg_cnt, st.loss_out, st.loss_acc, st.halt, st.tag_dev, \
-                       w.start, w.cursor, solo ? w.keys : nullptr, w.occ)
+                       w.start, w.cursor, places ? w.keys : nullptr, w.occ)
     if (tpg == 4) DP_COEF(4);
     else if (tpg == 2) DP_COEF(2);
     else DP_COEF(1);
@@ -665,6 +665,9 @@ int dp_step(const rsx_dp_lgcn_step& st, hipStream_t s) {
     static const int solo_knob = env_knob("RSX_DP_SOLO", 1, 0, 1);
     const bool solo = solo_knob && sim_w <= 0 && W == 1;
     if (solo) cs = s;
+    // (RSX_DP_PLACES_IN_LOSS=1: the loss pass takes the run places at W > 1 too, for timing)
+    static const int places_knob = env_knob("RSX_DP_PLACES_IN_LOSS", 0, 0, 1);
+    const bool places = solo || places_knob;
     hipEvent_t fork = nullptr;
     if (cs != s) {
         fork = comm_event(st.comm);
@@ -704,7 +707,7 @@ int dp_step(const rsx_dp_lgcn_step& st, hipStream_t s) {
     hipLaunchKernelGGL(dp_alloc, go, dim3(kBlk), 0, cs, st.slots, W, cap, nu, st.reg_cnt, w.start, w.meta,
                        solo ? step_dev : nullptr);
     DP_TRY(last_rc());
-    if (!solo) {  // (one real rank: dp_bpr_coef takes the places)
+    if (!places) {  // (one real rank: dp_bpr_coef takes the places)
         hipLaunchKernelGGL(dp_scatter, go, dim3(kBlk), 0, cs, st.slots, W, cap, nu, w.start, w.cursor, w.keys,
                            w.occ);
         DP_TRY(last_rc());
@@ -731,10 +734,10 @@ int dp_step(const rsx_dp_lgcn_step& st, hipStream_t s) {
     // (3) the global batch's loss and G' = dL/dfinal / (K+1) on every rank
     if (j_sort) DP_TRY(hip_rc(hipStreamWaitEvent(s, j_sort, 0)));
     switch (d) {
-        case 32: DP_TRY(dp_loss_kernels<32>(st, w, W, solo, s)); break;
-        case 64: DP_TRY(dp_loss_kernels<64>(st, w, W, solo, s)); break;
-        case 128: DP_TRY(dp_loss_kernels<128>(st, w, W, solo, s)); break;
-        case 256: DP_TRY(dp_loss_kernels<256>(st, w, W, solo, s)); break;
+        case 32: DP_TRY(dp_loss_kernels<32>(st, w, W, places, s)); break;
+        case 64: DP_TRY(dp_loss_kernels<64>(st, w, W, places, s)); break;
+        case 128: DP_TRY(dp_loss_kernels<128>(st, w, W, places, s)); break;
+        case 256: DP_TRY(dp_loss_kernels<256>(st, w, W, places, s)); break;
         default: return RSX_ERR_UNSUPPORTED;
     }
     // (4) backward on the union rows: H = G' + A H from H = G', Adam on g = H^K + R with the

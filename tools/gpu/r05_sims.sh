@@ -37,6 +37,15 @@ for i in 1 2; do
   run dp_forked_n1_$i 300 RSX_DP_SOLO=0 || exit 1
 done
 fi
+if [ "${PART:-dp}" = places ]; then  # W > 1: the run places taken in the loss pass vs dp_scatter
+ARGS="--dp --steps 300 --warmup 30 --no-cpu-baseline"
+for W in 2 4 8; do
+  run dp_sim_w${W}_inloss 300 RSX_COMM_SIM=$W RSX_DP_PLACES_IN_LOSS=1 || exit 1
+  run dp_sim_w${W}_scatter 300 RSX_COMM_SIM=$W RSX_DP_PLACES_IN_LOSS=0 || exit 1
+  run dp_sim_w${W}_inloss2 300 RSX_COMM_SIM=$W RSX_DP_PLACES_IN_LOSS=1 || exit 1
+  run dp_sim_w${W}_scatter2 300 RSX_COMM_SIM=$W RSX_DP_PLACES_IN_LOSS=0 || exit 1
+done
+fi
 if [ "${PART:-dp}" = c5 ]; then
 ARGS="--workload c5 --steps 30 --warmup 6 --no-cpu-baseline"
 run c5_n1 600 RSX_X=0 || exit 1
