@@ -504,6 +504,15 @@ def load_graph(workload, rank, world, c4_chunks=None, replicated=False):
             "reference split rule), users row-sharded over the ranks, items replicated, B=2048 per rank")
 
 
+def replica_hash(t: torch.Tensor) -> torch.Tensor:
+    """A position-dependent 64-bit hash of a tensor's words (int64 arithmetic wraps):
+    sum_i w_i * (2654435761 i + 1).  A word moved to another index or two differences
+    that cancel in a plain sum change it (the plain sum could not tell)."""
+    w = t.detach().contiguous().view(torch.int32).reshape(-1).to(torch.int64)
+    k = torch.arange(w.numel(), dtype=torch.int64, device=w.device) * 2654435761 + 1
+    return (w * k).sum()
+
+
 def _json_line(out):
     """The one JSON line, on the real stdout (library banners were sent to stderr)."""
     os.write(_STDOUT_FD, (json.dumps(out) + "\n").encode())
@@ -531,12 +540,39 @@ def _init_group(local: int):
         dist.init_process_group(backend)
 
 
-def _free_port():
+def ephemeral_port_range():
+    """The kernel's ephemeral (auto-bind) port range, /proc/sys/net/ipv4/ip_local_port_range."""
+    try:
+        with open("/proc/sys/net/ipv4/ip_local_port_range") as f:
+            lo, hi = (int(x) for x in f.read().split()[:2])
+        return lo, hi
+    except (OSError, ValueError):
+        return 32768, 60999  # the Linux default
+
+
+def rendezvous_port():
+    """MASTER_PORT for the ranks this launcher starts: a free port OUTSIDE the ephemeral
+    range.  A port taken by binding port 0 lies inside that range, so between closing the
+    probe socket and rank 0's TCPStore listen the kernel can hand it to any connect() --
+    including a peer rank's own retrying client, which then connects to itself
+    (GPUTEST_r05: EADDRINUSE).  The kernel never auto-assigns a port outside the range,
+    so only an explicit bind elsewhere could take this one."""
     import socket
 
-    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    lo, hi = ephemeral_port_range()
+    pool = list(range(20000, lo)) if lo > 20000 else list(range(hi + 1, 65536))
+    if not pool:  # the whole port space is ephemeral: nothing better than a probe
+        pool = [29500]
+    start = (os.getpid() * 7919) % len(pool)
+    for k in range(min(len(pool), 256)):
+        p = pool[(start + k) % len(pool)]
+        with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+            try:
+                s.bind(("127.0.0.1", p))
+            except OSError:
+                continue
+        return p
+    return pool[start]
 
 
 def launch(argv, n):
@@ -549,7 +585,7 @@ def launch(argv, n):
     import subprocess
     import tempfile
 
-    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    port = os.environ.get("MASTER_PORT") or str(rendezvous_port())  # an explicit override wins
     out_path = tempfile.mkstemp(prefix="rsx_bench_rank0_", suffix=".json")[1]
     procs = []
     base = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=port, WORLD_SIZE=str(n),
@@ -639,7 +675,8 @@ def dry_run(args):
         _json_line({"metric": METRIC, "value": None, "unit": "interactions/s", "n_gpus": world,
                     "steps": args.steps, "warmup": args.warmup, "ms_per_step": tmax * 1e3 / args.steps,
                     "dry_run": True, "launcher": os.environ.get("RSX_BENCH_LAUNCHER", "external"),
-                    "world_size_observed": int(ones.item()), "per_rank": per_rank})
+                    "world_size_observed": int(ones.item()), "per_rank": per_rank,
+                    "master_port": int(os.environ["MASTER_PORT"]) if "MASTER_PORT" in os.environ else None})
     if world > 1:
         dist.destroy_process_group()
 
@@ -676,6 +713,8 @@ def main():
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU only: exercise the N-rank launch and report (gloo), no GPU work")
     args = ap.parse_args()
+    if os.environ.get("RSX_COMM_SIM"):  # the bench is the latency-injection mode's one user
+        os.environ.setdefault("RSX_COMM_SIM_OPT_IN", "1")
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # no external launcher (torchrun sets WORLD_SIZE): start the N ranks here
         raise SystemExit(launch(sys.argv[1:], args.gpus))
@@ -744,7 +783,7 @@ def main():
 
         if world == 1:  # a one-rank group for the sharded engine
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 1000))
+            os.environ.setdefault("MASTER_PORT", str(rendezvous_port()))
             os.environ.setdefault("RANK", "0")
             os.environ.setdefault("WORLD_SIZE", "1")
         torch.cuda.set_device(local)
@@ -831,11 +870,11 @@ def main():
                 "rsx_comm_allreduce_f32")
         rccl_world = int(round(float(ones.item())))
     # data-parallel: the replicas must stay bit-identical with no parameter exchange (§6.1):
-    # an exact integer checksum of every rank's parameter table and Adam moments, compared
+    # a position-dependent hash of every rank's parameter table and Adam moments, compared
     # across the ranks after the timed steps (outside the timed region)
     replicas_identical = None
     if dp and world > 1:
-        ck = torch.stack([t.detach().contiguous().view(torch.int32).to(torch.int64).sum() for t in (eng.p, eng.m, eng.v)])
+        ck = torch.stack([replica_hash(t) for t in (eng.p, eng.m, eng.v)])
         if torch.distributed.get_backend() != "nccl":
             ck = ck.cpu()
         cks = [torch.empty_like(ck) for _ in range(world)]
@@ -954,25 +993,25 @@ def main():
         return None
 
     traffic = pmc_bytes("spmm_traffic.json")
-    traffic_note = None
+    prior = None
     if big and d == 256:
-        # C4: the FETCH_SIZE passes of one rank's 1/8 share (1.25M users x 1M items,
-        # profiles/r03/c4/c4_spmm_traffic.json, gfx950-corrected): per STORE product launch,
-        # two products (user rows, item rows) per layer, plus the rows written (the WRITE
-        # pass did not finish: the algorithmic 4 B x rows x d)
+        # C4: no PMC pass runs inside this process, so `traffic` stays null; the round-3
+        # FETCH_SIZE passes of one rank's 1/8 share (1.25M users x 1M items, gfx950-corrected;
+        # an older kernel than this HEAD's) are quoted beside it, labelled as such
         tfile = os.path.join(HERE, "profiles", "r03", "c4", "c4_spmm_traffic.json")
         if os.path.exists(tfile) and abs(nu - 1_250_000) <= 1000:
             try:
                 per = json.load(open(tfile))["per_kind_fetch_bytes_per_launch"]["spmm_main<256, 0>"]
-                traffic = 2 * per + 4.0 * (nu + ni) * d
-                traffic_note = ("PMC FETCH_SIZE of the 1/8-share product launches (profiles/r03/c4/c4_spmm_traffic.json) "
-                                "x 2 products + the written rows")
+                prior = {"bytes_per_layer": 2 * per + 4.0 * (nu + ni) * d,
+                         "source": "round-3 PMC FETCH_SIZE of the 1/8-share product launches "
+                                   "(profiles/r03/c4/c4_spmm_traffic.json) x 2 products + the written rows; "
+                                   "measured on the round-3 kernel, not on this HEAD"}
             except Exception:  # noqa: BLE001
-                traffic = None
+                prior = None
     store = {"bound": "hbm", "kernel": f"spmm_main<{d},STORE> (hub-row fixups in-launch) one propagation layer",
              "launches_per_step": 2 if not sharded else None,
              "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-             "traffic": traffic, **({"traffic_source": traffic_note} if traffic_note else {}),
+             "traffic": traffic, **({"traffic_prior_profile": prior} if prior else {}),
              "algorithmic_bytes_per_launch": alg, "avg_launch_ms": spmm_ms,
              "note": ("the sports/baby working set (<50 MB) is Infinity-Cache resident" if not big else
                       "C4 shard: tables of GBs, gathers from HBM")}

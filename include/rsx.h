@@ -247,7 +247,9 @@ int rsx_rowwise(int64_t n_rows, int32_t d, const rsx_epilogue* epi, rsx_stream_t
  * Workspace: rsx_bpr_ws_bytes(B).
  * RSX_BPR_SMORE_ROWS: RSX_BPR_SMORE on compact batch rows — n_users = B, n_items = 2 B and
  * triplets (b, b, B + b), so every row of the [3 B, d] g_final is one triplet's: written
- * (=), not added, and g_final needs no zero fill.
+ * (=), not added, and g_final needs no zero fill. Triplets of any other layout make the
+ * loss NaN (checked on the device, so the NaN halt stops the step; rsx/ops.py only lets
+ * rsx.smore_fuse's compact-rows loss, which builds the triplets itself, request it).
  */
 enum { RSX_BPR_LIGHTGCN = 0, RSX_BPR_LAYERGCN = 1, RSX_BPR_SMORE = 2, RSX_BPR_SMORE_ROWS = 3 };
 

@@ -97,6 +97,12 @@ __global__ __launch_bounds__(kBprBlock) void bpr_fwd(BprArgs a) {
             term = softplus_neg(delta);          // mean over the batch
             coef = -sigmoidf(-delta) / (float)a.batch;
         }
+        // compact rows: bpr_bwd STORES each triplet's three gradient rows, which is only
+        // race-free (and complete) for the layout (b, b, B + b). Any other triplets poison
+        // the loss with NaN, so the NaN halt stops the step instead of leaving racing or
+        // unwritten rows in g_final
+        if (a.rows && (u != b || a.trip[a.batch + b] != b || a.trip[2 * a.batch + b] != a.batch + b))
+            term = __builtin_nanf("");
         // squared norms for the regulariser
         float qu = 0.f, qp = 0.f, qn = 0.f;
         if (a.variant == RSX_BPR_SMORE) {

@@ -88,11 +88,25 @@ def model_busbw_gbs(world: int) -> float:
     return min(world - 1, XGMI_LINKS) * XGMI_LINK_GBS * RING_EFF
 
 
+SIM_OPT_IN = "RSX_COMM_SIM_OPT_IN"  # set to 1 by bench.py and the tests only
+
+
 def sim_comm_params():
     """RSX_COMM_SIM = "W[:busbw_gbs[:latency_us[:blocks]]]": run the one-rank engine over a
-    latency-injected communicator modelling a W-rank job (rsx_comm_init_sim); None if unset."""
+    latency-injected communicator modelling a W-rank job (rsx_comm_init_sim); None if unset.
+
+    The modelled job trains rank 0's share on stand-in peer data (the DP step's other
+    slots hold frozen triplets), so it is a measurement mode, never a training run: it
+    needs the second variable RSX_COMM_SIM_OPT_IN=1, which only bench.py and the tests
+    set.  RSX_COMM_SIM alone (say, left over in a shell) is ignored with a warning."""
     v = os.environ.get("RSX_COMM_SIM")
     if not v:
+        return None
+    if os.environ.get(SIM_OPT_IN) != "1":
+        import warnings
+
+        warnings.warn(f"RSX_COMM_SIM={v} ignored: latency injection is a benchmark mode that trains on "
+                      f"stand-in peer data; set {SIM_OPT_IN}=1 as well to run it", RuntimeWarning, stacklevel=2)
         return None
     f = v.split(":")
     w = int(f[0])
@@ -649,13 +663,26 @@ class ShardedLightGCNEngine:
 
     def check_err(self):
         """Raise if a step's sparse row lists met an out-of-range id or overflowed (bits of
-        rsx_sharded_lgcn_step.err; reading it synchronises the stream)."""
+        rsx_sharded_lgcn_step.err; reading it synchronises the stream).
+
+        The bits depend on each rank's own batches and neighbour lists, so the word is
+        OR-ed over the group first (a MAX all-reduce of each bit) and every rank raises
+        together: a rank raising alone would leave its peers blocked in the next
+        collective.  A collective: every rank calls it at the same point (flush())."""
         err = getattr(self, "err", None)
-        if err is not None and self.native:
+        if err is None or not self.native:
+            return
+        if self.world > 1:
+            bits = (err.to(torch.int64) >> torch.arange(2, device=err.device)) & 1
+            if dist.get_backend(self.group) != "nccl":
+                bits = bits.cpu()
+            dist.all_reduce(bits, op=dist.ReduceOp.MAX, group=self.group)
+            e = int((bits.cpu() << torch.arange(2)).sum())
+        else:
             e = int(err.item())
-            if e:
-                raise RuntimeError(f"sharded LightGCN step: row-list error bits {e:#x} "
-                                   "(1: an item id outside [0, n_items); 2: neighbour list over nbr_cap)")
+        if e:
+            raise RuntimeError(f"sharded LightGCN step: row-list error bits {e:#x} on some rank "
+                               "(1: an item id outside [0, n_items); 2: neighbour list over nbr_cap)")
 
     def forward(self):
         self.flush()

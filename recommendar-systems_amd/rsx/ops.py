@@ -303,11 +303,16 @@ def _ws(device, nbytes: int) -> torch.Tensor:
 def bpr(variant: int, final: torch.Tensor, ego: torch.Tensor | None, n_users: int, n_items: int,
         triplets: torch.Tensor, reg: float, batch_cfg: float | None = None,
         g_final: torch.Tensor | None = None, g_ego: torch.Tensor | None = None,
-        loss_acc: torch.Tensor | None = None):
+        loss_acc: torch.Tensor | None = None, compact_rows: bool = False):
     """Fused BPR loss forward+backward; returns (loss[1], g_final, g_ego).
 
     LightGCN: reference lightgcn.py:132-156; LayerGCN: layergcn.py:142-177; SMORE: smore.py:366-378.
+    RSX_BPR_SMORE_ROWS is internal to rsx.smore_fuse's compact-rows loss (compact_rows=True,
+    triplets (b, b, B + b) it builds itself); the kernel also NaN-poisons any other layout.
     """
+    if (variant == L.RSX_BPR_SMORE_ROWS) != compact_rows:
+        raise RuntimeError("bpr: RSX_BPR_SMORE_ROWS is the compact-rows loss's internal variant "
+                           "(rsx.smore_fuse.smore_loss_rows)")
     _gpu(final, ego, triplets)
     if triplets.dtype != torch.int64 or triplets.dim() != 2 or triplets.shape[0] < 3:
         raise RuntimeError("bpr: triplets must be int64 [3, B]")

@@ -402,7 +402,8 @@ class _SmoreLossRows(torch.autograd.Function):
         side_c, content_c = _c(side_c), _c(content_c)
         d = side_c.shape[1]
         # compact rows (b, b, B + b): the gradient rows are stored, no zero fill
-        bl, gf, _ = ops.bpr(L.RSX_BPR_SMORE_ROWS, all_c.contiguous(), None, B, 2 * B, trip, reg, batch_cfg)
+        bl, gf, _ = ops.bpr(L.RSX_BPR_SMORE_ROWS, all_c.contiguous(), None, B, 2 * B, trip, reg, batch_cfg,
+                            compact_rows=True)
         lib = L.lib()
         ws = torch.empty(max(int(lib.rsx_smore_infonce_ws_bytes(B, d)), 4), dtype=torch.uint8, device=side_c.device)
         out = torch.empty(3, dtype=torch.float32, device=side_c.device)  # cl_items, cl_users, total

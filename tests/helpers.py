@@ -1,8 +1,36 @@
-"""Shared test helpers: fixture decoding and comparisons."""
+"""Shared test helpers: fixture decoding, comparisons and the multi-process rendezvous."""
 from __future__ import annotations
+
+import atexit
+import os
+import shutil
+import tempfile
 
 import numpy as np
 import torch
+
+
+def store_path() -> str:
+    """A fresh rendezvous file for `init_pg` (one per spawned job).
+
+    Spawned tests rendezvous through a torch FileStore, not a TCP port: a port picked by
+    binding port 0 and closing the socket can be taken again before rank 0 listens on it
+    (GPUTEST_r05: EADDRINUSE), and a rank retrying connect to a not-yet-listening
+    ephemeral port can connect to itself. A file cannot race that way."""
+    d = tempfile.mkdtemp(prefix="rsx_pg_")
+    atexit.register(shutil.rmtree, d, True)
+    return os.path.join(d, "store")
+
+
+def init_pg(backend: str, rank: int, world: int, store: str, **kw):
+    """torch.distributed.init_process_group over the FileStore at `store`; RANK and
+    WORLD_SIZE are exported too, as a torchrun launch would (rsx reads WORLD_SIZE)."""
+    import torch.distributed as dist
+
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world))
+    for k in ("MASTER_ADDR", "MASTER_PORT"):
+        os.environ.pop(k, None)
+    dist.init_process_group(backend, init_method="file://" + store, rank=rank, world_size=world, **kw)
 
 
 def coo_from(z, prefix, n):

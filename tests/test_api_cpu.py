@@ -129,3 +129,20 @@ def test_device_metric_dict_falls_back_to_user_order_sums(monkeypatch):
     assert calls == [False, True]
     assert got == float(round(np.float64(state["exact"] / n), 4))
     assert E.sum_order_bound(n, 1.0) < 1e-12
+
+
+def test_latency_injection_needs_the_second_switch(monkeypatch):
+    """RSX_COMM_SIM alone (left over in a shell) must not turn a real run into
+    the benchmark's modelled job (stand-in peer triplets in every step)."""
+    import warnings
+
+    from rsx.dist import sim_comm_params
+
+    monkeypatch.setenv("RSX_COMM_SIM", "4")
+    monkeypatch.delenv("RSX_COMM_SIM_OPT_IN", raising=False)
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        assert sim_comm_params() is None
+    assert any("ignored" in str(x.message) for x in w)
+    monkeypatch.setenv("RSX_COMM_SIM_OPT_IN", "1")
+    assert sim_comm_params()["world"] == 4

@@ -8,7 +8,6 @@ sum_g L_ref(batch_g) on the union graph (reference LightGCN loss per rank
 batch, src/models/lightgcn.py:132-156) followed by torch.optim.Adam.
 """
 import os
-import socket
 import tempfile
 
 import numpy as np
@@ -16,6 +15,7 @@ import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
+from helpers import init_pg, store_path
 
 import rsx_oracle as O
 from rsx import _lib as L
@@ -144,11 +144,9 @@ def _local_graph(rank):
     return tu, ti, trip
 
 
-def _worker(rank, world, port, out_dir, sparse=False, k=K):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
+def _worker(rank, world, store, out_dir, sparse=False, k=K):
     torch.set_num_threads(1)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    init_pg("gloo", rank, world, store)
     from rsx.dist import ShardedLightGCNEngine
 
     torch.manual_seed(7)
@@ -165,13 +163,6 @@ def _worker(rank, world, port, out_dir, sparse=False, k=K):
     dist.destroy_process_group()
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
 
 @pytest.mark.parametrize("world,sparse,k", [(2, False, 3), (2, True, 3), (4, True, 3), (8, True, 3), (8, False, 3),
                                             (2, False, 4), (4, False, 4), (2, True, 2), (2, False, 1)])
@@ -181,7 +172,7 @@ def test_sharded_step_matches_global_objective(world, sparse, k):
     k = 4: the reference's default depth (src/configs/model/LightGCN.yaml:3)."""
     K = k
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(world, _free_port(), d, sparse, k), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, store_path(), d, sparse, k), nprocs=world, join=True)
         res = [dict(np.load(os.path.join(d, f"r{r}.npz"))) for r in range(world)]
     # global graph: users of rank g offset by g*NU
     gu, gi, trips = [], [], []
@@ -220,14 +211,12 @@ def test_sharded_step_matches_global_objective(world, sparse, k):
     assert abs(sum(float(x["loss"][0]) for x in res) - loss.item()) < 1e-5
 
 
-def _slices_worker(rank, world, port, out_dir):
+def _slices_worker(rank, world, store, out_dir):
     """Unequal shards with more steps per epoch than the small shard's batch (the case a
     fixed per-rank batch walked past the shard's end): every rank runs the common step
     count over balanced slices of its own interactions and visits each exactly once."""
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
     torch.set_num_threads(1)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    init_pg("gloo", rank, world, store)
     from rsx.dist import ShardedLightGCNEngine
 
     e_r = [11, 5, 7][rank]
@@ -263,7 +252,7 @@ def _slices_worker(rank, world, port, out_dir):
 def test_balanced_slices_visit_every_interaction_once():
     world = 3
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_slices_worker, args=(world, _free_port(), d), nprocs=world, join=True)
+        mp.spawn(_slices_worker, args=(world, store_path(), d), nprocs=world, join=True)
         res = [dict(np.load(os.path.join(d, f"r{r}.npz"))) for r in range(world)]
     steps = int(res[0]["steps"])
     for r in res:
@@ -289,13 +278,11 @@ def test_slice_bounds_partition(E, S):
         assert b[j][0] <= t < b[j][1]
 
 
-def _dp_worker(rank, world, port, out_dir, k):
+def _dp_worker(rank, world, store, out_dir, k):
     """rsx.dp's data-parallel step (its CPU restatement) on `world` gloo ranks: the
     graph and tables replicated, rank r's own triplets, one global batch per step."""
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
     torch.set_num_threads(1)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    init_pg("gloo", rank, world, store)
     from rsx.dp import DataParallelLightGCNEngine
 
     tu, ti, _ = _local_graph(0)  # one graph for every rank
@@ -320,7 +307,7 @@ def test_data_parallel_step_matches_global_batch(world, k):
     global batch (every rank's triplets concatenated, rank order) of the one graph;
     the replicas stay bit-identical."""
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_dp_worker, args=(world, _free_port(), d, k), nprocs=world, join=True)
+        mp.spawn(_dp_worker, args=(world, store_path(), d, k), nprocs=world, join=True)
         res = [dict(np.load(os.path.join(d, f"r{r}.npz"))) for r in range(world)]
     tu, ti, _ = _local_graph(0)
     A = O.lightgcn_norm_adj_vec(tu, ti, NU, NI)
@@ -342,3 +329,39 @@ def test_data_parallel_step_matches_global_batch(world, k):
         np.testing.assert_allclose(p[:NU], u.detach().numpy(), rtol=0, atol=2e-6)
         np.testing.assert_allclose(p[NU:], i.detach().numpy(), rtol=0, atol=2e-6)
         assert np.array_equal(res[0]["p"], p)  # replicas bit-identical
+
+
+def _err_worker(rank, world, store, out_dir, bad_rank, bits):
+    """ShardedLightGCNEngine.check_err on a rank group where only `bad_rank` holds error
+    bits in its row-list word (its own batch met an out-of-range id, or its neighbour
+    list overflowed)."""
+    from types import SimpleNamespace
+
+    init_pg("gloo", rank, world, store)
+    from rsx.dist import ShardedLightGCNEngine
+
+    me = SimpleNamespace(err=torch.tensor([bits if rank == bad_rank else 0], dtype=torch.int32), native=True,
+                         world=world, group=None)
+    try:
+        ShardedLightGCNEngine.check_err(me)
+        msg = ""
+    except RuntimeError as e:
+        msg = str(e)
+    dist.barrier()  # no rank is left blocked: every rank reaches the next collective
+    with open(os.path.join(out_dir, f"r{rank}.txt"), "w") as f:
+        f.write(msg)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,bad,bits", [(2, 1, 1), (3, 0, 2), (3, 2, 3), (2, 0, 0)])
+def test_row_list_error_raises_on_every_rank(world, bad, bits):
+    """the sticky row-list error word is per rank; check_err ORs it over the
+    group so that all ranks raise together instead of one rank raising while its peers
+    block in the epoch's loss all-reduce."""
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_err_worker, args=(world, store_path(), d, bad, bits), nprocs=world, join=True)
+        msgs = [open(os.path.join(d, f"r{r}.txt")).read() for r in range(world)]
+    if bits == 0:
+        assert msgs == [""] * world
+    else:
+        assert all(f"bits {bits:#x}" in m for m in msgs), msgs

@@ -2,7 +2,6 @@
 test box, collectives over gloo (RCCL needs one GPU per rank; the 8-GPU RCCL run
 is the driver's).  One step must equal the single-process global objective."""
 import os
-import socket
 import tempfile
 
 import numpy as np
@@ -10,6 +9,7 @@ import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
+from helpers import init_pg, store_path
 
 import rsx_oracle as O
 from test_dist_gloo import D, K, LR, NI, NU, REG, _local_graph
@@ -17,13 +17,11 @@ from test_dist_gloo import D, K, LR, NI, NU, REG, _local_graph
 pytestmark = pytest.mark.gpu
 
 
-def _worker(rank, world, port, out_dir, native, sparse, k=K, fused=True, head=None):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
+def _worker(rank, world, store, out_dir, native, sparse, k=K, fused=True, head=None):
     os.environ["RSX_SHARDED_FUSED"] = "1" if fused else "0"
     if head is not None:  # the step's first item partial in `head` row pieces (rsx_sharded_lgcn_step.n_head)
         os.environ["RSX_SHARDED_HEAD"] = str(head)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    init_pg("gloo", rank, world, store)
     from rsx.dist import ShardedLightGCNEngine
 
     torch.manual_seed(7)
@@ -54,13 +52,6 @@ def _worker(rank, world, port, out_dir, native, sparse, k=K, fused=True, head=No
     dist.destroy_process_group()
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
 
 @pytest.mark.parametrize("native,sparse,k,fused", [(False, False, 3, True), (True, False, 3, True),
                                                    (True, False, 3, False), (True, False, 2, True),
@@ -81,7 +72,7 @@ def test_sharded_hip_step_matches_global_objective(native, sparse, k, fused):
     if fused == "head3":
         fused, head = False, 3
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(world, _free_port(), d, native, sparse, k, fused, head), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, store_path(), d, native, sparse, k, fused, head), nprocs=world, join=True)
         res = [dict(np.load(os.path.join(d, f"r{r}.npz"))) for r in range(world)]
     gu, gi, trips = [], [], []
     for r in range(world):
@@ -115,12 +106,10 @@ def test_sharded_hip_step_matches_global_objective(native, sparse, k, fused):
     assert np.isfinite(res[0]["after"]).all()
 
 
-def _native_worker(rank, world, port, out_dir, SPARSE=True):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
+def _native_worker(rank, world, store, out_dir, SPARSE=True):
     os.environ["RSX_SHARDED_FUSED"] = "0" if SPARSE else "1"  # dense: the fused-round schedule, graph-captured
     torch.cuda.set_device(0)
-    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    init_pg("nccl", rank, world, store, device_id=torch.device("cuda", 0))
     from rsx.dist import ShardedLightGCNEngine
 
     torch.manual_seed(7)
@@ -182,7 +171,7 @@ def test_native_sharded_step_equals_python_sequence(sparse):
     bit, training within 1e-5.  sparse: the sparse schedule's collectives (all-gather,
     reduce-scatter); dense: the fused-round schedule, graph-captured too."""
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_native_worker, args=(1, _free_port(), d, sparse), nprocs=1, join=True)
+        mp.spawn(_native_worker, args=(1, store_path(), d, sparse), nprocs=1, join=True)
         z = dict(np.load(os.path.join(d, "native.npz")))
     # forward before any step: same kernels, same order -> bit-identical; after the
     # steps the BPR gradient scatter's float atomics (duplicate rows in a batch, as the
@@ -197,17 +186,15 @@ def test_native_sharded_step_equals_python_sequence(sparse):
     assert np.isfinite(z["True_1"]).all()
 
 
-def _sim_worker(rank, world, port, out_dir):
+def _sim_worker(rank, world, store, out_dir):
     """The one-rank sharded engine over the latency-injected communicator (RSX_COMM_SIM):
     every collective is the one-rank identity plus a comm-stream kernel holding the
     modelled time, so the trained tables equal the plain one-rank engine's and the step
     takes at least the modelled exchange time."""
     import time
 
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
     torch.cuda.set_device(0)
-    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    init_pg("nccl", rank, world, store, device_id=torch.device("cuda", 0))
     from rsx import _lib as L
     from rsx.dist import ShardedLightGCNEngine
 
@@ -216,6 +203,7 @@ def _sim_worker(rank, world, port, out_dir):
     U0 = torch.nn.init.xavier_uniform_(torch.empty(NU, D)).numpy()
     tu, ti, trip = _local_graph(0)
     out = {}
+    os.environ["RSX_COMM_SIM_OPT_IN"] = "1"  # the benchmark mode's second switch (rsx.dist.sim_comm_params)
     for sim in (None, "4:1.0:200"):  # 4 ranks at 1 GB/s bus bandwidth + 200 us per collective
         if sim:
             os.environ["RSX_COMM_SIM"] = sim
@@ -244,7 +232,7 @@ def _sim_worker(rank, world, port, out_dir):
 
 def test_latency_injected_comm_is_data_identity_and_takes_the_modelled_time():
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_sim_worker, args=(1, _free_port(), d), nprocs=1, join=True)
+        mp.spawn(_sim_worker, args=(1, store_path(), d), nprocs=1, join=True)
         z = dict(np.load(os.path.join(d, "sim.npz")))
     np.testing.assert_allclose(z["p_True"], z["p_False"], rtol=0, atol=1e-6)
     # model: 2 (W-1)/W X / busbw + latency for an all-reduce of the item block X
@@ -286,19 +274,18 @@ def _hub_batches(tu, ti, n=6, B=16):
     return out
 
 
-def _order_worker(rank, world, port, out_dir):
+def _order_worker(rank, world, store, out_dir):
     """The sparse native step over the POISONED latency-injected communicator (every
     collective's buffer reads NaN / id -1 for its modelled time, then is restored): each
     combination of the owner-Adam placement and the deferred all-gather, graph-replayed
     and eager, with the comm stream at the greatest priority."""
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
     os.environ["RSX_COMM_SIM"] = "4:1.0:100"  # 4 modelled ranks, 1 GB/s, 100 us per collective
+    os.environ["RSX_COMM_SIM_OPT_IN"] = "1"
     os.environ["RSX_COMM_SIM_POISON"] = "1"
     os.environ["RSX_COMM_PRIORITY"] = "1"
     os.environ.pop("RSX_COMM_SIM_SHARE", None)
     torch.cuda.set_device(0)
-    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    init_pg("nccl", rank, world, store, device_id=torch.device("cuda", 0))
     from rsx.dist import ShardedLightGCNEngine
 
     torch.manual_seed(7)
@@ -340,7 +327,7 @@ def test_sparse_step_stream_order_under_poisoned_collectives():
     the neighbour list holds each distinct batch user once (a repeated hub
     user overflowed nbr_cap)."""
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_order_worker, args=(1, _free_port(), d), nprocs=1, join=True)
+        mp.spawn(_order_worker, args=(1, store_path(), d), nprocs=1, join=True)
         z = dict(np.load(os.path.join(d, "order.npz")))
     tu, ti = _hub_graph()
     A = O.lightgcn_norm_adj_vec(tu, ti, NU, NI)

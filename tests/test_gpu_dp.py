@@ -8,7 +8,6 @@
   single-GPU fused step (rsx_lightgcn_step) on the same triplets.
 """
 import os
-import socket
 import tempfile
 
 import numpy as np
@@ -16,19 +15,13 @@ import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
+from helpers import init_pg, store_path
 
 import rsx_oracle as O
 from test_dist_gloo import D, LR, NI, NU, REG, _local_graph
 
 pytestmark = pytest.mark.gpu
 
-
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
 
 
 def _trip(s, r, hot=False):
@@ -39,11 +32,9 @@ def _trip(s, r, hot=False):
     return t
 
 
-def _worker(rank, world, port, out_dir, k, groups="0", hot=False):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
+def _worker(rank, world, store, out_dir, k, groups="0", hot=False):
     os.environ["RSX_DP_GROUPS"] = groups  # the loss passes' lane-group form (read at the first step)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    init_pg("gloo", rank, world, store)
     from rsx.dp import DataParallelLightGCNEngine
 
     tu, ti, _ = _local_graph(0)
@@ -87,7 +78,7 @@ def test_dp_hip_step_matches_global_batch(world, k, groups, hot):
     batch form), wide (2: 4 triplets / 16 places, the large batch form) or middle (3: 2 / 8)
     lane groups."""
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(world, _free_port(), d, k, groups, hot), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, store_path(), d, k, groups, hot), nprocs=world, join=True)
         res = [dict(np.load(os.path.join(d, f"r{r}.npz"))) for r in range(world)]
     tu, ti, _ = _local_graph(0)
     A = O.lightgcn_norm_adj_vec(tu, ti, NU, NI)
@@ -113,12 +104,10 @@ def test_dp_hip_step_matches_global_batch(world, k, groups, hot):
     assert np.isfinite(res[0]["after"]).all()
 
 
-def _rccl_worker(rank, world, port, out_dir, k, graph="1"):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
+def _rccl_worker(rank, world, store, out_dir, k, graph="1", hot=False):
     os.environ["RSX_DP_GRAPH"] = graph  # read by the engine's constructor
     torch.cuda.set_device(0)
-    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    init_pg("nccl", rank, world, store, device_id=torch.device("cuda", 0))
     from rsx.dp import DataParallelLightGCNEngine
     from rsx.engine import LightGCNEngine
 
@@ -129,6 +118,10 @@ def _rccl_worker(rank, world, port, out_dir, k, graph="1"):
                                     batch=512)
     one = LightGCNEngine(z["train_u"], z["train_i"], nu, ni, 64, k, 1e-2, 1e-3, "cuda:0", U0, I0, batch=512)
     trips = torch.from_numpy(z["epoch0_triplets"].astype(np.int64)).cuda()
+    if hot:  # one positive item for every triplet, one user for half of them: runs of equal
+        trips = trips.clone()  # rows crossing many chunks of the solo step's run places
+        trips[1, :] = 0
+        trips[0, ::2] = trips[0, 0]
     la, lb = [], []
     for s in range(6):  # eager, eager (warm), captured, replayed ...; a partial batch at the end
         t = trips[:, s * 512:(s + 1) * 512] if s < 5 else trips[:, 5 * 512: 5 * 512 + 300]
@@ -144,28 +137,31 @@ def _rccl_worker(rank, world, port, out_dir, k, graph="1"):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("k,graph", [(3, "1"), (4, "1"), (3, "0")])
-def test_dp_one_rank_rccl_equals_single_gpu_step(k, graph):
+@pytest.mark.parametrize("k,graph,hot", [(3, "1", False), (4, "1", False), (3, "0", False), (3, "0", True),
+                                         (4, "1", True)])
+def test_dp_one_rank_rccl_equals_single_gpu_step(k, graph, hot):
     """World 1 over RCCL, graph-captured (RSX_DP_GRAPH=1) or issued eagerly (the default):
     the same arithmetic as the single-GPU stored-layer step (only the BPR scatter's float
-    atomics order differently run to run)."""
+    atomics order differently run to run).  hot: the eager one-rank step is the solo path
+    (the loss pass takes the run places, csrc/dp.hip) and meets runs of equal rows that
+    cross chunk boundaries."""
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_rccl_worker, args=(1, _free_port(), d, k, graph), nprocs=1, join=True)
+        mp.spawn(_rccl_worker, args=(1, store_path(), d, k, graph, hot), nprocs=1, join=True)
         z = dict(np.load(os.path.join(d, "rccl.npz")))
     np.testing.assert_allclose(z["la"], z["lb"], rtol=1e-6)
     np.testing.assert_allclose(z["pa"], z["pb"], rtol=0, atol=1e-6)
-    np.testing.assert_allclose(z["ma"], z["mb"], rtol=0, atol=1e-7)
+    # hot rows sum ~1,000 float atomics in the single-GPU step: its moments carry their order
+    np.testing.assert_allclose(z["ma"], z["mb"], rtol=0, atol=1e-6 if hot else 1e-7)
     if graph == "1":
         assert 512 in z["graphs"].tolist()  # full batches replayed from a captured graph
     else:
         assert z["graphs"].size == 0
 
 
-def _trainer_worker(rank, world, port, root, out):
+def _trainer_worker(rank, world, store, root, out):
     """LightGCN with config rsx_dist: dp through the reference's training flow (rsx.trainer
     fused epochs + sharded evaluation), two ranks on one GPU over gloo."""
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    init_pg("gloo", rank, world, store)
     import test_gpu_sharded_trainer as TS
     from rsx.lightgcn import LightGCN
     from rsx.trainer import Trainer
@@ -222,7 +218,7 @@ def test_dp_trainer_fit_and_evaluate(cuda):
                     os.path.join(root, "baby", "baby.inter"))
         out = os.path.join(root, "out")
         os.makedirs(out)
-        mp.spawn(_trainer_worker, args=(world, _free_port(), root, out), nprocs=world, join=True)
+        mp.spawn(_trainer_worker, args=(world, store_path(), root, out), nprocs=world, join=True)
         res = [dict(np.load(os.path.join(out, f"r{r}.npz"))) for r in range(world)]
         c, _, valid = TS._setup(root)
     for x in res[1:]:

@@ -124,11 +124,19 @@ def test_bpr_smore_rows_stores_what_smore_adds(cuda, d):
     trip = torch.stack([ar, ar, ar + B]).contiguous()
     l0, g0, _ = ops.bpr(L.RSX_BPR_SMORE, fin, None, B, 2 * B, trip, 1e-2, batch_cfg=2048.0)
     junk = torch.full((3 * B, d), float("nan"), device=cuda)
-    l1, g1, _ = ops.bpr(L.RSX_BPR_SMORE_ROWS, fin, None, B, 2 * B, trip, 1e-2, batch_cfg=2048.0, g_final=junk)
+    l1, g1, _ = ops.bpr(L.RSX_BPR_SMORE_ROWS, fin, None, B, 2 * B, trip, 1e-2, batch_cfg=2048.0, g_final=junk,
+                        compact_rows=True)
     assert torch.equal(l0, l1)
     assert torch.equal(g0 + 0.0, g1 + 0.0)  # (+0.0: a stored -0.0 equals the added +0.0)
     with pytest.raises(RuntimeError):
-        ops.bpr(L.RSX_BPR_SMORE_ROWS, fin, None, B + 1, 2 * B - 1, trip, 1e-2, batch_cfg=2048.0)
+        ops.bpr(L.RSX_BPR_SMORE_ROWS, fin, None, B + 1, 2 * B - 1, trip, 1e-2, batch_cfg=2048.0, compact_rows=True)
+    with pytest.raises(RuntimeError):  # internal variant: only the compact-rows loss may request it
+        ops.bpr(L.RSX_BPR_SMORE_ROWS, fin, None, B, 2 * B, trip, 1e-2, batch_cfg=2048.0)
+    # right sizes, wrong layout (a repeated row: stores would race): the device check NaN-poisons the loss
+    bad = trip.clone()
+    bad[1, 7] = 3
+    l2, _, _ = ops.bpr(L.RSX_BPR_SMORE_ROWS, fin, None, B, 2 * B, bad, 1e-2, batch_cfg=2048.0, compact_rows=True)
+    assert torch.isnan(l2).all()
 
 
 def test_adam_vs_torch(cuda):

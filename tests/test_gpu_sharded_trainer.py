@@ -9,7 +9,6 @@ rank's users, all-gathered metric sums) loses nothing; item replicas stay equal;
 losses are finite and every rank ran the same number of steps."""
 import os
 import shutil
-import socket
 import tempfile
 
 import numpy as np
@@ -17,6 +16,7 @@ import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
+from helpers import init_pg, store_path
 
 pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
@@ -42,9 +42,8 @@ def _setup(root, **extra):
     return c, train, valid
 
 
-def _worker(rank, world, port, root, out):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+def _worker(rank, world, store, root, out):
+    init_pg("gloo", rank, world, store)
     from rsx.lightgcn import LightGCN
     from rsx.trainer import Trainer
     from rsx.utils import init_seed
@@ -91,13 +90,6 @@ def _worker(rank, world, port, root, out):
     dist.destroy_process_group()
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
 
 def test_sharded_trainer_fit_and_evaluate(cuda):
     from rsx import ops
@@ -109,7 +101,7 @@ def test_sharded_trainer_fit_and_evaluate(cuda):
         shutil.copy(os.path.join(GOLD, "gold_small.inter"), os.path.join(root, "baby", "baby.inter"))
         out = os.path.join(root, "out")
         os.makedirs(out)
-        mp.spawn(_worker, args=(world, _free_port(), root, out), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, store_path(), root, out), nprocs=world, join=True)
         res = [dict(np.load(os.path.join(out, f"r{r}.npz"))) for r in range(world)]
         c, _, valid = _setup(root)
     for r in range(1, world):

@@ -16,7 +16,6 @@ of each rank's own batch.
   mirror gradient, RsxAdam, the NaN gate) against the single-process Trainer fed the
   same rank batches: losses 1e-4 relative, parameters within 2e-4, replicas equal."""
 import os
-import socket
 import tempfile
 from pathlib import Path
 
@@ -25,6 +24,7 @@ import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
+from helpers import init_pg, store_path
 
 pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
@@ -97,9 +97,8 @@ def _oracle_grads(z, c, batches):
     return [x.item() for x in losses], {n: p.grad.detach() for n, p in m.named_parameters()}
 
 
-def _worker(rank, world, port, root, out, fx, item_shard=True):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+def _worker(rank, world, store, root, out, fx, item_shard=True):
+    init_pg("gloo", rank, world, store)
     from rsx.evaluator import TopKEvaluator
 
     z, c, train, valid, sm, ref = _models(root, rank, fx, item_shard)
@@ -139,19 +138,11 @@ def _worker(rank, world, port, root, out, fx, item_shard=True):
     dist.destroy_process_group()
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
-
 def _spawn(fn, world, *args):
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, "out")
         os.makedirs(out)
-        mp.spawn(fn, args=(world, _free_port(), d, out) + args, nprocs=world, join=True)
+        mp.spawn(fn, args=(world, store_path(), d, out) + args, nprocs=world, join=True)
         return [dict(np.load(os.path.join(out, f"r{r}.npz"))) for r in range(world)]
 
 
@@ -174,9 +165,8 @@ def test_sharded_smore_hip_matches_single_process(cuda, fx, world, item_shard):
                 assert np.array_equal(x[n], res[0][n]), n
 
 
-def _trainer_worker(rank, world, port, root, out, fx):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+def _trainer_worker(rank, world, store, root, out, fx):
+    init_pg("gloo", rank, world, store)
     from rsx.trainer import Trainer
 
     z, c, train, valid, sm, ref = _models(root, rank, fx)

@@ -13,7 +13,6 @@ one all-reduce, the preference weights' gradients summed) and that the replicas 
 identical.  One batch: losses, every gradient and one Adam step; and two batches with
 the model-level mirror gradient (global alpha over the sharded parameter vector)."""
 import os
-import socket
 import tempfile
 
 import numpy as np
@@ -21,6 +20,7 @@ import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
+from helpers import init_pg, store_path
 import torch.nn.functional as F
 
 import rsx_oracle as O
@@ -179,10 +179,9 @@ def rank_batches(z, nu, world, per=120):
 CFG = dict(reg_weight=1e-5, batch_size=2048, cl_loss=0.01, cl_temp=0.2, dropout_rate=0.0)
 
 
-def _setup_rank(rank, world, port, item_shard=False):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+def _setup_rank(rank, world, store, item_shard=False):
     torch.set_num_threads(1)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    init_pg("gloo", rank, world, store)
     from rsx.smore_dist import Comm, SmoreShard, param_container
 
     _, init, graphs, z, nu, ni = reference_setup()
@@ -200,8 +199,8 @@ def _sharded_names(item_shard):
     return set(SHARDED) | (set(ITEM_SHARDED) if item_shard else set())
 
 
-def _worker(rank, world, port, out, item_shard=False):
-    core, m, inter = _setup_rank(rank, world, port, item_shard)
+def _worker(rank, world, store, out, item_shard=False):
+    core, m, inter = _setup_rank(rank, world, store, item_shard)
     loss = core.loss(m, inter, None)
     loss.backward()
     grads = {n: p.grad.clone().numpy() for n, p in m.named_parameters()}
@@ -212,13 +211,6 @@ def _worker(rank, world, port, out, item_shard=False):
              **{"g." + k: v for k, v in grads.items()}, **{"p." + k: v for k, v in params.items()})
     dist.destroy_process_group()
 
-
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
 
 
 def _close(a, b, name, tol=2e-5):
@@ -233,7 +225,7 @@ def test_sharded_smore_step_matches_single_process(world, item_shard):
     computed on each rank's item rows, the raw feature tables row-sharded with it."""
     SHARDED = _sharded_names(item_shard)
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(world, _free_port(), d, item_shard), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, store_path(), d, item_shard), nprocs=world, join=True)
         res = [dict(np.load(os.path.join(d, f"r{r}.npz"))) for r in range(world)]
     m, _, _, z, nu, ni = reference_setup()
     batches = rank_batches(z, nu, world)
@@ -295,8 +287,8 @@ def _shard_train_batch(core, m, inter, opt, lr, step_id, mg_interval, base=0.5, 
     return value
 
 
-def _mg_worker(rank, world, port, out, steps, item_shard=False):
-    core, m, inter = _setup_rank(rank, world, port, item_shard)
+def _mg_worker(rank, world, store, out, steps, item_shard=False):
+    core, m, inter = _setup_rank(rank, world, store, item_shard)
     opt = torch.optim.Adam(m.parameters(), lr=1e-3)
     losses = [_shard_train_batch(core, m, inter, opt, 1e-3, s + 1, 1) for s in range(steps)]
     params = {n: p.detach().clone().numpy() for n, p in m.named_parameters()}
@@ -328,7 +320,7 @@ def test_sharded_smore_mirror_gradient_matches_single_process(world, item_shard)
     SHARDED = _sharded_names(item_shard)
     steps = 2
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_mg_worker, args=(world, _free_port(), d, steps, item_shard), nprocs=world, join=True)
+        mp.spawn(_mg_worker, args=(world, store_path(), d, steps, item_shard), nprocs=world, join=True)
         res = [dict(np.load(os.path.join(d, f"r{r}.npz"))) for r in range(world)]
     m, _, _, z, nu, ni = reference_setup()
     batches = rank_batches(z, nu, world)
