@@ -10,15 +10,18 @@ A step = one training batch end to end on the device: triplet sampling
 (shuffle + rejection negatives), 3-layer propagation, BPR loss + backward,
 Horner backward propagation, Adam — one `rsx_lightgcn_step` C-ABI call.
 
-N>1 (one process per GPU, torchrun or `--gpus N`): weak scaling, data-parallel
-by default (`--dist dp`, rsx.dp / csrc/dp.hip): every rank holds the same
-sports-shaped graph and a bit-identical replica of the tables, and trains its own
-2048 triplets of the global batch of N*2048 (the reference objective at that
-batch); per step the ranks all-gather their triplets and their loss-gradient rows
-(~1.6 MB per rank) over RCCL/xGMI and run the same backward and Adam.
-`--dist rowshard`: the row-sharded design (rsx.dist): every rank owns
-its own sports-shaped block of users over the same items, the item partials
-all-reduced per layer.  value = all ranks' interactions / max-over-ranks time.
+N>1 (one process per GPU, torchrun or `--gpus N`): weak scaling, row-sharded by
+default (`--dist rowshard`, SURVEY 8e, rsx.dist / csrc/dist.hip): every rank owns its
+own sports-shaped block of users over the same items (N=1 is exactly the C2 graph),
+propagates only its users' rows and its item partials, and the item partials are
+all-reduced per layer over RCCL/xGMI: the ranks divide the propagation, so the per-N
+values compare with the N=1 line.  `--dist dp` (rsx.dp / csrc/dp.hip): the graph and
+tables replicated, every rank evaluating the whole global batch of N*2048 triplets
+after one triplet all-gather -- its speed-up comes from the larger batch, not from
+dividing work (a one-GPU `--batch N*2048` line is its comparator).
+`--workload c4 [--dim 64]`: strong scaling on the fixed 10M-user graph (global batch
+2048 split over the ranks; `--dim 64` = the metric's d, whose N=1 anchor fits one GPU).
+value = all ranks' interactions / max-over-ranks time.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
 Prints ONE JSON line on rank 0.
@@ -247,8 +250,10 @@ WORKLOADS = {
 def bench_model(args):
     """C1 / C3 / C5 through the drop-in surface (Config -> RecDataset -> loaders -> model ->
     Trainer): a step = one training batch exactly as Trainer runs it.  SMORE (c3, c5) at
-    WORLD_SIZE > 1: the users-sharded model (rsx.smore_dist: items replicated, one item
-    all-reduce per UI layer over RCCL), every rank stepping on its own batch."""
+    WORLD_SIZE > 1: data-parallel by default (rsx.smore scheme "dp": every table replicated,
+    every rank stepping on its own batch, one batch-row gradient all-gather + one weight
+    all-reduce per backward over RCCL); RSX_SMORE_SCHEME=usershard: the users-sharded model
+    (rsx.smore_dist: one item all-reduce per UI layer)."""
     import tempfile
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -279,10 +284,14 @@ def bench_model(args):
         np.save(os.path.join(root, w["dataset"], ft), feats[1])
     cfg = dict(data_path=root + "/", train_batch_size=args.batch, rsx_sampler="device",
                is_multimodal_model=w["model"] == "SMORE", **w["cfg"])
+    if w["model"] == "SMORE" and os.environ.get("RSX_SMORE_SCHEME"):
+        cfg["rsx_smore_scheme"] = os.environ["RSX_SMORE_SCHEME"]
     from rsx.dist import sim_comm_params
 
     sim = sim_comm_params() if (world == 1 and w["model"] == "SMORE") else None
-    if sim:  # rank 0 of a modelled W-rank users-sharded job (rsx.smore_dist.Comm's latency injection)
+    if sim or (w["model"] == "SMORE" and os.environ.get("RSX_BENCH_SHARDED") == "1"):
+        # rank 0 of a modelled W-rank job (rsx.smore_dist.Comm's latency injection), or (diagnosis)
+        # the multi-rank model on one rank: its exchange work without a collective
         cfg["rsx_sharded"] = True
     if os.environ.get("RSX_BENCH_GRAPH") == "0":  # diagnosis: the model's batches eagerly
         cfg["rsx_graph_step"] = False
@@ -428,7 +437,8 @@ def bench_model(args):
                 + ("; N(0,1) features" if w["model"] == "SMORE" else ""),
         "config": {"workload": w["desc"], "model": w["model"], "embedding_size": int(c["embedding_size"]),
                    "global_batch": int(getattr(model, "local_batch", args.batch)) * world,
-                   "parallelism": f"usershard{world}" if sharded else "single", "fused_step": bool(t.fused),
+                   "parallelism": f"{getattr(model, 'scheme', None) or 'usershard'}{world}" if sharded else "single",
+                   "fused_step": bool(t.fused),
                    "graph_step": t._graph is not None and t._graph.replays > 0},
         "launcher": os.environ.get("RSX_BENCH_LAUNCHER", "torchrun" if world > 1 else "single process"),
         "rccl_world_size": rccl_world, "per_rank": per_rank,
@@ -438,13 +448,17 @@ def bench_model(args):
     }
     if sim:
         Wm = int(sim["world"])
-        out["config"]["parallelism"] = f"usershard{Wm} (latency-injected, rank 0 of {Wm})"
+        out["config"]["parallelism"] = f"{model.scheme}{Wm} (latency-injected, rank 0 of {Wm})"
         out["config"]["global_batch"] = int(getattr(model, "local_batch", args.batch)) * Wm
         out["latency_injection"] = dict(
             sim, modelled_job={"world": Wm, "interactions_per_s": Wm * n / wall, "ms_per_step": wall * 1e3 / args.steps},
-            note="value / ms_per_step: rank 0 of the modelled job (its 1/W of the users and item rows, a batch of "
-                 "its own; every collective a comm-stream stand-in of the modelled time): the job's rate is world x "
-                 "value; the fullsort figures are this rank's users only")
+            note=("value / ms_per_step: rank 0 of the modelled job (" +
+                  ("every table replicated, a batch of its own from its 1/W of the users; the batch-row gradient "
+                   "all-gather and the preference weights' all-reduce comm-stream stand-ins of the modelled time, "
+                   "the peers' packs copies of its own" if model.scheme == "dp" else
+                   "its 1/W of the users and item rows, a batch of its own; every collective a comm-stream "
+                   "stand-in of the modelled time") +
+                  "): the job's rate is world x value; the fullsort figures are this rank's users only"))
     if rank == 0:
         _json_line(out)
     if world > 1 or sim:
@@ -452,6 +466,82 @@ def bench_model(args):
             model.comm.close()
     if world > 1:
         torch.distributed.destroy_process_group()
+
+
+def bench_c1_cpu(args):
+    """BASELINE config C1 as the reference runs it: LayerGCN K=2 d=64 on a baby-shaped graph
+    on the CPU (src/models/layergcn.py:127-177, src/common/trainer.py:186-238), through the
+    drop-in rsx LayerGCN with use_gpu False -- its steps go through torch.ops.rsx's C++ CPU
+    kernels (rsx.cpu_engine, csrc/cpu_ops.cpp): the reference's host sampler, the per-epoch
+    edge-dropout rebuild, propagation, BPR, backward, Adam.  Timed as whole epochs (each
+    with its rebuild), beside the CPU port of the reference (oracle.LayerGCNCPU: torch
+    sparse ops + autograd + torch Adam) on the same graph and the same host threads."""
+    import tempfile
+
+    from rsx import synth
+    from rsx.config import Config
+    from rsx.data import RecDataset, TrainDataLoader
+    from rsx.trainer import Trainer
+    from rsx.utils import get_model, init_seed
+
+    threads = torch.get_num_threads()
+    root = tempfile.mkdtemp(prefix="rsx_bench_c1_")
+    df = synth.shaped("baby", seed=0)
+    synth.write_inter(df, root, "baby")
+    c = Config("LayerGCN", "baby", dict(data_path=root + "/", train_batch_size=args.batch, use_gpu=False,
+                                        is_multimodal_model=False, n_layers=[2], reg_weight=[1e-2], dropout=[0.1]))
+    for k in c["hyper_parameters"]:
+        if isinstance(c[k], list):
+            c[k] = c[k][0]
+    assert c["device"].type == "cpu"
+    init_seed(c["seed"])
+    ds = RecDataset(c)
+    tr, va, te = ds.split()
+    for x in (ds, tr, va, te):
+        str(x)
+    train = TrainDataLoader(c, tr, batch_size=args.batch, shuffle=True)
+    train.pretrain_setup()
+    model = get_model("LayerGCN")(c, train)
+    t = Trainer(c, model)
+    model.train()
+
+    def epoch(ep):
+        model.pre_epoch_processing()
+        n = 0
+        for b in train:
+            if t.fused:
+                model.fused_step(b, t.current_lr())
+            else:
+                t.train_step(b, n, model.calculate_loss)
+            n += int(b.shape[1])
+        return n
+
+    epoch(0)  # untimed: first use of every kernel
+    n_ep = max(1, int(args.steps)) if args.steps is not None else 2
+    t0 = time.perf_counter()
+    n = sum(epoch(1 + e) for e in range(n_ep))
+    wall = time.perf_counter() - t0
+    cpu = None
+    if not args.no_cpu_baseline:
+        tr_df = df[df.x_label == 0]
+        tu_, ti_ = tr_df.userID.values.astype(np.int64), tr_df.itemID.values.astype(np.int64)
+        cpu = cpu_baseline_layergcn(tu_, ti_, int(df.userID.max()) + 1, int(df.itemID.max()) + 1, 2, 1e-2, 0.1,
+                                    args.cpu_budget, -(-tu_.size // args.batch))
+    out = {"metric": METRIC, "value": n / wall, "unit": "interactions/s", "n_gpus": 0, "device": "cpu",
+           "cores": threads, "epochs": n_ep, "s_per_epoch": wall / n_ep, "ms_per_step": wall * 1e3 / (n / args.batch),
+           "higher_is_better": True, "vs_baseline": None, "dtype": "f32",
+           "data": "synthetic Amazon-baby-shaped graph (rsx.synth seed 0)",
+           "config": {"workload": "C1: LayerGCN K=2 d=64, baby-shaped (19,445 users x 7,050 items), B=2048, "
+                                  "edge dropout 0.1, on the CPU through torch.ops.rsx's C++ kernels "
+                                  "(rsx.cpu_engine, csrc/cpu_ops.cpp); the reference's host sampler",
+                      "model": "LayerGCN", "fused_step": bool(t.fused)},
+           "includes": "every epoch's edge-dropout rebuild and host triplet sampling",
+           "cpu_baseline": cpu,
+           "speedup_vs_cpu_port": (n / wall) / cpu["value"] if cpu else None,
+           "reference_measured": {"value": 24776, "unit": "interactions/s", "cores": 8,
+                                  "source": "SURVEY.md 6: the reference itself on baby, this container"},
+           "roofline": None}
+    _json_line(out)
 
 
 def _c4_chunk(args):
@@ -462,7 +552,7 @@ def _c4_chunk(args):
     return c, u, i, lab
 
 
-def load_graph(workload, rank, world, c4_chunks=None, replicated=False):
+def load_graph(workload, rank, world, c4_chunks=None, replicated=False, c4_dim=256):
     """(train users, train items, valid users, valid items, n_users, n_items, d, desc) of
     this rank.  c2: every rank owns its own sports-shaped block of users (rank-seeded)
     over the same items (row-sharded weak scaling), or with `replicated` every rank the
@@ -498,10 +588,13 @@ def load_graph(workload, rank, world, c4_chunks=None, replicated=False):
         ti.append(i[tr])
         vu.append(u[va] + off)
         vi.append(i[va])
+    head = ("C4: LightGCN K=3 d=256" if c4_dim == 256 else
+            f"C4-d{c4_dim} (the metric's d={c4_dim} on C4's graph): LightGCN K=3 d={c4_dim}")
     return (np.concatenate(tu), np.concatenate(ti), np.concatenate(vu), np.concatenate(vi),
-            (c1 - c0) * C["chunk_users"], C["n_items"], 256,
-            "C4: LightGCN K=3 d=256, synthetic 10M users x 1M items (~10 interactions/user, Zipf(0.8) items; "
-            "reference split rule), users row-sharded over the ranks, items replicated, B=2048 per rank")
+            (c1 - c0) * C["chunk_users"], C["n_items"], c4_dim,
+            head + ", synthetic 10M users x 1M items (~10 interactions/user, Zipf(0.8) items; "
+            "reference split rule), users row-sharded over the ranks, items replicated, global batch 2048 "
+            "split over the ranks")
 
 
 def replica_hash(t: torch.Tensor) -> torch.Tensor:
@@ -700,16 +793,24 @@ def main():
     ap.add_argument("--sharded", action="store_true",
                     help="use the row-sharded engine even at N=1 (measures its host/launch overhead)")
     ap.add_argument("--dist", choices=["dp", "rowshard"], default=None,
-                    help="N>1 scheme for c2/baby: dp (default: the graph replicated, the global batch split, "
-                         "rsx.dp) or rowshard (users row-sharded, rsx.dist); c4 is always rowshard")
+                    help="N>1 scheme for c2/baby: rowshard (default: every rank its own sports-shaped user block "
+                         "over the same items, users row-sharded, item partials reduced per layer, rsx.dist: the "
+                         "ranks divide the propagation) or dp (the graph replicated, every rank evaluating the "
+                         "global batch, rsx.dp); c4 is always rowshard")
     ap.add_argument("--dp", action="store_true",
                     help="use the data-parallel engine even at N=1 (measures its exchange-free overhead)")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--eval-users", type=int, default=None, help="default: all valid users (c4: 32768 per rank)")
     ap.add_argument("--c4-chunks", type=int, default=None,
                     help="c4: build only the first N of the 8 1.25M-user chunks (1 = one rank's share at 8 GPUs)")
+    ap.add_argument("--dim", type=int, default=None, choices=[64, 128, 256],
+                    help="c4 only: embedding size (default 256 = config C4; 64 = the metric's d on C4's graph, "
+                         "the strong-scaling leg whose N=1 anchor fits one GPU)")
     ap.add_argument("--n-layers", type=int, default=3,
                     help="LightGCN depth (c2/baby/c4; default 3 = configs C2/C4; the reference's YAML default is 4)")
+    ap.add_argument("--cpu", action="store_true",
+                    help="c1 only: the CPU configuration (BASELINE config 1) through torch.ops.rsx's C++ CPU "
+                         "kernels, whole epochs timed beside the CPU port; --steps = epochs (default 2)")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU only: exercise the N-rank launch and report (gloo), no GPU work")
     args = ap.parse_args()
@@ -724,7 +825,13 @@ def main():
         args.steps = args.steps if args.steps is not None else 3
         args.warmup = args.warmup if args.warmup is not None else 1
         return dry_run(args)
+    if args.cpu:
+        if args.workload != "c1" or args.gpus != 1:
+            raise SystemExit("--cpu is the one-process C1 configuration (--workload c1)")
+        return bench_c1_cpu(args)
     big = args.workload == "c4"
+    if args.dim is not None and not big:
+        raise SystemExit("--dim applies to --workload c4")
     args.steps = args.steps if args.steps is not None else (20 if big else 200)
     args.warmup = args.warmup if args.warmup is not None else (3 if big else 20)
     args.eval_users = args.eval_users if args.eval_users is not None else (32768 if big else 0)
@@ -758,16 +865,22 @@ def main():
     B = args.batch // w_eff if big else args.batch
     if big and B * w_eff != args.batch:
         raise SystemExit(f"--batch {args.batch} does not split evenly over {w_eff} ranks")
-    scheme = args.dist or ("rowshard" if big else "dp")
+    # N > 1 default: row-sharded (the ranks divide the propagation); dp is opt-in (--dist dp)
+    scheme = args.dist or "rowshard"
     if big and scheme != "rowshard":
         raise SystemExit("--workload c4 is the row-sharded strong-scaling leg")
     dp = not big and not args.sharded and (args.dp or ((world > 1 or sim is not None) and scheme == "dp"))
-    tu, ti, vu_all, vi_all, nu, ni, d, desc = load_graph(args.workload, rank, world, args.c4_chunks, replicated=dp)
+    tu, ti, vu_all, vi_all, nu, ni, d, desc = load_graph(args.workload, rank, world, args.c4_chunks, replicated=dp,
+                                                         c4_dim=args.dim or 256)
     if big and args.c4_chunks:
         desc += f" [only {args.c4_chunks} of 8 user chunks built]"
     if sim and big:
         desc += (f" [latency-injected model of rank 0 of a {sim['world']}-rank job: its {args.c4_chunks}/8 user "
                  f"share, batch {B}, every collective a comm-stream kernel of the modelled time at "
+                 f"{sim['busbw_gbs']:.0f} GB/s bus bandwidth + {sim['latency_us']:.0f} us]")
+    elif sim and not dp:
+        desc += (f" [latency-injected model of rank 0 of a {sim['world']}-rank row-sharded job: its own user "
+                 f"block, B={B}, every item-partial collective a comm-stream kernel of the modelled time at "
                  f"{sim['busbw_gbs']:.0f} GB/s bus bandwidth + {sim['latency_us']:.0f} us]")
     elif sim:
         desc += (f" [latency-injected model of rank 0 of a {sim['world']}-rank data-parallel job: the graph "
@@ -777,7 +890,7 @@ def main():
     if dp:
         desc = desc.replace("per rank), B=2048 per rank", "), the graph replicated on every rank, "
                                                               f"B={B} per rank, global batch {B * world}")
-    sharded = (world > 1 or big or args.sharded) and not dp
+    sharded = (world > 1 or big or args.sharded or (sim is not None and scheme == "rowshard")) and not dp
     if sharded or dp:
         import torch.distributed as dist
 
@@ -1163,11 +1276,14 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             del buf
+            Wm = sim["world"]
             out["latency_injection"] = dict(sim, per_collective_ms={
                 "allreduce_item_block": 1e3 * lib.rsx_comm_sim_seconds(eng._comm, L.RSX_COLL_ALLREDUCE, X),
                 "reduce_scatter_or_all_gather_item_block":
                     1e3 * lib.rsx_comm_sim_seconds(eng._comm, L.RSX_COLL_ALLGATHER, X)},
                 measured_allreduce_item_block_ms=e0.elapsed_time(e1),
+                modelled_job={"world": Wm, "interactions_per_s": Wm * total_inter / wall, "ms_per_step": ms,
+                              "global_batch": B * Wm},
                 note="value / ms_per_step: one rank's share of the modelled job (the job's rate is world x value "
                      "when every rank holds the same share)")
         _json_line(out)

@@ -644,6 +644,27 @@ int rsx_smore_pref_rows(int32_t backward, const float* const* W, const float* co
                         rsx_stream_t stream);
 size_t rsx_smore_pref_rows_occ_floats(int64_t n, int32_t d);
 /*
+ * Data-parallel SMORE's batch-row gradient exchange (csrc/rowx.hip; the objective is the
+ * sum over ranks of src/models/smore.py:366-411's loss of each rank's batch, and every
+ * path from that loss to the parameters runs through the preference block's backward,
+ * smore.py:320-341, whose table gradients are defined on the batch rows only).
+ *   rsx_rowx_pack: bumps *tag_dev, then packs this rank's n occurrences (rows may
+ *     repeat) into packed[n_max][rsx_rowx_entry_floats(T, d)]: per entry the row (int64 in
+ *     two f32 words), a flag 1.0 on the first occurrence of its row, a pad word, then
+ *     the row of each of the T [N, d] tables; entries n..n_max-1 pad (row = rows[0],
+ *     flag 0).  lead: uint64 [N] scratch, zeroed once and kept across calls.
+ *   rsx_rowx_combine: packed = the world ranks' packs in rank order (after an
+ *     all-gather); zeroes every packed row of the T tables, writes the rows to
+ *     union_rows[world * n_max], then adds each rank's flagged rows in rank order: every
+ *     rank that runs it on the same packs gets bit-identical tables.
+ * T <= 8, d a multiple of 4.
+ */
+size_t rsx_rowx_entry_floats(int32_t n_tables, int32_t d);
+int rsx_rowx_pack(const int64_t* rows, int64_t n, int64_t n_max, const float* const* tables, int32_t n_tables,
+                  int32_t d, uint64_t* lead, int32_t* tag_dev, float* packed, rsx_stream_t stream);
+int rsx_rowx_combine(const float* packed, int32_t world, int64_t n_max, float* const* tables, int32_t n_tables,
+                     int32_t d, int64_t* union_rows, rsx_stream_t stream);
+/*
  * dW[p] = dz[p]^T x[p] ([d, d]) and db[p] = colsum(dz[p]) (db[p] may be NULL) for up to
  * 8 pairs of [n, d] row sets: row-split partials + one ordered reduction.
  */
@@ -1103,6 +1124,21 @@ int rsx_cpu_fullsort_topk(const float* user_emb, const int64_t* users, int64_t n
                           float* scores_out, int64_t* idx_out);
 int rsx_cpu_adam(float* p, const float* g, float* m, float* v, int64_t n, int64_t step, float lr, float beta1,
                  float beta2, float eps, float weight_decay);
+/*
+ * One training batch of the CPU configuration in one call (the C1 path; replaces the
+ * reference's calculate_loss + loss.backward() + optimizer.step(), trainer.py:186-238, for
+ * lightgcn.py:117-156 (kind 0) and layergcn.py:127-177 (kind 1)): propagation with the last
+ * layer on the batch rows only, BPR + regulariser on those rows, the backward propagation
+ * (LightGCN: Horner on G, A symmetric; LayerGCN: the cosine-gate backward layer by layer),
+ * Adam (`step` already incremented) over the whole [n_users + n_items, d] table p.
+ * triplets int64 [3][batch] (item ids local); loss_out[0] = the batch loss.
+ * Workspace: rsx_cpu_gcn_step_ws_floats(kind, n, d, n_layers, batch) floats.
+ */
+size_t rsx_cpu_gcn_step_ws_floats(int32_t kind, int64_t n, int32_t d, int32_t n_layers, int64_t batch);
+int rsx_cpu_gcn_step(int32_t kind, const int64_t* rowptr, const int32_t* col, const float* val, int64_t n_users,
+                     int64_t n_items, int32_t d, int32_t n_layers, const int64_t* triplets, int64_t batch, float reg,
+                     float* p, float* m, float* v, int64_t step, float lr, float beta1, float beta2, float eps,
+                     float weight_decay, float* ws, size_t ws_floats, float* loss_out);
 
 #ifdef __cplusplus
 }

@@ -20,7 +20,7 @@ INCLUDE = os.path.join(REPO, "include")
 LIBDIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIBDIR, "librsx.so")
 SOURCES = ["spmm.hip", "bpr.hip", "fullsort.hip", "step.hip", "smore.hip", "metrics.hip", "linear.hip", "dist.hip",
-           "dp.hip", "smore_fuse.hip", "knn.hip", "graph.hip",
+           "dp.hip", "smore_fuse.hip", "knn.hip", "graph.hip", "rowx.hip",
            "cpu_ops.cpp"]  # host-only C++ (the torch.ops.rsx CPU kernels), compiled as plain C++
 ARCH = os.environ.get("RSX_OFFLOAD_ARCH", "gfx950")
 
@@ -68,8 +68,9 @@ def build(force: bool = False, verbose: bool = True) -> str:
     def compile_one(src):
         obj = os.path.join(objdir, os.path.splitext(src)[0] + ".o")
         if src.endswith(".cpp"):  # host code: no device pass
-            cmd = [hipcc, "-x", "c++", "-O3", "-fPIC", "-std=c++17", "-pthread", f"-I{INCLUDE}", f"-I{CSRC}", "-c",
-                   os.path.join(CSRC, src), "-o", obj]
+            # x86-64-v3 (AVX2 + FMA): every host these runs use (EPYC GPU boxes, this Xeon) has it
+            cmd = [hipcc, "-x", "c++", "-O3", "-march=x86-64-v3", "-fPIC", "-std=c++17", "-pthread", f"-I{INCLUDE}",
+                   f"-I{CSRC}", "-c", os.path.join(CSRC, src), "-o", obj]
         else:
             cmd = [hipcc, *_flags(src), "-c", os.path.join(CSRC, src), "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)

@@ -16,6 +16,8 @@ Graphs are host CSR tensors (rowptr int64, col int32, val f32); the parameters a
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -57,6 +59,10 @@ class CpuGCNEngine:
         self.loss_acc = torch.zeros(1, dtype=torch.float64)
         self.step_count = 0
         self._eval = None
+        self.kind_id = 0 if kind == "lightgcn" else 1
+        self.use_ops = os.environ.get("RSX_CPU_STEP", "fused") == "ops"
+        self._ws = None
+        self._loss = torch.zeros(1, dtype=torch.float32)
 
     # -- graphs ------------------------------------------------------------------
     def set_train_graph(self, rowptr, col, val):
@@ -83,13 +89,34 @@ class CpuGCNEngine:
         return torch.ops.rsx.bpr_loss(f, x, triplets[:3].contiguous(), self.n_users, self.reg, self.variant, 0.0)
 
     def step(self, triplets: torch.Tensor):
+        """One batch: `rsx_cpu_gcn_step` (the whole step in one C-ABI call, csrc/cpu_ops.cpp);
+        with `use_ops` the torch.ops.rsx sequence (propagate + bpr_loss + autograd + adam_),
+        the same formulas (tests/test_cpu_e2e.py checks the two against each other)."""
         self.step_count += 1
-        x = self.p.detach().requires_grad_(True)
-        loss = self.loss(x, triplets)
-        (g,) = torch.autograd.grad(loss, [x])
+        if self.use_ops or self.K < 1:
+            x = self.p.detach().requires_grad_(True)
+            loss = self.loss(x, triplets)
+            (g,) = torch.autograd.grad(loss, [x])
+            self.step_t += 1
+            torch.ops.rsx.adam_(self.p, g, self.m, self.v, self.step_t, self.lr, 0.9, 0.999, 1e-8, self.wd)
+            self.loss_acc += loss.detach().double()
+            self._eval = None
+            return
+        trip = triplets[:3].to(torch.int64).contiguous()
+        B = int(trip.shape[1])
+        n = self.n_users + self.n_items
+        lib = L.lib()
+        need = int(lib.rsx_cpu_gcn_step_ws_floats(self.kind_id, n, self.d, self.K, B))
+        if self._ws is None or self._ws.numel() < need:
+            self._ws = torch.empty(need, dtype=torch.float32)
+        rp, col, val = self.train_adj
         self.step_t += 1
-        torch.ops.rsx.adam_(self.p, g, self.m, self.v, self.step_t, self.lr, 0.9, 0.999, 1e-8, self.wd)
-        self.loss_acc += loss.detach().double()
+        L.check(lib.rsx_cpu_gcn_step(self.kind_id, rp.data_ptr(), col.data_ptr(), val.data_ptr(), self.n_users,
+                                     self.n_items, self.d, self.K, trip.data_ptr(), B, self.reg, self.p.data_ptr(),
+                                     self.m.data_ptr(), self.v.data_ptr(), int(self.step_t), self.lr, 0.9, 0.999,
+                                     1e-8, self.wd, self._ws.data_ptr(), self._ws.numel(), self._loss.data_ptr()),
+                "rsx_cpu_gcn_step")
+        self.loss_acc += self._loss.double()
         self._eval = None
 
     def forward(self) -> torch.Tensor:

@@ -435,8 +435,76 @@ class SMORE(GeneralRecommender):
         world, rank = _world()
         flag = config["rsx_sharded"]  # None: shard whenever the process group has > 1 rank
         self.sharded = bool(flag) if flag is not None else world > 1
-        if self.sharded:
+        # multi-rank scheme: "dp" (default; every table replicated, each rank its own batch, one
+        # batch-row gradient exchange per backward: rsx.smore_dist.RowGradExchange) or
+        # "usershard" (users row-sharded, the item partials all-reduced per UI layer: SmoreShard)
+        self.scheme = str(config.get("rsx_smore_scheme") or "dp") if self.sharded else None
+        if self.scheme not in (None, "dp", "usershard"):
+            raise ValueError(f"rsx_smore_scheme must be 'dp' or 'usershard', got {self.scheme!r}")
+        self._exch = None
+        if self.scheme == "usershard":
             self._init_sharded(config, rp, col, val, (rows, col[:e].astype(np.int64) - nu, val[:e]), world, rank)
+        elif self.scheme == "dp":
+            self._init_dp(config, world)
+
+    def _epoch_slices(self, config, sel, world):
+        """(steps per epoch, this rank's largest slice) for a rank holding the `sel`
+        interactions: every rank cuts its epoch into the same number of balanced slices
+        (each interaction visited once); a rank with fewer interactions than steps is
+        refused on every rank alike."""
+        import torch.distributed as dist
+
+        e_r = int(sel.sum())
+        B = int(config["train_batch_size"])
+        # the global count in int64 (an f32 sum is exact only to 2^24 interactions)
+        group = dist.is_available() and dist.is_initialized()
+        cdev = self.device if group and dist.get_backend() == "nccl" else torch.device("cpu")
+        stats = torch.tensor([e_r, -e_r], dtype=torch.int64, device=cdev)
+        tot = stats[:1].clone()
+        if group:
+            dist.all_reduce(tot)
+        steps = max(1, -(-int(tot.item()) // (world * B)))
+        if group:
+            dist.all_reduce(stats, op=dist.ReduceOp.MAX)  # [max E_r, -min E_r]
+        if -int(stats[1].item()) < steps:
+            raise RuntimeError(f"sharded SMORE: a rank holds {-int(stats[1].item())} training interactions, fewer than "
+                               f"the {steps} steps per epoch (world {world}, batch {B}); use fewer ranks")
+        return steps, -(-e_r // steps)
+
+    def _init_dp(self, config, world):
+        """Data-parallel SMORE: every table replicated on every rank (the
+        reference's initial weights, drawn identically under init_seed); rank r trains on
+        its own batches of the interactions of its user block [a_r, b_r) (global ids, so
+        the single-process loss path runs unchanged); the objective is the sum over ranks
+        of the reference loss of each rank's batch.  The preference block's backward
+        exchanges the batch-row table gradients and its weights' gradients once
+        (RowGradExchange); everything after it is identical on every rank."""
+        import torch.distributed as dist
+
+        from .smore_dist import Comm, RowGradExchange, ranges
+
+        nu, ni = self.n_users, self.n_items
+        self.comm = Comm(None, self.device)
+        W, r = self.comm.world, self.comm.rank
+        a, b = ranges(nu, W)[r]
+        self.user_range = (a, b)
+        im = self.interaction_matrix
+        rows, cols = im.row.astype(np.int64), im.col.astype(np.int64)
+        sel = (rows >= a) & (rows < b)
+        self.steps_per_epoch, self.local_batch = self._epoch_slices(config, sel, world)
+        self._sampler = ops.DeviceSampler(rows[sel], cols[sel], nu, self.device, seed=int(config["seed"] or 0) + r)
+        # negatives from the whole training-item list, as the reference's sampler draws them
+        self._sampler.all_items = torch.from_numpy(np.unique(cols).astype(np.int32)).to(self.device)
+        self._epoch_buf = None
+        self._epoch_of_buf = None
+        self._gate_buf = torch.zeros(1, dtype=torch.float32, device=self.device)
+        lb = torch.tensor([self.local_batch], dtype=torch.int64,
+                          device=self.device if dist.is_initialized() and dist.get_backend() == "nccl" else "cpu")
+        if dist.is_available() and dist.is_initialized():
+            dist.all_reduce(lb, op=dist.ReduceOp.MAX)
+        self._exch = RowGradExchange(self.comm, nu + ni, self.embedding_dim, 3 * int(lb.item()), self.device)
+        # the step's collectives are captured with it only over RCCL (a gloo group's are host calls)
+        self.supports_graph_step = self.comm.native
 
     def _init_sharded(self, config, rp, col, val, r_coo, world, rank):
         """Users sharded over the process group, the item side replicated (rsx.smore_dist):
@@ -474,27 +542,7 @@ class SMORE(GeneralRecommender):
         im = self.interaction_matrix
         rows, cols = im.row.astype(np.int64), im.col.astype(np.int64)
         sel = (rows >= a) & (rows < b)
-        e_r = int(sel.sum())
-        B = int(config["train_batch_size"])
-        # the global count in int64 (an f32 sum is exact only to 2^24 interactions); every
-        # rank's epoch is cut into `steps` balanced slices of its E_r interactions, so a
-        # rank with fewer interactions than steps is refused on every rank alike
-        import torch.distributed as dist
-
-        group = dist.is_available() and dist.is_initialized()
-        cdev = self.device if group and dist.get_backend() == "nccl" else torch.device("cpu")
-        stats = torch.tensor([e_r, -e_r], dtype=torch.int64, device=cdev)
-        tot = stats[:1].clone()
-        if group:
-            dist.all_reduce(tot)
-        steps = max(1, -(-int(tot.item()) // (world * B)))
-        if group:
-            dist.all_reduce(stats, op=dist.ReduceOp.MAX)  # [max E_r, -min E_r]
-        if -int(stats[1].item()) < steps:
-            raise RuntimeError(f"sharded SMORE: a rank holds {-int(stats[1].item())} training interactions, fewer than "
-                               f"the {steps} steps per epoch (world {world}, batch {B}); use fewer ranks")
-        self.local_batch = -(-e_r // steps)  # this rank's largest slice
-        self.steps_per_epoch = steps
+        self.steps_per_epoch, self.local_batch = self._epoch_slices(config, sel, world)
         self._sampler = ops.DeviceSampler(rows[sel] - a, cols[sel], b - a, self.device,
                                           seed=int(config["seed"] or 0) + rank)
         self._epoch_buf = None
@@ -511,9 +559,10 @@ class SMORE(GeneralRecommender):
         return st
 
     def local_batches(self, epoch: int):
-        """This rank's training batches of `epoch` (device-sampled [3, B_j] triplets: users
-        as local row ids, items global): steps_per_epoch balanced slices of its epoch on
-        every rank (sizes differ by at most one), each interaction visited once."""
+        """This rank's training batches of `epoch` (device-sampled [3, B_j] triplets; users
+        as local row ids under "usershard", global ids under "dp"; items global):
+        steps_per_epoch balanced slices of its epoch on every rank (sizes differ by at
+        most one), each interaction visited once."""
         S = self.steps_per_epoch
         if self._epoch_of_buf != epoch:
             self._epoch_buf = self._sampler.sample_epoch_slices(epoch, S, out=self._epoch_buf)
@@ -530,11 +579,21 @@ class SMORE(GeneralRecommender):
         return self.comm.allreduce_(self._gate_buf)
 
     def mg_alpha_global(self, params, grads, base, lr, rel_step, max_scale, lr_dev=None):
-        """The mirror gradient's alpha over the global parameter vector (sharded model)."""
+        """The mirror gradient's alpha over the global parameter vector (sharded model).
+        "dp": every rank holds the whole vector and the same summed gradient, so the
+        single-process reduction already is the global one (no exchange)."""
+        if self.scheme == "dp":
+            return SF.mg_alpha(params, grads, base, lr, rel_step, max_scale, lr_dev)
         return self._shard.mg_alpha(self, params, grads, base, lr, rel_step, max_scale, lr_dev)
 
     def full_sort_topk_local(self, eval_users, k: int, eval_data):
         """(positions in eval_users of this rank's users, their top-k item ids)."""
+        if self.scheme == "dp":  # the replicated tables: this rank ranks its user block's share
+            a, b = self.user_range
+            pos = torch.nonzero((eval_users >= a) & (eval_users < b)).flatten()
+            users = eval_users.index_select(0, pos).contiguous()
+            _, topk = self.full_sort_topk([users], k, eval_data)
+            return pos, topk
         return self._shard.full_sort_topk_local(self, self._drop_seed, eval_users, k, eval_data.mask_rowptr,
                                                 eval_data.mask_col)
 
@@ -607,7 +666,7 @@ class SMORE(GeneralRecommender):
         gradients (the UI backbone's _PropMeanRows, the views' _ViewProp3)."""
         return rows is not None and 1 <= self.n_ui_layers <= 4 and self.batch_views
 
-    def _views_fused(self, train=False, rows=None):
+    def _views_fused(self, train=False, rows=None, bw_rows=None):
         """Everything before the preference block: (content, image, text, fusion tables,
         dropout seed).  With `rows` (the batch rows) content is exact on those rows only.
 
@@ -617,7 +676,10 @@ class SMORE(GeneralRecommender):
         (autograd keeps each op's backward on its forward's stream), overlapping the
         item side's backward.  Both are latency-bound chains of mid-size launches, and
         in a captured step the two streams become parallel branches of the HIP graph.
-        RSX_SMORE_STREAMS=0 keeps everything on one stream."""
+        RSX_SMORE_STREAMS=0 keeps everything on one stream.  `bw_rows`: the rows the
+        backward's incoming gradients are defined on, when they are not `rows` (data-parallel
+        SMORE: the union of the ranks' batch rows, filled in by the exchange)."""
+        bw = bw_rows if bw_rows is not None else rows
         # the leaves enter the graph through views made on THIS stream, so every leaf has one
         # consumer on one stream: its AccumulateGrad runs on the stream of the node that
         # produces its gradient (a leaf read on both streams had its accumulator bound to
@@ -637,7 +699,7 @@ class SMORE(GeneralRecommender):
                 if self._tags is None:
                     self._tags = _RowTags(self.n_users + self.n_items, self.device)
                 self._tags.mark(rows)
-                content = _PropMeanRows.apply(ego, self.norm_adj_csr, self.n_ui_layers, self._tags, rows)
+                content = _PropMeanRows.apply(ego, self.norm_adj_csr, self.n_ui_layers, self._tags, bw)
             else:
                 content = _PropMean.apply(ego, self.norm_adj_csr, self.n_ui_layers)
         if self.item_fused and type(self)._projected_spectrum is SMORE._projected_spectrum:
@@ -662,7 +724,7 @@ class SMORE(GeneralRecommender):
                 gtags = self._vtags
             image_embeds, text_embeds, fusion_embeds = SF.view_prop3(
                 (img_i, txt_i, fus_i), (self.image_graph, self.text_graph, self.fusion_graph), self.R, L_, nu,
-                tags=tags, gtags=gtags, rows=rows if gtags is not None else None)
+                tags=tags, gtags=gtags, rows=bw if gtags is not None else None)
         else:
             image_embeds = SF.view_prop(img_i, self.image_graph, self.R, L_, nu)
             text_embeds = SF.view_prop(txt_i, self.text_graph, self.R, L_, nu)
@@ -710,9 +772,11 @@ class SMORE(GeneralRecommender):
         nu, B = self.n_users, interaction.shape[1]
         ar, trip = self._batch_index(B)
         rows = interaction[:3].reshape(-1) + self._rows_off[B]  # [users; nu + positives; nu + negatives]
-        content, image_embeds, text_embeds, fusion_embeds, seed = self._views_fused(train=True, rows=rows)
+        exch = self._exch  # data-parallel SMORE: the batch-row gradient exchange
+        content, image_embeds, text_embeds, fusion_embeds, seed = self._views_fused(
+            train=True, rows=rows, bw_rows=exch.union if exch is not None else None)
         all_c, side_c, content_c = SF.preference_rows(self, content, image_embeds, text_embeds, fusion_embeds,
-                                                      rows, seed, sparse_grads=self._sparse_rows(rows))
+                                                      rows, seed, sparse_grads=self._sparse_rows(rows), exch=exch)
         self.global_step += 1
         total, parts = SF.smore_loss_rows(all_c, side_c, content_c, trip, ar, B, self.reg_weight, self.batch_size,
                                           self.cl_loss, self.cl_temp)
@@ -720,13 +784,15 @@ class SMORE(GeneralRecommender):
         return total
 
     def calculate_loss(self, interaction):
-        if self.sharded:  # this rank's batch (users as local row ids): rsx.smore_dist
+        if self.scheme == "usershard":  # this rank's batch (users as local row ids): rsx.smore_dist
             if self.training and self.dropout.p > 0:
                 self._drop_seed.add_(1)
             self.global_step += 1
             return self._shard.loss(self, interaction, self._drop_seed)
-        if self.batch_rows:
+        if self.batch_rows:  # (data-parallel: this rank's batch, global ids, the same path)
             return self._calculate_loss_rows(interaction)
+        if self.scheme == "dp":
+            raise RuntimeError("data-parallel SMORE trains on the batch rows (rsx_smore_batch_rows: True)")
         users, pos, neg = interaction[0], interaction[1], interaction[2]
         all_embeds, side, content = self._forward_all(train=True)
         self.global_step += 1
@@ -738,14 +804,14 @@ class SMORE(GeneralRecommender):
         return bpr + self.cl_loss * (cl_items + cl_users)
 
     def full_sort_predict(self, interaction):
-        if self.sharded:
+        if self.scheme == "usershard":
             raise NotImplementedError("the sharded SMORE evaluates through full_sort_topk_local")
         with torch.no_grad():
             u, i = self.forward(self.norm_adj_csr)
         return ops.score_dense(u.contiguous(), interaction[0].contiguous(), i.contiguous())
 
     def full_sort_topk(self, interaction, k, eval_data):
-        if self.sharded:
+        if self.scheme == "usershard":
             raise NotImplementedError("the sharded SMORE evaluates through full_sort_topk_local")
         with torch.no_grad():
             if getattr(self, "_eval_cache", None) is None:

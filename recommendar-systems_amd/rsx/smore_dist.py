@@ -204,6 +204,122 @@ def allreduce_grad(comm, *ts):
     return _AllReduceGrad.apply(comm, *ts)
 
 
+class RowGradExchange:
+    """Data-parallel SMORE's one exchange per backward (rsx.smore scheme "dp"): every table
+    replicated, each rank its own batch, the objective the sum over ranks of the reference
+    loss of each rank's batch (src/models/smore.py:366-411).  Every path from a rank's
+    loss to the parameters runs through the preference block on its batch rows
+    (smore.py:320-341), so that block's backward is the exchange point:
+
+    * its four [N, d] table gradients (content, image, text, fusion), defined on this
+      rank's batch rows, are packed one entry per occurrence (a flag on each row's first
+      occurrence), all-gathered, and every rank rebuilds the same tables on the union of
+      the ranks' rows: the rows zeroed, then each rank's rows added in rank order
+      (csrc/rowx.hip: no float atomics, so all ranks hold the same bits);
+    * its seven weights' and biases' gradients (rank-local rows) are summed in one
+      all-reduce, which leaves the same bits on every rank.
+
+    The rest of the backward (UI backbone, the views, the item side) then runs on
+    identical inputs everywhere: identical parameter gradients, replicas that stay
+    bit-identical under the per-element Adam, and no other collective in the step.
+    `union` receives the union row list (the tag-aware backward consumers re-tag it).
+    Off the GPU (gloo tests) the same steps run as torch ops."""
+
+    T = 4
+
+    def __init__(self, comm: Comm, n_rows: int, d: int, n_max: int, device):
+        self.comm, self.d, self.n_max = comm, int(d), int(n_max)
+        self.device = torch.device(device)
+        self.hip = self.device.type == "cuda"
+        W = comm.world
+        self.E = 4 + self.T * self.d
+        self.packed = torch.zeros(W, self.n_max, self.E, dtype=torch.float32, device=self.device)
+        self.union = torch.zeros(W * self.n_max, dtype=torch.int64, device=self.device)
+        self.lead = torch.zeros(int(n_rows), dtype=torch.int64, device=self.device)
+        self.tag = torch.zeros(1, dtype=torch.int32, device=self.device)
+
+    def exchange(self, rows: torch.Tensor, tables, wgrads):
+        """tables: the T [N, d] gradients (valid on `rows`; rebuilt in place on the union
+        rows); wgrads: weight / bias gradients (None entries kept), returned summed."""
+        n = int(rows.numel())
+        if n > self.n_max or n < 1:
+            raise RuntimeError(f"RowGradExchange: {n} batch rows (capacity {self.n_max})")
+        W, r = self.comm.world, self.comm.rank
+        if self.hip:
+            lib = L.lib()
+            tp = (C.c_void_p * self.T)(*[t.data_ptr() for t in tables])
+            L.check(lib.rsx_rowx_pack(ops._p(rows), n, self.n_max, tp, self.T, self.d, ops._p(self.lead),
+                                      ops._p(self.tag), ops._p(self.packed[r]), ops._stream()), "rsx_rowx_pack")
+        else:
+            self._pack_torch(rows, tables, self.packed[r])
+        if self.comm.sim is not None:
+            # latency injection: the modelled peers' packs are this rank's (so the combine does
+            # the work of W real packs; the collective itself is the modelled stand-in)
+            for q in range(W):
+                if q != r:
+                    self.packed[q].copy_(self.packed[r])
+        self.comm.allgather_(self.packed.view(-1), self.n_max * self.E)
+        if self.hip:
+            tp = (C.c_void_p * self.T)(*[t.data_ptr() for t in tables])
+            L.check(L.lib().rsx_rowx_combine(ops._p(self.packed), W, self.n_max, tp, self.T, self.d,
+                                             ops._p(self.union), ops._stream()), "rsx_rowx_combine")
+        else:
+            self._combine_torch(tables)
+        live = [g for g in wgrads if g is not None]
+        if live and W > 1:
+            flat = torch.cat([g.reshape(-1) for g in live])
+            self.comm.allreduce_(flat)
+            out, o = [], 0
+            for g in wgrads:
+                if g is None:
+                    out.append(None)
+                    continue
+                out.append(flat[o:o + g.numel()].view_as(g))
+                o += g.numel()
+            wgrads = out
+        return wgrads
+
+    # the CPU statement of csrc/rowx.hip (gloo tests)
+    def _pack_torch(self, rows, tables, out):
+        n, d = rows.numel(), self.d
+        first = torch.zeros(n, dtype=torch.bool)
+        seen = set()
+        for j, x in enumerate(rows.tolist()):
+            if x not in seen:
+                seen.add(x)
+                first[j] = True
+        out.zero_()
+        head = torch.full((self.n_max,), int(rows[0]), dtype=torch.int64)  # padding names a real row
+        head[:n] = rows.cpu()
+        out[:, :2] = _i64_words(head).to(out.device)
+        out[:n, 2] = first.float().to(out.device)
+        for t, tab in enumerate(tables):
+            out[:n, 4 + t * d:4 + (t + 1) * d] = tab[rows]
+
+    def _combine_torch(self, tables):
+        d, W = self.d, self.comm.world
+        ents = self.packed.view(W * self.n_max, self.E)
+        rows = _words_i64(ents[:, :2])
+        self.union.copy_(rows)
+        for tab in tables:
+            tab[rows] = 0.0
+        for q in range(W):
+            e = self.packed[q]
+            sel = e[:, 2] != 0
+            rq = _words_i64(e[sel, :2])
+            for t, tab in enumerate(tables):
+                tab[rq] += e[sel, 4 + t * d:4 + (t + 1) * d]
+
+
+def _i64_words(x: torch.Tensor) -> torch.Tensor:
+    """int64 [n] -> its two 32-bit words as float32 [n, 2] (a bit copy, as the kernel's)."""
+    return x.contiguous().view(torch.int32).view(-1, 2).view(torch.float32)
+
+
+def _words_i64(w: torch.Tensor) -> torch.Tensor:
+    return w.contiguous().view(torch.int32).view(torch.int64).view(-1)
+
+
 class _GatherRows(torch.autograd.Function):
     """Every rank's rows of k row-sharded tables (rank r: rows [r q, r q + n_r) of each,
     n_r <= q) gathered into [k, n, d] on every rank in ONE all-gather of [k, q, d] slices

@@ -167,7 +167,8 @@ class _PrefRows(torch.autograd.Function):
     full zero tables (rsx_smore_pref_rows with occ: deterministic, no float atomics)."""
 
     @staticmethod
-    def forward(ctx, C_, IE, TE, FE, rows, p_drop, seed, sparse, *wb):
+    def forward(ctx, C_, IE, TE, FE, rows, p_drop, seed, sparse, exch, *wb):
+        ctx.exch = exch
         W = [_c(x) for x in wb[:7]]
         b = [None if x is None else _c(x) for x in wb[7:]]
         C_, IE, TE, FE, rows = _c(C_), _c(IE), _c(TE), _c(FE), _c(rows)
@@ -216,17 +217,21 @@ class _PrefRows(torch.autograd.Function):
         grads = _wgrad([(dz[i], xs[i], ctx.has_b[i]) for i in range(7)], d, C_.device)
         gW = [g[0] for g in grads]
         gb = [g[1] for g in grads]
-        return (gC, gIE, gTE, gFE, None, None, None, None, *gW, *gb)
+        if ctx.exch is not None:  # data-parallel SMORE: the one exchange (rsx.smore_dist.RowGradExchange)
+            gwb = ctx.exch.exchange(rows, (gC, gIE, gTE, gFE), gW + gb)
+            gW, gb = gwb[:7], gwb[7:]
+        return (gC, gIE, gTE, gFE, None, None, None, None, None, *gW, *gb)
 
 
 def preference_rows(model, content, image_embeds, text_embeds, fusion_embeds, rows, seed, weights=None,
-                    sparse_grads=False):
+                    sparse_grads=False, exch=None):
     """(all, side, content) rows of the reference's preference block at table rows
     `rows` only (the training loss reads no other row; the block is row-local).
     `weights`: the 7 weights then the 7 biases (None where absent) to use instead of
     the model's own tensors (the sharded model passes them through a gradient sum).
     `sparse_grads`: the four table gradients are defined on the batch rows only (their
-    consumers read nothing else: see _PrefRows.backward)."""
+    consumers read nothing else: see _PrefRows.backward).  `exch`: data-parallel SMORE's
+    RowGradExchange, run on the block's gradients in its backward."""
     m = model
     if weights is None:
         lin = [m.query_v[0], m.query_v[2], m.query_t[0], m.query_t[2], m.gate_image_prefer[0],
@@ -234,7 +239,7 @@ def preference_rows(model, content, image_embeds, text_embeds, fusion_embeds, ro
         weights = [x.weight for x in lin] + [x.bias for x in lin]
     p = float(m.dropout.p) if m.training else 0.0
     return _PrefRows.apply(content, image_embeds, text_embeds, fusion_embeds, rows, p, seed, bool(sparse_grads),
-                           *weights)
+                           exch, *weights)
 
 
 # ---------------------------------------------------------------------------

@@ -355,9 +355,9 @@ class Trainer:
         if not parts:
             return 0.0, loss_batches
         host = torch.stack(parts).double()
-        if sharded:  # the epoch loss of the job: every rank's batches
-            import torch.distributed as dist
+        import torch.distributed as dist
 
+        if sharded and dist.is_available() and dist.is_initialized():  # the job's epoch loss: every rank's batches
             host = host.float().contiguous()
             if dist.get_backend() == "nccl":
                 dist.all_reduce(host)

@@ -123,3 +123,33 @@ def test_main_layergcn_baby_trains_without_a_gpu(tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     log = "".join(open(os.path.join(tmp_path, "log", f)).read() for f in os.listdir(tmp_path / "log"))
     assert "epoch 1 training" in log and "recall@20" in log and "All Over" in log
+
+
+@pytest.mark.parametrize("kind,K", [("layergcn", 2), ("layergcn", 1), ("layergcn", 3), ("lightgcn", 3),
+                                    ("lightgcn", 1)])
+def test_cpu_whole_step_equals_the_ops_sequence(kind, K, monkeypatch):
+    """rsx_cpu_gcn_step (one C-ABI call a batch: the last layer on the batch rows only, BPR on
+    compact rows, the backward propagation, Adam) against the torch.ops.rsx sequence
+    (propagate + bpr_loss + autograd + adam_) over three batches with repeated rows."""
+    from rsx.cpu_engine import CpuGCNEngine
+
+    z = np.load(os.path.join(GOLD, "lightgcn_small.npz"))
+    nu, ni = int(z["n_users"]), int(z["n_items"])
+    U0, I0 = z["init.embedding_dict.user_emb"], z["init.embedding_dict.item_emb"]
+    trips = torch.from_numpy(z["epoch0_triplets"].astype(np.int64))
+    trips[1, :40] = trips[1, 0]  # a hot item
+    runs = []
+    for mode in ("ops", "fused"):
+        monkeypatch.setenv("RSX_CPU_STEP", mode)
+        eng = CpuGCNEngine(kind, z["train_u"], z["train_i"], nu, ni, 64, K, 1e-2, 1e-3, U0, I0)
+        losses = []
+        for s in range(3):
+            before = float(eng.loss_acc)
+            eng.step(trips[:, s * 256:(s + 1) * 256])
+            losses.append(float(eng.loss_acc) - before)
+        runs.append((losses, eng.p.clone(), eng.m.clone(), eng.v.clone()))
+    (la, pa, ma, va), (lb, pb, mb, vb) = runs
+    np.testing.assert_allclose(lb, la, rtol=2e-6)
+    np.testing.assert_allclose(pb.numpy(), pa.numpy(), rtol=0, atol=2e-6)
+    np.testing.assert_allclose(mb.numpy(), ma.numpy(), rtol=0, atol=1e-7)
+    np.testing.assert_allclose(vb.numpy(), va.numpy(), rtol=1e-4, atol=1e-12)

@@ -641,3 +641,54 @@ def test_tagged_step_vs_fixture(cuda, golden):
     out = eng.p.cpu().numpy()
     np.testing.assert_allclose(out[:nu], pu, rtol=0, atol=2e-6)
     np.testing.assert_allclose(out[nu:], pi, rtol=0, atol=2e-6)
+
+
+@pytest.mark.parametrize("d,world,n_max", [(64, 2, 300), (128, 4, 777), (128, 1, 64)])
+def test_rowx_pack_combine_equals_the_torch_statement(cuda, d, world, n_max):
+    """csrc/rowx.hip (data-parallel SMORE's batch-row gradient exchange) against its CPU
+    statement (rsx.smore_dist.RowGradExchange._pack_torch / _combine_torch): the packs of
+    `world` ranks, a hot repeated row, unequal batches (pad entries), garbage off the rows;
+    the packed words, the union rows and the rebuilt tables bit for bit; a second call
+    (the tag moves on, stale first-occurrence keys must not count)."""
+    import ctypes as C
+
+    from rsx.smore_dist import RowGradExchange
+
+    class _C:  # a stand-in communicator: one process holds every rank's pack
+        sim, rank = None, 0
+
+        def __init__(self, w):
+            self.world = w
+
+    n_rows = 5000
+    lib = L.lib()
+    for call in range(2):
+        g = torch.Generator().manual_seed(7 + call)
+        ex_h = RowGradExchange(_C(world), n_rows, d, n_max, "cpu")
+        ex_d = RowGradExchange(_C(world), n_rows, d, n_max, cuda) if call == 0 else ex_d
+        tabs_h = [torch.full((n_rows, d), float("nan")) for _ in range(4)]
+        tabs_d = [t.to(cuda) for t in tabs_h]
+        for r in range(world):
+            n = n_max - (r % 2) * 5
+            rows = torch.randint(0, n_rows, (n,), generator=g)
+            rows[: n // 4] = rows[1]
+            full = [torch.randn(n_rows, d, generator=g) for _ in range(4)]  # one value per row (rows repeat)
+            for th, td, f in zip(tabs_h, tabs_d, full):
+                th[rows] = f[rows]
+                td[rows.to(cuda)] = f[rows].to(cuda)
+            ex_h._pack_torch(rows, tabs_h, ex_h.packed[r])
+            tp = (C.c_void_p * 4)(*[t.data_ptr() for t in tabs_d])
+            rd = rows.to(cuda)
+            L.check(lib.rsx_rowx_pack(rd.data_ptr(), n, n_max, tp, 4, d, ex_d.lead.data_ptr(), ex_d.tag.data_ptr(),
+                                      ex_d.packed[r].data_ptr(), ops._stream()), "rsx_rowx_pack")
+            torch.cuda.synchronize()
+            assert torch.equal(ex_d.packed[r].cpu().view(torch.int32), ex_h.packed[r].view(torch.int32)), r
+        ex_h._combine_torch(tabs_h)
+        tp = (C.c_void_p * 4)(*[t.data_ptr() for t in tabs_d])
+        L.check(lib.rsx_rowx_combine(ex_d.packed.data_ptr(), world, n_max, tp, 4, d, ex_d.union.data_ptr(),
+                                     ops._stream()), "rsx_rowx_combine")
+        torch.cuda.synchronize()
+        assert torch.equal(ex_d.union.cpu(), ex_h.union)
+        u = ex_h.union.unique()
+        for th, td in zip(tabs_h, tabs_d):
+            assert torch.equal(td.cpu()[u].view(torch.int32), th[u].view(torch.int32))

@@ -34,7 +34,7 @@ def _golden(name):
     return dict(np.load(os.path.join(GOLD, name + ".npz")))
 
 
-def _models(root, rank, fx, item_shard=True):
+def _models(root, rank, fx, item_shard=True, scheme="usershard"):
     """(config, train, valid, sharded model, single-process model), both from the
     reference's initial weights (init_seed before each)."""
     import test_gpu_smore as T
@@ -43,8 +43,9 @@ def _models(root, rank, fx, item_shard=True):
     c["rsx_sampler"] = "device"  # the sharded model samples its own users on the device
     c["rsx_knn"] = "host"  # the kNN graphs of the fixture tests (tests/test_gpu_smore.py)
     c["rsx_smore_item_shard"] = item_shard
+    c["rsx_smore_scheme"] = scheme
     sm = T._model(c, train)
-    assert sm.sharded
+    assert sm.sharded and sm.scheme == scheme
     c["rsx_sharded"] = False
     ref = T._model(c, train)
     c["rsx_sharded"] = None
@@ -59,7 +60,8 @@ def _global_batch(sm, inter):
     dist.all_gather(sizes, B)
     mx = int(max(s.item() for s in sizes))
     g = inter.cpu().clone()
-    g[0] += sm.user_range[0]
+    if sm.scheme == "usershard":  # local user row ids ("dp" batches carry global ids)
+        g[0] += sm.user_range[0]
     pad = torch.zeros(3, mx, dtype=torch.int64)
     pad[:, : g.shape[1]] = g
     parts = [torch.zeros_like(pad) for _ in sizes]
@@ -69,6 +71,8 @@ def _global_batch(sm, inter):
 
 def _own_rows(sm, n, t):
     """The rows of a (full-table) tensor `t` that rank's parameter `n` holds."""
+    if sm.scheme == "dp":  # every table replicated
+        return t
     if n == "user_embedding.weight":
         a, b = sm.user_range
         return t[a:b]
@@ -79,6 +83,8 @@ def _own_rows(sm, n, t):
 
 
 def _sharded_param(sm, n):
+    if sm.scheme == "dp":
+        return False
     return n == "user_embedding.weight" or (sm._shard.item_shard and n in ("image_embedding.weight",
                                                                             "text_embedding.weight"))
 
@@ -97,12 +103,13 @@ def _oracle_grads(z, c, batches):
     return [x.item() for x in losses], {n: p.grad.detach() for n, p in m.named_parameters()}
 
 
-def _worker(rank, world, store, root, out, fx, item_shard=True):
+def _worker(rank, world, store, root, out, fx, item_shard=True, scheme="usershard"):
     init_pg("gloo", rank, world, store)
     from rsx.evaluator import TopKEvaluator
 
-    z, c, train, valid, sm, ref = _models(root, rank, fx, item_shard)
-    assert sm._shard.item_shard == item_shard
+    z, c, train, valid, sm, ref = _models(root, rank, fx, item_shard, scheme)
+    if scheme == "usershard":
+        assert sm._shard.item_shard == item_shard
     sm.train()
     ref.train()
     inter = next(iter(sm.local_batches(0)))
@@ -146,11 +153,16 @@ def _spawn(fn, world, *args):
         return [dict(np.load(os.path.join(out, f"r{r}.npz"))) for r in range(world)]
 
 
-@pytest.mark.parametrize("fx,world,item_shard", [("smore_small", 2, True), ("smore_d128_small", 2, True),
-                                                 ("smore_small", 4, True), ("smore_d128_small", 4, True),
-                                                 ("smore_small", 2, False)])
-def test_sharded_smore_hip_matches_single_process(cuda, fx, world, item_shard):
-    res = _spawn(_worker, world, fx, item_shard)
+@pytest.mark.parametrize("fx,world,item_shard,scheme", [
+    ("smore_small", 2, True, "usershard"), ("smore_d128_small", 2, True, "usershard"),
+    ("smore_small", 4, True, "usershard"), ("smore_d128_small", 4, True, "usershard"),
+    ("smore_small", 2, False, "usershard"),
+    ("smore_small", 2, True, "dp"), ("smore_d128_small", 2, True, "dp"), ("smore_small", 4, True, "dp"),
+    ("smore_d128_small", 4, True, "dp"), ("smore_small", 3, True, "dp")])
+def test_sharded_smore_hip_matches_single_process(cuda, fx, world, item_shard, scheme):
+    """usershard: users row-sharded, the item partials all-reduced per UI layer; dp: every
+    table replicated, the batch-row gradients exchanged once (RowGradExchange)."""
+    res = _spawn(_worker, world, fx, item_shard, scheme)
     for x in res:
         assert abs(float(x["loss"]) - float(x["ref"])) <= 2e-5 * abs(float(x["ref"]))
         assert abs(float(x["loss"]) - float(x["oracle"])) <= 2e-5 * abs(float(x["oracle"]))
@@ -165,11 +177,11 @@ def test_sharded_smore_hip_matches_single_process(cuda, fx, world, item_shard):
                 assert np.array_equal(x[n], res[0][n]), n
 
 
-def _trainer_worker(rank, world, store, root, out, fx):
+def _trainer_worker(rank, world, store, root, out, fx, scheme="usershard"):
     init_pg("gloo", rank, world, store)
     from rsx.trainer import Trainer
 
-    z, c, train, valid, sm, ref = _models(root, rank, fx)
+    z, c, train, valid, sm, ref = _models(root, rank, fx, scheme=scheme)
     ts, tr = Trainer(c, sm), Trainer(c, ref)
     assert sm.mg_enable and not ts.fused and not sm.supports_graph_step  # gloo: eager steps
     # the rank batches of epoch 0, gathered: the single-process run trains step j on sum_g L(batch_g,j)
@@ -196,12 +208,13 @@ def _trainer_worker(rank, world, store, root, out, fx):
     dist.destroy_process_group()
 
 
-def test_sharded_smore_trainer_epoch_matches_single_process(cuda):
+@pytest.mark.parametrize("scheme", ["usershard", "dp"])
+def test_sharded_smore_trainer_epoch_matches_single_process(cuda, scheme):
     """gloo world 4 through rsx.trainer.Trainer: one epoch of the sharded SMORE (each rank
     its own device-sampled batches, the mirror gradient with the global alpha) equals the
     single-process Trainer on the joint objective of the same batches."""
     world = 4
-    res = _spawn(_trainer_worker, world, "smore_small")
+    res = _spawn(_trainer_worker, world, "smore_small", scheme)
     for x in res:
         assert int(x["steps"]) >= 2 and int(x["gstep"]) == int(x["rstep"])
         assert abs(float(x["loss"]) - float(x["ref"])) <= 1e-4 * abs(float(x["ref"]))

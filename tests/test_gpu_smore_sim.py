@@ -1,5 +1,5 @@
-"""The users-sharded SMORE step captured as a HIP graph over the latency-injected
-communicator (rsx_comm_init_sim, RSX_COMM_SIM=W): this one process is rank 0 of a
+"""The multi-rank SMORE step (users-sharded and data-parallel) captured as a HIP graph
+over the latency-injected communicator (rsx_comm_init_sim, RSX_COMM_SIM=W): this one process is rank 0 of a
 modelled W-rank job, every collective is the one-rank identity plus a comm-stream
 stand-in holding the modelled time, and with RSX_COMM_SIM_POISON=1 the stand-in fills
 the collective's buffer with NaN for that time before restoring it.
@@ -27,7 +27,7 @@ import test_gpu_smore as T
 pytestmark = pytest.mark.gpu
 
 
-def _run(tmp_path, golden, graph):
+def _run(tmp_path, golden, graph, scheme):
     from rsx.trainer import Trainer
 
     z, c, train, valid, test = T._setup(tmp_path, golden)
@@ -36,8 +36,9 @@ def _run(tmp_path, golden, graph):
     c["rsx_knn"] = "host"
     c["train_batch_size"] = 64  # several steps per epoch on rank 0's 1/W of the fixture
     c["rsx_graph_step"] = graph
+    c["rsx_smore_scheme"] = scheme
     m = T._model(c, train)
-    assert m.sharded and m.comm.sim is not None and m.supports_graph_step
+    assert m.sharded and m.scheme == scheme and m.comm.sim is not None and m.supports_graph_step
     t = Trainer(c, m)
     losses, replays = [], 0
     try:
@@ -55,13 +56,13 @@ def _run(tmp_path, golden, graph):
         m.comm.close()
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_sharded_smore_sim_graph_replay_equals_eager(tmp_path, golden, monkeypatch, world):
+@pytest.mark.parametrize("world,scheme", [(2, "usershard"), (4, "usershard"), (2, "dp"), (4, "dp")])
+def test_sharded_smore_sim_graph_replay_equals_eager(tmp_path, golden, monkeypatch, world, scheme):
     monkeypatch.setenv("RSX_COMM_SIM", f"{world}:1.0:100")  # 1 GB/s, 100 us: wide poison windows
     monkeypatch.setenv("RSX_COMM_SIM_OPT_IN", "1")
     monkeypatch.setenv("RSX_COMM_SIM_POISON", "1")
-    eager = _run(tmp_path / "eager", golden, False)
-    graph = _run(tmp_path / "graph", golden, True)
+    eager = _run(tmp_path / "eager", golden, False, scheme)
+    graph = _run(tmp_path / "graph", golden, True, scheme)
     assert eager["steps"] >= 4 and eager["replays"] == 0 and graph["replays"] >= 2 * eager["steps"] - 4
     assert graph["step"] == eager["step"]
     assert np.isfinite(eager["losses"]).all() and np.isfinite(graph["losses"]).all()

@@ -332,3 +332,51 @@ def test_sharded_smore_mirror_gradient_matches_single_process(world, item_shard)
         want = p.detach().numpy()
         got = np.concatenate([x["p." + name] for x in res]) if name in SHARDED else res[0]["p." + name]
         np.testing.assert_allclose(got, want, rtol=0, atol=2e-5, err_msg=name)
+
+
+def _rowx_worker(rank, world, store, out, n_rows, d, n_max):
+    """RowGradExchange (data-parallel SMORE's one exchange) on `world` gloo ranks, its CPU
+    statement of csrc/rowx.hip: rank r's four tables are defined on its own batch rows only
+    (garbage elsewhere), its rows repeat, its batch may be shorter than n_max."""
+    from rsx.smore_dist import Comm, RowGradExchange
+
+    init_pg("gloo", rank, world, store)
+    g = torch.Generator().manual_seed(100 + rank)
+    n = n_max - (rank % 2)  # unequal batches: the pad entries
+    rows = torch.randint(0, n_rows, (n,), generator=g)
+    rows[: n // 3] = rows[0]  # a hot row, repeated
+    tables = [torch.full((n_rows, d), float("nan")) for _ in range(4)]  # garbage off the batch rows
+    for t in tables:
+        t[rows] = torch.randn(rows.numel(), d, generator=g)
+    mine = [t[rows].clone() for t in tables]
+    wg = [torch.randn(d, d, generator=g), None, torch.randn(d, generator=g)]
+    ex = RowGradExchange(Comm(None, "cpu"), n_rows, d, n_max, "cpu")
+    got = ex.exchange(rows, tables, wg)
+    np.savez(os.path.join(out, f"r{rank}.npz"), rows=rows.numpy(), mine=np.stack([m.numpy() for m in mine]),
+             union=ex.union.numpy(), tabs=np.stack([t.numpy() for t in tables]), wg0=wg[0].numpy(),
+             wg2=wg[2].numpy(), got0=got[0].numpy(), got2=got[2].numpy(), none1=np.array(got[1] is None))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_row_grad_exchange_sums_the_ranks_rows_in_rank_order(world):
+    n_rows, d, n_max = 97, 8, 40
+    with tempfile.TemporaryDirectory() as out:
+        mp.spawn(_rowx_worker, args=(world, store_path(), out, n_rows, d, n_max), nprocs=world, join=True)
+        res = [dict(np.load(os.path.join(out, f"r{r}.npz"))) for r in range(world)]
+    want = np.zeros((4, n_rows, d), np.float32)
+    for x in res:  # each rank's row value once, ranks in order (f32 adds)
+        seen = set()
+        for j, row in enumerate(x["rows"].tolist()):
+            if row not in seen:
+                seen.add(row)
+                want[:, row] = want[:, row] + x["mine"][:, j]
+    union = sorted(set(np.concatenate([x["rows"] for x in res]).tolist()))
+    for x in res:
+        assert set(x["union"].tolist()) == set(union)
+        assert np.array_equal(x["tabs"][:, union], want[:, union])  # bit for bit, every rank
+        assert np.array_equal(x["tabs"][:, union], res[0]["tabs"][:, union])
+        np.testing.assert_allclose(x["got0"], sum(y["wg0"] for y in res), rtol=1e-6, atol=1e-6)
+        np.testing.assert_allclose(x["got2"], sum(y["wg2"] for y in res), rtol=1e-6, atol=1e-6)
+        assert bool(x["none1"])
+        assert np.array_equal(x["got0"], res[0]["got0"])
