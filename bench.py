@@ -10,17 +10,15 @@ A step = one training batch end to end on the device: triplet sampling
 (shuffle + rejection negatives), 3-layer propagation, BPR loss + backward,
 Horner backward propagation, Adam — one `rsx_lightgcn_step` C-ABI call.
 
-N>1 (one process per GPU, torchrun or `--gpus N`): weak scaling, row-sharded by
-default (`--dist rowshard`, SURVEY 8e, rsx.dist / csrc/dist.hip): every rank owns its
-own sports-shaped block of users over the same items (N=1 is exactly the C2 graph),
-propagates only its users' rows and its item partials, and the item partials are
-all-reduced per layer over RCCL/xGMI: the ranks divide the propagation, so the per-N
-values compare with the N=1 line.  `--dist dp` (rsx.dp / csrc/dp.hip): the graph and
-tables replicated, every rank evaluating the whole global batch of N*2048 triplets
-after one triplet all-gather -- its speed-up comes from the larger batch, not from
-dividing work (a one-GPU `--batch N*2048` line is its comparator).
-`--workload c4 [--dim 64]`: strong scaling on the fixed 10M-user graph (global batch
-2048 split over the ranks; `--dim 64` = the metric's d, whose N=1 anchor fits one GPU).
+N>1 (one process per GPU, torchrun or `--gpus N`): by default the metric's d = 64
+LightGCN on the fixed 10M-user graph (`--workload c4 --dim 64`), users row-sharded
+over the ranks (rsx.dist / csrc/dist.hip), the global batch of 2048 split
+over them: strong scaling, the ranks divide the graph.  Its one-GPU anchor is
+`--workload c4 --dim 64 --gpus 1` (the N=1 default stays C2).  The sports graph does
+not divide profitably: `--workload c2 --dist rowshard` (every rank its own sports
+block, item partials all-reduced per layer) and `--workload c2 --dist dp` (graph and
+tables replicated, one triplet all-gather, every rank evaluating the whole global
+batch) both lose to one GPU at the same global batch (`--batch N*2048`).
 value = all ranks' interactions / max-over-ranks time.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
@@ -63,6 +61,29 @@ def time_kernel(fn, reps):
     e.record()
     torch.cuda.synchronize()
     return s.elapsed_time(e) / reps  # ms
+
+
+def time_graph(fn, reps, stream=None):
+    """time_kernel for a multi-launch host sequence: fn captured once as a HIP graph and
+    replayed, so the figure is the launches' device time (as in the graph-replayed
+    training step), not the host's issue rate of an eager torch.autograd sequence.
+    `stream`: the capture stream -- for a torch.autograd backward it must be the stream its
+    forward ran on (autograd issues each backward op on its forward op's stream)."""
+    with torch.cuda.stream(stream) if stream is not None else torch.cuda.stream(torch.cuda.current_stream()):
+        fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=stream):
+        fn()
+    g.replay()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        g.replay()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps
 
 
 def _oracle():
@@ -164,7 +185,8 @@ def _roof_mfma(name, flops, ms, note, calls):
 
 def smore_kernel_rooflines(model, B, d):
     """SMORE's dominant launches per forward/backward pass, each timed alone (HIP events on
-    the stream the kernels use) on the model's own operands, with its algorithmic work:
+    the stream the kernels use; multi-launch sequences captured once and replayed, as the
+    training step runs them) on the model's own operands, with its algorithmic work:
       * the three item views' kNN products in one launch (spmm_batch STORE): per view
         4(NI+1) + 8 nnz + 4 NI d (X read once) + 4 NI d (Y written) bytes;
       * the projections' backward (rsx_linear_bwd, one per modality): dW = g^T X and
@@ -196,7 +218,7 @@ def smore_kernel_rooflines(model, B, d):
     W = model.image_trs.weight.detach()
     nv = V.shape[0]
     gi = torch.randn(nv, d, generator=g).to(dev)
-    ms = time_kernel(lambda: ops.linear_bwd(gi, V, W), 20)
+    ms = time_graph(lambda: ops.linear_bwd(gi, V, W), 20)
     out.append(_roof_mfma(f"rsx_linear_bwd (wgrad_partial<DX>) projection backward {nv}x{V.shape[1]}->{d}",
                           4.0 * nv * d * V.shape[1], ms, "f32 MFMA 32x32x2 (dW) + 16x16x4 (dX)", 2))
     # preference block backward on 3B rows
@@ -205,13 +227,16 @@ def smore_kernel_rooflines(model, B, d):
     tabs = [torch.randn(n, d, generator=g).to(dev).requires_grad_() for _ in range(4)]
     rows = torch.randint(0, n, (3 * B,), generator=g).to(dev)
     seed = torch.zeros(1, dtype=torch.int64, device=dev)
-    outs = SF.preference_rows(model, *tabs, rows, seed)
-    gos = [torch.randn_like(o) for o in outs]
+    cs = torch.cuda.Stream(device=dev)  # the forwards run on the capture stream (time_graph)
+    cs.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(cs):
+        outs = SF.preference_rows(model, *tabs, rows, seed)
+        gos = [torch.randn_like(o) for o in outs]
 
     def pref_bwd():
         torch.autograd.grad(outs, tabs, gos, retain_graph=True)
 
-    ms = time_kernel(pref_bwd, 20)
+    ms = time_graph(pref_bwd, 20, cs)
     out.append(_roof_mfma(f"pref_rows<{d}> backward + weight gradients ({3 * B} batch rows)", 28.0 * 3 * B * d * d,
                           ms, "16x16x4 f32 MFMA row tiles; one 16-row tile per wave", 1))
     # InfoNCE backward of both terms (compact rows)
@@ -220,12 +245,14 @@ def smore_kernel_rooflines(model, B, d):
     allc = torch.randn(3 * B, d, generator=g).to(dev).requires_grad_()
     ar = torch.arange(B, device=dev)
     trip = torch.stack([ar, ar, ar + B]).contiguous()
-    tot, _ = SF.smore_loss_rows(allc, side, cont, trip, ar, B, 1e-5, 2048.0, 0.01, 0.2)
+    cs.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(cs):
+        tot, _ = SF.smore_loss_rows(allc, side, cont, trip, ar, B, 1e-5, 2048.0, 0.01, 0.2)
 
     def nce_bwd():
         torch.autograd.grad(tot, [side, cont], retain_graph=True)
 
-    ms = time_kernel(nce_bwd, 20)
+    ms = time_graph(nce_bwd, 20, cs)
     out.append(_roof_mfma(f"nce_bwd<{d}> InfoNCE backward, both terms (B = {B})", 8.0 * B * B * d, ms,
                           "f32 MFMA; the B x B similarity tiles recomputed flash-style", 1))
     out.sort(key=lambda r: -r["avg_launch_ms"] * r["launches_per_pass"])
@@ -347,6 +374,11 @@ def bench_model(args):
     n_warm = args.warmup
     if w["model"] == "LayerGCN":
         n_warm = max(n_warm, 2 * len(train) + 1)
+    if sharded:
+        # a rank's balanced slices come in two sizes: one whole epoch (+ a few) untimed, so every
+        # (slice size, batch kind) graph has been captured before the timed steps, as in the
+        # one-GPU line, whose single batch size is captured within its warm-up
+        n_warm = max(n_warm, int(model.steps_per_epoch) + 6)
     for _ in range(n_warm):
         one_step()
     torch.cuda.synchronize()
@@ -552,6 +584,39 @@ def _c4_chunk(args):
     return c, u, i, lab
 
 
+def relabel_graph(df, how):
+    """The interaction frame with users and items renumbered (experiment: SpMM gather locality,
+    DESIGN §3): "degree" (each side by descending training degree) or "rcm" (reverse
+    Cuthill-McKee of the symmetric bipartite graph, users and items each kept in their RCM
+    order).  A permutation of rows only: the propagation's values per node are unchanged."""
+    import scipy.sparse as sp
+    from scipy.sparse.csgraph import reverse_cuthill_mckee
+
+    u = df.userID.values.astype(np.int64)
+    i = df.itemID.values.astype(np.int64)
+    nu, ni = int(u.max()) + 1, int(i.max()) + 1
+    tr = df.x_label.values == 0
+    if how == "degree":
+        ou = np.argsort(-np.bincount(u[tr], minlength=nu), kind="stable")
+        oi = np.argsort(-np.bincount(i[tr], minlength=ni), kind="stable")
+    elif how == "rcm":
+        n = nu + ni
+        a = sp.coo_matrix((np.ones(int(tr.sum()), np.float32), (u[tr], nu + i[tr])), shape=(n, n)).tocsr()
+        order = reverse_cuthill_mckee((a + a.T).tocsr(), symmetric_mode=True)
+        ou = order[order < nu]
+        oi = order[order >= nu] - nu
+    else:
+        raise SystemExit(f"RSX_BENCH_RELABEL={how!r}: degree or rcm")
+    new_u = np.empty(nu, np.int64)
+    new_u[ou] = np.arange(nu)
+    new_i = np.empty(ni, np.int64)
+    new_i[oi] = np.arange(ni)
+    out = df.copy()
+    out["userID"] = new_u[u]
+    out["itemID"] = new_i[i]
+    return out
+
+
 def load_graph(workload, rank, world, c4_chunks=None, replicated=False, c4_dim=256):
     """(train users, train items, valid users, valid items, n_users, n_items, d, desc) of
     this rank.  c2: every rank owns its own sports-shaped block of users (rank-seeded)
@@ -564,6 +629,9 @@ def load_graph(workload, rank, world, c4_chunks=None, replicated=False, c4_dim=2
         shape = "sports" if workload == "c2" else "baby"
         nu0, ni, ne0 = synth.SHAPES[shape]
         df = synth.amazon_like(nu0, ni, ne0, seed=0 if replicated else rank)
+        relabel = os.environ.get("RSX_BENCH_RELABEL")
+        if relabel:  # locality experiment: the same graph under a node relabelling (a permutation)
+            df = relabel_graph(df, relabel)
         tr, va = df[df.x_label == 0], df[df.x_label == 1]
         desc = (f"C2: LightGCN K=3 d=64, sports-shaped (35,598 users x 18,357 items per rank), B=2048 per rank, "
                 f"device sampler, fused step" if workload == "c2" else
@@ -781,10 +849,11 @@ def main():
     _STDOUT_FD = os.dup(1)
     os.dup2(2, 1)
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", default="c2", choices=["c2", "baby", "c1", "c3", "c4", "c5"],
-                    help="c2 (default): the headline LightGCN sports config; baby: LightGCN on baby (north_star's "
-                         "10x leg); c1/c3: LayerGCN / SMORE on baby; c5: SMORE d=128 CLIP on clothing; "
-                         "c4: LightGCN d=256 on the 10M-user graph, row-sharded")
+    ap.add_argument("--workload", default=None, choices=["c2", "baby", "c1", "c3", "c4", "c5"],
+                    help="default: c2 at N = 1 (the headline LightGCN sports config), c4 --dim 64 at N > 1 (the "
+                         "metric's d = 64 on the 10M-user graph, strong scaling: the ranks divide the graph); "
+                         "baby: LightGCN on baby (north_star's 10x leg); c1/c3: LayerGCN / SMORE on baby; "
+                         "c5: SMORE d=128 CLIP on clothing; c4: LightGCN d=256 on the 10M-user graph, row-sharded")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=None, help="default 200 (c4: 20)")
     ap.add_argument("--warmup", type=int, default=None, help="default 20 (c4: 3)")
@@ -793,7 +862,7 @@ def main():
     ap.add_argument("--sharded", action="store_true",
                     help="use the row-sharded engine even at N=1 (measures its host/launch overhead)")
     ap.add_argument("--dist", choices=["dp", "rowshard"], default=None,
-                    help="N>1 scheme for c2/baby: rowshard (default: every rank its own sports-shaped user block "
+                    help="N>1 scheme for --workload c2/baby: rowshard (default: every rank its own sports-shaped user block "
                          "over the same items, users row-sharded, item partials reduced per layer, rsx.dist: the "
                          "ranks divide the propagation) or dp (the graph replicated, every rank evaluating the "
                          "global batch, rsx.dp); c4 is always rowshard")
@@ -814,6 +883,15 @@ def main():
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU only: exercise the N-rank launch and report (gloo), no GPU work")
     args = ap.parse_args()
+    n_ranks = int(os.environ.get("WORLD_SIZE", args.gpus))
+    if args.workload is None:
+        # N = 1: C2, the config the metric is quoted on.  N > 1: the metric's d = 64 LightGCN on
+        # the 10M-user graph, row-sharded (strong scaling).  The sports graph cannot be divided
+        # profitably (0.14 ms a step on one GPU): its row-sharded and data-parallel multi-GPU
+        # legs both lose to one GPU at the same global batch
+        args.workload = "c2" if n_ranks <= 1 else "c4"
+        if args.workload == "c4" and args.dim is None:
+            args.dim = 64
     if os.environ.get("RSX_COMM_SIM"):  # the bench is the latency-injection mode's one user
         os.environ.setdefault("RSX_COMM_SIM_OPT_IN", "1")
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -1251,6 +1329,11 @@ def main():
             "gpu_ms_per_step_events": gpu_ms / args.steps,
             "train_loss_mean": loss_mean,
         }
+        if big and d == 64:
+            out["scaling_note"] = ("N > 1 default: the metric's d = 64 LightGCN on the fixed 10M-user graph, strong "
+                                   "scaling; its one-GPU anchor is `bench.py --workload c4 --dim 64` (round 6: "
+                                   "40.5 ms/step, 50.6 k interactions/s, profiles/r06/c4d64/), not the N = 1 default "
+                                   "line (C2, the sports graph), so value_N / (N x value_C2) is not an efficiency")
         if sim and dp:
             lib = L.lib()
             Wm = sim["world"]

@@ -1143,7 +1143,13 @@ __global__ __launch_bounds__(64 * kNceWaves) void nce_bwd_t(NceArgs a) {
     // MFMAs (NG = 2 halves the L2 reads of the other view's tiles; same K split over the
     // waves, same order, so the results are NG = 1's bit for bit)
     constexpr int T = D / 16;
-    __shared__ __attribute__((aligned(16))) float red[kNceWaves][16][D];
+    // rows padded by 8 floats: the epilogue's ds_read_b128 of red[i][c][16 t + 4 g] (lane
+    // c + 16 g) then puts the 16 lanes of each of its lane groups on 16 distinct 4-bank
+    // segments (row stride 8 c mod 64 banks, g shifting by 4); unpadded, the 8 lanes of one
+    // g in a group hit the same 4 banks (8-way: PMC conflict share 0.75).  The
+    // ds_write_b32 of the partials stays at most 2-way (free for that instruction).
+    constexpr int LDR = D + 8;
+    __shared__ __attribute__((aligned(16))) float red[kNceWaves][16][LDR];
     nce_extra(a);
     const int term = blockIdx.z, mode = blockIdx.y;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;

@@ -550,8 +550,14 @@ class SMORE(GeneralRecommender):
         self._gate_buf = torch.zeros(1, dtype=torch.float32, device=self.device)
 
     def _side_stream(self):
-        """The UI backbone's stream (one per model), or None (RSX_SMORE_STREAMS=0)."""
+        """The UI backbone's stream (one per model), or None (RSX_SMORE_STREAMS=0).  None as
+        well for a multi-rank model over an rsx communicator: its captured step, with the
+        UI backbone's branch and the exchange's comm-stream branch beside the main stream,
+        replayed at 9.2 ms a C5 step (latency-injected, W = 4) where the same step without
+        the side branch takes 6.1 and eagerly issued 6.2 (profiles/r06/c5_dp/diag)."""
         if os.environ.get("RSX_SMORE_STREAMS", "1") == "0":
+            return None
+        if self.sharded and getattr(getattr(self, "comm", None), "native", False):
             return None
         st = getattr(self, "_ui_stream", None)
         if st is None:

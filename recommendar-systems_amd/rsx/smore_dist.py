@@ -150,6 +150,18 @@ class Comm:
         if self.handle is not None:
             L.check(L.lib().rsx_comm_wait(self.handle, ops._stream()), "rsx_comm_wait")
 
+    def allgather_start_(self, t: torch.Tensor, count: int) -> torch.Tensor:
+        """allgather_ without the wait (RCCL: on the communicator's stream, paired with
+        wait()); host collectives are synchronous."""
+        if self.world == 1 or self.handle is None:
+            return self.allgather_(t, count)
+        if t.dtype != torch.float32 or not t.is_contiguous() or t.numel() < self.world * count:
+            raise RuntimeError("Comm.allgather_start_: a contiguous float32 tensor of world * count elements")
+        n = int(count) * (self.world if self.sim else 1)
+        L.check(L.lib().rsx_comm_allgather_f32_start(self.handle, t.data_ptr(), n, ops._stream()),
+                "rsx_comm_allgather_f32_start")
+        return t
+
     def allgather_(self, t: torch.Tensor, count: int) -> torch.Tensor:
         """t[r count:(r+1) count] := rank r's slice, every r (t: world * count floats)."""
         if self.world == 1:
@@ -241,6 +253,13 @@ class RowGradExchange:
     def exchange(self, rows: torch.Tensor, tables, wgrads):
         """tables: the T [N, d] gradients (valid on `rows`; rebuilt in place on the union
         rows); wgrads: weight / bias gradients (None entries kept), returned summed."""
+        self.start(rows, tables)
+        return self.finish(tables, wgrads)
+
+    def start(self, rows: torch.Tensor, tables):
+        """Pack this rank's rows and start the all-gather (its comm-stream branch runs while
+        the caller's stream goes on, e.g. with the weights' gradient products); finish()
+        joins it."""
         n = int(rows.numel())
         if n > self.n_max or n < 1:
             raise RuntimeError(f"RowGradExchange: {n} batch rows (capacity {self.n_max})")
@@ -258,7 +277,13 @@ class RowGradExchange:
             for q in range(W):
                 if q != r:
                     self.packed[q].copy_(self.packed[r])
-        self.comm.allgather_(self.packed.view(-1), self.n_max * self.E)
+        self.comm.allgather_start_(self.packed.view(-1), self.n_max * self.E)
+
+    def finish(self, tables, wgrads):
+        """Join the all-gather, rebuild the tables on the union rows, sum the weights'
+        gradients (one all-reduce); returns the summed weight gradients."""
+        W = self.comm.world
+        self.comm.wait()
         if self.hip:
             tp = (C.c_void_p * self.T)(*[t.data_ptr() for t in tables])
             L.check(L.lib().rsx_rowx_combine(ops._p(self.packed), W, self.n_max, tp, self.T, self.d,

@@ -213,12 +213,15 @@ class _PrefRows(torch.autograd.Function):
                                             ctx.p_drop, _p(seed), None, None, None, None, _p(g_all), _p(g_side),
                                             _p(g_crows), _p(gC), _p(gIE), _p(gTE), _p(gFE), _p(hv), _p(ht),
                                             _arr(dz), _p(occ), ops._stream()), "rsx_smore_pref_rows")
+        tables = (gC, gIE, gTE, gFE)
+        if ctx.exch is not None:  # data-parallel SMORE: the exchange (RowGradExchange) starts here,
+            ctx.exch.start(rows, tables)  # its all-gather overlapping the weight-gradient products
         xs = [f_rows, hv, f_rows, ht, c_rows, c_rows, c_rows]
         grads = _wgrad([(dz[i], xs[i], ctx.has_b[i]) for i in range(7)], d, C_.device)
         gW = [g[0] for g in grads]
         gb = [g[1] for g in grads]
-        if ctx.exch is not None:  # data-parallel SMORE: the one exchange (rsx.smore_dist.RowGradExchange)
-            gwb = ctx.exch.exchange(rows, (gC, gIE, gTE, gFE), gW + gb)
+        if ctx.exch is not None:
+            gwb = ctx.exch.finish(tables, gW + gb)
             gW, gb = gwb[:7], gwb[7:]
         return (gC, gIE, gTE, gFE, None, None, None, None, None, *gW, *gb)
 
