@@ -905,10 +905,6 @@ int rsx_comm_wait(rsx_comm_t comm, rsx_stream_t stream);
 /* buf[r n, (r+1) n) := rank r's slice for every rank r (buf holds world * n floats), in
  * place, stream-ordered as above. */
 int rsx_comm_allgather_f32(rsx_comm_t comm, float* buf, int64_t n, rsx_stream_t stream);
-/* The same all-gather without the wait, paired with rsx_comm_wait as the all-reduce start
- * (data-parallel SMORE overlaps its batch-row exchange with the preference weights'
- * gradient products). */
-int rsx_comm_allgather_f32_start(rsx_comm_t comm, float* buf, int64_t n, rsx_stream_t stream);
 
 /*
  * One LightGCN batch on this rank's shard (the sharded twin of rsx_lightgcn_step;

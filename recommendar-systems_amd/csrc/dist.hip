@@ -1124,16 +1124,6 @@ int rsx_comm_allgather_f32(rsx_comm_t c, float* buf, int64_t count, rsx_stream_t
     return rsx::wait(s, j);
 }
 
-int rsx_comm_allgather_f32_start(rsx_comm_t c, float* buf, int64_t count, rsx_stream_t stream) {
-    if (!c || (!buf && count > 0) || count < 0) return RSX_ERR_ARG;
-    if (c->pending) return RSX_ERR_ARG;  // one exchange in flight: every start pairs with one rsx_comm_wait
-    int rc = 0;
-    hipEvent_t j = rsx::collective(c, RSX_COLL_ALLGATHER, buf, count, RSX_COLL_F32, rsx::as_stream(stream), &rc);
-    if (!j) return rc;
-    c->pending = j;
-    return RSX_OK;
-}
-
 int rsx_sharded_lightgcn_forward(const rsx_sharded_lgcn_step* st, rsx_stream_t stream) {
     if (!rsx::valid(st)) return RSX_ERR_ARG;
     if (st->row_tag && (st->n_layers == 2 || st->n_layers == 3))

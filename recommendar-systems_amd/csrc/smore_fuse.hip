@@ -1143,13 +1143,14 @@ __global__ __launch_bounds__(64 * kNceWaves) void nce_bwd_t(NceArgs a) {
     // MFMAs (NG = 2 halves the L2 reads of the other view's tiles; same K split over the
     // waves, same order, so the results are NG = 1's bit for bit)
     constexpr int T = D / 16;
-    // rows padded by 8 floats: the epilogue's ds_read_b128 of red[i][c][16 t + 4 g] (lane
-    // c + 16 g) then puts the 16 lanes of each of its lane groups on 16 distinct 4-bank
-    // segments (row stride 8 c mod 64 banks, g shifting by 4); unpadded, the 8 lanes of one
-    // g in a group hit the same 4 banks (8-way: PMC conflict share 0.75).  The
-    // ds_write_b32 of the partials stays at most 2-way (free for that instruction).
-    constexpr int LDR = D + 8;
-    __shared__ __attribute__((aligned(16))) float red[kNceWaves][16][LDR];
+    // The partials' tile red[w][row][col] is stored with row r's columns rotated by 8 sig(r)
+    // floats (sig below).  Unrotated, the epilogue's ds_read_b128 of row c, columns 16 t + 4 g
+    // put the 8 lanes of one g in a lane group on the same 4 banks (8-way: PMC conflict share
+    // 0.75).  sig gives every ds_read_b128 lane group ({0-3,12-15,20-27}, ...)
+    // 16 distinct 4-bank segments, and every ds_write_b32 half-wave (rows 4g + q, g = 0, 1)
+    // 32 distinct banks (rows 4 apart rotate 16 banks apart): conflict-free both ways.
+    __shared__ __attribute__((aligned(16))) float red[kNceWaves][16][D];
+    auto rot = [](int r) { return 8 * ((2 * r + 2 * (r >> 2) + ((r >> 3) & 1)) & 7); };
     nce_extra(a);
     const int term = blockIdx.z, mode = blockIdx.y;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
@@ -1249,14 +1250,15 @@ __global__ __launch_bounds__(64 * kNceWaves) void nce_bwd_t(NceArgs a) {
 #pragma unroll
         for (int tk = 0; tk < T; ++tk)
 #pragma unroll
-            for (int q = 0; q < 4; ++q) red[w][4 * g + q][16 * tk + c] = O[h][tk][q];
+            for (int q = 0; q < 4; ++q) red[w][4 * g + q][(16 * tk + c + rot(4 * g + q)) & (D - 1)] = O[h][tk][q];
         __syncthreads();
         if (w == h) {
 #pragma unroll
             for (int t = 0; t < T; ++t) {
-                floatx4 s = *reinterpret_cast<const floatx4*>(&red[0][c][16 * t + 4 * g]);
+                const int col = (16 * t + 4 * g + rot(c)) & (D - 1);
+                floatx4 s = *reinterpret_cast<const floatx4*>(&red[0][c][col]);
 #pragma unroll
-                for (int i = 1; i < kNceWaves; ++i) s += *reinterpret_cast<const floatx4*>(&red[i][c][16 * t + 4 * g]);
+                for (int i = 1; i < kNceWaves; ++i) s += *reinterpret_cast<const floatx4*>(&red[i][c][col]);
                 S.f[t] = s;
             }
         }

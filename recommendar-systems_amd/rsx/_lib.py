@@ -135,7 +135,6 @@ def _declare(lib):
         "rsx_dp_lightgcn_step": (C.c_int, [C.POINTER(DpStep), P]),
         "rsx_comm_init_sim": (C.c_int, [C.POINTER(P), I32, C.c_double, C.c_double, I32, I64]),
         "rsx_comm_allgather_f32": (C.c_int, [P, P, I64, P]),
-        "rsx_comm_allgather_f32_start": (C.c_int, [P, P, I64, P]),
         "rsx_comm_allreduce_f32_start": (C.c_int, [P, P, I64, P]),
         "rsx_comm_wait": (C.c_int, [P, P]),
         "rsx_comm_sim_seconds": (C.c_double, [P, I32, C.c_double]),
@@ -231,7 +230,7 @@ EXPORTED = ["rsx_version", "rsx_csr_schedule_host", "rsx_csr_schedule_rebind", "
             "rsx_comm_init_host",
             "rsx_comm_allreduce_f32", "rsx_sharded_lightgcn_step", "rsx_sharded_lightgcn_forward", "rsx_sharded_lightgcn_flush",
             "rsx_dp_lightgcn_step", "rsx_dp_work_bytes", "rsx_comm_init_sim", "rsx_comm_sim_seconds",
-            "rsx_comm_allgather_f32", "rsx_comm_allgather_f32_start", "rsx_comm_allreduce_f32_start", "rsx_comm_wait",
+            "rsx_comm_allgather_f32", "rsx_comm_allreduce_f32_start", "rsx_comm_wait",
             "rsx_smore_gates", "rsx_smore_pref", "rsx_smore_pref_rows", "rsx_smore_pref_rows_occ_floats", "rsx_tag_rows", "rsx_rowx_entry_floats", "rsx_rowx_pack", "rsx_rowx_combine", "rsx_smore_wgrad_ws_bytes", "rsx_smore_wgrad",
             "rsx_smore_infonce_ws_bytes", "rsx_smore_infonce_fwd", "rsx_smore_infonce_bwd", "rsx_smore_infonce_fwd_total", "rsx_smore_infonce_bwd_scaled", "rsx_smore_loss_rows_bwd", "rsx_adam_multi", "rsx_adam_multi_scaled", "rsx_adam_multi_mg",
             "rsx_smore_unit_weights", "rsx_smore_unit_weights_bwd", "rsx_mg_alpha_ws_bytes", "rsx_mg_alpha",

@@ -150,18 +150,6 @@ class Comm:
         if self.handle is not None:
             L.check(L.lib().rsx_comm_wait(self.handle, ops._stream()), "rsx_comm_wait")
 
-    def allgather_start_(self, t: torch.Tensor, count: int) -> torch.Tensor:
-        """allgather_ without the wait (RCCL: on the communicator's stream, paired with
-        wait()); host collectives are synchronous."""
-        if self.world == 1 or self.handle is None:
-            return self.allgather_(t, count)
-        if t.dtype != torch.float32 or not t.is_contiguous() or t.numel() < self.world * count:
-            raise RuntimeError("Comm.allgather_start_: a contiguous float32 tensor of world * count elements")
-        n = int(count) * (self.world if self.sim else 1)
-        L.check(L.lib().rsx_comm_allgather_f32_start(self.handle, t.data_ptr(), n, ops._stream()),
-                "rsx_comm_allgather_f32_start")
-        return t
-
     def allgather_(self, t: torch.Tensor, count: int) -> torch.Tensor:
         """t[r count:(r+1) count] := rank r's slice, every r (t: world * count floats)."""
         if self.world == 1:
@@ -257,9 +245,11 @@ class RowGradExchange:
         return self.finish(tables, wgrads)
 
     def start(self, rows: torch.Tensor, tables):
-        """Pack this rank's rows and start the all-gather (its comm-stream branch runs while
-        the caller's stream goes on, e.g. with the weights' gradient products); finish()
-        joins it."""
+        """Pack this rank's rows and all-gather the packs.  (The all-gather is joined before
+        the caller's next launch: started asynchronously beside the preference weights'
+        gradient products, the captured C5 step replayed at 9.3-10.4 ms instead of 6.0-6.4
+        under latency injection, profiles/r06/c5_dp/overlap_dropped/ -- the same pathology as
+        a side-stream branch next to the comm branch, §6.5 of DESIGN.md.)"""
         n = int(rows.numel())
         if n > self.n_max or n < 1:
             raise RuntimeError(f"RowGradExchange: {n} batch rows (capacity {self.n_max})")
@@ -277,13 +267,12 @@ class RowGradExchange:
             for q in range(W):
                 if q != r:
                     self.packed[q].copy_(self.packed[r])
-        self.comm.allgather_start_(self.packed.view(-1), self.n_max * self.E)
+        self.comm.allgather_(self.packed.view(-1), self.n_max * self.E)
 
     def finish(self, tables, wgrads):
-        """Join the all-gather, rebuild the tables on the union rows, sum the weights'
-        gradients (one all-reduce); returns the summed weight gradients."""
+        """Rebuild the tables on the union rows, sum the weights' gradients (one
+        all-reduce); returns the summed weight gradients."""
         W = self.comm.world
-        self.comm.wait()
         if self.hip:
             tp = (C.c_void_p * self.T)(*[t.data_ptr() for t in tables])
             L.check(L.lib().rsx_rowx_combine(ops._p(self.packed), W, self.n_max, tp, self.T, self.d,

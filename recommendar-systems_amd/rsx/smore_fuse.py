@@ -214,8 +214,8 @@ class _PrefRows(torch.autograd.Function):
                                             _p(g_crows), _p(gC), _p(gIE), _p(gTE), _p(gFE), _p(hv), _p(ht),
                                             _arr(dz), _p(occ), ops._stream()), "rsx_smore_pref_rows")
         tables = (gC, gIE, gTE, gFE)
-        if ctx.exch is not None:  # data-parallel SMORE: the exchange (RowGradExchange) starts here,
-            ctx.exch.start(rows, tables)  # its all-gather overlapping the weight-gradient products
+        if ctx.exch is not None:  # data-parallel SMORE: the exchange (RowGradExchange)
+            ctx.exch.start(rows, tables)
         xs = [f_rows, hv, f_rows, ht, c_rows, c_rows, c_rows]
         grads = _wgrad([(dz[i], xs[i], ctx.has_b[i]) for i in range(7)], d, C_.device)
         gW = [g[0] for g in grads]
