@@ -122,10 +122,13 @@ namespace rsx {
 // fork / join events (tests/test_gpu_dist.py runs the poisoned stand-in with it on).
 hipError_t comm_streams_create(rsx_comm_s* c) {
     const int prio_on = env_knob("RSX_COMM_PRIORITY", 1, 0, 1);  // read per communicator
+    // diagnosis only (tools/gpu/diag_priority.py): captured collectives on the priority stream
+    // too, the round-4 configuration whose graph replays segfaulted
+    const int cap_prio = env_knob("RSX_COMM_CAPTURE_PRIORITY", 0, 0, 1);
     int least = 0, greatest = 0;
     if (prio_on && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess && greatest != least) {
         hipError_t e = hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, greatest);
-        if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream_cap, hipStreamNonBlocking);
+        if (e == hipSuccess && !cap_prio) e = hipStreamCreateWithFlags(&c->stream_cap, hipStreamNonBlocking);
         return e;
     }
     return hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
