@@ -1081,11 +1081,14 @@ int rsx_comm_destroy(rsx_comm_t c) {
     if (c->stream_cap) (void)hipStreamSynchronize(c->stream_cap);
     if (c->sim_scratch) (void)hipFree(c->sim_scratch);
     if (c->sim_save) (void)hipFree(c->sim_save);
-    if (c->nccl) rsx::rccl().destroy(c->nccl);
+    // diagnosis only (tools/gpu/diag_priority3.py): leak the comm stream (1),
+    // the RCCL communicator (2) or the fork / join events (4) instead of destroying them
+    const int keep = rsx::env_knob("RSX_COMM_DIAG_KEEP", 0, 0, 7);
+    if (c->nccl && !(keep & 2)) rsx::rccl().destroy(c->nccl);
     for (int i = 0; i < rsx::kJoinEvents; ++i)
-        if (c->join[i]) (void)hipEventDestroy(c->join[i]);
-    if (c->fork) (void)hipEventDestroy(c->fork);
-    if (c->stream) (void)hipStreamDestroy(c->stream);
+        if (c->join[i] && !(keep & 4)) (void)hipEventDestroy(c->join[i]);
+    if (c->fork && !(keep & 4)) (void)hipEventDestroy(c->fork);
+    if (c->stream && !(keep & 1)) (void)hipStreamDestroy(c->stream);
     if (c->stream_cap) (void)hipStreamDestroy(c->stream_cap);
     delete c;
     return RSX_OK;
