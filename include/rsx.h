@@ -596,6 +596,17 @@ int rsx_smore_gates(int32_t backward, const float* const* conv, const float* ite
                     const float* const* gout, float* g_item, float* const* g_conv, float* const* dz,
                     rsx_stream_t stream);
 /*
+ * rsx_smore_gates keeping the sigmoid rows (same reference site): with `saved`
+ * ([3][n][d]) the forward also writes each gate's sigmoid(Linear(conv)) rows, and the
+ * residual-mode backward reads them instead of recomputing the product (one matrix
+ * product a row instead of two).  The mul-mode backward ignores it.  saved = NULL is
+ * rsx_smore_gates.
+ */
+int rsx_smore_gates_saved(int32_t backward, const float* const* conv, const float* item, const float* const* W,
+                          const float* const* b, int64_t n, int32_t d, float scale, int32_t mul, float* const* out,
+                          const float* const* gout, float* g_item, float* const* g_conv, float* const* dz,
+                          float* saved, rsx_stream_t stream);
+/*
  * Preference block (reference src/models/smore.py:320-341), over every user+item row:
  *   W[7] / b[7]: query_v.0, query_v.2 (no bias), query_t.0, query_t.2 (no bias),
  *   gate_image_prefer.0, gate_text_prefer.0, gate_fusion_prefer.0.
@@ -643,6 +654,25 @@ int rsx_smore_pref_rows(int32_t backward, const float* const* W, const float* co
                         float* g_text, float* g_fusion, float* hv, float* ht, float* const* dz, float* occ,
                         rsx_stream_t stream);
 size_t rsx_smore_pref_rows_occ_floats(int64_t n, int32_t d);
+/*
+ * rsx_smore_pref_rows with the forward's activations kept (same reference site,
+ * src/models/smore.py:320-341, and its autograd backward): `saved`
+ * ([rsx_smore_pref_rows_saved_floats(n, d)], compact rows) is written by the split batch-row
+ * forward (scratch hv required) -- the fusion gate's sigmoid, then per view the query
+ * MLP's tanh row, its softmax row and the preference gate's sigmoid, slots
+ * [fusion, h_img, s_img, p_img, h_txt, s_txt, p_txt] -- and read by the backward, which then
+ * recomputes no forward product (7 matrix products instead of 20); hv / ht may be NULL
+ * there (the weight gradients read the saved tanh rows, slots 1 and 4).  saved = NULL is
+ * rsx_smore_pref_rows.
+ */
+int rsx_smore_pref_rows_saved(int32_t backward, const float* const* W, const float* const* b, const float* content,
+                              const float* image_emb, const float* text_emb, const float* fusion_emb,
+                              const int64_t* rows, int64_t n, int32_t d, float p_drop, const int64_t* seed_dev,
+                              float* all_out, float* side_out, float* content_out, float* fusion_out,
+                              const float* g_all, const float* g_side, const float* g_content_in, float* g_content,
+                              float* g_image, float* g_text, float* g_fusion, float* hv, float* ht, float* const* dz,
+                              float* occ, float* saved, rsx_stream_t stream);
+size_t rsx_smore_pref_rows_saved_floats(int64_t n, int32_t d);
 /*
  * Data-parallel SMORE's batch-row gradient exchange (csrc/rowx.hip; the objective is the
  * sum over ranks of src/models/smore.py:366-411's loss of each rank's batch, and every

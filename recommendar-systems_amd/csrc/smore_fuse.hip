@@ -56,6 +56,8 @@ struct GateArgs {
     float* g_conv[3];
     float* dz[3];           // pre-activation gradients (wgrad rows)
     int64_t nbx;            // 64-row blocks of n (grid.x may be fewer: blocks stride over them)
+    float* saved;           // optional [3][n][D]: the gates' sigmoid rows (forward writes them,
+                            // gates_bwd_res_sv reads them instead of recomputing the product)
 };
 
 // Blocks stride over the 64-row blocks (grid.x <= a.nbx): a gate's weight is staged once
@@ -80,6 +82,7 @@ __global__ __launch_bounds__(256) void gates_fwd(GateArgs a) {
             const Fld<D> it = fload<D>(a.item, row, g);
             cvn = fload<D>(a.conv[m], row_of(bx + gridDim.x), g);
             const Fld<D> s = fmap<D>(mv_p<D, kLd<D>>(W, a.b[m], cv, lane), sigm);
+            if (a.saved) fstore<D>(a.saved + (int64_t)m * a.n * D, row, g, s);
             const Fld<D> o = a.mul ? fmap2<D>(it, s, [](float x, float y) { return x * y; })
                                    : fmap2<D>(it, s, [&](float x, float y) { return x + a.scale * y; });
             fstore<D>(a.out[m], row, g, o);
@@ -97,6 +100,7 @@ __global__ __launch_bounds__(256) void gates_fwd(GateArgs a) {
             const Fld<D> cv = fload<D>(a.conv[m], row, g);
             const float* W = split ? wl : stage_w<D>(wl, a.W[m]);
             const Fld<D> s = fmap<D>(mv_p<D, kLd<D>>(W, a.b[m], cv, lane), sigm);
+            if (a.saved) fstore<D>(a.saved + (int64_t)m * a.n * D, row, g, s);
             const Fld<D> o = a.mul ? fmap2<D>(it, s, [](float x, float y) { return x * y; })
                                    : fmap2<D>(it, s, [&](float x, float y) { return x + a.scale * y; });
             fstore<D>(a.out[m], row, g, o);
@@ -189,6 +193,44 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void g
     }
 }
 
+// gates_bwd_res from the forward's sigmoid rows (GateArgs::saved): one matrix product a
+// row block (d conv = W^T dz) instead of two; the same element formulas.  The next row
+// block's sigmoid and upstream-gradient rows load during this block's product.
+template <int D>
+__global__ __launch_bounds__(256) void gates_bwd_res_sv(GateArgs a) {
+    __shared__ __attribute__((aligned(16))) float wl[D * kLd<D>];
+    const int lane = threadIdx.x & 63, g = lane >> 4;
+    const int m = (int)blockIdx.y;
+    const float* W = stage_w<D>(wl, a.W[m]);
+    const float* S = a.saved + (int64_t)m * a.n * D;
+    auto row_of = [&](int64_t bx) {
+        const int64_t r = (bx * 4 + (threadIdx.x >> 6)) * 16 + (lane & 15);
+        return bx < a.nbx && r < a.n ? r : (int64_t)-1;
+    };
+    int64_t r0 = row_of(blockIdx.x);
+    Fld<D> sn = fload<D>(S, r0, g);
+    Fld<D> gn = a.gout[m] ? fload<D>(a.gout[m], r0, g) : fzero<D>();
+#pragma unroll 1
+    for (int64_t bx = blockIdx.x; bx < a.nbx; bx += gridDim.x) {  // block-uniform
+        const int64_t row = row_of(bx);
+        if (m == 0) {  // g_item = sum of the three upstream gradients, in gate order
+            Fld<D> gi = fzero<D>();
+#pragma unroll 1
+            for (int q = 0; q < 3; ++q)
+                gi = fmap2<D>(gi, a.gout[q] ? fload<D>(a.gout[q], row, g) : fzero<D>(),
+                              [](float acc, float x) { return acc + x; });
+            fstore<D>(a.g_item, row, g, gi);
+        }
+        const Fld<D> dz = fmap2<D>(fmap<D>(gn, [&](float x) { return a.scale * x; }), sn,
+                                   [](float x, float y) { return x * ((1.f - y) * y); });
+        const int64_t rn = row_of(bx + gridDim.x);
+        sn = fload<D>(S, rn, g);
+        gn = a.gout[m] ? fload<D>(a.gout[m], rn, g) : fzero<D>();
+        fstore<D>(a.dz[m], row, g, dz);
+        fstore<D>(a.g_conv[m], row, g, mvt_p<D, kLd<D>>(W, dz, lane));
+    }
+}
+
 // ---------------------------------------------------------------------------
 // preference block (smore.py:320-341)
 // ---------------------------------------------------------------------------
@@ -226,7 +268,22 @@ struct PrefArgs {
     // backward (batch rows, optional): [kOcc][n][D] per-occurrence row gradients instead of
     // float atomics into the tables; pref_segsum then sums them per table row in a fixed order
     float* occ;
+    // batch rows, optional: [kSv][n][D] the forward's activations (written by pref_fwd_rows,
+    // read by pref_bwd_rows_sv instead of recomputing 13 of the backward's 20 products)
+    float* saved;
 };
+
+// the saved activation slots: the fusion gate's sigmoid, then per view v (image 0, text 1)
+// the query MLP's tanh row, its softmax row and the preference gate's sigmoid (all before
+// the dropout mask, which the backward recomputes from the seed)
+constexpr int kSvF = 0, kSv = 7;
+__host__ __device__ constexpr int sv_h(int v) { return 1 + 3 * v; }
+__host__ __device__ constexpr int sv_s(int v) { return 2 + 3 * v; }
+__host__ __device__ constexpr int sv_p(int v) { return 3 + 3 * v; }
+template <int D>
+__device__ __forceinline__ float* sv_slot(const PrefArgs& a, int k) {
+    return a.saved ? a.saved + (int64_t)k * a.n * D : nullptr;
+}
 
 // the per-occurrence slots of pref_bwd_rows (occ): the three gC shares (parts 0, 3, 4),
 // the three gFE shares (parts 0, 1, 2), gIE, gTE
@@ -394,6 +451,7 @@ __global__ __launch_bounds__(256) void pref_fwd_rows(PrefArgs a) {
         const Fld<D> C = fload<D>(a.C, row, g);
         fstore<D>(a.c_out, out, g, C);
         Fld<D> fp = fmap<D>(lin(kWfp, C), sigm);
+        fstore<D>(sv_slot<D>(a, kSvF), out, g, fp);
         if (a.p_drop > 0.f) fp = fmap2<D>(fp, drop_scale<D>(seed, 2, row, g, a.p_drop, a.drop_scale), mul);
         const Fld<D> FE = fload<D>(a.FE, row, g);
         fstore<D>(a.fe_out, out, g, FE);
@@ -404,9 +462,12 @@ __global__ __launch_bounds__(256) void pref_fwd_rows(PrefArgs a) {
     Fld<D> s;
     {
         const Fld<D> h = fmap<D>(lin(v ? kW1t : kW1v, fload<D>(a.FE, row, g)), tanh_);
+        fstore<D>(sv_slot<D>(a, sv_h(v)), out, g, h);
         s = softmax_row<D>(lin(v ? kW2t : kW2v, h));
+        fstore<D>(sv_slot<D>(a, sv_s(v)), out, g, s);
     }
     Fld<D> pg = fmap<D>(lin(v ? kWtp : kWip, fload<D>(a.C, row, g)), sigm);
+    fstore<D>(sv_slot<D>(a, sv_p(v)), out, g, pg);
     if (a.p_drop > 0.f) pg = fmap2<D>(pg, drop_scale<D>(seed, v, row, g, a.p_drop, a.drop_scale), mul);
     const Fld<D> x = fmap3<D>(pg, s, fload<D>(v ? a.TE : a.IE, row, g), [](float p, float q, float e) { return p * (q * e); });
     fstore<D>(v ? a.hv : a.all, out, g, x);
@@ -502,6 +563,71 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
     fstore<D>(a.dz[w2], out, g, dq);
     const Fld<D> dh = mvt_p<D, kLd<D>>(stage_w<D>(wl, a.W[w2]), dq, lane);
     const Fld<D> h = fload<D>(v ? a.ht : a.hv, out, g);  // this lane's own store above
+    const Fld<D> dz1 = fmap2<D>(dh, h, [](float gy, float y) { return gy * (1.f - y * y); });
+    fstore<D>(a.dz[w1], out, g, dz1);
+    radd<D>(a, v ? kOccF2 : kOccF1, a.gFE, row, out, g, mvt_p<D, kLd<D>>(stage_w<D>(wl, a.W[w1]), dz1, lane));
+}
+
+// pref_bwd_rows from the forward's saved activations (PrefArgs::saved): the same block
+// rows, occurrence slots and element formulas, but no forward product is recomputed --
+// 7 matrix products (part 0: W_fp^T; parts 1 / 2: W_2^T then W_1^T; parts 3 / 4: W_p^T)
+// instead of 20.  The tanh rows the weight gradients read are the saved ones.
+template <int D>
+__global__ __launch_bounds__(256) void pref_bwd_rows_sv(PrefArgs a) {
+    __shared__ __attribute__((aligned(16))) float wl[D * kLd<D>];
+    const int lane = threadIdx.x & 63, g = lane >> 4;
+    const int64_t n0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 16;
+    const int64_t out = n0 + (lane & 15) < a.n ? n0 + (lane & 15) : -1;
+    const int64_t row = src_row(a, out);
+    const uint64_t seed = a.p_drop > 0.f ? (uint64_t)*a.seed : 0;
+    const auto mul = [](float x, float y) { return x * y; };
+    const auto add = [](float x, float y) { return x + y; };
+    const auto sig_bwd = [](float gy, float y) { return gy * ((1.f - y) * y); };
+    const auto g1_of = [&]() __attribute__((always_inline)) {  // d side / 3 (each stacked view's share)
+        const Fld<D> gA = fload<D>(a.g_all, out, g);
+        return a.g_side ? fmap2<D>(gA, fload<D>(a.g_side, out, g), [](float u, float v) { return (u + v) * (1.f / 3.f); })
+                        : fmap<D>(gA, [](float u) { return u * (1.f / 3.f); });
+    };
+    const int part = (int)blockIdx.y;
+    if (part == 0) {  // fusion view x3 = fp * FE, and d all -> d content
+        const Fld<D> sf = fload<D>(sv_slot<D>(a, kSvF), out, g);
+        const Fld<D> mf = a.p_drop > 0.f ? drop_scale<D>(seed, 2, row, g, a.p_drop, a.drop_scale) : Fld<D>{};
+        const Fld<D> g1 = g1_of();
+        Fld<D> dp = fmap2<D>(g1, fload<D>(a.FE, row, g), mul);
+        if (a.p_drop > 0.f) dp = fmap2<D>(dp, mf, mul);
+        const Fld<D> dz = fmap2<D>(dp, sf, sig_bwd);
+        fstore<D>(a.dz[kWfp], out, g, dz);
+        const Fld<D> fp = a.p_drop > 0.f ? fmap2<D>(sf, mf, mul) : sf;
+        radd<D>(a, kOccF0, a.gFE, row, out, g, fmap2<D>(g1, fp, mul));
+        const Fld<D> gA = fload<D>(a.g_all, out, g);
+        const Fld<D> gC = a.g_cin ? fmap2<D>(gA, fload<D>(a.g_cin, out, g), add) : gA;
+        radd<D>(a, kOccC0, a.gC, row, out, g, fmap2<D>(gC, mvt_p<D, kLd<D>>(stage_w<D>(wl, a.W[kWfp]), dz, lane), add));
+        return;
+    }
+    const int v = (part - 1) & 1;  // 0: image view, 1: text view
+    const bool gate_part = part >= 3;
+    const int w1 = v ? kW1t : kW1v, w2 = v ? kW2t : kW2v, wp = v ? kWtp : kWip;
+    const Fld<D> sp = fload<D>(sv_slot<D>(a, sv_p(v)), out, g);
+    const Fld<D> s = fload<D>(sv_slot<D>(a, sv_s(v)), out, g);
+    const Fld<D> mp = a.p_drop > 0.f ? drop_scale<D>(seed, v, row, g, a.p_drop, a.drop_scale) : Fld<D>{};
+    const Fld<D> g1 = g1_of();
+    if (gate_part) {
+        Fld<D> dpp = fmap3<D>(g1, s, fload<D>(v ? a.TE : a.IE, row, g), [](float u, float q, float e) { return u * (q * e); });
+        if (a.p_drop > 0.f) dpp = fmap2<D>(dpp, mp, mul);
+        const Fld<D> dzp = fmap2<D>(dpp, sp, sig_bwd);
+        fstore<D>(a.dz[wp], out, g, dzp);
+        radd<D>(a, v ? kOccC4 : kOccC3, a.gC, row, out, g, mvt_p<D, kLd<D>>(stage_w<D>(wl, a.W[wp]), dzp, lane));
+        return;
+    }
+    const Fld<D> pp = a.p_drop > 0.f ? fmap2<D>(sp, mp, mul) : sp;
+    Fld<D> da = fmap2<D>(g1, pp, mul);  // d (s * E)
+    radd<D>(a, v ? kOccT : kOccI, v ? a.gTE : a.gIE, row, out, g, fmap2<D>(da, s, mul));
+    da = fmap2<D>(da, fload<D>(v ? a.TE : a.IE, row, g), mul);  // d softmax output
+    const float dot = rsum<D>(fmap2<D>(da, s, mul));
+    const Fld<D> dq = fmap2<D>(s, da, [&](float y, float gy) { return y * (gy - dot); });
+    fstore<D>(a.dz[w2], out, g, dq);
+    const Fld<D> dh = mvt_p<D, kLd<D>>(stage_w<D>(wl, a.W[w2]), dq, lane);
+    const Fld<D> h = fload<D>(sv_slot<D>(a, sv_h(v)), out, g);
     const Fld<D> dz1 = fmap2<D>(dh, h, [](float gy, float y) { return gy * (1.f - y * y); });
     fstore<D>(a.dz[w1], out, g, dz1);
     radd<D>(a, v ? kOccF2 : kOccF1, a.gFE, row, out, g, mvt_p<D, kLd<D>>(stage_w<D>(wl, a.W[w1]), dz1, lane));
@@ -1614,6 +1740,14 @@ int rsx_smore_gates(int32_t backward, const float* const* conv, const float* ite
                     const float* const* b, int64_t n, int32_t d, float scale, int32_t mul, float* const* out,
                     const float* const* gout, float* g_item, float* const* g_conv, float* const* dz,
                     rsx_stream_t stream) {
+    return rsx_smore_gates_saved(backward, conv, item, W, b, n, d, scale, mul, out, gout, g_item, g_conv, dz,
+                                 nullptr, stream);
+}
+
+int rsx_smore_gates_saved(int32_t backward, const float* const* conv, const float* item, const float* const* W,
+                          const float* const* b, int64_t n, int32_t d, float scale, int32_t mul, float* const* out,
+                          const float* const* gout, float* g_item, float* const* g_conv, float* const* dz,
+                          float* saved, rsx_stream_t stream) {
     if (n < 0 || !conv || !item || !W || !b) return RSX_ERR_ARG;
     if (n == 0) return RSX_OK;
     sf::GateArgs a{};
@@ -1638,6 +1772,7 @@ int rsx_smore_gates(int32_t backward, const float* const* conv, const float* ite
     a.scale = scale;
     a.mul = mul;
     a.g_item = g_item;
+    a.saved = saved;  // the mul-mode backward (gates_bwd) recomputes the sigmoids regardless
     // one gate per block row, except the mul-mode backward (its g_item needs all three
     // sigmoids of a row: one block runs the three gates)
     a.nbx = ((n + 15) / 16 + 3) / 4;
@@ -1652,12 +1787,14 @@ int rsx_smore_gates(int32_t backward, const float* const* conv, const float* ite
     hipStream_t s = as_stream(stream);
     switch (d) {
         case 64:
-            if (backward && !mul) hipLaunchKernelGGL(sf::gates_bwd_res<64>, grid, dim3(256), 0, s, a);
+            if (backward && !mul && saved) hipLaunchKernelGGL(sf::gates_bwd_res_sv<64>, grid, dim3(256), 0, s, a);
+            else if (backward && !mul) hipLaunchKernelGGL(sf::gates_bwd_res<64>, grid, dim3(256), 0, s, a);
             else if (backward) hipLaunchKernelGGL(sf::gates_bwd<64>, grid, dim3(256), 0, s, a);
             else hipLaunchKernelGGL(sf::gates_fwd<64>, grid, dim3(256), 0, s, a);
             break;
         case 128:
-            if (backward && !mul) hipLaunchKernelGGL(sf::gates_bwd_res<128>, grid, dim3(256), 0, s, a);
+            if (backward && !mul && saved) hipLaunchKernelGGL(sf::gates_bwd_res_sv<128>, grid, dim3(256), 0, s, a);
+            else if (backward && !mul) hipLaunchKernelGGL(sf::gates_bwd_res<128>, grid, dim3(256), 0, s, a);
             else if (backward) hipLaunchKernelGGL(sf::gates_bwd<128>, grid, dim3(256), 0, s, a);
             else hipLaunchKernelGGL(sf::gates_fwd<128>, grid, dim3(256), 0, s, a);
             break;
@@ -1698,8 +1835,23 @@ int rsx_smore_pref_rows(int32_t backward, const float* const* W, const float* co
                         const float* g_side, const float* g_content_in, float* g_content, float* g_image,
                         float* g_text, float* g_fusion, float* hv, float* ht, float* const* dz, float* occ,
                         rsx_stream_t stream) {
+    return rsx_smore_pref_rows_saved(backward, W, b, content, image_emb, text_emb, fusion_emb, rows, n, d, p_drop,
+                                     seed_dev, all_out, side_out, content_out, fusion_out, g_all, g_side,
+                                     g_content_in, g_content, g_image, g_text, g_fusion, hv, ht, dz, occ, nullptr,
+                                     stream);
+}
+
+int rsx_smore_pref_rows_saved(int32_t backward, const float* const* W, const float* const* b, const float* content,
+                              const float* image_emb, const float* text_emb, const float* fusion_emb,
+                              const int64_t* rows, int64_t n, int32_t d, float p_drop, const int64_t* seed_dev,
+                              float* all_out, float* side_out, float* content_out, float* fusion_out,
+                              const float* g_all, const float* g_side, const float* g_content_in, float* g_content,
+                              float* g_image, float* g_text, float* g_fusion, float* hv, float* ht, float* const* dz,
+                              float* occ, float* saved, rsx_stream_t stream) {
     if (n < 0 || !W || !b || !content || !image_emb || !text_emb || !fusion_emb) return RSX_ERR_ARG;
     if (occ && (!backward || !rows)) return RSX_ERR_ARG;
+    // the saved activations exist for the batch-row split forward (scratch hv) and its backward
+    if (saved && (!rows || (!backward && !hv))) return RSX_ERR_ARG;
     if (p_drop < 0.f || p_drop >= 1.f || (p_drop > 0.f && !seed_dev)) return RSX_ERR_ARG;
     if (n == 0) return RSX_OK;
     sf::PrefArgs a{};
@@ -1712,7 +1864,8 @@ int rsx_smore_pref_rows(int32_t backward, const float* const* W, const float* co
             a.dz[i] = dz[i];
         }
     }
-    if (backward ? (!g_all || !g_content || !g_image || !g_text || !g_fusion || !hv || !ht) : (!all_out || !side_out))
+    if (backward ? (!g_all || !g_content || !g_image || !g_text || !g_fusion || (!saved && (!hv || !ht)))
+                 : (!all_out || !side_out))
         return RSX_ERR_ARG;
     a.C = content;
     a.IE = image_emb;
@@ -1737,6 +1890,7 @@ int rsx_smore_pref_rows(int32_t backward, const float* const* W, const float* co
     a.fe_out = backward ? nullptr : fusion_out;
     a.g_cin = backward ? g_content_in : nullptr;
     a.occ = occ;
+    a.saved = saved;
     // batch-row backward: the three views' chains as three block rows (gradients are atomics
     // there); batch-row forward with the scratch hv: likewise, then pref_combine
     const bool split_fwd = !backward && rows && hv;
@@ -1754,12 +1908,14 @@ int rsx_smore_pref_rows(int32_t backward, const float* const* W, const float* co
     }
     switch (d) {
         case 64:
-            if (backward && rows) hipLaunchKernelGGL(sf::pref_bwd_rows<64>, grid, dim3(256), 0, s, a);
+            if (backward && saved) hipLaunchKernelGGL(sf::pref_bwd_rows_sv<64>, grid, dim3(256), 0, s, a);
+            else if (backward && rows) hipLaunchKernelGGL(sf::pref_bwd_rows<64>, grid, dim3(256), 0, s, a);
             else if (backward) hipLaunchKernelGGL(sf::pref_bwd<64>, grid, dim3(256), 0, s, a);
             else hipLaunchKernelGGL(sf::pref_fwd<64>, grid, dim3(256), 0, s, a);
             break;
         case 128:
-            if (backward && rows) hipLaunchKernelGGL(sf::pref_bwd_rows<128>, grid, dim3(256), 0, s, a);
+            if (backward && saved) hipLaunchKernelGGL(sf::pref_bwd_rows_sv<128>, grid, dim3(256), 0, s, a);
+            else if (backward && rows) hipLaunchKernelGGL(sf::pref_bwd_rows<128>, grid, dim3(256), 0, s, a);
             else if (backward) hipLaunchKernelGGL(sf::pref_bwd<128>, grid, dim3(256), 0, s, a);
             else hipLaunchKernelGGL(sf::pref_fwd<128>, grid, dim3(256), 0, s, a);
             break;
@@ -1781,6 +1937,7 @@ int rsx_smore_pref_rows(int32_t backward, const float* const* W, const float* co
 }
 
 size_t rsx_smore_pref_rows_occ_floats(int64_t n, int32_t d) { return (size_t)sf::kOcc * (size_t)n * (size_t)d; }
+size_t rsx_smore_pref_rows_saved_floats(int64_t n, int32_t d) { return (size_t)sf::kSv * (size_t)n * (size_t)d; }
 
 size_t rsx_smore_wgrad_ws_bytes(int64_t n, int32_t d, int32_t n_pairs) {
     const int64_t rows = sf::wg_rows(n, d, n_pairs);

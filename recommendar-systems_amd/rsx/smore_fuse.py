@@ -22,6 +22,7 @@ rounding, which tests/test_gpu_smore_fuse.py checks against torch autograd.
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import torch
 
@@ -29,6 +30,12 @@ from . import _lib as L
 from . import ops
 
 _p = ops._p
+
+
+# RSX_PREF_SAVED=0: the batch-row preference backward and the gates' backward recompute the
+# forward's activations (the round-5 form; A/B and tests) instead of reading the ones their
+# forwards saved
+_SAVED = os.environ.get("RSX_PREF_SAVED", "1") != "0"
 
 
 def _arr(ts):
@@ -68,30 +75,38 @@ class _Gates(torch.autograd.Function):
         item = _c(item)
         n, d = item.shape
         outs = [torch.empty_like(item) for _ in range(3)]
-        L.check(L.lib().rsx_smore_gates(0, _arr(conv), _p(item), _arr(W), _arr(b), n, d, float(scale), int(mul),
-                                        _arr(outs), None, None, None, None, ops._stream()), "rsx_smore_gates")
-        ctx.save_for_backward(*conv, item, *W, *b)
+        # residual mode: the sigmoid rows for the backward (one product a row there, not two)
+        saved = (torch.empty(3, n, d, dtype=torch.float32, device=item.device)
+                 if _SAVED and not mul and any(ctx.needs_input_grad) else None)
+        L.check(L.lib().rsx_smore_gates_saved(0, _arr(conv), _p(item), _arr(W), _arr(b), n, d, float(scale),
+                                              int(mul), _arr(outs), None, None, None, None, _p(saved),
+                                              ops._stream()), "rsx_smore_gates_saved")
+        ctx.save_for_backward(*conv, item, *W, *b, saved if saved is not None else torch.empty(0))
+        ctx.has_saved = saved is not None
         ctx.cfg = (float(scale), int(mul))
         return tuple(outs)
 
     @staticmethod
     def backward(ctx, gv, gt, gf):
-        cv, ct, cf, item, Wv, Wt, Wf, bv, bt, bf = ctx.saved_tensors
-        gc, gi, wg = _gates_backward((cv, ct, cf), item, (Wv, Wt, Wf), (bv, bt, bf), ctx.cfg, (gv, gt, gf))
+        cv, ct, cf, item, Wv, Wt, Wf, bv, bt, bf, saved = ctx.saved_tensors
+        gc, gi, wg = _gates_backward((cv, ct, cf), item, (Wv, Wt, Wf), (bv, bt, bf), ctx.cfg, (gv, gt, gf),
+                                     saved if ctx.has_saved else None)
         return (*gc, gi, *wg, None, None)
 
 
-def _gates_backward(conv, item, W, b, cfg, gouts):
+def _gates_backward(conv, item, W, b, cfg, gouts, saved=None):
     """(d conv[3], d item, (d Wv, d bv, d Wt, d bt, d Wf, d bf)) of the gates: one launch
-    for the row gradients, one rsx_smore_wgrad pair for the weights."""
+    for the row gradients, one rsx_smore_wgrad pair for the weights.  `saved`: the
+    forward's [3, n, d] sigmoid rows (rsx_smore_gates_saved), or None (recomputed)."""
     scale, mul = cfg
     n, d = item.shape
     gi = torch.empty_like(item)
     gc = [torch.empty_like(item) for _ in range(3)]
     dz = [torch.empty_like(item) for _ in range(3)]
     gouts = [None if g is None else _c(g) for g in gouts]
-    L.check(L.lib().rsx_smore_gates(1, _arr(list(conv)), _p(item), _arr(list(W)), _arr(list(b)), n, d, scale, mul,
-                                    None, _arr(gouts), _p(gi), _arr(gc), _arr(dz), ops._stream()), "rsx_smore_gates")
+    L.check(L.lib().rsx_smore_gates_saved(1, _arr(list(conv)), _p(item), _arr(list(W)), _arr(list(b)), n, d, scale,
+                                          mul, None, _arr(gouts), _p(gi), _arr(gc), _arr(dz), _p(saved),
+                                          ops._stream()), "rsx_smore_gates_saved")
     (gWv, gbv), (gWt, gbt), (gWf, gbf) = _wgrad([(dz[0], conv[0], True), (dz[1], conv[1], True),
                                                  (dz[2], conv[2], True)], d, item.device)
     return gc, gi, (gWv, gbv, gWt, gbt, gWf, gbf)
@@ -176,11 +191,16 @@ class _PrefRows(torch.autograd.Function):
         n, d = rows.numel(), C_.shape[1]
         out = torch.empty(5, n, d, dtype=torch.float32, device=C_.device)
         all_, side, c_rows, f_rows, x2 = out.unbind(0)  # x2: the split forward's scratch
-        L.check(L.lib().rsx_smore_pref_rows(0, _arr(W), _arr(b), _p(C_), _p(IE), _p(TE), _p(FE), _p(rows), n, d,
-                                            float(p_drop), _p(seed), _p(all_), _p(side), _p(c_rows), _p(f_rows),
-                                            None, None, None, None, None, None, None, _p(x2), None, None, None,
-                                            ops._stream()), "rsx_smore_pref_rows")
-        ctx.save_for_backward(C_, IE, TE, FE, rows, seed, c_rows, f_rows, *W,
+        # the forward's activations for the backward (7 products instead of 20 there)
+        saved = torch.empty(int(L.lib().rsx_smore_pref_rows_saved_floats(n, d)), dtype=torch.float32,
+                            device=C_.device) if _SAVED and any(ctx.needs_input_grad) else None
+        L.check(L.lib().rsx_smore_pref_rows_saved(0, _arr(W), _arr(b), _p(C_), _p(IE), _p(TE), _p(FE), _p(rows), n,
+                                                  d, float(p_drop), _p(seed), _p(all_), _p(side), _p(c_rows),
+                                                  _p(f_rows), None, None, None, None, None, None, None, _p(x2), None,
+                                                  None, None, _p(saved), ops._stream()), "rsx_smore_pref_rows_saved")
+        ctx.has_saved = saved is not None
+        ctx.save_for_backward(C_, IE, TE, FE, rows, seed, c_rows, f_rows,
+                              saved if saved is not None else torch.empty(0), *W,
                               *[x if x is not None else torch.empty(0) for x in b])
         ctx.has_b = [x is not None for x in b]
         ctx.p_drop = float(p_drop)
@@ -189,9 +209,9 @@ class _PrefRows(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g_all, g_side, g_crows):
         sv = ctx.saved_tensors
-        C_, IE, TE, FE, rows, seed, c_rows, f_rows = sv[:8]
-        W = list(sv[8:15])
-        b = [x if h else None for x, h in zip(sv[15:22], ctx.has_b)]
+        C_, IE, TE, FE, rows, seed, c_rows, f_rows, saved = sv[:9]
+        W = list(sv[9:16])
+        b = [x if h else None for x, h in zip(sv[16:23], ctx.has_b)]
         n, d = rows.numel(), C_.shape[1]
         if g_all is None:
             g_all = torch.zeros_like(c_rows)
@@ -204,15 +224,24 @@ class _PrefRows(torch.autograd.Function):
         alloc = torch.empty if ctx.sparse else torch.zeros
         gfull = alloc(4, *C_.shape, dtype=torch.float32, device=C_.device)
         gC, gIE, gTE, gFE = gfull.unbind(0)
-        # hv, ht, dz[7] and the per-occurrence row gradients (deterministic sums, no atomics)
+        # hv, ht (the tanh rows: saved by the forward, else recomputed here), dz[7] and the
+        # per-occurrence row gradients (deterministic sums, no atomics)
         occ_n = int(L.lib().rsx_smore_pref_rows_occ_floats(n, d))
-        scratch = torch.empty(9 * n * d + occ_n, dtype=torch.float32, device=C_.device)
-        hv, ht, *dz = scratch[: 9 * n * d].view(9, n, d).unbind(0)
-        occ = scratch[9 * n * d:]
-        L.check(L.lib().rsx_smore_pref_rows(1, _arr(W), _arr(b), _p(C_), _p(IE), _p(TE), _p(FE), _p(rows), n, d,
-                                            ctx.p_drop, _p(seed), None, None, None, None, _p(g_all), _p(g_side),
-                                            _p(g_crows), _p(gC), _p(gIE), _p(gTE), _p(gFE), _p(hv), _p(ht),
-                                            _arr(dz), _p(occ), ops._stream()), "rsx_smore_pref_rows")
+        nh = 0 if ctx.has_saved else 2
+        scratch = torch.empty((7 + nh) * n * d + occ_n, dtype=torch.float32, device=C_.device)
+        fields = scratch[: (7 + nh) * n * d].view(7 + nh, n, d).unbind(0)
+        if ctx.has_saved:
+            dz = list(fields)
+            hv, ht = saved.view(-1, n, d)[1], saved.view(-1, n, d)[4]  # slots h_img, h_txt
+        else:
+            hv, ht, *dz = fields
+        occ = scratch[(7 + nh) * n * d:]
+        L.check(L.lib().rsx_smore_pref_rows_saved(1, _arr(W), _arr(b), _p(C_), _p(IE), _p(TE), _p(FE), _p(rows), n,
+                                                  d, ctx.p_drop, _p(seed), None, None, None, None, _p(g_all),
+                                                  _p(g_side), _p(g_crows), _p(gC), _p(gIE), _p(gTE), _p(gFE),
+                                                  None if ctx.has_saved else _p(hv), None if ctx.has_saved else _p(ht),
+                                                  _arr(dz), _p(occ), _p(saved) if ctx.has_saved else None,
+                                                  ops._stream()), "rsx_smore_pref_rows_saved")
         tables = (gC, gIE, gTE, gFE)
         if ctx.exch is not None:  # data-parallel SMORE: the exchange (RowGradExchange)
             ctx.exch.start(rows, tables)

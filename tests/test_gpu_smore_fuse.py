@@ -75,6 +75,28 @@ def test_gates_vs_torch(cuda, d, n, mul):
         _close(a, b, f"grad{i}")
 
 
+@pytest.mark.parametrize("d,n", [(64, 7050), (128, 1001)])
+def test_gates_saved_equals_recompute(cuda, d, n, monkeypatch):
+    """rsx_smore_gates_saved (residual mode): the backward from the forward's sigmoid rows
+    against the backward that recomputes them: every gradient agrees to float rounding."""
+    from rsx import smore_fuse as SF
+
+    gen = torch.Generator().manual_seed(3 * d + n)
+    mk = lambda: torch.randn(n, d, generator=gen).to(cuda).requires_grad_()  # noqa: E731
+    cv, ct, cf, item = mk(), mk(), mk(), mk()
+    gates = [torch.nn.Sequential(_lin(d, gen, cuda), torch.nn.Sigmoid()) for _ in range(3)]
+    up = [torch.randn(n, d, generator=gen).to(cuda) for _ in range(3)]
+    params = [cv, ct, cf, item] + [p for gm in gates for p in gm.parameters()]
+    res = {}
+    for saved in (True, False):
+        monkeypatch.setattr(SF, "_SAVED", saved)
+        got = SF.gates(cv, ct, cf, item, *gates, 0.7, False)
+        res[saved] = tuple(got) + tuple(torch.autograd.grad(sum((o * u).sum() for o, u in zip(got, up)), params))
+    for i, (x, y) in enumerate(zip(res[True], res[False])):
+        scale = float(y.abs().max()) + 1e-30
+        assert float((x - y).abs().max()) <= 1e-6 * scale, i
+
+
 class _PrefModel(torch.nn.Module):
     """The reference's preference-module submodules (smore.py:104-120)."""
 
@@ -170,6 +192,34 @@ def test_preference_rows_vs_torch_and_deterministic(cuda, d, N, n, p):
     _, _, _, gg2 = run()
     for name, a, b in zip(names[:4], gg, gg2):
         assert torch.equal(a, b), name  # the table gradients: bit-stable run to run
+
+
+@pytest.mark.parametrize("d,p", [(64, 0.0), (128, 0.1)])
+def test_preference_rows_saved_equals_recompute(cuda, d, p, monkeypatch):
+    """rsx_smore_pref_rows_saved: the backward from the forward's saved activations
+    (7 products) against the backward that recomputes them (20 products): the same
+    formulas on the same values, so every gradient agrees to float rounding."""
+    from rsx import smore_fuse as SF
+
+    gen = torch.Generator().manual_seed(5 * d)
+    N, n = 2000, 3000
+    mk = lambda: torch.randn(N, d, generator=gen).to(cuda).requires_grad_()  # noqa: E731
+    C_, IE, TE, FE = mk(), mk(), mk(), mk()
+    m = _PrefModel(d, gen, cuda, p).train()
+    rows = torch.randint(0, N, (n,), generator=gen).to(cuda)
+    seed = torch.tensor([99], dtype=torch.int64, device=cuda)
+    up = [torch.randn(n, d, generator=gen).to(cuda) for _ in range(3)]
+    params = [C_, IE, TE, FE] + list(m.parameters())
+    out = {}
+    for saved in (True, False):
+        monkeypatch.setattr(SF, "_SAVED", saved)
+        a, s_, c = SF.preference_rows(m, C_, IE, TE, FE, rows, seed)
+        out[saved] = (a, s_, c) + tuple(torch.autograd.grad((a * up[0]).sum() + (s_ * up[1]).sum() +
+                                                            (c * up[2]).sum(), params))
+    names = ["all", "side", "content_rows", "content", "image", "text", "fusion"] + [k for k, _ in m.named_parameters()]
+    for name, x, y in zip(names, out[True], out[False]):
+        scale = float(y.abs().max()) + 1e-30
+        assert float((x - y).abs().max()) <= 1e-6 * scale, name
 
 
 def test_view_prop_vs_torch(cuda):
