@@ -2011,7 +2011,8 @@ static int nce_setup(sf::NceArgs& a, const float* side, const float* content, co
     a.ttl = a.norms + 4 * batch;
     a.lrow = a.ttl + 2 * batch;
     a.E = batch <= sf::kNceStoreMax ? a.lrow + 2 * batch : nullptr;
-    a.nrmT = a.E && d == 128 ? a.E + 2 * batch * batch : nullptr;  // read by nce_bwd_t<128> only
+    static const int t64 = env_knob("RSX_NCE_T64", 1, 0, 1);
+    a.nrmT = a.E && (d == 128 || t64) ? a.E + 2 * batch * batch : nullptr;  // read by nce_bwd_t only
     return RSX_OK;
 }
 
@@ -2097,15 +2098,15 @@ int rsx_smore_loss_rows_bwd(const float* side_c, const float* content_c, const i
 
 static int nce_bwd_launch(sf::NceArgs& a, int64_t batch, int32_t d, hipStream_t s) {
     const dim3 grid((unsigned)((batch + 15) / 16), 2, 2);
-    if (a.E && d == 128) {  // the forward's exp tiles and transposed rows (same workspace, same batch);
-        // d = 64 stays on nce_bwd (the transposed-tile form measured no faster there: 95-141 vs 88 us)
+    if (a.E && a.nrmT) {  // the forward's exp tiles and transposed rows (same workspace, same batch);
+        // d = 64 too since round 6 (its reduction tile conflict-free: C3's backward 81 -> 54 us;
+        // RSX_NCE_T64=0 keeps nce_bwd<64> there, the round-5 form, for A/B)
         static const int ng = env_knob("RSX_NCE_GROUPS", 2, 1, 2);
-        if (ng == 2) {
-            const dim3 g2((unsigned)((batch + 31) / 32), 2, 2);
-            hipLaunchKernelGGL((sf::nce_bwd_t<128, 2>), g2, dim3(64 * sf::kNceWaves), 0, s, a);
-        } else {
-            hipLaunchKernelGGL((sf::nce_bwd_t<128, 1>), grid, dim3(64 * sf::kNceWaves), 0, s, a);
-        }
+        const dim3 g2((unsigned)((batch + 31) / 32), 2, 2);
+        if (d == 128 && ng == 2) hipLaunchKernelGGL((sf::nce_bwd_t<128, 2>), g2, dim3(64 * sf::kNceWaves), 0, s, a);
+        else if (d == 128) hipLaunchKernelGGL((sf::nce_bwd_t<128, 1>), grid, dim3(64 * sf::kNceWaves), 0, s, a);
+        else if (ng == 2) hipLaunchKernelGGL((sf::nce_bwd_t<64, 2>), g2, dim3(64 * sf::kNceWaves), 0, s, a);
+        else hipLaunchKernelGGL((sf::nce_bwd_t<64, 1>), grid, dim3(64 * sf::kNceWaves), 0, s, a);
     } else {
         if (d == 64) hipLaunchKernelGGL(sf::nce_bwd<64>, grid, dim3(64 * sf::kNceWaves), 0, s, a);
         else hipLaunchKernelGGL(sf::nce_bwd<128>, grid, dim3(64 * sf::kNceWaves), 0, s, a);
