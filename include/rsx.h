@@ -574,6 +574,18 @@ int rsx_topk_metrics_fast(const int64_t* topk_idx, int64_t n_users, int32_t k_ma
 size_t rsx_linear_bwd_ws_bytes(int64_t n, int32_t out_dim, int32_t in_dim);
 int rsx_linear_bwd(const float* g, const float* x, const float* W, int64_t n, int32_t out_dim, int32_t in_dim,
                    float* dw, float* dx, float* db, void* ws, size_t ws_bytes, rsx_stream_t stream);
+/*
+ * rsx_linear_bwd of two Linears over the same n rows and out_dim in one launch pair (the
+ * image_trs / text_trs backward of src/models/smore.py:256-259): problem 0 (g0, x0 [n, in0],
+ * W0) and problem 1 (g1, x1 [n, in1], W1), each result as rsx_linear_bwd defines it
+ * (deterministic).  RSX_ERR_UNSUPPORTED when the two shapes need different kernel tilings
+ * (the caller then issues two rsx_linear_bwd).
+ */
+size_t rsx_linear_bwd_pair_ws_bytes(int64_t n, int32_t out_dim, int32_t in0, int32_t in1);
+int rsx_linear_bwd_pair(const float* g0, const float* x0, const float* W0, int32_t in0, float* dw0, float* dx0,
+                        float* db0, const float* g1, const float* x1, const float* W1, int32_t in1, float* dw1,
+                        float* dx1, float* db1, int64_t n, int32_t out_dim, void* ws, size_t ws_bytes,
+                        rsx_stream_t stream);
 size_t rsx_linear_wgrad_ws_bytes(int64_t n, int32_t out_dim, int32_t in_dim);
 int rsx_linear_wgrad(const float* g, const float* x, int64_t n, int32_t out_dim, int32_t in_dim, float* dw,
                      void* ws, size_t ws_bytes, rsx_stream_t stream);
@@ -662,8 +674,8 @@ size_t rsx_smore_pref_rows_occ_floats(int64_t n, int32_t d);
  * MLP's tanh row, its softmax row and the preference gate's sigmoid, slots
  * [fusion, h_img, s_img, p_img, h_txt, s_txt, p_txt] -- and read by the backward, which then
  * recomputes no forward product (7 matrix products instead of 20); hv / ht may be NULL
- * there (the weight gradients read the saved tanh rows, slots 1 and 4).  saved = NULL is
- * rsx_smore_pref_rows.
+ * there (the weight gradients read the saved tanh rows, slots 1 and 4).  saved = plan =
+ * lead = NULL is rsx_smore_pref_rows.
  */
 int rsx_smore_pref_rows_saved(int32_t backward, const float* const* W, const float* const* b, const float* content,
                               const float* image_emb, const float* text_emb, const float* fusion_emb,
@@ -671,8 +683,17 @@ int rsx_smore_pref_rows_saved(int32_t backward, const float* const* W, const flo
                               float* all_out, float* side_out, float* content_out, float* fusion_out,
                               const float* g_all, const float* g_side, const float* g_content_in, float* g_content,
                               float* g_image, float* g_text, float* g_fusion, float* hv, float* ht, float* const* dz,
-                              float* occ, float* saved, rsx_stream_t stream);
+                              float* occ, float* saved, int32_t* plan, uint64_t* lead, rsx_stream_t stream);
 size_t rsx_smore_pref_rows_saved_floats(int64_t n, int32_t d);
+/*
+ * The occurrence plan of rsx_smore_pref_rows_saved (optional, `plan` int32
+ * [rsx_smore_pref_plan_words(n)]): the split forward lists, for each table row of `rows`,
+ * its occurrences under its first one (no scan of the row ids); the backward's per-row
+ * sums read the lists instead of scanning (same order, same result).  The forward needs
+ * `lead`, u64 [1 + table rows] scratch, zero before its first use and then owned by the
+ * caller's stream (word 0 counts the calls; keys are tagged with it, so no clearing).
+ */
+size_t rsx_smore_pref_plan_words(int64_t n);
 /*
  * Data-parallel SMORE's batch-row gradient exchange (csrc/rowx.hip; the objective is the
  * sum over ranks of src/models/smore.py:366-411's loss of each rank's batch, and every

@@ -10,6 +10,7 @@
 // strip over its rows (fp32 MFMA, exact f32 fma chains, next chunk prefetched, one
 // g value feeding IG MFMAs) and writes it to its partial slot; a second pass adds
 // the slots in a fixed order.  Deterministic: the result depends only on the shapes.
+#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 
@@ -87,12 +88,48 @@ static WgPlan wg_plan(int64_t n, int out_dim, int in_dim, int max_ig = 4, int64_
 // 16x16x4 f32 MFMA tiles from the g chunk already in LDS) and, in the blocks of
 // the first i column, the bias-gradient partials colsum(g) (the av values the dW
 // MFMAs read, summed per lane) into the slot's tail [out] floats.
+template <int IG, int OTB, bool DX>
+__device__ __forceinline__ void wgrad_partial_body(int64_t bid, const float* __restrict__ g, const float* __restrict__ x,
+                                                   int64_t n, int out_dim, int in_dim, int64_t rows, int64_t nob,
+                                                   int64_t nib, float* __restrict__ part, const float* __restrict__ W,
+                                                   float* __restrict__ dx, int do_db);
+
 template <int IG, int OTB, bool DX = false>
 __global__ __launch_bounds__(256) void wgrad_partial(const float* __restrict__ g, const float* __restrict__ x,
                                                      int64_t n, int out_dim, int in_dim, int64_t rows, int64_t nob,
                                                      int64_t nib, float* __restrict__ part,
                                                      const float* __restrict__ W = nullptr, float* __restrict__ dx = nullptr,
                                                      int do_db = 0) {
+    wgrad_partial_body<IG, OTB, DX>(blockIdx.x, g, x, n, out_dim, in_dim, rows, nob, nib, part, W, dx, do_db);
+}
+
+// Two fused projection backwards of the same rows and output width in one launch (SMORE's
+// image and text projections, src/models/smore.py:256-259): blocks [0, nb0) are problem 0's,
+// the rest problem 1's, each with its own plan (rows per split, i blocks, partial slots).
+struct LbwdProb {
+    const float* g;
+    const float* x;
+    const float* W;
+    float* dx;
+    float* part;
+    int64_t rows, nib;
+    int32_t in_dim, do_db;
+};
+
+template <int IG, int OTB>
+__global__ __launch_bounds__(256) void wgrad_partial_pair(LbwdProb p0, LbwdProb p1, int64_t nb0, int64_t n,
+                                                          int out_dim) {
+    const bool first = (int64_t)blockIdx.x < nb0;
+    const LbwdProb& q = first ? p0 : p1;
+    wgrad_partial_body<IG, OTB, true>(first ? (int64_t)blockIdx.x : (int64_t)blockIdx.x - nb0, q.g, q.x, n, out_dim,
+                                      q.in_dim, q.rows, 1, q.nib, q.part, q.W, q.dx, q.do_db);
+}
+
+template <int IG, int OTB, bool DX>
+__device__ __forceinline__ void wgrad_partial_body(int64_t bid, const float* __restrict__ g, const float* __restrict__ x,
+                                                   int64_t n, int out_dim, int in_dim, int64_t rows, int64_t nob,
+                                                   int64_t nib, float* __restrict__ part, const float* __restrict__ W,
+                                                   float* __restrict__ dx, int do_db) {
     constexpr int RW = 4 / OTB;
     constexpr int OC = 32 * OTB, IC = 32 * IG;   // block's o / i columns
     constexpr int CH = kWgChunk * RW;            // rows per block step
@@ -104,7 +141,7 @@ __global__ __launch_bounds__(256) void wgrad_partial(const float* __restrict__ g
     __shared__ __attribute__((aligned(16))) float xs[2][CH * XP];
     __shared__ __attribute__((aligned(16))) float wl[DX ? IC * WPT : 4];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, j = lane & 31, h = lane >> 5;
-    const int64_t bo = blockIdx.x % nob, bi = (blockIdx.x / nob) % nib, s = blockIdx.x / (nob * nib);
+    const int64_t bo = bid % nob, bi = (bid / nob) % nib, s = bid / (nob * nib);
     const int ob = (int)bo * OC, ib = (int)bi * IC;
     const int wo = (wave % OTB) * 32;  // wave's o strip within the block
     const int r = wave / OTB;          // row group
@@ -355,6 +392,43 @@ __global__ __launch_bounds__(256) void wgrad_reduce_dwdb(const float* __restrict
     }
 }
 
+// wgrad_reduce_dwdb of two problems in one launch: blocks [0, nb0) reduce problem 0's slots
+struct DwdbProb {
+    const float* part;
+    int S;
+    int64_t sz, stride;
+    float* dw;
+    float* db;
+};
+
+__global__ __launch_bounds__(256) void wgrad_reduce_dwdb_pair(DwdbProb p0, DwdbProb p1, int64_t nb0) {
+    __shared__ float q[4][64];
+    const bool first = (int64_t)blockIdx.x < nb0;
+    const DwdbProb& r = first ? p0 : p1;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t e = (first ? (int64_t)blockIdx.x : (int64_t)blockIdx.x - nb0) * 64 + lane;
+    const int b = (int)((int64_t)r.S * wave / 4), en = (int)((int64_t)r.S * (wave + 1) / 4);
+    float acc = 0.f;
+    if (e < r.stride) {
+        int p = b;
+        for (; p + 8 <= en; p += 8) {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = r.part[(int64_t)(p + u) * r.stride + e];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) acc += v[u];
+        }
+        for (; p < en; ++p) acc += r.part[(int64_t)p * r.stride + e];
+    }
+    q[wave][lane] = acc;
+    __syncthreads();
+    if (wave == 0 && e < r.stride) {
+        const float v = ((q[0][lane] + q[1][lane]) + q[2][lane]) + q[3][lane];
+        if (e < r.sz) r.dw[e] = v;
+        else if (r.db) r.db[e - r.sz] = v;
+    }
+}
+
 }  // namespace rsx
 
 using namespace rsx;
@@ -430,6 +504,71 @@ extern "C" int rsx_linear_bwd(const float* g, const float* x, const float* W, in
         hipLaunchKernelGGL(wgrad_reduce_strided, dim3((unsigned)((sz + 63) / 64)), dim3(256), 0, s,
                            (const float*)part, p.slots(), sz, sz, dw);
     }
+    return last_rc();
+}
+
+// the pair's plans: the 2048-wave budget split by input width (the blocks of both problems
+// then carry about the same rows x columns each, so they finish together)
+static void pair_plans(int64_t n, int32_t out_dim, int32_t in0, int32_t in1, WgPlan& p0, WgPlan& p1) {
+    const int64_t w = bwd_waves();
+    const int64_t w0 = std::max<int64_t>(4, w * in0 / (in0 + in1)), w1 = std::max<int64_t>(4, w - w0);
+    p0 = wg_plan(n, out_dim, in0, bwd_ig(), w0);
+    p1 = wg_plan(n, out_dim, in1, bwd_ig(), w1);
+}
+
+extern "C" size_t rsx_linear_bwd_pair_ws_bytes(int64_t n, int32_t out_dim, int32_t in0, int32_t in1) {
+    if (n <= 0 || (out_dim != 32 && out_dim != 64 && out_dim != 128) || in0 <= 0 || in1 <= 0 || (in0 % 4) || (in1 % 4))
+        return 0;
+    WgPlan p0, p1;
+    pair_plans(n, out_dim, in0, in1, p0, p1);
+    const size_t s0 = (size_t)p0.slots() * ((size_t)out_dim * (size_t)in0 + (size_t)out_dim);
+    const size_t s1 = (size_t)p1.slots() * ((size_t)out_dim * (size_t)in1 + (size_t)out_dim);
+    return (s0 + s1) * sizeof(float) + 256;
+}
+
+// rsx_linear_bwd of two Linears over the same n rows and out_dim in one launch pair (SMORE's
+// image_trs / text_trs backward, src/models/smore.py:256-259): each problem's results equal
+// its own rsx_linear_bwd's with the pair's plan (deterministic).  The image and text problems
+// each filled the chip alone; the text one (a few hundred columns) was latency-bound behind
+// the image one.  RSX_ERR_UNSUPPORTED when the two plans need different kernel shapes.
+extern "C" int rsx_linear_bwd_pair(const float* g0, const float* x0, const float* W0, int32_t in0, float* dw0,
+                                   float* dx0, float* db0, const float* g1, const float* x1, const float* W1,
+                                   int32_t in1, float* dw1, float* dx1, float* db1, int64_t n, int32_t out_dim,
+                                   void* ws, size_t ws_bytes, rsx_stream_t stream) {
+    if (n <= 0 || in0 <= 0 || in1 <= 0 || !dw0 || !dw1 || !W0 || !W1 || !dx0 || !dx1 || !g0 || !g1 || !x0 || !x1)
+        return RSX_ERR_ARG;
+    if ((out_dim != 32 && out_dim != 64 && out_dim != 128) || (in0 % 4) || (in1 % 4)) return RSX_ERR_UNSUPPORTED;
+    if (!ws || ws_bytes < rsx_linear_bwd_pair_ws_bytes(n, out_dim, in0, in1)) return RSX_ERR_WORKSPACE;
+    WgPlan p0, p1;
+    pair_plans(n, out_dim, in0, in1, p0, p1);
+    if (p0.nob != 1 || p1.nob != 1 || p0.ig != p1.ig || p0.otb != p1.otb) return RSX_ERR_UNSUPPORTED;
+    float* part0 = static_cast<float*>(ws);
+    float* part1 = part0 + (size_t)p0.slots() * ((size_t)out_dim * (size_t)in0 + (size_t)out_dim);
+    const LbwdProb a{g0, x0, W0, dx0, part0, p0.rows, p0.nib, in0, db0 != nullptr};
+    const LbwdProb b{g1, x1, W1, dx1, part1, p1.rows, p1.nib, in1, db1 != nullptr};
+    const int64_t nb0 = p0.nib * p0.splits, nb1 = p1.nib * p1.splits;
+    hipStream_t s = as_stream(stream);
+    const dim3 grid((unsigned)(nb0 + nb1));
+#define RSX_WGP(IG, OTB) hipLaunchKernelGGL((wgrad_partial_pair<IG, OTB>), grid, dim3(256), 0, s, a, b, nb0, n, (int)out_dim)
+    switch (p0.ig * 8 + p0.otb) {
+        case 4 * 8 + 4: RSX_WGP(4, 4); break;
+        case 4 * 8 + 2: RSX_WGP(4, 2); break;
+        case 4 * 8 + 1: RSX_WGP(4, 1); break;
+        case 2 * 8 + 4: RSX_WGP(2, 4); break;
+        case 2 * 8 + 2: RSX_WGP(2, 2); break;
+        case 2 * 8 + 1: RSX_WGP(2, 1); break;
+        case 1 * 8 + 4: RSX_WGP(1, 4); break;
+        case 1 * 8 + 2: RSX_WGP(1, 2); break;
+        default: RSX_WGP(1, 1); break;
+    }
+#undef RSX_WGP
+    const int64_t sz0 = (int64_t)out_dim * in0, sz1 = (int64_t)out_dim * in1;
+    // a slot is the sz weight partials, then (with a bias) the out_dim bias partials
+    const int64_t st0 = sz0 + (db0 ? out_dim : 0), st1 = sz1 + (db1 ? out_dim : 0);
+    const DwdbProb r0{part0, p0.slots(), sz0, st0, dw0, db0};
+    const DwdbProb r1{part1, p1.slots(), sz1, st1, dw1, db1};
+    const int64_t rb0 = (st0 + 63) / 64, rb1 = (st1 + 63) / 64;
+    hipLaunchKernelGGL(wgrad_reduce_dwdb_pair, dim3((unsigned)(rb0 + rb1)), dim3(256), 0, s, r0, r1, rb0);
     return last_rc();
 }
 

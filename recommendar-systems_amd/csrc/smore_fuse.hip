@@ -271,7 +271,15 @@ struct PrefArgs {
     // batch rows, optional: [kSv][n][D] the forward's activations (written by pref_fwd_rows,
     // read by pref_bwd_rows_sv instead of recomputing 13 of the backward's 20 products)
     float* saved;
+    // batch rows, optional: the occurrence plan the split forward builds for the backward's
+    // per-row sums -- plan = [n] counts then [n][kPlanCap] occurrence lists (pref_segsum_plan),
+    // lead = [1 + table rows] u64 scratch: word 0 the call counter, then one key per table row
+    int32_t* plan;
+    unsigned long long* lead;
 };
+
+// Occurrences listed per leading occurrence (more: that row falls back to segsum_one's scan)
+constexpr int kPlanCap = 128;
 
 // the saved activation slots: the fusion gate's sigmoid, then per view v (image 0, text 1)
 // the query MLP's tanh row, its softmax row and the preference gate's sigmoid (all before
@@ -448,6 +456,13 @@ __global__ __launch_bounds__(256) void pref_fwd_rows(PrefArgs a) {
     const auto lin = [&](int k, const Fld<D>& x) { return mv_p<D, kLd<D>>(stage_w<D>(wl, a.W[k]), a.b[k], x, lane); };
     const int part = (int)blockIdx.y;
     if (part == 0) {
+        if (a.plan && out >= 0 && g == 0) {
+            // occurrence plan, step 1: each table row's key keeps its first occurrence
+            // (the largest key: this call's counter in the high word, ~j in the low one)
+            const unsigned long long call = a.lead[0] + 1ull;
+            atomicMax(a.lead + 1 + row, (call << 32) | (unsigned long long)(0xFFFFFFFFu - (uint32_t)out));
+            a.plan[out] = 0;
+        }
         const Fld<D> C = fload<D>(a.C, row, g);
         fstore<D>(a.c_out, out, g, C);
         Fld<D> fp = fmap<D>(lin(kWfp, C), sigm);
@@ -476,6 +491,18 @@ __global__ __launch_bounds__(256) void pref_fwd_rows(PrefArgs a) {
 // side = ((x1 + x2) + x3) * (1/3), all = C + side over the compact rows (float4 a thread)
 template <int D>
 __global__ __launch_bounds__(256) void pref_combine(PrefArgs a) {
+    if (a.plan) {
+        // occurrence plan, step 2: occurrence j joins its row's first occurrence l's list
+        // (in any order: pref_segsum_plan sorts it); thread 0 advances the call counter
+        // (nothing in this launch reads it)
+        const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+        if (j < a.n) {
+            const int64_t l = (int64_t)(0xFFFFFFFFu - (uint32_t)a.lead[1 + a.rows[j]]);
+            const int pos = atomicAdd(a.plan + l, 1);
+            if (pos < kPlanCap) a.plan[a.n + l * kPlanCap + pos] = (int32_t)j;
+        }
+        if (j == 0) atomicAdd(a.lead, 1ull);
+    }
     const int64_t e = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
     if (e >= a.n * D) return;
     const int64_t r = e / D, f = e % D;
@@ -641,12 +668,24 @@ __global__ __launch_bounds__(256) void pref_bwd_rows_sv(PrefArgs a) {
 // made every wave a chain of ~n / 64 dependent round trips).  The row ids come from
 // `RowAt`: the global int64 array, or (pref_segsum_lds) the block's int32 copy in LDS.
 constexpr int kSegList = 128;  // a wave's occurrence list (LDS int32)
+#ifndef RSX_SEGSUM_UB
+#define RSX_SEGSUM_UB 0  // 0: 8 occurrences a round at d = 64, 4 at d = 128 (16 at d = 64 spilled: 4x slower)
+#endif
+// RSX_SEGSUM_ABL (timing ablations, tools/build_variant.py only): 1 skips the occurrence
+// loads of pref_segsum_plan, 2 its table stores
+#ifndef RSX_SEGSUM_ABL
+#define RSX_SEGSUM_ABL 0
+#endif
+template <int D>
+constexpr int kSegUB = RSX_SEGSUM_UB ? RSX_SEGSUM_UB : (D <= 64 ? 8 : 4);  // occurrences summed per round
 template <int D, typename RowAt>
 __device__ __forceinline__ void segsum_one(int64_t j, int64_t n, RowAt row_at, const float* __restrict__ occ,
                                            float* __restrict__ gC, float* __restrict__ gIE, float* __restrict__ gTE,
                                            float* __restrict__ gFE, int32_t* lst) {
     constexpr int PL = D / 64;  // columns per lane: lane + 64 p
-    constexpr int UC = 8, US = 4, UB = 4;
+    // UB occurrences' loads in flight at once: a hot row's sum is ceil(count / UB) dependent
+    // rounds (a batch's most popular item has ~80 occurrences)
+    constexpr int UC = 8, US = 4, UB = kSegUB<D>;
     const int lane = threadIdx.x & 63;
     const int64_t x = row_at(j);
     for (int64_t c = 0; c < j; c += 64 * UC) {
@@ -763,6 +802,95 @@ __global__ __launch_bounds__(64 * kSegWaves) void pref_segsum_lds(const int64_t*
     const int64_t j = (int64_t)blockIdx.x * kSegWaves + (threadIdx.x >> 6);
     if (j >= n) return;
     segsum_one<D>(j, n, [&](int64_t k) { return (int64_t)rl[k]; }, occ, gC, gIE, gTE, gFE, lst[threadIdx.x >> 6]);
+}
+
+// The per-row sums from the forward's occurrence plan: one wave per occurrence j; j leads
+// its row when its plan count is non-zero.  The leader sorts its (unordered) list into
+// ascending occurrence order and sums it as segsum_one does (same order, same bits); a row
+// with more than kPlanCap occurrences takes segsum_one's scan.  No row-id scan, no LDS copy
+// of the ids: the launch is the gathers and the stores.
+template <int D>
+__global__ __launch_bounds__(256) void pref_segsum_plan(const int64_t* __restrict__ rows, int64_t n,
+                                                        const int32_t* __restrict__ plan, const float* __restrict__ occ,
+                                                        float* __restrict__ gC, float* __restrict__ gIE,
+                                                        float* __restrict__ gTE, float* __restrict__ gFE) {
+    __shared__ int32_t lst[4][kSegList];
+    const int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (j >= n) return;
+    const int cnt = plan[j];
+    if (cnt == 0) return;  // not a first occurrence
+    int32_t* L = lst[threadIdx.x >> 6];
+    if (cnt > kPlanCap) {
+        segsum_one<D>(j, n, [&](int64_t k) { return rows[k]; }, occ, gC, gIE, gTE, gFE, L);
+        return;
+    }
+    constexpr int PL = D / 64;
+    constexpr int UB = kSegUB<D>;
+    static_assert(kPlanCap <= 128 && kPlanCap <= kSegList, "two list entries a lane");
+    const int lane = threadIdx.x & 63;
+    const int32_t* lp = plan + n + j * kPlanCap;
+    const int32_t e0 = lane < cnt ? lp[lane] : 0x7fffffff;
+    const int32_t e1 = 64 + lane < cnt ? lp[64 + lane] : 0x7fffffff;
+    int r0 = 0, r1 = 0;  // ranks: the list sorted ascending (entries are distinct)
+    for (int k = 0; k < cnt; ++k) {
+        const int32_t x = k < 64 ? __shfl(e0, k) : __shfl(e1, k - 64);
+        r0 += x < e0;
+        r1 += x < e1;
+    }
+    if (lane < cnt) L[r0] = e0;
+    if (64 + lane < cnt) L[r1] = e1;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the list stores before any lane reads it
+    __builtin_amdgcn_wave_barrier();
+    const int64_t sl = n * D;
+    float aC[PL], aF[PL], aI[PL], aT[PL];
+#pragma unroll
+    for (int p = 0; p < PL; ++p) aC[p] = aF[p] = aI[p] = aT[p] = 0.f;
+    for (int i0 = 0; i0 < cnt; i0 += UB) {
+        float v[UB][8][PL];
+#pragma unroll
+        for (int t = 0; t < UB; ++t) {
+            const int64_t k = i0 + t < cnt ? (int64_t)L[i0 + t] : j;
+            const float* o = occ + k * D + lane;
+#pragma unroll
+            for (int p = 0; p < PL; ++p) {
+                const int64_t q = 64 * p;
+                if (RSX_SEGSUM_ABL == 1) {
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) v[t][u][p] = (float)k;
+                    continue;
+                }
+                v[t][0][p] = o[kOccC0 * sl + q];
+                v[t][1][p] = o[kOccC3 * sl + q];
+                v[t][2][p] = o[kOccC4 * sl + q];
+                v[t][3][p] = o[kOccF0 * sl + q];
+                v[t][4][p] = o[kOccF1 * sl + q];
+                v[t][5][p] = o[kOccF2 * sl + q];
+                v[t][6][p] = o[kOccI * sl + q];
+                v[t][7][p] = o[kOccT * sl + q];
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < UB; ++t) {
+            if (i0 + t >= cnt) break;
+#pragma unroll
+            for (int p = 0; p < PL; ++p) {
+                aC[p] = ((aC[p] + v[t][0][p]) + v[t][1][p]) + v[t][2][p];
+                aF[p] = ((aF[p] + v[t][3][p]) + v[t][4][p]) + v[t][5][p];
+                aI[p] += v[t][6][p];
+                aT[p] += v[t][7][p];
+            }
+        }
+    }
+    const int64_t x = rows[j];
+    if (RSX_SEGSUM_ABL == 2 && aC[0] != 12345.f) return;
+#pragma unroll
+    for (int p = 0; p < PL; ++p) {
+        const int64_t col = x * D + lane + 64 * p;
+        gC[col] = aC[p];
+        gFE[col] = aF[p];
+        gIE[col] = aI[p];
+        gTE[col] = aT[p];
+    }
 }
 
 // Batch-row tags (rsx_tag_rows): row_tag[rows[j]] = *tag_dev for every j (duplicates
@@ -1838,7 +1966,7 @@ int rsx_smore_pref_rows(int32_t backward, const float* const* W, const float* co
     return rsx_smore_pref_rows_saved(backward, W, b, content, image_emb, text_emb, fusion_emb, rows, n, d, p_drop,
                                      seed_dev, all_out, side_out, content_out, fusion_out, g_all, g_side,
                                      g_content_in, g_content, g_image, g_text, g_fusion, hv, ht, dz, occ, nullptr,
-                                     stream);
+                                     nullptr, nullptr, stream);
 }
 
 int rsx_smore_pref_rows_saved(int32_t backward, const float* const* W, const float* const* b, const float* content,
@@ -1847,11 +1975,13 @@ int rsx_smore_pref_rows_saved(int32_t backward, const float* const* W, const flo
                               float* all_out, float* side_out, float* content_out, float* fusion_out,
                               const float* g_all, const float* g_side, const float* g_content_in, float* g_content,
                               float* g_image, float* g_text, float* g_fusion, float* hv, float* ht, float* const* dz,
-                              float* occ, float* saved, rsx_stream_t stream) {
+                              float* occ, float* saved, int32_t* plan, uint64_t* lead, rsx_stream_t stream) {
     if (n < 0 || !W || !b || !content || !image_emb || !text_emb || !fusion_emb) return RSX_ERR_ARG;
     if (occ && (!backward || !rows)) return RSX_ERR_ARG;
     // the saved activations exist for the batch-row split forward (scratch hv) and its backward
     if (saved && (!rows || (!backward && !hv))) return RSX_ERR_ARG;
+    // the occurrence plan: built by the split forward (lead scratch needed), read by the backward's sums
+    if (plan && (!rows || n > 0x7fffffffll || (backward ? !occ : (!hv || !lead)))) return RSX_ERR_ARG;
     if (p_drop < 0.f || p_drop >= 1.f || (p_drop > 0.f && !seed_dev)) return RSX_ERR_ARG;
     if (n == 0) return RSX_OK;
     sf::PrefArgs a{};
@@ -1891,6 +2021,8 @@ int rsx_smore_pref_rows_saved(int32_t backward, const float* const* W, const flo
     a.g_cin = backward ? g_content_in : nullptr;
     a.occ = occ;
     a.saved = saved;
+    a.plan = backward ? nullptr : plan;  // the kernels build it in the forward only
+    a.lead = reinterpret_cast<unsigned long long*>(lead);
     // batch-row backward: the three views' chains as three block rows (gradients are atomics
     // there); batch-row forward with the scratch hv: likewise, then pref_combine
     const bool split_fwd = !backward && rows && hv;
@@ -1923,7 +2055,11 @@ int rsx_smore_pref_rows_saved(int32_t backward, const float* const* W, const flo
     }
     if (occ) {  // the per-occurrence rows summed per table row (deterministic)
         if (n > 0x7fffffffll) return RSX_ERR_UNSUPPORTED;  // occurrence indices listed as int32
-        if (n <= sf::kSegLds && !seg_global()) {  // row ids < 2^31 (table rows)
+        if (plan) {  // the forward's occurrence plan
+            const dim3 sg((unsigned)((n + 3) / 4));
+            if (d == 64) hipLaunchKernelGGL(sf::pref_segsum_plan<64>, sg, dim3(256), 0, s, rows, n, plan, occ, g_content, g_image, g_text, g_fusion);
+            else hipLaunchKernelGGL(sf::pref_segsum_plan<128>, sg, dim3(256), 0, s, rows, n, plan, occ, g_content, g_image, g_text, g_fusion);
+        } else if (n <= sf::kSegLds && !seg_global()) {  // row ids < 2^31 (table rows)
             const dim3 sg((unsigned)((n + sf::kSegWaves - 1) / sf::kSegWaves)), sb(64 * sf::kSegWaves);
             if (d == 64) hipLaunchKernelGGL(sf::pref_segsum_lds<64>, sg, sb, 0, s, rows, n, occ, g_content, g_image, g_text, g_fusion);
             else hipLaunchKernelGGL(sf::pref_segsum_lds<128>, sg, sb, 0, s, rows, n, occ, g_content, g_image, g_text, g_fusion);
@@ -1938,6 +2074,7 @@ int rsx_smore_pref_rows_saved(int32_t backward, const float* const* W, const flo
 
 size_t rsx_smore_pref_rows_occ_floats(int64_t n, int32_t d) { return (size_t)sf::kOcc * (size_t)n * (size_t)d; }
 size_t rsx_smore_pref_rows_saved_floats(int64_t n, int32_t d) { return (size_t)sf::kSv * (size_t)n * (size_t)d; }
+size_t rsx_smore_pref_plan_words(int64_t n) { return (size_t)n * (size_t)(1 + sf::kPlanCap); }
 
 size_t rsx_smore_wgrad_ws_bytes(int64_t n, int32_t d, int32_t n_pairs) {
     const int64_t rows = sf::wg_rows(n, d, n_pairs);

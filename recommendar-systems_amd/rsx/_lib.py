@@ -30,6 +30,8 @@ RSX_BPR_LAYERGCN = 1
 RSX_BPR_SMORE = 2
 RSX_BPR_SMORE_ROWS = 3
 
+RSX_ERR_UNSUPPORTED = 1002
+
 _ERRORS = {1001: "RSX_ERR_ARG (bad size or null pointer)",
            1002: "RSX_ERR_UNSUPPORTED (embedding width / k not compiled)",
            1003: "RSX_ERR_WORKSPACE (workspace too small)",
@@ -158,6 +160,8 @@ def _declare(lib):
         "rsx_linear_wgrad": (C.c_int, [P, P, I64, I32, I32, P, P, C.c_size_t, P]),
         "rsx_linear_bwd_ws_bytes": (C.c_size_t, [I64, I32, I32]),
         "rsx_linear_bwd": (C.c_int, [P, P, P, I64, I32, I32, P, P, P, P, C.c_size_t, P]),
+        "rsx_linear_bwd_pair_ws_bytes": (C.c_size_t, [I64, I32, I32, I32]),
+        "rsx_linear_bwd_pair": (C.c_int, [P, P, P, I32, P, P, P, P, P, P, I32, P, P, P, I64, I32, P, C.c_size_t, P]),
         "rsx_comm_unique_id_bytes": (C.c_size_t, []),
         "rsx_comm_get_unique_id": (C.c_int, [P]),
         "rsx_comm_init": (C.c_int, [C.POINTER(P), P, I32, I32]),
@@ -174,8 +178,9 @@ def _declare(lib):
                                           P, P, P, P, P, P]),
         "rsx_smore_pref_rows_occ_floats": (C.c_size_t, [I64, I32]),
         "rsx_smore_pref_rows_saved": (C.c_int, [I32, P, P, P, P, P, P, P, I64, I32, F32, P, P, P, P, P, P, P, P, P, P,
-                                                P, P, P, P, P, P, P, P]),
+                                                P, P, P, P, P, P, P, P, P, P]),
         "rsx_smore_pref_rows_saved_floats": (C.c_size_t, [I64, I32]),
+        "rsx_smore_pref_plan_words": (C.c_size_t, [I64]),
         "rsx_tag_rows": (C.c_int, [P, P, I64, P, P]),
         "rsx_rowx_entry_floats": (C.c_size_t, [I32, I32]),
         "rsx_rowx_pack": (C.c_int, [P, I64, I64, P, I32, I32, P, P, P, P]),
@@ -229,13 +234,13 @@ EXPORTED = ["rsx_version", "rsx_csr_schedule_host", "rsx_csr_schedule_rebind", "
             "rsx_smore_spectral_spec_floats", "rsx_smore_spectral_fwd_ws_bytes", "rsx_smore_spectral_fwd",
             "rsx_smore_spectral_bwd",
             "rsx_smore_spectral_bwd_partials", "rsx_smore_spectral_bwd_ws_bytes", "rsx_smore_item_tiles", "rsx_smore_item_fwd",
-            "rsx_topk_metrics_ws_bytes", "rsx_topk_metrics", "rsx_topk_metrics_fast", "rsx_linear_wgrad_ws_bytes", "rsx_linear_wgrad", "rsx_linear_bwd_ws_bytes", "rsx_linear_bwd",
+            "rsx_topk_metrics_ws_bytes", "rsx_topk_metrics", "rsx_topk_metrics_fast", "rsx_linear_wgrad_ws_bytes", "rsx_linear_wgrad", "rsx_linear_bwd_ws_bytes", "rsx_linear_bwd", "rsx_linear_bwd_pair_ws_bytes", "rsx_linear_bwd_pair",
             "rsx_comm_unique_id_bytes", "rsx_comm_get_unique_id", "rsx_comm_init", "rsx_comm_destroy",
             "rsx_comm_init_host",
             "rsx_comm_allreduce_f32", "rsx_sharded_lightgcn_step", "rsx_sharded_lightgcn_forward", "rsx_sharded_lightgcn_flush",
             "rsx_dp_lightgcn_step", "rsx_dp_work_bytes", "rsx_comm_init_sim", "rsx_comm_sim_seconds",
             "rsx_comm_allgather_f32", "rsx_comm_allreduce_f32_start", "rsx_comm_wait",
-            "rsx_smore_gates", "rsx_smore_gates_saved", "rsx_smore_pref", "rsx_smore_pref_rows", "rsx_smore_pref_rows_occ_floats", "rsx_smore_pref_rows_saved", "rsx_smore_pref_rows_saved_floats", "rsx_tag_rows", "rsx_rowx_entry_floats", "rsx_rowx_pack", "rsx_rowx_combine", "rsx_smore_wgrad_ws_bytes", "rsx_smore_wgrad",
+            "rsx_smore_gates", "rsx_smore_gates_saved", "rsx_smore_pref", "rsx_smore_pref_rows", "rsx_smore_pref_rows_occ_floats", "rsx_smore_pref_rows_saved", "rsx_smore_pref_rows_saved_floats", "rsx_smore_pref_plan_words", "rsx_tag_rows", "rsx_rowx_entry_floats", "rsx_rowx_pack", "rsx_rowx_combine", "rsx_smore_wgrad_ws_bytes", "rsx_smore_wgrad",
             "rsx_smore_infonce_ws_bytes", "rsx_smore_infonce_fwd", "rsx_smore_infonce_bwd", "rsx_smore_infonce_fwd_total", "rsx_smore_infonce_bwd_scaled", "rsx_smore_loss_rows_bwd", "rsx_adam_multi", "rsx_adam_multi_scaled", "rsx_adam_multi_mg",
             "rsx_smore_unit_weights", "rsx_smore_unit_weights_bwd", "rsx_mg_alpha_ws_bytes", "rsx_mg_alpha",
             "rsx_axpy_multi", "rsx_knn_ws_bytes", "rsx_knn_graph", "rsx_adj_build_ws_bytes", "rsx_adj_build",

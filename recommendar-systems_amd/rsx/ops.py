@@ -408,6 +408,32 @@ def linear_bwd(g: torch.Tensor, x: torch.Tensor, W: torch.Tensor, bias: bool = T
     return dw, dx, db
 
 
+def linear_bwd_pair(p0, p1):
+    """linear_bwd of two Linears over the same rows and output width, p = (g, x, W, bias),
+    in one launch pair (rsx_linear_bwd_pair); None when the two need different kernel
+    tilings (call linear_bwd twice then)."""
+    (g0, x0, W0, b0), (g1, x1, W1, b1) = p0, p1
+    g0, x0, W0, g1, x1, W1 = (t.contiguous() for t in (g0, x0, W0, g1, x1, W1))
+    n, o = g0.shape
+    i0, i1 = x0.shape[1], x1.shape[1]
+    if g1.shape != (n, o) or x1.shape[0] != n:
+        return None
+    lib = L.lib()
+    dev = g0.device
+    out = []
+    for i, b in ((i0, b0), (i1, b1)):
+        out.append((torch.empty(o, i, dtype=torch.float32, device=dev), torch.empty(n, i, dtype=torch.float32, device=dev),
+                    torch.empty(o, dtype=torch.float32, device=dev) if b else None))
+    ws = _ws(dev, lib.rsx_linear_bwd_pair_ws_bytes(n, o, i0, i1))
+    (dw0, dx0, db0), (dw1, dx1, db1) = out
+    rc = lib.rsx_linear_bwd_pair(_p(g0), _p(x0), _p(W0), i0, _p(dw0), _p(dx0), _p(db0), _p(g1), _p(x1), _p(W1), i1,
+                                 _p(dw1), _p(dx1), _p(db1), n, o, _p(ws), ws.numel(), _stream())
+    if rc == L.RSX_ERR_UNSUPPORTED:
+        return None
+    L.check(rc, "rsx_linear_bwd_pair")
+    return out
+
+
 def linear_wgrad(g: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
     """dW = g^T x for nn.Linear over many rows (rsx_linear_wgrad): split-K over row
     blocks with an ordered partial sum, where a library GEMM would see a 64x64

@@ -36,6 +36,20 @@ _p = ops._p
 # forward's activations (the round-5 form; A/B and tests) instead of reading the ones their
 # forwards saved
 _SAVED = os.environ.get("RSX_PREF_SAVED", "1") != "0"
+# RSX_PREF_PLAN=0: the backward's per-row sums scan the row ids (pref_segsum_lds) instead of
+# reading the occurrence plan the forward built (pref_segsum_plan; same sums, same order)
+_PLAN = os.environ.get("RSX_PREF_PLAN", "1") != "0"
+_LEAD = {}
+
+
+def _lead_scratch(n_rows: int, device) -> torch.Tensor:
+    """The occurrence plan's u64 [1 + table rows] key scratch (zeroed once, then tagged per
+    call by the kernels; one per device and table size, used in stream order)."""
+    key = (torch.device(device).index, int(n_rows))
+    t = _LEAD.get(key)
+    if t is None:
+        t = _LEAD[key] = torch.zeros(1 + int(n_rows), dtype=torch.int64, device=device)
+    return t
 
 
 def _arr(ts):
@@ -192,13 +206,20 @@ class _PrefRows(torch.autograd.Function):
         out = torch.empty(5, n, d, dtype=torch.float32, device=C_.device)
         all_, side, c_rows, f_rows, x2 = out.unbind(0)  # x2: the split forward's scratch
         # the forward's activations for the backward (7 products instead of 20 there)
+        grad = any(ctx.needs_input_grad)
         saved = torch.empty(int(L.lib().rsx_smore_pref_rows_saved_floats(n, d)), dtype=torch.float32,
-                            device=C_.device) if _SAVED and any(ctx.needs_input_grad) else None
+                            device=C_.device) if _SAVED and grad else None
+        # the occurrence plan of the backward's per-row sums, built by this forward
+        plan = torch.empty(int(L.lib().rsx_smore_pref_plan_words(n)), dtype=torch.int32,
+                           device=C_.device) if _PLAN and grad and n > 0 else None
+        lead = _lead_scratch(C_.shape[0], C_.device) if plan is not None else None
         L.check(L.lib().rsx_smore_pref_rows_saved(0, _arr(W), _arr(b), _p(C_), _p(IE), _p(TE), _p(FE), _p(rows), n,
                                                   d, float(p_drop), _p(seed), _p(all_), _p(side), _p(c_rows),
                                                   _p(f_rows), None, None, None, None, None, None, None, _p(x2), None,
-                                                  None, None, _p(saved), ops._stream()), "rsx_smore_pref_rows_saved")
+                                                  None, None, _p(saved), _p(plan), _p(lead), ops._stream()),
+                "rsx_smore_pref_rows_saved")
         ctx.has_saved = saved is not None
+        ctx.plan = plan
         ctx.save_for_backward(C_, IE, TE, FE, rows, seed, c_rows, f_rows,
                               saved if saved is not None else torch.empty(0), *W,
                               *[x if x is not None else torch.empty(0) for x in b])
@@ -241,7 +262,7 @@ class _PrefRows(torch.autograd.Function):
                                                   _p(g_side), _p(g_crows), _p(gC), _p(gIE), _p(gTE), _p(gFE),
                                                   None if ctx.has_saved else _p(hv), None if ctx.has_saved else _p(ht),
                                                   _arr(dz), _p(occ), _p(saved) if ctx.has_saved else None,
-                                                  ops._stream()), "rsx_smore_pref_rows_saved")
+                                                  _p(ctx.plan), None, ops._stream()), "rsx_smore_pref_rows_saved")
         tables = (gC, gIE, gTE, gFE)
         if ctx.exch is not None:  # data-parallel SMORE: the exchange (RowGradExchange)
             ctx.exch.start(rows, tables)

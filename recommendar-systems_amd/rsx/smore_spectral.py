@@ -16,8 +16,13 @@ from __future__ import annotations
 
 import torch
 
+import os
+
 from . import _lib as L
 from . import ops
+
+# RSX_LBWD_PAIR=0: the two projection backwards as two launches (A/B)
+_PAIR = os.environ.get("RSX_LBWD_PAIR", "1") != "0"
 
 
 def spectral_supported(d: int, dv: int, dt: int) -> bool:
@@ -99,6 +104,12 @@ def _spectral_backward(saved, nd, need, g_conv, g_img_out=None, g_txt_out=None):
     grv, grt, grf = torch.empty_like(rv), torch.empty_like(rt), torch.empty_like(rf)
     L.check(lib.rsx_smore_unit_weights_bwd(p(part), part.numel() // (6 * nb), p(rv), p(rt), p(rf), d, normalize,
                                            p(grv), p(grt), p(grf), ops._stream()), "rsx_smore_unit_weights_bwd")
+    # both projections' d W, d X, d b in one launch pair (rsx_linear_bwd_pair)
+    if all(need[:6]) and _PAIR:
+        res = ops.linear_bwd_pair((gi, V, Wv, True), (gt, T, Wt, True))
+        if res is not None:
+            (dWv, dV, dbv), (dWt, dT, dbt) = res
+            return (dV, dWv, dbv, dT, dWt, dbt, grv, grt, grf)
     grads = []
     for g, X, Wx, k in ((gi, V, Wv, 0), (gt, T, Wt, 3)):
         if not (need[k] or need[k + 1] or need[k + 2]):

@@ -446,6 +446,38 @@ def test_linear_bwd_vs_torch(cuda, n, o, i):
     assert none is None
 
 
+@pytest.mark.parametrize("n,o,i0,i1,bias", [(7050, 64, 4096, 384, (True, True)), (23033, 128, 768, 384, (True, True)),
+                                             (513, 32, 192, 64, (True, False)), (200, 64, 128, 64, (False, True))])
+def test_linear_bwd_pair_vs_torch(cuda, n, o, i0, i1, bias):
+    """rsx_linear_bwd_pair (SMORE's image + text projection backward in one launch pair):
+    each problem's dW, dx, db against f64 products (as test_linear_bwd_vs_torch), and
+    deterministic; None (two single launches then) only when the tilings differ."""
+    from rsx import ops
+
+    gen = torch.Generator(device="cpu").manual_seed(n + o + i0 + i1)
+    probs = []
+    for i, b in ((i0, bias[0]), (i1, bias[1])):
+        probs.append((torch.randn(n, o, generator=gen).to(cuda), torch.randn(n, i, generator=gen).to(cuda),
+                      torch.randn(o, i, generator=gen).to(cuda), b))
+    res = ops.linear_bwd_pair(*probs)
+    if res is None:  # e.g. 48 and 24 columns tile differently: the caller's two-launch path
+        pytest.skip("tilings differ")
+    for (g, x, W, b), (dw, dx, db) in zip(probs, res):
+        gd, xd, Wd = g.double(), x.double(), W.double()
+        checks = [(dw, gd.t() @ xd, gd.abs().t() @ xd.abs()), (dx, gd @ Wd, gd.abs() @ Wd.abs())]
+        if b:
+            checks.append((db, gd.sum(0), gd.abs().sum(0)))
+        else:
+            assert db is None
+        for got, want, scale in checks:
+            assert got.shape == want.shape
+            assert torch.all((got.double() - want).abs() <= 2e-6 * scale + 1e-6), (got.double() - want).abs().max()
+    res2 = ops.linear_bwd_pair(*probs)
+    for a, b in zip(res, res2):
+        for x, y in zip(a, b):
+            assert (x is None and y is None) or torch.equal(x, y)
+
+
 def test_rsx_linear_matches_nn_linear(cuda):
     from rsx.nn import RsxLinear
 

@@ -222,6 +222,36 @@ def test_preference_rows_saved_equals_recompute(cuda, d, p, monkeypatch):
         assert float((x - y).abs().max()) <= 1e-6 * scale, name
 
 
+@pytest.mark.parametrize("d", [64, 128])
+def test_preference_rows_plan_equals_scan(cuda, d, monkeypatch):
+    """The backward's per-row sums from the forward's occurrence plan (pref_segsum_plan)
+    against the scan (pref_segsum_lds): the same occurrences in the same order, so the table
+    gradients are bit-identical; rows past the plan's 128-entry lists take the scan."""
+    from rsx import smore_fuse as SF
+
+    gen = torch.Generator().manual_seed(11 * d)
+    N, n = 3000, 6144
+    mk = lambda: torch.randn(N, d, generator=gen).to(cuda).requires_grad_()  # noqa: E731
+    C_, IE, TE, FE = mk(), mk(), mk(), mk()
+    m = _PrefModel(d, gen, cuda, 0.0).train()
+    vhot = torch.randint(0, 4, (800,), generator=gen)  # ~200 occurrences each: the scan
+    hot = torch.randint(4, 44, (n // 3,), generator=gen)  # ~50 each: long lists
+    warm = torch.randint(44, 400, (n // 3,), generator=gen)  # ~6 each
+    rows = torch.cat([vhot, hot, warm, torch.randint(0, N, (n - 2 * (n // 3) - 800,), generator=gen)])
+    rows = rows[torch.randperm(n, generator=gen)].to(cuda)
+    seed = torch.tensor([5], dtype=torch.int64, device=cuda)
+    up = [torch.randn(n, d, generator=gen).to(cuda) for _ in range(3)]
+    out = {}
+    for plan in (True, False, True):
+        monkeypatch.setattr(SF, "_PLAN", plan)
+        a, s_, c = SF.preference_rows(m, C_, IE, TE, FE, rows, seed)
+        out.setdefault(plan, []).append(torch.autograd.grad((a * up[0]).sum() + (s_ * up[1]).sum() + (c * up[2]).sum(),
+                                                            [C_, IE, TE, FE]))
+    for name, x, y, z in zip(["content", "image", "text", "fusion"], out[True][0], out[False][0], out[True][1]):
+        assert torch.equal(x, y), name
+        assert torch.equal(x, z), name  # a second call (the next plan tag) gives the same bits
+
+
 def test_view_prop_vs_torch(cuda):
     from rsx import smore_fuse as SF
     from rsx.smore import _DevGraph
