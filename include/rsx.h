@@ -657,6 +657,12 @@ int rsx_smore_pref(int32_t backward, const float* const* W, const float* const* 
  * A product with row_tag / tag_dev then treats exactly these rows as tagged.
  */
 int rsx_tag_rows(int32_t* row_tag, const int64_t* rows, int64_t n, const int32_t* tag_dev, rsx_stream_t stream);
+/*
+ * rsx_tag_rows with the bump in the same launch: tag2 = {tag, ticket} (int32 [2], zero
+ * before the first call); row_tag[rows[j]] = tag2[0] + 1, then tag2[0] holds the new tag
+ * (the caller does not bump).  Products then take tag_dev = tag2.
+ */
+int rsx_tag_rows_next(int32_t* row_tag, const int64_t* rows, int64_t n, int32_t* tag2, rsx_stream_t stream);
 
 int rsx_smore_pref_rows(int32_t backward, const float* const* W, const float* const* b, const float* content,
                         const float* image_emb, const float* text_emb, const float* fusion_emb, const int64_t* rows,

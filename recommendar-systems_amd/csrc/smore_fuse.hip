@@ -600,7 +600,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
 // 7 matrix products (part 0: W_fp^T; parts 1 / 2: W_2^T then W_1^T; parts 3 / 4: W_p^T)
 // instead of 20.  The tanh rows the weight gradients read are the saved ones.
 template <int D>
-__global__ __launch_bounds__(256) void pref_bwd_rows_sv(PrefArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void pref_bwd_rows_sv(PrefArgs a) {
     __shared__ __attribute__((aligned(16))) float wl[D * kLd<D>];
     const int lane = threadIdx.x & 63, g = lane >> 4;
     const int64_t n0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 16;
@@ -890,6 +890,22 @@ __global__ __launch_bounds__(256) void pref_segsum_plan(const int64_t* __restric
         gFE[col] = aF[p];
         gIE[col] = aI[p];
         gTE[col] = aT[p];
+    }
+}
+
+// rsx_tag_rows_next: tag_rows_k with the tag bump in the same launch.  tag2 = {tag, ticket}:
+// every thread tags with tag2[0] + 1; each block takes a ticket when its stores are issued,
+// and the last block (every other block has read tag2[0] by then) stores the new tag and
+// re-arms the ticket.  One launch instead of torch's add_ plus tag_rows_k.
+__global__ __launch_bounds__(256) void tag_rows_next_k(int32_t* __restrict__ row_tag, const int64_t* __restrict__ rows,
+                                                       int64_t n, int32_t* __restrict__ tag2) {
+    const int32_t t1 = tag2[0] + 1;
+    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (j < n) row_tag[rows[j]] = t1;
+    __syncthreads();
+    if (threadIdx.x == 0 && atomicAdd(tag2 + 1, 1) == (int)gridDim.x - 1) {
+        atomicExch(tag2, t1);
+        atomicExch(tag2 + 1, 0);
     }
 }
 
@@ -1939,6 +1955,20 @@ int rsx_smore_pref(int32_t backward, const float* const* W, const float* const* 
     return rsx_smore_pref_rows(backward, W, b, content, image_emb, text_emb, fusion_emb, nullptr, n, d, p_drop,
                                seed_dev, all_out, side_out, nullptr, nullptr, g_all, g_side, nullptr, g_content,
                                g_image, g_text, g_fusion, hv, ht, dz, nullptr, stream);
+}
+
+int rsx_tag_rows_next(int32_t* row_tag, const int64_t* rows, int64_t n, int32_t* tag2, rsx_stream_t stream) {
+    if (n < 0 || !row_tag || !tag2 || (n > 0 && !rows)) return RSX_ERR_ARG;
+    if (n == 0) n = 1, rows = nullptr;  // still one block: the bump
+    const int64_t nb = (n + 255) / 256;
+    if (nb > 0x7fffffffll) return RSX_ERR_UNSUPPORTED;
+    if (!rows) {  // no rows: the bump alone (one thread's worth of work in one block)
+        hipLaunchKernelGGL(sf::tag_rows_next_k, dim3(1), dim3(256), 0, as_stream(stream), row_tag, rows, (int64_t)0,
+                           tag2);
+        return last_rc();
+    }
+    hipLaunchKernelGGL(sf::tag_rows_next_k, dim3((unsigned)nb), dim3(256), 0, as_stream(stream), row_tag, rows, n, tag2);
+    return last_rc();
 }
 
 int rsx_tag_rows(int32_t* row_tag, const int64_t* rows, int64_t n, const int32_t* tag_dev, rsx_stream_t stream) {

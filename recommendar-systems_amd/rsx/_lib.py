@@ -182,6 +182,7 @@ def _declare(lib):
         "rsx_smore_pref_rows_saved_floats": (C.c_size_t, [I64, I32]),
         "rsx_smore_pref_plan_words": (C.c_size_t, [I64]),
         "rsx_tag_rows": (C.c_int, [P, P, I64, P, P]),
+        "rsx_tag_rows_next": (C.c_int, [P, P, I64, P, P]),
         "rsx_rowx_entry_floats": (C.c_size_t, [I32, I32]),
         "rsx_rowx_pack": (C.c_int, [P, I64, I64, P, I32, I32, P, P, P, P]),
         "rsx_rowx_combine": (C.c_int, [P, I32, I64, P, I32, I32, P, P]),
@@ -240,7 +241,7 @@ EXPORTED = ["rsx_version", "rsx_csr_schedule_host", "rsx_csr_schedule_rebind", "
             "rsx_comm_allreduce_f32", "rsx_sharded_lightgcn_step", "rsx_sharded_lightgcn_forward", "rsx_sharded_lightgcn_flush",
             "rsx_dp_lightgcn_step", "rsx_dp_work_bytes", "rsx_comm_init_sim", "rsx_comm_sim_seconds",
             "rsx_comm_allgather_f32", "rsx_comm_allreduce_f32_start", "rsx_comm_wait",
-            "rsx_smore_gates", "rsx_smore_gates_saved", "rsx_smore_pref", "rsx_smore_pref_rows", "rsx_smore_pref_rows_occ_floats", "rsx_smore_pref_rows_saved", "rsx_smore_pref_rows_saved_floats", "rsx_smore_pref_plan_words", "rsx_tag_rows", "rsx_rowx_entry_floats", "rsx_rowx_pack", "rsx_rowx_combine", "rsx_smore_wgrad_ws_bytes", "rsx_smore_wgrad",
+            "rsx_smore_gates", "rsx_smore_gates_saved", "rsx_smore_pref", "rsx_smore_pref_rows", "rsx_smore_pref_rows_occ_floats", "rsx_smore_pref_rows_saved", "rsx_smore_pref_rows_saved_floats", "rsx_smore_pref_plan_words", "rsx_tag_rows", "rsx_tag_rows_next", "rsx_rowx_entry_floats", "rsx_rowx_pack", "rsx_rowx_combine", "rsx_smore_wgrad_ws_bytes", "rsx_smore_wgrad",
             "rsx_smore_infonce_ws_bytes", "rsx_smore_infonce_fwd", "rsx_smore_infonce_bwd", "rsx_smore_infonce_fwd_total", "rsx_smore_infonce_bwd_scaled", "rsx_smore_loss_rows_bwd", "rsx_adam_multi", "rsx_adam_multi_scaled", "rsx_adam_multi_mg",
             "rsx_smore_unit_weights", "rsx_smore_unit_weights_bwd", "rsx_mg_alpha_ws_bytes", "rsx_mg_alpha",
             "rsx_axpy_multi", "rsx_knn_ws_bytes", "rsx_knn_graph", "rsx_adj_build_ws_bytes", "rsx_adj_build",

@@ -112,17 +112,17 @@ def _ego(u: torch.Tensor, i: torch.Tensor) -> torch.Tensor:
 class _RowTags:
     """Batch-row tags for the tagged propagation: row r is in the batch when
     row_tag[r] == *tag_dev; `mark` bumps the device tag and tags the batch's rows
-    (two device ops, no host sync: graph-capture safe)."""
+    (one launch, rsx_tag_rows_next; no host sync: graph-capture safe).  tag_dev is
+    {tag, ticket}: the products read word 0."""
 
     def __init__(self, n: int, device):
         self.row_tag = torch.zeros(n, dtype=torch.int32, device=device)
-        self.tag_dev = torch.zeros(1, dtype=torch.int32, device=device)
+        self.tag_dev = torch.zeros(2, dtype=torch.int32, device=device)
 
     def mark(self, rows: torch.Tensor):
-        self.tag_dev.add_(1)
         rows = rows.to(torch.int64).contiguous()
-        L.check(L.lib().rsx_tag_rows(ops._p(self.row_tag), ops._p(rows), rows.numel(), ops._p(self.tag_dev),
-                                     ops._stream()), "rsx_tag_rows")
+        L.check(L.lib().rsx_tag_rows_next(ops._p(self.row_tag), ops._p(rows), rows.numel(), ops._p(self.tag_dev),
+                                          ops._stream()), "rsx_tag_rows_next")
 
 
 class _PropMeanRows(torch.autograd.Function):

@@ -601,3 +601,25 @@ def test_loss_rows_backward_one_launch_equals_the_parts(cuda, d):
     torch.cuda.synchronize()
     assert torch.equal(got + 0.0, ref + 0.0)
     assert torch.equal(gall, gbpr * gt)
+
+
+def test_tag_rows_next_bumps_once_per_call(cuda):
+    """rsx_tag_rows_next: one launch tags rows[j] with the next tag and leaves it in
+    tag2[0] (the last of many blocks bumps it; the ticket word is re-armed), and an empty
+    row list still bumps."""
+    from rsx import _lib as L
+    from rsx import ops
+
+    n_rows, n = 9000, 5000  # 20 blocks
+    gen = torch.Generator().manual_seed(3)
+    row_tag = torch.zeros(n_rows, dtype=torch.int32, device=cuda)
+    tag2 = torch.zeros(2, dtype=torch.int32, device=cuda)
+    for call in (1, 2, 3):
+        rows = torch.randint(0, n_rows, (n,), generator=gen).to(cuda)
+        L.check(L.lib().rsx_tag_rows_next(ops._p(row_tag), ops._p(rows), n, ops._p(tag2), ops._stream()),
+                "rsx_tag_rows_next")
+        assert tag2.tolist() == [call, 0]
+        assert torch.all(row_tag[rows] == call)
+        assert int((row_tag == call).sum()) == int(torch.unique(rows).numel())
+    L.check(L.lib().rsx_tag_rows_next(ops._p(row_tag), None, 0, ops._p(tag2), ops._stream()), "rsx_tag_rows_next")
+    assert tag2.tolist() == [4, 0]
