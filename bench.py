@@ -253,8 +253,8 @@ def smore_kernel_rooflines(model, B, d):
         torch.autograd.grad(tot, [side, cont], retain_graph=True)
 
     ms = time_graph(nce_bwd, 20, cs)
-    out.append(_roof_mfma(f"nce_bwd<{d}> InfoNCE backward, both terms (B = {B})", 8.0 * B * B * d, ms,
-                          "f32 MFMA; the B x B similarity tiles recomputed flash-style", 1))
+    out.append(_roof_mfma(f"nce_bwd_t<{d},2> InfoNCE backward, both terms (B = {B})", 8.0 * B * B * d, ms,
+                          "f32 MFMA; the forward's exp(S/tau) tiles and transposed row tiles reused", 1))
     out.sort(key=lambda r: -r["avg_launch_ms"] * r["launches_per_pass"])
     return out
 
