@@ -62,9 +62,10 @@ template <int D>
 constexpr int kPjLds = 2 * kPjItems * kPjPad + 2 * D * kPjPad;
 
 // Block `bid`'s share of the projection (all 256 threads); returns its item tile.
-// lds: kPjLds<D> floats.
-template <int D>
-__device__ __forceinline__ int proj_block(const SpecProjArgs& a, int bid, float* __restrict__ lds) {
+// lds: kPjLds<D> floats.  DS > D (smore_proj_half): the block computes output features
+// [fh D, fh D + D) of rows DS wide, from W's rows fh D .. fh D + D - 1.
+template <int D, int DS = D>
+__device__ __forceinline__ int proj_block(const SpecProjArgs& a, int bid, float* __restrict__ lds, int fh = 0) {
     constexpr int FT = D / 32;            // feature tiles
     constexpr int TPW = 2 * FT / 4;       // tiles per wave (FT/2: 1 for d=64, 2 for d=128)
     constexpr int NX = kPjItems * kPjK / 4, NW = D * kPjK / 4;  // float4s per chunk
@@ -79,8 +80,8 @@ __device__ __forceinline__ int proj_block(const SpecProjArgs& a, int bid, float*
     const int S = a.S[m];
     const int tile = bid % a.tiles, sp = bid / a.tiles;
     const float* __restrict__ X = a.X[m];
-    const float* __restrict__ W = a.W[m];
     const int K = a.K[m];
+    const float* __restrict__ W = a.W[m] + (int64_t)fh * D * K;
     const int nch_all = (K + kPjK - 1) / kPjK;
     const int per = (nch_all + S - 1) / S;
     const int c_beg = sp * per, c_end = min(nch_all, c_beg + per);
@@ -161,14 +162,14 @@ __device__ __forceinline__ int proj_block(const SpecProjArgs& a, int bid, float*
         if (c + 1 < nch) step(c + 1, std::integral_constant<int, 1>{});
     }
     // C layout: lane holds column (feature) ft*32 + j, rows (items) it*32 + (e&3) + 8(e>>2) + 4h
-    float* out = a.out[m][sp];
+    float* out = a.out[m][sp] + fh * D;
 #pragma unroll
     for (int q = 0; q < TPW; ++q) {
         const int f = ((wave >> 1) + 2 * q) * 32 + j;
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
             const int64_t row = i0 + it * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-            if (row < a.n) out[row * D + f] = acc[q][e];
+            if (row < a.n) out[row * DS + f] = acc[q][e];
         }
     }
     return tile;
@@ -178,6 +179,21 @@ template <int D>
 __global__ __launch_bounds__(256) void smore_proj(SpecProjArgs a) {
     __shared__ __attribute__((aligned(16))) float lds[kPjLds<D>];
     proj_block<D>(a, blockIdx.x, lds);
+}
+
+// smore_proj at d = 128 as two blocks per (item tile, K split), one per half of the output
+// features: the d = 64 block's LDS footprint (37 KB instead of 55 KB: four blocks a CU, not
+// two), so twice the waves hide the K-chunk loads.  The two halves of a pair are blocks
+// b and b + 8 (the same XCD under the round-robin deal): the X chunks come from its L2 for
+// the second.  Same products in the same K order: the results are smore_proj<128>'s bits.
+// Grid: 16 * ceil(nb / 8) for nb = tiles * (S0 + S1); blocks past nb exit.
+template <int D>
+__global__ __launch_bounds__(256) void smore_proj_half(SpecProjArgs a, int nb) {
+    __shared__ __attribute__((aligned(16))) float lds[kPjLds<D / 2>];
+    const int b = blockIdx.x;
+    const int bid = (b & 7) | ((b >> 4) << 3);
+    if (bid >= nb) return;
+    proj_block<D / 2, D>(a, bid, lds, (b >> 3) & 1);
 }
 
 // ---------------------------------------------------------------------------
@@ -913,7 +929,10 @@ extern "C" int rsx_smore_spectral_fwd(const float* V, int32_t dv, const float* W
         hipLaunchKernelGGL(smore_proj<64>, gp, dim3(256), 0, s, p);
         hipLaunchKernelGGL(smore_spec_fwd<64>, gs, dim3(256), 0, s, a);
     } else {
-        hipLaunchKernelGGL(smore_proj<128>, gp, dim3(256), 0, s, p);
+        static const int half = env_knob("RSX_PROJ_HALF", 1, 0, 1);  // 0: one block per (tile, split) (A/B)
+        const int nb = (int)(p.tiles * (p.S[0] + p.S[1]));
+        if (half) hipLaunchKernelGGL(smore_proj_half<128>, dim3((unsigned)(16 * ((nb + 7) / 8))), dim3(256), 0, s, p, nb);
+        else hipLaunchKernelGGL(smore_proj<128>, gp, dim3(256), 0, s, p);
         hipLaunchKernelGGL(smore_spec_fwd<128>, gs, dim3(256), 0, s, a);
     }
     return last_rc();
