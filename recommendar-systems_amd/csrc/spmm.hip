@@ -364,6 +364,10 @@ __device__ __forceinline__ float4 gather16(float4 acc, int cm, float vm, int n, 
 #else
 #define RSX_SPMM_ATTR
 #endif
+// RSX_ADAM_WAVES (tuning): the minimum waves a SIMD for the ADAM kind alone
+#ifndef RSX_ADAM_WAVES
+#define RSX_ADAM_WAVES 0
+#endif
 
 // One group of G lanes per work item {row, slot, begin, end}.
 typedef float v4f __attribute__((ext_vector_type(4)));
@@ -547,7 +551,8 @@ __device__ __forceinline__ void spmm_main_body(const rsx_csr& a, const float* __
 // (the next descriptor is loaded before the current item is processed); blocks
 // [n_main, n_main + n_long) are the long rows' fixups (fix_only: every block is one).
 template <int D, int KIND>
-__global__ RSX_SPMM_ATTR __launch_bounds__(kBlock) void spmm_main(rsx_csr a, const float* __restrict__ x,
+__global__ RSX_SPMM_ATTR __launch_bounds__(kBlock)
+__attribute__((amdgpu_waves_per_eu(KIND == RSX_EPI_ADAM && RSX_ADAM_WAVES ? RSX_ADAM_WAVES : 1))) void spmm_main(rsx_csr a, const float* __restrict__ x,
                                                                   rsx_epilogue e, float* __restrict__ slab,
                                                                   int64_t n_main, int fix_only, TagJob tj) {
     constexpr int G = D / 4;
