@@ -24,8 +24,11 @@ namespace rsx {
 // ---------------------------------------------------------------------------
 // row epilogues
 // ---------------------------------------------------------------------------
+// RSX_ADAM_LATE=1 (since round 6): the ADAM epilogue loads p, m, v after the gathers rather
+// than before them (102 instead of 115 VGPRs; the C2 ADAM launch 32.4-33.1 against
+// 33.3-33.4 us in six alternating runs, profiles/r06/spmm_occ/)
 #ifndef RSX_ADAM_LATE
-#define RSX_ADAM_LATE 0
+#define RSX_ADAM_LATE 1
 #endif
 
 // Row operands of an epilogue, loaded by epi_load right after the work item is
