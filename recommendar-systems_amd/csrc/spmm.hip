@@ -30,6 +30,10 @@ namespace rsx {
 #ifndef RSX_ADAM_LATE
 #define RSX_ADAM_LATE 1
 #endif
+// RSX_FINAL_LATE (A/B): the FINAL epilogue's four stored layers loaded after the gathers
+#ifndef RSX_FINAL_LATE
+#define RSX_FINAL_LATE 0
+#endif
 
 // Row operands of an epilogue, loaded by epi_load right after the work item is
 // known so that they are in flight during the neighbour gathers (the ADAM kind
@@ -60,10 +64,12 @@ __device__ __forceinline__ EpiIn epi_load(const rsx_epilogue& e, int64_t row, in
     if constexpr (KIND == RSX_EPI_LAYERSUM || KIND == RSX_EPI_AXPBY) {
         if (s_in) in.a = ld4(s_in + off);
     } else if constexpr (KIND == RSX_EPI_FINAL) {
-        if (s_in) in.a = ld4(s_in + off);
-        if (r_add) in.b = ld4(r_add + off);
-        if (e.aux) in.c = ld4(e.aux + off);
-        if (e.e0) in.d = ld4(e.e0 + off);
+        if (!RSX_FINAL_LATE) {
+            if (s_in) in.a = ld4(s_in + off);
+            if (r_add) in.b = ld4(r_add + off);
+            if (e.aux) in.c = ld4(e.aux + off);
+            if (e.e0) in.d = ld4(e.e0 + off);
+        }
     } else if constexpr (KIND == RSX_EPI_ADD) {
         if (s_in) in.a = ld4(s_in + off);
         if (r_add) in.b = ld4(r_add + off);
@@ -130,10 +136,20 @@ __device__ __forceinline__ void epilogue(const rsx_epilogue& e, int64_t row, flo
         st4(e.s_out + off, s);
     } else if constexpr (KIND == RSX_EPI_FINAL) {
         // (((s_in + r_add) + aux) + e0) + acc: the stored layers summed in layer order
-        float4 t = in.a;
-        if (e.r_add) t = add4(t, in.b);
-        if (e.aux) t = add4(t, in.c);
-        if (e.e0) t = add4(t, in.d);
+        float4 a4 = in.a, b4 = in.b, c4 = in.c, d4 = in.d;
+        if (RSX_FINAL_LATE) {  // epi_load's operands, loaded here (the same rows, the same tag rules)
+            const int tf = tag_flags(e);
+            const float* s_in = (!(tf & RSX_TAG_SPARSE_S) || in.tagged) ? e.s_in : nullptr;
+            const float* r_add = (!(tf & RSX_TAG_SPARSE_R) || in.tagged) ? e.r_add : nullptr;
+            a4 = s_in ? ld4(s_in + off) : f4(0.f);
+            b4 = r_add ? ld4(r_add + off) : f4(0.f);
+            c4 = e.aux ? ld4(e.aux + off) : f4(0.f);
+            d4 = e.e0 ? ld4(e.e0 + off) : f4(0.f);
+        }
+        float4 t = a4;
+        if (e.r_add) t = add4(t, b4);
+        if (e.aux) t = add4(t, c4);
+        if (e.e0) t = add4(t, d4);
         const float4 s = (e.s_in || e.r_add || e.aux || e.e0) ? add4(t, acc) : acc;
         st4(e.f + off, mul4(e.beta, s));
     } else if constexpr (KIND == RSX_EPI_AXPBY) {
